@@ -1,0 +1,171 @@
+"""Pin the CPU oracle against the golden vectors produced by the reference itself.
+
+If these pass, the oracle is a faithful restatement of game.py / train.py on every fixture, and the
+GPU parity tests (tests/test_gpu_*.py) can use it as the checker.
+"""
+
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import oracle as O
+
+
+def test_philox_known_answers():
+    # Random123 kat_vectors for philox4x32_10
+    assert list(O.philox4x32_10([0, 0, 0, 0], [0, 0])) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    assert list(O.philox4x32_10([0xFFFFFFFF] * 4, [0xFFFFFFFF] * 2)) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6,
+                                                                         0x6D5451FD]
+    assert list(O.philox4x32_10([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344], [0xA4093822, 0x299F31D0])) == [
+        0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+@pytest.mark.parametrize("seed", [0, 1, 42, 2**32 - 1, 2**32 + 17, 2**63 + 5])
+def test_mt_matches_cpython(seed):
+    import random
+    r = random.Random(seed)
+    ref = np.array([r.getrandbits(32) for _ in range(2000)], np.uint32)
+    assert np.array_equal(O.MTStates([seed]).u32(2000), ref)
+
+
+def test_row_table_left_right():
+    g = golden("rows.npz")
+    rows = g["rows"]
+    n = len(rows)
+    boards = np.zeros((n, 16), np.int8)
+    boards[:, :4] = rows
+    for d, key in ((O.LEFT, "left"), (O.RIGHT, "right")):
+        out, pts, mx = O.move(boards, d)
+        assert np.array_equal(out[:, :4], g[key])
+        assert np.array_equal(pts, g[f"{key}_points"])
+        assert np.array_equal(mx, g[f"{key}_max"])
+    m = O.legal_mask(boards)
+    assert np.array_equal((m >> O.LEFT) & 1, g["legal_lr"][:, 0])
+    assert np.array_equal((m >> O.RIGHT) & 1, g["legal_lr"][:, 1])
+    # columns: the same rows laid out as column 0 must behave identically under UP/DOWN
+    cols = np.zeros((n, 16), np.int8)
+    cols[:, 0::4] = rows
+    for d, key in ((O.UP, "left"), (O.DOWN, "right")):
+        out, pts, _ = O.move(cols, d)
+        assert np.array_equal(out[:, 0::4], g[key])
+        assert np.array_equal(pts, g[f"{key}_points"])
+
+
+def test_seeded_games_bit_exact(games):
+    g = games
+    n_games = int(g["game"].max()) + 1
+    seeds = np.arange(n_games, dtype=np.uint64)
+    mt = O.MTStates(seeds)
+    boards = O.reset(n_games, O.RNG_MT, mt=mt)
+    assert np.array_equal(boards, g["init_boards"])
+    # replay all games in lock-step; finished games are dropped from the batch
+    steps_by_game = [np.nonzero(g["game"] == s)[0] for s in range(n_games)]
+    max_t = max(len(x) for x in steps_by_game)
+    for t in range(max_t):
+        live = [s for s in range(n_games) if t < len(steps_by_game[s])]
+        idx = np.array([steps_by_game[s][t] for s in live])
+        sub = MTSub(mt, live)
+        assert np.array_equal(boards[live], g["before"][idx])
+        after, f, info, moved = O.step(boards[live], g["action"][idx], O.RNG_MT, mt=sub.view(), full_info=True)
+        sub.writeback()
+        for k in ("points", "max_tile", "mono_b", "mono_a", "empt_b", "empt_a", "invalid", "done"):
+            assert np.array_equal(f[k], g[k][idx]), (t, k)
+        assert np.array_equal(moved, g["moved"][idx])
+        assert np.array_equal(after, g["after"][idx])
+        for col, key in enumerate(("smooth_d", "corner_d", "adj_d", "chain_d", "topo_d")):
+            assert np.array_equal(info[:, col], g[key][idx]), key
+        valid = f["invalid"] == 0
+        assert np.array_equal(f["maxexp_b"][valid], g["maxexp_b"][idx][valid])
+        assert np.array_equal(O.legal_mask(after), g["mask_after"][idx])
+        boards[live] = after
+
+
+class MTSub:
+    """Gather/scatter a subset of per-env MT states so finished games can be dropped."""
+
+    def __init__(self, mt, live):
+        self.mt, self.live = mt, live
+        nb = mt.nbytes
+        self.sub = O.MTStates(np.zeros(len(live), np.uint64))
+        for j, s in enumerate(live):
+            self.sub.buf[j * nb:(j + 1) * nb] = mt.buf[s * nb:(s + 1) * nb]
+
+    def view(self):
+        return self.sub
+
+    def writeback(self):
+        nb = self.mt.nbytes
+        for j, s in enumerate(self.live):
+            self.mt.buf[s * nb:(s + 1) * nb] = self.sub.buf[j * nb:(j + 1) * nb]
+
+
+def test_best_game_replay_with_injected_spawns():
+    g = golden("best_game.npz")
+    boards = g["before"][:1].copy()
+    for t in range(len(g["action"])):
+        assert np.array_equal(boards[0], g["before"][t])
+        after, f, _, moved = O.step(boards, [g["action"][t]], O.RNG_INJECT, inj_k=[g["spawn_k"][t]],
+                                    inj_v=[g["spawn_val"][t]])
+        assert f["points"][0] == g["points"][t]
+        assert np.array_equal(moved[0], g["moved"][t])
+        assert np.array_equal(after[0], g["after"][t])
+        boards = after
+    assert O.legal_mask(boards)[0] == 0  # the shipped best game ends on a terminal board
+    assert int(g["points"].sum()) == int(g["score"])
+
+
+def test_monotonicity_closed_form_equivalence():
+    """The kernels use max(L,R)+max(T,B) + corner rule; check it equals the rotation form."""
+    rng = np.random.default_rng(0)
+    b = rng.integers(0, 12, size=(50000, 16)).astype(np.int8)
+    b[rng.random(b.shape) < 0.4] = 0
+    mono, empt = O.potentials(b)
+    g = b.reshape(-1, 4, 4).astype(int)
+    nzh = (g[:, :, :-1] > 0) & (g[:, :, 1:] > 0)
+    nzv = (g[:, :-1, :] > 0) & (g[:, 1:, :] > 0)
+    L = (nzh & (g[:, :, :-1] >= g[:, :, 1:])).sum((1, 2))
+    R = (nzh & (g[:, :, :-1] <= g[:, :, 1:])).sum((1, 2))
+    T = (nzv & (g[:, :-1, :] >= g[:, 1:, :])).sum((1, 2))
+    B = (nzv & (g[:, :-1, :] <= g[:, 1:, :])).sum((1, 2))
+    best = np.maximum(L, R) + np.maximum(T, B)
+    first = np.argmax(b == b.max(axis=1, keepdims=True), axis=1)
+    corner = np.isin(first, [0, 3, 12, 15])
+    assert np.array_equal(mono, np.where(corner, best * 2, best // 2))
+    assert np.array_equal(empt, (b == 0).sum(1))
+
+
+def test_obs_encoding_matches_reference():
+    g = golden("mlp.npz")
+    assert np.array_equal(O.obs_encode(g["boards"]).view(np.uint32), g["obs"].view(np.uint32))
+
+
+def test_masked_policy_matches_reference():
+    g = golden("sampler.npz")
+    p, ent, logp = O.masked_policy(g["logits"], g["invalid"])
+    np.testing.assert_allclose(p, g["probs"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(ent, g["entropy"], rtol=1e-5, atol=1e-6)
+    fin = np.isfinite(g["logp"])
+    assert np.array_equal(fin, np.isfinite(logp))
+    np.testing.assert_allclose(logp[fin], g["logp"][fin], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("case", range(5))
+def test_reward_rtg_matches_calculate_advantage(case):
+    a = golden("advantage.npz")
+    gamma, wp, wm, we, beta, m2, mu, step = a["cases"][case]
+    ep = a["episode"]
+    ends = np.r_[ep[1:] != ep[:-1], True]
+    r = O.reward_rtg_normalize(a["points"], a["mono_b"], a["mono_a"], a["empt_b"], a["empt_a"], a["done"],
+                               a["value"], ends, gamma, wp, wm, we, beta, m2, mu, int(step))
+    assert np.array_equal(r["reward"], a[f"c{case}_reward"])
+    np.testing.assert_allclose(r["g_raw"], a[f"c{case}_g_raw"], rtol=1e-13, atol=1e-9)
+    np.testing.assert_allclose(r["g_norm"], a[f"c{case}_g_norm"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(r["adv"], a[f"c{case}_adv"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(r["moments"], a[f"c{case}_moments"], rtol=1e-12)
+
+
+def test_random_rollout_counts():
+    b = O.reset(64, O.RNG_PHILOX, seed=0x2048)
+    n, b2 = O.random_rollout(b, 50, seed=0x2048)
+    assert n == 64 * 50
+    assert ((b2 >= 0) & (b2 <= 17)).all()
