@@ -1,0 +1,255 @@
+// board.hpp -- device-side 2048 board arithmetic for gfx950 (CDNA4), one 4x4 board per lane.
+//
+// A board is 16 int8 exponents held in one uint4 (x,y,z,w = rows 0..3, byte j of a row dword =
+// column j), i.e. exactly the 16 bytes of one [N,16] row, loaded with a single global_load_dwordx4.
+// All per-cell predicates are SWAR on those four dwords (exponents are < 0x80, so per-byte adds
+// never carry across bytes):
+//   nz(x)    = (x + 0x7F7F7F7F) & 0x80808080       bit 7 of a byte set  <=> byte != 0
+//   ge(a,b)  = ((a | 0x80808080) - b) & 0x80808080  bit 7 of a byte set  <=> a_byte >= b_byte
+// The slide/merge itself runs on four scalar bytes per row after a branch-free transform of the
+// board into the LEFT frame (transpose for UP/DOWN, byte-reverse for RIGHT/DOWN), so every lane of
+// a wave executes the same instruction stream whatever its action.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace g2048 {
+
+__device__ __forceinline__ uint32_t nzm(uint32_t x) { return (x + 0x7F7F7F7Fu) & 0x80808080u; }
+__device__ __forceinline__ uint32_t zm(uint32_t x) { return ~(x + 0x7F7F7F7Fu) & 0x80808080u; }
+__device__ __forceinline__ uint32_t gem(uint32_t a, uint32_t b) { return ((a | 0x80808080u) - b) & 0x80808080u; }
+__device__ __forceinline__ uint32_t eqm(uint32_t a, uint32_t b) { return zm(a ^ b); }
+
+__device__ __forceinline__ uint32_t row(const uint4 &b, int i) {
+    return i == 0 ? b.x : i == 1 ? b.y : i == 2 ? b.z : b.w;
+}
+
+// Bit a of the result = action a legal; the reference's scans (game.py:260-330) reduce to
+// "an empty cell before a tile" or "two equal adjacent tiles" along the move axis.
+__device__ __forceinline__ uint32_t legal_mask(const uint4 &b) {
+    const uint32_t r[4] = {b.x, b.y, b.z, b.w};
+    uint32_t L = 0, R = 0, U = 0, D = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t x = r[i], y = x >> 8;  // y byte j == x byte j+1 (j <= 2)
+        const uint32_t nx = nzm(x), ny = nzm(y) & 0x00808080u;
+        const uint32_t zx = zm(x) & 0x00808080u, zy = zm(y) & 0x00808080u;
+        const uint32_t mh = nx & eqm(x, y) & 0x00808080u;
+        L |= (zx & ny) | mh;
+        R |= (nx & zy) | mh;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const uint32_t a = r[i], c = r[i + 1];
+        const uint32_t na = nzm(a), nc = nzm(c);
+        const uint32_t mv = na & eqm(a, c);
+        U |= (zm(a) & nc) | mv;
+        D |= (na & zm(c)) | mv;
+    }
+    return (U ? 1u : 0u) | (D ? 2u : 0u) | (L ? 4u : 0u) | (R ? 8u : 0u);
+}
+
+__device__ __forceinline__ uint32_t bytemax(uint32_t a, uint32_t b) {
+    const uint32_t sel = (gem(a, b) >> 7) * 0xFFu;
+    return (a & sel) | (b & ~sel);
+}
+
+__device__ __forceinline__ int emptiness(const uint4 &b) {  // game.py:671-680
+    return __popc(zm(b.x)) + __popc(zm(b.y)) + __popc(zm(b.z)) + __popc(zm(b.w));
+}
+
+// game.py:683-800.  The best of the four clockwise rotations of (#left>=right + #top>=bottom over
+// non-empty adjacent pairs) equals max(L,R) + max(T,B) with L/R/T/B those pair counts in the four
+// orientations (each rotation pairs one horizontal with one vertical orientation).  Then x2 if the
+// first row-major maximum sits in a corner, else floor(/2).
+__device__ __forceinline__ int monotonicity(const uint4 &b) {
+    const uint32_t r[4] = {b.x, b.y, b.z, b.w};
+    int Lc = 0, Rc = 0, Tc = 0, Bc = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t x = r[i], y = x >> 8;
+        const uint32_t both = nzm(x) & nzm(y) & 0x00808080u;
+        Lc += __popc(both & gem(x, y));
+        Rc += __popc(both & gem(y, x));
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const uint32_t a = r[i], c = r[i + 1];
+        const uint32_t both = nzm(a) & nzm(c);
+        Tc += __popc(both & gem(a, c));
+        Bc += __popc(both & gem(c, a));
+    }
+    const int best = max(Lc, Rc) + max(Tc, Bc);
+    uint32_t m = bytemax(bytemax(r[0], r[1]), bytemax(r[2], r[3]));
+    m = bytemax(m, m >> 8);
+    m = bytemax(m, m >> 16);
+    const uint32_t mb = (m & 0xFFu) * 0x01010101u;
+    const uint64_t e01 = (uint64_t)eqm(r[0], mb) | ((uint64_t)eqm(r[1], mb) << 32);
+    const uint64_t e23 = (uint64_t)eqm(r[2], mb) | ((uint64_t)eqm(r[3], mb) << 32);
+    const int bit = e01 ? __builtin_ctzll(e01) : 64 + __builtin_ctzll(e23);
+    const int pos = bit >> 3;  // first row-major cell holding the max
+    const bool corner = (0x9009u >> pos) & 1u;
+    return corner ? best * 2 : best >> 1;
+}
+
+__device__ __forceinline__ uint4 transpose(const uint4 &b) {
+    const uint32_t r0 = b.x, r1 = b.y, r2 = b.z, r3 = b.w;
+    uint4 c;
+    c.x = (r0 & 0xFFu) | ((r1 & 0xFFu) << 8) | ((r2 & 0xFFu) << 16) | (r3 << 24);
+    c.y = ((r0 >> 8) & 0xFFu) | (r1 & 0xFF00u) | ((r2 & 0xFF00u) << 8) | ((r3 & 0xFF00u) << 16);
+    c.z = ((r0 >> 16) & 0xFFu) | ((r1 >> 8) & 0xFF00u) | (r2 & 0xFF0000u) | ((r3 & 0xFF0000u) << 8);
+    c.w = (r0 >> 24) | ((r1 >> 16) & 0xFF00u) | ((r2 >> 8) & 0xFF0000u) | (r3 & 0xFF000000u);
+    return c;
+}
+
+__device__ __forceinline__ uint4 bswap4(const uint4 &b) {
+    return make_uint4(__builtin_bswap32(b.x), __builtin_bswap32(b.y), __builtin_bswap32(b.z),
+                      __builtin_bswap32(b.w));
+}
+
+__device__ __forceinline__ uint4 sel4(bool c, const uint4 &a, const uint4 &b) {
+    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+
+// _merge_and_shift_left_with_score (game.py:225-244) on one row dword.  Compaction is a stable
+// zero-bubbling network, then the greedy leading-edge merge written as selects.
+__device__ __forceinline__ uint32_t slide_row_left(uint32_t x, uint32_t &pts, uint32_t &mx) {
+    uint32_t y0 = x & 0xFFu, y1 = (x >> 8) & 0xFFu, y2 = (x >> 16) & 0xFFu, y3 = x >> 24;
+#define G2048_CSWAP(a, b)              \
+    {                                  \
+        const bool z = (a) == 0u;      \
+        (a) = z ? (b) : (a);           \
+        (b) = z ? 0u : (b);            \
+    }
+    G2048_CSWAP(y0, y1) G2048_CSWAP(y1, y2) G2048_CSWAP(y2, y3)
+    G2048_CSWAP(y0, y1) G2048_CSWAP(y1, y2)
+    G2048_CSWAP(y0, y1)
+#undef G2048_CSWAP
+    const bool m01 = (y0 != 0u) & (y0 == y1);
+    const bool m12 = !m01 & (y1 != 0u) & (y1 == y2);
+    const bool m23 = (y2 != 0u) & (y2 == y3) & !m12;
+    const uint32_t o0 = y0 + (m01 ? 1u : 0u);
+    const uint32_t o1 = m01 ? y2 + (m23 ? 1u : 0u) : y1 + (m12 ? 1u : 0u);
+    const uint32_t o2 = m01 ? (m23 ? 0u : y3) : (m12 ? y3 : y2 + (m23 ? 1u : 0u));
+    const uint32_t o3 = (m01 | m12 | m23) ? 0u : y3;
+    pts += (m01 ? (1u << (y0 + 1u)) : 0u) + (m12 ? (1u << (y1 + 1u)) : 0u) + (m23 ? (1u << (y2 + 1u)) : 0u);
+    mx = max(mx, max(m01 ? y0 + 1u : 0u, max(m12 ? y1 + 1u : 0u, m23 ? y2 + 1u : 0u)));
+    return o0 | (o1 << 8) | (o2 << 16) | (o3 << 24);
+}
+
+// simulate_move (game.py:122-160) for a per-lane action, branch-free.
+__device__ __forceinline__ uint4 apply_move(const uint4 &b, uint32_t action, uint32_t &pts, uint32_t &mx) {
+    const bool vert = action < 2u;                         // UP, DOWN work on columns
+    const bool rev = (action == 1u) | (action == 3u);      // DOWN, RIGHT slide toward the far edge
+    uint4 w = sel4(vert, transpose(b), b);
+    w = sel4(rev, bswap4(w), w);
+    pts = 0u;
+    mx = 0u;
+    w.x = slide_row_left(w.x, pts, mx);
+    w.y = slide_row_left(w.y, pts, mx);
+    w.z = slide_row_left(w.z, pts, mx);
+    w.w = slide_row_left(w.w, pts, mx);
+    w = sel4(rev, bswap4(w), w);
+    return sel4(vert, transpose(w), w);
+}
+
+__device__ __forceinline__ uint32_t nibble_of(uint32_t m80) {  // bits 7,15,23,31 -> bits 0..3
+    const uint32_t t = m80 >> 7;
+    return (t | (t >> 7) | (t >> 14) | (t >> 21)) & 0xFu;
+}
+
+__device__ __forceinline__ uint32_t empty_mask16(const uint4 &b) {  // bit 4i+j = cell (i,j) empty
+    return nibble_of(zm(b.x)) | (nibble_of(zm(b.y)) << 4) | (nibble_of(zm(b.z)) << 8) |
+           (nibble_of(zm(b.w)) << 12);
+}
+
+// position of the k-th (0-based) set bit of a 16-bit mask (k < popcount)
+__device__ __forceinline__ uint32_t kth_bit16(uint32_t m, uint32_t k) {
+    uint32_t pos = 0, c;
+    c = __popc(m & 0xFFu); if (k >= c) { k -= c; m >>= 8; pos += 8; }
+    c = __popc(m & 0xFu);  if (k >= c) { k -= c; m >>= 4; pos += 4; }
+    c = __popc(m & 0x3u);  if (k >= c) { k -= c; m >>= 2; pos += 2; }
+    c = m & 1u;            if (k >= c) { pos += 1; }
+    return pos;
+}
+
+__device__ __forceinline__ void set_cell(uint4 &b, uint32_t pos, uint32_t v) {
+    const uint32_t sh = (pos & 3u) * 8u, bits = v << sh, r = pos >> 2;
+    b.x |= r == 0u ? bits : 0u;
+    b.y |= r == 1u ? bits : 0u;
+    b.z |= r == 2u ? bits : 0u;
+    b.w |= r == 3u ? bits : 0u;
+}
+
+__device__ __forceinline__ bool eq4(const uint4 &a, const uint4 &b) {
+    return ((a.x ^ b.x) | (a.y ^ b.y) | (a.z ^ b.z) | (a.w ^ b.w)) == 0u;
+}
+
+// ---------------------------------------------------------------- Philox4x32-10 -------------
+__device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        c0 = hi1 ^ c1 ^ k0;
+        c1 = lo1;
+        c2 = hi0 ^ c3 ^ k1;
+        c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return make_uint4(c0, c1, c2, c3);
+}
+
+__device__ __forceinline__ uint4 philox_draw(uint64_t seed, uint64_t step, uint32_t env, uint32_t stream) {
+    return philox((uint32_t)step, (uint32_t)(step >> 32), env, stream, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// 0.9 threshold of `random.random() < 0.9` (game.py:939) on a 32-bit uniform: u*2^-32 < 0.9
+constexpr uint32_t kTwoThreshold = 3865470567u;
+
+// ---------------------------------------------------------------- MT19937 (parity) ----------
+// Word-major state: word w of env e lives at st[w * n + e] (w = 624 is the output index), so a
+// wave's accesses to the same word are contiguous.
+struct MT {
+    uint32_t *st = nullptr;
+    int64_t n = 0, e = 0;
+    uint32_t idx = 0;
+    __device__ void load(uint32_t *s, int64_t n_, int64_t e_) {
+        st = s;
+        n = n_;
+        e = e_;
+        idx = st[624 * n + e];
+    }
+    __device__ void save() { st[624 * n + e] = idx; }
+    __device__ uint32_t &w(int k) { return st[(int64_t)k * n + e]; }
+    __device__ uint32_t next() {
+        if (idx >= 624u) {
+            for (int kk = 0; kk < 624; kk++) {
+                const uint32_t y = (w(kk) & 0x80000000u) | (w(kk + 1 < 624 ? kk + 1 : 0) & 0x7fffffffu);
+                const int src = kk + 397 < 624 ? kk + 397 : kk + 397 - 624;
+                w(kk) = w(src) ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+            }
+            idx = 0;
+        }
+        uint32_t y = w(idx++);
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= (y >> 18);
+        return y;
+    }
+    __device__ uint32_t randbelow(uint32_t m) {  // random.Random._randbelow_with_getrandbits
+        const int k = 32 - __clz(m);
+        for (;;) {
+            const uint32_t r = next() >> (32 - k);
+            if (r < m) return r;
+        }
+    }
+    __device__ bool below_09() {  // random.random() < 0.9
+        const uint32_t a = next() >> 5, b = next() >> 6;
+        return (a * 67108864.0 + b) * (1.0 / 9007199254740992.0) < 0.9;
+    }
+};
+
+}  // namespace g2048

@@ -1,0 +1,577 @@
+// g2048.hip -- libg2048.so: HIP kernels for gfx950 + the C ABI declared in include/g2048.h.
+//
+// Kernels (one lane = one env unless stated):
+//   env_step_kernel<Rng>   Game2048.step (game.py:952-1030), optional random-legal action and
+//                          auto-reset / skip-done.  The hot kernel: 16-B board load, ~40 B out.
+//   env_reset_kernel<Rng>  Game2048.reset (game.py:942-950)
+//   legal_kernel           current_valid_directions (game.py:295-299)
+//   obs_kernel<T>          to_model_format (game.py:92-101); one lane per 4 output values so the
+//                          [N,48] stores are contiguous per wave
+//   sample_kernel          masked softmax / sample / entropy / log_softmax (train.py:266-326)
+//   rtg_kernel             reward + reverse discounted scan + normalisation + advantage
+//                          (train.py:699-772), time-major [T][N], float64 arithmetic
+//   rtg_reduce / prepare / finalize   batch moments and the EMA update (train.py:731-754, 898-901)
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#include "board.hpp"
+#include "../../include/g2048.h"
+
+using namespace g2048;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+enum : uint32_t { FLAG_INVALID = 0x10u, FLAG_RESET = 0x20u, FLAG_INACTIVE = 0x40u, FLAG_DONE = 0x80u };
+
+struct RngArgs {
+    uint64_t seed;
+    uint64_t counter;
+    const uint64_t *counter_dev;
+    uint32_t env_base;
+    uint32_t *mt;
+    const int32_t *inject;
+};
+
+__device__ __forceinline__ uint64_t rng_counter(const RngArgs &r) {
+    return r.counter + (r.counter_dev ? *r.counter_dev : 0ull);
+}
+
+// One spawn on `b` (game.py:923-940).  `slot` selects which pair of the Philox block is used, so a
+// reset's two spawns come from one 4-word draw.
+template <int Mode>
+__device__ __forceinline__ void spawn(uint4 &b, const uint4 &ph, int slot, MT *mt, const RngArgs &r, int64_t i) {
+    const uint32_t em = empty_mask16(b);
+    const uint32_t cnt = __popc(em);
+    if (cnt == 0u) return;
+    uint32_t k, v;
+    if constexpr (Mode == G2048_RNG_PHILOX) {
+        const uint32_t u0 = slot ? ph.z : ph.x, u1 = slot ? ph.w : ph.y;
+        k = (uint32_t)(((uint64_t)u0 * cnt) >> 32);
+        v = u1 < kTwoThreshold ? 1u : 2u;
+    } else if constexpr (Mode == G2048_RNG_MT19937) {
+        k = mt->randbelow(cnt);
+        v = mt->below_09() ? 1u : 2u;
+    } else {
+        k = (uint32_t)r.inject[2 * i];
+        v = (uint32_t)r.inject[2 * i + 1];
+        k = k < cnt ? k : cnt - 1u;
+    }
+    set_cell(b, kth_bit16(em, k), v);
+}
+
+template <int Mode>
+__device__ __forceinline__ uint4 fresh_board(MT *mt, const RngArgs &r, int64_t i, uint64_t ctr) {
+    uint4 b = make_uint4(0u, 0u, 0u, 0u);
+    uint4 ph = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (Mode == G2048_RNG_PHILOX) ph = philox_draw(r.seed, ctr, r.env_base + (uint32_t)i, 2u);
+    spawn<Mode>(b, ph, 0, mt, r, i);
+    spawn<Mode>(b, ph, 1, mt, r, i);
+    return b;
+}
+
+struct StepResult {
+    uint32_t action, pts, mx, pot, fl;
+};
+
+// Game2048.step (game.py:952-1030) on a board held in registers.  has_action == false draws the
+// uniform random legal action of the synthetic benchmark policy (Philox stream 1).
+template <int Mode>
+__device__ __forceinline__ StepResult step_board(uint4 &b, bool has_action, uint32_t action_in, MT *mt,
+                                                 const RngArgs &rng, int64_t i, uint64_t ctr, uint32_t opts) {
+    StepResult res{0u, 0u, 0u, 0u, 0u};
+    const uint32_t env = rng.env_base + (uint32_t)i;
+    uint32_t legal_in = 0u;
+    const bool need_legal = !has_action || (opts & G2048_OPT_SKIP_DONE);
+    if (need_legal) legal_in = legal_mask(b);
+    if ((opts & G2048_OPT_SKIP_DONE) && legal_in == 0u) {  // episodic mode: this game is already over
+        res.action = 0xFFu;
+        res.fl = FLAG_INACTIVE | FLAG_DONE;
+        return res;
+    }
+    uint32_t a;
+    if (has_action) {
+        a = action_in & 3u;
+    } else {
+        const uint4 d = philox_draw(rng.seed, ctr, env, 1u);
+        const uint32_t nl = __popc(legal_in);
+        a = nl ? kth_bit16(legal_in, (uint32_t)(((uint64_t)d.x * nl) >> 32)) : 0u;  // k-th legal action
+    }
+    res.action = a;
+    const int mono_b = monotonicity(b);
+    const int empt_b = emptiness(b);
+    uint32_t pts, mx;
+    uint4 moved = apply_move(b, a, pts, mx);
+    if (eq4(moved, b)) {
+        // illegal action: no-op, zero points and potentials, done = no legal move (game.py:959-978)
+        if (!need_legal) legal_in = legal_mask(b);
+        res.fl = FLAG_INVALID | legal_in | (legal_in ? 0u : FLAG_DONE);
+    } else {
+        const int mono_a = monotonicity(moved);
+        const int empt_a = emptiness(moved);
+        res.pot = (uint32_t)(mono_b & 0xFF) | ((uint32_t)(mono_a & 0xFF) << 8) | ((uint32_t)(empt_b & 0xFF) << 16) |
+                  ((uint32_t)(empt_a & 0xFF) << 24);
+        res.pts = pts;
+        res.mx = mx;
+        uint4 ph = make_uint4(0u, 0u, 0u, 0u);
+        if constexpr (Mode == G2048_RNG_PHILOX) ph = philox_draw(rng.seed, ctr, env, 0u);
+        spawn<Mode>(moved, ph, 0, mt, rng, i);
+        b = moved;
+        const uint32_t lm = legal_mask(b);
+        res.fl = lm | (lm ? 0u : FLAG_DONE);
+    }
+    if ((res.fl & FLAG_DONE) && (opts & G2048_OPT_AUTO_RESET)) {
+        b = fresh_board<Mode>(mt, rng, i, ctr);
+        res.fl = (res.fl & ~0xFu) | FLAG_RESET | legal_mask(b);
+    }
+    return res;
+}
+
+template <int Mode>
+__global__ __launch_bounds__(kBlock) void env_step_kernel(const uint4 *__restrict__ bin, uint4 *__restrict__ bout,
+                                                          const uint8_t *__restrict__ ain, uint8_t *__restrict__ aout,
+                                                          int32_t *__restrict__ points, int8_t *__restrict__ maxt,
+                                                          uint32_t *__restrict__ pot, uint8_t *__restrict__ flags,
+                                                          int64_t n, RngArgs rng, uint32_t opts) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    uint4 b = bin[i];
+    MT mt;
+    if constexpr (Mode == G2048_RNG_MT19937) mt.load(rng.mt, n, i);
+    const StepResult r = step_board<Mode>(b, ain != nullptr, ain ? ain[i] : 0u, &mt, rng, i, rng_counter(rng), opts);
+    if constexpr (Mode == G2048_RNG_MT19937) mt.save();
+    bout[i] = b;
+    points[i] = (int32_t)r.pts;
+    if (maxt) maxt[i] = (int8_t)r.mx;
+    if (pot) pot[i] = r.pot;
+    if (aout) aout[i] = (uint8_t)r.action;
+    flags[i] = (uint8_t)r.fl;
+}
+
+// Synthetic random-legal rollout (the benchmark workload of BASELINE.md): `steps` env steps per
+// launch with the board kept in registers, auto-reset on done, one time-major trajectory record per
+// step: the board the action was taken on [T][N][16], action, points, potentials, flags.
+__global__ __launch_bounds__(kBlock) void env_rollout_kernel(uint4 *__restrict__ boards, int64_t n, int64_t steps,
+                                                             uint4 *__restrict__ tb, uint8_t *__restrict__ ta,
+                                                             int32_t *__restrict__ tp, uint32_t *__restrict__ tpot,
+                                                             uint8_t *__restrict__ tf, RngArgs rng) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    uint4 b = boards[i];
+    const uint64_t ctr0 = rng_counter(rng);
+    for (int64_t t = 0; t < steps; t++) {
+        const int64_t o = t * n + i;
+        if (tb) tb[o] = b;
+        const StepResult r = step_board<G2048_RNG_PHILOX>(b, false, 0u, nullptr, rng, i, ctr0 + (uint64_t)t,
+                                                          G2048_OPT_AUTO_RESET);
+        if (ta) ta[o] = (uint8_t)r.action;
+        if (tp) tp[o] = (int32_t)r.pts;
+        if (tpot) tpot[o] = r.pot;
+        if (tf) tf[o] = (uint8_t)r.fl;
+    }
+    boards[i] = b;
+}
+
+template <int Mode>
+__global__ __launch_bounds__(kBlock) void env_reset_kernel(uint4 *__restrict__ boards, uint8_t *__restrict__ flags,
+                                                           const uint8_t *__restrict__ where, int64_t n, RngArgs rng) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    if (where && !where[i]) return;
+    MT mt;
+    if constexpr (Mode == G2048_RNG_MT19937) mt.load(rng.mt, n, i);
+    const uint4 b = fresh_board<Mode>(&mt, rng, i, rng_counter(rng));
+    if constexpr (Mode == G2048_RNG_MT19937) mt.save();
+    boards[i] = b;
+    if (flags) flags[i] = (uint8_t)legal_mask(b);
+}
+
+__global__ __launch_bounds__(kBlock) void legal_kernel(const uint4 *__restrict__ boards, uint8_t *__restrict__ flags,
+                                                       int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t m = legal_mask(boards[i]);
+    flags[i] = (uint8_t)(m | (m ? 0u : FLAG_DONE));
+}
+
+// CPython random.seed(int) == init_by_array over the 32-bit words of the seed.
+__global__ __launch_bounds__(kBlock) void mt_seed_kernel(uint32_t *__restrict__ st, const uint64_t *__restrict__ seeds,
+                                                         int64_t n) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n) return;
+    auto W = [&](int k) -> uint32_t & { return st[(int64_t)k * n + e]; };
+    const uint64_t s = seeds[e];
+    const uint32_t key[2] = {(uint32_t)s, (uint32_t)(s >> 32)};
+    const int klen = key[1] ? 2 : 1;
+    W(0) = 19650218u;
+    for (int k = 1; k < 624; k++) W(k) = 1812433253u * (W(k - 1) ^ (W(k - 1) >> 30)) + (uint32_t)k;
+    int i = 1, j = 0;
+    for (int k = 624; k; k--) {
+        W(i) = (W(i) ^ ((W(i - 1) ^ (W(i - 1) >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+        i++; j++;
+        if (i >= 624) { W(0) = W(623); i = 1; }
+        if (j >= klen) j = 0;
+    }
+    for (int k = 623; k; k--) {
+        W(i) = (W(i) ^ ((W(i - 1) ^ (W(i - 1) >> 30)) * 1566083941u)) - (uint32_t)i;
+        i++;
+        if (i >= 624) { W(0) = W(623); i = 1; }
+    }
+    W(0) = 0x80000000u;
+    W(624) = 624u;
+}
+
+// to_model_format: value f = 3*cell + k of board i is (e, row/3, col/3)[k].  Lane = 4 values.
+__constant__ float kThirds[4] = {0.0f, 1.0f / 3.0f, 2.0f / 3.0f, 1.0f};
+
+template <typename T>
+__device__ __forceinline__ T cvt(float x);
+template <>
+__device__ __forceinline__ float cvt<float>(float x) { return x; }
+template <>
+__device__ __forceinline__ __hip_bfloat16 cvt<__hip_bfloat16>(float x) { return __float2bfloat16(x); }
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void obs_kernel(const int8_t *__restrict__ boards, T *__restrict__ obs, int64_t n) {
+    const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // chunk of 4 values
+    if (q >= n * 12) return;
+    const int64_t i = q / 12;
+    const int f0 = (int)(q - i * 12) * 4;
+    T v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int f = f0 + u, cell = f / 3, k = f - cell * 3;
+        const float x = k == 0 ? (float)boards[i * 16 + cell] : kThirds[k == 1 ? (cell >> 2) : (cell & 3)];
+        v[u] = cvt<T>(x);
+    }
+    T *dst = obs + q * 4;
+#pragma unroll
+    for (int u = 0; u < 4; u++) dst[u] = v[u];
+}
+
+__global__ __launch_bounds__(kBlock) void sample_kernel(const float *__restrict__ logits, int64_t stride,
+                                                        const uint8_t *__restrict__ flags, uint8_t *__restrict__ actions,
+                                                        float *__restrict__ logp, float *__restrict__ entropy, int64_t n,
+                                                        RngArgs rng) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t legal = flags[i] & 0xFu;
+    const uint4 d = philox_draw(rng.seed, rng_counter(rng), rng.env_base + (uint32_t)i, 1u);
+    float l[4];
+#pragma unroll
+    for (int a = 0; a < 4; a++) l[a] = logits ? logits[i * stride + a] : 0.0f;
+    float m = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+        if ((legal >> a) & 1u) m = fmaxf(m, l[a]);
+    float e[4], s = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        e[a] = ((legal >> a) & 1u) ? expf(l[a] - m) : 0.0f;
+        s += e[a];
+    }
+    const float ls = logf(s), inv = 1.0f / s;
+    const float u = (float)(d.x >> 8) * (1.0f / 16777216.0f);
+    float cum = 0.0f, h = 0.0f;
+    uint32_t act = 0xFFu;
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        const bool ok = (legal >> a) & 1u;
+        const float p = e[a] * inv, lp = (l[a] - m) - ls;
+        if (ok) {
+            cum += p;
+            if (act == 0xFFu && u < cum) act = (uint32_t)a;
+            if (p > 0.0f) h -= p * lp;
+        }
+        if (logp) logp[i * 4 + a] = ok ? lp : -INFINITY;
+    }
+    if (act == 0xFFu) {  // rounding left u >= cum: take the last legal action
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+            if ((legal >> a) & 1u) act = (uint32_t)a;
+        if (!legal) act = 0u;
+    }
+    actions[i] = (uint8_t)act;
+    if (entropy) entropy[i] = legal ? h : 0.0f;
+}
+
+// ---------------------------------------------------------------- reward / return-to-go ------
+struct RewardArgs {
+    double gamma, wp, wm, we;
+};
+
+template <int NW>
+__device__ __forceinline__ double block_sum(double v, double *sh) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) sh[w] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0)
+        for (int k = 0; k < NW; k++) t += sh[k];
+    return t;  // valid on thread 0
+}
+
+__global__ __launch_bounds__(kBlock) void rtg_kernel(const int32_t *__restrict__ points, const uint32_t *__restrict__ pot,
+                                                     const uint8_t *__restrict__ flags, const float *__restrict__ value,
+                                                     int64_t T, int64_t n, RewardArgs ra, const double *__restrict__ state,
+                                                     float *__restrict__ g_raw, float *__restrict__ g_norm,
+                                                     float *__restrict__ adv, double *__restrict__ partial) {
+    __shared__ double sh[kBlock / 64];
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const double mu_c = state[4], denom = state[5] + 1e-8;
+    double s1 = 0.0, s2 = 0.0, cnt = 0.0;
+    if (i < n) {
+        double G = 0.0;
+        for (int64_t t = T - 1; t >= 0; t--) {
+            const int64_t o = t * n + i;
+            const uint32_t fl = flags[o];
+            if (fl & FLAG_INACTIVE) {
+                G = 0.0;
+                g_raw[o] = 0.0f;
+                g_norm[o] = 0.0f;
+                adv[o] = 0.0f;
+                continue;
+            }
+            const uint32_t pw = pot[o];
+            const bool done = (fl & FLAG_DONE) != 0u;
+            const double mb = (double)(int8_t)(pw & 0xFFu), ma = done ? 0.0 : (double)(int8_t)((pw >> 8) & 0xFFu);
+            const double eb = (double)(int8_t)((pw >> 16) & 0xFFu), ea = done ? 0.0 : (double)(int8_t)(pw >> 24);
+            // same operation order as train.py:702-719 (float64, no contraction: built -ffp-contract=off)
+            double shaped = ra.wm * (ra.gamma * ma - mb);
+            shaped = shaped + ra.we * (ra.gamma * ea - eb);
+            const double r = (double)points[o] * ra.wp + shaped;
+            if (done) G = 0.0;  // the episode ended on this step: nothing flows back across it
+            G = r + ra.gamma * G;
+            const double gn = (G - mu_c) / denom;
+            g_raw[o] = (float)G;
+            g_norm[o] = (float)gn;
+            adv[o] = (float)(gn - (double)value[o]);
+            const double dv = G - mu_c;
+            s1 += dv;
+            s2 += dv * dv;
+            cnt += 1.0;
+        }
+    }
+    const double b1 = block_sum<kBlock / 64>(s1, sh);
+    const double b2 = block_sum<kBlock / 64>(s2, sh);
+    const double b3 = block_sum<kBlock / 64>(cnt, sh);
+    if (threadIdx.x == 0) {
+        partial[3 * blockIdx.x + 0] = b1;
+        partial[3 * blockIdx.x + 1] = b2;
+        partial[3 * blockIdx.x + 2] = b3;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void rtg_reduce_kernel(const double *__restrict__ part, int nb, double *__restrict__ out) {
+    __shared__ double sh[kBlock / 64];
+    double a = 0.0, b = 0.0, c = 0.0;
+    for (int k = threadIdx.x; k < nb; k += kBlock) {
+        a += part[3 * k];
+        b += part[3 * k + 1];
+        c += part[3 * k + 2];
+    }
+    a = block_sum<kBlock / 64>(a, sh);
+    b = block_sum<kBlock / 64>(b, sh);
+    c = block_sum<kBlock / 64>(c, sh);
+    if (threadIdx.x == 0) {
+        out[0] = a;
+        out[1] = b;
+        out[2] = c;
+    }
+}
+
+__global__ void rtg_prepare_kernel(double *state, double beta) {
+    const double eps = 1e-8;
+    const double step = state[3] < 1.0 ? 1.0 : state[3];
+    const double bc = fmax(1.0 - pow(beta, step), eps);  // train.py:746
+    const double mu_c = state[0] / bc, m2_c = state[1] / bc;
+    state[4] = mu_c;
+    state[5] = sqrt(fmax(m2_c - mu_c * mu_c, eps));
+}
+
+__global__ void rtg_finalize_kernel(double *state, const double *part, double beta) {
+    const double n = part[2];
+    if (n <= 0.0) return;
+    const double m1 = part[0] / n;
+    const double mean = state[4] + m1;
+    const double var = n <= 1.0 ? 0.0 : fmax(part[1] / n - m1 * m1, 0.0);
+    state[6] = mean;
+    state[7] = var;
+    const double mu = beta * state[0] + (1.0 - beta) * mean;       // train.py:900
+    state[1] = beta * state[1] + (1.0 - beta) * (var + mean * mean);  // train.py:899
+    state[0] = mu;
+    state[2] = mu;  // train.py:901
+    state[3] = state[3] + 1.0;
+}
+
+inline int launch_status() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK : (int)e;
+}
+
+inline unsigned blocks_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0u; }
+
+inline RngArgs rng_args(const g2048_rng *r) {
+    RngArgs a{};
+    if (r) {
+        a.seed = r->seed;
+        a.counter = r->counter;
+        a.counter_dev = r->counter_dev;
+        a.env_base = r->env_base;
+        a.mt = r->mt_state;
+        a.inject = r->inject;
+    }
+    return a;
+}
+
+inline bool rng_ok(const g2048_rng *r) {
+    if (!r) return false;
+    if (r->mode == G2048_RNG_MT19937) return r->mt_state != nullptr;
+    if (r->mode == G2048_RNG_INJECT) return r->inject != nullptr;
+    return r->mode == G2048_RNG_PHILOX;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t g2048_mt_state_words(void) { return 625; }
+
+int g2048_mt_seed(g2048_stream_t stream, uint32_t *mt_state, const uint64_t *seeds, int64_t n) {
+    if (n < 0 || (n > 0 && (!mt_state || !seeds))) return G2048_EINVAL;
+    if (n == 0) return G2048_OK;
+    hipLaunchKernelGGL(mt_seed_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, (hipStream_t)stream, mt_state, seeds, n);
+    return launch_status();
+}
+
+int g2048_env_reset(g2048_stream_t stream, int8_t *boards, uint8_t *flags, const uint8_t *where, int64_t n,
+                    const g2048_rng *rng) {
+    if (n < 0 || !rng_ok(rng) || (n > 0 && (!boards || !aligned16(boards)))) return G2048_EINVAL;
+    if (n == 0) return G2048_OK;
+    const RngArgs a = rng_args(rng);
+    const dim3 g(blocks_for(n)), b(kBlock);
+    hipStream_t s = (hipStream_t)stream;
+    uint4 *bd = (uint4 *)boards;
+    switch (rng->mode) {
+        case G2048_RNG_PHILOX: hipLaunchKernelGGL(env_reset_kernel<G2048_RNG_PHILOX>, g, b, 0, s, bd, flags, where, n, a); break;
+        case G2048_RNG_MT19937: hipLaunchKernelGGL(env_reset_kernel<G2048_RNG_MT19937>, g, b, 0, s, bd, flags, where, n, a); break;
+        default: hipLaunchKernelGGL(env_reset_kernel<G2048_RNG_INJECT>, g, b, 0, s, bd, flags, where, n, a); break;
+    }
+    return launch_status();
+}
+
+int g2048_env_step(g2048_stream_t stream, const int8_t *boards_in, int8_t *boards_out, const uint8_t *actions_in,
+                   uint8_t *actions_out, int32_t *points, int8_t *max_tile, int8_t *pot, uint8_t *flags, int64_t n,
+                   const g2048_rng *rng, uint32_t options) {
+    if (n < 0 || !rng_ok(rng)) return G2048_EINVAL;
+    if (n == 0) return G2048_OK;
+    if (!boards_in || !boards_out || !points || !flags || !aligned16(boards_in) || !aligned16(boards_out)) return G2048_EINVAL;
+    if (pot && ((uintptr_t)pot & 3u)) return G2048_EINVAL;
+    if (options & ~(uint32_t)(G2048_OPT_AUTO_RESET | G2048_OPT_SKIP_DONE)) return G2048_EINVAL;
+    const RngArgs a = rng_args(rng);
+    const dim3 g(blocks_for(n)), b(kBlock);
+    hipStream_t s = (hipStream_t)stream;
+    const uint4 *bi = (const uint4 *)boards_in;
+    uint4 *bo = (uint4 *)boards_out;
+    uint32_t *pw = (uint32_t *)pot;
+    switch (rng->mode) {
+        case G2048_RNG_PHILOX:
+            hipLaunchKernelGGL(env_step_kernel<G2048_RNG_PHILOX>, g, b, 0, s, bi, bo, actions_in, actions_out, points,
+                               max_tile, pw, flags, n, a, options);
+            break;
+        case G2048_RNG_MT19937:
+            hipLaunchKernelGGL(env_step_kernel<G2048_RNG_MT19937>, g, b, 0, s, bi, bo, actions_in, actions_out, points,
+                               max_tile, pw, flags, n, a, options);
+            break;
+        default:
+            hipLaunchKernelGGL(env_step_kernel<G2048_RNG_INJECT>, g, b, 0, s, bi, bo, actions_in, actions_out, points,
+                               max_tile, pw, flags, n, a, options);
+            break;
+    }
+    return launch_status();
+}
+
+int g2048_env_rollout_random(g2048_stream_t stream, int8_t *boards, int64_t n, int64_t steps, int8_t *traj_boards,
+                             uint8_t *traj_actions, int32_t *traj_points, int8_t *traj_pot, uint8_t *traj_flags,
+                             const g2048_rng *rng) {
+    if (n < 0 || steps < 0 || !rng || rng->mode != G2048_RNG_PHILOX) return G2048_EINVAL;
+    if (n == 0 || steps == 0) return G2048_OK;
+    if (!boards || !aligned16(boards) || (traj_boards && !aligned16(traj_boards)) ||
+        (traj_pot && ((uintptr_t)traj_pot & 3u)))
+        return G2048_EINVAL;
+    hipLaunchKernelGGL(env_rollout_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, (hipStream_t)stream, (uint4 *)boards, n,
+                       steps, (uint4 *)traj_boards, traj_actions, traj_points, (uint32_t *)traj_pot, traj_flags,
+                       rng_args(rng));
+    return launch_status();
+}
+
+int g2048_legal_mask(g2048_stream_t stream, const int8_t *boards, uint8_t *flags, int64_t n) {
+    if (n < 0 || (n > 0 && (!boards || !flags || !aligned16(boards)))) return G2048_EINVAL;
+    if (n == 0) return G2048_OK;
+    hipLaunchKernelGGL(legal_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, (hipStream_t)stream, (const uint4 *)boards,
+                       flags, n);
+    return launch_status();
+}
+
+int g2048_obs_encode(g2048_stream_t stream, const int8_t *boards, void *obs, int32_t dtype, int64_t n) {
+    if (n < 0 || (n > 0 && (!boards || !obs)) || (dtype != G2048_DTYPE_F32 && dtype != G2048_DTYPE_BF16))
+        return G2048_EINVAL;
+    if (n == 0) return G2048_OK;
+    const dim3 g(blocks_for(n * 12)), b(kBlock);
+    if (dtype == G2048_DTYPE_F32)
+        hipLaunchKernelGGL(obs_kernel<float>, g, b, 0, (hipStream_t)stream, boards, (float *)obs, n);
+    else
+        hipLaunchKernelGGL(obs_kernel<__hip_bfloat16>, g, b, 0, (hipStream_t)stream, boards, (__hip_bfloat16 *)obs, n);
+    return launch_status();
+}
+
+int g2048_sample_actions(g2048_stream_t stream, const float *logits, int64_t logits_stride, const uint8_t *flags,
+                         uint8_t *actions, float *logp, float *entropy, int64_t n, const g2048_rng *rng) {
+    if (n < 0 || !rng || rng->mode != G2048_RNG_PHILOX) return G2048_EINVAL;
+    if (n == 0) return G2048_OK;
+    if (!flags || !actions || (logits && logits_stride < 4)) return G2048_EINVAL;
+    hipLaunchKernelGGL(sample_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, (hipStream_t)stream, logits,
+                       logits_stride, flags, actions, logp, entropy, n, rng_args(rng));
+    return launch_status();
+}
+
+size_t g2048_reward_rtg_workspace_bytes(int64_t n) { return (size_t)blocks_for(n > 0 ? n : 1) * 3 * sizeof(double); }
+
+int g2048_rtg_prepare(g2048_stream_t stream, double *state, const g2048_reward_cfg *cfg) {
+    if (!state || !cfg) return G2048_EINVAL;
+    hipLaunchKernelGGL(rtg_prepare_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, state, cfg->beta);
+    return launch_status();
+}
+
+int g2048_reward_rtg(g2048_stream_t stream, const int32_t *points, const int8_t *pot, const uint8_t *flags,
+                     const float *value, int64_t T, int64_t n, const g2048_reward_cfg *cfg, const double *state,
+                     float *g_raw, float *g_norm, float *adv, double *partials, void *workspace,
+                     size_t workspace_bytes) {
+    if (T < 0 || n < 0 || !cfg || !state || !partials) return G2048_EINVAL;
+    if (workspace_bytes < g2048_reward_rtg_workspace_bytes(n) || !workspace) return G2048_EINVAL;
+    if (T > 0 && n > 0 && (!points || !pot || !flags || !value || !g_raw || !g_norm || !adv)) return G2048_EINVAL;
+    if (pot && ((uintptr_t)pot & 3u)) return G2048_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned nb = blocks_for(n > 0 ? n : 1);
+    const RewardArgs ra{cfg->gamma, cfg->w_points, cfg->w_mono, cfg->w_empt};
+    hipLaunchKernelGGL(rtg_kernel, dim3(nb), dim3(kBlock), 0, s, points, (const uint32_t *)pot, flags, value,
+                       (n > 0 ? T : 0), n, ra, state, g_raw, g_norm, adv, (double *)workspace);
+    hipLaunchKernelGGL(rtg_reduce_kernel, dim3(1), dim3(kBlock), 0, s, (const double *)workspace, (int)nb, partials);
+    return launch_status();
+}
+
+int g2048_rtg_finalize(g2048_stream_t stream, double *state, const double *partials, const g2048_reward_cfg *cfg) {
+    if (!state || !partials || !cfg) return G2048_EINVAL;
+    hipLaunchKernelGGL(rtg_finalize_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, state, partials, cfg->beta);
+    return launch_status();
+}
+
+const char *g2048_build_info(void) { return "libg2048 gfx950 v0.1"; }
+
+}  // extern "C"

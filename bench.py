@@ -1,0 +1,310 @@
+#!/usr/bin/env python3
+"""bench.py -- env-steps/s of the 2048 hot path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 65536] [--chunk 64]
+
+For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL).  Workload (BASELINE.md /
+SURVEY.md §8d): `--envs` independent 4x4 boards per GPU, uniform random legal actions (Philox
+keyed by 0x2048 + rank), auto-reset on done.  One bench "step" = one launch of the fused
+rollout kernel `env_rollout_kernel` = `--chunk` consecutive env steps of every board, writing the
+full per-step trajectory record (board, action, points, potentials, flags).  value = total legal
+transitions of all ranks / max-over-ranks wall time of the K timed steps (weak scaling: the boards
+per GPU are fixed; the envs are independent, so no data-path collective exists).
+
+Also reported in the same JSON line:
+  roofline       env_rollout_kernel vs HBM peak: algorithmic bytes per launch / avg launch time
+                 (HIP events on the launch stream, timed region only)
+  single_step    the one-launch-per-step kernel (env_step_kernel, 42 B/step, §8d) captured in a
+                 hipGraph, its steps/s and roofline
+  train_loop     full training iteration (policy rollout with the MLP h=196 + reward/RTG scan +
+                 PPO update with Muon/AdamW) when --train-iters > 0
+  cpu_baseline   the CPU restatement (oracle/, rank 0 only) on a bounded sample of the workload
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "2048-ppo_amd"))
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak (spec)
+ROLLOUT_STEP_BYTES = 16 + 1 + 4 + 4 + 1  # per env-step: board record, action, points, pot, flags
+ROLLOUT_LAUNCH_BYTES = 32  # per env per launch: board in + board out
+SINGLE_STEP_BYTES = 42  # board in 16 + action 1 + board out 16 + points 4 + flags 1 + pot 4
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--envs", type=int, default=65536)
+    p.add_argument("--chunk", type=int, default=64, help="env steps per rollout launch")
+    p.add_argument("--single-steps", type=int, default=256, help="graph-captured one-launch-per-step steps (0=off)")
+    p.add_argument("--train-iters", type=int, default=0, help="timed full training iterations (0=off)")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of each CPU-baseline leg (0=off)")
+    p.add_argument("--sweep", default="", help="comma list of extra board counts for the rollout kernel")
+    return p.parse_args()
+
+
+def setup_dist(args):
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return rank, world, local
+
+
+def barrier(world):
+    import torch.distributed as dist
+    if world > 1:
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: float, world: int) -> float:
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t)
+    return float(t.item())
+
+
+class RolloutBench:
+    """Fused random-legal rollout: `chunk` env steps of every board per launch."""
+
+    def __init__(self, n, chunk, rank, dev):
+        import torch
+        from g2048 import _lib as L
+        from g2048.env import VecEnv
+        self.L, self.n, self.chunk = L, n, chunk
+        self.env = VecEnv(n, dev, seed=0x2048 + rank, env_base=rank * n)
+        self.env.reset()
+        self.tb = torch.empty(chunk, n, 16, dtype=torch.int8, device=dev)
+        self.ta = torch.empty(chunk, n, dtype=torch.uint8, device=dev)
+        self.tp = torch.empty(chunk, n, dtype=torch.int32, device=dev)
+        self.tpot = torch.empty(chunk, n, 4, dtype=torch.int8, device=dev)
+        self.tf = torch.empty(chunk, n, dtype=torch.uint8, device=dev)
+        self.counter = 1
+
+    def launch(self):
+        L = self.L
+        rng = L.make_rng(L.RNG_PHILOX, self.env.seed, self.counter, self.env.env_base)
+        L.env_rollout_random(self.env.boards, self.chunk, self.tb, self.ta, self.tp, self.tpot, self.tf, rng)
+        self.counter += self.chunk
+
+    def bytes_per_launch(self):
+        return self.n * (self.chunk * ROLLOUT_STEP_BYTES + ROLLOUT_LAUNCH_BYTES)
+
+
+def time_region(fn, k, world):
+    """Barrier + sync on both sides; HIP events on the launch stream bracket the same region."""
+    import torch
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(k):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    wall = time.perf_counter() - t0
+    return wall, e0.elapsed_time(e1) / 1e3
+
+
+def bench_single_step(n, steps, rank, dev, world):
+    """One launch per env step (env_step_kernel, §8d's 42 B/step), captured in a hipGraph so host
+    launch overhead is excluded; the Philox counter base lives on the device and the graph bumps it."""
+    import torch
+    from g2048 import _lib as L
+    from g2048.env import VecEnv
+    env = VecEnv(n, dev, seed=0x3048 + rank, env_base=rank * n)
+    env.reset()
+    ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+    aout = torch.empty(n, dtype=torch.uint8, device=dev)
+    pts = torch.empty(n, dtype=torch.int32, device=dev)
+    pot = torch.empty(n, 4, dtype=torch.int8, device=dev)
+    fl = torch.empty(n, dtype=torch.uint8, device=dev)
+    per_graph = 64
+
+    def body():
+        for t in range(per_graph):
+            rng = L.make_rng(L.RNG_PHILOX, env.seed, t, env.env_base, counter_dev=ctr)
+            L.env_step(env.boards, env.boards, None, aout, pts, None, pot, fl, rng, L.OPT_AUTO_RESET)
+        ctr.add_(per_graph)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        body()  # warm-up outside capture
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        body()
+    reps = max(1, steps // per_graph)
+    g.replay()
+    torch.cuda.synchronize()
+    wall, ev = time_region(g.replay, reps, world)
+    total = reps * per_graph
+    wall = max_over_ranks(wall, world)
+    ev = max_over_ranks(ev, world)
+    avg = ev / total  # includes the per-launch dispatch gap inside the graph (conservative)
+    return {
+        "kernel": "env_step_kernel<Philox>",
+        "steps_per_s": n * total * world / wall,
+        "ms_per_env_step": wall / total * 1e3,
+        "avg_launch_us": avg * 1e6,
+        "roofline": {"bound": "hbm", "achieved": n * SINGLE_STEP_BYTES / avg / 1e9, "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": n * SINGLE_STEP_BYTES / avg / 1e9 / HBM_PEAK_GBPS,
+                     "bytes_per_step": SINGLE_STEP_BYTES},
+    }
+
+
+def cpu_baselines(seconds):
+    """CPU restatement of game.step (oracle/, incl. the 17 heuristic evaluations of game.py:981-1002),
+    random legal actions, auto-reset: (1) pure-Python loops like the reference, 1 core; (2) the C
+    oracle on all host cores.  Bounded by `seconds` each."""
+    out = {}
+    try:
+        from oracle import oracle as O
+        from oracle import pyref
+    except Exception as e:  # pragma: no cover
+        return {"error": f"oracle unavailable: {e}"}
+    # (1) pure-Python restatement, 1 core: the reference's own per-step cost structure
+    r = pyref.time_random_steps(seconds)
+    out["python_1core"] = r
+    # (2) C oracle, all cores (process pool over independent env shards)
+    import multiprocessing as mp
+    cores = min(len(os.sched_getaffinity(0)), 16)
+    n_envs, steps = 4096, 8
+    t0 = time.perf_counter()
+    _c_chunk((0, n_envs, steps))
+    one = time.perf_counter() - t0
+    steps = max(1, int(steps * seconds / max(one * 4, 1e-3)))
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(cores) as pool:
+        total = sum(pool.map(_c_chunk, [(i, n_envs, steps) for i in range(cores)]))
+    dt = time.perf_counter() - t0
+    out["c_oracle"] = {"value": total / dt, "unit": "env-steps/s", "cores": cores,
+                       "sample": f"{cores} procs x {n_envs} boards x {steps} random-legal steps, full info heuristics"}
+    return out
+
+
+def _c_chunk(args):
+    from oracle import oracle as O
+    i, n, steps = args
+    b = O.reset(n, O.RNG_PHILOX, seed=0x2048, env_base=i * n)
+    cnt, _ = O.random_rollout(b, steps, seed=0x2048, step0=1, env_base=i * n, full_info=True)
+    return cnt
+
+
+def main():
+    args = parse()
+    import torch
+    rank, world, local = setup_dist(args)
+    dev = torch.device("cuda", local)
+    from g2048 import _lib as L
+    L.load()
+
+    rb = RolloutBench(args.envs, args.chunk, rank, dev)
+    for _ in range(args.warmup):
+        rb.launch()
+    torch.cuda.synchronize()
+    wall, ev = time_region(rb.launch, args.steps, world)
+    wall = max_over_ranks(wall, world)
+    ev_max = max_over_ranks(ev, world)
+    env_steps = args.envs * args.chunk * args.steps * world
+    value = env_steps / wall
+    avg_launch = ev / args.steps
+    achieved = rb.bytes_per_launch() / avg_launch / 1e9
+
+    result = {
+        "metric": "env-steps/sec (whole node) at 65536 parallel 4x4 boards, 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8",
+        "data": "synthetic: random-legal-action rollouts (Philox keyed 0x2048+rank), auto-reset",
+        "config": {"workload": f"{args.envs} boards/GPU x {args.chunk} env steps per launch, random legal policy",
+                   "boards_per_gpu": args.envs, "env_steps_per_step": args.envs * args.chunk,
+                   "parallelism": f"env-shard x{world} (no data-path collective)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "env_rollout_kernel",
+                     "avg_launch_us": avg_launch * 1e6, "event_ms_max_rank": ev_max * 1e3,
+                     "bytes_per_launch": rb.bytes_per_launch()},
+    }
+    del rb
+    torch.cuda.empty_cache()
+
+    if args.sweep:
+        sweep = {}
+        for s in [int(x) for x in args.sweep.split(",") if x]:
+            b = RolloutBench(s, args.chunk, rank, dev)
+            b.launch()
+            torch.cuda.synchronize()
+            k = max(3, args.steps // 5)
+            w, e = time_region(b.launch, k, world)
+            sweep[str(s)] = {"env_steps_per_s_per_gpu": s * args.chunk * k / w,
+                             "achieved_GBps": b.bytes_per_launch() / (e / k) / 1e9}
+            del b
+            torch.cuda.empty_cache()
+        result["sweep"] = sweep
+
+    if args.single_steps > 0:
+        result["single_step"] = bench_single_step(args.envs, args.single_steps, rank, dev, world)
+
+    if args.train_iters > 0:
+        from g2048 import benchloop
+        result["train_loop"] = benchloop.bench_train(args, rank, world, dev)
+
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cb = cpu_baselines(args.cpu_seconds)
+        py = cb.get("python_1core")
+        if py:
+            result["cpu_baseline"] = {"value": py["value"], "unit": "env-steps/s", "cores": 1, "kind": "port",
+                                      "sample": py["sample"]}
+        if "c_oracle" in cb:
+            result["cpu_baseline_c"] = cb["c_oracle"]
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,55 @@
+"""CPU-side checks of the C ABI: the library loads and exports every symbol include/g2048.h declares,
+and the Python seam refuses CPU tensors (no silent CPU fallback)."""
+
+import ctypes
+import re
+
+import pytest
+import torch
+
+from conftest import ROOT
+
+
+def declared_functions():
+    text = (ROOT / "include" / "g2048.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(g2048_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for required in ("g2048_env_step", "g2048_env_reset", "g2048_legal_mask", "g2048_obs_encode",
+                     "g2048_sample_actions", "g2048_reward_rtg", "g2048_rtg_prepare", "g2048_rtg_finalize",
+                     "g2048_mt_seed"):
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol():
+    from g2048 import _lib
+    lib = _lib.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert set(_lib.EXPORTED) == set(declared_functions())
+    assert b"gfx950" in lib.g2048_build_info()
+    assert lib.g2048_mt_state_words() == 625
+
+
+def test_library_is_gfx950_code_object():
+    from g2048 import _lib
+    data = _lib.LIB_PATH.read_bytes()
+    assert b"gfx950" in data
+
+
+def test_cpu_tensors_are_rejected():
+    from g2048 import _lib
+    b = torch.zeros(4, 16, dtype=torch.int8)
+    f = torch.zeros(4, dtype=torch.uint8)
+    with pytest.raises(_lib.G2048Error):
+        _lib.legal_mask(b, f)
+
+
+def test_struct_layouts_match_header():
+    from g2048 import _lib
+    assert ctypes.sizeof(_lib.Rng) == 48
+    assert _lib.Rng.counter_dev.offset == 24
+    assert ctypes.sizeof(_lib.RewardCfg) == 40

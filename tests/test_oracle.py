@@ -169,3 +169,32 @@ def test_random_rollout_counts():
     n, b2 = O.random_rollout(b, 50, seed=0x2048)
     assert n == 64 * 50
     assert ((b2 >= 0) & (b2 <= 17)).all()
+
+
+def test_pure_python_restatement_matches_golden_games(games):
+    """oracle/pyref.py (the CPU-baseline loop) replays the reference games exactly, info included."""
+    import random
+    from oracle import pyref
+    g = games
+    for s in range(8):
+        rnd = random.Random(s)
+        b = pyref.reset(rnd)
+        assert b == g["init_boards"][s].tolist()
+        for i in np.nonzero(g["game"] == s)[0]:
+            assert b == g["before"][i].tolist()
+            pts, done, info = pyref.step(b, int(g["action"][i]), rnd)
+            assert pts == g["points"][i] and done == bool(g["done"][i])
+            assert b == g["after"][i].tolist()
+            if not info["invalid_move"]:
+                assert info["monotonicity_before"] == g["mono_b"][i] and info["monotonicity_after"] == g["mono_a"][i]
+                assert info["emptiness_before"] == g["empt_b"][i] and info["emptiness_after"] == g["empt_a"][i]
+                for key, gk in (("smoothness_delta", "smooth_d"), ("corner_delta", "corner_d"),
+                                ("adjacency_delta", "adj_d"), ("chain_delta", "chain_d"),
+                                ("topological_delta", "topo_d")):
+                    assert info[key] == g[gk][i], key
+
+
+def test_pure_python_baseline_runs():
+    from oracle import pyref
+    r = pyref.time_random_steps(0.3)
+    assert r["steps"] > 100 and r["value"] > 0
