@@ -1,0 +1,260 @@
+"""agent.py -- the policy/value nn.Module interface of the 2048 trainer.
+
+The reference's `agent.py` is empty; its modules live in game.py (GameMLP game.py:1049-1220,
+GameURM game.py:1355-1458, configs game.py:24-42).  This module provides the same call contract
+and the same state_dict keys, so a reference checkpoint (docs/data/best_model.pt, written by
+train.py:1893-1901) loads unchanged:
+
+  forward(x[B,48]) -> (logits[B,4], value[B,1]), logits ordered UP, DOWN, LEFT, RIGHT
+  .directions, .get_param_groups(value_lr, other_lr), .action_head, .value_head
+
+Sub-modules are created in the reference's order and re-initialised with the same Kaiming-uniform
+scheme, so under the same torch seed the initial weights are identical to the reference's.
+On MI355X the heavy lifting is hipBLASLt GEMMs (bf16 MFMA under autocast) from these modules in
+the update, and the fused HIP rollout policy (g2048.policy) during rollouts.
+"""
+
+from __future__ import annotations
+
+from enum import Enum
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from pydantic import BaseModel
+
+N_CELLS = 16
+N_FEATURES = 3 * N_CELLS
+N_ACTIONS = 4
+
+
+class Direction(Enum):
+    """game.py:14-18; also the model head order (game.py:1087-1092)."""
+    UP = "up"
+    DOWN = "down"
+    LEFT = "left"
+    RIGHT = "right"
+
+
+ACTION_ORDER = [Direction.UP, Direction.DOWN, Direction.LEFT, Direction.RIGHT]
+
+
+class MLPConfig(BaseModel):
+    hidden_dim: int = 64
+    num_layers: int = 2
+    dropout: float = 0.1
+    decouple_critic: bool = False
+
+
+class GameURMConfig(BaseModel):
+    hidden_dim: int = 64
+    num_layers: int = 2
+    num_heads: int = 4
+    expansion: float = 2.67
+    dropout: float = 0.1
+    num_loops: int = 4
+    num_truncated_loops: int = 1
+    conv_kernel: int = 2
+    rms_norm_eps: float = 1e-5
+
+
+def _kaiming_linear(m: nn.Module) -> None:
+    if isinstance(m, nn.Linear):
+        nn.init.kaiming_uniform_(m.weight, nonlinearity="relu")
+        if m.bias is not None:
+            nn.init.zeros_(m.bias)
+
+
+def _split_param_groups(model: nn.Module, value_lr: float, other_lr: float) -> list[dict]:
+    """[other 2-D, other 1-D, value-head 2-D, value-head 1-D] (game.py:1093-1127): 2-D go to Muon,
+    1-D (LayerNorm, biases) to AdamW in the trainer."""
+    groups = {("o", 2): [], ("o", 1): [], ("v", 2): [], ("v", 1): []}
+    for name, child in model.named_children():
+        side = "v" if name == "value_head" else "o"
+        for p in child.parameters():
+            groups[(side, 2 if p.ndim >= 2 else 1)].append(p)
+    return [{"params": groups[("o", 2)], "lr": other_lr}, {"params": groups[("o", 1)], "lr": other_lr},
+            {"params": groups[("v", 2)], "lr": value_lr}, {"params": groups[("v", 1)], "lr": value_lr}]
+
+
+class ResidualBlock(nn.Module):
+    """x + Dropout(ReLU(LayerNorm(W x)))  (game.py:1033-1046)."""
+
+    def __init__(self, hidden_dim: int, dropout: float = 0.1):
+        super().__init__()
+        self.mlp = nn.Sequential(nn.Linear(hidden_dim, hidden_dim, bias=False), nn.LayerNorm(hidden_dim), nn.ReLU(),
+                                 nn.Dropout(dropout))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return x + self.mlp(x)
+
+
+class GameMLP(nn.Module):
+    """Residual MLP policy + value heads (game.py:1049-1220)."""
+
+    N = N_CELLS
+    NUM_ACTIONS = N_ACTIONS
+
+    def __init__(self, config: MLPConfig) -> None:
+        super().__init__()
+        h = config.hidden_dim
+        self.config = config
+        self.decouple_critic = config.decouple_critic
+        self.stem = nn.Sequential(nn.Linear(N_FEATURES, h, bias=False), nn.LayerNorm(h), nn.ReLU())
+        self.backbone = nn.ModuleList(ResidualBlock(h, config.dropout) for _ in range(config.num_layers))
+        self.action_head = nn.Linear(h, N_ACTIONS)
+        self.value_head = nn.Linear(h, 1)
+        self.apply(_kaiming_linear)
+
+    @property
+    def directions(self) -> list[Direction]:
+        return list(ACTION_ORDER)
+
+    def get_param_groups(self, value_lr: float, other_lr: float) -> list[dict]:
+        return _split_param_groups(self, value_lr, other_lr)
+
+    def get_1d_and_2d_params(self) -> tuple[list, list]:
+        one = [p for p in self.parameters() if p.ndim == 1]
+        two = [p for p in self.parameters() if p.ndim >= 2]
+        return one, two
+
+    def features(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.stem(x)
+        for block in self.backbone:
+            x = block(x)
+        return x
+
+    def forward(self, inputs: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        if inputs.ndim <= 1:
+            raise ValueError(f"input must consist of shape (batch, channel), got: {inputs.shape}")
+        if inputs.shape[-1] != N_FEATURES:
+            raise AssertionError(f"{inputs.shape[-1]} does not equal {N_FEATURES}")
+        x = self.features(inputs.to(torch.float32))
+        logits = self.action_head(x)
+        value = self.value_head(x.detach() if self.decouple_critic else x)
+        return logits, value
+
+
+# ------------------------------------------------------------------------------------ URM ------
+def rms_norm(x: torch.Tensor, eps: float) -> torch.Tensor:
+    """Parameter-free RMSNorm computed in float32 (game.py:1223-1229)."""
+    dt = x.dtype
+    x32 = x.to(torch.float32)
+    return (x32 * torch.rsqrt(x32.pow(2).mean(-1, keepdim=True) + eps)).to(dt)
+
+
+class GameConvSwiGLU(nn.Module):
+    """SwiGLU + depthwise causal-trimmed Conv1d over the 16 cells (game.py:1232-1276)."""
+
+    def __init__(self, hidden_size: int, expansion: float, conv_kernel: int = 2):
+        super().__init__()
+        inter = round(expansion * hidden_size * 2 / 3)
+        inter = -(-inter // 8) * 8
+        self.inter = inter
+        self.gate_up_proj = nn.Linear(hidden_size, 2 * inter, bias=False)
+        self.dwconv = nn.Conv1d(inter, inter, kernel_size=conv_kernel, padding=conv_kernel // 2, groups=inter,
+                                bias=True)
+        self.down_proj = nn.Linear(inter, hidden_size, bias=False)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        gate, up = self.gate_up_proj(x).chunk(2, dim=-1)
+        y = F.silu(gate) * up                                        # [B, S, I]
+        y = self.dwconv(y.transpose(1, 2))[..., : x.shape[1]]       # [B, I, S] trimmed to S
+        return self.down_proj(F.silu(y).transpose(1, 2).contiguous())
+
+
+class GameURMAttention(nn.Module):
+    """Bidirectional multi-head self-attention over the 16 cells (game.py:1279-1317)."""
+
+    def __init__(self, hidden_size: int, num_heads: int, dropout: float = 0.0):
+        super().__init__()
+        self.hidden_size = hidden_size
+        self.num_heads = num_heads
+        self.head_dim = hidden_size // num_heads
+        self.dropout = dropout
+        self.qkv_proj = nn.Linear(hidden_size, 3 * hidden_size, bias=False)
+        self.o_proj = nn.Linear(hidden_size, hidden_size, bias=False)
+
+    def forward(self, h: torch.Tensor) -> torch.Tensor:
+        b, s, _ = h.shape
+        q, k, v = self.qkv_proj(h).view(b, s, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).unbind(0)
+        o = F.scaled_dot_product_attention(q, k, v, dropout_p=self.dropout if self.training else 0.0, is_causal=False)
+        return self.o_proj(o.transpose(1, 2).reshape(b, s, self.hidden_size))
+
+
+class GameURMBlock(nn.Module):
+    """post-norm: h = rms(h + attn(h)); h = rms(h + mlp(h))  (game.py:1320-1352)."""
+
+    def __init__(self, config: GameURMConfig):
+        super().__init__()
+        self.attn = GameURMAttention(config.hidden_dim, config.num_heads, config.dropout)
+        self.mlp = GameConvSwiGLU(config.hidden_dim, config.expansion, config.conv_kernel)
+        self.norm_eps = config.rms_norm_eps
+
+    def forward(self, h: torch.Tensor) -> torch.Tensor:
+        h = rms_norm(h + self.attn(h), self.norm_eps)
+        return rms_norm(h + self.mlp(h), self.norm_eps)
+
+
+class GameURM(nn.Module):
+    """Universal-reasoning transformer policy (game.py:1355-1458): shared blocks looped num_loops
+    times over the 16 cell tokens, the first num_truncated_loops without gradient, mean-pooled heads."""
+
+    N = N_CELLS
+    NUM_ACTIONS = N_ACTIONS
+
+    def __init__(self, config: GameURMConfig):
+        super().__init__()
+        self.config = config
+        h = config.hidden_dim
+        self.stem = nn.Sequential(nn.Linear(3, h, bias=False), nn.LayerNorm(h), nn.SiLU())
+        self.layers = nn.ModuleList(GameURMBlock(config) for _ in range(config.num_layers))
+        self.init_hidden = nn.Parameter(torch.zeros(1, N_CELLS, h))
+        nn.init.trunc_normal_(self.init_hidden, std=0.02)
+        self.action_head = nn.Linear(h, N_ACTIONS)
+        self.value_head = nn.Linear(h, 1)
+        for m in self.modules():
+            _kaiming_linear(m)
+
+    @property
+    def directions(self) -> list[Direction]:
+        return list(ACTION_ORDER)
+
+    def get_param_groups(self, value_lr: float, other_lr: float) -> list[dict]:
+        return _split_param_groups(self, value_lr, other_lr)
+
+    def _loop(self, h: torch.Tensor, emb: torch.Tensor) -> torch.Tensor:
+        h = h + emb
+        for layer in self.layers:
+            h = layer(h)
+        return h
+
+    def forward(self, inputs: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        if inputs.ndim == 1:
+            inputs = inputs.unsqueeze(0)
+        b = inputs.shape[0]
+        emb = self.stem(inputs.view(b, N_CELLS, 3))
+        h = self.init_hidden.expand(b, -1, -1).clone()
+        n_trunc = self.config.num_truncated_loops
+        if n_trunc > 0:
+            with torch.no_grad():
+                for _ in range(n_trunc):
+                    h = self._loop(h, emb)
+        for _ in range(self.config.num_loops - n_trunc):
+            h = self._loop(h, emb)
+        pooled = h.mean(dim=1)
+        return self.action_head(pooled), self.value_head(pooled)
+
+
+def mlp_flops_per_sample(hidden: int, layers: int) -> int:
+    """Forward FLOPs of GameMLP per board (2 x MACs of the linears)."""
+    macs = N_FEATURES * hidden + layers * hidden * hidden + hidden * (N_ACTIONS + 1)
+    return 2 * macs
+
+
+def param_count(model: nn.Module) -> int:
+    return sum(p.numel() for p in model.parameters())
+
+
+__all__ = ["Direction", "MLPConfig", "GameURMConfig", "ResidualBlock", "GameMLP", "rms_norm", "GameConvSwiGLU",
+           "GameURMAttention", "GameURMBlock", "GameURM", "mlp_flops_per_sample", "param_count"]

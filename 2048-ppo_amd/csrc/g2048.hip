@@ -188,6 +188,22 @@ __global__ __launch_bounds__(kBlock) void env_reset_kernel(uint4 *__restrict__ b
     if (flags) flags[i] = (uint8_t)legal_mask(b);
 }
 
+// preview_move_rewards (game.py:167-184): merge points of each direction, 0 where illegal.
+__global__ __launch_bounds__(kBlock) void preview_kernel(const uint4 *__restrict__ boards, int4 *__restrict__ out,
+                                                         int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint4 b = boards[i];
+    int r[4];
+#pragma unroll
+    for (uint32_t a = 0; a < 4u; a++) {
+        uint32_t pts, mx;
+        const uint4 m = apply_move(b, a, pts, mx);
+        r[a] = eq4(m, b) ? 0 : (int)pts;
+    }
+    out[i] = make_int4(r[0], r[1], r[2], r[3]);
+}
+
 __global__ __launch_bounds__(kBlock) void legal_kernel(const uint4 *__restrict__ boards, uint8_t *__restrict__ flags,
                                                        int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -508,6 +524,14 @@ int g2048_env_rollout_random(g2048_stream_t stream, int8_t *boards, int64_t n, i
     hipLaunchKernelGGL(env_rollout_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, (hipStream_t)stream, (uint4 *)boards, n,
                        steps, (uint4 *)traj_boards, traj_actions, traj_points, (uint32_t *)traj_pot, traj_flags,
                        rng_args(rng));
+    return launch_status();
+}
+
+int g2048_preview_points(g2048_stream_t stream, const int8_t *boards, int32_t *points4, int64_t n) {
+    if (n < 0 || (n > 0 && (!boards || !points4 || !aligned16(boards) || !aligned16(points4)))) return G2048_EINVAL;
+    if (n == 0) return G2048_OK;
+    hipLaunchKernelGGL(preview_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, (hipStream_t)stream, (const uint4 *)boards,
+                       (int4 *)points4, n);
     return launch_status();
 }
 

@@ -24,7 +24,7 @@ RTG_STATE_DOUBLES = 8
 
 EXPORTED = (
     "g2048_mt_state_words", "g2048_mt_seed", "g2048_env_reset", "g2048_env_step", "g2048_env_rollout_random",
-    "g2048_legal_mask",
+    "g2048_preview_points", "g2048_legal_mask",
     "g2048_obs_encode", "g2048_sample_actions", "g2048_rtg_prepare", "g2048_reward_rtg_workspace_bytes",
     "g2048_reward_rtg", "g2048_rtg_finalize", "g2048_build_info",
 )
@@ -74,6 +74,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_env_reset": (ctypes.c_int, [vp, vp, vp, vp, i64, rp]),
         "g2048_env_step": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, rp, u32]),
         "g2048_env_rollout_random": (ctypes.c_int, [vp, vp, i64, i64, vp, vp, vp, vp, vp, rp]),
+        "g2048_preview_points": (ctypes.c_int, [vp, vp, vp, i64]),
         "g2048_legal_mask": (ctypes.c_int, [vp, vp, vp, i64]),
         "g2048_obs_encode": (ctypes.c_int, [vp, vp, vp, i32, i64]),
         "g2048_sample_actions": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp, i64, rp]),
@@ -147,6 +148,11 @@ def env_rollout_random(boards, steps, traj_boards, traj_actions, traj_points, tr
         _dev(traj_boards, torch.int8, "traj_boards"), _dev(traj_actions, torch.uint8, "traj_actions"),
         _dev(traj_points, torch.int32, "traj_points"), _dev(traj_pot, torch.int8, "traj_pot"),
         _dev(traj_flags, torch.uint8, "traj_flags"), ctypes.byref(rng)), "g2048_env_rollout_random")
+
+
+def preview_points(boards, points4):
+    _check(load().g2048_preview_points(_stream(boards), _dev(boards, torch.int8, "boards"),
+                                       _dev(points4, torch.int32, "points4"), boards.shape[0]), "g2048_preview_points")
 
 
 def legal_mask(boards, flags):

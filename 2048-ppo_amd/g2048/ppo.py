@@ -1,0 +1,128 @@
+"""PPO-clip policy-gradient update (model_optimize_step, train.py:414-642), tensor-native.
+
+Per minibatch (same math as the reference):
+  masked = logits.masked_fill(invalid, -inf);  logpi = log_softmax(masked)            :497-515
+  rho = exp(clamp(logpi(a) - logpi_old(a), -20, 20));  ppo = min(A rho, A clip(rho, 0.8, 1.2)) :517-523
+  H = -sum_valid softmax(clamp(masked, -20, 20)) * log_softmax(...)                  :531-535
+  v = smooth_l1(V, G_norm)                                                           :544-546
+  loss = -mean(ppo - c v + beta H);  backward;  [all-reduce];  clip 1.0;  Muon+AdamW  :553-568
+  KL(old || new) diagnostic on a no-grad re-forward (train mode, as in the reference) :578-601
+Differences by design: minibatches are gathered on the device from the flat [T*N] trajectory with
+a device permutation (no DataLoader, no per-sample Python), statistics stay on the device (one
+host sync per train step), and the forward runs under bf16 autocast on MI355X.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+STAT_KEYS = ("loss", "policy_loss", "entropy_loss", "value_loss", "grad_norm", "entropy", "kl_total", "kl_average",
+             "kl_max")
+
+
+@dataclass
+class PPOConfig:
+    batch_size: int = 65536
+    epochs: int = 1
+    clip_eps: float = 0.2
+    critic: float = 1.0          # --critic (critic_strength)
+    max_grad_norm: float = 1.0
+    amp_dtype: torch.dtype | None = torch.bfloat16
+
+
+def invalid_from_legal(legal: torch.Tensor) -> torch.Tensor:
+    """uint8 legal mask (bit a = action a legal) -> bool [B,4] invalid mask (train.py:268)."""
+    bits = torch.arange(4, device=legal.device, dtype=torch.int32)
+    return ((legal.to(torch.int32).unsqueeze(-1) >> bits) & 1) == 0
+
+
+def ppo_losses(logits, value, actions, invalid, old_logp, adv, ret, beta, critic, clip_eps=0.2):
+    """Returns (loss, parts) for one minibatch; logits/value float32."""
+    masked = logits.masked_fill(invalid, float("-inf"))
+    new_lp_all = masked.log_softmax(dim=-1)
+    a = actions.long().unsqueeze(1)
+    new_lp = new_lp_all.gather(1, a).squeeze(1)
+    old_lp = old_logp.gather(1, a).squeeze(1)
+    ratio = (new_lp - old_lp).clamp(-20, 20).exp()
+    ppo = torch.minimum(adv * ratio, adv * ratio.clamp(1 - clip_eps, 1 + clip_eps))
+    lp2 = masked.clamp(-20, 20).log_softmax(dim=-1)
+    ent = -(lp2 * lp2.exp()).masked_fill(invalid, 0.0).sum(dim=-1)
+    v = value.reshape(-1)
+    vloss = F.smooth_l1_loss(v, ret, reduction="none")
+    loss = -(ppo - critic * vloss + beta * ent).mean()
+    return loss, {"ppo": ppo, "entropy": ent, "vloss": vloss, "masked": masked}
+
+
+def kl_old_new(old_masked_logits, new_logits, invalid):
+    """torch.masked KL(old || new) over valid actions (train.py:594-601)."""
+    new_masked = new_logits.masked_fill(invalid, float("-inf"))
+    lo = old_masked_logits.log_softmax(dim=-1)
+    ln = new_masked.log_softmax(dim=-1)
+    term = lo.exp() * (lo - ln)
+    return term.masked_fill(invalid, 0.0).sum(dim=-1)
+
+
+class PPOUpdater:
+    """Minibatch PPO over a flat trajectory.  `grads` is a dist.GradBucket (flat .grad views)."""
+
+    def __init__(self, model, optimizer, cfg: PPOConfig, grads, generator: torch.Generator | None = None):
+        self.model, self.opt, self.cfg, self.grads = model, optimizer, cfg, grads
+        self.gen = generator
+        self.dev = next(model.parameters()).device
+        self.stats = torch.zeros(len(STAT_KEYS), dtype=torch.float32, device=self.dev)
+
+    def _forward(self, obs):
+        if self.cfg.amp_dtype is not None and obs.is_cuda:
+            with torch.autocast("cuda", dtype=self.cfg.amp_dtype):
+                logits, value = self.model(obs)
+        else:
+            logits, value = self.model(obs)
+        return logits.float(), value.float()
+
+    def update(self, data: dict, beta: float, encode) -> dict:
+        """data: flat tensors boards [M,16] int8, actions [M], legal [M] uint8, logp [M,4], adv [M], ret [M].
+        `encode(boards) -> obs [B,48]` builds the model input of a gathered minibatch."""
+        cfg = self.cfg
+        m_total = data["actions"].shape[0]
+        bs = min(cfg.batch_size, m_total)
+        self.stats.zero_()
+        nb = 0
+        self.model.train()
+        for _ in range(cfg.epochs):
+            perm = torch.randperm(m_total, device=self.dev, generator=self.gen)
+            for s in range(0, m_total, bs):
+                idx = perm[s:s + bs]
+                self._minibatch(idx, data, beta, encode)
+                nb += 1
+        st = self.stats / max(nb, 1)
+        st[STAT_KEYS.index("kl_max")] = self.stats[STAT_KEYS.index("kl_max")]
+        return {k: st[i] for i, k in enumerate(STAT_KEYS)}
+
+    def _minibatch(self, idx, data, beta, encode):
+        cfg = self.cfg
+        obs = encode(data["boards"].index_select(0, idx))
+        actions = data["actions"].index_select(0, idx)
+        invalid = invalid_from_legal(data["legal"].index_select(0, idx))
+        old_logp = data["logp"].index_select(0, idx)
+        adv = data["adv"].index_select(0, idx)
+        ret = data["ret"].index_select(0, idx)
+        logits, value = self._forward(obs)
+        loss, parts = ppo_losses(logits, value, actions, invalid, old_logp, adv, ret, beta, cfg.critic, cfg.clip_eps)
+        self.grads.zero()
+        loss.backward()
+        self.grads.allreduce_mean()
+        gn = self.grads.clip_(cfg.max_grad_norm)
+        self.opt.step()
+        with torch.no_grad():
+            new_logits, _ = self._forward(obs)
+            kl = kl_old_new(parts["masked"].detach(), new_logits, invalid)
+            vals = torch.stack([
+                loss.detach(), -parts["ppo"].detach().mean(), -beta * parts["entropy"].detach().mean(),
+                cfg.critic * parts["vloss"].detach().mean(), gn, parts["entropy"].detach().mean(), kl.sum(),
+                kl.mean(), torch.zeros((), device=self.dev)])
+            self.stats.add_(vals)
+            k = STAT_KEYS.index("kl_max")
+            self.stats[k] = torch.maximum(self.stats[k], kl.max())

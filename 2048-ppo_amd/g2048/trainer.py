@@ -1,0 +1,323 @@
+"""Vectorised trainer: rollout -> reward/RTG/advantage -> PPO update, all on the device
+(the train() loop of train.py:1669-1908 for N envs per GPU, one process per GPU).
+
+Two rollout modes:
+  episodic (horizon = 0, the reference's semantics): every env plays exactly one full game per
+      train step (play_game_for_episode / play_games_batched); finished envs go inactive
+      (G2048_OPT_SKIP_DONE) and the step ends when every game is over or --max-steps is reached.
+  fixed horizon (horizon = T > 0, throughput mode): T steps of every env per train step with
+      auto-reset; returns are cut at episode ends and bootstrap 0 at the horizon, like --max-steps.
+"""
+
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+
+import torch
+
+from . import _lib as L
+from .advantage import RewardWeights, RTGTracker
+from .dist import GradBucket, allreduce_sum_, world
+from .optim import build_optimizer
+from .ppo import PPOConfig, PPOUpdater
+from .rollout import InferencePolicy, Rollout
+
+
+@dataclass
+class TrainConfig:
+    steps: int = 1000
+    lr: float = 1e-3
+    critic_lr: float = 1e-3
+    gamma: float = 0.99
+    entropy: float = 0.1
+    critic: float = 1.0
+    episodes: int = 1              # envs per rank (--episodes)
+    batch_size: int = 1
+    epochs: int = 1
+    max_steps: int | None = None
+    hidden: int = 64
+    num_layers: int = 2
+    dropout: float = 0.1
+    decouple_critic: bool = False
+    points: float = 0.0
+    mono: float = 0.0
+    emptiness: float = 0.0
+    rtg_beta: float = 0.9
+    warmup_steps: int = 200
+    beta1: float = 0.9
+    beta2: float = 0.999
+    weight_decay: float = 0.01
+    adaptive_beta: bool = False
+    target_entropy: float = 0.7
+    beta_min: float = 0.001
+    beta_max: float = 1.0
+    beta_lr: float = 0.01
+    horizon: int = 0
+    seed: int = 0x2048
+    graph: bool = True
+    amp: bool = True
+    episodic_cap: int = 4096       # step cap of an episodic rollout without --max-steps
+    chunk: int = 32                # episodic: steps between "all games over?" checks
+    unused_weights: dict = field(default_factory=dict)
+
+
+class VecTrainer:
+    def __init__(self, cfg: TrainConfig, device, model: torch.nn.Module | None = None):
+        import agent
+        self.cfg = cfg
+        self.dev = torch.device(device)
+        self.rank, self.world = world()
+        if model is None:
+            model = agent.GameMLP(agent.MLPConfig(hidden_dim=cfg.hidden, num_layers=cfg.num_layers,
+                                                  dropout=cfg.dropout, decouple_critic=cfg.decouple_critic))
+            with torch.no_grad():  # train.py:1559-1567
+                model.action_head.weight.zero_()
+                model.action_head.bias.zero_()
+                model.value_head.weight.zero_()
+                model.value_head.bias.zero_()
+        self.model = model.to(self.dev)
+        if self.world > 1:  # identical initial replicas
+            for p in self.model.parameters():
+                torch.distributed.broadcast(p.data, 0)
+        self.grads = GradBucket(self.model.parameters())
+        self.opt = build_optimizer(self.model, cfg.lr, cfg.critic_lr, cfg.beta1, cfg.beta2, cfg.weight_decay,
+                                   cfg.warmup_steps, cfg.steps)
+        self.policy = InferencePolicy(self.model, torch.bfloat16 if cfg.amp else torch.float32)
+        n = cfg.episodes
+        self.episodic = cfg.horizon <= 0
+        T = cfg.horizon if not self.episodic else (cfg.max_steps or cfg.episodic_cap)
+        if self.episodic:
+            T = int(math.ceil(T / cfg.chunk) * cfg.chunk)
+        self.rollout = Rollout(n, T, self.dev, seed=cfg.seed + 7919 * self.rank, env_base=self.rank * n,
+                               episodic=self.episodic, obs_dtype=torch.bfloat16 if cfg.amp else torch.float32)
+        self.weights = RewardWeights(cfg.gamma, cfg.points, cfg.mono, cfg.emptiness, cfg.rtg_beta)
+        self.rtg = RTGTracker(n, self.dev, self.weights, allreduce=allreduce_sum_ if self.world > 1 else None)
+        gen = torch.Generator(device=self.dev)
+        gen.manual_seed(cfg.seed + 104729 * self.rank)
+        self.ppo = PPOUpdater(self.model, self.opt, PPOConfig(batch_size=cfg.batch_size, epochs=cfg.epochs,
+                                                              critic=cfg.critic,
+                                                              amp_dtype=torch.bfloat16 if cfg.amp else None),
+                              self.grads, gen)
+        self.beta = cfg.entropy
+        self.obs_mb = None
+        self.run_score = torch.zeros(n, dtype=torch.int64, device=self.dev)
+        self.run_maxexp = torch.zeros(n, dtype=torch.int32, device=self.dev)
+        self.highest = 0
+        self.ema = {"avg_score": 0.0, "pct_512": 0.0, "pct_1024": 0.0, "pct_2048": 0.0, "explained_var": 0.0}
+        self._started = False
+        self._chunk_graphs = {}
+
+    # ------------------------------------------------------------------ rollout ---------------
+    def _encode(self, boards: torch.Tensor) -> torch.Tensor:
+        if self.obs_mb is None or self.obs_mb.shape[0] != boards.shape[0]:
+            self.obs_mb = torch.empty(boards.shape[0], 48, dtype=torch.float32, device=self.dev)
+        L.obs_encode(boards.contiguous(), self.obs_mb)
+        return self.obs_mb
+
+    def _collect_episodic(self):
+        ro, b = self.rollout, self.rollout.buf
+        ro.reset()
+        self.run_score.zero_()
+        self.run_maxexp.zero_()
+        used = 0
+        for c0 in range(0, ro.T, self.cfg.chunk):
+            key = c0
+            if self.cfg.graph:
+                g = self._chunk_graphs.get(key)
+                if g is None:
+                    g = self._capture_chunk(c0)
+                    self._chunk_graphs[key] = g
+                g.replay()
+            else:
+                for t in range(c0, c0 + self.cfg.chunk):
+                    ro._step(t, self.policy)
+            used = c0 + self.cfg.chunk
+            if bool(((b.flags[used] & L.FLAG_LEGAL) == 0).all()):  # every game is over
+                break
+        ro.counter.add_(2 * ro.T)
+        return used
+
+    def _capture_chunk(self, c0):
+        ro = self.rollout
+        b = ro.buf
+        snap = (b.boards[c0].clone(), b.flags[c0].clone())
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for t in range(c0, c0 + self.cfg.chunk):
+                ro._step(t, self.policy)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for t in range(c0, c0 + self.cfg.chunk):
+                ro._step(t, self.policy)
+        b.boards[c0].copy_(snap[0])
+        b.flags[c0].copy_(snap[1])
+        return g
+
+    # ------------------------------------------------------------------ train step ------------
+    def train_step(self, step: int) -> dict:
+        cfg, ro, b = self.cfg, self.rollout, self.rollout.buf
+        self.model.eval()
+        self.policy.sync()
+        if self.episodic:
+            T = self._collect_episodic()
+        else:
+            if not self._started:
+                ro.reset()
+                self._started = True
+            else:
+                b.carry_over()
+            ro.collect(self.policy, graph=cfg.graph)
+            T = ro.T
+        sf = b.step_flags[:T]
+        self.rtg.compute(b.points[:T], b.pot[:T], sf, b.value[:T], b.g_raw[:T], b.g_norm[:T], b.adv[:T])
+        n = ro.n
+        data = {"boards": b.boards[:T].reshape(T * n, 16), "actions": b.actions[:T].reshape(-1),
+                "legal": b.flags[:T].reshape(-1), "logp": b.logp[:T].reshape(T * n, 4),
+                "adv": b.adv[:T].reshape(-1), "ret": b.g_norm[:T].reshape(-1)}
+        valid = None
+        if self.episodic:
+            valid_mask = (sf & L.FLAG_INACTIVE) == 0
+            valid = torch.nonzero(valid_mask.reshape(-1)).squeeze(1)
+            data = {k: v.index_select(0, valid) for k, v in data.items()}
+        ustats = self.ppo.update(data, self.beta, self._encode)
+        self.opt.scheduler_step()
+        metrics = self._metrics(T, valid, ustats)
+        if cfg.adaptive_beta:  # train.py:1740-1746
+            err = cfg.target_entropy - metrics["entropy"]
+            self.beta = max(cfg.beta_min, min(cfg.beta_max, self.beta * (1.0 + cfg.beta_lr * err)))
+        metrics["current_beta"] = self.beta
+        return metrics
+
+    # ------------------------------------------------------------------ metrics ---------------
+    def _episode_stats(self, T):
+        """Per-episode (score, max tile exponent) of the games that finished in this rollout."""
+        b = self.rollout.buf
+        sf = b.step_flags[:T]
+        done = ((sf & L.FLAG_DONE) != 0) & ((sf & L.FLAG_INACTIVE) == 0)
+        scores, tiles = [], []
+        if self.episodic:
+            pts = torch.where((sf & L.FLAG_INACTIVE) == 0, b.points[:T], 0).sum(0)
+            mx = b.boards[T].max(dim=1).values.to(torch.int32)
+            return pts, mx, torch.ones_like(pts, dtype=torch.bool)
+        rs, rm = self.run_score, self.run_maxexp
+        for t in range(T):
+            rs += b.points[t]
+            rm = torch.maximum(rm, torch.maximum(b.boards[t].max(dim=1).values.to(torch.int32),
+                                                 b.max_tile[t].to(torch.int32)))
+            d = done[t]
+            scores.append(torch.where(d, rs, -1))
+            tiles.append(torch.where(d, rm, -1))
+            rs = torch.where(d, 0, rs)
+            rm = torch.where(d, 0, rm)
+        self.run_score, self.run_maxexp = rs, rm
+        s, m = torch.stack(scores), torch.stack(tiles)
+        fin = s >= 0
+        return s[fin], m[fin], None
+
+    def _metrics(self, T, valid, ustats) -> dict:
+        b, w = self.rollout.buf, self.weights
+        sf = b.step_flags[:T]
+        done = ((sf & L.FLAG_DONE) != 0).float()
+        pot = b.pot[:T].float()
+        r = (b.points[:T].float() * w.points + w.mono * (w.gamma * pot[..., 1] * (1 - done) - pot[..., 0])
+             + w.emptiness * (w.gamma * pot[..., 3] * (1 - done) - pot[..., 2]))
+        fields = [r, b.adv[:T], b.g_norm[:T], b.g_raw[:T], b.value[:T]]
+        if valid is not None:
+            fields = [f.reshape(-1).index_select(0, valid) for f in fields]
+        else:
+            fields = [f.reshape(-1) for f in fields]
+        r, a, gn, gr, v = fields
+        starts = torch.zeros_like(sf, dtype=torch.bool)
+        if self.episodic:
+            starts[0] = True
+        else:
+            starts[1:] = (sf[:-1] & L.FLAG_RESET) != 0
+        g0 = b.g_raw[:T][starts]
+        scores, tiles, _ = self._episode_stats(T)
+        dev = self.dev
+        zero = torch.zeros((), device=dev)
+        vec = torch.stack([
+            torch.tensor(float(r.numel()), device=dev), r.mean(), r.var(unbiased=False), (r == 0).float().mean() * 100,
+            a.mean(), a.var(unbiased=False), a.pow(2).sum().sqrt(), a.min(), a.max(),
+            gn.mean(), gn.std(unbiased=False), gn.min(), gn.max(), gr.std(unbiased=False), v.std(unbiased=False),
+            g0.mean() if g0.numel() else zero,
+            scores.float().mean() if scores.numel() else zero,
+            scores.float().median() if scores.numel() else zero,
+            scores.max().float() if scores.numel() else zero,
+            (tiles >= 9).float().mean() * 100 if tiles.numel() else zero,
+            (tiles >= 10).float().mean() * 100 if tiles.numel() else zero,
+            (tiles >= 11).float().mean() * 100 if tiles.numel() else zero,
+            torch.tensor(float(scores.numel()), device=dev),
+            *[ustats[k] for k in ("loss", "policy_loss", "entropy_loss", "value_loss", "grad_norm", "entropy",
+                                  "kl_total", "kl_average", "kl_max")],
+        ]).tolist()  # the one host synchronisation of the train step
+        (n, rm, rv, zr, am, av, al2, amin, amax, gnm, gns, gnmin, gnmax, grs, vs, g0m, avg_s, med_s, max_s, p512,
+         p1024, p2048, n_eps, loss, pl, el, vl, gnorm, ent, klt, kla, klm) = vec
+        if n_eps > 0:
+            self.highest = max(self.highest, int(max_s))
+            d = 0.001
+            for k, val in (("avg_score", avg_s), ("pct_512", p512), ("pct_1024", p1024), ("pct_2048", p2048)):
+                self.ema[k] = (1 - d) * self.ema[k] + d * val
+        explained = 1.0 - av / (gns ** 2) if gns > 0 else 0.0
+        self.ema["explained_var"] = (1 - 0.001) * self.ema["explained_var"] + 0.001 * explained
+        lrs = [g["lr"] for g in self.opt.optimizers[0].param_groups]
+        return {
+            "samples": int(n), "augmented_samples": 0, "actor_loss": 0, "critic_loss": 0, "total_loss": 0,
+            "policy_loss": pl, "entropy_loss": el, "value_loss": vl, "actor_grad_norm": 0, "critic_grad_norm": 0,
+            "grad_norm": gnorm, "entropy": ent, "peak_score": self.highest, "avg_score": avg_s,
+            "ema_avg_score": self.ema["avg_score"], "median_score": med_s, "avg_episode_return": g0m,
+            "pct_512": p512, "ema_pct_512": self.ema["pct_512"], "pct_1024": p1024, "ema_pct_1024": self.ema["pct_1024"],
+            "pct_2048": p2048, "ema_pct_2048": self.ema["pct_2048"], "reward_var": rv, "reward_mean": rm,
+            "zero_reward_pct": zr, "advantage_mean": am, "advantage_var": av, "advantage_l2": al2, "adv_min": amin,
+            "adv_max": amax, "G_norm_mean": gnm, "G_norm_std": gns, "G_norm_min": gnmin, "G_norm_max": gnmax,
+            "G_raw_std": grs, "V_std": vs, "A_std": math.sqrt(max(av, 0.0)),
+            "var_reduction": (gns - math.sqrt(max(av, 0.0))) / gns * 100 if gns > 0 else 0.0,
+            "explained_var": explained, "ema_explained_var": self.ema["explained_var"], "kl_total": klt,
+            "kl_average": kla, "kl_max": klm, "actor_lr": lrs[0], "critic_lr": lrs[1] if len(lrs) > 1 else lrs[0],
+            "loss": loss, "episodes_finished": int(n_eps), "env_steps": int(n),
+        }
+
+    # ------------------------------------------------------------------ evaluation ------------
+    @torch.no_grad()
+    def evaluate(self, games: int = 100, max_steps: int | None = None) -> dict:
+        """train.py:1840-1876: `games` episodic games, game i seeded like random.seed(i)."""
+        from .episodes import play_games
+        was = self.model.training
+        self.model.eval()
+        res = play_games(self.model, games, max_steps, self.dev, seeds=list(range(games)), record=False)
+        self.model.train(was)
+        scores = res["scores"]
+        tiles = res["max_tiles"]
+        k = len(scores)
+        srt = sorted(scores)
+        return {"eval/max_score": max(scores), "eval/avg_score": sum(scores) / k, "eval/median_score": srt[k // 2],
+                "eval/pct_512": sum(1 for t in tiles if t >= 512) / k * 100,
+                "eval/pct_1024": sum(1 for t in tiles if t >= 1024) / k * 100,
+                "eval/pct_2048": sum(1 for t in tiles if t >= 2048) / k * 100}
+
+    def save_checkpoint(self, path, eval_avg_score: float, train_step: int):
+        import agent
+        path = Path(path)
+        path.parent.mkdir(parents=True, exist_ok=True)
+        cfg = agent.MLPConfig(hidden_dim=self.cfg.hidden, num_layers=self.cfg.num_layers,
+                              decouple_critic=self.cfg.decouple_critic)
+        torch.save({"model_state_dict": self.model.state_dict(), "config": cfg.model_dump(),
+                    "eval_avg_score": eval_avg_score, "train_step": train_step,
+                    "optimizer": self.opt.state_dict(), "rtg_state": self.rtg.state.cpu()}, path)
+
+
+def smoke_iteration(device) -> dict:
+    """One tiny fixed-horizon train step (smoke test of the whole path)."""
+    cfg = TrainConfig(steps=10, episodes=256, horizon=16, batch_size=1024, hidden=32, points=0.1, mono=1.0,
+                      rtg_beta=0.99, gamma=0.99, entropy=0.02, critic=0.2, warmup_steps=0, graph=True)
+    tr = VecTrainer(cfg, device)
+    t0 = time.perf_counter()
+    m = tr.train_step(0)
+    m2 = tr.train_step(1)
+    return {"loss": m2["loss"], "entropy": m2["entropy"], "grad_norm": m["grad_norm"],
+            "samples": m2["samples"], "seconds": time.perf_counter() - t0}

@@ -108,6 +108,10 @@ int g2048_env_rollout_random(g2048_stream_t stream, int8_t *boards, int64_t n, i
                              int8_t *traj_boards, uint8_t *traj_actions, int32_t *traj_points,
                              int8_t *traj_pot, uint8_t *traj_flags, const g2048_rng *rng);
 
+/* Game2048.preview_move_rewards (game.py:167-184): points4[i] = merge points of UP, DOWN, LEFT,
+   RIGHT on board i, 0 for an illegal direction.  points4 is int32 [N][4], 16-B aligned. */
+int g2048_preview_points(g2048_stream_t stream, const int8_t *boards, int32_t *points4, int64_t n);
+
 /* Legal-action mask per board (can_move_in_direction || can_merge_in_direction,
    game.py:260-330 / current_valid_directions game.py:295-299) into flags bits 0-3, done bit 7. */
 int g2048_legal_mask(g2048_stream_t stream, const int8_t *boards, uint8_t *flags, int64_t n);

@@ -1,0 +1,269 @@
+"""GPU parity of the training path: reward/RTG scan vs calculate_advantage, sampler vs the
+reference's masked softmax, seeded whole games vs the reference's spawns, the batched_rollout seam,
+graph-vs-eager determinism, and short training runs."""
+
+import math
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.fail("no ROCm device visible")
+    return torch.device("cuda:0")
+
+
+def _episodes_from_fixture(a):
+    eps, cur, last = [], None, None
+    for i in range(len(a["episode"])):
+        if a["episode"][i] != last:
+            cur = {"moves": [], "total_points": 0, "total_steps": 0, "final_state": None}
+            eps.append(cur)
+            last = a["episode"][i]
+        done = bool(a["done"][i])
+        cur["moves"].append({"points_earned": int(a["points"][i]), "monotonicity_before": int(a["mono_b"][i]),
+                             "monotonicity_after": 0 if done else int(a["mono_a"][i]),
+                             "emptiness_before": int(a["empt_b"][i]), "emptiness_after": 0 if done else int(a["empt_a"][i]),
+                             "predicted_future_value": float(a["value"][i])})
+    return eps
+
+
+@pytest.mark.parametrize("case", range(5))
+def test_calculate_advantage_matches_reference(dev, case):
+    import train
+    a = golden("advantage.npz")
+    gamma, wp, wm, we, beta, m2, mu, step = a["cases"][case]
+    eps = _episodes_from_fixture(a)
+    eps, aug, fm, nm2, nmu = train.calculate_advantage(eps, gamma, mu, wp, 1, 1, 1, 1, 1, wm, we, 1, 1000.0,
+                                                       rtg_beta=beta, rtg_m2=m2, rtg_mu=mu, rtg_step=int(step),
+                                                       device=dev)
+    moves = [m for ep in eps for m in ep["moves"]]
+    got = {k: np.array([m[k] for m in moves]) for k in ("reward", "future_reward_raw", "future_reward", "advantage")}
+    assert np.array_equal(got["reward"], a[f"c{case}_reward"])
+    g_raw = a[f"c{case}_g_raw"]
+    np.testing.assert_allclose(got["future_reward_raw"], g_raw, rtol=1e-6, atol=1e-5 * max(1.0, np.abs(g_raw).max()))
+    np.testing.assert_allclose(got["future_reward"], a[f"c{case}_g_norm"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(got["advantage"], a[f"c{case}_adv"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose([fm, nm2, nmu], a[f"c{case}_moments"], rtol=1e-9)
+    assert aug == []
+
+
+def test_rtg_scan_large_time_major_vs_oracle(dev):
+    """[T=96, N=4096] trajectory with auto-reset episode ends and inactive tails, fp64 oracle."""
+    from g2048 import _lib as L
+    T, n = 96, 4096
+    g = np.random.default_rng(0)
+    points = (g.integers(0, 5, size=(T, n)) * 4).astype(np.int32)
+    pot = g.integers(0, 17, size=(T, n, 4)).astype(np.int8)
+    flags = np.where(g.random((T, n)) < 0.02, L.FLAG_DONE, 0).astype(np.uint8)
+    tail = g.integers(T // 2, T + 1, size=n)
+    for e in range(n):
+        flags[tail[e]:, e] = L.FLAG_INACTIVE | L.FLAG_DONE
+    value = g.normal(size=(T, n)).astype(np.float32)
+    gamma, wp, wm, we, beta = 0.97, 0.1, 1.0, 0.5, 0.95
+    state0 = [3.0, 40.0, 3.0, 5.0]
+    st = torch.tensor(state0 + [0, 1, 0, 0], dtype=torch.float64, device=dev)
+    cfg = L.RewardCfg(gamma, wp, wm, we, beta)
+    outs = [torch.zeros(T, n, dtype=torch.float32, device=dev) for _ in range(3)]
+    part = torch.zeros(3, dtype=torch.float64, device=dev)
+    ws = torch.zeros(L.rtg_workspace_bytes(n), dtype=torch.uint8, device=dev)
+    td = lambda x: torch.from_numpy(x).to(dev)  # noqa: E731
+    L.rtg_prepare(st, cfg)
+    L.reward_rtg(td(points), td(pot), td(flags), td(value), st, *outs, part, ws, cfg)
+    L.rtg_finalize(st, part, cfg)
+    gr, gn, ad = (o.cpu().numpy() for o in outs)
+    # oracle: per env episodes in time order
+    exp_gr = np.zeros((T, n))
+    rows, ends, idx = [], [], []
+    for e in range(n):
+        for t in range(tail[e]):
+            idx.append((t, e))
+            ends.append(bool(flags[t, e] & L.FLAG_DONE) or t == tail[e] - 1)
+    ii = np.array(idx)
+    sel = (ii[:, 0], ii[:, 1])
+    r = O.reward_rtg_normalize(points[sel], pot[sel][:, 0], pot[sel][:, 1], pot[sel][:, 2], pot[sel][:, 3],
+                               (flags[sel] & L.FLAG_DONE) != 0, value[sel], np.array(ends), gamma, wp, wm, we, beta,
+                               state0[1], state0[0], int(state0[3]), state0[2])
+    np.testing.assert_allclose(gr[sel], r["g_raw"], rtol=1e-6, atol=1e-4)
+    np.testing.assert_allclose(gn[sel], r["g_norm"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ad[sel], r["adv"], rtol=1e-5, atol=1e-5)
+    s = st.cpu().numpy()
+    np.testing.assert_allclose([s[0], s[1], s[2]], r["moments"], rtol=1e-9)
+    assert s[3] == state0[3] + 1
+    assert (gr[flags == (L.FLAG_INACTIVE | L.FLAG_DONE)] == 0).all()
+
+
+def test_sampler_matches_reference_masked_softmax(dev):
+    from g2048 import _lib as L
+    g = golden("sampler.npz")
+    n = len(g["logits"])
+    legal = np.array([sum(1 << a for a in range(4) if not g["invalid"][i, a]) for i in range(n)], np.uint8)
+    lg = torch.from_numpy(g["logits"]).to(dev)
+    fl = torch.from_numpy(legal).to(dev)
+    act = torch.zeros(n, dtype=torch.uint8, device=dev)
+    lp = torch.zeros(n, 4, dtype=torch.float32, device=dev)
+    ent = torch.zeros(n, dtype=torch.float32, device=dev)
+    L.sample_actions(lg, fl, act, lp, ent, L.make_rng(L.RNG_PHILOX, 77, 12, 5))
+    torch.cuda.synchronize()
+    lpn, en, an = lp.cpu().numpy(), ent.cpu().numpy(), act.cpu().numpy()
+    fin = np.isfinite(g["logp"])
+    assert np.array_equal(np.isfinite(lpn), fin)
+    np.testing.assert_allclose(lpn[fin], g["logp"][fin], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(en, g["entropy"], rtol=1e-5, atol=1e-5)
+    # inverse CDF of the same Philox uniform (stream 1), away from CDF boundaries
+    u = (O.philox_draws(77, 12, n, 1, env_base=5)[:, 0] >> 8).astype(np.float64) / 2**24
+    cdf = np.cumsum(np.where(g["invalid"], 0.0, g["probs"]), axis=1)
+    expect = np.array([int(np.argmax(u[i] < cdf[i])) for i in range(n)])
+    near = np.abs(cdf - u[:, None]).min(axis=1) < 1e-5
+    assert np.array_equal(an[~near], expect[~near])
+    assert all(legal[i] >> an[i] & 1 for i in range(n))
+
+
+def test_sampler_distribution(dev):
+    from g2048 import _lib as L
+    n = 1 << 20
+    logits = torch.tensor([[0.0, 1.0, -1.0, 2.0]], device=dev).repeat(n, 1)
+    fl = torch.full((n,), 0b1011, dtype=torch.uint8, device=dev)  # LEFT illegal
+    act = torch.zeros(n, dtype=torch.uint8, device=dev)
+    L.sample_actions(logits, fl, act, None, None, L.make_rng(L.RNG_PHILOX, 1, 0))
+    freq = torch.bincount(act.long(), minlength=4).double().cpu().numpy() / n
+    p = np.exp([0.0, 1.0, -np.inf, 2.0])
+    p /= p.sum()
+    assert freq[2] == 0
+    assert np.abs(freq - p).max() < 3e-3
+
+
+def test_seeded_game_matches_reference_spawns(dev):
+    """play_game_for_episode(seed=s): replaying its actions through the pure-Python restatement
+    after random.seed(s) reproduces every board (game.py spawns, bit-exact)."""
+    import agent
+    import train
+    from oracle import pyref
+    torch.manual_seed(0)
+    model = agent.GameMLP(agent.MLPConfig(hidden_dim=32)).to(dev).eval()
+    for s in (0, 1, 2):
+        ep = train.play_game_for_episode(model, device=dev, seed=s)
+        rnd = random.Random(s)
+        b = pyref.reset(rnd)
+        for m in ep["moves"]:
+            assert [c for row in m["state_before"] for c in row] == b
+            pts, done, info = pyref.step(b, m["selected_direction"], rnd)
+            assert pts == m["points_earned"]
+            assert [c for row in m["result_state"] for c in row] == b
+            assert m["monotonicity_before"] == info["monotonicity_before"]
+            assert m["emptiness_before"] == info["emptiness_before"]
+        assert done and ep["total_steps"] == len(ep["moves"]) - 1
+        assert ep["final_state"] == [b[0:4], b[4:8], b[8:12], b[12:16]]
+
+
+def test_play_games_batched_schema(dev):
+    import agent
+    from batched_rollout import play_games_batched
+    torch.manual_seed(1)
+    model = agent.GameMLP(agent.MLPConfig(hidden_dim=32)).to(dev)
+    random.seed(4)
+    eps = play_games_batched(model, 64, max_steps=None, device=dev)
+    assert len(eps) == 64
+    keys = {"predicted_future_value", "selected_direction", "game_state", "state_before", "result_state",
+            "points_earned", "action_mask", "policy_logprobs", "monotonicity_before", "monotonicity_after",
+            "emptiness_before", "emptiness_after", "entropy", "max_tile_created", "points_possible"}
+    for ep in eps:
+        assert ep["moves"] and keys <= set(ep["moves"][0])
+        assert ep["total_points"] == sum(m["points_earned"] for m in ep["moves"])
+        assert O.legal_mask(np.array(ep["final_state"], np.int8).reshape(1, 16))[0] == 0
+        m = ep["moves"][-1]
+        assert m["monotonicity_after"] == 0.0 and m["emptiness_after"] == 0.0
+        for m in ep["moves"][:5]:
+            assert isinstance(m["predicted_future_value"], float) and m["game_state"].shape == (48,)
+            assert not m["action_mask"][m["selected_direction"]]
+            assert m["points_possible"][agent.Direction.UP] >= 0
+    random.seed(4)
+    again = play_games_batched(model, 64, max_steps=None, device=dev)
+    assert [e["total_points"] for e in again] == [e["total_points"] for e in eps]
+    capped = play_games_batched(model, 8, max_steps=7, device=dev)
+    assert all(len(e["moves"]) <= 7 for e in capped)
+
+
+def test_graph_and_eager_rollouts_identical(dev):
+    import agent
+    from g2048.rollout import InferencePolicy, Rollout
+    torch.manual_seed(2)
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=64)).to(dev)
+    pol = InferencePolicy(m)
+    outs = []
+    for graph in (False, True, True):
+        ro = Rollout(2048, 24, dev, seed=9)
+        ro.reset()
+        ro.collect(pol, graph=graph)
+        outs.append((ro.buf.boards.clone(), ro.buf.actions.clone(), ro.buf.points.clone()))
+    for o in outs[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(outs[0], o))
+
+
+@pytest.mark.parametrize("horizon", [32, 0])
+def test_trainer_runs_and_learns_signal(dev, horizon):
+    from g2048.trainer import TrainConfig, VecTrainer
+    cfg = TrainConfig(steps=6, episodes=1024, horizon=horizon, max_steps=256 if horizon == 0 else None,
+                      batch_size=8192, hidden=64, points=0.1, mono=1.0, rtg_beta=0.99, entropy=0.02, critic=0.2,
+                      warmup_steps=1, lr=1e-3, critic_lr=1e-4)
+    tr = VecTrainer(cfg, dev)
+    ms = [tr.train_step(s) for s in range(4)]
+    for m in ms:
+        for k, v in m.items():
+            assert v is None or not isinstance(v, float) or math.isfinite(v), k
+    assert ms[-1]["samples"] > 0 and ms[-1]["episodes_finished"] > 0
+    assert ms[1]["grad_norm"] > 0
+    assert 0 < ms[0]["entropy"] <= math.log(4) + 1e-5
+    mom = tr.rtg.moments()
+    assert mom["rtg_step"] == 5
+    ev = tr.evaluate(16, 200)
+    assert ev["eval/max_score"] >= ev["eval/avg_score"] > 0
+
+
+def test_ppo_updater_gpu_matches_compat_update(dev):
+    """Tensor-path PPOUpdater (fp32, one minibatch) == list-of-dict model_optimize_step on the same data."""
+    import agent
+    import train
+    from g2048 import _lib as L
+    from g2048.dist import GradBucket
+    from g2048.optim import build_optimizer
+    from g2048.ppo import PPOConfig, PPOUpdater
+    u = golden("update.npz")
+    n = len(u["actions"])
+    legal = np.array([sum(1 << a for a in range(4) if not u["invalid"][i, a]) for i in range(n)], np.uint8)
+    boards = np.rint(u["obs"][:, 0::3]).astype(np.int8)
+    res = []
+    for mode in ("tensor", "compat"):
+        torch.manual_seed(1234)
+        m = agent.GameMLP(agent.MLPConfig(hidden_dim=64, num_layers=2, dropout=0.0)).to(dev)
+        opt = build_optimizer(m, 1e-3, 1e-4, schedule=False)
+        if mode == "tensor":
+            up = PPOUpdater(m, opt, PPOConfig(batch_size=n, critic=0.2, amp_dtype=None), GradBucket(m.parameters()))
+
+            def enc(b):
+                o = torch.empty(b.shape[0], 48, dtype=torch.float32, device=dev)
+                L.obs_encode(b.contiguous(), o)
+                return o
+            data = {"boards": torch.from_numpy(boards).to(dev), "actions": torch.from_numpy(u["actions"]).to(dev),
+                    "legal": torch.from_numpy(legal).to(dev), "logp": torch.from_numpy(u["old_logprobs"]).to(dev),
+                    "adv": torch.from_numpy(u["advantage"]).to(dev), "ret": torch.from_numpy(u["future_reward"]).to(dev)}
+            st = {k: float(v) for k, v in up.update(data, 0.02, enc).items()}
+        else:
+            moves = [{"game_state": torch.from_numpy(u["obs"][i]), "selected_direction": int(u["actions"][i]),
+                      "action_mask": u["invalid"][i].tolist(), "advantage": float(u["advantage"][i]),
+                      "future_reward": float(u["future_reward"][i]), "policy_logprobs": u["old_logprobs"][i].tolist()}
+                     for i in range(n)]
+            st = train.model_optimize_step(m, [{"moves": moves}], opt, None, 0.02, 0.2, dev, n, 1)
+        res.append((torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy(), st))
+    np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-4, atol=2e-6)
+    for k in ("loss", "policy_loss", "value_loss", "entropy", "grad_norm"):
+        assert math.isclose(res[0][1][k], res[1][1][k], rel_tol=1e-4, abs_tol=1e-6), k

@@ -1,0 +1,127 @@
+"""Host-side logic on CPU: the PPO update against the reference's golden update step, the LR
+schedule, D4 augmentation, and the flat gradient bucket."""
+
+import math
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+
+def _golden_model():
+    import agent
+    u = golden("update.npz")
+    torch.manual_seed(1234)
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=64, num_layers=2, dropout=0.0))
+    return m, u
+
+
+def _moves(u):
+    return [{"game_state": torch.from_numpy(u["obs"][i]), "selected_direction": int(u["actions"][i]),
+             "action_mask": u["invalid"][i].tolist(), "advantage": float(u["advantage"][i]),
+             "future_reward": float(u["future_reward"][i]), "policy_logprobs": u["old_logprobs"][i].tolist()}
+            for i in range(len(u["actions"]))]
+
+
+def test_model_optimize_step_matches_reference_update():
+    """train.py:414-642 with Muon+AdamW at fixed lr, one minibatch: parameters after the step and the
+    returned statistics agree with the reference run (tests/golden/update.npz)."""
+    import train
+    from g2048.optim import MultiOptimizer
+    m, u = _golden_model()
+    lr, clr, b1, b2, wd, beta, critic = u["hparams"]
+    o2d, o1d, v2d, v1d = m.get_param_groups(clr, lr)
+    adamw = torch.optim.AdamW([o1d, v1d], betas=(b1, b2), weight_decay=wd)
+    muon = torch.optim.Muon([o2d, v2d], adjust_lr_fn="match_rms_adamw", weight_decay=wd)
+    stats = train.model_optimize_step(m, [{"moves": _moves(u)}], MultiOptimizer(muon, adamw), None, beta, critic,
+                                      None, batch_size=len(u["actions"]), epochs=1)
+    for k, v in m.state_dict().items():
+        np.testing.assert_allclose(v.numpy(), u[f"final::{k}"], rtol=1e-4, atol=2e-6, err_msg=k)
+    ref = dict(zip(u["stat_keys"].tolist(), u["stat_vals"].tolist()))
+    for k in ("loss", "policy_loss", "entropy_loss", "value_loss", "grad_norm", "entropy"):
+        assert math.isclose(stats[k], ref[k], rel_tol=1e-4, abs_tol=1e-6), (k, stats[k], ref[k])
+    assert stats["lr"] == ref["lr"] == 0.0
+
+
+def test_cosine_schedule_matches_transformers():
+    from transformers import get_scheduler
+    from g2048.optim import cosine_with_warmup
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.SGD([p], lr=1.0)
+    sch = get_scheduler("cosine", opt, num_warmup_steps=10, num_training_steps=100)
+    f = cosine_with_warmup(10, 100)
+    for step in range(120):
+        assert math.isclose(opt.param_groups[0]["lr"], f(step), rel_tol=1e-12, abs_tol=1e-15), step
+        opt.step()
+        sch.step()
+
+
+def test_augmentation_is_a_symmetry_of_the_game(games):
+    """A mirrored/rotated step, with its remapped action, must be a legal transition of the
+    transformed board (checked with the oracle's move)."""
+    from g2048.augment import augment_steps, encode_grid
+    from oracle import oracle as O
+    g = games
+    steps = []
+    for i in range(400):
+        if g["invalid"][i]:
+            continue
+        mask = [not (g["mask_before"][i] >> a & 1) for a in range(4)]
+        steps.append({"state_before": g["before"][i].reshape(4, 4).tolist(),
+                      "result_state": g["moved"][i].reshape(4, 4).tolist(),
+                      "selected_direction": int(g["action"][i]), "action_mask": mask,
+                      "policy_logprobs": [float(-k) for k in range(4)], "points_earned": int(g["points"][i])})
+    aug = augment_steps(steps, 0.5, random.Random(3))
+    assert len(aug) > 50
+    for s in aug:
+        before = np.array(s["state_before"], np.int8).reshape(16)
+        out, pts, _ = O.move(before[None], s["selected_direction"])
+        assert np.array_equal(out[0], np.array(s["result_state"], np.int8).reshape(16))
+        assert pts[0] == s["points_earned"]
+        legal = O.legal_mask(before[None])[0]
+        assert s["action_mask"] == [not (legal >> a & 1) for a in range(4)]
+        assert torch.equal(s["game_state"], encode_grid(s["state_before"]))
+        assert sorted(s["policy_logprobs"]) == [-3.0, -2.0, -1.0, 0.0]
+
+
+def test_augmentation_consumes_random_like_the_reference():
+    """Same sequence of `random` calls as train.py:779-881 (sample, then random()/choice per step)."""
+    from g2048.augment import augment_steps
+    steps = [{"state_before": [[0] * 4] * 4, "result_state": [[0] * 4] * 4, "selected_direction": k % 4,
+              "action_mask": [False] * 4, "policy_logprobs": [0.0] * 4} for k in range(40)]
+    r1 = random.Random(9)
+    aug = augment_steps(steps, 0.25, r1)
+    r2 = random.Random(9)
+    picked = r2.sample(steps, 10)
+    expect = 0
+    for _ in picked:
+        if r2.random() < 0.5:
+            r2.choice(["horizontal", "vertical"])
+            expect += 1
+        if r2.random() < 0.5:
+            r2.choice([90, 180, 270])
+            expect += 1
+    assert len(aug) == expect
+    assert r1.random() == r2.random()
+
+
+def test_grad_bucket_views_and_clip():
+    import agent
+    from g2048.dist import GradBucket
+    torch.manual_seed(0)
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=16, num_layers=1, dropout=0.0))
+    gb = GradBucket(m.parameters())
+    x = torch.randn(32, 48)
+    logits, v = m(x)
+    (logits.square().sum() + v.sum()).backward()
+    assert gb.check_views()
+    ref = torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone()
+    assert torch.equal(gb.flat, ref)
+    norm = gb.clip_(1.0)
+    assert math.isclose(float(norm), float(ref.norm()), rel_tol=1e-6)
+    assert math.isclose(float(gb.flat.norm()), 1.0, rel_tol=1e-4)
+    gb.zero()
+    assert float(gb.flat.abs().sum()) == 0.0 and gb.check_views()
