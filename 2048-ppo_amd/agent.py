@@ -129,7 +129,8 @@ class GameMLP(nn.Module):
             raise ValueError(f"input must consist of shape (batch, channel), got: {inputs.shape}")
         if inputs.shape[-1] != N_FEATURES:
             raise AssertionError(f"{inputs.shape[-1]} does not equal {N_FEATURES}")
-        x = self.features(inputs.to(torch.float32))
+        # float32 like the reference (game.py:1191); a low-precision inference copy keeps its own dtype
+        x = self.features(inputs.to(self.stem[0].weight.dtype))
         logits = self.action_head(x)
         value = self.value_head(x.detach() if self.decouple_critic else x)
         return logits, value
