@@ -109,6 +109,8 @@ class VecTrainer:
         self.ema = {"avg_score": 0.0, "pct_512": 0.0, "pct_1024": 0.0, "pct_2048": 0.0, "explained_var": 0.0}
         self._started = False
         self._chunk_graphs = {}
+        self.profile = False
+        self.timings: dict[str, float] = {}
 
     # ------------------------------------------------------------------ rollout ---------------
     def _encode(self, boards: torch.Tensor) -> torch.Tensor:
@@ -159,8 +161,23 @@ class VecTrainer:
         return g
 
     # ------------------------------------------------------------------ train step ------------
+    def _mark(self, name: str):
+        if self.profile:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self._events.append((name, e))
+
+    def _collect_timings(self):
+        if self.profile and self._events:
+            torch.cuda.synchronize()
+            for (n0, e0), (n1, e1) in zip(self._events[:-1], self._events[1:]):
+                self.timings[n1] = self.timings.get(n1, 0.0) + e0.elapsed_time(e1)
+        self._events = []
+
     def train_step(self, step: int) -> dict:
         cfg, ro, b = self.cfg, self.rollout, self.rollout.buf
+        self._events = []
+        self._mark("start")
         self.model.eval()
         self.policy.sync()
         if self.episodic:
@@ -173,8 +190,10 @@ class VecTrainer:
                 b.carry_over()
             ro.collect(self.policy, graph=cfg.graph)
             T = ro.T
+        self._mark("rollout_ms")
         sf = b.step_flags[:T]
         self.rtg.compute(b.points[:T], b.pot[:T], sf, b.value[:T], b.g_raw[:T], b.g_norm[:T], b.adv[:T])
+        self._mark("rtg_ms")
         n = ro.n
         data = {"boards": b.boards[:T].reshape(T * n, 16), "actions": b.actions[:T].reshape(-1),
                 "legal": b.flags[:T].reshape(-1), "logp": b.logp[:T].reshape(T * n, 4),
@@ -186,7 +205,10 @@ class VecTrainer:
             data = {k: v.index_select(0, valid) for k, v in data.items()}
         ustats = self.ppo.update(data, self.beta, self._encode)
         self.opt.scheduler_step()
+        self._mark("update_ms")
         metrics = self._metrics(T, valid, ustats)
+        self._mark("metrics_ms")
+        self._collect_timings()
         if cfg.adaptive_beta:  # train.py:1740-1746
             err = cfg.target_entropy - metrics["entropy"]
             self.beta = max(cfg.beta_min, min(cfg.beta_max, self.beta * (1.0 + cfg.beta_lr * err)))

@@ -49,7 +49,10 @@ def parse():
     p.add_argument("--envs", type=int, default=65536)
     p.add_argument("--chunk", type=int, default=64, help="env steps per rollout launch")
     p.add_argument("--single-steps", type=int, default=256, help="graph-captured one-launch-per-step steps (0=off)")
-    p.add_argument("--train-iters", type=int, default=0, help="timed full training iterations (0=off)")
+    p.add_argument("--train-iters", type=int, default=3, help="timed full training iterations (0=off)")
+    p.add_argument("--train-warmup", type=int, default=2)
+    p.add_argument("--train-horizon", type=int, default=64)
+    p.add_argument("--train-batch", type=int, default=65536)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of each CPU-baseline leg (0=off)")
     p.add_argument("--sweep", default="", help="comma list of extra board counts for the rollout kernel")
     return p.parse_args()
