@@ -42,13 +42,12 @@ __device__ __forceinline__ uint64_t rng_counter(const RngArgs &r) {
 // One spawn on `b` (game.py:923-940).  `slot` selects which pair of the Philox block is used, so a
 // reset's two spawns come from one 4-word draw.
 template <int Mode>
-__device__ __forceinline__ void spawn(uint4 &b, const uint4 &ph, int slot, MT *mt, const RngArgs &r, int64_t i) {
+__device__ __forceinline__ void spawn(uint4 &b, uint32_t u0, uint32_t u1, MT *mt, const RngArgs &r, int64_t i) {
     const uint32_t em = empty_mask16(b);
     const uint32_t cnt = __popc(em);
     if (cnt == 0u) return;
     uint32_t k, v;
     if constexpr (Mode == G2048_RNG_PHILOX) {
-        const uint32_t u0 = slot ? ph.z : ph.x, u1 = slot ? ph.w : ph.y;
         k = (uint32_t)(((uint64_t)u0 * cnt) >> 32);
         v = u1 < kTwoThreshold ? 1u : 2u;
     } else if constexpr (Mode == G2048_RNG_MT19937) {
@@ -67,8 +66,8 @@ __device__ __forceinline__ uint4 fresh_board(MT *mt, const RngArgs &r, int64_t i
     uint4 b = make_uint4(0u, 0u, 0u, 0u);
     uint4 ph = make_uint4(0u, 0u, 0u, 0u);
     if constexpr (Mode == G2048_RNG_PHILOX) ph = philox_draw(r.seed, ctr, r.env_base + (uint32_t)i, 2u);
-    spawn<Mode>(b, ph, 0, mt, r, i);
-    spawn<Mode>(b, ph, 1, mt, r, i);
+    spawn<Mode>(b, ph.x, ph.y, mt, r, i);
+    spawn<Mode>(b, ph.z, ph.w, mt, r, i);
     return b;
 }
 
@@ -92,12 +91,15 @@ __device__ __forceinline__ StepResult step_board(uint4 &b, bool has_action, uint
         return res;
     }
     uint32_t a;
+    uint32_t su0 = 0u, su1 = 0u;  // spawn words: one Philox draw per step when the action is drawn here
     if (has_action) {
         a = action_in & 3u;
     } else {
         const uint4 d = philox_draw(rng.seed, ctr, env, 1u);
         const uint32_t nl = __popc(legal_in);
         a = nl ? kth_bit16(legal_in, (uint32_t)(((uint64_t)d.x * nl) >> 32)) : 0u;  // k-th legal action
+        su0 = d.y;
+        su1 = d.z;
     }
     res.action = a;
     const int mono_b = monotonicity(b);
@@ -115,9 +117,14 @@ __device__ __forceinline__ StepResult step_board(uint4 &b, bool has_action, uint
                   ((uint32_t)(empt_a & 0xFF) << 24);
         res.pts = pts;
         res.mx = mx;
-        uint4 ph = make_uint4(0u, 0u, 0u, 0u);
-        if constexpr (Mode == G2048_RNG_PHILOX) ph = philox_draw(rng.seed, ctr, env, 0u);
-        spawn<Mode>(moved, ph, 0, mt, rng, i);
+        if constexpr (Mode == G2048_RNG_PHILOX) {
+            if (has_action) {  // policy actions: spawn draw from stream 0
+                const uint4 ph = philox_draw(rng.seed, ctr, env, 0u);
+                su0 = ph.x;
+                su1 = ph.y;
+            }
+        }
+        spawn<Mode>(moved, su0, su1, mt, rng, i);
         b = moved;
         const uint32_t lm = legal_mask(b);
         res.fl = lm | (lm ? 0u : FLAG_DONE);
@@ -153,6 +160,9 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(const uint4 *__restric
 // Synthetic random-legal rollout (the benchmark workload of BASELINE.md): `steps` env steps per
 // launch with the board kept in registers, auto-reset on done, one time-major trajectory record per
 // step: the board the action was taken on [T][N][16], action, points, potentials, flags.
+// Per step: ONE Philox draw (x: action, y/z: spawn), the legal mask carried from the previous
+// step (the action is always legal, so the illegal-move path of step_board cannot occur), and
+// trajectory pointers advanced by a uniform stride instead of 64-bit t*n products.
 __global__ __launch_bounds__(kBlock) void env_rollout_kernel(uint4 *__restrict__ boards, int64_t n, int64_t steps,
                                                              uint4 *__restrict__ tb, uint8_t *__restrict__ ta,
                                                              int32_t *__restrict__ tp, uint32_t *__restrict__ tpot,
@@ -161,15 +171,45 @@ __global__ __launch_bounds__(kBlock) void env_rollout_kernel(uint4 *__restrict__
     if (i >= n) return;
     uint4 b = boards[i];
     const uint64_t ctr0 = rng_counter(rng);
+    const uint32_t env = rng.env_base + (uint32_t)i;
+    uint32_t legal = legal_mask(b);
+    if (legal == 0u) {  // a finished board handed in: start a new game first (as auto-reset would)
+        b = fresh_board<G2048_RNG_PHILOX>(nullptr, rng, i, ctr0 + (uint64_t)steps);
+        legal = legal_mask(b);
+    }
+    if (tb) tb += i;
+    if (ta) ta += i;
+    if (tp) tp += i;
+    if (tpot) tpot += i;
+    if (tf) tf += i;
     for (int64_t t = 0; t < steps; t++) {
-        const int64_t o = t * n + i;
-        if (tb) tb[o] = b;
-        const StepResult r = step_board<G2048_RNG_PHILOX>(b, false, 0u, nullptr, rng, i, ctr0 + (uint64_t)t,
-                                                          G2048_OPT_AUTO_RESET);
-        if (ta) ta[o] = (uint8_t)r.action;
-        if (tp) tp[o] = (int32_t)r.pts;
-        if (tpot) tpot[o] = r.pot;
-        if (tf) tf[o] = (uint8_t)r.fl;
+        if (tb) { *tb = b; tb += n; }
+        const uint64_t ctr = ctr0 + (uint64_t)t;
+        const uint4 d = philox_draw(rng.seed, ctr, env, 1u);
+        const uint32_t a = kth_bit16(legal, (uint32_t)(((uint64_t)d.x * (uint32_t)__popc(legal)) >> 32));
+        const int mono_b = monotonicity(b);
+        const int empt_b = emptiness(b);
+        uint32_t pts, mx;
+        uint4 moved = apply_move(b, a, pts, mx);
+        const int mono_a = monotonicity(moved);
+        const int empt_a = emptiness(moved);
+        spawn<G2048_RNG_PHILOX>(moved, d.y, d.z, nullptr, rng, i);
+        b = moved;
+        legal = legal_mask(b);
+        uint32_t fl = legal;
+        if (legal == 0u) {
+            b = fresh_board<G2048_RNG_PHILOX>(nullptr, rng, i, ctr);
+            legal = legal_mask(b);
+            fl = FLAG_DONE | FLAG_RESET | legal;
+        }
+        if (ta) { *ta = (uint8_t)a; ta += n; }
+        if (tp) { *tp = (int32_t)pts; tp += n; }
+        if (tpot) {
+            *tpot = (uint32_t)(mono_b & 0xFF) | ((uint32_t)(mono_a & 0xFF) << 8) | ((uint32_t)(empt_b & 0xFF) << 16) |
+                    ((uint32_t)(empt_a & 0xFF) << 24);
+            tpot += n;
+        }
+        if (tf) { *tf = (uint8_t)fl; tf += n; }
     }
     boards[i] = b;
 }

@@ -462,8 +462,8 @@ typedef struct {
     int32_t inj_v;     /* mode 2: exponent (1 or 2) */
 } or_rng;
 
-/* game.py:923-940; with Philox the (k, value) draw is the build's fast-mode convention */
-static int add_tile(int8_t b[16], or_rng *r, const uint32_t *ph, int slot) {
+/* game.py:923-940; with Philox the (k, value) words u0/u1 are the build's fast-mode convention */
+static int add_tile(int8_t b[16], or_rng *r, uint32_t u0, uint32_t u1) {
     int empt[16], n = 0;
     for (int p = 0; p < 16; p++)
         if (b[p] == 0) empt[n++] = p;
@@ -473,8 +473,8 @@ static int add_tile(int8_t b[16], or_rng *r, const uint32_t *ph, int slot) {
         k = (int)or_mt_randbelow(r->mt, (uint32_t)n);
         v = or_mt_random(r->mt) < 0.9 ? 1 : 2;
     } else if (r->mode == OR_RNG_PHILOX) {
-        k = (int)(((uint64_t)ph[2 * slot] * (uint32_t)n) >> 32);
-        v = ph[2 * slot + 1] < 3865470567u ? 1 : 2; /* u32 * 2^-32 < 0.9 */
+        k = (int)(((uint64_t)u0 * (uint32_t)n) >> 32);
+        v = u1 < 3865470567u ? 1 : 2; /* u32 * 2^-32 < 0.9 */
     } else {
         k = r->inj_k;
         v = r->inj_v;
@@ -488,8 +488,8 @@ void or_reset(int8_t b[16], or_rng *r) {
     memset(b, 0, 16);
     uint32_t ph[4] = {0, 0, 0, 0};
     if (r->mode == OR_RNG_PHILOX) or_philox_draw(r->seed, r->step, r->env, 2u, ph);
-    add_tile(b, r, ph, 0);
-    add_tile(b, r, ph, 1);
+    add_tile(b, r, ph[0], ph[1]);
+    add_tile(b, r, ph[2], ph[3]);
 }
 
 typedef struct {
@@ -503,8 +503,29 @@ typedef struct {
     int8_t moved[16];
 } or_step_out;
 
-/* game.py:952-1030.  `full_info` = 1 computes the info-only heuristics like the reference does. */
+/* game.py:952-1030.  `full_info` = 1 computes the info-only heuristics like the reference does.
+   Philox spawn words: stream 0 of (seed, step, env) unless `spawn_words` supplies them. */
+static void step_impl(int8_t b[16], int dir, or_rng *r, int full_info, or_step_out *o, const uint32_t *spawn_words);
+
 void or_step(int8_t b[16], int dir, or_rng *r, int full_info, or_step_out *o) {
+    step_impl(b, dir, r, full_info, o, NULL);
+}
+
+/* The synthetic-policy step: ONE Philox draw of stream 1 gives the action (x: k-th legal action,
+   UP/DOWN/LEFT/RIGHT order) and the spawn (y: cell, z: value).  Returns the action. */
+int or_step_random(int8_t b[16], or_rng *r, int full_info, or_step_out *o) {
+    uint32_t d[4];
+    or_philox_draw(r->seed, r->step, r->env, 1u, d);
+    int m = or_legal_mask(b), nl = __builtin_popcount(m), dir = 0;
+    int k = (int)(((uint64_t)d[0] * (uint32_t)nl) >> 32);
+    for (int q = 0; q < 4; q++)
+        if (m >> q & 1) { if (k == 0) { dir = q; break; } k--; }
+    uint32_t w[2] = {d[1], d[2]};
+    step_impl(b, dir, r, full_info, o, w);
+    return dir;
+}
+
+static void step_impl(int8_t b[16], int dir, or_rng *r, int full_info, or_step_out *o, const uint32_t *spawn_words) {
     memset(o, 0, sizeof(*o));
     if (!(or_can_move(b, dir) || or_can_merge(b, dir))) {
         o->invalid = 1;
@@ -536,8 +557,11 @@ void or_step(int8_t b[16], int dir, or_rng *r, int full_info, or_step_out *o) {
     if (full_info) o->topo_d = or_topological(b, anchor) - tb;
     o->maxexp_a = gmax(b);
     uint32_t ph[4] = {0, 0, 0, 0};
-    if (r->mode == OR_RNG_PHILOX) or_philox_draw(r->seed, r->step, r->env, 0u, ph);
-    add_tile(b, r, ph, 0);
+    if (r->mode == OR_RNG_PHILOX) {
+        if (spawn_words) { ph[0] = spawn_words[0]; ph[1] = spawn_words[1]; }
+        else or_philox_draw(r->seed, r->step, r->env, 0u, ph);
+    }
+    add_tile(b, r, ph[0], ph[1]);
     o->done = or_legal_mask(b) == 0;
 }
 
@@ -635,29 +659,63 @@ void or_philox_batch(uint64_t seed, uint64_t step, uint32_t env_base, uint32_t s
 }
 
 /*
- * CPU baseline workload: `n_envs` independent games stepped `steps` times with uniform random
- * legal actions (Philox stream 1, same convention as the kernels), auto-reset on done, with the
- * full info-heuristic set like game.step.  Returns the number of legal transitions executed.
+ * CPU baseline workload / checker of env_rollout_kernel: `n_envs` independent games stepped
+ * `steps` times with the synthetic random-legal policy (or_step_random), auto-reset on done with
+ * the stream-2 draw of the same step.  A board handed in already finished is first reset with
+ * counter step0 + steps (the kernel's convention).  Optional records (time-major [steps][n_envs]):
+ * rec_boards [..][16] (board the action was taken on), rec_act, rec_pts, rec_pot [..][4], rec_flags.
+ * Returns the number of transitions executed.
  */
-int64_t or_random_rollout(int8_t *boards, int64_t n_envs, int64_t steps, uint64_t seed, uint64_t step0,
-                          uint32_t env_base, int full_info) {
+int64_t or_random_rollout_rec(int8_t *boards, int64_t n_envs, int64_t steps, uint64_t seed, uint64_t step0,
+                              uint32_t env_base, int full_info, int8_t *rec_boards, uint8_t *rec_act,
+                              int32_t *rec_pts, int8_t *rec_pot, uint8_t *rec_flags) {
     int64_t count = 0;
-    for (int64_t t = 0; t < steps; t++) {
-        for (int64_t i = 0; i < n_envs; i++) {
-            int8_t *b = boards + 16 * i;
-            uint32_t env = env_base + (uint32_t)i;
-            int m = or_legal_mask(b);
-            uint32_t a4[4];
-            or_philox_draw(seed, step0 + t, env, 1u, a4);
-            int nl = __builtin_popcount(m), k = (int)(((uint64_t)a4[0] * (uint32_t)nl) >> 32), dir = 0;
-            for (int d = 0; d < 4; d++)
-                if (m >> d & 1) { if (k == 0) { dir = d; break; } k--; }
-            or_rng r = {OR_RNG_PHILOX, env, seed, step0 + t, NULL, 0, 0};
-            or_step_out o;
-            or_step(b, dir, &r, full_info, &o);
+    for (int64_t i = 0; i < n_envs; i++) {
+        int8_t *b = boards + 16 * i;
+        uint32_t env = env_base + (uint32_t)i;
+        if (or_legal_mask(b) == 0) {
+            or_rng r0 = {OR_RNG_PHILOX, env, seed, step0 + (uint64_t)steps, NULL, 0, 0};
+            or_reset(b, &r0);
+        }
+        for (int64_t t = 0; t < steps; t++) {
+            int64_t o = t * n_envs + i;
+            if (rec_boards) memcpy(rec_boards + 16 * o, b, 16);
+            or_rng r = {OR_RNG_PHILOX, env, seed, step0 + (uint64_t)t, NULL, 0, 0};
+            or_step_out so;
+            int dir = or_step_random(b, &r, full_info, &so);
+            int m = or_legal_mask(b), fl = m;
+            if (so.done) {
+                or_reset(b, &r);
+                fl = 0x80 | 0x20 | or_legal_mask(b);
+            }
+            if (rec_act) rec_act[o] = (uint8_t)dir;
+            if (rec_pts) rec_pts[o] = (int32_t)so.points;
+            if (rec_pot) {
+                rec_pot[4 * o + 0] = (int8_t)so.mono_b; rec_pot[4 * o + 1] = (int8_t)so.mono_a;
+                rec_pot[4 * o + 2] = (int8_t)so.empt_b; rec_pot[4 * o + 3] = (int8_t)so.empt_a;
+            }
+            if (rec_flags) rec_flags[o] = (uint8_t)fl;
             count++;
-            if (o.done) or_reset(b, &r);
         }
     }
     return count;
+}
+
+int64_t or_random_rollout(int8_t *boards, int64_t n_envs, int64_t steps, uint64_t seed, uint64_t step0,
+                          uint32_t env_base, int full_info) {
+    return or_random_rollout_rec(boards, n_envs, steps, seed, step0, env_base, full_info, NULL, NULL, NULL, NULL,
+                                 NULL);
+}
+
+void or_step_random_batch(int8_t *boards, int64_t n, uint64_t seed, uint64_t step, uint32_t env_base,
+                          int64_t *out_i64 /* [n,11]: step fields + action */) {
+    for (int64_t i = 0; i < n; i++) {
+        or_rng r = {OR_RNG_PHILOX, env_base + (uint32_t)i, seed, step, NULL, 0, 0};
+        or_step_out o;
+        int dir = or_step_random(boards + 16 * i, &r, 0, &o);
+        int64_t *q = out_i64 + 11 * i;
+        q[0] = o.points; q[1] = o.max_tile; q[2] = o.invalid; q[3] = o.done;
+        q[4] = o.mono_b; q[5] = o.mono_a; q[6] = o.empt_b; q[7] = o.empt_a;
+        q[8] = o.maxexp_b; q[9] = o.maxexp_a; q[10] = dir;
+    }
 }

@@ -65,6 +65,9 @@ def _declare(L):
     L.or_philox4x32_10.argtypes = [vp, vp, vp]
     L.or_random_rollout.argtypes = [vp, i64, i64, u64, u64, u32, i32]
     L.or_random_rollout.restype = i64
+    L.or_random_rollout_rec.argtypes = [vp, i64, i64, u64, u64, u32, i32, vp, vp, vp, vp, vp]
+    L.or_random_rollout_rec.restype = i64
+    L.or_step_random_batch.argtypes = [vp, i64, u64, u64, u32, vp]
 
 
 def _boards(b) -> np.ndarray:
@@ -183,6 +186,26 @@ def random_rollout(boards, steps, seed, step0=0, env_base=0, full_info=True):
     """In-place CPU random-legal rollout with auto-reset; returns transitions executed."""
     b = _boards(boards)
     return lib().or_random_rollout(_p(b), len(b), steps, seed, step0, env_base, int(full_info)), b
+
+
+def random_rollout_record(boards, steps, seed, step0=0, env_base=0):
+    """Checker of env_rollout_kernel: returns (final boards, dict of [steps, n] records)."""
+    b = _boards(boards).copy()
+    n = len(b)
+    rec = {"boards": np.zeros((steps, n, 16), np.int8), "actions": np.zeros((steps, n), np.uint8),
+           "points": np.zeros((steps, n), np.int32), "pot": np.zeros((steps, n, 4), np.int8),
+           "flags": np.zeros((steps, n), np.uint8)}
+    lib().or_random_rollout_rec(_p(b), n, steps, seed, step0, env_base, 0, _p(rec["boards"]), _p(rec["actions"]),
+                                _p(rec["points"]), _p(rec["pot"]), _p(rec["flags"]))
+    return b, rec
+
+
+def step_random(boards, seed, step_idx=0, env_base=0):
+    """The synthetic-policy step (one stream-1 draw for action + spawn). Returns (boards, fields, actions)."""
+    b = _boards(boards).copy()
+    out = np.zeros((len(b), 11), np.int64)
+    lib().or_step_random_batch(_p(b), len(b), seed, step_idx, env_base, _p(out))
+    return b, {k: out[:, i] for i, k in enumerate(STEP_FIELDS)}, out[:, 10]
 
 
 # ---------------------------------------------------------------- policy / returns --------------

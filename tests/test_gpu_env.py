@@ -165,30 +165,45 @@ def test_best_game_replay_injected(dev):
 
 @pytest.mark.parametrize("seed", [1, 2])
 def test_philox_random_steps_match_oracle(dev, seed):
-    """Random legal actions + spawns drawn in-kernel (Philox) reproduce on the CPU oracle exactly."""
-    lib = L()
+    """Random legal actions + spawns drawn in-kernel (one Philox stream-1 draw) reproduce on the oracle."""
     n = 1 << 16
     boards = random_boards(n, seed, hi=17)
     ctr = 12345 + seed
     b, aout, pts, mx, pot, fl = gpu_step(boards, None, dev, seed=0x2048 + seed, counter=ctr, random_actions=True,
                                          env_base=777)
-    # oracle: the k-th legal action from Philox stream 1
-    masks = O.legal_mask(boards)
-    draws = O.philox_draws(0x2048 + seed, ctr, n, 1, env_base=777)
-    nl = np.array([bin(m).count("1") for m in masks], np.uint64)
-    k = (draws[:, 0].astype(np.uint64) * nl) >> np.uint64(32)
-    exp_a = np.zeros(n, np.int64)
-    for i in range(n):
-        legal = [d for d in range(4) if masks[i] >> d & 1]
-        exp_a[i] = legal[int(k[i])] if legal else 0
-    assert np.array_equal(aout, exp_a)
-    ob, f, _, _ = O.step(boards, exp_a, O.RNG_PHILOX, seed=0x2048 + seed, step_idx=ctr, env_base=777)
+    ob, f, oa = O.step_random(boards, 0x2048 + seed, ctr, env_base=777)
+    playable = O.legal_mask(boards) != 0
+    assert np.array_equal(aout[playable], oa[playable])
     assert np.array_equal(b, ob)
     assert np.array_equal(pts, f["points"])
     assert np.array_equal(pot[:, 0], f["mono_b"]) and np.array_equal(pot[:, 1], f["mono_a"])
     assert np.array_equal(pot[:, 2], f["empt_b"]) and np.array_equal(pot[:, 3], f["empt_a"])
     assert np.array_equal(fl >> 7, f["done"])
     assert np.array_equal(fl & 0xF, O.legal_mask(ob))
+
+
+@pytest.mark.parametrize("n,steps", [(4096, 200), (1000, 64)])
+def test_rollout_kernel_trajectories_match_oracle(dev, n, steps):
+    """env_rollout_kernel (the bench workload): every per-step record bit-exact vs the oracle."""
+    lib = L()
+    init = O.reset(n, O.RNG_PHILOX, seed=31, step_idx=0, env_base=5)
+    init[:7] = np.array([1, 2, 1, 2, 2, 1, 2, 1, 1, 2, 1, 2, 2, 1, 2, 1], np.int8)  # finished boards handed in
+    b = to_dev(init, torch.int8, dev)
+    tb = torch.zeros(steps, n, 16, dtype=torch.int8, device=dev)
+    ta = torch.zeros(steps, n, dtype=torch.uint8, device=dev)
+    tp = torch.zeros(steps, n, dtype=torch.int32, device=dev)
+    tpot = torch.zeros(steps, n, 4, dtype=torch.int8, device=dev)
+    tf = torch.zeros(steps, n, dtype=torch.uint8, device=dev)
+    lib.env_rollout_random(b, steps, tb, ta, tp, tpot, tf, lib.make_rng(lib.RNG_PHILOX, 31, 1, 5))
+    torch.cuda.synchronize()
+    ob, rec = O.random_rollout_record(init, steps, 31, step0=1, env_base=5)
+    assert np.array_equal(tb.cpu().numpy(), rec["boards"])
+    assert np.array_equal(ta.cpu().numpy(), rec["actions"])
+    assert np.array_equal(tp.cpu().numpy(), rec["points"])
+    assert np.array_equal(tpot.cpu().numpy(), rec["pot"])
+    assert np.array_equal(tf.cpu().numpy(), rec["flags"])
+    assert np.array_equal(b.cpu().numpy(), ob)
+    assert (rec["flags"] & 0x80).sum() > 0  # episodes ended and were reset inside the launch
 
 
 def test_auto_reset_matches_oracle(dev):
