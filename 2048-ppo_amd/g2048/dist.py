@@ -64,6 +64,10 @@ class GradBucket:
     def zero(self):
         self.flat.zero_()
 
+    @staticmethod
+    def world() -> int:
+        return dist.get_world_size() if dist.is_initialized() else 1
+
     def allreduce_mean(self):
         if dist.is_initialized() and dist.get_world_size() > 1:
             dist.all_reduce(self.flat)

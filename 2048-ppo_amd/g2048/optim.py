@@ -72,3 +72,151 @@ def build_optimizer(model, lr: float, critic_lr: float, beta1: float = 0.9, beta
     lam = cosine_with_warmup(warmup_steps, total_steps)
     return MultiOptimizer((muon, torch.optim.lr_scheduler.LambdaLR(muon, lam)),
                           (adamw, torch.optim.lr_scheduler.LambdaLR(adamw, lam)))
+
+
+class MuonAdamW:
+    """Graph-capturable Muon (2-D weights) + AdamW (1-D) with the reference's parameter groups.
+
+    Same arithmetic as torch.optim.Muon(adjust_lr_fn="match_rms_adamw", nesterov) and
+    torch.optim.AdamW, but learning rates and the Adam step count live in device tensors, so one
+    optimizer step contains no host scalars and can sit inside a captured hipGraph; the LR schedule
+    is applied with set_lr_scale() between replays.  The 1-D parameters (LayerNorm, biases) are
+    re-homed into one flat buffer per group, so AdamW is a handful of kernels on two flat vectors.
+    """
+
+    def __init__(self, model, lr: float, critic_lr: float, beta1=0.9, beta2=0.999, weight_decay=0.01,
+                 momentum=0.95, nesterov=True, ns_coefficients=(3.4445, -4.775, 2.0315), ns_steps=5,
+                 ns_eps=1e-7, adam_eps=1e-8):
+        o2d, o1d, v2d, v1d = model.get_param_groups(critic_lr, lr)
+        dev = next(model.parameters()).device
+        self.dev = dev
+        self.base = [o2d["lr"], o1d["lr"], v2d["lr"], v1d["lr"]]
+        self.lr = torch.tensor(self.base, dtype=torch.float32, device=dev)
+        self.wd, self.b1, self.b2, self.eps = weight_decay, beta1, beta2, adam_eps
+        self.momentum, self.nesterov = momentum, nesterov
+        self.ns, self.ns_steps, self.ns_eps = ns_coefficients, ns_steps, ns_eps
+        self.muon = [(p, 0) for p in o2d["params"]] + [(p, 2) for p in v2d["params"]]
+        self.muon_buf = [torch.zeros_like(p) for p, _ in self.muon]
+        self.adam_groups = []
+        for gi, grp in ((1, o1d), (3, v1d)):
+            ps = list(grp["params"])
+            if not ps:
+                continue
+            flat = torch.cat([p.detach().reshape(-1) for p in ps]).contiguous()
+            off = 0
+            for p in ps:
+                n = p.numel()
+                p.data = flat[off:off + n].view_as(p)
+                off += n
+            self.adam_groups.append({"idx": gi, "params": ps, "flat": flat, "m": torch.zeros_like(flat),
+                                     "v": torch.zeros_like(flat)})
+        self.step_t = torch.zeros((), dtype=torch.float32, device=dev)
+        self.scale = 1.0
+
+    def set_lr_scale(self, s: float):
+        self.scale = s
+        self.lr.copy_(torch.tensor([b * s for b in self.base], dtype=torch.float32))
+
+    def get_lr(self):
+        return [b * self.scale for b in self.base]
+
+    @staticmethod
+    def _flat_grad(group):
+        ps = group["params"]
+        base = ps[0].grad
+        # grads of a group are contiguous views when the GradBucket was built in the same order
+        if all(p.grad is not None for p in ps):
+            start = base.data_ptr()
+            total = sum(p.numel() for p in ps)
+            if all(p.grad.data_ptr() == start + 4 * sum(q.numel() for q in ps[:k]) for k, p in enumerate(ps)):
+                return base.reshape(-1).as_strided((total,), (1,))
+        return torch.cat([p.grad.reshape(-1) for p in ps])
+
+    def _newton_schulz(self, g):
+        a, b, c = self.ns
+        x = g.bfloat16()
+        tr = g.size(0) > g.size(1)
+        if tr:
+            x = x.T
+        x = x / x.norm().clamp(min=self.ns_eps)
+        for _ in range(self.ns_steps):
+            gram = x @ x.T
+            upd = torch.addmm(gram, gram, gram, beta=b, alpha=c)
+            x = torch.addmm(x, upd, x, beta=a)
+        if tr:
+            x = x.T
+        return x
+
+    @torch.no_grad()
+    def step(self):
+        # Muon (torch/optim/_muon.py semantics)
+        for (p, gi), buf in zip(self.muon, self.muon_buf):
+            g = p.grad
+            buf.lerp_(g, 1 - self.momentum)
+            upd = g.lerp(buf, self.momentum) if self.nesterov else buf
+            upd = self._newton_schulz(upd)
+            lr = self.lr[gi]
+            A, B = p.shape[:2]
+            p.mul_(1 - lr * self.wd)
+            p.sub_(upd.to(p.dtype) * (lr * (0.2 * math.sqrt(max(A, B)))))
+        # AdamW (torch/optim/adamw.py semantics, decoupled weight decay)
+        self.step_t.add_(1)
+        bc1 = 1 - self.b1 ** self.step_t
+        bc2_sqrt = (1 - self.b2 ** self.step_t).sqrt()
+        for grp in self.adam_groups:
+            lr = self.lr[grp["idx"]]
+            flat, m, v = grp["flat"], grp["m"], grp["v"]
+            g = self._flat_grad(grp)
+            flat.mul_(1 - lr * self.wd)
+            m.lerp_(g, 1 - self.b1)
+            v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+            denom = (v.sqrt() / bc2_sqrt).add_(self.eps)
+            flat.sub_((lr / bc1) * m / denom)
+
+    def zero_grad(self, set_to_none: bool = False):
+        pass  # gradients live in the trainer's GradBucket, zeroed there
+
+    def state_dict(self):
+        return {"lr": self.lr.cpu(), "step": self.step_t.cpu(), "muon_buf": [b.cpu() for b in self.muon_buf],
+                "adam": [{"m": g["m"].cpu(), "v": g["v"].cpu()} for g in self.adam_groups], "scale": self.scale}
+
+    def snapshot(self):
+        return ([b.clone() for b in self.muon_buf], [(g["m"].clone(), g["v"].clone()) for g in self.adam_groups],
+                self.step_t.clone())
+
+    def restore(self, snap):
+        bufs, adam, st = snap
+        for b, s in zip(self.muon_buf, bufs):
+            b.copy_(s)
+        for g, (m, v) in zip(self.adam_groups, adam):
+            g["m"].copy_(m)
+            g["v"].copy_(v)
+        self.step_t.copy_(st)
+
+
+class ScheduledMuonAdamW:
+    """MuonAdamW + the cosine-with-warmup schedule stepped once per train step (train.py:1598-1612, :625)."""
+
+    def __init__(self, opt: MuonAdamW, warmup: int, total: int):
+        self.opt = opt
+        self.fn = cosine_with_warmup(warmup, total)
+        self.t = 0
+        self.opt.set_lr_scale(self.fn(0))
+        self.optimizers = [self]
+
+    @property
+    def param_groups(self):
+        return [{"lr": lr} for lr in self.opt.get_lr()]
+
+    def step(self):
+        self.opt.step()
+
+    def zero_grad(self, set_to_none: bool = False):
+        pass
+
+    def scheduler_step(self):
+        self.t += 1
+        self.opt.set_lr_scale(self.fn(self.t))
+
+    def state_dict(self):
+        return {"opt": self.opt.state_dict(), "t": self.t}

@@ -66,17 +66,27 @@ def kl_old_new(old_masked_logits, new_logits, invalid):
 
 
 class PPOUpdater:
-    """Minibatch PPO over a flat trajectory.  `grads` is a dist.GradBucket (flat .grad views)."""
+    """Minibatch PPO over a flat trajectory.  `grads` is a dist.GradBucket (flat .grad views).
 
-    def __init__(self, model, optimizer, cfg: PPOConfig, grads, generator: torch.Generator | None = None):
+    graph=True (device tensors, graph-safe optimizer such as optim.MuonAdamW): the whole minibatch
+    step -- gather, encode, forward, loss, backward, clip, optimizer, KL diagnostic, statistics --
+    is captured once into a hipGraph and replayed per minibatch with a new index vector; with
+    several ranks the step is split into two graphs around the eager RCCL gradient all-reduce.
+    """
+
+    def __init__(self, model, optimizer, cfg: PPOConfig, grads, generator: torch.Generator | None = None,
+                 graph: bool = False):
         self.model, self.opt, self.cfg, self.grads = model, optimizer, cfg, grads
         self.gen = generator
         self.dev = next(model.parameters()).device
         self.stats = torch.zeros(len(STAT_KEYS), dtype=torch.float32, device=self.dev)
+        self.graph = graph and self.dev.type == "cuda"
+        self.beta_t = torch.zeros((), dtype=torch.float32, device=self.dev)
+        self._g = None
 
     def _forward(self, obs):
         if self.cfg.amp_dtype is not None and obs.is_cuda:
-            with torch.autocast("cuda", dtype=self.cfg.amp_dtype):
+            with torch.autocast("cuda", dtype=self.cfg.amp_dtype, cache_enabled=not self.graph):
                 logits, value = self.model(obs)
         else:
             logits, value = self.model(obs)
@@ -89,19 +99,27 @@ class PPOUpdater:
         m_total = data["actions"].shape[0]
         bs = min(cfg.batch_size, m_total)
         self.stats.zero_()
+        self.beta_t.fill_(beta)
         nb = 0
         self.model.train()
+        use_graph = self.graph and m_total % bs == 0
+        if use_graph:
+            self._ensure_graph(data, bs, encode)
         for _ in range(cfg.epochs):
             perm = torch.randperm(m_total, device=self.dev, generator=self.gen)
             for s in range(0, m_total, bs):
                 idx = perm[s:s + bs]
-                self._minibatch(idx, data, beta, encode)
+                if use_graph:
+                    self._replay(idx)
+                else:
+                    self._minibatch(idx, data, self.beta_t, encode)
                 nb += 1
         st = self.stats / max(nb, 1)
         st[STAT_KEYS.index("kl_max")] = self.stats[STAT_KEYS.index("kl_max")]
         return {k: st[i] for i, k in enumerate(STAT_KEYS)}
 
-    def _minibatch(self, idx, data, beta, encode):
+    # ---------------------------------------------------------------- eager minibatch ------
+    def _pre(self, idx, data, beta, encode):
         cfg = self.cfg
         obs = encode(data["boards"].index_select(0, idx))
         actions = data["actions"].index_select(0, idx)
@@ -113,16 +131,70 @@ class PPOUpdater:
         loss, parts = ppo_losses(logits, value, actions, invalid, old_logp, adv, ret, beta, cfg.critic, cfg.clip_eps)
         self.grads.zero()
         loss.backward()
-        self.grads.allreduce_mean()
+        return {"obs": obs, "invalid": invalid, "loss": loss.detach(), "ppo": parts["ppo"].detach(),
+                "entropy": parts["entropy"].detach(), "vloss": parts["vloss"].detach(),
+                "masked": parts["masked"].detach()}
+
+    def _post(self, st, beta):
+        cfg = self.cfg
         gn = self.grads.clip_(cfg.max_grad_norm)
         self.opt.step()
         with torch.no_grad():
-            new_logits, _ = self._forward(obs)
-            kl = kl_old_new(parts["masked"].detach(), new_logits, invalid)
+            new_logits, _ = self._forward(st["obs"])
+            kl = kl_old_new(st["masked"], new_logits, st["invalid"])
             vals = torch.stack([
-                loss.detach(), -parts["ppo"].detach().mean(), -beta * parts["entropy"].detach().mean(),
-                cfg.critic * parts["vloss"].detach().mean(), gn, parts["entropy"].detach().mean(), kl.sum(),
-                kl.mean(), torch.zeros((), device=self.dev)])
+                st["loss"], -st["ppo"].mean(), -beta * st["entropy"].mean(), cfg.critic * st["vloss"].mean(), gn,
+                st["entropy"].mean(), kl.sum(), kl.mean(), torch.zeros((), device=self.dev)])
             self.stats.add_(vals)
             k = STAT_KEYS.index("kl_max")
             self.stats[k] = torch.maximum(self.stats[k], kl.max())
+
+    def _minibatch(self, idx, data, beta, encode):
+        st = self._pre(idx, data, beta, encode)
+        self.grads.allreduce_mean()
+        self._post(st, beta)
+
+    # ---------------------------------------------------------------- graphed minibatch ----
+    def _ensure_graph(self, data, bs, encode):
+        key = (bs,) + tuple(t.data_ptr() for t in data.values())
+        if self._g is not None and self._g["key"] == key:
+            return
+        self._g = None
+        torch.cuda.synchronize()
+        split = self.grads.world() > 1
+        idx = torch.zeros(bs, dtype=torch.int64, device=self.dev)
+        params = [p for p in self.model.parameters()]
+        snap_p = [p.detach().clone() for p in params]
+        snap_o = self.opt.snapshot()
+        snap_s = self.stats.clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm-up outside the capture (library handles, autograd plans)
+                self._minibatch(idx, data, self.beta_t, encode)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g1, g2 = torch.cuda.CUDAGraph(), None
+        pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(g1, pool=pool):
+            st = self._pre(idx, data, self.beta_t, encode)
+            if not split:
+                self._post(st, self.beta_t)
+        if split:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2, pool=pool):
+                self._post(st, self.beta_t)
+        with torch.no_grad():
+            for p, q in zip(params, snap_p):
+                p.copy_(q)
+        self.opt.restore(snap_o)
+        self.stats.copy_(snap_s)
+        self._g = {"key": key, "idx": idx, "g1": g1, "g2": g2, "st": st}
+
+    def _replay(self, idx):
+        g = self._g
+        g["idx"].copy_(idx)
+        g["g1"].replay()
+        if g["g2"] is not None:
+            self.grads.allreduce_mean()
+            g["g2"].replay()

@@ -21,7 +21,7 @@ import torch
 from . import _lib as L
 from .advantage import RewardWeights, RTGTracker
 from .dist import GradBucket, allreduce_sum_, world
-from .optim import build_optimizer
+from .optim import MuonAdamW, ScheduledMuonAdamW, build_optimizer
 from .ppo import PPOConfig, PPOUpdater
 from .rollout import InferencePolicy, Rollout
 
@@ -58,6 +58,7 @@ class TrainConfig:
     horizon: int = 0
     seed: int = 0x2048
     graph: bool = True
+    graph_update: bool = True      # hipGraph-captured PPO minibatch step (graph-safe Muon+AdamW)
     amp: bool = True
     episodic_cap: int = 4096       # step cap of an episodic rollout without --max-steps
     chunk: int = 32                # episodic: steps between "all games over?" checks
@@ -82,9 +83,16 @@ class VecTrainer:
         if self.world > 1:  # identical initial replicas
             for p in self.model.parameters():
                 torch.distributed.broadcast(p.data, 0)
-        self.grads = GradBucket(self.model.parameters())
-        self.opt = build_optimizer(self.model, cfg.lr, cfg.critic_lr, cfg.beta1, cfg.beta2, cfg.weight_decay,
-                                   cfg.warmup_steps, cfg.steps)
+        if cfg.graph_update:
+            opt = MuonAdamW(self.model, cfg.lr, cfg.critic_lr, cfg.beta1, cfg.beta2, cfg.weight_decay)
+            self.opt = ScheduledMuonAdamW(opt, cfg.warmup_steps, cfg.steps)
+            # grads of the AdamW groups contiguous in the bucket (2-D first, then each 1-D group)
+            order = [p for p, _ in opt.muon] + [p for g in opt.adam_groups for p in g["params"]]
+            self.grads = GradBucket(order)
+        else:
+            self.grads = GradBucket(self.model.parameters())
+            self.opt = build_optimizer(self.model, cfg.lr, cfg.critic_lr, cfg.beta1, cfg.beta2, cfg.weight_decay,
+                                       cfg.warmup_steps, cfg.steps)
         self.policy = InferencePolicy(self.model, torch.bfloat16 if cfg.amp else torch.float32)
         n = cfg.episodes
         self.episodic = cfg.horizon <= 0
@@ -100,7 +108,7 @@ class VecTrainer:
         self.ppo = PPOUpdater(self.model, self.opt, PPOConfig(batch_size=cfg.batch_size, epochs=cfg.epochs,
                                                               critic=cfg.critic,
                                                               amp_dtype=torch.bfloat16 if cfg.amp else None),
-                              self.grads, gen)
+                              self.grads, gen, graph=cfg.graph_update and not self.episodic)
         self.beta = cfg.entropy
         self.obs_mb = None
         self.run_score = torch.zeros(n, dtype=torch.int64, device=self.dev)
@@ -288,6 +296,8 @@ class VecTrainer:
         explained = 1.0 - av / (gns ** 2) if gns > 0 else 0.0
         self.ema["explained_var"] = (1 - 0.001) * self.ema["explained_var"] + 0.001 * explained
         lrs = [g["lr"] for g in self.opt.optimizers[0].param_groups]
+        if len(lrs) == 4:  # MuonAdamW groups: other 2-D, other 1-D, value 2-D, value 1-D
+            lrs = [lrs[0], lrs[2]]
         return {
             "samples": int(n), "augmented_samples": 0, "actor_loss": 0, "critic_loss": 0, "total_loss": 0,
             "policy_loss": pl, "entropy_loss": el, "value_loss": vl, "actor_grad_norm": 0, "critic_grad_norm": 0,

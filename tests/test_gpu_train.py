@@ -267,3 +267,44 @@ def test_ppo_updater_gpu_matches_compat_update(dev):
     np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-4, atol=2e-6)
     for k in ("loss", "policy_loss", "value_loss", "entropy", "grad_norm"):
         assert math.isclose(res[0][1][k], res[1][1][k], rel_tol=1e-4, abs_tol=1e-6), k
+
+
+def test_graphed_update_equals_eager_update(dev):
+    """The hipGraph-captured PPO minibatch step (graph-safe Muon+AdamW) == the same step run eagerly."""
+    import agent
+    from g2048 import _lib as L
+    from g2048.dist import GradBucket
+    from g2048.optim import MuonAdamW
+    from g2048.ppo import PPOConfig, PPOUpdater
+    g = np.random.default_rng(0)
+    M = 8192
+    boards = g.integers(0, 10, size=(M, 16)).astype(np.int8)
+    legal = O.legal_mask(boards)
+    legal[legal == 0] = 1
+    acts = np.array([[a for a in range(4) if m >> a & 1][0] for m in legal], np.uint8)
+    data = {"boards": torch.from_numpy(boards).to(dev), "actions": torch.from_numpy(acts).to(dev),
+            "legal": torch.from_numpy(legal).to(dev),
+            "logp": torch.from_numpy(np.log(np.full((M, 4), 0.25, np.float32))).to(dev),
+            "adv": torch.from_numpy(g.normal(size=M).astype(np.float32)).to(dev),
+            "ret": torch.from_numpy(g.normal(size=M).astype(np.float32)).to(dev)}
+
+    def enc(b):
+        o = torch.empty(b.shape[0], 48, dtype=torch.float32, device=dev)
+        L.obs_encode(b.contiguous(), o)
+        return o
+    out = []
+    for graph in (False, True):
+        torch.manual_seed(3)
+        m = agent.GameMLP(agent.MLPConfig(hidden_dim=64, num_layers=2, dropout=0.0)).to(dev)
+        opt = MuonAdamW(m, 1e-3, 1e-4)
+        order = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(5)
+        up = PPOUpdater(m, opt, PPOConfig(batch_size=2048, critic=0.2), GradBucket(order), gen, graph=graph)
+        st = None
+        for _ in range(3):
+            st = {k: float(v) for k, v in up.update(data, 0.02, enc).items()}
+        out.append((torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy(), st))
+    np.testing.assert_allclose(out[0][0], out[1][0], rtol=1e-5, atol=1e-6)
+    for k in ("loss", "entropy", "grad_norm", "kl_average"):
+        assert math.isclose(out[0][1][k], out[1][1][k], rel_tol=1e-4, abs_tol=1e-6), k
