@@ -218,5 +218,11 @@ class ScheduledMuonAdamW:
         self.t += 1
         self.opt.set_lr_scale(self.fn(self.t))
 
+    def snapshot(self):
+        return self.opt.snapshot()
+
+    def restore(self, snap):
+        self.opt.restore(snap)
+
     def state_dict(self):
         return {"opt": self.opt.state_dict(), "t": self.t}
