@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "board.hpp"
+#include "rowtable.hpp"
 #include "../../include/g2048.h"
 
 using namespace g2048;
@@ -157,61 +158,156 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(const uint4 *__restric
     flags[i] = (uint8_t)r.fl;
 }
 
+__device__ const lut::RowTable kRowLeft = lut::RowTable();
+__device__ const lut::F2Table kF2 = lut::F2Table();
+
+// nibble-pack a row dword whose bytes are < 16: b0 | b1<<4 | b2<<8 | b3<<12
+__device__ __forceinline__ uint32_t pack_nib(uint32_t x) {
+    const uint32_t t = x | (x >> 4);
+    return (t & 0xFFu) | ((t >> 8) & 0xFF00u);
+}
+// inverse of pack_nib
+__device__ __forceinline__ uint32_t unpack_nib(uint32_t r) {
+    const uint32_t t = (r | (r << 8)) & 0x00FF00FFu;
+    return (t & 0x000F000Fu) | ((t & 0x00F000F0u) << 4);
+}
+
+struct LdsTables {
+    const uint16_t *row;
+    const uint32_t *f2;
+    __device__ uint32_t F(uint32_t nib) const { return f2[nib & 0xFFu] + f2[nib >> 8]; }
+};
+
+// LEFT-frame board rows -> moved rows via the LDS table; returns F(moved rows) in fmoved.
+__device__ __forceinline__ uint4 slide_lut(const uint4 &w, const LdsTables &tb, uint32_t &fmoved) {
+    const uint32_t i0 = pack_nib(w.x), i1 = pack_nib(w.y), i2 = pack_nib(w.z), i3 = pack_nib(w.w);
+    const uint32_t o0 = tb.row[i0], o1 = tb.row[i1], o2 = tb.row[i2], o3 = tb.row[i3];
+    fmoved = tb.F(o0) + tb.F(o1) + tb.F(o2) + tb.F(o3);
+    return make_uint4(unpack_nib(o0), unpack_nib(o1), unpack_nib(o2), unpack_nib(o3));
+}
+
+__device__ __forceinline__ uint32_t board_F(const uint4 &b, const LdsTables &tb) {
+    return tb.F(pack_nib(b.x)) + tb.F(pack_nib(b.y)) + tb.F(pack_nib(b.z)) + tb.F(pack_nib(b.w));
+}
+
+// spawn on the k-th empty cell (row-major), k = floor(u0 * count / 2^32), value 1 if u1 < 0.9*2^32
+// (same result as spawn<Philox>, computed from per-row popcounts instead of a 16-bit mask)
+__device__ __forceinline__ uint32_t spawn_rows(uint4 &b, uint32_t u0, uint32_t u1) {
+    const uint32_t z0 = zm(b.x), z1 = zm(b.y), z2 = zm(b.z), z3 = zm(b.w);
+    const uint32_t c0 = __popc(z0), c1 = __popc(z1), c2 = __popc(z2), c3 = __popc(z3);
+    const uint32_t cnt = c0 + c1 + c2 + c3;
+    uint32_t k = (uint32_t)(((uint64_t)u0 * cnt) >> 32);
+    const bool g0 = k >= c0;
+    k -= g0 ? c0 : 0u;
+    const bool g1 = g0 && k >= c1;
+    k -= g1 ? c1 : 0u;
+    const bool g2 = g1 && k >= c2;
+    k -= g2 ? c2 : 0u;
+    const uint32_t row = (uint32_t)g0 + (uint32_t)g1 + (uint32_t)g2;
+    const uint32_t z = g2 ? z3 : g1 ? z2 : g0 ? z1 : z0;
+    const uint32_t b0 = (z >> 7) & 1u, b1 = (z >> 15) & 1u, b2 = (z >> 23) & 1u;
+    const uint32_t col = (uint32_t)(k >= b0) + (uint32_t)(k >= b0 + b1) + (uint32_t)(k >= b0 + b1 + b2);
+    const uint32_t v = u1 < kTwoThreshold ? 1u : 2u;
+    const uint32_t bits = v << (8u * col);
+    b.x |= row == 0u ? bits : 0u;
+    b.y |= row == 1u ? bits : 0u;
+    b.z |= row == 2u ? bits : 0u;
+    b.w |= row == 3u ? bits : 0u;
+    return v;
+}
+
+__device__ __forceinline__ uint32_t board_max(const uint4 &b) {
+    uint32_t m = bytemax(bytemax(b.x, b.y), bytemax(b.z, b.w));
+    m = bytemax(m, m >> 8);
+    m = bytemax(m, m >> 16);
+    return m & 0xFFu;
+}
+
 // Synthetic random-legal rollout (the benchmark workload of BASELINE.md): `steps` env steps per
-// launch with the board kept in registers, auto-reset on done, one time-major trajectory record per
+// board per launch, board in registers, auto-reset on done, one time-major trajectory record per
 // step: the board the action was taken on [T][N][16], action, points, potentials, flags.
-// Per step: ONE Philox draw (x: action, y/z: spawn), the legal mask carried from the previous
-// step (the action is always legal, so the illegal-move path of step_board cannot occur), and
-// trajectory pointers advanced by a uniform stride instead of 64-bit t*n products.
-__global__ __launch_bounds__(kBlock) void env_rollout_kernel(uint4 *__restrict__ boards, int64_t n, int64_t steps,
-                                                             uint4 *__restrict__ tb, uint8_t *__restrict__ ta,
-                                                             int32_t *__restrict__ tp, uint32_t *__restrict__ tpot,
-                                                             uint8_t *__restrict__ tf, RngArgs rng) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    uint4 b = boards[i];
+// Per step: ONE Philox draw (x: action, y/z: spawn); the legal mask carried from the previous
+// step (the action is always legal); the move through the LDS row table while every exponent is
+// <= 14 (the SWAR compute path otherwise); merge points from the F identity.  Workgroups are
+// persistent over boards, so large N keeps several waves per SIMD with one LDS table per CU.
+__global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ boards, int64_t n, int64_t steps,
+                                                           uint4 *__restrict__ tb, uint8_t *__restrict__ ta,
+                                                           int32_t *__restrict__ tp, uint32_t *__restrict__ tpot,
+                                                           uint8_t *__restrict__ tf, RngArgs rng) {
+    __shared__ __attribute__((aligned(16))) uint16_t s_row[65536];
+    __shared__ uint32_t s_f2[256];
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(kRowLeft.v);
+        uint4 *dst = reinterpret_cast<uint4 *>(s_row);
+        for (int k = threadIdx.x; k < 65536 * 2 / 16; k += blockDim.x) dst[k] = src[k];
+        for (int k = threadIdx.x; k < 256; k += blockDim.x) s_f2[k] = kF2.v[k];
+    }
+    __syncthreads();
+    const LdsTables tabs{s_row, s_f2};
     const uint64_t ctr0 = rng_counter(rng);
-    const uint32_t env = rng.env_base + (uint32_t)i;
-    uint32_t legal = legal_mask(b);
-    if (legal == 0u) {  // a finished board handed in: start a new game first (as auto-reset would)
-        b = fresh_board<G2048_RNG_PHILOX>(nullptr, rng, i, ctr0 + (uint64_t)steps);
-        legal = legal_mask(b);
-    }
-    if (tb) tb += i;
-    if (ta) ta += i;
-    if (tp) tp += i;
-    if (tpot) tpot += i;
-    if (tf) tf += i;
-    for (int64_t t = 0; t < steps; t++) {
-        if (tb) { *tb = b; tb += n; }
-        const uint64_t ctr = ctr0 + (uint64_t)t;
-        const uint4 d = philox_draw(rng.seed, ctr, env, 1u);
-        const uint32_t a = kth_bit16(legal, (uint32_t)(((uint64_t)d.x * (uint32_t)__popc(legal)) >> 32));
-        const int mono_b = monotonicity(b);
-        const int empt_b = emptiness(b);
-        uint32_t pts, mx;
-        uint4 moved = apply_move(b, a, pts, mx);
-        const int mono_a = monotonicity(moved);
-        const int empt_a = emptiness(moved);
-        spawn<G2048_RNG_PHILOX>(moved, d.y, d.z, nullptr, rng, i);
-        b = moved;
-        legal = legal_mask(b);
-        uint32_t fl = legal;
-        if (legal == 0u) {
-            b = fresh_board<G2048_RNG_PHILOX>(nullptr, rng, i, ctr);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint4 b = boards[i];
+        const uint32_t env = rng.env_base + (uint32_t)i;
+        uint32_t legal = legal_mask(b);
+        if (legal == 0u) {  // a finished board handed in: start a new game first (as auto-reset would)
+            b = fresh_board<G2048_RNG_PHILOX>(nullptr, rng, i, ctr0 + (uint64_t)steps);
             legal = legal_mask(b);
-            fl = FLAG_DONE | FLAG_RESET | legal;
         }
-        if (ta) { *ta = (uint8_t)a; ta += n; }
-        if (tp) { *tp = (int32_t)pts; tp += n; }
-        if (tpot) {
-            *tpot = (uint32_t)(mono_b & 0xFF) | ((uint32_t)(mono_a & 0xFF) << 8) | ((uint32_t)(empt_b & 0xFF) << 16) |
+        uint32_t fb = board_max(b) <= 14u ? board_F(b, tabs) : 0u;
+        uint4 *pb = tb + i;
+        uint8_t *pa = ta + i, *pf = tf + i;
+        int32_t *pp = tp + i;
+        uint32_t *ppot = tpot + i;
+        for (int64_t t = 0; t < steps; t++) {
+            *pb = b;
+            pb += n;
+            const uint64_t ctr = ctr0 + (uint64_t)t;
+            const uint4 d = philox_draw(rng.seed, ctr, env, 1u);
+            const uint32_t a = kth_bit16(legal, (uint32_t)(((uint64_t)d.x * (uint32_t)__popc(legal)) >> 32));
+            const int mono_b = monotonicity(b);
+            const int empt_b = emptiness(b);
+            uint32_t pts;
+            uint4 moved;
+            if (board_max(b) <= 14u) {
+                const bool vert = a < 2u, rev = (a == 1u) | (a == 3u);
+                uint4 w = sel4(vert, transpose(b), b);
+                w = sel4(rev, bswap4(w), w);
+                uint32_t fm;
+                w = slide_lut(w, tabs, fm);
+                w = sel4(rev, bswap4(w), w);
+                moved = sel4(vert, transpose(w), w);
+                pts = fm - fb;
+                fb = fm;
+            } else {
+                uint32_t mx;
+                moved = apply_move(b, a, pts, mx);
+            }
+            const int mono_a = monotonicity(moved);
+            const int empt_a = emptiness(moved);
+            const uint32_t v = spawn_rows(moved, d.y, d.z);
+            fb += v == 2u ? 4u : 0u;  // F(2^2) = 4, F(2^1) = 0
+            b = moved;
+            legal = legal_mask(b);
+            uint32_t fl = legal;
+            if (legal == 0u) {
+                b = fresh_board<G2048_RNG_PHILOX>(nullptr, rng, i, ctr);
+                legal = legal_mask(b);
+                fl = FLAG_DONE | FLAG_RESET | legal;
+                fb = board_F(b, tabs);
+            }
+            *pa = (uint8_t)a;
+            pa += n;
+            *pp = (int32_t)pts;
+            pp += n;
+            *ppot = (uint32_t)(mono_b & 0xFF) | ((uint32_t)(mono_a & 0xFF) << 8) | ((uint32_t)(empt_b & 0xFF) << 16) |
                     ((uint32_t)(empt_a & 0xFF) << 24);
-            tpot += n;
+            ppot += n;
+            *pf = (uint8_t)fl;
+            pf += n;
         }
-        if (tf) { *tf = (uint8_t)fl; tf += n; }
+        boards[i] = b;
     }
-    boards[i] = b;
 }
 
 template <int Mode>
@@ -558,12 +654,18 @@ int g2048_env_rollout_random(g2048_stream_t stream, int8_t *boards, int64_t n, i
                              const g2048_rng *rng) {
     if (n < 0 || steps < 0 || !rng || rng->mode != G2048_RNG_PHILOX) return G2048_EINVAL;
     if (n == 0 || steps == 0) return G2048_OK;
-    if (!boards || !aligned16(boards) || (traj_boards && !aligned16(traj_boards)) ||
-        (traj_pot && ((uintptr_t)traj_pot & 3u)))
+    if (!boards || !traj_boards || !traj_actions || !traj_points || !traj_pot || !traj_flags || !aligned16(boards) ||
+        !aligned16(traj_boards) || ((uintptr_t)traj_pot & 3u) || ((uintptr_t)traj_points & 3u))
         return G2048_EINVAL;
-    hipLaunchKernelGGL(env_rollout_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, (hipStream_t)stream, (uint4 *)boards, n,
-                       steps, (uint4 *)traj_boards, traj_actions, traj_points, (uint32_t *)traj_pot, traj_flags,
-                       rng_args(rng));
+    // one workgroup per CU holds the 129 KiB LDS tables; its size scales with N up to 1024 threads
+    // so that large N runs 4 waves per SIMD while N = 65 536 still spreads over all 256 CUs
+    int64_t threads = (n + 255) / 256;
+    threads = threads < 64 ? 64 : threads > 1024 ? 1024 : ((threads + 63) / 64) * 64;
+    int64_t grid = (n + threads - 1) / threads;
+    grid = grid > 256 ? 256 : grid;
+    hipLaunchKernelGGL(env_rollout_kernel, dim3((unsigned)grid), dim3((unsigned)threads), 0, (hipStream_t)stream,
+                       (uint4 *)boards, n, steps, (uint4 *)traj_boards, traj_actions, traj_points, (uint32_t *)traj_pot,
+                       traj_flags, rng_args(rng));
     return launch_status();
 }
 

@@ -100,7 +100,7 @@ int g2048_env_step(g2048_stream_t stream, const int8_t *boards_in, int8_t *board
 /* Synthetic random-action rollout (the BASELINE.md throughput workload): `steps` consecutive
    Game2048.step calls per env in ONE launch, board held in registers, uniform random legal actions
    (Philox stream 1), auto-reset on done.  Step t uses Philox counter rng->counter + t (+ *counter_dev).
-   Time-major trajectory records (each nullable): traj_boards [steps][N][16] = the board the action
+   Time-major trajectory records (all required): traj_boards [steps][N][16] = the board the action
    was taken on, traj_actions/traj_flags [steps][N] uint8, traj_points [steps][N] int32,
    traj_pot [steps][N][4] int8.  boards [N,16] is read at the start and written at the end.
    Replaces the per-env `play` / random-agent loop of train.py:2184-2297 batched over N envs. */
