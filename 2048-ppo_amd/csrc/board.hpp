@@ -62,34 +62,68 @@ __device__ __forceinline__ int emptiness(const uint4 &b) {  // game.py:671-680
 // non-empty adjacent pairs) equals max(L,R) + max(T,B) with L/R/T/B those pair counts in the four
 // orientations (each rotation pairs one horizontal with one vertical orientation).  Then x2 if the
 // first row-major maximum sits in a corner, else floor(/2).
-__device__ __forceinline__ int monotonicity(const uint4 &b) {
+struct MonoStats {
+    int L, R, T, B;
+    uint32_t M;    // max exponent
+    uint32_t pos;  // first row-major cell holding M
+};
+
+__device__ __forceinline__ MonoStats mono_stats(const uint4 &b) {
     const uint32_t r[4] = {b.x, b.y, b.z, b.w};
-    int Lc = 0, Rc = 0, Tc = 0, Bc = 0;
+    uint32_t nz[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) nz[i] = nzm(r[i]);
+    MonoStats s{0, 0, 0, 0, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const uint32_t x = r[i], y = x >> 8;
-        const uint32_t both = nzm(x) & nzm(y) & 0x00808080u;
-        Lc += __popc(both & gem(x, y));
-        Rc += __popc(both & gem(y, x));
+        const uint32_t both = nz[i] & (nz[i] >> 8) & 0x00808080u;
+        s.L += __popc(both & gem(x, y));
+        s.R += __popc(both & gem(y, x));
     }
 #pragma unroll
     for (int i = 0; i < 3; i++) {
-        const uint32_t a = r[i], c = r[i + 1];
-        const uint32_t both = nzm(a) & nzm(c);
-        Tc += __popc(both & gem(a, c));
-        Bc += __popc(both & gem(c, a));
+        const uint32_t both = nz[i] & nz[i + 1];
+        s.T += __popc(both & gem(r[i], r[i + 1]));
+        s.B += __popc(both & gem(r[i + 1], r[i]));
     }
-    const int best = max(Lc, Rc) + max(Tc, Bc);
     uint32_t m = bytemax(bytemax(r[0], r[1]), bytemax(r[2], r[3]));
     m = bytemax(m, m >> 8);
     m = bytemax(m, m >> 16);
-    const uint32_t mb = (m & 0xFFu) * 0x01010101u;
+    s.M = m & 0xFFu;
+    const uint32_t mb = s.M * 0x01010101u;
     const uint64_t e01 = (uint64_t)eqm(r[0], mb) | ((uint64_t)eqm(r[1], mb) << 32);
     const uint64_t e23 = (uint64_t)eqm(r[2], mb) | ((uint64_t)eqm(r[3], mb) << 32);
     const int bit = e01 ? __builtin_ctzll(e01) : 64 + __builtin_ctzll(e23);
-    const int pos = bit >> 3;  // first row-major cell holding the max
-    const bool corner = (0x9009u >> pos) & 1u;
-    return corner ? best * 2 : best >> 1;
+    s.pos = (uint32_t)(bit >> 3);
+    return s;
+}
+
+__device__ __forceinline__ int mono_value(const MonoStats &s) {
+    const int best = max(s.L, s.R) + max(s.T, s.B);
+    return ((0x9009u >> s.pos) & 1u) ? best * 2 : best >> 1;
+}
+
+__device__ __forceinline__ int monotonicity(const uint4 &b) { return mono_value(mono_stats(b)); }
+
+// Statistics after placing exponent v on the EMPTY cell p of board b (the spawn): only the (up to
+// four) pairs through p change, and the max / first-argmax.
+__device__ __forceinline__ MonoStats mono_add_tile(MonoStats s, const uint4 &b, uint32_t p, uint32_t v) {
+    const uint32_t r = p >> 2, c = p & 3u, sh = 8u * c;
+    const uint32_t row = r == 0u ? b.x : r == 1u ? b.y : r == 2u ? b.z : b.w;
+    const uint32_t upr = r == 1u ? b.x : r == 2u ? b.y : r == 3u ? b.z : 0u;
+    const uint32_t dnr = r == 0u ? b.y : r == 1u ? b.z : r == 2u ? b.w : 0u;
+    const uint32_t left = c > 0u ? (row >> (sh - 8u)) & 0xFFu : 0u;
+    const uint32_t right = c < 3u ? (row >> (sh + 8u)) & 0xFFu : 0u;
+    const uint32_t up = (upr >> sh) & 0xFFu, dn = (dnr >> sh) & 0xFFu;
+    s.L += (left && left >= v) + (right && v >= right);
+    s.R += (left && v >= left) + (right && right >= v);
+    s.T += (up && up >= v) + (dn && v >= dn);
+    s.B += (up && v >= up) + (dn && dn >= v);
+    const bool gt = v > s.M, eq = v == s.M;
+    s.pos = gt ? p : (eq ? min(s.pos, p) : s.pos);
+    s.M = gt ? v : s.M;
+    return s;
 }
 
 __device__ __forceinline__ uint4 transpose(const uint4 &b) {

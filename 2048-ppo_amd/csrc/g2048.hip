@@ -192,7 +192,7 @@ __device__ __forceinline__ uint32_t board_F(const uint4 &b, const LdsTables &tb)
 
 // spawn on the k-th empty cell (row-major), k = floor(u0 * count / 2^32), value 1 if u1 < 0.9*2^32
 // (same result as spawn<Philox>, computed from per-row popcounts instead of a 16-bit mask)
-__device__ __forceinline__ uint32_t spawn_rows(uint4 &b, uint32_t u0, uint32_t u1) {
+__device__ __forceinline__ uint32_t spawn_rows(uint4 &b, uint32_t u0, uint32_t u1, uint32_t &pos) {
     const uint32_t z0 = zm(b.x), z1 = zm(b.y), z2 = zm(b.z), z3 = zm(b.w);
     const uint32_t c0 = __popc(z0), c1 = __popc(z1), c2 = __popc(z2), c3 = __popc(z3);
     const uint32_t cnt = c0 + c1 + c2 + c3;
@@ -208,6 +208,7 @@ __device__ __forceinline__ uint32_t spawn_rows(uint4 &b, uint32_t u0, uint32_t u
     const uint32_t b0 = (z >> 7) & 1u, b1 = (z >> 15) & 1u, b2 = (z >> 23) & 1u;
     const uint32_t col = (uint32_t)(k >= b0) + (uint32_t)(k >= b0 + b1) + (uint32_t)(k >= b0 + b1 + b2);
     const uint32_t v = u1 < kTwoThreshold ? 1u : 2u;
+    pos = 4u * row + col;
     const uint32_t bits = v << (8u * col);
     b.x |= row == 0u ? bits : 0u;
     b.y |= row == 1u ? bits : 0u;
@@ -221,44 +222,6 @@ __device__ __forceinline__ uint32_t board_max(const uint4 &b) {
     m = bytemax(m, m >> 8);
     m = bytemax(m, m >> 16);
     return m & 0xFFu;
-}
-
-// ---------------------------------------------------------------- lane-pair rollout ----------
-// Exchange a dword with the partner lane (lane ^ 1) through DPP quad_perm [1,0,3,2].
-__device__ __forceinline__ uint32_t pair_swap(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
-}
-
-// Legal-move bits of two rows (horizontal) and two vertical row pairs; OR of both lanes' parts
-// gives legal_mask() of the board.
-__device__ __forceinline__ uint32_t legal_part(uint32_t ra, uint32_t rb, uint32_t va0, uint32_t vc0, uint32_t va1,
-                                               uint32_t vc1) {
-    uint32_t L = 0, R = 0, U = 0, D = 0;
-    const uint32_t rr[2] = {ra, rb};
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-        const uint32_t x = rr[i], y = x >> 8;
-        const uint32_t nx = nzm(x), ny = nx >> 8;
-        const uint32_t zx = (nx ^ 0x80808080u) & 0x00808080u, zy = (ny ^ 0x00808080u) & 0x00808080u;
-        const uint32_t mh = nx & eqm(x, y) & 0x00808080u;
-        L |= (zx & ny) | mh;
-        R |= (nx & zy) | mh;
-    }
-    const uint32_t va[2] = {va0, va1}, vc[2] = {vc0, vc1};
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-        const uint32_t na = nzm(va[i]), nc = nzm(vc[i]);
-        const uint32_t mv = na & eqm(va[i], vc[i]);
-        U |= ((na ^ 0x80808080u) & nc) | mv;
-        D |= (na & (nc ^ 0x80808080u)) | mv;
-    }
-    return (U ? 1u : 0u) | (D ? 2u : 0u) | (L ? 4u : 0u) | (R ? 8u : 0u);
-}
-
-// lane A (odd = false): rows 0,1 and vertical pairs (0,1),(1,2); lane B: rows 2,3 and pair (2,3).
-__device__ __forceinline__ uint32_t legal_pair(const uint4 &b, bool odd) {
-    const uint32_t part = odd ? legal_part(b.z, b.w, b.z, b.w, 0u, 0u) : legal_part(b.x, b.y, b.x, b.y, b.y, b.z);
-    return part | pair_swap(part);
 }
 
 // Fresh board from one 4-word draw: the two spawns of reset() on an empty board (same result as
@@ -277,19 +240,14 @@ __device__ __forceinline__ uint4 fresh_from_words(const uint4 &r, uint32_t &f) {
 }
 
 // Synthetic random-legal rollout (the benchmark workload of BASELINE.md): `steps` env steps per
-// board per launch, auto-reset on done, one time-major trajectory record per step: the board the
-// action was taken on [T][N][16], action, points, potentials, flags.
-// Two adjacent lanes own one board (both hold it in registers) and split each step's work so
-// that N = 65 536 boards still runs two waves per SIMD:
-//   * Philox: lane A draws stream 1 (action x, spawn y/z), lane B stream 2 (reset words); DPP swap
-//   * move: each lane slides two of the four LEFT-frame rows through the LDS row table
-//     (exponents <= 14; the SWAR compute path otherwise), rows and F partials swapped back
-//   * potentials: lane A monotonicity/emptiness of the board, lane B of the moved board
-//   * legality: rows split between the lanes, masks OR-ed through a swap
-//   * stores: A writes board bytes 0-7, action, points; B bytes 8-15, flags, potentials
-// Merge points come from the F identity (rowtable.hpp).  Workgroups are persistent over boards.
+// board per launch, board in registers, auto-reset on done, one time-major trajectory record per
+// step: the board the action was taken on [T][N][16], action, points, potentials, flags.
+// Per step: ONE Philox draw (x: action, y/z: spawn); the legal mask carried from the previous
+// step (the action is always legal); the move through the LDS row table while every exponent is
+// <= 14 (the SWAR compute path otherwise); merge points from the F identity.  Workgroups are
+// persistent over boards, so large N keeps several waves per SIMD with one LDS table per CU.
 __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ boards, int64_t n, int64_t steps,
-                                                           uint2 *__restrict__ tb, uint8_t *__restrict__ ta,
+                                                           uint4 *__restrict__ tb, uint8_t *__restrict__ ta,
                                                            int32_t *__restrict__ tp, uint32_t *__restrict__ tpot,
                                                            uint8_t *__restrict__ tf, RngArgs rng) {
     __shared__ __attribute__((aligned(16))) uint16_t s_row[65536];
@@ -303,45 +261,39 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
     __syncthreads();
     const LdsTables tabs{s_row, s_f2};
     const uint64_t ctr0 = rng_counter(rng);
-    const bool odd = (threadIdx.x & 1u) != 0u;
-    const int64_t pairs_per_grid = ((int64_t)gridDim.x * blockDim.x) >> 1;
-    // blockDim is even, so a pair never straddles workgroups and both lanes run the same trip count
-    for (int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 1; j < n; j += pairs_per_grid) {
-        uint4 b = boards[j];
-        const uint32_t env = rng.env_base + (uint32_t)j;
-        uint32_t legal = legal_pair(b, odd);
-        if (legal == 0u) {  // a finished board handed in: new game first (counter ctr0 + steps)
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint4 b = boards[i];
+        const uint32_t env = rng.env_base + (uint32_t)i;
+        uint32_t legal = legal_mask(b);
+        if (legal == 0u) {  // a finished board handed in: start a new game first (counter ctr0 + steps)
             uint32_t f0;
             b = fresh_from_words(philox_draw(rng.seed, ctr0 + (uint64_t)steps, env, 2u), f0);
-            legal = legal_pair(b, odd);
+            legal = legal_mask(b);
         }
-        uint32_t fb = board_max(b) <= 14u ? board_F(b, tabs) : 0u;
-        uint2 *pb = tb + 2 * j + (odd ? 1 : 0);
-        uint8_t *pbyte = (odd ? tf : ta) + j;
-        uint32_t *pword = odd ? tpot + j : reinterpret_cast<uint32_t *>(tp) + j;
+        // carried across steps: potentials of the current board and F(board)
+        MonoStats sb = mono_stats(b);
+        int empt_b = emptiness(b);
+        uint32_t fb = sb.M <= 14u ? board_F(b, tabs) : 0u;
+        uint4 *pb = tb + i;
+        uint8_t *pa = ta + i, *pf = tf + i;
+        int32_t *pp = tp + i;
+        uint32_t *ppot = tpot + i;
         for (int64_t t = 0; t < steps; t++) {
-            *pb = odd ? make_uint2(b.z, b.w) : make_uint2(b.x, b.y);
-            pb += 2 * n;
+            *pb = b;
+            pb += n;
             const uint64_t ctr = ctr0 + (uint64_t)t;
-            const uint4 own = philox_draw(rng.seed, ctr, env, odd ? 2u : 1u);
-            const uint4 other = make_uint4(pair_swap(own.x), pair_swap(own.y), pair_swap(own.z), pair_swap(own.w));
-            const uint4 d = odd ? other : own;   // stream 1: action + spawn
-            const uint4 rw = odd ? own : other;  // stream 2: reset
+            const uint4 d = philox_draw(rng.seed, ctr, env, 1u);
             const uint32_t a = kth_bit16(legal, (uint32_t)(((uint64_t)d.x * (uint32_t)__popc(legal)) >> 32));
+            const int mono_b = mono_value(sb);
             uint32_t pts;
             uint4 moved;
-            const bool small = board_max(b) <= 14u;
-            if (small) {
+            if (sb.M <= 14u) {
                 const bool vert = a < 2u, rev = (a == 1u) | (a == 3u);
                 uint4 w = sel4(vert, transpose(b), b);
                 w = sel4(rev, bswap4(w), w);
-                const uint32_t i0 = pack_nib(odd ? w.z : w.x), i1 = pack_nib(odd ? w.w : w.y);
-                const uint32_t o0 = tabs.row[i0], o1 = tabs.row[i1];
-                const uint32_t fpart = tabs.F(o0) + tabs.F(o1);
-                const uint32_t u0 = unpack_nib(o0), u1 = unpack_nib(o1);
-                const uint32_t q0 = pair_swap(u0), q1 = pair_swap(u1);
-                const uint32_t fm = fpart + pair_swap(fpart);
-                w = odd ? make_uint4(q0, q1, u0, u1) : make_uint4(u0, u1, q0, q1);
+                uint32_t fm;
+                w = slide_lut(w, tabs, fm);
                 w = sel4(rev, bswap4(w), w);
                 moved = sel4(vert, transpose(w), w);
                 pts = fm - fb;
@@ -350,28 +302,36 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
                 uint32_t mx;
                 moved = apply_move(b, a, pts, mx);
             }
-            const int mono_own = monotonicity(odd ? moved : b);
-            const int mono_other = (int)pair_swap((uint32_t)mono_own);
-            const int mono_b = odd ? mono_other : mono_own, mono_a = odd ? mono_own : mono_other;
-            const int empt_b = emptiness(b), empt_a = emptiness(moved);
-            const uint32_t v = spawn_rows(moved, d.y, d.z);
+            const MonoStats sa = mono_stats(moved);
+            const int mono_a = mono_value(sa);
+            const int empt_a = emptiness(moved);
+            uint32_t sp;
+            const uint4 pre = moved;
+            const uint32_t v = spawn_rows(moved, d.y, d.z, sp);
             fb += v == 2u ? 4u : 0u;  // F(2^2) = 4, F(2^1) = 0
+            sb = mono_add_tile(sa, pre, sp, v);
+            const int empt_next = empt_a - 1;
             b = moved;
-            legal = legal_pair(b, odd);
+            legal = legal_mask(b);
             uint32_t fl = legal;
             if (legal == 0u) {
-                b = fresh_from_words(rw, fb);
-                legal = legal_pair(b, odd);
+                b = fresh_from_words(philox_draw(rng.seed, ctr, env, 2u), fb);
+                legal = legal_mask(b);
                 fl = FLAG_DONE | FLAG_RESET | legal;
+                sb = mono_stats(b);
             }
-            const uint32_t potw = (uint32_t)(mono_b & 0xFF) | ((uint32_t)(mono_a & 0xFF) << 8) |
-                                  ((uint32_t)(empt_b & 0xFF) << 16) | ((uint32_t)(empt_a & 0xFF) << 24);
-            *pword = odd ? potw : pts;
-            pword += n;
-            *pbyte = (uint8_t)(odd ? fl : a);
-            pbyte += n;
+            *pa = (uint8_t)a;
+            pa += n;
+            *pp = (int32_t)pts;
+            pp += n;
+            *ppot = (uint32_t)(mono_b & 0xFF) | ((uint32_t)(mono_a & 0xFF) << 8) | ((uint32_t)(empt_b & 0xFF) << 16) |
+                    ((uint32_t)(empt_a & 0xFF) << 24);
+            ppot += n;
+            *pf = (uint8_t)fl;
+            pf += n;
+            empt_b = (fl & FLAG_RESET) ? 14 : empt_next;
         }
-        if (!odd) boards[j] = b;
+        boards[i] = b;
     }
 }
 
@@ -724,14 +684,12 @@ int g2048_env_rollout_random(g2048_stream_t stream, int8_t *boards, int64_t n, i
         return G2048_EINVAL;
     // one workgroup per CU holds the 129 KiB LDS tables; its size scales with N up to 1024 threads
     // so that large N runs 4 waves per SIMD while N = 65 536 still spreads over all 256 CUs
-    // two lanes per board
-    const int64_t lanes = 2 * n;
-    int64_t threads = (lanes + 255) / 256;
+    int64_t threads = (n + 255) / 256;
     threads = threads < 64 ? 64 : threads > 1024 ? 1024 : ((threads + 63) / 64) * 64;
-    int64_t grid = (lanes + threads - 1) / threads;
+    int64_t grid = (n + threads - 1) / threads;
     grid = grid > 256 ? 256 : grid;
     hipLaunchKernelGGL(env_rollout_kernel, dim3((unsigned)grid), dim3((unsigned)threads), 0, (hipStream_t)stream,
-                       (uint4 *)boards, n, steps, (uint2 *)traj_boards, traj_actions, traj_points, (uint32_t *)traj_pot,
+                       (uint4 *)boards, n, steps, (uint4 *)traj_boards, traj_actions, traj_points, (uint32_t *)traj_pot,
                        traj_flags, rng_args(rng));
     return launch_status();
 }
