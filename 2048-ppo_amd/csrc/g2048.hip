@@ -239,6 +239,30 @@ __device__ __forceinline__ uint4 fresh_from_words(const uint4 &r, uint32_t &f) {
     return b;
 }
 
+// Copy the 128 KiB row table + 1 KiB F table into LDS with 8 independent 16-B loads per lane in
+// flight per batch (a load->store loop would pay one L2/MALL latency per 16 B).
+__device__ __forceinline__ void stage_tables(uint16_t *s_row, uint32_t *s_f2) {
+    constexpr int kChunks = 65536 * 2 / 16;  // uint4 pieces of the row table
+    const uint4 *src = reinterpret_cast<const uint4 *>(kRowLeft.v);
+    uint4 *dst = reinterpret_cast<uint4 *>(s_row);
+    const int nt = blockDim.x;
+    for (int base = 0; base < kChunks; base += 8 * nt) {
+        uint4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int k = base + u * nt + threadIdx.x;
+            v[u] = k < kChunks ? src[k] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int k = base + u * nt + threadIdx.x;
+            if (k < kChunks) dst[k] = v[u];
+        }
+    }
+    for (int k = threadIdx.x; k < 256; k += nt) s_f2[k] = kF2.v[k];
+    __syncthreads();
+}
+
 // Synthetic random-legal rollout (the benchmark workload of BASELINE.md): `steps` env steps per
 // board per launch, board in registers, auto-reset on done, one time-major trajectory record per
 // step: the board the action was taken on [T][N][16], action, points, potentials, flags.
@@ -252,13 +276,7 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
                                                            uint8_t *__restrict__ tf, RngArgs rng) {
     __shared__ __attribute__((aligned(16))) uint16_t s_row[65536];
     __shared__ uint32_t s_f2[256];
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(kRowLeft.v);
-        uint4 *dst = reinterpret_cast<uint4 *>(s_row);
-        for (int k = threadIdx.x; k < 65536 * 2 / 16; k += blockDim.x) dst[k] = src[k];
-        for (int k = threadIdx.x; k < 256; k += blockDim.x) s_f2[k] = kF2.v[k];
-    }
-    __syncthreads();
+    stage_tables(s_row, s_f2);
     const LdsTables tabs{s_row, s_f2};
     const uint64_t ctr0 = rng_counter(rng);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
