@@ -1,0 +1,786 @@
+// ppo_update.hip -- fused kernels of the PPO minibatch step (model_optimize_step, train.py:414-642)
+// for GameMLP (game.py:1033-1220): everything of the forward/backward except the GEMMs.
+//
+//   obs_gather_kernel     boards[idx] -> to_model_format (game.py:92-101), bf16 [m,48]
+//   ln_fwd_kernel<J,D>    y = res + Dropout(ReLU(LayerNorm(g)))          (ResidualBlock / stem)
+//   ln_bwd_kernel<J,D>    its backward: dg, the residual gradient, dgamma/dbeta partials
+//   head_loss_kernel<J>   action/value heads + PPO-clip loss + entropy + smooth-L1 + backward
+//   head_kl_kernel<J>     KL(old || new) of the post-step re-forward (train.py:578-601)
+//   colsum1/2             deterministic two-level column sums of per-block partials
+//
+// One wave per row: lane l owns columns 4(l + 64j), j < J = ceil(h/256), so a row is J
+// coalesced 8-B (bf16) or 16-B (fp32) accesses per lane and every row reduction is a wave
+// butterfly -- no LDS, no barriers in the row loop.  The kernels are HBM-bound: per row the
+// forward moves 6h bytes (g, res in; y out), the backward 12h-14h.  Dropout masks are Philox
+// draws regenerated from (row, column group, layer, pass, counter), never stored.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "board.hpp"
+#include "../../include/g2048_ppo.h"
+
+using g2048::philox;
+
+namespace {
+
+constexpr int kWaves = 4;  // waves per block
+constexpr int kThreads = 64 * kWaves;
+constexpr float kLnEps = 1e-5f;
+
+__device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
+
+__device__ __forceinline__ uint32_t f2bf(float f) {  // round to nearest even, NaN stays NaN
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7FFFFFFFu) > 0x7F800000u) return 0x7FC0u;
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return u >> 16;
+}
+
+__device__ __forceinline__ void load_bf4(const uint16_t *p, float v[4]) {
+    const uint2 q = *reinterpret_cast<const uint2 *>(p);
+    v[0] = bf2f(q.x & 0xFFFFu);
+    v[1] = bf2f(q.x >> 16);
+    v[2] = bf2f(q.y & 0xFFFFu);
+    v[3] = bf2f(q.y >> 16);
+}
+
+__device__ __forceinline__ void store_bf4(uint16_t *p, const float v[4]) {
+    uint2 q;
+    q.x = f2bf(v[0]) | (f2bf(v[1]) << 16);
+    q.y = f2bf(v[2]) | (f2bf(v[3]) << 16);
+    *reinterpret_cast<uint2 *>(p) = q;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
+struct DropArgs {
+    uint32_t thr;       // keep iff draw >= thr  (thr = round(p 2^32))
+    float scale;        // 1 / (1 - p)
+    uint32_t c1base;    // layer << 12 | pass << 20
+    uint32_t k0, k1;    // seed
+    uint64_t counter;
+    const uint64_t *counter_dev;
+};
+
+struct Drop {
+    uint32_t thr, c1base, c2, c3, k0, k1;
+    float scale;
+};
+
+__device__ __forceinline__ Drop make_drop(const DropArgs &a) {
+    const uint64_t c = a.counter + (a.counter_dev ? *a.counter_dev : 0ull);
+    return Drop{a.thr, a.c1base, (uint32_t)c, (uint32_t)(c >> 32), a.k0, a.k1, a.scale};
+}
+
+// keep multipliers (0 or 1/(1-p)) of columns 4cg .. 4cg+3 of `row`
+__device__ __forceinline__ void drop_mult(const Drop &d, uint32_t row, uint32_t cg, float k[4]) {
+    const uint4 r = philox(row, cg | d.c1base, d.c2, d.c3, d.k0, d.k1);
+    k[0] = r.x >= d.thr ? d.scale : 0.0f;
+    k[1] = r.y >= d.thr ? d.scale : 0.0f;
+    k[2] = r.z >= d.thr ? d.scale : 0.0f;
+    k[3] = r.w >= d.thr ? d.scale : 0.0f;
+}
+
+__constant__ float kThirds[4] = {0.0f, 1.0f / 3.0f, 2.0f / 3.0f, 1.0f};
+
+// ------------------------------------------------------------------ obs gather ---------------
+__global__ __launch_bounds__(256) void obs_gather_kernel(const int8_t *__restrict__ boards,
+                                                         const int64_t *__restrict__ idx, uint16_t *__restrict__ obs,
+                                                         int64_t m) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // chunk of 4 features
+    if (q >= m * 12) return;
+    const int64_t r = q / 12;
+    const int f0 = (int)(q - r * 12) * 4;
+    const int8_t *b = boards + idx[r] * 16;
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int f = f0 + u, cell = f / 3, k = f - cell * 3;
+        v[u] = k == 0 ? (float)b[cell] : kThirds[k == 1 ? (cell >> 2) : (cell & 3)];
+    }
+    store_bf4(obs + q * 4, v);
+}
+
+// ------------------------------------------------------------------ LayerNorm forward --------
+template <int J, bool DROP>
+__global__ __launch_bounds__(kThreads) void ln_fwd_kernel(const uint16_t *__restrict__ g, const float *__restrict__ gamma,
+                                                          const float *__restrict__ beta,
+                                                          const uint16_t *__restrict__ res, uint16_t *__restrict__ y,
+                                                          float *__restrict__ mean_out, float *__restrict__ rstd_out,
+                                                          int64_t m, int h, DropArgs da) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * kWaves;
+    const Drop d = make_drop(da);
+    float gm[J][4], bt[J][4];
+    bool ok[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const int c = 4 * (lane + 64 * j);
+        ok[j] = c < h;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            gm[j][u] = ok[j] ? gamma[c + u] : 0.0f;
+            bt[j][u] = ok[j] ? beta[c + u] : 0.0f;
+        }
+    }
+    const float inv_h = 1.0f / (float)h;
+    for (int64_t r = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); r < m; r += nw) {
+        float x[J][4];
+        float s = 0.0f;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (ok[j]) {
+                load_bf4(g + r * h + 4 * (lane + 64 * j), x[j]);
+            } else {
+                x[j][0] = x[j][1] = x[j][2] = x[j][3] = 0.0f;
+            }
+            s += (x[j][0] + x[j][1]) + (x[j][2] + x[j][3]);
+        }
+        const float mean = wave_sum(s) * inv_h;
+        float v = 0.0f;
+#pragma unroll
+        for (int j = 0; j < J; j++)
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const float t = ok[j] ? x[j][u] - mean : 0.0f;
+                v += t * t;
+            }
+        const float rstd = 1.0f / sqrtf(wave_sum(v) * inv_h + kLnEps);
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (!ok[j]) continue;
+            const int c = 4 * (lane + 64 * j);
+            float o[4], k[4], rs[4];
+            if (DROP) drop_mult(d, (uint32_t)r, (uint32_t)(lane + 64 * j), k);
+            if (res) load_bf4(res + r * h + c, rs);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                float a = fmaxf((x[j][u] - mean) * rstd * gm[j][u] + bt[j][u], 0.0f);
+                if (DROP) a *= k[u];
+                o[u] = res ? rs[u] + a : a;
+            }
+            store_bf4(y + r * h + c, o);
+        }
+        if (lane == 0) {
+            mean_out[r] = mean;
+            rstd_out[r] = rstd;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ LayerNorm backward -------
+// Block partials: part[blockIdx][0:h] = sum dz*xhat (dgamma), part[blockIdx][h:2h] = sum dz (dbeta).
+// dres_out may alias dres_in (each element is read, then written, by the same lane).
+template <int J, bool DROP>
+__global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
+    const float *dres_in, const uint16_t *__restrict__ p_in, const uint16_t *__restrict__ g,
+    const float *__restrict__ mean_in, const float *__restrict__ rstd_in, const float *__restrict__ gamma,
+    const float *__restrict__ beta, uint16_t *__restrict__ dg, float *dres_out, float *__restrict__ part,
+    int64_t m, int h, DropArgs da) {
+    extern __shared__ float lds[];  // [kWaves][2h]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t nw = (int64_t)gridDim.x * kWaves;
+    const Drop d = make_drop(da);
+    float gm[J][4], bt[J][4], ag[J][4], ab[J][4];
+    bool ok[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const int c = 4 * (lane + 64 * j);
+        ok[j] = c < h;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            gm[j][u] = ok[j] ? gamma[c + u] : 0.0f;
+            bt[j][u] = ok[j] ? beta[c + u] : 0.0f;
+            ag[j][u] = ab[j][u] = 0.0f;
+        }
+    }
+    const float inv_h = 1.0f / (float)h;
+    for (int64_t r = (int64_t)blockIdx.x * kWaves + wave; r < m; r += nw) {
+        const float mean = mean_in[r], rstd = rstd_in[r];
+        float xh[J][4], dxh[J][4];
+        float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (!ok[j]) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) xh[j][u] = dxh[j][u] = 0.0f;
+                continue;
+            }
+            const int c = 4 * (lane + 64 * j);
+            float x[4], dy[4] = {0.0f, 0.0f, 0.0f, 0.0f}, k[4];
+            load_bf4(g + r * h + c, x);
+            if (dres_in) {
+                const float4 t = *reinterpret_cast<const float4 *>(dres_in + r * h + c);
+                dy[0] = t.x; dy[1] = t.y; dy[2] = t.z; dy[3] = t.w;
+            }
+            if (p_in) {
+                float t[4];
+                load_bf4(p_in + r * h + c, t);
+#pragma unroll
+                for (int u = 0; u < 4; u++) dy[u] += t[u];
+            }
+            if (dres_out) *reinterpret_cast<float4 *>(dres_out + r * h + c) = make_float4(dy[0], dy[1], dy[2], dy[3]);
+            if (DROP) drop_mult(d, (uint32_t)r, (uint32_t)(lane + 64 * j), k);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const float xhat = (x[u] - mean) * rstd;
+                const float z = xhat * gm[j][u] + bt[j][u];
+                float dz = z > 0.0f ? dy[u] : 0.0f;
+                if (DROP) dz *= k[u];
+                ag[j][u] += dz * xhat;
+                ab[j][u] += dz;
+                xh[j][u] = xhat;
+                dxh[j][u] = dz * gm[j][u];
+                s1 += dxh[j][u];
+                s2 += dxh[j][u] * xhat;
+            }
+        }
+        s1 = wave_sum(s1) * inv_h;
+        s2 = wave_sum(s2) * inv_h;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (!ok[j]) continue;
+            float o[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) o[u] = rstd * (dxh[j][u] - s1 - xh[j][u] * s2);
+            store_bf4(dg + r * h + 4 * (lane + 64 * j), o);
+        }
+    }
+    // block reduction of the dgamma / dbeta accumulators
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        if (!ok[j]) continue;
+        const int c = 4 * (lane + 64 * j);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            lds[wave * 2 * h + c + u] = ag[j][u];
+            lds[wave * 2 * h + h + c + u] = ab[j][u];
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * h; c += kThreads) {
+        float t = 0.0f;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) t += lds[w * 2 * h + c];
+        part[(int64_t)blockIdx.x * 2 * h + c] = t;
+    }
+}
+
+// ------------------------------------------------------------------ heads + PPO loss ---------
+struct HeadLossArgs {
+    const int64_t *idx;
+    const uint8_t *action;
+    const uint8_t *legal;
+    const float *old_logp;
+    const float *adv;
+    const float *ret;
+    const float *beta_dev;
+    float critic, clip_lo, clip_hi, inv_m;
+    int decouple;
+};
+
+// Block partials: [dwa 4h | dwv h | dba 4 | dbv 1 | sum ppo, sum H, sum v]  (5h + 8 floats)
+template <int J>
+__global__ __launch_bounds__(kThreads) void head_loss_kernel(const uint16_t *__restrict__ xin,
+                                                             const float *__restrict__ wa, const float *__restrict__ ba,
+                                                             const float *__restrict__ wv, const float *__restrict__ bv,
+                                                             int64_t m, int h, HeadLossArgs a,
+                                                             float *__restrict__ masked_out, float *__restrict__ dx_out,
+                                                             float *__restrict__ part) {
+    extern __shared__ float lds[];  // [kWaves][5h + 8]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t nw = (int64_t)gridDim.x * kWaves;
+    const int C = 5 * h + 8;
+    float w[5][J][4], acc[5][J][4];
+    bool ok[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const int c = 4 * (lane + 64 * j);
+        ok[j] = c < h;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) w[k][j][u] = ok[j] ? wa[k * h + c + u] : 0.0f;
+            w[4][j][u] = ok[j] ? wv[c + u] : 0.0f;
+#pragma unroll
+            for (int k = 0; k < 5; k++) acc[k][j][u] = 0.0f;
+        }
+    }
+    float bias[5];
+#pragma unroll
+    for (int k = 0; k < 4; k++) bias[k] = ba[k];
+    bias[4] = bv[0];
+    const float beta_c = *a.beta_dev;
+    float sb[5] = {0, 0, 0, 0, 0}, s_ppo = 0.0f, s_ent = 0.0f, s_v = 0.0f;
+
+    for (int64_t r = (int64_t)blockIdx.x * kWaves + wave; r < m; r += nw) {
+        const int64_t i = a.idx[r];
+        float x[J][4], z[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (ok[j]) {
+                load_bf4(xin + r * h + 4 * (lane + 64 * j), x[j]);
+            } else {
+                x[j][0] = x[j][1] = x[j][2] = x[j][3] = 0.0f;
+            }
+#pragma unroll
+            for (int k = 0; k < 5; k++)
+#pragma unroll
+                for (int u = 0; u < 4; u++) z[k] += x[j][u] * w[k][j][u];
+        }
+#pragma unroll
+        for (int k = 0; k < 5; k++) z[k] = wave_sum(z[k]) + bias[k];
+
+        // ---- the loss of this row (every lane redundantly; scalars are wave-uniform)
+        const int act = a.action[i] & 3;
+        const uint32_t legal = a.legal[i] & 0xFu;
+        float mk[4], mx = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            mk[k] = (legal >> k) & 1u ? z[k] : -INFINITY;
+            mx = fmaxf(mx, mk[k]);
+        }
+        float se = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 4; k++) se += (legal >> k) & 1u ? expf(mk[k] - mx) : 0.0f;
+        const float lse = mx + logf(se);
+        float sm[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) sm[k] = (legal >> k) & 1u ? expf(mk[k] - lse) : 0.0f;
+        const float lp_a = mk[act] - lse;
+        const float dlt = lp_a - a.old_logp[i * 4 + act];
+        const float ratio = expf(fminf(fmaxf(dlt, -20.0f), 20.0f));
+        const bool in20 = dlt >= -20.0f && dlt <= 20.0f;
+        const float A = a.adv[i];
+        const float rc = fminf(fmaxf(ratio, a.clip_lo), a.clip_hi);
+        const bool inr = ratio >= a.clip_lo && ratio <= a.clip_hi;
+        const float t1 = A * ratio, t2 = A * rc;
+        const float ppo = fminf(t1, t2);
+        // torch.minimum backward: the smaller side takes the gradient, a tie splits it in halves
+        float dp;
+        if (t1 < t2) dp = A;
+        else if (t1 > t2) dp = inr ? A : 0.0f;
+        else dp = 0.5f * A + (inr ? 0.5f * A : 0.0f);
+        const float dd = in20 ? dp * ratio : 0.0f;  // d ppo / d (logpi(a) - old)
+
+        // entropy of softmax(clamp(masked, -20, 20)) summed over the legal actions
+        float ck[4], cmx = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            ck[k] = fminf(fmaxf(mk[k], -20.0f), 20.0f);
+            cmx = fmaxf(cmx, ck[k]);
+        }
+        float se2 = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 4; k++) se2 += expf(ck[k] - cmx);
+        const float lse2 = cmx + logf(se2);
+        float lp2[4], p2[4], ent = 0.0f, S = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            lp2[k] = ck[k] - lse2;
+            p2[k] = expf(lp2[k]);
+            if ((legal >> k) & 1u) {
+                ent -= p2[k] * lp2[k];
+                S += p2[k] * (lp2[k] + 1.0f);
+            }
+        }
+        const float dv0 = z[4] - a.ret[i];
+        const float adv0 = fabsf(dv0);
+        const float vl = adv0 < 1.0f ? 0.5f * dv0 * dv0 : adv0 - 0.5f;
+        const float dvl = fminf(fmaxf(dv0, -1.0f), 1.0f);
+
+        float dz[5];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const bool valid = (legal >> k) & 1u;
+            const bool cpass = valid && mk[k] >= -20.0f && mk[k] <= 20.0f;
+            const float dent = -(p2[k] * (lp2[k] + 1.0f) - p2[k] * S);
+            const float g = dd * ((k == act ? 1.0f : 0.0f) - sm[k]) + (cpass ? beta_c * dent : 0.0f);
+            dz[k] = valid ? -a.inv_m * g : 0.0f;
+        }
+        dz[4] = a.inv_m * a.critic * dvl;
+
+        // ---- backward into x and the head parameters
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (!ok[j]) continue;
+            float o[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                float t = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 4; k++) t += dz[k] * w[k][j][u];
+                if (!a.decouple) t += dz[4] * w[4][j][u];
+                o[u] = t;
+#pragma unroll
+                for (int k = 0; k < 5; k++) acc[k][j][u] += dz[k] * x[j][u];
+            }
+            *reinterpret_cast<float4 *>(dx_out + r * h + 4 * (lane + 64 * j)) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+#pragma unroll
+        for (int k = 0; k < 5; k++) sb[k] += dz[k];
+        s_ppo += ppo;
+        s_ent += ent;
+        s_v += vl;
+        if (lane == 0)
+            *reinterpret_cast<float4 *>(masked_out + r * 4) = make_float4(mk[0], mk[1], mk[2], mk[3]);
+    }
+    float *mine = lds + wave * C;
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        if (!ok[j]) continue;
+        const int c = 4 * (lane + 64 * j);
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int k = 0; k < 5; k++) mine[k * h + c + u] = acc[k][j][u];
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; k++) mine[5 * h + k] = sb[k];
+        mine[5 * h + 5] = s_ppo;
+        mine[5 * h + 6] = s_ent;
+        mine[5 * h + 7] = s_v;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += kThreads) {
+        float t = 0.0f;
+#pragma unroll
+        for (int w2 = 0; w2 < kWaves; w2++) t += lds[w2 * C + c];
+        part[(int64_t)blockIdx.x * C + c] = t;
+    }
+}
+
+// ------------------------------------------------------------------ KL diagnostic ------------
+// Block partials: [sum KL, max KL]
+template <int J>
+__global__ __launch_bounds__(kThreads) void head_kl_kernel(const uint16_t *__restrict__ xin, const float *__restrict__ wa,
+                                                           const float *__restrict__ ba, int64_t m, int h,
+                                                           const float *__restrict__ old_masked,
+                                                           float *__restrict__ part) {
+    __shared__ float lds[kWaves][2];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t nw = (int64_t)gridDim.x * kWaves;
+    float w[4][J][4];
+    bool ok[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const int c = 4 * (lane + 64 * j);
+        ok[j] = c < h;
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int k = 0; k < 4; k++) w[k][j][u] = ok[j] ? wa[k * h + c + u] : 0.0f;
+    }
+    float bias[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) bias[k] = ba[k];
+    float ksum = 0.0f, kmax = -INFINITY;
+    for (int64_t r = (int64_t)blockIdx.x * kWaves + wave; r < m; r += nw) {
+        float z[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (!ok[j]) continue;
+            float x[4];
+            load_bf4(xin + r * h + 4 * (lane + 64 * j), x);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+#pragma unroll
+                for (int u = 0; u < 4; u++) z[k] += x[u] * w[k][j][u];
+        }
+        const float4 o4 = *reinterpret_cast<const float4 *>(old_masked + r * 4);
+        const float o[4] = {o4.x, o4.y, o4.z, o4.w};
+        bool valid[4];
+        float mo = -INFINITY, mn = -INFINITY, nz[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            z[k] = wave_sum(z[k]) + bias[k];
+            valid[k] = o[k] != -INFINITY;
+            nz[k] = valid[k] ? z[k] : -INFINITY;
+            mo = fmaxf(mo, o[k]);
+            mn = fmaxf(mn, nz[k]);
+        }
+        float so = 0.0f, sn = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            so += valid[k] ? expf(o[k] - mo) : 0.0f;
+            sn += valid[k] ? expf(nz[k] - mn) : 0.0f;
+        }
+        const float lso = mo + logf(so), lsn = mn + logf(sn);
+        float kl = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (!valid[k]) continue;
+            const float lo = o[k] - lso, ln = nz[k] - lsn;
+            kl += expf(lo) * (lo - ln);
+        }
+        ksum += kl;
+        kmax = fmaxf(kmax, kl);
+    }
+    if (lane == 0) {
+        lds[wave][0] = ksum;
+        lds[wave][1] = kmax;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float s = 0.0f, mx = -INFINITY;
+        for (int w2 = 0; w2 < kWaves; w2++) {
+            s += lds[w2][0];
+            mx = fmaxf(mx, lds[w2][1]);
+        }
+        part[blockIdx.x * 2] = s;
+        part[blockIdx.x * 2 + 1] = mx;
+    }
+}
+
+// ------------------------------------------------------------------ column sums --------------
+// Stage 1: grid (ceil(C/64), kSlices); block (64 columns x 4 row groups) sums rows of slice y.
+constexpr int kSlices = 32;
+
+__global__ __launch_bounds__(256) void colsum1_kernel(const float *__restrict__ part, int nb, int C,
+                                                      float *__restrict__ part2, int max_col) {
+    __shared__ float lds[4][64];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+    const int per = (nb + kSlices - 1) / kSlices;
+    const int b0 = blockIdx.y * per, b1 = min(nb, b0 + per);
+    float t = 0.0f, mx = -INFINITY;
+    if (c < C)
+        for (int b = b0 + rg; b < b1; b += 4) {
+            const float v = part[(int64_t)b * C + c];
+            t += v;
+            mx = fmaxf(mx, v);
+        }
+    lds[rg][threadIdx.x & 63] = c == max_col ? mx : t;
+    __syncthreads();
+    if (rg == 0 && c < C) {
+        const int l = threadIdx.x;
+        part2[blockIdx.y * C + c] = c == max_col ? fmaxf(fmaxf(lds[0][l], lds[1][l]), fmaxf(lds[2][l], lds[3][l]))
+                                                 : (lds[0][l] + lds[1][l]) + (lds[2][l] + lds[3][l]);
+    }
+}
+
+struct Segs {
+    float *dst[5];
+    int len[5];
+    int n;
+};
+
+__global__ __launch_bounds__(256) void colsum2_kernel(const float *__restrict__ part2, int C, Segs segs, int max_col) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    float t = 0.0f, mx = -INFINITY;
+#pragma unroll 8
+    for (int s = 0; s < kSlices; s++) {
+        const float v = part2[s * C + c];
+        t += v;
+        mx = fmaxf(mx, v);
+    }
+    int off = 0;
+    for (int k = 0; k < segs.n; k++) {
+        if (c < off + segs.len[k]) {
+            segs.dst[k][c - off] = c == max_col ? mx : t;
+            return;
+        }
+        off += segs.len[k];
+    }
+}
+
+__global__ __launch_bounds__(256) void dropout_mask_kernel(int64_t m, int h, DropArgs da, uint8_t *__restrict__ mask) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int groups = h / 4;
+    if (q >= m * groups) return;
+    const int64_t r = q / groups;
+    const int cg = (int)(q - r * groups);
+    const Drop d = make_drop(da);
+    float k[4];
+    drop_mult(d, (uint32_t)r, (uint32_t)cg, k);
+    for (int u = 0; u < 4; u++) mask[r * h + 4 * cg + u] = k[u] != 0.0f ? 1 : 0;
+}
+
+// ------------------------------------------------------------------ host helpers -------------
+inline int status() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK : (int)e;
+}
+
+inline bool shape_ok(int64_t m, int32_t h) { return m >= 0 && h > 0 && h % 4 == 0 && h <= 1024 && m < (1ll << 31); }
+
+inline bool al(const void *p, unsigned a) { return ((uintptr_t)p % a) == 0u; }
+
+// blocks of a partial-producing kernel: >= 4 rows per wave, <= 2048 blocks
+inline int partial_blocks(int64_t m) {
+    const int64_t b = (m + 4 * kWaves - 1) / (4 * kWaves);
+    return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
+}
+
+inline DropArgs drop_args(const g2048_dropout *d) {
+    DropArgs a{};
+    a.thr = 0;
+    a.scale = 1.0f;
+    if (d && d->p > 0.0f) {
+        const double t = (double)d->p * 4294967296.0;
+        a.thr = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)(t + 0.5);
+        a.scale = 1.0f / (1.0f - d->p);
+        a.c1base = (d->layer << 12) | (d->pass << 20);
+        a.k0 = (uint32_t)d->seed;
+        a.k1 = (uint32_t)(d->seed >> 32);
+        a.counter = d->counter;
+        a.counter_dev = d->counter_dev;
+    }
+    return a;
+}
+
+inline bool drop_on(const g2048_dropout *d) { return d && d->p > 0.0f; }
+
+int colsum(hipStream_t s, const float *part, int nb, int C, float *scratch2, const Segs &segs, int max_col) {
+    hipLaunchKernelGGL(colsum1_kernel, dim3((C + 63) / 64, kSlices), dim3(256), 0, s, part, nb, C, scratch2, max_col);
+    hipLaunchKernelGGL(colsum2_kernel, dim3((C + 255) / 256), dim3(256), 0, s, scratch2, C, segs, max_col);
+    return status();
+}
+
+#define G2048_DISPATCH_J(h, BODY)            \
+    do {                                     \
+        const int jj_ = ((h) + 255) / 256;  \
+        if (jj_ == 1) { constexpr int J = 1; BODY; } \
+        else if (jj_ == 2) { constexpr int J = 2; BODY; } \
+        else if (jj_ == 3) { constexpr int J = 3; BODY; } \
+        else { constexpr int J = 4; BODY; }  \
+    } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int g2048_obs_gather(g2048_stream_t stream, const int8_t *boards, const int64_t *idx, int64_t m, uint16_t *obs) {
+    if (m < 0 || (m > 0 && (!boards || !idx || !obs || !al(obs, 8)))) return G2048_EINVAL;
+    if (m == 0) return G2048_OK;
+    hipLaunchKernelGGL(obs_gather_kernel, dim3((unsigned)((m * 12 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       boards, idx, obs, m);
+    return status();
+}
+
+int g2048_ln_act_fwd(g2048_stream_t stream, const uint16_t *g, const float *gamma, const float *beta,
+                     const uint16_t *res, uint16_t *y, float *mean, float *rstd, int64_t m, int32_t h,
+                     const g2048_dropout *drop) {
+    if (!shape_ok(m, h)) return G2048_EINVAL;
+    if (m == 0) return G2048_OK;
+    if (!g || !gamma || !beta || !y || !mean || !rstd || !al(g, 8) || !al(y, 8) || (res && !al(res, 8)))
+        return G2048_EINVAL;
+    const DropArgs da = drop_args(drop);
+    const int64_t blocks64 = (m + kWaves - 1) / kWaves;
+    const dim3 grid((unsigned)(blocks64 > 16384 ? 16384 : blocks64)), blk(kThreads);
+    const hipStream_t s = (hipStream_t)stream;
+    if (drop_on(drop))
+        G2048_DISPATCH_J(h, hipLaunchKernelGGL((ln_fwd_kernel<J, true>), grid, blk, 0, s, g, gamma, beta, res, y, mean,
+                                               rstd, m, h, da));
+    else
+        G2048_DISPATCH_J(h, hipLaunchKernelGGL((ln_fwd_kernel<J, false>), grid, blk, 0, s, g, gamma, beta, res, y,
+                                               mean, rstd, m, h, da));
+    return status();
+}
+
+size_t g2048_ln_act_bwd_partials(int64_t m, int32_t h) {
+    if (!shape_ok(m, h)) return 0;
+    return (size_t)partial_blocks(m) * 2 * h + (size_t)kSlices * 2 * h;
+}
+
+int g2048_ln_act_bwd(g2048_stream_t stream, const float *dres_in, const uint16_t *p_in, const uint16_t *g,
+                     const float *mean, const float *rstd, const float *gamma, const float *beta, uint16_t *dg,
+                     float *dres_out, float *partials, float *dgamma, float *dbeta, int64_t m, int32_t h,
+                     const g2048_dropout *drop) {
+    if (!shape_ok(m, h)) return G2048_EINVAL;
+    if (!g || !mean || !rstd || !gamma || !beta || !dg || !partials || !dgamma || !dbeta) return G2048_EINVAL;
+    if (!al(g, 8) || !al(dg, 8) || (p_in && !al(p_in, 8)) || (dres_in && !al(dres_in, 16)) ||
+        (dres_out && !al(dres_out, 16)))
+        return G2048_EINVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    if (m == 0) {
+        (void)hipMemsetAsync(dgamma, 0, sizeof(float) * h, s);
+        (void)hipMemsetAsync(dbeta, 0, sizeof(float) * h, s);
+        return status();
+    }
+    const DropArgs da = drop_args(drop);
+    const int nb = partial_blocks(m);
+    const size_t lds = sizeof(float) * kWaves * 2 * h;
+    if (drop_on(drop))
+        G2048_DISPATCH_J(h, hipLaunchKernelGGL((ln_bwd_kernel<J, true>), dim3(nb), dim3(kThreads), lds, s, dres_in, p_in,
+                                               g, mean, rstd, gamma, beta, dg, dres_out, partials, m, h, da));
+    else
+        G2048_DISPATCH_J(h, hipLaunchKernelGGL((ln_bwd_kernel<J, false>), dim3(nb), dim3(kThreads), lds, s, dres_in,
+                                               p_in, g, mean, rstd, gamma, beta, dg, dres_out, partials, m, h, da));
+    Segs segs{};
+    segs.n = 2;
+    segs.dst[0] = dgamma;
+    segs.len[0] = h;
+    segs.dst[1] = dbeta;
+    segs.len[1] = h;
+    return colsum(s, partials, nb, 2 * h, partials + (size_t)nb * 2 * h, segs, -1);
+}
+
+size_t g2048_ppo_head_partials(int64_t m, int32_t h) {
+    if (!shape_ok(m, h)) return 0;
+    return (size_t)partial_blocks(m) * (5 * h + 8) + (size_t)kSlices * (5 * h + 8);
+}
+
+int g2048_ppo_head_loss(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, const float *wv,
+                        const float *bv, int64_t m, int32_t h, const g2048_ppo_batch *batch, const float *beta_dev,
+                        float critic, float clip_eps, int32_t decouple_critic, float *masked, float *dx,
+                        float *partials, float *dwa, float *dba, float *dwv, float *dbv, float *sums) {
+    if (!shape_ok(m, h) || m == 0 || !batch) return G2048_EINVAL;
+    if (!x || !wa || !ba || !wv || !bv || !beta_dev || !masked || !dx || !partials || !dwa || !dba || !dwv || !dbv ||
+        !sums || !batch->idx || !batch->action || !batch->legal || !batch->old_logp || !batch->adv || !batch->ret)
+        return G2048_EINVAL;
+    if (!al(x, 8) || !al(masked, 16) || !al(dx, 16)) return G2048_EINVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    HeadLossArgs a{batch->idx, batch->action, batch->legal, batch->old_logp, batch->adv, batch->ret, beta_dev,
+                   critic, 1.0f - clip_eps, 1.0f + clip_eps, 1.0f / (float)m, decouple_critic};
+    const int nb = partial_blocks(m);
+    const int C = 5 * h + 8;
+    const size_t lds = sizeof(float) * kWaves * C;
+    G2048_DISPATCH_J(h, hipLaunchKernelGGL((head_loss_kernel<J>), dim3(nb), dim3(kThreads), lds, s, x, wa, ba, wv, bv,
+                                           m, h, a, masked, dx, partials));
+    Segs segs{};
+    segs.n = 5;
+    segs.dst[0] = dwa; segs.len[0] = 4 * h;
+    segs.dst[1] = dwv; segs.len[1] = h;
+    segs.dst[2] = dba; segs.len[2] = 4;
+    segs.dst[3] = dbv; segs.len[3] = 1;
+    segs.dst[4] = sums; segs.len[4] = 3;
+    return colsum(s, partials, nb, C, partials + (size_t)nb * C, segs, -1);
+}
+
+int g2048_ppo_head_kl(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, int64_t m,
+                      int32_t h, const float *old_masked, float *partials, float *out) {
+    if (!shape_ok(m, h) || m == 0 || !x || !wa || !ba || !old_masked || !partials || !out) return G2048_EINVAL;
+    if (!al(x, 8) || !al(old_masked, 16)) return G2048_EINVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    const int nb = partial_blocks(m);
+    G2048_DISPATCH_J(h, hipLaunchKernelGGL((head_kl_kernel<J>), dim3(nb), dim3(kThreads), 0, s, x, wa, ba, m, h,
+                                           old_masked, partials));
+    Segs segs{};
+    segs.n = 1;
+    segs.dst[0] = out;
+    segs.len[0] = 2;
+    return colsum(s, partials, nb, 2, partials + (size_t)nb * 2, segs, 1);
+}
+
+int g2048_dropout_mask(g2048_stream_t stream, int64_t m, int32_t h, const g2048_dropout *drop, uint8_t *mask) {
+    if (!shape_ok(m, h) || !mask) return G2048_EINVAL;
+    if (m == 0) return G2048_OK;
+    DropArgs da = drop_args(drop);
+    hipLaunchKernelGGL(dropout_mask_kernel, dim3((unsigned)((m * (h / 4) + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, m, h, da, mask);
+    return status();
+}
+
+}  // extern "C"

@@ -27,6 +27,9 @@ EXPORTED = (
     "g2048_preview_points", "g2048_legal_mask",
     "g2048_obs_encode", "g2048_sample_actions", "g2048_rtg_prepare", "g2048_reward_rtg_workspace_bytes",
     "g2048_reward_rtg", "g2048_rtg_finalize", "g2048_build_info",
+    # include/g2048_ppo.h
+    "g2048_obs_gather", "g2048_ln_act_fwd", "g2048_ln_act_bwd_partials", "g2048_ln_act_bwd",
+    "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask",
 )
 
 
@@ -53,6 +56,19 @@ class RewardCfg(ctypes.Structure):
                 ("w_empt", ctypes.c_double), ("beta", ctypes.c_double)]
 
 
+class Dropout(ctypes.Structure):
+    """struct g2048_dropout"""
+    _fields_ = [("p", ctypes.c_float), ("layer", ctypes.c_uint32), ("pass_", ctypes.c_uint32),
+                ("pad_", ctypes.c_uint32), ("seed", ctypes.c_uint64), ("counter", ctypes.c_uint64),
+                ("counter_dev", ctypes.c_void_p)]
+
+
+class PPOBatch(ctypes.Structure):
+    """struct g2048_ppo_batch"""
+    _fields_ = [("idx", ctypes.c_void_p), ("action", ctypes.c_void_p), ("legal", ctypes.c_void_p),
+                ("old_logp", ctypes.c_void_p), ("adv", ctypes.c_void_p), ("ret", ctypes.c_void_p)]
+
+
 _lib = None
 
 
@@ -68,6 +84,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     L = ctypes.CDLL(str(p))
     vp, i64, i32, u32, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_size_t
     rp, cp = ctypes.POINTER(Rng), ctypes.POINTER(RewardCfg)
+    dp, bp = ctypes.POINTER(Dropout), ctypes.POINTER(PPOBatch)
     sig = {
         "g2048_mt_state_words": (sz, []),
         "g2048_mt_seed": (ctypes.c_int, [vp, vp, vp, i64]),
@@ -83,6 +100,15 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_reward_rtg": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, cp, vp, vp, vp, vp, vp, vp, sz]),
         "g2048_rtg_finalize": (ctypes.c_int, [vp, vp, vp, cp]),
         "g2048_build_info": (ctypes.c_char_p, []),
+        "g2048_obs_gather": (ctypes.c_int, [vp, vp, vp, i64, vp]),
+        "g2048_ln_act_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, dp]),
+        "g2048_ln_act_bwd_partials": (sz, [i64, i32]),
+        "g2048_ln_act_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, dp]),
+        "g2048_ppo_head_partials": (sz, [i64, i32]),
+        "g2048_ppo_head_loss": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, bp, vp, ctypes.c_float,
+                                               ctypes.c_float, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "g2048_ppo_head_kl": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, vp, vp, vp]),
+        "g2048_dropout_mask": (ctypes.c_int, [vp, i64, i32, dp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -207,3 +233,75 @@ def rtg_finalize(state, partials, cfg: RewardCfg):
     _check(load().g2048_rtg_finalize(_stream(state), _dev(state, torch.float64, "state"),
                                      _dev(partials, torch.float64, "partials"), ctypes.byref(cfg)),
            "g2048_rtg_finalize")
+
+
+# ------------------------------------------------------------- PPO update (g2048_ppo.h) -------
+def make_dropout(p=0.0, layer=0, pass_=0, seed=0, counter=0, counter_dev=None) -> Dropout:
+    return Dropout(float(p), layer, pass_, 0, seed & (2**64 - 1), counter,
+                   _dev(counter_dev, torch.int64, "counter_dev"))
+
+
+def obs_gather(boards, idx, obs):
+    _check(load().g2048_obs_gather(_stream(idx), _dev(boards, torch.int8, "boards"), _dev(idx, torch.int64, "idx"),
+                                   idx.shape[0], _dev(obs, torch.bfloat16, "obs")), "g2048_obs_gather")
+
+
+def ln_act_fwd(g, gamma, beta, res, y, mean, rstd, drop: Dropout | None = None):
+    m, h = g.shape
+    _check(load().g2048_ln_act_fwd(
+        _stream(g), _dev(g, torch.bfloat16, "g"), _dev(gamma, torch.float32, "gamma"),
+        _dev(beta, torch.float32, "beta"), _dev(res, torch.bfloat16, "res"), _dev(y, torch.bfloat16, "y"),
+        _dev(mean, torch.float32, "mean"), _dev(rstd, torch.float32, "rstd"), m, h,
+        ctypes.byref(drop) if drop is not None else None), "g2048_ln_act_fwd")
+
+
+def ln_act_bwd_partials(m: int, h: int) -> int:
+    return int(load().g2048_ln_act_bwd_partials(m, h))
+
+
+def ln_act_bwd(dres_in, p_in, g, mean, rstd, gamma, beta, dg, dres_out, partials, dgamma, dbeta,
+               drop: Dropout | None = None):
+    m, h = g.shape
+    _check(load().g2048_ln_act_bwd(
+        _stream(g), _dev(dres_in, torch.float32, "dres_in"), _dev(p_in, torch.bfloat16, "p_in"),
+        _dev(g, torch.bfloat16, "g"), _dev(mean, torch.float32, "mean"), _dev(rstd, torch.float32, "rstd"),
+        _dev(gamma, torch.float32, "gamma"), _dev(beta, torch.float32, "beta"), _dev(dg, torch.bfloat16, "dg"),
+        _dev(dres_out, torch.float32, "dres_out"), _dev(partials, torch.float32, "partials"),
+        _dev(dgamma, torch.float32, "dgamma"), _dev(dbeta, torch.float32, "dbeta"), m, h,
+        ctypes.byref(drop) if drop is not None else None), "g2048_ln_act_bwd")
+
+
+def ppo_head_partials(m: int, h: int) -> int:
+    return int(load().g2048_ppo_head_partials(m, h))
+
+
+def make_ppo_batch(idx, action, legal, old_logp, adv, ret) -> PPOBatch:
+    return PPOBatch(_dev(idx, torch.int64, "idx"), _dev(action, torch.uint8, "action"),
+                    _dev(legal, torch.uint8, "legal"), _dev(old_logp, torch.float32, "old_logp"),
+                    _dev(adv, torch.float32, "adv"), _dev(ret, torch.float32, "ret"))
+
+
+def ppo_head_loss(x, wa, ba, wv, bv, batch: PPOBatch, beta_dev, critic, clip_eps, decouple, masked, dx, partials,
+                  dwa, dba, dwv, dbv, sums):
+    m, h = x.shape
+    _check(load().g2048_ppo_head_loss(
+        _stream(x), _dev(x, torch.bfloat16, "x"), _dev(wa, torch.float32, "wa"), _dev(ba, torch.float32, "ba"),
+        _dev(wv, torch.float32, "wv"), _dev(bv, torch.float32, "bv"), m, h, ctypes.byref(batch),
+        _dev(beta_dev, torch.float32, "beta"), float(critic), float(clip_eps), int(bool(decouple)),
+        _dev(masked, torch.float32, "masked"), _dev(dx, torch.float32, "dx"),
+        _dev(partials, torch.float32, "partials"), _dev(dwa, torch.float32, "dwa"), _dev(dba, torch.float32, "dba"),
+        _dev(dwv, torch.float32, "dwv"), _dev(dbv, torch.float32, "dbv"), _dev(sums, torch.float32, "sums")),
+        "g2048_ppo_head_loss")
+
+
+def ppo_head_kl(x, wa, ba, old_masked, partials, out):
+    m, h = x.shape
+    _check(load().g2048_ppo_head_kl(
+        _stream(x), _dev(x, torch.bfloat16, "x"), _dev(wa, torch.float32, "wa"), _dev(ba, torch.float32, "ba"), m, h,
+        _dev(old_masked, torch.float32, "old_masked"), _dev(partials, torch.float32, "partials"),
+        _dev(out, torch.float32, "out")), "g2048_ppo_head_kl")
+
+
+def dropout_mask(m: int, h: int, drop: Dropout, mask):
+    _check(load().g2048_dropout_mask(_stream(mask), m, h, ctypes.byref(drop), _dev(mask, torch.uint8, "mask")),
+           "g2048_dropout_mask")

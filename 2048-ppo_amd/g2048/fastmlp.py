@@ -1,0 +1,169 @@
+"""The PPO minibatch step of GameMLP as explicit kernels (model_optimize_step, train.py:414-642).
+
+PPOUpdater runs the reference's step through torch autograd.  For the reference's own policy,
+GameMLP (game.py:1049-1220: stem Linear-LayerNorm-ReLU, L x [x + Dropout(ReLU(LN(W x)))],
+action/value heads), FusedPPOUpdater writes the forward and backward out by hand:
+
+    forward   X0 = obs(boards[idx])                          g2048_obs_gather
+              G_l = H_{l-1} W_l^T                             GEMM (hipBLASLt, bf16 in, bf16 out)
+              H_l = H_{l-1} + Drop(ReLU(LN(G_l)))             g2048_ln_act_fwd
+    loss      heads + PPO-clip + entropy + smooth-L1 and      g2048_ppo_head_loss
+              d/dH_L, d/d(head params), loss sums
+    backward  dG_l, dgamma_l, dbeta_l, residual grad          g2048_ln_act_bwd
+              P = dG_l W_l,  dW_l = dG_l^T H_{l-1}             GEMMs (dW in fp32, straight into the
+                                                              flat gradient bucket)
+    step      [RCCL all-reduce] clip, Muon + AdamW            dist.GradBucket / optim.MuonAdamW
+    KL        re-forward with the new weights (train mode)    g2048_ln_act_fwd + g2048_ppo_head_kl
+
+Activations are bf16, LayerNorm statistics / gradients / reductions fp32, master weights fp32.
+Dropout keep masks are Philox draws regenerated in the backward pass (nothing stored); they are
+statistically, not bitwise, the reference's torch.nn.Dropout.  The whole step is one hipGraph
+(two around the all-reduce with several ranks), replayed per minibatch.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+from .ppo import STAT_KEYS, PPOConfig, PPOUpdater
+
+
+def supports(model) -> bool:
+    """FusedPPOUpdater handles the reference's GameMLP (hidden % 4 == 0, <= 1024)."""
+    try:
+        import agent
+    except ImportError:  # pragma: no cover
+        return False
+    if not isinstance(model, agent.GameMLP):
+        return False
+    h = model.config.hidden_dim
+    return h % 4 == 0 and h <= 1024
+
+
+def _mm(a, b, out):
+    """out = a @ b with fp32 accumulation (bf16 operands); fp32 `out` gets an fp32 result."""
+    if out.dtype == a.dtype:
+        torch.mm(a, b, out=out)
+    else:
+        out.copy_(torch.mm(a, b, out_dtype=out.dtype))
+
+
+class FusedPPOUpdater(PPOUpdater):
+    def __init__(self, model, optimizer, cfg: PPOConfig, grads, generator: torch.Generator | None = None,
+                 graph: bool = False, seed: int = 0x5EED):
+        if not supports(model):
+            raise ValueError("FusedPPOUpdater needs an agent.GameMLP with hidden_dim % 4 == 0 and <= 1024")
+        super().__init__(model, optimizer, cfg, grads, generator, graph)
+        self.h = model.config.hidden_dim
+        self.p_drop = float(model.config.dropout)
+        self.decouple = bool(model.decouple_critic)
+        self.lin = [model.stem[0].weight] + [b.mlp[0].weight for b in model.backbone]
+        self.ln = [model.stem[1]] + [b.mlp[1] for b in model.backbone]
+        self.wa, self.ba = model.action_head.weight, model.action_head.bias
+        self.wv, self.bv = model.value_head.weight, model.value_head.bias
+        self.wbf = [torch.empty_like(w, dtype=torch.bfloat16) for w in self.lin]
+        self.counter = torch.zeros(1, dtype=torch.int64, device=self.dev)  # dropout counter base
+        self.seed = seed
+        self.bs = 0
+
+    # ---------------------------------------------------------------- buffers -------------
+    def _alloc(self, bs: int):
+        if self.bs == bs:
+            return
+        d, h, nl = self.dev, self.h, len(self.lin)
+        bf = torch.bfloat16
+        self.x0 = torch.empty(bs, 48, dtype=bf, device=d)
+        self.G = [torch.empty(bs, h, dtype=bf, device=d) for _ in range(nl)]
+        self.H = [torch.empty(bs, h, dtype=bf, device=d) for _ in range(nl)]
+        self.mean = [torch.empty(bs, dtype=torch.float32, device=d) for _ in range(nl)]
+        self.rstd = [torch.empty(bs, dtype=torch.float32, device=d) for _ in range(nl)]
+        self.masked = torch.empty(bs, 4, dtype=torch.float32, device=d)
+        self.dres = torch.empty(bs, h, dtype=torch.float32, device=d)
+        self.dg = torch.empty(bs, h, dtype=bf, device=d)
+        self.P = torch.empty(bs, h, dtype=bf, device=d)
+        n = max(L.ln_act_bwd_partials(bs, h), L.ppo_head_partials(bs, h))
+        self.partials = torch.empty(n, dtype=torch.float32, device=d)
+        self.sums = torch.zeros(3, dtype=torch.float32, device=d)
+        self.kl = torch.zeros(2, dtype=torch.float32, device=d)
+        self.bs = bs
+
+    def _drop(self, layer: int, pass_: int):
+        return L.make_dropout(self.p_drop if self.model.training else 0.0, layer, pass_, self.seed, 0, self.counter)
+
+    @torch.no_grad()
+    def refresh_weights(self):
+        for w, b in zip(self.lin, self.wbf):
+            b.copy_(w)
+
+    # ---------------------------------------------------------------- passes --------------
+    def forward_features(self, boards, idx, pass_: int):
+        """H_L of the minibatch boards[idx] (train mode: dropout of pass `pass_`)."""
+        L.obs_gather(boards, idx, self.x0)
+        return self._layers(pass_)
+
+    def _layers(self, pass_: int):
+        x = self.x0
+        for l, (w, ln) in enumerate(zip(self.wbf, self.ln)):
+            _mm(x, w.t(), self.G[l])
+            L.ln_act_fwd(self.G[l], ln.weight, ln.bias, x if l > 0 else None, self.H[l], self.mean[l], self.rstd[l],
+                         self._drop(l, pass_) if l > 0 else None)
+            x = self.H[l]
+        return x
+
+    def loss_backward(self, data, idx, beta):
+        """Heads + PPO loss + backward of the minibatch; gradients land in the GradBucket views."""
+        nl = len(self.lin)
+        batch = L.make_ppo_batch(idx, data["actions"], data["legal"], data["logp"], data["adv"], data["ret"])
+        L.ppo_head_loss(self.H[-1], self.wa, self.ba, self.wv, self.bv, batch, beta, self.cfg.critic,
+                        self.cfg.clip_eps, self.decouple, self.masked, self.dres, self.partials,
+                        self.wa.grad, self.ba.grad, self.wv.grad, self.bv.grad, self.sums)
+        p_in = None
+        for l in range(nl - 1, -1, -1):
+            ln = self.ln[l]
+            L.ln_act_bwd(self.dres, p_in, self.G[l], self.mean[l], self.rstd[l], ln.weight, ln.bias, self.dg,
+                         self.dres if l > 0 else None, self.partials, ln.weight.grad, ln.bias.grad,
+                         self._drop(l, 0) if l > 0 else None)
+            x_in = self.H[l - 1] if l > 0 else self.x0
+            _mm(self.dg.t(), x_in, self.lin[l].grad)
+            if l > 0:
+                _mm(self.dg, self.wbf[l], self.P)
+                p_in = self.P
+
+    # ---------------------------------------------------------------- PPOUpdater hooks ----
+    def update(self, data: dict, beta: float, encode=None) -> dict:
+        bs = min(self.cfg.batch_size, data["actions"].shape[0])
+        self._alloc(bs)
+        self.refresh_weights()
+        return super().update(data, beta, encode)
+
+    def _pre(self, idx, data, beta, encode):
+        if idx.shape[0] != self.bs:  # ragged last minibatch of an eager pass
+            self._alloc(idx.shape[0])
+        self.counter.add_(1)
+        self.forward_features(data["boards"], idx, 0)
+        self.loss_backward(data, idx, beta)
+        return {}
+
+    def _post(self, st, beta):
+        cfg, m = self.cfg, self.bs
+        gn = self.grads.clip_(cfg.max_grad_norm)
+        self.opt.step()
+        self.refresh_weights()
+        with torch.no_grad():
+            x = self._layers(1)  # KL re-forward of the same minibatch (x0 still holds its encoding)
+            L.ppo_head_kl(x, self.wa, self.ba, self.masked, self.partials, self.kl)
+            s_ppo, s_ent, s_v = self.sums[0] / m, self.sums[1] / m, self.sums[2] / m
+            b = beta if torch.is_tensor(beta) else torch.tensor(beta, device=self.dev)
+            vals = torch.stack([-(s_ppo - cfg.critic * s_v + b * s_ent), -s_ppo, -b * s_ent, cfg.critic * s_v, gn,
+                                s_ent, self.kl[0], self.kl[0] / m, torch.zeros((), device=self.dev)])
+            self.stats.add_(vals)
+            k = STAT_KEYS.index("kl_max")
+            self.stats[k] = torch.maximum(self.stats[k], self.kl[1])
+
+    def _extra_snapshot(self):
+        return self.counter.clone()
+
+    def _extra_restore(self, snap):
+        self.counter.copy_(snap)
+        self.refresh_weights()  # the capture warm-up stepped (and then restored) the master weights

@@ -167,6 +167,7 @@ class PPOUpdater:
         snap_p = [p.detach().clone() for p in params]
         snap_o = self.opt.snapshot()
         snap_s = self.stats.clone()
+        snap_x = self._extra_snapshot()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -189,7 +190,14 @@ class PPOUpdater:
                 p.copy_(q)
         self.opt.restore(snap_o)
         self.stats.copy_(snap_s)
+        self._extra_restore(snap_x)
         self._g = {"key": key, "idx": idx, "g1": g1, "g2": g2, "st": st}
+
+    def _extra_snapshot(self):
+        return None
+
+    def _extra_restore(self, snap):
+        pass
 
     def _replay(self, idx):
         g = self._g

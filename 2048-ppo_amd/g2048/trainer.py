@@ -19,6 +19,7 @@ from pathlib import Path
 import torch
 
 from . import _lib as L
+from . import fastmlp
 from .advantage import RewardWeights, RTGTracker
 from .dist import GradBucket, allreduce_sum_, world
 from .optim import MuonAdamW, ScheduledMuonAdamW, build_optimizer
@@ -59,6 +60,7 @@ class TrainConfig:
     seed: int = 0x2048
     graph: bool = True
     graph_update: bool = True      # hipGraph-captured PPO minibatch step (graph-safe Muon+AdamW)
+    fused_update: bool = True      # GameMLP forward/backward as explicit kernels (g2048/fastmlp.py)
     amp: bool = True
     episodic_cap: int = 4096       # step cap of an episodic rollout without --max-steps
     chunk: int = 32                # episodic: steps between "all games over?" checks
@@ -105,10 +107,14 @@ class VecTrainer:
         self.rtg = RTGTracker(n, self.dev, self.weights, allreduce=allreduce_sum_ if self.world > 1 else None)
         gen = torch.Generator(device=self.dev)
         gen.manual_seed(cfg.seed + 104729 * self.rank)
-        self.ppo = PPOUpdater(self.model, self.opt, PPOConfig(batch_size=cfg.batch_size, epochs=cfg.epochs,
-                                                              critic=cfg.critic,
-                                                              amp_dtype=torch.bfloat16 if cfg.amp else None),
-                              self.grads, gen, graph=cfg.graph_update and not self.episodic)
+        pcfg = PPOConfig(batch_size=cfg.batch_size, epochs=cfg.epochs, critic=cfg.critic,
+                         amp_dtype=torch.bfloat16 if cfg.amp else None)
+        graph_up = cfg.graph_update and not self.episodic
+        if cfg.fused_update and cfg.amp and self.dev.type == "cuda" and fastmlp.supports(self.model):
+            self.ppo = fastmlp.FusedPPOUpdater(self.model, self.opt, pcfg, self.grads, gen, graph=graph_up,
+                                               seed=cfg.seed * 31 + self.rank)
+        else:
+            self.ppo = PPOUpdater(self.model, self.opt, pcfg, self.grads, gen, graph=graph_up)
         self.beta = cfg.entropy
         self.obs_mb = None
         self.run_score = torch.zeros(n, dtype=torch.int64, device=self.dev)

@@ -1,0 +1,106 @@
+/*
+ * g2048_ppo.h -- C ABI of the PPO-update kernels in libg2048.so: the GameMLP forward/backward and
+ * the PPO-clip loss of model_optimize_step (train.py:414-642) around the model's GEMMs.
+ *
+ * The reference runs this step through torch autograd (agent GameMLP, game.py:1033-1220; loss
+ * train.py:497-568).  Here the minibatch step is explicit: the GEMMs X W^T / dG W / dG^T X go to
+ * the platform BLAS (hipBLASLt through torch), everything between them is one of the fused kernels
+ * below, and the whole step is captured in a hipGraph by the caller (g2048/fastmlp.py).
+ *
+ * Conventions: as g2048.h (device pointers, asynchronous on `stream`, no allocation, no host
+ * synchronisation, 0 / G2048_EINVAL / hipError_t).  Activations are bf16 (raw uint16 bits),
+ * row-major [m, h] with h % 4 == 0 and h <= 1024; LayerNorm statistics, gradients and all
+ * reductions are fp32.  Reductions over rows go through per-block partials in a fixed order, so
+ * every entry point is deterministic run to run.
+ */
+#ifndef G2048_PPO_H
+#define G2048_PPO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "g2048.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* nn.Dropout(p) of a ResidualBlock (game.py:1033-1046), train mode.  The keep mask of element
+ * (row, col) is a Philox4x32-10 draw keyed by `seed` with counter
+ * {row, col/4 | layer << 12 | pass << 20, *counter_dev + counter} -- regenerated, never stored, so
+ * the backward pass sees exactly the forward's mask.  p == 0 disables it. */
+typedef struct g2048_dropout {
+    float p;
+    uint32_t layer;
+    uint32_t pass;
+    uint32_t pad_;
+    uint64_t seed;
+    uint64_t counter;
+    const uint64_t *counter_dev; /* optional device counter base (graph replays advance it) */
+} g2048_dropout;
+
+/* to_model_format (game.py:92-101) of boards[idx[r]] for r < m -> bf16 [m, 48]: the gather of a
+ * minibatch out of the flat trajectory fused with the encoding. */
+int g2048_obs_gather(g2048_stream_t stream, const int8_t *boards, const int64_t *idx, int64_t m, uint16_t *obs);
+
+/* y = res + Dropout(ReLU(LayerNorm(g)))  (res == NULL: the stem, y = ReLU(LayerNorm(g))).
+ * LayerNorm eps 1e-5 with affine gamma/beta (nn.LayerNorm defaults); writes the per-row mean and
+ * 1/sqrt(var + eps) for the backward pass. */
+int g2048_ln_act_fwd(g2048_stream_t stream, const uint16_t *g, const float *gamma, const float *beta,
+                     const uint16_t *res, uint16_t *y, float *mean, float *rstd, int64_t m, int32_t h,
+                     const g2048_dropout *drop);
+
+/* Scratch floats of g2048_ln_act_bwd for (m, h). */
+size_t g2048_ln_act_bwd_partials(int64_t m, int32_t h);
+
+/* Backward of g2048_ln_act_fwd.  The incoming gradient of y is dy = dres_in + p_in (either may be
+ * NULL; dres_in fp32 [m,h] is the residual stream's gradient from above, p_in bf16 [m,h] the
+ * matmul gradient dG_next W_next).  Writes dg (bf16 [m,h], gradient of the pre-norm activation),
+ * dy itself to dres_out (fp32, optional: the residual gradient passed further down), and
+ * dgamma / dbeta (fp32 [h], overwritten). */
+int g2048_ln_act_bwd(g2048_stream_t stream, const float *dres_in, const uint16_t *p_in, const uint16_t *g,
+                     const float *mean, const float *rstd, const float *gamma, const float *beta, uint16_t *dg,
+                     float *dres_out, float *partials, float *dgamma, float *dbeta, int64_t m, int32_t h,
+                     const g2048_dropout *drop);
+
+/* Per-minibatch inputs of the PPO loss, gathered on the fly through idx from the flat trajectory
+ * (train.py:466-496). */
+typedef struct g2048_ppo_batch {
+    const int64_t *idx;    /* [m] rows of the flat trajectory */
+    const uint8_t *action; /* [M] */
+    const uint8_t *legal;  /* [M] bit a = action a legal */
+    const float *old_logp; /* [M, 4] log_softmax of the masked rollout logits */
+    const float *adv;      /* [M] */
+    const float *ret;      /* [M] normalised return-to-go (value target) */
+} g2048_ppo_batch;
+
+/* Scratch floats of g2048_ppo_head_loss / g2048_ppo_head_kl for (m, h). */
+size_t g2048_ppo_head_partials(int64_t m, int32_t h);
+
+/* Policy/value heads + PPO-clip loss + their backward for one minibatch (train.py:497-568):
+ *   logits = x Wa^T + ba, value = x Wv^T + bv;  masked = logits with -inf at illegal actions;
+ *   ratio = exp(clamp(logpi(a) - old_logp(a), -20, 20));  ppo = min(A ratio, A clip(ratio, 1-eps, 1+eps));
+ *   H = -sum_legal softmax(clamp(masked,-20,20)) log_softmax(...);  v = smooth_l1(value, ret);
+ *   loss = -mean(ppo - critic v + beta H)
+ * Writes masked (fp32 [m,4], for the KL diagnostic), dx = dloss/dx (fp32 [m,h]; the value branch
+ * is excluded when decouple_critic, game.py:1213-1219), the head gradients dwa [4,h], dba [4],
+ * dwv [h], dbv [1] (overwritten) and sums[3] = {sum ppo, sum H, sum v} over the minibatch.
+ * beta_dev: device float (the entropy coefficient, a device scalar so replays see updates). */
+int g2048_ppo_head_loss(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, const float *wv,
+                        const float *bv, int64_t m, int32_t h, const g2048_ppo_batch *batch, const float *beta_dev,
+                        float critic, float clip_eps, int32_t decouple_critic, float *masked, float *dx,
+                        float *partials, float *dwa, float *dba, float *dwv, float *dbv, float *sums);
+
+/* KL(old || new) diagnostic after the optimizer step (train.py:578-601): new logits x Wa^T + ba
+ * against the stored masked logits (illegal = -inf).  out[2] = {sum KL, max KL} (overwritten). */
+int g2048_ppo_head_kl(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, int64_t m,
+                      int32_t h, const float *old_masked, float *partials, float *out);
+
+/* Test hook: the dropout keep mask (uint8 [m,h], 1 = kept) g2048_ln_act_fwd applies. */
+int g2048_dropout_mask(g2048_stream_t stream, int64_t m, int32_t h, const g2048_dropout *drop, uint8_t *mask);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* G2048_PPO_H */

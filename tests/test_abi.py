@@ -1,4 +1,4 @@
-"""CPU-side checks of the C ABI: the library loads and exports every symbol include/g2048.h declares,
+"""CPU-side checks of the C ABI: the library loads and exports every symbol include/*.h declares,
 and the Python seam refuses CPU tensors (no silent CPU fallback)."""
 
 import ctypes
@@ -11,7 +11,7 @@ from conftest import ROOT
 
 
 def declared_functions():
-    text = (ROOT / "include" / "g2048.h").read_text()
+    text = "\n".join(p.read_text() for p in sorted((ROOT / "include").glob("*.h")))
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(g2048_[a-z0-9_]+)\s*\(", text)))
 
@@ -20,7 +20,8 @@ def test_header_declares_the_boundary():
     names = declared_functions()
     for required in ("g2048_env_step", "g2048_env_reset", "g2048_legal_mask", "g2048_obs_encode",
                      "g2048_sample_actions", "g2048_reward_rtg", "g2048_rtg_prepare", "g2048_rtg_finalize",
-                     "g2048_mt_seed"):
+                     "g2048_mt_seed", "g2048_obs_gather", "g2048_ln_act_fwd", "g2048_ln_act_bwd",
+                     "g2048_ppo_head_loss", "g2048_ppo_head_kl"):
         assert required in names
 
 
@@ -53,3 +54,6 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.Rng) == 48
     assert _lib.Rng.counter_dev.offset == 24
     assert ctypes.sizeof(_lib.RewardCfg) == 40
+    assert ctypes.sizeof(_lib.Dropout) == 40
+    assert _lib.Dropout.counter_dev.offset == 32
+    assert ctypes.sizeof(_lib.PPOBatch) == 48
