@@ -6,6 +6,7 @@
 //   ln_bwd_kernel<J,D>    its backward: dg, the residual gradient, dgamma/dbeta partials
 //   head_loss_kernel<J>   action/value heads + PPO-clip loss + entropy + smooth-L1 + backward
 //   head_kl_kernel<J>     KL(old || new) of the post-step re-forward (train.py:578-601)
+//   wgrad_kernel<BI,BJ>   dW = dG^T X on bf16 MFMA (tall-skinny, K = minibatch rows)
 //   colsum1/2             deterministic two-level column sums of per-block partials
 //
 // One wave per row: lane l owns columns 4(l + 64j), j < J = ceil(h/256), so a row is J
@@ -543,6 +544,134 @@ __global__ __launch_bounds__(kThreads) void head_kl_kernel(const uint16_t *__res
     }
 }
 
+
+// ------------------------------------------------------------------ weight gradient ----------
+// C[n1][n2] = sum_m A[m][n1] B[m][n2]  (dW = dG^T X of a Linear layer, A = dG, B = X, both bf16
+// row-major [M, n]).  A tall-skinny reduction GEMM on bf16 MFMA (v_mfma_f32_16x16x32_bf16):
+// each 256-thread block owns a slab of rows and the WHOLE output (waves tiled WI x WJ, each wave
+// BI x BJ 16x16 tiles in registers), stages 64 rows of A and B per step into LDS (two buffers,
+// the next step's global loads in flight during the MFMAs) and reads both operands with the
+// hardware-transposing ds_read_b64_tr_b16 from the row-major image, so no transpose pass.
+// The k order inside a 32-row block is permuted (group g of a half reads rows 4g..4g+3 and
+// 16+4g..16+4g+3) identically for both operands; with the row pitch == 32 mod 256 bytes the
+// 8 rows a 32-lane half touches fill the 64 banks exactly (conflict-free).  Per-block partial
+// outputs are summed in a fixed order by colsum1/2 (deterministic).
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kWgRows = 64;
+constexpr int kWgThreads = 256;  // 4 waves: one 139-KB-LDS block per CU, 512 registers per lane
+constexpr int kWgItems = 14;  // 8-B staging chunks per thread per step and operand (n <= 224)
+
+__device__ __forceinline__ bf16x8_t wg_frag(const char *buf, int pitch, int kb, int c0, int lane) {
+    const int g = (lane >> 4) & 3, q = (lane >> 2) & 3, p = lane & 3;
+    const char *a1 = buf + (kb * 32 + 4 * g + q) * pitch + (c0 + 4 * p) * 2;
+    const s16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)a1);
+    const s16x4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(a1 + 16 * pitch));
+    // whole-vector reinterpretation (element-wise __bf16 casts of the i16 lanes miscompile)
+    const s16x8_t v = __builtin_shufflevector(t1, t2, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <int BI, int BJ>
+__global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t *__restrict__ A, const uint16_t *__restrict__ B,
+                                                           int64_t M, int n1, int n2, int pa, int pb, int wi_n,
+                                                           int64_t rows_per_block, float *__restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ti0 = (wave % wi_n) * BI, tj0 = (wave / wi_n) * BJ;  // wave-uniform: scalar branches
+    const int TI = (n1 + 15) >> 4, TJ = (n2 + 15) >> 4;
+    const int stage_bytes = kWgRows * (pa + pb);
+    for (int o = tid * 16; o < 2 * stage_bytes; o += kWgThreads * 16) *reinterpret_cast<uint4 *>(smem + o) = make_uint4(0, 0, 0, 0);
+
+    // Staging: the 64 rows of a step are one contiguous span of A (and of B) in HBM, read as
+    // 8-byte chunks c = tid + 256u; each chunk's LDS slot (row pitch pa / pb) is fixed per thread.
+    const int ga = n1 >> 2, gb = n2 >> 2, ca = kWgRows * ga, cb = kWgRows * gb;
+    const int64_t r_begin = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r_end = min(M, r_begin + rows_per_block);
+    int offa[kWgItems], offb[kWgItems];
+#pragma unroll
+    for (int u = 0; u < kWgItems; u++) {
+        const int c = tid + u * kWgThreads;
+        const int ra = c / ga, rb = c / gb;
+        offa[u] = ra * pa + 8 * (c - ra * ga);
+        offb[u] = kWgRows * pa + rb * pb + 8 * (c - rb * gb);
+    }
+    uint2 rega[kWgItems], regb[kWgItems];
+    auto load = [&](int64_t r0) {
+        const char *sa = reinterpret_cast<const char *>(A + r0 * n1);
+        const char *sb = reinterpret_cast<const char *>(B + r0 * n2);
+        const int64_t va = (r_end - r0) * ga, vb = (r_end - r0) * gb;  // valid chunks
+#pragma unroll
+        for (int u = 0; u < kWgItems; u++) {
+            const int c = tid + u * kWgThreads;
+            rega[u] = (c < ca && c < va) ? *reinterpret_cast<const uint2 *>(sa + 8 * c) : make_uint2(0, 0);
+            regb[u] = (c < cb && c < vb) ? *reinterpret_cast<const uint2 *>(sb + 8 * c) : make_uint2(0, 0);
+        }
+    };
+    auto store = [&](int s) {
+        char *base = smem + s * stage_bytes;
+#pragma unroll
+        for (int u = 0; u < kWgItems; u++) {
+            const int c = tid + u * kWgThreads;
+            if (c < ca) *reinterpret_cast<uint2 *>(base + offa[u]) = rega[u];
+            if (c < cb) *reinterpret_cast<uint2 *>(base + offb[u]) = regb[u];
+        }
+    };
+    f32x4_t acc[BI][BJ];
+#pragma unroll
+    for (int i = 0; i < BI; i++)
+#pragma unroll
+        for (int j = 0; j < BJ; j++) acc[i][j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+
+    __syncthreads();  // zero fill done before the first tile lands
+    if (r_begin < r_end) {
+        load(r_begin);
+        store(0);
+    }
+    __syncthreads();
+    int s = 0;
+    for (int64_t r0 = r_begin; r0 < r_end; r0 += kWgRows) {
+        const bool more = r0 + kWgRows < r_end;
+        if (more) load(r0 + kWgRows);
+        const char *ba = smem + s * stage_bytes, *bb = ba + kWgRows * pa;
+#pragma unroll
+        for (int kb = 0; kb < 2; kb++) {
+            bf16x8_t fa[BI], fb[BJ];
+#pragma unroll
+            for (int i = 0; i < BI; i++)
+                if (ti0 + i < TI) fa[i] = wg_frag(ba, pa, kb, 16 * (ti0 + i), lane);
+#pragma unroll
+            for (int j = 0; j < BJ; j++)
+                if (tj0 + j < TJ) fb[j] = wg_frag(bb, pb, kb, 16 * (tj0 + j), lane);
+#pragma unroll
+            for (int i = 0; i < BI; i++)
+#pragma unroll
+                for (int j = 0; j < BJ; j++)
+                    if (ti0 + i < TI && tj0 + j < TJ)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+        if (more) store(s ^ 1);
+        __syncthreads();
+        s ^= 1;
+    }
+    float *out = part + (int64_t)blockIdx.x * n1 * n2;
+    const int col = lane & 15, rowq = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < BI; i++)
+#pragma unroll
+        for (int j = 0; j < BJ; j++) {
+            const int ii = 16 * (ti0 + i) + rowq, jj = 16 * (tj0 + j) + col;
+            if (ti0 + i < TI && tj0 + j < TJ && jj < n2)
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    if (ii + r < n1) out[(int64_t)(ii + r) * n2 + jj] = acc[i][j][r];
+        }
+}
+
 // ------------------------------------------------------------------ column sums --------------
 // Stage 1: grid (ceil(C/64), kSlices); block (64 columns x 4 row groups) sums rows of slice y.
 constexpr int kSlices = 32;
@@ -646,6 +775,44 @@ int colsum(hipStream_t s, const float *part, int nb, int C, float *scratch2, con
     hipLaunchKernelGGL(colsum1_kernel, dim3((C + 63) / 64, kSlices), dim3(256), 0, s, part, nb, C, scratch2, max_col);
     hipLaunchKernelGGL(colsum2_kernel, dim3((C + 255) / 256), dim3(256), 0, s, scratch2, C, segs, max_col);
     return status();
+}
+
+
+// weight-gradient launch geometry
+struct WgPlan {
+    int bi, bj, wi, nb, pa, pb;
+    int64_t rows;
+    size_t lds;
+};
+
+inline int wg_pitch(int n) {  // LDS row bytes: >= 2 * pad16(n) and == 32 (mod 256)
+    const int b = ((n + 15) / 16) * 32;
+    return b + (((32 - b) % 256) + 256) % 256;
+}
+
+inline bool wg_plan(int64_t m, int n1, int n2, WgPlan &p) {
+    if (n1 <= 0 || n2 <= 0 || n1 % 4 || n2 % 4 || n1 > 224 || n2 > 224 || m <= 0) return false;
+    const int TI = (n1 + 15) / 16, TJ = (n2 + 15) / 16;
+    static const int menu[3][2] = {{2, 2}, {4, 4}, {7, 7}};
+    static const int arr[3][2] = {{2, 2}, {4, 1}, {1, 4}};
+    for (auto &mb : menu)
+        for (auto &a : arr)
+            if (a[0] * mb[0] >= TI && a[1] * mb[1] >= TJ) {
+                p.bi = mb[0];
+                p.bj = mb[1];
+                p.wi = a[0];
+                int64_t nb = m / 512;
+                nb = nb < 1 ? 1 : (nb > 256 ? 256 : nb);
+                int64_t rows = (m + nb - 1) / nb;
+                rows = (rows + kWgRows - 1) / kWgRows * kWgRows;
+                p.nb = (int)((m + rows - 1) / rows);
+                p.rows = rows;
+                p.pa = wg_pitch(n1);
+                p.pb = wg_pitch(n2);
+                p.lds = (size_t)2 * kWgRows * (p.pa + p.pb);
+                return true;
+            }
+    return false;
 }
 
 #define G2048_DISPATCH_J(h, BODY)            \
@@ -772,6 +939,35 @@ int g2048_ppo_head_kl(g2048_stream_t stream, const uint16_t *x, const float *wa,
     segs.dst[0] = out;
     segs.len[0] = 2;
     return colsum(s, partials, nb, 2, partials + (size_t)nb * 2, segs, 1);
+}
+
+
+size_t g2048_wgrad_partials(int64_t m, int32_t n1, int32_t n2) {
+    WgPlan p;
+    if (!wg_plan(m, n1, n2, p)) return 0;
+    return (size_t)p.nb * n1 * n2 + (size_t)kSlices * n1 * n2;
+}
+
+int g2048_wgrad(g2048_stream_t stream, const uint16_t *a, const uint16_t *b, int64_t m, int32_t n1, int32_t n2,
+                float *partials, float *out) {
+    WgPlan p;
+    if (!a || !b || !partials || !out || !al(a, 8) || !al(b, 8)) return G2048_EINVAL;
+    if (!wg_plan(m, n1, n2, p)) return G2048_EINVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    const dim3 grid(p.nb), blk(kWgThreads);
+    if (p.bi == 2)
+        hipLaunchKernelGGL((wgrad_kernel<2, 2>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, partials);
+    else if (p.bi == 4)
+        hipLaunchKernelGGL((wgrad_kernel<4, 4>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, partials);
+    else
+        hipLaunchKernelGGL((wgrad_kernel<7, 7>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, partials);
+    const int st = status();
+    if (st) return st;
+    Segs segs{};
+    segs.n = 1;
+    segs.dst[0] = out;
+    segs.len[0] = n1 * n2;
+    return colsum(s, partials, p.nb, n1 * n2, partials + (size_t)p.nb * n1 * n2, segs, -1);
 }
 
 int g2048_dropout_mask(g2048_stream_t stream, int64_t m, int32_t h, const g2048_dropout *drop, uint8_t *mask) {

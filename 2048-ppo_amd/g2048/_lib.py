@@ -30,6 +30,7 @@ EXPORTED = (
     # include/g2048_ppo.h
     "g2048_obs_gather", "g2048_ln_act_fwd", "g2048_ln_act_bwd_partials", "g2048_ln_act_bwd",
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask",
+    "g2048_wgrad_partials", "g2048_wgrad",
 )
 
 
@@ -109,6 +110,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
                                                ctypes.c_float, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
         "g2048_ppo_head_kl": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, vp, vp, vp]),
         "g2048_dropout_mask": (ctypes.c_int, [vp, i64, i32, dp, vp]),
+        "g2048_wgrad_partials": (sz, [i64, i32, i32]),
+        "g2048_wgrad": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -305,3 +308,19 @@ def ppo_head_kl(x, wa, ba, old_masked, partials, out):
 def dropout_mask(m: int, h: int, drop: Dropout, mask):
     _check(load().g2048_dropout_mask(_stream(mask), m, h, ctypes.byref(drop), _dev(mask, torch.uint8, "mask")),
            "g2048_dropout_mask")
+
+
+def wgrad_partials(m: int, n1: int, n2: int) -> int:
+    """Scratch floats of wgrad (0 = shape not supported by the MFMA kernel)."""
+    return int(load().g2048_wgrad_partials(m, n1, n2))
+
+
+def wgrad(a, b, partials, out):
+    """out[n1, n2] = a^T b for bf16 a [m, n1], b [m, n2]; fp32 out."""
+    m, n1 = a.shape
+    n2 = b.shape[1]
+    if b.shape[0] != m or tuple(out.shape) != (n1, n2):
+        raise G2048Error(f"wgrad shapes: a {tuple(a.shape)} b {tuple(b.shape)} out {tuple(out.shape)}")
+    _check(load().g2048_wgrad(_stream(a), _dev(a, torch.bfloat16, "a"), _dev(b, torch.bfloat16, "b"), m, n1, n2,
+                              _dev(partials, torch.float32, "partials"), _dev(out, torch.float32, "out")),
+           "g2048_wgrad")

@@ -10,8 +10,9 @@ action/value heads), FusedPPOUpdater writes the forward and backward out by hand
     loss      heads + PPO-clip + entropy + smooth-L1 and      g2048_ppo_head_loss
               d/dH_L, d/d(head params), loss sums
     backward  dG_l, dgamma_l, dbeta_l, residual grad          g2048_ln_act_bwd
-              P = dG_l W_l,  dW_l = dG_l^T H_{l-1}             GEMMs (dW in fp32, straight into the
-                                                              flat gradient bucket)
+              P = dG_l W_l                                    GEMM (hipBLASLt)
+              dW_l = dG_l^T H_{l-1}                           g2048_wgrad (bf16 MFMA, fp32 straight
+                                                              into the flat gradient bucket)
     step      [RCCL all-reduce] clip, Muon + AdamW            dist.GradBucket / optim.MuonAdamW
     KL        re-forward with the new weights (train mode)    g2048_ln_act_fwd + g2048_ppo_head_kl
 
@@ -82,7 +83,9 @@ class FusedPPOUpdater(PPOUpdater):
         self.dres = torch.empty(bs, h, dtype=torch.float32, device=d)
         self.dg = torch.empty(bs, h, dtype=bf, device=d)
         self.P = torch.empty(bs, h, dtype=bf, device=d)
-        n = max(L.ln_act_bwd_partials(bs, h), L.ppo_head_partials(bs, h))
+        self.wg_ok = [L.wgrad_partials(bs, w.shape[0], w.shape[1]) > 0 for w in self.lin]
+        n = max([L.ln_act_bwd_partials(bs, h), L.ppo_head_partials(bs, h)] +
+                [L.wgrad_partials(bs, w.shape[0], w.shape[1]) for w in self.lin])
         self.partials = torch.empty(n, dtype=torch.float32, device=d)
         self.sums = torch.zeros(3, dtype=torch.float32, device=d)
         self.kl = torch.zeros(2, dtype=torch.float32, device=d)
@@ -125,7 +128,10 @@ class FusedPPOUpdater(PPOUpdater):
                          self.dres if l > 0 else None, self.partials, ln.weight.grad, ln.bias.grad,
                          self._drop(l, 0) if l > 0 else None)
             x_in = self.H[l - 1] if l > 0 else self.x0
-            _mm(self.dg.t(), x_in, self.lin[l].grad)
+            if self.wg_ok[l]:  # dW = dG^T X on the MFMA weight-gradient kernel
+                L.wgrad(self.dg, x_in, self.partials, self.lin[l].grad)
+            else:
+                _mm(self.dg.t(), x_in, self.lin[l].grad)
             if l > 0:
                 _mm(self.dg, self.wbf[l], self.P)
                 p_in = self.P

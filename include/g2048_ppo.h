@@ -96,6 +96,15 @@ int g2048_ppo_head_loss(g2048_stream_t stream, const uint16_t *x, const float *w
 int g2048_ppo_head_kl(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, int64_t m,
                       int32_t h, const float *old_masked, float *partials, float *out);
 
+/* Scratch floats of g2048_wgrad for (m, n1, n2); 0 when the shape is unsupported. */
+size_t g2048_wgrad_partials(int64_t m, int32_t n1, int32_t n2);
+
+/* Weight gradient of a Linear layer: out[n1][n2] = sum_{r<m} a[r][n1] b[r][n2] (out = dG^T X with
+ * a = dG bf16 [m,n1], b = X bf16 [m,n2]), fp32 accumulate on bf16 MFMA, fp32 out (overwritten).
+ * n1, n2 % 4 == 0 and <= 224. */
+int g2048_wgrad(g2048_stream_t stream, const uint16_t *a, const uint16_t *b, int64_t m, int32_t n1, int32_t n2,
+                float *partials, float *out);
+
 /* Test hook: the dropout keep mask (uint8 [m,h], 1 = kept) g2048_ln_act_fwd applies. */
 int g2048_dropout_mask(g2048_stream_t stream, int64_t m, int32_t h, const g2048_dropout *drop, uint8_t *mask);
 

@@ -210,6 +210,31 @@ def test_ppo_head_kl_matches_torch(dev):
     assert math.isclose(float(out[1]), float(kl.max()), rel_tol=1e-4)
 
 
+@pytest.mark.parametrize("m,n1,n2", [(65536, 196, 196), (65536, 196, 48), (5000, 64, 64), (130, 196, 48),
+                                     (64, 224, 224), (1000, 100, 20), (777, 4, 8)])
+def test_wgrad_matches_matmul(dev, m, n1, n2):
+    from g2048 import _lib as L
+    torch.manual_seed(m + n1 + n2)
+    a = _bf(torch.randn(m, n1, device=dev))
+    b = _bf(torch.randn(m, n2, device=dev) * 3)
+    part = torch.empty(L.wgrad_partials(m, n1, n2), device=dev)
+    out = torch.empty(n1, n2, device=dev)
+    L.wgrad(a, b, part, out)
+    ref = a.double().T @ b.double()
+    err = (out.double() - ref).abs().max().item()
+    assert err <= 1e-4 * ref.abs().max().item() + 1e-3, err
+    out2 = torch.empty_like(out)
+    L.wgrad(a, b, part, out2)
+    assert torch.equal(out, out2)  # deterministic
+
+
+def test_wgrad_rejects_unsupported_shapes():
+    from g2048 import _lib as L
+    assert L.wgrad_partials(100, 256, 196) == 0
+    assert L.wgrad_partials(100, 196, 6) == 0
+    assert L.wgrad_partials(0, 196, 196) == 0
+
+
 def test_obs_gather_matches_encode(dev):
     from g2048 import _lib as L
     g = np.random.default_rng(2)
