@@ -31,6 +31,7 @@ EXPORTED = (
     "g2048_obs_gather", "g2048_ln_act_fwd", "g2048_ln_act_bwd_partials", "g2048_ln_act_bwd",
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask",
     "g2048_wgrad_partials", "g2048_wgrad",
+    "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
 )
 
 
@@ -68,6 +69,27 @@ class PPOBatch(ctypes.Structure):
     """struct g2048_ppo_batch"""
     _fields_ = [("idx", ctypes.c_void_p), ("action", ctypes.c_void_p), ("legal", ctypes.c_void_p),
                 ("old_logp", ctypes.c_void_p), ("adv", ctypes.c_void_p), ("ret", ctypes.c_void_p)]
+
+
+class MuonMatrix(ctypes.Structure):
+    """struct g2048_muon_matrix"""
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("momentum", ctypes.c_void_p),
+                ("param_bf16", ctypes.c_void_p), ("rows", ctypes.c_int32), ("cols", ctypes.c_int32),
+                ("lr_index", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
+
+class MuonCfg(ctypes.Structure):
+    """struct g2048_muon_cfg"""
+    _fields_ = [("momentum", ctypes.c_float), ("weight_decay", ctypes.c_float), ("ns_a", ctypes.c_float),
+                ("ns_b", ctypes.c_float), ("ns_c", ctypes.c_float), ("ns_eps", ctypes.c_float),
+                ("ns_steps", ctypes.c_int32), ("nesterov", ctypes.c_int32)]
+
+
+class AdamWGroup(ctypes.Structure):
+    """struct g2048_adamw_group"""
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("n", ctypes.c_int64), ("lr_index", ctypes.c_int32),
+                ("pad_", ctypes.c_int32)]
 
 
 _lib = None
@@ -112,6 +134,11 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_dropout_mask": (ctypes.c_int, [vp, i64, i32, dp, vp]),
         "g2048_wgrad_partials": (sz, [i64, i32, i32]),
         "g2048_wgrad": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, vp, vp]),
+        "g2048_grad_clip": (ctypes.c_int, [vp, vp, i64, ctypes.c_float, vp, vp]),
+        "g2048_muon_supported": (ctypes.c_int, [i32, i32]),
+        "g2048_muon_step": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.POINTER(MuonCfg)]),
+        "g2048_adamw_step": (ctypes.c_int, [vp, ctypes.POINTER(AdamWGroup), i32, vp, vp, vp, ctypes.c_float,
+                                            ctypes.c_float, ctypes.c_float, ctypes.c_float]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -324,3 +351,26 @@ def wgrad(a, b, partials, out):
     _check(load().g2048_wgrad(_stream(a), _dev(a, torch.bfloat16, "a"), _dev(b, torch.bfloat16, "b"), m, n1, n2,
                               _dev(partials, torch.float32, "partials"), _dev(out, torch.float32, "out")),
            "g2048_wgrad")
+
+
+# ------------------------------------------------------------- optimizer step -------------------
+def grad_clip(grad, max_norm: float, norm_out, coef_out):
+    _check(load().g2048_grad_clip(_stream(grad), _dev(grad, torch.float32, "grad"), grad.numel(), float(max_norm),
+                                  _dev(norm_out, torch.float32, "norm_out"), _dev(coef_out, torch.float32, "coef_out")),
+           "g2048_grad_clip")
+
+
+def muon_supported(rows: int, cols: int) -> bool:
+    return bool(load().g2048_muon_supported(rows, cols))
+
+
+def muon_step(mats, lr_dev, clip_coef_dev, cfg: MuonCfg, stream_tensor):
+    """mats: a ctypes array of MuonMatrix (built once; device pointers stay valid)."""
+    _check(load().g2048_muon_step(_stream(stream_tensor), mats, len(mats), _dev(lr_dev, torch.float32, "lr"),
+                                  _dev(clip_coef_dev, torch.float32, "clip"), ctypes.byref(cfg)), "g2048_muon_step")
+
+
+def adamw_step(groups, lr_dev, step_dev, clip_coef_dev, beta1, beta2, eps, weight_decay):
+    _check(load().g2048_adamw_step(_stream(lr_dev), groups, len(groups), _dev(lr_dev, torch.float32, "lr"),
+                                   _dev(step_dev, torch.float32, "step"), _dev(clip_coef_dev, torch.float32, "clip"),
+                                   float(beta1), float(beta2), float(eps), float(weight_decay)), "g2048_adamw_step")

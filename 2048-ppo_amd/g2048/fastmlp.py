@@ -65,6 +65,10 @@ class FusedPPOUpdater(PPOUpdater):
         self.wv, self.bv = model.value_head.weight, model.value_head.bias
         self.wbf = [torch.empty_like(w, dtype=torch.bfloat16) for w in self.lin]
         self.counter = torch.zeros(1, dtype=torch.int64, device=self.dev)  # dropout counter base
+        # a fused optimizer (optim.FusedMuonAdamW) clips, steps and refreshes the bf16 weights itself
+        self.fused_opt = bool(getattr(optimizer, "fused", False) or getattr(optimizer, "supported", False))
+        if self.fused_opt:
+            optimizer.set_bf16_copies(dict(zip(self.lin, self.wbf)))
         self.seed = seed
         self.bs = 0
 
@@ -153,9 +157,12 @@ class FusedPPOUpdater(PPOUpdater):
 
     def _post(self, st, beta):
         cfg, m = self.cfg, self.bs
-        gn = self.grads.clip_(cfg.max_grad_norm)
-        self.opt.step()
-        self.refresh_weights()
+        if self.fused_opt:
+            gn = self.opt.step_clipped(self.grads.flat, cfg.max_grad_norm)
+        else:
+            gn = self.grads.clip_(cfg.max_grad_norm)
+            self.opt.step()
+            self.refresh_weights()
         with torch.no_grad():
             x = self._layers(1)  # KL re-forward of the same minibatch (x0 still holds its encoding)
             L.ppo_head_kl(x, self.wa, self.ba, self.masked, self.partials, self.kl)

@@ -194,6 +194,76 @@ class MuonAdamW:
         self.step_t.copy_(st)
 
 
+class FusedMuonAdamW(MuonAdamW):
+    """MuonAdamW with its step as three kernels (include/g2048_ppo.h, csrc/optim.hip): the gradient
+    clip coefficient, every Muon matrix in one launch (momentum, Newton-Schulz on bf16 MFMA in LDS,
+    weight decay, scaled update, bf16 weight copy) and every AdamW group in one launch.
+
+    Same arithmetic as MuonAdamW up to the accumulation order of the bf16 Newton-Schulz products.
+    `supported` is False when a matrix does not fit the one-block Newton-Schulz kernel (h > 196);
+    callers then use MuonAdamW.
+    """
+
+    def __init__(self, model, *args, **kwargs):
+        super().__init__(model, *args, **kwargs)
+        from . import _lib as L
+        self._L = L
+        self.supported = (self.dev.type == "cuda" and 0 < len(self.muon) <= 8 and len(self.adam_groups) <= 4
+                          and all(p.ndim == 2 and L.muon_supported(*p.shape) for p, _ in self.muon))
+        self.norm_t = torch.zeros((), dtype=torch.float32, device=self.dev)
+        self.coef_t = torch.ones((), dtype=torch.float32, device=self.dev)
+        self._bf16 = {}
+        self._mats = self._groups = None
+        self._cfg = L.MuonCfg(self.momentum, self.wd, self.ns[0], self.ns[1], self.ns[2], self.ns_eps, self.ns_steps,
+                              int(self.nesterov))
+
+    def set_bf16_copies(self, mapping: dict):
+        """{parameter: bf16 tensor} refreshed by the Muon kernel after each step."""
+        self._bf16 = {id(p): t for p, t in mapping.items()}
+        self._mats = None
+
+    def _build(self):
+        L = self._L
+        mats = (L.MuonMatrix * len(self.muon))()
+        for k, ((p, gi), buf) in enumerate(zip(self.muon, self.muon_buf)):
+            if p.grad is None or not p.grad.is_contiguous():
+                raise RuntimeError("FusedMuonAdamW needs contiguous gradients (a GradBucket)")
+            bf = self._bf16.get(id(p))
+            mats[k] = L.MuonMatrix(p.data_ptr(), p.grad.data_ptr(), buf.data_ptr(), bf.data_ptr() if bf is not None else None,
+                                   p.shape[0], p.shape[1], gi, 0)
+        groups = (L.AdamWGroup * len(self.adam_groups))()
+        for k, grp in enumerate(self.adam_groups):
+            g = self._flat_grad(grp)
+            if g.data_ptr() != grp["params"][0].grad.data_ptr():
+                raise RuntimeError("FusedMuonAdamW needs each AdamW group's gradients contiguous in the bucket")
+            groups[k] = L.AdamWGroup(grp["flat"].data_ptr(), g.data_ptr(), grp["m"].data_ptr(), grp["v"].data_ptr(),
+                                     grp["flat"].numel(), grp["idx"], 0)
+        self._mats, self._groups = mats, groups
+
+    def _run(self, clip):
+        if self._mats is None:
+            self._build()
+        L = self._L
+        L.muon_step(self._mats, self.lr, clip, self._cfg, self.lr)
+        self.step_t.add_(1)
+        if len(self._groups):
+            L.adamw_step(self._groups, self.lr, self.step_t, clip, self.b1, self.b2, self.eps, self.wd)
+
+    @torch.no_grad()
+    def step(self):
+        if not self.supported:
+            return super().step()
+        self._run(None)
+
+    @torch.no_grad()
+    def step_clipped(self, flat_grad: torch.Tensor, max_norm: float) -> torch.Tensor:
+        """clip_grad_norm_(max_norm) folded into the step (the bucket itself is left unclipped);
+        returns the pre-clip norm as a device scalar."""
+        self._L.grad_clip(flat_grad, max_norm, self.norm_t, self.coef_t)
+        self._run(self.coef_t)
+        return self.norm_t
+
+
 class ScheduledMuonAdamW:
     """MuonAdamW + the cosine-with-warmup schedule stepped once per train step (train.py:1598-1612, :625)."""
 
@@ -210,6 +280,16 @@ class ScheduledMuonAdamW:
 
     def step(self):
         self.opt.step()
+
+    @property
+    def fused(self) -> bool:
+        return getattr(self.opt, "supported", False)
+
+    def step_clipped(self, flat_grad, max_norm):
+        return self.opt.step_clipped(flat_grad, max_norm)
+
+    def set_bf16_copies(self, mapping):
+        self.opt.set_bf16_copies(mapping)
 
     def zero_grad(self, set_to_none: bool = False):
         pass

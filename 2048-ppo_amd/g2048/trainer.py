@@ -22,7 +22,7 @@ from . import _lib as L
 from . import fastmlp
 from .advantage import RewardWeights, RTGTracker
 from .dist import GradBucket, allreduce_sum_, world
-from .optim import MuonAdamW, ScheduledMuonAdamW, build_optimizer
+from .optim import FusedMuonAdamW, MuonAdamW, ScheduledMuonAdamW, build_optimizer
 from .ppo import PPOConfig, PPOUpdater
 from .rollout import InferencePolicy, Rollout
 
@@ -86,7 +86,13 @@ class VecTrainer:
             for p in self.model.parameters():
                 torch.distributed.broadcast(p.data, 0)
         if cfg.graph_update:
-            opt = MuonAdamW(self.model, cfg.lr, cfg.critic_lr, cfg.beta1, cfg.beta2, cfg.weight_decay)
+            opt = None
+            if cfg.fused_update and self.dev.type == "cuda":
+                opt = FusedMuonAdamW(self.model, cfg.lr, cfg.critic_lr, cfg.beta1, cfg.beta2, cfg.weight_decay)
+                if not opt.supported:
+                    opt = None
+            if opt is None:
+                opt = MuonAdamW(self.model, cfg.lr, cfg.critic_lr, cfg.beta1, cfg.beta2, cfg.weight_decay)
             self.opt = ScheduledMuonAdamW(opt, cfg.warmup_steps, cfg.steps)
             # grads of the AdamW groups contiguous in the bucket (2-D first, then each 1-D group)
             order = [p for p, _ in opt.muon] + [p for g in opt.adam_groups for p in g["params"]]

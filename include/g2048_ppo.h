@@ -105,6 +105,55 @@ size_t g2048_wgrad_partials(int64_t m, int32_t n1, int32_t n2);
 int g2048_wgrad(g2048_stream_t stream, const uint16_t *a, const uint16_t *b, int64_t m, int32_t n1, int32_t n2,
                 float *partials, float *out);
 
+/* ---- optimizer step (train.py:553-568, :1587-1612) ------------------------------------------ */
+
+/* clip_grad_norm_ of the flat gradient bucket, without touching it: norm_out = ||grad||,
+ * coef_out = min(max_norm / (norm + 1e-6), 1) (device scalars read by the optimizer kernels). */
+int g2048_grad_clip(g2048_stream_t stream, const float *grad, int64_t n, float max_norm, float *norm_out,
+                    float *coef_out);
+
+/* One Muon-optimised weight matrix (torch.optim.Muon, adjust_lr_fn="match_rms_adamw"). */
+typedef struct g2048_muon_matrix {
+    float *param;          /* [rows, cols] fp32, updated in place */
+    const float *grad;     /* [rows, cols] fp32 (multiplied by *clip_coef_dev when given) */
+    float *momentum;       /* [rows, cols] fp32 momentum buffer */
+    uint16_t *param_bf16;  /* optional: bf16 copy of the updated weight */
+    int32_t rows, cols;
+    int32_t lr_index;      /* this matrix's learning rate is lr_dev[lr_index] */
+    int32_t pad_;
+} g2048_muon_matrix;
+
+typedef struct g2048_muon_cfg {
+    float momentum, weight_decay, ns_a, ns_b, ns_c, ns_eps;
+    int32_t ns_steps, nesterov;
+} g2048_muon_cfg;
+
+/* 1 if a [rows, cols] matrix fits the one-block-per-matrix Newton-Schulz kernel (min dim <= 224,
+ * max dim <= 224, both LDS images <= ~159 KB: h <= 196 for square weights). */
+int g2048_muon_supported(int32_t rows, int32_t cols);
+
+/* Muon step of up to 8 matrices, all concurrently: momentum (nesterov), Newton-Schulz
+ * orthogonalisation in bf16 (ns_steps iterations of X <- a X + (b G + c G^2) X, G = X X^T, on the
+ * wide orientation), decoupled weight decay, update scaled by 0.2 sqrt(max(rows, cols)). */
+int g2048_muon_step(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_t count, const float *lr_dev,
+                    const float *clip_coef_dev, const g2048_muon_cfg *cfg);
+
+/* One flat group of 1-D parameters for AdamW (torch.optim.AdamW, decoupled weight decay). */
+typedef struct g2048_adamw_group {
+    float *param;
+    const float *grad;
+    float *exp_avg;
+    float *exp_avg_sq;
+    int64_t n;
+    int32_t lr_index;
+    int32_t pad_;
+} g2048_adamw_group;
+
+/* AdamW step of up to 4 groups; *step_dev is the (already incremented) step count. */
+int g2048_adamw_step(g2048_stream_t stream, const g2048_adamw_group *groups, int32_t count, const float *lr_dev,
+                     const float *step_dev, const float *clip_coef_dev, float beta1, float beta2, float eps,
+                     float weight_decay);
+
 /* Test hook: the dropout keep mask (uint8 [m,h], 1 = kept) g2048_ln_act_fwd applies. */
 int g2048_dropout_mask(g2048_stream_t stream, int64_t m, int32_t h, const g2048_dropout *drop, uint8_t *mask);
 

@@ -363,23 +363,72 @@ def _synthetic_data(dev, M, seed=0):
             "ret": torch.from_numpy(g.normal(size=M).astype(np.float32)).to(dev)}
 
 
-def test_fused_graphed_update_equals_eager(dev):
+def _muon_models(dev, h=196):
+    import agent
+    from g2048.dist import GradBucket
+    from g2048.optim import FusedMuonAdamW, MuonAdamW
+    out = []
+    for cls in (MuonAdamW, FusedMuonAdamW):
+        torch.manual_seed(21)
+        m = agent.GameMLP(agent.MLPConfig(hidden_dim=h, num_layers=2, dropout=0.0)).to(dev)
+        opt = cls(m, 2e-3, 5e-4)
+        order = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
+        out.append((m, opt, GradBucket(order)))
+    return out
+
+
+@pytest.mark.parametrize("h", [196, 64])
+def test_fused_muon_adamw_matches_torch_ops_step(dev, h):
+    """FusedMuonAdamW (clip + Muon + AdamW kernels) vs MuonAdamW (torch ops, itself checked against
+    torch.optim.Muon/AdamW) over three steps on the same gradients."""
+    (m0, o0, b0), (m1, o1, b1) = _muon_models(dev, h)
+    assert o1.supported
+    init = [p.detach().clone() for p in m0.parameters()]
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    for step in range(3):
+        grads = torch.randn(b0.flat.shape, generator=g, device=dev) * (0.5 if step else 3.0)  # step 0 clips
+        b0.flat.copy_(grads)
+        b1.flat.copy_(grads)
+        n0 = b0.clip_(1.0)
+        o0.step()
+        n1 = o1.step_clipped(b1.flat, 1.0)
+        assert math.isclose(float(n0), float(n1), rel_tol=1e-5)
+    for (name, p0), p1, q in zip(m0.named_parameters(), m1.parameters(), init):
+        d0, d1 = (p0 - q).reshape(-1), (p1 - q).reshape(-1)
+        if p0.ndim >= 2:  # bf16 Newton-Schulz: same direction and size up to accumulation order
+            assert float(F.cosine_similarity(d0, d1, dim=0)) > 0.999, name
+            assert math.isclose(float(d0.norm()), float(d1.norm()), rel_tol=1e-2), name
+        else:
+            torch.testing.assert_close(p1, p0, rtol=1e-5, atol=1e-6)
+
+
+def test_fused_muon_supported_shapes():
+    from g2048 import _lib as L
+    assert L.muon_supported(196, 196) and L.muon_supported(196, 48) and L.muon_supported(4, 196)
+    assert L.muon_supported(1, 196) and L.muon_supported(64, 64)
+    assert not L.muon_supported(256, 256) and not L.muon_supported(196, 6)
+
+
+@pytest.mark.parametrize("fused_opt", [False, True])
+def test_fused_graphed_update_equals_eager(dev, fused_opt):
     """The captured fused step (dropout on, graph-safe Muon+AdamW) is bitwise the eager one."""
     import agent
     from g2048.dist import GradBucket
     from g2048.fastmlp import FusedPPOUpdater
-    from g2048.optim import MuonAdamW
+    from g2048.optim import FusedMuonAdamW, MuonAdamW
     from g2048.ppo import PPOConfig
     data = _synthetic_data(dev, 8192)
     out = []
     for graph in (False, True):
         torch.manual_seed(3)
         m = agent.GameMLP(agent.MLPConfig(hidden_dim=196, num_layers=2, dropout=0.1)).to(dev)
-        opt = MuonAdamW(m, 1e-3, 1e-4)
+        opt = (FusedMuonAdamW if fused_opt else MuonAdamW)(m, 1e-3, 1e-4)
         order = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
         gen = torch.Generator(device=dev)
         gen.manual_seed(5)
         up = FusedPPOUpdater(m, opt, PPOConfig(batch_size=2048, critic=0.2), GradBucket(order), gen, graph=graph)
+        assert up.fused_opt == fused_opt
         st = None
         for _ in range(3):
             st = {k: float(v) for k, v in up.update(data, 0.02).items()}

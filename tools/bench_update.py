@@ -25,13 +25,13 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--hidden", type=int, default=196)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--which", default="autograd,fused")
+    ap.add_argument("--which", default="autograd,fused_torchopt,fused")
     a = ap.parse_args()
     import agent
     from g2048 import _lib as L
     from g2048.dist import GradBucket
     from g2048.fastmlp import FusedPPOUpdater
-    from g2048.optim import MuonAdamW
+    from g2048.optim import FusedMuonAdamW, MuonAdamW
     from g2048.ppo import PPOConfig, PPOUpdater
     dev = torch.device("cuda:0")
     g = np.random.default_rng(0)
@@ -56,11 +56,11 @@ def main():
     for which in a.which.split(","):
         torch.manual_seed(0)
         m = agent.GameMLP(agent.MLPConfig(hidden_dim=a.hidden, num_layers=2, dropout=0.1)).to(dev)
-        opt = MuonAdamW(m, 1e-3, 1e-4)
+        opt = (FusedMuonAdamW if which == "fused" else MuonAdamW)(m, 1e-3, 1e-4)
         order = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
         gen = torch.Generator(device=dev)
         gen.manual_seed(1)
-        cls = FusedPPOUpdater if which == "fused" else PPOUpdater
+        cls = FusedPPOUpdater if which.startswith("fused") else PPOUpdater
         up = cls(m, opt, PPOConfig(batch_size=a.batch, critic=0.2), GradBucket(order), gen, graph=True)
         up.update(data, 0.02, enc)
         torch.cuda.synchronize()

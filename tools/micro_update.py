@@ -1,0 +1,91 @@
+"""Micro-timings of the pieces of one fused PPO minibatch step (GPU only): the GEMM shapes, the
+Muon+AdamW optimizer step and the fused kernels, each in a captured graph replayed many times.
+
+    python tools/micro_update.py
+"""
+
+from __future__ import annotations
+
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "2048-ppo_amd"))
+
+import torch  # noqa: E402
+
+
+def timed(fn, reps=50):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(10):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / (reps * 10) * 1e3  # us per call
+
+
+def main():
+    import agent
+    from g2048 import _lib as L
+    from g2048.optim import MuonAdamW
+    dev = torch.device("cuda:0")
+    M, h = 65536, 196
+    bf = torch.bfloat16
+    X = torch.randn(M, h, device=dev, dtype=bf)
+    X0 = torch.randn(M, 48, device=dev, dtype=bf)
+    W = torch.randn(h, h, device=dev, dtype=bf)
+    Ws = torch.randn(h, 48, device=dev, dtype=bf)
+    G = torch.empty(M, h, device=dev, dtype=bf)
+    out = {}
+    out["fwd X W^T [65536x196x196]"] = timed(lambda: torch.mm(X, W.t(), out=G))
+    out["fwd stem X0 Ws^T [65536x48->196]"] = timed(lambda: torch.mm(X0, Ws.t(), out=G))
+    out["bwd dG W [65536x196x196]"] = timed(lambda: torch.mm(X, W, out=G))
+    dW = torch.empty(h, h, device=dev)
+    part = torch.empty(L.wgrad_partials(M, h, h), device=dev)
+    out["wgrad dG^T X (MFMA kernel)"] = timed(lambda: L.wgrad(X, X, part, dW))
+    out["wgrad torch.mm out_dtype f32"] = timed(lambda: dW.copy_(torch.mm(X.t(), X, out_dtype=torch.float32)))
+    A = torch.randn(h, h, device=dev, dtype=bf)
+    C = torch.empty(h, h, device=dev, dtype=bf)
+    out["ns gemm 196^3 bf16"] = timed(lambda: torch.mm(A, A, out=C))
+    A2 = torch.randn(2, h, h, device=dev, dtype=bf)
+    C2 = torch.empty(2, h, h, device=dev, dtype=bf)
+    out["ns bmm 2x196^3 bf16"] = timed(lambda: torch.bmm(A2, A2, out=C2))
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=h, num_layers=2, dropout=0.1)).to(dev)
+    opt = MuonAdamW(m, 1e-3, 1e-4)
+    for p in m.parameters():
+        p.grad = torch.randn_like(p) * 1e-2
+    out["MuonAdamW.step (all params)"] = timed(opt.step, reps=10)
+    g = torch.randn(h, h, device=dev)
+    out["newton_schulz 196x196"] = timed(lambda: opt._newton_schulz(g), reps=10)
+    y = torch.empty(M, h, device=dev, dtype=bf)
+    mean = torch.empty(M, device=dev)
+    rstd = torch.empty(M, device=dev)
+    ln = m.backbone[0].mlp[1]
+    ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+    drop = L.make_dropout(0.1, 1, 0, 7, 0, ctr)
+    out["ln_act_fwd (res, drop)"] = timed(lambda: L.ln_act_fwd(X, ln.weight, ln.bias, X, y, mean, rstd, drop))
+    dres = torch.randn(M, h, device=dev)
+    pb = torch.empty(L.ln_act_bwd_partials(M, h), device=dev)
+    dgam = torch.empty(h, device=dev)
+    dbet = torch.empty(h, device=dev)
+    out["ln_act_bwd (res, p, drop)"] = timed(lambda: L.ln_act_bwd(dres, X, X, mean, rstd, ln.weight, ln.bias, G, dres, pb,
+                                                                  dgam, dbet, drop))
+    for k, v in out.items():
+        print(f"{k:40s} {v:9.1f} us")
+
+
+if __name__ == "__main__":
+    main()
