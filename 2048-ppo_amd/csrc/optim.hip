@@ -4,7 +4,7 @@
 //
 //   grad_norm_kernel     ||g|| over the flat gradient bucket and the clip coefficient
 //                        min(max_norm / (||g|| + 1e-6), 1) into device scalars
-//   muon_kernel          one 256-thread block per weight matrix: momentum + nesterov, bf16 cast,
+//   muon_kernel          one 512-thread block per weight matrix: momentum + nesterov, bf16 cast,
 //                        Frobenius normalisation, the 5 Newton-Schulz iterations
 //                            G = X X^T;  U = b G + c G G;  X = a X + U X
 //                        entirely in LDS on bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulate,
@@ -29,14 +29,17 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float bf2f(uint32_t b) { return __uint_as_float(b << 16); }
 
-__device__ __forceinline__ uint32_t f2bf(float f) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7FFFFFFFu) > 0x7F800000u) return 0x7FC0u;
-    u += 0x7FFFu + ((u >> 16) & 1u);
-    return u >> 16;
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// round-to-nearest-even float -> bf16 on the hardware converter (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+    const bf16x2_t v = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
 }
 
-__device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+__device__ __forceinline__ uint32_t f2bf(float f) { return pack_bf2(f, 0.0f) & 0xFFFFu; }
+
+__device__ __forceinline__ float round_bf(float f) { return (float)(__bf16)f; }
 
 // ------------------------------------------------------------------ gradient norm ------------
 constexpr int kNormThreads = 1024;
@@ -61,10 +64,10 @@ __global__ __launch_bounds__(kNormThreads) void grad_norm_kernel(const float *__
 }
 
 // ------------------------------------------------------------------ Muon ---------------------
-constexpr int kMuonThreads = 256;        // 4 waves (one per SIMD, 512 registers), 2 x 2 tile blocks
-constexpr int kBI = 7, kBJ = 7;          // 16x16 tiles per wave: the block covers 224 x 224
+constexpr int kMuonThreads = 512;        // 8 waves, 2 (tile rows) x 4 (tile columns) blocks
+constexpr int kBI = 7, kBJ = 4;          // 16x16 tiles per wave: the block covers 224 x 256
 constexpr int kMuonMaxMats = 8;
-constexpr int kMuonLds = 160 * 1024 - 1024;
+constexpr int kMuonLds = 160 * 1024 - 256;  // minus the static red[] / s_norm
 
 struct MuonMat {
     float *param;
@@ -83,63 +86,67 @@ struct MuonArgs {
     const float *clip;
 };
 
-// A-operand style fragment: 8 consecutive k of one row of a row-major bf16 LDS matrix (pitch in
-// bytes); rows >= nrows and k >= K read as zero.
-__device__ __forceinline__ bf16x8_t row_frag(const char *base, int pitch, int row, int nrows, int k0, int K) {
-    uint4 w = make_uint4(0u, 0u, 0u, 0u);
-    if (row < nrows) {
-        const char *p = base + row * pitch + k0 * 2;
-        const uint2 lo = *reinterpret_cast<const uint2 *>(p);
-        const uint2 hi = *reinterpret_cast<const uint2 *>(p + 8);
-        w = make_uint4(lo.x, lo.y, hi.x, hi.y);
-        if (k0 + 8 > K) {  // K tail: zero the elements k >= K
-            const int valid = K - k0;  // < 8, may be <= 0
-            w.x = valid >= 2 ? w.x : (valid == 1 ? (w.x & 0xFFFFu) : 0u);
-            w.y = valid >= 4 ? w.y : (valid == 3 ? (w.y & 0xFFFFu) : 0u);
-            w.z = valid >= 6 ? w.z : (valid == 5 ? (w.z & 0xFFFFu) : 0u);
-            w.w = valid == 7 ? (w.w & 0xFFFFu) : 0u;
-        }
-    }
-    return __builtin_bit_cast(bf16x8_t, w);
-}
+// LDS images are row-major bf16 with the K dimension zero-padded to a multiple of 8 (pitch =
+// 2 * round8(cols) bytes, a multiple of 16), so a fragment is one aligned 16-byte read and every
+// out-of-range fragment is redirected to a zero block: the MFMA loops are branch-free per lane.
 
-// B-operand fragment of a row-major [K][N] bf16 LDS matrix via the transposing read: lane (g, i)
-// gets B[k0 + 8g + j][n0 + i]; rows >= K come from a zero row.
-__device__ __forceinline__ bf16x8_t col_frag(const char *base, int pitch, int k0, int K, int n0, const char *zero,
-                                             int lane) {
-    const int g = (lane >> 4) & 3, q = (lane >> 2) & 3, p = lane & 3;
-    const int r1 = k0 + 8 * g + q, r2 = r1 + 4;
-    const char *a1 = r1 < K ? base + r1 * pitch + (n0 + 4 * p) * 2 : zero;
-    const char *a2 = r2 < K ? base + r2 * pitch + (n0 + 4 * p) * 2 : zero;
-    const s16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)a1);
-    const s16x4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)a2);
-    return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(t1, t2, 0, 1, 2, 3, 4, 5, 6, 7));
-}
-
-// acc += A[M x K] B[K x N] over this wave's tile block.  A: rows of a row-major matrix.  B: either
-// given by the rows of B^T (BT_ROWS, so B[k][n] = Bt[n][k]) or row-major (transposing read).
-// The A fragments of a k-step stay in registers; B fragments are loaded one tile column at a time.
-template <bool BT_ROWS>
-__device__ __forceinline__ void gemm_block(f32x4_t (&acc)[kBI][kBJ], const char *A, int pa, const char *B, int pb,
-                                        int M, int N, int K, int ti0, int tj0, const char *zero, int lane) {
-    const int TI = (M + 15) >> 4, TJ = (N + 15) >> 4;
-    const int ni = min(kBI, TI - ti0), nj = min(kBJ, TJ - tj0);  // wave-uniform
-    if (ni <= 0 || nj <= 0) return;
-    for (int k0 = 0; k0 < K; k0 += 32) {
-        const int kl = k0 + 8 * (lane >> 4);
-        bf16x8_t fa[kBI];
+// acc += A[M x K] B[K x N] over this wave's tile block (ti0, tj0: wave-uniform).  B is given by
+// the rows of B^T (B[k][n] = Bt[n][k]).  A is read by rows (a_rows) or, for A = X^T of a
+// row-major X [K][M], with the transposing read.  kp = round8(K) = the padded K of row images.
+// One copy of this loop serves all three Newton-Schulz products (a_rows is wave-uniform): the
+// kernel has to fit the instruction cache, unrolled per product it does not.
+__device__ __forceinline__ void gemm_block(f32x4_t (&acc)[kBI][kBJ], const char *A, int pa, bool a_rows,
+                                           const char *B, int pb, int M, int N, int K, int ti0, int tj0,
+                                           const char *zero, int lane) {
+    const int TI = (M + 15) >> 4, TJ = (N + 15) >> 4, kp = (K + 7) & ~7;
+    if (ti0 >= TI || tj0 >= TJ) return;  // wave-uniform: nothing of this wave's block is in range
+    // Per-lane row offsets are fixed for the whole product (-1: out of range -> zero block).
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    int boff[kBJ], aoff[kBI];
 #pragma unroll
-        for (int i = 0; i < kBI; i++)
-            if (i < ni) fa[i] = row_frag(A, pa, 16 * (ti0 + i) + (lane & 15), M, kl, K);
+    for (int j = 0; j < kBJ; j++) {
+        const int row = 16 * (tj0 + j) + (lane & 15);
+        boff[j] = row < N ? row * pb : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < kBI; i++) {
+        const int row = 16 * (ti0 + i) + (lane & 15);
+        aoff[i] = a_rows ? (row < M ? row * pa : -1) : (16 * (ti0 + i) + 4 * p) * 2;  // col bytes for tr reads
+    }
+    // Every MFMA of the block is issued unconditionally (out-of-range tiles multiply zero fragments
+    // and are never stored): a guarded MFMA makes the compiler copy its accumulator out and wait
+    // for it, serialising the whole loop.
+    for (int k0 = 0; k0 < kp; k0 += 32) {
+        const int kl = k0 + 8 * g;
+        const bool kin = kl < kp;
+        bf16x8_t fb[kBJ], fa[kBI];
 #pragma unroll
         for (int j = 0; j < kBJ; j++) {
-            if (j >= nj) break;
-            const bf16x8_t fb = BT_ROWS ? row_frag(B, pb, 16 * (tj0 + j) + (lane & 15), N, kl, K)
-                                        : col_frag(B, pb, k0, K, 16 * (tj0 + j), zero, lane);
-#pragma unroll
-            for (int i = 0; i < kBI; i++)
-                if (i < ni) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc[i][j], 0, 0, 0);
+            const char *pp = (kin && boff[j] >= 0) ? B + boff[j] + 2 * kl : zero;
+            fb[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(pp));
         }
+        if (a_rows) {
+#pragma unroll
+            for (int i = 0; i < kBI; i++) {
+                const char *pp = (kin && aoff[i] >= 0) ? A + aoff[i] + 2 * kl : zero;
+                fa[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(pp));
+            }
+        } else {  // A = X^T: lane (g, i) needs X[k0 + 8g + j][m0 + i], two transposing reads
+            const int r1 = k0 + 8 * g + q, r2 = r1 + 4;
+            const char *b1 = A + r1 * pa, *b2 = A + r2 * pa;
+#pragma unroll
+            for (int i = 0; i < kBI; i++) {
+                const char *a1 = r1 < K ? b1 + aoff[i] : zero;
+                const char *a2 = r2 < K ? b2 + aoff[i] : zero;
+                const s16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)a1);
+                const s16x4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)a2);
+                fa[i] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(t1, t2, 0, 1, 2, 3, 4, 5, 6, 7));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < kBI; i++)
+#pragma unroll
+            for (int j = 0; j < kBJ; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
 }
 
@@ -150,28 +157,91 @@ __device__ __forceinline__ void zero_acc(f32x4_t (&acc)[kBI][kBJ]) {
         for (int j = 0; j < kBJ; j++) acc[i][j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
 }
 
-// out[row][col] (row-major bf16, pitch) = round_bf(alpha * acc + beta * prev[row][col]) for the
-// tile block; prev may alias out (read here, by the same lane, before the write -- callers put a
-// barrier between the GEMM's last operand read and this).
-__device__ __forceinline__ void store_block(const f32x4_t (&acc)[kBI][kBJ], char *out, int pitch, int M, int N,
-                                            int ti0, int tj0, float alpha, float beta, int lane) {
+// Stores the TRANSPOSE of the accumulated block: out[col][row] = bf16(alpha * acc[row][col] +
+// beta * out[col][row]) for cols < N and rows < round4(M).  A lane holds 4 consecutive rows of one
+// column, i.e. 4 consecutive elements of one output row: one 8-byte LDS read-modify-write.  Rows
+// M .. round4(M)-1 land in the zero K padding and are zero (their operands are zero fragments).
+// Callers put a barrier between the GEMM's last read of `out` and this.
+__device__ __forceinline__ void store_block_t(const f32x4_t (&acc)[kBI][kBJ], char *out, int pitch, int M, int N,
+                                              int ti0, int tj0, float alpha, float beta, int lane) {
     const int TI = (M + 15) >> 4, TJ = (N + 15) >> 4;
+    if (ti0 >= TI || tj0 >= TJ) return;
 #pragma unroll
     for (int i = 0; i < kBI; i++)
 #pragma unroll
         for (int j = 0; j < kBJ; j++) {
-            if (ti0 + i >= TI || tj0 + j >= TJ) continue;
             const int col = 16 * (tj0 + j) + (lane & 15);
-            if (col >= N) continue;
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int row = 16 * (ti0 + i) + 4 * (lane >> 4) + r;
-                if (row >= M) continue;
-                uint16_t *p = reinterpret_cast<uint16_t *>(out + row * pitch) + col;
-                const float prev = beta != 0.0f ? bf2f(*p) : 0.0f;
-                *p = (uint16_t)f2bf(alpha * acc[i][j][r] + beta * prev);
+            const int row0 = 16 * (ti0 + i) + 4 * (lane >> 4);
+            if (col < N && row0 < M) {
+                uint2 *p = reinterpret_cast<uint2 *>(out + col * pitch + row0 * 2);
+                const uint2 q = *p;
+                const float v0 = alpha * acc[i][j][0] + beta * bf2f(q.x & 0xFFFFu);
+                const float v1 = alpha * acc[i][j][1] + beta * bf2f(q.x >> 16);
+                const float v2 = alpha * acc[i][j][2] + beta * bf2f(q.y & 0xFFFFu);
+                const float v3 = alpha * acc[i][j][3] + beta * bf2f(q.y >> 16);
+                *p = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
             }
         }
+}
+
+// momentum + nesterov + bf16 cast (+ transpose) of the gradient into the LDS image X; returns the
+// thread's sum of squares of the bf16 values.  Separate function so the restrict qualifiers let the
+// compiler overlap the iterations' loads with the previous stores.
+__device__ __forceinline__ float muon_prologue(const float *__restrict__ grad, float *__restrict__ mom, char *sX,
+                                               int px, int R, int C, bool tr, float coef, float mu, bool nesterov,
+                                               int tid) {
+    const int n4 = (R * C) >> 2;
+    float ss = 0.0f;
+#pragma unroll 4
+    for (int e4 = tid; e4 < n4; e4 += kMuonThreads) {
+        const float4 g4 = reinterpret_cast<const float4 *>(grad)[e4];
+        const float4 b4 = reinterpret_cast<const float4 *>(mom)[e4];
+        const float gv[4] = {g4.x * coef, g4.y * coef, g4.z * coef, g4.w * coef};
+        float bv[4] = {b4.x, b4.y, b4.z, b4.w};
+        const int i = (4 * e4) / C, j0 = 4 * e4 - i * C;  // C % 4 == 0: a float4 stays in one row
+        float ub[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            bv[u] = bv[u] + (1.0f - mu) * (gv[u] - bv[u]);                               // buf.lerp_(g, 1 - mu)
+            const float up = nesterov ? bv[u] - (bv[u] - gv[u]) * (1.0f - mu) : bv[u];  // g.lerp(buf, mu)
+            ub[u] = round_bf(up);
+            ss += ub[u] * ub[u];
+        }
+        if (tr) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) reinterpret_cast<uint16_t *>(sX + (j0 + u) * px)[i] = (uint16_t)f2bf(ub[u]);
+        } else {
+            *reinterpret_cast<uint2 *>(sX + i * px + 2 * j0) = make_uint2(pack_bf2(ub[0], ub[1]), pack_bf2(ub[2], ub[3]));
+        }
+        reinterpret_cast<float4 *>(mom)[e4] = make_float4(bv[0], bv[1], bv[2], bv[3]);
+    }
+    return ss;
+}
+
+__device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_t *__restrict__ pbf, const char *sX,
+                                              int px, int R, int C, bool tr, float decay, float step, int tid) {
+    const int n4 = (R * C) >> 2;
+#pragma unroll 4
+    for (int e4 = tid; e4 < n4; e4 += kMuonThreads) {
+        const float4 p4 = reinterpret_cast<const float4 *>(param)[e4];
+        float pv[4] = {p4.x, p4.y, p4.z, p4.w};
+        const int i = (4 * e4) / C, j0 = 4 * e4 - i * C;
+        float x[4];
+        if (tr) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) x[u] = bf2f(reinterpret_cast<const uint16_t *>(sX + (j0 + u) * px)[i]);
+        } else {
+            const uint2 w = *reinterpret_cast<const uint2 *>(sX + i * px + 2 * j0);
+            x[0] = bf2f(w.x & 0xFFFFu);
+            x[1] = bf2f(w.x >> 16);
+            x[2] = bf2f(w.y & 0xFFFFu);
+            x[3] = bf2f(w.y >> 16);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) pv[u] = pv[u] * decay - x[u] * step;
+        reinterpret_cast<float4 *>(param)[e4] = make_float4(pv[0], pv[1], pv[2], pv[3]);
+        if (pbf) reinterpret_cast<uint2 *>(pbf)[e4] = make_uint2(pack_bf2(pv[0], pv[1]), pack_bf2(pv[2], pv[3]));
+    }
 }
 
 __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
@@ -180,32 +250,23 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     const int R = mt.rows, C = mt.cols;
     const bool tr = R > C;  // iterate on the wide orientation (r <= c), like torch
     const int r = tr ? C : R, c = tr ? R : C;
-    const int px = c * 2, pg = r * 2;  // row pitches (bytes), multiples of 8 since r, c % 4 == 0
+    const int px = ((c + 7) & ~7) * 2, pg = ((r + 7) & ~7) * 2;  // padded row pitches (bytes)
     char *sX = smem;
     char *sG = smem + ((r * px + 127) & ~127);
-    char *zero = sG + ((r * pg + 127) & ~127);  // 64 zero bytes (+ slack for tail reads)
+    char *zero = sG + ((r * pg + 127) & ~127);  // 64 zero bytes
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ti0 = (wave & 1) * kBI, tj0 = (wave >> 1) * kBJ;  // wave-uniform
     __shared__ float red[kMuonThreads / 64];
     __shared__ float s_norm;
-    if (tid < 64) reinterpret_cast<uint32_t *>(zero)[tid] = 0u;
-
-    // momentum + nesterov + bf16 cast (+ transpose) into sX; sum of squares of the bf16 values
-    const float coef = args.clip ? *args.clip : 1.0f;
-    const float mu = args.momentum;
-    float ss = 0.0f;
-    for (int e = tid; e < R * C; e += kMuonThreads) {
-        const float g = mt.grad[e] * coef;
-        float buf = mt.mom[e];
-        buf = buf + (1.0f - mu) * (g - buf);                      // buf.lerp_(g, 1 - mu)
-        mt.mom[e] = buf;
-        const float u = args.nesterov ? buf - (buf - g) * (1.0f - mu) : buf;  // g.lerp(buf, mu)
-        const float ub = round_bf(u);
-        ss += ub * ub;
-        const int i = e / C, j = e - i * C;
-        const int xr = tr ? j : i, xc = tr ? i : j;
-        reinterpret_cast<uint16_t *>(sX + xr * px)[xc] = (uint16_t)f2bf(ub);
+    // zero both images (their K padding must read as zero) and the zero block
+    {
+        const int bytes = (int)(zero - smem) + 64;
+        for (int o = tid * 16; o < bytes; o += kMuonThreads * 16) *reinterpret_cast<uint4 *>(smem + o) = make_uint4(0, 0, 0, 0);
     }
+    __syncthreads();
+
+    const float coef = args.clip ? *args.clip : 1.0f;
+    float ss = muon_prologue(mt.grad, mt.mom, sX, px, R, C, tr, coef, args.momentum, args.nesterov != 0, tid);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
     if (lane == 0) red[wave] = ss;
@@ -217,46 +278,43 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     }
     __syncthreads();
     const float nrm = s_norm;
-    for (int e = tid; e < r * c; e += kMuonThreads) {
-        const int i = e / c, j = e - i * c;
-        uint16_t *p = reinterpret_cast<uint16_t *>(sX + i * px) + j;
-        *p = (uint16_t)f2bf(bf2f(*p) / nrm);
+    // X /= ||X|| over the flat image (the zero padding stays zero): 4 elements per access
+    for (int e4 = tid; e4 < (r * px) >> 3; e4 += kMuonThreads) {
+        uint2 *p = reinterpret_cast<uint2 *>(sX) + e4;
+        const uint2 w = *p;
+        *p = make_uint2(pack_bf2(bf2f(w.x & 0xFFFFu) / nrm, bf2f(w.x >> 16) / nrm),
+                        pack_bf2(bf2f(w.y & 0xFFFFu) / nrm, bf2f(w.y >> 16) / nrm));
     }
     __syncthreads();
 
+    // Newton-Schulz, three products per iteration, all through ONE gemm/store code path:
+    //   0: G = X X^T                      (A = X rows, B^T = X rows; G symmetric)
+    //   1: U = b G + c G G                (A = G rows, B^T = G rows; U symmetric)
+    //   2: X^T = a X^T + X^T U            (A = X^T by the transposing read, B^T = U rows)
+    // Every product stores its transpose (= G, U, and X itself for phase 2).
     f32x4_t acc[kBI][kBJ];
-    for (int it = 0; it < args.steps; it++) {
-        // G = X X^T
+    for (int ph = 0; ph < 3 * args.steps; ph++) {
+        const int k = ph % 3;
+        const char *A = k == 1 ? sG : sX;
+        const int pa = k == 1 ? pg : px;
+        const char *B = k == 0 ? sX : sG;
+        const int pb = k == 0 ? px : pg;
+        const int M = k == 2 ? c : r, N = r, K = k == 0 ? c : r;
+        char *out = k == 2 ? sX : sG;
+        const int po = k == 2 ? px : pg;
+        const float alpha = k == 1 ? args.c : 1.0f;
+        const float beta = k == 0 ? 0.0f : (k == 1 ? args.b : args.a);
         zero_acc(acc);
-        gemm_block<true>(acc, sX, px, sX, px, r, r, c, ti0, tj0, zero, lane);
-        store_block(acc, sG, pg, r, r, ti0, tj0, 1.0f, 0.0f, lane);  // sG is free (last read before a barrier)
+        gemm_block(acc, A, pa, k != 2, B, pb, M, N, K, ti0, tj0, zero, lane);
         __syncthreads();
-        // U = b G + c G G   (G symmetric: G[k][n] = G[n][k], read by rows)
-        zero_acc(acc);
-        gemm_block<true>(acc, sG, pg, sG, pg, r, r, r, ti0, tj0, zero, lane);
-        __syncthreads();
-        store_block(acc, sG, pg, r, r, ti0, tj0, args.c, args.b, lane);
-        __syncthreads();
-        // X = a X + U X
-        zero_acc(acc);
-        gemm_block<false>(acc, sG, pg, sX, px, r, c, r, ti0, tj0, zero, lane);
-        __syncthreads();
-        store_block(acc, sX, px, r, c, ti0, tj0, 1.0f, args.a, lane);
+        store_block_t(acc, out, po, M, N, ti0, tj0, alpha, beta, lane);
         __syncthreads();
     }
 
     // decoupled weight decay + the match_rms_adamw-scaled update, and the bf16 weight copy
     const float lr = args.lr[mt.lr_index];
     const float step = lr * (0.2f * sqrtf((float)(R > C ? R : C)));
-    const float decay = 1.0f - lr * args.wd;
-    for (int e = tid; e < R * C; e += kMuonThreads) {
-        const int i = e / C, j = e - i * C;
-        const int xr = tr ? j : i, xc = tr ? i : j;
-        const float x = bf2f(reinterpret_cast<const uint16_t *>(sX + xr * px)[xc]);
-        const float p = mt.param[e] * decay - x * step;
-        mt.param[e] = p;
-        if (mt.pbf) mt.pbf[e] = (uint16_t)f2bf(p);
-    }
+    muon_epilogue(mt.param, mt.pbf, sX, px, R, C, tr, 1.0f - lr * args.wd, step, tid);
 }
 
 // ------------------------------------------------------------------ AdamW --------------------
@@ -307,7 +365,8 @@ inline int status() {
 
 inline size_t muon_lds_bytes(int R, int C) {
     const int r = R > C ? C : R, c = R > C ? R : C;
-    return (size_t)((r * c * 2 + 127) & ~127) + (size_t)((r * r * 2 + 127) & ~127) + 1024;
+    const int px = ((c + 7) & ~7) * 2, pg = ((r + 7) & ~7) * 2;
+    return (size_t)((r * px + 127) & ~127) + (size_t)((r * pg + 127) & ~127) + 64;
 }
 
 }  // namespace
@@ -325,8 +384,8 @@ int g2048_grad_clip(g2048_stream_t stream, const float *grad, int64_t n, float m
 int g2048_muon_supported(int32_t rows, int32_t cols) {
     if (rows <= 0 || cols <= 0) return 0;
     const int r = rows > cols ? cols : rows, c = rows > cols ? rows : cols;
-    if (c % 4 || (r % 4 && r != 1)) return 0;  // 8-byte LDS row pitches (a single row needs none)
-    if (r > 16 * 2 * kBI || c > 16 * 2 * kBJ) return 0;
+    if (cols % 4) return 0;  // the element passes read float4s within a row
+    if (r > 16 * 2 * kBI || c > 16 * 4 * kBJ) return 0;
     return muon_lds_bytes(rows, cols) <= (size_t)kMuonLds ? 1 : 0;
 }
 
@@ -338,6 +397,8 @@ int g2048_muon_step(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_
     for (int i = 0; i < count; i++) {
         const g2048_muon_matrix &m = mats[i];
         if (!m.param || !m.grad || !m.momentum || !g2048_muon_supported(m.rows, m.cols)) return G2048_EINVAL;
+        if (((uintptr_t)m.param | (uintptr_t)m.grad | (uintptr_t)m.momentum) % 16 || (uintptr_t)m.param_bf16 % 8)
+            return G2048_EINVAL;
         a.m[i] = MuonMat{m.param, m.grad, m.momentum, m.param_bf16, m.rows, m.cols, m.lr_index, 0};
         const size_t b = muon_lds_bytes(m.rows, m.cols);
         lds = b > lds ? b : lds;

@@ -128,8 +128,8 @@ typedef struct g2048_muon_cfg {
     int32_t ns_steps, nesterov;
 } g2048_muon_cfg;
 
-/* 1 if a [rows, cols] matrix fits the one-block-per-matrix Newton-Schulz kernel (min dim <= 224,
- * max dim <= 224, both LDS images <= ~159 KB: h <= 196 for square weights). */
+/* 1 if a [rows, cols] matrix fits the one-block-per-matrix Newton-Schulz kernel (cols % 4 == 0,
+ * min dim <= 224, max dim <= 256, both LDS images <= ~159 KB: h <= 196 for square weights). */
 int g2048_muon_supported(int32_t rows, int32_t cols);
 
 /* Muon step of up to 8 matrices, all concurrently: momentum (nesterov), Newton-Schulz

@@ -406,7 +406,7 @@ def test_fused_muon_adamw_matches_torch_ops_step(dev, h):
 def test_fused_muon_supported_shapes():
     from g2048 import _lib as L
     assert L.muon_supported(196, 196) and L.muon_supported(196, 48) and L.muon_supported(4, 196)
-    assert L.muon_supported(1, 196) and L.muon_supported(64, 64)
+    assert L.muon_supported(1, 196) and L.muon_supported(64, 64) and L.muon_supported(6, 196)
     assert not L.muon_supported(256, 256) and not L.muon_supported(196, 6)
 
 
