@@ -2,7 +2,7 @@
 // Muon for the 2-D weights, AdamW for the 1-D LayerNorm / bias parameters; torch.optim.Muon with
 // adjust_lr_fn="match_rms_adamw", nesterov, 5 Newton-Schulz steps in bf16) as three launches:
 //
-//   grad_norm_kernel     ||g|| over the flat gradient bucket and the clip coefficient
+//   grad_sumsq/norm      ||g|| over the flat gradient bucket and the clip coefficient
 //                        min(max_norm / (||g|| + 1e-6), 1) into device scalars
 //   muon_kernel          one 512-thread block per weight matrix: momentum + nesterov, bf16 cast,
 //                        Frobenius normalisation, the 5 Newton-Schulz iterations
@@ -42,22 +42,34 @@ __device__ __forceinline__ uint32_t f2bf(float f) { return pack_bf2(f, 0.0f) & 0
 __device__ __forceinline__ float round_bf(float f) { return (float)(__bf16)f; }
 
 // ------------------------------------------------------------------ gradient norm ------------
-constexpr int kNormThreads = 1024;
+// Two deterministic stages: kNormBlocks partial sums of squares, then one block sums them in order.
+constexpr int kNormBlocks = 64;
 
-__global__ __launch_bounds__(kNormThreads) void grad_norm_kernel(const float *__restrict__ g, int64_t n, float max_norm,
-                                                                 float *__restrict__ norm_out,
-                                                                 float *__restrict__ coef_out) {
-    __shared__ float red[kNormThreads / 64];
+__global__ __launch_bounds__(256) void grad_sumsq_kernel(const float *__restrict__ g, int64_t n,
+                                                         float *__restrict__ part) {
+    __shared__ float red[4];
     float s = 0.0f;
-    for (int64_t i = threadIdx.x; i < n; i += kNormThreads) s += g[i] * g[i];
+    const int64_t n4 = n >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)kNormBlocks * 256) {
+        const float4 v = reinterpret_cast<const float4 *>(g)[i];
+        s += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+    }
+    if (blockIdx.x == 0)
+        for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += 256) s += g[i] * g[i];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(64) void grad_norm_kernel(const float *__restrict__ part, float max_norm,
+                                                       float *__restrict__ norm_out, float *__restrict__ coef_out) {
+    float s = part[threadIdx.x];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
     if (threadIdx.x == 0) {
-        float t = 0.0f;
-        for (int w = 0; w < kNormThreads / 64; w++) t += red[w];
-        const float nrm = sqrtf(t);
+        const float nrm = sqrtf(s);
         *norm_out = nrm;
         *coef_out = fminf(max_norm / (nrm + 1e-6f), 1.0f);
     }
@@ -374,10 +386,11 @@ inline size_t muon_lds_bytes(int R, int C) {
 extern "C" {
 
 int g2048_grad_clip(g2048_stream_t stream, const float *grad, int64_t n, float max_norm, float *norm_out,
-                    float *coef_out) {
-    if (!grad || !norm_out || !coef_out || n <= 0) return G2048_EINVAL;
-    hipLaunchKernelGGL(grad_norm_kernel, dim3(1), dim3(kNormThreads), 0, (hipStream_t)stream, grad, n, max_norm,
-                       norm_out, coef_out);
+                    float *coef_out, float *partials) {
+    if (!grad || !norm_out || !coef_out || !partials || n <= 0 || ((uintptr_t)grad & 15u)) return G2048_EINVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(grad_sumsq_kernel, dim3(kNormBlocks), dim3(256), 0, s, grad, n, partials);
+    hipLaunchKernelGGL(grad_norm_kernel, dim3(1), dim3(kNormBlocks), 0, s, partials, max_norm, norm_out, coef_out);
     return status();
 }
 

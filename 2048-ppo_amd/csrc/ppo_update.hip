@@ -113,12 +113,16 @@ __global__ __launch_bounds__(256) void obs_gather_kernel(const int8_t *__restric
 }
 
 // ------------------------------------------------------------------ LayerNorm forward --------
+// RPW rows per wave and iteration: their loads are all in flight before the first reduction.
+constexpr int kFwdRows = 4;
+
 template <int J, bool DROP>
 __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(const uint16_t *__restrict__ g, const float *__restrict__ gamma,
                                                           const float *__restrict__ beta,
                                                           const uint16_t *__restrict__ res, uint16_t *__restrict__ y,
                                                           float *__restrict__ mean_out, float *__restrict__ rstd_out,
                                                           int64_t m, int h, DropArgs da) {
+    constexpr int RPW = kFwdRows;
     const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * kWaves;
     const Drop d = make_drop(da);
@@ -135,46 +139,63 @@ __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(const uint16_t *__rest
         }
     }
     const float inv_h = 1.0f / (float)h;
-    for (int64_t r = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); r < m; r += nw) {
-        float x[J][4];
-        float s = 0.0f;
+    for (int64_t r0 = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * RPW; r0 < m; r0 += nw * RPW) {
+        float x[RPW][J][4], rs[RPW][J][4];
+        float s[RPW], v[RPW], mean[RPW], rstd[RPW];
 #pragma unroll
-        for (int j = 0; j < J; j++) {
-            if (ok[j]) {
-                load_bf4(g + r * h + 4 * (lane + 64 * j), x[j]);
-            } else {
-                x[j][0] = x[j][1] = x[j][2] = x[j][3] = 0.0f;
+        for (int q = 0; q < RPW; q++) {
+            const int64_t r = r0 + q;
+            s[q] = 0.0f;
+#pragma unroll
+            for (int j = 0; j < J; j++) {
+                const int c = 4 * (lane + 64 * j);
+                if (ok[j] && r < m) {
+                    load_bf4(g + r * h + c, x[q][j]);
+                    if (res) load_bf4(res + r * h + c, rs[q][j]);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; u++) x[q][j][u] = rs[q][j][u] = 0.0f;
+                }
+                s[q] += (x[q][j][0] + x[q][j][1]) + (x[q][j][2] + x[q][j][3]);
             }
-            s += (x[j][0] + x[j][1]) + (x[j][2] + x[j][3]);
         }
-        const float mean = wave_sum(s) * inv_h;
-        float v = 0.0f;
 #pragma unroll
-        for (int j = 0; j < J; j++)
+        for (int q = 0; q < RPW; q++) mean[q] = wave_sum(s[q]) * inv_h;
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const float t = ok[j] ? x[j][u] - mean : 0.0f;
-                v += t * t;
-            }
-        const float rstd = 1.0f / sqrtf(wave_sum(v) * inv_h + kLnEps);
+        for (int q = 0; q < RPW; q++) {
+            v[q] = 0.0f;
 #pragma unroll
-        for (int j = 0; j < J; j++) {
-            if (!ok[j]) continue;
-            const int c = 4 * (lane + 64 * j);
-            float o[4], k[4], rs[4];
-            if (DROP) drop_mult(d, (uint32_t)r, (uint32_t)(lane + 64 * j), k);
-            if (res) load_bf4(res + r * h + c, rs);
+            for (int j = 0; j < J; j++)
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                float a = fmaxf((x[j][u] - mean) * rstd * gm[j][u] + bt[j][u], 0.0f);
-                if (DROP) a *= k[u];
-                o[u] = res ? rs[u] + a : a;
-            }
-            store_bf4(y + r * h + c, o);
+                for (int u = 0; u < 4; u++) {
+                    const float t = ok[j] ? x[q][j][u] - mean[q] : 0.0f;
+                    v[q] += t * t;
+                }
         }
-        if (lane == 0) {
-            mean_out[r] = mean;
-            rstd_out[r] = rstd;
+#pragma unroll
+        for (int q = 0; q < RPW; q++) rstd[q] = 1.0f / sqrtf(wave_sum(v[q]) * inv_h + kLnEps);
+#pragma unroll
+        for (int q = 0; q < RPW; q++) {
+            const int64_t r = r0 + q;
+            if (r >= m) break;
+#pragma unroll
+            for (int j = 0; j < J; j++) {
+                if (!ok[j]) continue;
+                const int c = 4 * (lane + 64 * j);
+                float o[4], k[4];
+                if (DROP) drop_mult(d, (uint32_t)r, (uint32_t)(lane + 64 * j), k);
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    float a = fmaxf((x[q][j][u] - mean[q]) * rstd[q] * gm[j][u] + bt[j][u], 0.0f);
+                    if (DROP) a *= k[u];
+                    o[u] = res ? rs[q][j][u] + a : a;
+                }
+                store_bf4(y + r * h + c, o);
+            }
+            if (lane == 0) {
+                mean_out[r] = mean[q];
+                rstd_out[r] = rstd[q];
+            }
         }
     }
 }
@@ -182,12 +203,15 @@ __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(const uint16_t *__rest
 // ------------------------------------------------------------------ LayerNorm backward -------
 // Block partials: part[blockIdx][0:h] = sum dz*xhat (dgamma), part[blockIdx][h:2h] = sum dz (dbeta).
 // dres_out may alias dres_in (each element is read, then written, by the same lane).
+constexpr int kBwdRows = 2;
+
 template <int J, bool DROP>
 __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
     const float *dres_in, const uint16_t *__restrict__ p_in, const uint16_t *__restrict__ g,
     const float *__restrict__ mean_in, const float *__restrict__ rstd_in, const float *__restrict__ gamma,
     const float *__restrict__ beta, uint16_t *__restrict__ dg, float *dres_out, float *__restrict__ part,
     int64_t m, int h, DropArgs da) {
+    constexpr int RPW = kBwdRows;
     extern __shared__ float lds[];  // [kWaves][2h]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t nw = (int64_t)gridDim.x * kWaves;
@@ -206,55 +230,83 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
         }
     }
     const float inv_h = 1.0f / (float)h;
-    for (int64_t r = (int64_t)blockIdx.x * kWaves + wave; r < m; r += nw) {
-        const float mean = mean_in[r], rstd = rstd_in[r];
-        float xh[J][4], dxh[J][4];
-        float s1 = 0.0f, s2 = 0.0f;
+    for (int64_t r0 = ((int64_t)blockIdx.x * kWaves + wave) * RPW; r0 < m; r0 += nw * RPW) {
+        float x[RPW][J][4], dy[RPW][J][4], xh[RPW][J][4], dxh[RPW][J][4];
+        float mean[RPW], rstd[RPW], s1[RPW], s2[RPW];
 #pragma unroll
-        for (int j = 0; j < J; j++) {
-            if (!ok[j]) {
+        for (int q = 0; q < RPW; q++) {
+            const int64_t r = r0 + q;
+            const bool rv = r < m;
+            mean[q] = rv ? mean_in[r] : 0.0f;
+            rstd[q] = rv ? rstd_in[r] : 0.0f;
 #pragma unroll
-                for (int u = 0; u < 4; u++) xh[j][u] = dxh[j][u] = 0.0f;
-                continue;
-            }
-            const int c = 4 * (lane + 64 * j);
-            float x[4], dy[4] = {0.0f, 0.0f, 0.0f, 0.0f}, k[4];
-            load_bf4(g + r * h + c, x);
-            if (dres_in) {
-                const float4 t = *reinterpret_cast<const float4 *>(dres_in + r * h + c);
-                dy[0] = t.x; dy[1] = t.y; dy[2] = t.z; dy[3] = t.w;
-            }
-            if (p_in) {
-                float t[4];
-                load_bf4(p_in + r * h + c, t);
+            for (int j = 0; j < J; j++) {
+                const int c = 4 * (lane + 64 * j);
 #pragma unroll
-                for (int u = 0; u < 4; u++) dy[u] += t[u];
-            }
-            if (dres_out) *reinterpret_cast<float4 *>(dres_out + r * h + c) = make_float4(dy[0], dy[1], dy[2], dy[3]);
-            if (DROP) drop_mult(d, (uint32_t)r, (uint32_t)(lane + 64 * j), k);
+                for (int u = 0; u < 4; u++) x[q][j][u] = dy[q][j][u] = 0.0f;
+                if (!(ok[j] && rv)) continue;
+                load_bf4(g + r * h + c, x[q][j]);
+                if (dres_in) {
+                    const float4 t = *reinterpret_cast<const float4 *>(dres_in + r * h + c);
+                    dy[q][j][0] = t.x;
+                    dy[q][j][1] = t.y;
+                    dy[q][j][2] = t.z;
+                    dy[q][j][3] = t.w;
+                }
+                if (p_in) {
+                    float t[4];
+                    load_bf4(p_in + r * h + c, t);
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const float xhat = (x[u] - mean) * rstd;
-                const float z = xhat * gm[j][u] + bt[j][u];
-                float dz = z > 0.0f ? dy[u] : 0.0f;
-                if (DROP) dz *= k[u];
-                ag[j][u] += dz * xhat;
-                ab[j][u] += dz;
-                xh[j][u] = xhat;
-                dxh[j][u] = dz * gm[j][u];
-                s1 += dxh[j][u];
-                s2 += dxh[j][u] * xhat;
+                    for (int u = 0; u < 4; u++) dy[q][j][u] += t[u];
+                }
             }
         }
-        s1 = wave_sum(s1) * inv_h;
-        s2 = wave_sum(s2) * inv_h;
 #pragma unroll
-        for (int j = 0; j < J; j++) {
-            if (!ok[j]) continue;
-            float o[4];
+        for (int q = 0; q < RPW; q++) {
+            const int64_t r = r0 + q;
+            const bool rv = r < m;
+            s1[q] = s2[q] = 0.0f;
 #pragma unroll
-            for (int u = 0; u < 4; u++) o[u] = rstd * (dxh[j][u] - s1 - xh[j][u] * s2);
-            store_bf4(dg + r * h + 4 * (lane + 64 * j), o);
+            for (int j = 0; j < J; j++) {
+                const bool live = ok[j] && rv;
+                const int c = 4 * (lane + 64 * j);
+                float k[4];
+                if (live && dres_out)
+                    *reinterpret_cast<float4 *>(dres_out + r * h + c) =
+                        make_float4(dy[q][j][0], dy[q][j][1], dy[q][j][2], dy[q][j][3]);
+                if (DROP) drop_mult(d, (uint32_t)r, (uint32_t)(lane + 64 * j), k);
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const float xhat = live ? (x[q][j][u] - mean[q]) * rstd[q] : 0.0f;
+                    const float z = xhat * gm[j][u] + bt[j][u];
+                    float dz = (live && z > 0.0f) ? dy[q][j][u] : 0.0f;
+                    if (DROP) dz *= k[u];
+                    ag[j][u] += dz * xhat;
+                    ab[j][u] += dz;
+                    xh[q][j][u] = xhat;
+                    dxh[q][j][u] = dz * gm[j][u];
+                    s1[q] += dxh[q][j][u];
+                    s2[q] += dxh[q][j][u] * xhat;
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < RPW; q++) {
+            s1[q] = wave_sum(s1[q]) * inv_h;
+            s2[q] = wave_sum(s2[q]) * inv_h;
+        }
+#pragma unroll
+        for (int q = 0; q < RPW; q++) {
+            const int64_t r = r0 + q;
+            if (r >= m) break;
+#pragma unroll
+            for (int j = 0; j < J; j++) {
+                if (!ok[j]) continue;
+                float o[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) o[u] = rstd[q] * (dxh[q][j][u] - s1[q] - xh[q][j][u] * s2[q]);
+                store_bf4(dg + r * h + 4 * (lane + 64 * j), o);
+            }
         }
     }
     // block reduction of the dgamma / dbeta accumulators
@@ -844,8 +896,8 @@ int g2048_ln_act_fwd(g2048_stream_t stream, const uint16_t *g, const float *gamm
     if (!g || !gamma || !beta || !y || !mean || !rstd || !al(g, 8) || !al(y, 8) || (res && !al(res, 8)))
         return G2048_EINVAL;
     const DropArgs da = drop_args(drop);
-    const int64_t blocks64 = (m + kWaves - 1) / kWaves;
-    const dim3 grid((unsigned)(blocks64 > 16384 ? 16384 : blocks64)), blk(kThreads);
+    const int64_t blocks64 = (m + kWaves * kFwdRows - 1) / (kWaves * kFwdRows);
+    const dim3 grid((unsigned)(blocks64 > 2048 ? 2048 : blocks64)), blk(kThreads);
     const hipStream_t s = (hipStream_t)stream;
     if (drop_on(drop))
         G2048_DISPATCH_J(h, hipLaunchKernelGGL((ln_fwd_kernel<J, true>), grid, blk, 0, s, g, gamma, beta, res, y, mean,

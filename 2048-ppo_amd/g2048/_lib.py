@@ -134,7 +134,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_dropout_mask": (ctypes.c_int, [vp, i64, i32, dp, vp]),
         "g2048_wgrad_partials": (sz, [i64, i32, i32]),
         "g2048_wgrad": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, vp, vp]),
-        "g2048_grad_clip": (ctypes.c_int, [vp, vp, i64, ctypes.c_float, vp, vp]),
+        "g2048_grad_clip": (ctypes.c_int, [vp, vp, i64, ctypes.c_float, vp, vp, vp]),
         "g2048_muon_supported": (ctypes.c_int, [i32, i32]),
         "g2048_muon_step": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.POINTER(MuonCfg)]),
         "g2048_adamw_step": (ctypes.c_int, [vp, ctypes.POINTER(AdamWGroup), i32, vp, vp, vp, ctypes.c_float,
@@ -354,10 +354,11 @@ def wgrad(a, b, partials, out):
 
 
 # ------------------------------------------------------------- optimizer step -------------------
-def grad_clip(grad, max_norm: float, norm_out, coef_out):
+def grad_clip(grad, max_norm: float, norm_out, coef_out, partials):
+    """partials: >= 64 float32 of scratch."""
     _check(load().g2048_grad_clip(_stream(grad), _dev(grad, torch.float32, "grad"), grad.numel(), float(max_norm),
-                                  _dev(norm_out, torch.float32, "norm_out"), _dev(coef_out, torch.float32, "coef_out")),
-           "g2048_grad_clip")
+                                  _dev(norm_out, torch.float32, "norm_out"), _dev(coef_out, torch.float32, "coef_out"),
+                                  _dev(partials, torch.float32, "partials")), "g2048_grad_clip")
 
 
 def muon_supported(rows: int, cols: int) -> bool:

@@ -212,6 +212,7 @@ class FusedMuonAdamW(MuonAdamW):
                           and all(p.ndim == 2 and L.muon_supported(*p.shape) for p, _ in self.muon))
         self.norm_t = torch.zeros((), dtype=torch.float32, device=self.dev)
         self.coef_t = torch.ones((), dtype=torch.float32, device=self.dev)
+        self.norm_part = torch.zeros(64, dtype=torch.float32, device=self.dev)
         self._bf16 = {}
         self._mats = self._groups = None
         self._cfg = L.MuonCfg(self.momentum, self.wd, self.ns[0], self.ns[1], self.ns[2], self.ns_eps, self.ns_steps,
@@ -259,7 +260,7 @@ class FusedMuonAdamW(MuonAdamW):
     def step_clipped(self, flat_grad: torch.Tensor, max_norm: float) -> torch.Tensor:
         """clip_grad_norm_(max_norm) folded into the step (the bucket itself is left unclipped);
         returns the pre-clip norm as a device scalar."""
-        self._L.grad_clip(flat_grad, max_norm, self.norm_t, self.coef_t)
+        self._L.grad_clip(flat_grad, max_norm, self.norm_t, self.coef_t, self.norm_part)
         self._run(self.coef_t)
         return self.norm_t
 

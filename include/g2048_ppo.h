@@ -108,9 +108,10 @@ int g2048_wgrad(g2048_stream_t stream, const uint16_t *a, const uint16_t *b, int
 /* ---- optimizer step (train.py:553-568, :1587-1612) ------------------------------------------ */
 
 /* clip_grad_norm_ of the flat gradient bucket, without touching it: norm_out = ||grad||,
- * coef_out = min(max_norm / (norm + 1e-6), 1) (device scalars read by the optimizer kernels). */
+ * coef_out = min(max_norm / (norm + 1e-6), 1) (device scalars read by the optimizer kernels).
+ * grad 16-byte aligned; partials: 64 floats of scratch. */
 int g2048_grad_clip(g2048_stream_t stream, const float *grad, int64_t n, float max_norm, float *norm_out,
-                    float *coef_out);
+                    float *coef_out, float *partials);
 
 /* One Muon-optimised weight matrix (torch.optim.Muon, adjust_lr_fn="match_rms_adamw"). */
 typedef struct g2048_muon_matrix {

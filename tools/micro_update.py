@@ -83,6 +83,33 @@ def main():
     dbet = torch.empty(h, device=dev)
     out["ln_act_bwd (res, p, drop)"] = timed(lambda: L.ln_act_bwd(dres, X, X, mean, rstd, ln.weight, ln.bias, G, dres, pb,
                                                                   dgam, dbet, drop))
+    from g2048.optim import FusedMuonAdamW
+    fo = FusedMuonAdamW(m, 1e-3, 1e-4)
+    from g2048.dist import GradBucket
+    order = [p for p, _ in fo.muon] + [p for grp in fo.adam_groups for p in grp["params"]]
+    bk = GradBucket(order)
+    bk.flat.normal_()
+    out["FusedMuonAdamW.step_clipped"] = timed(lambda: fo.step_clipped(bk.flat, 1.0), reps=10)
+    xa = torch.randn(M, h, device=dev, dtype=bf)
+    wa, ba, wv, bv = (torch.randn(4, h, device=dev) * 0.05, torch.zeros(4, device=dev), torch.randn(1, h, device=dev),
+                      torch.zeros(1, device=dev))
+    idx = torch.arange(M, device=dev)
+    act = torch.zeros(M, dtype=torch.uint8, device=dev)
+    leg = torch.full((M,), 15, dtype=torch.uint8, device=dev)
+    olp = torch.full((M, 4), -1.3862944, device=dev)
+    adv = torch.randn(M, device=dev)
+    ret = torch.randn(M, device=dev)
+    batch = L.make_ppo_batch(idx, act, leg, olp, adv, ret)
+    beta_t = torch.tensor(0.02, device=dev)
+    masked = torch.empty(M, 4, device=dev)
+    dx = torch.empty(M, h, device=dev)
+    hp = torch.empty(L.ppo_head_partials(M, h), device=dev)
+    dwa, dba, dwv, dbv = (torch.empty_like(t) for t in (wa, ba, wv, bv))
+    sums = torch.empty(3, device=dev)
+    out["ppo_head_loss"] = timed(lambda: L.ppo_head_loss(xa, wa, ba, wv, bv, batch, beta_t, 0.2, 0.2, False, masked, dx,
+                                                         hp, dwa, dba, dwv, dbv, sums))
+    klo = torch.empty(2, device=dev)
+    out["ppo_head_kl"] = timed(lambda: L.ppo_head_kl(xa, wa, ba, masked, hp, klo))
     for k, v in out.items():
         print(f"{k:40s} {v:9.1f} us")
 
