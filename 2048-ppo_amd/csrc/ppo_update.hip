@@ -6,6 +6,7 @@
 //   ln_bwd_kernel<J,D>    its backward: dg, the residual gradient, dgamma/dbeta partials
 //   head_loss_kernel<J>   action/value heads + PPO-clip loss + entropy + smooth-L1 + backward
 //   head_kl_kernel<J>     KL(old || new) of the post-step re-forward (train.py:578-601)
+//   mlp_fwd_kernel<NT,..> G = X W^T on bf16 MFMA + the LayerNorm/ReLU/dropout/residual epilogue
 //   wgrad_kernel<BI,BJ>   dW = dG^T X on bf16 MFMA (tall-skinny, K = minibatch rows)
 //   colsum1/2             deterministic two-level column sums of per-block partials
 //
@@ -50,6 +51,11 @@ __device__ __forceinline__ void store_bf4(uint16_t *p, const float v[4]) {
     q.x = f2bf(v[0]) | (f2bf(v[1]) << 16);
     q.y = f2bf(v[2]) | (f2bf(v[3]) << 16);
     *reinterpret_cast<uint2 *>(p) = q;
+}
+
+__device__ __forceinline__ void store_bf4(uint16_t *p, const __attribute__((ext_vector_type(4))) float &v) {
+    const float t[4] = {v[0], v[1], v[2], v[3]};
+    store_bf4(p, t);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -724,6 +730,150 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t *__res
         }
 }
 
+
+// ------------------------------------------------------------------ fused Linear + LN block --
+// One ResidualBlock (or the stem) forward in one kernel:
+//     G = X W^T (bf16, kept for the backward),  Y = [X +] Dropout(ReLU(LayerNorm(G)))
+// computed as Y^T = W X^T on v_mfma_f32_16x16x32_bf16 so that a lane ends up holding 4
+// consecutive features of one row per 16-feature tile: the LayerNorm row reductions are two
+// cross-lane steps and every G / Y / residual access is an 8-byte vector.  W (<= 256 x 256 bf16)
+// is staged once per block in LDS; X is read from HBM exactly once, straight into MFMA fragments.
+// Per 65536 x 196 layer this moves X + G + Y (+ X again for the residual): ~77-103 MB, instead
+// of the GEMM's X + G plus the separate LayerNorm pass's G + X + Y.
+constexpr int kMfWaves = 4;
+constexpr int kMfThreads = 64 * kMfWaves;
+constexpr int kMfMT = 1;  // 16-row tiles per wave: a block covers 64 rows
+
+template <int NT, bool RES, bool DROP>
+__global__ __launch_bounds__(kMfThreads) void mlp_fwd_kernel(const uint16_t *__restrict__ X,
+                                                             const uint16_t *__restrict__ W,
+                                                             const float *__restrict__ gamma,
+                                                             const float *__restrict__ beta, uint16_t *__restrict__ G,
+                                                             uint16_t *__restrict__ Y, float *__restrict__ mean_out,
+                                                             float *__restrict__ rstd_out, int64_t M, int N, int K,
+                                                             DropArgs da) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int kp = (K + 7) & ~7, pw = kp * 2;  // W image: N rows of kp bf16
+    char *sW = smem;
+    char *zero = smem + ((N * pw + 15) & ~15);
+    float *sgb = reinterpret_cast<float *>(zero + 64);  // gamma[N], beta[N]
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, col = lane & 15;
+    // stage W (rows of kp with zero K padding): a wave per row, a lane per 8-byte chunk (kp <= 256)
+    for (int n = wave; n < N; n += kMfWaves) {
+        if (lane < (kp >> 2)) {
+            const uint2 v = 4 * lane < K ? *reinterpret_cast<const uint2 *>(W + (int64_t)n * K + 4 * lane)
+                                         : make_uint2(0u, 0u);
+            *reinterpret_cast<uint2 *>(sW + n * pw + 8 * lane) = v;
+        }
+    }
+    if (tid < 16) reinterpret_cast<uint32_t *>(zero)[tid] = 0u;
+    for (int e = tid; e < N; e += kMfThreads) {
+        sgb[e] = gamma[e];
+        sgb[N + e] = beta[e];
+    }
+    __syncthreads();
+    const Drop d = make_drop(da);
+    const float inv_n = 1.0f / (float)N;
+    const int64_t nblk = (M + 16 * kMfMT * kMfWaves - 1) / (16 * kMfMT * kMfWaves);
+
+    for (int64_t mb = blockIdx.x; mb < nblk; mb += gridDim.x) {
+        const int64_t m0 = mb * (16 * kMfMT * kMfWaves) + wave * (16 * kMfMT);
+        f32x4_t acc[kMfMT][NT];
+#pragma unroll
+        for (int t = 0; t < kMfMT; t++)
+#pragma unroll
+            for (int n = 0; n < NT; n++) acc[t][n] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+        // X fragments (B operand: X^T[k][m] = X[m][k .. k+7]) straight from HBM, one k-step ahead
+        auto load_x = [&](int k0, bf16x8_t (&fx)[kMfMT]) {
+            const int kl = k0 + 8 * g;
+#pragma unroll
+            for (int t = 0; t < kMfMT; t++) {
+                const int64_t m = m0 + 16 * t + col;
+                uint4 w = make_uint4(0u, 0u, 0u, 0u);
+                if (m < M && kl < K) {
+                    const uint16_t *src = X + m * K + kl;
+                    const uint2 lo = *reinterpret_cast<const uint2 *>(src);
+                    const uint2 hi = kl + 8 <= K ? *reinterpret_cast<const uint2 *>(src + 4) : make_uint2(0u, 0u);
+                    w = make_uint4(lo.x, lo.y, hi.x, hi.y);  // K % 4 == 0: a K tail is one 4-element half
+                }
+                fx[t] = __builtin_bit_cast(bf16x8_t, w);
+            }
+        };
+        bf16x8_t fx[kMfMT];
+        load_x(0, fx);
+        for (int k0 = 0; k0 < kp; k0 += 32) {
+            const int kl = k0 + 8 * g;
+            bf16x8_t nx[kMfMT];
+            if (k0 + 32 < kp) load_x(k0 + 32, nx);
+#pragma unroll
+            for (int n = 0; n < NT; n++) {  // A operand: W[n][k .. k+7] from LDS
+                const int row = 16 * n + col;
+                const char *pp = (row < N && kl < kp) ? sW + row * pw + 2 * kl : zero;
+                const bf16x8_t fw = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(pp));
+#pragma unroll
+                for (int t = 0; t < kMfMT; t++)
+                    acc[t][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw, fx[t], acc[t][n], 0, 0, 0);
+            }
+#pragma unroll
+            for (int t = 0; t < kMfMT; t++) fx[t] = nx[t];
+        }
+        // epilogue: lane holds row m = m0 + 16t + col, features 16n + 4g + r
+#pragma unroll
+        for (int t = 0; t < kMfMT; t++) {
+            const int64_t m = m0 + 16 * t + col;
+            float sum = 0.0f;
+#pragma unroll
+            for (int n = 0; n < NT; n++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const float v = (float)(__bf16)acc[t][n][r];  // G as stored (bf16)
+                    acc[t][n][r] = v;
+                    sum += 16 * n + 4 * g < N ? v : 0.0f;
+                }
+            sum += __shfl_xor(sum, 16);
+            sum += __shfl_xor(sum, 32);
+            const float mean = sum * inv_n;
+            float var = 0.0f;
+#pragma unroll
+            for (int n = 0; n < NT; n++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const float dv = 16 * n + 4 * g < N ? acc[t][n][r] - mean : 0.0f;
+                    var += dv * dv;
+                }
+            var += __shfl_xor(var, 16);
+            var += __shfl_xor(var, 32);
+            const float rstd = 1.0f / sqrtf(var * inv_n + kLnEps);
+            if (m < M) {
+                if (g == 0) {
+                    mean_out[m] = mean;
+                    rstd_out[m] = rstd;
+                }
+#pragma unroll
+                for (int n = 0; n < NT; n++) {
+                    const int f0 = 16 * n + 4 * g;
+                    if (f0 >= N) continue;
+                    const float4 ga = *reinterpret_cast<const float4 *>(sgb + f0);
+                    const float4 be = *reinterpret_cast<const float4 *>(sgb + N + f0);
+                    const float gg[4] = {ga.x, ga.y, ga.z, ga.w}, bb[4] = {be.x, be.y, be.z, be.w};
+                    float k[4], rs[4], o[4];
+                    if (DROP) drop_mult(d, (uint32_t)m, (uint32_t)(f0 >> 2), k);
+                    if (RES) load_bf4(X + m * K + f0, rs);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        float a = fmaxf((acc[t][n][r] - mean) * rstd * gg[r] + bb[r], 0.0f);
+                        if (DROP) a *= k[r];
+                        o[r] = RES ? rs[r] + a : a;
+                    }
+                    store_bf4(G + m * N + f0, acc[t][n]);
+                    store_bf4(Y + m * N + f0, o);
+                }
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ column sums --------------
 // Stage 1: grid (ceil(C/64), kSlices); block (64 columns x 4 row groups) sums rows of slice y.
 constexpr int kSlices = 32;
@@ -1020,6 +1170,58 @@ int g2048_wgrad(g2048_stream_t stream, const uint16_t *a, const uint16_t *b, int
     segs.dst[0] = out;
     segs.len[0] = n1 * n2;
     return colsum(s, partials, p.nb, n1 * n2, partials + (size_t)p.nb * n1 * n2, segs, -1);
+}
+
+
+size_t g2048_mlp_fwd_lds_bytes(int32_t n, int32_t k) {
+    if (n <= 0 || k <= 0 || n > 256 || k > 256 || n % 4 || k % 4) return 0;
+    const int kp = (k + 7) & ~7;
+    return (size_t)((n * kp * 2 + 15) & ~15) + 64 + (size_t)8 * n;
+}
+
+int g2048_mlp_fwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, const float *gamma, const float *beta,
+                  int32_t residual, uint16_t *g, uint16_t *y, float *mean, float *rstd, int64_t m, int32_t n, int32_t k,
+                  const g2048_dropout *drop) {
+    const size_t lds = g2048_mlp_fwd_lds_bytes(n, k);
+    if (!lds || m < 0 || !x || !w || !gamma || !beta || !g || !y || !mean || !rstd) return G2048_EINVAL;
+    if (residual && n != k) return G2048_EINVAL;
+    if (!al(x, 8) || !al(w, 8) || !al(g, 8) || !al(y, 8) || !al(gamma, 16) || !al(beta, 16)) return G2048_EINVAL;
+    if (m == 0) return G2048_OK;
+    const hipStream_t s = (hipStream_t)stream;
+    const DropArgs da = drop_args(drop);
+    const int64_t nblk = (m + 16 * kMfMT * kMfWaves - 1) / (16 * kMfMT * kMfWaves);
+    const dim3 grid((unsigned)(nblk > 1024 ? 1024 : nblk)), blk(kMfThreads);
+    const bool dr = drop_on(drop);
+    const int nt = (n + 15) / 16;
+#define G2048_MF_LAUNCH(NT_)                                                                                       \
+    do {                                                                                                           \
+        if (residual && dr)                                                                                        \
+            hipLaunchKernelGGL((mlp_fwd_kernel<NT_, true, true>), grid, blk, lds, s, x, w, gamma, beta, g, y, mean, \
+                               rstd, m, n, k, da);                                                                 \
+        else if (residual)                                                                                         \
+            hipLaunchKernelGGL((mlp_fwd_kernel<NT_, true, false>), grid, blk, lds, s, x, w, gamma, beta, g, y,     \
+                               mean, rstd, m, n, k, da);                                                           \
+        else if (dr)                                                                                               \
+            hipLaunchKernelGGL((mlp_fwd_kernel<NT_, false, true>), grid, blk, lds, s, x, w, gamma, beta, g, y,     \
+                               mean, rstd, m, n, k, da);                                                           \
+        else                                                                                                       \
+            hipLaunchKernelGGL((mlp_fwd_kernel<NT_, false, false>), grid, blk, lds, s, x, w, gamma, beta, g, y,    \
+                               mean, rstd, m, n, k, da);                                                           \
+    } while (0)
+    switch (nt) {
+        case 1: G2048_MF_LAUNCH(1); break;
+        case 2: G2048_MF_LAUNCH(2); break;
+        case 3: G2048_MF_LAUNCH(3); break;
+        case 4: G2048_MF_LAUNCH(4); break;
+        case 5: case 6: G2048_MF_LAUNCH(6); break;
+        case 7: case 8: G2048_MF_LAUNCH(8); break;
+        case 9: case 10: G2048_MF_LAUNCH(10); break;
+        case 11: case 12: G2048_MF_LAUNCH(12); break;
+        case 13: G2048_MF_LAUNCH(13); break;
+        default: G2048_MF_LAUNCH(16); break;
+    }
+#undef G2048_MF_LAUNCH
+    return status();
 }
 
 int g2048_dropout_mask(g2048_stream_t stream, int64_t m, int32_t h, const g2048_dropout *drop, uint8_t *mask) {

@@ -32,6 +32,7 @@ EXPORTED = (
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask",
     "g2048_wgrad_partials", "g2048_wgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
+    "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd",
 )
 
 
@@ -135,6 +136,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_wgrad_partials": (sz, [i64, i32, i32]),
         "g2048_wgrad": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, vp, vp]),
         "g2048_grad_clip": (ctypes.c_int, [vp, vp, i64, ctypes.c_float, vp, vp, vp]),
+        "g2048_mlp_fwd_lds_bytes": (sz, [i32, i32]),
+        "g2048_mlp_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, i64, i32, i32, dp]),
         "g2048_muon_supported": (ctypes.c_int, [i32, i32]),
         "g2048_muon_step": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.POINTER(MuonCfg)]),
         "g2048_adamw_step": (ctypes.c_int, [vp, ctypes.POINTER(AdamWGroup), i32, vp, vp, vp, ctypes.c_float,
@@ -375,3 +378,18 @@ def adamw_step(groups, lr_dev, step_dev, clip_coef_dev, beta1, beta2, eps, weigh
     _check(load().g2048_adamw_step(_stream(lr_dev), groups, len(groups), _dev(lr_dev, torch.float32, "lr"),
                                    _dev(step_dev, torch.float32, "step"), _dev(clip_coef_dev, torch.float32, "clip"),
                                    float(beta1), float(beta2), float(eps), float(weight_decay)), "g2048_adamw_step")
+
+
+def mlp_fwd_supported(n: int, k: int) -> bool:
+    return int(load().g2048_mlp_fwd_lds_bytes(n, k)) > 0
+
+
+def mlp_fwd(x, w, gamma, beta, residual: bool, g, y, mean, rstd, drop: Dropout | None = None):
+    """g = x w^T; y = [x +] Dropout(ReLU(LayerNorm(g))) in one MFMA kernel (bf16 x [m,k], w [n,k])."""
+    m, k = x.shape
+    n = w.shape[0]
+    _check(load().g2048_mlp_fwd(
+        _stream(x), _dev(x, torch.bfloat16, "x"), _dev(w, torch.bfloat16, "w"), _dev(gamma, torch.float32, "gamma"),
+        _dev(beta, torch.float32, "beta"), int(bool(residual)), _dev(g, torch.bfloat16, "g"),
+        _dev(y, torch.bfloat16, "y"), _dev(mean, torch.float32, "mean"), _dev(rstd, torch.float32, "rstd"), m, n, k,
+        ctypes.byref(drop) if drop is not None else None), "g2048_mlp_fwd")

@@ -5,8 +5,8 @@ GameMLP (game.py:1049-1220: stem Linear-LayerNorm-ReLU, L x [x + Dropout(ReLU(LN
 action/value heads), FusedPPOUpdater writes the forward and backward out by hand:
 
     forward   X0 = obs(boards[idx])                          g2048_obs_gather
-              G_l = H_{l-1} W_l^T                             GEMM (hipBLASLt, bf16 in, bf16 out)
-              H_l = H_{l-1} + Drop(ReLU(LN(G_l)))             g2048_ln_act_fwd
+              G_l = H_{l-1} W_l^T                             g2048_mlp_fwd: one MFMA kernel per layer
+              H_l = H_{l-1} + Drop(ReLU(LN(G_l)))             (hipBLASLt + g2048_ln_act_fwd beyond h=256)
     loss      heads + PPO-clip + entropy + smooth-L1 and      g2048_ppo_head_loss
               d/dH_L, d/d(head params), loss sums
     backward  dG_l, dgamma_l, dbeta_l, residual grad          g2048_ln_act_bwd
@@ -64,6 +64,7 @@ class FusedPPOUpdater(PPOUpdater):
         self.wa, self.ba = model.action_head.weight, model.action_head.bias
         self.wv, self.bv = model.value_head.weight, model.value_head.bias
         self.wbf = [torch.empty_like(w, dtype=torch.bfloat16) for w in self.lin]
+        self.mf_ok = [L.mlp_fwd_supported(w.shape[0], w.shape[1]) for w in self.lin]
         self.counter = torch.zeros(1, dtype=torch.int64, device=self.dev)  # dropout counter base
         # a fused optimizer (optim.FusedMuonAdamW) clips, steps and refreshes the bf16 weights itself
         self.fused_opt = bool(getattr(optimizer, "fused", False) or getattr(optimizer, "supported", False))
@@ -112,9 +113,13 @@ class FusedPPOUpdater(PPOUpdater):
     def _layers(self, pass_: int):
         x = self.x0
         for l, (w, ln) in enumerate(zip(self.wbf, self.ln)):
-            _mm(x, w.t(), self.G[l])
-            L.ln_act_fwd(self.G[l], ln.weight, ln.bias, x if l > 0 else None, self.H[l], self.mean[l], self.rstd[l],
-                         self._drop(l, pass_) if l > 0 else None)
+            drop = self._drop(l, pass_) if l > 0 else None
+            if self.mf_ok[l]:  # Linear + LayerNorm + ReLU + dropout + residual in one MFMA kernel
+                L.mlp_fwd(x, w, ln.weight, ln.bias, l > 0, self.G[l], self.H[l], self.mean[l], self.rstd[l], drop)
+            else:
+                _mm(x, w.t(), self.G[l])
+                L.ln_act_fwd(self.G[l], ln.weight, ln.bias, x if l > 0 else None, self.H[l], self.mean[l],
+                             self.rstd[l], drop)
             x = self.H[l]
         return x
 

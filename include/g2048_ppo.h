@@ -50,6 +50,18 @@ int g2048_ln_act_fwd(g2048_stream_t stream, const uint16_t *g, const float *gamm
                      const uint16_t *res, uint16_t *y, float *mean, float *rstd, int64_t m, int32_t h,
                      const g2048_dropout *drop);
 
+/* Dynamic LDS bytes of g2048_mlp_fwd for an [n, k] weight (0 = unsupported: n, k % 4 != 0 or > 256). */
+size_t g2048_mlp_fwd_lds_bytes(int32_t n, int32_t k);
+
+/* A whole Linear(bias=False) + LayerNorm + ReLU [+ Dropout + residual] layer forward on MFMA:
+ *   g = x w^T (bf16 [m, n], kept for the backward);  y = [x +] Dropout(ReLU(LayerNorm(g)))
+ * x bf16 [m, k], w bf16 [n, k]; residual requires n == k (ResidualBlock); mean / rstd as
+ * g2048_ln_act_fwd.  Same results as a bf16 GEMM followed by g2048_ln_act_fwd, up to fp32
+ * summation order. */
+int g2048_mlp_fwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, const float *gamma, const float *beta,
+                  int32_t residual, uint16_t *g, uint16_t *y, float *mean, float *rstd, int64_t m, int32_t n, int32_t k,
+                  const g2048_dropout *drop);
+
 /* Scratch floats of g2048_ln_act_bwd for (m, h). */
 size_t g2048_ln_act_bwd_partials(int64_t m, int32_t h);
 

@@ -69,6 +69,33 @@ def test_ln_act_fwd_matches_torch(dev, h, m, p, with_res):
     torch.testing.assert_close(rstd, 1 / torch.sqrt(gf.var(1, unbiased=False) + 1e-5), rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("m,n,k,res,p", [(65536, 196, 196, True, 0.1), (5000, 196, 48, False, 0.0),
+                                         (777, 64, 64, True, 0.2), (100, 192, 192, True, 0.0),
+                                         (1030, 256, 256, True, 0.1), (33, 196, 48, False, 0.0)])
+def test_mlp_fwd_matches_gemm_plus_ln(dev, m, n, k, res, p):
+    """The fused MFMA Linear+LN layer == bf16 GEMM followed by g2048_ln_act_fwd (same dropout mask)."""
+    from g2048 import _lib as L
+    torch.manual_seed(m + n + k)
+    x = _bf(torch.randn(m, k, device=dev))
+    w = _bf(torch.randn(n, k, device=dev) / k ** 0.5)
+    gamma = torch.rand(n, device=dev) + 0.5
+    beta = torch.randn(n, device=dev) * 0.1
+    ctr = torch.tensor([5], dtype=torch.int64, device=dev)
+    drop = L.make_dropout(p, 1, 0, 77, 0, ctr)
+    g1, y1 = (torch.empty(m, n, dtype=torch.bfloat16, device=dev) for _ in range(2))
+    mean1, rstd1 = torch.empty(m, device=dev), torch.empty(m, device=dev)
+    L.mlp_fwd(x, w, gamma, beta, res, g1, y1, mean1, rstd1, drop)
+    g0 = (x.float() @ w.float().T).to(torch.bfloat16)
+    y0 = torch.empty_like(g0)
+    mean0, rstd0 = torch.empty(m, device=dev), torch.empty(m, device=dev)
+    L.ln_act_fwd(g0, gamma, beta, x if res else None, y0, mean0, rstd0, drop)
+    # G: same bf16 rounding of (nearly) the same fp32 sum -> equal or 1 ulp apart
+    torch.testing.assert_close(g1.float(), g0.float(), rtol=8e-3, atol=1e-2)
+    torch.testing.assert_close(mean1, mean0, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(rstd1, rstd0, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(y1.float(), y0.float(), rtol=2e-2, atol=3e-2)
+
+
 def test_dropout_mask_depends_on_counter_layer_pass(dev):
     from g2048 import _lib as L
     m, h = 512, 196

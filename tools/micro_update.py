@@ -76,6 +76,12 @@ def main():
     ln = m.backbone[0].mlp[1]
     ctr = torch.zeros(1, dtype=torch.int64, device=dev)
     drop = L.make_dropout(0.1, 1, 0, 7, 0, ctr)
+    gm_ = torch.empty(M, h, device=dev, dtype=bf)
+    out["mlp_fwd fused (res, drop)"] = timed(lambda: L.mlp_fwd(X, W, ln.weight, ln.bias, True, gm_, y, mean, rstd, drop))
+    out["mlp_fwd fused (res, no drop)"] = timed(lambda: L.mlp_fwd(X, W, ln.weight, ln.bias, True, gm_, y, mean, rstd,
+                                                                  None))
+    out["mlp_fwd fused stem (48->196)"] = timed(lambda: L.mlp_fwd(X0, Ws, ln.weight, ln.bias, False, gm_, y, mean, rstd,
+                                                                  None))
     out["ln_act_fwd (res, drop)"] = timed(lambda: L.ln_act_fwd(X, ln.weight, ln.bias, X, y, mean, rstd, drop))
     dres = torch.randn(M, h, device=dev)
     pb = torch.empty(L.ln_act_bwd_partials(M, h), device=dev)
