@@ -7,6 +7,7 @@
 //   head_loss_kernel<J>   action/value heads + PPO-clip loss + entropy + smooth-L1 + backward
 //   head_kl_kernel<J>     KL(old || new) of the post-step re-forward (train.py:578-601)
 //   mlp_fwd_kernel<NT,..> G = X W^T on bf16 MFMA + the LayerNorm/ReLU/dropout/residual epilogue
+//   head_fwd_kernel<KS>   rollout policy heads (logits + value) on MFMA
 //   wgrad_kernel<BI,BJ>   dW = dG^T X on bf16 MFMA (tall-skinny, K = minibatch rows)
 //   colsum1/2             deterministic two-level column sums of per-block partials
 //
@@ -382,24 +383,40 @@ __global__ __launch_bounds__(kThreads) void head_loss_kernel(const uint16_t *__r
     const float beta_c = *a.beta_dev;
     float sb[5] = {0, 0, 0, 0, 0}, s_ppo = 0.0f, s_ent = 0.0f, s_v = 0.0f;
 
-    for (int64_t r = (int64_t)blockIdx.x * kWaves + wave; r < m; r += nw) {
-        const int64_t i = a.idx[r];
-        float x[J][4], z[5] = {0, 0, 0, 0, 0};
+    constexpr int RPW = 2;  // rows per wave and iteration: their loads and reductions overlap
+    for (int64_t r0 = ((int64_t)blockIdx.x * kWaves + wave) * RPW; r0 < m; r0 += nw * RPW) {
+        float xs[RPW][J][4], zs[RPW][5];
+        int64_t is[RPW];
 #pragma unroll
-        for (int j = 0; j < J; j++) {
-            if (ok[j]) {
-                load_bf4(xin + r * h + 4 * (lane + 64 * j), x[j]);
-            } else {
-                x[j][0] = x[j][1] = x[j][2] = x[j][3] = 0.0f;
+        for (int q = 0; q < RPW; q++) {
+            const int64_t r = r0 + q;
+            is[q] = r < m ? a.idx[r] : 0;
+#pragma unroll
+            for (int k = 0; k < 5; k++) zs[q][k] = 0.0f;
+#pragma unroll
+            for (int j = 0; j < J; j++) {
+                if (ok[j] && r < m) {
+                    load_bf4(xin + r * h + 4 * (lane + 64 * j), xs[q][j]);
+                } else {
+                    xs[q][j][0] = xs[q][j][1] = xs[q][j][2] = xs[q][j][3] = 0.0f;
+                }
+#pragma unroll
+                for (int k = 0; k < 5; k++)
+#pragma unroll
+                    for (int u = 0; u < 4; u++) zs[q][k] += xs[q][j][u] * w[k][j][u];
             }
-#pragma unroll
-            for (int k = 0; k < 5; k++)
-#pragma unroll
-                for (int u = 0; u < 4; u++) z[k] += x[j][u] * w[k][j][u];
         }
 #pragma unroll
-        for (int k = 0; k < 5; k++) z[k] = wave_sum(z[k]) + bias[k];
-
+        for (int q = 0; q < RPW; q++)
+#pragma unroll
+            for (int k = 0; k < 5; k++) zs[q][k] = wave_sum(zs[q][k]) + bias[k];
+#pragma unroll
+        for (int q = 0; q < RPW; q++) {
+        const int64_t r = r0 + q;
+        if (r >= m) break;
+        const int64_t i = is[q];
+        float (&x)[J][4] = xs[q];
+        float (&z)[5] = zs[q];
         // ---- the loss of this row (every lane redundantly; scalars are wave-uniform)
         const int act = a.action[i] & 3;
         const uint32_t legal = a.legal[i] & 0xFu;
@@ -493,6 +510,7 @@ __global__ __launch_bounds__(kThreads) void head_loss_kernel(const uint16_t *__r
         s_v += vl;
         if (lane == 0)
             *reinterpret_cast<float4 *>(masked_out + r * 4) = make_float4(mk[0], mk[1], mk[2], mk[3]);
+        }
     }
     float *mine = lds + wave * C;
 #pragma unroll
@@ -545,25 +563,41 @@ __global__ __launch_bounds__(kThreads) void head_kl_kernel(const uint16_t *__res
 #pragma unroll
     for (int k = 0; k < 4; k++) bias[k] = ba[k];
     float ksum = 0.0f, kmax = -INFINITY;
-    for (int64_t r = (int64_t)blockIdx.x * kWaves + wave; r < m; r += nw) {
-        float z[4] = {0, 0, 0, 0};
+    constexpr int RPW = 4;
+    for (int64_t r0 = ((int64_t)blockIdx.x * kWaves + wave) * RPW; r0 < m; r0 += nw * RPW) {
+        float zs[RPW][4];
 #pragma unroll
-        for (int j = 0; j < J; j++) {
-            if (!ok[j]) continue;
-            float x[4];
-            load_bf4(xin + r * h + 4 * (lane + 64 * j), x);
+        for (int q = 0; q < RPW; q++) {
+            const int64_t r = r0 + q;
 #pragma unroll
-            for (int k = 0; k < 4; k++)
+            for (int k = 0; k < 4; k++) zs[q][k] = 0.0f;
 #pragma unroll
-                for (int u = 0; u < 4; u++) z[k] += x[u] * w[k][j][u];
+            for (int j = 0; j < J; j++) {
+                if (!ok[j] || r >= m) continue;
+                float x[4];
+                load_bf4(xin + r * h + 4 * (lane + 64 * j), x);
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+#pragma unroll
+                    for (int u = 0; u < 4; u++) zs[q][k] += x[u] * w[k][j][u];
+            }
         }
+#pragma unroll
+        for (int q = 0; q < RPW; q++)
+#pragma unroll
+            for (int k = 0; k < 4; k++) zs[q][k] = wave_sum(zs[q][k]);
+#pragma unroll
+        for (int q = 0; q < RPW; q++) {
+        const int64_t r = r0 + q;
+        if (r >= m) break;
+        float (&z)[4] = zs[q];
         const float4 o4 = *reinterpret_cast<const float4 *>(old_masked + r * 4);
         const float o[4] = {o4.x, o4.y, o4.z, o4.w};
         bool valid[4];
         float mo = -INFINITY, mn = -INFINITY, nz[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            z[k] = wave_sum(z[k]) + bias[k];
+            z[k] += bias[k];  // already wave-reduced above
             valid[k] = o[k] != -INFINITY;
             nz[k] = valid[k] ? z[k] : -INFINITY;
             mo = fmaxf(mo, o[k]);
@@ -585,6 +619,7 @@ __global__ __launch_bounds__(kThreads) void head_kl_kernel(const uint16_t *__res
         }
         ksum += kl;
         kmax = fmaxf(kmax, kl);
+        }
     }
     if (lane == 0) {
         lds[wave][0] = ksum;
@@ -846,7 +881,7 @@ __global__ __launch_bounds__(kMfThreads) void mlp_fwd_kernel(const uint16_t *__r
             var += __shfl_xor(var, 32);
             const float rstd = 1.0f / sqrtf(var * inv_n + kLnEps);
             if (m < M) {
-                if (g == 0) {
+                if (g == 0 && mean_out) {
                     mean_out[m] = mean;
                     rstd_out[m] = rstd;
                 }
@@ -866,10 +901,66 @@ __global__ __launch_bounds__(kMfThreads) void mlp_fwd_kernel(const uint16_t *__r
                         if (DROP) a *= k[r];
                         o[r] = RES ? rs[r] + a : a;
                     }
-                    store_bf4(G + m * N + f0, acc[t][n]);
+                    if (G) store_bf4(G + m * N + f0, acc[t][n]);
                     store_bf4(Y + m * N + f0, o);
                 }
             }
+        }
+    }
+}
+
+
+// ------------------------------------------------------------------ policy / value heads -----
+// logits = x Wa^T + ba, value = x Wv^T + bv for the rollout policy (GameMLP.forward, game.py:
+// 1208-1219): one v_mfma_f32_16x16x32_bf16 tile per 16 rows with the 5 head rows as the 16-wide
+// N (columns 5..15 zero), head weights held as bf16 B fragments in registers for the whole launch.
+template <int KS>
+__global__ __launch_bounds__(256) void head_fwd_kernel(const uint16_t *__restrict__ X, const float *__restrict__ wa,
+                                                       const float *__restrict__ ba, const float *__restrict__ wv,
+                                                       const float *__restrict__ bv, int64_t M, int K,
+                                                       float *__restrict__ logits, int64_t lstride,
+                                                       float *__restrict__ value) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    bf16x8_t fb[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ks++) {
+        s16x8_t v;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int k = 32 * ks + 8 * g + j;
+            const float wgt = (c < 5 && k < K) ? (c < 4 ? wa[c * K + k] : wv[k]) : 0.0f;
+            v[j] = __builtin_bit_cast(short, (__bf16)wgt);
+        }
+        fb[ks] = __builtin_bit_cast(bf16x8_t, v);
+    }
+    const float bias = c < 4 ? ba[c] : (c == 4 ? bv[0] : 0.0f);
+    const int64_t tiles = (M + 15) >> 4;
+    for (int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); tile < tiles; tile += (int64_t)gridDim.x * 4) {
+        const int64_t m0 = tile * 16, mr = m0 + c;
+        bf16x8_t fa[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            const int kl = 32 * ks + 8 * g;
+            uint4 w = make_uint4(0u, 0u, 0u, 0u);
+            if (mr < M && kl < K) {
+                const uint16_t *src = X + mr * K + kl;
+                const uint2 lo = *reinterpret_cast<const uint2 *>(src);
+                const uint2 hi = kl + 8 <= K ? *reinterpret_cast<const uint2 *>(src + 4) : make_uint2(0u, 0u);
+                w = make_uint4(lo.x, lo.y, hi.x, hi.y);
+            }
+            fa[ks] = __builtin_bit_cast(bf16x8_t, w);
+        }
+        f32x4_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks], fb[ks], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int64_t row = m0 + 4 * g + r;
+            if (row >= M) continue;
+            if (c < 4)
+                logits[row * lstride + c] = acc[r] + bias;
+            else if (c == 4)
+                value[row] = acc[r] + bias;
         }
     }
 }
@@ -1183,9 +1274,9 @@ int g2048_mlp_fwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, c
                   int32_t residual, uint16_t *g, uint16_t *y, float *mean, float *rstd, int64_t m, int32_t n, int32_t k,
                   const g2048_dropout *drop) {
     const size_t lds = g2048_mlp_fwd_lds_bytes(n, k);
-    if (!lds || m < 0 || !x || !w || !gamma || !beta || !g || !y || !mean || !rstd) return G2048_EINVAL;
+    if (!lds || m < 0 || !x || !w || !gamma || !beta || !y || (!mean) != (!rstd)) return G2048_EINVAL;
     if (residual && n != k) return G2048_EINVAL;
-    if (!al(x, 8) || !al(w, 8) || !al(g, 8) || !al(y, 8) || !al(gamma, 16) || !al(beta, 16)) return G2048_EINVAL;
+    if (!al(x, 8) || !al(w, 8) || (g && !al(g, 8)) || !al(y, 8) || !al(gamma, 16) || !al(beta, 16)) return G2048_EINVAL;
     if (m == 0) return G2048_OK;
     const hipStream_t s = (hipStream_t)stream;
     const DropArgs da = drop_args(drop);
@@ -1221,6 +1312,25 @@ int g2048_mlp_fwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, c
         default: G2048_MF_LAUNCH(16); break;
     }
 #undef G2048_MF_LAUNCH
+    return status();
+}
+
+
+int g2048_head_fwd(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, const float *wv,
+                   const float *bv, int64_t m, int32_t h, float *logits, int64_t logits_stride, float *value) {
+    if (m < 0 || h <= 0 || h % 4 || h > 256 || !x || !wa || !ba || !wv || !bv || !logits || !value) return G2048_EINVAL;
+    if (!al(x, 8) || logits_stride < 4) return G2048_EINVAL;
+    if (m == 0) return G2048_OK;
+    const int64_t tiles = (m + 15) / 16;
+    const int64_t blocks = (tiles + 3) / 4;
+    const dim3 grid((unsigned)(blocks > 2048 ? 2048 : blocks)), blk(256);
+    const hipStream_t s = (hipStream_t)stream;
+    switch ((h + 31) / 32) {
+#define G2048_HF(KS_) case KS_: hipLaunchKernelGGL((head_fwd_kernel<KS_>), grid, blk, 0, s, x, wa, ba, wv, bv, m, h, \
+                                                  logits, logits_stride, value); break;
+        G2048_HF(1) G2048_HF(2) G2048_HF(3) G2048_HF(4) G2048_HF(5) G2048_HF(6) G2048_HF(7) G2048_HF(8)
+#undef G2048_HF
+    }
     return status();
 }
 

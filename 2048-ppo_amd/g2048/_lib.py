@@ -32,7 +32,7 @@ EXPORTED = (
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask",
     "g2048_wgrad_partials", "g2048_wgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
-    "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd",
+    "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd",
 )
 
 
@@ -138,6 +138,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_grad_clip": (ctypes.c_int, [vp, vp, i64, ctypes.c_float, vp, vp, vp]),
         "g2048_mlp_fwd_lds_bytes": (sz, [i32, i32]),
         "g2048_mlp_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, i64, i32, i32, dp]),
+        "g2048_head_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, vp, i64, vp]),
         "g2048_muon_supported": (ctypes.c_int, [i32, i32]),
         "g2048_muon_step": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.POINTER(MuonCfg)]),
         "g2048_adamw_step": (ctypes.c_int, [vp, ctypes.POINTER(AdamWGroup), i32, vp, vp, vp, ctypes.c_float,
@@ -393,3 +394,14 @@ def mlp_fwd(x, w, gamma, beta, residual: bool, g, y, mean, rstd, drop: Dropout |
         _dev(beta, torch.float32, "beta"), int(bool(residual)), _dev(g, torch.bfloat16, "g"),
         _dev(y, torch.bfloat16, "y"), _dev(mean, torch.float32, "mean"), _dev(rstd, torch.float32, "rstd"), m, n, k,
         ctypes.byref(drop) if drop is not None else None), "g2048_mlp_fwd")
+
+
+def head_fwd(x, wa, ba, wv, bv, logits, value):
+    """logits [m, >=4] (row stride may exceed 4) and value [m] of the GameMLP heads on MFMA."""
+    m, h = x.shape
+    if logits.stride(-1) != 1 or logits.dtype != torch.float32 or not logits.is_cuda:
+        raise G2048Error("logits must be a float32 device tensor with unit inner stride")
+    _check(load().g2048_head_fwd(
+        _stream(x), _dev(x, torch.bfloat16, "x"), _dev(wa, torch.float32, "wa"), _dev(ba, torch.float32, "ba"),
+        _dev(wv, torch.float32, "wv"), _dev(bv, torch.float32, "bv"), m, h, ctypes.c_void_p(logits.data_ptr()),
+        logits.stride(0), _dev(value, torch.float32, "value")), "g2048_head_fwd")

@@ -43,6 +43,70 @@ class InferencePolicy:
         return logits.float(), value.float().view(-1)
 
 
+class FusedPolicy:
+    """The reference's GameMLP in eval mode (game.py:1145-1220) as MFMA kernels for the rollout:
+    per layer one g2048_mlp_fwd (Linear + LayerNorm + ReLU [+ residual]), then g2048_head_fwd for
+    the action logits and the value.  bf16 weights are refreshed in place by sync() (addresses stay
+    fixed for a captured rollout graph); LayerNorm and head parameters are read from the master.
+    Drop-in for InferencePolicy: __call__(obs bf16 [n, 48]) -> (logits fp32 [n, 4], value fp32 [n])."""
+
+    def __init__(self, model: torch.nn.Module):
+        self.master = model
+        self.dtype = torch.bfloat16
+        self.lin = [model.stem[0].weight] + [b.mlp[0].weight for b in model.backbone]
+        self.ln = [model.stem[1]] + [b.mlp[1] for b in model.backbone]
+        self.heads = (model.action_head.weight, model.action_head.bias, model.value_head.weight, model.value_head.bias)
+        self.wbf = [torch.empty_like(w, dtype=torch.bfloat16) for w in self.lin]
+        self._n = -1
+        self.sync()
+
+    @staticmethod
+    def supports(model) -> bool:
+        try:
+            import agent
+        except ImportError:  # pragma: no cover
+            return False
+        if not isinstance(model, agent.GameMLP):
+            return False
+        lin = [model.stem[0].weight] + [b.mlp[0].weight for b in model.backbone]
+        return all(L.mlp_fwd_supported(w.shape[0], w.shape[1]) for w in lin) and model.config.hidden_dim <= 256
+
+    @torch.no_grad()
+    def sync(self):
+        for w, b in zip(self.lin, self.wbf):
+            b.copy_(w)
+
+    def _buffers(self, n: int, dev):
+        if self._n != n:
+            h = self.lin[0].shape[0]
+            self.h = [torch.empty(n, h, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+            self.logits = torch.empty(n, 4, dtype=torch.float32, device=dev)
+            self.value = torch.empty(n, dtype=torch.float32, device=dev)
+            self._n = n
+
+    @torch.no_grad()
+    def __call__(self, obs: torch.Tensor):
+        if obs.dtype != torch.bfloat16:
+            obs = obs.to(torch.bfloat16)
+        self._buffers(obs.shape[0], obs.device)
+        x = obs.contiguous()
+        for l, (w, ln) in enumerate(zip(self.wbf, self.ln)):
+            y = self.h[l % 2]
+            L.mlp_fwd(x, w, ln.weight, ln.bias, l > 0, None, y, None, None, None)
+            x = y
+        L.head_fwd(x, *self.heads, self.logits, self.value)
+        return self.logits, self.value
+
+
+def make_policy(model: torch.nn.Module, dtype=torch.bfloat16):
+    """The rollout policy: FusedPolicy for the reference's GameMLP on a ROCm device (bf16), the
+    generic module copy (InferencePolicy) otherwise."""
+    dev = next(model.parameters()).device
+    if dtype == torch.bfloat16 and dev.type == "cuda" and FusedPolicy.supports(model):
+        return FusedPolicy(model)
+    return InferencePolicy(model, dtype)
+
+
 class RolloutBuffers:
     """Time-major trajectory storage for `horizon` steps of `n` envs."""
 

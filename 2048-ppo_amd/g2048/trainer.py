@@ -24,7 +24,7 @@ from .advantage import RewardWeights, RTGTracker
 from .dist import GradBucket, allreduce_sum_, world
 from .optim import FusedMuonAdamW, MuonAdamW, ScheduledMuonAdamW, build_optimizer
 from .ppo import PPOConfig, PPOUpdater
-from .rollout import InferencePolicy, Rollout
+from .rollout import Rollout, make_policy
 
 
 @dataclass
@@ -101,7 +101,7 @@ class VecTrainer:
             self.grads = GradBucket(self.model.parameters())
             self.opt = build_optimizer(self.model, cfg.lr, cfg.critic_lr, cfg.beta1, cfg.beta2, cfg.weight_decay,
                                        cfg.warmup_steps, cfg.steps)
-        self.policy = InferencePolicy(self.model, torch.bfloat16 if cfg.amp else torch.float32)
+        self.policy = make_policy(self.model, torch.bfloat16 if cfg.amp else torch.float32)
         n = cfg.episodes
         self.episodic = cfg.horizon <= 0
         T = cfg.horizon if not self.episodic else (cfg.max_steps or cfg.episodic_cap)

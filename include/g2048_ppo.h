@@ -57,10 +57,16 @@ size_t g2048_mlp_fwd_lds_bytes(int32_t n, int32_t k);
  *   g = x w^T (bf16 [m, n], kept for the backward);  y = [x +] Dropout(ReLU(LayerNorm(g)))
  * x bf16 [m, k], w bf16 [n, k]; residual requires n == k (ResidualBlock); mean / rstd as
  * g2048_ln_act_fwd.  Same results as a bf16 GEMM followed by g2048_ln_act_fwd, up to fp32
- * summation order. */
+ * summation order.  Inference (the rollout policy) passes g = mean = rstd = NULL. */
 int g2048_mlp_fwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, const float *gamma, const float *beta,
                   int32_t residual, uint16_t *g, uint16_t *y, float *mean, float *rstd, int64_t m, int32_t n, int32_t k,
                   const g2048_dropout *drop);
+
+/* Rollout policy heads (GameMLP.forward, game.py:1208-1219) on MFMA: logits[r * logits_stride + a]
+ * = x[r] . wa[a] + ba[a] (a < 4), value[r] = x[r] . wv + bv; x bf16 [m, h], weights fp32 (used as
+ * bf16), fp32 accumulate. */
+int g2048_head_fwd(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, const float *wv,
+                   const float *bv, int64_t m, int32_t h, float *logits, int64_t logits_stride, float *value);
 
 /* Scratch floats of g2048_ln_act_bwd for (m, h). */
 size_t g2048_ln_act_bwd_partials(int64_t m, int32_t h);

@@ -495,3 +495,51 @@ def test_fused_update_tracks_autograd_update_with_dropout(dev):
     for a, b in zip(res[0], res[1]):
         for k in ("policy_loss", "value_loss", "entropy", "grad_norm"):
             assert math.isclose(a[k], b[k], rel_tol=0.1, abs_tol=2e-3), (k, a[k], b[k])
+
+
+@pytest.mark.parametrize("h,n", [(196, 65536), (64, 1000), (192, 4097)])
+def test_fused_policy_matches_module(dev, h, n):
+    """FusedPolicy (MFMA layers + heads) == the bf16 eval-mode module (InferencePolicy) and tracks
+    the fp32 reference forward (game.py:1145-1220)."""
+    import agent
+    from g2048 import _lib as L
+    from g2048.rollout import FusedPolicy, InferencePolicy
+    torch.manual_seed(h)
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=h, num_layers=2)).to(dev)
+    with torch.no_grad():
+        for p in m.parameters():  # non-trivial heads / LayerNorm affine
+            p.add_(torch.randn_like(p) * 0.05)
+    g = np.random.default_rng(h)
+    boards = torch.from_numpy(g.integers(0, 14, size=(n, 16)).astype(np.int8)).to(dev)
+    obs = torch.empty(n, 48, dtype=torch.bfloat16, device=dev)
+    L.obs_encode(boards, obs)
+    fp = FusedPolicy(m)
+    lf, vf = fp(obs)
+    lb, vb = InferencePolicy(m)(obs)
+    m.eval()
+    with torch.no_grad():
+        l32, v32 = m(obs.float())
+    # two bf16 evaluations of the same network: rounding-level differences, a few at the tail
+    for a, b in ((lf, lb), (vf, vb)):
+        d = (a - b).abs()
+        assert float(d.mean()) < 5e-3 and float(d.max()) < 0.1, (float(d.mean()), float(d.max()))
+    # bf16 vs the fp32 reference: the same order of error as torch's own bf16 module
+    err_f = float((lf - l32).abs().max())
+    err_b = float((lb - l32).abs().max())
+    assert err_f <= max(2 * err_b, 2e-2), (err_f, err_b)
+
+
+def test_fused_policy_graph_rollout_matches_eager(dev):
+    import agent
+    from g2048.rollout import FusedPolicy, Rollout
+    torch.manual_seed(2)
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=196)).to(dev)
+    pol = FusedPolicy(m)
+    outs = []
+    for graph in (False, True, True):
+        ro = Rollout(4096, 24, dev, seed=9)
+        ro.reset()
+        ro.collect(pol, graph=graph)
+        outs.append((ro.buf.boards.clone(), ro.buf.actions.clone(), ro.buf.logp.clone(), ro.buf.value.clone()))
+    for o in outs[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(outs[0], o))
