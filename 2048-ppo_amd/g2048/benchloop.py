@@ -49,7 +49,7 @@ def bench_train(args, rank: int, world: int, dev) -> dict:
         "iters": args.train_iters, "warmup": args.train_warmup,
         "config": {"workload": "65536 envs/GPU MLP h=196 bf16: rollout + RTG/entropy + PPO update",
                    "envs_per_gpu": args.envs, "horizon": args.train_horizon, "minibatch": args.train_batch,
-                   "minibatches_per_iter": n_mb, "optimizer": "Muon(2-D)+AdamW(1-D)", "dtype": "bf16 autocast"},
+                   "minibatches_per_iter": n_mb, "optimizer": "Muon(2-D)+AdamW(1-D)", "dtype": "bf16 activations / fp32 master weights (MFMA kernels)"},
         "phase_ms_one_iter": {k: round(v, 3) for k, v in tr.timings.items()},
         "last_metrics": {k: m[k] for k in ("loss", "entropy", "avg_score", "episodes_finished", "grad_norm")},
     }

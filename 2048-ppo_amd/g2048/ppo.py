@@ -9,7 +9,9 @@ Per minibatch (same math as the reference):
   KL(old || new) diagnostic on a no-grad re-forward (train mode, as in the reference) :578-601
 Differences by design: minibatches are gathered on the device from the flat [T*N] trajectory with
 a device permutation (no DataLoader, no per-sample Python), statistics stay on the device (one
-host sync per train step), and the forward runs under bf16 autocast on MI355X.
+host sync per train step), and the forward runs under bf16 autocast on MI355X.  For the
+reference's GameMLP the trainer uses fastmlp.FusedPPOUpdater instead: the same step written out
+as MFMA / fused kernels.
 """
 
 from __future__ import annotations

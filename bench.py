@@ -229,6 +229,23 @@ def _c_chunk(args):
     return cnt
 
 
+PMC_PROFILE = Path(__file__).resolve().parent / "profiles" / "r01c"
+
+
+def pmc_traffic(kernel: str, args):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes of this bench at its
+    default configuration (tools/profile.sh -> tools/summarize_profile.py: 2 x FETCH_SIZE +
+    WRITE_SIZE, the gfx950 FETCH correction).  None when this run's configuration differs."""
+    f = PMC_PROFILE / "pmc_summary.json"
+    if not f.exists() or args.envs != 65536 or args.chunk != 64:
+        return None, None
+    import json as _json
+    e = _json.loads(f.read_text()).get(kernel, {})
+    b = e.get("hbm_bytes_per_dispatch")
+    return (float(b), f"{f.relative_to(Path(__file__).resolve().parent)} (rocprofv3 --pmc FETCH_SIZE / "
+                      "WRITE_SIZE passes of tools/profile.sh; 2 x FETCH + WRITE)") if b else (None, None)
+
+
 def main():
     args = parse()
     import torch
@@ -249,6 +266,7 @@ def main():
     avg_launch = ev / args.steps
     achieved = rb.bytes_per_launch() / avg_launch / 1e9
 
+    traffic, traffic_src = pmc_traffic("env_rollout_kernel", args)
     result = {
         "metric": "env-steps/sec (whole node) at 65536 parallel 4x4 boards, 1/2/4/8 MI355X",
         "value": value,
@@ -266,7 +284,8 @@ def main():
                    "boards_per_gpu": args.envs, "env_steps_per_step": args.envs * args.chunk,
                    "parallelism": f"env-shard x{world} (no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "env_rollout_kernel",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_unit": "B/launch",
+                     "traffic_source": traffic_src, "kernel": "env_rollout_kernel",
                      "avg_launch_us": avg_launch * 1e6, "event_ms_max_rank": ev_max * 1e3,
                      "bytes_per_launch": rb.bytes_per_launch()},
     }
