@@ -499,8 +499,8 @@ def test_fused_update_tracks_autograd_update_with_dropout(dev):
 
 @pytest.mark.parametrize("h,n", [(196, 65536), (64, 1000), (192, 4097)])
 def test_fused_policy_matches_module(dev, h, n):
-    """FusedPolicy (MFMA layers + heads) == the bf16 eval-mode module (InferencePolicy) and tracks
-    the fp32 reference forward (game.py:1145-1220)."""
+    """FusedPolicy (MFMA layers + heads) tracks the fp32 reference forward (game.py:1145-1220) as
+    closely as the bf16 eval-mode module (InferencePolicy) does."""
     import agent
     from g2048 import _lib as L
     from g2048.rollout import FusedPolicy, InferencePolicy
@@ -519,14 +519,12 @@ def test_fused_policy_matches_module(dev, h, n):
     m.eval()
     with torch.no_grad():
         l32, v32 = m(obs.float())
-    # two bf16 evaluations of the same network: rounding-level differences, a few at the tail
-    for a, b in ((lf, lb), (vf, vb)):
-        d = (a - b).abs()
-        assert float(d.mean()) < 5e-3 and float(d.max()) < 0.1, (float(d.mean()), float(d.max()))
-    # bf16 vs the fp32 reference: the same order of error as torch's own bf16 module
-    err_f = float((lf - l32).abs().max())
-    err_b = float((lb - l32).abs().max())
-    assert err_f <= max(2 * err_b, 2e-2), (err_f, err_b)
+    v32 = v32.view(-1)
+    # both bf16 evaluations against the fp32 reference: FusedPolicy is as accurate as the bf16 module
+    for got, mod, ref in ((lf, lb, l32), (vf, vb, v32)):
+        e_f, e_b = (got - ref).abs(), (mod - ref).abs()
+        assert float(e_f.mean()) <= 1.5 * float(e_b.mean()) + 1e-3, (float(e_f.mean()), float(e_b.mean()))
+        assert float(e_f.max()) <= 2.0 * float(e_b.max()) + 2e-2, (float(e_f.max()), float(e_b.max()))
 
 
 def test_fused_policy_graph_rollout_matches_eager(dev):
