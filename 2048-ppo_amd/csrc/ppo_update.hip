@@ -965,6 +965,27 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const uint16_t *__restric
     }
 }
 
+
+// ------------------------------------------------------------------ minibatch statistics -----
+// The per-minibatch accumulation of model_optimize_step's returned statistics (train.py:603-642)
+// in one thread: stats[0..8] += {loss, policy_loss, entropy_loss, value_loss, grad_norm, entropy,
+// kl_total, kl_average}, stats[8] = max(stats[8], kl_max); optionally bumps a device counter.
+__global__ void ppo_stats_kernel(const float *__restrict__ sums, const float *__restrict__ kl,
+                                 const float *__restrict__ gn, const float *__restrict__ beta, float critic, float m,
+                                 float *__restrict__ stats, uint64_t *__restrict__ counter) {
+    const float s_ppo = sums[0] / m, s_ent = sums[1] / m, s_v = sums[2] / m, b = *beta;
+    stats[0] += -(s_ppo - critic * s_v + b * s_ent);
+    stats[1] += -s_ppo;
+    stats[2] += -b * s_ent;
+    stats[3] += critic * s_v;
+    stats[4] += *gn;
+    stats[5] += s_ent;
+    stats[6] += kl[0];
+    stats[7] += kl[0] / m;
+    stats[8] = fmaxf(stats[8], kl[1]);
+    if (counter) *counter += 1ull;
+}
+
 // ------------------------------------------------------------------ column sums --------------
 // Stage 1: grid (ceil(C/64), kSlices); block (64 columns x 4 row groups) sums rows of slice y.
 constexpr int kSlices = 32;
@@ -1331,6 +1352,15 @@ int g2048_head_fwd(g2048_stream_t stream, const uint16_t *x, const float *wa, co
         G2048_HF(1) G2048_HF(2) G2048_HF(3) G2048_HF(4) G2048_HF(5) G2048_HF(6) G2048_HF(7) G2048_HF(8)
 #undef G2048_HF
     }
+    return status();
+}
+
+
+int g2048_ppo_stats(g2048_stream_t stream, const float *sums, const float *kl, const float *grad_norm,
+                    const float *beta_dev, float critic, int64_t m, float *stats, uint64_t *counter) {
+    if (!sums || !kl || !grad_norm || !beta_dev || !stats || m <= 0) return G2048_EINVAL;
+    hipLaunchKernelGGL(ppo_stats_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, sums, kl, grad_norm, beta_dev,
+                       critic, (float)m, stats, counter);
     return status();
 }
 

@@ -32,7 +32,7 @@ EXPORTED = (
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask",
     "g2048_wgrad_partials", "g2048_wgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
-    "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd",
+    "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
 )
 
 
@@ -139,6 +139,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_mlp_fwd_lds_bytes": (sz, [i32, i32]),
         "g2048_mlp_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, i64, i32, i32, dp]),
         "g2048_head_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, vp, i64, vp]),
+        "g2048_ppo_stats": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_float, i64, vp, vp]),
         "g2048_muon_supported": (ctypes.c_int, [i32, i32]),
         "g2048_muon_step": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.POINTER(MuonCfg)]),
         "g2048_adamw_step": (ctypes.c_int, [vp, ctypes.POINTER(AdamWGroup), i32, vp, vp, vp, ctypes.c_float,
@@ -405,3 +406,10 @@ def head_fwd(x, wa, ba, wv, bv, logits, value):
         _stream(x), _dev(x, torch.bfloat16, "x"), _dev(wa, torch.float32, "wa"), _dev(ba, torch.float32, "ba"),
         _dev(wv, torch.float32, "wv"), _dev(bv, torch.float32, "bv"), m, h, ctypes.c_void_p(logits.data_ptr()),
         logits.stride(0), _dev(value, torch.float32, "value")), "g2048_head_fwd")
+
+
+def ppo_stats(sums, kl, grad_norm, beta_dev, critic: float, m: int, stats, counter=None):
+    _check(load().g2048_ppo_stats(_stream(stats), _dev(sums, torch.float32, "sums"), _dev(kl, torch.float32, "kl"),
+                                  _dev(grad_norm, torch.float32, "grad_norm"), _dev(beta_dev, torch.float32, "beta"),
+                                  float(critic), int(m), _dev(stats, torch.float32, "stats"),
+                                  _dev(counter, torch.int64, "counter")), "g2048_ppo_stats")

@@ -155,7 +155,6 @@ class FusedPPOUpdater(PPOUpdater):
     def _pre(self, idx, data, beta, encode):
         if idx.shape[0] != self.bs:  # ragged last minibatch of an eager pass
             self._alloc(idx.shape[0])
-        self.counter.add_(1)
         self.forward_features(data["boards"], idx, 0)
         self.loss_backward(data, idx, beta)
         return {}
@@ -171,13 +170,11 @@ class FusedPPOUpdater(PPOUpdater):
         with torch.no_grad():
             x = self._layers(1)  # KL re-forward of the same minibatch (x0 still holds its encoding)
             L.ppo_head_kl(x, self.wa, self.ba, self.masked, self.partials, self.kl)
-            s_ppo, s_ent, s_v = self.sums[0] / m, self.sums[1] / m, self.sums[2] / m
-            b = beta if torch.is_tensor(beta) else torch.tensor(beta, device=self.dev)
-            vals = torch.stack([-(s_ppo - cfg.critic * s_v + b * s_ent), -s_ppo, -b * s_ent, cfg.critic * s_v, gn,
-                                s_ent, self.kl[0], self.kl[0] / m, torch.zeros((), device=self.dev)])
-            self.stats.add_(vals)
-            k = STAT_KEYS.index("kl_max")
-            self.stats[k] = torch.maximum(self.stats[k], self.kl[1])
+            b = beta if torch.is_tensor(beta) else torch.tensor(float(beta), device=self.dev)
+            if gn.dim() != 0:
+                gn = gn.reshape(())
+            # one launch: the statistics of this minibatch, and the next minibatch's dropout counter
+            L.ppo_stats(self.sums, self.kl, gn.float().contiguous(), b, cfg.critic, m, self.stats, self.counter)
 
     def _extra_snapshot(self):
         return self.counter.clone()

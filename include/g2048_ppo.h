@@ -114,6 +114,13 @@ int g2048_ppo_head_loss(g2048_stream_t stream, const uint16_t *x, const float *w
 int g2048_ppo_head_kl(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, int64_t m,
                       int32_t h, const float *old_masked, float *partials, float *out);
 
+/* Accumulates one minibatch into the update statistics (train.py:603-642): stats[0..7] +=
+ * {loss, policy_loss, entropy_loss, value_loss, grad_norm, entropy, kl_total, kl_average} from the
+ * head_loss sums, the KL {sum, max}, the pre-clip gradient norm and beta; stats[8] = max(stats[8],
+ * KL max).  counter (optional) is incremented (the next minibatch's dropout counter). */
+int g2048_ppo_stats(g2048_stream_t stream, const float *sums, const float *kl, const float *grad_norm,
+                    const float *beta_dev, float critic, int64_t m, float *stats, uint64_t *counter);
+
 /* Scratch floats of g2048_wgrad for (m, n1, n2); 0 when the shape is unsupported. */
 size_t g2048_wgrad_partials(int64_t m, int32_t n1, int32_t n2);
 
