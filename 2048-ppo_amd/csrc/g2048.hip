@@ -603,6 +603,43 @@ __global__ void rtg_finalize_kernel(double *state, const double *part, double be
     state[3] = state[3] + 1.0;
 }
 
+
+// Episode bookkeeping of a fixed-horizon rollout (the score / max-tile statistics of
+// compute_batch_stats, train.py:1040-1120): per env, walk t = 0..T-1 carrying the running score and
+// max tile of the current game across rollouts; where step t ends a game, emit (score, max tile
+// exponent), else -1.  One thread per env, time-major reads.
+__global__ __launch_bounds__(kBlock) void episode_scan_kernel(const int32_t *__restrict__ points,
+                                                              const uint4 *__restrict__ boards,
+                                                              const int8_t *__restrict__ max_tile,
+                                                              const uint8_t *__restrict__ step_flags, int64_t T,
+                                                              int64_t n, int64_t *__restrict__ run_score,
+                                                              int32_t *__restrict__ run_max,
+                                                              int64_t *__restrict__ scores, int32_t *__restrict__ tiles) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n) return;
+    int64_t rs = run_score[e];
+    int32_t rm = run_max[e];
+    for (int64_t t = 0; t < T; t++) {
+        const int64_t k = t * n + e;
+        rs += points[k];
+        uint4 b = boards[k];
+        uint32_t m = bytemax(bytemax(b.x, b.y), bytemax(b.z, b.w));
+        m = bytemax(m, m >> 8);
+        m = bytemax(m, m >> 16);
+        rm = max(rm, max((int32_t)(m & 0xFFu), (int32_t)max_tile[k]));
+        const uint8_t f = step_flags[k];
+        const bool done = (f & FLAG_DONE) && !(f & FLAG_INACTIVE);
+        scores[k] = done ? rs : -1;
+        tiles[k] = done ? rm : -1;
+        if (done) {
+            rs = 0;
+            rm = 0;
+        }
+    }
+    run_score[e] = rs;
+    run_max[e] = rm;
+}
+
 inline int launch_status() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK : (int)e;
@@ -778,6 +815,18 @@ int g2048_reward_rtg(g2048_stream_t stream, const int32_t *points, const int8_t 
 int g2048_rtg_finalize(g2048_stream_t stream, double *state, const double *partials, const g2048_reward_cfg *cfg) {
     if (!state || !partials || !cfg) return G2048_EINVAL;
     hipLaunchKernelGGL(rtg_finalize_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, state, partials, cfg->beta);
+    return launch_status();
+}
+
+int g2048_episode_scan(g2048_stream_t stream, const int32_t *points, const int8_t *boards, const int8_t *max_tile,
+                       const uint8_t *step_flags, int64_t T, int64_t n, int64_t *run_score, int32_t *run_max,
+                       int64_t *scores, int32_t *tiles) {
+    if (T < 0 || n < 0 || !points || !boards || !max_tile || !step_flags || !run_score || !run_max || !scores || !tiles)
+        return G2048_EINVAL;
+    if (!aligned16(boards)) return G2048_EINVAL;
+    if (n == 0 || T == 0) return G2048_OK;
+    hipLaunchKernelGGL(episode_scan_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, (hipStream_t)stream, points,
+                       (const uint4 *)boards, max_tile, step_flags, T, n, run_score, run_max, scores, tiles);
     return launch_status();
 }
 

@@ -26,7 +26,7 @@ EXPORTED = (
     "g2048_mt_state_words", "g2048_mt_seed", "g2048_env_reset", "g2048_env_step", "g2048_env_rollout_random",
     "g2048_preview_points", "g2048_legal_mask",
     "g2048_obs_encode", "g2048_sample_actions", "g2048_rtg_prepare", "g2048_reward_rtg_workspace_bytes",
-    "g2048_reward_rtg", "g2048_rtg_finalize", "g2048_build_info",
+    "g2048_reward_rtg", "g2048_rtg_finalize", "g2048_build_info", "g2048_episode_scan",
     # include/g2048_ppo.h
     "g2048_obs_gather", "g2048_ln_act_fwd", "g2048_ln_act_bwd_partials", "g2048_ln_act_bwd",
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask",
@@ -124,6 +124,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_reward_rtg": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, cp, vp, vp, vp, vp, vp, vp, sz]),
         "g2048_rtg_finalize": (ctypes.c_int, [vp, vp, vp, cp]),
         "g2048_build_info": (ctypes.c_char_p, []),
+        "g2048_episode_scan": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp]),
         "g2048_obs_gather": (ctypes.c_int, [vp, vp, vp, i64, vp]),
         "g2048_ln_act_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, dp]),
         "g2048_ln_act_bwd_partials": (sz, [i64, i32]),
@@ -262,6 +263,16 @@ def reward_rtg(points, pot, flags, value, state, g_raw, g_norm, adv, partials, w
         _dev(g_norm, torch.float32, "g_norm"), _dev(adv, torch.float32, "adv"),
         _dev(partials, torch.float64, "partials"), _dev(workspace, torch.uint8, "workspace"), workspace.numel()),
         "g2048_reward_rtg")
+
+
+def episode_scan(points, boards, max_tile, step_flags, run_score, run_max, scores, tiles):
+    """points/max_tile/step_flags [T, n], boards [T, n, 16]; run_score int64 / run_max int32 [n] carried."""
+    T, n = points.shape[0], points.shape[1]
+    _check(load().g2048_episode_scan(
+        _stream(points), _dev(points, torch.int32, "points"), _dev(boards, torch.int8, "boards"),
+        _dev(max_tile, torch.int8, "max_tile"), _dev(step_flags, torch.uint8, "step_flags"), T, n,
+        _dev(run_score, torch.int64, "run_score"), _dev(run_max, torch.int32, "run_max"),
+        _dev(scores, torch.int64, "scores"), _dev(tiles, torch.int32, "tiles")), "g2048_episode_scan")
 
 
 def rtg_finalize(state, partials, cfg: RewardCfg):

@@ -237,29 +237,21 @@ class VecTrainer:
 
     # ------------------------------------------------------------------ metrics ---------------
     def _episode_stats(self, T):
-        """Per-episode (score, max tile exponent) of the games that finished in this rollout."""
+        """(scores, max tile exponents, finished mask) of the games that end in this rollout, as dense
+        device tensors (no compaction, no host sync): g2048_episode_scan carries each env's running
+        score / max tile across rollouts in fixed-horizon mode."""
         b = self.rollout.buf
         sf = b.step_flags[:T]
-        done = ((sf & L.FLAG_DONE) != 0) & ((sf & L.FLAG_INACTIVE) == 0)
-        scores, tiles = [], []
         if self.episodic:
             pts = torch.where((sf & L.FLAG_INACTIVE) == 0, b.points[:T], 0).sum(0)
             mx = b.boards[T].max(dim=1).values.to(torch.int32)
             return pts, mx, torch.ones_like(pts, dtype=torch.bool)
-        rs, rm = self.run_score, self.run_maxexp
-        for t in range(T):
-            rs += b.points[t]
-            rm = torch.maximum(rm, torch.maximum(b.boards[t].max(dim=1).values.to(torch.int32),
-                                                 b.max_tile[t].to(torch.int32)))
-            d = done[t]
-            scores.append(torch.where(d, rs, -1))
-            tiles.append(torch.where(d, rm, -1))
-            rs = torch.where(d, 0, rs)
-            rm = torch.where(d, 0, rm)
-        self.run_score, self.run_maxexp = rs, rm
-        s, m = torch.stack(scores), torch.stack(tiles)
-        fin = s >= 0
-        return s[fin], m[fin], None
+        if getattr(self, "_ep_scores", None) is None or self._ep_scores.shape[0] != T:
+            self._ep_scores = torch.empty(T, self.rollout.n, dtype=torch.int64, device=self.dev)
+            self._ep_tiles = torch.empty(T, self.rollout.n, dtype=torch.int32, device=self.dev)
+        L.episode_scan(b.points[:T], b.boards[:T], b.max_tile[:T], sf, self.run_score, self.run_maxexp,
+                       self._ep_scores, self._ep_tiles)
+        return self._ep_scores, self._ep_tiles, self._ep_scores >= 0
 
     def _metrics(self, T, valid, ustats) -> dict:
         b, w = self.rollout.buf, self.weights
@@ -279,22 +271,27 @@ class VecTrainer:
             starts[0] = True
         else:
             starts[1:] = (sf[:-1] & L.FLAG_RESET) != 0
-        g0 = b.g_raw[:T][starts]
-        scores, tiles, _ = self._episode_stats(T)
+        g0 = (b.g_raw[:T] * starts).sum() / starts.sum().clamp(min=1)  # mean return of episode starts
+        scores, tiles, fin = self._episode_stats(T)
         dev = self.dev
-        zero = torch.zeros((), device=dev)
+        s_flat = torch.where(fin, scores, -1).reshape(-1).to(torch.int32)
+        cnt = fin.sum()
+        cntf = cnt.float().clamp(min=1.0)
+        # median without compaction: finished scores sort to the top of the -1 filler
+        srt = torch.sort(s_flat).values
+        med_idx = (s_flat.numel() - cnt + (cnt - 1).clamp(min=0) // 2).clamp(max=s_flat.numel() - 1)
         vec = torch.stack([
             torch.tensor(float(r.numel()), device=dev), r.mean(), r.var(unbiased=False), (r == 0).float().mean() * 100,
             a.mean(), a.var(unbiased=False), a.pow(2).sum().sqrt(), a.min(), a.max(),
             gn.mean(), gn.std(unbiased=False), gn.min(), gn.max(), gr.std(unbiased=False), v.std(unbiased=False),
-            g0.mean() if g0.numel() else zero,
-            scores.float().mean() if scores.numel() else zero,
-            scores.float().median() if scores.numel() else zero,
-            scores.max().float() if scores.numel() else zero,
-            (tiles >= 9).float().mean() * 100 if tiles.numel() else zero,
-            (tiles >= 10).float().mean() * 100 if tiles.numel() else zero,
-            (tiles >= 11).float().mean() * 100 if tiles.numel() else zero,
-            torch.tensor(float(scores.numel()), device=dev),
+            g0,
+            torch.where(fin, scores, 0).sum().float() / cntf,
+            srt[med_idx].float(),
+            s_flat.max().float(),
+            (fin & (tiles >= 9)).sum().float() / cntf * 100,
+            (fin & (tiles >= 10)).sum().float() / cntf * 100,
+            (fin & (tiles >= 11)).sum().float() / cntf * 100,
+            cnt.float(),
             *[ustats[k] for k in ("loss", "policy_loss", "entropy_loss", "value_loss", "grad_norm", "entropy",
                                   "kl_total", "kl_average", "kl_max")],
         ]).tolist()  # the one host synchronisation of the train step

@@ -165,6 +165,15 @@ int g2048_reward_rtg(g2048_stream_t stream, const int32_t *points, const int8_t 
                      float *adv, double *partials, void *workspace, size_t workspace_bytes);
 
 /* EMA moment update with the batch statistics (train.py:898-901); advances rtg_step. */
+/* Episode statistics of a fixed-horizon rollout (compute_batch_stats' scores and tiles,
+ * train.py:1040-1120): per env, the running score / max tile exponent of its current game is
+ * carried across calls in run_score [n] / run_max [n]; scores[t][e] / tiles[t][e] are the finished
+ * game's final score and max tile where step t ends a game (FLAG_DONE, not INACTIVE), else -1.
+ * points / max_tile / step_flags [T][n]; boards [T][n][16] (the board before each step). */
+int g2048_episode_scan(g2048_stream_t stream, const int32_t *points, const int8_t *boards, const int8_t *max_tile,
+                       const uint8_t *step_flags, int64_t T, int64_t n, int64_t *run_score, int32_t *run_max,
+                       int64_t *scores, int32_t *tiles);
+
 int g2048_rtg_finalize(g2048_stream_t stream, double *state, const double *partials,
                        const g2048_reward_cfg *cfg);
 

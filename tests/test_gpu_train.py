@@ -308,3 +308,33 @@ def test_graphed_update_equals_eager_update(dev):
     np.testing.assert_allclose(out[0][0], out[1][0], rtol=1e-5, atol=1e-6)
     for k in ("loss", "entropy", "grad_norm", "kl_average"):
         assert math.isclose(out[0][1][k], out[1][1][k], rel_tol=1e-4, abs_tol=1e-6), k
+
+
+def test_episode_scan_matches_loop(dev):
+    """g2048_episode_scan == the per-step torch loop it replaced (scores / max tiles of finished games,
+    running state carried across two rollouts)."""
+    from g2048 import _lib as L
+    g = np.random.default_rng(3)
+    T, n = 40, 3000
+    pts = torch.from_numpy(g.integers(0, 64, size=(T, n)).astype(np.int32)).to(dev)
+    boards = torch.from_numpy(g.integers(0, 12, size=(T, n, 16)).astype(np.int8)).to(dev)
+    mt = torch.from_numpy(g.integers(0, 13, size=(T, n)).astype(np.int8)).to(dev)
+    fl = torch.from_numpy(np.where(g.random((T, n)) < 0.05, 0x80, 0).astype(np.uint8)
+                          | np.where(g.random((T, n)) < 0.02, 0x40, 0).astype(np.uint8)).to(dev)
+    rs = torch.zeros(n, dtype=torch.int64, device=dev)
+    rm = torch.zeros(n, dtype=torch.int32, device=dev)
+    rs2, rm2 = rs.clone(), rm.clone()
+    for _ in range(2):
+        sc = torch.empty(T, n, dtype=torch.int64, device=dev)
+        ti = torch.empty(T, n, dtype=torch.int32, device=dev)
+        L.episode_scan(pts, boards, mt, fl, rs, rm, sc, ti)
+        done = ((fl & 0x80) != 0) & ((fl & 0x40) == 0)
+        for t in range(T):
+            rs2 += pts[t]
+            rm2 = torch.maximum(rm2, torch.maximum(boards[t].max(dim=1).values.to(torch.int32), mt[t].to(torch.int32)))
+            d = done[t]
+            assert torch.equal(sc[t], torch.where(d, rs2, -1))
+            assert torch.equal(ti[t], torch.where(d, rm2, -1))
+            rs2 = torch.where(d, 0, rs2)
+            rm2 = torch.where(d, 0, rm2)
+        assert torch.equal(rs, rs2) and torch.equal(rm, rm2)
