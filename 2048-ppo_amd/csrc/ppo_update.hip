@@ -32,12 +32,15 @@ constexpr float kLnEps = 1e-5f;
 
 __device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
 
-__device__ __forceinline__ uint32_t f2bf(float f) {  // round to nearest even, NaN stays NaN
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7FFFFFFFu) > 0x7F800000u) return 0x7FC0u;
-    u += 0x7FFFu + ((u >> 16) & 1u);
-    return u >> 16;
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// round-to-nearest-even float -> bf16 pair on the hardware converter (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+    const bf16x2_t v = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
 }
+
+__device__ __forceinline__ uint32_t f2bf(float f) { return pack_bf2(f, 0.0f) & 0xFFFFu; }
 
 __device__ __forceinline__ void load_bf4(const uint16_t *p, float v[4]) {
     const uint2 q = *reinterpret_cast<const uint2 *>(p);
@@ -48,10 +51,7 @@ __device__ __forceinline__ void load_bf4(const uint16_t *p, float v[4]) {
 }
 
 __device__ __forceinline__ void store_bf4(uint16_t *p, const float v[4]) {
-    uint2 q;
-    q.x = f2bf(v[0]) | (f2bf(v[1]) << 16);
-    q.y = f2bf(v[2]) | (f2bf(v[3]) << 16);
-    *reinterpret_cast<uint2 *>(p) = q;
+    *reinterpret_cast<uint2 *>(p) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
 }
 
 __device__ __forceinline__ void store_bf4(uint16_t *p, const __attribute__((ext_vector_type(4))) float &v) {
@@ -72,7 +72,7 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 struct DropArgs {
-    uint32_t thr;       // keep iff draw >= thr  (thr = round(p 2^32))
+    uint32_t thr;       // keep iff 16-bit draw >= thr  (thr = round(p 2^16))
     float scale;        // 1 / (1 - p)
     uint32_t c1base;    // layer << 12 | pass << 20
     uint32_t k0, k1;    // seed
@@ -90,13 +90,32 @@ __device__ __forceinline__ Drop make_drop(const DropArgs &a) {
     return Drop{a.thr, a.c1base, (uint32_t)c, (uint32_t)(c >> 32), a.k0, a.k1, a.scale};
 }
 
+// One Philox4x32-10 call gives 8 16-bit uniforms: the keep draws of column groups cg and cg ^ 4
+// (cg = 8a + 4h + b shares the call (a, b); h picks the half), so a lane that owns both -- the
+// fused forward's layout -- draws once per two groups.
+__device__ __forceinline__ uint4 drop_draw4(const Drop &d, uint32_t row, uint32_t cg) {
+    const uint32_t pair = ((cg >> 3) << 2) | (cg & 3u);
+    return philox(row, pair | d.c1base, d.c2, d.c3, d.k0, d.k1);
+}
+
+__device__ __forceinline__ uint2 drop_half(const uint4 &r, uint32_t cg) {
+    return (cg & 4u) ? make_uint2(r.z, r.w) : make_uint2(r.x, r.y);
+}
+
+__device__ __forceinline__ uint2 drop_draw(const Drop &d, uint32_t row, uint32_t cg) {
+    return drop_half(drop_draw4(d, row, cg), cg);
+}
+
+__device__ __forceinline__ void drop_mult_bits(const Drop &d, uint2 w, float k[4]) {
+    k[0] = (w.x & 0xFFFFu) >= d.thr ? d.scale : 0.0f;
+    k[1] = (w.x >> 16) >= d.thr ? d.scale : 0.0f;
+    k[2] = (w.y & 0xFFFFu) >= d.thr ? d.scale : 0.0f;
+    k[3] = (w.y >> 16) >= d.thr ? d.scale : 0.0f;
+}
+
 // keep multipliers (0 or 1/(1-p)) of columns 4cg .. 4cg+3 of `row`
 __device__ __forceinline__ void drop_mult(const Drop &d, uint32_t row, uint32_t cg, float k[4]) {
-    const uint4 r = philox(row, cg | d.c1base, d.c2, d.c3, d.k0, d.k1);
-    k[0] = r.x >= d.thr ? d.scale : 0.0f;
-    k[1] = r.y >= d.thr ? d.scale : 0.0f;
-    k[2] = r.z >= d.thr ? d.scale : 0.0f;
-    k[3] = r.w >= d.thr ? d.scale : 0.0f;
+    drop_mult_bits(d, drop_draw(d, row, cg), k);
 }
 
 __constant__ float kThirds[4] = {0.0f, 1.0f / 3.0f, 2.0f / 3.0f, 1.0f};
@@ -777,7 +796,17 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t *__res
 // of the GEMM's X + G plus the separate LayerNorm pass's G + X + Y.
 constexpr int kMfWaves = 4;
 constexpr int kMfThreads = 64 * kMfWaves;
-constexpr int kMfMT = 1;  // 16-row tiles per wave: a block covers 64 rows
+constexpr int kMfRows = 16 * kMfWaves;  // rows per slab: a 16-row MFMA tile per wave
+constexpr int kMfItems = 16;            // 8-byte staging chunks per thread per slab (K <= 256)
+
+// LDS row pitch (bytes) of a bf16 image with kp columns: 16 rows read at the same column by a
+// 16-byte fragment load fall into 16 distinct 4-bank groups when pitch/4 is an odd multiple of 4.
+__host__ __device__ inline int mf_pitch(int kp) {
+    int dw = (kp + 1) / 2;
+    dw = (dw + 3) & ~3;
+    if (((dw >> 2) & 1) == 0) dw += 4;
+    return dw * 4;
+}
 
 template <int NT, bool RES, bool DROP>
 __global__ __launch_bounds__(kMfThreads) void mlp_fwd_kernel(const uint16_t *__restrict__ X,
@@ -788,127 +817,162 @@ __global__ __launch_bounds__(kMfThreads) void mlp_fwd_kernel(const uint16_t *__r
                                                              float *__restrict__ rstd_out, int64_t M, int N, int K,
                                                              DropArgs da) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int kp = (K + 7) & ~7, pw = kp * 2;  // W image: N rows of kp bf16
+    const int kp = (K + 7) & ~7, pw = mf_pitch(kp);  // W image: N rows, zero K padding
     char *sW = smem;
-    char *zero = smem + ((N * pw + 15) & ~15);
+    char *sX0 = smem + ((N * pw + 15) & ~15);       // two 64-row X slabs (double buffer)
+    const int xbytes = kMfRows * pw;
+    char *zero = sX0 + 2 * xbytes;
     float *sgb = reinterpret_cast<float *>(zero + 64);  // gamma[N], beta[N]
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, col = lane & 15;
-    // stage W (rows of kp with zero K padding): a wave per row, a lane per 8-byte chunk (kp <= 256)
-    for (int n = wave; n < N; n += kMfWaves) {
-        if (lane < (kp >> 2)) {
-            const uint2 v = 4 * lane < K ? *reinterpret_cast<const uint2 *>(W + (int64_t)n * K + 4 * lane)
-                                         : make_uint2(0u, 0u);
-            *reinterpret_cast<uint2 *>(sW + n * pw + 8 * lane) = v;
+    // zero everything once (K padding of W and of both X buffers must read as zero)
+    for (int o = tid * 16; o < (int)(zero - smem) + 64; o += kMfThreads * 16)
+        *reinterpret_cast<uint4 *>(smem + o) = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    {  // W is one contiguous span: 8-byte chunks, 16 loads in flight per thread per batch
+        const int q4w = K >> 2, nw = N * q4w;
+        for (int c0 = 0; c0 < nw; c0 += 16 * kMfThreads) {
+            uint2 v[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                const int c = c0 + tid + u * kMfThreads;
+                v[u] = c < nw ? *reinterpret_cast<const uint2 *>(W + 4 * (int64_t)c) : make_uint2(0u, 0u);
+            }
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                const int c = c0 + tid + u * kMfThreads;
+                if (c < nw) {
+                    const int r = c / q4w;
+                    *reinterpret_cast<uint2 *>(sW + r * pw + 8 * (c - r * q4w)) = v[u];
+                }
+            }
         }
     }
-    if (tid < 16) reinterpret_cast<uint32_t *>(zero)[tid] = 0u;
     for (int e = tid; e < N; e += kMfThreads) {
         sgb[e] = gamma[e];
         sgb[N + e] = beta[e];
     }
-    __syncthreads();
     const Drop d = make_drop(da);
     const float inv_n = 1.0f / (float)N;
-    const int64_t nblk = (M + 16 * kMfMT * kMfWaves - 1) / (16 * kMfMT * kMfWaves);
+    const int64_t nslab = (M + kMfRows - 1) / kMfRows;
 
-    for (int64_t mb = blockIdx.x; mb < nblk; mb += gridDim.x) {
-        const int64_t m0 = mb * (16 * kMfMT * kMfWaves) + wave * (16 * kMfMT);
-        f32x4_t acc[kMfMT][NT];
+    // staging of a slab: its rows are one contiguous span of X, read as 8-byte chunks
+    const int q4 = K >> 2, nchunk = kMfRows * q4;
+    int off[kMfItems];
 #pragma unroll
-        for (int t = 0; t < kMfMT; t++)
+    for (int u = 0; u < kMfItems; u++) {
+        const int c = tid + u * kMfThreads, r = c / q4;
+        off[u] = r * pw + 8 * (c - r * q4);
+    }
+    uint2 reg[kMfItems];
+    auto load = [&](int64_t slab) {
+        const uint16_t *src = X + slab * kMfRows * K;
+        const int64_t valid = (M - slab * kMfRows) * q4;  // chunks inside the matrix
 #pragma unroll
-            for (int n = 0; n < NT; n++) acc[t][n] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-        // X fragments (B operand: X^T[k][m] = X[m][k .. k+7]) straight from HBM, one k-step ahead
-        auto load_x = [&](int k0, bf16x8_t (&fx)[kMfMT]) {
-            const int kl = k0 + 8 * g;
+        for (int u = 0; u < kMfItems; u++) {
+            const int c = tid + u * kMfThreads;
+            reg[u] = (c < nchunk && c < valid) ? *reinterpret_cast<const uint2 *>(src + 4 * c) : make_uint2(0u, 0u);
+        }
+    };
+    auto store = [&](char *buf) {
 #pragma unroll
-            for (int t = 0; t < kMfMT; t++) {
-                const int64_t m = m0 + 16 * t + col;
-                uint4 w = make_uint4(0u, 0u, 0u, 0u);
-                if (m < M && kl < K) {
-                    const uint16_t *src = X + m * K + kl;
-                    const uint2 lo = *reinterpret_cast<const uint2 *>(src);
-                    const uint2 hi = kl + 8 <= K ? *reinterpret_cast<const uint2 *>(src + 4) : make_uint2(0u, 0u);
-                    w = make_uint4(lo.x, lo.y, hi.x, hi.y);  // K % 4 == 0: a K tail is one 4-element half
-                }
-                fx[t] = __builtin_bit_cast(bf16x8_t, w);
-            }
-        };
-        bf16x8_t fx[kMfMT];
-        load_x(0, fx);
+        for (int u = 0; u < kMfItems; u++) {
+            const int c = tid + u * kMfThreads;
+            if (c < nchunk) *reinterpret_cast<uint2 *>(buf + off[u]) = reg[u];
+        }
+    };
+    int64_t slab = blockIdx.x;
+    if (slab < nslab) {
+        load(slab);
+        store(sX0);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (; slab < nslab; slab += gridDim.x) {
+        const bool more = slab + gridDim.x < nslab;
+        if (more) load(slab + gridDim.x);  // next slab's HBM reads in flight during this slab
+        const char *sx = sX0 + cur * xbytes;
+        const char *xrow = sx + (wave * 16 + col) * pw;
+        f32x4_t acc[NT];
+#pragma unroll
+        for (int n = 0; n < NT; n++) acc[n] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
         for (int k0 = 0; k0 < kp; k0 += 32) {
             const int kl = k0 + 8 * g;
-            bf16x8_t nx[kMfMT];
-            if (k0 + 32 < kp) load_x(k0 + 32, nx);
+            const bf16x8_t fx =
+                __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(kl < kp ? xrow + 2 * kl : zero));
 #pragma unroll
-            for (int n = 0; n < NT; n++) {  // A operand: W[n][k .. k+7] from LDS
+            for (int n = 0; n < NT; n++) {  // A operand: W[n][k .. k+7]
                 const int row = 16 * n + col;
                 const char *pp = (row < N && kl < kp) ? sW + row * pw + 2 * kl : zero;
                 const bf16x8_t fw = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(pp));
-#pragma unroll
-                for (int t = 0; t < kMfMT; t++)
-                    acc[t][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw, fx[t], acc[t][n], 0, 0, 0);
-            }
-#pragma unroll
-            for (int t = 0; t < kMfMT; t++) fx[t] = nx[t];
-        }
-        // epilogue: lane holds row m = m0 + 16t + col, features 16n + 4g + r
-#pragma unroll
-        for (int t = 0; t < kMfMT; t++) {
-            const int64_t m = m0 + 16 * t + col;
-            float sum = 0.0f;
-#pragma unroll
-            for (int n = 0; n < NT; n++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const float v = (float)(__bf16)acc[t][n][r];  // G as stored (bf16)
-                    acc[t][n][r] = v;
-                    sum += 16 * n + 4 * g < N ? v : 0.0f;
-                }
-            sum += __shfl_xor(sum, 16);
-            sum += __shfl_xor(sum, 32);
-            const float mean = sum * inv_n;
-            float var = 0.0f;
-#pragma unroll
-            for (int n = 0; n < NT; n++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const float dv = 16 * n + 4 * g < N ? acc[t][n][r] - mean : 0.0f;
-                    var += dv * dv;
-                }
-            var += __shfl_xor(var, 16);
-            var += __shfl_xor(var, 32);
-            const float rstd = 1.0f / sqrtf(var * inv_n + kLnEps);
-            if (m < M) {
-                if (g == 0 && mean_out) {
-                    mean_out[m] = mean;
-                    rstd_out[m] = rstd;
-                }
-#pragma unroll
-                for (int n = 0; n < NT; n++) {
-                    const int f0 = 16 * n + 4 * g;
-                    if (f0 >= N) continue;
-                    const float4 ga = *reinterpret_cast<const float4 *>(sgb + f0);
-                    const float4 be = *reinterpret_cast<const float4 *>(sgb + N + f0);
-                    const float gg[4] = {ga.x, ga.y, ga.z, ga.w}, bb[4] = {be.x, be.y, be.z, be.w};
-                    float k[4], rs[4], o[4];
-                    if (DROP) drop_mult(d, (uint32_t)m, (uint32_t)(f0 >> 2), k);
-                    if (RES) load_bf4(X + m * K + f0, rs);
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        float a = fmaxf((acc[t][n][r] - mean) * rstd * gg[r] + bb[r], 0.0f);
-                        if (DROP) a *= k[r];
-                        o[r] = RES ? rs[r] + a : a;
-                    }
-                    if (G) store_bf4(G + m * N + f0, acc[t][n]);
-                    store_bf4(Y + m * N + f0, o);
-                }
+                acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw, fx, acc[n], 0, 0, 0);
             }
         }
+        // epilogue: lane holds row m = slab*64 + 16*wave + col, features 16n + 4g + r
+        const int64_t m = slab * kMfRows + wave * 16 + col;
+        float sum = 0.0f;
+#pragma unroll
+        for (int n = 0; n < NT; n++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float v = (float)(__bf16)acc[n][r];  // G as stored (bf16)
+                acc[n][r] = v;
+                sum += 16 * n + 4 * g < N ? v : 0.0f;
+            }
+        sum += __shfl_xor(sum, 16);
+        sum += __shfl_xor(sum, 32);
+        const float mean = sum * inv_n;
+        float var = 0.0f;
+#pragma unroll
+        for (int n = 0; n < NT; n++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float dv = 16 * n + 4 * g < N ? acc[n][r] - mean : 0.0f;
+                var += dv * dv;
+            }
+        var += __shfl_xor(var, 16);
+        var += __shfl_xor(var, 32);
+        const float rstd = 1.0f / sqrtf(var * inv_n + kLnEps);
+        if (m < M) {
+            if (g == 0 && mean_out) {
+                mean_out[m] = mean;
+                rstd_out[m] = rstd;
+            }
+            uint4 dpair = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int n = 0; n < NT; n++) {
+                const int f0 = 16 * n + 4 * g;
+                if (f0 >= N) continue;
+                const float4 ga = *reinterpret_cast<const float4 *>(sgb + f0);
+                const float4 be = *reinterpret_cast<const float4 *>(sgb + N + f0);
+                const float gg[4] = {ga.x, ga.y, ga.z, ga.w}, bb[4] = {be.x, be.y, be.z, be.w};
+                float k[4], rs[4], o[4];
+                if (DROP) {  // tiles n, n+1 hold column groups 4n+g, 4n+4+g: one Philox call
+                    if ((n & 1) == 0) dpair = drop_draw4(d, (uint32_t)m, (uint32_t)(f0 >> 2));
+                    drop_mult_bits(d, drop_half(dpair, (uint32_t)(f0 >> 2)), k);
+                }
+                if (RES) {  // the residual is this layer's input, already in LDS
+                    const uint2 w = *reinterpret_cast<const uint2 *>(xrow + 2 * f0);
+                    rs[0] = bf2f(w.x & 0xFFFFu);
+                    rs[1] = bf2f(w.x >> 16);
+                    rs[2] = bf2f(w.y & 0xFFFFu);
+                    rs[3] = bf2f(w.y >> 16);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    float a = fmaxf((acc[n][r] - mean) * rstd * gg[r] + bb[r], 0.0f);
+                    if (DROP) a *= k[r];
+                    o[r] = RES ? rs[r] + a : a;
+                }
+                if (G) store_bf4(G + m * N + f0, acc[n]);
+                store_bf4(Y + m * N + f0, o);
+            }
+        }
+        if (more) store(sX0 + (cur ^ 1) * xbytes);  // the other buffer: last read one slab ago
+        __syncthreads();
+        cur ^= 1;
     }
 }
-
 
 // ------------------------------------------------------------------ policy / value heads -----
 // logits = x Wa^T + ba, value = x Wv^T + bv for the rollout policy (GameMLP.forward, game.py:
@@ -1071,8 +1135,8 @@ inline DropArgs drop_args(const g2048_dropout *d) {
     a.thr = 0;
     a.scale = 1.0f;
     if (d && d->p > 0.0f) {
-        const double t = (double)d->p * 4294967296.0;
-        a.thr = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)(t + 0.5);
+        const double t = (double)d->p * 65536.0;
+        a.thr = t >= 65536.0 ? 0x10000u : (uint32_t)(t + 0.5);
         a.scale = 1.0f / (1.0f - d->p);
         a.c1base = (d->layer << 12) | (d->pass << 20);
         a.k0 = (uint32_t)d->seed;
@@ -1287,8 +1351,9 @@ int g2048_wgrad(g2048_stream_t stream, const uint16_t *a, const uint16_t *b, int
 
 size_t g2048_mlp_fwd_lds_bytes(int32_t n, int32_t k) {
     if (n <= 0 || k <= 0 || n > 256 || k > 256 || n % 4 || k % 4) return 0;
-    const int kp = (k + 7) & ~7;
-    return (size_t)((n * kp * 2 + 15) & ~15) + 64 + (size_t)8 * n;
+    const int kp = (k + 7) & ~7, pw = mf_pitch(kp);
+    const size_t b = (size_t)((n * pw + 15) & ~15) + (size_t)2 * kMfRows * pw + 64 + (size_t)8 * n;
+    return b <= 160 * 1024 ? b : 0;
 }
 
 int g2048_mlp_fwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, const float *gamma, const float *beta,
@@ -1301,8 +1366,8 @@ int g2048_mlp_fwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, c
     if (m == 0) return G2048_OK;
     const hipStream_t s = (hipStream_t)stream;
     const DropArgs da = drop_args(drop);
-    const int64_t nblk = (m + 16 * kMfMT * kMfWaves - 1) / (16 * kMfMT * kMfWaves);
-    const dim3 grid((unsigned)(nblk > 1024 ? 1024 : nblk)), blk(kMfThreads);
+    const int64_t nslab = (m + kMfRows - 1) / kMfRows;
+    const dim3 grid((unsigned)(nslab > 256 ? 256 : nslab)), blk(kMfThreads);  // one persistent block per CU
     const bool dr = drop_on(drop);
     const int nt = (n + 15) / 16;
 #define G2048_MF_LAUNCH(NT_)                                                                                       \

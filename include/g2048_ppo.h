@@ -25,10 +25,12 @@
 extern "C" {
 #endif
 
-/* nn.Dropout(p) of a ResidualBlock (game.py:1033-1046), train mode.  The keep mask of element
- * (row, col) is a Philox4x32-10 draw keyed by `seed` with counter
- * {row, col/4 | layer << 12 | pass << 20, *counter_dev + counter} -- regenerated, never stored, so
- * the backward pass sees exactly the forward's mask.  p == 0 disables it. */
+/* nn.Dropout(p) of a ResidualBlock (game.py:1033-1046), train mode.  Element (row, col) of column
+ * group cg = col / 4 = 8a + 4h + b is kept iff its 16-bit uniform >= round(p 2^16), the uniforms
+ * being the 8 halves of one Philox4x32-10 draw keyed by `seed` with counter
+ * {row, (4a + b) | layer << 12 | pass << 20, *counter_dev + counter} (h picks words {x,y} or {z,w},
+ * col % 4 the half-word) -- regenerated, never stored, so the backward pass sees exactly the
+ * forward's mask.  p == 0 disables it. */
 typedef struct g2048_dropout {
     float p;
     uint32_t layer;
