@@ -691,37 +691,41 @@ __device__ __forceinline__ bf16x8_t wg_frag(const char *buf, int pitch, int kb, 
 template <int BI, int BJ>
 __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t *__restrict__ A, const uint16_t *__restrict__ B,
                                                            int64_t M, int n1, int n2, int pa, int pb, int wi_n,
-                                                           int64_t rows_per_block, float *__restrict__ part) {
+                                                           int64_t rows_per_block, int bw, float *__restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ti0 = (wave % wi_n) * BI, tj0 = (wave / wi_n) * BJ;  // wave-uniform: scalar branches
-    const int TI = (n1 + 15) >> 4, TJ = (n2 + 15) >> 4;
+    // blockIdx.y picks a band of bw output columns (B columns cb0 .. cb0 + w): more blocks in flight
+    const int cb0 = (int)blockIdx.y * bw, w = min(bw, n2 - cb0);
+    const int TI = (n1 + 15) >> 4, TJ = (w + 15) >> 4;
     const int stage_bytes = kWgRows * (pa + pb);
     for (int o = tid * 16; o < 2 * stage_bytes; o += kWgThreads * 16) *reinterpret_cast<uint4 *>(smem + o) = make_uint4(0, 0, 0, 0);
 
     // Staging: the 64 rows of a step are one contiguous span of A (and of B) in HBM, read as
     // 8-byte chunks c = tid + 256u; each chunk's LDS slot (row pitch pa / pb) is fixed per thread.
-    const int ga = n1 >> 2, gb = n2 >> 2, ca = kWgRows * ga, cb = kWgRows * gb;
+    const int ga = n1 >> 2, gb = w >> 2, ca = kWgRows * ga, cb = kWgRows * gb;
     const int64_t r_begin = (int64_t)blockIdx.x * rows_per_block;
     const int64_t r_end = min(M, r_begin + rows_per_block);
-    int offa[kWgItems], offb[kWgItems];
+    int offa[kWgItems], offb[kWgItems], srcb[kWgItems], rowb[kWgItems];
 #pragma unroll
     for (int u = 0; u < kWgItems; u++) {
         const int c = tid + u * kWgThreads;
-        const int ra = c / ga, rb = c / gb;
+        const int ra = c / ga, rb = c / gb, qb = c - rb * gb;
         offa[u] = ra * pa + 8 * (c - ra * ga);
-        offb[u] = kWgRows * pa + rb * pb + 8 * (c - rb * gb);
+        offb[u] = kWgRows * pa + rb * pb + 8 * qb;
+        srcb[u] = rb * n2 + cb0 + 4 * qb;  // element offset of the chunk from the step's first row
+        rowb[u] = rb;
     }
     uint2 rega[kWgItems], regb[kWgItems];
     auto load = [&](int64_t r0) {
         const char *sa = reinterpret_cast<const char *>(A + r0 * n1);
-        const char *sb = reinterpret_cast<const char *>(B + r0 * n2);
-        const int64_t va = (r_end - r0) * ga, vb = (r_end - r0) * gb;  // valid chunks
+        const uint16_t *sb = B + r0 * n2;
+        const int64_t va = (r_end - r0) * ga, vrows = r_end - r0;  // valid chunks / rows
 #pragma unroll
         for (int u = 0; u < kWgItems; u++) {
             const int c = tid + u * kWgThreads;
             rega[u] = (c < ca && c < va) ? *reinterpret_cast<const uint2 *>(sa + 8 * c) : make_uint2(0, 0);
-            regb[u] = (c < cb && c < vb) ? *reinterpret_cast<const uint2 *>(sb + 8 * c) : make_uint2(0, 0);
+            regb[u] = (c < cb && rowb[u] < vrows) ? *reinterpret_cast<const uint2 *>(sb + srcb[u]) : make_uint2(0, 0);
         }
     };
     auto store = [&](int s) {
@@ -750,21 +754,21 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t *__res
         const bool more = r0 + kWgRows < r_end;
         if (more) load(r0 + kWgRows);
         const char *ba = smem + s * stage_bytes, *bb = ba + kWgRows * pa;
+        if (ti0 < TI && tj0 < TJ) {  // wave-uniform; inside, every MFMA is unconditional (a guarded
+                                     // MFMA makes the compiler copy its accumulator out and wait)
 #pragma unroll
-        for (int kb = 0; kb < 2; kb++) {
-            bf16x8_t fa[BI], fb[BJ];
+            for (int kb = 0; kb < 2; kb++) {
+                bf16x8_t fb[BJ];
 #pragma unroll
-            for (int i = 0; i < BI; i++)
-                if (ti0 + i < TI) fa[i] = wg_frag(ba, pa, kb, 16 * (ti0 + i), lane);
+                for (int j = 0; j < BJ; j++) fb[j] = wg_frag(bb, pb, kb, 16 * (tj0 + j), lane);
 #pragma unroll
-            for (int j = 0; j < BJ; j++)
-                if (tj0 + j < TJ) fb[j] = wg_frag(bb, pb, kb, 16 * (tj0 + j), lane);
+                for (int i = 0; i < BI; i++) {
+                    const bf16x8_t fa = wg_frag(ba, pa, kb, 16 * (ti0 + i), lane);
 #pragma unroll
-            for (int i = 0; i < BI; i++)
-#pragma unroll
-                for (int j = 0; j < BJ; j++)
-                    if (ti0 + i < TI && tj0 + j < TJ)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < BJ; j++)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[j], acc[i][j], 0, 0, 0);
+                }
+            }
         }
         if (more) store(s ^ 1);
         __syncthreads();
@@ -776,8 +780,8 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t *__res
     for (int i = 0; i < BI; i++)
 #pragma unroll
         for (int j = 0; j < BJ; j++) {
-            const int ii = 16 * (ti0 + i) + rowq, jj = 16 * (tj0 + j) + col;
-            if (ti0 + i < TI && tj0 + j < TJ && jj < n2)
+            const int ii = 16 * (ti0 + i) + rowq, jj = cb0 + 16 * (tj0 + j) + col;
+            if (ti0 + i < TI && tj0 + j < TJ && jj < cb0 + w)
 #pragma unroll
                 for (int r = 0; r < 4; r++)
                     if (ii + r < n1) out[(int64_t)(ii + r) * n2 + jj] = acc[i][j][r];
@@ -1158,7 +1162,7 @@ int colsum(hipStream_t s, const float *part, int nb, int C, float *scratch2, con
 
 // weight-gradient launch geometry
 struct WgPlan {
-    int bi, bj, wi, nb, pa, pb;
+    int bi, bj, wi, nb, pa, pb, bw, ny;
     int64_t rows;
     size_t lds;
 };
@@ -1170,8 +1174,12 @@ inline int wg_pitch(int n) {  // LDS row bytes: >= 2 * pad16(n) and == 32 (mod 2
 
 inline bool wg_plan(int64_t m, int n1, int n2, WgPlan &p) {
     if (n1 <= 0 || n2 <= 0 || n1 % 4 || n2 % 4 || n1 > 224 || n2 > 224 || m <= 0) return false;
-    const int TI = (n1 + 15) / 16, TJ = (n2 + 15) / 16;
-    static const int menu[3][2] = {{2, 2}, {4, 4}, {7, 7}};
+    const int TI = (n1 + 15) / 16, TJ0 = (n2 + 15) / 16;
+    // split the output columns into ny bands of whole 16-column tiles when there are enough
+    // tiles: twice the blocks, each staging its band of B only
+    const int ny = TJ0 >= 4 ? 2 : 1;
+    const int TJ = (TJ0 + ny - 1) / ny;
+    static const int menu[3][2] = {{2, 2}, {4, 4}, {7, 4}};  // n <= 224: TI <= 14, TJ <= 7 after the split
     static const int arr[3][2] = {{2, 2}, {4, 1}, {1, 4}};
     for (auto &mb : menu)
         for (auto &a : arr)
@@ -1179,6 +1187,8 @@ inline bool wg_plan(int64_t m, int n1, int n2, WgPlan &p) {
                 p.bi = mb[0];
                 p.bj = mb[1];
                 p.wi = a[0];
+                p.ny = ny;
+                p.bw = 16 * TJ;
                 int64_t nb = m / 512;
                 nb = nb < 1 ? 1 : (nb > 256 ? 256 : nb);
                 int64_t rows = (m + nb - 1) / nb;
@@ -1186,7 +1196,7 @@ inline bool wg_plan(int64_t m, int n1, int n2, WgPlan &p) {
                 p.nb = (int)((m + rows - 1) / rows);
                 p.rows = rows;
                 p.pa = wg_pitch(n1);
-                p.pb = wg_pitch(n2);
+                p.pb = wg_pitch(p.bw < n2 ? p.bw : n2);
                 p.lds = (size_t)2 * kWgRows * (p.pa + p.pb);
                 return true;
             }
@@ -1332,13 +1342,16 @@ int g2048_wgrad(g2048_stream_t stream, const uint16_t *a, const uint16_t *b, int
     if (!a || !b || !partials || !out || !al(a, 8) || !al(b, 8)) return G2048_EINVAL;
     if (!wg_plan(m, n1, n2, p)) return G2048_EINVAL;
     const hipStream_t s = (hipStream_t)stream;
-    const dim3 grid(p.nb), blk(kWgThreads);
+    const dim3 grid(p.nb, p.ny), blk(kWgThreads);
     if (p.bi == 2)
-        hipLaunchKernelGGL((wgrad_kernel<2, 2>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, partials);
+        hipLaunchKernelGGL((wgrad_kernel<2, 2>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, p.bw,
+                           partials);
     else if (p.bi == 4)
-        hipLaunchKernelGGL((wgrad_kernel<4, 4>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, partials);
+        hipLaunchKernelGGL((wgrad_kernel<4, 4>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, p.bw,
+                           partials);
     else
-        hipLaunchKernelGGL((wgrad_kernel<7, 7>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, partials);
+        hipLaunchKernelGGL((wgrad_kernel<7, 4>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, p.bw,
+                           partials);
     const int st = status();
     if (st) return st;
     Segs segs{};
