@@ -4,8 +4,8 @@
 //   obs_gather_kernel     boards[idx] -> to_model_format (game.py:92-101), bf16 [m,48]
 //   ln_fwd_kernel<J,D>    y = res + Dropout(ReLU(LayerNorm(g)))          (ResidualBlock / stem)
 //   ln_bwd_kernel<J,D>    its backward: dg, the residual gradient, dgamma/dbeta partials
-//   head_loss_kernel<J>   action/value heads + PPO-clip loss + entropy + smooth-L1 + backward
-//   head_kl_kernel<J>     KL(old || new) of the post-step re-forward (train.py:578-601)
+//   head_loss_kernel<..>  action/value heads + PPO-clip loss + entropy + smooth-L1 + backward
+//   head_kl_kernel<..>    KL(old || new) of the post-step re-forward (train.py:578-601)
 //   mlp_fwd_kernel<NT,..> G = X W^T on bf16 MFMA + the LayerNorm/ReLU/dropout/residual epilogue
 //   head_fwd_kernel<KS>   rollout policy heads (logits + value) on MFMA
 //   wgrad_kernel<BI,BJ>   dW = dG^T X on bf16 MFMA (tall-skinny, K = minibatch rows)
@@ -33,6 +33,11 @@ constexpr float kLnEps = 1e-5f;
 __device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
 
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 // round-to-nearest-even float -> bf16 pair on the hardware converter (v_cvt_pk_bf16_f32)
 __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
@@ -41,6 +46,14 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
 }
 
 __device__ __forceinline__ uint32_t f2bf(float f) { return pack_bf2(f, 0.0f) & 0xFFFFu; }
+
+__device__ __forceinline__ void load_bf4_lds(const char *p, float v[4]) {
+    const uint2 t = *reinterpret_cast<const uint2 *>(p);
+    v[0] = __uint_as_float(t.x << 16);
+    v[1] = __uint_as_float(t.x & 0xFFFF0000u);
+    v[2] = __uint_as_float(t.y << 16);
+    v[3] = __uint_as_float(t.y & 0xFFFF0000u);
+}
 
 __device__ __forceinline__ void load_bf4(const uint16_t *p, float v[4]) {
     const uint2 q = *reinterpret_cast<const uint2 *>(p);
@@ -227,13 +240,19 @@ __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(const uint16_t *__rest
 }
 
 // ------------------------------------------------------------------ LayerNorm backward -------
+// The heads' contribution to dy, recomputed from their output gradient dz [m][8] (4 logits, value,
+// 3 pad): dy += dz[0:4] wa + dz[4] wv  (wv NULL = decoupled critic: the value branch is cut).
+struct HeadGrad {
+    const float *dz, *wa, *wv;
+};
+
 // Block partials: part[blockIdx][0:h] = sum dz*xhat (dgamma), part[blockIdx][h:2h] = sum dz (dbeta).
 // dres_out may alias dres_in (each element is read, then written, by the same lane).
 constexpr int kBwdRows = 2;
 
-template <int J, bool DROP>
+template <int J, bool DROP, bool HEAD>
 __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
-    const float *dres_in, const uint16_t *__restrict__ p_in, const uint16_t *__restrict__ g,
+    const float *dres_in, const uint16_t *__restrict__ p_in, HeadGrad hg, const uint16_t *__restrict__ g,
     const float *__restrict__ mean_in, const float *__restrict__ rstd_in, const float *__restrict__ gamma,
     const float *__restrict__ beta, uint16_t *__restrict__ dg, float *dres_out, float *__restrict__ part,
     int64_t m, int h, DropArgs da) {
@@ -242,7 +261,7 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t nw = (int64_t)gridDim.x * kWaves;
     const Drop d = make_drop(da);
-    float gm[J][4], bt[J][4], ag[J][4], ab[J][4];
+    float gm[J][4], bt[J][4], ag[J][4], ab[J][4], wh[HEAD ? 5 : 1][J][4];
     bool ok[J];
 #pragma unroll
     for (int j = 0; j < J; j++) {
@@ -253,6 +272,11 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
             gm[j][u] = ok[j] ? gamma[c + u] : 0.0f;
             bt[j][u] = ok[j] ? beta[c + u] : 0.0f;
             ag[j][u] = ab[j][u] = 0.0f;
+            if (HEAD) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) wh[k][j][u] = ok[j] ? hg.wa[k * h + c + u] : 0.0f;
+                wh[HEAD ? 4 : 0][j][u] = ok[j] && hg.wv ? hg.wv[c + u] : 0.0f;
+            }
         }
     }
     const float inv_h = 1.0f / (float)h;
@@ -265,6 +289,15 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
             const bool rv = r < m;
             mean[q] = rv ? mean_in[r] : 0.0f;
             rstd[q] = rv ? rstd_in[r] : 0.0f;
+            float dz[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+            if (HEAD && rv) {  // the heads' output gradient of this row (wave-uniform broadcast loads)
+                const float4 d0 = *reinterpret_cast<const float4 *>(hg.dz + r * 8);
+                dz[0] = d0.x;
+                dz[1] = d0.y;
+                dz[2] = d0.z;
+                dz[3] = d0.w;
+                dz[4] = hg.dz[r * 8 + 4];
+            }
 #pragma unroll
             for (int j = 0; j < J; j++) {
                 const int c = 4 * (lane + 64 * j);
@@ -272,12 +305,21 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
                 for (int u = 0; u < 4; u++) x[q][j][u] = dy[q][j][u] = 0.0f;
                 if (!(ok[j] && rv)) continue;
                 load_bf4(g + r * h + c, x[q][j]);
+                if (HEAD) {
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        float t = 0.0f;
+#pragma unroll
+                        for (int k = 0; k < 5; k++) t += dz[k] * wh[HEAD ? k : 0][j][u];
+                        dy[q][j][u] = t;
+                    }
+                }
                 if (dres_in) {
                     const float4 t = *reinterpret_cast<const float4 *>(dres_in + r * h + c);
-                    dy[q][j][0] = t.x;
-                    dy[q][j][1] = t.y;
-                    dy[q][j][2] = t.z;
-                    dy[q][j][3] = t.w;
+                    dy[q][j][0] += t.x;
+                    dy[q][j][1] += t.y;
+                    dy[q][j][2] += t.z;
+                    dy[q][j][3] += t.w;
                 }
                 if (p_in) {
                     float t[4];
@@ -368,178 +410,341 @@ struct HeadLossArgs {
     int decouple;
 };
 
+// The PPO-clip / entropy / smooth-L1 loss of one row and its gradient w.r.t. the 5 head outputs
+// (train.py:497-546, with torch's backward conventions: minimum splits ties, clamp passes its
+// bounds); z = {4 logits, value}, i = the row's index in the flat trajectory.
+struct RowIn {
+    uint32_t act, legal;
+    float olp[4], adv, ret;
+};
+
+// The per-row inputs of trajectory row i (independent loads, issued together).
+__device__ __forceinline__ RowIn load_row_in(const HeadLossArgs &a, int64_t i) {
+    RowIn in;
+    in.act = a.action[i] & 3u;
+    in.legal = a.legal[i] & 0xFu;
+    const float4 o = *reinterpret_cast<const float4 *>(a.old_logp + i * 4);
+    in.olp[0] = o.x;
+    in.olp[1] = o.y;
+    in.olp[2] = o.z;
+    in.olp[3] = o.w;
+    in.adv = a.adv[i];
+    in.ret = a.ret[i];
+    return in;
+}
+
+__device__ __forceinline__ void row_loss(const float z[5], const RowIn &in, const HeadLossArgs &a, float beta_c,
+                                         float dz[5], float mk[4], float &ppo_out, float &ent_out, float &vl_out) {
+    const int act = (int)in.act;
+    const uint32_t legal = in.legal;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        mk[k] = (legal >> k) & 1u ? z[k] : -INFINITY;
+        mx = fmaxf(mx, mk[k]);
+    }
+    float se = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) se += (legal >> k) & 1u ? expf(mk[k] - mx) : 0.0f;
+    const float lse = mx + logf(se);
+    float sm[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) sm[k] = (legal >> k) & 1u ? expf(mk[k] - lse) : 0.0f;
+    const float lp_a = mk[act] - lse;
+    const float olp_a = act == 0 ? in.olp[0] : act == 1 ? in.olp[1] : act == 2 ? in.olp[2] : in.olp[3];
+    const float dlt = lp_a - olp_a;
+    const float ratio = expf(fminf(fmaxf(dlt, -20.0f), 20.0f));
+    const bool in20 = dlt >= -20.0f && dlt <= 20.0f;
+    const float A = in.adv;
+    const float rc = fminf(fmaxf(ratio, a.clip_lo), a.clip_hi);
+    const bool inr = ratio >= a.clip_lo && ratio <= a.clip_hi;
+    const float t1 = A * ratio, t2 = A * rc;
+    const float ppo = fminf(t1, t2);
+    // torch.minimum backward: the smaller side takes the gradient, a tie splits it in halves
+    float dp;
+    if (t1 < t2) dp = A;
+    else if (t1 > t2) dp = inr ? A : 0.0f;
+    else dp = 0.5f * A + (inr ? 0.5f * A : 0.0f);
+    const float dd = in20 ? dp * ratio : 0.0f;  // d ppo / d (logpi(a) - old)
+
+    // entropy of softmax(clamp(masked, -20, 20)) summed over the legal actions
+    float ck[4], cmx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        ck[k] = fminf(fmaxf(mk[k], -20.0f), 20.0f);
+        cmx = fmaxf(cmx, ck[k]);
+    }
+    float se2 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) se2 += expf(ck[k] - cmx);
+    const float lse2 = cmx + logf(se2);
+    float lp2[4], p2[4], ent = 0.0f, S = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        lp2[k] = ck[k] - lse2;
+        p2[k] = expf(lp2[k]);
+        if ((legal >> k) & 1u) {
+            ent -= p2[k] * lp2[k];
+            S += p2[k] * (lp2[k] + 1.0f);
+        }
+    }
+    const float dv0 = z[4] - in.ret;
+    const float adv0 = fabsf(dv0);
+    const float vl = adv0 < 1.0f ? 0.5f * dv0 * dv0 : adv0 - 0.5f;
+    const float dvl = fminf(fmaxf(dv0, -1.0f), 1.0f);
+
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const bool valid = (legal >> k) & 1u;
+        const bool cpass = valid && mk[k] >= -20.0f && mk[k] <= 20.0f;
+        const float dent = -(p2[k] * (lp2[k] + 1.0f) - p2[k] * S);
+        const float g = dd * ((k == act ? 1.0f : 0.0f) - sm[k]) + (cpass ? beta_c * dent : 0.0f);
+        dz[k] = valid ? -a.inv_m * g : 0.0f;
+    }
+    dz[4] = a.inv_m * a.critic * dvl;
+
+    ppo_out = ppo;
+    ent_out = ent;
+    vl_out = vl;
+}
+
+// B fragments (lane (g, c): k = 32 ks + 8 g + j, column c) of the head matrix [wa (4 rows); wv],
+// zero beyond column 4 and row h, split w = hi + mid + lo into three bf16 terms.
+template <int KS>
+__device__ __forceinline__ void load_head_b3(bf16x8_t fb[3][KS], const float *wa, const float *wv, int h, int g,
+                                             int c, int k0 = 0) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ks++) {
+        s16x8_t v0, v1, v2;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int k = k0 + 32 * ks + 8 * g + j;
+            const float wgt = (c < 5 && k < h) ? (c < 4 ? wa[c * h + k] : wv ? wv[k] : 0.0f) : 0.0f;
+            const __bf16 hi = (__bf16)wgt;
+            const float r1 = wgt - (float)hi;
+            const __bf16 mid = (__bf16)r1;
+            const __bf16 lo = (__bf16)(r1 - (float)mid);
+            v0[j] = __builtin_bit_cast(short, hi);
+            v1[j] = __builtin_bit_cast(short, mid);
+            v2[j] = __builtin_bit_cast(short, lo);
+        }
+        fb[0][ks] = __builtin_bit_cast(bf16x8_t, v0);
+        fb[1][ks] = __builtin_bit_cast(bf16x8_t, v1);
+        fb[2][ks] = __builtin_bit_cast(bf16x8_t, v2);
+    }
+}
+
+// z[64 rows][5] = x[r0 .. r0+63] [wa; wv]^T on MFMA, into the wave's LDS tile (without bias).
+// KS k-steps of 32 per chunk; with MULTI the weights are re-split per 256-column chunk (h > 256).
+// With xs (STAGE), the 64 rows come from the wave's LDS image (row-major, pitch 2h bytes).
+template <int KS, bool MULTI, bool STAGE = false>
+__device__ __forceinline__ void head_tiles(float (*zt)[5], bf16x8_t fb[3][KS], const uint16_t *xin, const float *wa,
+                                           const float *wv, int64_t m, int h, int64_t r0, int g, int c, int nout,
+                                           const char *xs = nullptr) {
+    f32x4_t z[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) z[t] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int k0 = 0; k0 < h; k0 += 32 * KS) {
+        if (MULTI) load_head_b3<KS>(fb, wa, wv, h, g, c, k0);
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int64_t mr = r0 + 16 * t + c;
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) {
+                const int kl = k0 + 32 * ks + 8 * g;
+                uint4 q = make_uint4(0u, 0u, 0u, 0u);
+                if (STAGE) {  // rows past m hold stale LDS: they only feed their own (unused) outputs
+                    if (kl < h) {
+                        const char *src = xs + (16 * t + c) * 2 * h + 2 * kl;
+                        const uint2 lo = *reinterpret_cast<const uint2 *>(src);
+                        const uint2 hi = kl + 8 <= h ? *reinterpret_cast<const uint2 *>(src + 8) : make_uint2(0u, 0u);
+                        q = make_uint4(lo.x, lo.y, hi.x, hi.y);
+                    }
+                } else if (mr < m && kl < h) {
+                    const uint16_t *src = xin + mr * h + kl;
+                    const uint2 lo = *reinterpret_cast<const uint2 *>(src);
+                    const uint2 hi = kl + 8 <= h ? *reinterpret_cast<const uint2 *>(src + 4) : make_uint2(0u, 0u);
+                    q = make_uint4(lo.x, lo.y, hi.x, hi.y);
+                }
+                const bf16x8_t xa = __builtin_bit_cast(bf16x8_t, q);
+                z[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, fb[2][ks], z[t], 0, 0, 0);
+                z[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, fb[1][ks], z[t], 0, 0, 0);
+                z[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, fb[0][ks], z[t], 0, 0, 0);
+            }
+        }
+        if (!MULTI) break;
+    }
+    if (c < nout) {
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) zt[16 * t + 4 * g + r][c] = z[t][r];
+    }
+}
+
 // Block partials: [dwa 4h | dwv h | dba 4 | dbv 1 | sum ppo, sum H, sum v]  (5h + 8 floats)
-template <int J>
+//
+// 64 rows per wave and iteration, three layouts:
+//   heads    logits/value of the 64 rows on MFMA (head_fwd's tiles), through a per-wave LDS
+//            transpose to lane = row;
+//   loss     lane = row: the scalar loss math runs once per row (not once per lane of a row);
+//   backward lane = 4 features: for each row, dx = dz W (20 FMA per lane, row-contiguous float4
+//            stores) and the head-weight gradient accumulates dz x in registers.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+// Copies nbytes (a multiple of 8) from global src to the wave's LDS image dst with 16-byte
+// LDS-DMA loads (1 KiB per wave instruction, no VGPR staging); an 8-byte tail goes through lane 0.
+__device__ __forceinline__ void wave_stage(char *dst, const char *src, int nbytes, int lane) {
+    const int n16 = nbytes & ~15;
+    for (int off = 0; off < n16; off += 1024) {
+        if (off + 16 * lane < n16)
+            __builtin_amdgcn_global_load_lds((glb_void_t *)(src + off + 16 * lane), (lds_void_t *)(dst + off), 16, 0, 0);
+    }
+    if (n16 < nbytes && lane == 0)
+        *reinterpret_cast<uint2 *>(dst + n16) = *reinterpret_cast<const uint2 *>(src + n16);
+}
+
+template <int J, int KS, bool MULTI, bool DX>
 __global__ __launch_bounds__(kThreads) void head_loss_kernel(const uint16_t *__restrict__ xin,
                                                              const float *__restrict__ wa, const float *__restrict__ ba,
                                                              const float *__restrict__ wv, const float *__restrict__ bv,
                                                              int64_t m, int h, HeadLossArgs a,
                                                              float *__restrict__ masked_out, float *__restrict__ dx_out,
-                                                             float *__restrict__ part) {
-    extern __shared__ float lds[];  // [kWaves][5h + 8]
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+                                                             float *__restrict__ dz_out, float *__restrict__ part) {
+    // dynamic LDS: per wave the 64-row image of x (h <= 256: STAGE), then the block reduction
+    // [kWaves][5h + 8] over the same bytes
+    constexpr bool STAGE = !MULTI;
+    extern __shared__ float lds[];
+    __shared__ float zs[kWaves][64][5], dzs[kWaves][64][5];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
     const int64_t nw = (int64_t)gridDim.x * kWaves;
     const int C = 5 * h + 8;
-    float w[5][J][4], acc[5][J][4];
+    char *xs = reinterpret_cast<char *>(lds) + (size_t)wave * 128 * h;
+    // MFMA B fragments of the head weights, B[k][n] = W_head n [k] (n < 5), as an exact 3-term bf16
+    // split (hi + mid + lo carries all 24 mantissa bits): the logits keep fp32 weights
+    bf16x8_t fb[3][KS];
+    if (!MULTI) load_head_b3<KS>(fb, wa, wv, h, g, c);
+    float w[DX ? 5 : 1][J][4], acc[5][J][4];
     bool ok[J];
 #pragma unroll
     for (int j = 0; j < J; j++) {
-        const int c = 4 * (lane + 64 * j);
-        ok[j] = c < h;
+        const int cc = 4 * (lane + 64 * j);
+        ok[j] = cc < h;
 #pragma unroll
         for (int u = 0; u < 4; u++) {
+            if (DX) {
 #pragma unroll
-            for (int k = 0; k < 4; k++) w[k][j][u] = ok[j] ? wa[k * h + c + u] : 0.0f;
-            w[4][j][u] = ok[j] ? wv[c + u] : 0.0f;
+                for (int k = 0; k < 4; k++) w[DX ? k : 0][j][u] = ok[j] ? wa[k * h + cc + u] : 0.0f;
+                w[DX ? 4 : 0][j][u] = ok[j] ? wv[cc + u] : 0.0f;
+            }
 #pragma unroll
             for (int k = 0; k < 5; k++) acc[k][j][u] = 0.0f;
         }
     }
-    float bias[5];
-#pragma unroll
-    for (int k = 0; k < 4; k++) bias[k] = ba[k];
-    bias[4] = bv[0];
+    const float bsa[4] = {ba[0], ba[1], ba[2], ba[3]}, bsv = bv[0];
     const float beta_c = *a.beta_dev;
     float sb[5] = {0, 0, 0, 0, 0}, s_ppo = 0.0f, s_ent = 0.0f, s_v = 0.0f;
 
-    constexpr int RPW = 2;  // rows per wave and iteration: their loads and reductions overlap
-    for (int64_t r0 = ((int64_t)blockIdx.x * kWaves + wave) * RPW; r0 < m; r0 += nw * RPW) {
-        float xs[RPW][J][4], zs[RPW][5];
-        int64_t is[RPW];
+    for (int64_t r0 = ((int64_t)blockIdx.x * kWaves + wave) * 64; r0 < m; r0 += nw * 64) {
+        // ---- heads on MFMA: 4 tiles of 16 rows, lane (g, c) gets rows 4g + r, head c
+        const int nr = (int)min((int64_t)64, m - r0);
+        // the rows' loss inputs and (STAGE) the 64 x rows into LDS, all in flight together
+        RowIn in{};
+        if (lane < nr) in = load_row_in(a, a.idx[r0 + lane]);
+        if (STAGE) {
+            wave_stage(xs, reinterpret_cast<const char *>(xin + r0 * h), nr * 2 * h, lane);
+            __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0): the image has landed (own wave only)
+        }
+        // ---- heads on MFMA: 4 tiles of 16 rows, lane (g, c) gets rows 4g + r, head c
+        head_tiles<KS, MULTI, STAGE>(zs[wave], fb, xin, wa, wv, m, h, r0, g, c, 5, xs);
+        // ---- loss: lane = row (LDS ops of a wave execute in order: the writes above land first)
+        {
+            const int64_t r = r0 + lane;
+            float dz[5] = {0, 0, 0, 0, 0};
+            if (lane < nr) {
+                float z[5], mk[4], ppo, ent, vl;
 #pragma unroll
-        for (int q = 0; q < RPW; q++) {
-            const int64_t r = r0 + q;
-            is[q] = r < m ? a.idx[r] : 0;
+                for (int k = 0; k < 5; k++) z[k] = zs[wave][lane][k] + (k < 4 ? bsa[k] : bsv);
+                row_loss(z, in, a, beta_c, dz, mk, ppo, ent, vl);
+                *reinterpret_cast<float4 *>(masked_out + r * 4) = make_float4(mk[0], mk[1], mk[2], mk[3]);
+                s_ppo += ppo;
+                s_ent += ent;
+                s_v += vl;
+            }
 #pragma unroll
-            for (int k = 0; k < 5; k++) zs[q][k] = 0.0f;
+            for (int k = 0; k < 5; k++) {
+                dzs[wave][lane][k] = dz[k];
+                sb[k] += dz[k];
+            }
+            if (dz_out && lane < nr) {
+                *reinterpret_cast<float4 *>(dz_out + r * 8) = make_float4(dz[0], dz[1], dz[2], dz[3]);
+                *reinterpret_cast<float4 *>(dz_out + r * 8 + 4) = make_float4(dz[4], 0.0f, 0.0f, 0.0f);
+            }
+        }
+        // ---- backward: lane = 4 features, one row after the other (8 rows' loads in flight)
+        constexpr int RB = J == 1 ? 8 : (J == 2 ? 4 : 2);
+        for (int q0 = 0; q0 < nr; q0 += RB) {
+            float x[RB][J][4];
 #pragma unroll
-            for (int j = 0; j < J; j++) {
-                if (ok[j] && r < m) {
-                    load_bf4(xin + r * h + 4 * (lane + 64 * j), xs[q][j]);
-                } else {
-                    xs[q][j][0] = xs[q][j][1] = xs[q][j][2] = xs[q][j][3] = 0.0f;
+            for (int qq = 0; qq < RB; qq++) {
+                const int q = q0 + qq;
+#pragma unroll
+                for (int j = 0; j < J; j++) {
+                    if (ok[j] && q < nr) {
+                        if (STAGE) load_bf4_lds(xs + q * 2 * h + 8 * (lane + 64 * j), x[qq][j]);
+                        else load_bf4(xin + (r0 + q) * h + 4 * (lane + 64 * j), x[qq][j]);
+                    } else {
+                        x[qq][j][0] = x[qq][j][1] = x[qq][j][2] = x[qq][j][3] = 0.0f;
+                    }
                 }
-#pragma unroll
-                for (int k = 0; k < 5; k++)
-#pragma unroll
-                    for (int u = 0; u < 4; u++) zs[q][k] += xs[q][j][u] * w[k][j][u];
             }
-        }
 #pragma unroll
-        for (int q = 0; q < RPW; q++)
+            for (int qq = 0; qq < RB; qq++) {
+                const int q = q0 + qq;
+                if (q >= nr) break;
+                float dz[5];
 #pragma unroll
-            for (int k = 0; k < 5; k++) zs[q][k] = wave_sum(zs[q][k]) + bias[k];
+                for (int k = 0; k < 5; k++) dz[k] = dzs[wave][q][k];
 #pragma unroll
-        for (int q = 0; q < RPW; q++) {
-        const int64_t r = r0 + q;
-        if (r >= m) break;
-        const int64_t i = is[q];
-        float (&x)[J][4] = xs[q];
-        float (&z)[5] = zs[q];
-        // ---- the loss of this row (every lane redundantly; scalars are wave-uniform)
-        const int act = a.action[i] & 3;
-        const uint32_t legal = a.legal[i] & 0xFu;
-        float mk[4], mx = -INFINITY;
+                for (int j = 0; j < J; j++) {
+                    if (!ok[j]) continue;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            mk[k] = (legal >> k) & 1u ? z[k] : -INFINITY;
-            mx = fmaxf(mx, mk[k]);
-        }
-        float se = 0.0f;
+                    for (int u = 0; u < 4; u++)
 #pragma unroll
-        for (int k = 0; k < 4; k++) se += (legal >> k) & 1u ? expf(mk[k] - mx) : 0.0f;
-        const float lse = mx + logf(se);
-        float sm[4];
+                        for (int k = 0; k < 5; k++) acc[k][j][u] += dz[k] * x[qq][j][u];
+                    if (!DX) continue;
+                    float o[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) sm[k] = (legal >> k) & 1u ? expf(mk[k] - lse) : 0.0f;
-        const float lp_a = mk[act] - lse;
-        const float dlt = lp_a - a.old_logp[i * 4 + act];
-        const float ratio = expf(fminf(fmaxf(dlt, -20.0f), 20.0f));
-        const bool in20 = dlt >= -20.0f && dlt <= 20.0f;
-        const float A = a.adv[i];
-        const float rc = fminf(fmaxf(ratio, a.clip_lo), a.clip_hi);
-        const bool inr = ratio >= a.clip_lo && ratio <= a.clip_hi;
-        const float t1 = A * ratio, t2 = A * rc;
-        const float ppo = fminf(t1, t2);
-        // torch.minimum backward: the smaller side takes the gradient, a tie splits it in halves
-        float dp;
-        if (t1 < t2) dp = A;
-        else if (t1 > t2) dp = inr ? A : 0.0f;
-        else dp = 0.5f * A + (inr ? 0.5f * A : 0.0f);
-        const float dd = in20 ? dp * ratio : 0.0f;  // d ppo / d (logpi(a) - old)
-
-        // entropy of softmax(clamp(masked, -20, 20)) summed over the legal actions
-        float ck[4], cmx = -INFINITY;
+                    for (int u = 0; u < 4; u++) {
+                        float t = 0.0f;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            ck[k] = fminf(fmaxf(mk[k], -20.0f), 20.0f);
-            cmx = fmaxf(cmx, ck[k]);
-        }
-        float se2 = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 4; k++) se2 += expf(ck[k] - cmx);
-        const float lse2 = cmx + logf(se2);
-        float lp2[4], p2[4], ent = 0.0f, S = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            lp2[k] = ck[k] - lse2;
-            p2[k] = expf(lp2[k]);
-            if ((legal >> k) & 1u) {
-                ent -= p2[k] * lp2[k];
-                S += p2[k] * (lp2[k] + 1.0f);
+                        for (int k = 0; k < 4; k++) t += dz[k] * w[DX ? k : 0][j][u];
+                        if (!a.decouple) t += dz[4] * w[DX ? 4 : 0][j][u];
+                        o[u] = t;
+                    }
+                    *reinterpret_cast<float4 *>(dx_out + (r0 + q) * h + 4 * (lane + 64 * j)) =
+                        make_float4(o[0], o[1], o[2], o[3]);
+                }
             }
-        }
-        const float dv0 = z[4] - a.ret[i];
-        const float adv0 = fabsf(dv0);
-        const float vl = adv0 < 1.0f ? 0.5f * dv0 * dv0 : adv0 - 0.5f;
-        const float dvl = fminf(fmaxf(dv0, -1.0f), 1.0f);
-
-        float dz[5];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const bool valid = (legal >> k) & 1u;
-            const bool cpass = valid && mk[k] >= -20.0f && mk[k] <= 20.0f;
-            const float dent = -(p2[k] * (lp2[k] + 1.0f) - p2[k] * S);
-            const float g = dd * ((k == act ? 1.0f : 0.0f) - sm[k]) + (cpass ? beta_c * dent : 0.0f);
-            dz[k] = valid ? -a.inv_m * g : 0.0f;
-        }
-        dz[4] = a.inv_m * a.critic * dvl;
-
-        // ---- backward into x and the head parameters
-#pragma unroll
-        for (int j = 0; j < J; j++) {
-            if (!ok[j]) continue;
-            float o[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                float t = 0.0f;
-#pragma unroll
-                for (int k = 0; k < 4; k++) t += dz[k] * w[k][j][u];
-                if (!a.decouple) t += dz[4] * w[4][j][u];
-                o[u] = t;
-#pragma unroll
-                for (int k = 0; k < 5; k++) acc[k][j][u] += dz[k] * x[j][u];
-            }
-            *reinterpret_cast<float4 *>(dx_out + r * h + 4 * (lane + 64 * j)) = make_float4(o[0], o[1], o[2], o[3]);
-        }
-#pragma unroll
-        for (int k = 0; k < 5; k++) sb[k] += dz[k];
-        s_ppo += ppo;
-        s_ent += ent;
-        s_v += vl;
-        if (lane == 0)
-            *reinterpret_cast<float4 *>(masked_out + r * 4) = make_float4(mk[0], mk[1], mk[2], mk[3]);
         }
     }
+    // block reduction: head weight grads (per lane), bias grads and loss sums (per lane -> wave)
+#pragma unroll
+    for (int k = 0; k < 5; k++) sb[k] = wave_sum(sb[k]);
+    s_ppo = wave_sum(s_ppo);
+    s_ent = wave_sum(s_ent);
+    s_v = wave_sum(s_v);
+    if (STAGE) __syncthreads();  // the reduction overwrites the other waves' images
     float *mine = lds + wave * C;
 #pragma unroll
     for (int j = 0; j < J; j++) {
         if (!ok[j]) continue;
-        const int c = 4 * (lane + 64 * j);
+        const int cc = 4 * (lane + 64 * j);
 #pragma unroll
         for (int u = 0; u < 4; u++)
 #pragma unroll
-            for (int k = 0; k < 5; k++) mine[k * h + c + u] = acc[k][j][u];
+            for (int k = 0; k < 5; k++) mine[k * h + cc + u] = acc[k][j][u];
     }
     if (lane == 0) {
 #pragma unroll
@@ -549,97 +754,65 @@ __global__ __launch_bounds__(kThreads) void head_loss_kernel(const uint16_t *__r
         mine[5 * h + 7] = s_v;
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < C; c += kThreads) {
+    for (int cc = threadIdx.x; cc < C; cc += kThreads) {
         float t = 0.0f;
 #pragma unroll
-        for (int w2 = 0; w2 < kWaves; w2++) t += lds[w2 * C + c];
-        part[(int64_t)blockIdx.x * C + c] = t;
+        for (int w2 = 0; w2 < kWaves; w2++) t += lds[w2 * C + cc];
+        part[(int64_t)blockIdx.x * C + cc] = t;
     }
 }
 
 // ------------------------------------------------------------------ KL diagnostic ------------
-// Block partials: [sum KL, max KL]
-template <int J>
+// Block partials: [sum KL, max KL].  Logits of 64 rows per wave on MFMA (fp32 weights as the
+// 3-term bf16 split of head_loss), transposed through LDS to lane = row for the KL.
+template <int KS, bool MULTI>
 __global__ __launch_bounds__(kThreads) void head_kl_kernel(const uint16_t *__restrict__ xin, const float *__restrict__ wa,
                                                            const float *__restrict__ ba, int64_t m, int h,
                                                            const float *__restrict__ old_masked,
                                                            float *__restrict__ part) {
     __shared__ float lds[kWaves][2];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ float zs[kWaves][64][5];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
     const int64_t nw = (int64_t)gridDim.x * kWaves;
-    float w[4][J][4];
-    bool ok[J];
-#pragma unroll
-    for (int j = 0; j < J; j++) {
-        const int c = 4 * (lane + 64 * j);
-        ok[j] = c < h;
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-#pragma unroll
-            for (int k = 0; k < 4; k++) w[k][j][u] = ok[j] ? wa[k * h + c + u] : 0.0f;
-    }
-    float bias[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) bias[k] = ba[k];
+    bf16x8_t fb[3][KS];
+    if (!MULTI) load_head_b3<KS>(fb, wa, nullptr, h, g, c);
+    const float bias[4] = {ba[0], ba[1], ba[2], ba[3]};
     float ksum = 0.0f, kmax = -INFINITY;
-    constexpr int RPW = 4;
-    for (int64_t r0 = ((int64_t)blockIdx.x * kWaves + wave) * RPW; r0 < m; r0 += nw * RPW) {
-        float zs[RPW][4];
+    for (int64_t r0 = ((int64_t)blockIdx.x * kWaves + wave) * 64; r0 < m; r0 += nw * 64) {
+        head_tiles<KS, MULTI>(zs[wave], fb, xin, wa, nullptr, m, h, r0, g, c, 4);
+        const int64_t r = r0 + lane;
+        if (r < m) {
+            const float4 o4 = *reinterpret_cast<const float4 *>(old_masked + r * 4);
+            const float o[4] = {o4.x, o4.y, o4.z, o4.w};
+            bool valid[4];
+            float mo = -INFINITY, mn = -INFINITY, nz[4];
 #pragma unroll
-        for (int q = 0; q < RPW; q++) {
-            const int64_t r = r0 + q;
-#pragma unroll
-            for (int k = 0; k < 4; k++) zs[q][k] = 0.0f;
-#pragma unroll
-            for (int j = 0; j < J; j++) {
-                if (!ok[j] || r >= m) continue;
-                float x[4];
-                load_bf4(xin + r * h + 4 * (lane + 64 * j), x);
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-#pragma unroll
-                    for (int u = 0; u < 4; u++) zs[q][k] += x[u] * w[k][j][u];
+            for (int k = 0; k < 4; k++) {
+                valid[k] = o[k] != -INFINITY;
+                nz[k] = valid[k] ? zs[wave][lane][k] + bias[k] : -INFINITY;
+                mo = fmaxf(mo, o[k]);
+                mn = fmaxf(mn, nz[k]);
             }
-        }
+            float so = 0.0f, sn = 0.0f;
 #pragma unroll
-        for (int q = 0; q < RPW; q++)
+            for (int k = 0; k < 4; k++) {
+                so += valid[k] ? expf(o[k] - mo) : 0.0f;
+                sn += valid[k] ? expf(nz[k] - mn) : 0.0f;
+            }
+            const float lso = mo + logf(so), lsn = mn + logf(sn);
+            float kl = 0.0f;
 #pragma unroll
-            for (int k = 0; k < 4; k++) zs[q][k] = wave_sum(zs[q][k]);
-#pragma unroll
-        for (int q = 0; q < RPW; q++) {
-        const int64_t r = r0 + q;
-        if (r >= m) break;
-        float (&z)[4] = zs[q];
-        const float4 o4 = *reinterpret_cast<const float4 *>(old_masked + r * 4);
-        const float o[4] = {o4.x, o4.y, o4.z, o4.w};
-        bool valid[4];
-        float mo = -INFINITY, mn = -INFINITY, nz[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            z[k] += bias[k];  // already wave-reduced above
-            valid[k] = o[k] != -INFINITY;
-            nz[k] = valid[k] ? z[k] : -INFINITY;
-            mo = fmaxf(mo, o[k]);
-            mn = fmaxf(mn, nz[k]);
-        }
-        float so = 0.0f, sn = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            so += valid[k] ? expf(o[k] - mo) : 0.0f;
-            sn += valid[k] ? expf(nz[k] - mn) : 0.0f;
-        }
-        const float lso = mo + logf(so), lsn = mn + logf(sn);
-        float kl = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            if (!valid[k]) continue;
-            const float lo = o[k] - lso, ln = nz[k] - lsn;
-            kl += expf(lo) * (lo - ln);
-        }
-        ksum += kl;
-        kmax = fmaxf(kmax, kl);
+            for (int k = 0; k < 4; k++) {
+                if (!valid[k]) continue;
+                const float lo = o[k] - lso, ln = nz[k] - lsn;
+                kl += expf(lo) * (lo - ln);
+            }
+            ksum += kl;
+            kmax = fmaxf(kmax, kl);
         }
     }
+    ksum = wave_sum(ksum);
+    kmax = wave_max(kmax);
     if (lane == 0) {
         lds[wave][0] = ksum;
         lds[wave][1] = kmax;
@@ -668,11 +841,6 @@ __global__ __launch_bounds__(kThreads) void head_kl_kernel(const uint16_t *__res
 // 16+4g..16+4g+3) identically for both operands; with the row pitch == 32 mod 256 bytes the
 // 8 rows a 32-lane half touches fill the 64 banks exactly (conflict-free).  Per-block partial
 // outputs are summed in a fixed order by colsum1/2 (deterministic).
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef short s16x4_t __attribute__((ext_vector_type(4)));
-typedef short s16x8_t __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kWgRows = 64;
 constexpr int kWgThreads = 256;  // 4 waves: one 139-KB-LDS block per CU, 512 registers per lane
@@ -1128,6 +1296,12 @@ inline bool shape_ok(int64_t m, int32_t h) { return m >= 0 && h > 0 && h % 4 == 
 
 inline bool al(const void *p, unsigned a) { return ((uintptr_t)p % a) == 0u; }
 
+// blocks of the head kernels: one 64-row group per wave and step, <= 1024 blocks (<= partial_blocks)
+inline int head_blocks(int64_t m) {
+    const int64_t b = (m + 64 * kWaves - 1) / (64 * kWaves);
+    return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+}
+
 // blocks of a partial-producing kernel: >= 4 rows per wave, <= 2048 blocks
 inline int partial_blocks(int64_t m) {
     const int64_t b = (m + 4 * kWaves - 1) / (4 * kWaves);
@@ -1249,15 +1423,16 @@ size_t g2048_ln_act_bwd_partials(int64_t m, int32_t h) {
     return (size_t)partial_blocks(m) * 2 * h + (size_t)kSlices * 2 * h;
 }
 
-int g2048_ln_act_bwd(g2048_stream_t stream, const float *dres_in, const uint16_t *p_in, const uint16_t *g,
-                     const float *mean, const float *rstd, const float *gamma, const float *beta, uint16_t *dg,
-                     float *dres_out, float *partials, float *dgamma, float *dbeta, int64_t m, int32_t h,
+int g2048_ln_act_bwd(g2048_stream_t stream, const float *dres_in, const uint16_t *p_in, const g2048_head_grad *head,
+                     const uint16_t *g, const float *mean, const float *rstd, const float *gamma, const float *beta,
+                     uint16_t *dg, float *dres_out, float *partials, float *dgamma, float *dbeta, int64_t m, int32_t h,
                      const g2048_dropout *drop) {
     if (!shape_ok(m, h)) return G2048_EINVAL;
     if (!g || !mean || !rstd || !gamma || !beta || !dg || !partials || !dgamma || !dbeta) return G2048_EINVAL;
     if (!al(g, 8) || !al(dg, 8) || (p_in && !al(p_in, 8)) || (dres_in && !al(dres_in, 16)) ||
         (dres_out && !al(dres_out, 16)))
         return G2048_EINVAL;
+    if (head && (!head->dz || !head->wa || !al(head->dz, 16))) return G2048_EINVAL;
     const hipStream_t s = (hipStream_t)stream;
     if (m == 0) {
         (void)hipMemsetAsync(dgamma, 0, sizeof(float) * h, s);
@@ -1265,14 +1440,20 @@ int g2048_ln_act_bwd(g2048_stream_t stream, const float *dres_in, const uint16_t
         return status();
     }
     const DropArgs da = drop_args(drop);
+    const HeadGrad hg{head ? head->dz : nullptr, head ? head->wa : nullptr, head ? head->wv : nullptr};
     const int nb = partial_blocks(m);
     const size_t lds = sizeof(float) * kWaves * 2 * h;
-    if (drop_on(drop))
-        G2048_DISPATCH_J(h, hipLaunchKernelGGL((ln_bwd_kernel<J, true>), dim3(nb), dim3(kThreads), lds, s, dres_in, p_in,
-                                               g, mean, rstd, gamma, beta, dg, dres_out, partials, m, h, da));
-    else
-        G2048_DISPATCH_J(h, hipLaunchKernelGGL((ln_bwd_kernel<J, false>), dim3(nb), dim3(kThreads), lds, s, dres_in,
-                                               p_in, g, mean, rstd, gamma, beta, dg, dres_out, partials, m, h, da));
+#define G2048_LB(D_, H_)                                                                                          \
+    G2048_DISPATCH_J(h, hipLaunchKernelGGL((ln_bwd_kernel<J, D_, H_>), dim3(nb), dim3(kThreads), lds, s, dres_in, p_in, \
+                                           hg, g, mean, rstd, gamma, beta, dg, dres_out, partials, m, h, da))
+    if (drop_on(drop)) {
+        if (head) G2048_LB(true, true);
+        else G2048_LB(true, false);
+    } else {
+        if (head) G2048_LB(false, true);
+        else G2048_LB(false, false);
+    }
+#undef G2048_LB
     Segs segs{};
     segs.n = 2;
     segs.dst[0] = dgamma;
@@ -1289,21 +1470,47 @@ size_t g2048_ppo_head_partials(int64_t m, int32_t h) {
 
 int g2048_ppo_head_loss(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, const float *wv,
                         const float *bv, int64_t m, int32_t h, const g2048_ppo_batch *batch, const float *beta_dev,
-                        float critic, float clip_eps, int32_t decouple_critic, float *masked, float *dx,
+                        float critic, float clip_eps, int32_t decouple_critic, float *masked, float *dx, float *dz,
                         float *partials, float *dwa, float *dba, float *dwv, float *dbv, float *sums) {
     if (!shape_ok(m, h) || m == 0 || !batch) return G2048_EINVAL;
-    if (!x || !wa || !ba || !wv || !bv || !beta_dev || !masked || !dx || !partials || !dwa || !dba || !dwv || !dbv ||
-        !sums || !batch->idx || !batch->action || !batch->legal || !batch->old_logp || !batch->adv || !batch->ret)
+    if (!x || !wa || !ba || !wv || !bv || !beta_dev || !masked || (!dx && !dz) || !partials || !dwa || !dba || !dwv ||
+        !dbv || !sums || !batch->idx || !batch->action || !batch->legal || !batch->old_logp || !batch->adv ||
+        !batch->ret)
         return G2048_EINVAL;
-    if (!al(x, 8) || !al(masked, 16) || !al(dx, 16)) return G2048_EINVAL;
+    if (!al(x, 8) || !al(masked, 16) || (dx && !al(dx, 16)) || (dz && !al(dz, 16))) return G2048_EINVAL;
     const hipStream_t s = (hipStream_t)stream;
     HeadLossArgs a{batch->idx, batch->action, batch->legal, batch->old_logp, batch->adv, batch->ret, beta_dev,
                    critic, 1.0f - clip_eps, 1.0f + clip_eps, 1.0f / (float)m, decouple_critic};
-    const int nb = partial_blocks(m);
+    const int nb = head_blocks(m);
     const int C = 5 * h + 8;
-    const size_t lds = sizeof(float) * kWaves * C;
-    G2048_DISPATCH_J(h, hipLaunchKernelGGL((head_loss_kernel<J>), dim3(nb), dim3(kThreads), lds, s, x, wa, ba, wv, bv,
-                                           m, h, a, masked, dx, partials));
+    const size_t red = sizeof(float) * kWaves * C, img = (size_t)kWaves * 128 * h;
+    const size_t lds = h <= 256 && img > red ? img : red;
+    // h <= 256: J = 1 and all KS = ceil(h/32) k-steps of the heads in registers; wider: 256-column chunks
+#define G2048_HL(J_, KS_, MULTI_)                                                                                  \
+    do {                                                                                                          \
+        if (dx)                                                                                                   \
+            hipLaunchKernelGGL((head_loss_kernel<J_, KS_, MULTI_, true>), dim3(nb), dim3(kThreads), lds, s, x, wa, \
+                               ba, wv, bv, m, h, a, masked, dx, dz, partials);                                    \
+        else                                                                                                      \
+            hipLaunchKernelGGL((head_loss_kernel<J_, KS_, MULTI_, false>), dim3(nb), dim3(kThreads), lds, s, x, wa, \
+                               ba, wv, bv, m, h, a, masked, dx, dz, partials);                                    \
+    } while (0)
+    switch ((h + 31) / 32) {
+        case 1: G2048_HL(1, 1, false); break;
+        case 2: G2048_HL(1, 2, false); break;
+        case 3: G2048_HL(1, 3, false); break;
+        case 4: G2048_HL(1, 4, false); break;
+        case 5: G2048_HL(1, 5, false); break;
+        case 6: G2048_HL(1, 6, false); break;
+        case 7: G2048_HL(1, 7, false); break;
+        case 8: G2048_HL(1, 8, false); break;
+        default:
+            if (h <= 512) G2048_HL(2, 8, true);
+            else if (h <= 768) G2048_HL(3, 8, true);
+            else G2048_HL(4, 8, true);
+            break;
+    }
+#undef G2048_HL
     Segs segs{};
     segs.n = 5;
     segs.dst[0] = dwa; segs.len[0] = 4 * h;
@@ -1319,9 +1526,21 @@ int g2048_ppo_head_kl(g2048_stream_t stream, const uint16_t *x, const float *wa,
     if (!shape_ok(m, h) || m == 0 || !x || !wa || !ba || !old_masked || !partials || !out) return G2048_EINVAL;
     if (!al(x, 8) || !al(old_masked, 16)) return G2048_EINVAL;
     const hipStream_t s = (hipStream_t)stream;
-    const int nb = partial_blocks(m);
-    G2048_DISPATCH_J(h, hipLaunchKernelGGL((head_kl_kernel<J>), dim3(nb), dim3(kThreads), 0, s, x, wa, ba, m, h,
-                                           old_masked, partials));
+    const int nb = head_blocks(m);
+    switch ((h + 31) / 32) {
+#define G2048_HK(KS_, MULTI_) \
+    hipLaunchKernelGGL((head_kl_kernel<KS_, MULTI_>), dim3(nb), dim3(kThreads), 0, s, x, wa, ba, m, h, old_masked, partials)
+        case 1: G2048_HK(1, false); break;
+        case 2: G2048_HK(2, false); break;
+        case 3: G2048_HK(3, false); break;
+        case 4: G2048_HK(4, false); break;
+        case 5: G2048_HK(5, false); break;
+        case 6: G2048_HK(6, false); break;
+        case 7: G2048_HK(7, false); break;
+        case 8: G2048_HK(8, false); break;
+        default: G2048_HK(8, true); break;
+#undef G2048_HK
+    }
     Segs segs{};
     segs.n = 1;
     segs.dst[0] = out;

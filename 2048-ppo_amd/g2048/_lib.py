@@ -72,6 +72,11 @@ class PPOBatch(ctypes.Structure):
                 ("old_logp", ctypes.c_void_p), ("adv", ctypes.c_void_p), ("ret", ctypes.c_void_p)]
 
 
+class HeadGrad(ctypes.Structure):
+    """struct g2048_head_grad"""
+    _fields_ = [("dz", ctypes.c_void_p), ("wa", ctypes.c_void_p), ("wv", ctypes.c_void_p)]
+
+
 class MuonMatrix(ctypes.Structure):
     """struct g2048_muon_matrix"""
     _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("momentum", ctypes.c_void_p),
@@ -128,10 +133,11 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_obs_gather": (ctypes.c_int, [vp, vp, vp, i64, vp]),
         "g2048_ln_act_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, dp]),
         "g2048_ln_act_bwd_partials": (sz, [i64, i32]),
-        "g2048_ln_act_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, dp]),
+        "g2048_ln_act_bwd": (ctypes.c_int, [vp, vp, vp, ctypes.POINTER(HeadGrad), vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                            vp, i64, i32, dp]),
         "g2048_ppo_head_partials": (sz, [i64, i32]),
         "g2048_ppo_head_loss": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, bp, vp, ctypes.c_float,
-                                               ctypes.c_float, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
+                                               ctypes.c_float, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "g2048_ppo_head_kl": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, vp, vp, vp]),
         "g2048_dropout_mask": (ctypes.c_int, [vp, i64, i32, dp, vp]),
         "g2048_wgrad_partials": (sz, [i64, i32, i32]),
@@ -305,12 +311,17 @@ def ln_act_bwd_partials(m: int, h: int) -> int:
     return int(load().g2048_ln_act_bwd_partials(m, h))
 
 
+def make_head_grad(dz, wa, wv) -> HeadGrad:
+    """The heads' share of the last block's output gradient (wv None: decoupled critic)."""
+    return HeadGrad(_dev(dz, torch.float32, "dz"), _dev(wa, torch.float32, "wa"), _dev(wv, torch.float32, "wv"))
+
+
 def ln_act_bwd(dres_in, p_in, g, mean, rstd, gamma, beta, dg, dres_out, partials, dgamma, dbeta,
-               drop: Dropout | None = None):
+               drop: Dropout | None = None, head: HeadGrad | None = None):
     m, h = g.shape
     _check(load().g2048_ln_act_bwd(
         _stream(g), _dev(dres_in, torch.float32, "dres_in"), _dev(p_in, torch.bfloat16, "p_in"),
-        _dev(g, torch.bfloat16, "g"), _dev(mean, torch.float32, "mean"), _dev(rstd, torch.float32, "rstd"),
+        ctypes.byref(head) if head is not None else None, _dev(g, torch.bfloat16, "g"), _dev(mean, torch.float32, "mean"), _dev(rstd, torch.float32, "rstd"),
         _dev(gamma, torch.float32, "gamma"), _dev(beta, torch.float32, "beta"), _dev(dg, torch.bfloat16, "dg"),
         _dev(dres_out, torch.float32, "dres_out"), _dev(partials, torch.float32, "partials"),
         _dev(dgamma, torch.float32, "dgamma"), _dev(dbeta, torch.float32, "dbeta"), m, h,
@@ -328,13 +339,13 @@ def make_ppo_batch(idx, action, legal, old_logp, adv, ret) -> PPOBatch:
 
 
 def ppo_head_loss(x, wa, ba, wv, bv, batch: PPOBatch, beta_dev, critic, clip_eps, decouple, masked, dx, partials,
-                  dwa, dba, dwv, dbv, sums):
+                  dwa, dba, dwv, dbv, sums, dz=None):
     m, h = x.shape
     _check(load().g2048_ppo_head_loss(
         _stream(x), _dev(x, torch.bfloat16, "x"), _dev(wa, torch.float32, "wa"), _dev(ba, torch.float32, "ba"),
         _dev(wv, torch.float32, "wv"), _dev(bv, torch.float32, "bv"), m, h, ctypes.byref(batch),
         _dev(beta_dev, torch.float32, "beta"), float(critic), float(clip_eps), int(bool(decouple)),
-        _dev(masked, torch.float32, "masked"), _dev(dx, torch.float32, "dx"),
+        _dev(masked, torch.float32, "masked"), _dev(dx, torch.float32, "dx"), _dev(dz, torch.float32, "dz"),
         _dev(partials, torch.float32, "partials"), _dev(dwa, torch.float32, "dwa"), _dev(dba, torch.float32, "dba"),
         _dev(dwv, torch.float32, "dwv"), _dev(dbv, torch.float32, "dbv"), _dev(sums, torch.float32, "sums")),
         "g2048_ppo_head_loss")

@@ -86,6 +86,7 @@ class FusedPPOUpdater(PPOUpdater):
         self.rstd = [torch.empty(bs, dtype=torch.float32, device=d) for _ in range(nl)]
         self.masked = torch.empty(bs, 4, dtype=torch.float32, device=d)
         self.dres = torch.empty(bs, h, dtype=torch.float32, device=d)
+        self.dz = torch.empty(bs, 8, dtype=torch.float32, device=d)
         self.dg = torch.empty(bs, h, dtype=bf, device=d)
         self.P = torch.empty(bs, h, dtype=bf, device=d)
         self.wg_ok = [L.wgrad_partials(bs, w.shape[0], w.shape[1]) > 0 for w in self.lin]
@@ -127,15 +128,19 @@ class FusedPPOUpdater(PPOUpdater):
         """Heads + PPO loss + backward of the minibatch; gradients land in the GradBucket views."""
         nl = len(self.lin)
         batch = L.make_ppo_batch(idx, data["actions"], data["legal"], data["logp"], data["adv"], data["ret"])
+        # the heads write only their output gradient dz [m, 8]; the last block's backward recomputes
+        # their share dz W of its output gradient (no [m, h] head gradient in HBM)
         L.ppo_head_loss(self.H[-1], self.wa, self.ba, self.wv, self.bv, batch, beta, self.cfg.critic,
-                        self.cfg.clip_eps, self.decouple, self.masked, self.dres, self.partials,
-                        self.wa.grad, self.ba.grad, self.wv.grad, self.bv.grad, self.sums)
+                        self.cfg.clip_eps, self.decouple, self.masked, None, self.partials,
+                        self.wa.grad, self.ba.grad, self.wv.grad, self.bv.grad, self.sums, dz=self.dz)
+        head = L.make_head_grad(self.dz, self.wa, None if self.decouple else self.wv)
         p_in = None
         for l in range(nl - 1, -1, -1):
             ln = self.ln[l]
-            L.ln_act_bwd(self.dres, p_in, self.G[l], self.mean[l], self.rstd[l], ln.weight, ln.bias, self.dg,
-                         self.dres if l > 0 else None, self.partials, ln.weight.grad, ln.bias.grad,
-                         self._drop(l, 0) if l > 0 else None)
+            top = l == nl - 1
+            L.ln_act_bwd(None if top else self.dres, p_in, self.G[l], self.mean[l], self.rstd[l], ln.weight, ln.bias,
+                         self.dg, self.dres if l > 0 else None, self.partials, ln.weight.grad, ln.bias.grad,
+                         self._drop(l, 0) if l > 0 else None, head=head if top else None)
             x_in = self.H[l - 1] if l > 0 else self.x0
             if self.wg_ok[l]:  # dW = dG^T X on the MFMA weight-gradient kernel
                 L.wgrad(self.dg, x_in, self.partials, self.lin[l].grad)

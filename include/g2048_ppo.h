@@ -73,14 +73,24 @@ int g2048_head_fwd(g2048_stream_t stream, const uint16_t *x, const float *wa, co
 /* Scratch floats of g2048_ln_act_bwd for (m, h). */
 size_t g2048_ln_act_bwd_partials(int64_t m, int32_t h);
 
-/* Backward of g2048_ln_act_fwd.  The incoming gradient of y is dy = dres_in + p_in (either may be
- * NULL; dres_in fp32 [m,h] is the residual stream's gradient from above, p_in bf16 [m,h] the
- * matmul gradient dG_next W_next).  Writes dg (bf16 [m,h], gradient of the pre-norm activation),
- * dy itself to dres_out (fp32, optional: the residual gradient passed further down), and
- * dgamma / dbeta (fp32 [h], overwritten). */
-int g2048_ln_act_bwd(g2048_stream_t stream, const float *dres_in, const uint16_t *p_in, const uint16_t *g,
-                     const float *mean, const float *rstd, const float *gamma, const float *beta, uint16_t *dg,
-                     float *dres_out, float *partials, float *dgamma, float *dbeta, int64_t m, int32_t h,
+/* The policy/value heads' share of a layer's output gradient, recomputed from their output gradient
+ * (the last residual block's backward, so that the heads never write a [m,h] gradient):
+ * dy += dz[:, 0:4] wa + dz[:, 4] wv.  dz fp32 [m, 8] as g2048_ppo_head_loss writes it (columns
+ * 5..7 unused); wa fp32 [4, h]; wv fp32 [h] or NULL when the critic is decoupled (game.py:1213-1219). */
+typedef struct g2048_head_grad {
+    const float *dz;
+    const float *wa;
+    const float *wv;
+} g2048_head_grad;
+
+/* Backward of g2048_ln_act_fwd.  The incoming gradient of y is dy = dres_in + p_in + head (each may
+ * be NULL; dres_in fp32 [m,h] is the residual stream's gradient from above, p_in bf16 [m,h] the
+ * matmul gradient dG_next W_next, head the heads' share above).  Writes dg (bf16 [m,h], gradient
+ * of the pre-norm activation), dy itself to dres_out (fp32, optional: the residual gradient passed
+ * further down), and dgamma / dbeta (fp32 [h], overwritten). */
+int g2048_ln_act_bwd(g2048_stream_t stream, const float *dres_in, const uint16_t *p_in, const g2048_head_grad *head,
+                     const uint16_t *g, const float *mean, const float *rstd, const float *gamma, const float *beta,
+                     uint16_t *dg, float *dres_out, float *partials, float *dgamma, float *dbeta, int64_t m, int32_t h,
                      const g2048_dropout *drop);
 
 /* Per-minibatch inputs of the PPO loss, gathered on the fly through idx from the flat trajectory
@@ -102,13 +112,14 @@ size_t g2048_ppo_head_partials(int64_t m, int32_t h);
  *   ratio = exp(clamp(logpi(a) - old_logp(a), -20, 20));  ppo = min(A ratio, A clip(ratio, 1-eps, 1+eps));
  *   H = -sum_legal softmax(clamp(masked,-20,20)) log_softmax(...);  v = smooth_l1(value, ret);
  *   loss = -mean(ppo - critic v + beta H)
- * Writes masked (fp32 [m,4], for the KL diagnostic), dx = dloss/dx (fp32 [m,h]; the value branch
- * is excluded when decouple_critic, game.py:1213-1219), the head gradients dwa [4,h], dba [4],
+ * Writes masked (fp32 [m,4], for the KL diagnostic), dx = dloss/dx (fp32 [m,h], optional; the value
+ * branch is excluded when decouple_critic, game.py:1213-1219) and/or dz = dloss/d(logits, value)
+ * (fp32 [m,8], optional: columns 0..4, for g2048_head_grad), the head gradients dwa [4,h], dba [4],
  * dwv [h], dbv [1] (overwritten) and sums[3] = {sum ppo, sum H, sum v} over the minibatch.
  * beta_dev: device float (the entropy coefficient, a device scalar so replays see updates). */
 int g2048_ppo_head_loss(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, const float *wv,
                         const float *bv, int64_t m, int32_t h, const g2048_ppo_batch *batch, const float *beta_dev,
-                        float critic, float clip_eps, int32_t decouple_critic, float *masked, float *dx,
+                        float critic, float clip_eps, int32_t decouple_critic, float *masked, float *dx, float *dz,
                         float *partials, float *dwa, float *dba, float *dwv, float *dbv, float *sums);
 
 /* KL(old || new) diagnostic after the optimizer step (train.py:578-601): new logits x Wa^T + ba

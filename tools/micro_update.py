@@ -115,6 +115,12 @@ def main():
     out["ppo_head_loss"] = timed(lambda: L.ppo_head_loss(xa, wa, ba, wv, bv, batch, beta_t, 0.2, 0.2, False, masked, dx,
                                                          hp, dwa, dba, dwv, dbv, sums))
     klo = torch.empty(2, device=dev)
+    dzb = torch.empty(M, 8, device=dev)
+    out["ppo_head_loss (dz only)"] = timed(lambda: L.ppo_head_loss(xa, wa, ba, wv, bv, batch, beta_t, 0.2, 0.2, False,
+                                                                   masked, None, hp, dwa, dba, dwv, dbv, sums, dz=dzb))
+    hg = L.make_head_grad(dzb, wa, wv)
+    out["ln_act_bwd (head, drop)"] = timed(lambda: L.ln_act_bwd(None, None, X, mean, rstd, ln.weight, ln.bias, G, dres,
+                                                                pb, dgam, dbet, drop, head=hg))
     out["ppo_head_kl"] = timed(lambda: L.ppo_head_kl(xa, wa, ba, masked, hp, klo))
     for k, v in out.items():
         print(f"{k:40s} {v:9.1f} us")
