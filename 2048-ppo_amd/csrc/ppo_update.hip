@@ -240,26 +240,34 @@ __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(const uint16_t *__rest
 }
 
 // ------------------------------------------------------------------ LayerNorm backward -------
-// The heads' contribution to dy, recomputed from their output gradient dz [m][8] (4 logits, value,
-// 3 pad): dy += dz[0:4] wa + dz[4] wv  (wv NULL = decoupled critic: the value branch is cut).
-struct HeadGrad {
+// The sources of a block's output gradient: dy = dres + sum_i p[i] + the heads' share, recomputed
+// from their output gradient dz [m][8] (4 logits, value, 3 pad) as dz[0:4] wa + dz[4] wv (wv NULL =
+// decoupled critic: the value branch is cut).
+static_assert(sizeof(g2048_dy) == 64 && offsetof(g2048_dy, dz) == 40, "g2048_dy layout (tests/test_abi.py)");
+
+struct DySrc {
+    const float *dres;
+    const uint16_t *p[G2048_DY_MAX_P];
+    int np;
     const float *dz, *wa, *wv;
 };
 
 // Block partials: part[blockIdx][0:h] = sum dz*xhat (dgamma), part[blockIdx][h:2h] = sum dz (dbeta).
 // dres_out may alias dres_in (each element is read, then written, by the same lane).
 constexpr int kBwdRows = 2;
+constexpr int kBwdWaves = 16;  // 1024-thread blocks, <= 256 of them: few partial rows to reduce
+constexpr int kBwdThreads = 64 * kBwdWaves;
 
 template <int J, bool DROP, bool HEAD>
-__global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
-    const float *dres_in, const uint16_t *__restrict__ p_in, HeadGrad hg, const uint16_t *__restrict__ g,
+__global__ __launch_bounds__(kBwdThreads) void ln_bwd_kernel(
+    DySrc src, const uint16_t *__restrict__ g,
     const float *__restrict__ mean_in, const float *__restrict__ rstd_in, const float *__restrict__ gamma,
     const float *__restrict__ beta, uint16_t *__restrict__ dg, float *dres_out, float *__restrict__ part,
     int64_t m, int h, DropArgs da) {
     constexpr int RPW = kBwdRows;
-    extern __shared__ float lds[];  // [kWaves][2h]
+    extern __shared__ float lds[];  // [kBwdWaves][2h]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t nw = (int64_t)gridDim.x * kWaves;
+    const int64_t nw = (int64_t)gridDim.x * kBwdWaves;
     const Drop d = make_drop(da);
     float gm[J][4], bt[J][4], ag[J][4], ab[J][4], wh[HEAD ? 5 : 1][J][4];
     bool ok[J];
@@ -274,13 +282,13 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
             ag[j][u] = ab[j][u] = 0.0f;
             if (HEAD) {
 #pragma unroll
-                for (int k = 0; k < 4; k++) wh[k][j][u] = ok[j] ? hg.wa[k * h + c + u] : 0.0f;
-                wh[HEAD ? 4 : 0][j][u] = ok[j] && hg.wv ? hg.wv[c + u] : 0.0f;
+                for (int k = 0; k < 4; k++) wh[k][j][u] = ok[j] ? src.wa[k * h + c + u] : 0.0f;
+                wh[HEAD ? 4 : 0][j][u] = ok[j] && src.wv ? src.wv[c + u] : 0.0f;
             }
         }
     }
     const float inv_h = 1.0f / (float)h;
-    for (int64_t r0 = ((int64_t)blockIdx.x * kWaves + wave) * RPW; r0 < m; r0 += nw * RPW) {
+    for (int64_t r0 = ((int64_t)blockIdx.x * kBwdWaves + wave) * RPW; r0 < m; r0 += nw * RPW) {
         float x[RPW][J][4], dy[RPW][J][4], xh[RPW][J][4], dxh[RPW][J][4];
         float mean[RPW], rstd[RPW], s1[RPW], s2[RPW];
 #pragma unroll
@@ -291,12 +299,12 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
             rstd[q] = rv ? rstd_in[r] : 0.0f;
             float dz[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
             if (HEAD && rv) {  // the heads' output gradient of this row (wave-uniform broadcast loads)
-                const float4 d0 = *reinterpret_cast<const float4 *>(hg.dz + r * 8);
+                const float4 d0 = *reinterpret_cast<const float4 *>(src.dz + r * 8);
                 dz[0] = d0.x;
                 dz[1] = d0.y;
                 dz[2] = d0.z;
                 dz[3] = d0.w;
-                dz[4] = hg.dz[r * 8 + 4];
+                dz[4] = src.dz[r * 8 + 4];
             }
 #pragma unroll
             for (int j = 0; j < J; j++) {
@@ -314,16 +322,18 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
                         dy[q][j][u] = t;
                     }
                 }
-                if (dres_in) {
-                    const float4 t = *reinterpret_cast<const float4 *>(dres_in + r * h + c);
+                if (src.dres) {
+                    const float4 t = *reinterpret_cast<const float4 *>(src.dres + r * h + c);
                     dy[q][j][0] += t.x;
                     dy[q][j][1] += t.y;
                     dy[q][j][2] += t.z;
                     dy[q][j][3] += t.w;
                 }
-                if (p_in) {
+#pragma unroll
+                for (int i = 0; i < G2048_DY_MAX_P; i++) {
+                    if (i >= src.np) break;
                     float t[4];
-                    load_bf4(p_in + r * h + c, t);
+                    load_bf4(src.p[i] + r * h + c, t);
 #pragma unroll
                     for (int u = 0; u < 4; u++) dy[q][j][u] += t[u];
                 }
@@ -389,10 +399,10 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
         }
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < 2 * h; c += kThreads) {
+    for (int c = threadIdx.x; c < 2 * h; c += kBwdThreads) {
         float t = 0.0f;
 #pragma unroll
-        for (int w = 0; w < kWaves; w++) t += lds[w * 2 * h + c];
+        for (int w = 0; w < kBwdWaves; w++) t += lds[w * 2 * h + c];
         part[(int64_t)blockIdx.x * 2 * h + c] = t;
     }
 }
@@ -1206,9 +1216,34 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const uint16_t *__restric
 // The per-minibatch accumulation of model_optimize_step's returned statistics (train.py:603-642)
 // in one thread: stats[0..8] += {loss, policy_loss, entropy_loss, value_loss, grad_norm, entropy,
 // kl_total, kl_average}, stats[8] = max(stats[8], kl_max); optionally bumps a device counter.
-__global__ void ppo_stats_kernel(const float *__restrict__ sums, const float *__restrict__ kl,
-                                 const float *__restrict__ gn, const float *__restrict__ beta, float critic, float m,
-                                 float *__restrict__ stats, uint64_t *__restrict__ counter) {
+__global__ __launch_bounds__(256) void ppo_stats_kernel(const float *__restrict__ sums, const float *__restrict__ kl,
+                                                        int kl_rows, const float *__restrict__ gn,
+                                                        const float *__restrict__ beta, float critic, float m,
+                                                        float *__restrict__ stats, uint64_t *__restrict__ counter) {
+    __shared__ float red[2][256];
+    float ks = 0.0f, km = -INFINITY;
+    if (kl_rows > 0) {  // the KL kernel's partial rows: fixed-order sums
+        for (int b = threadIdx.x; b < kl_rows; b += 256) {
+            ks += kl[2 * b];
+            km = fmaxf(km, kl[2 * b + 1]);
+        }
+        red[0][threadIdx.x] = ks;
+        red[1][threadIdx.x] = km;
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            if ((int)threadIdx.x < w) {
+                red[0][threadIdx.x] += red[0][threadIdx.x + w];
+                red[1][threadIdx.x] = fmaxf(red[1][threadIdx.x], red[1][threadIdx.x + w]);
+            }
+            __syncthreads();
+        }
+        ks = red[0][0];
+        km = red[1][0];
+    } else {
+        ks = kl[0];
+        km = kl[1];
+    }
+    if (threadIdx.x != 0) return;
     const float s_ppo = sums[0] / m, s_ent = sums[1] / m, s_v = sums[2] / m, b = *beta;
     stats[0] += -(s_ppo - critic * s_v + b * s_ent);
     stats[1] += -s_ppo;
@@ -1216,9 +1251,9 @@ __global__ void ppo_stats_kernel(const float *__restrict__ sums, const float *__
     stats[3] += critic * s_v;
     stats[4] += *gn;
     stats[5] += s_ent;
-    stats[6] += kl[0];
-    stats[7] += kl[0] / m;
-    stats[8] = fmaxf(stats[8], kl[1]);
+    stats[6] += ks;
+    stats[7] += ks / m;
+    stats[8] = fmaxf(stats[8], km);
     if (counter) *counter += 1ull;
 }
 
@@ -1274,6 +1309,48 @@ __global__ __launch_bounds__(256) void colsum2_kernel(const float *__restrict__ 
     }
 }
 
+// All deferred column sums in one launch: block = 64 columns x 16 row groups of one job (the job
+// found from the block index); each thread sums its rows in order, then a fixed-order LDS combine.
+static_assert(sizeof(g2048_colsum_job) == 88, "g2048_colsum_job layout (tests/test_abi.py)");
+struct ColsumBatch {
+    g2048_colsum_job job[G2048_COLSUM_MAX_JOBS];
+    int first[G2048_COLSUM_MAX_JOBS + 1];
+    int njobs;
+};
+
+__global__ __launch_bounds__(1024) void colsum_batch_kernel(const ColsumBatch cb) {
+    __shared__ float lds[16][64];
+    int j = 0;
+    while (j + 1 < cb.njobs && (int)blockIdx.x >= cb.first[j + 1]) j++;
+    const g2048_colsum_job &jb = cb.job[j];
+    const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    const int c = ((int)blockIdx.x - cb.first[j]) * 64 + cl;
+    const bool is_max = c == jb.max_col;
+    float t = is_max ? -INFINITY : 0.0f;
+    if (c < jb.cols) {
+        const float *p = jb.part + c;
+#pragma unroll 4
+        for (int b = rg; b < jb.nb; b += 16) {
+            const float v = p[(int64_t)b * jb.cols];
+            t = is_max ? fmaxf(t, v) : t + v;
+        }
+    }
+    lds[rg][cl] = t;
+    __syncthreads();
+    if (rg != 0 || c >= jb.cols) return;
+    float acc = lds[0][cl];
+#pragma unroll
+    for (int g = 1; g < 16; g++) acc = is_max ? fmaxf(acc, lds[g][cl]) : acc + lds[g][cl];
+    int off = 0;
+    for (int k = 0; k < jb.nseg; k++) {
+        if (c < off + jb.len[k]) {
+            jb.dst[k][c - off] = acc;
+            return;
+        }
+        off += jb.len[k];
+    }
+}
+
 __global__ __launch_bounds__(256) void dropout_mask_kernel(int64_t m, int h, DropArgs da, uint8_t *__restrict__ mask) {
     const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int groups = h / 4;
@@ -1296,10 +1373,16 @@ inline bool shape_ok(int64_t m, int32_t h) { return m >= 0 && h > 0 && h % 4 == 
 
 inline bool al(const void *p, unsigned a) { return ((uintptr_t)p % a) == 0u; }
 
-// blocks of the head kernels: one 64-row group per wave and step, <= 1024 blocks (<= partial_blocks)
+// blocks of the head kernels: one 64-row group per wave and step, <= 256 blocks (<= partial_blocks)
 inline int head_blocks(int64_t m) {
     const int64_t b = (m + 64 * kWaves - 1) / (64 * kWaves);
-    return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+    return (int)(b < 1 ? 1 : (b > 256 ? 256 : b));
+}
+
+// blocks of ln_bwd: 1024 threads, >= 4 rows per wave, <= 256 blocks (<= partial_blocks)
+inline int bwd_blocks(int64_t m) {
+    const int64_t b = (m + 4 * kBwdWaves - 1) / (4 * kBwdWaves);
+    return (int)(b < 1 ? 1 : (b > 256 ? 256 : b));
 }
 
 // blocks of a partial-producing kernel: >= 4 rows per wave, <= 2048 blocks
@@ -1327,7 +1410,21 @@ inline DropArgs drop_args(const g2048_dropout *d) {
 
 inline bool drop_on(const g2048_dropout *d) { return d && d->p > 0.0f; }
 
-int colsum(hipStream_t s, const float *part, int nb, int C, float *scratch2, const Segs &segs, int max_col) {
+int colsum(hipStream_t s, const float *part, int nb, int C, float *scratch2, const Segs &segs, int max_col,
+           g2048_colsum_job *defer = nullptr) {
+    if (defer) {  // described, summed later by g2048_colsum_batch
+        *defer = g2048_colsum_job{};
+        defer->part = part;
+        defer->nb = nb;
+        defer->cols = C;
+        defer->max_col = max_col;
+        defer->nseg = segs.n;
+        for (int k = 0; k < segs.n; k++) {
+            defer->dst[k] = segs.dst[k];
+            defer->len[k] = segs.len[k];
+        }
+        return status();
+    }
     hipLaunchKernelGGL(colsum1_kernel, dim3((C + 63) / 64, kSlices), dim3(256), 0, s, part, nb, C, scratch2, max_col);
     hipLaunchKernelGGL(colsum2_kernel, dim3((C + 255) / 256), dim3(256), 0, s, scratch2, C, segs, max_col);
     return status();
@@ -1423,29 +1520,39 @@ size_t g2048_ln_act_bwd_partials(int64_t m, int32_t h) {
     return (size_t)partial_blocks(m) * 2 * h + (size_t)kSlices * 2 * h;
 }
 
-int g2048_ln_act_bwd(g2048_stream_t stream, const float *dres_in, const uint16_t *p_in, const g2048_head_grad *head,
-                     const uint16_t *g, const float *mean, const float *rstd, const float *gamma, const float *beta,
-                     uint16_t *dg, float *dres_out, float *partials, float *dgamma, float *dbeta, int64_t m, int32_t h,
-                     const g2048_dropout *drop) {
-    if (!shape_ok(m, h)) return G2048_EINVAL;
+int g2048_ln_act_bwd(g2048_stream_t stream, const g2048_dy *dy, const uint16_t *g, const float *mean,
+                     const float *rstd, const float *gamma, const float *beta, uint16_t *dg, float *dres_out,
+                     float *partials, float *dgamma, float *dbeta, int64_t m, int32_t h, const g2048_dropout *drop,
+                     g2048_colsum_job *defer) {
+    if (!shape_ok(m, h) || !dy) return G2048_EINVAL;
     if (!g || !mean || !rstd || !gamma || !beta || !dg || !partials || !dgamma || !dbeta) return G2048_EINVAL;
-    if (!al(g, 8) || !al(dg, 8) || (p_in && !al(p_in, 8)) || (dres_in && !al(dres_in, 16)) ||
-        (dres_out && !al(dres_out, 16)))
+    if (!al(g, 8) || !al(dg, 8) || (dy->dres && !al(dy->dres, 16)) || (dres_out && !al(dres_out, 16)))
         return G2048_EINVAL;
-    if (head && (!head->dz || !head->wa || !al(head->dz, 16))) return G2048_EINVAL;
+    DySrc src{};
+    src.dres = dy->dres;
+    for (int i = 0; i < G2048_DY_MAX_P; i++) {
+        if (!dy->p[i]) continue;  // the non-NULL entries, packed
+        if (!al(dy->p[i], 8)) return G2048_EINVAL;
+        src.p[src.np++] = dy->p[i];
+    }
+    const bool head = dy->dz != nullptr;
+    if (head && (!dy->wa || !al(dy->dz, 16))) return G2048_EINVAL;
+    src.dz = dy->dz;
+    src.wa = dy->wa;
+    src.wv = dy->wv;
     const hipStream_t s = (hipStream_t)stream;
     if (m == 0) {
+        if (defer) *defer = g2048_colsum_job{};  // an empty job: g2048_colsum_batch skips it
         (void)hipMemsetAsync(dgamma, 0, sizeof(float) * h, s);
         (void)hipMemsetAsync(dbeta, 0, sizeof(float) * h, s);
         return status();
     }
     const DropArgs da = drop_args(drop);
-    const HeadGrad hg{head ? head->dz : nullptr, head ? head->wa : nullptr, head ? head->wv : nullptr};
-    const int nb = partial_blocks(m);
-    const size_t lds = sizeof(float) * kWaves * 2 * h;
-#define G2048_LB(D_, H_)                                                                                          \
-    G2048_DISPATCH_J(h, hipLaunchKernelGGL((ln_bwd_kernel<J, D_, H_>), dim3(nb), dim3(kThreads), lds, s, dres_in, p_in, \
-                                           hg, g, mean, rstd, gamma, beta, dg, dres_out, partials, m, h, da))
+    const int nb = bwd_blocks(m);
+    const size_t lds = sizeof(float) * kBwdWaves * 2 * h;
+#define G2048_LB(D_, H_)                                                                                             \
+    G2048_DISPATCH_J(h, hipLaunchKernelGGL((ln_bwd_kernel<J, D_, H_>), dim3(nb), dim3(kBwdThreads), lds, s, src, g, \
+                                           mean, rstd, gamma, beta, dg, dres_out, partials, m, h, da))
     if (drop_on(drop)) {
         if (head) G2048_LB(true, true);
         else G2048_LB(true, false);
@@ -1460,7 +1567,7 @@ int g2048_ln_act_bwd(g2048_stream_t stream, const float *dres_in, const uint16_t
     segs.len[0] = h;
     segs.dst[1] = dbeta;
     segs.len[1] = h;
-    return colsum(s, partials, nb, 2 * h, partials + (size_t)nb * 2 * h, segs, -1);
+    return colsum(s, partials, nb, 2 * h, partials + (size_t)nb * 2 * h, segs, -1, defer);
 }
 
 size_t g2048_ppo_head_partials(int64_t m, int32_t h) {
@@ -1471,7 +1578,8 @@ size_t g2048_ppo_head_partials(int64_t m, int32_t h) {
 int g2048_ppo_head_loss(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, const float *wv,
                         const float *bv, int64_t m, int32_t h, const g2048_ppo_batch *batch, const float *beta_dev,
                         float critic, float clip_eps, int32_t decouple_critic, float *masked, float *dx, float *dz,
-                        float *partials, float *dwa, float *dba, float *dwv, float *dbv, float *sums) {
+                        float *partials, float *dwa, float *dba, float *dwv, float *dbv, float *sums,
+                        g2048_colsum_job *defer) {
     if (!shape_ok(m, h) || m == 0 || !batch) return G2048_EINVAL;
     if (!x || !wa || !ba || !wv || !bv || !beta_dev || !masked || (!dx && !dz) || !partials || !dwa || !dba || !dwv ||
         !dbv || !sums || !batch->idx || !batch->action || !batch->legal || !batch->old_logp || !batch->adv ||
@@ -1518,11 +1626,11 @@ int g2048_ppo_head_loss(g2048_stream_t stream, const uint16_t *x, const float *w
     segs.dst[2] = dba; segs.len[2] = 4;
     segs.dst[3] = dbv; segs.len[3] = 1;
     segs.dst[4] = sums; segs.len[4] = 3;
-    return colsum(s, partials, nb, C, partials + (size_t)nb * C, segs, -1);
+    return colsum(s, partials, nb, C, partials + (size_t)nb * C, segs, -1, defer);
 }
 
 int g2048_ppo_head_kl(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, int64_t m,
-                      int32_t h, const float *old_masked, float *partials, float *out) {
+                      int32_t h, const float *old_masked, float *partials, float *out, g2048_colsum_job *defer) {
     if (!shape_ok(m, h) || m == 0 || !x || !wa || !ba || !old_masked || !partials || !out) return G2048_EINVAL;
     if (!al(x, 8) || !al(old_masked, 16)) return G2048_EINVAL;
     const hipStream_t s = (hipStream_t)stream;
@@ -1545,7 +1653,7 @@ int g2048_ppo_head_kl(g2048_stream_t stream, const uint16_t *x, const float *wa,
     segs.n = 1;
     segs.dst[0] = out;
     segs.len[0] = 2;
-    return colsum(s, partials, nb, 2, partials + (size_t)nb * 2, segs, 1);
+    return colsum(s, partials, nb, 2, partials + (size_t)nb * 2, segs, 1, defer);
 }
 
 
@@ -1556,7 +1664,7 @@ size_t g2048_wgrad_partials(int64_t m, int32_t n1, int32_t n2) {
 }
 
 int g2048_wgrad(g2048_stream_t stream, const uint16_t *a, const uint16_t *b, int64_t m, int32_t n1, int32_t n2,
-                float *partials, float *out) {
+                float *partials, float *out, g2048_colsum_job *defer) {
     WgPlan p;
     if (!a || !b || !partials || !out || !al(a, 8) || !al(b, 8)) return G2048_EINVAL;
     if (!wg_plan(m, n1, n2, p)) return G2048_EINVAL;
@@ -1577,7 +1685,7 @@ int g2048_wgrad(g2048_stream_t stream, const uint16_t *a, const uint16_t *b, int
     segs.n = 1;
     segs.dst[0] = out;
     segs.len[0] = n1 * n2;
-    return colsum(s, partials, p.nb, n1 * n2, partials + (size_t)p.nb * n1 * n2, segs, -1);
+    return colsum(s, partials, p.nb, n1 * n2, partials + (size_t)p.nb * n1 * n2, segs, -1, defer);
 }
 
 
@@ -1653,11 +1761,36 @@ int g2048_head_fwd(g2048_stream_t stream, const uint16_t *x, const float *wa, co
 }
 
 
-int g2048_ppo_stats(g2048_stream_t stream, const float *sums, const float *kl, const float *grad_norm,
+int g2048_ppo_stats(g2048_stream_t stream, const float *sums, const float *kl, int32_t kl_rows, const float *grad_norm,
                     const float *beta_dev, float critic, int64_t m, float *stats, uint64_t *counter) {
-    if (!sums || !kl || !grad_norm || !beta_dev || !stats || m <= 0) return G2048_EINVAL;
-    hipLaunchKernelGGL(ppo_stats_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, sums, kl, grad_norm, beta_dev,
-                       critic, (float)m, stats, counter);
+    if (!sums || !kl || kl_rows < 0 || !grad_norm || !beta_dev || !stats || m <= 0) return G2048_EINVAL;
+    hipLaunchKernelGGL(ppo_stats_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, sums, kl, kl_rows, grad_norm,
+                       beta_dev, critic, (float)m, stats, counter);
+    return status();
+}
+
+int g2048_colsum_batch(g2048_stream_t stream, const g2048_colsum_job *jobs, int32_t njobs) {
+    if (njobs < 0 || njobs > G2048_COLSUM_MAX_JOBS || (njobs && !jobs)) return G2048_EINVAL;
+    ColsumBatch cb{};
+    int blocks = 0;
+    for (int j = 0; j < njobs; j++) {
+        const g2048_colsum_job &jb = jobs[j];
+        if (!jb.part && jb.cols == 0) continue;  // empty (m = 0) job
+        if (!jb.part || jb.nb <= 0 || jb.cols <= 0 || jb.nseg <= 0 || jb.nseg > G2048_COLSUM_SEGS) return G2048_EINVAL;
+        int64_t tot = 0;
+        for (int k = 0; k < jb.nseg; k++) {
+            if (!jb.dst[k] || jb.len[k] <= 0) return G2048_EINVAL;
+            tot += jb.len[k];
+        }
+        if (tot != jb.cols) return G2048_EINVAL;
+        cb.job[cb.njobs] = jb;
+        cb.first[cb.njobs] = blocks;
+        cb.njobs++;
+        blocks += (jb.cols + 63) / 64;
+    }
+    cb.first[cb.njobs] = blocks;
+    if (!blocks) return G2048_OK;
+    hipLaunchKernelGGL(colsum_batch_kernel, dim3(blocks), dim3(1024), 0, (hipStream_t)stream, cb);
     return status();
 }
 

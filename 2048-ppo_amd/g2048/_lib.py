@@ -29,7 +29,7 @@ EXPORTED = (
     "g2048_reward_rtg", "g2048_rtg_finalize", "g2048_build_info", "g2048_episode_scan",
     # include/g2048_ppo.h
     "g2048_obs_gather", "g2048_ln_act_fwd", "g2048_ln_act_bwd_partials", "g2048_ln_act_bwd",
-    "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask",
+    "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
     "g2048_wgrad_partials", "g2048_wgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
@@ -72,9 +72,22 @@ class PPOBatch(ctypes.Structure):
                 ("old_logp", ctypes.c_void_p), ("adv", ctypes.c_void_p), ("ret", ctypes.c_void_p)]
 
 
-class HeadGrad(ctypes.Structure):
-    """struct g2048_head_grad"""
-    _fields_ = [("dz", ctypes.c_void_p), ("wa", ctypes.c_void_p), ("wv", ctypes.c_void_p)]
+DY_MAX_P = 4
+COLSUM_SEGS = 5
+COLSUM_MAX_JOBS = 16
+
+
+class ColsumJob(ctypes.Structure):
+    """struct g2048_colsum_job: a deferred fixed-order column sum"""
+    _fields_ = [("part", ctypes.c_void_p), ("nb", ctypes.c_int32), ("cols", ctypes.c_int32),
+                ("max_col", ctypes.c_int32), ("nseg", ctypes.c_int32), ("dst", ctypes.c_void_p * COLSUM_SEGS),
+                ("len", ctypes.c_int32 * COLSUM_SEGS), ("pad_", ctypes.c_int32)]
+
+
+class Dy(ctypes.Structure):
+    """struct g2048_dy: the sources of a block's output gradient"""
+    _fields_ = [("dres", ctypes.c_void_p), ("p", ctypes.c_void_p * DY_MAX_P), ("dz", ctypes.c_void_p),
+                ("wa", ctypes.c_void_p), ("wv", ctypes.c_void_p)]
 
 
 class MuonMatrix(ctypes.Structure):
@@ -114,6 +127,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     vp, i64, i32, u32, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_size_t
     rp, cp = ctypes.POINTER(Rng), ctypes.POINTER(RewardCfg)
     dp, bp = ctypes.POINTER(Dropout), ctypes.POINTER(PPOBatch)
+    jp = ctypes.POINTER(ColsumJob)
     sig = {
         "g2048_mt_state_words": (sz, []),
         "g2048_mt_seed": (ctypes.c_int, [vp, vp, vp, i64]),
@@ -133,20 +147,21 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_obs_gather": (ctypes.c_int, [vp, vp, vp, i64, vp]),
         "g2048_ln_act_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, dp]),
         "g2048_ln_act_bwd_partials": (sz, [i64, i32]),
-        "g2048_ln_act_bwd": (ctypes.c_int, [vp, vp, vp, ctypes.POINTER(HeadGrad), vp, vp, vp, vp, vp, vp, vp, vp, vp,
-                                            vp, i64, i32, dp]),
+        "g2048_ln_act_bwd": (ctypes.c_int, [vp, ctypes.POINTER(Dy), vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32,
+                                            dp, jp]),
+        "g2048_colsum_batch": (ctypes.c_int, [vp, jp, i32]),
         "g2048_ppo_head_partials": (sz, [i64, i32]),
         "g2048_ppo_head_loss": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, bp, vp, ctypes.c_float,
-                                               ctypes.c_float, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
-        "g2048_ppo_head_kl": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, vp, vp, vp]),
+                                               ctypes.c_float, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, jp]),
+        "g2048_ppo_head_kl": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, vp, vp, vp, jp]),
         "g2048_dropout_mask": (ctypes.c_int, [vp, i64, i32, dp, vp]),
         "g2048_wgrad_partials": (sz, [i64, i32, i32]),
-        "g2048_wgrad": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, vp, vp]),
+        "g2048_wgrad": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, vp, vp, jp]),
         "g2048_grad_clip": (ctypes.c_int, [vp, vp, i64, ctypes.c_float, vp, vp, vp]),
         "g2048_mlp_fwd_lds_bytes": (sz, [i32, i32]),
         "g2048_mlp_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, i64, i32, i32, dp]),
         "g2048_head_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, vp, i64, vp]),
-        "g2048_ppo_stats": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_float, i64, vp, vp]),
+        "g2048_ppo_stats": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, ctypes.c_float, i64, vp, vp]),
         "g2048_muon_supported": (ctypes.c_int, [i32, i32]),
         "g2048_muon_step": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.POINTER(MuonCfg)]),
         "g2048_adamw_step": (ctypes.c_int, [vp, ctypes.POINTER(AdamWGroup), i32, vp, vp, vp, ctypes.c_float,
@@ -311,21 +326,38 @@ def ln_act_bwd_partials(m: int, h: int) -> int:
     return int(load().g2048_ln_act_bwd_partials(m, h))
 
 
-def make_head_grad(dz, wa, wv) -> HeadGrad:
-    """The heads' share of the last block's output gradient (wv None: decoupled critic)."""
-    return HeadGrad(_dev(dz, torch.float32, "dz"), _dev(wa, torch.float32, "wa"), _dev(wv, torch.float32, "wv"))
+def make_dy(dres=None, ps=(), head=None) -> Dy:
+    """dy = dres + sum(ps) + heads; head = (dz, wa, wv) with wv None for a decoupled critic."""
+    ps = [p for p in ps if p is not None]
+    if len(ps) > DY_MAX_P:
+        raise G2048Error(f"at most {DY_MAX_P} matmul gradients per LayerNorm backward")
+    d = Dy()
+    d.dres = _dev(dres, torch.float32, "dres")
+    for i, p in enumerate(ps):
+        d.p[i] = _dev(p, torch.bfloat16, f"p[{i}]")
+    if head is not None:
+        dz, wa, wv = head
+        d.dz, d.wa, d.wv = _dev(dz, torch.float32, "dz"), _dev(wa, torch.float32, "wa"), _dev(wv, torch.float32, "wv")
+    return d
+
+
+def _defer(job):
+    return ctypes.byref(job) if job is not None else None
 
 
 def ln_act_bwd(dres_in, p_in, g, mean, rstd, gamma, beta, dg, dres_out, partials, dgamma, dbeta,
-               drop: Dropout | None = None, head: HeadGrad | None = None):
+               drop: Dropout | None = None, head=None, dy: Dy | None = None, defer: ColsumJob | None = None):
+    """LayerNorm/ReLU/dropout backward; the output gradient is `dy` (a Dy) or dres_in + p_in (+ head)."""
     m, h = g.shape
+    if dy is None:
+        dy = make_dy(dres_in, [p_in], head)
     _check(load().g2048_ln_act_bwd(
-        _stream(g), _dev(dres_in, torch.float32, "dres_in"), _dev(p_in, torch.bfloat16, "p_in"),
-        ctypes.byref(head) if head is not None else None, _dev(g, torch.bfloat16, "g"), _dev(mean, torch.float32, "mean"), _dev(rstd, torch.float32, "rstd"),
-        _dev(gamma, torch.float32, "gamma"), _dev(beta, torch.float32, "beta"), _dev(dg, torch.bfloat16, "dg"),
-        _dev(dres_out, torch.float32, "dres_out"), _dev(partials, torch.float32, "partials"),
-        _dev(dgamma, torch.float32, "dgamma"), _dev(dbeta, torch.float32, "dbeta"), m, h,
-        ctypes.byref(drop) if drop is not None else None), "g2048_ln_act_bwd")
+        _stream(g), ctypes.byref(dy), _dev(g, torch.bfloat16, "g"), _dev(mean, torch.float32, "mean"),
+        _dev(rstd, torch.float32, "rstd"), _dev(gamma, torch.float32, "gamma"), _dev(beta, torch.float32, "beta"),
+        _dev(dg, torch.bfloat16, "dg"), _dev(dres_out, torch.float32, "dres_out"),
+        _dev(partials, torch.float32, "partials"), _dev(dgamma, torch.float32, "dgamma"),
+        _dev(dbeta, torch.float32, "dbeta"), m, h, ctypes.byref(drop) if drop is not None else None, _defer(defer)),
+        "g2048_ln_act_bwd")
 
 
 def ppo_head_partials(m: int, h: int) -> int:
@@ -339,7 +371,7 @@ def make_ppo_batch(idx, action, legal, old_logp, adv, ret) -> PPOBatch:
 
 
 def ppo_head_loss(x, wa, ba, wv, bv, batch: PPOBatch, beta_dev, critic, clip_eps, decouple, masked, dx, partials,
-                  dwa, dba, dwv, dbv, sums, dz=None):
+                  dwa, dba, dwv, dbv, sums, dz=None, defer: ColsumJob | None = None):
     m, h = x.shape
     _check(load().g2048_ppo_head_loss(
         _stream(x), _dev(x, torch.bfloat16, "x"), _dev(wa, torch.float32, "wa"), _dev(ba, torch.float32, "ba"),
@@ -347,16 +379,16 @@ def ppo_head_loss(x, wa, ba, wv, bv, batch: PPOBatch, beta_dev, critic, clip_eps
         _dev(beta_dev, torch.float32, "beta"), float(critic), float(clip_eps), int(bool(decouple)),
         _dev(masked, torch.float32, "masked"), _dev(dx, torch.float32, "dx"), _dev(dz, torch.float32, "dz"),
         _dev(partials, torch.float32, "partials"), _dev(dwa, torch.float32, "dwa"), _dev(dba, torch.float32, "dba"),
-        _dev(dwv, torch.float32, "dwv"), _dev(dbv, torch.float32, "dbv"), _dev(sums, torch.float32, "sums")),
-        "g2048_ppo_head_loss")
+        _dev(dwv, torch.float32, "dwv"), _dev(dbv, torch.float32, "dbv"), _dev(sums, torch.float32, "sums"),
+        _defer(defer)), "g2048_ppo_head_loss")
 
 
-def ppo_head_kl(x, wa, ba, old_masked, partials, out):
+def ppo_head_kl(x, wa, ba, old_masked, partials, out, defer: ColsumJob | None = None):
     m, h = x.shape
     _check(load().g2048_ppo_head_kl(
         _stream(x), _dev(x, torch.bfloat16, "x"), _dev(wa, torch.float32, "wa"), _dev(ba, torch.float32, "ba"), m, h,
         _dev(old_masked, torch.float32, "old_masked"), _dev(partials, torch.float32, "partials"),
-        _dev(out, torch.float32, "out")), "g2048_ppo_head_kl")
+        _dev(out, torch.float32, "out"), _defer(defer)), "g2048_ppo_head_kl")
 
 
 def dropout_mask(m: int, h: int, drop: Dropout, mask):
@@ -369,15 +401,27 @@ def wgrad_partials(m: int, n1: int, n2: int) -> int:
     return int(load().g2048_wgrad_partials(m, n1, n2))
 
 
-def wgrad(a, b, partials, out):
+def wgrad(a, b, partials, out, defer: ColsumJob | None = None):
     """out[n1, n2] = a^T b for bf16 a [m, n1], b [m, n2]; fp32 out."""
     m, n1 = a.shape
     n2 = b.shape[1]
     if b.shape[0] != m or tuple(out.shape) != (n1, n2):
         raise G2048Error(f"wgrad shapes: a {tuple(a.shape)} b {tuple(b.shape)} out {tuple(out.shape)}")
     _check(load().g2048_wgrad(_stream(a), _dev(a, torch.bfloat16, "a"), _dev(b, torch.bfloat16, "b"), m, n1, n2,
-                              _dev(partials, torch.float32, "partials"), _dev(out, torch.float32, "out")),
-           "g2048_wgrad")
+                              _dev(partials, torch.float32, "partials"), _dev(out, torch.float32, "out"),
+                              _defer(defer)), "g2048_wgrad")
+
+
+def colsum_batch(jobs):
+    """Performs deferred column sums (ColsumJob list, at most COLSUM_MAX_JOBS) in one launch; `jobs`
+    may also be a ctypes array built once (graph-captured callers)."""
+    n = len(jobs)
+    if n > COLSUM_MAX_JOBS:
+        raise G2048Error(f"at most {COLSUM_MAX_JOBS} column-sum jobs per launch")
+    if not isinstance(jobs, ctypes.Array):
+        jobs = (ColsumJob * max(1, n))(*jobs)
+    stream = torch.cuda.current_stream().cuda_stream
+    _check(load().g2048_colsum_batch(ctypes.c_void_p(stream), jobs, n), "g2048_colsum_batch")
 
 
 # ------------------------------------------------------------- optimizer step -------------------
@@ -430,8 +474,10 @@ def head_fwd(x, wa, ba, wv, bv, logits, value):
         logits.stride(0), _dev(value, torch.float32, "value")), "g2048_head_fwd")
 
 
-def ppo_stats(sums, kl, grad_norm, beta_dev, critic: float, m: int, stats, counter=None):
+def ppo_stats(sums, kl, grad_norm, beta_dev, critic: float, m: int, stats, counter=None, kl_rows: int = 0):
+    """kl: final {sum, max}, or (kl_rows > 0) the partial rows of a deferred ppo_head_kl."""
     _check(load().g2048_ppo_stats(_stream(stats), _dev(sums, torch.float32, "sums"), _dev(kl, torch.float32, "kl"),
+                                  int(kl_rows),
                                   _dev(grad_norm, torch.float32, "grad_norm"), _dev(beta_dev, torch.float32, "beta"),
                                   float(critic), int(m), _dev(stats, torch.float32, "stats"),
                                   _dev(counter, torch.int64, "counter")), "g2048_ppo_stats")

@@ -9,8 +9,9 @@ action/value heads), FusedPPOUpdater writes the forward and backward out by hand
               H_l = H_{l-1} + Drop(ReLU(LN(G_l)))             (hipBLASLt + g2048_ln_act_fwd beyond h=256)
     loss      heads + PPO-clip + entropy + smooth-L1 and      g2048_ppo_head_loss
               d/dH_L, d/d(head params), loss sums
-    backward  dG_l, dgamma_l, dbeta_l, residual grad          g2048_ln_act_bwd
-              P = dG_l W_l                                    GEMM (hipBLASLt)
+    backward  dG_l, dgamma_l, dbeta_l from dy_l =            g2048_ln_act_bwd
+              heads(dz) + sum_{j>l} P_j
+              P_l = dG_l W_l                                  GEMM (hipBLASLt)
               dW_l = dG_l^T H_{l-1}                           g2048_wgrad (bf16 MFMA, fp32 straight
                                                               into the flat gradient bucket)
     step      [RCCL all-reduce] clip, Muon + AdamW            dist.GradBucket / optim.MuonAdamW
@@ -85,14 +86,22 @@ class FusedPPOUpdater(PPOUpdater):
         self.mean = [torch.empty(bs, dtype=torch.float32, device=d) for _ in range(nl)]
         self.rstd = [torch.empty(bs, dtype=torch.float32, device=d) for _ in range(nl)]
         self.masked = torch.empty(bs, 4, dtype=torch.float32, device=d)
-        self.dres = torch.empty(bs, h, dtype=torch.float32, device=d)
         self.dz = torch.empty(bs, 8, dtype=torch.float32, device=d)
         self.dg = torch.empty(bs, h, dtype=bf, device=d)
-        self.P = torch.empty(bs, h, dtype=bf, device=d)
+        # matmul gradients P_l = dG_l W_l of the blocks (l >= 1); with few blocks every one is kept and
+        # each LayerNorm backward sums the ones above it (no fp32 residual-gradient round trips)
+        self.keep_p = nl - 1 <= L.DY_MAX_P
+        self.P = [torch.empty(bs, h, dtype=bf, device=d) for _ in range(nl if self.keep_p else 1)]
+        self.dres = None if self.keep_p else torch.empty(bs, h, dtype=torch.float32, device=d)
         self.wg_ok = [L.wgrad_partials(bs, w.shape[0], w.shape[1]) > 0 for w in self.lin]
-        n = max([L.ln_act_bwd_partials(bs, h), L.ppo_head_partials(bs, h)] +
-                [L.wgrad_partials(bs, w.shape[0], w.shape[1]) for w in self.lin])
-        self.partials = torch.empty(n, dtype=torch.float32, device=d)
+        # per-reduction partial rows: every column sum of the backward is deferred into ONE
+        # g2048_colsum_batch launch (and the KL's into the statistics kernel)
+        f32 = torch.float32
+        self.part_head = torch.empty(L.ppo_head_partials(bs, h), dtype=f32, device=d)
+        self.part_kl = torch.empty(L.ppo_head_partials(bs, h), dtype=f32, device=d)
+        self.part_ln = [torch.empty(L.ln_act_bwd_partials(bs, h), dtype=f32, device=d) for _ in range(nl)]
+        self.part_wg = [torch.empty(max(1, L.wgrad_partials(bs, w.shape[0], w.shape[1])), dtype=f32, device=d)
+                        for w in self.lin]
         self.sums = torch.zeros(3, dtype=torch.float32, device=d)
         self.kl = torch.zeros(2, dtype=torch.float32, device=d)
         self.bs = bs
@@ -130,25 +139,34 @@ class FusedPPOUpdater(PPOUpdater):
         batch = L.make_ppo_batch(idx, data["actions"], data["legal"], data["logp"], data["adv"], data["ret"])
         # the heads write only their output gradient dz [m, 8]; the last block's backward recomputes
         # their share dz W of its output gradient (no [m, h] head gradient in HBM)
+        jobs = [L.ColsumJob()]
         L.ppo_head_loss(self.H[-1], self.wa, self.ba, self.wv, self.bv, batch, beta, self.cfg.critic,
-                        self.cfg.clip_eps, self.decouple, self.masked, None, self.partials,
-                        self.wa.grad, self.ba.grad, self.wv.grad, self.bv.grad, self.sums, dz=self.dz)
-        head = L.make_head_grad(self.dz, self.wa, None if self.decouple else self.wv)
-        p_in = None
+                        self.cfg.clip_eps, self.decouple, self.masked, None, self.part_head,
+                        self.wa.grad, self.ba.grad, self.wv.grad, self.bv.grad, self.sums, dz=self.dz, defer=jobs[-1])
+        head = (self.dz, self.wa, None if self.decouple else self.wv)
         for l in range(nl - 1, -1, -1):
             ln = self.ln[l]
-            top = l == nl - 1
-            L.ln_act_bwd(None if top else self.dres, p_in, self.G[l], self.mean[l], self.rstd[l], ln.weight, ln.bias,
-                         self.dg, self.dres if l > 0 else None, self.partials, ln.weight.grad, ln.bias.grad,
-                         self._drop(l, 0) if l > 0 else None, head=head if top else None)
+            if self.keep_p:  # dy_l = heads + sum_{j > l} P_j
+                dy = L.make_dy(None, self.P[l + 1:], head)
+                dres_out = None
+            else:  # deep nets: the fp32 residual gradient dres accumulates P_{l+1} layer by layer
+                dy = L.make_dy(self.dres if l < nl - 1 else None, [self.P[0]] if l < nl - 1 else [],
+                               head if l == nl - 1 else None)
+                dres_out = self.dres if l > 0 else None
+            jobs.append(L.ColsumJob())
+            L.ln_act_bwd(None, None, self.G[l], self.mean[l], self.rstd[l], ln.weight, ln.bias, self.dg, dres_out,
+                         self.part_ln[l], ln.weight.grad, ln.bias.grad, self._drop(l, 0) if l > 0 else None, dy=dy,
+                         defer=jobs[-1])
             x_in = self.H[l - 1] if l > 0 else self.x0
             if self.wg_ok[l]:  # dW = dG^T X on the MFMA weight-gradient kernel
-                L.wgrad(self.dg, x_in, self.partials, self.lin[l].grad)
+                jobs.append(L.ColsumJob())
+                L.wgrad(self.dg, x_in, self.part_wg[l], self.lin[l].grad, defer=jobs[-1])
             else:
                 _mm(self.dg.t(), x_in, self.lin[l].grad)
             if l > 0:
-                _mm(self.dg, self.wbf[l], self.P)
-                p_in = self.P
+                _mm(self.dg, self.wbf[l], self.P[l if self.keep_p else 0])
+        for i in range(0, len(jobs), L.COLSUM_MAX_JOBS):  # every deferred column sum, in one launch
+            L.colsum_batch(jobs[i:i + L.COLSUM_MAX_JOBS])
 
     # ---------------------------------------------------------------- PPOUpdater hooks ----
     def update(self, data: dict, beta: float, encode=None) -> dict:
@@ -174,12 +192,14 @@ class FusedPPOUpdater(PPOUpdater):
             self.refresh_weights()
         with torch.no_grad():
             x = self._layers(1)  # KL re-forward of the same minibatch (x0 still holds its encoding)
-            L.ppo_head_kl(x, self.wa, self.ba, self.masked, self.partials, self.kl)
+            kl_job = L.ColsumJob()  # the KL partial rows are reduced by the statistics kernel
+            L.ppo_head_kl(x, self.wa, self.ba, self.masked, self.part_kl, self.kl, defer=kl_job)
             b = beta if torch.is_tensor(beta) else torch.tensor(float(beta), device=self.dev)
             if gn.dim() != 0:
                 gn = gn.reshape(())
             # one launch: the statistics of this minibatch, and the next minibatch's dropout counter
-            L.ppo_stats(self.sums, self.kl, gn.float().contiguous(), b, cfg.critic, m, self.stats, self.counter)
+            L.ppo_stats(self.sums, self.part_kl, gn.float().contiguous(), b, cfg.critic, m, self.stats, self.counter,
+                        kl_rows=kl_job.nb)
 
     def _extra_snapshot(self):
         return self.counter.clone()

@@ -73,25 +73,48 @@ int g2048_head_fwd(g2048_stream_t stream, const uint16_t *x, const float *wa, co
 /* Scratch floats of g2048_ln_act_bwd for (m, h). */
 size_t g2048_ln_act_bwd_partials(int64_t m, int32_t h);
 
-/* The policy/value heads' share of a layer's output gradient, recomputed from their output gradient
- * (the last residual block's backward, so that the heads never write a [m,h] gradient):
- * dy += dz[:, 0:4] wa + dz[:, 4] wv.  dz fp32 [m, 8] as g2048_ppo_head_loss writes it (columns
- * 5..7 unused); wa fp32 [4, h]; wv fp32 [h] or NULL when the critic is decoupled (game.py:1213-1219). */
-typedef struct g2048_head_grad {
+/* A deferred column reduction.  Every kernel below that reduces over the minibatch rows writes
+ * per-block partial rows part[nb][cols] and, by default, sums them itself (two extra launches).
+ * Given a non-NULL `defer`, it instead describes that sum here and g2048_colsum_batch performs any
+ * number of them in ONE launch: dst <- the fixed-order (deterministic) column sums of part, the
+ * column max_col (>= 0) taking the max instead, split into nseg segments of len[i] columns. */
+#define G2048_COLSUM_SEGS 5
+typedef struct g2048_colsum_job {
+    const float *part;
+    int32_t nb, cols, max_col, nseg;
+    float *dst[G2048_COLSUM_SEGS];
+    int32_t len[G2048_COLSUM_SEGS];
+    int32_t pad_;
+} g2048_colsum_job;
+
+#define G2048_COLSUM_MAX_JOBS 16
+int g2048_colsum_batch(g2048_stream_t stream, const g2048_colsum_job *jobs, int32_t njobs);
+
+#define G2048_DY_MAX_P 4
+
+/* The sources of a residual block's output gradient dy (each optional):
+ *   dres  fp32 [m,h]  a residual-stream gradient accumulated above;
+ *   p[i]  bf16 [m,h]  matmul gradients dG_j W_j of the blocks above (NULL entries are skipped);
+ *   dz    fp32 [m,8]  the policy/value heads' output gradient as g2048_ppo_head_loss writes it
+ *                     (columns 0..4); their share dz[:,0:4] wa + dz[:,4] wv is recomputed in the
+ *                     kernel, so no [m,h] head gradient goes through HBM; wa fp32 [4,h]; wv fp32 [h]
+ *                     or NULL when the critic is decoupled (game.py:1213-1219).
+ * dy = dres + sum_i p[i] + heads, summed in fp32. */
+typedef struct g2048_dy {
+    const float *dres;
+    const uint16_t *p[G2048_DY_MAX_P];
     const float *dz;
     const float *wa;
     const float *wv;
-} g2048_head_grad;
+} g2048_dy;
 
-/* Backward of g2048_ln_act_fwd.  The incoming gradient of y is dy = dres_in + p_in + head (each may
- * be NULL; dres_in fp32 [m,h] is the residual stream's gradient from above, p_in bf16 [m,h] the
- * matmul gradient dG_next W_next, head the heads' share above).  Writes dg (bf16 [m,h], gradient
- * of the pre-norm activation), dy itself to dres_out (fp32, optional: the residual gradient passed
+/* Backward of g2048_ln_act_fwd for the output gradient *dy (above).  Writes dg (bf16 [m,h], gradient
+ * of the pre-norm activation), dy itself to dres_out (fp32, optional: a residual gradient passed
  * further down), and dgamma / dbeta (fp32 [h], overwritten). */
-int g2048_ln_act_bwd(g2048_stream_t stream, const float *dres_in, const uint16_t *p_in, const g2048_head_grad *head,
-                     const uint16_t *g, const float *mean, const float *rstd, const float *gamma, const float *beta,
-                     uint16_t *dg, float *dres_out, float *partials, float *dgamma, float *dbeta, int64_t m, int32_t h,
-                     const g2048_dropout *drop);
+int g2048_ln_act_bwd(g2048_stream_t stream, const g2048_dy *dy, const uint16_t *g, const float *mean,
+                     const float *rstd, const float *gamma, const float *beta, uint16_t *dg, float *dres_out,
+                     float *partials, float *dgamma, float *dbeta, int64_t m, int32_t h, const g2048_dropout *drop,
+                     g2048_colsum_job *defer);
 
 /* Per-minibatch inputs of the PPO loss, gathered on the fly through idx from the flat trajectory
  * (train.py:466-496). */
@@ -114,24 +137,27 @@ size_t g2048_ppo_head_partials(int64_t m, int32_t h);
  *   loss = -mean(ppo - critic v + beta H)
  * Writes masked (fp32 [m,4], for the KL diagnostic), dx = dloss/dx (fp32 [m,h], optional; the value
  * branch is excluded when decouple_critic, game.py:1213-1219) and/or dz = dloss/d(logits, value)
- * (fp32 [m,8], optional: columns 0..4, for g2048_head_grad), the head gradients dwa [4,h], dba [4],
+ * (fp32 [m,8], optional: columns 0..4, for g2048_dy.dz), the head gradients dwa [4,h], dba [4],
  * dwv [h], dbv [1] (overwritten) and sums[3] = {sum ppo, sum H, sum v} over the minibatch.
  * beta_dev: device float (the entropy coefficient, a device scalar so replays see updates). */
 int g2048_ppo_head_loss(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, const float *wv,
                         const float *bv, int64_t m, int32_t h, const g2048_ppo_batch *batch, const float *beta_dev,
                         float critic, float clip_eps, int32_t decouple_critic, float *masked, float *dx, float *dz,
-                        float *partials, float *dwa, float *dba, float *dwv, float *dbv, float *sums);
+                        float *partials, float *dwa, float *dba, float *dwv, float *dbv, float *sums,
+                        g2048_colsum_job *defer);
 
 /* KL(old || new) diagnostic after the optimizer step (train.py:578-601): new logits x Wa^T + ba
  * against the stored masked logits (illegal = -inf).  out[2] = {sum KL, max KL} (overwritten). */
 int g2048_ppo_head_kl(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, int64_t m,
-                      int32_t h, const float *old_masked, float *partials, float *out);
+                      int32_t h, const float *old_masked, float *partials, float *out, g2048_colsum_job *defer);
 
 /* Accumulates one minibatch into the update statistics (train.py:603-642): stats[0..7] +=
  * {loss, policy_loss, entropy_loss, value_loss, grad_norm, entropy, kl_total, kl_average} from the
  * head_loss sums, the KL {sum, max}, the pre-clip gradient norm and beta; stats[8] = max(stats[8],
- * KL max).  counter (optional) is incremented (the next minibatch's dropout counter). */
-int g2048_ppo_stats(g2048_stream_t stream, const float *sums, const float *kl, const float *grad_norm,
+ * KL max).  counter (optional) is incremented (the next minibatch's dropout counter).  kl is either
+ * the final {sum, max} (kl_rows = 0) or the [kl_rows][2] partial rows of a deferred
+ * g2048_ppo_head_kl (its job's part / nb), reduced here in a fixed order. */
+int g2048_ppo_stats(g2048_stream_t stream, const float *sums, const float *kl, int32_t kl_rows, const float *grad_norm,
                     const float *beta_dev, float critic, int64_t m, float *stats, uint64_t *counter);
 
 /* Scratch floats of g2048_wgrad for (m, n1, n2); 0 when the shape is unsupported. */
@@ -141,7 +167,7 @@ size_t g2048_wgrad_partials(int64_t m, int32_t n1, int32_t n2);
  * a = dG bf16 [m,n1], b = X bf16 [m,n2]), fp32 accumulate on bf16 MFMA, fp32 out (overwritten).
  * n1, n2 % 4 == 0 and <= 224. */
 int g2048_wgrad(g2048_stream_t stream, const uint16_t *a, const uint16_t *b, int64_t m, int32_t n1, int32_t n2,
-                float *partials, float *out);
+                float *partials, float *out, g2048_colsum_job *defer);
 
 /* ---- optimizer step (train.py:553-568, :1587-1612) ------------------------------------------ */
 

@@ -118,7 +118,7 @@ def main():
     dzb = torch.empty(M, 8, device=dev)
     out["ppo_head_loss (dz only)"] = timed(lambda: L.ppo_head_loss(xa, wa, ba, wv, bv, batch, beta_t, 0.2, 0.2, False,
                                                                    masked, None, hp, dwa, dba, dwv, dbv, sums, dz=dzb))
-    hg = L.make_head_grad(dzb, wa, wv)
+    hg = (dzb, wa, wv)
     out["ln_act_bwd (head, drop)"] = timed(lambda: L.ln_act_bwd(None, None, X, mean, rstd, ln.weight, ln.bias, G, dres,
                                                                 pb, dgam, dbet, drop, head=hg))
     out["ppo_head_kl"] = timed(lambda: L.ppo_head_kl(xa, wa, ba, masked, hp, klo))
