@@ -15,8 +15,16 @@
 
 namespace g2048 {
 
+// v_bitop3_b32 (gfx950): any 3-input bitwise function in one VALU op.  The immediate is the truth
+// table written with kA/kB/kC standing for the inputs a/b/c (e.g. kA ^ kB ^ kC = three-way xor).
+constexpr uint32_t kA = 0xF0u, kB = 0xCCu, kC = 0xAAu;
+template <uint32_t Imm>
+__device__ __forceinline__ uint32_t bop3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, Imm & 0xFFu);
+}
+
+__device__ __forceinline__ uint32_t zm(uint32_t x) { return bop3<~kA & kC>(x + 0x7F7F7F7Fu, 0u, 0x80808080u); }
 __device__ __forceinline__ uint32_t nzm(uint32_t x) { return (x + 0x7F7F7F7Fu) & 0x80808080u; }
-__device__ __forceinline__ uint32_t zm(uint32_t x) { return ~(x + 0x7F7F7F7Fu) & 0x80808080u; }
 __device__ __forceinline__ uint32_t gem(uint32_t a, uint32_t b) { return ((a | 0x80808080u) - b) & 0x80808080u; }
 __device__ __forceinline__ uint32_t eqm(uint32_t a, uint32_t b) { return zm(a ^ b); }
 
@@ -25,33 +33,49 @@ __device__ __forceinline__ uint32_t row(const uint4 &b, int i) {
 }
 
 // Bit a of the result = action a legal; the reference's scans (game.py:260-330) reduce to
-// "an empty cell before a tile" or "two equal adjacent tiles" along the move axis.
-__device__ __forceinline__ uint32_t legal_mask(const uint4 &b) {
-    const uint32_t r[4] = {b.x, b.y, b.z, b.w};
-    uint32_t L = 0, R = 0, U = 0, D = 0;
+// "an empty cell before a tile" or "two equal adjacent tiles" along the move axis.  Z[i] = bit 7
+// of every empty byte of row i; every term is one or two v_bitop3.
+__device__ __forceinline__ uint32_t legal_mask_z(const uint32_t (&r)[4], const uint32_t (&Z)[4]) {
+    uint32_t L = 0u, R = 0u, U = 0u, D = 0u;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        const uint32_t x = r[i], y = x >> 8;  // y byte j == x byte j+1 (j <= 2)
-        const uint32_t nx = nzm(x), ny = nzm(y) & 0x00808080u;
-        const uint32_t zx = zm(x) & 0x00808080u, zy = zm(y) & 0x00808080u;
-        const uint32_t mh = nx & eqm(x, y) & 0x00808080u;
-        L |= (zx & ny) | mh;
-        R |= (nx & zy) | mh;
+        const uint32_t zs = Z[i] >> 8;  // byte j: cell j+1 empty (byte 3: never)
+        const uint32_t eq = bop3<~kA & ~kB & kC>((r[i] ^ (r[i] >> 8)) + 0x7F7F7F7Fu, Z[i], 0x00808080u);
+        L |= bop3<(kA & ~kB & kC)>(Z[i], zs, 0x00808080u) | eq;  // empty j, tile j+1
+        R |= bop3<(~kA & kB) | kC>(Z[i], zs, eq);                // tile j, empty j+1
     }
 #pragma unroll
     for (int i = 0; i < 3; i++) {
-        const uint32_t a = r[i], c = r[i + 1];
-        const uint32_t na = nzm(a), nc = nzm(c);
-        const uint32_t mv = na & eqm(a, c);
-        U |= (zm(a) & nc) | mv;
-        D |= (na & zm(c)) | mv;
+        const uint32_t eq = bop3<~kA & ~kB & kC>((r[i] ^ r[i + 1]) + 0x7F7F7F7Fu, Z[i], 0x80808080u);
+        U |= bop3<(kA & ~kB) | kC>(Z[i], Z[i + 1], eq);  // empty above a tile
+        D |= bop3<(~kA & kB) | kC>(Z[i], Z[i + 1], eq);  // tile above an empty cell
     }
     return (U ? 1u : 0u) | (D ? 2u : 0u) | (L ? 4u : 0u) | (R ? 8u : 0u);
 }
 
+__device__ __forceinline__ uint32_t legal_mask(const uint4 &b) {
+    const uint32_t r[4] = {b.x, b.y, b.z, b.w};
+    const uint32_t Z[4] = {zm(b.x), zm(b.y), zm(b.z), zm(b.w)};
+    return legal_mask_z(r, Z);
+}
+
 __device__ __forceinline__ uint32_t bytemax(uint32_t a, uint32_t b) {
-    const uint32_t sel = (gem(a, b) >> 7) * 0xFFu;
-    return (a & sel) | (b & ~sel);
+    const uint32_t g = gem(a, b);
+    return bop3<(kC & kA) | (~kC & kB)>(a, b, g | (g - (g >> 7)));
+}
+
+// max exponent of a board: bytes split into 16-bit lanes, packed v_pk_max_u16 tree
+typedef uint16_t g2048_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t board_max(const uint4 &b) {
+    auto pk = [](uint32_t x) { return __builtin_bit_cast(g2048_u16x2, x); };
+    const uint32_t m8 = 0x00FF00FFu;
+    const g2048_u16x2 m0 = __builtin_elementwise_max(pk(b.x & m8), pk((b.x >> 8) & m8));
+    const g2048_u16x2 m1 = __builtin_elementwise_max(pk(b.y & m8), pk((b.y >> 8) & m8));
+    const g2048_u16x2 m2 = __builtin_elementwise_max(pk(b.z & m8), pk((b.z >> 8) & m8));
+    const g2048_u16x2 m3 = __builtin_elementwise_max(pk(b.w & m8), pk((b.w >> 8) & m8));
+    const uint32_t m = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_elementwise_max(m0, m1),
+                                                                              __builtin_elementwise_max(m2, m3)));
+    return max(m & 0xFFFFu, m >> 16);
 }
 
 __device__ __forceinline__ int emptiness(const uint4 &b) {  // game.py:671-680
@@ -68,35 +92,49 @@ struct MonoStats {
     uint32_t pos;  // first row-major cell holding M
 };
 
-__device__ __forceinline__ MonoStats mono_stats(const uint4 &b) {
-    const uint32_t r[4] = {b.x, b.y, b.z, b.w};
-    uint32_t nz[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) nz[i] = nzm(r[i]);
-    MonoStats s{0, 0, 0, 0, 0u, 0u};
+// first row-major cell whose byte equals M (M present on the board): per-row v_ffbl (~0 for a row
+// without M, which never wins the unsigned min), row i offset by OR-ing 32*i into the bit index
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) { return (uint32_t)__builtin_ctzg(x, -1); }
+__device__ __forceinline__ uint32_t first_cell_eq(const uint32_t (&r)[4], uint32_t M) {
+    const uint32_t mb = M * 0x01010101u;
+    const uint32_t f0 = ffbl(zm(r[0] ^ mb)), f1 = ffbl(zm(r[1] ^ mb)) | 32u;
+    const uint32_t f2 = ffbl(zm(r[2] ^ mb)) | 64u, f3 = ffbl(zm(r[3] ^ mb)) | 96u;
+    return min(min(f0, f1), min(f2, f3)) >> 3;
+}
+
+__device__ __forceinline__ MonoStats mono_stats_z(const uint32_t (&r)[4], const uint32_t (&Z)[4], uint32_t M) {
+    MonoStats s{0, 0, 0, 0, M, 0u};
+    uint32_t X[4], NZ[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        const uint32_t x = r[i], y = x >> 8;
-        const uint32_t both = nz[i] & (nz[i] >> 8) & 0x00808080u;
-        s.L += __popc(both & gem(x, y));
-        s.R += __popc(both & gem(y, x));
+        X[i] = r[i] | 0x80808080u;
+        NZ[i] = Z[i] ^ 0x80808080u;
+    }
+    uint32_t L = 0u, R = 0u, T = 0u, B = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t both = NZ[i] & (NZ[i] >> 8);
+        L = __popc((X[i] - (r[i] >> 8)) & both) + L;
+        R = __popc(((X[i] >> 8) - r[i]) & both) + R;
     }
 #pragma unroll
     for (int i = 0; i < 3; i++) {
-        const uint32_t both = nz[i] & nz[i + 1];
-        s.T += __popc(both & gem(r[i], r[i + 1]));
-        s.B += __popc(both & gem(r[i + 1], r[i]));
+        const uint32_t both = NZ[i] & NZ[i + 1];
+        T = __popc((X[i] - r[i + 1]) & both) + T;
+        B = __popc((X[i + 1] - r[i]) & both) + B;
     }
-    uint32_t m = bytemax(bytemax(r[0], r[1]), bytemax(r[2], r[3]));
-    m = bytemax(m, m >> 8);
-    m = bytemax(m, m >> 16);
-    s.M = m & 0xFFu;
-    const uint32_t mb = s.M * 0x01010101u;
-    const uint64_t e01 = (uint64_t)eqm(r[0], mb) | ((uint64_t)eqm(r[1], mb) << 32);
-    const uint64_t e23 = (uint64_t)eqm(r[2], mb) | ((uint64_t)eqm(r[3], mb) << 32);
-    const int bit = e01 ? __builtin_ctzll(e01) : 64 + __builtin_ctzll(e23);
-    s.pos = (uint32_t)(bit >> 3);
+    s.L = (int)L;
+    s.R = (int)R;
+    s.T = (int)T;
+    s.B = (int)B;
+    s.pos = first_cell_eq(r, M);
     return s;
+}
+
+__device__ __forceinline__ MonoStats mono_stats(const uint4 &b) {
+    const uint32_t r[4] = {b.x, b.y, b.z, b.w};
+    const uint32_t Z[4] = {zm(b.x), zm(b.y), zm(b.z), zm(b.w)};
+    return mono_stats_z(r, Z, board_max(b));
 }
 
 __device__ __forceinline__ int mono_value(const MonoStats &s) {
@@ -106,20 +144,29 @@ __device__ __forceinline__ int mono_value(const MonoStats &s) {
 
 __device__ __forceinline__ int monotonicity(const uint4 &b) { return mono_value(mono_stats(b)); }
 
+// select dword i (0..3) of a board without a branch (arguments by value: a select between two
+// fields of one in-memory uint4 would become a dynamically indexed private array)
+__device__ __forceinline__ uint32_t pick_row(uint32_t x, uint32_t y, uint32_t z, uint32_t w, uint32_t i) {
+    const uint64_t lo = ((uint64_t)y << 32) | x, hi = ((uint64_t)w << 32) | z;
+    return (uint32_t)(((i & 2u) ? hi : lo) >> (32u * (i & 1u)));
+}
+
 // Statistics after placing exponent v on the EMPTY cell p of board b (the spawn): only the (up to
 // four) pairs through p change, and the max / first-argmax.
 __device__ __forceinline__ MonoStats mono_add_tile(MonoStats s, const uint4 &b, uint32_t p, uint32_t v) {
     const uint32_t r = p >> 2, c = p & 3u, sh = 8u * c;
-    const uint32_t row = r == 0u ? b.x : r == 1u ? b.y : r == 2u ? b.z : b.w;
-    const uint32_t upr = r == 1u ? b.x : r == 2u ? b.y : r == 3u ? b.z : 0u;
-    const uint32_t dnr = r == 0u ? b.y : r == 1u ? b.z : r == 2u ? b.w : 0u;
+    const uint32_t bx = b.x, by = b.y, bz = b.z, bw = b.w;
+    const uint32_t row = pick_row(bx, by, bz, bw, r);
+    const uint32_t upr = pick_row(0u, bx, by, bz, r);  // row r-1 (0 above the board)
+    const uint32_t dnr = pick_row(by, bz, bw, 0u, r);  // row r+1 (0 below the board)
     const uint32_t left = c > 0u ? (row >> (sh - 8u)) & 0xFFu : 0u;
-    const uint32_t right = c < 3u ? (row >> (sh + 8u)) & 0xFFu : 0u;
+    const uint32_t right = (row >> sh) >> 8;  // c == 3: 0
+    const uint32_t rt = right & 0xFFu;
     const uint32_t up = (upr >> sh) & 0xFFu, dn = (dnr >> sh) & 0xFFu;
-    s.L += (left && left >= v) + (right && v >= right);
-    s.R += (left && v >= left) + (right && right >= v);
-    s.T += (up && up >= v) + (dn && v >= dn);
-    s.B += (up && v >= up) + (dn && dn >= v);
+    s.L += (int)((left != 0u) & (left >= v)) + (int)((rt != 0u) & (v >= rt));
+    s.R += (int)((left != 0u) & (v >= left)) + (int)((rt != 0u) & (rt >= v));
+    s.T += (int)((up != 0u) & (up >= v)) + (int)((dn != 0u) & (v >= dn));
+    s.B += (int)((up != 0u) & (v >= up)) + (int)((dn != 0u) & (dn >= v));
     const bool gt = v > s.M, eq = v == s.M;
     s.pos = gt ? p : (eq ? min(s.pos, p) : s.pos);
     s.M = gt ? v : s.M;
@@ -207,6 +254,19 @@ __device__ __forceinline__ uint32_t kth_bit16(uint32_t m, uint32_t k) {
     return pos;
 }
 
+// k-th (0-based) set bit of a 4-bit mask m (k < popcount(m)): 2-bit answers packed per k in a
+// 32-bit constant indexed by m
+__device__ __forceinline__ uint32_t kth_bit4(uint32_t m, uint32_t k) {
+    constexpr uint32_t T[4] = {
+        [] { uint32_t t = 0; for (uint32_t m = 1; m < 16; m++) { uint32_t j = 0; while (!((m >> j) & 1u)) j++; t |= j << (2 * m); } return t; }(),
+        [] { uint32_t t = 0; for (uint32_t m = 1; m < 16; m++) { uint32_t c = 0, j = 0; for (; j < 4; j++) if ((m >> j) & 1u) { if (c == 1) break; c++; } t |= (j & 3u) << (2 * m); } return t; }(),
+        [] { uint32_t t = 0; for (uint32_t m = 1; m < 16; m++) { uint32_t c = 0, j = 0; for (; j < 4; j++) if ((m >> j) & 1u) { if (c == 2) break; c++; } t |= (j & 3u) << (2 * m); } return t; }(),
+        [] { uint32_t t = 0; for (uint32_t m = 1; m < 16; m++) { uint32_t c = 0, j = 0; for (; j < 4; j++) if ((m >> j) & 1u) { if (c == 3) break; c++; } t |= (j & 3u) << (2 * m); } return t; }(),
+    };
+    const uint32_t t01 = (k & 1u) ? T[1] : T[0], t23 = (k & 1u) ? T[3] : T[2];
+    return ((k & 2u) ? t23 : t01) >> (2u * m) & 3u;
+}
+
 __device__ __forceinline__ void set_cell(uint4 &b, uint32_t pos, uint32_t v) {
     const uint32_t sh = (pos & 3u) * 8u, bits = v << sh, r = pos >> 2;
     b.x |= r == 0u ? bits : 0u;
@@ -226,9 +286,9 @@ __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, u
     for (int r = 0; r < 10; r++) {
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-        c0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        c0 = bop3<kA ^ kB ^ kC>((uint32_t)(p1 >> 32), c1, k0);
         c1 = (uint32_t)p1;
-        c2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c2 = bop3<kA ^ kB ^ kC>((uint32_t)(p0 >> 32), c3, k1);
         c3 = (uint32_t)p0;
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;

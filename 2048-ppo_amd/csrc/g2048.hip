@@ -191,10 +191,10 @@ __device__ __forceinline__ uint32_t board_F(const uint4 &b, const LdsTables &tb)
 }
 
 // spawn on the k-th empty cell (row-major), k = floor(u0 * count / 2^32), value 1 if u1 < 0.9*2^32
-// (same result as spawn<Philox>, computed from per-row popcounts instead of a 16-bit mask)
-__device__ __forceinline__ uint32_t spawn_rows(uint4 &b, uint32_t u0, uint32_t u1, uint32_t &pos) {
-    const uint32_t z0 = zm(b.x), z1 = zm(b.y), z2 = zm(b.z), z3 = zm(b.w);
-    const uint32_t c0 = __popc(z0), c1 = __popc(z1), c2 = __popc(z2), c3 = __popc(z3);
+// (same result as spawn<Philox>, computed from the per-row empty masks Z instead of a 16-bit mask)
+__device__ __forceinline__ uint32_t spawn_rows(uint4 &b, const uint32_t (&Z)[4], uint32_t u0, uint32_t u1,
+                                               uint32_t &pos) {
+    const uint32_t c0 = __popc(Z[0]), c1 = __popc(Z[1]), c2 = __popc(Z[2]), c3 = __popc(Z[3]);
     const uint32_t cnt = c0 + c1 + c2 + c3;
     uint32_t k = (uint32_t)(((uint64_t)u0 * cnt) >> 32);
     const bool g0 = k >= c0;
@@ -204,7 +204,7 @@ __device__ __forceinline__ uint32_t spawn_rows(uint4 &b, uint32_t u0, uint32_t u
     const bool g2 = g1 && k >= c2;
     k -= g2 ? c2 : 0u;
     const uint32_t row = (uint32_t)g0 + (uint32_t)g1 + (uint32_t)g2;
-    const uint32_t z = g2 ? z3 : g1 ? z2 : g0 ? z1 : z0;
+    const uint32_t z = g2 ? Z[3] : g1 ? Z[2] : g0 ? Z[1] : Z[0];
     const uint32_t b0 = (z >> 7) & 1u, b1 = (z >> 15) & 1u, b2 = (z >> 23) & 1u;
     const uint32_t col = (uint32_t)(k >= b0) + (uint32_t)(k >= b0 + b1) + (uint32_t)(k >= b0 + b1 + b2);
     const uint32_t v = u1 < kTwoThreshold ? 1u : 2u;
@@ -217,26 +217,52 @@ __device__ __forceinline__ uint32_t spawn_rows(uint4 &b, uint32_t u0, uint32_t u
     return v;
 }
 
-__device__ __forceinline__ uint32_t board_max(const uint4 &b) {
-    uint32_t m = bytemax(bytemax(b.x, b.y), bytemax(b.z, b.w));
-    m = bytemax(m, m >> 8);
-    m = bytemax(m, m >> 16);
-    return m & 0xFFu;
-}
-
-// Fresh board from one 4-word draw: the two spawns of reset() on an empty board (same result as
-// fresh_board<Philox>: 16 empties, then 15).
-__device__ __forceinline__ uint4 fresh_from_words(const uint4 &r, uint32_t &f) {
-    const uint32_t p1 = r.x >> 28;  // (x * 16) >> 32
-    const uint32_t v1 = r.y < kTwoThreshold ? 1u : 2u;
+// Game2048.reset (game.py:942-950) from the four words of one Philox draw: the two spawns of reset()
+// on an empty board (same result as fresh_board<Philox>: 16 empties, then 15).  f = F(board).
+__device__ __forceinline__ uint4 fresh_from_words(const uint4 &r, uint32_t &f, uint32_t &p1, uint32_t &v1,
+                                                  uint32_t &p2, uint32_t &v2) {
+    p1 = r.x >> 28;  // (x * 16) >> 32
+    v1 = r.y < kTwoThreshold ? 1u : 2u;
     const uint32_t k2 = (uint32_t)(((uint64_t)r.z * 15u) >> 32);
-    const uint32_t p2 = k2 + (k2 >= p1 ? 1u : 0u);
-    const uint32_t v2 = r.w < kTwoThreshold ? 1u : 2u;
+    p2 = k2 + (k2 >= p1 ? 1u : 0u);
+    v2 = r.w < kTwoThreshold ? 1u : 2u;
     uint4 b = make_uint4(0u, 0u, 0u, 0u);
     set_cell(b, p1, v1);
     set_cell(b, p2, v2);
     f = (v1 == 2u ? 4u : 0u) + (v2 == 2u ? 4u : 0u);
     return b;
+}
+
+__device__ __forceinline__ uint4 fresh_from_words(const uint4 &r, uint32_t &f) {
+    uint32_t p1, v1, p2, v2;
+    return fresh_from_words(r, f, p1, v1, p2, v2);
+}
+
+// Legal mask and monotonicity statistics of a fresh two-tile board in closed form (tiles v1 at p1,
+// v2 at p2, p1 != p2).  A direction is blocked only when both tiles already sit against its edge
+// on different lines, or they are the two leading cells of one line with different values.
+__device__ __forceinline__ uint32_t fresh_stats(uint32_t p1, uint32_t v1, uint32_t p2, uint32_t v2, MonoStats &s) {
+    const uint32_t r1 = p1 >> 2, c1 = p1 & 3u, r2 = p2 >> 2, c2 = p2 & 3u;
+    const bool same_row = r1 == r2, same_col = c1 == c2, ne = v1 != v2;
+    const uint32_t sc = c1 + c2, sr = r1 + r2;
+    // blocked-direction bits as 0/1 integers (bool selects here compile to divergent branches)
+    const uint32_t srw = same_row, scl = same_col, nev = ne;
+    const uint32_t left_blk = (srw & nev & (uint32_t)(sc == 1u)) | ((srw ^ 1u) & (uint32_t)(sc == 0u));
+    const uint32_t right_blk = (srw & nev & (uint32_t)(sc == 5u)) | ((srw ^ 1u) & (uint32_t)(sc == 6u));
+    const uint32_t up_blk = (scl & nev & (uint32_t)(sr == 1u)) | ((scl ^ 1u) & (uint32_t)(sr == 0u));
+    const uint32_t down_blk = (scl & nev & (uint32_t)(sr == 5u)) | ((scl ^ 1u) & (uint32_t)(sr == 6u));
+    const uint32_t legal = 15u ^ (up_blk | (down_blk << 1) | (left_blk << 2) | (right_blk << 3));
+    const bool hadj = same_row & ((max(c1, c2) - min(c1, c2)) == 1u);
+    const bool vadj = same_col & ((max(r1, r2) - min(r1, r2)) == 1u);
+    const uint32_t lv = c1 < c2 ? v1 : v2, rv = c1 < c2 ? v2 : v1;  // left / right tile (same row)
+    const uint32_t tv = r1 < r2 ? v1 : v2, bv = r1 < r2 ? v2 : v1;  // top / bottom tile (same column)
+    s.L = (int)(hadj & (lv >= rv));
+    s.R = (int)(hadj & (rv >= lv));
+    s.T = (int)(vadj & (tv >= bv));
+    s.B = (int)(vadj & (bv >= tv));
+    s.M = max(v1, v2);
+    s.pos = v1 > v2 ? p1 : v2 > v1 ? p2 : min(p1, p2);
+    return legal;
 }
 
 // Copy the 128 KiB row table + 1 KiB F table into LDS with 8 independent 16-B loads per lane in
@@ -284,59 +310,63 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
         uint4 b = boards[i];
         const uint32_t env = rng.env_base + (uint32_t)i;
         uint32_t legal = legal_mask(b);
+        MonoStats sb;
+        uint32_t fb;
         if (legal == 0u) {  // a finished board handed in: start a new game first (counter ctr0 + steps)
-            uint32_t f0;
-            b = fresh_from_words(philox_draw(rng.seed, ctr0 + (uint64_t)steps, env, 2u), f0);
-            legal = legal_mask(b);
+            uint32_t p1, v1, p2, v2;
+            b = fresh_from_words(philox_draw(rng.seed, ctr0 + (uint64_t)steps, env, 2u), fb, p1, v1, p2, v2);
+            legal = fresh_stats(p1, v1, p2, v2, sb);
+        } else {
+            // carried across steps: potentials of the current board and F(board)
+            sb = mono_stats(b);
+            fb = sb.M <= 14u ? board_F(b, tabs) : 0u;
         }
-        // carried across steps: potentials of the current board and F(board)
-        MonoStats sb = mono_stats(b);
         int empt_b = emptiness(b);
-        uint32_t fb = sb.M <= 14u ? board_F(b, tabs) : 0u;
         uint4 *pb = tb + i;
         uint8_t *pa = ta + i, *pf = tf + i;
         int32_t *pp = tp + i;
         uint32_t *ppot = tpot + i;
+        uint4 d = philox_draw(rng.seed, ctr0, env, 1u);
         for (int64_t t = 0; t < steps; t++) {
             *pb = b;
             pb += n;
             const uint64_t ctr = ctr0 + (uint64_t)t;
-            const uint4 d = philox_draw(rng.seed, ctr, env, 1u);
-            const uint32_t a = kth_bit16(legal, (uint32_t)(((uint64_t)d.x * (uint32_t)__popc(legal)) >> 32));
+            const uint32_t a = kth_bit4(legal, (uint32_t)(((uint64_t)d.x * (uint32_t)__popc(legal)) >> 32));
             const int mono_b = mono_value(sb);
-            uint32_t pts;
-            uint4 moved;
-            if (sb.M <= 14u) {
-                const bool vert = a < 2u, rev = (a == 1u) | (a == 3u);
-                uint4 w = sel4(vert, transpose(b), b);
-                w = sel4(rev, bswap4(w), w);
-                uint32_t fm;
-                w = slide_lut(w, tabs, fm);
-                w = sel4(rev, bswap4(w), w);
-                moved = sel4(vert, transpose(w), w);
-                pts = fm - fb;
-                fb = fm;
-            } else {
+            // the move through the LDS row table (rows packed as nibbles; a lane holding a tile above
+            // 2^14 reads a meaningless in-range entry and redoes the move on the compute path below)
+            const bool vert = a < 2u, rev = (a & 1u) != 0u;
+            uint4 w = sel4(vert, transpose(b), b);
+            w = sel4(rev, bswap4(w), w);
+            uint32_t fm;
+            w = slide_lut(w, tabs, fm);
+            // the next step's draw does not depend on the board: it fills the LDS latency
+            const uint4 dn = philox_draw(rng.seed, ctr + 1u, env, 1u);
+            w = sel4(rev, bswap4(w), w);
+            uint4 moved = sel4(vert, transpose(w), w);
+            uint32_t pts = fm - fb;
+            fb = fm;
+            if (sb.M > 14u) {
                 uint32_t mx;
                 moved = apply_move(b, a, pts, mx);
             }
-            const MonoStats sa = mono_stats(moved);
+            const uint32_t rm[4] = {moved.x, moved.y, moved.z, moved.w};
+            const uint32_t Zm[4] = {zm(moved.x), zm(moved.y), zm(moved.z), zm(moved.w)};
+            const MonoStats sa = mono_stats_z(rm, Zm, board_max(moved));
             const int mono_a = mono_value(sa);
-            const int empt_a = emptiness(moved);
+            const int empt_a = __popc(Zm[0]) + __popc(Zm[1]) + __popc(Zm[2]) + __popc(Zm[3]);
             uint32_t sp;
-            const uint4 pre = moved;
-            const uint32_t v = spawn_rows(moved, d.y, d.z, sp);
+            const uint32_t v = spawn_rows(moved, Zm, d.y, d.z, sp);
             fb += v == 2u ? 4u : 0u;  // F(2^2) = 4, F(2^1) = 0
-            sb = mono_add_tile(sa, pre, sp, v);
-            const int empt_next = empt_a - 1;
             b = moved;
+            sb = mono_add_tile(sa, b, sp, v);  // cells other than sp are unchanged by the spawn
             legal = legal_mask(b);
             uint32_t fl = legal;
             if (legal == 0u) {
-                b = fresh_from_words(philox_draw(rng.seed, ctr, env, 2u), fb);
-                legal = legal_mask(b);
+                uint32_t p1, v1, p2, v2;
+                b = fresh_from_words(philox_draw(rng.seed, ctr, env, 2u), fb, p1, v1, p2, v2);
+                legal = fresh_stats(p1, v1, p2, v2, sb);
                 fl = FLAG_DONE | FLAG_RESET | legal;
-                sb = mono_stats(b);
             }
             *pa = (uint8_t)a;
             pa += n;
@@ -347,7 +377,8 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
             ppot += n;
             *pf = (uint8_t)fl;
             pf += n;
-            empt_b = (fl & FLAG_RESET) ? 14 : empt_next;
+            empt_b = (fl & FLAG_RESET) ? 14 : empt_a - 1;
+            d = dn;
         }
         boards[i] = b;
     }
