@@ -296,6 +296,27 @@ __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, u
     return make_uint4(c0, c1, c2, c3);
 }
 
+// Philox in two pieces (rounds [R0, R1) on a running state) so a kernel can place the halves into
+// memory-latency windows; philox_rounds<0,10> of the initial state == philox().
+struct PhiloxState {
+    uint32_t c0, c1, c2, c3, k0, k1;
+};
+__device__ __forceinline__ PhiloxState philox_start(uint64_t seed, uint64_t step, uint32_t env, uint32_t stream) {
+    return PhiloxState{(uint32_t)step, (uint32_t)(step >> 32), env, stream, (uint32_t)seed, (uint32_t)(seed >> 32)};
+}
+template <int R0, int R1>
+__device__ __forceinline__ void philox_rounds(PhiloxState &s) {
+#pragma unroll
+    for (int r = R0; r < R1; r++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * s.c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * s.c2;
+        s.c0 = bop3<kA ^ kB ^ kC>((uint32_t)(p1 >> 32), s.c1, s.k0 + (uint32_t)r * 0x9E3779B9u);
+        s.c1 = (uint32_t)p1;
+        s.c2 = bop3<kA ^ kB ^ kC>((uint32_t)(p0 >> 32), s.c3, s.k1 + (uint32_t)r * 0xBB67AE85u);
+        s.c3 = (uint32_t)p0;
+    }
+}
+
 __device__ __forceinline__ uint4 philox_draw(uint64_t seed, uint64_t step, uint32_t env, uint32_t stream) {
     return philox((uint32_t)step, (uint32_t)(step >> 32), env, stream, (uint32_t)seed, (uint32_t)(seed >> 32));
 }

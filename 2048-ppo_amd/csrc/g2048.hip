@@ -332,29 +332,42 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
             pb += n;
             const uint64_t ctr = ctr0 + (uint64_t)t;
             const uint32_t a = kth_bit4(legal, (uint32_t)(((uint64_t)d.x * (uint32_t)__popc(legal)) >> 32));
-            const int mono_b = mono_value(sb);
             // the move through the LDS row table (rows packed as nibbles; a lane holding a tile above
-            // 2^14 reads a meaningless in-range entry and redoes the move on the compute path below)
+            // 2^14 reads a meaningless in-range entry and redoes the move on the compute path below).
+            // The next step's Philox draw does not depend on the board: empty asm statements place its
+            // two halves inside the two LDS round trips (row table, then F table): the first starts
+            // after the loads are issued (memory clobber), the loaded values are consumed after it.
             const bool vert = a < 2u, rev = (a & 1u) != 0u;
             uint4 w = sel4(vert, transpose(b), b);
             w = sel4(rev, bswap4(w), w);
-            uint32_t fm;
-            w = slide_lut(w, tabs, fm);
-            // the next step's draw does not depend on the board: it fills the LDS latency
-            const uint4 dn = philox_draw(rng.seed, ctr + 1u, env, 1u);
+            uint32_t o0 = tabs.row[pack_nib(w.x)], o1 = tabs.row[pack_nib(w.y)];
+            uint32_t o2 = tabs.row[pack_nib(w.z)], o3 = tabs.row[pack_nib(w.w)];
+            uint32_t env_l = env;
+            asm volatile("" : "+v"(env_l)::"memory");
+            PhiloxState ph = philox_start(rng.seed, ctr + 1u, env_l, 1u);
+            philox_rounds<0, 5>(ph);
+            asm volatile("" : "+v"(ph.c0), "+v"(ph.c1), "+v"(ph.c2), "+v"(ph.c3), "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
+            uint32_t f0 = tabs.f2[o0 & 0xFFu], f1 = tabs.f2[o0 >> 8], f2 = tabs.f2[o1 & 0xFFu], f3 = tabs.f2[o1 >> 8];
+            uint32_t f4 = tabs.f2[o2 & 0xFFu], f5 = tabs.f2[o2 >> 8], f6 = tabs.f2[o3 & 0xFFu], f7 = tabs.f2[o3 >> 8];
+            asm volatile("" : "+v"(ph.c0), "+v"(ph.c1), "+v"(ph.c2), "+v"(ph.c3)::"memory");
+            const int mono_b = mono_value(sb);
+            w = make_uint4(unpack_nib(o0), unpack_nib(o1), unpack_nib(o2), unpack_nib(o3));
             w = sel4(rev, bswap4(w), w);
             uint4 moved = sel4(vert, transpose(w), w);
-            uint32_t pts = fm - fb;
-            fb = fm;
-            if (sb.M > 14u) {
-                uint32_t mx;
-                moved = apply_move(b, a, pts, mx);
-            }
+            const bool slow = sb.M > 14u;
+            uint32_t mx, pts_slow = 0u;
+            if (slow) moved = apply_move(b, a, pts_slow, mx);
             const uint32_t rm[4] = {moved.x, moved.y, moved.z, moved.w};
             const uint32_t Zm[4] = {zm(moved.x), zm(moved.y), zm(moved.z), zm(moved.w)};
             const MonoStats sa = mono_stats_z(rm, Zm, board_max(moved));
             const int mono_a = mono_value(sa);
             const int empt_a = __popc(Zm[0]) + __popc(Zm[1]) + __popc(Zm[2]) + __popc(Zm[3]);
+            philox_rounds<5, 10>(ph);
+            const uint4 dn = make_uint4(ph.c0, ph.c1, ph.c2, ph.c3);
+            asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3), "+v"(f4), "+v"(f5), "+v"(f6), "+v"(f7), "+v"(ph.c0));
+            const uint32_t fm = f0 + f1 + f2 + f3 + f4 + f5 + f6 + f7;
+            const uint32_t pts = slow ? pts_slow : fm - fb;
+            fb = fm;
             uint32_t sp;
             const uint32_t v = spawn_rows(moved, Zm, d.y, d.z, sp);
             fb += v == 2u ? 4u : 0u;  // F(2^2) = 4, F(2^1) = 0
