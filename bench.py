@@ -229,7 +229,7 @@ def _c_chunk(args):
     return cnt
 
 
-PMC_PROFILE = Path(__file__).resolve().parent / "profiles" / "r01c"
+PMC_PROFILE = Path(__file__).resolve().parent / "profiles" / "r01d"
 
 
 def pmc_traffic(kernel: str, args):
