@@ -158,45 +158,35 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(const uint4 *__restric
     flags[i] = (uint8_t)r.fl;
 }
 
-__device__ const lut::RowTable kRowLeft = lut::RowTable();
-__device__ const lut::F2Table kF2 = lut::F2Table();
+__device__ const lut::Row12Table kRow12 = lut::Row12Table();
 
-// nibble-pack a row dword whose bytes are < 16: b0 | b1<<4 | b2<<8 | b3<<12
-__device__ __forceinline__ uint32_t pack_nib(uint32_t x) {
-    const uint32_t t = x | (x >> 4);
-    return (t & 0xFFu) | ((t >> 8) & 0xFF00u);
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+
+// kRow12 index of a LEFT-frame row dword (byte j = cell j): c0 + 12 c1 + 144 c2 + 1728 c3 as two
+// packed-u16 dot products.  Bytes are masked to 4 bits so any row (even one holding exponents >= 12,
+// whose lane takes the compute path) indexes inside the 128 KiB LDS allocation.
+__device__ __forceinline__ uint32_t row12_index(uint32_t x) {
+    const u16x2 k02 = {1, 144}, k13 = {12, 1728};
+    return __builtin_amdgcn_udot2(as_u16x2((x >> 8) & 0x000F000Fu), k13,
+                                  __builtin_amdgcn_udot2(as_u16x2(x & 0x000F000Fu), k02, 0u, false), false);
 }
-// inverse of pack_nib
-__device__ __forceinline__ uint32_t unpack_nib(uint32_t r) {
-    const uint32_t t = (r | (r << 8)) & 0x00FF00FFu;
+
+// nibble-packed row (bits 0..15 of a table entry) -> row dword with one exponent per byte
+__device__ __forceinline__ uint32_t unpack_row(uint32_t e) {
+    const uint32_t t = __builtin_amdgcn_perm(0u, e, 0x0C010C00u);  // bytes {e.b0, 0, e.b1, 0}
     return (t & 0x000F000Fu) | ((t & 0x00F000F0u) << 4);
 }
 
-struct LdsTables {
-    const uint16_t *row;
-    const uint32_t *f2;
-    __device__ uint32_t F(uint32_t nib) const { return f2[nib & 0xFFu] + f2[nib >> 8]; }
-};
-
-// LEFT-frame board rows -> moved rows via the LDS table; returns F(moved rows) in fmoved.
-__device__ __forceinline__ uint4 slide_lut(const uint4 &w, const LdsTables &tb, uint32_t &fmoved) {
-    const uint32_t i0 = pack_nib(w.x), i1 = pack_nib(w.y), i2 = pack_nib(w.z), i3 = pack_nib(w.w);
-    const uint32_t o0 = tb.row[i0], o1 = tb.row[i1], o2 = tb.row[i2], o3 = tb.row[i3];
-    fmoved = tb.F(o0) + tb.F(o1) + tb.F(o2) + tb.F(o3);
-    return make_uint4(unpack_nib(o0), unpack_nib(o1), unpack_nib(o2), unpack_nib(o3));
-}
-
-__device__ __forceinline__ uint32_t board_F(const uint4 &b, const LdsTables &tb) {
-    return tb.F(pack_nib(b.x)) + tb.F(pack_nib(b.y)) + tb.F(pack_nib(b.z)) + tb.F(pack_nib(b.w));
-}
-
-// spawn on the k-th empty cell (row-major), k = floor(u0 * count / 2^32), value 1 if u1 < 0.9*2^32
-// (same result as spawn<Philox>, computed from the per-row empty masks Z instead of a 16-bit mask)
-__device__ __forceinline__ uint32_t spawn_rows(uint4 &b, const uint32_t (&Z)[4], uint32_t u0, uint32_t u1,
-                                               uint32_t &pos) {
-    const uint32_t c0 = __popc(Z[0]), c1 = __popc(Z[1]), c2 = __popc(Z[2]), c3 = __popc(Z[3]);
-    const uint32_t cnt = c0 + c1 + c2 + c3;
-    uint32_t k = (uint32_t)(((uint64_t)u0 * cnt) >> 32);
+// spawn on the k-th empty cell (row-major) of a board whose rows have empty masks Z (cnt empties),
+// from ONE uniform word r: k = floor(r * cnt / 2^32), value 1 if the low word of r * cnt is below
+// 0.9 * 2^32 (given k that low word is uniform to within cnt / 2^32).
+__device__ __forceinline__ uint32_t spawn_chain(uint4 &b, const uint32_t (&Z)[4], uint32_t cnt, uint32_t r,
+                                                uint32_t &pos) {
+    const uint64_t prod = (uint64_t)r * cnt;
+    uint32_t k = (uint32_t)(prod >> 32);
+    const uint32_t v = (uint32_t)prod < kTwoThreshold ? 1u : 2u;
+    const uint32_t c0 = __popc(Z[0]), c1 = __popc(Z[1]), c2 = __popc(Z[2]);
     const bool g0 = k >= c0;
     k -= g0 ? c0 : 0u;
     const bool g1 = g0 && k >= c1;
@@ -207,7 +197,6 @@ __device__ __forceinline__ uint32_t spawn_rows(uint4 &b, const uint32_t (&Z)[4],
     const uint32_t z = g2 ? Z[3] : g1 ? Z[2] : g0 ? Z[1] : Z[0];
     const uint32_t b0 = (z >> 7) & 1u, b1 = (z >> 15) & 1u, b2 = (z >> 23) & 1u;
     const uint32_t col = (uint32_t)(k >= b0) + (uint32_t)(k >= b0 + b1) + (uint32_t)(k >= b0 + b1 + b2);
-    const uint32_t v = u1 < kTwoThreshold ? 1u : 2u;
     pos = 4u * row + col;
     const uint32_t bits = v << (8u * col);
     b.x |= row == 0u ? bits : 0u;
@@ -218,9 +207,9 @@ __device__ __forceinline__ uint32_t spawn_rows(uint4 &b, const uint32_t (&Z)[4],
 }
 
 // Game2048.reset (game.py:942-950) from the four words of one Philox draw: the two spawns of reset()
-// on an empty board (same result as fresh_board<Philox>: 16 empties, then 15).  f = F(board).
-__device__ __forceinline__ uint4 fresh_from_words(const uint4 &r, uint32_t &f, uint32_t &p1, uint32_t &v1,
-                                                  uint32_t &p2, uint32_t &v2) {
+// on an empty board (same result as fresh_board<Philox>: 16 empties, then 15).
+__device__ __forceinline__ uint4 fresh_from_words(const uint4 &r, uint32_t &p1, uint32_t &v1, uint32_t &p2,
+                                                  uint32_t &v2) {
     p1 = r.x >> 28;  // (x * 16) >> 32
     v1 = r.y < kTwoThreshold ? 1u : 2u;
     const uint32_t k2 = (uint32_t)(((uint64_t)r.z * 15u) >> 32);
@@ -229,13 +218,23 @@ __device__ __forceinline__ uint4 fresh_from_words(const uint4 &r, uint32_t &f, u
     uint4 b = make_uint4(0u, 0u, 0u, 0u);
     set_cell(b, p1, v1);
     set_cell(b, p2, v2);
-    f = (v1 == 2u ? 4u : 0u) + (v2 == 2u ? 4u : 0u);
     return b;
 }
 
-__device__ __forceinline__ uint4 fresh_from_words(const uint4 &r, uint32_t &f) {
-    uint32_t p1, v1, p2, v2;
-    return fresh_from_words(r, f, p1, v1, p2, v2);
+// The rollout kernel's auto-reset from two spare words (oracle or_reset_words): cell 1 = a >> 28,
+// its value from the other 28 bits of a; cell 2 = floor(bw * 15 / 2^32) among the 15 cells left,
+// its value from the low word of bw * 15.
+__device__ __forceinline__ uint4 fresh_from_pair(uint32_t a, uint32_t bw, uint32_t &p1, uint32_t &v1, uint32_t &p2,
+                                                 uint32_t &v2) {
+    p1 = a >> 28;
+    v1 = (a << 4) < kTwoThreshold ? 1u : 2u;
+    const uint32_t k2 = __umulhi(bw, 15u);
+    p2 = k2 + (k2 >= p1 ? 1u : 0u);
+    v2 = bw * 15u < kTwoThreshold ? 1u : 2u;
+    uint4 b = make_uint4(0u, 0u, 0u, 0u);
+    set_cell(b, p1, v1);
+    set_cell(b, p2, v2);
+    return b;
 }
 
 // Legal mask and monotonicity statistics of a fresh two-tile board in closed form (tiles v1 at p1,
@@ -265,11 +264,11 @@ __device__ __forceinline__ uint32_t fresh_stats(uint32_t p1, uint32_t v1, uint32
     return legal;
 }
 
-// Copy the 128 KiB row table + 1 KiB F table into LDS with 8 independent 16-B loads per lane in
-// flight per batch (a load->store loop would pay one L2/MALL latency per 16 B).
-__device__ __forceinline__ void stage_tables(uint16_t *s_row, uint32_t *s_f2) {
-    constexpr int kChunks = 65536 * 2 / 16;  // uint4 pieces of the row table
-    const uint4 *src = reinterpret_cast<const uint4 *>(kRowLeft.v);
+// Copy the 81 KiB row table into LDS with 8 independent 16-B loads per lane in flight per batch (a
+// load->store loop would pay one L2/MALL latency per 16 B).
+__device__ __forceinline__ void stage_row_table(uint32_t *s_row) {
+    constexpr int kChunks = (int)(lut::kRowEntries * 4u / 16u);  // uint4 pieces of the table
+    const uint4 *src = reinterpret_cast<const uint4 *>(kRow12.v);
     uint4 *dst = reinterpret_cast<uint4 *>(s_row);
     const int nt = blockDim.x;
     for (int base = 0; base < kChunks; base += 8 * nt) {
@@ -285,115 +284,143 @@ __device__ __forceinline__ void stage_tables(uint16_t *s_row, uint32_t *s_f2) {
             if (k < kChunks) dst[k] = v[u];
         }
     }
-    for (int k = threadIdx.x; k < 256; k += nt) s_f2[k] = kF2.v[k];
     __syncthreads();
+}
+
+// Per-lane state of the rollout carried from step to step.
+struct RolloutLane {
+    uint4 b;          // current board (never finished between steps)
+    uint32_t legal;   // its legal mask
+    MonoStats sb;     // its monotonicity statistics
+    int empt_b;       // its empty-cell count
+    uint4 D;          // Philox draw of the current pair of steps: x / y = the two steps' words,
+                      // z / w = the words of a reset inside the pair (at most one: a reset board
+                      // cannot end again one move later)
+    PhiloxState ph;   // draw of the next pair, computed half per step inside the LDS round trip
+};
+
+struct TrajRows {  // row t of each time-major trajectory array
+    uint4 *b;
+    uint8_t *a;
+    int32_t *p;
+    uint32_t *pot;
+    uint8_t *f;
+};
+
+// One env step of the synthetic random-legal policy (oracle or_step_word + auto-reset).  kOdd = the
+// second step of the pair.  One 32-bit word u per step: action k = floor(u * nlegal / 2^32); the
+// low word r of that product (uniform given k) picks the spawn cell and value (spawn_chain).
+template <bool kOdd>
+__device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__restrict__ tab, const TrajRows &tr,
+                                             uint32_t li, uint64_t seed, uint64_t next_pair, uint32_t env) {
+    tr.b[li] = s.b;
+    const uint32_t u = kOdd ? s.D.y : s.D.x;
+    const uint64_t pa = (uint64_t)u * (uint32_t)__popc(s.legal);
+    const uint32_t a = kth_bit4(s.legal, (uint32_t)(pa >> 32)), r = (uint32_t)pa;
+    // the move through the LDS row table in the LEFT frame.  Half of the next pair's Philox rounds
+    // fill the LDS round trip: the empty asm statements start them after the table loads are issued
+    // (memory clobber) and consume the loaded entries after them.
+    const bool vert = a < 2u, rev = (a & 1u) != 0u;
+    uint4 w = sel4(vert, transpose(s.b), s.b);
+    w = sel4(rev, bswap4(w), w);
+    uint32_t e0 = tab[row12_index(w.x)], e1 = tab[row12_index(w.y)];
+    uint32_t e2 = tab[row12_index(w.z)], e3 = tab[row12_index(w.w)];
+    asm volatile("" : "+v"(s.ph.c0), "+v"(s.ph.c1), "+v"(s.ph.c2), "+v"(s.ph.c3)::"memory");
+    if constexpr (kOdd) philox_rounds<5, 10>(s.ph);
+    else philox_rounds<0, 5>(s.ph);
+    asm volatile("" : "+v"(s.ph.c0), "+v"(s.ph.c1), "+v"(s.ph.c2), "+v"(s.ph.c3), "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3));
+    const int mono_b = mono_value(s.sb);
+    w = make_uint4(unpack_row(e0), unpack_row(e1), unpack_row(e2), unpack_row(e3));
+    w = sel4(rev, bswap4(w), w);
+    uint4 moved = sel4(vert, transpose(w), w);
+    // merge points / 4 of the four rows in the high halves, summed as packed u16
+    const uint32_t q = __builtin_bit_cast(uint32_t, (as_u16x2(e0) + as_u16x2(e1)) + (as_u16x2(e2) + as_u16x2(e3)));
+    uint32_t pts = (q >> 16) << 2;
+    if (s.sb.M > 11u) {  // an exponent outside the table: the SWAR compute path
+        uint32_t mx;
+        moved = apply_move(s.b, a, pts, mx);
+    }
+    const uint32_t rm[4] = {moved.x, moved.y, moved.z, moved.w};
+    const uint32_t Zm[4] = {zm(moved.x), zm(moved.y), zm(moved.z), zm(moved.w)};
+    const MonoStats sa = mono_stats_z(rm, Zm, board_max(moved));
+    const int mono_a = mono_value(sa);
+    const int empt_a = __popc(Zm[0]) + __popc(Zm[1]) + __popc(Zm[2]) + __popc(Zm[3]);
+    uint32_t sp;
+    const uint32_t v = spawn_chain(moved, Zm, (uint32_t)empt_a, r, sp);
+    s.b = moved;
+    s.sb = mono_add_tile(sa, moved, sp, v);  // cells other than sp are unchanged by the spawn
+    s.legal = legal_mask(s.b);
+    uint32_t fl = s.legal;
+    if (s.legal == 0u) {  // game over: a new game from the pair's spare words
+        uint32_t p1, v1, p2, v2;
+        s.b = fresh_from_pair(s.D.z, s.D.w, p1, v1, p2, v2);
+        s.legal = fresh_stats(p1, v1, p2, v2, s.sb);
+        fl = FLAG_DONE | FLAG_RESET | s.legal;
+    }
+    tr.a[li] = (uint8_t)a;
+    tr.p[li] = (int32_t)pts;
+    tr.pot[li] = (uint32_t)(mono_b & 0xFF) | ((uint32_t)(mono_a & 0xFF) << 8) | ((uint32_t)(s.empt_b & 0xFF) << 16) |
+                 ((uint32_t)(empt_a & 0xFF) << 24);
+    tr.f[li] = (uint8_t)fl;
+    s.empt_b = (fl & FLAG_RESET) ? 14 : empt_a - 1;
+    if constexpr (kOdd) {
+        s.D = make_uint4(s.ph.c0, s.ph.c1, s.ph.c2, s.ph.c3);
+        s.ph = philox_start(seed, next_pair, env, 1u);
+    }
 }
 
 // Synthetic random-legal rollout (the benchmark workload of BASELINE.md): `steps` env steps per
 // board per launch, board in registers, auto-reset on done, one time-major trajectory record per
 // step: the board the action was taken on [T][N][16], action, points, potentials, flags.
-// Per step: ONE Philox draw (x: action, y/z: spawn); the legal mask carried from the previous
-// step (the action is always legal); the move through the LDS row table while every exponent is
-// <= 14 (the SWAR compute path otherwise); merge points from the F identity.  Workgroups are
-// persistent over boards, so large N keeps several waves per SIMD with one LDS table per CU.
+// Step c (absolute Philox counter) takes word c & 1 of the stream-1 draw at counter c >> 1, so one
+// Philox draw serves two steps (and the reset that may end one of them).  The legal mask is
+// carried from the previous step (the action is always legal); the move goes through the LDS row
+// table while every exponent is <= 11 (the SWAR compute path otherwise); points come from the
+// table.  Workgroups are persistent over boards, so large N keeps several waves per SIMD with one
+// LDS table per CU.
 __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ boards, int64_t n, int64_t steps,
                                                            uint4 *__restrict__ tb, uint8_t *__restrict__ ta,
                                                            int32_t *__restrict__ tp, uint32_t *__restrict__ tpot,
                                                            uint8_t *__restrict__ tf, RngArgs rng) {
-    __shared__ __attribute__((aligned(16))) uint16_t s_row[65536];
-    __shared__ uint32_t s_f2[256];
-    stage_tables(s_row, s_f2);
-    const LdsTables tabs{s_row, s_f2};
+    // 32 Ki entries: every 4-bit-masked index (< 15 * 1885) stays inside; the first 20 736 are staged
+    __shared__ __attribute__((aligned(16))) uint32_t s_row[32768];
+    stage_row_table(s_row);
     const uint64_t ctr0 = rng_counter(rng);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        uint4 b = boards[i];
+        RolloutLane s;
+        s.b = boards[i];
         const uint32_t env = rng.env_base + (uint32_t)i;
-        uint32_t legal = legal_mask(b);
-        MonoStats sb;
-        uint32_t fb;
-        if (legal == 0u) {  // a finished board handed in: start a new game first (counter ctr0 + steps)
+        const uint32_t li = (uint32_t)i;
+        s.legal = legal_mask(s.b);
+        if (s.legal == 0u) {  // a finished board handed in: start a new game first (counter ctr0 + steps)
             uint32_t p1, v1, p2, v2;
-            b = fresh_from_words(philox_draw(rng.seed, ctr0 + (uint64_t)steps, env, 2u), fb, p1, v1, p2, v2);
-            legal = fresh_stats(p1, v1, p2, v2, sb);
+            s.b = fresh_from_words(philox_draw(rng.seed, ctr0 + (uint64_t)steps, env, 2u), p1, v1, p2, v2);
+            s.legal = fresh_stats(p1, v1, p2, v2, s.sb);
         } else {
-            // carried across steps: potentials of the current board and F(board)
-            sb = mono_stats(b);
-            fb = sb.M <= 14u ? board_F(b, tabs) : 0u;
+            s.sb = mono_stats(s.b);
         }
-        int empt_b = emptiness(b);
-        uint4 *pb = tb + i;
-        uint8_t *pa = ta + i, *pf = tf + i;
-        int32_t *pp = tp + i;
-        uint32_t *ppot = tpot + i;
-        uint4 d = philox_draw(rng.seed, ctr0, env, 1u);
-        for (int64_t t = 0; t < steps; t++) {
-            *pb = b;
-            pb += n;
-            const uint64_t ctr = ctr0 + (uint64_t)t;
-            const uint32_t a = kth_bit4(legal, (uint32_t)(((uint64_t)d.x * (uint32_t)__popc(legal)) >> 32));
-            // the move through the LDS row table (rows packed as nibbles; a lane holding a tile above
-            // 2^14 reads a meaningless in-range entry and redoes the move on the compute path below).
-            // The next step's Philox draw does not depend on the board: empty asm statements place its
-            // two halves inside the two LDS round trips (row table, then F table): the first starts
-            // after the loads are issued (memory clobber), the loaded values are consumed after it.
-            const bool vert = a < 2u, rev = (a & 1u) != 0u;
-            uint4 w = sel4(vert, transpose(b), b);
-            w = sel4(rev, bswap4(w), w);
-            uint32_t o0 = tabs.row[pack_nib(w.x)], o1 = tabs.row[pack_nib(w.y)];
-            uint32_t o2 = tabs.row[pack_nib(w.z)], o3 = tabs.row[pack_nib(w.w)];
-            uint32_t env_l = env;
-            asm volatile("" : "+v"(env_l)::"memory");
-            PhiloxState ph = philox_start(rng.seed, ctr + 1u, env_l, 1u);
-            philox_rounds<0, 5>(ph);
-            asm volatile("" : "+v"(ph.c0), "+v"(ph.c1), "+v"(ph.c2), "+v"(ph.c3), "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
-            uint32_t f0 = tabs.f2[o0 & 0xFFu], f1 = tabs.f2[o0 >> 8], f2 = tabs.f2[o1 & 0xFFu], f3 = tabs.f2[o1 >> 8];
-            uint32_t f4 = tabs.f2[o2 & 0xFFu], f5 = tabs.f2[o2 >> 8], f6 = tabs.f2[o3 & 0xFFu], f7 = tabs.f2[o3 >> 8];
-            asm volatile("" : "+v"(ph.c0), "+v"(ph.c1), "+v"(ph.c2), "+v"(ph.c3)::"memory");
-            const int mono_b = mono_value(sb);
-            w = make_uint4(unpack_nib(o0), unpack_nib(o1), unpack_nib(o2), unpack_nib(o3));
-            w = sel4(rev, bswap4(w), w);
-            uint4 moved = sel4(vert, transpose(w), w);
-            const bool slow = sb.M > 14u;
-            uint32_t mx, pts_slow = 0u;
-            if (slow) moved = apply_move(b, a, pts_slow, mx);
-            const uint32_t rm[4] = {moved.x, moved.y, moved.z, moved.w};
-            const uint32_t Zm[4] = {zm(moved.x), zm(moved.y), zm(moved.z), zm(moved.w)};
-            const MonoStats sa = mono_stats_z(rm, Zm, board_max(moved));
-            const int mono_a = mono_value(sa);
-            const int empt_a = __popc(Zm[0]) + __popc(Zm[1]) + __popc(Zm[2]) + __popc(Zm[3]);
-            philox_rounds<5, 10>(ph);
-            const uint4 dn = make_uint4(ph.c0, ph.c1, ph.c2, ph.c3);
-            asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3), "+v"(f4), "+v"(f5), "+v"(f6), "+v"(f7), "+v"(ph.c0));
-            const uint32_t fm = f0 + f1 + f2 + f3 + f4 + f5 + f6 + f7;
-            const uint32_t pts = slow ? pts_slow : fm - fb;
-            fb = fm;
-            uint32_t sp;
-            const uint32_t v = spawn_rows(moved, Zm, d.y, d.z, sp);
-            fb += v == 2u ? 4u : 0u;  // F(2^2) = 4, F(2^1) = 0
-            b = moved;
-            sb = mono_add_tile(sa, b, sp, v);  // cells other than sp are unchanged by the spawn
-            legal = legal_mask(b);
-            uint32_t fl = legal;
-            if (legal == 0u) {
-                uint32_t p1, v1, p2, v2;
-                b = fresh_from_words(philox_draw(rng.seed, ctr, env, 2u), fb, p1, v1, p2, v2);
-                legal = fresh_stats(p1, v1, p2, v2, sb);
-                fl = FLAG_DONE | FLAG_RESET | legal;
-            }
-            *pa = (uint8_t)a;
-            pa += n;
-            *pp = (int32_t)pts;
-            pp += n;
-            *ppot = (uint32_t)(mono_b & 0xFF) | ((uint32_t)(mono_a & 0xFF) << 8) | ((uint32_t)(empt_b & 0xFF) << 16) |
-                    ((uint32_t)(empt_a & 0xFF) << 24);
-            ppot += n;
-            *pf = (uint8_t)fl;
-            pf += n;
-            empt_b = (fl & FLAG_RESET) ? 14 : empt_a - 1;
-            d = dn;
+        s.empt_b = emptiness(s.b);
+        uint64_t pair = ctr0 >> 1;
+        s.D = philox_draw(rng.seed, pair, env, 1u);
+        s.ph = philox_start(rng.seed, pair + 1u, env, 1u);
+        auto rows = [&](int64_t t) {
+            const int64_t o = t * n;
+            return TrajRows{tb + o, ta + o, tp + o, tpot + o, tf + o};
+        };
+        int64_t t = 0;
+        if ((ctr0 & 1u) && steps > 0) {  // the launch starts on the second step of a pair
+            philox_rounds<0, 5>(s.ph);
+            rollout_step<true>(s, s_row, rows(0), li, rng.seed, pair + 2u, env);
+            pair++;
+            t = 1;
         }
-        boards[i] = b;
+        for (; t + 2 <= steps; t += 2, pair++) {
+            rollout_step<false>(s, s_row, rows(t), li, rng.seed, pair + 2u, env);
+            rollout_step<true>(s, s_row, rows(t + 1), li, rng.seed, pair + 2u, env);
+        }
+        if (t < steps) rollout_step<false>(s, s_row, rows(t), li, rng.seed, pair + 2u, env);
+        boards[i] = s.b;
     }
 }
 
@@ -776,7 +803,8 @@ int g2048_env_step(g2048_stream_t stream, const int8_t *boards_in, int8_t *board
 int g2048_env_rollout_random(g2048_stream_t stream, int8_t *boards, int64_t n, int64_t steps, int8_t *traj_boards,
                              uint8_t *traj_actions, int32_t *traj_points, int8_t *traj_pot, uint8_t *traj_flags,
                              const g2048_rng *rng) {
-    if (n < 0 || steps < 0 || !rng || rng->mode != G2048_RNG_PHILOX) return G2048_EINVAL;
+    // n < 2^28: a lane's byte offset into a trajectory row (16 * board id) fits the 32-bit saddr offset
+    if (n < 0 || n >= (int64_t(1) << 28) || steps < 0 || !rng || rng->mode != G2048_RNG_PHILOX) return G2048_EINVAL;
     if (n == 0 || steps == 0) return G2048_OK;
     if (!boards || !traj_boards || !traj_actions || !traj_points || !traj_pot || !traj_flags || !aligned16(boards) ||
         !aligned16(traj_boards) || ((uintptr_t)traj_pot & 3u) || ((uintptr_t)traj_points & 3u))

@@ -99,7 +99,9 @@ int g2048_env_step(g2048_stream_t stream, const int8_t *boards_in, int8_t *board
 
 /* Synthetic random-action rollout (the BASELINE.md throughput workload): `steps` consecutive
    Game2048.step calls per env in ONE launch, board held in registers, uniform random legal actions
-   (Philox stream 1), auto-reset on done.  Step t uses Philox counter rng->counter + t (+ *counter_dev).
+   (Philox stream 1), auto-reset on done.  Step t uses Philox counter rng->counter + t (+ *counter_dev):
+   words x/y/z give the action and the spawn; a game that ends at step t restarts from the 4th words
+   of the draws of steps t and t+1 (oracle or_reset_words).  1 <= N < 2^28 (0 is a no-op).
    Time-major trajectory records (all required): traj_boards [steps][N][16] = the board the action
    was taken on, traj_actions/traj_flags [steps][N] uint8, traj_points [steps][N] int32,
    traj_pot [steps][N][4] int8.  boards [N,16] is read at the start and written at the end.

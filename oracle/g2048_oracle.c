@@ -492,6 +492,16 @@ void or_reset(int8_t b[16], or_rng *r) {
     add_tile(b, r, ph[2], ph[3]);
 }
 
+/* The rollout kernel's auto-reset (build convention, no reference counterpart): the two spawns of
+   reset() from two words a, b.  Cell 1 = a >> 28 (16 empties), its value from the remaining 28 bits
+   (a << 4 < 0.9 * 2^32); cell 2 = floor(b * 15 / 2^32), its value from the low word of b * 15. */
+void or_reset_words(int8_t b[16], uint32_t a, uint32_t bw) {
+    or_rng r = {OR_RNG_PHILOX, 0, 0, 0, NULL, 0, 0};
+    memset(b, 0, 16);
+    add_tile(b, &r, a, a << 4);
+    add_tile(b, &r, bw, bw * 15u);
+}
+
 typedef struct {
     int64_t points;
     int32_t max_tile;
@@ -505,10 +515,11 @@ typedef struct {
 
 /* game.py:952-1030.  `full_info` = 1 computes the info-only heuristics like the reference does.
    Philox spawn words: stream 0 of (seed, step, env) unless `spawn_words` supplies them. */
-static void step_impl(int8_t b[16], int dir, or_rng *r, int full_info, or_step_out *o, const uint32_t *spawn_words);
+static void step_impl(int8_t b[16], int dir, or_rng *r, int full_info, or_step_out *o, const uint32_t *spawn_words,
+                      int chain);
 
 void or_step(int8_t b[16], int dir, or_rng *r, int full_info, or_step_out *o) {
-    step_impl(b, dir, r, full_info, o, NULL);
+    step_impl(b, dir, r, full_info, o, NULL, 0);
 }
 
 /* The synthetic-policy step: ONE Philox draw of stream 1 gives the action (x: k-th legal action,
@@ -521,11 +532,27 @@ int or_step_random(int8_t b[16], or_rng *r, int full_info, or_step_out *o) {
     for (int q = 0; q < 4; q++)
         if (m >> q & 1) { if (k == 0) { dir = q; break; } k--; }
     uint32_t w[2] = {d[1], d[2]};
-    step_impl(b, dir, r, full_info, o, w);
+    step_impl(b, dir, r, full_info, o, w, 0);
     return dir;
 }
 
-static void step_impl(int8_t b[16], int dir, or_rng *r, int full_info, or_step_out *o, const uint32_t *spawn_words) {
+/* The rollout kernel's synthetic-policy step: ONE 32-bit word u.  Action k = floor(u * nlegal / 2^32)
+   (k-th legal action); the low word r of that product picks the spawn: cell floor(r * nempty / 2^32),
+   value 1 if the low word of r * nempty is below 0.9 * 2^32.  Returns the action. */
+int or_step_word(int8_t b[16], uint32_t u, int full_info, or_step_out *o) {
+    int m = or_legal_mask(b), nl = __builtin_popcount(m), dir = 0;
+    uint64_t pa = (uint64_t)u * (uint32_t)nl;
+    int k = (int)(pa >> 32);
+    for (int q = 0; q < 4; q++)
+        if (m >> q & 1) { if (k == 0) { dir = q; break; } k--; }
+    uint32_t w[2] = {(uint32_t)pa, 0u};
+    or_rng r = {OR_RNG_PHILOX, 0, 0, 0, NULL, 0, 0};
+    step_impl(b, dir, &r, full_info, o, w, 1);
+    return dir;
+}
+
+static void step_impl(int8_t b[16], int dir, or_rng *r, int full_info, or_step_out *o, const uint32_t *spawn_words,
+                      int chain) {
     memset(o, 0, sizeof(*o));
     if (!(or_can_move(b, dir) || or_can_merge(b, dir))) {
         o->invalid = 1;
@@ -558,7 +585,10 @@ static void step_impl(int8_t b[16], int dir, or_rng *r, int full_info, or_step_o
     o->maxexp_a = gmax(b);
     uint32_t ph[4] = {0, 0, 0, 0};
     if (r->mode == OR_RNG_PHILOX) {
-        if (spawn_words) { ph[0] = spawn_words[0]; ph[1] = spawn_words[1]; }
+        if (spawn_words) {
+            ph[0] = spawn_words[0];
+            ph[1] = chain ? (uint32_t)((uint64_t)ph[0] * (uint32_t)or_emptiness(b)) : spawn_words[1];
+        }
         else or_philox_draw(r->seed, r->step, r->env, 0u, ph);
     }
     add_tile(b, r, ph[0], ph[1]);
@@ -660,9 +690,10 @@ void or_philox_batch(uint64_t seed, uint64_t step, uint32_t env_base, uint32_t s
 
 /*
  * CPU baseline workload / checker of env_rollout_kernel: `n_envs` independent games stepped
- * `steps` times with the synthetic random-legal policy (or_step_random), auto-reset on done with
- * the stream-2 draw of the same step.  A board handed in already finished is first reset with
- * counter step0 + steps (the kernel's convention).  Optional records (time-major [steps][n_envs]):
+ * `steps` times with the synthetic random-legal policy: step c = step0 + t takes word c & 1 of the
+ * stream-1 draw at counter c >> 1 (or_step_word); a game that ends at step c restarts from words 2
+ * and 3 of that draw (or_reset_words; a pair of steps holds at most one reset).  A board handed in
+ * already finished is first reset with counter step0 + steps, stream 2 (the kernel's convention).  Optional records (time-major [steps][n_envs]):
  * rec_boards [..][16] (board the action was taken on), rec_act, rec_pts, rec_pot [..][4], rec_flags.
  * Returns the number of transitions executed.
  */
@@ -680,12 +711,14 @@ int64_t or_random_rollout_rec(int8_t *boards, int64_t n_envs, int64_t steps, uin
         for (int64_t t = 0; t < steps; t++) {
             int64_t o = t * n_envs + i;
             if (rec_boards) memcpy(rec_boards + 16 * o, b, 16);
-            or_rng r = {OR_RNG_PHILOX, env, seed, step0 + (uint64_t)t, NULL, 0, 0};
+            uint64_t c = step0 + (uint64_t)t;
+            uint32_t d[4];
+            or_philox_draw(seed, c >> 1, env, 1u, d);
             or_step_out so;
-            int dir = or_step_random(b, &r, full_info, &so);
+            int dir = or_step_word(b, d[c & 1u], full_info, &so);
             int m = or_legal_mask(b), fl = m;
             if (so.done) {
-                or_reset(b, &r);
+                or_reset_words(b, d[2], d[3]);
                 fl = 0x80 | 0x20 | or_legal_mask(b);
             }
             if (rec_act) rec_act[o] = (uint8_t)dir;
