@@ -740,6 +740,172 @@ inline bool rng_ok(const g2048_rng *r) {
     return r->mode == G2048_RNG_PHILOX;
 }
 
+
+// ------------------------------------------------------------------ D4 up-sampling ------------
+// calculate_advantage's augmentation (train.py:774-881): k distinct source samples, each with an
+// independent 1/2 chance of a mirror copy (game.py:509-535, axis 1/2 each) and of a rotation copy
+// (game.py:537-590, 90/180/270 degrees clockwise, 1/3 each).  Transform codes: 0 mirror horizontal
+// (flip columns), 1 mirror vertical (flip rows), 2/3/4 rotation by 90/180/270 degrees.
+struct AugPlan {
+    uint32_t src;    // source row
+    uint32_t mirror; // 0 none, else 1 + code
+    uint32_t rot;    // 0 none, else 1 + code
+};
+
+__device__ __forceinline__ uint32_t lowbias32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
+    h ^= h >> 15;
+    h *= 0x846CA68Bu;
+    h ^= h >> 16;
+    return h;
+}
+
+// Sample j -> source row: a 4-round Feistel permutation of [0, 2^bits) (bits even, 2^bits >= n),
+// cycle-walked into [0, n), so k < n samples are k DISTINCT rows (random.sample without replacement).
+__device__ __forceinline__ uint32_t feistel_row(uint32_t j, uint32_t n, uint32_t half, const uint4 &key) {
+    const uint32_t mask = (1u << half) - 1u;
+    const uint32_t rk[4] = {key.x, key.y, key.z, key.w};
+    uint32_t x = j;
+    do {
+        uint32_t l = x >> half, r = x & mask;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t f = lowbias32(r ^ rk[q]) & mask;
+            const uint32_t t = l ^ f;
+            l = r;
+            r = t;
+        }
+        x = (l << half) | r;
+    } while (x >= n);
+    return x;
+}
+
+__device__ __forceinline__ AugPlan aug_plan(uint32_t j, uint32_t n, uint32_t half, const uint4 &key, uint64_t seed,
+                                            uint64_t counter) {
+    const uint4 u = philox_draw(seed, counter, j, 3u);
+    AugPlan p;
+    p.src = feistel_row(j, n, half, key);
+    p.mirror = u.x < 0x80000000u ? 1u + (u.y >> 31) : 0u;
+    p.rot = u.z < 0x80000000u ? 3u + (uint32_t)(((uint64_t)u.w * 3u) >> 32) : 0u;
+    return p;
+}
+
+// direction remap of each transform (UP, DOWN, LEFT, RIGHT = 0..3), 2 bits per direction:
+// mirror h swaps LEFT/RIGHT, mirror v swaps UP/DOWN; 90 degrees: UP->RIGHT->DOWN->LEFT->UP
+__device__ __forceinline__ uint32_t aug_dir(uint32_t code, uint32_t d) {
+    constexpr uint32_t kMap[5] = {0u | 1u << 2 | 3u << 4 | 2u << 6, 1u | 0u << 2 | 2u << 4 | 3u << 6,
+                                  3u | 2u << 2 | 0u << 4 | 1u << 6, 1u | 0u << 2 | 3u << 4 | 2u << 6,
+                                  2u | 3u << 2 | 1u << 4 | 0u << 6};
+    const uint32_t m = code == 0u ? kMap[0] : code == 1u ? kMap[1] : code == 2u ? kMap[2] : code == 3u ? kMap[3] : kMap[4];
+    return (m >> (2u * d)) & 3u;
+}
+
+__device__ __forceinline__ uint4 aug_board(uint32_t code, const uint4 &b) {
+    switch (code) {
+        case 0u: return bswap4(b);                                        // new[i][3-j] = old[i][j]
+        case 1u: return make_uint4(b.w, b.z, b.y, b.x);                   // new[3-i][j] = old[i][j]
+        case 2u: return bswap4(transpose(b));                             // new[j][3-i] = old[i][j]
+        case 3u: { const uint4 r = bswap4(b); return make_uint4(r.w, r.z, r.y, r.x); }
+        default: { const uint4 t = transpose(b); return make_uint4(t.w, t.z, t.y, t.x); }  // new[3-j][i]
+    }
+}
+
+struct AugArgs {
+    uint4 *boards;
+    uint8_t *actions, *legal;
+    float4 *logp;
+    float *adv, *ret;
+    uint32_t n, k, half;
+    uint4 key;
+    uint64_t seed, counter;
+};
+
+__device__ __forceinline__ void aug_write(const AugArgs &a, uint32_t code, uint32_t src, int64_t dst) {
+    a.boards[dst] = aug_board(code, a.boards[src]);
+    a.actions[dst] = (uint8_t)aug_dir(code, a.actions[src] & 3u);
+    const uint32_t lg = a.legal[src];
+    uint32_t nl = lg & ~0xFu;
+    const float4 lp = a.logp[src];
+    const float o[4] = {lp.x, lp.y, lp.z, lp.w};
+    float np[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (uint32_t d = 0; d < 4u; d++) {
+        const uint32_t e = aug_dir(code, d);
+        nl |= ((lg >> d) & 1u) << e;
+        np[e] = o[d];  // new[remap(d)] = old[d] (train.py:810-824)
+    }
+    a.legal[dst] = (uint8_t)nl;
+    a.logp[dst] = make_float4(np[0], np[1], np[2], np[3]);
+    a.adv[dst] = a.adv[src];
+    a.ret[dst] = a.ret[src];
+}
+
+constexpr int kAugBlock = 256;
+
+// pass 1: copies emitted per block of samples
+__global__ __launch_bounds__(kAugBlock) void aug_count_kernel(AugArgs a, uint32_t *__restrict__ counts) {
+    __shared__ uint32_t red[kAugBlock / 64];
+    const uint32_t j = blockIdx.x * kAugBlock + threadIdx.x;
+    uint32_t c = 0u;
+    if (j < a.k) {
+        const uint4 u = philox_draw(a.seed, a.counter, j, 3u);
+        c = (u.x < 0x80000000u ? 1u : 0u) + (u.z < 0x80000000u ? 1u : 0u);
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0u;
+        for (int w = 0; w < kAugBlock / 64; w++) t += red[w];
+        counts[blockIdx.x] = t;
+    }
+}
+
+// pass 2 (one block): exclusive scan of the block counts in place; *count = n + total
+__global__ __launch_bounds__(1024) void aug_scan_kernel(uint32_t *__restrict__ counts, int nblk, uint32_t n,
+                                                        int64_t *__restrict__ count) {
+    __shared__ uint32_t sh[1024];
+    const int per = (nblk + 1023) / 1024, b0 = threadIdx.x * per;
+    uint32_t loc = 0u;
+    for (int q = 0; q < per && b0 + q < nblk; q++) loc += counts[b0 + q];
+    sh[threadIdx.x] = loc;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+        const uint32_t v = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0u;
+        __syncthreads();
+        sh[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = sh[threadIdx.x] - loc;
+    for (int q = 0; q < per && b0 + q < nblk; q++) {
+        const uint32_t c = counts[b0 + q];
+        counts[b0 + q] = run;
+        run += c;
+    }
+    if (threadIdx.x == 1023) *count = (int64_t)n + (int64_t)sh[1023];
+}
+
+// pass 3: the copies, sample by sample (mirror before rotation), after the n real rows
+__global__ __launch_bounds__(kAugBlock) void aug_emit_kernel(AugArgs a, const uint32_t *__restrict__ offsets) {
+    __shared__ uint32_t sh[kAugBlock];
+    const uint32_t j = blockIdx.x * kAugBlock + threadIdx.x;
+    AugPlan p{0u, 0u, 0u};
+    if (j < a.k) p = aug_plan(j, a.n, a.half, a.key, a.seed, a.counter);
+    const uint32_t c = (p.mirror ? 1u : 0u) + (p.rot ? 1u : 0u);
+    sh[threadIdx.x] = c;
+    __syncthreads();
+    for (int o = 1; o < kAugBlock; o <<= 1) {
+        const uint32_t v = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0u;
+        __syncthreads();
+        sh[threadIdx.x] += v;
+        __syncthreads();
+    }
+    int64_t dst = (int64_t)a.n + offsets[blockIdx.x] + (sh[threadIdx.x] - c);
+    if (p.mirror) aug_write(a, p.mirror - 1u, p.src, dst++);
+    if (p.rot) aug_write(a, p.rot - 1u, p.src, dst);
+}
+
 }  // namespace
 
 extern "C" {
@@ -899,6 +1065,51 @@ int g2048_episode_scan(g2048_stream_t stream, const int32_t *points, const int8_
     if (n == 0 || T == 0) return G2048_OK;
     hipLaunchKernelGGL(episode_scan_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, (hipStream_t)stream, points,
                        (const uint4 *)boards, max_tile, step_flags, T, n, run_score, run_max, scores, tiles);
+    return launch_status();
+}
+
+// Philox4x32-10 on the host (the Feistel round keys of g2048_augment)
+static uint4 philox_host(uint64_t seed, uint64_t step, uint32_t env, uint32_t stream) {
+    uint32_t c0 = (uint32_t)step, c1 = (uint32_t)(step >> 32), c2 = env, c3 = stream;
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    for (int r = 0; r < 10; r++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        c0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        c1 = (uint32_t)p1;
+        c2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c3 = (uint32_t)p0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return make_uint4(c0, c1, c2, c3);
+}
+
+size_t g2048_augment_workspace_bytes(int64_t k) {
+    return (size_t)((k > 0 ? k : 1) + kAugBlock - 1) / kAugBlock * sizeof(uint32_t);
+}
+
+int g2048_augment(g2048_stream_t stream, int8_t *boards, uint8_t *actions, uint8_t *legal, float *logp, float *adv,
+                  float *ret, int64_t n, int64_t k, uint64_t seed, uint64_t counter, void *workspace,
+                  size_t workspace_bytes, int64_t *count) {
+    if (n < 0 || n >= (int64_t(1) << 31) || k < 0 || k > n || !count) return G2048_EINVAL;
+    if (k > 0 && (!boards || !actions || !legal || !logp || !adv || !ret || !workspace || !aligned16(boards) ||
+                  !aligned16(logp) || workspace_bytes < g2048_augment_workspace_bytes(k)))
+        return G2048_EINVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    if (k == 0) {  // no copies: *count = n
+        hipLaunchKernelGGL(aug_scan_kernel, dim3(1), dim3(1024), 0, s, (uint32_t *)nullptr, 0, (uint32_t)n, count);
+        return launch_status();
+    }
+    uint32_t bits = 2u;
+    while ((1ull << bits) < (uint64_t)n) bits += 2u;
+    const uint4 key = philox_host(seed, counter, 0xFFFFFFFFu, 4u);
+    AugArgs a{(uint4 *)boards, actions, legal, (float4 *)logp, adv, ret, (uint32_t)n, (uint32_t)k, bits / 2u, key,
+              seed, counter};
+    const int nblk = (int)((k + kAugBlock - 1) / kAugBlock);
+    uint32_t *counts = (uint32_t *)workspace;
+    hipLaunchKernelGGL(aug_count_kernel, dim3(nblk), dim3(kAugBlock), 0, s, a, counts);
+    hipLaunchKernelGGL(aug_scan_kernel, dim3(1), dim3(1024), 0, s, counts, nblk, (uint32_t)n, count);
+    hipLaunchKernelGGL(aug_emit_kernel, dim3(nblk), dim3(kAugBlock), 0, s, a, (const uint32_t *)counts);
     return launch_status();
 }
 

@@ -416,6 +416,7 @@ struct HeadLossArgs {
     const float *adv;
     const float *ret;
     const float *beta_dev;
+    const int64_t *rows;  // nullable: valid-row count of a padded minibatch
     float critic, clip_lo, clip_hi, inv_m;
     int decouple;
 };
@@ -622,6 +623,9 @@ __global__ __launch_bounds__(kThreads) void head_loss_kernel(const uint16_t *__r
                                                              int64_t m, int h, HeadLossArgs a,
                                                              float *__restrict__ masked_out, float *__restrict__ dx_out,
                                                              float *__restrict__ dz_out, float *__restrict__ part) {
+    // rows >= mv are padding: no loss, zero gradient; the mean is over the mv valid rows
+    const int64_t mv = a.rows ? min(*a.rows, m) : m;
+    if (a.rows) a.inv_m = 1.0f / (float)max(mv, (int64_t)1);
     // dynamic LDS: per wave the 64-row image of x (h <= 256: STAGE), then the block reduction
     // [kWaves][5h + 8] over the same bytes
     constexpr bool STAGE = !MULTI;
@@ -672,7 +676,7 @@ __global__ __launch_bounds__(kThreads) void head_loss_kernel(const uint16_t *__r
         {
             const int64_t r = r0 + lane;
             float dz[5] = {0, 0, 0, 0, 0};
-            if (lane < nr) {
+            if (lane < nr && r < mv) {
                 float z[5], mk[4], ppo, ent, vl;
 #pragma unroll
                 for (int k = 0; k < 5; k++) z[k] = zs[wave][lane][k] + (k < 4 ? bsa[k] : bsv);
@@ -779,7 +783,7 @@ template <int KS, bool MULTI>
 __global__ __launch_bounds__(kThreads) void head_kl_kernel(const uint16_t *__restrict__ xin, const float *__restrict__ wa,
                                                            const float *__restrict__ ba, int64_t m, int h,
                                                            const float *__restrict__ old_masked,
-                                                           float *__restrict__ part) {
+                                                           const int64_t *__restrict__ rows, float *__restrict__ part) {
     __shared__ float lds[kWaves][2];
     __shared__ float zs[kWaves][64][5];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
@@ -788,10 +792,11 @@ __global__ __launch_bounds__(kThreads) void head_kl_kernel(const uint16_t *__res
     if (!MULTI) load_head_b3<KS>(fb, wa, nullptr, h, g, c);
     const float bias[4] = {ba[0], ba[1], ba[2], ba[3]};
     float ksum = 0.0f, kmax = -INFINITY;
+    const int64_t mv = rows ? min(*rows, m) : m;  // rows >= mv: padding of a ragged minibatch
     for (int64_t r0 = ((int64_t)blockIdx.x * kWaves + wave) * 64; r0 < m; r0 += nw * 64) {
         head_tiles<KS, MULTI>(zs[wave], fb, xin, wa, nullptr, m, h, r0, g, c, 4);
         const int64_t r = r0 + lane;
-        if (r < m) {
+        if (r < mv) {
             const float4 o4 = *reinterpret_cast<const float4 *>(old_masked + r * 4);
             const float o[4] = {o4.x, o4.y, o4.z, o4.w};
             bool valid[4];
@@ -1219,7 +1224,8 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const uint16_t *__restric
 __global__ __launch_bounds__(256) void ppo_stats_kernel(const float *__restrict__ sums, const float *__restrict__ kl,
                                                         int kl_rows, const float *__restrict__ gn,
                                                         const float *__restrict__ beta, float critic, float m,
-                                                        float *__restrict__ stats, uint64_t *__restrict__ counter) {
+                                                        const int64_t *__restrict__ rows, float *__restrict__ stats,
+                                                        uint64_t *__restrict__ counter) {
     __shared__ float red[2][256];
     float ks = 0.0f, km = -INFINITY;
     if (kl_rows > 0) {  // the KL kernel's partial rows: fixed-order sums
@@ -1244,6 +1250,7 @@ __global__ __launch_bounds__(256) void ppo_stats_kernel(const float *__restrict_
         km = kl[1];
     }
     if (threadIdx.x != 0) return;
+    if (rows) m = (float)max(*rows, (int64_t)1);
     const float s_ppo = sums[0] / m, s_ent = sums[1] / m, s_v = sums[2] / m, b = *beta;
     stats[0] += -(s_ppo - critic * s_v + b * s_ent);
     stats[1] += -s_ppo;
@@ -1588,7 +1595,7 @@ int g2048_ppo_head_loss(g2048_stream_t stream, const uint16_t *x, const float *w
     if (!al(x, 8) || !al(masked, 16) || (dx && !al(dx, 16)) || (dz && !al(dz, 16))) return G2048_EINVAL;
     const hipStream_t s = (hipStream_t)stream;
     HeadLossArgs a{batch->idx, batch->action, batch->legal, batch->old_logp, batch->adv, batch->ret, beta_dev,
-                   critic, 1.0f - clip_eps, 1.0f + clip_eps, 1.0f / (float)m, decouple_critic};
+                   batch->rows, critic, 1.0f - clip_eps, 1.0f + clip_eps, 1.0f / (float)m, decouple_critic};
     const int nb = head_blocks(m);
     const int C = 5 * h + 8;
     const size_t red = sizeof(float) * kWaves * C, img = (size_t)kWaves * 128 * h;
@@ -1630,14 +1637,16 @@ int g2048_ppo_head_loss(g2048_stream_t stream, const uint16_t *x, const float *w
 }
 
 int g2048_ppo_head_kl(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, int64_t m,
-                      int32_t h, const float *old_masked, float *partials, float *out, g2048_colsum_job *defer) {
+                      int32_t h, const float *old_masked, const int64_t *rows, float *partials, float *out,
+                      g2048_colsum_job *defer) {
     if (!shape_ok(m, h) || m == 0 || !x || !wa || !ba || !old_masked || !partials || !out) return G2048_EINVAL;
     if (!al(x, 8) || !al(old_masked, 16)) return G2048_EINVAL;
     const hipStream_t s = (hipStream_t)stream;
     const int nb = head_blocks(m);
     switch ((h + 31) / 32) {
 #define G2048_HK(KS_, MULTI_) \
-    hipLaunchKernelGGL((head_kl_kernel<KS_, MULTI_>), dim3(nb), dim3(kThreads), 0, s, x, wa, ba, m, h, old_masked, partials)
+    hipLaunchKernelGGL((head_kl_kernel<KS_, MULTI_>), dim3(nb), dim3(kThreads), 0, s, x, wa, ba, m, h, old_masked, rows, \
+                       partials)
         case 1: G2048_HK(1, false); break;
         case 2: G2048_HK(2, false); break;
         case 3: G2048_HK(3, false); break;
@@ -1762,10 +1771,11 @@ int g2048_head_fwd(g2048_stream_t stream, const uint16_t *x, const float *wa, co
 
 
 int g2048_ppo_stats(g2048_stream_t stream, const float *sums, const float *kl, int32_t kl_rows, const float *grad_norm,
-                    const float *beta_dev, float critic, int64_t m, float *stats, uint64_t *counter) {
+                    const float *beta_dev, float critic, int64_t m, const int64_t *rows, float *stats,
+                    uint64_t *counter) {
     if (!sums || !kl || kl_rows < 0 || !grad_norm || !beta_dev || !stats || m <= 0) return G2048_EINVAL;
     hipLaunchKernelGGL(ppo_stats_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, sums, kl, kl_rows, grad_norm,
-                       beta_dev, critic, (float)m, stats, counter);
+                       beta_dev, critic, (float)m, rows, stats, counter);
     return status();
 }
 

@@ -27,6 +27,7 @@ EXPORTED = (
     "g2048_preview_points", "g2048_legal_mask",
     "g2048_obs_encode", "g2048_sample_actions", "g2048_rtg_prepare", "g2048_reward_rtg_workspace_bytes",
     "g2048_reward_rtg", "g2048_rtg_finalize", "g2048_build_info", "g2048_episode_scan",
+    "g2048_augment_workspace_bytes", "g2048_augment",
     # include/g2048_ppo.h
     "g2048_obs_gather", "g2048_ln_act_fwd", "g2048_ln_act_bwd_partials", "g2048_ln_act_bwd",
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
@@ -69,7 +70,8 @@ class Dropout(ctypes.Structure):
 class PPOBatch(ctypes.Structure):
     """struct g2048_ppo_batch"""
     _fields_ = [("idx", ctypes.c_void_p), ("action", ctypes.c_void_p), ("legal", ctypes.c_void_p),
-                ("old_logp", ctypes.c_void_p), ("adv", ctypes.c_void_p), ("ret", ctypes.c_void_p)]
+                ("old_logp", ctypes.c_void_p), ("adv", ctypes.c_void_p), ("ret", ctypes.c_void_p),
+                ("rows", ctypes.c_void_p)]
 
 
 DY_MAX_P = 4
@@ -125,6 +127,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
                          f"or `make -C 2048-ppo_amd/csrc`")
     L = ctypes.CDLL(str(p))
     vp, i64, i32, u32, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_size_t
+    u64 = ctypes.c_uint64
     rp, cp = ctypes.POINTER(Rng), ctypes.POINTER(RewardCfg)
     dp, bp = ctypes.POINTER(Dropout), ctypes.POINTER(PPOBatch)
     jp = ctypes.POINTER(ColsumJob)
@@ -144,6 +147,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_rtg_finalize": (ctypes.c_int, [vp, vp, vp, cp]),
         "g2048_build_info": (ctypes.c_char_p, []),
         "g2048_episode_scan": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp]),
+        "g2048_augment_workspace_bytes": (ctypes.c_size_t, [i64]),
+        "g2048_augment": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, i64, u64, u64, vp, ctypes.c_size_t, vp]),
         "g2048_obs_gather": (ctypes.c_int, [vp, vp, vp, i64, vp]),
         "g2048_ln_act_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, dp]),
         "g2048_ln_act_bwd_partials": (sz, [i64, i32]),
@@ -153,7 +158,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_ppo_head_partials": (sz, [i64, i32]),
         "g2048_ppo_head_loss": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, bp, vp, ctypes.c_float,
                                                ctypes.c_float, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, jp]),
-        "g2048_ppo_head_kl": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, vp, vp, vp, jp]),
+        "g2048_ppo_head_kl": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, vp, vp, vp, vp, jp]),
         "g2048_dropout_mask": (ctypes.c_int, [vp, i64, i32, dp, vp]),
         "g2048_wgrad_partials": (sz, [i64, i32, i32]),
         "g2048_wgrad": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, vp, vp, jp]),
@@ -161,7 +166,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_mlp_fwd_lds_bytes": (sz, [i32, i32]),
         "g2048_mlp_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, i64, i32, i32, dp]),
         "g2048_head_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, vp, i64, vp]),
-        "g2048_ppo_stats": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, ctypes.c_float, i64, vp, vp]),
+        "g2048_ppo_stats": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, ctypes.c_float, i64, vp, vp, vp]),
         "g2048_muon_supported": (ctypes.c_int, [i32, i32]),
         "g2048_muon_step": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.POINTER(MuonCfg)]),
         "g2048_adamw_step": (ctypes.c_int, [vp, ctypes.POINTER(AdamWGroup), i32, vp, vp, vp, ctypes.c_float,
@@ -296,6 +301,27 @@ def episode_scan(points, boards, max_tile, step_flags, run_score, run_max, score
         _dev(scores, torch.int64, "scores"), _dev(tiles, torch.int32, "tiles")), "g2048_episode_scan")
 
 
+def augment_workspace_bytes(k: int) -> int:
+    return int(load().g2048_augment_workspace_bytes(int(k)))
+
+
+def augment(boards, actions, legal, logp, adv, ret, n: int, k: int, seed: int, counter: int, workspace, count):
+    """D4 up-sampling (train.py:774-881): appends the copies of k sampled rows of the pool after its
+    n real rows; count (int64 [1], device) = n + copies.  Pool capacity >= n + 2k."""
+    cap = boards.shape[0]
+    for t, nm in ((actions, "actions"), (legal, "legal"), (logp, "logp"), (adv, "adv"), (ret, "ret")):
+        if t.shape[0] != cap:
+            raise G2048Error(f"augment: {nm} has {t.shape[0]} rows, boards {cap}")
+    if k > 0 and cap < n + 2 * k:
+        raise G2048Error(f"augment: pool capacity {cap} < n + 2k = {n + 2 * k}")
+    _check(load().g2048_augment(
+        _stream(boards), _dev(boards, torch.int8, "boards"), _dev(actions, torch.uint8, "actions"),
+        _dev(legal, torch.uint8, "legal"), _dev(logp, torch.float32, "logp"), _dev(adv, torch.float32, "adv"),
+        _dev(ret, torch.float32, "ret"), int(n), int(k), int(seed) & (2**64 - 1), int(counter) & (2**64 - 1),
+        _dev(workspace, None, "workspace"), workspace.numel() * workspace.element_size(),
+        _dev(count, torch.int64, "count")), "g2048_augment")
+
+
 def rtg_finalize(state, partials, cfg: RewardCfg):
     _check(load().g2048_rtg_finalize(_stream(state), _dev(state, torch.float64, "state"),
                                      _dev(partials, torch.float64, "partials"), ctypes.byref(cfg)),
@@ -364,10 +390,11 @@ def ppo_head_partials(m: int, h: int) -> int:
     return int(load().g2048_ppo_head_partials(m, h))
 
 
-def make_ppo_batch(idx, action, legal, old_logp, adv, ret) -> PPOBatch:
+def make_ppo_batch(idx, action, legal, old_logp, adv, ret, rows=None) -> PPOBatch:
+    """rows (optional int64 device scalar): valid rows of a padded ragged minibatch."""
     return PPOBatch(_dev(idx, torch.int64, "idx"), _dev(action, torch.uint8, "action"),
                     _dev(legal, torch.uint8, "legal"), _dev(old_logp, torch.float32, "old_logp"),
-                    _dev(adv, torch.float32, "adv"), _dev(ret, torch.float32, "ret"))
+                    _dev(adv, torch.float32, "adv"), _dev(ret, torch.float32, "ret"), _dev(rows, torch.int64, "rows"))
 
 
 def ppo_head_loss(x, wa, ba, wv, bv, batch: PPOBatch, beta_dev, critic, clip_eps, decouple, masked, dx, partials,
@@ -383,11 +410,12 @@ def ppo_head_loss(x, wa, ba, wv, bv, batch: PPOBatch, beta_dev, critic, clip_eps
         _defer(defer)), "g2048_ppo_head_loss")
 
 
-def ppo_head_kl(x, wa, ba, old_masked, partials, out, defer: ColsumJob | None = None):
+def ppo_head_kl(x, wa, ba, old_masked, partials, out, defer: ColsumJob | None = None, rows=None):
     m, h = x.shape
     _check(load().g2048_ppo_head_kl(
         _stream(x), _dev(x, torch.bfloat16, "x"), _dev(wa, torch.float32, "wa"), _dev(ba, torch.float32, "ba"), m, h,
-        _dev(old_masked, torch.float32, "old_masked"), _dev(partials, torch.float32, "partials"),
+        _dev(old_masked, torch.float32, "old_masked"), _dev(rows, torch.int64, "rows"),
+        _dev(partials, torch.float32, "partials"),
         _dev(out, torch.float32, "out"), _defer(defer)), "g2048_ppo_head_kl")
 
 
@@ -474,10 +502,11 @@ def head_fwd(x, wa, ba, wv, bv, logits, value):
         logits.stride(0), _dev(value, torch.float32, "value")), "g2048_head_fwd")
 
 
-def ppo_stats(sums, kl, grad_norm, beta_dev, critic: float, m: int, stats, counter=None, kl_rows: int = 0):
+def ppo_stats(sums, kl, grad_norm, beta_dev, critic: float, m: int, stats, counter=None, kl_rows: int = 0, rows=None):
     """kl: final {sum, max}, or (kl_rows > 0) the partial rows of a deferred ppo_head_kl."""
     _check(load().g2048_ppo_stats(_stream(stats), _dev(sums, torch.float32, "sums"), _dev(kl, torch.float32, "kl"),
                                   int(kl_rows),
                                   _dev(grad_norm, torch.float32, "grad_norm"), _dev(beta_dev, torch.float32, "beta"),
-                                  float(critic), int(m), _dev(stats, torch.float32, "stats"),
+                                  float(critic), int(m), _dev(rows, torch.int64, "rows"),
+                                  _dev(stats, torch.float32, "stats"),
                                   _dev(counter, torch.int64, "counter")), "g2048_ppo_stats")

@@ -20,7 +20,9 @@ action/value heads), FusedPPOUpdater writes the forward and backward out by hand
 Activations are bf16, LayerNorm statistics / gradients / reductions fp32, master weights fp32.
 Dropout keep masks are Philox draws regenerated in the backward pass (nothing stored); they are
 statistically, not bitwise, the reference's torch.nn.Dropout.  The whole step is one hipGraph
-(two around the all-reduce with several ranks), replayed per minibatch.
+(two around the all-reduce with several ranks), replayed per minibatch; the ragged last minibatch of
+an epoch replays the same graph, padded, with a device row count that masks the padding out of
+the loss, the gradient and the statistics.
 """
 
 from __future__ import annotations
@@ -104,6 +106,7 @@ class FusedPPOUpdater(PPOUpdater):
                         for w in self.lin]
         self.sums = torch.zeros(3, dtype=torch.float32, device=d)
         self.kl = torch.zeros(2, dtype=torch.float32, device=d)
+        self.rows = torch.full((1,), bs, dtype=torch.int64, device=d)  # valid rows (ragged last minibatch)
         self.bs = bs
 
     def _drop(self, layer: int, pass_: int):
@@ -136,7 +139,8 @@ class FusedPPOUpdater(PPOUpdater):
     def loss_backward(self, data, idx, beta):
         """Heads + PPO loss + backward of the minibatch; gradients land in the GradBucket views."""
         nl = len(self.lin)
-        batch = L.make_ppo_batch(idx, data["actions"], data["legal"], data["logp"], data["adv"], data["ret"])
+        batch = L.make_ppo_batch(idx, data["actions"], data["legal"], data["logp"], data["adv"], data["ret"],
+                                 rows=self.rows)
         # the heads write only their output gradient dz [m, 8]; the last block's backward recomputes
         # their share dz W of its output gradient (no [m, h] head gradient in HBM)
         jobs = [L.ColsumJob()]
@@ -169,6 +173,11 @@ class FusedPPOUpdater(PPOUpdater):
             L.colsum_batch(jobs[i:i + L.COLSUM_MAX_JOBS])
 
     # ---------------------------------------------------------------- PPOUpdater hooks ----
+    ragged_pad = True  # the ragged last minibatch runs padded to full size (g2048_ppo_batch.rows)
+
+    def _set_rows(self, n: int):
+        self.rows.fill_(n)
+
     def update(self, data: dict, beta: float, encode=None) -> dict:
         bs = min(self.cfg.batch_size, data["actions"].shape[0])
         self._alloc(bs)
@@ -193,13 +202,13 @@ class FusedPPOUpdater(PPOUpdater):
         with torch.no_grad():
             x = self._layers(1)  # KL re-forward of the same minibatch (x0 still holds its encoding)
             kl_job = L.ColsumJob()  # the KL partial rows are reduced by the statistics kernel
-            L.ppo_head_kl(x, self.wa, self.ba, self.masked, self.part_kl, self.kl, defer=kl_job)
+            L.ppo_head_kl(x, self.wa, self.ba, self.masked, self.part_kl, self.kl, defer=kl_job, rows=self.rows)
             b = beta if torch.is_tensor(beta) else torch.tensor(float(beta), device=self.dev)
             if gn.dim() != 0:
                 gn = gn.reshape(())
             # one launch: the statistics of this minibatch, and the next minibatch's dropout counter
             L.ppo_stats(self.sums, self.part_kl, gn.float().contiguous(), b, cfg.critic, m, self.stats, self.counter,
-                        kl_rows=kl_job.nb)
+                        kl_rows=kl_job.nb, rows=self.rows)
 
     def _extra_snapshot(self):
         return self.counter.clone()

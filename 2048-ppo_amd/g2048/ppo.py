@@ -86,6 +86,11 @@ class PPOUpdater:
         self.beta_t = torch.zeros((), dtype=torch.float32, device=self.dev)
         self._g = None
 
+    ragged_pad = False  # True: the updater runs a ragged minibatch padded to full size (_set_rows)
+
+    def _set_rows(self, n: int):
+        raise NotImplementedError
+
     def _forward(self, obs):
         if self.cfg.amp_dtype is not None and obs.is_cuda:
             with torch.autocast("cuda", dtype=self.cfg.amp_dtype, cache_enabled=not self.graph):
@@ -104,17 +109,23 @@ class PPOUpdater:
         self.beta_t.fill_(beta)
         nb = 0
         self.model.train()
-        use_graph = self.graph and m_total % bs == 0
+        use_graph = self.graph and (m_total % bs == 0 or self.ragged_pad)
         if use_graph:
             self._ensure_graph(data, bs, encode)
         for _ in range(cfg.epochs):
             perm = torch.randperm(m_total, device=self.dev, generator=self.gen)
             for s in range(0, m_total, bs):
                 idx = perm[s:s + bs]
+                n = idx.shape[0]
+                if n < bs and self.ragged_pad:  # DataLoader's ragged last batch (drop_last=False), padded
+                    idx = torch.cat([idx, idx.new_zeros(bs - n)])
+                    self._set_rows(n)
                 if use_graph:
                     self._replay(idx)
                 else:
                     self._minibatch(idx, data, self.beta_t, encode)
+                if n < bs and self.ragged_pad:
+                    self._set_rows(bs)
                 nb += 1
         st = self.stats / max(nb, 1)
         st[STAT_KEYS.index("kl_max")] = self.stats[STAT_KEYS.index("kl_max")]

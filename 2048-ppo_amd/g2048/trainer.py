@@ -56,6 +56,7 @@ class TrainConfig:
     beta_min: float = 0.001
     beta_max: float = 1.0
     beta_lr: float = 0.01
+    upsample_ratio: float = 0.0    # --upsample-ratio: D4 copies of int(ratio * samples) samples (device kernel)
     horizon: int = 0
     seed: int = 0x2048
     graph: bool = True
@@ -128,6 +129,7 @@ class VecTrainer:
         self.highest = 0
         self.ema = {"avg_score": 0.0, "pct_512": 0.0, "pct_1024": 0.0, "pct_2048": 0.0, "explained_var": 0.0}
         self._started = False
+        self._pool = None  # sample pool (real + D4 copies) when --upsample-ratio > 0
         self._chunk_graphs = {}
         self.profile = False
         self.timings: dict[str, float] = {}
@@ -223,10 +225,15 @@ class VecTrainer:
             valid_mask = (sf & L.FLAG_INACTIVE) == 0
             valid = torch.nonzero(valid_mask.reshape(-1)).squeeze(1)
             data = {k: v.index_select(0, valid) for k, v in data.items()}
+        n_aug = 0
+        if cfg.upsample_ratio > 0:
+            data, n_aug = self._augment(data, step)
+        self._mark("augment_ms")
         ustats = self.ppo.update(data, self.beta, self._encode)
         self.opt.scheduler_step()
         self._mark("update_ms")
         metrics = self._metrics(T, valid, ustats)
+        metrics["augmented_samples"] = n_aug
         self._mark("metrics_ms")
         self._collect_timings()
         if cfg.adaptive_beta:  # train.py:1740-1746
@@ -234,6 +241,30 @@ class VecTrainer:
             self.beta = max(cfg.beta_min, min(cfg.beta_max, self.beta * (1.0 + cfg.beta_lr * err)))
         metrics["current_beta"] = self.beta
         return metrics
+
+    def _augment(self, data: dict, step: int):
+        """calculate_advantage's D4 up-sampling (train.py:774-881) on the device: the real samples are
+        copied into a fixed pool (stable pointers for the captured update) and g2048_augment appends
+        the mirror / rotation copies of int(n * ratio) distinct samples.  Returns (pool views over
+        real + copies, number of copies); one host read of the copy count."""
+        n = data["actions"].shape[0]
+        k = min(int(n * self.cfg.upsample_ratio), n)
+        cap = n + 2 * k
+        if self._pool is None or self._pool["actions"].shape[0] < cap:
+            cap = cap if not self.episodic else int(cap * 1.25) + 1  # episodic sizes vary per step
+            self._pool = {key: torch.empty((cap,) + tuple(v.shape[1:]), dtype=v.dtype, device=self.dev)
+                          for key, v in data.items()}
+            self._aug_ws = torch.empty(L.augment_workspace_bytes(max(k, 1) * 2), dtype=torch.uint8, device=self.dev)
+            self._aug_count = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        pool = self._pool
+        for key, v in data.items():
+            pool[key][:n].copy_(v)
+        if self._aug_ws.numel() < L.augment_workspace_bytes(k):
+            self._aug_ws = torch.empty(L.augment_workspace_bytes(k), dtype=torch.uint8, device=self.dev)
+        L.augment(pool["boards"], pool["actions"], pool["legal"], pool["logp"], pool["adv"], pool["ret"], n, k,
+                  self.cfg.seed * 131 + self.rank, step, self._aug_ws, self._aug_count)
+        c = int(self._aug_count.item())
+        return {key: v[:c] for key, v in pool.items()}, c - n
 
     # ------------------------------------------------------------------ metrics ---------------
     def _episode_stats(self, T):

@@ -272,8 +272,8 @@ def train(
                       points=points_weight, mono=monotonicity_weight, emptiness=emptiness_weight, rtg_beta=rtg_beta,
                       warmup_steps=warmup_steps, beta1=beta1, beta2=beta2, weight_decay=weight_decay,
                       adaptive_beta=adaptive_beta, target_entropy=target_entropy, beta_min=beta_min,
-                      beta_max=beta_max, beta_lr=beta_lr, horizon=horizon, seed=seed, graph=not no_graph,
-                      amp=not fp32)
+                      beta_max=beta_max, beta_lr=beta_lr, upsample_ratio=upsample_ratio, horizon=horizon, seed=seed,
+                      graph=not no_graph, amp=not fp32)
     logger.print(f"Creating GameMLP model (hidden={hidden_size}, layers={num_layers}); {num_episodes} envs/GPU x {ws}")
     tr = VecTrainer(cfg, device)
     best_eval = 0.0

@@ -53,6 +53,7 @@ def parse():
     p.add_argument("--train-warmup", type=int, default=2)
     p.add_argument("--train-horizon", type=int, default=64)
     p.add_argument("--train-batch", type=int, default=65536)
+    p.add_argument("--train-upsample", type=float, default=0.25, help="--upsample-ratio of the README command")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of each CPU-baseline leg (0=off)")
     p.add_argument("--sweep", default="", help="comma list of extra board counts for the rollout kernel")
     return p.parse_args()

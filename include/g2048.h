@@ -166,7 +166,6 @@ int g2048_reward_rtg(g2048_stream_t stream, const int32_t *points, const int8_t 
                      const g2048_reward_cfg *cfg, const double *state, float *g_raw, float *g_norm,
                      float *adv, double *partials, void *workspace, size_t workspace_bytes);
 
-/* EMA moment update with the batch statistics (train.py:898-901); advances rtg_step. */
 /* Episode statistics of a fixed-horizon rollout (compute_batch_stats' scores and tiles,
  * train.py:1040-1120): per env, the running score / max tile exponent of its current game is
  * carried across calls in run_score [n] / run_max [n]; scores[t][e] / tiles[t][e] are the finished
@@ -176,8 +175,26 @@ int g2048_episode_scan(g2048_stream_t stream, const int32_t *points, const int8_
                        const uint8_t *step_flags, int64_t T, int64_t n, int64_t *run_score, int32_t *run_max,
                        int64_t *scores, int32_t *tiles);
 
+/* EMA moment update with the batch statistics (train.py:898-901); advances rtg_step. */
 int g2048_rtg_finalize(g2048_stream_t stream, double *state, const double *partials,
                        const g2048_reward_cfg *cfg);
+
+/* D4 up-sampling of training samples on the device (calculate_advantage's augmentation,
+ * train.py:774-881; mirror_grid / rotate_grid game.py:509-590).  Replaces the host loop over
+ * random.sample(...) with:  sample j < k -> source row perm(j) of a keyed 4-round Feistel
+ * permutation of [0, n) (cycle-walked: k DISTINCT rows, like random.sample); per sample the Philox
+ * draw (seed, counter, j, stream 3) = {x, y, z, w}: x < 2^31 -> a mirror copy (y < 2^31 horizontal =
+ * flip columns, else vertical = flip rows); independently z < 2^31 -> a rotation copy by
+ * 90 * (1 + floor(3 w / 2^32)) degrees clockwise.  Copies are appended after the n real rows of the
+ * sample pool, sample by sample, mirror before rotation; each copy remaps the board, the action,
+ * bits 0-3 of legal (the other flag bits are kept) and the 4 old log-probs (new[remap(d)] = old[d],
+ * train.py:810-824), and copies adv / ret.  Pool arrays (capacity >= n + 2k rows): boards [.,16]
+ * int8, actions / legal [.] uint8, logp [.,4] f32, adv / ret [.] f32.  *count (device int64) =
+ * n + number of copies.  Needs n < 2^31, k <= n, workspace of g2048_augment_workspace_bytes(k). */
+size_t g2048_augment_workspace_bytes(int64_t k);
+int g2048_augment(g2048_stream_t stream, int8_t *boards, uint8_t *actions, uint8_t *legal, float *logp, float *adv,
+                  float *ret, int64_t n, int64_t k, uint64_t seed, uint64_t counter, void *workspace,
+                  size_t workspace_bytes, int64_t *count);
 
 /* Library build identification (gfx target, version). */
 const char *g2048_build_info(void);

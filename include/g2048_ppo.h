@@ -125,6 +125,9 @@ typedef struct g2048_ppo_batch {
     const float *old_logp; /* [M, 4] log_softmax of the masked rollout logits */
     const float *adv;      /* [M] */
     const float *ret;      /* [M] normalised return-to-go (value target) */
+    const int64_t *rows;   /* nullable device count n <= m: rows >= n of the minibatch are padding (the
+                              ragged last minibatch of an epoch run at full size): zero loss and
+                              gradient, left out of every sum, and the loss mean is over n rows */
 } g2048_ppo_batch;
 
 /* Scratch floats of g2048_ppo_head_loss / g2048_ppo_head_kl for (m, h). */
@@ -147,18 +150,22 @@ int g2048_ppo_head_loss(g2048_stream_t stream, const uint16_t *x, const float *w
                         g2048_colsum_job *defer);
 
 /* KL(old || new) diagnostic after the optimizer step (train.py:578-601): new logits x Wa^T + ba
- * against the stored masked logits (illegal = -inf).  out[2] = {sum KL, max KL} (overwritten). */
+ * against the stored masked logits (illegal = -inf).  out[2] = {sum KL, max KL} (overwritten).
+ * rows (nullable): device count of the valid rows (g2048_ppo_batch.rows). */
 int g2048_ppo_head_kl(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, int64_t m,
-                      int32_t h, const float *old_masked, float *partials, float *out, g2048_colsum_job *defer);
+                      int32_t h, const float *old_masked, const int64_t *rows, float *partials, float *out,
+                      g2048_colsum_job *defer);
 
 /* Accumulates one minibatch into the update statistics (train.py:603-642): stats[0..7] +=
  * {loss, policy_loss, entropy_loss, value_loss, grad_norm, entropy, kl_total, kl_average} from the
  * head_loss sums, the KL {sum, max}, the pre-clip gradient norm and beta; stats[8] = max(stats[8],
  * KL max).  counter (optional) is incremented (the next minibatch's dropout counter).  kl is either
  * the final {sum, max} (kl_rows = 0) or the [kl_rows][2] partial rows of a deferred
- * g2048_ppo_head_kl (its job's part / nb), reduced here in a fixed order. */
+ * g2048_ppo_head_kl (its job's part / nb), reduced here in a fixed order.  The means are over m rows,
+ * or over *rows (device count, nullable) for a padded ragged minibatch. */
 int g2048_ppo_stats(g2048_stream_t stream, const float *sums, const float *kl, int32_t kl_rows, const float *grad_norm,
-                    const float *beta_dev, float critic, int64_t m, float *stats, uint64_t *counter);
+                    const float *beta_dev, float critic, int64_t m, const int64_t *rows, float *stats,
+                    uint64_t *counter);
 
 /* Scratch floats of g2048_wgrad for (m, n1, n2); 0 when the shape is unsupported. */
 size_t g2048_wgrad_partials(int64_t m, int32_t n1, int32_t n2);

@@ -264,3 +264,125 @@ def reward_rtg_normalize(points, mono_b, mono_a, empt_b, empt_a, done, value, ep
     new_m2 = rtg_beta * rtg_m2 + (1 - rtg_beta) * (var + mean ** 2)
     return {"reward": reward, "g_raw": g_raw, "g_norm": g_norm, "adv": adv,
             "moments": (new_mu, new_m2, new_mu), "batch": (mean, var), "mu_c": mu_c, "std": std}
+
+
+# ---------------------------------------------------------------- D4 up-sampling ----------------
+# calculate_advantage's augmentation (train.py:774-881) with the build's device sampling convention
+# (include/g2048.h g2048_augment): which rows and transforms are drawn is the build's (Feistel +
+# Philox instead of Python's `random`), the transforms themselves restate the reference.
+
+def mirror_grid(g, direction):
+    """Game2048.mirror_grid (game.py:509-535), 4x4 nested lists or arrays."""
+    out = [[0] * 4 for _ in range(4)]
+    for i in range(4):
+        for j in range(4):
+            if direction == "horizontal":
+                out[i][3 - j] = g[i][j]
+            else:
+                out[3 - i][j] = g[i][j]
+    return out
+
+
+def rotate_grid(g, degrees):
+    """Game2048.rotate_grid (game.py:537-590), clockwise."""
+    out = [[0] * 4 for _ in range(4)]
+    for i in range(4):
+        for j in range(4):
+            if degrees == 90:
+                out[j][3 - i] = g[i][j]
+            elif degrees == 180:
+                out[3 - i][3 - j] = g[i][j]
+            else:
+                out[3 - j][i] = g[i][j]
+    return out
+
+
+_DIRS = [UP, DOWN, LEFT, RIGHT]
+_ROT90 = {UP: RIGHT, RIGHT: DOWN, DOWN: LEFT, LEFT: UP}  # train.py:797-803
+
+
+def remap_direction_mirror(d, axis):  # train.py:784-793
+    if axis == "horizontal" and d in (LEFT, RIGHT):
+        return LEFT if d == RIGHT else RIGHT
+    if axis == "vertical" and d in (UP, DOWN):
+        return UP if d == DOWN else DOWN
+    return d
+
+
+def remap_direction_rotate(d, degrees):  # train.py:795-808
+    for _ in range(degrees // 90):
+        d = _ROT90[d]
+    return d
+
+
+def _lowbias32(h):
+    h = np.uint32(h)
+    h ^= h >> np.uint32(16)
+    h = np.uint32((int(h) * 0x7FEB352D) & 0xFFFFFFFF)
+    h ^= h >> np.uint32(15)
+    h = np.uint32((int(h) * 0x846CA68B) & 0xFFFFFFFF)
+    h ^= h >> np.uint32(16)
+    return int(h)
+
+
+def augment_plan(n, k, seed, counter):
+    """[(source row, transforms)] of the build's sampler: sample j -> row perm(j) of a 4-round
+    Feistel permutation (keys = Philox (seed, counter, 0xFFFFFFFF, stream 4)) cycle-walked into
+    [0, n); Philox (seed, counter, j, stream 3) = x, y, z, w: x < 2^31 -> mirror (y < 2^31
+    horizontal), z < 2^31 -> rotation by 90 * (1 + floor(3 w / 2^32)).  Pure Python (small k)."""
+    bits = 2
+    while (1 << bits) < n:
+        bits += 2
+    half = bits // 2
+    mask = (1 << half) - 1
+    key = [int(v) for v in philox4x32_10([counter & 0xFFFFFFFF, counter >> 32, 0xFFFFFFFF, 4],
+                                         [seed & 0xFFFFFFFF, seed >> 32])]
+    draws = philox_draws(seed, counter, k, 3)
+    plan = []
+    for j in range(k):
+        x = j
+        while True:
+            lo, hi = x & mask, x >> half
+            l, r = hi, lo
+            for q in range(4):
+                l, r = r, l ^ (_lowbias32(r ^ key[q]) & mask)
+            x = (l << half) | r
+            if x < n:
+                break
+        u = [int(v) for v in draws[j]]
+        tr = []
+        if u[0] < 2 ** 31:
+            tr.append(("mirror", "horizontal" if u[1] < 2 ** 31 else "vertical"))
+        if u[2] < 2 ** 31:
+            tr.append(("rotate", 90 * (1 + ((u[3] * 3) >> 32))))
+        plan.append((x, tr))
+    return plan
+
+
+def augment_rows(boards, actions, legal, logp, adv, ret, plan):
+    """The copies of train.py:826-881 for `plan`, in order (mirror before rotation per sample):
+    returns arrays (boards [c,16] int8, actions, legal (bits 0-3 remapped, others kept), logp [c,4],
+    adv, ret)."""
+    ob, oa, ol, op, oad, ort = [], [], [], [], [], []
+    for src, trs in plan:
+        g = np.asarray(boards[src], np.int8).reshape(4, 4).tolist()
+        for kind, arg in trs:
+            if kind == "mirror":
+                ng, fn = mirror_grid(g, arg), (lambda d, a=arg: remap_direction_mirror(d, a))
+            else:
+                ng, fn = rotate_grid(g, arg), (lambda d, a=arg: remap_direction_rotate(d, a))
+            lg = int(legal[src])
+            nl = lg & ~0xF
+            nlp = [0.0] * 4
+            for d in range(4):
+                nl |= ((lg >> d) & 1) << fn(d)
+                nlp[fn(d)] = float(logp[src][d])
+            ob.append(np.asarray(ng, np.int8).reshape(16))
+            oa.append(fn(int(actions[src])))
+            ol.append(nl)
+            op.append(nlp)
+            oad.append(float(adv[src]))
+            ort.append(float(ret[src]))
+    c = len(ob)
+    return (np.asarray(ob, np.int8).reshape(c, 16), np.asarray(oa, np.uint8), np.asarray(ol, np.uint8),
+            np.asarray(op, np.float32).reshape(c, 4), np.asarray(oad, np.float32), np.asarray(ort, np.float32))

@@ -56,6 +56,6 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.RewardCfg) == 40
     assert ctypes.sizeof(_lib.Dropout) == 40
     assert _lib.Dropout.counter_dev.offset == 32
-    assert ctypes.sizeof(_lib.PPOBatch) == 48
+    assert ctypes.sizeof(_lib.PPOBatch) == 56 and _lib.PPOBatch.rows.offset == 48
     assert ctypes.sizeof(_lib.Dy) == 64 and _lib.Dy.dz.offset == 40 and _lib.DY_MAX_P == 4
     assert ctypes.sizeof(_lib.ColsumJob) == 88 and _lib.ColsumJob.len.offset == 64

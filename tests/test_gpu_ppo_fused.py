@@ -484,9 +484,40 @@ def test_fused_muon_supported_shapes():
     assert not L.muon_supported(256, 256) and not L.muon_supported(196, 6)
 
 
-@pytest.mark.parametrize("fused_opt", [False, True])
-def test_fused_graphed_update_equals_eager(dev, fused_opt):
-    """The captured fused step (dropout on, graph-safe Muon+AdamW) is bitwise the eager one."""
+def test_padded_ragged_minibatch_matches_unpadded(dev):
+    """The ragged last minibatch run padded to full size with a device row count (g2048_ppo_batch.rows)
+    gives the gradients and loss sums of the same rows run unpadded."""
+    import agent
+    from g2048.dist import GradBucket
+    from g2048.fastmlp import FusedPPOUpdater
+    from g2048.optim import build_optimizer
+    from g2048.ppo import PPOConfig
+    data = _synthetic_data(dev, 6000, seed=8)
+    bs, n = 4096, 1904
+    idx = torch.randperm(6000, device=dev)[:n]
+    res = []
+    for pad in (False, True):
+        torch.manual_seed(2)
+        m = agent.GameMLP(agent.MLPConfig(hidden_dim=196, num_layers=2, dropout=0.0)).to(dev).train()
+        up = FusedPPOUpdater(m, build_optimizer(m, 1e-3, 1e-4, schedule=False), PPOConfig(batch_size=bs, critic=0.2),
+                             GradBucket(m.parameters()))
+        up._alloc(bs if pad else n)
+        up.refresh_weights()
+        up.beta_t.fill_(0.02)
+        ix = torch.cat([idx, idx.new_zeros(bs - n)]) if pad else idx
+        if pad:
+            up._set_rows(n)
+        up._pre(ix, data, up.beta_t, None)
+        res.append(([p.grad.clone() for p in m.parameters()], up.sums.clone()))
+    for (name, _), a, b in zip(m.named_parameters(), res[0][0], res[1][0]):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-6, msg=name)
+    torch.testing.assert_close(res[1][1], res[0][1], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("fused_opt,bs", [(False, 2048), (True, 2048), (True, 3000)])
+def test_fused_graphed_update_equals_eager(dev, fused_opt, bs):
+    """The captured fused step (dropout on, graph-safe Muon+AdamW) is bitwise the eager one, also with
+    a ragged last minibatch (8192 = 2 x 3000 + 2192: padded replay of the same graph)."""
     import agent
     from g2048.dist import GradBucket
     from g2048.fastmlp import FusedPPOUpdater
@@ -501,7 +532,7 @@ def test_fused_graphed_update_equals_eager(dev, fused_opt):
         order = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
         gen = torch.Generator(device=dev)
         gen.manual_seed(5)
-        up = FusedPPOUpdater(m, opt, PPOConfig(batch_size=2048, critic=0.2), GradBucket(order), gen, graph=graph)
+        up = FusedPPOUpdater(m, opt, PPOConfig(batch_size=bs, critic=0.2), GradBucket(order), gen, graph=graph)
         assert up.fused_opt == fused_opt
         st = None
         for _ in range(3):

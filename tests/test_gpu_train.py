@@ -209,14 +209,19 @@ def test_graph_and_eager_rollouts_identical(dev):
         assert all(torch.equal(a, b) for a, b in zip(outs[0], o))
 
 
-@pytest.mark.parametrize("horizon", [32, 0])
-def test_trainer_runs_and_learns_signal(dev, horizon):
+@pytest.mark.parametrize("horizon,ratio,hidden", [(32, 0.0, 64), (0, 0.0, 64), (32, 0.25, 196), (0, 0.25, 64)])
+def test_trainer_runs_and_learns_signal(dev, horizon, ratio, hidden):
+    """Fixed-horizon and episodic training steps, with and without the device D4 up-sampling
+    (--upsample-ratio: about ratio x samples copies; the ragged last minibatch runs padded)."""
     from g2048.trainer import TrainConfig, VecTrainer
     cfg = TrainConfig(steps=6, episodes=1024, horizon=horizon, max_steps=256 if horizon == 0 else None,
-                      batch_size=8192, hidden=64, points=0.1, mono=1.0, rtg_beta=0.99, entropy=0.02, critic=0.2,
-                      warmup_steps=1, lr=1e-3, critic_lr=1e-4)
+                      batch_size=8192, hidden=hidden, points=0.1, mono=1.0, rtg_beta=0.99, entropy=0.02, critic=0.2,
+                      warmup_steps=1, lr=1e-3, critic_lr=1e-4, upsample_ratio=ratio)
     tr = VecTrainer(cfg, dev)
     ms = [tr.train_step(s) for s in range(4)]
+    for m in ms:
+        k = int(m["samples"] * ratio)
+        assert (m["augmented_samples"] == 0) if ratio == 0 else abs(m["augmented_samples"] - k) < 6 * k ** 0.5 + 2
     for m in ms:
         for k, v in m.items():
             assert v is None or not isinstance(v, float) or math.isfinite(v), k
@@ -338,3 +343,38 @@ def test_episode_scan_matches_loop(dev):
             rs2 = torch.where(d, 0, rs2)
             rm2 = torch.where(d, 0, rm2)
         assert torch.equal(rs, rs2) and torch.equal(rm, rm2)
+
+
+@pytest.mark.parametrize("n,k", [(3000, 750), (257, 256), (1000, 0)])
+def test_augment_kernel_matches_oracle(dev, n, k):
+    """g2048_augment (D4 up-sampling, train.py:774-881) vs oracle.augment_plan + augment_rows: the
+    same source rows and transforms in the same order, bit-exact copies; real rows untouched."""
+    from g2048 import _lib as L
+    g = np.random.default_rng(n + k)
+    cap = n + 2 * k
+    boards = np.zeros((cap, 16), np.int8)
+    boards[:n] = g.integers(0, 12, size=(n, 16))
+    actions = np.zeros(cap, np.uint8)
+    actions[:n] = g.integers(0, 4, size=n)
+    legal = np.zeros(cap, np.uint8)
+    legal[:n] = g.integers(0, 256, size=n)
+    logp = np.zeros((cap, 4), np.float32)
+    logp[:n] = g.normal(size=(n, 4))
+    adv = np.zeros(cap, np.float32)
+    adv[:n] = g.normal(size=n)
+    ret = np.zeros(cap, np.float32)
+    ret[:n] = g.normal(size=n)
+    t = [torch.from_numpy(a.copy()).to(dev) for a in (boards, actions, legal, logp, adv, ret)]
+    ws = torch.zeros(L.augment_workspace_bytes(k), dtype=torch.uint8, device=dev)
+    count = torch.zeros(1, dtype=torch.int64, device=dev)
+    seed, counter = 0x5EED + k, 11
+    L.augment(*t, n, k, seed, counter, ws, count)
+    torch.cuda.synchronize()
+    plan = O.augment_plan(n, k, seed, counter)
+    want = O.augment_rows(boards, actions, legal, logp, adv, ret, plan)
+    c = int(count.item())
+    assert c == n + len(want[0])
+    got = [x.cpu().numpy() for x in t]
+    for a, w, full in zip(got, want, (boards, actions, legal, logp, adv, ret)):
+        assert np.array_equal(a[:n], full[:n])
+        assert np.array_equal(a[n:c], w)

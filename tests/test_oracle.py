@@ -198,3 +198,55 @@ def test_pure_python_baseline_runs():
     from oracle import pyref
     r = pyref.time_random_steps(0.3)
     assert r["steps"] > 100 and r["value"] > 0
+
+
+def test_oracle_augmentation_transforms_are_game_symmetries():
+    """oracle.augment_rows (train.py:826-881 with game.py:509-590): every copy of a golden transition
+    is the transition of the transformed board under the remapped action (same points), with the
+    legal mask and log-probs permuted like the directions; matches the host augment.py restatement."""
+    import sys
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1] / "2048-ppo_amd"))
+    from g2048 import augment as A
+    g = golden("games.npz")
+    ok = [i for i in range(600) if not g["invalid"][i]]
+    boards = g["before"][ok]
+    actions = g["action"][ok].astype(np.uint8)
+    legal = (O.legal_mask(boards) | 0x40).astype(np.uint8)  # an extra flag bit must be kept
+    logp = -np.arange(4, dtype=np.float32)[None].repeat(len(ok), 0) - np.arange(len(ok))[:, None] * 10
+    adv = np.arange(len(ok), dtype=np.float32)
+    plan = [(i, [("mirror", "horizontal"), ("rotate", 90)]) for i in range(0, len(ok), 3)]
+    plan += [(i, [("mirror", "vertical"), ("rotate", 180)]) for i in range(1, len(ok), 3)]
+    plan += [(i, [("rotate", 270)]) for i in range(2, len(ok), 3)]
+    ob, oa, ol, op, oad, ort = O.augment_rows(boards, actions, legal, logp, adv, adv, plan)
+    q = 0
+    for src, trs in plan:
+        for kind, arg in trs:
+            moved_src, pts_src, _ = O.move(boards[src][None], int(actions[src]))
+            out, pts, _ = O.move(ob[q][None], int(oa[q]))
+            grid_fn, dir_fn = (A.mirror_grid, A.remap_mirror) if kind == "mirror" else (A.rotate_grid, A.remap_rotate)
+            want = np.array(grid_fn(moved_src[0].reshape(4, 4).tolist(), arg), np.int8).reshape(16)
+            assert np.array_equal(out[0], want) and pts[0] == pts_src[0]
+            assert np.array_equal(ob[q], np.array(grid_fn(boards[src].reshape(4, 4).tolist(), arg), np.int8).reshape(16))
+            assert oa[q] == dir_fn(int(actions[src]), arg)
+            assert ol[q] == (O.legal_mask(ob[q][None])[0] | 0x40)
+            for d in range(4):
+                assert op[q][dir_fn(d, arg)] == logp[src][d]
+            assert oad[q] == adv[src]
+            q += 1
+    assert q == len(ob)
+
+
+def test_augment_plan_samples_distinct_rows():
+    """The build's sampler: k distinct source rows (random.sample without replacement), about half
+    of the samples mirrored and half rotated, the three angles about equally often."""
+    plan = O.augment_plan(5000, 1250, 0x2048, 3)
+    srcs = [s for s, _ in plan]
+    assert len(set(srcs)) == 1250 and 0 <= min(srcs) and max(srcs) < 5000
+    kinds = [t for _, trs in plan for t in trs]
+    n_m = sum(1 for k, _ in kinds if k == "mirror")
+    n_r = len(kinds) - n_m
+    assert abs(n_m - 625) < 100 and abs(n_r - 625) < 100
+    angles = [a for k, a in kinds if k == "rotate"]
+    for a in (90, 180, 270):
+        assert abs(angles.count(a) - n_r / 3) < 70
+    assert O.augment_plan(5000, 1250, 0x2048, 4) != plan  # a new permutation per counter
