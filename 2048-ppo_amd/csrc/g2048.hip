@@ -158,18 +158,27 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(const uint4 *__restric
     flags[i] = (uint8_t)r.fl;
 }
 
-__device__ const lut::Row12Table kRow12 = lut::Row12Table();
+__device__ const lut::Row12Table kRow12 __attribute__((aligned(16))) = lut::Row12Table();
 
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
 
-// kRow12 index of a LEFT-frame row dword (byte j = cell j): c0 + 12 c1 + 144 c2 + 1728 c3 as two
-// packed-u16 dot products.  Bytes are masked to 4 bits so any row (even one holding exponents >= 12,
-// whose lane takes the compute path) indexes inside the 128 KiB LDS allocation.
-__device__ __forceinline__ uint32_t row12_index(uint32_t x) {
-    const u16x2 k02 = {1, 144}, k13 = {12, 1728};
+// LDS byte address of the kRow12 entry of a LEFT-frame row dword (byte j = cell j):
+// 4 (c0 + 12 c1 + 144 c2 + 1728 c3) as two packed-u16 dot products.  Bytes are masked to 4 bits
+// so any row (even one holding exponents >= 12, whose lane takes the compute path) addresses
+// inside the 128 KiB LDS allocation (< 15 * 1885 * 4 bytes).
+__device__ __forceinline__ uint32_t row12_addr(uint32_t x) {
+    const u16x2 k02 = {4, 576}, k13 = {48, 6912};
     return __builtin_amdgcn_udot2(as_u16x2((x >> 8) & 0x000F000Fu), k13,
                                   __builtin_amdgcn_udot2(as_u16x2(x & 0x000F000Fu), k02, 0u, false), false);
+}
+__device__ __forceinline__ uint32_t lds_word(const uint32_t *tab, uint32_t addr) {
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(tab) + addr);
+}
+// byte-reverse each row when the lane's selector says so (one v_perm per row, no select)
+__device__ __forceinline__ uint4 perm4(const uint4 &w, uint32_t sel) {
+    return make_uint4(__builtin_amdgcn_perm(w.x, w.x, sel), __builtin_amdgcn_perm(w.y, w.y, sel),
+                      __builtin_amdgcn_perm(w.z, w.z, sel), __builtin_amdgcn_perm(w.w, w.w, sel));
 }
 
 // nibble-packed row (bits 0..15 of a table entry) -> row dword with one exponent per byte
@@ -264,26 +273,21 @@ __device__ __forceinline__ uint32_t fresh_stats(uint32_t p1, uint32_t v1, uint32
     return legal;
 }
 
-// Copy the 81 KiB row table into LDS with 8 independent 16-B loads per lane in flight per batch (a
-// load->store loop would pay one L2/MALL latency per 16 B).
+// Copy the 81 KiB row table into LDS by LDS-DMA: each wave instruction moves 1 KiB (16 B per lane)
+// straight from global memory into LDS with no VGPR staging, and every piece of the wave is in
+// flight before the single wait (one L2/MALL round trip per launch instead of one per batch).
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
 __device__ __forceinline__ void stage_row_table(uint32_t *s_row) {
-    constexpr int kChunks = (int)(lut::kRowEntries * 4u / 16u);  // uint4 pieces of the table
-    const uint4 *src = reinterpret_cast<const uint4 *>(kRow12.v);
-    uint4 *dst = reinterpret_cast<uint4 *>(s_row);
-    const int nt = blockDim.x;
-    for (int base = 0; base < kChunks; base += 8 * nt) {
-        uint4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int k = base + u * nt + threadIdx.x;
-            v[u] = k < kChunks ? src[k] : make_uint4(0u, 0u, 0u, 0u);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int k = base + u * nt + threadIdx.x;
-            if (k < kChunks) dst[k] = v[u];
-        }
-    }
+    constexpr int kPieces = (int)(lut::kRowEntries * 4u / 1024u);  // 81 pieces of 1 KiB
+    static_assert(lut::kRowEntries * 4u % 1024u == 0u, "whole 1 KiB pieces");
+    const char *src = reinterpret_cast<const char *>(kRow12.v);
+    char *dst = reinterpret_cast<char *>(s_row);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int c = wave; c < kPieces; c += nw)
+        __builtin_amdgcn_global_load_lds((glb_void_t *)(src + 1024 * c + 16 * lane), (lds_void_t *)(dst + 1024 * c), 16,
+                                         0, 0);
+    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0): this wave's pieces have landed
     __syncthreads();
 }
 
@@ -320,18 +324,17 @@ __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__r
     // the move through the LDS row table in the LEFT frame.  Half of the next pair's Philox rounds
     // fill the LDS round trip: the empty asm statements start them after the table loads are issued
     // (memory clobber) and consume the loaded entries after them.
-    const bool vert = a < 2u, rev = (a & 1u) != 0u;
-    uint4 w = sel4(vert, transpose(s.b), s.b);
-    w = sel4(rev, bswap4(w), w);
-    uint32_t e0 = tab[row12_index(w.x)], e1 = tab[row12_index(w.y)];
-    uint32_t e2 = tab[row12_index(w.z)], e3 = tab[row12_index(w.w)];
+    const bool vert = a < 2u;
+    const uint32_t rsel = (a & 1u) ? 0x00010203u : 0x03020100u;  // DOWN / RIGHT: byte-reversed rows
+    uint4 w = perm4(sel4(vert, transpose(s.b), s.b), rsel);
+    uint32_t e0 = lds_word(tab, row12_addr(w.x)), e1 = lds_word(tab, row12_addr(w.y));
+    uint32_t e2 = lds_word(tab, row12_addr(w.z)), e3 = lds_word(tab, row12_addr(w.w));
     asm volatile("" : "+v"(s.ph.c0), "+v"(s.ph.c1), "+v"(s.ph.c2), "+v"(s.ph.c3)::"memory");
     if constexpr (kOdd) philox_rounds<5, 10>(s.ph);
     else philox_rounds<0, 5>(s.ph);
     asm volatile("" : "+v"(s.ph.c0), "+v"(s.ph.c1), "+v"(s.ph.c2), "+v"(s.ph.c3), "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3));
     const int mono_b = mono_value(s.sb);
-    w = make_uint4(unpack_row(e0), unpack_row(e1), unpack_row(e2), unpack_row(e3));
-    w = sel4(rev, bswap4(w), w);
+    w = perm4(make_uint4(unpack_row(e0), unpack_row(e1), unpack_row(e2), unpack_row(e3)), rsel);
     uint4 moved = sel4(vert, transpose(w), w);
     // merge points / 4 of the four rows in the high halves, summed as packed u16
     const uint32_t q = __builtin_bit_cast(uint32_t, (as_u16x2(e0) + as_u16x2(e1)) + (as_u16x2(e2) + as_u16x2(e3)));

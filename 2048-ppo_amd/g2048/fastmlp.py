@@ -128,7 +128,9 @@ class FusedPPOUpdater(PPOUpdater):
         for l, (w, ln) in enumerate(zip(self.wbf, self.ln)):
             drop = self._drop(l, pass_) if l > 0 else None
             if self.mf_ok[l]:  # Linear + LayerNorm + ReLU + dropout + residual in one MFMA kernel
-                L.mlp_fwd(x, w, ln.weight, ln.bias, l > 0, self.G[l], self.H[l], self.mean[l], self.rstd[l], drop)
+                keep = pass_ == 0  # the KL re-forward (pass 1) needs no G / LayerNorm statistics
+                L.mlp_fwd(x, w, ln.weight, ln.bias, l > 0, self.G[l] if keep else None, self.H[l],
+                          self.mean[l] if keep else None, self.rstd[l] if keep else None, drop)
             else:
                 _mm(x, w.t(), self.G[l])
                 L.ln_act_fwd(self.G[l], ln.weight, ln.bias, x if l > 0 else None, self.H[l], self.mean[l],

@@ -7,9 +7,11 @@ For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL).  Workload 
 SURVEY.md §8d): `--envs` independent 4x4 boards per GPU, uniform random legal actions (Philox
 keyed by 0x2048 + rank), auto-reset on done.  One bench "step" = one launch of the fused
 rollout kernel `env_rollout_kernel` = `--chunk` consecutive env steps of every board, writing the
-full per-step trajectory record (board, action, points, potentials, flags).  value = total legal
-transitions of all ranks / max-over-ranks wall time of the K timed steps (weak scaling: the boards
-per GPU are fixed; the envs are independent, so no data-path collective exists).
+full per-step trajectory record (board, action, points, potentials, flags); the launch and its
+device-side Philox counter bump are replayed from a hipGraph (host issue cost: one graph launch per
+step).  value = total legal transitions of all ranks / max-over-ranks wall time of the K timed
+steps (weak scaling: the boards per GPU are fixed; the envs are independent, so no data-path
+collective exists).
 
 Also reported in the same JSON line:
   roofline       env_rollout_kernel vs HBM peak: algorithmic bytes per launch / avg launch time
@@ -44,8 +46,8 @@ SINGLE_STEP_BYTES = 42  # board in 16 + action 1 + board out 1
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--envs", type=int, default=65536)
     p.add_argument("--chunk", type=int, default=64, help="env steps per rollout launch")
     p.add_argument("--single-steps", type=int, default=256, help="graph-captured one-launch-per-step steps (0=off)")
@@ -114,13 +116,29 @@ class RolloutBench:
         self.tp = torch.empty(chunk, n, dtype=torch.int32, device=dev)
         self.tpot = torch.empty(chunk, n, 4, dtype=torch.int8, device=dev)
         self.tf = torch.empty(chunk, n, dtype=torch.uint8, device=dev)
-        self.counter = 1
+        # the Philox counter base lives on the device: the launch (and its counter bump) can be
+        # replayed from a hipGraph, so the host issue cost per bench step is one graph launch
+        self.ctr = torch.ones(1, dtype=torch.int64, device=dev)
+        self.rng = L.make_rng(L.RNG_PHILOX, self.env.seed, 0, self.env.env_base, counter_dev=self.ctr)
+        self.graph = None
 
     def launch(self):
-        L = self.L
-        rng = L.make_rng(L.RNG_PHILOX, self.env.seed, self.counter, self.env.env_base)
-        L.env_rollout_random(self.env.boards, self.chunk, self.tb, self.ta, self.tp, self.tpot, self.tf, rng)
-        self.counter += self.chunk
+        self.L.env_rollout_random(self.env.boards, self.chunk, self.tb, self.ta, self.tp, self.tpot, self.tf, self.rng)
+        self.ctr.add_(self.chunk)
+
+    def capture(self):
+        import torch
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self.launch()  # warm-up outside the capture
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.launch()
+
+    def step(self):
+        self.graph.replay()
 
     def bytes_per_launch(self):
         return self.n * (self.chunk * ROLLOUT_STEP_BYTES + ROLLOUT_LAUNCH_BYTES)
@@ -256,10 +274,11 @@ def main():
     L.load()
 
     rb = RolloutBench(args.envs, args.chunk, rank, dev)
+    rb.capture()
     for _ in range(args.warmup):
-        rb.launch()
+        rb.step()
     torch.cuda.synchronize()
-    wall, ev = time_region(rb.launch, args.steps, world)
+    wall, ev = time_region(rb.step, args.steps, world)
     wall = max_over_ranks(wall, world)
     ev_max = max_over_ranks(ev, world)
     env_steps = args.envs * args.chunk * args.steps * world
@@ -297,10 +316,10 @@ def main():
         sweep = {}
         for s in [int(x) for x in args.sweep.split(",") if x]:
             b = RolloutBench(s, args.chunk, rank, dev)
-            b.launch()
+            b.capture()
             torch.cuda.synchronize()
-            k = max(3, args.steps // 5)
-            w, e = time_region(b.launch, k, world)
+            k = max(3, args.steps // 10)
+            w, e = time_region(b.step, k, world)
             sweep[str(s)] = {"env_steps_per_s_per_gpu": s * args.chunk * k / w,
                              "achieved_GBps": b.bytes_per_launch() / (e / k) / 1e9}
             del b
