@@ -37,6 +37,21 @@ def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
     return rank, ws, local
 
 
+def equal_rows(data: dict) -> dict:
+    """Trim every rank's flat sample set to the smallest rank's row count (one MIN all-reduce), so all
+    ranks run the same number of minibatches -- one gradient all-reduce each -- with equal minibatch
+    sizes.  D4 copies sit after the real rows, so only copies are dropped unless a
+    rank has fewer real rows (episodic mode), like DistributedSampler(drop_last=True)."""
+    m = next(iter(data.values())).shape[0]
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return data
+    dev = next(iter(data.values())).device
+    t = torch.tensor([m], dtype=torch.int64, device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    k = int(t.item())
+    return data if k == m else {key: v[:k] for key, v in data.items()}
+
+
 def allreduce_sum_(t: torch.Tensor) -> torch.Tensor:
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t)

@@ -21,7 +21,7 @@ import torch
 from . import _lib as L
 from . import fastmlp
 from .advantage import RewardWeights, RTGTracker
-from .dist import GradBucket, allreduce_sum_, world
+from .dist import GradBucket, allreduce_sum_, equal_rows, world
 from .optim import FusedMuonAdamW, MuonAdamW, ScheduledMuonAdamW, build_optimizer
 from .ppo import PPOConfig, PPOUpdater
 from .rollout import Rollout, make_policy
@@ -228,6 +228,8 @@ class VecTrainer:
         n_aug = 0
         if cfg.upsample_ratio > 0:
             data, n_aug = self._augment(data, step)
+        if self.world > 1:  # every rank runs the same number of minibatches (one all-reduce each)
+            data = equal_rows(data)
         self._mark("augment_ms")
         ustats = self.ppo.update(data, self.beta, self._encode)
         self.opt.scheduler_step()

@@ -93,3 +93,38 @@ def test_two_rank_update_equals_single_process():
     m1 = s1 / n
     mean, var = 38.5 + m1, s2 / n - m1 * m1
     assert np.isclose(mean, g.mean(), rtol=1e-12) and np.isclose(var, g.var(), rtol=1e-9)
+
+
+def _ragged_worker(rank, world, port, out):
+    """Ranks with different sample counts (D4 copies / episodic games vary per rank): equal_rows trims
+    to the smallest, so both run the same number of minibatches and the update completes."""
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, str(ROOT / "2048-ppo_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import agent
+    from g2048.dist import GradBucket, equal_rows
+    from g2048.optim import build_optimizer
+    from g2048.ppo import PPOConfig, PPOUpdater
+    data = equal_rows(_data(300 if rank == 0 else 257, 3 + rank))
+    torch.manual_seed(0)
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=32, num_layers=2, dropout=0.0))
+    opt = build_optimizer(m, 1e-3, 1e-4, warmup_steps=0, total_steps=10, schedule=False)
+    up = PPOUpdater(m, opt, PPOConfig(batch_size=100, amp_dtype=None), GradBucket(m.parameters()))
+    up.update(data, beta=0.02, encode=_encode)
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    gathered = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    out[rank] = {"rows": int(data["actions"].shape[0]), "same": all(torch.equal(gathered[0], x) for x in gathered)}
+    dist.destroy_process_group()
+
+
+def test_unequal_rank_sample_counts_are_equalized():
+    port = _free_port()
+    with mp.Manager() as man:
+        out = man.dict()
+        mp.start_processes(_ragged_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+        res = dict(out)
+    assert res[0]["rows"] == res[1]["rows"] == 257
+    assert res[0]["same"] and res[1]["same"]
