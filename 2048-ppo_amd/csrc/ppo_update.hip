@@ -995,7 +995,13 @@ __host__ __device__ inline int mf_pitch(int kp) {
     return dw * 4;
 }
 
-template <int NT, bool RES, bool DROP>
+// KS > 0: the fixed-shape path (KS k-steps of 32 columns: the h = 196 blocks KS = 7, the stem KS = 2):
+// both LDS images are zero-padded to NT * 16 W rows and KS * 32 columns at a compile-time pitch, so
+// the MFMA loop is fully unrolled with immediate LDS offsets and no per-fragment address arithmetic
+// or range selects.
+__host__ __device__ constexpr int mf_fixed_pitch(int ks) { return 64 * ks + 16; }  // 16 B x odd
+
+template <int NT, int KS, bool RES, bool DROP>
 __global__ __launch_bounds__(kMfThreads) void mlp_fwd_kernel(const uint16_t *__restrict__ X,
                                                              const uint16_t *__restrict__ W,
                                                              const float *__restrict__ gamma,
@@ -1004,9 +1010,11 @@ __global__ __launch_bounds__(kMfThreads) void mlp_fwd_kernel(const uint16_t *__r
                                                              float *__restrict__ rstd_out, int64_t M, int N, int K,
                                                              DropArgs da) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int kp = (K + 7) & ~7, pw = mf_pitch(kp);  // W image: N rows, zero K padding
+    // W image: N rows (fixed path: NT * 16, the extra rows zero), zero K padding
+    const int kp = (K + 7) & ~7, pw = KS ? mf_fixed_pitch(KS) : mf_pitch(kp);
+    const int wrows = KS ? 16 * NT : N;
     char *sW = smem;
-    char *sX0 = smem + ((N * pw + 15) & ~15);       // two 64-row X slabs (double buffer)
+    char *sX0 = smem + ((wrows * pw + 15) & ~15);   // two 64-row X slabs (double buffer)
     const int xbytes = kMfRows * pw;
     char *zero = sX0 + 2 * xbytes;
     float *sgb = reinterpret_cast<float *>(zero + 64);  // gamma[N], beta[N]
@@ -1083,6 +1091,19 @@ __global__ __launch_bounds__(kMfThreads) void mlp_fwd_kernel(const uint16_t *__r
         f32x4_t acc[NT];
 #pragma unroll
         for (int n = 0; n < NT; n++) acc[n] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+        if constexpr (KS > 0) {  // every fragment in range: unrolled, immediate offsets
+            const char *xb = xrow + 16 * g, *wb = sW + col * pw + 16 * g;
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) {
+                const bf16x8_t fx = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(xb + 64 * ks));
+#pragma unroll
+                for (int n = 0; n < NT; n++) {
+                    const bf16x8_t fw =
+                        __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(wb + n * 16 * pw + 64 * ks));
+                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw, fx, acc[n], 0, 0, 0);
+                }
+            }
+        } else
         for (int k0 = 0; k0 < kp; k0 += 32) {
             const int kl = k0 + 8 * g;
             const bf16x8_t fx =
@@ -1705,11 +1726,25 @@ size_t g2048_mlp_fwd_lds_bytes(int32_t n, int32_t k) {
     return b <= 160 * 1024 ? b : 0;
 }
 
+// the fixed-shape fast path of mlp_fwd_kernel: the h = 196 model's blocks (KS = 7) and stem (KS = 2)
+static size_t mf_fixed_lds(int n, int ks) {
+    const int pw = mf_fixed_pitch(ks);
+    return (size_t)((16 * 13 * pw + 15) & ~15) + (size_t)2 * kMfRows * pw + 64 + (size_t)8 * n;
+}
+static int mf_fixed_ks(int n, int k) {
+    if ((n + 15) / 16 != 13) return 0;
+    const int ks = (((k + 7) & ~7) + 31) / 32;
+    if (ks != 7 && ks != 2) return 0;
+    return mf_fixed_lds(n, ks) <= 160 * 1024 ? ks : 0;
+}
+
 int g2048_mlp_fwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, const float *gamma, const float *beta,
                   int32_t residual, uint16_t *g, uint16_t *y, float *mean, float *rstd, int64_t m, int32_t n, int32_t k,
                   const g2048_dropout *drop) {
-    const size_t lds = g2048_mlp_fwd_lds_bytes(n, k);
-    if (!lds || m < 0 || !x || !w || !gamma || !beta || !y || (!mean) != (!rstd)) return G2048_EINVAL;
+    const size_t lds_generic = g2048_mlp_fwd_lds_bytes(n, k);
+    if (!lds_generic || m < 0 || !x || !w || !gamma || !beta || !y || (!mean) != (!rstd)) return G2048_EINVAL;
+    const int fks = mf_fixed_ks(n, k);
+    const size_t lds = fks ? mf_fixed_lds(n, fks) : lds_generic;
     if (residual && n != k) return G2048_EINVAL;
     if (!al(x, 8) || !al(w, 8) || (g && !al(g, 8)) || !al(y, 8) || !al(gamma, 16) || !al(beta, 16)) return G2048_EINVAL;
     if (m == 0) return G2048_OK;
@@ -1719,21 +1754,30 @@ int g2048_mlp_fwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, c
     const dim3 grid((unsigned)(nslab > 256 ? 256 : nslab)), blk(kMfThreads);  // one persistent block per CU
     const bool dr = drop_on(drop);
     const int nt = (n + 15) / 16;
-#define G2048_MF_LAUNCH(NT_)                                                                                       \
+#define G2048_MF_LAUNCH_KS(NT_, KS_)                                                                               \
     do {                                                                                                           \
         if (residual && dr)                                                                                        \
-            hipLaunchKernelGGL((mlp_fwd_kernel<NT_, true, true>), grid, blk, lds, s, x, w, gamma, beta, g, y, mean, \
-                               rstd, m, n, k, da);                                                                 \
+            hipLaunchKernelGGL((mlp_fwd_kernel<NT_, KS_, true, true>), grid, blk, lds, s, x, w, gamma, beta, g, y,  \
+                               mean, rstd, m, n, k, da);                                                           \
         else if (residual)                                                                                         \
-            hipLaunchKernelGGL((mlp_fwd_kernel<NT_, true, false>), grid, blk, lds, s, x, w, gamma, beta, g, y,     \
+            hipLaunchKernelGGL((mlp_fwd_kernel<NT_, KS_, true, false>), grid, blk, lds, s, x, w, gamma, beta, g, y, \
                                mean, rstd, m, n, k, da);                                                           \
         else if (dr)                                                                                               \
-            hipLaunchKernelGGL((mlp_fwd_kernel<NT_, false, true>), grid, blk, lds, s, x, w, gamma, beta, g, y,     \
+            hipLaunchKernelGGL((mlp_fwd_kernel<NT_, KS_, false, true>), grid, blk, lds, s, x, w, gamma, beta, g, y, \
                                mean, rstd, m, n, k, da);                                                           \
         else                                                                                                       \
-            hipLaunchKernelGGL((mlp_fwd_kernel<NT_, false, false>), grid, blk, lds, s, x, w, gamma, beta, g, y,    \
-                               mean, rstd, m, n, k, da);                                                           \
+            hipLaunchKernelGGL((mlp_fwd_kernel<NT_, KS_, false, false>), grid, blk, lds, s, x, w, gamma, beta, g,   \
+                               y, mean, rstd, m, n, k, da);                                                        \
     } while (0)
+#define G2048_MF_LAUNCH(NT_) G2048_MF_LAUNCH_KS(NT_, 0)
+    if (fks == 7) {
+        G2048_MF_LAUNCH_KS(13, 7);
+        return status();
+    }
+    if (fks == 2) {
+        G2048_MF_LAUNCH_KS(13, 2);
+        return status();
+    }
     switch (nt) {
         case 1: G2048_MF_LAUNCH(1); break;
         case 2: G2048_MF_LAUNCH(2); break;
@@ -1747,6 +1791,7 @@ int g2048_mlp_fwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, c
         default: G2048_MF_LAUNCH(16); break;
     }
 #undef G2048_MF_LAUNCH
+#undef G2048_MF_LAUNCH_KS
     return status();
 }
 

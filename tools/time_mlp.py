@@ -8,7 +8,7 @@ import torch  # noqa: E402
 from g2048 import _lib as L  # noqa: E402
 
 if len(sys.argv) > 1 and sys.argv[1] != "-":  # an alternative build of the library (A/B timing)
-    L.load(sys.argv[1])
+    L._lib = L.load(sys.argv[1])  # load(path) alone does not replace the module's library
 
 dev = torch.device("cuda:0")
 M, h = 65536, 196
@@ -29,6 +29,7 @@ cases = {
     "block KL (dropout, residual)": (lambda: L.mlp_fwd(X, W, gam, bet, True, None, Y, None, None, drop), 2 * 25.7),
     "block inference (residual)": (lambda: L.mlp_fwd(X, W, gam, bet, True, None, Y, None, None, None), 2 * 25.7),
 }
+print("library:", L.load()._name)
 only = sys.argv[2] if len(sys.argv) > 2 else None  # substring: time one case only (PMC passes)
 for name, (fn, mb) in cases.items():
     if only and only not in name:
