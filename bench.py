@@ -248,7 +248,7 @@ def _c_chunk(args):
     return cnt
 
 
-PMC_PROFILE = Path(__file__).resolve().parent / "profiles" / "r01f"
+PMC_PROFILE = Path(__file__).resolve().parent / "profiles" / "r01g"
 
 
 def pmc_traffic(kernel: str, args):
