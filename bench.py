@@ -266,7 +266,7 @@ def _c_chunk(args):
     return cnt
 
 
-PMC_PROFILE = Path(__file__).resolve().parent / "profiles" / "r01g"
+PMC_PROFILE = Path(__file__).resolve().parent / "profiles" / "r01h"
 
 
 def pmc_traffic(kernel: str, args):
