@@ -584,45 +584,74 @@ __device__ __forceinline__ double block_sum(double v, double *sh) {
     return t;  // valid on thread 0
 }
 
+// One lane per env walks t = T-1 .. 0.  The recurrence is serial, but its inputs are not: the loads
+// of kRtgU consecutive steps are issued together before the arithmetic of that group, so a lane
+// waits for one memory round trip per kRtgU steps instead of one per step (at 65 536 envs there
+// is one wave per SIMD and nothing else hides the latency).
+constexpr int kRtgU = 16;
+
 __global__ __launch_bounds__(kBlock) void rtg_kernel(const int32_t *__restrict__ points, const uint32_t *__restrict__ pot,
                                                      const uint8_t *__restrict__ flags, const float *__restrict__ value,
                                                      int64_t T, int64_t n, RewardArgs ra, const double *__restrict__ state,
                                                      float *__restrict__ g_raw, float *__restrict__ g_norm,
-                                                     float *__restrict__ adv, double *__restrict__ partial) {
+                                                     float *__restrict__ adv, double *__restrict__ reward,
+                                                     double *__restrict__ partial) {
     __shared__ double sh[kBlock / 64];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const double mu_c = state[4], denom = state[5] + 1e-8;
+    const double mu_c = state[4], inv = 1.0 / (state[5] + 1e-8);
     double s1 = 0.0, s2 = 0.0, cnt = 0.0;
     if (i < n) {
         double G = 0.0;
-        for (int64_t t = T - 1; t >= 0; t--) {
-            const int64_t o = t * n + i;
-            const uint32_t fl = flags[o];
-            if (fl & FLAG_INACTIVE) {
-                G = 0.0;
-                g_raw[o] = 0.0f;
-                g_norm[o] = 0.0f;
-                adv[o] = 0.0f;
-                continue;
+        for (int64_t t1 = T; t1 > 0; t1 -= kRtgU) {
+            const int64_t t0 = t1 - kRtgU > 0 ? t1 - kRtgU : 0;
+            int32_t P[kRtgU];
+            uint32_t W[kRtgU], F[kRtgU];
+            float V[kRtgU];
+#pragma unroll
+            for (int u = 0; u < kRtgU; u++) {
+                const int64_t t = t1 - 1 - u;
+                if (t >= t0) {
+                    const int64_t o = t * n + i;
+                    P[u] = points[o];
+                    W[u] = pot[o];
+                    F[u] = flags[o];
+                    V[u] = value[o];
+                }
             }
-            const uint32_t pw = pot[o];
-            const bool done = (fl & FLAG_DONE) != 0u;
-            const double mb = (double)(int8_t)(pw & 0xFFu), ma = done ? 0.0 : (double)(int8_t)((pw >> 8) & 0xFFu);
-            const double eb = (double)(int8_t)((pw >> 16) & 0xFFu), ea = done ? 0.0 : (double)(int8_t)(pw >> 24);
-            // same operation order as train.py:702-719 (float64, no contraction: built -ffp-contract=off)
-            double shaped = ra.wm * (ra.gamma * ma - mb);
-            shaped = shaped + ra.we * (ra.gamma * ea - eb);
-            const double r = (double)points[o] * ra.wp + shaped;
-            if (done) G = 0.0;  // the episode ended on this step: nothing flows back across it
-            G = r + ra.gamma * G;
-            const double gn = (G - mu_c) / denom;
-            g_raw[o] = (float)G;
-            g_norm[o] = (float)gn;
-            adv[o] = (float)(gn - (double)value[o]);
-            const double dv = G - mu_c;
-            s1 += dv;
-            s2 += dv * dv;
-            cnt += 1.0;
+#pragma unroll
+            for (int u = 0; u < kRtgU; u++) {
+                const int64_t t = t1 - 1 - u;
+                if (t < t0) break;
+                const int64_t o = t * n + i;
+                const uint32_t fl = F[u];
+                if (fl & FLAG_INACTIVE) {
+                    G = 0.0;
+                    g_raw[o] = 0.0f;
+                    g_norm[o] = 0.0f;
+                    adv[o] = 0.0f;
+                    if (reward) reward[o] = 0.0;
+                    continue;
+                }
+                const uint32_t pw = W[u];
+                const bool done = (fl & FLAG_DONE) != 0u;
+                const double mb = (double)(int8_t)(pw & 0xFFu), ma = done ? 0.0 : (double)(int8_t)((pw >> 8) & 0xFFu);
+                const double eb = (double)(int8_t)((pw >> 16) & 0xFFu), ea = done ? 0.0 : (double)(int8_t)(pw >> 24);
+                // same operation order as train.py:702-719 (float64, no contraction: built -ffp-contract=off)
+                double shaped = ra.wm * (ra.gamma * ma - mb);
+                shaped = shaped + ra.we * (ra.gamma * ea - eb);
+                const double r = (double)P[u] * ra.wp + shaped;
+                if (done) G = 0.0;  // the episode ended on this step: nothing flows back across it
+                G = r + ra.gamma * G;
+                const double gn = (G - mu_c) * inv;  // train.py:751 divides; the reciprocal is within 1 ulp
+                g_raw[o] = (float)G;
+                g_norm[o] = (float)gn;
+                adv[o] = (float)(gn - (double)V[u]);
+                if (reward) reward[o] = r;
+                const double dv = G - mu_c;
+                s1 += dv;
+                s2 += dv * dv;
+                cnt += 1.0;
+            }
         }
     }
     const double b1 = block_sum<kBlock / 64>(s1, sh);
@@ -1040,6 +1069,14 @@ int g2048_reward_rtg(g2048_stream_t stream, const int32_t *points, const int8_t 
                      const float *value, int64_t T, int64_t n, const g2048_reward_cfg *cfg, const double *state,
                      float *g_raw, float *g_norm, float *adv, double *partials, void *workspace,
                      size_t workspace_bytes) {
+    return g2048_reward_rtg_ex(stream, points, pot, flags, value, T, n, cfg, state, g_raw, g_norm, adv, nullptr,
+                               partials, workspace, workspace_bytes);
+}
+
+int g2048_reward_rtg_ex(g2048_stream_t stream, const int32_t *points, const int8_t *pot, const uint8_t *flags,
+                        const float *value, int64_t T, int64_t n, const g2048_reward_cfg *cfg, const double *state,
+                        float *g_raw, float *g_norm, float *adv, double *reward, double *partials, void *workspace,
+                        size_t workspace_bytes) {
     if (T < 0 || n < 0 || !cfg || !state || !partials) return G2048_EINVAL;
     if (workspace_bytes < g2048_reward_rtg_workspace_bytes(n) || !workspace) return G2048_EINVAL;
     if (T > 0 && n > 0 && (!points || !pot || !flags || !value || !g_raw || !g_norm || !adv)) return G2048_EINVAL;
@@ -1048,7 +1085,7 @@ int g2048_reward_rtg(g2048_stream_t stream, const int32_t *points, const int8_t 
     const unsigned nb = blocks_for(n > 0 ? n : 1);
     const RewardArgs ra{cfg->gamma, cfg->w_points, cfg->w_mono, cfg->w_empt};
     hipLaunchKernelGGL(rtg_kernel, dim3(nb), dim3(kBlock), 0, s, points, (const uint32_t *)pot, flags, value,
-                       (n > 0 ? T : 0), n, ra, state, g_raw, g_norm, adv, (double *)workspace);
+                       (n > 0 ? T : 0), n, ra, state, g_raw, g_norm, adv, reward, (double *)workspace);
     hipLaunchKernelGGL(rtg_reduce_kernel, dim3(1), dim3(kBlock), 0, s, (const double *)workspace, (int)nb, partials);
     return launch_status();
 }

@@ -26,7 +26,7 @@ EXPORTED = (
     "g2048_mt_state_words", "g2048_mt_seed", "g2048_env_reset", "g2048_env_step", "g2048_env_rollout_random",
     "g2048_preview_points", "g2048_legal_mask",
     "g2048_obs_encode", "g2048_sample_actions", "g2048_rtg_prepare", "g2048_reward_rtg_workspace_bytes",
-    "g2048_reward_rtg", "g2048_rtg_finalize", "g2048_build_info", "g2048_episode_scan",
+    "g2048_reward_rtg", "g2048_reward_rtg_ex", "g2048_rtg_finalize", "g2048_build_info", "g2048_episode_scan",
     "g2048_augment_workspace_bytes", "g2048_augment",
     # include/g2048_ppo.h
     "g2048_obs_gather", "g2048_ln_act_fwd", "g2048_ln_act_bwd_partials", "g2048_ln_act_bwd",
@@ -144,6 +144,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_rtg_prepare": (ctypes.c_int, [vp, vp, cp]),
         "g2048_reward_rtg_workspace_bytes": (sz, [i64]),
         "g2048_reward_rtg": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, cp, vp, vp, vp, vp, vp, vp, sz]),
+        "g2048_reward_rtg_ex": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, cp, vp, vp, vp, vp, vp, vp, vp, sz]),
         "g2048_rtg_finalize": (ctypes.c_int, [vp, vp, vp, cp]),
         "g2048_build_info": (ctypes.c_char_p, []),
         "g2048_episode_scan": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp]),
@@ -280,15 +281,18 @@ def rtg_prepare(state, cfg: RewardCfg):
            "g2048_rtg_prepare")
 
 
-def reward_rtg(points, pot, flags, value, state, g_raw, g_norm, adv, partials, workspace, cfg: RewardCfg):
+def reward_rtg(points, pot, flags, value, state, g_raw, g_norm, adv, partials, workspace, cfg: RewardCfg,
+               reward=None):
+    """reward (optional) float64 [T, n]: the per-step reward the scan used."""
     T, n = points.shape[0], points.shape[1]
-    _check(load().g2048_reward_rtg(
+    _check(load().g2048_reward_rtg_ex(
         _stream(points), _dev(points, torch.int32, "points"), _dev(pot, torch.int8, "pot"),
         _dev(flags, torch.uint8, "flags"), _dev(value, torch.float32, "value"), T, n, ctypes.byref(cfg),
         _dev(state, torch.float64, "state"), _dev(g_raw, torch.float32, "g_raw"),
         _dev(g_norm, torch.float32, "g_norm"), _dev(adv, torch.float32, "adv"),
+        _dev(reward, torch.float64, "reward") if reward is not None else None,
         _dev(partials, torch.float64, "partials"), _dev(workspace, torch.uint8, "workspace"), workspace.numel()),
-        "g2048_reward_rtg")
+        "g2048_reward_rtg_ex")
 
 
 def episode_scan(points, boards, max_tile, step_flags, run_score, run_max, scores, tiles):

@@ -37,19 +37,35 @@ def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
     return rank, ws, local
 
 
-def equal_rows(data: dict) -> dict:
+def equal_rows(data: dict, n_real: int | None = None, generator: torch.Generator | None = None) -> dict:
     """Trim every rank's flat sample set to the smallest rank's row count (one MIN all-reduce), so all
     ranks run the same number of minibatches -- one gradient all-reduce each -- with equal minibatch
-    sizes.  D4 copies sit after the real rows, so only copies are dropped unless a
-    rank has fewer real rows (episodic mode), like DistributedSampler(drop_last=True)."""
+    sizes.  The first `n_real` rows are the real samples, D4 copies follow them:
+    copies are dropped first (they are already a random subset); when a rank must also drop real
+    rows (episodic mode) it keeps a uniformly random subset of them -- rows are time-major, so a
+    tail trim would drop only the latest moves of every game."""
     m = next(iter(data.values())).shape[0]
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return data
     dev = next(iter(data.values())).device
     t = torch.tensor([m], dtype=torch.int64, device=dev if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
-    k = int(t.item())
-    return data if k == m else {key: v[:k] for key, v in data.items()}
+    return trim_rows(data, int(t.item()), n_real, generator)
+
+
+def trim_rows(data: dict, k: int, n_real: int | None = None, generator: torch.Generator | None = None) -> dict:
+    """Keep k rows of `data`: all real rows and the first copies when k >= n_real, else a random
+    k-subset of the real rows (in their original order)."""
+    m = next(iter(data.values())).shape[0]
+    n_real = m if n_real is None else min(int(n_real), m)
+    if k >= m:
+        return data
+    if k >= n_real:
+        return {key: v[:k] for key, v in data.items()}
+    dev = next(iter(data.values())).device
+    gdev = generator.device if generator is not None else dev
+    keep = torch.randperm(n_real, generator=generator, device=gdev)[:k].sort().values.to(dev)
+    return {key: v.index_select(0, keep) for key, v in data.items()}
 
 
 def allreduce_sum_(t: torch.Tensor) -> torch.Tensor:

@@ -174,7 +174,9 @@ class PPOUpdater:
             return
         self._g = None
         torch.cuda.synchronize()
-        split = self.grads.world() > 1
+        # several ranks: the gradient all-reduce runs eagerly between two graphs (g1: forward, loss,
+        # backward; g2: clip, optimizer, KL); force_split exercises that path on one GPU
+        split = self.grads.world() > 1 or self.force_split
         idx = torch.zeros(bs, dtype=torch.int64, device=self.dev)
         params = [p for p in self.model.parameters()]
         snap_p = [p.detach().clone() for p in params]
@@ -205,6 +207,8 @@ class PPOUpdater:
         self.stats.copy_(snap_s)
         self._extra_restore(snap_x)
         self._g = {"key": key, "idx": idx, "g1": g1, "g2": g2, "st": st}
+
+    force_split = False
 
     def _extra_snapshot(self):
         return None

@@ -114,6 +114,8 @@ class VecTrainer:
         self.rtg = RTGTracker(n, self.dev, self.weights, allreduce=allreduce_sum_ if self.world > 1 else None)
         gen = torch.Generator(device=self.dev)
         gen.manual_seed(cfg.seed + 104729 * self.rank)
+        self.trim_gen = torch.Generator(device=self.dev)  # equal_rows' random row subset
+        self.trim_gen.manual_seed(cfg.seed + 15485863 * (self.rank + 1))
         pcfg = PPOConfig(batch_size=cfg.batch_size, epochs=cfg.epochs, critic=cfg.critic,
                          amp_dtype=torch.bfloat16 if cfg.amp else None)
         graph_up = cfg.graph_update and not self.episodic
@@ -142,41 +144,45 @@ class VecTrainer:
         return self.obs_mb
 
     def _collect_episodic(self):
+        """Play every env's game until all are over or the step cap (--max-steps, train.py:240:
+        `step < max_steps`) is reached; returns the number of steps played (<= the cap).  Steps run
+        in chunks of `chunk` captured in hipGraphs; the last chunk stops at the cap."""
         ro, b = self.rollout, self.rollout.buf
         ro.reset()
         self.run_score.zero_()
         self.run_maxexp.zero_()
+        cap = min(ro.T, self.cfg.max_steps or self.cfg.episodic_cap)
         used = 0
-        for c0 in range(0, ro.T, self.cfg.chunk):
-            key = c0
+        for c0 in range(0, cap, self.cfg.chunk):
+            c1 = min(c0 + self.cfg.chunk, cap)
             if self.cfg.graph:
-                g = self._chunk_graphs.get(key)
+                g = self._chunk_graphs.get((c0, c1))
                 if g is None:
-                    g = self._capture_chunk(c0)
-                    self._chunk_graphs[key] = g
+                    g = self._capture_chunk(c0, c1)
+                    self._chunk_graphs[(c0, c1)] = g
                 g.replay()
             else:
-                for t in range(c0, c0 + self.cfg.chunk):
+                for t in range(c0, c1):
                     ro._step(t, self.policy)
-            used = c0 + self.cfg.chunk
+            used = c1
             if bool(((b.flags[used] & L.FLAG_LEGAL) == 0).all()):  # every game is over
                 break
         ro.counter.add_(2 * ro.T)
         return used
 
-    def _capture_chunk(self, c0):
+    def _capture_chunk(self, c0, c1):
         ro = self.rollout
         b = ro.buf
         snap = (b.boards[c0].clone(), b.flags[c0].clone())
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            for t in range(c0, c0 + self.cfg.chunk):
+            for t in range(c0, c1):
                 ro._step(t, self.policy)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            for t in range(c0, c0 + self.cfg.chunk):
+            for t in range(c0, c1):
                 ro._step(t, self.policy)
         b.boards[c0].copy_(snap[0])
         b.flags[c0].copy_(snap[1])
@@ -226,10 +232,11 @@ class VecTrainer:
             valid = torch.nonzero(valid_mask.reshape(-1)).squeeze(1)
             data = {k: v.index_select(0, valid) for k, v in data.items()}
         n_aug = 0
+        n_real = data["actions"].shape[0]
         if cfg.upsample_ratio > 0:
             data, n_aug = self._augment(data, step)
         if self.world > 1:  # every rank runs the same number of minibatches (one all-reduce each)
-            data = equal_rows(data)
+            data = equal_rows(data, n_real, self.trim_gen)
         self._mark("augment_ms")
         ustats = self.ppo.update(data, self.beta, self._encode)
         self.opt.scheduler_step()

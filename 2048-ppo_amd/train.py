@@ -89,17 +89,18 @@ def calculate_advantage(episodes, discount_rate, rtg_first_moment, points_weight
                       device=dev)
     cfg = L.RewardCfg(discount_rate, points_weight, monotonicity_weight, emptiness_weight, rtg_beta)
     g_raw, g_norm, adv = (torch.zeros(T, n, dtype=torch.float32, device=dev) for _ in range(3))
+    reward = torch.zeros(T, n, dtype=torch.float64, device=dev)
     part = torch.zeros(3, dtype=torch.float64, device=dev)
     ws = torch.zeros(L.rtg_workspace_bytes(n), dtype=torch.uint8, device=dev)
     L.rtg_prepare(st, cfg)
-    L.reward_rtg(t(points, None), t(pot, None), t(flags, None), t(value, None), st, g_raw, g_norm, adv, part, ws, cfg)
+    L.reward_rtg(t(points, None), t(pot, None), t(flags, None), t(value, None), st, g_raw, g_norm, adv, part, ws, cfg,
+                 reward=reward)
     L.rtg_finalize(st, part, cfg)
     gr, gn, ad, s = g_raw.cpu().numpy(), g_norm.cpu().numpy(), adv.cpu().numpy(), st.tolist()
+    rw = reward.cpu().numpy()
     for e, ep in enumerate(eps):
         for k, m in enumerate(ep["moves"]):
-            shaped = monotonicity_weight * (discount_rate * m["monotonicity_after"] - m["monotonicity_before"])
-            shaped += emptiness_weight * (discount_rate * m["emptiness_after"] - m["emptiness_before"])
-            m["reward"] = m["points_earned"] * points_weight + shaped
+            m["reward"] = float(rw[k, e])  # the scan kernel's own float64 reward (train.py:702-719)
             m["future_reward_raw"] = float(gr[k, e])
             m["future_reward"] = float(gn[k, e])
             m["advantage"] = float(ad[k, e])

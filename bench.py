@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
 """bench.py -- env-steps/s of the 2048 hot path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 65536] [--chunk 64]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 65536] [--chunk 256]
 
-For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL).  Workload (BASELINE.md /
+For N > 1 either launch it under torch.distributed.run (one rank per GPU, RCCL; WORLD_SIZE must
+equal --gpus) or let it hand itself to torch.distributed.run: without WORLD_SIZE in the
+environment and --gpus N > 1, the parent starts N fresh ranks before it touches the GPU and exits
+with their status.  Workload (BASELINE.md /
 SURVEY.md §8d): `--envs` independent 4x4 boards per GPU, uniform random legal actions (Philox
 keyed by 0x2048 + rank), auto-reset on done.  One bench "step" = one launch of the fused
 rollout kernel `env_rollout_kernel` = `--chunk` consecutive env steps of every board, writing the
@@ -14,8 +17,12 @@ steps (weak scaling: the boards per GPU are fixed; the envs are independent, so 
 collective exists).
 
 Also reported in the same JSON line:
-  roofline       env_rollout_kernel vs HBM peak: algorithmic bytes per launch / avg launch time
-                 (HIP events on the launch stream, timed region only)
+  roofline       env_rollout_kernel: SURVEY.md §8(d)'s 42 algorithmic bytes per env-step x env-steps
+                 per launch / avg launch time (HIP events on the launch stream, timed region only)
+                 against the HBM peak; the bytes the kernel really moves (26 B per step + 32 B per
+                 board per launch) as a separate field; the VALU issue rate from the committed SQ
+                 counters of this build, and `bound` = whichever of the two is nearer its peak
+  sweep          the same kernel at 2^20 / 2^22 / 2^24 boards (beyond the 256 MiB Infinity Cache)
   single_step    the one-launch-per-step kernel (env_step_kernel, 42 B/step, §8d) captured in a
                  hipGraph, its steps/s and roofline
   train_loop     full training iteration (policy rollout with the MLP h=196 + reward/RTG scan +
@@ -38,9 +45,12 @@ sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak (spec)
-ROLLOUT_STEP_BYTES = 16 + 1 + 4 + 4 + 1  # per env-step: board record, action, points, pot, flags
-ROLLOUT_LAUNCH_BYTES = 32  # per env per launch: board in + board out
-SINGLE_STEP_BYTES = 42  # board in 16 + action 1 + board out 16 + points 4 + flags 1 + pot 4
+VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2  # wave-instructions/s: 1 024 SIMDs, one 64-lane VALU op per 2 cycles
+STEP_BYTES = 42  # SURVEY.md §8(d) algorithmic bytes per env-step: board in 16 + action 1 + board out 16
+                 # + points 4 + flags 1 + pot 4 (the roofline basis)
+ROLLOUT_STEP_BYTES = 16 + 1 + 4 + 4 + 1  # bytes the fused rollout really writes per env-step
+ROLLOUT_LAUNCH_BYTES = 32  # ... plus per board per launch: board in + board out
+SINGLE_STEP_BYTES = STEP_BYTES
 
 
 def parse():
@@ -49,7 +59,7 @@ def parse():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--envs", type=int, default=65536)
-    p.add_argument("--chunk", type=int, default=64, help="env steps per rollout launch")
+    p.add_argument("--chunk", type=int, default=256, help="env steps per rollout launch (one bench step)")
     p.add_argument("--launches-per-graph", type=int, default=8,
                    help="rollout launches captured per hipGraph replay (the timed steps stay K launches)")
     p.add_argument("--single-steps", type=int, default=256, help="graph-captured one-launch-per-step steps (0=off)")
@@ -59,8 +69,33 @@ def parse():
     p.add_argument("--train-batch", type=int, default=65536)
     p.add_argument("--train-upsample", type=float, default=0.25, help="--upsample-ratio of the README command")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of each CPU-baseline leg (0=off)")
-    p.add_argument("--sweep", default="", help="comma list of extra board counts for the rollout kernel")
+    p.add_argument("--sweep", default="1048576,4194304,16777216",
+                   help="comma list of board counts for the rollout-kernel sweep ('' = off)")
+    p.add_argument("--sweep-chunk", type=int, default=64, help="env steps per launch in the sweep")
     return p.parse_args()
+
+
+def hand_off_to_ranks(args):
+    """`--gpus N` without a torch.distributed.run environment: start N fresh ranks (one per GPU)
+    through torch.distributed.run as a child process -- before this process touches the GPU -- and
+    exit with their status.  Under a launcher, WORLD_SIZE must equal --gpus."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}; launch one rank per GPU")
+        return
+    if args.gpus <= 1:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve()), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    raise SystemExit(subprocess.call(cmd, env=env))
 
 
 def setup_dist(args):
@@ -266,25 +301,51 @@ def _c_chunk(args):
     return cnt
 
 
-PMC_PROFILE = Path(__file__).resolve().parent / "profiles" / "r01h"
+PMC_PROFILE = ROOT / "profiles" / "r02a"
 
 
-def pmc_traffic(kernel: str, args):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes of this bench at its
-    default configuration (tools/profile.sh -> tools/summarize_profile.py: 2 x FETCH_SIZE +
-    WRITE_SIZE, the gfx950 FETCH correction).  None when this run's configuration differs."""
-    f = PMC_PROFILE / "pmc_summary.json"
-    if not f.exists() or args.envs != 65536 or args.chunk != 64:
-        return None, None
-    import json as _json
-    e = _json.loads(f.read_text()).get(kernel, {})
-    b = e.get("hbm_bytes_per_dispatch")
-    return (float(b), f"{f.relative_to(Path(__file__).resolve().parent)} (rocprofv3 --pmc FETCH_SIZE / "
-                      "WRITE_SIZE passes of tools/profile.sh; 2 x FETCH + WRITE)") if b else (None, None)
+def rollout_counters():
+    """Committed rocprofv3 counters of env_rollout_kernel for this build (tools/profile.sh +
+    tools/pmc_sq.sh -> tools/summarize_rollout_pmc.py): per env-step HBM bytes (2 x FETCH_SIZE +
+    WRITE_SIZE, the gfx950 FETCH correction) and per wave-step SQ instruction counts."""
+    f = PMC_PROFILE / "pmc_env_rollout.json"
+    if not f.exists():
+        return None
+    return dict(json.loads(f.read_text()), source=str(f.relative_to(ROOT)))
+
+
+def rollout_roofline(rb, avg_launch_s, pmc):
+    """roofline / valu blocks of the headline kernel for one launch of `rb` lasting avg_launch_s."""
+    steps = rb.n * rb.chunk  # env-steps per launch
+    achieved = steps * STEP_BYTES / avg_launch_s / 1e9
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "traffic_unit": "B/launch",
+            "kernel": "env_rollout_kernel", "avg_launch_us": avg_launch_s * 1e6,
+            "bytes_per_step": STEP_BYTES, "algorithmic_bytes_per_launch": steps * STEP_BYTES,
+            "bytes_written_per_launch": rb.bytes_per_launch(),
+            "bytes_written_GBps": rb.bytes_per_launch() / avg_launch_s / 1e9}
+    valu = None
+    if pmc:
+        roof["traffic"] = pmc["hbm_bytes_per_env_step"] * steps
+        roof["traffic_source"] = pmc["source"] + f" ({pmc['envs']} boards x {pmc['chunk']} steps per launch, scaled per env-step)"
+        waves = -(-rb.n // 64)
+        vws = pmc["valu_per_wave_step"]
+        rate = vws * waves * rb.chunk / avg_launch_s
+        valu = {"valu_per_wave_step": vws, "lds_per_wave_step": pmc["lds_per_wave_step"],
+                "lds_bank_conflict_cycles_per_lds_inst": pmc["lds_conflict_per_lds_inst"],
+                "waves_per_simd": waves / 1024,
+                "cycles_per_valu_per_wave": avg_launch_s * 2.4e9 * min(1.0, 1024 / waves) / (vws * rb.chunk),
+                "achieved": rate, "peak": VALU_ISSUE_PEAK, "unit": "wave-instructions/s",
+                "frac": rate / VALU_ISSUE_PEAK, "source": pmc["source"]}
+        if valu["frac"] > roof["frac"]:
+            roof["bound"] = "valu"
+        roof["bound_basis"] = "nearer peak of HBM (42 B/step) and VALU issue (SQ_INSTS_VALU, 1 024 SIMDs x 1.2 G/s)"
+    return roof, valu
 
 
 def main():
     args = parse()
+    hand_off_to_ranks(args)  # --gpus N > 1 without a launcher: N fresh ranks, before any GPU call
     import torch
     rank, world, local = setup_dist(args)
     dev = torch.device("cuda", local)
@@ -300,10 +361,9 @@ def main():
     ev_max = max_over_ranks(ev, world)
     env_steps = args.envs * args.chunk * args.steps * world
     value = env_steps / wall
-    avg_launch = ev / args.steps
-    achieved = rb.bytes_per_launch() / avg_launch / 1e9
-
-    traffic, traffic_src = pmc_traffic("env_rollout_kernel", args)
+    roof, valu = rollout_roofline(rb, ev / args.steps, rollout_counters())
+    roof["event_ms_max_rank"] = ev_max * 1e3
+    roof["frac_of_value"] = value / world * STEP_BYTES / 1e9 / HBM_PEAK_GBPS  # same basis from the wall clock
     result = {
         "metric": "env-steps/sec (whole node) at 65536 parallel 4x4 boards, 1/2/4/8 MI355X",
         "value": value,
@@ -321,25 +381,27 @@ def main():
                    "boards_per_gpu": args.envs, "env_steps_per_step": args.envs * args.chunk,
                    "launches_per_graph": rb.per_graph,
                    "parallelism": f"env-shard x{world} (no data-path collective)"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_unit": "B/launch",
-                     "traffic_source": traffic_src, "kernel": "env_rollout_kernel",
-                     "avg_launch_us": avg_launch * 1e6, "event_ms_max_rank": ev_max * 1e3,
-                     "bytes_per_launch": rb.bytes_per_launch()},
+        "roofline": roof,
     }
+    if valu:
+        result["valu"] = valu
     del rb
     torch.cuda.empty_cache()
 
     if args.sweep:
         sweep = {}
         for s in [int(x) for x in args.sweep.split(",") if x]:
-            b = RolloutBench(s, args.chunk, rank, dev)
-            b.capture()
+            b = RolloutBench(s, args.sweep_chunk, rank, dev)
+            b.capture(1)
+            b.step()
             torch.cuda.synchronize()
-            k = max(3, args.steps // 10)
+            k = 5
             w, e = time_region(b.step, k, world)
-            sweep[str(s)] = {"env_steps_per_s_per_gpu": s * args.chunk * k / w,
-                             "achieved_GBps": b.bytes_per_launch() / (e / k) / 1e9}
+            w = max_over_ranks(w, world)
+            sweep[str(s)] = {"env_steps_per_s_per_gpu": s * args.sweep_chunk * k / w, "chunk": args.sweep_chunk,
+                             "launches": k, "avg_launch_us": e / k * 1e6,
+                             "achieved_GBps_42B": s * args.sweep_chunk * STEP_BYTES / (e / k) / 1e9,
+                             "written_GBps": b.bytes_per_launch() / (e / k) / 1e9}
             del b
             torch.cuda.empty_cache()
         result["sweep"] = sweep
@@ -357,8 +419,9 @@ def main():
         if py:
             result["cpu_baseline"] = {"value": py["value"], "unit": "env-steps/s", "cores": 1, "kind": "port",
                                       "sample": py["sample"]}
-        if "c_oracle" in cb:
-            result["cpu_baseline_c"] = cb["c_oracle"]
+        for k in ("c_oracle", "python_pool", "train_loop_cpu"):
+            if k in cb:
+                result[f"cpu_baseline_{k}"] = cb[k]
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

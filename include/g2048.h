@@ -165,6 +165,13 @@ int g2048_reward_rtg(g2048_stream_t stream, const int32_t *points, const int8_t 
                      const uint8_t *flags, const float *value, int64_t T, int64_t n,
                      const g2048_reward_cfg *cfg, const double *state, float *g_raw, float *g_norm,
                      float *adv, double *partials, void *workspace, size_t workspace_bytes);
+/* g2048_reward_rtg plus the per-step reward itself (train.py:702-719, float64, bit-identical to the
+ * reference's Python floats; 0 on inactive steps) into reward [T][n] when it is not NULL. */
+int g2048_reward_rtg_ex(g2048_stream_t stream, const int32_t *points, const int8_t *pot,
+                        const uint8_t *flags, const float *value, int64_t T, int64_t n,
+                        const g2048_reward_cfg *cfg, const double *state, float *g_raw, float *g_norm,
+                        float *adv, double *reward, double *partials, void *workspace,
+                        size_t workspace_bytes);
 
 /* Episode statistics of a fixed-horizon rollout (compute_batch_stats' scores and tiles,
  * train.py:1040-1120): per env, the running score / max tile exponent of its current game is

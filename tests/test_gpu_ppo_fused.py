@@ -665,3 +665,69 @@ def test_deferred_column_sums_match_immediate(dev):
     L.ppo_stats(got[4], kl_ref, gn, beta_t, 0.5, m, stats_a)
     L.ppo_stats(got[4], part["kl"], gn, beta_t, 0.5, m, stats_b, kl_rows=kl_job.nb)
     torch.testing.assert_close(stats_b, stats_a, rtol=1e-5, atol=1e-7)
+
+
+def test_fused_split_graph_equals_unsplit(dev):
+    """The multi-rank capture (g1 = forward/loss/backward, the eager gradient all-reduce, g2 = clip +
+    Muon/AdamW + KL; g2048/ppo.py _ensure_graph / _replay) forced on one GPU, where the all-reduce is
+    a no-op: parameters, optimizer state and statistics are bitwise the single-graph step's, also
+    over a ragged padded last minibatch."""
+    import agent
+    from g2048.dist import GradBucket
+    from g2048.fastmlp import FusedPPOUpdater
+    from g2048.optim import FusedMuonAdamW
+    from g2048.ppo import PPOConfig
+    data = _synthetic_data(dev, 8192, seed=11)
+    out = []
+    for split in (False, True):
+        torch.manual_seed(4)
+        m = agent.GameMLP(agent.MLPConfig(hidden_dim=196, num_layers=2, dropout=0.1)).to(dev)
+        opt = FusedMuonAdamW(m, 1e-3, 1e-4)
+        order = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(6)
+        up = FusedPPOUpdater(m, opt, PPOConfig(batch_size=3000, critic=0.2), GradBucket(order), gen, graph=True)
+        up.force_split = split
+        sts = [{k: float(v) for k, v in up.update(data, 0.02).items()} for _ in range(2)]
+        assert (up._g["g2"] is not None) == split
+        def flat(x):
+            if torch.is_tensor(x):
+                return [x.detach().cpu()]
+            return [t for y in (x if isinstance(x, (list, tuple)) else []) for t in flat(y)]
+        state = flat(opt.snapshot())
+        assert state
+        out.append((torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy(), sts, state))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
+    for a, b in zip(out[0][2], out[1][2]):
+        assert torch.equal(a, b)
+
+
+def test_fused_policy_on_reference_checkpoint_matches_golden(dev):
+    """FusedPolicy (g2048_mlp_fwd per layer + g2048_head_fwd, bf16 MFMA) on the reference's own
+    best_model.pt weights (h=192, tests/golden/mlp.npz) against the reference's fp32 forward of the
+    256 fixture boards.  Absolute bounds, set from the bf16 rounding of weights and activations
+    (torch's bf16 module on the same weights reaches max 0.051 / mean 0.009 on the logits, whose
+    range is +-8, and max 0.025 / mean 0.004 on the value): logits max 0.08, mean 0.015; value max
+    0.04, mean 0.008; the greedy legal action equals the reference's wherever its top-2 logit
+    margin exceeds 0.16."""
+    import agent
+    from g2048.rollout import FusedPolicy
+    g = golden("mlp.npz")
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=int(g["hidden_dim"]), num_layers=int(g["num_layers"]))).to(dev)
+    m.load_state_dict({k[3:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("w::")}, strict=True)
+    m.eval()
+    assert FusedPolicy.supports(m)
+    obs = torch.from_numpy(g["obs"]).to(dev).to(torch.bfloat16)
+    lf, vf = FusedPolicy(m)(obs)
+    el = np.abs(lf.cpu().numpy() - g["logits"])
+    ev = np.abs(vf.cpu().numpy() - g["value"][:, 0])
+    assert el.max() <= 0.08 and el.mean() <= 0.015, (el.max(), el.mean())
+    assert ev.max() <= 0.04 and ev.mean() <= 0.008, (ev.max(), ev.mean())
+    legal = O.legal_mask(g["boards"]) & 0xF
+    mask = ((legal[:, None] >> np.arange(4)) & 1).astype(bool)
+    ref = np.where(mask, g["logits"], -np.inf)
+    got = np.where(mask, lf.cpu().numpy(), -np.inf)
+    srt = np.sort(ref, axis=1)
+    clear = (srt[:, -1] - srt[:, -2] > 0.16) & (mask.sum(1) > 0)
+    assert np.array_equal(got.argmax(1)[clear], ref.argmax(1)[clear])

@@ -125,3 +125,22 @@ def test_grad_bucket_views_and_clip():
     assert math.isclose(float(gb.flat.norm()), 1.0, rel_tol=1e-4)
     gb.zero()
     assert float(gb.flat.abs().sum()) == 0.0 and gb.check_views()
+
+
+def test_trim_rows_drops_copies_first_then_random_real_rows():
+    """dist.trim_rows (equal_rows' local part): D4 copies go first; real rows are dropped as a
+    uniformly random subset kept in order (a tail trim of time-major rows would drop only late moves)."""
+    import torch
+    from g2048.dist import trim_rows
+    m, n_real = 100, 60
+    data = {"a": torch.arange(m), "b": torch.arange(m) * 10}
+    out = trim_rows(data, 80, n_real)
+    assert torch.equal(out["a"], torch.arange(80))
+    g = torch.Generator().manual_seed(0)
+    out = trim_rows(data, 30, n_real, g)
+    a = out["a"]
+    assert a.numel() == 30 and torch.equal(out["b"], a * 10)
+    assert bool((a < n_real).all()) and bool((a[1:] > a[:-1]).all())  # real rows only, original order
+    assert int(a.max()) >= 45  # not a head/tail slice of the time-major rows
+    assert a.tolist() != list(range(30))
+    assert trim_rows(data, m, n_real) is data

@@ -3,10 +3,13 @@
     python tools/summarize_profile.py gpurun_out/prof_<tag> profiles/<tag>
 
 Writes kernel_stats.csv (rocprofv3 --stats of the trace pass, copied), domain_stats.csv when
-present, and pmc_summary.json: per kernel the average FETCH_SIZE / WRITE_SIZE per dispatch (KB =
+present, pmc_summary.json: per kernel the average FETCH_SIZE / WRITE_SIZE per dispatch (KB =
 1024 B, as rocprofv3 reports) and the HBM traffic per dispatch = 2 x FETCH_SIZE + WRITE_SIZE
 (gfx950 counts a wide coalesced streaming read at half its bytes in FETCH_SIZE:
-/opt/skills/guides/MI355X_MICROARCH.md, HBM section).
+/opt/skills/guides/MI355X_MICROARCH.md, HBM section), pmc_sq.json: per kernel the average of
+every SQ/GRBM counter of the sqa/sqb passes, and pmc_env_rollout.json: the headline kernel's
+counters normalised per env-step / per wave-step for bench.py (PMC_ENVS / PMC_CHUNK = the
+rollout configuration of the PMC passes, default 65536 x 256).
 """
 
 from __future__ import annotations
@@ -14,6 +17,7 @@ from __future__ import annotations
 import collections
 import csv
 import json
+import os
 import shutil
 import sys
 from pathlib import Path
@@ -49,6 +53,29 @@ def main(src: str, dst: str):
             e["hbm_bytes_per_dispatch"] = (2 * sum(f) / len(f) + sum(w) / len(w)) * 1024
         summary[k] = e
     (dst_p / "pmc_summary.json").write_text(json.dumps(summary, indent=1) + "\n")
+    sq = collections.defaultdict(dict)
+    for sub in ("sqa", "sqb"):
+        for f in (src_p / sub).rglob("*counter_collection.csv") if (src_p / sub).exists() else []:
+            acc = collections.defaultdict(list)
+            for r in csv.DictReader(open(f)):
+                acc[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+            for (k, c), v in acc.items():
+                sq[k][c] = sum(v) / len(v)
+    if sq:
+        (dst_p / "pmc_sq.json").write_text(json.dumps(sq, indent=1, sort_keys=True) + "\n")
+    roll = next((k for k in summary if k.startswith("env_rollout_kernel")), None)
+    sqr = next((v for k, v in sq.items() if k.startswith("env_rollout_kernel")), None)
+    if roll and sqr and "hbm_bytes_per_dispatch" in summary[roll]:
+        envs, chunk = int(os.environ.get("PMC_ENVS", 65536)), int(os.environ.get("PMC_CHUNK", 256))
+        steps = envs * chunk
+        ws = sqr["SQ_WAVES"] * chunk
+        out = {"envs": envs, "chunk": chunk, "hbm_bytes_per_dispatch": summary[roll]["hbm_bytes_per_dispatch"],
+               "hbm_bytes_per_env_step": summary[roll]["hbm_bytes_per_dispatch"] / steps,
+               "valu_per_wave_step": sqr["SQ_INSTS_VALU"] / ws, "lds_per_wave_step": sqr["SQ_INSTS_LDS"] / ws,
+               "salu_per_wave_step": sqr.get("SQ_INSTS_SALU", 0.0) / ws,
+               "lds_conflict_per_lds_inst": sqr.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(sqr["SQ_INSTS_LDS"], 1.0),
+               "counters": sqr}
+        (dst_p / "pmc_env_rollout.json").write_text(json.dumps(out, indent=1) + "\n")
     print(json.dumps({k: v.get("hbm_bytes_per_dispatch") for k, v in summary.items()}, indent=1))
 
 
