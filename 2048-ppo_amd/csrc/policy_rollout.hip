@@ -1,0 +1,532 @@
+// policy_rollout.hip -- the fused persistent policy rollout: K consecutive
+// steps of play_game_for_episode's loop body (train.py:240-337) for every env in ONE launch,
+//
+//     obs = to_model_format(board)                        game.py:92-101
+//     logits, value = GameMLP(obs)  (eval mode)           game.py:1145-1220
+//     action ~ masked softmax(logits)                     train.py:266-291, 326
+//     board = Game2048.step(board, action)                game.py:952-1030
+//
+// writing the same time-major records as the per-step path of g2048/rollout.py (Rollout._step:
+// obs_encode -> FusedPolicy = 3 x g2048_mlp_fwd + g2048_head_fwd -> g2048_sample_actions ->
+// g2048_env_step), and with the same arithmetic: every operand fragment, MFMA accumulation chain,
+// rounding and reduction order of those kernels is reproduced, so the records are bitwise those of
+// the per-step path at the same seed and counter (tests/test_gpu_policy_rollout.py).
+//
+// Layout (one 256-thread workgroup per CU, persistent over groups of 256 boards):
+//   * lane = board: each of the 4 waves owns 64 boards (4 MFMA board tiles of 16); the board, its
+//     legal mask and the env step stay in the lane's registers for all K steps.
+//   * GameMLP on v_mfma_f32_16x16x32_bf16 as Y^T = W X^T (g2048_mlp_fwd's orientation): lane (g, c)
+//     of board tile bt holds features 16n + 4g + r of board 16 bt + c.  A layer's output becomes the
+//     next layer's B operand in registers: for k-step ks, two v_permlane32_swap + two
+//     v_permlane16_swap per dword pair turn tiles 2ks, 2ks+1 ("lane g holds features 4g..4g+3")
+//     into the fragment ("lane g holds k = 8g..8g+7") -- no LDS round trip, natural k order.
+//   * LDS (160 KiB): the two h x h block weights (bf16, row pitch round_up(h, 8)), the three
+//     LayerNorm affines (fp32) and a zero fragment.  The stem
+//     (h x 48) and the heads are read from global memory (L1/L2-resident, 19 KB + 2 KB).
+//   * heads: one MFMA chain over (board tile, k-step) whose A operand is non-zero only in rows
+//     4 bt .. 4 bt + 3 for board tile bt, so lane (g, c) ends with the 4 logits of board 16 g + c --
+//     its own env lane -- with no transpose; a second chain does the value.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "board.hpp"
+#include "step.hpp"
+#include "../../include/g2048.h"
+#include "../../include/g2048_ppo.h"
+
+using namespace g2048;
+
+namespace {
+
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr float kLnEps = 1e-5f;
+constexpr int kPrThreads = 256;
+constexpr int kPrLdsMax = 163840;
+constexpr int kMaxLayers = 3;  // stem + 2 residual blocks (GameMLP num_layers = 2)
+#ifndef PR_TILES
+#define PR_TILES 2
+#endif
+constexpr int kQ = PR_TILES;  // board tiles (of 16 boards) per MLP pass: accumulators of kQ x NT tiles
+
+__constant__ float kThirdsPr[4] = {0.0f, 1.0f / 3.0f, 2.0f / 3.0f, 1.0f};
+
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+    const bf16x2_t v = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+__device__ __forceinline__ bf16x8_t as_frag(const uint4 &v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+// LDS geometry of one block weight image for hidden size h: row pitch P = round_up(h, 8) bf16 in
+// 16-byte granules.  (At h = 196, P = 400 B: the 16 rows of a fragment load hit 2-way bank
+// conflicts; a conflict-free pitch, 544 B, does not fit two images in 160 KiB.)
+__host__ __device__ constexpr int pr_pitch(int h) { return ((2 * ((h + 7) & ~7)) + 15) & ~15; }
+__host__ __device__ constexpr int pr_shift(int, int) { return 0; }
+__host__ __device__ constexpr int pr_wbytes(int h) { return h * pr_pitch(h); }
+__host__ __device__ constexpr int pr_ln_floats(int nt) { return 16 * nt; }  // one affine vector, zero padded
+__host__ __device__ constexpr int pr_lds_bytes(int h, int nt) {
+    return 2 * pr_wbytes(h) + 2 * kMaxLayers * pr_ln_floats(nt) * 4 + 16;
+}
+
+struct PrArgs {
+    uint4 *boards;      // [T+1][n][16] int8: row t0 read, rows t0+1 .. t1 written
+    uint8_t *flags;     // [T+1][n]
+    uint8_t *actions;   // [T][n]
+    float *logp;        // [T][n][4]
+    float *entropy;     // [T][n]
+    float *value;       // [T][n]
+    int32_t *points;    // [T][n]
+    int8_t *max_tile;   // [T][n]
+    uint32_t *pot;      // [T][n] (mono_b, mono_a, empt_b, empt_a)
+    int64_t n;
+    int32_t t0, t1, h, opts;
+    const uint16_t *w0;            // stem Linear bf16 [h][48]
+    const uint16_t *w1, *w2;       // block Linears bf16 [h][h]
+    const float *gamma[kMaxLayers], *beta[kMaxLayers];
+    const uint16_t *head;          // bf16 [5][32 KS]: action_head rows 0..3, value_head row 4, zero padded
+    const float *ba, *bv;          // head biases (fp32)
+    uint64_t seed;
+    const uint64_t *counter_dev;
+    uint64_t counter;
+    uint32_t env_base;
+    float *debug;  // optional test hook: layer outputs and head outputs of step t0
+};
+
+// debug: layer l's output (bf16 values as fp32) of board `board` into debug[(l n + board) 16 NT + f]
+template <int NT>
+__device__ __forceinline__ void debug_act(const PrArgs &a, int l, int64_t board, const uint2 (&act)[NT], int g) {
+    if (board >= a.n) return;
+    float *d = a.debug + ((int64_t)l * a.n + board) * (16 * NT);
+#pragma unroll
+    for (int n = 0; n < NT; n++) {
+        const int f = 16 * n + 4 * g;
+        d[f] = bf_lo(act[n].x);
+        d[f + 1] = bf_hi(act[n].x);
+        d[f + 2] = bf_lo(act[n].y);
+        d[f + 3] = bf_hi(act[n].y);
+    }
+}
+
+// --------------------------------------------------------------- layer epilogues --------------
+// g2048_mlp_fwd's epilogue (ppo_update.hip, mlp_fwd_kernel) on one board tile: G = bf16(acc),
+// LayerNorm statistics in the same order (features in tile order, then the xor-16 and xor-32 lane
+// sums), Y = [X +] ReLU(LN(G)) rounded to bf16.  act[n] holds the layer input (residual) on entry
+// and the output on exit; features >= h are zero.
+template <int NT, bool RES>
+__device__ __forceinline__ void ln_epilogue(f32x4_t (&acc)[NT], uint2 (&act)[NT], const float *sgam, const float *sbet,
+                                            int h, int g, float inv_n) {
+    // this file is built -ffp-contract=off (the sampler and env step must round like g2048.hip);
+    // mlp_fwd_kernel is built with contraction, so its epilogue contracts here too
+#pragma clang fp contract(fast)
+    float sum = 0.0f;
+#pragma unroll
+    for (int n = 0; n < NT; n++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const float v = (float)(__bf16)acc[n][r];
+            acc[n][r] = v;
+            sum += 16 * n + 4 * g < h ? v : 0.0f;
+        }
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    const float mean = sum * inv_n;
+    float var = 0.0f;
+#pragma unroll
+    for (int n = 0; n < NT; n++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const float dv = 16 * n + 4 * g < h ? acc[n][r] - mean : 0.0f;
+            var += dv * dv;
+        }
+    var += __shfl_xor(var, 16);
+    var += __shfl_xor(var, 32);
+    const float rstd = 1.0f / sqrtf(var * inv_n + kLnEps);
+#pragma unroll
+    for (int n = 0; n < NT; n++) {
+        const int f0 = 16 * n + 4 * g;
+        const float4 ga = *reinterpret_cast<const float4 *>(sgam + f0);
+        const float4 be = *reinterpret_cast<const float4 *>(sbet + f0);
+        const float gg[4] = {ga.x, ga.y, ga.z, ga.w}, bb[4] = {be.x, be.y, be.z, be.w};
+        float rs[4] = {0.0f, 0.0f, 0.0f, 0.0f}, o[4];
+        if (RES) {
+            rs[0] = bf_lo(act[n].x);
+            rs[1] = bf_hi(act[n].x);
+            rs[2] = bf_lo(act[n].y);
+            rs[3] = bf_hi(act[n].y);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const float a = fmaxf((acc[n][r] - mean) * rstd * gg[r] + bb[r], 0.0f);
+            o[r] = RES ? rs[r] + a : a;
+        }
+        const bool ok = f0 < h;
+        act[n] = ok ? make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3])) : make_uint2(0u, 0u);
+        if (n & 1) __builtin_amdgcn_sched_barrier(0);  // bound the affine loads in flight
+    }
+}
+
+// The B fragment of k-step ks (k = 32 ks + 8 g .. + 7 of the board in column c) from the layer
+// output tiles 2 ks and 2 ks + 1 held as "lane g: features 4g .. 4g+3" (see the file comment).
+template <int NT>
+__device__ __forceinline__ uint4 act_frag(const uint2 (&act)[NT], int ks) {
+    const int t0 = 2 * ks, t1 = 2 * ks + 1;
+    const uint32_t a0 = act[t0].x, a1 = act[t0].y;
+    const uint32_t b0 = t1 < NT ? act[t1 < NT ? t1 : 0].x : 0u, b1 = t1 < NT ? act[t1 < NT ? t1 : 0].y : 0u;
+    const auto s0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+    const auto s1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+    const auto f0 = __builtin_amdgcn_permlane16_swap(s0[0], s0[1], false, false);
+    const auto f1 = __builtin_amdgcn_permlane16_swap(s1[0], s1[1], false, false);
+    return make_uint4(f0[0], f1[0], f0[1], f1[1]);
+}
+
+// The sampler of g2048_sample_actions (g2048.hip, sample_kernel; built there with
+// -ffp-contract=off): masked softmax, inverse-CDF action of the stream-1 Philox uniform, entropy,
+// log_softmax with -inf on illegal actions.
+__device__ __forceinline__ uint32_t sample_row(const float (&l)[4], uint32_t legal, uint32_t u32, float (&lp)[4],
+                                               float &ent) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+        if ((legal >> a) & 1u) m = fmaxf(m, l[a]);
+    float e[4], s = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        e[a] = ((legal >> a) & 1u) ? expf(l[a] - m) : 0.0f;
+        s += e[a];
+    }
+    const float ls = logf(s), inv = 1.0f / s;
+    const float u = (float)(u32 >> 8) * (1.0f / 16777216.0f);
+    float cum = 0.0f, hh = 0.0f;
+    uint32_t act = 0xFFu;
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        const bool ok = (legal >> a) & 1u;
+        const float p = e[a] * inv, lq = (l[a] - m) - ls;
+        if (ok) {
+            cum += p;
+            if (act == 0xFFu && u < cum) act = (uint32_t)a;
+            if (p > 0.0f) hh -= p * lq;
+        }
+        lp[a] = ok ? lq : -INFINITY;
+    }
+    if (act == 0xFFu) {
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+            if ((legal >> a) & 1u) act = (uint32_t)a;
+        if (!legal) act = 0u;
+    }
+    ent = legal ? hh : 0.0f;
+    return act;
+}
+
+template <int NT, int KS>
+__global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int h = a.h;
+    const int P = pr_pitch(h), WB = pr_wbytes(h);
+    char *sW[2] = {smem, smem + WB};  // block weight images (LDS offsets 0 and WB)
+    float *sLN = reinterpret_cast<float *>(smem + 2 * WB);  // [layer][gamma | beta][16 NT]
+    char *sZero = smem + 2 * WB + 2 * kMaxLayers * pr_ln_floats(NT) * 4;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, col = lane & 15;
+
+    // ---- stage the block weights (bank-spread rows, zero K padding), LayerNorm affines, zero block
+    {
+        const int q8 = P / 8, h4 = h / 4;  // 8-byte pieces per LDS row / per global row
+        const uint16_t *wsrc[2] = {a.w1, a.w2};
+        for (int l = 0; l < 2; l++)
+            for (int c = tid; c < h * q8; c += kPrThreads) {
+                const int r = c / q8, q = c - r * q8;
+                const uint2 v = q < h4 ? *reinterpret_cast<const uint2 *>(wsrc[l] + (int64_t)r * h + 4 * q) : make_uint2(0u, 0u);
+                *reinterpret_cast<uint2 *>(sW[l] + r * P + pr_shift(h, r) + 8 * q) = v;
+            }
+        for (int e = tid; e < kMaxLayers * 2 * 16 * NT; e += kPrThreads) {
+            const int l = e / (32 * NT), rem = e - l * 32 * NT, which = rem / (16 * NT), f = rem - which * 16 * NT;
+            const float *src = which ? a.beta[l] : a.gamma[l];
+            sLN[e] = f < h ? src[f] : 0.0f;
+        }
+        if (tid < 4) reinterpret_cast<uint32_t *>(sZero)[tid] = 0u;
+    }
+    __syncthreads();
+
+    const float inv_n = 1.0f / (float)h;
+    const int hp8 = (h + 7) & ~7;
+    const int KP = 32 * KS;  // padded row length of the head buffer
+    const uint64_t ctr0 = a.counter + (a.counter_dev ? *a.counter_dev : 0ull);
+    RngArgs rng{a.seed, 0ull, nullptr, a.env_base, nullptr, nullptr};
+
+    // per-lane constants of the stem fragments (obs features k = 32 ks + 8 g + j, cell k/3, kind k%3)
+    float xc[2][8];
+    uint32_t xmask[2], xsel[2], xpair[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++) {
+        xmask[ks] = 0u;
+        int first = -1;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int k = 32 * ks + 8 * g + j, cell = k / 3, kind = k - 3 * cell;
+            const bool in = k < 48;
+            xc[ks][j] = (!in || kind == 0) ? 0.0f : kThirdsPr[kind == 1 ? (cell >> 2) : (cell & 3)];
+            if (in && kind == 0) {
+                xmask[ks] |= 1u << j;
+                if (first < 0) first = cell;
+            }
+        }
+        // the (up to 3) exponent cells first, first+1, first+2 lie in board dwords d, d + 1
+        const int c0 = first < 0 ? 0 : first, d = (c0 >> 2) < 3 ? (c0 >> 2) : 2;
+        xpair[ks] = (uint32_t)d;
+        uint32_t sel = 0x0C0C0C0Cu;  // v_perm: bytes 0..2 = cells c0, c0+1, c0+2 of {dword d+1, dword d}
+#pragma unroll
+        for (int s = 0; s < 3; s++) {
+            const int byte = c0 + s - 4 * d;  // 0..7 within the pair (low dword = bytes 0..3)
+            if (byte < 8) sel = (sel & ~(0xFFu << (8 * s))) | ((uint32_t)byte << (8 * s));
+        }
+        xsel[ks] = sel;
+    }
+    // A-fragment LDS offsets of the block weights: row 16 n + col, k = 32 ks + 8 g (+ 16 n P per tile)
+    const int wlane = col * P + pr_shift(h, col) + 16 * g;
+    const int zoff = (int)(sZero - smem);
+    const int last_rows = h - 16 * (NT - 1);  // valid rows of the last tile
+
+    for (int64_t base = (int64_t)blockIdx.x * kPrThreads; base < a.n; base += (int64_t)gridDim.x * kPrThreads) {
+        if (base + 64 * wave >= a.n) continue;  // an empty wave (no barrier below)
+        const int64_t i = base + 64 * wave + lane;
+        const bool live = i < a.n;
+        uint4 b = live ? a.boards[(int64_t)a.t0 * a.n + i] : make_uint4(0u, 0u, 0u, 0u);
+        uint32_t legal = live ? (uint32_t)(a.flags[(int64_t)a.t0 * a.n + i] & 0xFu) : 0u;
+
+        for (int t = a.t0; t < a.t1; t++) {
+            // opaque per-step copies of the lane offsets: without them the compiler hoists every
+            // (tile, k-step) fragment address out of the step loop and spills them
+            int wlane_t = wlane, glane_t = (col * 48 + 8 * g) * 2, hlane_t = ((col & 3) * KP + 8 * g) * 2;
+            asm volatile("" : "+v"(wlane_t), "+v"(glane_t), "+v"(hlane_t));
+            const char *w0b = reinterpret_cast<const char *>(a.w0) + glane_t;
+            const char *hdb = reinterpret_cast<const char *>(a.head) + hlane_t;
+            const char *hvb = reinterpret_cast<const char *>(a.head) + (4 * KP + 8 * g) * 2;
+            // The MLP runs on two board tiles at a time (accumulators of 2 x NT tiles; the weight
+            // fragments are read once per pair): stem, blocks and the pair's share of the head
+            // chains.  A pair's epilogue overwrites its own layer input (the residual) in place.
+            f32x4_t accL = {0.0f, 0.0f, 0.0f, 0.0f}, accV = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 1
+            for (int pr = 0; pr < 4 / kQ; pr++) {
+                uint2 act[kQ][NT];
+                // ---------------- stem: obs fragments (to_model_format, natural k order) ------
+                uint4 xs[kQ][2];
+#pragma unroll
+                for (int q = 0; q < kQ; q++) {
+                    const int src = 16 * (kQ * pr + q) + col;
+                    const uint32_t B0 = __shfl(b.x, src), B1 = __shfl(b.y, src), B2 = __shfl(b.z, src),
+                                   B3 = __shfl(b.w, src);
+#pragma unroll
+                    for (int ks = 0; ks < 2; ks++) {
+                        const uint32_t d = xpair[ks];
+                        const uint32_t lo = d == 0u ? B0 : d == 1u ? B1 : B2;
+                        const uint32_t hi = d == 0u ? B1 : d == 1u ? B2 : B3;
+                        const uint32_t X = __builtin_amdgcn_perm(hi, lo, xsel[ks]);
+                        const float f[3] = {(float)(X & 0xFFu), (float)((X >> 8) & 0xFFu), (float)((X >> 16) & 0xFFu)};
+                        float e[8];
+#pragma unroll
+                        for (int j = 0; j < 8; j++) e[j] = ((xmask[ks] >> j) & 1u) ? f[j / 3] : xc[ks][j];
+                        xs[q][ks] = make_uint4(pack_bf2(e[0], e[1]), pack_bf2(e[2], e[3]), pack_bf2(e[4], e[5]),
+                                               pack_bf2(e[6], e[7]));
+                    }
+                }
+                f32x4_t acc[kQ][NT];
+#pragma unroll
+                for (int q = 0; q < kQ; q++)
+#pragma unroll
+                    for (int n = 0; n < NT; n++) acc[q][n] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int ks = 0; ks < 2; ks++) {
+#pragma unroll
+                    for (int n = 0; n < NT; n++) {
+                        const int row = 16 * n + col, k = 32 * ks + 8 * g;
+                        uint4 fw = make_uint4(0u, 0u, 0u, 0u);
+                        if (row < h && k < 48) fw = *reinterpret_cast<const uint4 *>(w0b + 2 * (16 * n * 48 + 32 * ks));
+#pragma unroll
+                        for (int q = 0; q < kQ; q++)
+                            acc[q][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(fw), as_frag(xs[q][ks]), acc[q][n], 0, 0, 0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int q = 0; q < kQ; q++) ln_epilogue<NT, false>(acc[q], act[q], sLN, sLN + 16 * NT, h, g, inv_n);
+                if (a.debug && t == a.t0)
+                    for (int q = 0; q < kQ; q++) debug_act<NT>(a, 0, base + 64 * wave + 16 * (kQ * pr + q) + col, act[q], g);
+
+                // ---------------- residual blocks ---------------------------------------------
+#pragma unroll
+                for (int l = 0; l < 2; l++) {
+#pragma unroll
+                    for (int q = 0; q < kQ; q++)
+#pragma unroll
+                        for (int n = 0; n < NT; n++) acc[q][n] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+                    const int wbase = l * WB + wlane_t;
+#pragma unroll
+                    for (int ks = 0; ks < KS; ks++) {
+                        uint4 bf[kQ];
+#pragma unroll
+                        for (int q = 0; q < kQ; q++) bf[q] = act_frag<NT>(act[q], ks);
+                        const bool kok = 32 * ks + 8 * g < hp8;
+                        int kbase = wbase + 64 * ks;  // materialised here, per k-step (see wlane_t)
+                        asm volatile("" : "+v"(kbase));
+#pragma unroll
+                        for (int n = 0; n < NT; n++) {
+                            const bool rok = n < NT - 1 || col < last_rows;
+                            const int off = (kok && rok) ? kbase + 16 * n * P : zoff;
+                            const uint4 fw = *reinterpret_cast<const uint4 *>(smem + off);
+#pragma unroll
+                            for (int q = 0; q < kQ; q++)
+                                acc[q][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(fw), as_frag(bf[q]), acc[q][n], 0, 0, 0);
+                        }
+                        // keep the scheduler from hoisting the fragment loads of later k-steps
+                        // (they would all be live at once)
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    const float *lnp = sLN + (l + 1) * 32 * NT;
+                    if (a.debug && t == a.t0 && l == 0)  // raw G of the first block (debug region 3)
+                        for (int q = 0; q < kQ; q++) {
+                            const int64_t bd = base + 64 * wave + 16 * (kQ * pr + q) + col;
+                            if (bd < a.n)
+                                for (int n = 0; n < NT; n++)
+                                    for (int r = 0; r < 4; r++)
+                                        a.debug[(3 * a.n + bd) * (16 * NT) + 16 * n + 4 * g + r] = acc[q][n][r];
+                        }
+#pragma unroll
+                    for (int q = 0; q < kQ; q++) ln_epilogue<NT, true>(acc[q], act[q], lnp, lnp + 16 * NT, h, g, inv_n);
+                    if (a.debug && t == a.t0)
+                        for (int q = 0; q < kQ; q++)
+                            debug_act<NT>(a, l + 1, base + 64 * wave + 16 * (kQ * pr + q) + col, act[q], g);
+                }
+                // ---------------- heads: logits of board 16 g + col land in lane (g, col) -------
+#pragma unroll
+                for (int q = 0; q < kQ; q++) {
+                    const int bt = kQ * pr + q;
+#pragma unroll
+                    for (int ks = 0; ks < KS; ks++) {
+                        const uint4 bf = act_frag<NT>(act[q], ks);
+                        const uint4 hl = *reinterpret_cast<const uint4 *>(hdb + 64 * ks);
+                        const uint4 hv = *reinterpret_cast<const uint4 *>(hvb + 64 * ks);
+                        const bool mine_l = (col >> 2) == bt, mine_v = col == 4 * bt;
+                        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+                        accL = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(mine_l ? hl : z), as_frag(bf), accL, 0, 0, 0);
+                        accV = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(mine_v ? hv : z), as_frag(bf), accV, 0, 0, 0);
+                    }
+                }
+            }
+
+            float lg[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) lg[r] = accL[r] + a.ba[r];
+            const float val = accV[0] + a.bv[0];
+            if (a.debug && t == a.t0 && live) {
+                float *d = a.debug + 4 * a.n * (16 * NT) + 5 * i;
+                d[0] = lg[0], d[1] = lg[1], d[2] = lg[2], d[3] = lg[3], d[4] = val;
+            }
+
+            // ---------------- sample + env step (lane = board) ----------------------------------
+            const uint64_t cs = ctr0 + 2ull * (uint64_t)t;
+            const uint4 d = philox_draw(a.seed, cs, a.env_base + (uint32_t)i, 1u);
+            float lp[4], ent;
+            const uint32_t act_a = sample_row(lg, legal, d.x, lp, ent);
+            const StepResult res = step_board<G2048_RNG_PHILOX>(b, true, act_a, nullptr, rng, i, cs + 1ull, (uint32_t)a.opts);
+            legal = res.fl & 0xFu;
+            if (live) {
+                const int64_t o = (int64_t)t * a.n + i;
+                a.value[o] = val;
+                a.actions[o] = (uint8_t)act_a;
+                *reinterpret_cast<float4 *>(a.logp + 4 * o) = make_float4(lp[0], lp[1], lp[2], lp[3]);
+                a.entropy[o] = ent;
+                a.points[o] = (int32_t)res.pts;
+                a.max_tile[o] = (int8_t)res.mx;
+                a.pot[o] = res.pot;
+                a.boards[o + a.n] = b;
+                a.flags[o + a.n] = (uint8_t)res.fl;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t g2048_policy_rollout_lds_bytes(int32_t h) {
+    if (h <= 0 || h % 4 != 0) return 0;
+    const int nt = (h + 15) / 16;
+    const size_t b = (size_t)pr_lds_bytes(h, nt);
+    return b <= (size_t)kPrLdsMax ? b : 0;
+}
+
+int g2048_policy_rollout(g2048_stream_t stream, const g2048_policy_rollout_args *p) {
+    if (!p) return G2048_EINVAL;
+    const int h = p->hidden;
+    if (p->num_layers != 2 || h <= 0 || h % 4 != 0 || !g2048_policy_rollout_lds_bytes(h)) return G2048_EINVAL;
+    if (p->n < 0 || p->n >= (int64_t(1) << 31) || p->t0 < 0 || p->t1 < p->t0) return G2048_EINVAL;
+    if (p->n == 0 || p->t1 == p->t0) return G2048_OK;
+    if (!p->boards || !p->flags || !p->actions || !p->logp || !p->entropy || !p->value || !p->points || !p->max_tile ||
+        !p->pot || !p->w_stem || !p->w_block[0] || !p->w_block[1] || !p->head_bf16 || !p->head_bias_action ||
+        !p->head_bias_value)
+        return G2048_EINVAL;
+    for (int l = 0; l < 3; l++)
+        if (!p->ln_gamma[l] || !p->ln_beta[l]) return G2048_EINVAL;
+    if (((uintptr_t)p->boards & 15u) || ((uintptr_t)p->logp & 15u) || ((uintptr_t)p->pot & 3u) ||
+        ((uintptr_t)p->w_stem & 15u) || ((uintptr_t)p->w_block[0] & 7u) || ((uintptr_t)p->w_block[1] & 7u) ||
+        ((uintptr_t)p->head_bf16 & 15u))
+        return G2048_EINVAL;
+    if (p->opts & ~(uint32_t)(G2048_OPT_AUTO_RESET | G2048_OPT_SKIP_DONE)) return G2048_EINVAL;
+    PrArgs a{};
+    a.boards = (uint4 *)p->boards;
+    a.flags = p->flags;
+    a.actions = p->actions;
+    a.logp = p->logp;
+    a.entropy = p->entropy;
+    a.value = p->value;
+    a.points = p->points;
+    a.max_tile = p->max_tile;
+    a.pot = (uint32_t *)p->pot;
+    a.n = p->n;
+    a.t0 = (int32_t)p->t0;
+    a.t1 = (int32_t)p->t1;
+    a.h = h;
+    a.opts = (int32_t)p->opts;
+    a.w0 = (const uint16_t *)p->w_stem;
+    a.w1 = (const uint16_t *)p->w_block[0];
+    a.w2 = (const uint16_t *)p->w_block[1];
+    for (int l = 0; l < 3; l++) {
+        a.gamma[l] = p->ln_gamma[l];
+        a.beta[l] = p->ln_beta[l];
+    }
+    a.head = (const uint16_t *)p->head_bf16;
+    a.ba = p->head_bias_action;
+    a.bv = p->head_bias_value;
+    a.seed = p->seed;
+    a.counter_dev = p->counter_dev;
+    a.counter = p->counter;
+    a.env_base = p->env_base;
+    a.debug = p->debug;
+    const int nt = (h + 15) / 16;
+    const size_t lds = g2048_policy_rollout_lds_bytes(h);
+    const int64_t groups = (p->n + kPrThreads - 1) / kPrThreads;
+    const unsigned grid = (unsigned)(groups < 256 ? groups : 256);
+    hipStream_t s = (hipStream_t)stream;
+    if (nt == 13) hipLaunchKernelGGL((policy_rollout_kernel<13, 7>), dim3(grid), dim3(kPrThreads), lds, s, a);
+    else if (nt == 12) hipLaunchKernelGGL((policy_rollout_kernel<12, 6>), dim3(grid), dim3(kPrThreads), lds, s, a);
+    else if (nt == 4) hipLaunchKernelGGL((policy_rollout_kernel<4, 2>), dim3(grid), dim3(kPrThreads), lds, s, a);
+    else if (nt == 2) hipLaunchKernelGGL((policy_rollout_kernel<2, 1>), dim3(grid), dim3(kPrThreads), lds, s, a);
+    else return G2048_EINVAL;
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK : (int)e;
+}
+
+int g2048_policy_rollout_supported(int32_t hidden, int32_t num_layers) {
+    if (num_layers != 2 || !g2048_policy_rollout_lds_bytes(hidden)) return 0;
+    const int nt = (hidden + 15) / 16;
+    return nt == 13 || nt == 12 || nt == 4 || nt == 2;
+}
+
+}  // extern "C"

@@ -34,6 +34,7 @@ EXPORTED = (
     "g2048_wgrad_partials", "g2048_wgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
+    "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
 )
 
 
@@ -113,6 +114,18 @@ class AdamWGroup(ctypes.Structure):
                 ("pad_", ctypes.c_int32)]
 
 
+class PolicyRolloutArgs(ctypes.Structure):
+    """struct g2048_policy_rollout_args"""
+    vp = ctypes.c_void_p
+    _fields_ = [("boards", vp), ("flags", vp), ("actions", vp), ("logp", vp), ("entropy", vp), ("value", vp),
+                ("points", vp), ("max_tile", vp), ("pot", vp), ("n", ctypes.c_int64), ("t0", ctypes.c_int64),
+                ("t1", ctypes.c_int64), ("hidden", ctypes.c_int32), ("num_layers", ctypes.c_int32),
+                ("opts", ctypes.c_uint32), ("env_base", ctypes.c_uint32), ("w_stem", vp), ("w_block", vp * 2),
+                ("ln_gamma", vp * 3), ("ln_beta", vp * 3), ("head_bf16", vp), ("head_bias_action", vp),
+                ("head_bias_value", vp), ("seed", ctypes.c_uint64), ("counter", ctypes.c_uint64),
+                ("counter_dev", vp), ("debug", vp)]
+
+
 _lib = None
 
 
@@ -168,6 +181,9 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_mlp_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, i64, i32, i32, dp]),
         "g2048_head_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, vp, i64, vp]),
         "g2048_ppo_stats": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, ctypes.c_float, i64, vp, vp, vp]),
+        "g2048_policy_rollout_supported": (ctypes.c_int, [i32, i32]),
+        "g2048_policy_rollout_lds_bytes": (sz, [i32]),
+        "g2048_policy_rollout": (ctypes.c_int, [vp, ctypes.POINTER(PolicyRolloutArgs)]),
         "g2048_muon_supported": (ctypes.c_int, [i32, i32]),
         "g2048_muon_step": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.POINTER(MuonCfg)]),
         "g2048_adamw_step": (ctypes.c_int, [vp, ctypes.POINTER(AdamWGroup), i32, vp, vp, vp, ctypes.c_float,
@@ -504,6 +520,47 @@ def head_fwd(x, wa, ba, wv, bv, logits, value):
         _stream(x), _dev(x, torch.bfloat16, "x"), _dev(wa, torch.float32, "wa"), _dev(ba, torch.float32, "ba"),
         _dev(wv, torch.float32, "wv"), _dev(bv, torch.float32, "bv"), m, h, ctypes.c_void_p(logits.data_ptr()),
         logits.stride(0), _dev(value, torch.float32, "value")), "g2048_head_fwd")
+
+
+def policy_rollout_supported(hidden: int, num_layers: int) -> bool:
+    return bool(load().g2048_policy_rollout_supported(int(hidden), int(num_layers)))
+
+
+def policy_rollout(buf, t0: int, t1: int, w_stem, w_block, ln_gamma, ln_beta, head_bf16, ba, bv, seed: int,
+                   env_base: int, counter_dev, opts: int, counter: int = 0, debug=None):
+    """Steps t0 .. t1-1 of a rollout buffer (g2048/rollout.RolloutBuffers) in one fused launch:
+    GameMLP (bf16 weights w_stem [h,48], w_block[2] [h,h]; fp32 LayerNorm affines; bf16 heads
+    head_bf16 [5, 32*ceil(h/32)]) + sampler + env step, records bitwise the per-step path's."""
+    n = buf.boards.shape[1]
+    h = w_stem.shape[0]
+    T = buf.actions.shape[0]
+    if not (0 <= t0 <= t1 <= T) or len(w_block) != 2 or len(ln_gamma) != 3 or len(ln_beta) != 3:
+        raise G2048Error("policy_rollout: bad step range or layer count")
+    a = PolicyRolloutArgs()
+    a.boards = _dev(buf.boards, torch.int8, "boards")
+    a.flags = _dev(buf.flags, torch.uint8, "flags")
+    a.actions = _dev(buf.actions, torch.uint8, "actions")
+    a.logp = _dev(buf.logp, torch.float32, "logp")
+    a.entropy = _dev(buf.entropy, torch.float32, "entropy")
+    a.value = _dev(buf.value, torch.float32, "value")
+    a.points = _dev(buf.points, torch.int32, "points")
+    a.max_tile = _dev(buf.max_tile, torch.int8, "max_tile")
+    a.pot = _dev(buf.pot, torch.int8, "pot")
+    a.n, a.t0, a.t1, a.hidden, a.num_layers = n, t0, t1, h, len(w_block)
+    a.opts, a.env_base = opts, env_base
+    a.w_stem = _dev(w_stem, torch.bfloat16, "w_stem")
+    for i, w in enumerate(w_block):
+        a.w_block[i] = _dev(w, torch.bfloat16, "w_block")
+    for i in range(3):
+        a.ln_gamma[i] = _dev(ln_gamma[i], torch.float32, "ln_gamma")
+        a.ln_beta[i] = _dev(ln_beta[i], torch.float32, "ln_beta")
+    a.head_bf16 = _dev(head_bf16, torch.bfloat16, "head_bf16")
+    a.head_bias_action = _dev(ba, torch.float32, "ba")
+    a.head_bias_value = _dev(bv, torch.float32, "bv")
+    a.seed, a.counter = seed & (2**64 - 1), counter
+    a.counter_dev = _dev(counter_dev, torch.int64, "counter_dev")
+    a.debug = _dev(debug, torch.float32, "debug")
+    _check(load().g2048_policy_rollout(_stream(buf.boards), ctypes.byref(a)), "g2048_policy_rollout")
 
 
 def ppo_stats(sums, kl, grad_norm, beta_dev, critic: float, m: int, stats, counter=None, kl_rows: int = 0, rows=None):

@@ -57,6 +57,11 @@ class FusedPolicy:
         self.ln = [model.stem[1]] + [b.mlp[1] for b in model.backbone]
         self.heads = (model.action_head.weight, model.action_head.bias, model.value_head.weight, model.value_head.bias)
         self.wbf = [torch.empty_like(w, dtype=torch.bfloat16) for w in self.lin]
+        h = self.lin[0].shape[0]
+        # the fused rollout kernel (g2048_policy_rollout) reads the heads as one zero-padded bf16
+        # [5, 32 ceil(h/32)] block: action_head rows 0..3, value_head row 4
+        self.fused_rollout = L.policy_rollout_supported(h, len(self.lin) - 1)
+        self.head_bf = torch.zeros(5, 32 * ((h + 31) // 32), dtype=torch.bfloat16, device=self.lin[0].device)
         self._n = -1
         self.sync()
 
@@ -75,6 +80,16 @@ class FusedPolicy:
     def sync(self):
         for w, b in zip(self.lin, self.wbf):
             b.copy_(w)
+        h = self.lin[0].shape[0]
+        self.head_bf[:4, :h].copy_(self.heads[0])
+        self.head_bf[4, :h].copy_(self.heads[2][0])
+
+    def rollout_steps(self, ro, t0: int, t1: int):
+        """Steps t0 .. t1-1 of Rollout `ro` in ONE g2048_policy_rollout launch (bitwise the per-step
+        path: obs_encode + this policy + sample_actions + env_step per step)."""
+        L.policy_rollout(ro.buf, t0, t1, self.wbf[0], self.wbf[1:], [ln.weight for ln in self.ln],
+                         [ln.bias for ln in self.ln], self.head_bf, self.heads[1], self.heads[3], ro.seed,
+                         ro.env_base, ro.counter, ro.opts)
 
     def _buffers(self, n: int, dev):
         if self._n != n:
@@ -153,6 +168,7 @@ class Rollout:
         self.counter = torch.zeros(1, dtype=torch.int64, device=self.buf.device)
         self.opts = L.OPT_SKIP_DONE if episodic else L.OPT_AUTO_RESET
         self._graph = None
+        self.use_fused = True  # fused persistent policy rollout when the policy supports it
         # spawns: Philox by default; per-env CPython MT19937 streams when seeds are given, so game i
         # spawns exactly like the reference after random.seed(mt_seeds[i]) (train.py:227-228)
         self.mt_state = None
@@ -170,6 +186,19 @@ class Rollout:
         b = self.buf
         L.env_reset(b.boards[0], b.flags[0], self._spawn_rng(0))
         self.counter.add_(1)
+
+    def fused(self, policy) -> bool:
+        """Whether steps run in the fused persistent kernel (FusedPolicy of a 2-block GameMLP whose
+        weights fit LDS, Philox spawns) rather than one Rollout._step per step."""
+        return self.use_fused and self.mt_state is None and getattr(policy, "fused_rollout", False)
+
+    def steps(self, t0: int, t1: int, policy):
+        """Steps t0 .. t1-1 (no counter bump): one fused launch, or the per-step path."""
+        if self.fused(policy):
+            policy.rollout_steps(self, t0, t1)
+        else:
+            for t in range(t0, t1):
+                self._step(t, policy)
 
     def _step(self, t: int, policy):
         b = self.buf
@@ -189,8 +218,7 @@ class Rollout:
                 self._graph = self._capture(policy)
             self._graph.replay()
         else:
-            for t in range(self.T):
-                self._step(t, policy)
+            self.steps(0, self.T, policy)
             self.counter.add_(2 * self.T)
         return self.buf
 
@@ -200,13 +228,11 @@ class Rollout:
         snap_b, snap_f, snap_c = self.buf.boards[0].clone(), self.buf.flags[0].clone(), self.counter.clone()
         snap_mt = self.mt_state.clone() if self.mt_state is not None else None
         with torch.cuda.stream(s):  # warm-up (allocator, library handles) outside the capture
-            for t in range(self.T):
-                self._step(t, policy)
+            self.steps(0, self.T, policy)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            for t in range(self.T):
-                self._step(t, policy)
+            self.steps(0, self.T, policy)
             self.counter.add_(2 * self.T)
         # capture does not execute: restore the pre-warm-up state so replay #1 is the first rollout
         self.buf.boards[0].copy_(snap_b)

@@ -162,8 +162,7 @@ class VecTrainer:
                     self._chunk_graphs[(c0, c1)] = g
                 g.replay()
             else:
-                for t in range(c0, c1):
-                    ro._step(t, self.policy)
+                ro.steps(c0, c1, self.policy)
             used = c1
             if bool(((b.flags[used] & L.FLAG_LEGAL) == 0).all()):  # every game is over
                 break
@@ -177,13 +176,11 @@ class VecTrainer:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            for t in range(c0, c1):
-                ro._step(t, self.policy)
+            ro.steps(c0, c1, self.policy)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            for t in range(c0, c1):
-                ro._step(t, self.policy)
+            ro.steps(c0, c1, self.policy)
         b.boards[c0].copy_(snap[0])
         b.flags[c0].copy_(snap[1])
         return g

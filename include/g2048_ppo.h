@@ -70,6 +70,50 @@ int g2048_mlp_fwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, c
 int g2048_head_fwd(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, const float *wv,
                    const float *bv, int64_t m, int32_t h, float *logits, int64_t logits_stride, float *value);
 
+/* The fused persistent policy rollout (play_game_for_episode's loop body, train.py:240-337, for
+ * every env at once; replaces one Rollout._step per step = g2048_obs_encode + FusedPolicy (three
+ * g2048_mlp_fwd + g2048_head_fwd) + g2048_sample_actions + g2048_env_step).  Steps t0 .. t1-1 of
+ * all n envs in ONE launch: boards / flags rows t0 are the start state, rows t0+1 .. t1 and the
+ * per-step records of rows t0 .. t1-1 are written exactly as the per-step path writes them -- the
+ * same time-major [T(+1)][n] layouts as g2048_env_step / g2048_sample_actions, the same Philox
+ * streams (action uniform: stream 1 at counter c + 2t; spawns: stream 0, resets: stream 2, at
+ * c + 2t + 1; c = counter + *counter_dev) and the same arithmetic (bitwise equal records).
+ * GameMLP eval mode with num_layers == 2 and hidden % 4 == 0 whose two h x h block weights fit
+ * LDS (g2048_policy_rollout_supported; h = 196 and 192 do).  Weights: the bf16 copies
+ * FusedPolicy keeps (w_stem [h][48], w_block[l] [h][h], 8-byte aligned, stem 16-byte), the fp32
+ * LayerNorm affines, the heads as bf16 head_bf16 [5][32 ceil(h / 32)] (action_head rows 0..3,
+ * value_head row 4, zero padded, 16-byte aligned) and the fp32 biases.  opts: G2048_OPT_AUTO_RESET
+ * (fixed horizon) or G2048_OPT_SKIP_DONE (episodic).  Philox spawns only. */
+typedef struct g2048_policy_rollout_args {
+    int8_t *boards;          /* [T+1][n][16] */
+    uint8_t *flags;          /* [T+1][n] legal mask | done / reset / invalid / inactive bits */
+    uint8_t *actions;        /* [T][n] */
+    float *logp;             /* [T][n][4] log_softmax of the masked logits (-inf where illegal) */
+    float *entropy;          /* [T][n] */
+    float *value;            /* [T][n] */
+    int32_t *points;         /* [T][n] */
+    int8_t *max_tile;        /* [T][n] */
+    int8_t *pot;             /* [T][n][4] mono_b, mono_a, empt_b, empt_a */
+    int64_t n, t0, t1;
+    int32_t hidden, num_layers;
+    uint32_t opts, env_base;
+    const void *w_stem;
+    const void *w_block[2];
+    const float *ln_gamma[3], *ln_beta[3];
+    const void *head_bf16;
+    const float *head_bias_action, *head_bias_value;
+    uint64_t seed, counter;
+    const uint64_t *counter_dev; /* optional device counter base */
+    float *debug;            /* optional test hook (NULL): step t0's layer outputs [3][n][16 ceil(h/16)]
+                                followed by its head outputs [n][5] (4 logits, value) */
+} g2048_policy_rollout_args;
+
+/* 1 when g2048_policy_rollout handles a GameMLP of this shape. */
+int g2048_policy_rollout_supported(int32_t hidden, int32_t num_layers);
+/* Dynamic LDS bytes the rollout kernel uses for hidden size h (0 = does not fit). */
+size_t g2048_policy_rollout_lds_bytes(int32_t h);
+int g2048_policy_rollout(g2048_stream_t stream, const g2048_policy_rollout_args *args);
+
 /* Scratch floats of g2048_ln_act_bwd for (m, h). */
 size_t g2048_ln_act_bwd_partials(int64_t m, int32_t h);
 
