@@ -1,0 +1,77 @@
+// ln_row.hpp -- the LayerNorm + ReLU row epilogue of a GameMLP layer (game.py:1033-1046, stem
+// :1145-1150) in the MFMA output layout "lane (g, c) holds features 16 n + 4 g + r of its row",
+// shared by mlp_fwd_kernel (ppo_update.hip: the update's forward and the per-step rollout policy)
+// and policy_rollout_kernel (the fused rollout).  Every floating-point operation is written out
+// (explicit fmas, fixed summation order, packed fp32 only where it is per element the same
+// operation), so both kernels compute bitwise the same activations whatever the contraction flags
+// of their translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace g2048 {
+namespace lnrow {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+constexpr float kEps = 1e-5f;  // nn.LayerNorm default
+
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {  // RNE (v_cvt_pk_bf16_f32)
+    const bf16x2 v = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+
+// G = bf16(acc) as the layer stores it: gbits (packed bf16) and v (the same values as fp32 pairs)
+template <int NT>
+__device__ __forceinline__ void round_g(const f32x4 (&acc)[NT], f32x2 (&v)[NT][2], uint2 (&gbits)[NT]) {
+#pragma unroll
+    for (int n = 0; n < NT; n++) {
+        const uint32_t w0 = pack_bf2(acc[n][0], acc[n][1]), w1 = pack_bf2(acc[n][2], acc[n][3]);
+        gbits[n] = make_uint2(w0, w1);
+        v[n][0] = f32x2{bf_lo(w0), bf_hi(w0)};
+        v[n][1] = f32x2{bf_lo(w1), bf_hi(w1)};
+    }
+}
+
+// Row statistics over the valid features (valid(n): tile n's 4-group of this lane is < h): the sum
+// in tile order then the xor-16 / xor-32 lane sums; v becomes dv = v - sum/h (one fma); the
+// variance of dv likewise; rstd = 1 / sqrt(var/h + eps).  Returns the mean (sum/h) and rstd.
+template <int NT, class Valid>
+__device__ __forceinline__ void stats(f32x2 (&v)[NT][2], Valid valid, float inv_n, float &mean, float &rstd) {
+    float sum = 0.0f;
+#pragma unroll
+    for (int n = 0; n < NT; n++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) sum += valid(n) ? v[n][r >> 1][r & 1] : 0.0f;
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    const f32x2 nsum = {-sum, -sum}, invn = {inv_n, inv_n};
+    float var = 0.0f;
+#pragma unroll
+    for (int n = 0; n < NT; n++) {
+        v[n][0] = __builtin_elementwise_fma(nsum, invn, v[n][0]);
+        v[n][1] = __builtin_elementwise_fma(nsum, invn, v[n][1]);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const float dv = valid(n) ? v[n][r >> 1][r & 1] : 0.0f;
+            var = __builtin_fmaf(dv, dv, var);
+        }
+    }
+    var += __shfl_xor(var, 16);
+    var += __shfl_xor(var, 32);
+    mean = sum * inv_n;
+    rstd = 1.0f / sqrtf(__builtin_fmaf(var, inv_n, kEps));
+}
+
+// ReLU(LayerNorm) of a feature pair: max(fma(dv * rstd, gamma, beta), 0)
+__device__ __forceinline__ f32x2 affine_relu(f32x2 dv, float rstd, f32x2 gamma, f32x2 beta) {
+    const f32x2 y = __builtin_elementwise_fma(dv * f32x2{rstd, rstd}, gamma, beta);
+    return f32x2{fmaxf(y.x, 0.0f), fmaxf(y.y, 0.0f)};
+}
+
+}  // namespace lnrow
+}  // namespace g2048

@@ -31,6 +31,7 @@
 
 #include "board.hpp"
 #include "step.hpp"
+#include "ln_row.hpp"
 #include "../../include/g2048.h"
 #include "../../include/g2048_ppo.h"
 
@@ -41,6 +42,7 @@ namespace {
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr float kLnEps = 1e-5f;
 constexpr int kPrThreads = 256;
@@ -51,7 +53,62 @@ constexpr int kMaxLayers = 3;  // stem + 2 residual blocks (GameMLP num_layers =
 #endif
 constexpr int kQ = PR_TILES;  // board tiles (of 16 boards) per MLP pass: accumulators of kQ x NT tiles
 
-__constant__ float kThirdsPr[4] = {0.0f, 1.0f / 3.0f, 2.0f / 3.0f, 1.0f};
+// ---------------------------------------------------------------- stem fragment table -------
+// The stem's B fragment of k-step ks for lane group g holds obs features k = 32 ks + 8 g + j
+// (to_model_format order: [exponent, row/3, col/3] per cell).  Per (g, ks): the position features
+// as bf16 constants (exponent slots zero), the up to three exponent cells c0 .. c0+2 (inside board
+// dwords d, d+1; `xsel` gathers their bytes), and per fragment dword a v_perm selector merging the
+// exponents (bf16) into the constants.
+struct StemFrag {
+    uint32_t c[4], sel[4], xsel, d, pad_[2];
+};
+struct StemTable {
+    StemFrag f[4][2];
+    static constexpr uint32_t bf16_rne(float x) {
+        const uint32_t u = __builtin_bit_cast(uint32_t, x);
+        return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+    }
+    constexpr StemTable() : f{} {
+        constexpr float thirds[4] = {0.0f, 1.0f / 3.0f, 2.0f / 3.0f, 1.0f};
+        for (int g = 0; g < 4; g++)
+            for (int ks = 0; ks < 2; ks++) {
+                StemFrag &e = f[g][ks];
+                int c0 = -1, slot[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+                uint32_t val[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                for (int j = 0; j < 8; j++) {
+                    const int k = 32 * ks + 8 * g + j, cell = k / 3, kind = k % 3;
+                    if (k >= 48) continue;
+                    if (kind == 0) {
+                        if (c0 < 0) c0 = cell;
+                        slot[j] = cell - c0;  // exponent number 0..2
+                    } else {
+                        val[j] = bf16_rne(thirds[kind == 1 ? (cell >> 2) : (cell & 3)]);
+                    }
+                }
+                const int cc = c0 < 0 ? 0 : c0;
+                const int d = (cc >> 2) < 3 ? (cc >> 2) : 2;
+                e.d = (uint32_t)d;
+                e.xsel = 0x0C0C0C0Cu;
+                for (int s = 0; s < 3; s++) {
+                    const int byte = cc + s - 4 * d;
+                    if (byte < 8) e.xsel = (e.xsel & ~(0xFFu << (8 * s))) | ((uint32_t)byte << (8 * s));
+                }
+                for (int w = 0; w < 4; w++) {
+                    e.c[w] = val[2 * w] | (val[2 * w + 1] << 16);
+                    uint32_t sel = 0;
+                    for (int p = 0; p < 2; p++) {
+                        const int j = 2 * w + p, sl = slot[j];
+                        // exponent s: bf16 in E01 (s = 0: bytes 0,1; s = 1: bytes 2,3) or E2 (bytes
+                        // 0,1) = the v_perm high source (selector 4..7); a constant: bytes of c[w]
+                        const uint32_t b0 = sl < 0 ? (uint32_t)(2 * p) : (uint32_t)(4 + 2 * (sl == 1));
+                        sel |= (b0 | ((b0 + 1u) << 8)) << (16 * p);
+                    }
+                    e.sel[w] = sel;
+                }
+            }
+    }
+};
+__constant__ const StemTable kStem = StemTable();
 
 __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
     const bf16x2_t v = {(__bf16)a, (__bf16)b};
@@ -116,56 +173,28 @@ __device__ __forceinline__ void debug_act(const PrArgs &a, int l, int64_t board,
 // LayerNorm statistics in the same order (features in tile order, then the xor-16 and xor-32 lane
 // sums), Y = [X +] ReLU(LN(G)) rounded to bf16.  act[n] holds the layer input (residual) on entry
 // and the output on exit; features >= h are zero.
-template <int NT, bool RES>
+template <int NT, int h, bool RES>
 __device__ __forceinline__ void ln_epilogue(f32x4_t (&acc)[NT], uint2 (&act)[NT], const float *sgam, const float *sbet,
-                                            int h, int g, float inv_n) {
-    // this file is built -ffp-contract=off (the sampler and env step must round like g2048.hip);
-    // mlp_fwd_kernel is built with contraction, so its epilogue contracts here too
-#pragma clang fp contract(fast)
-    float sum = 0.0f;
-#pragma unroll
-    for (int n = 0; n < NT; n++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const float v = (float)(__bf16)acc[n][r];
-            acc[n][r] = v;
-            sum += 16 * n + 4 * g < h ? v : 0.0f;
-        }
-    sum += __shfl_xor(sum, 16);
-    sum += __shfl_xor(sum, 32);
-    const float mean = sum * inv_n;
-    float var = 0.0f;
-#pragma unroll
-    for (int n = 0; n < NT; n++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const float dv = 16 * n + 4 * g < h ? acc[n][r] - mean : 0.0f;
-            var += dv * dv;
-        }
-    var += __shfl_xor(var, 16);
-    var += __shfl_xor(var, 32);
-    const float rstd = 1.0f / sqrtf(var * inv_n + kLnEps);
+                                            int g, float inv_n) {
+    namespace R = lnrow;
+    R::f32x2 v[NT][2];
+    uint2 gb[NT];
+    R::round_g<NT>(acc, v, gb);
+    auto valid = [&](int n) { return 16 * n + 4 * g < h; };  // folds to true except in the last tile
+    float mean, rstd;
+    R::stats<NT>(v, valid, inv_n, mean, rstd);
 #pragma unroll
     for (int n = 0; n < NT; n++) {
         const int f0 = 16 * n + 4 * g;
         const float4 ga = *reinterpret_cast<const float4 *>(sgam + f0);
         const float4 be = *reinterpret_cast<const float4 *>(sbet + f0);
-        const float gg[4] = {ga.x, ga.y, ga.z, ga.w}, bb[4] = {be.x, be.y, be.z, be.w};
-        float rs[4] = {0.0f, 0.0f, 0.0f, 0.0f}, o[4];
-        if (RES) {
-            rs[0] = bf_lo(act[n].x);
-            rs[1] = bf_hi(act[n].x);
-            rs[2] = bf_lo(act[n].y);
-            rs[3] = bf_hi(act[n].y);
+        R::f32x2 y0 = R::affine_relu(v[n][0], rstd, R::f32x2{ga.x, ga.y}, R::f32x2{be.x, be.y});
+        R::f32x2 y1 = R::affine_relu(v[n][1], rstd, R::f32x2{ga.z, ga.w}, R::f32x2{be.z, be.w});
+        if (RES) {  // Y = X + ..., the residual being this layer's input
+            y0 = R::f32x2{bf_lo(act[n].x), bf_hi(act[n].x)} + y0;
+            y1 = R::f32x2{bf_lo(act[n].y), bf_hi(act[n].y)} + y1;
         }
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const float a = fmaxf((acc[n][r] - mean) * rstd * gg[r] + bb[r], 0.0f);
-            o[r] = RES ? rs[r] + a : a;
-        }
-        const bool ok = f0 < h;
-        act[n] = ok ? make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3])) : make_uint2(0u, 0u);
-        if (n & 1) __builtin_amdgcn_sched_barrier(0);  // bound the affine loads in flight
+        act[n] = valid(n) ? make_uint2(pack_bf2(y0.x, y0.y), pack_bf2(y1.x, y1.y)) : make_uint2(0u, 0u);
     }
 }
 
@@ -223,11 +252,13 @@ __device__ __forceinline__ uint32_t sample_row(const float (&l)[4], uint32_t leg
     return act;
 }
 
-template <int NT, int KS>
+// H = the hidden size (compile time: every feature-validity test of the last tile folds away).
+template <int H>
 __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a) {
+    constexpr int NT = (H + 15) / 16, KS = ((H + 7) / 8 * 8 + 31) / 32;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int h = a.h;
-    const int P = pr_pitch(h), WB = pr_wbytes(h);
+    constexpr int h = H;
+    constexpr int P = pr_pitch(h), WB = pr_wbytes(h);
     char *sW[2] = {smem, smem + WB};  // block weight images (LDS offsets 0 and WB)
     float *sLN = reinterpret_cast<float *>(smem + 2 * WB);  // [layer][gamma | beta][16 NT]
     char *sZero = smem + 2 * WB + 2 * kMaxLayers * pr_ln_floats(NT) * 4;
@@ -253,44 +284,27 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
     }
     __syncthreads();
 
-    const float inv_n = 1.0f / (float)h;
-    const int hp8 = (h + 7) & ~7;
-    const int KP = 32 * KS;  // padded row length of the head buffer
+    constexpr float inv_n = 1.0f / (float)h;
+    constexpr int hp8 = (h + 7) & ~7;
+    constexpr int KP = 32 * KS;  // padded row length of the head buffer
     const uint64_t ctr0 = a.counter + (a.counter_dev ? *a.counter_dev : 0ull);
     RngArgs rng{a.seed, 0ull, nullptr, a.env_base, nullptr, nullptr};
 
-    // per-lane constants of the stem fragments (obs features k = 32 ks + 8 g + j, cell k/3, kind k%3)
-    float xc[2][8];
-    uint32_t xmask[2], xsel[2], xpair[2];
+    // this lane group's stem fragment recipe (kStem)
+    uint4 sc[2], ss[2];
+    uint32_t sx[2], sd[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ks++) {
-        xmask[ks] = 0u;
-        int first = -1;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int k = 32 * ks + 8 * g + j, cell = k / 3, kind = k - 3 * cell;
-            const bool in = k < 48;
-            xc[ks][j] = (!in || kind == 0) ? 0.0f : kThirdsPr[kind == 1 ? (cell >> 2) : (cell & 3)];
-            if (in && kind == 0) {
-                xmask[ks] |= 1u << j;
-                if (first < 0) first = cell;
-            }
-        }
-        // the (up to 3) exponent cells first, first+1, first+2 lie in board dwords d, d + 1
-        const int c0 = first < 0 ? 0 : first, d = (c0 >> 2) < 3 ? (c0 >> 2) : 2;
-        xpair[ks] = (uint32_t)d;
-        uint32_t sel = 0x0C0C0C0Cu;  // v_perm: bytes 0..2 = cells c0, c0+1, c0+2 of {dword d+1, dword d}
-#pragma unroll
-        for (int s = 0; s < 3; s++) {
-            const int byte = c0 + s - 4 * d;  // 0..7 within the pair (low dword = bytes 0..3)
-            if (byte < 8) sel = (sel & ~(0xFFu << (8 * s))) | ((uint32_t)byte << (8 * s));
-        }
-        xsel[ks] = sel;
+        const StemFrag &e = kStem.f[g][ks];
+        sc[ks] = make_uint4(e.c[0], e.c[1], e.c[2], e.c[3]);
+        ss[ks] = make_uint4(e.sel[0], e.sel[1], e.sel[2], e.sel[3]);
+        sx[ks] = e.xsel;
+        sd[ks] = e.d;
     }
     // A-fragment LDS offsets of the block weights: row 16 n + col, k = 32 ks + 8 g (+ 16 n P per tile)
     const int wlane = col * P + pr_shift(h, col) + 16 * g;
     const int zoff = (int)(sZero - smem);
-    const int last_rows = h - 16 * (NT - 1);  // valid rows of the last tile
+    constexpr int last_rows = h - 16 * (NT - 1);  // valid rows of the last tile
 
     for (int64_t base = (int64_t)blockIdx.x * kPrThreads; base < a.n; base += (int64_t)gridDim.x * kPrThreads) {
         if (base + 64 * wave >= a.n) continue;  // an empty wave (no barrier below)
@@ -323,16 +337,16 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
                                    B3 = __shfl(b.w, src);
 #pragma unroll
                     for (int ks = 0; ks < 2; ks++) {
-                        const uint32_t d = xpair[ks];
+                        const uint32_t d = sd[ks];
                         const uint32_t lo = d == 0u ? B0 : d == 1u ? B1 : B2;
                         const uint32_t hi = d == 0u ? B1 : d == 1u ? B2 : B3;
-                        const uint32_t X = __builtin_amdgcn_perm(hi, lo, xsel[ks]);
-                        const float f[3] = {(float)(X & 0xFFu), (float)((X >> 8) & 0xFFu), (float)((X >> 16) & 0xFFu)};
-                        float e[8];
-#pragma unroll
-                        for (int j = 0; j < 8; j++) e[j] = ((xmask[ks] >> j) & 1u) ? f[j / 3] : xc[ks][j];
-                        xs[q][ks] = make_uint4(pack_bf2(e[0], e[1]), pack_bf2(e[2], e[3]), pack_bf2(e[4], e[5]),
-                                               pack_bf2(e[6], e[7]));
+                        const uint32_t X = __builtin_amdgcn_perm(hi, lo, sx[ks]);  // the exponents' bytes
+                        const uint32_t e01 = pack_bf2((float)(X & 0xFFu), (float)((X >> 8) & 0xFFu));
+                        const uint32_t e2 = pack_bf2((float)((X >> 16) & 0xFFu), 0.0f);
+                        xs[q][ks] = make_uint4(__builtin_amdgcn_perm(e01, sc[ks].x, ss[ks].x),
+                                               __builtin_amdgcn_perm(e01, sc[ks].y, ss[ks].y),
+                                               __builtin_amdgcn_perm(e01, sc[ks].z, ss[ks].z),
+                                               __builtin_amdgcn_perm(e2, sc[ks].w, ss[ks].w));
                     }
                 }
                 f32x4_t acc[kQ][NT];
@@ -354,7 +368,7 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
                     __builtin_amdgcn_sched_barrier(0);
                 }
 #pragma unroll
-                for (int q = 0; q < kQ; q++) ln_epilogue<NT, false>(acc[q], act[q], sLN, sLN + 16 * NT, h, g, inv_n);
+                for (int q = 0; q < kQ; q++) ln_epilogue<NT, H, false>(acc[q], act[q], sLN, sLN + 16 * NT, g, inv_n);
                 if (a.debug && t == a.t0)
                     for (int q = 0; q < kQ; q++) debug_act<NT>(a, 0, base + 64 * wave + 16 * (kQ * pr + q) + col, act[q], g);
 
@@ -388,16 +402,8 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
                         __builtin_amdgcn_sched_barrier(0);
                     }
                     const float *lnp = sLN + (l + 1) * 32 * NT;
-                    if (a.debug && t == a.t0 && l == 0)  // raw G of the first block (debug region 3)
-                        for (int q = 0; q < kQ; q++) {
-                            const int64_t bd = base + 64 * wave + 16 * (kQ * pr + q) + col;
-                            if (bd < a.n)
-                                for (int n = 0; n < NT; n++)
-                                    for (int r = 0; r < 4; r++)
-                                        a.debug[(3 * a.n + bd) * (16 * NT) + 16 * n + 4 * g + r] = acc[q][n][r];
-                        }
 #pragma unroll
-                    for (int q = 0; q < kQ; q++) ln_epilogue<NT, true>(acc[q], act[q], lnp, lnp + 16 * NT, h, g, inv_n);
+                    for (int q = 0; q < kQ; q++) ln_epilogue<NT, H, true>(acc[q], act[q], lnp, lnp + 16 * NT, g, inv_n);
                     if (a.debug && t == a.t0)
                         for (int q = 0; q < kQ; q++)
                             debug_act<NT>(a, l + 1, base + 64 * wave + 16 * (kQ * pr + q) + col, act[q], g);
@@ -514,19 +520,22 @@ int g2048_policy_rollout(g2048_stream_t stream, const g2048_policy_rollout_args 
     const int64_t groups = (p->n + kPrThreads - 1) / kPrThreads;
     const unsigned grid = (unsigned)(groups < 256 ? groups : 256);
     hipStream_t s = (hipStream_t)stream;
-    if (nt == 13) hipLaunchKernelGGL((policy_rollout_kernel<13, 7>), dim3(grid), dim3(kPrThreads), lds, s, a);
-    else if (nt == 12) hipLaunchKernelGGL((policy_rollout_kernel<12, 6>), dim3(grid), dim3(kPrThreads), lds, s, a);
-    else if (nt == 4) hipLaunchKernelGGL((policy_rollout_kernel<4, 2>), dim3(grid), dim3(kPrThreads), lds, s, a);
-    else if (nt == 2) hipLaunchKernelGGL((policy_rollout_kernel<2, 1>), dim3(grid), dim3(kPrThreads), lds, s, a);
-    else return G2048_EINVAL;
+    (void)nt;
+    switch (h) {
+    case 196: hipLaunchKernelGGL((policy_rollout_kernel<196>), dim3(grid), dim3(kPrThreads), lds, s, a); break;
+    case 192: hipLaunchKernelGGL((policy_rollout_kernel<192>), dim3(grid), dim3(kPrThreads), lds, s, a); break;
+    case 128: hipLaunchKernelGGL((policy_rollout_kernel<128>), dim3(grid), dim3(kPrThreads), lds, s, a); break;
+    case 64: hipLaunchKernelGGL((policy_rollout_kernel<64>), dim3(grid), dim3(kPrThreads), lds, s, a); break;
+    case 32: hipLaunchKernelGGL((policy_rollout_kernel<32>), dim3(grid), dim3(kPrThreads), lds, s, a); break;
+    default: return G2048_EINVAL;
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK : (int)e;
 }
 
 int g2048_policy_rollout_supported(int32_t hidden, int32_t num_layers) {
     if (num_layers != 2 || !g2048_policy_rollout_lds_bytes(hidden)) return 0;
-    const int nt = (hidden + 15) / 16;
-    return nt == 13 || nt == 12 || nt == 4 || nt == 2;
+    return hidden == 196 || hidden == 192 || hidden == 128 || hidden == 64 || hidden == 32;
 }
 
 }  // extern "C"

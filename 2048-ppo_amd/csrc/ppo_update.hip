@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "board.hpp"
+#include "ln_row.hpp"
 #include "../../include/g2048_ppo.h"
 
 using g2048::philox;
@@ -1116,31 +1117,15 @@ __global__ __launch_bounds__(kMfThreads) void mlp_fwd_kernel(const uint16_t *__r
                 acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw, fx, acc[n], 0, 0, 0);
             }
         }
-        // epilogue: lane holds row m = slab*64 + 16*wave + col, features 16n + 4g + r
+        // epilogue: lane holds row m = slab*64 + 16*wave + col, features 16n + 4g + r.  The
+        // LayerNorm arithmetic is ln_row.hpp's (shared bitwise with the fused rollout kernel).
+        namespace R = g2048::lnrow;
         const int64_t m = slab * kMfRows + wave * 16 + col;
-        float sum = 0.0f;
-#pragma unroll
-        for (int n = 0; n < NT; n++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const float v = (float)(__bf16)acc[n][r];  // G as stored (bf16)
-                acc[n][r] = v;
-                sum += 16 * n + 4 * g < N ? v : 0.0f;
-            }
-        sum += __shfl_xor(sum, 16);
-        sum += __shfl_xor(sum, 32);
-        const float mean = sum * inv_n;
-        float var = 0.0f;
-#pragma unroll
-        for (int n = 0; n < NT; n++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const float dv = 16 * n + 4 * g < N ? acc[n][r] - mean : 0.0f;
-                var += dv * dv;
-            }
-        var += __shfl_xor(var, 16);
-        var += __shfl_xor(var, 32);
-        const float rstd = 1.0f / sqrtf(var * inv_n + kLnEps);
+        R::f32x2 v[NT][2];
+        uint2 gb[NT];
+        R::round_g<NT>(acc, v, gb);
+        float mean, rstd;
+        R::stats<NT>(v, [&](int n) { return 16 * n + 4 * g < N; }, inv_n, mean, rstd);
         if (m < M) {
             if (g == 0 && mean_out) {
                 mean_out[m] = mean;
@@ -1153,27 +1138,22 @@ __global__ __launch_bounds__(kMfThreads) void mlp_fwd_kernel(const uint16_t *__r
                 if (f0 >= N) continue;
                 const float4 ga = *reinterpret_cast<const float4 *>(sgb + f0);
                 const float4 be = *reinterpret_cast<const float4 *>(sgb + N + f0);
-                const float gg[4] = {ga.x, ga.y, ga.z, ga.w}, bb[4] = {be.x, be.y, be.z, be.w};
-                float k[4], rs[4], o[4];
+                R::f32x2 y0 = R::affine_relu(v[n][0], rstd, R::f32x2{ga.x, ga.y}, R::f32x2{be.x, be.y});
+                R::f32x2 y1 = R::affine_relu(v[n][1], rstd, R::f32x2{ga.z, ga.w}, R::f32x2{be.z, be.w});
                 if (DROP) {  // tiles n, n+1 hold column groups 4n+g, 4n+4+g: one Philox call
+                    float k[4];
                     if ((n & 1) == 0) dpair = drop_draw4(d, (uint32_t)m, (uint32_t)(f0 >> 2));
                     drop_mult_bits(d, drop_half(dpair, (uint32_t)(f0 >> 2)), k);
+                    y0 = y0 * R::f32x2{k[0], k[1]};
+                    y1 = y1 * R::f32x2{k[2], k[3]};
                 }
                 if (RES) {  // the residual is this layer's input, already in LDS
                     const uint2 w = *reinterpret_cast<const uint2 *>(xrow + 2 * f0);
-                    rs[0] = bf2f(w.x & 0xFFFFu);
-                    rs[1] = bf2f(w.x >> 16);
-                    rs[2] = bf2f(w.y & 0xFFFFu);
-                    rs[3] = bf2f(w.y >> 16);
+                    y0 = R::f32x2{R::bf_lo(w.x), R::bf_hi(w.x)} + y0;
+                    y1 = R::f32x2{R::bf_lo(w.y), R::bf_hi(w.y)} + y1;
                 }
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    float a = fmaxf((acc[n][r] - mean) * rstd * gg[r] + bb[r], 0.0f);
-                    if (DROP) a *= k[r];
-                    o[r] = RES ? rs[r] + a : a;
-                }
-                if (G) store_bf4(G + m * N + f0, acc[n]);
-                store_bf4(Y + m * N + f0, o);
+                if (G) *reinterpret_cast<uint2 *>(G + m * N + f0) = gb[n];
+                *reinterpret_cast<uint2 *>(Y + m * N + f0) = make_uint2(R::pack_bf2(y0.x, y0.y), R::pack_bf2(y1.x, y1.y));
             }
         }
         if (more) store(sX0 + (cur ^ 1) * xbytes);  // the other buffer: last read one slab ago
