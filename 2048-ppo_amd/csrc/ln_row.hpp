@@ -25,6 +25,19 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {  // RNE (v_cvt_
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
 
+// x + (x of the lane 16 / 32 away), i.e. the butterfly steps of __shfl_xor(x, 16) / (x, 32), on the
+// VALU cross-lane swaps instead of an LDS round trip (fp add is commutative: same bits)
+__device__ __forceinline__ float xor16_add(float x) {
+    const uint32_t u = __float_as_uint(x);
+    const auto s = __builtin_amdgcn_permlane16_swap(u, u, false, false);  // rows {0,0,2,2} / {1,1,3,3}
+    return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+__device__ __forceinline__ float xor32_add(float x) {
+    const uint32_t u = __float_as_uint(x);
+    const auto s = __builtin_amdgcn_permlane32_swap(u, u, false, false);  // rows {0,1,0,1} / {2,3,2,3}
+    return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+
 // G = bf16(acc) as the layer stores it: gbits (packed bf16) and v (the same values as fp32 pairs)
 template <int NT>
 __device__ __forceinline__ void round_g(const f32x4 (&acc)[NT], f32x2 (&v)[NT][2], uint2 (&gbits)[NT]) {
@@ -47,8 +60,7 @@ __device__ __forceinline__ void stats(f32x2 (&v)[NT][2], Valid valid, float inv_
     for (int n = 0; n < NT; n++)
 #pragma unroll
         for (int r = 0; r < 4; r++) sum += valid(n) ? v[n][r >> 1][r & 1] : 0.0f;
-    sum += __shfl_xor(sum, 16);
-    sum += __shfl_xor(sum, 32);
+    sum = xor32_add(xor16_add(sum));
     const f32x2 nsum = {-sum, -sum}, invn = {inv_n, inv_n};
     float var = 0.0f;
 #pragma unroll
@@ -61,8 +73,7 @@ __device__ __forceinline__ void stats(f32x2 (&v)[NT][2], Valid valid, float inv_
             var = __builtin_fmaf(dv, dv, var);
         }
     }
-    var += __shfl_xor(var, 16);
-    var += __shfl_xor(var, 32);
+    var = xor32_add(xor16_add(var));
     mean = sum * inv_n;
     rstd = 1.0f / sqrtf(__builtin_fmaf(var, inv_n, kEps));
 }
