@@ -13,8 +13,9 @@ Semantics chosen where the reference is silent (the module is missing, so this i
   * spawns: Philox4x32-10 keyed from Python's `random` module state, so `random.seed(s)` makes a
     batch reproducible; action sampling: the device sampler (torch.multinomial's stream is not
     reproducible across implementations in any case).
-  * info-only heuristic deltas (smoothness/corner/adjacency/chain/topological) are reported as 0.0:
-    they never reach the reward (train.py:702-719).
+  * info-only heuristic deltas (smoothness/corner/adjacency/chain/topological, game.py:981-1002)
+    come from the g2048_info_deltas kernel, bit-identical to game.step's; they never reach the
+    reward (train.py:702-719) but feed the breakdown tables and the --viz-dir export.
 """
 
 from __future__ import annotations

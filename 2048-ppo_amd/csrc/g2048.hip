@@ -455,6 +455,190 @@ __global__ __launch_bounds__(kBlock) void sample_kernel(const float *__restrict_
     if (entropy) entropy[i] = legal ? h : 0.0f;
 }
 
+// ---------------------------------------------------------------- info heuristics ----------
+// The info-only heuristics Game2048.step computes around every move (game.py:981-1002): smoothness
+// (:339-357), corner bonus (:359-399), adjacency bonus (:401-442), monotonic chain (:444-506, a DFS
+// with a visited set), topological score with the pre-move anchor corner (:610-668, :802-921),
+// before the move and after it (pre-spawn).  They never reach the reward (train.py:702-719) but
+// fill the EpisodeData records, the episode breakdown tables and the viz export.  float64 in the
+// reference's operation order (this file is built -ffp-contract=off): bit-identical deltas.
+namespace info {
+__device__ __forceinline__ int at(const int8_t *b, int i, int j) { return b[4 * i + j]; }
+__device__ __forceinline__ int bmax(const int8_t *b) {
+    int m = 0;
+    for (int p = 0; p < 16; p++) m = b[p] > m ? b[p] : m;
+    return m;
+}
+__device__ double smoothness(const int8_t *b) {
+    double s = 0.0;
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            const int x = at(b, i, j);
+            if (x == 0) continue;
+            if (j < 3 && at(b, i, j + 1) != 0) s -= abs(x - at(b, i, j + 1));
+            if (i < 3 && at(b, i + 1, j) != 0) s -= abs(x - at(b, i + 1, j));
+        }
+    return s;
+}
+__device__ double corner(const int8_t *b) {
+    const int m = bmax(b);
+    if (m == 0) return 0.0;
+    return (b[0] == m || b[3] == m || b[12] == m || b[15] == m) ? (double)m : -(double)m;
+}
+__device__ double adjacency(const int8_t *b) {
+    int m = 0, mi = 0, mj = 0;
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++)
+            if (at(b, i, j) > m) m = at(b, i, j), mi = i, mj = j;
+    double bonus = 0.0;
+    const int di[4] = {-1, 1, 0, 0}, dj[4] = {0, 0, -1, 1};
+    for (int d = 0; d < 4; d++) {
+        const int ni = mi + di[d], nj = mj + dj[d];
+        if (ni >= 0 && ni < 4 && nj >= 0 && nj < 4 && at(b, ni, nj) > 0) bonus += at(b, ni, nj) * 0.5;
+    }
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            const int x = at(b, i, j);
+            if (x < 5) continue;
+            if (j < 3 && at(b, i, j + 1) >= 5) bonus += (x + at(b, i, j + 1)) * 0.25;
+            if (i < 3 && at(b, i + 1, j) >= 5) bonus += (x + at(b, i + 1, j)) * 0.25;
+        }
+    return bonus;
+}
+// the best chain from cell p: cells of values m, m-1, m-2, ... along orthogonal steps without
+// revisiting, score = sum of the values; an explicit stack replaces the reference's recursion
+// (depth <= 18: the value drops by one per step and 0 matches only as the last cell)
+__device__ double chain_from(const int8_t *b, int p0, int m) {
+    int cell[20], dir[20];
+    uint32_t visited = 1u << p0;
+    double sum[20], best[20];
+    int depth = 0;
+    cell[0] = p0, dir[0] = 0, sum[0] = (double)m, best[0] = 0.0;
+    const int di[4] = {-1, 1, 0, 0}, dj[4] = {0, 0, -1, 1};
+    for (;;) {
+        if (dir[depth] < 4) {
+            const int d = dir[depth]++;
+            const int i = cell[depth] / 4 + di[d], j = cell[depth] % 4 + dj[d];
+            const int expected = m - 1 - depth;
+            if (i < 0 || i > 3 || j < 0 || j > 3) continue;
+            const int q = 4 * i + j;
+            if ((visited >> q) & 1u) continue;
+            if (b[q] != expected || depth + 1 >= 20) continue;
+            visited |= 1u << q;
+            depth++;
+            cell[depth] = q, dir[depth] = 0, sum[depth] = (double)expected, best[depth] = 0.0;
+        } else {  // all children tried: this node's chain = its value + the best child chain
+            const double c = sum[depth] + best[depth];
+            visited &= ~(1u << cell[depth]);
+            if (depth == 0) return c;
+            depth--;
+            if (c > best[depth]) best[depth] = c;
+        }
+    }
+}
+__device__ double chain(const int8_t *b) {
+    const int m = bmax(b);
+    if (m == 0) return 0.0;
+    double best = 0.0;
+    for (int p = 0; p < 16; p++)
+        if (b[p] == m) {
+            const double c = chain_from(b, p, m);
+            if (c > best) best = c;
+        }
+    return best;
+}
+__device__ int anchor(const int8_t *b) {  // the corner (packed 4 row + col) holding or nearest the max
+    const int corners[4] = {0, 3, 12, 15};
+    int m = 0, first = -1;
+    uint32_t maxpos = 0;
+    for (int p = 0; p < 16; p++) {
+        if (b[p] > m) m = b[p], maxpos = 1u << p, first = p;
+        else if (b[p] == m && m > 0) maxpos |= 1u << p;
+    }
+    if (first < 0) return 0;
+    for (int p = 0; p < 16; p++)
+        if ((maxpos >> p) & 1u)
+            for (int c = 0; c < 4; c++)
+                if (corners[c] == p) return p;
+    const int ti = first / 4, tj = first % 4;
+    int best = corners[0], bd = 1 << 30;
+    for (int c = 0; c < 4; c++) {
+        const int d = abs(corners[c] / 4 - ti) + abs(corners[c] % 4 - tj);
+        if (d < bd) bd = d, best = corners[c];
+    }
+    return best;
+}
+__device__ double topological(const int8_t *b, int corner_p) {
+    const int m = bmax(b);
+    if (m == 0) return 0.0;
+    int order[16], idx_of[16];
+    const int cr = corner_p / 4, cc = corner_p % 4, rd = cr == 0 ? 1 : -1, cd = cc == 0 ? 1 : -1;
+    for (int i = 0, k = 0; i < 4; i++)
+        for (int s = 0; s < 4; s++, k++) order[k] = 4 * (cr + i * rd) + ((i % 2 == 0) ? cc + s * cd : cc + (3 - s) * cd);
+    for (int k = 0; k < 16; k++) idx_of[order[k]] = k;
+    double score = 0.0;
+    for (int p = 0; p < 16; p++)
+        if (b[p] > 0) score += (double)((16 - idx_of[p]) * b[p]) * 0.1;
+    double prev = INFINITY, mono = 0.0, inv = 0.0;
+    for (int k = 0; k < 16; k++) {
+        const int v = b[order[k]];
+        if (v == 0) continue;
+        if ((double)v <= prev) mono += v * 0.2;
+        else inv += ((double)v - prev) * 0.5;
+        prev = (double)v;
+    }
+    score += mono - inv;
+    if (b[corner_p] == m) score += m * 2.0;
+    const int di[4] = {-1, 1, 0, 0}, dj[4] = {0, 0, -1, 1};
+    for (int p = 0; p < 16; p++) {
+        const int v = b[p];
+        if (v < 4) continue;
+        int lower = 0, tot = 0;
+        const int i = p / 4, j = p % 4;
+        for (int d = 0; d < 4; d++) {
+            const int ni = i + di[d], nj = j + dj[d];
+            if (ni >= 0 && ni < 4 && nj >= 0 && nj < 4 && at(b, ni, nj) > 0) {
+                tot++;
+                if (at(b, ni, nj) < v - 2) lower++;
+            }
+        }
+        if (tot >= 2 && lower >= tot - 1 && idx_of[p] > 4) score -= v * 1.0;
+    }
+    return score;
+}
+}  // namespace info
+
+// out[i] = {smoothness, corner, adjacency, chain, topological} deltas of action a[i] on board i
+// (zeros for an illegal action: game.py:959-978 returns no deltas), anchor[i] = the anchor corner.
+__global__ __launch_bounds__(kBlock) void info_kernel(const uint4 *__restrict__ boards, const uint8_t *__restrict__ acts,
+                                                      double *__restrict__ out, int8_t *__restrict__ anchor_out,
+                                                      int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint4 w = boards[i];
+    uint32_t pts, mx;
+    const uint4 mw = apply_move(w, acts[i] & 3u, pts, mx);
+    double d[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    int anc = 0;
+    if (!eq4(mw, w)) {
+        int8_t b[16], m[16];
+        const uint32_t bw[4] = {w.x, w.y, w.z, w.w}, mm[4] = {mw.x, mw.y, mw.z, mw.w};
+        for (int r = 0; r < 4; r++)
+            for (int c = 0; c < 4; c++) {
+                b[4 * r + c] = (int8_t)((bw[r] >> (8 * c)) & 0xFFu);
+                m[4 * r + c] = (int8_t)((mm[r] >> (8 * c)) & 0xFFu);
+            }
+        anc = info::anchor(b);
+        d[0] = info::smoothness(m) - info::smoothness(b);
+        d[1] = info::corner(m) - info::corner(b);
+        d[2] = info::adjacency(m) - info::adjacency(b);
+        d[3] = info::chain(m) - info::chain(b);
+        d[4] = info::topological(m, anc) - info::topological(b, anc);
+    }
+    for (int k = 0; k < 5; k++) out[5 * i + k] = d[k];
+    if (anchor_out) anchor_out[i] = (int8_t)anc;
+}
+
 // ---------------------------------------------------------------- reward / return-to-go ------
 struct RewardArgs {
     double gamma, wp, wm, we;
@@ -921,6 +1105,16 @@ int g2048_legal_mask(g2048_stream_t stream, const int8_t *boards, uint8_t *flags
     if (n == 0) return G2048_OK;
     hipLaunchKernelGGL(legal_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, (hipStream_t)stream, (const uint4 *)boards,
                        flags, n);
+    return launch_status();
+}
+
+int g2048_info_deltas(g2048_stream_t stream, const int8_t *boards, const uint8_t *actions, double *deltas,
+                      int8_t *anchor, int64_t n) {
+    if (n < 0) return G2048_EINVAL;
+    if (n == 0) return G2048_OK;
+    if (!boards || !actions || !deltas || !aligned16(boards)) return G2048_EINVAL;
+    hipLaunchKernelGGL(info_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, (hipStream_t)stream, (const uint4 *)boards,
+                       actions, deltas, anchor, n);
     return launch_status();
 }
 

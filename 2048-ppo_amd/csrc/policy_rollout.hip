@@ -44,7 +44,6 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-constexpr float kLnEps = 1e-5f;
 constexpr int kPrThreads = 256;
 constexpr int kPrLdsMax = 163840;
 constexpr int kMaxLayers = 3;  // stem + 2 residual blocks (GameMLP num_layers = 2)

@@ -25,7 +25,7 @@ RTG_STATE_DOUBLES = 8
 EXPORTED = (
     "g2048_mt_state_words", "g2048_mt_seed", "g2048_env_reset", "g2048_env_step", "g2048_env_rollout_random",
     "g2048_preview_points", "g2048_legal_mask",
-    "g2048_obs_encode", "g2048_sample_actions", "g2048_rtg_prepare", "g2048_reward_rtg_workspace_bytes",
+    "g2048_obs_encode", "g2048_info_deltas", "g2048_sample_actions", "g2048_rtg_prepare", "g2048_reward_rtg_workspace_bytes",
     "g2048_reward_rtg", "g2048_reward_rtg_ex", "g2048_rtg_finalize", "g2048_build_info", "g2048_episode_scan",
     "g2048_augment_workspace_bytes", "g2048_augment",
     # include/g2048_ppo.h
@@ -153,6 +153,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_preview_points": (ctypes.c_int, [vp, vp, vp, i64]),
         "g2048_legal_mask": (ctypes.c_int, [vp, vp, vp, i64]),
         "g2048_obs_encode": (ctypes.c_int, [vp, vp, vp, i32, i64]),
+        "g2048_info_deltas": (ctypes.c_int, [vp, vp, vp, vp, vp, i64]),
         "g2048_sample_actions": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp, i64, rp]),
         "g2048_rtg_prepare": (ctypes.c_int, [vp, vp, cp]),
         "g2048_reward_rtg_workspace_bytes": (sz, [i64]),
@@ -271,6 +272,15 @@ def obs_encode(boards, obs):
         raise G2048Error(f"obs dtype {obs.dtype} unsupported")
     _check(load().g2048_obs_encode(_stream(boards), _dev(boards, torch.int8, "boards"), _dev(obs, None, "obs"), dt,
                                    boards.shape[0]), "g2048_obs_encode")
+
+
+def info_deltas(boards, actions, deltas, anchor=None):
+    """boards int8 [n, 16], actions uint8 [n] -> deltas float64 [n, 5] (smoothness, corner, adjacency,
+    chain, topological after - before the move), anchor int8 [n] (optional)."""
+    n = boards.shape[0]
+    _check(load().g2048_info_deltas(_stream(boards), _dev(boards, torch.int8, "boards"),
+                                    _dev(actions, torch.uint8, "actions"), _dev(deltas, torch.float64, "deltas"),
+                                    _dev(anchor, torch.int8, "anchor"), n), "g2048_info_deltas")
 
 
 def sample_actions(logits, flags, actions, logp, entropy, rng: Rng):

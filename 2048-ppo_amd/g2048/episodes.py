@@ -97,6 +97,13 @@ def to_episode_data(ro: Rollout, T: int, n_moves: torch.Tensor, limit: int) -> l
     prev = torch.zeros(T, n, 4, dtype=torch.int32, device=b.device)
     for t in range(T):
         L.preview_points(b.boards[t], prev[t])
+    # the info-only heuristic deltas of every step (game.py:981-1002), on the device
+    info = torch.zeros(T * n, 5, dtype=torch.float64, device=b.device)
+    anchor = torch.zeros(T * n, dtype=torch.int8, device=b.device)
+    if T > 0:
+        L.info_deltas(b.boards[:T].reshape(T * n, 16), b.actions[:T].reshape(T * n), info, anchor)
+    info = info.view(T, n, 5).cpu().numpy()
+    anchor = anchor.view(T, n).cpu().numpy()
     obs = obs.cpu()
     prev = prev.cpu().numpy()
     sf = b.step_flags[:T].cpu().numpy()
@@ -133,8 +140,10 @@ def to_episode_data(ro: Rollout, T: int, n_moves: torch.Tensor, limit: int) -> l
                 "points_earned": int(pts[t, e]),
                 "points_possible": dict(zip(dirs, p4)),
                 "action_mask": [not (legal[t, e] >> a & 1) for a in range(4)],
-                "smoothness_delta": 0.0, "corner_delta": 0.0, "adjacency_delta": 0.0, "chain_delta": 0.0,
-                "topological_delta": 0.0,
+                "smoothness_delta": float(info[t, e, 0]), "corner_delta": float(info[t, e, 1]),
+                "adjacency_delta": float(info[t, e, 2]), "chain_delta": float(info[t, e, 3]),
+                "topological_delta": float(info[t, e, 4]),
+                "topological_anchor": (int(anchor[t, e]) // 4, int(anchor[t, e]) % 4),
                 "max_tile_created": int(mxt[t, e]),
                 "max_exponent_before": mexp_b,
                 "max_exponent_after": max(mexp_b, int(mxt[t, e])),

@@ -216,6 +216,7 @@ class VecTrainer:
             ro.collect(self.policy, graph=cfg.graph)
             T = ro.T
         self._mark("rollout_ms")
+        self._last_T = T
         sf = b.step_flags[:T]
         self.rtg.compute(b.points[:T], b.pot[:T], sf, b.value[:T], b.g_raw[:T], b.g_norm[:T], b.adv[:T])
         self._mark("rtg_ms")
@@ -359,6 +360,31 @@ class VecTrainer:
             "kl_average": kla, "kl_max": klm, "actor_lr": lrs[0], "critic_lr": lrs[1] if len(lrs) > 1 else lrs[0],
             "loss": loss, "episodes_finished": int(n_eps), "env_steps": int(n),
         }
+
+    # ------------------------------------------------------------------ reports ---------------
+    def best_episode(self) -> dict:
+        """EpisodeData of the env with the most points in the last rollout (the reference's "best game
+        this batch", train.py:1800): episodic mode = its whole game, fixed horizon = its window of
+        T steps.  Records carry the device info deltas, advantages and rewards of that env."""
+        from types import SimpleNamespace
+        from .episodes import to_episode_data
+        ro, b = self.rollout, self.rollout.buf
+        T = self._last_T
+        sf = b.step_flags[:T]
+        live = (sf & L.FLAG_INACTIVE) == 0
+        e = int(torch.where(live, b.points[:T], 0).sum(0).argmax())
+        col = lambda x, k: x[:k, e:e + 1].contiguous()  # noqa: E731
+        sub = SimpleNamespace(boards=col(b.boards, T + 1), flags=col(b.flags, T + 1), actions=col(b.actions, T),
+                              logp=col(b.logp, T), entropy=col(b.entropy, T), value=col(b.value, T),
+                              points=col(b.points, T), max_tile=col(b.max_tile, T), pot=col(b.pot, T),
+                              device=b.device)
+        sub.step_flags = sub.flags[1:]
+        n_moves = live[:, e].sum().reshape(1)
+        ep = to_episode_data(SimpleNamespace(buf=sub, n=1), T, n_moves, T)[0]
+        adv, ret = b.adv[:T, e].tolist(), b.g_norm[:T, e].tolist()
+        for k, m in enumerate(ep["moves"]):
+            m["advantage"], m["future_reward"] = adv[k], ret[k]
+        return ep
 
     # ------------------------------------------------------------------ evaluation ------------
     @torch.no_grad()

@@ -4,9 +4,9 @@
         --gamma 0.99 --entropy 0.02 --points 0.10 --mono 1.0 --critic 0.2 --rtg-beta 0.99 --episodes 65536 --gpu
 
 Every reference flag is accepted with the same default.  Flags that never reach the reference's
-reward (--smoothness --tile-bonus --corner --adjacency --chain --topo --win-bonus) and its dead
-flags (--epsilon --momentum --workers) are accepted and ignored, as in the reference
-(SURVEY.md §0.5).  New flags: --horizon (0 = one full game per env per train step, the reference's
+reward (--smoothness --tile-bonus --corner --adjacency --chain --topo --win-bonus) only weight the
+printed breakdown table and the --viz-dir export, as in the reference; its dead flags
+(--epsilon --momentum --workers) are accepted and ignored.  New flags: --horizon (0 = one full game per env per train step, the reference's
 semantics; T > 0 = fixed-horizon auto-reset throughput mode), --seed, --no-graph, --fp32.
 For several GPUs run it under `python -m torch.distributed.run --nproc-per-node N` (one rank per
 GPU; --episodes is per rank).
@@ -278,11 +278,29 @@ def train(
     logger.print(f"Creating GameMLP model (hidden={hidden_size}, layers={num_layers}); {num_episodes} envs/GPU x {ws}")
     tr = VecTrainer(cfg, device)
     best_eval = 0.0
+    highest = 0
     from tqdm import tqdm
+    from g2048 import report
+    weights = report.RewardWeights(points=points_weight, smoothness=smoothness_weight, max_tile=max_tile_weight,
+                                   corner=corner_weight, adjacency=adjacency_weight, chain=chain_weight,
+                                   monotonicity=monotonicity_weight, emptiness=emptiness_weight,
+                                   topological=topological_weight)
     it = tqdm(range(steps), desc="Running RL training", disable=rank != 0)
     for step in it:
         m = tr.train_step(step)
-        logger.log(m, step=step, verbose=(step % print_frequency == 0))
+        should_print = step % print_frequency == 0
+        logger.log(m, step=step, verbose=should_print)
+        new_high = m["peak_score"] > highest  # train.py:1754-1755
+        highest = max(highest, m["peak_score"])
+        if rank == 0 and (should_print or (new_high and viz_dir)):
+            best = tr.best_episode()  # train.py:1800-1837: tables, last steps, final state, viz export
+            if should_print:
+                report.print_episode_breakdown(logger, best, weights, gamma)
+                if show_last_steps > 0:
+                    report.print_last_steps(logger, best, show_last_steps)
+                report.print_final_state(logger, best)
+            if viz_dir:
+                report.export_episode_visualization(viz_dir, step, best, weights, gamma)
         if step > 0 and eval_freq and step % eval_freq == 0:
             ev = tr.evaluate(eval_games, max_steps)
             logger.log(ev, step=step)

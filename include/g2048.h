@@ -173,6 +173,16 @@ int g2048_reward_rtg_ex(g2048_stream_t stream, const int32_t *points, const int8
                         float *adv, double *reward, double *partials, void *workspace,
                         size_t workspace_bytes);
 
+/* The info-only heuristic deltas of Game2048.step (game.py:981-1002; smoothness :339-357, corner
+ * :359-399, adjacency :401-442, monotonic chain :444-506, topological with the pre-move anchor
+ * corner :610-668 / :802-921): for board i [n][16] and action i [n], deltas[5 i + k] = heuristic k
+ * after the move (pre-spawn) minus before, k = {smoothness, corner, adjacency, chain, topological}
+ * (all 0 for an illegal action, game.py:959-978), float64 bit-identical to the reference;
+ * anchor[i] (optional) = the anchor corner as 4 row + col.  They never reach the reward
+ * (train.py:702-719): the EpisodeData records, breakdown tables and viz export use them. */
+int g2048_info_deltas(g2048_stream_t stream, const int8_t *boards, const uint8_t *actions, double *deltas,
+                      int8_t *anchor, int64_t n);
+
 /* Episode statistics of a fixed-horizon rollout (compute_batch_stats' scores and tiles,
  * train.py:1040-1120): per env, the running score / max tile exponent of its current game is
  * carried across calls in run_score [n] / run_max [n]; scores[t][e] / tiles[t][e] are the finished

@@ -334,3 +334,41 @@ def test_large_n_invariants_and_determinism(dev):
     # env ids of the subsample differ from 0..len(sub)-1: only compare the deterministic parts
     assert np.array_equal(pts[sub.to(dev)].cpu().numpy(), f["points"])
     assert np.array_equal((fl[sub.to(dev)].cpu().numpy() >> 4) & 1, f["invalid"])
+
+
+def test_info_deltas_match_reference_games(dev):
+    """g2048_info_deltas (smoothness / corner / adjacency / chain / topological after - before the
+    move, game.py:981-1002) on the 8 200 golden transitions of the reference's seeded games:
+    bit-identical float64 deltas, zeros on the illegal actions."""
+    from g2048 import _lib as L
+    g = golden("games.npz")
+    b = torch.from_numpy(g["before"]).to(dev)
+    a = torch.from_numpy(g["action"].astype(np.uint8)).to(dev)
+    out = torch.zeros(len(b), 5, dtype=torch.float64, device=dev)
+    anc = torch.zeros(len(b), dtype=torch.int8, device=dev)
+    L.info_deltas(b, a, out, anc)
+    got = out.cpu().numpy()
+    for col, key in enumerate(("smooth_d", "corner_d", "adj_d", "chain_d", "topo_d")):
+        np.testing.assert_array_equal(got[:, col], g[key], err_msg=key)
+    assert (got[g["invalid"] == 1] == 0).all()
+    # anchors vs the C oracle's restatement of _choose_anchor_corner
+    _, want = O.info_heuristics(g["before"])
+    live = g["invalid"] == 0
+    np.testing.assert_array_equal(anc.cpu().numpy()[live], want[live])
+
+
+def test_info_deltas_high_tiles(dev):
+    """Boards with long chains and tiles up to 2^17 (deep DFS) vs the C oracle."""
+    from g2048 import _lib as L
+    rng = np.random.default_rng(5)
+    n = 20000
+    boards = rng.integers(0, 18, size=(n, 16)).astype(np.int8)
+    boards[rng.random((n, 16)) < 0.3] = 0
+    snake = np.array([17, 16, 15, 14, 10, 11, 12, 13, 9, 8, 7, 6, 2, 3, 4, 5], np.int8)
+    boards[:500] = snake
+    acts = rng.integers(0, 4, size=n).astype(np.uint8)
+    out = torch.zeros(n, 5, dtype=torch.float64, device=dev)
+    L.info_deltas(torch.from_numpy(boards).to(dev), torch.from_numpy(acts).to(dev), out)
+    _, f, info, _ = O.step(boards, acts.astype(np.int64), O.RNG_INJECT, inj_k=np.zeros(n, np.int32),
+                           inj_v=np.ones(n, np.int32), full_info=True)
+    np.testing.assert_array_equal(out.cpu().numpy(), np.where(f["invalid"][:, None] == 1, 0.0, info))
