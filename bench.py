@@ -264,21 +264,44 @@ def bench_single_step(n, steps, rank, dev, world):
 
 
 def cpu_baselines(seconds):
-    """CPU restatement of game.step (oracle/, incl. the 17 heuristic evaluations of game.py:981-1002),
-    random legal actions, auto-reset: (1) pure-Python loops like the reference, 1 core; (2) the C
-    oracle on all host cores.  Bounded by `seconds` each."""
+    """CPU restatements (oracle/, rank 0 only), each bounded by `seconds`: (1) game.step's pure-Python
+    restatement (incl. the 17 heuristic evaluations of game.py:981-1002), random legal actions,
+    auto-reset, 1 core; (2) the same loop on P processes (aggregate); (3) the README train loop
+    (oracle/pyloop.py), 1 process; (4) the C oracle on P cores.  (1)-(3) are also reported scaled to
+    the reference's own speed by the port/reference ratios measured in the build container
+    (profiles/<tag>/cpu_ref_ratio.json, tools/cpu_ref_ratio.py)."""
     out = {}
     try:
-        from oracle import oracle as O
-        from oracle import pyref
+        from oracle import oracle as O  # noqa: F401
+        from oracle import pyloop, pyref
     except Exception as e:  # pragma: no cover
         return {"error": f"oracle unavailable: {e}"}
-    # (1) pure-Python restatement, 1 core: the reference's own per-step cost structure
-    r = pyref.time_random_steps(seconds)
-    out["python_1core"] = r
-    # (2) C oracle, all cores (process pool over independent env shards)
     import multiprocessing as mp
     cores = min(len(os.sched_getaffinity(0)), 16)
+    ratio = json.loads(CPU_RATIO.read_text()) if CPU_RATIO.exists() else None
+    src = str(CPU_RATIO.relative_to(ROOT))
+
+    def scaled(d, leg):
+        if ratio:
+            r = ratio[leg]["port_over_reference"]
+            d.update(port_measured=d["value"], value=d["value"] / r, port_over_reference=r, ratio_source=src)
+        return d
+    # (1) pure-Python restatement, 1 core: the reference's own per-step cost structure
+    r = pyref.time_random_steps(seconds)
+    out["python_1core"] = scaled({"value": r["value"], "sample": r["sample"]}, "random_step")
+    # (2) the same loop on `cores` processes
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(cores) as pool:
+        parts = pool.map(_py_chunk, [(seconds, 0x2048 + i) for i in range(cores)])
+    dt = time.perf_counter() - t0
+    out["python_pool"] = scaled({"value": sum(p["steps"] for p in parts) / dt, "unit": "env-steps/s", "cores": cores,
+                                 "sample": f"{cores} procs x pure-Python random-legal loop, {dt:.1f} s wall"},
+                                "random_step")
+    # (3) README train loop (rollout + advantage + minibatch-4 Muon/AdamW update), 1 process
+    t = pyloop.time_train_loop(seconds)
+    out["train_loop_cpu"] = scaled({"value": t["value"], "unit": "env-steps/s", "cores": 1, "sample": t["sample"]},
+                                   "train_loop")
+    # (4) C oracle, all cores (process pool over independent env shards)
     n_envs, steps = 4096, 8
     t0 = time.perf_counter()
     _c_chunk((0, n_envs, steps))
@@ -293,6 +316,12 @@ def cpu_baselines(seconds):
     return out
 
 
+def _py_chunk(args):
+    from oracle import pyref
+    seconds, seed = args
+    return pyref.time_random_steps(seconds, seed)
+
+
 def _c_chunk(args):
     from oracle import oracle as O
     i, n, steps = args
@@ -302,6 +331,7 @@ def _c_chunk(args):
 
 
 PMC_PROFILE = ROOT / "profiles" / "r02a"
+CPU_RATIO = ROOT / "profiles" / "r02" / "cpu_ref_ratio.json"
 
 
 def rollout_counters():
@@ -417,8 +447,7 @@ def main():
         cb = cpu_baselines(args.cpu_seconds)
         py = cb.get("python_1core")
         if py:
-            result["cpu_baseline"] = {"value": py["value"], "unit": "env-steps/s", "cores": 1, "kind": "port",
-                                      "sample": py["sample"]}
+            result["cpu_baseline"] = dict(py, unit="env-steps/s", cores=1, kind="port")
         for k in ("c_oracle", "python_pool", "train_loop_cpu"):
             if k in cb:
                 result[f"cpu_baseline_{k}"] = cb[k]

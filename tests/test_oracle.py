@@ -250,3 +250,10 @@ def test_augment_plan_samples_distinct_rows():
     for a in (90, 180, 270):
         assert abs(angles.count(a) - n_r / 3) < 70
     assert O.augment_plan(5000, 1250, 0x2048, 4) != plan  # a new permutation per counter
+
+
+def test_readme_train_loop_restatement_runs():
+    """oracle/pyloop.py (bench's README train-loop CPU leg): one train step of one game."""
+    from oracle import pyloop
+    r = pyloop.time_train_loop(0.0, hidden=32, max_iters=1)
+    assert r["iters"] == 1 and r["steps"] > 0 and r["value"] > 0
