@@ -222,7 +222,14 @@ class GameURM(nn.Module):
         return list(ACTION_ORDER)
 
     def get_param_groups(self, value_lr: float, other_lr: float) -> list[dict]:
-        return _split_param_groups(self, value_lr, other_lr)
+        """The reference's GameURM has no parameter groups (its trainer refuses URM, train.py:1523-1532);
+        these follow GameMLP's split with Muon taking only the 2-D Linear weights: the depthwise conv
+        kernels [inter, 1, 2] and init_hidden [1, 16, h] (a direct parameter, not a child module) go
+        to the AdamW group with the norms and biases."""
+        o2, o1, v2, v1 = _split_param_groups(self, value_lr, other_lr)
+        o1["params"] = [p for p in o2["params"] if p.ndim != 2] + o1["params"] + [self.init_hidden]
+        o2["params"] = [p for p in o2["params"] if p.ndim == 2]
+        return [o2, o1, v2, v1]
 
     def _loop(self, h: torch.Tensor, emb: torch.Tensor) -> torch.Tensor:
         h = h + emb

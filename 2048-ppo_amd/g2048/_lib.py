@@ -35,6 +35,9 @@ EXPORTED = (
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
+    # include/g2048_urm.h
+    "g2048_urm_stem", "g2048_urm_attention", "g2048_urm_residual_rms", "g2048_urm_swiglu_conv",
+    "g2048_urm_pool_heads",
 )
 
 
@@ -185,6 +188,11 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_policy_rollout_supported": (ctypes.c_int, [i32, i32]),
         "g2048_policy_rollout_lds_bytes": (sz, [i32]),
         "g2048_policy_rollout": (ctypes.c_int, [vp, ctypes.POINTER(PolicyRolloutArgs)]),
+        "g2048_urm_stem": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, i64, i32]),
+        "g2048_urm_attention": (ctypes.c_int, [vp, vp, vp, i64, i32, i32]),
+        "g2048_urm_residual_rms": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, ctypes.c_float]),
+        "g2048_urm_swiglu_conv": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32]),
+        "g2048_urm_pool_heads": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32]),
         "g2048_muon_supported": (ctypes.c_int, [i32, i32]),
         "g2048_muon_step": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.POINTER(MuonCfg)]),
         "g2048_adamw_step": (ctypes.c_int, [vp, ctypes.POINTER(AdamWGroup), i32, vp, vp, vp, ctypes.c_float,
@@ -581,3 +589,45 @@ def ppo_stats(sums, kl, grad_norm, beta_dev, critic: float, m: int, stats, count
                                   float(critic), int(m), _dev(rows, torch.int64, "rows"),
                                   _dev(stats, torch.float32, "stats"),
                                   _dev(counter, torch.int64, "counter")), "g2048_ppo_stats")
+
+
+# ---------------------------------------------------------------- GameURM (include/g2048_urm.h) ----
+def urm_stem(obs, w, ln_w, ln_b, init_hidden, emb, x, xb):
+    """emb = SiLU(LayerNorm(obs-cell features W^T)); x = init_hidden + emb; xb = bf16(x)."""
+    n = obs.shape[0]
+    h = w.shape[0]
+    if obs.dtype not in (torch.float32, torch.bfloat16):
+        raise G2048Error("obs must be float32 or bfloat16")
+    _check(load().g2048_urm_stem(_stream(obs), _dev(obs, None, "obs"), int(obs.dtype == torch.bfloat16),
+                                 _dev(w, torch.float32, "w"), _dev(ln_w, torch.float32, "ln_w"),
+                                 _dev(ln_b, torch.float32, "ln_b"), _dev(init_hidden, torch.float32, "init_hidden"),
+                                 _dev(emb, torch.float32, "emb"), _dev(x, torch.float32, "x"),
+                                 _dev(xb, torch.bfloat16, "xb"), n, h), "g2048_urm_stem")
+
+
+def urm_attention(qkv, out, heads: int):
+    rows, h3 = qkv.shape
+    _check(load().g2048_urm_attention(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"), _dev(out, torch.bfloat16, "out"),
+                                      rows // 16, h3 // 3, int(heads)), "g2048_urm_attention")
+
+
+def urm_residual_rms(x, y, emb, xb, eps: float):
+    rows, h = x.shape
+    _check(load().g2048_urm_residual_rms(_stream(x), _dev(x, torch.float32, "x"), _dev(y, torch.bfloat16, "y"),
+                                         _dev(emb, torch.float32, "emb"), _dev(xb, torch.bfloat16, "xb"), rows, h,
+                                         float(eps)), "g2048_urm_residual_rms")
+
+
+def urm_swiglu_conv(gu, w, b, out):
+    rows, inter2 = gu.shape
+    _check(load().g2048_urm_swiglu_conv(_stream(gu), _dev(gu, torch.bfloat16, "gu"), _dev(w, torch.float32, "w"),
+                                        _dev(b, torch.float32, "b"), _dev(out, torch.bfloat16, "out"), rows // 16,
+                                        inter2 // 2), "g2048_urm_swiglu_conv")
+
+
+def urm_pool_heads(x, wa, ba, wv, bv, logits, value):
+    rows, h = x.shape
+    _check(load().g2048_urm_pool_heads(_stream(x), _dev(x, torch.float32, "x"), _dev(wa, torch.float32, "wa"),
+                                       _dev(ba, torch.float32, "ba"), _dev(wv, torch.float32, "wv"),
+                                       _dev(bv, torch.float32, "bv"), _dev(logits, torch.float32, "logits"),
+                                       _dev(value, torch.float32, "value"), rows // 16, h), "g2048_urm_pool_heads")

@@ -114,11 +114,14 @@ class FusedPolicy:
 
 
 def make_policy(model: torch.nn.Module, dtype=torch.bfloat16):
-    """The rollout policy: FusedPolicy for the reference's GameMLP on a ROCm device (bf16), the
-    generic module copy (InferencePolicy) otherwise."""
+    """The rollout policy: FusedPolicy for the reference's GameMLP and URMPolicy (g2048/urm.py) for its
+    GameURM on a ROCm device (bf16), the generic module copy (InferencePolicy) otherwise."""
     dev = next(model.parameters()).device
     if dtype == torch.bfloat16 and dev.type == "cuda" and FusedPolicy.supports(model):
         return FusedPolicy(model)
+    from .urm import URMPolicy
+    if dtype == torch.bfloat16 and dev.type == "cuda" and URMPolicy.supports(model):
+        return URMPolicy(model)
     return InferencePolicy(model, dtype)
 
 

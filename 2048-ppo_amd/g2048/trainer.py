@@ -42,6 +42,10 @@ class TrainConfig:
     hidden: int = 64
     num_layers: int = 2
     dropout: float = 0.1
+    model_type: str = "mlp"        # "mlp" (GameMLP) or "urm" (GameURM, g2048/urm.py rollout policy)
+    num_heads: int = 4             # URM only
+    num_loops: int = 4
+    num_truncated_loops: int = 1
     decouple_critic: bool = False
     points: float = 0.0
     mono: float = 0.0
@@ -75,8 +79,14 @@ class VecTrainer:
         self.dev = torch.device(device)
         self.rank, self.world = world()
         if model is None:
-            model = agent.GameMLP(agent.MLPConfig(hidden_dim=cfg.hidden, num_layers=cfg.num_layers,
-                                                  dropout=cfg.dropout, decouple_critic=cfg.decouple_critic))
+            if cfg.model_type == "urm":
+                model = agent.GameURM(agent.GameURMConfig(hidden_dim=cfg.hidden, num_layers=cfg.num_layers,
+                                                          num_heads=cfg.num_heads, dropout=cfg.dropout,
+                                                          num_loops=cfg.num_loops,
+                                                          num_truncated_loops=cfg.num_truncated_loops))
+            else:
+                model = agent.GameMLP(agent.MLPConfig(hidden_dim=cfg.hidden, num_layers=cfg.num_layers,
+                                                      dropout=cfg.dropout, decouple_critic=cfg.decouple_critic))
             with torch.no_grad():  # train.py:1559-1567
                 model.action_head.weight.zero_()
                 model.action_head.bias.zero_()
@@ -118,7 +128,8 @@ class VecTrainer:
         self.trim_gen.manual_seed(cfg.seed + 15485863 * (self.rank + 1))
         pcfg = PPOConfig(batch_size=cfg.batch_size, epochs=cfg.epochs, critic=cfg.critic,
                          amp_dtype=torch.bfloat16 if cfg.amp else None)
-        graph_up = cfg.graph_update and not self.episodic
+        # the autograd update of a GameURM (SDPA backward) runs eagerly; GameMLP's is captured
+        graph_up = cfg.graph_update and not self.episodic and isinstance(self.model, agent.GameMLP)
         if cfg.fused_update and cfg.amp and self.dev.type == "cuda" and fastmlp.supports(self.model):
             self.ppo = fastmlp.FusedPPOUpdater(self.model, self.opt, pcfg, self.grads, gen, graph=graph_up,
                                                seed=cfg.seed * 31 + self.rank)
@@ -408,8 +419,10 @@ class VecTrainer:
         import agent
         path = Path(path)
         path.parent.mkdir(parents=True, exist_ok=True)
-        cfg = agent.MLPConfig(hidden_dim=self.cfg.hidden, num_layers=self.cfg.num_layers,
-                              decouple_critic=self.cfg.decouple_critic)
+        cfg = getattr(self.model, "config", None)
+        if not isinstance(cfg, (agent.MLPConfig, agent.GameURMConfig)):
+            cfg = agent.MLPConfig(hidden_dim=self.cfg.hidden, num_layers=self.cfg.num_layers,
+                                  decouple_critic=self.cfg.decouple_critic)
         torch.save({"model_state_dict": self.model.state_dict(), "config": cfg.model_dump(),
                     "eval_avg_score": eval_avg_score, "train_step": train_step,
                     "optimizer": self.opt.state_dict(), "rtg_state": self.rtg.state.cpu()}, path)

@@ -1,0 +1,104 @@
+"""GameURM policy forward on the device (game.py:1355-1458) for rollouts: the URM transformer's
+kernels of include/g2048_urm.h around its projections (hipBLASLt through torch.mm, bf16 operands,
+fp32 accumulate).
+
+Per forward of n boards (16 n token rows):
+  urm_stem                         emb = SiLU(LN(Linear(3->h))),  x = init_hidden + emb
+  num_loops x num_layers blocks:   qkv = xb Wqkv^T -> urm_attention -> o Wo^T -> urm_residual_rms
+                                   gu = xb Wgu^T -> urm_swiglu_conv -> a Wd^T -> urm_residual_rms
+                                   (the last block of a loop adds emb: the next loop's input)
+  urm_pool_heads                   mean over the 16 tokens, action / value heads
+Every buffer is allocated once per batch size and the weights are refreshed in place by sync(), so
+a captured rollout graph keeps working across updates (same contract as rollout.FusedPolicy).
+The truncated loops (no-grad in training, game.py:1437-1443) are ordinary loops in inference.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+
+
+class URMPolicy:
+    """Drop-in for rollout.InferencePolicy with a GameURM master: __call__(obs [n, 48] fp32/bf16) ->
+    (logits fp32 [n, 4], value fp32 [n])."""
+
+    def __init__(self, model: torch.nn.Module):
+        self.master = model
+        self.dtype = torch.bfloat16
+        cfg = model.config
+        self.h, self.heads = cfg.hidden_dim, cfg.num_heads
+        self.loops, self.eps = cfg.num_loops, float(cfg.rms_norm_eps)
+        self.inter = model.layers[0].mlp.inter
+        self.mats = []  # per layer (Wqkv, Wo, Wgu, Wd) as bf16 copies
+        for blk in model.layers:
+            self.mats.append([torch.empty_like(w, dtype=torch.bfloat16) for w in
+                              (blk.attn.qkv_proj.weight, blk.attn.o_proj.weight, blk.mlp.gate_up_proj.weight,
+                               blk.mlp.down_proj.weight)])
+        dev = model.stem[0].weight.device
+        self.conv_w = [torch.empty(self.inter, 2, dtype=torch.float32, device=dev) for _ in model.layers]
+        self.init_hidden = torch.empty(16, self.h, dtype=torch.float32, device=dev)
+        self._n = -1
+        self.sync()
+
+    @staticmethod
+    def supports(model) -> bool:
+        try:
+            import agent
+        except ImportError:  # pragma: no cover
+            return False
+        if not isinstance(model, agent.GameURM):
+            return False
+        c = model.config
+        return (c.conv_kernel == 2 and c.hidden_dim % 4 == 0 and c.hidden_dim <= 512 and c.hidden_dim % c.num_heads == 0
+                and c.hidden_dim // c.num_heads <= 64)
+
+    @torch.no_grad()
+    def sync(self):
+        for blk, mats, cw in zip(self.master.layers, self.mats, self.conv_w):
+            for dst, src in zip(mats, (blk.attn.qkv_proj.weight, blk.attn.o_proj.weight, blk.mlp.gate_up_proj.weight,
+                                       blk.mlp.down_proj.weight)):
+                dst.copy_(src)
+            cw.copy_(blk.mlp.dwconv.weight.view(self.inter, 2))
+        self.init_hidden.copy_(self.master.init_hidden.view(16, self.h))
+
+    def _buffers(self, n: int, dev):
+        if self._n == n:
+            return
+        r, h, i = 16 * n, self.h, self.inter
+        bf = torch.bfloat16
+        self.emb = torch.empty(r, h, dtype=torch.float32, device=dev)
+        self.x = torch.empty(r, h, dtype=torch.float32, device=dev)
+        self.xb = torch.empty(r, h, dtype=bf, device=dev)
+        self.qkv = torch.empty(r, 3 * h, dtype=bf, device=dev)
+        self.att = torch.empty(r, h, dtype=bf, device=dev)
+        self.y = torch.empty(r, h, dtype=bf, device=dev)
+        self.gu = torch.empty(r, 2 * i, dtype=bf, device=dev)
+        self.act = torch.empty(r, i, dtype=bf, device=dev)
+        self.logits = torch.empty(n, 4, dtype=torch.float32, device=dev)
+        self.value = torch.empty(n, dtype=torch.float32, device=dev)
+        self._n = n
+
+    @torch.no_grad()
+    def __call__(self, obs: torch.Tensor):
+        m = self.master
+        n = obs.shape[0]
+        self._buffers(n, obs.device)
+        L.urm_stem(obs.contiguous(), m.stem[0].weight, m.stem[1].weight, m.stem[1].bias, self.init_hidden, self.emb,
+                   self.x, self.xb)
+        nl = len(self.mats)
+        for loop in range(self.loops):
+            for li, (blk, (wqkv, wo, wgu, wd), cw) in enumerate(zip(m.layers, self.mats, self.conv_w)):
+                torch.mm(self.xb, wqkv.t(), out=self.qkv)
+                L.urm_attention(self.qkv, self.att, self.heads)
+                torch.mm(self.att, wo.t(), out=self.y)
+                L.urm_residual_rms(self.x, self.y, None, self.xb, self.eps)
+                torch.mm(self.xb, wgu.t(), out=self.gu)
+                L.urm_swiglu_conv(self.gu, cw, blk.mlp.dwconv.bias, self.act)
+                torch.mm(self.act, wd.t(), out=self.y)
+                nxt = self.emb if (li == nl - 1 and loop < self.loops - 1) else None
+                L.urm_residual_rms(self.x, self.y, nxt, self.xb, self.eps)
+        L.urm_pool_heads(self.x, m.action_head.weight, m.action_head.bias, m.value_head.weight, m.value_head.bias,
+                         self.logits, self.value)
+        return self.logits, self.value

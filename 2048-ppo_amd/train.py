@@ -8,6 +8,8 @@ reward (--smoothness --tile-bonus --corner --adjacency --chain --topo --win-bonu
 printed breakdown table and the --viz-dir export, as in the reference; its dead flags
 (--epsilon --momentum --workers) are accepted and ignored.  New flags: --horizon (0 = one full game per env per train step, the reference's
 semantics; T > 0 = fixed-horizon auto-reset throughput mode), --seed, --no-graph, --fp32.
+--model-type urm trains the GameURM transformer (the reference refuses it, train.py:1523-1532):
+rollouts through g2048/urm.py's kernels, the update through autograd (bf16 autocast).
 For several GPUs run it under `python -m torch.distributed.run --nproc-per-node N` (one rank per
 GPU; --episodes is per rank).
 
@@ -259,11 +261,7 @@ def train(
         logger.print("this path is not available")  # train.py:1508-1514
         logger.close()
         raise typer.Exit(0)
-    if model_type.lower() == "urm":
-        logger.print("this model type is not available")  # train.py:1523-1532
-        logger.close()
-        raise typer.Exit(1)
-    if model_type.lower() != "mlp":
+    if model_type.lower() not in ("mlp", "urm"):
         logger.print(f"Unknown model type: {model_type}. Use 'mlp' or 'urm'.")
         logger.close()
         raise typer.Exit(1)
@@ -274,8 +272,12 @@ def train(
                       warmup_steps=warmup_steps, beta1=beta1, beta2=beta2, weight_decay=weight_decay,
                       adaptive_beta=adaptive_beta, target_entropy=target_entropy, beta_min=beta_min,
                       beta_max=beta_max, beta_lr=beta_lr, upsample_ratio=upsample_ratio, horizon=horizon, seed=seed,
-                      graph=not no_graph, amp=not fp32)
-    logger.print(f"Creating GameMLP model (hidden={hidden_size}, layers={num_layers}); {num_episodes} envs/GPU x {ws}")
+                      graph=not no_graph, amp=not fp32, model_type=model_type.lower(), num_heads=num_heads,
+                      num_loops=num_loops, num_truncated_loops=num_truncated_loops)
+    name = "GameURM" if model_type.lower() == "urm" else "GameMLP"
+    extra = f", heads={num_heads}, loops={num_loops}/{num_truncated_loops}" if name == "GameURM" else ""
+    logger.print(f"Creating {name} model (hidden={hidden_size}, layers={num_layers}{extra}); "
+                 f"{num_episodes} envs/GPU x {ws}")
     tr = VecTrainer(cfg, device)
     best_eval = 0.0
     highest = 0

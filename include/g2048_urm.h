@@ -1,0 +1,70 @@
+/*
+ * g2048_urm.h -- C ABI of the GameURM policy forward (game.py:1223-1458) in libg2048.so: the
+ * non-GEMM parts of the Universal-Reasoning-Model transformer over the 16 cell tokens, as fused
+ * HIP kernels for gfx950.  The four projections of a block (qkv_proj, o_proj, gate_up_proj,
+ * down_proj: plain x W^T GEMMs) go to the platform BLAS (hipBLASLt through torch); everything
+ * between them is one of the kernels below (g2048/urm.py strings them together and the rollout
+ * captures the whole forward in a hipGraph).
+ *
+ * Token layout: board b's 16 cells are rows 16 b .. 16 b + 15 of every [rows, .] activation
+ * (row-major, cell order of to_model_format, game.py:92-101), so a board's sequence is contiguous.
+ * The residual stream x is fp32 [16 n, h]; GEMM operands are bf16 (raw uint16 bits).  h % 4 == 0,
+ * h <= 512, heads | h, head_dim = h / heads <= 64.
+ *
+ * Conventions: as g2048.h (device pointers, asynchronous on `stream`, no allocation, no host
+ * synchronisation; 0 / G2048_EINVAL / hipError_t).
+ */
+#ifndef G2048_URM_H
+#define G2048_URM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "g2048.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Stem and first loop input (game.py:1376-1380, 1425-1431, 1441):
+ *   emb = SiLU(LayerNorm(Linear(3 -> h, no bias)(cell features)))      fp32 [16 n, h]
+ *   x   = init_hidden + emb;  xb = bf16(x)                              (loop 1's input)
+ * obs [n, 48] fp32 (obs_dtype 0) or bf16 (1); w [h, 3], ln_w / ln_b [h], init_hidden [16, h]
+ * fp32; LayerNorm eps 1e-5 (nn.LayerNorm default). */
+int g2048_urm_stem(g2048_stream_t stream, const void *obs, int32_t obs_dtype, const float *w, const float *ln_w,
+                   const float *ln_b, const float *init_hidden, float *emb, float *x, uint16_t *xb, int64_t n,
+                   int32_t h);
+
+/* Bidirectional multi-head attention core of GameURMAttention (game.py:1296-1317,
+ * scaled_dot_product_attention with scale 1/sqrt(head_dim), no mask, eval mode):
+ * qkv bf16 [16 n, 3 h] = x W_qkv^T viewed as (3, heads, head_dim) per token -> out bf16 [16 n, h]
+ * (heads concatenated, the o_proj operand).  One wave per (board, head) on
+ * v_mfma_f32_16x16x16_bf16: S^T = K Q^T (head_dim zero-padded to 16), masked-free softmax over the
+ * 16 keys in registers (fp32), O^T = V^T P^T. */
+int g2048_urm_attention(g2048_stream_t stream, const uint16_t *qkv, uint16_t *out, int64_t n, int32_t h,
+                        int32_t heads);
+
+/* Post-norm residual (game.py:1346, 1350 with rms_norm :1223-1229):
+ *   x = x + y;  x = x * rsqrt(mean(x^2) + eps)  [+ emb, the next loop's input, game.py:1447];
+ *   xb = bf16(x).
+ * x fp32 [rows, h] in place, y bf16 [rows, h] (a projection output), emb fp32 or NULL. */
+int g2048_urm_residual_rms(g2048_stream_t stream, float *x, const uint16_t *y, const float *emb, uint16_t *xb,
+                           int64_t rows, int32_t h, float eps);
+
+/* GameConvSwiGLU between its two projections (game.py:1264-1276): gu bf16 [16 n, 2 inter] =
+ * x W_gate_up^T -> a = SiLU(gate) * up; depthwise Conv1d(kernel 2, padding 1, trimmed to 16
+ * tokens) over each board's sequence: c_t = w[ch][0] a_{t-1} + w[ch][1] a_t + b[ch] (a_{-1} = 0);
+ * out = bf16(SiLU(c)) [16 n, inter] (the down_proj operand).  w fp32 [inter, 2], b fp32 [inter]. */
+int g2048_urm_swiglu_conv(g2048_stream_t stream, const uint16_t *gu, const float *w, const float *b, uint16_t *out,
+                          int64_t n, int32_t inter);
+
+/* Mean pooling over the 16 tokens and the two heads (game.py:1452-1456): logits fp32 [n, 4] =
+ * pooled wa^T + ba, value fp32 [n] = pooled wv^T + bv;  x fp32 [16 n, h], wa [4, h], wv [1, h]. */
+int g2048_urm_pool_heads(g2048_stream_t stream, const float *x, const float *wa, const float *ba, const float *wv,
+                         const float *bv, float *logits, float *value, int64_t n, int32_t h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* G2048_URM_H */

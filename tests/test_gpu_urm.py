@@ -1,0 +1,232 @@
+"""GameURM policy forward on the device (g2048/urm.py over include/g2048_urm.h) vs the reference's
+own fp32 forward (tests/golden/urm.npz, game.py:1355-1458) and vs the fp32 module at the default
+and README-like sizes; and rollouts driven by it.
+
+Two stated bounds on the fp32 logits / value:
+  * vs the fp32 forward (the reference's numbers): |got - ref| <= 0.05 + 0.03 |ref| on the golden
+    case; on the random-init module cases max |got - ref| <= 0.08 max|ref| (measured 0.016-0.067 of
+    the logit scale; torch's own bf16 autocast of the module errs 0.015-0.098 on the same cases).  The
+    projections take bf16 operands (rel. rounding 2^-9) through num_loops x num_layers = 8 post-norm
+    blocks; a torch restatement with bf16 rounding at exactly the kernels' points (_emulate below)
+    shows the same error (0.042 max on urm.npz), so this is the bf16 operand effect, not the kernels.
+  * vs that bf16-rounding restatement: mean |got - emul| <= 3e-3 and max <= 0.06 (fp32 summation
+    order and __expf only; an occasional flipped bf16 rounding propagates through the later blocks,
+    so the max over thousands of boards is of the order of one bf16 step of the logits)."""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+ATOL, RTOL = 0.05, 0.03
+EMUL_MEAN, EMUL_MAX = 3e-3, 0.06
+SCALE_REL = 0.08
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.fail("no ROCm device visible: GPU tests must run on an MI355X")
+    return torch.device("cuda:0")
+
+
+def _golden_model(dev):
+    import agent
+    g = golden("urm.npz")
+    h, nl, heads, loops, trunc, k = (int(x) for x in g["config"])
+    cfg = agent.GameURMConfig(hidden_dim=h, num_layers=nl, num_heads=heads, num_loops=loops, num_truncated_loops=trunc,
+                              conv_kernel=k, dropout=0.0, expansion=float(g["expansion"]), rms_norm_eps=float(g["eps"]))
+    m = agent.GameURM(cfg).eval()
+    m.load_state_dict({kk[3:]: torch.from_numpy(g[kk]) for kk in g.files if kk.startswith("w::")}, strict=True)
+    return m.to(dev), g
+
+
+def _emulate(m, obs):
+    """torch fp32 restatement of g2048/urm.py with bf16 rounding where the kernels round: GEMM
+    operands and outputs, attention probabilities and output, the SwiGLU-conv output."""
+    import torch.nn.functional as F
+    r = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
+    c = m.config
+    n, h, heads = obs.shape[0], c.hidden_dim, c.num_heads
+    hd = h // heads
+    with torch.no_grad():
+        emb = F.silu(m.stem[1](obs.float().view(n, 16, 3) @ m.stem[0].weight.t()))
+        x = m.init_hidden + emb
+        for loop in range(c.num_loops):
+            for li, blk in enumerate(m.layers):
+                qkv = r(r(x) @ r(blk.attn.qkv_proj.weight).t())
+                q, k, v = qkv.view(n, 16, 3, heads, hd).permute(2, 0, 3, 1, 4)
+                p = r(((q @ k.transpose(-1, -2)) / hd ** 0.5).softmax(-1))
+                o = r(p @ v).transpose(1, 2).reshape(n, 16, h)
+                x = x + r(o @ r(blk.attn.o_proj.weight).t())
+                x = x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + c.rms_norm_eps)
+                ga, up = r(r(x) @ r(blk.mlp.gate_up_proj.weight).t()).chunk(2, -1)
+                a = F.silu(ga) * up
+                w, b = blk.mlp.dwconv.weight.view(-1, 2), blk.mlp.dwconv.bias
+                prev = torch.cat([torch.zeros_like(a[:, :1]), a[:, :-1]], 1)
+                act = r(F.silu(prev * w[:, 0] + a * w[:, 1] + b))
+                x = x + r(act @ r(blk.mlp.down_proj.weight).t())
+                x = x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + c.rms_norm_eps)
+                if li == len(m.layers) - 1 and loop < c.num_loops - 1:
+                    x = x + emb
+        pooled = x.mean(1)
+        return m.action_head(pooled), m.value_head(pooled).view(-1)
+
+
+def _check_emul(got_l, got_v, m, obs):
+    el, ev = _emulate(m, obs)
+    d = torch.cat([(got_l - el).abs().reshape(-1), (got_v - ev).abs().reshape(-1)])
+    print(f"vs bf16-rounding restatement: mean {d.mean().item():.3g} max {d.max().item():.3g}")
+    assert d.mean().item() <= EMUL_MEAN and d.max().item() <= EMUL_MAX
+
+
+def _check(got, want, what):
+    got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
+    err = np.abs(got - want)
+    bound = ATOL + RTOL * np.abs(want)
+    assert (err <= bound).all(), f"{what}: max err {err.max():.4g}, worst excess {(err - bound).max():.4g}"
+    return err.max()
+
+
+def test_urm_policy_matches_reference_golden(dev):
+    from g2048.urm import URMPolicy
+    m, g = _golden_model(dev)
+    assert URMPolicy.supports(m)
+    pol = URMPolicy(m)
+    logits, value = pol(torch.from_numpy(g["obs"]).to(dev))
+    _check(logits.cpu().numpy(), g["logits"], "logits")
+    _check(value.cpu().numpy(), g["value"].reshape(-1), "value")
+    _check_emul(logits, value, m, torch.from_numpy(g["obs"]).to(dev))
+    # bf16 obs (the rollout's obs buffer) stays within the same bound
+    lb, vb = pol(torch.from_numpy(g["obs"]).to(dev).to(torch.bfloat16))
+    _check(lb.cpu().numpy(), g["logits"], "logits (bf16 obs)")
+    _check(vb.cpu().numpy(), g["value"].reshape(-1), "value (bf16 obs)")
+
+
+@pytest.mark.parametrize("h,heads,layers,loops,n", [(64, 4, 2, 4, 4096), (64, 2, 2, 4, 1000), (196, 4, 2, 2, 2048),
+                                                     (128, 8, 1, 3, 333)])
+def test_urm_policy_matches_fp32_module(dev, h, heads, layers, loops, n):
+    """Default config (h 64, inter 120, head_dim 16), head_dim 32, head_dim 49 (zero-padded MFMA
+    k-steps, unaligned head columns), head_dim 16 with 8 heads; ragged board counts."""
+    import agent
+    from g2048 import _lib as L
+    from g2048.urm import URMPolicy
+    torch.manual_seed(h + heads + n)
+    m = agent.GameURM(agent.GameURMConfig(hidden_dim=h, num_heads=heads, num_layers=layers, num_loops=loops,
+                                          num_truncated_loops=1, dropout=0.0)).to(dev).eval()
+    rng = np.random.default_rng(n)
+    boards = rng.integers(0, 14, size=(n, 16)).astype(np.int8)
+    boards[rng.random(boards.shape) < 0.4] = 0
+    obs = torch.empty(n, 48, dtype=torch.float32, device=dev)
+    L.obs_encode(torch.from_numpy(boards).to(dev), obs)
+    with torch.no_grad():
+        ref_l, ref_v = m(obs)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            ac_l, ac_v = m(obs)
+    got_l, got_v = URMPolicy(m)(obs)
+    ea = max((ac_l.float() - ref_l).abs().max().item(), (ac_v.float() - ref_v).abs().max().item())
+    eg = max((got_l - ref_l).abs().max().item(), (got_v - ref_v.view(-1)).abs().max().item())
+    print(f"h={h} heads={heads}: max err vs fp32 {eg:.4g} (torch bf16 autocast {ea:.4g}), "
+          f"max |logit| {ref_l.abs().max().item():.3g}")
+    _check_emul(got_l, got_v, m, obs)
+    assert eg <= SCALE_REL * ref_l.abs().max().item(), eg
+
+
+def test_urm_policy_weight_sync_and_graph(dev):
+    """sync() refreshes the bf16 copies in place; a captured forward replays with the new weights."""
+    import agent
+    from g2048.urm import URMPolicy
+    torch.manual_seed(3)
+    m = agent.GameURM(agent.GameURMConfig(dropout=0.0)).to(dev).eval()
+    pol = URMPolicy(m)
+    obs = torch.rand(512, 48, device=dev) * 5
+    pol(obs)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        pol(obs)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out_l, out_v = pol(obs)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(0.01 * torch.randn_like(p))
+    pol.sync()
+    g.replay()
+    torch.cuda.synchronize()
+    want_l, want_v = [t.clone() for t in pol(obs)]
+    assert torch.equal(out_l, want_l) and torch.equal(out_v, want_v)
+    with torch.no_grad():
+        ref_l, _ = m(obs)
+    _check(want_l.cpu().numpy(), ref_l.cpu().numpy(), "logits after sync")
+
+
+def test_urm_rollout_drives_envs(dev):
+    """Rollout with the URM policy (per-step path: obs -> URM -> sampler -> env step): legal actions,
+    finite log-probs, logp rows of the sampler consistent with the URM logits."""
+    import agent
+    from g2048 import _lib as L
+    from g2048.rollout import Rollout, make_policy
+    from g2048.urm import URMPolicy
+    torch.manual_seed(5)
+    m = agent.GameURM(agent.GameURMConfig(dropout=0.0)).to(dev).eval()
+    pol = make_policy(m)
+    assert isinstance(pol, URMPolicy)
+    ro = Rollout(2048, 24, dev, seed=9)
+    ro.reset()
+    b = ro.collect(pol, graph=True)
+    torch.cuda.synchronize()
+    legal = b.flags[:24] & L.FLAG_LEGAL
+    a = b.actions.long()
+    assert ((legal.long() >> a) & 1).all()  # every action legal on its board
+    assert torch.isfinite(b.logp.gather(2, a.unsqueeze(2))).all()
+    assert torch.isfinite(b.value).all() and (b.entropy >= 0).all()
+    # the step-0 log-probs are the masked log-softmax of the URM logits of boards[0]
+    obs = torch.empty(2048, 48, dtype=torch.bfloat16, device=dev)
+    L.obs_encode(b.boards[0], obs)
+    lg, _ = pol(obs)
+    mask = ((b.flags[0].long().unsqueeze(1) >> torch.arange(4, device=dev)) & 1).bool()
+    want = torch.where(mask, lg, torch.tensor(-torch.inf, device=dev)).log_softmax(-1)
+    got = b.logp[0]
+    np.testing.assert_allclose(torch.where(mask, got, 0).cpu().numpy(), torch.where(mask, want, 0).cpu().numpy(),
+                               rtol=1e-5, atol=1e-5)
+
+
+def test_urm_kernels_reject_bad_arguments(dev):
+    from g2048 import _lib as L
+    qkv = torch.zeros(32, 3 * 66, dtype=torch.bfloat16, device=dev)
+    out = torch.zeros(32, 66, dtype=torch.bfloat16, device=dev)
+    with pytest.raises(L.G2048Error):
+        L.urm_attention(qkv, out, 4)  # h % 4 != 0
+    qkv = torch.zeros(32, 3 * 256, dtype=torch.bfloat16, device=dev)
+    out = torch.zeros(32, 256, dtype=torch.bfloat16, device=dev)
+    with pytest.raises(L.G2048Error):
+        L.urm_attention(qkv, out, 2)  # head_dim 128 > 64
+
+
+@pytest.mark.parametrize("horizon", [16, 0])
+def test_urm_trainer_steps(dev, horizon):
+    """VecTrainer with --model-type urm: URMPolicy rollouts, autograd bf16 update with Muon on the
+    2-D weights and AdamW on the rest (incl. init_hidden and the conv kernels); parameters move,
+    metrics finite; fixed-horizon and episodic modes."""
+    import math
+    from g2048.rollout import Rollout  # noqa: F401
+    from g2048.trainer import TrainConfig, VecTrainer
+    from g2048.urm import URMPolicy
+    cfg = TrainConfig(steps=4, episodes=256, horizon=horizon, max_steps=48 if horizon == 0 else None, batch_size=1024,
+                      hidden=64, model_type="urm", points=0.1, mono=1.0, rtg_beta=0.99, gamma=0.99, entropy=0.02,
+                      critic=0.2, warmup_steps=0)
+    tr = VecTrainer(cfg, dev)
+    assert isinstance(tr.policy, URMPolicy)
+    before = {k: v.detach().clone() for k, v in tr.model.named_parameters()}
+    for s in range(2):
+        m = tr.train_step(s)
+        for k in ("loss", "entropy", "grad_norm", "avg_score", "explained_var"):
+            assert math.isfinite(m[k]), (k, m[k])
+        assert m["samples"] > 0
+    moved = {k for k, v in tr.model.named_parameters() if not torch.equal(v, before[k])}
+    assert "init_hidden" in moved and "layers.0.attn.qkv_proj.weight" in moved and "layers.1.mlp.dwconv.weight" in moved
