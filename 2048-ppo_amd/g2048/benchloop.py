@@ -55,3 +55,64 @@ def bench_train(args, rank: int, world: int, dev) -> dict:
         "last_metrics": {k: m[k] for k in ("loss", "entropy", "avg_score", "episodes_finished", "grad_norm",
                                            "augmented_samples")},
     }
+
+
+def bench_urm(args, rank: int, world: int, dev) -> dict:
+    """BASELINE.json configs[4] on this GPU: the GameURM transformer policy (default GameURMConfig:
+    h 64, 2 layers, 4 heads, 4 loops / 1 truncated, inter 120) driving 65 536 envs.  (1) rollout:
+    `--urm-steps` policy steps (obs -> URM forward on g2048/urm.py's kernels + hipBLASLt projections
+    -> sampler -> env step), captured in one hipGraph, timed over replays; (2) one full training
+    iteration at horizon `--urm-steps` (RTG + autograd bf16 update in minibatches of --train-batch)."""
+    import agent
+    from g2048.rollout import Rollout, make_policy
+    from g2048.trainer import TrainConfig, VecTrainer
+    torch.manual_seed(0x2048 + rank)
+    m = agent.GameURM(agent.GameURMConfig(dropout=0.0)).to(dev)
+    pol = make_policy(m)
+    T = args.urm_steps
+    ro = Rollout(args.envs, T, dev, seed=0x2048 + rank, env_base=rank * args.envs)
+    ro.reset()
+    ro.collect(pol, graph=True)  # capture + first replay
+    torch.cuda.synchronize()
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ro.buf.carry_over()
+        ro.collect(pol, graph=True)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    # forward alone (one call of the policy on the obs buffer), events on the current stream
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    pol(ro.buf.obs)
+    e0.record()
+    for _ in range(5):
+        pol(ro.buf.obs)
+    e1.record()
+    torch.cuda.synchronize()
+    fwd_ms = e0.elapsed_time(e1) / 5
+    c = m.config
+    flops_tok = 2 * c.num_loops * c.num_layers * (4 * c.hidden_dim ** 2 + 3 * m.layers[0].mlp.inter * c.hidden_dim
+                                                  + 2 * 16 * c.hidden_dim)
+    out = {"value": args.envs * T * reps * world / wall, "unit": "env-steps/s", "ms_per_step": wall / (reps * T) * 1e3,
+           "forward_ms": fwd_ms, "forward_TFLOPs": flops_tok * 16 * args.envs / (fwd_ms * 1e-3) / 1e12,
+           "config": {"workload": f"{args.envs} envs/GPU, GameURM h={c.hidden_dim} L={c.num_layers} heads={c.num_heads} "
+                                  f"loops={c.num_loops}/{c.num_truncated_loops} inter={m.layers[0].mlp.inter}, bf16",
+                      "steps_per_graph": T, "replays": reps}}
+    del ro, pol
+    torch.cuda.empty_cache()
+    cfg = TrainConfig(steps=1000, lr=1e-3, critic_lr=1e-4, gamma=0.99, entropy=0.02, critic=0.2, episodes=args.envs,
+                      batch_size=args.train_batch, hidden=64, model_type="urm", points=0.1, mono=1.0, rtg_beta=0.99,
+                      warmup_steps=10, horizon=T, seed=0x2048, graph=True, amp=True)
+    tr = VecTrainer(cfg, dev)
+    tr.train_step(0)
+    torch.cuda.synchronize()
+    tr.profile = True
+    tr.timings = {}
+    t0 = time.perf_counter()
+    mt = tr.train_step(1)
+    torch.cuda.synchronize()
+    it = time.perf_counter() - t0
+    out["train_iter"] = {"value": args.envs * T * world / it, "unit": "env-steps/s", "ms_per_iter": it * 1e3,
+                         "phase_ms": {k: round(v, 3) for k, v in tr.timings.items()},
+                         "minibatch": args.train_batch, "loss": mt["loss"], "entropy": mt["entropy"]}
+    return out

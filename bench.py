@@ -68,6 +68,7 @@ def parse():
     p.add_argument("--train-horizon", type=int, default=64)
     p.add_argument("--train-batch", type=int, default=65536)
     p.add_argument("--train-upsample", type=float, default=0.25, help="--upsample-ratio of the README command")
+    p.add_argument("--urm-steps", type=int, default=16, help="GameURM policy rollout leg: steps per graph (0=off)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of each CPU-baseline leg (0=off)")
     p.add_argument("--sweep", default="1048576,4194304,16777216",
                    help="comma list of board counts for the rollout-kernel sweep ('' = off)")
@@ -442,6 +443,10 @@ def main():
     if args.train_iters > 0:
         from g2048 import benchloop
         result["train_loop"] = benchloop.bench_train(args, rank, world, dev)
+
+    if args.urm_steps > 0:
+        from g2048 import benchloop
+        result["urm"] = benchloop.bench_urm(args, rank, world, dev)
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cb = cpu_baselines(args.cpu_seconds)
