@@ -14,7 +14,6 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
-#include <stdlib.h>
 
 #include "board.hpp"
 #include "rowtable.hpp"
@@ -314,225 +313,6 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
         }
         if (t < steps) rollout_step<false>(s, s_row, rows(t), li, rng.seed, pair + 2u, env);
         boards[i] = s.b;
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Producer / consumer split of the same rollout (the bench workload at N <= 2^16 boards).
-//
-// At 65 536 boards the one-board-per-lane kernel above runs exactly one wave per SIMD, and one wave
-// alone issues at most one VALU instruction per ~4 cycles (MI355X_MICROARCH.md, 'vector-instruction
-// ISSUE cost'), half of what the SIMD can take.  Only part of a step is on the board's critical
-// path (action -> move -> spawn -> next legal mask -> next action); the trajectory statistics
-// (monotonicity before/after, emptiness) and the five record stores are not.  So each 64-board
-// slice gets TWO waves on the same CU: a producer that runs the critical path (Philox, table move,
-// spawn, legality, resets) and a consumer that, one phase of K steps behind, rebuilds each board
-// from the producer's message, computes the statistics and writes every record.  Messages go
-// through an LDS ring of 2 x K slots (moved board 16 B + packed step info 8 B per lane), the two
-// halves alternating with one workgroup barrier per phase.  Records are bit-identical to
-// env_rollout_kernel's (same RNG convention, same arithmetic; tests/test_gpu_env.py).
-constexpr int kPcWaves = 4;                         // producer waves per block (and consumer waves)
-constexpr int kPcThreads = 2 * 64 * kPcWaves;       // 512
-constexpr int kPcBoards = 64 * kPcWaves;            // boards per block-group
-constexpr int kPcK = 4;                             // steps per phase
-constexpr int64_t kPcMaxBoards = int64_t(1) << 18;  // dispatch threshold (g2048_env_rollout_random)
-constexpr int kPcTabBytes = (int)(lut::kRowEntries * 4u);                    // 82 944
-constexpr int kPcRingMoved = 2 * kPcK * kPcBoards * 16;                      // 32 KiB
-constexpr int kPcRingInfo = 2 * kPcK * kPcBoards * 8;                        // 16 KiB
-// every 4-bit-masked table index (< 15 * 1885 entries) stays inside the allocation: lanes whose
-// rows hold an exponent >= 12 read (and discard) ring bytes instead of faulting
-static_assert(kPcTabBytes + kPcRingMoved + kPcRingInfo >= 15 * 1885 * 4 + 4, "table index range");
-
-struct PcProducer {
-    uint4 b;          // current board
-    uint32_t legal;   // its legal mask
-    bool big;         // it holds an exponent >= 12 (sticky until reset): the SWAR move path
-    uint4 D;          // Philox draw of the current pair of steps (see RolloutLane)
-    PhiloxState ph;   // draw of the next pair
-};
-
-// info word x: action (2) | spawn cell (4) << 2 | spawn value - 1 (1) << 6 | flags (8) << 8 |
-// reset tiles p1 (4) << 16 | v1 - 1 << 20 | p2 (4) << 21 | v2 - 1 << 25;  y: merge points
-template <bool kOdd>
-__device__ __forceinline__ void pc_produce(PcProducer &s, const uint32_t *__restrict__ tab, uint4 *slot_m,
-                                           uint2 *slot_i, uint64_t seed, uint64_t next_pair, uint32_t env) {
-    const uint32_t u = kOdd ? s.D.y : s.D.x;
-    const uint64_t pa = (uint64_t)u * (uint32_t)__popc(s.legal);
-    const uint32_t a = kth_bit4(s.legal, (uint32_t)(pa >> 32)), r = (uint32_t)pa;
-    const bool vert = a < 2u;
-    const uint32_t rsel = (a & 1u) ? 0x00010203u : 0x03020100u;
-    uint4 w = perm4(sel4(vert, transpose(s.b), s.b), rsel);
-    uint32_t e0 = lds_word(tab, row12_addr(w.x)), e1 = lds_word(tab, row12_addr(w.y));
-    uint32_t e2 = lds_word(tab, row12_addr(w.z)), e3 = lds_word(tab, row12_addr(w.w));
-    asm volatile("" : "+v"(s.ph.c0), "+v"(s.ph.c1), "+v"(s.ph.c2), "+v"(s.ph.c3)::"memory");
-    if constexpr (kOdd) philox_rounds<5, 10>(s.ph);
-    else philox_rounds<0, 5>(s.ph);
-    asm volatile("" : "+v"(s.ph.c0), "+v"(s.ph.c1), "+v"(s.ph.c2), "+v"(s.ph.c3), "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3));
-    w = perm4(make_uint4(unpack_row(e0), unpack_row(e1), unpack_row(e2), unpack_row(e3)), rsel);
-    uint4 moved = sel4(vert, transpose(w), w);
-    const uint32_t q = __builtin_bit_cast(uint32_t, (as_u16x2(e0) + as_u16x2(e1)) + (as_u16x2(e2) + as_u16x2(e3)));
-    uint32_t pts = (q >> 16) << 2;
-    if (s.big) {  // an exponent outside the table: the SWAR compute path
-        uint32_t mx;
-        moved = apply_move(s.b, a, pts, mx);
-    } else {      // table results are <= 12: a byte with bits 3 and 2 set is a new 12
-        const uint32_t t = bop3<kA & kB & kC>(moved.x, moved.x << 1, 0x08080808u) |
-                           bop3<kA & kB & kC>(moved.y, moved.y << 1, 0x08080808u) |
-                           bop3<kA & kB & kC>(moved.z, moved.z << 1, 0x08080808u) |
-                           bop3<kA & kB & kC>(moved.w, moved.w << 1, 0x08080808u);
-        s.big = t != 0u;
-    }
-    const uint32_t Zm[4] = {zm(moved.x), zm(moved.y), zm(moved.z), zm(moved.w)};
-    const uint32_t cnt = __popc(Zm[0]) + __popc(Zm[1]) + __popc(Zm[2]) + __popc(Zm[3]);
-    uint4 nb = moved;
-    uint32_t sp;
-    const uint32_t v = spawn_chain(nb, Zm, cnt, r, sp);
-    s.b = nb;
-    s.legal = legal_mask(s.b);
-    uint32_t info = a | (sp << 2) | ((v - 1u) << 6);
-    if (s.legal == 0u) {  // game over: a new game from the pair's spare words
-        uint32_t p1, v1, p2, v2;
-        s.b = fresh_from_pair(s.D.z, s.D.w, p1, v1, p2, v2);
-        MonoStats unused;
-        s.legal = fresh_stats(p1, v1, p2, v2, unused);
-        s.big = false;
-        info |= ((FLAG_DONE | FLAG_RESET | s.legal) << 8) | (p1 << 16) | ((v1 - 1u) << 20) | (p2 << 21) |
-                ((v2 - 1u) << 25);
-    } else {
-        info |= s.legal << 8;
-    }
-    *slot_m = moved;
-    *slot_i = make_uint2(info, pts);
-    if constexpr (kOdd) {
-        s.D = make_uint4(s.ph.c0, s.ph.c1, s.ph.c2, s.ph.c3);
-        s.ph = philox_start(seed, next_pair, env, 1u);
-    }
-}
-
-struct PcConsumer {
-    uint4 b;      // the producer's board, rebuilt from the messages
-    MonoStats sb; // its monotonicity statistics
-    int empt_b;   // its empty-cell count
-};
-
-__device__ __forceinline__ void pc_consume(PcConsumer &c, const uint4 *slot_m, const uint2 *slot_i, const TrajRows &tr,
-                                           uint32_t li, bool active) {
-    if (active) tr.b[li] = c.b;
-    const uint4 moved = *slot_m;
-    const uint2 inf = *slot_i;
-    const uint32_t a = inf.x & 3u, sp = (inf.x >> 2) & 15u, v = ((inf.x >> 6) & 1u) + 1u, fl = (inf.x >> 8) & 0xFFu;
-    const int mono_b = mono_value(c.sb);
-    const uint32_t rm[4] = {moved.x, moved.y, moved.z, moved.w};
-    const uint32_t Zm[4] = {zm(moved.x), zm(moved.y), zm(moved.z), zm(moved.w)};
-    const MonoStats sa = mono_stats_z(rm, Zm, board_max(moved));
-    const int mono_a = mono_value(sa);
-    const int empt_a = __popc(Zm[0]) + __popc(Zm[1]) + __popc(Zm[2]) + __popc(Zm[3]);
-    uint4 nb = moved;
-    set_cell(nb, sp, v);
-    c.sb = mono_add_tile(sa, nb, sp, v);  // only the neighbours of the (empty before) spawn cell are read
-    c.b = nb;
-    if (fl & FLAG_RESET) {
-        const uint32_t p1 = (inf.x >> 16) & 15u, v1 = ((inf.x >> 20) & 1u) + 1u;
-        const uint32_t p2 = (inf.x >> 21) & 15u, v2 = ((inf.x >> 25) & 1u) + 1u;
-        uint4 f = make_uint4(0u, 0u, 0u, 0u);
-        set_cell(f, p1, v1);
-        set_cell(f, p2, v2);
-        c.b = f;
-        fresh_stats(p1, v1, p2, v2, c.sb);
-    }
-    if (active) {
-        tr.a[li] = (uint8_t)a;
-        tr.p[li] = (int32_t)inf.y;
-        tr.pot[li] = (uint32_t)(mono_b & 0xFF) | ((uint32_t)(mono_a & 0xFF) << 8) |
-                     ((uint32_t)(c.empt_b & 0xFF) << 16) | ((uint32_t)(empt_a & 0xFF) << 24);
-        tr.f[li] = (uint8_t)fl;
-    }
-    c.empt_b = (fl & FLAG_RESET) ? 14 : empt_a - 1;
-}
-
-__global__ __launch_bounds__(kPcThreads) void env_rollout_pc_kernel(uint4 *__restrict__ boards, int64_t n,
-                                                                    int64_t steps, uint4 *__restrict__ tb,
-                                                                    uint8_t *__restrict__ ta, int32_t *__restrict__ tp,
-                                                                    uint32_t *__restrict__ tpot,
-                                                                    uint8_t *__restrict__ tf, RngArgs rng) {
-    __shared__ __attribute__((aligned(16))) char smem[kPcTabBytes + kPcRingMoved + kPcRingInfo];
-    uint32_t *s_row = reinterpret_cast<uint32_t *>(smem);
-    uint4 *ring_m = reinterpret_cast<uint4 *>(smem + kPcTabBytes);                 // [2][K][kPcBoards]
-    uint2 *ring_i = reinterpret_cast<uint2 *>(smem + kPcTabBytes + kPcRingMoved);  // [2][K][kPcBoards]
-    stage_row_table(s_row);
-    const uint64_t ctr0 = rng_counter(rng);
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const bool producer = wave < kPcWaves;
-    const int slot0 = (wave % kPcWaves) * 64 + lane;  // this lane's board within the block-group
-    const int64_t groups = (n + kPcBoards - 1) / kPcBoards;
-    const int64_t nph = (steps + kPcK - 1) / kPcK;
-    for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
-        const int64_t i = grp * kPcBoards + slot0;
-        const bool active = i < n;
-        const int64_t ic = active ? i : n - 1;
-        const uint32_t env = rng.env_base + (uint32_t)ic, li = (uint32_t)ic;
-        // both roles start from the same board (a finished board handed in is reset first)
-        uint4 b = boards[ic];
-        uint32_t legal = legal_mask(b);
-        MonoStats sb;
-        bool fresh = false;
-        if (legal == 0u) {
-            uint32_t p1, v1, p2, v2;
-            b = fresh_from_words(philox_draw(rng.seed, ctr0 + (uint64_t)steps, env, 2u), p1, v1, p2, v2);
-            legal = fresh_stats(p1, v1, p2, v2, sb);
-            fresh = true;
-        }
-        if (producer) {
-            PcProducer s;
-            s.b = b;
-            s.legal = legal;
-            s.big = board_max(b) > 11u;
-            uint64_t pair = ctr0 >> 1;
-            s.D = philox_draw(rng.seed, pair, env, 1u);
-            s.ph = philox_start(rng.seed, pair + 1u, env, 1u);
-            if (ctr0 & 1u) philox_rounds<0, 5>(s.ph);  // the launch starts on the second step of a pair
-            for (int64_t j = 0; j <= nph; j++) {
-                if (j < nph) {
-                    const int h = (int)(j & 1);
-#pragma unroll 1
-                    for (int k = 0; k < kPcK; k++) {
-                        const int64_t t = j * kPcK + k;
-                        if (t >= steps) break;
-                        uint4 *sm = ring_m + (h * kPcK + k) * kPcBoards + slot0;
-                        uint2 *si = ring_i + (h * kPcK + k) * kPcBoards + slot0;
-                        if ((ctr0 + (uint64_t)t) & 1u) {
-                            pc_produce<true>(s, s_row, sm, si, rng.seed, pair + 2u, env);
-                            pair++;
-                        } else {
-                            pc_produce<false>(s, s_row, sm, si, rng.seed, pair + 2u, env);
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-            if (active) boards[i] = s.b;
-        } else {
-            PcConsumer c;
-            c.b = b;
-            if (!fresh) sb = mono_stats(b);
-            c.sb = sb;
-            c.empt_b = emptiness(b);
-            for (int64_t j = 0; j <= nph; j++) {
-                if (j > 0) {
-                    const int h = (int)((j - 1) & 1);
-#pragma unroll 1
-                    for (int k = 0; k < kPcK; k++) {
-                        const int64_t t = (j - 1) * kPcK + k;
-                        if (t >= steps) break;
-                        const int64_t o = t * n;
-                        const TrajRows tr{tb + o, ta + o, tp + o, tpot + o, tf + o};
-                        pc_consume(c, ring_m + (h * kPcK + k) * kPcBoards + slot0,
-                                   ring_i + (h * kPcK + k) * kPcBoards + slot0, tr, li, active);
-                    }
-                }
-                __syncthreads();
-            }
-        }
     }
 }
 
@@ -1300,21 +1080,6 @@ int g2048_env_rollout_random(g2048_stream_t stream, int8_t *boards, int64_t n, i
     if (!boards || !traj_boards || !traj_actions || !traj_points || !traj_pot || !traj_flags || !aligned16(boards) ||
         !aligned16(traj_boards) || ((uintptr_t)traj_pot & 3u) || ((uintptr_t)traj_points & 3u))
         return G2048_EINVAL;
-    // Producer / consumer kernel (two waves per 64 boards) while it has all 256 CUs' worth of
-    // block-groups to itself; above G2048_PC_MAX_BOARDS boards the one-lane kernel already runs
-    // several waves per SIMD.  G2048_ROLLOUT_KERNEL=lane|pc overrides (tests, measurements).
-    static const int forced = [] {
-        const char *e = getenv("G2048_ROLLOUT_KERNEL");
-        return !e ? 0 : (e[0] == 'p' ? 1 : (e[0] == 'l' ? 2 : 0));
-    }();
-    if (forced == 1 || (forced == 0 && n <= kPcMaxBoards)) {
-        int64_t groups = (n + kPcBoards - 1) / kPcBoards;
-        groups = groups > 256 ? 256 : groups;
-        hipLaunchKernelGGL(env_rollout_pc_kernel, dim3((unsigned)groups), dim3(kPcThreads), 0, (hipStream_t)stream,
-                           (uint4 *)boards, n, steps, (uint4 *)traj_boards, traj_actions, traj_points,
-                           (uint32_t *)traj_pot, traj_flags, rng_args(rng));
-        return launch_status();
-    }
     // one workgroup per CU holds the 129 KiB LDS tables; its size scales with N up to 1024 threads
     // so that large N runs 4 waves per SIMD while N = 65 536 still spreads over all 256 CUs
     int64_t threads = (n + 255) / 256;
