@@ -1493,6 +1493,129 @@ inline bool wg_plan(int64_t m, int n1, int n2, WgPlan &p) {
 
 }  // namespace
 
+// ------------------------------------------------------------------ input gradient -----------
+// P = dG W  (the Linear input gradient, dG bf16 [m, n], W bf16 [n, k] = the layer weight [out, in],
+// P bf16 [m, k]) on bf16 MFMA in the forward kernels' orientation: P^T = W^T dG^T, so a lane's B
+// fragment is 16 contiguous bytes of one dG row and its result is 4 consecutive columns of one P
+// row (one 8-byte store).  W^T is staged once per block into LDS with a row pitch of 16 KS + 4
+// dwords (4 (4KS + 1), 4KS + 1 odd): the 16 rows a fragment read touches start on 16 distinct
+// 4-bank groups, so the ds_read_b128 of a wave is conflict-free.  A wave owns 32 rows of dG (two
+// B-fragment sets), so every W^T fragment read feeds two MFMAs.  KS = ceil(n / 32) k-steps,
+// CT = ceil(k / 16) output column tiles; m unbounded (persistent over row blocks).
+constexpr int kDgThreads = 512;
+
+template <int KS, int CT, int NH>  // NH 16-row halves of dG per wave (2 while the accumulators fit)
+__global__ __launch_bounds__(kDgThreads) void dgrad_kernel(const uint16_t *__restrict__ dg,
+                                                           const uint16_t *__restrict__ w,
+                                                           uint16_t *__restrict__ out, int64_t m, int n, int k) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int kPitch = 32 * KS + 8;  // bf16 elements per W^T row (16 KS + 4 dwords)
+    constexpr int kRowsT = 16 * CT;
+    uint16_t *wt = reinterpret_cast<uint16_t *>(smem);
+    const int tid = threadIdx.x;
+    // zero the padding (rows c >= k, columns j >= n), then W^T[c][j] = W[j][c] from 8-byte reads of
+    // W rows (k % 4 == 0), all of a thread's reads issued before its LDS writes
+    for (int e = tid; e < kRowsT * kPitch / 8; e += kDgThreads) reinterpret_cast<uint4 *>(smem)[e] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    {
+        const int k4 = k >> 2, total = n * k4;
+        constexpr int kU = 8;
+        for (int e0 = tid; e0 < total; e0 += kU * kDgThreads) {
+            uint2 v[kU];
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const int e = e0 + u * kDgThreads;
+                v[u] = e < total ? reinterpret_cast<const uint2 *>(w)[e] : make_uint2(0u, 0u);
+            }
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const int e = e0 + u * kDgThreads;
+                if (e >= total) break;
+                const int j = e / k4, c = 4 * (e - j * k4);
+                wt[(c + 0) * kPitch + j] = (uint16_t)(v[u].x & 0xFFFFu);
+                wt[(c + 1) * kPitch + j] = (uint16_t)(v[u].x >> 16);
+                wt[(c + 2) * kPitch + j] = (uint16_t)(v[u].y & 0xFFFFu);
+                wt[(c + 3) * kPitch + j] = (uint16_t)(v[u].y >> 16);
+            }
+        }
+    }
+    __syncthreads();
+    const int lane = tid & 63, wave = tid >> 6, rt = lane & 15, g = lane >> 4;
+    const int64_t stride = (int64_t)gridDim.x * (kDgThreads / 64) * 16 * NH;
+    for (int64_t rb = ((int64_t)blockIdx.x * (kDgThreads / 64) + wave) * 16 * NH; rb < m; rb += stride) {
+        bf16x8_t fb[NH][KS];
+#pragma unroll
+        for (int h = 0; h < NH; h++) {
+            const int64_t r = rb + 16 * h + rt;
+            const uint16_t *row = dg + (r < m ? r : 0) * (int64_t)n;
+#pragma unroll
+            for (int s = 0; s < KS; s++) {
+                const int kk = 32 * s + 8 * g;
+                uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                if (r < m) {
+                    if (kk + 8 <= n) {
+                        v = *reinterpret_cast<const uint4 *>(row + kk);
+                    } else if (kk < n) {  // n % 4 == 0: a 4-element tail
+                        const uint2 t = *reinterpret_cast<const uint2 *>(row + kk);
+                        v = make_uint4(t.x, t.y, 0u, 0u);
+                    }
+                }
+                fb[h][s] = __builtin_bit_cast(bf16x8_t, v);
+            }
+        }
+        f32x4_t acc[NH][CT];
+#pragma unroll
+        for (int h = 0; h < NH; h++)
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) acc[h][ct] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+        // W^T fragments one column tile ahead of the MFMAs; the empty asm with a memory clobber keeps
+        // the compiler from hoisting every tile's LDS reads to the top (which spills)
+        const char *base = smem + (rt * kPitch + 8 * g) * 2;
+        bf16x8_t fa[2][KS];
+#pragma unroll
+        for (int s = 0; s < KS; s++) fa[0][s] = *reinterpret_cast<const bf16x8_t *>(base + 64 * s);
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) {
+            if (ct + 1 < CT) {
+#pragma unroll
+                for (int s = 0; s < KS; s++)
+                    fa[(ct + 1) & 1][s] = *reinterpret_cast<const bf16x8_t *>(base + (16 * (ct + 1) * kPitch) * 2 + 64 * s);
+            }
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int s = 0; s < KS; s++)
+#pragma unroll
+                for (int h = 0; h < NH; h++)
+                    acc[h][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ct & 1][s], fb[h][s], acc[h][ct], 0, 0, 0);
+        }
+        // lane (col = row rt of half h, rows 4g .. 4g+3 of tile ct): P[r][16 ct + 4g .. +3]
+#pragma unroll
+        for (int h = 0; h < NH; h++) {
+            const int64_t r = rb + 16 * h + rt;
+            if (r >= m) continue;
+            uint16_t *orow = out + r * (int64_t)k;
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) {
+                const int c = 16 * ct + 4 * g;
+                if (c < k)
+                    *reinterpret_cast<uint2 *>(orow + c) = make_uint2(pack_bf2(acc[h][ct][0], acc[h][ct][1]),
+                                                                     pack_bf2(acc[h][ct][2], acc[h][ct][3]));
+            }
+        }
+    }
+}
+
+template <int KS, int CT, int NH>
+int launch_dgrad(hipStream_t s, const uint16_t *dg, const uint16_t *w, uint16_t *out, int64_t m, int n, int k) {
+    const size_t lds = (size_t)16 * CT * (32 * KS + 8) * 2;
+    const int64_t rows_per_block = (kDgThreads / 64) * 16 * NH;
+    int64_t blocks = (m + rows_per_block - 1) / rows_per_block;
+    blocks = blocks > 256 ? 256 : blocks;  // persistent: one block per CU holds W^T
+    hipLaunchKernelGGL((dgrad_kernel<KS, CT, NH>), dim3((unsigned)blocks), dim3(kDgThreads), lds, s, dg, w, out, m, n, k);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK : (int)e;
+}
+
 extern "C" {
 
 int g2048_obs_gather(g2048_stream_t stream, const int8_t *boards, const int64_t *idx, int64_t m, uint16_t *obs) {
@@ -1836,6 +1959,27 @@ int g2048_dropout_mask(g2048_stream_t stream, int64_t m, int32_t h, const g2048_
     hipLaunchKernelGGL(dropout_mask_kernel, dim3((unsigned)((m * (h / 4) + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, m, h, da, mask);
     return status();
+}
+
+
+int g2048_linear_dgrad_supported(int32_t n, int32_t k) {
+    // the shapes where it beats the library GEMM (m = 65 536: 7.8 / 15.0 / 25.0 us vs 19.9 / 19.8 /
+    // 42.5 us; at h = 256 hipBLASLt's power-of-two tiles win, 20.9 vs 34.9 us -- tools/time_dgrad.py)
+    auto ok = [](int32_t x) { return x == 64 || x == 128 || x == 196; };
+    return n == k && ok(n) ? 1 : 0;
+}
+
+int g2048_linear_dgrad(g2048_stream_t stream, const uint16_t *dg, const uint16_t *w, uint16_t *out, int64_t m,
+                       int32_t n, int32_t k) {
+    if (m < 0 || !g2048_linear_dgrad_supported(n, k)) return G2048_EINVAL;
+    if (m == 0) return G2048_OK;
+    if (!dg || !w || !out || ((uintptr_t)dg | (uintptr_t)out) % 8 || (uintptr_t)w % 2) return G2048_EINVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    switch (n) {
+        case 64: return launch_dgrad<2, 4, 2>(s, dg, w, out, m, n, k);
+        case 128: return launch_dgrad<4, 8, 2>(s, dg, w, out, m, n, k);
+        default: return launch_dgrad<7, 13, 1>(s, dg, w, out, m, n, k);
+    }
 }
 
 }  // extern "C"

@@ -31,7 +31,7 @@ EXPORTED = (
     # include/g2048_ppo.h
     "g2048_obs_gather", "g2048_ln_act_fwd", "g2048_ln_act_bwd_partials", "g2048_ln_act_bwd",
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
-    "g2048_wgrad_partials", "g2048_wgrad",
+    "g2048_wgrad_partials", "g2048_wgrad", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
@@ -188,6 +188,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_policy_rollout_supported": (ctypes.c_int, [i32, i32]),
         "g2048_policy_rollout_lds_bytes": (sz, [i32]),
         "g2048_policy_rollout": (ctypes.c_int, [vp, ctypes.POINTER(PolicyRolloutArgs)]),
+        "g2048_linear_dgrad_supported": (ctypes.c_int, [i32, i32]),
+        "g2048_linear_dgrad": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_stem": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, i64, i32]),
         "g2048_urm_attention": (ctypes.c_int, [vp, vp, vp, i64, i32, i32]),
         "g2048_urm_residual_rms": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, ctypes.c_float]),
@@ -538,6 +540,20 @@ def head_fwd(x, wa, ba, wv, bv, logits, value):
         _stream(x), _dev(x, torch.bfloat16, "x"), _dev(wa, torch.float32, "wa"), _dev(ba, torch.float32, "ba"),
         _dev(wv, torch.float32, "wv"), _dev(bv, torch.float32, "bv"), m, h, ctypes.c_void_p(logits.data_ptr()),
         logits.stride(0), _dev(value, torch.float32, "value")), "g2048_head_fwd")
+
+
+def linear_dgrad_supported(n: int, k: int) -> bool:
+    return bool(load().g2048_linear_dgrad_supported(int(n), int(k)))
+
+
+def linear_dgrad(dg, w, out):
+    """out = dg @ w on bf16 MFMA (dg [m, n], w [n, k] the Linear weight, out [m, k], all bf16)."""
+    m, n = dg.shape
+    k = w.shape[1]
+    if w.shape[0] != n or out.shape != (m, k):
+        raise G2048Error("linear_dgrad: shape mismatch")
+    _check(load().g2048_linear_dgrad(_stream(dg), _dev(dg, torch.bfloat16, "dg"), _dev(w, torch.bfloat16, "w"),
+                                     _dev(out, torch.bfloat16, "out"), m, n, k), "g2048_linear_dgrad")
 
 
 def policy_rollout_supported(hidden: int, num_layers: int) -> bool:

@@ -96,6 +96,7 @@ class FusedPPOUpdater(PPOUpdater):
         self.P = [torch.empty(bs, h, dtype=bf, device=d) for _ in range(nl if self.keep_p else 1)]
         self.dres = None if self.keep_p else torch.empty(bs, h, dtype=torch.float32, device=d)
         self.wg_ok = [L.wgrad_partials(bs, w.shape[0], w.shape[1]) > 0 for w in self.lin]
+        self.dgrad_ok = [L.linear_dgrad_supported(w.shape[0], w.shape[1]) for w in self.lin]
         # per-reduction partial rows: every column sum of the backward is deferred into ONE
         # g2048_colsum_batch launch (and the KL's into the statistics kernel)
         f32 = torch.float32
@@ -169,8 +170,11 @@ class FusedPPOUpdater(PPOUpdater):
                 L.wgrad(self.dg, x_in, self.part_wg[l], self.lin[l].grad, defer=jobs[-1])
             else:
                 _mm(self.dg.t(), x_in, self.lin[l].grad)
-            if l > 0:
-                _mm(self.dg, self.wbf[l], self.P[l if self.keep_p else 0])
+            if l > 0:  # P_l = dG_l W_l, the input gradient, on the MFMA dgrad kernel (library GEMM otherwise)
+                if self.dgrad_ok[l]:
+                    L.linear_dgrad(self.dg, self.wbf[l], self.P[l if self.keep_p else 0])
+                else:
+                    _mm(self.dg, self.wbf[l], self.P[l if self.keep_p else 0])
         for i in range(0, len(jobs), L.COLSUM_MAX_JOBS):  # every deferred column sum, in one launch
             L.colsum_batch(jobs[i:i + L.COLSUM_MAX_JOBS])
 

@@ -46,6 +46,13 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak (spec)
 VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2  # wave-instructions/s: 1 024 SIMDs, one 64-lane VALU op per 2 cycles
+# what the step's instruction mix can reach: at 65 536 boards there is one wave per SIMD, and one
+# wave alone issues an independent VALU op per 4 cycles at best (MI355X_MICROARCH.md constants,
+# 'vector-instruction ISSUE cost'); a second wave does not double it for this VOP3-heavy mix
+# (v_bitop3 / v_perm / v_bcnt / v_pk_* / v_mad_u64 sustain ~4.6 cycles per wave-instruction per
+# SIMD with 2 or 4 waves, profiles/r01e/valu_rate.log; the producer/consumer two-wave split of the
+# rollout measured slower, profiles/r02d)
+VALU_SINGLE_WAVE_PEAK = 1024 * 2.4e9 / 4
 STEP_BYTES = 42  # SURVEY.md §8(d) algorithmic bytes per env-step: board in 16 + action 1 + board out 16
                  # + points 4 + flags 1 + pot 4 (the roofline basis)
 ROLLOUT_STEP_BYTES = 16 + 1 + 4 + 4 + 1  # bytes the fused rollout really writes per env-step
@@ -367,6 +374,7 @@ def rollout_roofline(rb, avg_launch_s, pmc):
                 "waves_per_simd": waves / 1024,
                 "cycles_per_valu_per_wave": avg_launch_s * 2.4e9 * min(1.0, 1024 / waves) / (vws * rb.chunk),
                 "achieved": rate, "peak": VALU_ISSUE_PEAK, "unit": "wave-instructions/s",
+                "single_wave_peak": VALU_SINGLE_WAVE_PEAK, "frac_single_wave": rate / VALU_SINGLE_WAVE_PEAK,
                 "frac": rate / VALU_ISSUE_PEAK, "source": pmc["source"]}
         if valu["frac"] > roof["frac"]:
             roof["bound"] = "valu"

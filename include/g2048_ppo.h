@@ -220,6 +220,14 @@ size_t g2048_wgrad_partials(int64_t m, int32_t n1, int32_t n2);
 int g2048_wgrad(g2048_stream_t stream, const uint16_t *a, const uint16_t *b, int64_t m, int32_t n1, int32_t n2,
                 float *partials, float *out, g2048_colsum_job *defer);
 
+/* Input gradient of a Linear layer: out = dg w  (dg bf16 [m, n] = dL/d(output), w bf16 [n, k] = the
+ * weight [out, in], out bf16 [m, k] = dL/d(input), fp32 accumulate on bf16 MFMA, one rounding)
+ * -- the `dG W` GEMM of the backward pass (replaces the library GEMM).  Square layers with
+ * n = k in {64, 128, 196} (where it beats the library); dg / out 8-byte aligned. */
+int g2048_linear_dgrad_supported(int32_t n, int32_t k);
+int g2048_linear_dgrad(g2048_stream_t stream, const uint16_t *dg, const uint16_t *w, uint16_t *out, int64_t m,
+                       int32_t n, int32_t k);
+
 /* ---- optimizer step (train.py:553-568, :1587-1612) ------------------------------------------ */
 
 /* clip_grad_norm_ of the flat gradient bucket, without touching it: norm_out = ||grad||,

@@ -775,3 +775,26 @@ def test_fused_update_minibatch4_matches_autograd(dev):
             continue
         cos = (a * b).sum().item() / (na * nb)
         assert cos >= 0.97 and abs(nb / na - 1) < 0.05, (name, cos, na, nb)
+
+
+@pytest.mark.parametrize("h,m", [(196, 65536), (196, 1000), (64, 4099), (128, 333), (196, 17)])
+def test_linear_dgrad_matches_matmul(dev, h, m):
+    """g2048_linear_dgrad (P = dG W on MFMA, the backward's input gradient) vs the fp32 product of the
+    same bf16 operands: within one bf16 rounding of the output (2^-8 relative) plus fp32
+    accumulation-order noise; rows beyond m untouched; deterministic."""
+    from g2048 import _lib as L
+    g = torch.Generator(device=dev).manual_seed(h + m)
+    dg = torch.randn(m, h, generator=g, device=dev).to(torch.bfloat16)
+    w = (torch.randn(h, h, generator=g, device=dev) / h ** 0.5).to(torch.bfloat16)
+    out = torch.full((m + 3, h), 7.0, dtype=torch.bfloat16, device=dev)
+    L.linear_dgrad(dg, w, out[:m])
+    ref = dg.float() @ w.float()
+    got = out[:m].float()
+    err = (got - ref).abs()
+    assert (err <= 2.0 ** -8 * ref.abs() + 1e-3).all(), err.max().item()
+    assert (out[m:] == 7.0).all()
+    again = torch.empty(m, h, dtype=torch.bfloat16, device=dev)
+    L.linear_dgrad(dg, w, again)
+    assert torch.equal(again, out[:m])
+    assert not L.linear_dgrad_supported(196, 48) and L.linear_dgrad_supported(196, 196)
+    assert not L.linear_dgrad_supported(256, 256)  # the library GEMM is faster there
