@@ -96,6 +96,9 @@ struct MuonArgs {
     int steps, nesterov;
     const float *lr;
     const float *clip;
+    const float *partials;  // non-null: clip coefficient from the grad_sumsq partials (grad_norm folded in)
+    float max_norm;
+    float *norm_out, *coef_out;  // written by block 0 when partials is set
 };
 
 // LDS images are row-major bf16 with the K dimension zero-padded to a multiple of 8 (pitch =
@@ -204,28 +207,40 @@ __device__ __forceinline__ float muon_prologue(const float *__restrict__ grad, f
                                                int tid) {
     const int n4 = (R * C) >> 2;
     float ss = 0.0f;
-#pragma unroll 4
-    for (int e4 = tid; e4 < n4; e4 += kMuonThreads) {
-        const float4 g4 = reinterpret_cast<const float4 *>(grad)[e4];
-        const float4 b4 = reinterpret_cast<const float4 *>(mom)[e4];
-        const float gv[4] = {g4.x * coef, g4.y * coef, g4.z * coef, g4.w * coef};
-        float bv[4] = {b4.x, b4.y, b4.z, b4.w};
-        const int i = (4 * e4) / C, j0 = 4 * e4 - i * C;  // C % 4 == 0: a float4 stays in one row
-        float ub[4];
+    // kB float4 of the gradient and of the momentum in flight per thread before any is used: one
+    // HBM round trip per batch instead of one per element group (a single CU streams the matrix)
+    constexpr int kB = 6;
+    for (int base = tid; base < n4; base += kB * kMuonThreads) {
+        float4 g4[kB], b4[kB];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            bv[u] = bv[u] + (1.0f - mu) * (gv[u] - bv[u]);                               // buf.lerp_(g, 1 - mu)
-            const float up = nesterov ? bv[u] - (bv[u] - gv[u]) * (1.0f - mu) : bv[u];  // g.lerp(buf, mu)
-            ub[u] = round_bf(up);
-            ss += ub[u] * ub[u];
+        for (int u = 0; u < kB; u++) {
+            const int e4 = base + u * kMuonThreads;
+            g4[u] = e4 < n4 ? reinterpret_cast<const float4 *>(grad)[e4] : make_float4(0.f, 0.f, 0.f, 0.f);
+            b4[u] = e4 < n4 ? reinterpret_cast<const float4 *>(mom)[e4] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        if (tr) {
 #pragma unroll
-            for (int u = 0; u < 4; u++) reinterpret_cast<uint16_t *>(sX + (j0 + u) * px)[i] = (uint16_t)f2bf(ub[u]);
-        } else {
-            *reinterpret_cast<uint2 *>(sX + i * px + 2 * j0) = make_uint2(pack_bf2(ub[0], ub[1]), pack_bf2(ub[2], ub[3]));
+        for (int v = 0; v < kB; v++) {
+            const int e4 = base + v * kMuonThreads;
+            if (e4 >= n4) break;
+            const float gv[4] = {g4[v].x * coef, g4[v].y * coef, g4[v].z * coef, g4[v].w * coef};
+            float bv[4] = {b4[v].x, b4[v].y, b4[v].z, b4[v].w};
+            const int i = (4 * e4) / C, j0 = 4 * e4 - i * C;  // C % 4 == 0: a float4 stays in one row
+            float ub[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                bv[u] = bv[u] + (1.0f - mu) * (gv[u] - bv[u]);                               // buf.lerp_(g, 1 - mu)
+                const float up = nesterov ? bv[u] - (bv[u] - gv[u]) * (1.0f - mu) : bv[u];  // g.lerp(buf, mu)
+                ub[u] = round_bf(up);
+                ss += ub[u] * ub[u];
+            }
+            if (tr) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) reinterpret_cast<uint16_t *>(sX + (j0 + u) * px)[i] = (uint16_t)f2bf(ub[u]);
+            } else {
+                *reinterpret_cast<uint2 *>(sX + i * px + 2 * j0) = make_uint2(pack_bf2(ub[0], ub[1]), pack_bf2(ub[2], ub[3]));
+            }
+            reinterpret_cast<float4 *>(mom)[e4] = make_float4(bv[0], bv[1], bv[2], bv[3]);
         }
-        reinterpret_cast<float4 *>(mom)[e4] = make_float4(bv[0], bv[1], bv[2], bv[3]);
     }
     return ss;
 }
@@ -233,26 +248,36 @@ __device__ __forceinline__ float muon_prologue(const float *__restrict__ grad, f
 __device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_t *__restrict__ pbf, const char *sX,
                                               int px, int R, int C, bool tr, float decay, float step, int tid) {
     const int n4 = (R * C) >> 2;
-#pragma unroll 4
-    for (int e4 = tid; e4 < n4; e4 += kMuonThreads) {
-        const float4 p4 = reinterpret_cast<const float4 *>(param)[e4];
-        float pv[4] = {p4.x, p4.y, p4.z, p4.w};
-        const int i = (4 * e4) / C, j0 = 4 * e4 - i * C;
-        float x[4];
-        if (tr) {
+    constexpr int kB = 8;
+    for (int base = tid; base < n4; base += kB * kMuonThreads) {
+        float4 p4[kB];
 #pragma unroll
-            for (int u = 0; u < 4; u++) x[u] = bf2f(reinterpret_cast<const uint16_t *>(sX + (j0 + u) * px)[i]);
-        } else {
-            const uint2 w = *reinterpret_cast<const uint2 *>(sX + i * px + 2 * j0);
-            x[0] = bf2f(w.x & 0xFFFFu);
-            x[1] = bf2f(w.x >> 16);
-            x[2] = bf2f(w.y & 0xFFFFu);
-            x[3] = bf2f(w.y >> 16);
+        for (int u = 0; u < kB; u++) {
+            const int e4 = base + u * kMuonThreads;
+            p4[u] = e4 < n4 ? reinterpret_cast<const float4 *>(param)[e4] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) pv[u] = pv[u] * decay - x[u] * step;
-        reinterpret_cast<float4 *>(param)[e4] = make_float4(pv[0], pv[1], pv[2], pv[3]);
-        if (pbf) reinterpret_cast<uint2 *>(pbf)[e4] = make_uint2(pack_bf2(pv[0], pv[1]), pack_bf2(pv[2], pv[3]));
+        for (int v = 0; v < kB; v++) {
+            const int e4 = base + v * kMuonThreads;
+            if (e4 >= n4) break;
+            float pv[4] = {p4[v].x, p4[v].y, p4[v].z, p4[v].w};
+            const int i = (4 * e4) / C, j0 = 4 * e4 - i * C;
+            float x[4];
+            if (tr) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) x[u] = bf2f(reinterpret_cast<const uint16_t *>(sX + (j0 + u) * px)[i]);
+            } else {
+                const uint2 w = *reinterpret_cast<const uint2 *>(sX + i * px + 2 * j0);
+                x[0] = bf2f(w.x & 0xFFFFu);
+                x[1] = bf2f(w.x >> 16);
+                x[2] = bf2f(w.y & 0xFFFFu);
+                x[3] = bf2f(w.y >> 16);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) pv[u] = pv[u] * decay - x[u] * step;
+            reinterpret_cast<float4 *>(param)[e4] = make_float4(pv[0], pv[1], pv[2], pv[3]);
+            if (pbf) reinterpret_cast<uint2 *>(pbf)[e4] = make_uint2(pack_bf2(pv[0], pv[1]), pack_bf2(pv[2], pv[3]));
+        }
     }
 }
 
@@ -277,7 +302,25 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     }
     __syncthreads();
 
-    const float coef = args.clip ? *args.clip : 1.0f;
+    __shared__ float s_coef;
+    if (args.partials) {  // grad_norm_kernel's arithmetic, in every block (same order, same result)
+        if (wave == 0) {
+            float t = args.partials[lane];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+            const float nrm = sqrtf(t);
+            const float cf = fminf(args.max_norm / (nrm + 1e-6f), 1.0f);
+            if (lane == 0) {
+                s_coef = cf;
+                if (blockIdx.x == 0) {
+                    *args.norm_out = nrm;
+                    *args.coef_out = cf;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const float coef = args.partials ? s_coef : (args.clip ? *args.clip : 1.0f);
     float ss = muon_prologue(mt.grad, mt.mom, sX, px, R, C, tr, coef, args.momentum, args.nesterov != 0, tid);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
@@ -402,8 +445,31 @@ int g2048_muon_supported(int32_t rows, int32_t cols) {
     return muon_lds_bytes(rows, cols) <= (size_t)kMuonLds ? 1 : 0;
 }
 
+int g2048_grad_sumsq(g2048_stream_t stream, const float *grad, int64_t n, float *partials) {
+    if (!grad || !partials || n <= 0 || ((uintptr_t)grad & 15u)) return G2048_EINVAL;
+    hipLaunchKernelGGL(grad_sumsq_kernel, dim3(kNormBlocks), dim3(256), 0, (hipStream_t)stream, grad, n, partials);
+    return status();
+}
+
+static int muon_launch(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_t count, const float *lr_dev,
+                       const float *clip_coef_dev, const float *partials, float max_norm, float *norm_out,
+                       float *coef_out, const g2048_muon_cfg *cfg);
+
 int g2048_muon_step(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_t count, const float *lr_dev,
                     const float *clip_coef_dev, const g2048_muon_cfg *cfg) {
+    return muon_launch(stream, mats, count, lr_dev, clip_coef_dev, nullptr, 0.0f, nullptr, nullptr, cfg);
+}
+
+int g2048_muon_step_clip(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_t count, const float *lr_dev,
+                         const float *partials, float max_norm, float *norm_out, float *coef_out,
+                         const g2048_muon_cfg *cfg) {
+    if (!partials || !norm_out || !coef_out) return G2048_EINVAL;
+    return muon_launch(stream, mats, count, lr_dev, nullptr, partials, max_norm, norm_out, coef_out, cfg);
+}
+
+static int muon_launch(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_t count, const float *lr_dev,
+                       const float *clip_coef_dev, const float *partials, float max_norm, float *norm_out,
+                       float *coef_out, const g2048_muon_cfg *cfg) {
     if (!mats || count <= 0 || count > kMuonMaxMats || !lr_dev || !cfg) return G2048_EINVAL;
     MuonArgs a{};
     size_t lds = 0;
@@ -427,6 +493,10 @@ int g2048_muon_step(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_
     a.nesterov = cfg->nesterov;
     a.lr = lr_dev;
     a.clip = clip_coef_dev;
+    a.partials = partials;
+    a.max_norm = max_norm;
+    a.norm_out = norm_out;
+    a.coef_out = coef_out;
     hipLaunchKernelGGL(muon_kernel, dim3(count), dim3(kMuonThreads), lds, (hipStream_t)stream, a);
     return status();
 }

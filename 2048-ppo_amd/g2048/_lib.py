@@ -33,6 +33,7 @@ EXPORTED = (
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
+    "g2048_grad_sumsq", "g2048_muon_step_clip",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
     # include/g2048_urm.h
@@ -197,6 +198,9 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_urm_pool_heads": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32]),
         "g2048_muon_supported": (ctypes.c_int, [i32, i32]),
         "g2048_muon_step": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.POINTER(MuonCfg)]),
+        "g2048_grad_sumsq": (ctypes.c_int, [vp, vp, i64, vp]),
+        "g2048_muon_step_clip": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.c_float, vp, vp,
+                                                ctypes.POINTER(MuonCfg)]),
         "g2048_adamw_step": (ctypes.c_int, [vp, ctypes.POINTER(AdamWGroup), i32, vp, vp, vp, ctypes.c_float,
                                             ctypes.c_float, ctypes.c_float, ctypes.c_float]),
     }
@@ -508,6 +512,19 @@ def muon_step(mats, lr_dev, clip_coef_dev, cfg: MuonCfg, stream_tensor):
     """mats: a ctypes array of MuonMatrix (built once; device pointers stay valid)."""
     _check(load().g2048_muon_step(_stream(stream_tensor), mats, len(mats), _dev(lr_dev, torch.float32, "lr"),
                                   _dev(clip_coef_dev, torch.float32, "clip"), ctypes.byref(cfg)), "g2048_muon_step")
+
+
+def grad_sumsq(grad, partials):
+    _check(load().g2048_grad_sumsq(_stream(grad), _dev(grad, torch.float32, "grad"), grad.numel(),
+                                   _dev(partials, torch.float32, "partials")), "g2048_grad_sumsq")
+
+
+def muon_step_clip(mats, lr_dev, partials, max_norm: float, norm_out, coef_out, cfg: MuonCfg):
+    """Muon with the gradient clip folded in (partials from grad_sumsq; norm / coef published)."""
+    _check(load().g2048_muon_step_clip(_stream(lr_dev), mats, len(mats), _dev(lr_dev, torch.float32, "lr"),
+                                       _dev(partials, torch.float32, "partials"), float(max_norm),
+                                       _dev(norm_out, torch.float32, "norm_out"), _dev(coef_out, torch.float32, "coef_out"),
+                                       ctypes.byref(cfg)), "g2048_muon_step_clip")
 
 
 def adamw_step(groups, lr_dev, step_dev, clip_coef_dev, beta1, beta2, eps, weight_decay):

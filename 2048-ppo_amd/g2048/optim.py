@@ -241,11 +241,14 @@ class FusedMuonAdamW(MuonAdamW):
                                      grp["flat"].numel(), grp["idx"], 0)
         self._mats, self._groups = mats, groups
 
-    def _run(self, clip):
+    def _run(self, clip, max_norm=None):
         if self._mats is None:
             self._build()
         L = self._L
-        L.muon_step(self._mats, self.lr, clip, self._cfg, self.lr)
+        if max_norm is None:
+            L.muon_step(self._mats, self.lr, clip, self._cfg, self.lr)
+        else:  # the clip coefficient is computed inside the Muon launch from the grad_sumsq partials
+            L.muon_step_clip(self._mats, self.lr, self.norm_part, max_norm, self.norm_t, self.coef_t, self._cfg)
         self.step_t.add_(1)
         if len(self._groups):
             L.adamw_step(self._groups, self.lr, self.step_t, clip, self.b1, self.b2, self.eps, self.wd)
@@ -260,8 +263,8 @@ class FusedMuonAdamW(MuonAdamW):
     def step_clipped(self, flat_grad: torch.Tensor, max_norm: float) -> torch.Tensor:
         """clip_grad_norm_(max_norm) folded into the step (the bucket itself is left unclipped);
         returns the pre-clip norm as a device scalar."""
-        self._L.grad_clip(flat_grad, max_norm, self.norm_t, self.coef_t, self.norm_part)
-        self._run(self.coef_t)
+        self._L.grad_sumsq(flat_grad, self.norm_part)
+        self._run(self.coef_t, max_norm)
         return self.norm_t
 
 

@@ -262,6 +262,15 @@ int g2048_muon_supported(int32_t rows, int32_t cols);
 int g2048_muon_step(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_t count, const float *lr_dev,
                     const float *clip_coef_dev, const g2048_muon_cfg *cfg);
 
+/* The clip folded into the Muon launch (one launch fewer per optimizer step): g2048_grad_sumsq
+ * writes the 64 partial sums of squares of the flat gradient; g2048_muon_step_clip then computes
+ * ||g|| and the clip coefficient from them in every block exactly like g2048_grad_clip, block 0
+ * publishes them to norm_out / coef_out (device scalars read by g2048_adamw_step after it). */
+int g2048_grad_sumsq(g2048_stream_t stream, const float *grad, int64_t n, float *partials);
+int g2048_muon_step_clip(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_t count, const float *lr_dev,
+                         const float *partials, float max_norm, float *norm_out, float *coef_out,
+                         const g2048_muon_cfg *cfg);
+
 /* One flat group of 1-D parameters for AdamW (torch.optim.AdamW, decoupled weight decay). */
 typedef struct g2048_adamw_group {
     float *param;
