@@ -8,9 +8,10 @@
 //                      registers + two cross-lane steps (xor 16, xor 32);
 //                      O^T = V^T P^T -> the P fragment a lane holds is exactly its B operand
 //                      (B[k = key][n = query]), no shuffles; lane (i, g) gets O[i][4g .. 4g+3].
-//   residual_rms     one wave per row: x = rms_norm(x + y) [+ emb], bf16 copy for the next GEMM
-//   swiglu_conv      one thread per (board, channel): SiLU(gate)*up, the kernel-2 depthwise conv
-//                    along the board's 16 tokens carried in a register, SiLU
+//   residual_rms     x = rms_norm(x + y) [+ emb], bf16 copy for the next GEMM: h / 4 lanes per
+//                    row (rounded to a power of two), 4 columns per lane, 64 / P rows per wave
+//   swiglu_conv      one thread per (board, channel pair): SiLU(gate)*up, the kernel-2 depthwise
+//                    conv along the board's 16 tokens carried in registers, SiLU
 //   pool_heads       one wave per board: mean over the 16 tokens, action / value heads
 //
 // fp32 arithmetic throughout (bf16 only as GEMM operands / attention probabilities, like torch's
@@ -95,6 +96,7 @@ __global__ __launch_bounds__(kThreads) void urm_stem_kernel(const void *__restri
     }
 }
 
+template <bool kAligned>
 __global__ __launch_bounds__(kThreads) void urm_attn_kernel(const uint16_t *__restrict__ qkv,
                                                             uint16_t *__restrict__ out, int64_t tasks, int h,
                                                             int heads) {
@@ -112,11 +114,19 @@ __global__ __launch_bounds__(kThreads) void urm_attn_kernel(const uint16_t *__re
     f32x4 st = {0.0f, 0.0f, 0.0f, 0.0f};
     for (int d0 = 0; d0 < hd; d0 += 16) {
         s16x4 ka, qb;
+        const int dq = d0 + 4 * g;
+        if (kAligned) {  // 4 | head_dim: a fragment is one 8-byte load (or entirely padding)
+            const uint2 kv = dq < hd ? *reinterpret_cast<const uint2 *>(krow + dq) : make_uint2(0u, 0u);
+            const uint2 qv = dq < hd ? *reinterpret_cast<const uint2 *>(qrow + dq) : make_uint2(0u, 0u);
+            ka = __builtin_bit_cast(s16x4, kv);
+            qb = __builtin_bit_cast(s16x4, qv);
+        } else {
 #pragma unroll
-        for (int jj = 0; jj < 4; jj++) {
-            const int d = d0 + 4 * g + jj;
-            ka[jj] = d < hd ? (short)krow[d] : (short)0;
-            qb[jj] = d < hd ? (short)qrow[d] : (short)0;
+            for (int jj = 0; jj < 4; jj++) {
+                const int d = dq + jj;
+                ka[jj] = d < hd ? (short)krow[d] : (short)0;
+                qb[jj] = d < hd ? (short)qrow[d] : (short)0;
+            }
         }
         st = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ka, qb, st, 0, 0, 0);
     }
@@ -155,10 +165,15 @@ __global__ __launch_bounds__(kThreads) void urm_attn_kernel(const uint16_t *__re
         f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
         o = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, pb, o, 0, 0, 0);
         // lane (i, g): o[r] = O^T[d0 + 4g + r][i] = O[i][d0 + 4g + r]
+        const int dd = d0 + 4 * g;
+        if (kAligned) {
+            if (dd < hd)
+                *reinterpret_cast<uint2 *>(orow + dd) = make_uint2((uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16),
+                                                                   (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16));
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int dd = d0 + 4 * g + r;
-            if (dd < hd) orow[dd] = f2bf(o[r]);
+            for (int r = 0; r < 4; r++)
+                if (dd + r < hd) orow[dd + r] = f2bf(o[r]);
         }
     }
 }
@@ -189,6 +204,66 @@ __global__ __launch_bounds__(kThreads) void urm_residual_rms_kernel(float *__res
         if (emb) o += emb[row * h + c];
         x[row * h + c] = o;
         xb[row * h + c] = f2bf(o);
+    }
+}
+
+// h <= 256: P = pow2 >= h / 4 lanes per row (4 consecutive columns each, 16-byte fp32 / 8-byte
+// bf16 accesses), 64 / P rows per wave, the row reduction a P-lane butterfly
+template <int P>
+__global__ __launch_bounds__(kThreads) void urm_residual_rms_vec_kernel(float *__restrict__ x,
+                                                                        const uint16_t *__restrict__ y,
+                                                                        const float *__restrict__ emb,
+                                                                        uint16_t *__restrict__ xb, int64_t rows, int h,
+                                                                        float eps) {
+    const int lane = threadIdx.x & 63, sub = lane & (P - 1);
+    const int64_t row = ((int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) * (64 / P) + lane / P;
+    const int c = 4 * sub;
+    const bool on = row < rows && c < h;
+    const int64_t o = row * h + c;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (on) {
+        const float4 a = *reinterpret_cast<const float4 *>(x + o);
+        const uint2 b = *reinterpret_cast<const uint2 *>(y + o);
+        v = make_float4(a.x + bf2f(b.x & 0xFFFFu), a.y + bf2f(b.x >> 16), a.z + bf2f(b.y & 0xFFFFu), a.w + bf2f(b.y >> 16));
+    }
+    float ss = (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+#pragma unroll
+    for (int s = P / 2; s > 0; s >>= 1) ss += __shfl_xor(ss, s, 64);
+    const float r = rsqrtf(ss / (float)h + eps);
+    if (!on) return;
+    float4 out = make_float4(v.x * r, v.y * r, v.z * r, v.w * r);
+    if (emb) {
+        const float4 e = *reinterpret_cast<const float4 *>(emb + o);
+        out = make_float4(out.x + e.x, out.y + e.y, out.z + e.z, out.w + e.w);
+    }
+    *reinterpret_cast<float4 *>(x + o) = out;
+    *reinterpret_cast<uint2 *>(xb + o) = make_uint2((uint32_t)f2bf(out.x) | ((uint32_t)f2bf(out.y) << 16),
+                                                    (uint32_t)f2bf(out.z) | ((uint32_t)f2bf(out.w) << 16));
+}
+
+// two channels per thread (inter % 8 == 0): 4-byte bf16 pairs
+__global__ __launch_bounds__(kThreads) void urm_swiglu_conv2_kernel(const uint16_t *__restrict__ gu,
+                                                                    const float *__restrict__ w,
+                                                                    const float *__restrict__ bias,
+                                                                    uint16_t *__restrict__ out, int64_t n, int inter) {
+    const int half = inter >> 1;
+    const int64_t idx = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (idx >= n * half) return;
+    const int64_t b = idx / half;
+    const int c = 2 * (int)(idx - b * half);
+    const float4 wc = *reinterpret_cast<const float4 *>(w + 2 * c);  // w[c][0], w[c][1], w[c+1][0], w[c+1][1]
+    const float b0 = bias[c], b1 = bias[c + 1];
+    float p0 = 0.0f, p1 = 0.0f;
+    for (int t = 0; t < 16; t++) {
+        const int64_t row = b * 16 + t;
+        const uint32_t g2 = *reinterpret_cast<const uint32_t *>(gu + row * (2 * inter) + c);
+        const uint32_t u2 = *reinterpret_cast<const uint32_t *>(gu + row * (2 * inter) + inter + c);
+        const float a0 = silu(bf2f(g2 & 0xFFFFu)) * bf2f(u2 & 0xFFFFu);
+        const float a1 = silu(bf2f(g2 >> 16)) * bf2f(u2 >> 16);
+        const float c0 = fmaf(wc.y, a0, fmaf(wc.x, p0, b0)), c1 = fmaf(wc.w, a1, fmaf(wc.z, p1, b1));
+        *reinterpret_cast<uint32_t *>(out + row * inter + c) = (uint32_t)f2bf(silu(c0)) | ((uint32_t)f2bf(silu(c1)) << 16);
+        p0 = a0;
+        p1 = a1;
     }
 }
 
@@ -263,8 +338,12 @@ int g2048_urm_attention(g2048_stream_t stream, const uint16_t *qkv, uint16_t *ou
     if (n == 0) return G2048_OK;
     if (!qkv || !out) return G2048_EINVAL;
     const int64_t tasks = n * heads;
-    hipLaunchKernelGGL(urm_attn_kernel, dim3(blocks(tasks, kThreads / 64)), dim3(kThreads), 0, (hipStream_t)stream,
-                       qkv, out, tasks, (int)h, (int)heads);
+    if ((h / heads) % 4 == 0)
+        hipLaunchKernelGGL(urm_attn_kernel<true>, dim3(blocks(tasks, kThreads / 64)), dim3(kThreads), 0,
+                           (hipStream_t)stream, qkv, out, tasks, (int)h, (int)heads);
+    else
+        hipLaunchKernelGGL(urm_attn_kernel<false>, dim3(blocks(tasks, kThreads / 64)), dim3(kThreads), 0,
+                           (hipStream_t)stream, qkv, out, tasks, (int)h, (int)heads);
     return launch_status();
 }
 
@@ -273,8 +352,19 @@ int g2048_urm_residual_rms(g2048_stream_t stream, float *x, const uint16_t *y, c
     if (rows < 0 || !h_ok(h)) return G2048_EINVAL;
     if (rows == 0) return G2048_OK;
     if (!x || !y || !xb) return G2048_EINVAL;
-    hipLaunchKernelGGL(urm_residual_rms_kernel, dim3(blocks(rows, kThreads / 64)), dim3(kThreads), 0,
-                       (hipStream_t)stream, x, y, emb, xb, rows, (int)h, eps);
+    const hipStream_t s = (hipStream_t)stream;
+    if (h <= 64)
+        hipLaunchKernelGGL(urm_residual_rms_vec_kernel<16>, dim3(blocks(rows, 4 * (kThreads / 64))), dim3(kThreads), 0, s,
+                           x, y, emb, xb, rows, (int)h, eps);
+    else if (h <= 128)
+        hipLaunchKernelGGL(urm_residual_rms_vec_kernel<32>, dim3(blocks(rows, 2 * (kThreads / 64))), dim3(kThreads), 0, s,
+                           x, y, emb, xb, rows, (int)h, eps);
+    else if (h <= 256)
+        hipLaunchKernelGGL(urm_residual_rms_vec_kernel<64>, dim3(blocks(rows, kThreads / 64)), dim3(kThreads), 0, s, x,
+                           y, emb, xb, rows, (int)h, eps);
+    else
+        hipLaunchKernelGGL(urm_residual_rms_kernel, dim3(blocks(rows, kThreads / 64)), dim3(kThreads), 0, s, x, y, emb,
+                           xb, rows, (int)h, eps);
     return launch_status();
 }
 
@@ -283,8 +373,12 @@ int g2048_urm_swiglu_conv(g2048_stream_t stream, const uint16_t *gu, const float
     if (n < 0 || inter <= 0) return G2048_EINVAL;
     if (n == 0) return G2048_OK;
     if (!gu || !w || !b || !out) return G2048_EINVAL;
-    hipLaunchKernelGGL(urm_swiglu_conv_kernel, dim3(blocks(n * inter, kThreads)), dim3(kThreads), 0,
-                       (hipStream_t)stream, gu, w, b, out, n, (int)inter);
+    if (inter % 8 == 0)  // GameConvSwiGLU rounds inter up to a multiple of 8 (game.py:1248-1250)
+        hipLaunchKernelGGL(urm_swiglu_conv2_kernel, dim3(blocks(n * (inter / 2), kThreads)), dim3(kThreads), 0,
+                           (hipStream_t)stream, gu, w, b, out, n, (int)inter);
+    else
+        hipLaunchKernelGGL(urm_swiglu_conv_kernel, dim3(blocks(n * inter, kThreads)), dim3(kThreads), 0,
+                           (hipStream_t)stream, gu, w, b, out, n, (int)inter);
     return launch_status();
 }
 
