@@ -312,6 +312,202 @@ __global__ __launch_bounds__(kThreads) void urm_pool_heads_kernel(const float *_
     if (lane == 4) value[b] = acc[4] + bv[0];
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Projections with their epilogues fused (h <= 64, the default GameURMConfig): Y^T = W X^T on
+// v_mfma_f32_16x16x32_bf16 in the orientation of the MLP kernels -- a wave takes ONE board (its 16
+// token rows are the 16 MFMA columns; B fragment = 16 contiguous bytes of a token row), W [N, K]
+// is staged once per block in LDS (row pitch 16 KS + 4 dwords: conflict-free fragment reads), and
+// the lane holding token t gets 4 consecutive output features of it per column tile:
+//   EPI_STORE  qkv_proj:                    y bf16 [rows, N]
+//   EPI_RMS    o_proj / down_proj:          x = rms_norm(x + y) [+ emb], xb = bf16(x) -- the row's
+//              N features sit in the 4 lanes (g = 0..3) of token t: two cross-lane steps
+//   EPI_SWIGLU gate_up_proj:                W's rows staged so gate feature c and up feature c land
+//              in the same lane and register (tiles ct and ct + CT/2); a = SiLU(gate) * up, the
+//              token t-1 value of the same channel from the lane one to the left within its
+//              16-lane DPP row (row_shr:1; token 0 gets the conv's zero padding), then
+//              SiLU(w0 a_{t-1} + w1 a_t + b) -> act bf16 [rows, inter]
+// The projection outputs stay fp32 into the epilogue (no bf16 round trip through HBM).
+enum { EPI_STORE = 0, EPI_RMS = 1, EPI_SWIGLU = 2 };
+
+__device__ __forceinline__ float dpp_prev_token(float v) {  // lane t-1 of the 16-lane row, 0 for t = 0
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xF, 0xF, false));
+}
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <int KS, int CT, int EPI>
+__global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__restrict__ in,
+                                                              const uint16_t *__restrict__ w, int64_t rows, int K,
+                                                              int N, int inter, uint16_t *__restrict__ y,
+                                                              float *__restrict__ x, const float *__restrict__ emb,
+                                                              uint16_t *__restrict__ xb, float eps,
+                                                              const float *__restrict__ cw,
+                                                              const float *__restrict__ cb) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int kPitch = 32 * KS + 8;  // bf16 per staged row
+    constexpr int kRowsW = 16 * CT;
+    const int tid = threadIdx.x;
+    for (int e = tid; e < kRowsW * kPitch / 8; e += kThreads) reinterpret_cast<uint4 *>(smem)[e] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    {   // staged row q <- W row src(q) (EPI_SWIGLU: gate rows at q < kRowsW / 2, up rows above)
+        const int k4 = K >> 2;
+        for (int e = tid; e < kRowsW * k4; e += kThreads) {
+            const int q = e / k4, c4 = e - q * k4;
+            int src = q;
+            if (EPI == EPI_SWIGLU) {
+                const int hq = q - kRowsW / 2;
+                src = q < kRowsW / 2 ? (q < inter ? q : -1) : (hq < inter ? inter + hq : -1);
+            } else if (q >= N) {
+                src = -1;
+            }
+            if (src >= 0)
+                *reinterpret_cast<uint2 *>(smem + (q * kPitch + 4 * c4) * 2) =
+                    *reinterpret_cast<const uint2 *>(w + (int64_t)src * K + 4 * c4);
+        }
+    }
+    __syncthreads();
+    const int lane = tid & 63, wave = tid >> 6, t = lane & 15, g = lane >> 4;
+    const int64_t boards = rows >> 4;
+    for (int64_t bd = (int64_t)blockIdx.x * (kThreads / 64) + wave; bd < boards; bd += (int64_t)gridDim.x * (kThreads / 64)) {
+        const int64_t r = bd * 16 + t;
+        const uint16_t *xr = in + r * K;
+        bf16x8 fb[KS];
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+            const int kk = 32 * s + 8 * g;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (kk + 8 <= K) {
+                v = *reinterpret_cast<const uint4 *>(xr + kk);
+            } else if (kk < K) {  // K % 4 == 0: a 4-element tail
+                const uint2 tl = *reinterpret_cast<const uint2 *>(xr + kk);
+                v = make_uint4(tl.x, tl.y, 0u, 0u);
+            }
+            fb[s] = __builtin_bit_cast(bf16x8, v);
+        }
+        f32x4 acc[CT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) acc[ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        const char *base = smem + (t * kPitch + 8 * g) * 2;
+        bf16x8 fa[2][KS];
+#pragma unroll
+        for (int s = 0; s < KS; s++) fa[0][s] = *reinterpret_cast<const bf16x8 *>(base + 64 * s);
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) {
+            if (ct + 1 < CT) {
+#pragma unroll
+                for (int s = 0; s < KS; s++)
+                    fa[(ct + 1) & 1][s] = *reinterpret_cast<const bf16x8 *>(base + 16 * (ct + 1) * kPitch * 2 + 64 * s);
+            }
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int s = 0; s < KS; s++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ct & 1][s], fb[s], acc[ct], 0, 0, 0);
+        }
+        // lane (t, g), tile ct: acc[ct][i] = Y[r][16 ct + 4 g + i]
+        if constexpr (EPI == EPI_STORE) {
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) {
+                const int c = 16 * ct + 4 * g;
+                if (c < N)
+                    *reinterpret_cast<uint2 *>(y + r * N + c) =
+                        make_uint2((uint32_t)f2bf(acc[ct][0]) | ((uint32_t)f2bf(acc[ct][1]) << 16),
+                                   (uint32_t)f2bf(acc[ct][2]) | ((uint32_t)f2bf(acc[ct][3]) << 16));
+            }
+        } else if constexpr (EPI == EPI_RMS) {
+            float ss = 0.0f;
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) {
+                const int c = 16 * ct + 4 * g;
+                if (c < N) {
+                    const float4 a = *reinterpret_cast<const float4 *>(x + r * N + c);
+                    acc[ct][0] += a.x;
+                    acc[ct][1] += a.y;
+                    acc[ct][2] += a.z;
+                    acc[ct][3] += a.w;
+                    ss += (acc[ct][0] * acc[ct][0] + acc[ct][1] * acc[ct][1]) +
+                          (acc[ct][2] * acc[ct][2] + acc[ct][3] * acc[ct][3]);
+                }
+            }
+            ss += __shfl_xor(ss, 16, 64);
+            ss += __shfl_xor(ss, 32, 64);
+            const float rr = rsqrtf(ss / (float)N + eps);
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) {
+                const int c = 16 * ct + 4 * g;
+                if (c < N) {
+                    float4 o = make_float4(acc[ct][0] * rr, acc[ct][1] * rr, acc[ct][2] * rr, acc[ct][3] * rr);
+                    if (emb) {
+                        const float4 e = *reinterpret_cast<const float4 *>(emb + r * N + c);
+                        o = make_float4(o.x + e.x, o.y + e.y, o.z + e.z, o.w + e.w);
+                    }
+                    *reinterpret_cast<float4 *>(x + r * N + c) = o;
+                    *reinterpret_cast<uint2 *>(xb + r * N + c) =
+                        make_uint2((uint32_t)f2bf(o.x) | ((uint32_t)f2bf(o.y) << 16),
+                                   (uint32_t)f2bf(o.z) | ((uint32_t)f2bf(o.w) << 16));
+                }
+            }
+        } else {
+            constexpr int CH = CT / 2;
+#pragma unroll
+            for (int ct = 0; ct < CH; ct++) {
+                const int c = 16 * ct + 4 * g;
+                float o[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const float a = silu(acc[ct][i]) * acc[ct + CH][i];
+                    const float prev = dpp_prev_token(a);
+                    const int ch = c + i < inter ? c + i : 0;
+                    o[i] = silu(fmaf(cw[2 * ch + 1], a, fmaf(cw[2 * ch], prev, cb[ch])));
+                }
+                if (c < inter)
+                    *reinterpret_cast<uint2 *>(y + r * inter + c) =
+                        make_uint2((uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16),
+                                   (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16));
+            }
+        }
+    }
+}
+
+// (KS, CT) of a projection: K <= 32 KS, N (EPI_SWIGLU: 2 x 16 ceil(inter / 16)) <= 16 CT
+struct LinShape {
+    int ks, ct;
+};
+inline LinShape lin_shape(int K, int N, int inter, int epi) {
+    const int ks = (K + 31) / 32;
+    const int ct = epi == EPI_SWIGLU ? 2 * ((inter + 15) / 16) : (N + 15) / 16;
+    return {ks, ct};
+}
+
+template <int KS, int CT, int EPI>
+int launch_lin(hipStream_t s, const uint16_t *in, const uint16_t *w, int64_t rows, int K, int N, int inter,
+               uint16_t *y, float *x, const float *emb, uint16_t *xb, float eps, const float *cw, const float *cb) {
+    const size_t lds = (size_t)16 * CT * (32 * KS + 8) * 2;
+    int64_t grid = ((rows >> 4) + (kThreads / 64) - 1) / (kThreads / 64);
+    grid = grid > 1024 ? 1024 : grid;  // persistent over boards; W staged once per block
+    hipLaunchKernelGGL((urm_linear_kernel<KS, CT, EPI>), dim3((unsigned)grid), dim3(kThreads), lds, s, in, w, rows, K, N,
+                       inter, y, x, emb, xb, eps, cw, cb);
+    return launch_status();
+}
+
+// the instantiated shapes: GameURMConfig h = 64 (inter 120) and h = 32 (inter 64, the golden config)
+int dispatch_lin(hipStream_t s, int epi, const uint16_t *in, const uint16_t *w, int64_t rows, int K, int N, int inter,
+                 uint16_t *y, float *x, const float *emb, uint16_t *xb, float eps, const float *cw, const float *cb,
+                 bool dry) {
+    const LinShape sh = lin_shape(K, N, inter, epi);
+#define G2048_LIN(EPI_, KS_, CT_)                                                                              \
+    if (epi == EPI_ && sh.ks == KS_ && sh.ct == CT_)                                                            \
+        return dry ? G2048_OK : launch_lin<KS_, CT_, EPI_>(s, in, w, rows, K, N, inter, y, x, emb, xb, eps, cw, cb);
+    G2048_LIN(EPI_STORE, 2, 12)   // h 64 qkv
+    G2048_LIN(EPI_STORE, 1, 6)    // h 32 qkv
+    G2048_LIN(EPI_RMS, 2, 4)      // h 64 o_proj
+    G2048_LIN(EPI_RMS, 4, 4)      // h 64 down_proj (K = inter = 120)
+    G2048_LIN(EPI_RMS, 1, 2)      // h 32 o_proj
+    G2048_LIN(EPI_RMS, 2, 2)      // h 32 down_proj (K = 64)
+    G2048_LIN(EPI_SWIGLU, 2, 16)  // h 64 gate_up (inter 120 -> 2 x 8 tiles)
+    G2048_LIN(EPI_SWIGLU, 1, 8)   // h 32 gate_up (inter 64)
+#undef G2048_LIN
+    return G2048_EINVAL;
+}
 }  // namespace
 
 extern "C" {
@@ -390,6 +586,40 @@ int g2048_urm_pool_heads(g2048_stream_t stream, const float *x, const float *wa,
     hipLaunchKernelGGL(urm_pool_heads_kernel, dim3(blocks(n, kThreads / 64)), dim3(kThreads), 0,
                        (hipStream_t)stream, x, wa, ba, wv, bv, logits, value, n, (int)h);
     return launch_status();
+}
+
+
+int g2048_urm_linear_supported(int32_t epilogue, int32_t k, int32_t n, int32_t inter) {
+    if (epilogue < 0 || epilogue > 2 || k <= 0 || k % 4 || n <= 0 || n % 4 || (epilogue == 2 && (inter <= 0 || inter % 4)))
+        return 0;
+    return dispatch_lin(nullptr, epilogue, nullptr, nullptr, 0, k, n, inter, nullptr, nullptr, nullptr, nullptr, 0.0f,
+                        nullptr, nullptr, true) == G2048_OK ? 1 : 0;
+}
+
+int g2048_urm_linear(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, uint16_t *out, int64_t rows,
+                     int32_t k, int32_t n) {
+    if (rows < 0 || rows % 16 || !g2048_urm_linear_supported(0, k, n, 0)) return G2048_EINVAL;
+    if (rows == 0) return G2048_OK;
+    if (!in || !w || !out) return G2048_EINVAL;
+    return dispatch_lin((hipStream_t)stream, 0, in, w, rows, k, n, 0, out, nullptr, nullptr, nullptr, 0.0f, nullptr,
+                        nullptr, false);
+}
+
+int g2048_urm_linear_rms(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, float *x, const float *emb,
+                         uint16_t *xb, int64_t rows, int32_t k, int32_t h, float eps) {
+    if (rows < 0 || rows % 16 || !g2048_urm_linear_supported(1, k, h, 0)) return G2048_EINVAL;
+    if (rows == 0) return G2048_OK;
+    if (!in || !w || !x || !xb) return G2048_EINVAL;
+    return dispatch_lin((hipStream_t)stream, 1, in, w, rows, k, h, 0, nullptr, x, emb, xb, eps, nullptr, nullptr, false);
+}
+
+int g2048_urm_linear_swiglu(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *conv_w,
+                            const float *conv_b, uint16_t *out, int64_t rows, int32_t h, int32_t inter) {
+    if (rows < 0 || rows % 16 || !g2048_urm_linear_supported(2, h, 2 * inter, inter)) return G2048_EINVAL;
+    if (rows == 0) return G2048_OK;
+    if (!in || !w || !conv_w || !conv_b || !out) return G2048_EINVAL;
+    return dispatch_lin((hipStream_t)stream, 2, in, w, rows, h, 2 * inter, inter, out, nullptr, nullptr, nullptr, 0.0f,
+                        conv_w, conv_b, false);
 }
 
 }  // extern "C"

@@ -38,7 +38,8 @@ EXPORTED = (
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
     # include/g2048_urm.h
     "g2048_urm_stem", "g2048_urm_attention", "g2048_urm_residual_rms", "g2048_urm_swiglu_conv",
-    "g2048_urm_pool_heads",
+    "g2048_urm_pool_heads", "g2048_urm_linear_supported", "g2048_urm_linear", "g2048_urm_linear_rms",
+    "g2048_urm_linear_swiglu",
 )
 
 
@@ -196,6 +197,10 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_urm_residual_rms": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, ctypes.c_float]),
         "g2048_urm_swiglu_conv": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32]),
         "g2048_urm_pool_heads": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32]),
+        "g2048_urm_linear_supported": (ctypes.c_int, [i32, i32, i32, i32]),
+        "g2048_urm_linear": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
+        "g2048_urm_linear_rms": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32, ctypes.c_float]),
+        "g2048_urm_linear_swiglu": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32]),
         "g2048_muon_supported": (ctypes.c_int, [i32, i32]),
         "g2048_muon_step": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.POINTER(MuonCfg)]),
         "g2048_grad_sumsq": (ctypes.c_int, [vp, vp, i64, vp]),
@@ -664,3 +669,32 @@ def urm_pool_heads(x, wa, ba, wv, bv, logits, value):
                                        _dev(ba, torch.float32, "ba"), _dev(wv, torch.float32, "wv"),
                                        _dev(bv, torch.float32, "bv"), _dev(logits, torch.float32, "logits"),
                                        _dev(value, torch.float32, "value"), rows // 16, h), "g2048_urm_pool_heads")
+
+
+def urm_linear_supported(epilogue: int, k: int, n: int, inter: int = 0) -> bool:
+    return bool(load().g2048_urm_linear_supported(int(epilogue), int(k), int(n), int(inter)))
+
+
+def urm_linear(inp, w, out):
+    """out = inp w^T (bf16, fp32 accumulate) on the fused-projection kernel (qkv_proj)."""
+    rows, k = inp.shape
+    _check(load().g2048_urm_linear(_stream(inp), _dev(inp, torch.bfloat16, "in"), _dev(w, torch.bfloat16, "w"),
+                                   _dev(out, torch.bfloat16, "out"), rows, k, w.shape[0]), "g2048_urm_linear")
+
+
+def urm_linear_rms(inp, w, x, emb, xb, eps: float):
+    """x = rms_norm(x + inp w^T) [+ emb]; xb = bf16(x)  (o_proj / down_proj with the post-norm)."""
+    rows, k = inp.shape
+    _check(load().g2048_urm_linear_rms(_stream(inp), _dev(inp, torch.bfloat16, "in"), _dev(w, torch.bfloat16, "w"),
+                                       _dev(x, torch.float32, "x"), _dev(emb, torch.float32, "emb"),
+                                       _dev(xb, torch.bfloat16, "xb"), rows, k, w.shape[0], float(eps)),
+           "g2048_urm_linear_rms")
+
+
+def urm_linear_swiglu(inp, w, conv_w, conv_b, out):
+    """out = SiLU(dwconv(SiLU(gate) * up)) with [gate | up] = inp w^T (gate_up_proj + ConvSwiGLU)."""
+    rows, h = inp.shape
+    _check(load().g2048_urm_linear_swiglu(_stream(inp), _dev(inp, torch.bfloat16, "in"), _dev(w, torch.bfloat16, "w"),
+                                          _dev(conv_w, torch.float32, "conv_w"), _dev(conv_b, torch.float32, "conv_b"),
+                                          _dev(out, torch.bfloat16, "out"), rows, h, w.shape[0] // 2),
+           "g2048_urm_linear_swiglu")

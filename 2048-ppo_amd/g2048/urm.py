@@ -1,11 +1,15 @@
 """GameURM policy forward on the device (game.py:1355-1458) for rollouts: the URM transformer's
-kernels of include/g2048_urm.h around its projections (hipBLASLt through torch.mm, bf16 operands,
-fp32 accumulate).
+kernels of include/g2048_urm.h (fused-epilogue MFMA projections for h <= 64; hipBLASLt through
+torch.mm around the elementwise kernels otherwise; bf16 operands, fp32 accumulate).
 
 Per forward of n boards (16 n token rows):
   urm_stem                         emb = SiLU(LN(Linear(3->h))),  x = init_hidden + emb
-  num_loops x num_layers blocks:   qkv = xb Wqkv^T -> urm_attention -> o Wo^T -> urm_residual_rms
-                                   gu = xb Wgu^T -> urm_swiglu_conv -> a Wd^T -> urm_residual_rms
+  num_loops x num_layers blocks, h <= 64 (fused projections, no projection output in HBM):
+                                   urm_linear (qkv) -> urm_attention -> urm_linear_rms (o_proj + residual
+                                   + RMSNorm) -> urm_linear_swiglu (gate_up + SwiGLU + conv) ->
+                                   urm_linear_rms (down_proj + residual + RMSNorm [+ emb])
+  larger h:                        the same with torch.mm projections and urm_residual_rms /
+                                   urm_swiglu_conv between them
                                    (the last block of a loop adds emb: the next loop's input)
   urm_pool_heads                   mean over the 16 tokens, action / value heads
 Every buffer is allocated once per batch size and the weights are refreshed in place by sync(), so
@@ -39,6 +43,10 @@ class URMPolicy:
         dev = model.stem[0].weight.device
         self.conv_w = [torch.empty(self.inter, 2, dtype=torch.float32, device=dev) for _ in model.layers]
         self.init_hidden = torch.empty(16, self.h, dtype=torch.float32, device=dev)
+        h, i = self.h, self.inter
+        # projections with fused epilogues when the kernels cover these shapes (h <= 64)
+        self.fused = (L.urm_linear_supported(0, h, 3 * h) and L.urm_linear_supported(1, h, h)
+                      and L.urm_linear_supported(2, h, 2 * i, i) and L.urm_linear_supported(1, i, h))
         self._n = -1
         self.sync()
 
@@ -90,6 +98,14 @@ class URMPolicy:
         nl = len(self.mats)
         for loop in range(self.loops):
             for li, (blk, (wqkv, wo, wgu, wd), cw) in enumerate(zip(m.layers, self.mats, self.conv_w)):
+                nxt = self.emb if (li == nl - 1 and loop < self.loops - 1) else None
+                if self.fused:
+                    L.urm_linear(self.xb, wqkv, self.qkv)
+                    L.urm_attention(self.qkv, self.att, self.heads)
+                    L.urm_linear_rms(self.att, wo, self.x, None, self.xb, self.eps)
+                    L.urm_linear_swiglu(self.xb, wgu, cw, blk.mlp.dwconv.bias, self.act)
+                    L.urm_linear_rms(self.act, wd, self.x, nxt, self.xb, self.eps)
+                    continue
                 torch.mm(self.xb, wqkv.t(), out=self.qkv)
                 L.urm_attention(self.qkv, self.att, self.heads)
                 torch.mm(self.att, wo.t(), out=self.y)
@@ -97,7 +113,6 @@ class URMPolicy:
                 torch.mm(self.xb, wgu.t(), out=self.gu)
                 L.urm_swiglu_conv(self.gu, cw, blk.mlp.dwconv.bias, self.act)
                 torch.mm(self.act, wd.t(), out=self.y)
-                nxt = self.emb if (li == nl - 1 and loop < self.loops - 1) else None
                 L.urm_residual_rms(self.x, self.y, nxt, self.xb, self.eps)
         L.urm_pool_heads(self.x, m.action_head.weight, m.action_head.bias, m.value_head.weight, m.value_head.bias,
                          self.logits, self.value)

@@ -63,6 +63,22 @@ int g2048_urm_swiglu_conv(g2048_stream_t stream, const uint16_t *gu, const float
 int g2048_urm_pool_heads(g2048_stream_t stream, const float *x, const float *wa, const float *ba, const float *wv,
                          const float *bv, float *logits, float *value, int64_t n, int32_t h);
 
+/* The projections with their epilogues fused (small hidden sizes; g2048_urm_linear_supported says
+ * which): y = in W^T on bf16 MFMA, W bf16 [n, k] (nn.Linear weight), in bf16 [rows, k], rows % 16
+ * == 0 (whole boards), fp32 accumulate, and
+ *   g2048_urm_linear          out bf16 [rows, n] = y                                 (qkv_proj)
+ *   g2048_urm_linear_rms      x = rms_norm(x + y) [+ emb], xb = bf16(x), n = h       (o_proj, down_proj)
+ *   g2048_urm_linear_swiglu   out bf16 [rows, inter] = SiLU(conv(SiLU(gate) * up))  (gate_up_proj,
+ *                             w [2 inter, h]; the conv as g2048_urm_swiglu_conv)
+ * The projection output never goes through HBM.  epilogue: 0 / 1 / 2 as listed. */
+int g2048_urm_linear_supported(int32_t epilogue, int32_t k, int32_t n, int32_t inter);
+int g2048_urm_linear(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, uint16_t *out, int64_t rows,
+                     int32_t k, int32_t n);
+int g2048_urm_linear_rms(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, float *x, const float *emb,
+                         uint16_t *xb, int64_t rows, int32_t k, int32_t h, float eps);
+int g2048_urm_linear_swiglu(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *conv_w,
+                            const float *conv_b, uint16_t *out, int64_t rows, int32_t h, int32_t inter);
+
 #ifdef __cplusplus
 }
 #endif

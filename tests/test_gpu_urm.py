@@ -44,11 +44,14 @@ def _golden_model(dev):
     return m.to(dev), g
 
 
-def _emulate(m, obs):
+def _emulate(m, obs, fused=False):
     """torch fp32 restatement of g2048/urm.py with bf16 rounding where the kernels round: GEMM
-    operands and outputs, attention probabilities and output, the SwiGLU-conv output."""
+    operands, the qkv output, attention probabilities and output, the SwiGLU-conv output, and (only
+    on the library path, fused=False) the o_proj / gate_up / down_proj outputs -- the fused
+    projections keep those in fp32 into their epilogues."""
     import torch.nn.functional as F
     r = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
+    ro = (lambda t: t) if fused else r  # noqa: E731
     c = m.config
     n, h, heads = obs.shape[0], c.hidden_dim, c.num_heads
     hd = h // heads
@@ -61,14 +64,14 @@ def _emulate(m, obs):
                 q, k, v = qkv.view(n, 16, 3, heads, hd).permute(2, 0, 3, 1, 4)
                 p = r(((q @ k.transpose(-1, -2)) / hd ** 0.5).softmax(-1))
                 o = r(p @ v).transpose(1, 2).reshape(n, 16, h)
-                x = x + r(o @ r(blk.attn.o_proj.weight).t())
+                x = x + ro(o @ r(blk.attn.o_proj.weight).t())
                 x = x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + c.rms_norm_eps)
-                ga, up = r(r(x) @ r(blk.mlp.gate_up_proj.weight).t()).chunk(2, -1)
+                ga, up = ro(r(x) @ r(blk.mlp.gate_up_proj.weight).t()).chunk(2, -1)
                 a = F.silu(ga) * up
                 w, b = blk.mlp.dwconv.weight.view(-1, 2), blk.mlp.dwconv.bias
                 prev = torch.cat([torch.zeros_like(a[:, :1]), a[:, :-1]], 1)
                 act = r(F.silu(prev * w[:, 0] + a * w[:, 1] + b))
-                x = x + r(act @ r(blk.mlp.down_proj.weight).t())
+                x = x + ro(act @ r(blk.mlp.down_proj.weight).t())
                 x = x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + c.rms_norm_eps)
                 if li == len(m.layers) - 1 and loop < c.num_loops - 1:
                     x = x + emb
@@ -76,8 +79,8 @@ def _emulate(m, obs):
         return m.action_head(pooled), m.value_head(pooled).view(-1)
 
 
-def _check_emul(got_l, got_v, m, obs):
-    el, ev = _emulate(m, obs)
+def _check_emul(got_l, got_v, m, obs, fused=False):
+    el, ev = _emulate(m, obs, fused)
     d = torch.cat([(got_l - el).abs().reshape(-1), (got_v - ev).abs().reshape(-1)])
     print(f"vs bf16-rounding restatement: mean {d.mean().item():.3g} max {d.max().item():.3g}")
     assert d.mean().item() <= EMUL_MEAN and d.max().item() <= EMUL_MAX
@@ -99,7 +102,7 @@ def test_urm_policy_matches_reference_golden(dev):
     logits, value = pol(torch.from_numpy(g["obs"]).to(dev))
     _check(logits.cpu().numpy(), g["logits"], "logits")
     _check(value.cpu().numpy(), g["value"].reshape(-1), "value")
-    _check_emul(logits, value, m, torch.from_numpy(g["obs"]).to(dev))
+    _check_emul(logits, value, m, torch.from_numpy(g["obs"]).to(dev), pol.fused)
     # bf16 obs (the rollout's obs buffer) stays within the same bound
     lb, vb = pol(torch.from_numpy(g["obs"]).to(dev).to(torch.bfloat16))
     _check(lb.cpu().numpy(), g["logits"], "logits (bf16 obs)")
@@ -126,12 +129,13 @@ def test_urm_policy_matches_fp32_module(dev, h, heads, layers, loops, n):
         ref_l, ref_v = m(obs)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             ac_l, ac_v = m(obs)
-    got_l, got_v = URMPolicy(m)(obs)
+    pol = URMPolicy(m)
+    got_l, got_v = pol(obs)
     ea = max((ac_l.float() - ref_l).abs().max().item(), (ac_v.float() - ref_v).abs().max().item())
     eg = max((got_l - ref_l).abs().max().item(), (got_v - ref_v.view(-1)).abs().max().item())
     print(f"h={h} heads={heads}: max err vs fp32 {eg:.4g} (torch bf16 autocast {ea:.4g}), "
           f"max |logit| {ref_l.abs().max().item():.3g}")
-    _check_emul(got_l, got_v, m, obs)
+    _check_emul(got_l, got_v, m, obs, pol.fused)
     assert eg <= SCALE_REL * ref_l.abs().max().item(), eg
 
 
@@ -230,3 +234,61 @@ def test_urm_trainer_steps(dev, horizon):
         assert m["samples"] > 0
     moved = {k for k, v in tr.model.named_parameters() if not torch.equal(v, before[k])}
     assert "init_hidden" in moved and "layers.0.attn.qkv_proj.weight" in moved and "layers.1.mlp.dwconv.weight" in moved
+
+
+@pytest.mark.parametrize("h,inter,rows", [(64, 120, 16 * 4097), (32, 64, 16 * 33)])
+def test_urm_fused_projection_kernels(dev, h, inter, rows):
+    """g2048_urm_linear / _rms / _swiglu vs torch on the same bf16 operands (fp32 reference of the
+    same math): bf16 output rounding (2^-8 relative) plus accumulation order."""
+    import torch.nn.functional as F
+    from g2048 import _lib as L
+    g = torch.Generator(device=dev).manual_seed(h)
+    xb = torch.randn(rows, h, generator=g, device=dev).to(torch.bfloat16)
+    wq = (torch.randn(3 * h, h, generator=g, device=dev) / h ** 0.5).to(torch.bfloat16)
+    out = torch.empty(rows, 3 * h, dtype=torch.bfloat16, device=dev)
+    L.urm_linear(xb, wq, out)
+    ref = xb.float() @ wq.float().t()
+    assert ((out.float() - ref).abs() <= 2.0 ** -8 * ref.abs() + 1e-3).all()
+    # o_proj + residual + RMSNorm (+ emb)
+    wo = (torch.randn(h, h, generator=g, device=dev) / h ** 0.5).to(torch.bfloat16)
+    x0 = torch.randn(rows, h, generator=g, device=dev)
+    emb = torch.randn(rows, h, generator=g, device=dev)
+    for e in (None, emb):
+        x = x0.clone()
+        xo = torch.empty(rows, h, dtype=torch.bfloat16, device=dev)
+        L.urm_linear_rms(xb, wo, x, e, xo, 1e-5)
+        v = x0 + xb.float() @ wo.float().t()
+        want = v * torch.rsqrt(v.pow(2).mean(-1, keepdim=True) + 1e-5) + (0 if e is None else e)
+        torch.testing.assert_close(x, want, rtol=1e-4, atol=1e-4)
+        assert torch.equal(xo, x.to(torch.bfloat16))
+    # gate_up + SwiGLU + depthwise conv (kernel 2, per board of 16 tokens) + SiLU
+    wgu = (torch.randn(2 * inter, h, generator=g, device=dev) / h ** 0.5).to(torch.bfloat16)
+    cw = torch.randn(inter, 2, generator=g, device=dev) * 0.5
+    cb = torch.randn(inter, generator=g, device=dev) * 0.1
+    act = torch.empty(rows, inter, dtype=torch.bfloat16, device=dev)
+    L.urm_linear_swiglu(xb, wgu, cw, cb, act)
+    gate, up = (xb.float() @ wgu.float().t()).chunk(2, -1)
+    a = (F.silu(gate) * up).view(rows // 16, 16, inter)
+    prev = torch.cat([torch.zeros_like(a[:, :1]), a[:, :-1]], 1)
+    want = F.silu(prev * cw[:, 0] + a * cw[:, 1] + cb).reshape(rows, inter)
+    assert ((act.float() - want).abs() <= 2.0 ** -8 * want.abs() + 2e-3).all(), (act.float() - want).abs().max()
+    assert L.urm_linear_supported(2, h, 2 * inter, inter) and not L.urm_linear_supported(0, 196, 588)
+
+
+def test_urm_fused_and_library_paths_agree(dev):
+    """The default config through the fused projections vs the torch.mm path of the same policy."""
+    import agent
+    from g2048.urm import URMPolicy
+    torch.manual_seed(8)
+    m = agent.GameURM(agent.GameURMConfig(dropout=0.0)).to(dev).eval()
+    pol = URMPolicy(m)
+    assert pol.fused
+    obs = torch.rand(2048, 48, device=dev) * 6
+    lf, vf = [t.clone() for t in pol(obs)]
+    pol.fused = False
+    ll, vl = pol(obs)
+    with torch.no_grad():
+        ref_l, _ = m(obs)
+    e_f, e_l = (lf - ref_l).abs().max().item(), (ll - ref_l).abs().max().item()
+    print(f"fused {e_f:.4g} library {e_l:.4g} vs fp32")
+    assert e_f <= SCALE_REL * ref_l.abs().max().item() and (lf - ll).abs().max().item() <= 0.1
