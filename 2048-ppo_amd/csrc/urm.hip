@@ -35,7 +35,9 @@ __device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even (f
     const uint32_t u = __float_as_uint(f);
     return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
 }
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+// x * sigmoid(x) with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE division
+// sequence: exp overflow for x << 0 gives rcp(inf) = 0, i.e. -0
+__device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -347,6 +349,10 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int kPitch = 32 * KS + 8;  // bf16 per staged row
     constexpr int kRowsW = 16 * CT;
+    constexpr int kLinWBytes = kRowsW * kPitch * 2;
+    // per-wave LDS tile of EPI_STORE: the 16-row bf16 output (staging the fp32 residual stream of
+    // EPI_RMS the same way measured slower: 194 -> 213 us for o_proj)
+    constexpr int kLinTileBytes = EPI == EPI_STORE ? 16 * (2 * 16 * CT + 8) : 0;
     const int tid = threadIdx.x;
     for (int e = tid; e < kRowsW * kPitch / 8; e += kThreads) reinterpret_cast<uint4 *>(smem)[e] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
@@ -405,14 +411,29 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
         }
         // lane (t, g), tile ct: acc[ct][i] = Y[r][16 ct + 4 g + i]
         if constexpr (EPI == EPI_STORE) {
+            // the board's 16 x N outputs are one contiguous span of y: stage them in this wave's LDS
+            // tile (row pitch N + 4 bf16) and write the span with 16-byte stores, instead of 16 rows
+            // x 32-byte pieces per store instruction
+            char *tile = smem + kLinWBytes + wave * kLinTileBytes;
+            const int tp = 2 * N + 8;
 #pragma unroll
             for (int ct = 0; ct < CT; ct++) {
                 const int c = 16 * ct + 4 * g;
                 if (c < N)
-                    *reinterpret_cast<uint2 *>(y + r * N + c) =
+                    *reinterpret_cast<uint2 *>(tile + t * tp + 2 * c) =
                         make_uint2((uint32_t)f2bf(acc[ct][0]) | ((uint32_t)f2bf(acc[ct][1]) << 16),
                                    (uint32_t)f2bf(acc[ct][2]) | ((uint32_t)f2bf(acc[ct][3]) << 16));
             }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            const int per_row = N >> 3;  // 16-byte chunks per row (N % 8 == 0)
+            uint16_t *dst = y + bd * 16 * (int64_t)N;
+            for (int q = lane; q < 16 * per_row; q += 64) {
+                const int row = q / per_row, c8 = q - row * per_row;
+                *reinterpret_cast<uint4 *>(dst + row * N + 8 * c8) = *reinterpret_cast<const uint4 *>(tile + row * tp + 16 * c8);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();  // the tile is rewritten by the next board
         } else if constexpr (EPI == EPI_RMS) {
             float ss = 0.0f;
 #pragma unroll
@@ -451,13 +472,19 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
 #pragma unroll
             for (int ct = 0; ct < CH; ct++) {
                 const int c = 16 * ct + 4 * g;
+                // the 4 channels' conv taps and biases: three 16-byte loads (inter % 4 == 0)
+                const int cc = c < inter ? c : 0;
+                const float4 w01 = *reinterpret_cast<const float4 *>(cw + 2 * cc);      // w[c][0..1], w[c+1][0..1]
+                const float4 w23 = *reinterpret_cast<const float4 *>(cw + 2 * cc + 4);  // w[c+2][..], w[c+3][..]
+                const float4 bb = *reinterpret_cast<const float4 *>(cb + cc);
+                const float wk0[4] = {w01.x, w01.z, w23.x, w23.z}, wk1[4] = {w01.y, w01.w, w23.y, w23.w};
+                const float bk[4] = {bb.x, bb.y, bb.z, bb.w};
                 float o[4];
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
                     const float a = silu(acc[ct][i]) * acc[ct + CH][i];
                     const float prev = dpp_prev_token(a);
-                    const int ch = c + i < inter ? c + i : 0;
-                    o[i] = silu(fmaf(cw[2 * ch + 1], a, fmaf(cw[2 * ch], prev, cb[ch])));
+                    o[i] = silu(fmaf(wk1[i], a, fmaf(wk0[i], prev, bk[i])));
                 }
                 if (c < inter)
                     *reinterpret_cast<uint2 *>(y + r * inter + c) =
@@ -481,7 +508,8 @@ inline LinShape lin_shape(int K, int N, int inter, int epi) {
 template <int KS, int CT, int EPI>
 int launch_lin(hipStream_t s, const uint16_t *in, const uint16_t *w, int64_t rows, int K, int N, int inter,
                uint16_t *y, float *x, const float *emb, uint16_t *xb, float eps, const float *cw, const float *cb) {
-    const size_t lds = (size_t)16 * CT * (32 * KS + 8) * 2;
+    const size_t tile = EPI == EPI_STORE ? 16 * (2 * 16 * CT + 8) : 0;
+    const size_t lds = (size_t)16 * CT * (32 * KS + 8) * 2 + (size_t)(kThreads / 64) * tile;
     int64_t grid = ((rows >> 4) + (kThreads / 64) - 1) / (kThreads / 64);
     grid = grid > 1024 ? 1024 : grid;  // persistent over boards; W staged once per block
     hipLaunchKernelGGL((urm_linear_kernel<KS, CT, EPI>), dim3((unsigned)grid), dim3(kThreads), lds, s, in, w, rows, K, N,
@@ -598,7 +626,7 @@ int g2048_urm_linear_supported(int32_t epilogue, int32_t k, int32_t n, int32_t i
 
 int g2048_urm_linear(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, uint16_t *out, int64_t rows,
                      int32_t k, int32_t n) {
-    if (rows < 0 || rows % 16 || !g2048_urm_linear_supported(0, k, n, 0)) return G2048_EINVAL;
+    if (rows < 0 || rows % 16 || n % 8 || !g2048_urm_linear_supported(0, k, n, 0)) return G2048_EINVAL;
     if (rows == 0) return G2048_OK;
     if (!in || !w || !out) return G2048_EINVAL;
     return dispatch_lin((hipStream_t)stream, 0, in, w, rows, k, n, 0, out, nullptr, nullptr, nullptr, 0.0f, nullptr,
@@ -617,7 +645,7 @@ int g2048_urm_linear_swiglu(g2048_stream_t stream, const uint16_t *in, const uin
                             const float *conv_b, uint16_t *out, int64_t rows, int32_t h, int32_t inter) {
     if (rows < 0 || rows % 16 || !g2048_urm_linear_supported(2, h, 2 * inter, inter)) return G2048_EINVAL;
     if (rows == 0) return G2048_OK;
-    if (!in || !w || !conv_w || !conv_b || !out) return G2048_EINVAL;
+    if (!in || !w || !conv_w || !conv_b || !out || ((uintptr_t)conv_w | (uintptr_t)conv_b) % 16) return G2048_EINVAL;
     return dispatch_lin((hipStream_t)stream, 2, in, w, rows, h, 2 * inter, inter, out, nullptr, nullptr, nullptr, 0.0f,
                         conv_w, conv_b, false);
 }
