@@ -160,6 +160,14 @@ class GameConvSwiGLU(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         gate, up = self.gate_up_proj(x).chunk(2, dim=-1)
         y = F.silu(gate) * up                                        # [B, S, I]
+        if self.dwconv.kernel_size[0] == 2:
+            # the kernel-2, padding-1 depthwise conv trimmed to S is y_t w0 shifted by one token plus
+            # y_t w1 + b: written elementwise (same parameters and math; the library's depthwise
+            # Conv1d path for bf16 on this platform is a naive kernel, ~100x slower)
+            w = self.dwconv.weight.view(-1, 2)
+            prev = F.pad(y, (0, 0, 1, 0))[:, :-1]
+            y = prev * w[:, 0] + y * w[:, 1] + self.dwconv.bias
+            return self.down_proj(F.silu(y))
         y = self.dwconv(y.transpose(1, 2))[..., : x.shape[1]]       # [B, I, S] trimmed to S
         return self.down_proj(F.silu(y).transpose(1, 2).contiguous())
 

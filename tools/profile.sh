@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 TAG=${TAG:-r02}
 ARGS=${ARGS:---steps 20 --warmup 3 --cpu-seconds 0 --sweep=}
-PMC_ARGS=${PMC_ARGS:---steps 4 --warmup 1 --cpu-seconds 0 --single-steps 64 --train-iters 0 --sweep=}
+PMC_ARGS=${PMC_ARGS:---steps 4 --warmup 1 --cpu-seconds 0 --single-steps 64 --train-iters 0 --urm-steps 0 --sweep=}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 pass() {  # pass <name> <rocprofv3 options...>
