@@ -536,6 +536,343 @@ int dispatch_lin(hipStream_t s, int epi, const uint16_t *in, const uint16_t *w, 
 #undef G2048_LIN
     return G2048_EINVAL;
 }
+
+// ---------------------------------------------------------------------------------------------
+// The whole GameURM forward in ONE persistent kernel (the default config: h 64, 4 heads of 16,
+// inter 120, conv kernel 2, 1 or 2 layers, any number of loops).  Nothing but obs in and
+// logits / value out touches HBM: a wave carries one board (16 token lanes x 4 feature groups)
+// through every block with the residual stream x and the stem output emb in registers (acc
+// layout: lane (t, g) holds features 16 ct + 4 g + i of token t), and the workgroup streams the
+// weights of the layer being applied through LDS:
+//   per block application: __syncthreads, stage layer l's four bf16 matrices + conv taps (92 KB,
+//   every weight row padded to a conflict-free pitch), __syncthreads, then per board:
+//     qkv    12 tiles x 2 k-steps of v_mfma_f32_16x16x32_bf16 -> bf16 into the wave's LDS tile
+//     attn   per head: S^T = K Q^T and O^T = V^T P^T on v_mfma_f32_16x16x16_bf16, K / Q / V read
+//            from the tile (V transposed by the read), O written over its head's Q columns
+//     o_proj 4 x 2 MFMAs + x, RMSNorm across the token's 4 lanes      -> x (registers), xb (tile)
+//     gateup 16 x 2 MFMAs (gate / up of a channel in the same lane), SiLU * up, the token t-1
+//            value by a DPP row shift, conv, SiLU                      -> act (tile)
+//     down   4 x 4 MFMAs + x, RMSNorm [+ emb at the end of a loop]     -> x, xb
+// The tile is the hand-off between the MFMA result layout and the next product's operand layout
+// (16-byte fragment reads); wave-local s_waitcnt + wave barrier order the lanes' LDS accesses.
+namespace mk {
+constexpr int H = 64, QKV = 192, INTER = 120, GU = 256, KD = 128;
+constexpr int P64 = H + 8;     // bf16 pitch of K = 64 weight rows (36 dwords: conflict-free)
+constexpr int PD = KD + 8;     // bf16 pitch of the down-proj rows (68 dwords)
+constexpr int OFF_QKV = 0;
+constexpr int OFF_O = OFF_QKV + QKV * P64 * 2;
+constexpr int OFF_GU = OFF_O + H * P64 * 2;
+constexpr int OFF_D = OFF_GU + GU * P64 * 2;
+constexpr int OFF_CW = OFF_D + H * PD * 2;       // conv taps fp32 [128][2]
+constexpr int OFF_CB = OFF_CW + KD * 2 * 4;      // conv bias fp32 [128]
+constexpr int W_BYTES = OFF_CB + KD * 4;         // 92 672
+constexpr int TP = QKV + 8;                      // bf16 pitch of a wave's tile (100 dwords)
+constexpr int TILE_BYTES = 16 * TP * 2;          // 6 400
+constexpr int WAVES = 8;
+constexpr int THREADS = 64 * WAVES;
+constexpr int NB = 1;                            // boards per wave per batch
+}  // namespace mk
+
+struct UrmW {  // device pointers (see g2048_urm_weights)
+    const float *stem_w, *ln_w, *ln_b, *init, *wa, *ba, *wv, *bv;
+    const uint16_t *qkv[2], *o[2], *gu[2], *dn[2];
+    const float *cw[2], *cb[2];
+    int layers, loops;
+    float eps;
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// 16 B (8 bf16) from LDS
+__device__ __forceinline__ bf16x8 lds16(const char *p) { return *reinterpret_cast<const bf16x8 *>(p); }
+
+// acc-layout values (4 per tile) -> bf16 in the tile at [t][16 ct + 4 g]
+template <int CT>
+__device__ __forceinline__ void tile_put(char *tile, const f32x4 (&v)[CT], int t, int g, int col0 = 0) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ct++)
+        *reinterpret_cast<uint2 *>(tile + (t * mk::TP + col0 + 16 * ct + 4 * g) * 2) =
+            make_uint2((uint32_t)f2bf(v[ct][0]) | ((uint32_t)f2bf(v[ct][1]) << 16),
+                       (uint32_t)f2bf(v[ct][2]) | ((uint32_t)f2bf(v[ct][3]) << 16));
+}
+
+// acc[CT] = W X^T for the board in `tile` (B fragments [t][32 s + 8 g]); W rows at `w` with pitch
+// `pitch` bf16 (A fragments [16 ct + t][32 s + 8 g])
+template <int CT, int KS>
+__device__ __forceinline__ void tile_gemm(f32x4 (&acc)[CT], const char *w, int pitch, const char *tile, int t, int g) {
+    bf16x8 fb[KS], fa[2][KS];
+#pragma unroll
+    for (int s = 0; s < KS; s++) fb[s] = lds16(tile + (t * mk::TP + 32 * s + 8 * g) * 2);
+    const char *wb = w + (t * pitch + 8 * g) * 2;
+#pragma unroll
+    for (int s = 0; s < KS; s++) fa[0][s] = lds16(wb + 64 * s);
+    // W fragments one tile ahead; the empty asm keeps the compiler from hoisting every tile's
+    // reads (the register file would spill)
+#pragma unroll
+    for (int ct = 0; ct < CT; ct++) {
+        if (ct + 1 < CT) {
+#pragma unroll
+            for (int s = 0; s < KS; s++) fa[(ct + 1) & 1][s] = lds16(wb + 16 * (ct + 1) * pitch * 2 + 64 * s);
+        }
+        asm volatile("" ::: "memory");
+        acc[ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s = 0; s < KS; s++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ct & 1][s], fb[s], acc[ct], 0, 0, 0);
+    }
+}
+
+// x = rms_norm(x + y) [+ emb]  (the token's 64 features in 4 lanes x 16 values)
+__device__ __forceinline__ void rms_update(f32x4 (&x)[4], const f32x4 (&y)[4], const f32x4 (&emb)[4], bool add_emb,
+                                           float eps) {
+    float ss = 0.0f;
+#pragma unroll
+    for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            x[ct][i] += y[ct][i];
+            ss += x[ct][i] * x[ct][i];
+        }
+    ss += __shfl_xor(ss, 16, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    const float r = rsqrtf(ss * (1.0f / mk::H) + eps);
+#pragma unroll
+    for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) x[ct][i] = x[ct][i] * r + (add_emb ? emb[ct][i] : 0.0f);
+}
+
+template <bool kBf16Obs>
+__global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__restrict__ obs, UrmW W,
+                                                                  float *__restrict__ logits,
+                                                                  float *__restrict__ value, int64_t n) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, t = lane & 15, g = lane >> 4;
+    char *tile = smem + mk::W_BYTES + wave * mk::TILE_BYTES;
+    const float *cwl = reinterpret_cast<const float *>(smem + mk::OFF_CW);
+    const float *cbl = reinterpret_cast<const float *>(smem + mk::OFF_CB);
+    const int64_t per_batch = (int64_t)mk::WAVES * mk::NB;
+    const int64_t batches = (n + per_batch - 1) / per_batch;
+    const int apps = W.layers * W.loops;
+    for (int64_t bt = blockIdx.x; bt < batches; bt += gridDim.x) {
+        f32x4 x[mk::NB][4], emb[mk::NB][4];
+        // ---- stem: emb = SiLU(LayerNorm(Linear(3 -> 64)(cells))), x = init_hidden + emb
+#pragma unroll
+        for (int nb = 0; nb < mk::NB; nb++) {
+            int64_t b = bt * per_batch + wave * mk::NB + nb;
+            b = b < n ? b : n - 1;
+            float c[3];
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const int64_t o = b * 48 + 3 * t + k;
+                c[k] = kBf16Obs ? bf2f(static_cast<const uint16_t *>(obs)[o]) : static_cast<const float *>(obs)[o];
+            }
+            float s = 0.0f;
+#pragma unroll
+            for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int f = 16 * ct + 4 * g + i;
+                    const float y = fmaf(W.stem_w[3 * f + 2], c[2], fmaf(W.stem_w[3 * f + 1], c[1], W.stem_w[3 * f] * c[0]));
+                    emb[nb][ct][i] = y;
+                    s += y;
+                }
+            s += __shfl_xor(s, 16, 64);
+            s += __shfl_xor(s, 32, 64);
+            const float mean = s * (1.0f / mk::H);
+            float v = 0.0f;
+#pragma unroll
+            for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const float d = emb[nb][ct][i] - mean;
+                    v += d * d;
+                }
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            const float rstd = rsqrtf(v * (1.0f / mk::H) + 1e-5f);
+#pragma unroll
+            for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int f = 16 * ct + 4 * g + i;
+                    const float e = silu((emb[nb][ct][i] - mean) * rstd * W.ln_w[f] + W.ln_b[f]);
+                    emb[nb][ct][i] = e;
+                    x[nb][ct][i] = W.init[t * mk::H + f] + e;
+                }
+        }
+        for (int app = 0; app < apps; app++) {
+            const int l = app % W.layers;
+            const bool loop_end = (l == W.layers - 1) && (app < apps - 1);
+            if (app < W.layers || W.layers > 1) {  // (re)stage layer l's weights
+                __syncthreads();
+                auto stage = [&](const uint16_t *src, int rows, int k, int pitch, int off, int (*map)(int)) {
+                    const int k4 = k >> 2;
+                    for (int e = tid; e < rows * k4; e += mk::THREADS) {
+                        const int q = e / k4, c4 = e - q * k4;
+                        const int sr = map(q);
+                        uint2 v = make_uint2(0u, 0u);
+                        if (sr >= 0) v = *reinterpret_cast<const uint2 *>(src + (int64_t)sr * k + 4 * c4);
+                        *reinterpret_cast<uint2 *>(smem + off + (q * pitch + 4 * c4) * 2) = v;
+                    }
+                };
+                stage(W.qkv[l], mk::QKV, mk::H, mk::P64, mk::OFF_QKV, [](int q) { return q; });
+                stage(W.o[l], mk::H, mk::H, mk::P64, mk::OFF_O, [](int q) { return q; });
+                stage(W.gu[l], mk::GU, mk::H, mk::P64, mk::OFF_GU, [](int q) {
+                    return q < 128 ? (q < mk::INTER ? q : -1) : (q - 128 < mk::INTER ? mk::INTER + q - 128 : -1);
+                });
+                {   // down rows: K = 120 real columns, zero to 128
+                    for (int e = tid; e < mk::H * (mk::KD / 4); e += mk::THREADS) {
+                        const int q = e / (mk::KD / 4), c4 = e - q * (mk::KD / 4);
+                        uint2 v = make_uint2(0u, 0u);
+                        if (4 * c4 < mk::INTER) v = *reinterpret_cast<const uint2 *>(W.dn[l] + (int64_t)q * mk::INTER + 4 * c4);
+                        *reinterpret_cast<uint2 *>(smem + mk::OFF_D + (q * mk::PD + 4 * c4) * 2) = v;
+                    }
+                }
+                for (int e = tid; e < mk::KD; e += mk::THREADS) {
+                    float* cw = reinterpret_cast<float *>(smem + mk::OFF_CW);
+                    float* cb = reinterpret_cast<float *>(smem + mk::OFF_CB);
+                    const bool in = e < mk::INTER;
+                    cw[2 * e] = in ? W.cw[l][2 * e] : 0.0f;
+                    cw[2 * e + 1] = in ? W.cw[l][2 * e + 1] : 0.0f;
+                    cb[e] = in ? W.cb[l][e] : 0.0f;
+                }
+                __syncthreads();
+            }
+#pragma unroll 1
+            for (int nb = 0; nb < mk::NB; nb++) {
+                f32x4 *xr = x[nb];
+                // xb -> tile, qkv
+                tile_put<4>(tile, reinterpret_cast<const f32x4(&)[4]>(*xr), t, g);
+                wave_lds_sync();
+                {
+                    f32x4 q[12];
+                    tile_gemm<12, 2>(q, smem + mk::OFF_QKV, mk::P64, tile, t, g);
+                    wave_lds_sync();
+                    tile_put<12>(tile, q, t, g);
+                    wave_lds_sync();
+                }
+                // attention, per head: O over the head's Q columns
+#pragma unroll 1
+                for (int hh = 0; hh < 4; hh++) {
+                    const s16x4 ka = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint2 *>(tile + (t * mk::TP + 64 + 16 * hh + 4 * g) * 2));
+                    const s16x4 qb = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint2 *>(tile + (t * mk::TP + 16 * hh + 4 * g) * 2));
+                    s16x4 va;
+#pragma unroll
+                    for (int jj = 0; jj < 4; jj++)
+                        va[jj] = *reinterpret_cast<const short *>(tile + ((4 * g + jj) * mk::TP + 128 + 16 * hh + t) * 2);
+                    f32x4 st = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ka, qb, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+                    float p[4], m = -INFINITY;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        p[r] = st[r] * 0.25f;  // 1 / sqrt(head_dim 16)
+                        m = fmaxf(m, p[r]);
+                    }
+                    m = fmaxf(m, __shfl_xor(m, 16, 64));
+                    m = fmaxf(m, __shfl_xor(m, 32, 64));
+                    float sum = 0.0f;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        p[r] = __expf(p[r] - m);
+                        sum += p[r];
+                    }
+                    sum += __shfl_xor(sum, 16, 64);
+                    sum += __shfl_xor(sum, 32, 64);
+                    const float inv = 1.0f / sum;
+                    s16x4 pb;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) pb[r] = (short)f2bf(p[r] * inv);
+                    const f32x4 o = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, pb, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+                    wave_lds_sync();  // every lane's Q / K / V reads of this head are done
+                    *reinterpret_cast<uint2 *>(tile + (t * mk::TP + 16 * hh + 4 * g) * 2) =
+                        make_uint2((uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16),
+                                   (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16));
+                }
+                wave_lds_sync();
+                {   // o_proj + residual + RMSNorm
+                    f32x4 y[4];
+                    tile_gemm<4, 2>(y, smem + mk::OFF_O, mk::P64, tile, t, g);
+                    rms_update(reinterpret_cast<f32x4(&)[4]>(*xr), y, reinterpret_cast<const f32x4(&)[4]>(*emb[nb]), false, W.eps);
+                }
+                wave_lds_sync();
+                tile_put<4>(tile, reinterpret_cast<const f32x4(&)[4]>(*xr), t, g);
+                wave_lds_sync();
+                {   // gate_up + SwiGLU + depthwise conv + SiLU -> act (bf16, 128 columns); the gate and up
+                    // tiles of a channel group are produced together, so only 8 accumulators are live
+                    bf16x8 fb[2];
+                    fb[0] = lds16(tile + (t * mk::TP + 8 * g) * 2);
+                    fb[1] = lds16(tile + (t * mk::TP + 32 + 8 * g) * 2);
+                    const char *wb = smem + mk::OFF_GU + (t * mk::P64 + 8 * g) * 2;
+                    f32x4 a[8];
+#pragma unroll
+                    for (int ct = 0; ct < 8; ct++) {
+                        f32x4 ga = f32x4{0.0f, 0.0f, 0.0f, 0.0f}, up = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; s2++) {
+                            ga = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds16(wb + (16 * ct * mk::P64 + 32 * s2) * 2), fb[s2], ga, 0, 0, 0);
+                            up = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds16(wb + (16 * (ct + 8) * mk::P64 + 32 * s2) * 2), fb[s2], up, 0, 0, 0);
+                        }
+                        asm volatile("" ::: "memory");
+                        const int c = 16 * ct + 4 * g;
+                        const float4 w01 = *reinterpret_cast<const float4 *>(cwl + 2 * c);
+                        const float4 w23 = *reinterpret_cast<const float4 *>(cwl + 2 * c + 4);
+                        const float4 bb = *reinterpret_cast<const float4 *>(cbl + c);
+                        const float wk0[4] = {w01.x, w01.z, w23.x, w23.z}, wk1[4] = {w01.y, w01.w, w23.y, w23.w};
+                        const float bk[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const float av = silu(ga[i]) * up[i];
+                            const float prev = dpp_prev_token(av);
+                            a[ct][i] = c + i < mk::INTER ? silu(fmaf(wk1[i], av, fmaf(wk0[i], prev, bk[i]))) : 0.0f;
+                        }
+                    }
+                    wave_lds_sync();
+                    tile_put<8>(tile, a, t, g);
+                    wave_lds_sync();
+                }
+                {   // down_proj + residual + RMSNorm [+ emb]
+                    f32x4 y[4];
+                    tile_gemm<4, 4>(y, smem + mk::OFF_D, mk::PD, tile, t, g);
+                    rms_update(reinterpret_cast<f32x4(&)[4]>(*xr), y, reinterpret_cast<const f32x4(&)[4]>(*emb[nb]), loop_end, W.eps);
+                }
+                wave_lds_sync();
+            }
+        }
+        // ---- mean over the 16 tokens, heads
+#pragma unroll
+        for (int nb = 0; nb < mk::NB; nb++) {
+            const int64_t b = bt * per_batch + wave * mk::NB + nb;
+            float acc5[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    float pv = x[nb][ct][i];
+                    pv += __shfl_xor(pv, 1, 64);
+                    pv += __shfl_xor(pv, 2, 64);
+                    pv += __shfl_xor(pv, 4, 64);
+                    pv += __shfl_xor(pv, 8, 64);
+                    pv *= 1.0f / 16.0f;
+                    const int f = 16 * ct + 4 * g + i;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) acc5[k] = fmaf(pv, W.wa[k * mk::H + f], acc5[k]);
+                    acc5[4] = fmaf(pv, W.wv[f], acc5[4]);
+                }
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                acc5[k] += __shfl_xor(acc5[k], 16, 64);
+                acc5[k] += __shfl_xor(acc5[k], 32, 64);
+            }
+            if (b < n && lane == 0) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) logits[b * 4 + k] = acc5[k] + W.ba[k];
+                value[b] = acc5[4] + W.bv[0];
+            }
+        }
+    }
+}
 }  // namespace
 
 extern "C" {
@@ -648,6 +985,48 @@ int g2048_urm_linear_swiglu(g2048_stream_t stream, const uint16_t *in, const uin
     if (!in || !w || !conv_w || !conv_b || !out || ((uintptr_t)conv_w | (uintptr_t)conv_b) % 16) return G2048_EINVAL;
     return dispatch_lin((hipStream_t)stream, 2, in, w, rows, h, 2 * inter, inter, out, nullptr, nullptr, nullptr, 0.0f,
                         conv_w, conv_b, false);
+}
+
+
+int g2048_urm_forward_supported(int32_t hidden, int32_t heads, int32_t inter, int32_t num_layers, int32_t conv_kernel) {
+    return hidden == mk::H && heads == 4 && inter == mk::INTER && (num_layers == 1 || num_layers == 2) &&
+                   conv_kernel == 2 ? 1 : 0;
+}
+
+int g2048_urm_forward(g2048_stream_t stream, const g2048_urm_weights *w, const void *obs, int32_t obs_dtype,
+                      float *logits, float *value, int64_t n) {
+    if (!w || n < 0 || (obs_dtype != 0 && obs_dtype != 1) || w->num_loops <= 0 ||
+        !g2048_urm_forward_supported(w->hidden, w->heads, w->inter, w->num_layers, 2))
+        return G2048_EINVAL;
+    if (n == 0) return G2048_OK;
+    if (!obs || !logits || !value || !w->stem_w || !w->ln_w || !w->ln_b || !w->init_hidden || !w->wa || !w->ba ||
+        !w->wv || !w->bv)
+        return G2048_EINVAL;
+    UrmW a{};
+    a.stem_w = w->stem_w; a.ln_w = w->ln_w; a.ln_b = w->ln_b; a.init = w->init_hidden;
+    a.wa = w->wa; a.ba = w->ba; a.wv = w->wv; a.bv = w->bv;
+    for (int l = 0; l < w->num_layers; l++) {
+        if (!w->qkv[l] || !w->o[l] || !w->gate_up[l] || !w->down[l] || !w->conv_w[l] || !w->conv_b[l])
+            return G2048_EINVAL;
+        if (((uintptr_t)w->qkv[l] | (uintptr_t)w->o[l] | (uintptr_t)w->gate_up[l] | (uintptr_t)w->down[l]) % 8)
+            return G2048_EINVAL;
+        a.qkv[l] = w->qkv[l]; a.o[l] = w->o[l]; a.gu[l] = w->gate_up[l]; a.dn[l] = w->down[l];
+        a.cw[l] = w->conv_w[l]; a.cb[l] = w->conv_b[l];
+    }
+    a.layers = w->num_layers;
+    a.loops = w->num_loops;
+    a.eps = w->eps;
+    const int64_t per_batch = (int64_t)mk::WAVES * mk::NB;
+    int64_t grid = (n + per_batch - 1) / per_batch;
+    grid = grid > 256 ? 256 : grid;  // one block per CU: the layer's weights fill most of the LDS
+    const size_t lds = (size_t)mk::W_BYTES + (size_t)mk::WAVES * mk::TILE_BYTES;
+    if (obs_dtype == 1)
+        hipLaunchKernelGGL(urm_forward_kernel<true>, dim3((unsigned)grid), dim3(mk::THREADS), lds, (hipStream_t)stream,
+                           obs, a, logits, value, n);
+    else
+        hipLaunchKernelGGL(urm_forward_kernel<false>, dim3((unsigned)grid), dim3(mk::THREADS), lds, (hipStream_t)stream,
+                           obs, a, logits, value, n);
+    return launch_status();
 }
 
 }  // extern "C"

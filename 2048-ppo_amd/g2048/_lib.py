@@ -39,7 +39,7 @@ EXPORTED = (
     # include/g2048_urm.h
     "g2048_urm_stem", "g2048_urm_attention", "g2048_urm_residual_rms", "g2048_urm_swiglu_conv",
     "g2048_urm_pool_heads", "g2048_urm_linear_supported", "g2048_urm_linear", "g2048_urm_linear_rms",
-    "g2048_urm_linear_swiglu",
+    "g2048_urm_linear_swiglu", "g2048_urm_forward_supported", "g2048_urm_forward",
 )
 
 
@@ -58,6 +58,17 @@ class Rng(ctypes.Structure):
         ("mt_state", ctypes.c_void_p),
         ("inject", ctypes.c_void_p),
     ]
+
+
+class UrmWeights(ctypes.Structure):
+    """struct g2048_urm_weights"""
+    _fields_ = [("hidden", ctypes.c_int32), ("heads", ctypes.c_int32), ("inter", ctypes.c_int32),
+                ("num_layers", ctypes.c_int32), ("num_loops", ctypes.c_int32), ("eps", ctypes.c_float),
+                ("stem_w", ctypes.c_void_p), ("ln_w", ctypes.c_void_p), ("ln_b", ctypes.c_void_p),
+                ("init_hidden", ctypes.c_void_p), ("wa", ctypes.c_void_p), ("ba", ctypes.c_void_p),
+                ("wv", ctypes.c_void_p), ("bv", ctypes.c_void_p), ("qkv", ctypes.c_void_p * 2),
+                ("o", ctypes.c_void_p * 2), ("gate_up", ctypes.c_void_p * 2), ("down", ctypes.c_void_p * 2),
+                ("conv_w", ctypes.c_void_p * 2), ("conv_b", ctypes.c_void_p * 2)]
 
 
 class RewardCfg(ctypes.Structure):
@@ -198,6 +209,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_urm_swiglu_conv": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32]),
         "g2048_urm_pool_heads": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32]),
         "g2048_urm_linear_supported": (ctypes.c_int, [i32, i32, i32, i32]),
+        "g2048_urm_forward_supported": (ctypes.c_int, [i32, i32, i32, i32, i32]),
+        "g2048_urm_forward": (ctypes.c_int, [vp, ctypes.POINTER(UrmWeights), vp, i32, vp, vp, i64]),
         "g2048_urm_linear": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_linear_rms": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32, ctypes.c_float]),
         "g2048_urm_linear_swiglu": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32]),
@@ -698,3 +711,17 @@ def urm_linear_swiglu(inp, w, conv_w, conv_b, out):
                                           _dev(conv_w, torch.float32, "conv_w"), _dev(conv_b, torch.float32, "conv_b"),
                                           _dev(out, torch.bfloat16, "out"), rows, h, w.shape[0] // 2),
            "g2048_urm_linear_swiglu")
+
+
+def urm_forward_supported(hidden: int, heads: int, inter: int, num_layers: int, conv_kernel: int) -> bool:
+    return bool(load().g2048_urm_forward_supported(int(hidden), int(heads), int(inter), int(num_layers),
+                                                   int(conv_kernel)))
+
+
+def urm_forward(weights: UrmWeights, obs, logits, value):
+    """The whole GameURM forward in one launch (g2048_urm_forward); `weights` holds device pointers."""
+    if obs.dtype not in (torch.float32, torch.bfloat16):
+        raise G2048Error("obs must be float32 or bfloat16")
+    _check(load().g2048_urm_forward(_stream(obs), ctypes.byref(weights), _dev(obs, None, "obs"),
+                                    int(obs.dtype == torch.bfloat16), _dev(logits, torch.float32, "logits"),
+                                    _dev(value, torch.float32, "value"), obs.shape[0]), "g2048_urm_forward")

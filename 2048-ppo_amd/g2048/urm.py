@@ -2,7 +2,9 @@
 kernels of include/g2048_urm.h (fused-epilogue MFMA projections for h <= 64; hipBLASLt through
 torch.mm around the elementwise kernels otherwise; bf16 operands, fp32 accumulate).
 
-Per forward of n boards (16 n token rows):
+The default config (h 64, 4 heads, inter 120, 1-2 layers) runs as ONE persistent kernel
+(g2048_urm_forward: activations in registers / LDS, each layer's weights streamed through LDS).
+Otherwise, per forward of n boards (16 n token rows):
   urm_stem                         emb = SiLU(LN(Linear(3->h))),  x = init_hidden + emb
   num_loops x num_layers blocks, h <= 64 (fused projections, no projection output in HBM):
                                    urm_linear (qkv) -> urm_attention -> urm_linear_rms (o_proj + residual
@@ -47,6 +49,22 @@ class URMPolicy:
         # projections with fused epilogues when the kernels cover these shapes (h <= 64)
         self.fused = (L.urm_linear_supported(0, h, 3 * h) and L.urm_linear_supported(1, h, h)
                       and L.urm_linear_supported(2, h, 2 * i, i) and L.urm_linear_supported(1, i, h))
+        # the whole forward in one persistent launch for the default config (g2048_urm_forward)
+        self.mega = L.urm_forward_supported(h, self.heads, i, len(model.layers), cfg.conv_kernel)
+        self._w = None
+        if self.mega:
+            w = L.UrmWeights()
+            w.hidden, w.heads, w.inter, w.num_layers, w.num_loops = h, self.heads, i, len(model.layers), self.loops
+            w.eps = self.eps
+            ptr = lambda t: t.data_ptr()  # noqa: E731
+            w.stem_w, w.ln_w, w.ln_b = ptr(model.stem[0].weight), ptr(model.stem[1].weight), ptr(model.stem[1].bias)
+            w.init_hidden = ptr(self.init_hidden)
+            w.wa, w.ba = ptr(model.action_head.weight), ptr(model.action_head.bias)
+            w.wv, w.bv = ptr(model.value_head.weight), ptr(model.value_head.bias)
+            for l, (blk, mats, cw) in enumerate(zip(model.layers, self.mats, self.conv_w)):
+                w.qkv[l], w.o[l], w.gate_up[l], w.down[l] = (ptr(m) for m in mats)
+                w.conv_w[l], w.conv_b[l] = ptr(cw), ptr(blk.mlp.dwconv.bias)
+            self._w = w
         self._n = -1
         self.sync()
 
@@ -92,6 +110,13 @@ class URMPolicy:
     def __call__(self, obs: torch.Tensor):
         m = self.master
         n = obs.shape[0]
+        if self.mega:
+            if getattr(self, "_nm", -1) != n:
+                self.mlogits = torch.empty(n, 4, dtype=torch.float32, device=obs.device)
+                self.mvalue = torch.empty(n, dtype=torch.float32, device=obs.device)
+                self._nm = n
+            L.urm_forward(self._w, obs.contiguous(), self.mlogits, self.mvalue)
+            return self.mlogits, self.mvalue
         self._buffers(n, obs.device)
         L.urm_stem(obs.contiguous(), m.stem[0].weight, m.stem[1].weight, m.stem[1].bias, self.init_hidden, self.emb,
                    self.x, self.xb)

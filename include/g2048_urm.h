@@ -79,6 +79,24 @@ int g2048_urm_linear_rms(g2048_stream_t stream, const uint16_t *in, const uint16
 int g2048_urm_linear_swiglu(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *conv_w,
                             const float *conv_b, uint16_t *out, int64_t rows, int32_t h, int32_t inter);
 
+/* The whole forward in one persistent kernel (the default GameURMConfig: hidden 64, 4 heads,
+ * inter 120, conv kernel 2, 1 or 2 layers, any loop count): obs [n, 48] (fp32 / bf16) -> logits
+ * fp32 [n, 4], value fp32 [n]; every activation stays in registers / LDS, the weights of the layer
+ * being applied are streamed through LDS.  Weights: bf16 matrices in nn.Linear layout (qkv [192, 64],
+ * o [64, 64], gate_up [240, 64], down [64, 120]); conv_w fp32 [120, 2], conv_b fp32 [120]; stem,
+ * LayerNorm, init_hidden [16, 64] and head parameters fp32. */
+typedef struct g2048_urm_weights {
+    int32_t hidden, heads, inter, num_layers, num_loops;
+    float eps;
+    const float *stem_w, *ln_w, *ln_b, *init_hidden, *wa, *ba, *wv, *bv;
+    const uint16_t *qkv[2], *o[2], *gate_up[2], *down[2];
+    const float *conv_w[2], *conv_b[2];
+} g2048_urm_weights;
+
+int g2048_urm_forward_supported(int32_t hidden, int32_t heads, int32_t inter, int32_t num_layers, int32_t conv_kernel);
+int g2048_urm_forward(g2048_stream_t stream, const g2048_urm_weights *w, const void *obs, int32_t obs_dtype,
+                      float *logits, float *value, int64_t n);
+
 #ifdef __cplusplus
 }
 #endif

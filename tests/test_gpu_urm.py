@@ -283,6 +283,7 @@ def test_urm_fused_and_library_paths_agree(dev):
     m = agent.GameURM(agent.GameURMConfig(dropout=0.0)).to(dev).eval()
     pol = URMPolicy(m)
     assert pol.fused
+    pol.mega = False  # the per-op chain: fused projections vs library projections
     obs = torch.rand(2048, 48, device=dev) * 6
     lf, vf = [t.clone() for t in pol(obs)]
     pol.fused = False
@@ -292,3 +293,35 @@ def test_urm_fused_and_library_paths_agree(dev):
     e_f, e_l = (lf - ref_l).abs().max().item(), (ll - ref_l).abs().max().item()
     print(f"fused {e_f:.4g} library {e_l:.4g} vs fp32")
     assert e_f <= SCALE_REL * ref_l.abs().max().item() and (lf - ll).abs().max().item() <= 0.1
+
+
+@pytest.mark.parametrize("layers,loops,n", [(2, 4, 4096), (1, 3, 1001), (2, 2, 17)])
+def test_urm_forward_megakernel_matches_kernel_chain(dev, layers, loops, n):
+    """g2048_urm_forward (the whole forward in one launch) vs the per-op kernel chain of the same
+    policy (same rounding points: bf16 GEMM operands / qkv / attention probabilities and output / act,
+    fp32 projections into their epilogues): equal to accumulation-order noise, and within the fp32
+    bound of the module; ragged board counts."""
+    import agent
+    from g2048 import _lib as L
+    from g2048.urm import URMPolicy
+    torch.manual_seed(layers * 10 + loops)
+    m = agent.GameURM(agent.GameURMConfig(num_layers=layers, num_loops=loops, num_truncated_loops=1,
+                                          dropout=0.0)).to(dev).eval()
+    rng = np.random.default_rng(n)
+    boards = rng.integers(0, 14, size=(n, 16)).astype(np.int8)
+    boards[rng.random(boards.shape) < 0.4] = 0
+    obs = torch.empty(n, 48, dtype=torch.bfloat16, device=dev)
+    L.obs_encode(torch.from_numpy(boards).to(dev), obs)
+    pol = URMPolicy(m)
+    assert pol.mega and pol.fused
+    lm, vm = [t.clone() for t in pol(obs)]
+    pol.mega = False
+    lc, vc = pol(obs)
+    dd = torch.cat([(lm - lc).abs().reshape(-1), (vm - vc).abs().reshape(-1)])
+    d = dd.max().item()
+    with torch.no_grad():
+        ref_l, ref_v = m(obs.float())
+    e = max((lm - ref_l).abs().max().item(), (vm - ref_v.view(-1)).abs().max().item())
+    print(f"megakernel vs chain: max {d:.3g} mean {dd.mean().item():.3g}; vs fp32 {e:.3g}")
+    # a flipped bf16 rounding in one of the 8 blocks shows up as ~1e-2 at the logits
+    assert d <= 0.04 and dd.mean().item() <= 2e-3 and e <= SCALE_REL * ref_l.abs().max().item()
