@@ -570,6 +570,11 @@ constexpr int TP = QKV + 8;                      // bf16 pitch of a wave's tile 
 constexpr int TILE_BYTES = 16 * TP * 2;          // 6 400
 constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
+// small fp32 parameters staged once per kernel (lane-relative LDS offsets instead of dozens of
+// per-lane 64-bit global addresses held in registers)
+constexpr int PS_STEM = 0, PS_LNW = PS_STEM + 3 * H, PS_LNB = PS_LNW + H, PS_INIT = PS_LNB + H,
+              PS_WA = PS_INIT + 16 * H, PS_WV = PS_WA + 4 * H, PS_BA = PS_WV + H, PS_BV = PS_BA + 4,
+              PS_ALL = PS_BV + 4;
 constexpr int NB = 1;                            // boards per wave per batch
 }  // namespace mk
 
@@ -651,11 +656,27 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, t = lane & 15, g = lane >> 4;
     char *tile = smem + mk::W_BYTES + wave * mk::TILE_BYTES;
+    float *par = reinterpret_cast<float *>(smem + mk::W_BYTES + mk::WAVES * mk::TILE_BYTES);
+    {
+        auto put = [&](int off, const float *src, int cnt) {
+            for (int e = tid; e < cnt; e += mk::THREADS) par[off + e] = src[e];
+        };
+        put(mk::PS_STEM, W.stem_w, 3 * mk::H);
+        put(mk::PS_LNW, W.ln_w, mk::H);
+        put(mk::PS_LNB, W.ln_b, mk::H);
+        put(mk::PS_INIT, W.init, 16 * mk::H);
+        put(mk::PS_WA, W.wa, 4 * mk::H);
+        put(mk::PS_WV, W.wv, mk::H);
+        put(mk::PS_BA, W.ba, 4);
+        put(mk::PS_BV, W.bv, 1);
+    }
     const float *cwl = reinterpret_cast<const float *>(smem + mk::OFF_CW);
     const float *cbl = reinterpret_cast<const float *>(smem + mk::OFF_CB);
     const int64_t per_batch = (int64_t)mk::WAVES * mk::NB;
     const int64_t batches = (n + per_batch - 1) / per_batch;
     const int apps = W.layers * W.loops;
+    for (int e = tid; e < mk::W_BYTES / 16; e += mk::THREADS) reinterpret_cast<uint4 *>(smem)[e] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();  // the parameters and the zeroed padding are read by every wave
     for (int64_t bt = blockIdx.x; bt < batches; bt += gridDim.x) {
         f32x4 x[mk::NB][4], emb[mk::NB][4];
         // ---- stem: emb = SiLU(LayerNorm(Linear(3 -> 64)(cells))), x = init_hidden + emb
@@ -675,7 +696,8 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
                     const int f = 16 * ct + 4 * g + i;
-                    const float y = fmaf(W.stem_w[3 * f + 2], c[2], fmaf(W.stem_w[3 * f + 1], c[1], W.stem_w[3 * f] * c[0]));
+                    const float *sw = par + mk::PS_STEM + 3 * f;
+                    const float y = fmaf(sw[2], c[2], fmaf(sw[1], c[1], sw[0] * c[0]));
                     emb[nb][ct][i] = y;
                     s += y;
                 }
@@ -698,9 +720,9 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
                     const int f = 16 * ct + 4 * g + i;
-                    const float e = silu((emb[nb][ct][i] - mean) * rstd * W.ln_w[f] + W.ln_b[f]);
+                    const float e = silu((emb[nb][ct][i] - mean) * rstd * par[mk::PS_LNW + f] + par[mk::PS_LNB + f]);
                     emb[nb][ct][i] = e;
-                    x[nb][ct][i] = W.init[t * mk::H + f] + e;
+                    x[nb][ct][i] = par[mk::PS_INIT + t * mk::H + f] + e;
                 }
         }
         for (int app = 0; app < apps; app++) {
@@ -708,37 +730,47 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
             const bool loop_end = (l == W.layers - 1) && (app < apps - 1);
             if (app < W.layers || W.layers > 1) {  // (re)stage layer l's weights
                 __syncthreads();
-                auto stage = [&](const uint16_t *src, int rows, int k, int pitch, int off, int (*map)(int)) {
-                    const int k4 = k >> 2;
-                    for (int e = tid; e < rows * k4; e += mk::THREADS) {
-                        const int q = e / k4, c4 = e - q * k4;
-                        const int sr = map(q);
-                        uint2 v = make_uint2(0u, 0u);
-                        if (sr >= 0) v = *reinterpret_cast<const uint2 *>(src + (int64_t)sr * k + 4 * c4);
-                        *reinterpret_cast<uint2 *>(smem + off + (q * pitch + 4 * c4) * 2) = v;
+                // one flat list of 16-byte chunks (4 matrices + conv taps / bias), every load of a
+                // thread in flight before its LDS writes: one L2 round trip per staging.  Padding
+                // rows / columns were zeroed once and are never written.
+                constexpr int C_QKV = mk::QKV * 8, C_O = mk::H * 8, C_GU = 2 * mk::INTER * 8, C_D = mk::H * 15;
+                constexpr int C_CW = mk::INTER * 2 / 4, C_CB = mk::INTER / 4;
+                constexpr int C_ALL = C_QKV + C_O + C_GU + C_D + C_CW + C_CB;
+                constexpr int PER = (C_ALL + mk::THREADS - 1) / mk::THREADS;
+                uint4 v[PER];
+                int dst[PER];
+#pragma unroll
+                for (int u = 0; u < PER; u++) {
+                    int e = tid + u * mk::THREADS;
+                    const char *src = nullptr;
+                    int d = -1;
+                    if (e < C_QKV) {
+                        src = reinterpret_cast<const char *>(W.qkv[l]) + 16 * e;
+                        d = mk::OFF_QKV + (e >> 3) * mk::P64 * 2 + 16 * (e & 7);
+                    } else if ((e -= C_QKV) < C_O) {
+                        src = reinterpret_cast<const char *>(W.o[l]) + 16 * e;
+                        d = mk::OFF_O + (e >> 3) * mk::P64 * 2 + 16 * (e & 7);
+                    } else if ((e -= C_O) < C_GU) {
+                        const int r = e >> 3;
+                        src = reinterpret_cast<const char *>(W.gu[l]) + 16 * e;
+                        d = mk::OFF_GU + (r < mk::INTER ? r : r + 8) * mk::P64 * 2 + 16 * (e & 7);
+                    } else if ((e -= C_GU) < C_D) {
+                        const int r = e / 15, c = e - 15 * r;
+                        src = reinterpret_cast<const char *>(W.dn[l]) + 16 * e;
+                        d = mk::OFF_D + r * mk::PD * 2 + 16 * c;
+                    } else if ((e -= C_D) < C_CW) {
+                        src = reinterpret_cast<const char *>(W.cw[l]) + 16 * e;
+                        d = mk::OFF_CW + 16 * e;
+                    } else if ((e -= C_CW) < C_CB) {
+                        src = reinterpret_cast<const char *>(W.cb[l]) + 16 * e;
+                        d = mk::OFF_CB + 16 * e;
                     }
-                };
-                stage(W.qkv[l], mk::QKV, mk::H, mk::P64, mk::OFF_QKV, [](int q) { return q; });
-                stage(W.o[l], mk::H, mk::H, mk::P64, mk::OFF_O, [](int q) { return q; });
-                stage(W.gu[l], mk::GU, mk::H, mk::P64, mk::OFF_GU, [](int q) {
-                    return q < 128 ? (q < mk::INTER ? q : -1) : (q - 128 < mk::INTER ? mk::INTER + q - 128 : -1);
-                });
-                {   // down rows: K = 120 real columns, zero to 128
-                    for (int e = tid; e < mk::H * (mk::KD / 4); e += mk::THREADS) {
-                        const int q = e / (mk::KD / 4), c4 = e - q * (mk::KD / 4);
-                        uint2 v = make_uint2(0u, 0u);
-                        if (4 * c4 < mk::INTER) v = *reinterpret_cast<const uint2 *>(W.dn[l] + (int64_t)q * mk::INTER + 4 * c4);
-                        *reinterpret_cast<uint2 *>(smem + mk::OFF_D + (q * mk::PD + 4 * c4) * 2) = v;
-                    }
+                    v[u] = src ? *reinterpret_cast<const uint4 *>(src) : make_uint4(0u, 0u, 0u, 0u);
+                    dst[u] = d;
                 }
-                for (int e = tid; e < mk::KD; e += mk::THREADS) {
-                    float* cw = reinterpret_cast<float *>(smem + mk::OFF_CW);
-                    float* cb = reinterpret_cast<float *>(smem + mk::OFF_CB);
-                    const bool in = e < mk::INTER;
-                    cw[2 * e] = in ? W.cw[l][2 * e] : 0.0f;
-                    cw[2 * e + 1] = in ? W.cw[l][2 * e + 1] : 0.0f;
-                    cb[e] = in ? W.cb[l][e] : 0.0f;
-                }
+#pragma unroll
+                for (int u = 0; u < PER; u++)
+                    if (dst[u] >= 0) *reinterpret_cast<uint4 *>(smem + dst[u]) = v[u];
                 __syncthreads();
             }
 #pragma unroll 1
@@ -857,8 +889,8 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
                     pv *= 1.0f / 16.0f;
                     const int f = 16 * ct + 4 * g + i;
 #pragma unroll
-                    for (int k = 0; k < 4; k++) acc5[k] = fmaf(pv, W.wa[k * mk::H + f], acc5[k]);
-                    acc5[4] = fmaf(pv, W.wv[f], acc5[4]);
+                    for (int k = 0; k < 4; k++) acc5[k] = fmaf(pv, par[mk::PS_WA + k * mk::H + f], acc5[k]);
+                    acc5[4] = fmaf(pv, par[mk::PS_WV + f], acc5[4]);
                 }
 #pragma unroll
             for (int k = 0; k < 5; k++) {
@@ -867,8 +899,8 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
             }
             if (b < n && lane == 0) {
 #pragma unroll
-                for (int k = 0; k < 4; k++) logits[b * 4 + k] = acc5[k] + W.ba[k];
-                value[b] = acc5[4] + W.bv[0];
+                for (int k = 0; k < 4; k++) logits[b * 4 + k] = acc5[k] + par[mk::PS_BA + k];
+                value[b] = acc5[4] + par[mk::PS_BV];
             }
         }
     }
@@ -1008,8 +1040,9 @@ int g2048_urm_forward(g2048_stream_t stream, const g2048_urm_weights *w, const v
     for (int l = 0; l < w->num_layers; l++) {
         if (!w->qkv[l] || !w->o[l] || !w->gate_up[l] || !w->down[l] || !w->conv_w[l] || !w->conv_b[l])
             return G2048_EINVAL;
-        if (((uintptr_t)w->qkv[l] | (uintptr_t)w->o[l] | (uintptr_t)w->gate_up[l] | (uintptr_t)w->down[l]) % 8)
-            return G2048_EINVAL;
+        if (((uintptr_t)w->qkv[l] | (uintptr_t)w->o[l] | (uintptr_t)w->gate_up[l] | (uintptr_t)w->down[l] |
+             (uintptr_t)w->conv_w[l] | (uintptr_t)w->conv_b[l]) % 16)
+            return G2048_EINVAL;  // staged as 16-byte chunks
         a.qkv[l] = w->qkv[l]; a.o[l] = w->o[l]; a.gu[l] = w->gate_up[l]; a.dn[l] = w->down[l];
         a.cw[l] = w->conv_w[l]; a.cb[l] = w->conv_b[l];
     }
@@ -1019,7 +1052,7 @@ int g2048_urm_forward(g2048_stream_t stream, const g2048_urm_weights *w, const v
     const int64_t per_batch = (int64_t)mk::WAVES * mk::NB;
     int64_t grid = (n + per_batch - 1) / per_batch;
     grid = grid > 256 ? 256 : grid;  // one block per CU: the layer's weights fill most of the LDS
-    const size_t lds = (size_t)mk::W_BYTES + (size_t)mk::WAVES * mk::TILE_BYTES;
+    const size_t lds = (size_t)mk::W_BYTES + (size_t)mk::WAVES * mk::TILE_BYTES + (size_t)mk::PS_ALL * 4;
     if (obs_dtype == 1)
         hipLaunchKernelGGL(urm_forward_kernel<true>, dim3((unsigned)grid), dim3(mk::THREADS), lds, (hipStream_t)stream,
                            obs, a, logits, value, n);

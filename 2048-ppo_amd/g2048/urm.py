@@ -44,6 +44,9 @@ class URMPolicy:
                                blk.mlp.down_proj.weight)])
         dev = model.stem[0].weight.device
         self.conv_w = [torch.empty(self.inter, 2, dtype=torch.float32, device=dev) for _ in model.layers]
+        # own copies of the conv biases: an optimizer may re-home the 1-D parameters into a flat
+        # buffer at any 4-byte offset, and the one-launch forward stages them as 16-byte chunks
+        self.conv_b = [torch.empty(self.inter, dtype=torch.float32, device=dev) for _ in model.layers]
         self.init_hidden = torch.empty(16, self.h, dtype=torch.float32, device=dev)
         h, i = self.h, self.inter
         # projections with fused epilogues when the kernels cover these shapes (h <= 64)
@@ -63,7 +66,7 @@ class URMPolicy:
             w.wv, w.bv = ptr(model.value_head.weight), ptr(model.value_head.bias)
             for l, (blk, mats, cw) in enumerate(zip(model.layers, self.mats, self.conv_w)):
                 w.qkv[l], w.o[l], w.gate_up[l], w.down[l] = (ptr(m) for m in mats)
-                w.conv_w[l], w.conv_b[l] = ptr(cw), ptr(blk.mlp.dwconv.bias)
+                w.conv_w[l], w.conv_b[l] = ptr(cw), ptr(self.conv_b[l])
             self._w = w
         self._n = -1
         self.sync()
@@ -87,6 +90,8 @@ class URMPolicy:
                                        blk.mlp.down_proj.weight)):
                 dst.copy_(src)
             cw.copy_(blk.mlp.dwconv.weight.view(self.inter, 2))
+        for blk, cb in zip(self.master.layers, self.conv_b):
+            cb.copy_(blk.mlp.dwconv.bias)
         self.init_hidden.copy_(self.master.init_hidden.view(16, self.h))
 
     def _buffers(self, n: int, dev):

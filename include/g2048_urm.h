@@ -84,7 +84,8 @@ int g2048_urm_linear_swiglu(g2048_stream_t stream, const uint16_t *in, const uin
  * fp32 [n, 4], value fp32 [n]; every activation stays in registers / LDS, the weights of the layer
  * being applied are streamed through LDS.  Weights: bf16 matrices in nn.Linear layout (qkv [192, 64],
  * o [64, 64], gate_up [240, 64], down [64, 120]); conv_w fp32 [120, 2], conv_b fp32 [120]; stem,
- * LayerNorm, init_hidden [16, 64] and head parameters fp32. */
+ * LayerNorm, init_hidden [16, 64] and head parameters fp32; the matrices and conv arrays 16-byte
+ * aligned. */
 typedef struct g2048_urm_weights {
     int32_t hidden, heads, inter, num_layers, num_loops;
     float eps;
