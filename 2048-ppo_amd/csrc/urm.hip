@@ -575,7 +575,7 @@ constexpr int THREADS = 64 * WAVES;
 constexpr int PS_STEM = 0, PS_LNW = PS_STEM + 3 * H, PS_LNB = PS_LNW + H, PS_INIT = PS_LNB + H,
               PS_WA = PS_INIT + 16 * H, PS_WV = PS_WA + 4 * H, PS_BA = PS_WV + H, PS_BV = PS_BA + 4,
               PS_ALL = PS_BV + 4;
-constexpr int NB = 1;                            // boards per wave per batch
+constexpr int NB = 2;                            // boards per wave per batch (unrolled)
 }  // namespace mk
 
 struct UrmW {  // device pointers (see g2048_urm_weights)
@@ -585,6 +585,29 @@ struct UrmW {  // device pointers (see g2048_urm_weights)
     int layers, loops;
     float eps;
 };
+
+// butterfly steps across the 16-lane rows on the VALU lane swaps (v_permlane16/32_swap) instead of
+// ds_bpermute round trips through LDS: x op x[lane ^ 16], x op x[lane ^ 32]
+__device__ __forceinline__ float xsum16(float x) {
+    const uint32_t u = __float_as_uint(x);
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xsum32(float x) {
+    const uint32_t u = __float_as_uint(x);
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xmax16(float x) {
+    const uint32_t u = __float_as_uint(x);
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xmax32(float x) {
+    const uint32_t u = __float_as_uint(x);
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
 
 __device__ __forceinline__ void wave_lds_sync() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -629,6 +652,27 @@ __device__ __forceinline__ void tile_gemm(f32x4 (&acc)[CT], const char *w, int p
     }
 }
 
+// the same with the B fragments already in registers
+template <int CT, int KS>
+__device__ __forceinline__ void frag_gemm(f32x4 (&acc)[CT], const char *w, int pitch, const bf16x8 (&fb)[KS], int t,
+                                          int g) {
+    bf16x8 fa[2][KS];
+    const char *wb = w + (t * pitch + 8 * g) * 2;
+#pragma unroll
+    for (int s = 0; s < KS; s++) fa[0][s] = lds16(wb + 64 * s);
+#pragma unroll
+    for (int ct = 0; ct < CT; ct++) {
+        if (ct + 1 < CT) {
+#pragma unroll
+            for (int s = 0; s < KS; s++) fa[(ct + 1) & 1][s] = lds16(wb + 16 * (ct + 1) * pitch * 2 + 64 * s);
+        }
+        asm volatile("" ::: "memory");
+        acc[ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s = 0; s < KS; s++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ct & 1][s], fb[s], acc[ct], 0, 0, 0);
+    }
+}
+
 // x = rms_norm(x + y) [+ emb]  (the token's 64 features in 4 lanes x 16 values)
 __device__ __forceinline__ void rms_update(f32x4 (&x)[4], const f32x4 (&y)[4], const f32x4 (&emb)[4], bool add_emb,
                                            float eps) {
@@ -640,8 +684,7 @@ __device__ __forceinline__ void rms_update(f32x4 (&x)[4], const f32x4 (&y)[4], c
             x[ct][i] += y[ct][i];
             ss += x[ct][i] * x[ct][i];
         }
-    ss += __shfl_xor(ss, 16, 64);
-    ss += __shfl_xor(ss, 32, 64);
+    ss = xsum32(xsum16(ss));
     const float r = rsqrtf(ss * (1.0f / mk::H) + eps);
 #pragma unroll
     for (int ct = 0; ct < 4; ct++)
@@ -701,8 +744,7 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
                     emb[nb][ct][i] = y;
                     s += y;
                 }
-            s += __shfl_xor(s, 16, 64);
-            s += __shfl_xor(s, 32, 64);
+            s = xsum32(xsum16(s));
             const float mean = s * (1.0f / mk::H);
             float v = 0.0f;
 #pragma unroll
@@ -712,8 +754,7 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
                     const float d = emb[nb][ct][i] - mean;
                     v += d * d;
                 }
-            v += __shfl_xor(v, 16, 64);
-            v += __shfl_xor(v, 32, 64);
+            v = xsum32(xsum16(v));
             const float rstd = rsqrtf(v * (1.0f / mk::H) + 1e-5f);
 #pragma unroll
             for (int ct = 0; ct < 4; ct++)
@@ -773,17 +814,23 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
                     if (dst[u] >= 0) *reinterpret_cast<uint4 *>(smem + dst[u]) = v[u];
                 __syncthreads();
             }
-#pragma unroll 1
+#pragma unroll
             for (int nb = 0; nb < mk::NB; nb++) {
                 f32x4 *xr = x[nb];
                 // xb -> tile, qkv
                 tile_put<4>(tile, reinterpret_cast<const f32x4(&)[4]>(*xr), t, g);
                 wave_lds_sync();
-                {
-                    f32x4 q[12];
-                    tile_gemm<12, 2>(q, smem + mk::OFF_QKV, mk::P64, tile, t, g);
+                {   // qkv in three 64-feature chunks (16 accumulators live), xb fragments held in registers
+                    bf16x8 fb[2];
+                    fb[0] = lds16(tile + (t * mk::TP + 8 * g) * 2);
+                    fb[1] = lds16(tile + (t * mk::TP + 32 + 8 * g) * 2);
                     wave_lds_sync();
-                    tile_put<12>(tile, q, t, g);
+#pragma unroll
+                    for (int c = 0; c < 3; c++) {
+                        f32x4 q[4];
+                        frag_gemm<4, 2>(q, smem + mk::OFF_QKV + 64 * c * mk::P64 * 2, mk::P64, fb, t, g);
+                        tile_put<4>(tile, q, t, g, 64 * c);
+                    }
                     wave_lds_sync();
                 }
                 // attention, per head: O over the head's Q columns
@@ -802,16 +849,14 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
                         p[r] = st[r] * 0.25f;  // 1 / sqrt(head_dim 16)
                         m = fmaxf(m, p[r]);
                     }
-                    m = fmaxf(m, __shfl_xor(m, 16, 64));
-                    m = fmaxf(m, __shfl_xor(m, 32, 64));
+                    m = xmax32(xmax16(m));
                     float sum = 0.0f;
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         p[r] = __expf(p[r] - m);
                         sum += p[r];
                     }
-                    sum += __shfl_xor(sum, 16, 64);
-                    sum += __shfl_xor(sum, 32, 64);
+                    sum = xsum32(xsum16(sum));
                     const float inv = 1.0f / sum;
                     s16x4 pb;
 #pragma unroll
@@ -894,8 +939,7 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
                 }
 #pragma unroll
             for (int k = 0; k < 5; k++) {
-                acc5[k] += __shfl_xor(acc5[k], 16, 64);
-                acc5[k] += __shfl_xor(acc5[k], 32, 64);
+                acc5[k] = xsum32(xsum16(acc5[k]));
             }
             if (b < n && lane == 0) {
 #pragma unroll
