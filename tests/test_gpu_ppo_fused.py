@@ -330,9 +330,22 @@ def _golden_model(dev, u):
     return m
 
 
+# Absolute per-tensor bounds of the fused update vs the reference's fp32 step.  Muon moves a matrix
+# by the orthogonalised gradient (Newton-Schulz equalises its singular values), so a direction whose
+# singular value sits at bf16 noise level is scaled up like the others: the lower the gradient's
+# effective rank the looser the cosine.  Measured on MI355X (fused / torch bf16 autocast):
+# stem 0.9900 / 0.9918, backbone.0 0.9885 / 0.9905, backbone.1 0.9724 / 0.9775, action_head
+# (rank <= 4) 0.8859 / 0.8620, value_head (rank 1: Muon is a normalisation) 0.9990 / 0.9948.
+MUON_COS = {"stem.0.weight": 0.98, "backbone.0.mlp.0.weight": 0.98, "backbone.1.mlp.0.weight": 0.96,
+            "action_head.weight": 0.85, "value_head.weight": 0.99}
+ADAMW_SIGN = 0.95  # measured worst 0.9688 (backbone.1 LayerNorm bias; autocast 0.9688)
+
+
 def test_fused_update_matches_reference_step(dev):
-    """FusedPPOUpdater (bf16 activations) vs the reference's model_optimize_step (fp32 autograd),
-    judged against torch's own bf16 autocast of the same step (PPOUpdater with amp)."""
+    """FusedPPOUpdater (bf16 activations) vs the reference's model_optimize_step (fp32 autograd) on
+    the golden step (dropout 0, one minibatch): statistics within 2 %, every Muon matrix's move at
+    cosine >= MUON_COS[name] and norm within 5 %, every AdamW tensor's move sign-equal on >= ADAMW_SIGN
+    of its entries (absolute bounds; torch's bf16 autocast of the same step is printed beside them)."""
     from g2048 import _lib as L
     from g2048.dist import GradBucket
     from g2048.fastmlp import FusedPPOUpdater
@@ -364,18 +377,29 @@ def test_fused_update_matches_reference_step(dev):
                 assert math.isclose(st[k], ref_stats[k], rel_tol=2e-2, abs_tol=1e-4), (k, st[k], ref_stats[k])
         moves[mode] = {k: v.reshape(-1) - torch.from_numpy(u["init::" + k]).to(dev).reshape(-1)
                        for k, v in m.state_dict().items()}
+    rows, bad = [], []
     for k in moves["fused"]:
         want = torch.from_numpy(u["final::" + k] - u["init::" + k]).to(dev).reshape(-1)
         got, ac = moves["fused"][k], moves["autocast"][k]
         if u["init::" + k].ndim >= 2:  # Muon-updated matrices: direction and size of the move
             cos = float(F.cosine_similarity(got, want, dim=0))
             cos_ac = float(F.cosine_similarity(ac, want, dim=0))
-            assert cos > min(0.99, cos_ac - 0.01), (k, cos, cos_ac)
-            assert math.isclose(float(got.norm()), float(want.norm()), rel_tol=5e-2), k
-        # AdamW's first step is lr * sign(grad): the moves must agree in sign where autocast's do
-        agree = float(((got > 0) == (want > 0)).float().mean())
-        agree_ac = float(((ac > 0) == (want > 0)).float().mean())
-        assert agree >= min(0.95, agree_ac - 0.05), (k, agree, agree_ac)
+            ratio = float(got.norm() / want.norm())
+            rows.append(f"{k}: cos {cos:.4f} (autocast {cos_ac:.4f}), norm ratio {ratio:.4f}")
+            # stated bound: cosine >= MUON_COS[k] and the move's norm within 5 % of the reference's
+            if cos < MUON_COS[k] or abs(ratio - 1) > 5e-2:
+                bad.append(rows[-1])
+        else:
+            # AdamW's first step is lr * sign(grad) (|move| = lr where the gradient is not ~0): the
+            # sign must agree on >= ADAMW_SIGN of the entries (the rest are gradients within bf16
+            # noise of 0)
+            agree = float(((got > 0) == (want > 0)).float().mean())
+            agree_ac = float(((ac > 0) == (want > 0)).float().mean())
+            rows.append(f"{k}: sign agreement {agree:.4f} (autocast {agree_ac:.4f})")
+            if agree < ADAMW_SIGN:
+                bad.append(rows[-1])
+    print("\n".join(rows))
+    assert not bad, bad
 
 
 def test_fused_gradients_match_autograd(dev):
