@@ -51,29 +51,29 @@ __device__ __forceinline__ void round_g(const f32x4 (&acc)[NT], f32x2 (&v)[NT][2
 }
 
 // Row statistics over the valid features (valid(n): tile n's 4-group of this lane is < h): the sum
-// in tile order then the xor-16 / xor-32 lane sums; v becomes dv = v - sum/h (one fma); the
-// variance of dv likewise; rstd = 1 / sqrt(var/h + eps).  Returns the mean (sum/h) and rstd.
+// as packed fp32 pairs in tile order (element pairs (0, 1) and (2, 3) of a tile), the pair's two
+// halves added, then the xor-16 / xor-32 lane sums; v becomes dv = v - sum/h (one fma); the
+// variance of dv likewise (packed fmas); rstd = 1 / sqrt(var/h + eps).  Returns the mean (sum/h)
+// and rstd.
 template <int NT, class Valid>
 __device__ __forceinline__ void stats(f32x2 (&v)[NT][2], Valid valid, float inv_n, float &mean, float &rstd) {
-    float sum = 0.0f;
+    f32x2 s2 = {0.0f, 0.0f};
 #pragma unroll
-    for (int n = 0; n < NT; n++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) sum += valid(n) ? v[n][r >> 1][r & 1] : 0.0f;
-    sum = xor32_add(xor16_add(sum));
+    for (int n = 0; n < NT; n++) {
+        const f32x2 t = v[n][0] + v[n][1];
+        s2 = valid(n) ? s2 + t : s2;
+    }
+    float sum = xor32_add(xor16_add(s2.x + s2.y));
     const f32x2 nsum = {-sum, -sum}, invn = {inv_n, inv_n};
-    float var = 0.0f;
+    f32x2 q2 = {0.0f, 0.0f};
 #pragma unroll
     for (int n = 0; n < NT; n++) {
         v[n][0] = __builtin_elementwise_fma(nsum, invn, v[n][0]);
         v[n][1] = __builtin_elementwise_fma(nsum, invn, v[n][1]);
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const float dv = valid(n) ? v[n][r >> 1][r & 1] : 0.0f;
-            var = __builtin_fmaf(dv, dv, var);
-        }
+        const f32x2 q = __builtin_elementwise_fma(v[n][1], v[n][1], __builtin_elementwise_fma(v[n][0], v[n][0], q2));
+        q2 = valid(n) ? q : q2;
     }
-    var = xor32_add(xor16_add(var));
+    const float var = xor32_add(xor16_add(q2.x + q2.y));
     mean = sum * inv_n;
     rstd = 1.0f / sqrtf(__builtin_fmaf(var, inv_n, kEps));
 }

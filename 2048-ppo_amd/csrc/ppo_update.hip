@@ -18,6 +18,7 @@
 // draws regenerated from (row, column group, layer, pass, counter), never stored.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "board.hpp"
 #include "ln_row.hpp"
@@ -1162,6 +1163,200 @@ __global__ __launch_bounds__(kMfThreads) void mlp_fwd_kernel(const uint16_t *__r
     }
 }
 
+// The h = 196 layers (the README model: blocks 196 -> 196, stem 48 -> 196).  One image of W per CU
+// in LDS (conflict-free swizzled pitch), 8 waves, each owning 16-row tiles with no barrier after
+// the staging: the wave reads its X^T B fragments straight from HBM into registers (the first
+// tile's reads are issued before the W image is written, so they overlap the staging; later tiles'
+// reads go out as soon as the previous fragments are consumed), runs the 91 MFMAs, and the
+// LayerNorm / ReLU / dropout / residual epilogue of ln_row.hpp.  G and Y leave through a per-wave
+// LDS tile: the 16 rows of a tile are one contiguous 6 272-B span of the output, written as 16-B
+// lanes (the MFMA layout would scatter 32-B pieces over 16 rows).  Per accumulator the MFMA
+// sequence (k-steps in order, same fragments) and the epilogue are mlp_fwd_kernel's, so both
+// compute bitwise the same G / Y / statistics.  The residual is re-read in the epilogue's layout
+// (an L2 hit: the wave read the same rows moments before).  N and K are compile-time, so every
+// range test outside the last W tile / k-step folds away.
+//
+// Measured alternatives (tools/time_mlp.py, 65 536 rows): 32-row tiles per wave (two MFMAs per W
+// fragment) +8-30 % (registers: the dropout variant spills), 16 waves per CU (128-VGPR cap, spills)
+// +50 %, the slab kernel +40 %; removing any one of X reads, MFMAs or epilogue arithmetic from
+// this kernel saves only ~4 us each: it is latency-bound on the per-wave chain, not on one unit.
+constexpr int kMwWaves = 8;
+constexpr int kMwThreads = 64 * kMwWaves;
+constexpr int kMwNT = 13;
+constexpr int kMwN = 196;
+constexpr int kMwOut = 16 * kMwN * 2;  // bytes of one 16-row output tile (6 272)
+
+__host__ __device__ constexpr int mw_ks(int k) { return (k + 31) / 32; }
+// W image row pitch: 16 B x P with P = 4 or 12 mod 16 (>= 4 KS slots), and 16-B slot q of row r
+// stored at slot q ^ mw_swz(r).  A ds_read_b128 fragment read (lane (g, c) reads slot 4 ks + g of
+// row 16 n + c) then puts each of the instruction's four 16-lane bank groups ({0-3, 12-15, 20-27},
+// ... MI355X_MICROARCH.md, LDS) on 16 distinct slots of the 256-B bank row: conflict-free.
+__host__ __device__ constexpr int mw_pitch(int ks) {
+    return 16 * ((4 * ks) % 16 == 4 || (4 * ks) % 16 == 12 ? 4 * ks : 4 * ks + 4);
+}
+__device__ __forceinline__ int mw_swz(int r) { return (0x1230 >> (4 * ((r >> 2) & 3))) & 3; }  // 0, 3, 2, 1
+__host__ __device__ constexpr size_t mw_w_bytes(int k) { return (size_t)16 * kMwNT * mw_pitch(mw_ks(k)); }
+__host__ __device__ constexpr size_t mw_lds_bytes(int k) {
+    return mw_w_bytes(k) + (size_t)8 * kMwN + (size_t)kMwWaves * kMwOut;
+}
+
+// one 16-row output tile from the wave's LDS tile to HBM as contiguous 16-B lanes: `rows` valid
+// rows (a row is 392 B, so an odd count ends in the middle of a 16-B chunk: that chunk goes as 8 B)
+__device__ __forceinline__ void mw_flush(const char *t, uint16_t *dst, int rows, int lane) {
+    const int bytes = rows * 2 * kMwN;
+#pragma unroll
+    for (int i = 0; i < (kMwOut + 1023) / 1024; i++) {
+        const int o = 16 * (lane + 64 * i);
+        if (o + 16 <= bytes) {
+            *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(dst) + o) = *reinterpret_cast<const uint4 *>(t + o);
+        } else if (o < bytes) {
+            *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(dst) + o) = *reinterpret_cast<const uint2 *>(t + o);
+        }
+    }
+}
+
+template <int K, bool RES, bool DROP>
+__global__ __launch_bounds__(kMwThreads) void mlp_fwd_wide_kernel(const uint16_t *__restrict__ X,
+                                                                  const uint16_t *__restrict__ W,
+                                                                  const float *__restrict__ gamma,
+                                                                  const float *__restrict__ beta,
+                                                                  uint16_t *__restrict__ G, uint16_t *__restrict__ Y,
+                                                                  float *__restrict__ mean_out,
+                                                                  float *__restrict__ rstd_out, int64_t M,
+                                                                  DropArgs da) {
+    constexpr int N = kMwN, NT = kMwNT, KS = mw_ks(K), PW = mw_pitch(KS);
+    constexpr int CPR = 8 * KS;                                 // 8-byte chunks per padded W row (<= 64)
+    constexpr int RPW = (16 * NT + kMwWaves - 1) / kMwWaves;    // padded W rows staged per wave
+    static_assert(K % 4 == 0 && CPR <= 64 && 16 * NT >= N, "shape");
+    static_assert((PW / 16) % 16 == 4 || (PW / 16) % 16 == 12, "pitch");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char *sW = smem;
+    float *sgb = reinterpret_cast<float *>(smem + mw_w_bytes(K));  // gamma[N], beta[N]
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    char *sO = smem + mw_w_bytes(K) + 8 * N + wave * kMwOut;         // this wave's output tile
+    const int g = lane >> 4, col = lane & 15;
+    const int64_t ntile = (M + 15) >> 4, stride = (int64_t)gridDim.x * kMwWaves;
+    int64_t tile = (int64_t)blockIdx.x * kMwWaves + wave;
+
+    // the padded W image: wave w stages rows w, w + 8, ..., lane q its 8-byte chunk q; every
+    // global load in flight before the first LDS write
+    const bool qin = lane < CPR, qk = 4 * lane < K;
+    uint2 wv[RPW];
+#pragma unroll
+    for (int u = 0; u < RPW; u++) {
+        const int r = wave + kMwWaves * u;  // wave-uniform
+        const uint2 t = *reinterpret_cast<const uint2 *>(W + (int64_t)(r < N ? r : 0) * K + (qk ? 4 * lane : 0));
+        wv[u] = (r < N && qk) ? t : make_uint2(0u, 0u);
+    }
+    // B fragments of a tile: lane (g, col) holds row 16 t + col, columns 32 ks + 8 g .. + 7 (zero
+    // past K; K % 4 == 0 so a partial chunk is 4 columns).  Loads are unconditional from clamped
+    // addresses: a row past M reads row 0, which only feeds that row's own (never stored) outputs.
+    bf16x8_t fx[KS];
+    auto load_x = [&](int64_t t) {
+        const int64_t row = 16 * t + col;
+        const uint16_t *xr = X + (row < M ? row : 0) * K;
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            const int k0 = 32 * ks + 8 * g;
+            uint2 lo, hi;
+            if (32 * ks + 32 <= K) {  // the whole k-step inside K (folds after unrolling)
+                lo = *reinterpret_cast<const uint2 *>(xr + k0);
+                hi = *reinterpret_cast<const uint2 *>(xr + k0 + 4);
+            } else {
+                const uint2 a = *reinterpret_cast<const uint2 *>(xr + (k0 < K ? k0 : 0));
+                const uint2 b = *reinterpret_cast<const uint2 *>(xr + (k0 + 4 < K ? k0 + 4 : 0));
+                lo = k0 < K ? a : make_uint2(0u, 0u);
+                hi = k0 + 4 < K ? b : make_uint2(0u, 0u);
+            }
+            fx[ks] = __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+        }
+    };
+    if (tile < ntile) load_x(tile);  // in flight across the W image's LDS writes and the barrier
+    if (qin)
+#pragma unroll
+        for (int u = 0; u < RPW; u++) {
+            const int r = wave + kMwWaves * u;
+            if (r < 16 * NT)  // 8-byte chunk lane of 16-B slot lane / 2, swizzled
+                *reinterpret_cast<uint2 *>(sW + r * PW + 16 * ((lane >> 1) ^ mw_swz(r)) + 8 * (lane & 1)) = wv[u];
+        }
+    for (int e = tid; e < N; e += kMwThreads) {
+        sgb[e] = gamma[e];
+        sgb[N + e] = beta[e];
+    }
+    __syncthreads();
+    const Drop d = make_drop(da);
+    constexpr float inv_n = 1.0f / (float)N;
+    const char *wb = sW + col * PW + 16 * (g ^ mw_swz(col));  // rows 16 n + col share the swizzle
+    const bool lastok = 16 * (NT - 1) + 4 * g < N;           // this lane's 4-group of the last W tile is real
+    auto valid = [&](int n) { return n < NT - 1 || lastok; };
+    char *orow = sO + col * 2 * N + 8 * g;                    // lane's spot in the LDS output tile
+    namespace R = g2048::lnrow;
+    for (; tile < ntile; tile += stride) {
+        f32x4_t acc[NT];
+#pragma unroll
+        for (int n = 0; n < NT; n++)  // W tile-row outer: its KS fragments are the only ones in flight
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) {
+                const bf16x8_t fw =
+                    __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(wb + n * 16 * PW + 64 * ks));
+                const f32x4_t z = {0.0f, 0.0f, 0.0f, 0.0f};  // k-step 0 starts from the inline zero
+                acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw, fx[ks], ks ? acc[n] : z, 0, 0, 0);
+            }
+        const int64_t m = 16 * tile + col;
+        const int rows = (int)(M - 16 * tile < 16 ? M - 16 * tile : 16);  // valid rows of this tile
+        // the residual rows first, then (the fragments are consumed) the next tile's reads: loads
+        // complete in issue order, so the epilogue's wait for the residual never waits for them
+        uint2 xres[NT];
+        if (RES) {
+            const int64_t mc = m < M ? m : 0;
+#pragma unroll
+            for (int n = 0; n < NT; n++)
+                xres[n] = *reinterpret_cast<const uint2 *>(X + mc * K + 16 * n + 4 * g * valid(n));
+        }
+        if (tile + stride < ntile) load_x(tile + stride);
+        R::f32x2 v[NT][2];
+        {
+            uint2 gb[NT];
+            R::round_g<NT>(acc, v, gb);
+            if (G) {  // G through the LDS tile at once: its bits need no register past this point
+#pragma unroll
+                for (int n = 0; n < NT; n++)
+                    if (valid(n)) *reinterpret_cast<uint2 *>(orow + 32 * n) = gb[n];
+                mw_flush(sO, G + 16 * tile * N, rows, lane);
+            }
+        }
+        float mean, rstd;
+        R::stats<NT>(v, valid, inv_n, mean, rstd);
+        if (g == 0 && mean_out && m < M) {
+            mean_out[m] = mean;
+            rstd_out[m] = rstd;
+        }
+        uint4 dpair = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int n = 0; n < NT; n++) {
+            const int f0 = 16 * n + 4 * g;
+            if (!valid(n)) continue;
+            const float4 ga = *reinterpret_cast<const float4 *>(sgb + f0);
+            const float4 be = *reinterpret_cast<const float4 *>(sgb + N + f0);
+            R::f32x2 y0 = R::affine_relu(v[n][0], rstd, R::f32x2{ga.x, ga.y}, R::f32x2{be.x, be.y});
+            R::f32x2 y1 = R::affine_relu(v[n][1], rstd, R::f32x2{ga.z, ga.w}, R::f32x2{be.z, be.w});
+            if (DROP) {
+                float k[4];
+                if ((n & 1) == 0) dpair = drop_draw4(d, (uint32_t)m, (uint32_t)(f0 >> 2));
+                drop_mult_bits(d, drop_half(dpair, (uint32_t)(f0 >> 2)), k);
+                y0 = y0 * R::f32x2{k[0], k[1]};
+                y1 = y1 * R::f32x2{k[2], k[3]};
+            }
+            if (RES) {
+                y0 = R::f32x2{R::bf_lo(xres[n].x), R::bf_hi(xres[n].x)} + y0;
+                y1 = R::f32x2{R::bf_lo(xres[n].y), R::bf_hi(xres[n].y)} + y1;
+            }
+            *reinterpret_cast<uint2 *>(orow + 32 * n) = make_uint2(R::pack_bf2(y0.x, y0.y), R::pack_bf2(y1.x, y1.y));
+        }
+        mw_flush(sO, Y + 16 * tile * N, rows, lane);
+    }
+}
+
 // ------------------------------------------------------------------ policy / value heads -----
 // logits = x Wa^T + ba, value = x Wv^T + bv for the rollout policy (GameMLP.forward, game.py:
 // 1208-1219): one v_mfma_f32_16x16x32_bf16 tile per 16 rows with the 5 head rows as the 16-wide
@@ -1873,6 +2068,32 @@ int g2048_mlp_fwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, c
                                y, mean, rstd, m, n, k, da);                                                        \
     } while (0)
 #define G2048_MF_LAUNCH(NT_) G2048_MF_LAUNCH_KS(NT_, 0)
+    // the h = 196 shapes: mlp_fwd_wide_kernel (W-only LDS, 8 waves); G2048_MLP_FWD_SLAB set in the
+    // environment selects the slab kernel instead (bitwise the same outputs: A/B timing and tests)
+    if (n == kMwN && (k == kMwN || k == 48) && al(y, 16) && (!g || al(g, 16)) && !getenv("G2048_MLP_FWD_SLAB")) {
+        const int64_t ntile = (m + 15) / 16, nwg = (ntile + kMwWaves - 1) / kMwWaves;
+        const dim3 wgrid((unsigned)(nwg > 256 ? 256 : nwg)), wblk(kMwThreads);
+#define G2048_MW_LAUNCH(K_)                                                                                      \
+    do {                                                                                                         \
+        const size_t wl = mw_lds_bytes(K_);                                                                      \
+        if (residual && dr)                                                                                      \
+            hipLaunchKernelGGL((mlp_fwd_wide_kernel<K_, true, true>), wgrid, wblk, wl, s, x, w, gamma, beta, g, y, \
+                               mean, rstd, m, da);                                                               \
+        else if (residual)                                                                                       \
+            hipLaunchKernelGGL((mlp_fwd_wide_kernel<K_, true, false>), wgrid, wblk, wl, s, x, w, gamma, beta, g,  \
+                               y, mean, rstd, m, da);                                                            \
+        else if (dr)                                                                                             \
+            hipLaunchKernelGGL((mlp_fwd_wide_kernel<K_, false, true>), wgrid, wblk, wl, s, x, w, gamma, beta, g,  \
+                               y, mean, rstd, m, da);                                                            \
+        else                                                                                                     \
+            hipLaunchKernelGGL((mlp_fwd_wide_kernel<K_, false, false>), wgrid, wblk, wl, s, x, w, gamma, beta, g, \
+                               y, mean, rstd, m, da);                                                            \
+    } while (0)
+        if (k == kMwN) G2048_MW_LAUNCH(kMwN);
+        else G2048_MW_LAUNCH(48);
+#undef G2048_MW_LAUNCH
+        return status();
+    }
     if (fks == 7) {
         G2048_MF_LAUNCH_KS(13, 7);
         return status();

@@ -97,6 +97,35 @@ def test_mlp_fwd_matches_gemm_plus_ln(dev, m, n, k, res, p):
     torch.testing.assert_close(y1.float(), y0.float(), rtol=2e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("m,k,res,p", [(65536, 196, True, 0.1), (65536, 48, False, 0.0), (70001, 196, True, 0.0),
+                                       (1000, 196, False, 0.2), (33, 48, False, 0.1), (100000, 196, True, 0.1)])
+def test_mlp_fwd_wide_equals_slab_kernel(dev, m, k, res, p, monkeypatch):
+    """The h = 196 wide kernel (W-only LDS, X fragments from HBM, 32-row tiles) and the slab kernel
+    compute bitwise the same G, Y, mean and rstd (same MFMA sequence per accumulator, same
+    epilogue), including ragged M, a grid with several tiles per wave and dropout."""
+    from g2048 import _lib as L
+    n = 196
+    torch.manual_seed(m + k)
+    x = _bf(torch.randn(m, k, device=dev))
+    w = _bf(torch.randn(n, k, device=dev) / k ** 0.5)
+    gamma = torch.rand(n, device=dev) + 0.5
+    beta = torch.randn(n, device=dev) * 0.1
+    ctr = torch.tensor([3], dtype=torch.int64, device=dev)
+    drop = L.make_dropout(p, 2, 0, 91, 0, ctr) if p > 0 else None
+    outs = []
+    for slab in (False, True):
+        if slab:
+            monkeypatch.setenv("G2048_MLP_FWD_SLAB", "1")
+        g, y = (torch.full((m, n), float("nan"), dtype=torch.bfloat16, device=dev) for _ in range(2))
+        mean, rstd = torch.empty(m, device=dev), torch.empty(m, device=dev)
+        L.mlp_fwd(x, w, gamma, beta, res, g, y, mean, rstd, drop)
+        torch.cuda.synchronize()
+        outs.append((g, y, mean, rstd))
+    for a, b in zip(*outs):
+        assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
+                           b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32))
+
+
 def test_dropout_mask_depends_on_counter_layer_pass(dev):
     from g2048 import _lib as L
     m, h = 512, 196
