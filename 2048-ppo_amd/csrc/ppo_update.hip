@@ -1357,6 +1357,182 @@ __global__ __launch_bounds__(kMwThreads) void mlp_fwd_wide_kernel(const uint16_t
     }
 }
 
+// ------------------------------------------------------------------ h = 196 LayerNorm backward
+// ln_bwd_kernel for the README model's blocks (h = 196, dy = heads' share + up to 2 matmul
+// gradients, no fp32 residual gradient) in the MFMA epilogue layout of mlp_fwd_wide_kernel: a wave
+// owns 16-row tiles, lane (g, c) holds row 16 t + c, features 16 n + 4 g .. + 3 (n < 13), so a row
+// reduction is two cross-lane swaps, all 64 lanes are busy (208 slots for 196 features instead of
+// 256) and one dropout Philox call serves two tiles n, n + 1 (the forward's draw, drop_draw4).
+// The heads' share of dy, dz W_heads (rank 5), comes out of two v_mfma_f32_16x16x4_f32 per tile n
+// already in this layout (A = the head weights, held as fragments for the whole launch; B = the
+// tile's dz rows).  Pass 1 forms the masked gradient dzr (kept: 52 registers), the dgamma / dbeta
+// accumulators and the row sums; pass 2 recomputes xhat from the raw G bits and writes dG through
+// the wave's LDS tile as contiguous 16-B stores.  dgamma / dbeta: each lane accumulates its
+// features over its rows across tiles; one 16-lane rotate-sum per wave and one LDS sum per block
+// at the end give the same [block][2 h] partial rows as ln_bwd_kernel.
+constexpr int kLbWaves = 8;
+constexpr int kLbThreads = 64 * kLbWaves;
+constexpr int kLbPad = 16 * kMwNT;  // 208 feature slots
+
+__host__ __device__ constexpr size_t lb_lds_bytes() {
+    return (size_t)4 * 10 * kLbPad + (size_t)kLbWaves * (kMwOut > 4 * 2 * kLbPad ? kMwOut : 4 * 2 * kLbPad);
+}
+
+__device__ __forceinline__ float row16_sum(float v) {  // sum over the 16 lanes of a DPP row (every lane)
+    v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x128, 0xF, 0xF, false));  // row_ror:8
+    v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x124, 0xF, 0xF, false));  // row_ror:4
+    v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x122, 0xF, 0xF, false));  // row_ror:2
+    v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x121, 0xF, 0xF, false));  // row_ror:1
+    return v;
+}
+
+template <bool DROP, bool HEAD, int NP>
+__global__ __launch_bounds__(kLbThreads) void ln_bwd196_kernel(DySrc src, const uint16_t *__restrict__ g,
+                                                                const float *__restrict__ mean_in,
+                                                                const float *__restrict__ rstd_in,
+                                                                const float *__restrict__ gamma,
+                                                                const float *__restrict__ beta,
+                                                                uint16_t *__restrict__ dg, float *__restrict__ part,
+                                                                int64_t m, DropArgs da) {
+    constexpr int N = kMwN, NT = kMwNT;
+    namespace R = g2048::lnrow;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float *sgm = reinterpret_cast<float *>(smem), *sbt = sgm + kLbPad;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int gq = lane >> 4, col = lane & 15;
+    char *sO = smem + 4 * 10 * kLbPad + wave * (kMwOut > 4 * 2 * kLbPad ? kMwOut : 4 * 2 * kLbPad);
+    for (int e = tid; e < kLbPad; e += kLbThreads) {
+        sgm[e] = e < N ? gamma[e] : 0.0f;
+        sbt[e] = e < N ? beta[e] : 0.0f;
+    }
+    // head weights W_heads^T [208][8] (rows 5-7 and features past N zero) for the A fragments of
+    // v_mfma_f32_16x16x4_f32: lane (f = l & 15, k = l >> 4) reads swh[k][16 n + f], swh[4 + k][..]
+    float *swh = sbt + kLbPad;
+    for (int e = tid; e < 8 * kLbPad; e += kLbThreads) {
+        const int k = e / kLbPad, f = e - k * kLbPad;
+        float v = 0.0f;
+        if (HEAD && f < N) v = k < 4 ? src.wa[k * N + f] : (k == 4 && src.wv ? src.wv[f] : 0.0f);
+        swh[e] = v;
+    }
+    __syncthreads();
+    const Drop d = make_drop(da);
+    constexpr float inv_h = 1.0f / (float)N;
+    const bool lastok = 16 * (NT - 1) + 4 * gq < N;
+    auto valid = [&](int n) { return n < NT - 1 || lastok; };
+    char *orow = sO + col * 2 * N + 8 * gq;
+    R::f32x2 ag[NT][2], ab[NT][2];
+#pragma unroll
+    for (int n = 0; n < NT; n++) ag[n][0] = ag[n][1] = ab[n][0] = ab[n][1] = R::f32x2{0.0f, 0.0f};
+    const int64_t ntile = (m + 15) >> 4;
+    for (int64_t tile = (int64_t)blockIdx.x * kLbWaves + wave; tile < ntile; tile += (int64_t)gridDim.x * kLbWaves) {
+        const int64_t row = 16 * tile + col;
+        const bool live = row < m;
+        const int64_t rc = live ? row : 0;
+        const int rows = (int)(m - 16 * tile < 16 ? m - 16 * tile : 16);
+        uint2 gr[NT], pr[NP > 0 ? NP : 1][NT];
+#pragma unroll
+        for (int n = 0; n < NT; n++) {
+            const int f0 = 16 * n + 4 * gq * valid(n);  // an invalid lane re-reads an in-row group
+            gr[n] = *reinterpret_cast<const uint2 *>(g + rc * N + f0);
+#pragma unroll
+            for (int i = 0; i < NP; i++) pr[i][n] = *reinterpret_cast<const uint2 *>(src.p[i] + rc * N + f0);
+        }
+        const float mu = mean_in[rc], rs = rstd_in[rc];
+        // heads' share, B: lane (k = l >> 4, j = l & 15) holds dz[16 t + j][k] (value column 4 for k == 0)
+        const float b0 = HEAD ? src.dz[rc * 8 + gq] : 0.0f;
+        const float b1 = (HEAD && gq == 0) ? src.dz[rc * 8 + 4] : 0.0f;
+        // pass 1: dzr = dy * [z > 0] * keep, dgamma / dbeta accumulators, row sums
+        R::f32x2 dzr[NT][2];
+        R::f32x2 s1 = {0.0f, 0.0f}, s2 = {0.0f, 0.0f};
+        const R::f32x2 nmu = {-mu, -mu}, rs2 = {rs, rs};
+        uint4 dpair = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int n = 0; n < NT; n++) {
+            const int f0 = 16 * n + 4 * gq;
+            f32x4_t dy = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (HEAD) {
+                dy = __builtin_amdgcn_mfma_f32_16x16x4f32(swh[gq * kLbPad + 16 * n + col], b0, dy, 0, 0, 0);
+                dy = __builtin_amdgcn_mfma_f32_16x16x4f32(swh[(4 + gq) * kLbPad + 16 * n + col], b1, dy, 0, 0, 0);
+            }
+            float t[4] = {dy[0], dy[1], dy[2], dy[3]};
+#pragma unroll
+            for (int i = 0; i < NP; i++) {
+                t[0] += R::bf_lo(pr[i][n].x);
+                t[1] += R::bf_hi(pr[i][n].x);
+                t[2] += R::bf_lo(pr[i][n].y);
+                t[3] += R::bf_hi(pr[i][n].y);
+            }
+            const float4 gm = *reinterpret_cast<const float4 *>(sgm + f0);
+            const float4 bt = *reinterpret_cast<const float4 *>(sbt + f0);
+            const R::f32x2 xh0 = (R::f32x2{R::bf_lo(gr[n].x), R::bf_hi(gr[n].x)} + nmu) * rs2;
+            const R::f32x2 xh1 = (R::f32x2{R::bf_lo(gr[n].y), R::bf_hi(gr[n].y)} + nmu) * rs2;
+            const R::f32x2 z0 = __builtin_elementwise_fma(xh0, R::f32x2{gm.x, gm.y}, R::f32x2{bt.x, bt.y});
+            const R::f32x2 z1 = __builtin_elementwise_fma(xh1, R::f32x2{gm.z, gm.w}, R::f32x2{bt.z, bt.w});
+            const bool on = live && valid(n);
+            float k[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+            if (DROP) {
+                if ((n & 1) == 0) dpair = drop_draw4(d, (uint32_t)rc, (uint32_t)(f0 >> 2));
+                drop_mult_bits(d, drop_half(dpair, (uint32_t)(f0 >> 2)), k);
+            }
+            const R::f32x2 d0 = {(on && z0.x > 0.0f) ? t[0] * k[0] : 0.0f, (on && z0.y > 0.0f) ? t[1] * k[1] : 0.0f};
+            const R::f32x2 d1 = {(on && z1.x > 0.0f) ? t[2] * k[2] : 0.0f, (on && z1.y > 0.0f) ? t[3] * k[3] : 0.0f};
+            dzr[n][0] = d0;
+            dzr[n][1] = d1;
+            ag[n][0] = __builtin_elementwise_fma(d0, xh0, ag[n][0]);
+            ag[n][1] = __builtin_elementwise_fma(d1, xh1, ag[n][1]);
+            ab[n][0] = ab[n][0] + d0;
+            ab[n][1] = ab[n][1] + d1;
+            const R::f32x2 x0 = d0 * R::f32x2{gm.x, gm.y}, x1 = d1 * R::f32x2{gm.z, gm.w};  // dxhat
+            s1 = s1 + x0 + x1;
+            s2 = __builtin_elementwise_fma(x1, xh1, __builtin_elementwise_fma(x0, xh0, s2));
+        }
+        const float m1 = R::xor32_add(R::xor16_add(s1.x + s1.y)) * inv_h;
+        const float m2 = R::xor32_add(R::xor16_add(s2.x + s2.y)) * inv_h;
+        // pass 2: dG = rstd (dxhat - mean(dxhat) - xhat mean(dxhat xhat)) into the LDS tile
+        const R::f32x2 nm1 = {-m1, -m1}, nm2 = {-m2, -m2};
+#pragma unroll
+        for (int n = 0; n < NT; n++) {
+            if (!valid(n)) continue;
+            const int f0 = 16 * n + 4 * gq;
+            const float4 gm = *reinterpret_cast<const float4 *>(sgm + f0);
+            const R::f32x2 xh0 = (R::f32x2{R::bf_lo(gr[n].x), R::bf_hi(gr[n].x)} + nmu) * rs2;
+            const R::f32x2 xh1 = (R::f32x2{R::bf_lo(gr[n].y), R::bf_hi(gr[n].y)} + nmu) * rs2;
+            const R::f32x2 o0 = __builtin_elementwise_fma(xh0, nm2, dzr[n][0] * R::f32x2{gm.x, gm.y} + nm1) * rs2;
+            const R::f32x2 o1 = __builtin_elementwise_fma(xh1, nm2, dzr[n][1] * R::f32x2{gm.z, gm.w} + nm1) * rs2;
+            *reinterpret_cast<uint2 *>(orow + 32 * n) = make_uint2(R::pack_bf2(o0.x, o0.y), R::pack_bf2(o1.x, o1.y));
+        }
+        mw_flush(sO, dg + 16 * tile * N, rows, lane);
+    }
+    // dgamma / dbeta: the 16 rows of a lane group, then the block's waves (LDS), one partial row
+    float *red = reinterpret_cast<float *>(sO);  // this wave's [2][208] (its output tile is drained)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int n = 0; n < NT; n++)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; h2++) {
+            const float a0 = row16_sum(ag[n][h2].x), a1 = row16_sum(ag[n][h2].y);
+            const float b0 = row16_sum(ab[n][h2].x), b1 = row16_sum(ab[n][h2].y);
+            if (col == 0) {
+                const int f = 16 * n + 4 * gq + 2 * h2;
+                red[f] = a0;
+                red[f + 1] = a1;
+                red[kLbPad + f] = b0;
+                red[kLbPad + f + 1] = b1;
+            }
+        }
+    __syncthreads();
+    const int stride_w = (kMwOut > 4 * 2 * kLbPad ? kMwOut : 4 * 2 * kLbPad) / 4;  // floats between wave regions
+    const float *red0 = reinterpret_cast<const float *>(smem + 4 * 10 * kLbPad);
+    for (int c = tid; c < 2 * N; c += kLbThreads) {
+        const int o = c < N ? c : kLbPad + (c - N);
+        float t = 0.0f;
+#pragma unroll
+        for (int w = 0; w < kLbWaves; w++) t += red0[w * stride_w + o];
+        part[(int64_t)blockIdx.x * 2 * N + c] = t;
+    }
+}
+
 // ------------------------------------------------------------------ policy / value heads -----
 // logits = x Wa^T + ba, value = x Wv^T + bv for the rollout policy (GameMLP.forward, game.py:
 // 1208-1219): one v_mfma_f32_16x16x32_bf16 tile per 16 rows with the 5 head rows as the 16-wide
@@ -1874,6 +2050,37 @@ int g2048_ln_act_bwd(g2048_stream_t stream, const g2048_dy *dy, const uint16_t *
         return status();
     }
     const DropArgs da = drop_args(drop);
+    if (h == kMwN && src.np <= 2 && !src.dres && !dres_out && al(dg, 16)) {  // the h = 196 tile kernel
+        const int64_t nwg = ((m + 15) / 16 + kLbWaves - 1) / kLbWaves;
+        int nb = (int)(nwg < 256 ? nwg : 256);
+        nb = nb < partial_blocks(m) ? nb : partial_blocks(m);
+        const size_t lds = lb_lds_bytes();
+#define G2048_LB196(D_, H_, P_)                                                                                    \
+    hipLaunchKernelGGL((ln_bwd196_kernel<D_, H_, P_>), dim3(nb), dim3(kLbThreads), lds, s, src, g, mean, rstd, gamma, \
+                       beta, dg, partials, m, da)
+#define G2048_LB196_P(D_, H_)                        \
+    do {                                             \
+        if (src.np == 0) G2048_LB196(D_, H_, 0);     \
+        else if (src.np == 1) G2048_LB196(D_, H_, 1); \
+        else G2048_LB196(D_, H_, 2);                 \
+    } while (0)
+        if (drop_on(drop)) {
+            if (head) G2048_LB196_P(true, true);
+            else G2048_LB196_P(true, false);
+        } else {
+            if (head) G2048_LB196_P(false, true);
+            else G2048_LB196_P(false, false);
+        }
+#undef G2048_LB196_P
+#undef G2048_LB196
+        Segs segs{};
+        segs.n = 2;
+        segs.dst[0] = dgamma;
+        segs.len[0] = h;
+        segs.dst[1] = dbeta;
+        segs.len[1] = h;
+        return colsum(s, partials, nb, 2 * h, partials + (size_t)nb * 2 * h, segs, -1, defer);
+    }
     const int nb = bwd_blocks(m);
     const size_t lds = sizeof(float) * kBwdWaves * 2 * h;
 #define G2048_LB(D_, H_)                                                                                             \
