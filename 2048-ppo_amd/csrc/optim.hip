@@ -46,8 +46,9 @@ __device__ __forceinline__ float round_bf(float f) { return (float)(__bf16)f; }
 constexpr int kNormBlocks = 64;
 
 __global__ __launch_bounds__(256) void grad_sumsq_kernel(const float *__restrict__ g, int64_t n,
-                                                         float *__restrict__ part) {
+                                                         float *__restrict__ part, float *__restrict__ tick = nullptr) {
     __shared__ float red[4];
+    if (tick && blockIdx.x == 0 && threadIdx.x == 0) *tick += 1.0f;  // the optimizer's step count
     float s = 0.0f;
     const int64_t n4 = n >> 2;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)kNormBlocks * 256) {
@@ -75,6 +76,39 @@ __global__ __launch_bounds__(64) void grad_norm_kernel(const float *__restrict__
     }
 }
 
+// ------------------------------------------------------------------ AdamW --------------------
+constexpr int kAdamMaxGroups = 4;
+
+struct AdamGroup {
+    float *param;
+    const float *grad;
+    float *m, *v;
+    int64_t n;
+    int lr_index, pad;
+};
+
+struct AdamArgs {
+    AdamGroup g[kAdamMaxGroups];
+    int count;
+    float b1, b2, eps, wd;
+    const float *lr;
+    const float *step;
+    const float *clip;
+};
+
+// one AdamW update of element i (torch.optim.AdamW: decoupled decay, bias corrections)
+__device__ __forceinline__ void adamw_elem(const AdamGroup &gr, int64_t i, float lr, float coef, float b1, float b2,
+                                           float eps, float wd, float bc1, float bc2s) {
+    const float g = gr.grad[i] * coef;
+    float p = gr.param[i] * (1.0f - lr * wd);
+    const float m = gr.m[i] + (1.0f - b1) * (g - gr.m[i]);
+    const float v = gr.v[i] * b2 + (1.0f - b2) * g * g;
+    gr.m[i] = m;
+    gr.v[i] = v;
+    p -= (lr / bc1) * m / (sqrtf(v) / bc2s + eps);
+    gr.param[i] = p;
+}
+
 // ------------------------------------------------------------------ Muon ---------------------
 constexpr int kMuonThreads = 512;        // 8 waves, 2 (tile rows) x 4 (tile columns) blocks
 constexpr int kBI = 7, kBJ = 4;          // 16x16 tiles per wave: the block covers 224 x 256
@@ -99,6 +133,8 @@ struct MuonArgs {
     const float *partials;  // non-null: clip coefficient from the grad_sumsq partials (grad_norm folded in)
     float max_norm;
     float *norm_out, *coef_out;  // written by block 0 when partials is set
+    AdamArgs adam;               // adam.count > 0: blocks count .. count + nadam - 1 run AdamW
+    int nadam;
 };
 
 // LDS images are row-major bf16 with the K dimension zero-padded to a multiple of 8 (pitch =
@@ -283,6 +319,26 @@ __device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_
 
 __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    if ((int)blockIdx.x >= args.count) {  // the 1-D parameters' AdamW, in the same launch
+        float cf = 1.0f;
+        if (args.partials) {  // grad_norm_kernel's arithmetic, as in the Muon blocks (same result)
+            float t = args.partials[threadIdx.x & 63];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+            cf = fminf(args.max_norm / (sqrtf(t) + 1e-6f), 1.0f);
+        }
+        const AdamArgs &a = args.adam;
+        const float t = *a.step;
+        const float bc1 = 1.0f - powf(a.b1, t), bc2s = sqrtf(1.0f - powf(a.b2, t));
+        const int b = (int)blockIdx.x - args.count;
+        for (int k = 0; k < a.count; k++) {
+            const AdamGroup gr = a.g[k];
+            const float lr = a.lr[gr.lr_index];
+            for (int64_t i = (int64_t)b * kMuonThreads + threadIdx.x; i < gr.n; i += (int64_t)args.nadam * kMuonThreads)
+                adamw_elem(gr, i, lr, cf, a.b1, a.b2, a.eps, a.wd, bc1, bc2s);
+        }
+        return;
+    }
     const MuonMat mt = args.m[blockIdx.x];
     const int R = mt.rows, C = mt.cols;
     const bool tr = R > C;  // iterate on the wide orientation (r <= c), like torch
@@ -372,26 +428,6 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     muon_epilogue(mt.param, mt.pbf, sX, px, R, C, tr, 1.0f - lr * args.wd, step, tid);
 }
 
-// ------------------------------------------------------------------ AdamW --------------------
-constexpr int kAdamMaxGroups = 4;
-
-struct AdamGroup {
-    float *param;
-    const float *grad;
-    float *m, *v;
-    int64_t n;
-    int lr_index, pad;
-};
-
-struct AdamArgs {
-    AdamGroup g[kAdamMaxGroups];
-    int count;
-    float b1, b2, eps, wd;
-    const float *lr;
-    const float *step;
-    const float *clip;
-};
-
 __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
     const float t = *a.step;
     const float bc1 = 1.0f - powf(a.b1, t);
@@ -400,16 +436,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
     for (int k = 0; k < a.count; k++) {
         const AdamGroup gr = a.g[k];
         const float lr = a.lr[gr.lr_index];
-        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < gr.n; i += (int64_t)gridDim.x * 256) {
-            const float g = gr.grad[i] * coef;
-            float p = gr.param[i] * (1.0f - lr * a.wd);
-            const float m = gr.m[i] + (1.0f - a.b1) * (g - gr.m[i]);
-            const float v = gr.v[i] * a.b2 + (1.0f - a.b2) * g * g;
-            gr.m[i] = m;
-            gr.v[i] = v;
-            p -= (lr / bc1) * m / (sqrtf(v) / bc2s + a.eps);
-            gr.param[i] = p;
-        }
+        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < gr.n; i += (int64_t)gridDim.x * 256)
+            adamw_elem(gr, i, lr, coef, a.b1, a.b2, a.eps, a.wd, bc1, bc2s);
     }
 }
 
@@ -453,7 +481,10 @@ int g2048_grad_sumsq(g2048_stream_t stream, const float *grad, int64_t n, float 
 
 static int muon_launch(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_t count, const float *lr_dev,
                        const float *clip_coef_dev, const float *partials, float max_norm, float *norm_out,
-                       float *coef_out, const g2048_muon_cfg *cfg);
+                       float *coef_out, const g2048_muon_cfg *cfg, const AdamArgs *adam = nullptr);
+static int adam_args(const g2048_adamw_group *groups, int32_t count, const float *lr_dev, const float *step_dev,
+                     const float *clip_coef_dev, float beta1, float beta2, float eps, float weight_decay, AdamArgs &a,
+                     int64_t &nmax);
 
 int g2048_muon_step(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_t count, const float *lr_dev,
                     const float *clip_coef_dev, const g2048_muon_cfg *cfg) {
@@ -467,9 +498,32 @@ int g2048_muon_step_clip(g2048_stream_t stream, const g2048_muon_matrix *mats, i
     return muon_launch(stream, mats, count, lr_dev, nullptr, partials, max_norm, norm_out, coef_out, cfg);
 }
 
+int g2048_grad_sumsq_tick(g2048_stream_t stream, const float *grad, int64_t n, float *partials, float *step_dev) {
+    if (!grad || !partials || !step_dev || n <= 0 || ((uintptr_t)grad & 15u)) return G2048_EINVAL;
+    hipLaunchKernelGGL(grad_sumsq_kernel, dim3(kNormBlocks), dim3(256), 0, (hipStream_t)stream, grad, n, partials,
+                       step_dev);
+    return status();
+}
+
+int g2048_muon_adamw_step_clip(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_t count,
+                               const g2048_adamw_group *groups, int32_t ngroups, const float *lr_dev,
+                               const float *step_dev, const float *partials, float max_norm, float *norm_out,
+                               float *coef_out, const g2048_muon_cfg *cfg, float beta1, float beta2, float eps,
+                               float adam_weight_decay) {
+    if (!partials || !norm_out || !coef_out || ngroups < 0) return G2048_EINVAL;
+    AdamArgs a{};
+    int64_t nmax = 0;
+    if (ngroups > 0) {
+        const int st = adam_args(groups, ngroups, lr_dev, step_dev, nullptr, beta1, beta2, eps, adam_weight_decay, a, nmax);
+        if (st) return st;
+    }
+    return muon_launch(stream, mats, count, lr_dev, nullptr, partials, max_norm, norm_out, coef_out, cfg,
+                       ngroups > 0 ? &a : nullptr);
+}
+
 static int muon_launch(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_t count, const float *lr_dev,
                        const float *clip_coef_dev, const float *partials, float max_norm, float *norm_out,
-                       float *coef_out, const g2048_muon_cfg *cfg) {
+                       float *coef_out, const g2048_muon_cfg *cfg, const AdamArgs *adam) {
     if (!mats || count <= 0 || count > kMuonMaxMats || !lr_dev || !cfg) return G2048_EINVAL;
     MuonArgs a{};
     size_t lds = 0;
@@ -497,16 +551,22 @@ static int muon_launch(g2048_stream_t stream, const g2048_muon_matrix *mats, int
     a.max_norm = max_norm;
     a.norm_out = norm_out;
     a.coef_out = coef_out;
-    hipLaunchKernelGGL(muon_kernel, dim3(count), dim3(kMuonThreads), lds, (hipStream_t)stream, a);
+    if (adam) {  // AdamW blocks: ~2 elements per thread, at most 8 blocks
+        a.adam = *adam;
+        int64_t nmax = 0;
+        for (int k = 0; k < adam->count; k++) nmax = adam->g[k].n > nmax ? adam->g[k].n : nmax;
+        const int64_t nb = (nmax + 2 * kMuonThreads - 1) / (2 * kMuonThreads);
+        a.nadam = (int)(nb < 1 ? 1 : (nb > 8 ? 8 : nb));
+    }
+    hipLaunchKernelGGL(muon_kernel, dim3(count + a.nadam), dim3(kMuonThreads), lds, (hipStream_t)stream, a);
     return status();
 }
 
-int g2048_adamw_step(g2048_stream_t stream, const g2048_adamw_group *groups, int32_t count, const float *lr_dev,
-                     const float *step_dev, const float *clip_coef_dev, float beta1, float beta2, float eps,
-                     float weight_decay) {
+static int adam_args(const g2048_adamw_group *groups, int32_t count, const float *lr_dev, const float *step_dev,
+                     const float *clip_coef_dev, float beta1, float beta2, float eps, float weight_decay, AdamArgs &a,
+                     int64_t &nmax) {
     if (!groups || count <= 0 || count > kAdamMaxGroups || !lr_dev || !step_dev) return G2048_EINVAL;
-    AdamArgs a{};
-    int64_t nmax = 0;
+    nmax = 0;
     for (int i = 0; i < count; i++) {
         const g2048_adamw_group &g = groups[i];
         if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq || g.n < 0) return G2048_EINVAL;
@@ -521,6 +581,16 @@ int g2048_adamw_step(g2048_stream_t stream, const g2048_adamw_group *groups, int
     a.lr = lr_dev;
     a.step = step_dev;
     a.clip = clip_coef_dev;
+    return G2048_OK;
+}
+
+int g2048_adamw_step(g2048_stream_t stream, const g2048_adamw_group *groups, int32_t count, const float *lr_dev,
+                     const float *step_dev, const float *clip_coef_dev, float beta1, float beta2, float eps,
+                     float weight_decay) {
+    AdamArgs a{};
+    int64_t nmax = 0;
+    const int st = adam_args(groups, count, lr_dev, step_dev, clip_coef_dev, beta1, beta2, eps, weight_decay, a, nmax);
+    if (st) return st;
     int64_t blocks = (nmax + 255) / 256;
     blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);
     hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);

@@ -33,7 +33,7 @@ EXPORTED = (
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
-    "g2048_grad_sumsq", "g2048_muon_step_clip",
+    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
     # include/g2048_urm.h
@@ -221,6 +221,11 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
                                                 ctypes.POINTER(MuonCfg)]),
         "g2048_adamw_step": (ctypes.c_int, [vp, ctypes.POINTER(AdamWGroup), i32, vp, vp, vp, ctypes.c_float,
                                             ctypes.c_float, ctypes.c_float, ctypes.c_float]),
+        "g2048_grad_sumsq_tick": (ctypes.c_int, [vp, vp, i64, vp, vp]),
+        "g2048_muon_adamw_step_clip": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, ctypes.POINTER(AdamWGroup),
+                                                      i32, vp, vp, vp, ctypes.c_float, vp, vp,
+                                                      ctypes.POINTER(MuonCfg), ctypes.c_float, ctypes.c_float,
+                                                      ctypes.c_float, ctypes.c_float]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -543,6 +548,24 @@ def muon_step_clip(mats, lr_dev, partials, max_norm: float, norm_out, coef_out, 
                                        _dev(partials, torch.float32, "partials"), float(max_norm),
                                        _dev(norm_out, torch.float32, "norm_out"), _dev(coef_out, torch.float32, "coef_out"),
                                        ctypes.byref(cfg)), "g2048_muon_step_clip")
+
+
+def grad_sumsq_tick(grad, partials, step_dev):
+    """grad_sumsq + the optimizer's device step count += 1 (one launch)."""
+    _check(load().g2048_grad_sumsq_tick(_stream(grad), _dev(grad, torch.float32, "grad"), grad.numel(),
+                                        _dev(partials, torch.float32, "partials"), _dev(step_dev, torch.float32, "step")),
+           "g2048_grad_sumsq_tick")
+
+
+def muon_adamw_step_clip(mats, groups, lr_dev, step_dev, partials, max_norm: float, norm_out, coef_out, cfg: MuonCfg,
+                         beta1, beta2, eps, adam_weight_decay):
+    """muon_step_clip with the AdamW update of the 1-D groups in the same launch."""
+    _check(load().g2048_muon_adamw_step_clip(
+        _stream(lr_dev), mats, len(mats), groups, len(groups) if groups is not None else 0,
+        _dev(lr_dev, torch.float32, "lr"), _dev(step_dev, torch.float32, "step"),
+        _dev(partials, torch.float32, "partials"), float(max_norm), _dev(norm_out, torch.float32, "norm_out"),
+        _dev(coef_out, torch.float32, "coef_out"), ctypes.byref(cfg), float(beta1), float(beta2), float(eps),
+        float(adam_weight_decay)), "g2048_muon_adamw_step_clip")
 
 
 def adamw_step(groups, lr_dev, step_dev, clip_coef_dev, beta1, beta2, eps, weight_decay):

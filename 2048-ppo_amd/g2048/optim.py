@@ -263,8 +263,14 @@ class FusedMuonAdamW(MuonAdamW):
     def step_clipped(self, flat_grad: torch.Tensor, max_norm: float) -> torch.Tensor:
         """clip_grad_norm_(max_norm) folded into the step (the bucket itself is left unclipped);
         returns the pre-clip norm as a device scalar."""
-        self._L.grad_sumsq(flat_grad, self.norm_part)
-        self._run(self.coef_t, max_norm)
+        if self._mats is None:
+            self._build()
+        # two launches: partial sums of squares (+ the step count), then Muon with the clip folded in
+        # and the AdamW blocks of the 1-D groups
+        self._L.grad_sumsq_tick(flat_grad, self.norm_part, self.step_t)
+        self._L.muon_adamw_step_clip(self._mats, self._groups if len(self._groups) else None, self.lr, self.step_t,
+                                     self.norm_part, max_norm, self.norm_t, self.coef_t, self._cfg, self.b1, self.b2,
+                                     self.eps, self.wd)
         return self.norm_t
 
 

@@ -287,6 +287,18 @@ int g2048_adamw_step(g2048_stream_t stream, const g2048_adamw_group *groups, int
                      const float *step_dev, const float *clip_coef_dev, float beta1, float beta2, float eps,
                      float weight_decay);
 
+/* The whole clipped optimizer step in two launches: g2048_grad_sumsq_tick = g2048_grad_sumsq plus
+ * *step_dev += 1 (the AdamW step count, train.py's optimizer.step bookkeeping); then
+ * g2048_muon_adamw_step_clip = g2048_muon_step_clip whose launch also carries the AdamW update of
+ * the 1-D groups (extra blocks deriving the clip coefficient from the same partials; *step_dev is
+ * the incremented count).  Replaces g2048_muon_step_clip + a step increment + g2048_adamw_step. */
+int g2048_grad_sumsq_tick(g2048_stream_t stream, const float *grad, int64_t n, float *partials, float *step_dev);
+int g2048_muon_adamw_step_clip(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_t count,
+                               const g2048_adamw_group *groups, int32_t ngroups, const float *lr_dev,
+                               const float *step_dev, const float *partials, float max_norm, float *norm_out,
+                               float *coef_out, const g2048_muon_cfg *cfg, float beta1, float beta2, float eps,
+                               float adam_weight_decay);
+
 /* Test hook: the dropout keep mask (uint8 [m,h], 1 = kept) g2048_ln_act_fwd applies. */
 int g2048_dropout_mask(g2048_stream_t stream, int64_t m, int32_t h, const g2048_dropout *drop, uint8_t *mask);
 
