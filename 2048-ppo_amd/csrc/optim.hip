@@ -201,20 +201,34 @@ __device__ __forceinline__ void gemm_block(f32x4_t (&acc)[kBI][kBJ], const char 
     }
 }
 
-__device__ __forceinline__ void zero_acc(f32x4_t (&acc)[kBI][kBJ]) {
+// The accumulators start from the scaled previous output, (beta / alpha) * out[col][row] (zero when
+// beta == 0, and for tiles outside the product), read BEFORE the GEMM: the read and its conversion
+// overlap the MFMA work instead of sitting between the two barriers, and the store is a plain write.
+__device__ __forceinline__ void init_block_t(f32x4_t (&acc)[kBI][kBJ], const char *out, int pitch, int M, int N,
+                                             int ti0, int tj0, float ratio, bool use_old, int lane) {
 #pragma unroll
     for (int i = 0; i < kBI; i++)
 #pragma unroll
-        for (int j = 0; j < kBJ; j++) acc[i][j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int j = 0; j < kBJ; j++) {
+            const int col = 16 * (tj0 + j) + (lane & 15);
+            const int row0 = 16 * (ti0 + i) + 4 * (lane >> 4);
+            f32x4_t a = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (use_old && col < N && row0 < M) {
+                const uint2 q = *reinterpret_cast<const uint2 *>(out + col * pitch + row0 * 2);
+                a = f32x4_t{ratio * bf2f(q.x & 0xFFFFu), ratio * bf2f(q.x >> 16), ratio * bf2f(q.y & 0xFFFFu),
+                            ratio * bf2f(q.y >> 16)};
+            }
+            acc[i][j] = a;
+        }
 }
 
-// Stores the TRANSPOSE of the accumulated block: out[col][row] = bf16(alpha * acc[row][col] +
-// beta * out[col][row]) for cols < N and rows < round4(M).  A lane holds 4 consecutive rows of one
-// column, i.e. 4 consecutive elements of one output row: one 8-byte LDS read-modify-write.  Rows
-// M .. round4(M)-1 land in the zero K padding and are zero (their operands are zero fragments).
-// Callers put a barrier between the GEMM's last read of `out` and this.
+// Stores the TRANSPOSE of the accumulated block: out[col][row] = bf16(alpha * acc[row][col]) for
+// cols < N and rows < round4(M) (acc already holds (beta / alpha) * the old value: init_block_t).
+// A lane holds 4 consecutive rows of one column, i.e. 4 consecutive elements of one output row:
+// one 8-byte LDS write.  Rows M .. round4(M)-1 land in the zero K padding and are zero (their
+// operands are zero fragments).  Callers put a barrier between the GEMM's last read of `out` and this.
 __device__ __forceinline__ void store_block_t(const f32x4_t (&acc)[kBI][kBJ], char *out, int pitch, int M, int N,
-                                              int ti0, int tj0, float alpha, float beta, int lane) {
+                                              int ti0, int tj0, float alpha, int lane) {
     const int TI = (M + 15) >> 4, TJ = (N + 15) >> 4;
     if (ti0 >= TI || tj0 >= TJ) return;
 #pragma unroll
@@ -223,15 +237,10 @@ __device__ __forceinline__ void store_block_t(const f32x4_t (&acc)[kBI][kBJ], ch
         for (int j = 0; j < kBJ; j++) {
             const int col = 16 * (tj0 + j) + (lane & 15);
             const int row0 = 16 * (ti0 + i) + 4 * (lane >> 4);
-            if (col < N && row0 < M) {
-                uint2 *p = reinterpret_cast<uint2 *>(out + col * pitch + row0 * 2);
-                const uint2 q = *p;
-                const float v0 = alpha * acc[i][j][0] + beta * bf2f(q.x & 0xFFFFu);
-                const float v1 = alpha * acc[i][j][1] + beta * bf2f(q.x >> 16);
-                const float v2 = alpha * acc[i][j][2] + beta * bf2f(q.y & 0xFFFFu);
-                const float v3 = alpha * acc[i][j][3] + beta * bf2f(q.y >> 16);
-                *p = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
-            }
+            if (col < N && row0 < M)
+                *reinterpret_cast<uint2 *>(out + col * pitch + row0 * 2) =
+                    make_uint2(pack_bf2(alpha * acc[i][j][0], alpha * acc[i][j][1]),
+                               pack_bf2(alpha * acc[i][j][2], alpha * acc[i][j][3]));
         }
 }
 
@@ -415,10 +424,10 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
         const int po = k == 2 ? px : pg;
         const float alpha = k == 1 ? args.c : 1.0f;
         const float beta = k == 0 ? 0.0f : (k == 1 ? args.b : args.a);
-        zero_acc(acc);
+        init_block_t(acc, out, po, M, N, ti0, tj0, beta / alpha, beta != 0.0f, lane);
         gemm_block(acc, A, pa, k != 2, B, pb, M, N, K, ti0, tj0, zero, lane);
         __syncthreads();
-        store_block_t(acc, out, po, M, N, ti0, tj0, alpha, beta, lane);
+        store_block_t(acc, out, po, M, N, ti0, tj0, alpha, lane);
         __syncthreads();
     }
 
