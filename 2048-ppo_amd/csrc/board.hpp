@@ -173,14 +173,16 @@ __device__ __forceinline__ MonoStats mono_add_tile(MonoStats s, const uint4 &b, 
     return s;
 }
 
+// 4x4 byte transpose in two stages of v_perm_b32 (8 byte-selects instead of shift/mask/or chains):
+// interleave the low / high byte pairs of rows (0, 1) and (2, 3), then gather each column.
+// __builtin_amdgcn_perm(hi, lo, sel): selector bytes 0-3 pick bytes of lo, 4-7 bytes of hi.
 __device__ __forceinline__ uint4 transpose(const uint4 &b) {
-    const uint32_t r0 = b.x, r1 = b.y, r2 = b.z, r3 = b.w;
-    uint4 c;
-    c.x = (r0 & 0xFFu) | ((r1 & 0xFFu) << 8) | ((r2 & 0xFFu) << 16) | (r3 << 24);
-    c.y = ((r0 >> 8) & 0xFFu) | (r1 & 0xFF00u) | ((r2 & 0xFF00u) << 8) | ((r3 & 0xFF00u) << 16);
-    c.z = ((r0 >> 16) & 0xFFu) | ((r1 >> 8) & 0xFF00u) | (r2 & 0xFF0000u) | ((r3 & 0xFF0000u) << 8);
-    c.w = (r0 >> 24) | ((r1 >> 16) & 0xFF00u) | ((r2 >> 8) & 0xFF0000u) | (r3 & 0xFF000000u);
-    return c;
+    const uint32_t p = __builtin_amdgcn_perm(b.y, b.x, 0x05010400u);  // a0 b0 a1 b1
+    const uint32_t q = __builtin_amdgcn_perm(b.y, b.x, 0x07030602u);  // a2 b2 a3 b3
+    const uint32_t u = __builtin_amdgcn_perm(b.w, b.z, 0x05010400u);  // c0 d0 c1 d1
+    const uint32_t v = __builtin_amdgcn_perm(b.w, b.z, 0x07030602u);  // c2 d2 c3 d3
+    return make_uint4(__builtin_amdgcn_perm(u, p, 0x05040100u), __builtin_amdgcn_perm(u, p, 0x07060302u),
+                      __builtin_amdgcn_perm(v, q, 0x05040100u), __builtin_amdgcn_perm(v, q, 0x07060302u));
 }
 
 __device__ __forceinline__ uint4 bswap4(const uint4 &b) {
