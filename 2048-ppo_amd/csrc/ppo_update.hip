@@ -861,7 +861,12 @@ __global__ __launch_bounds__(kThreads) void head_kl_kernel(const uint16_t *__res
 
 constexpr int kWgRows = 64;
 constexpr int kWgThreads = 256;  // 4 waves: one 139-KB-LDS block per CU, 512 registers per lane
-constexpr int kWgItems = 14;  // 8-B staging chunks per thread per step and operand (n <= 224)
+// 8-B staging chunks per thread per step and operand (n <= 224): 64 rows x 56 chunks / threads
+__host__ __device__ constexpr int wg_items(int threads) { return (kWgRows * 56 + threads - 1) / threads; }
+// NW = 8 (the h = 196 layers): two waves per tile block split each 64-row step's two 32-row
+// k-blocks between them (two waves per SIMD: one's MFMAs overlap the other's fragment reads and
+// the staging), and the second half's accumulators are added through LDS before the store.
+__host__ __device__ constexpr size_t wg_combine_bytes(int bi, int bj) { return (size_t)4 * bi * bj * 256 * 4; }
 
 __device__ __forceinline__ bf16x8_t wg_frag(const char *buf, int pitch, int kb, int c0, int lane) {
     const int g = (lane >> 4) & 3, q = (lane >> 2) & 3, p = lane & 3;
@@ -873,42 +878,44 @@ __device__ __forceinline__ bf16x8_t wg_frag(const char *buf, int pitch, int kb, 
     return __builtin_bit_cast(bf16x8_t, v);
 }
 
-template <int BI, int BJ>
-__global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t *__restrict__ A, const uint16_t *__restrict__ B,
-                                                           int64_t M, int n1, int n2, int pa, int pb, int wi_n,
-                                                           int64_t rows_per_block, int bw, float *__restrict__ part) {
+template <int BI, int BJ, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void wgrad_kernel(const uint16_t *__restrict__ A, const uint16_t *__restrict__ B,
+                                                        int64_t M, int n1, int n2, int pa, int pb, int wi_n,
+                                                        int64_t rows_per_block, int bw, float *__restrict__ part) {
+    constexpr int kThr = 64 * NW, kItems = wg_items(kThr), KSPLIT = NW / 4;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tid = threadIdx.x, lane = tid & 63, wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wave = wave_all & 3, sub = wave_all >> 2;  // tile block, k-split half
     const int ti0 = (wave % wi_n) * BI, tj0 = (wave / wi_n) * BJ;  // wave-uniform: scalar branches
     // blockIdx.y picks a band of bw output columns (B columns cb0 .. cb0 + w): more blocks in flight
     const int cb0 = (int)blockIdx.y * bw, w = min(bw, n2 - cb0);
     const int TI = (n1 + 15) >> 4, TJ = (w + 15) >> 4;
     const int stage_bytes = kWgRows * (pa + pb);
-    for (int o = tid * 16; o < 2 * stage_bytes; o += kWgThreads * 16) *reinterpret_cast<uint4 *>(smem + o) = make_uint4(0, 0, 0, 0);
+    for (int o = tid * 16; o < 2 * stage_bytes; o += kThr * 16) *reinterpret_cast<uint4 *>(smem + o) = make_uint4(0, 0, 0, 0);
 
     // Staging: the 64 rows of a step are one contiguous span of A (and of B) in HBM, read as
     // 8-byte chunks c = tid + 256u; each chunk's LDS slot (row pitch pa / pb) is fixed per thread.
     const int ga = n1 >> 2, gb = w >> 2, ca = kWgRows * ga, cb = kWgRows * gb;
     const int64_t r_begin = (int64_t)blockIdx.x * rows_per_block;
     const int64_t r_end = min(M, r_begin + rows_per_block);
-    int offa[kWgItems], offb[kWgItems], srcb[kWgItems], rowb[kWgItems];
+    int offa[kItems], offb[kItems], srcb[kItems], rowb[kItems];
 #pragma unroll
-    for (int u = 0; u < kWgItems; u++) {
-        const int c = tid + u * kWgThreads;
+    for (int u = 0; u < kItems; u++) {
+        const int c = tid + u * kThr;
         const int ra = c / ga, rb = c / gb, qb = c - rb * gb;
         offa[u] = ra * pa + 8 * (c - ra * ga);
         offb[u] = kWgRows * pa + rb * pb + 8 * qb;
         srcb[u] = rb * n2 + cb0 + 4 * qb;  // element offset of the chunk from the step's first row
         rowb[u] = rb;
     }
-    uint2 rega[kWgItems], regb[kWgItems];
+    uint2 rega[kItems], regb[kItems];
     auto load = [&](int64_t r0) {
         const char *sa = reinterpret_cast<const char *>(A + r0 * n1);
         const uint16_t *sb = B + r0 * n2;
         const int64_t va = (r_end - r0) * ga, vrows = r_end - r0;  // valid chunks / rows
 #pragma unroll
-        for (int u = 0; u < kWgItems; u++) {
-            const int c = tid + u * kWgThreads;
+        for (int u = 0; u < kItems; u++) {
+            const int c = tid + u * kThr;
             rega[u] = (c < ca && c < va) ? *reinterpret_cast<const uint2 *>(sa + 8 * c) : make_uint2(0, 0);
             regb[u] = (c < cb && rowb[u] < vrows) ? *reinterpret_cast<const uint2 *>(sb + srcb[u]) : make_uint2(0, 0);
         }
@@ -916,8 +923,8 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t *__res
     auto store = [&](int s) {
         char *base = smem + s * stage_bytes;
 #pragma unroll
-        for (int u = 0; u < kWgItems; u++) {
-            const int c = tid + u * kWgThreads;
+        for (int u = 0; u < kItems; u++) {
+            const int c = tid + u * kThr;
             if (c < ca) *reinterpret_cast<uint2 *>(base + offa[u]) = rega[u];
             if (c < cb) *reinterpret_cast<uint2 *>(base + offb[u]) = regb[u];
         }
@@ -943,6 +950,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t *__res
                                      // MFMA makes the compiler copy its accumulator out and wait)
 #pragma unroll
             for (int kb = 0; kb < 2; kb++) {
+                if (KSPLIT == 2 && kb != sub) continue;  // wave-uniform
                 bf16x8_t fb[BJ];
 #pragma unroll
                 for (int j = 0; j < BJ; j++) fb[j] = wg_frag(bb, pb, kb, 16 * (tj0 + j), lane);
@@ -958,6 +966,21 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t *__res
         if (more) store(s ^ 1);
         __syncthreads();
         s ^= 1;
+    }
+    if (KSPLIT == 2) {  // the second k half's accumulators join the first's through LDS
+        f32x4_t *cmb = reinterpret_cast<f32x4_t *>(smem) + (size_t)wave * BI * BJ * 64;
+        if (sub == 1 && ti0 < TI && tj0 < TJ)
+#pragma unroll
+            for (int i = 0; i < BI; i++)
+#pragma unroll
+                for (int j = 0; j < BJ; j++) cmb[(i * BJ + j) * 64 + lane] = acc[i][j];
+        __syncthreads();
+        if (sub == 1) return;
+        if (ti0 < TI && tj0 < TJ)
+#pragma unroll
+            for (int i = 0; i < BI; i++)
+#pragma unroll
+                for (int j = 0; j < BJ; j++) acc[i][j] = acc[i][j] + cmb[(i * BJ + j) * 64 + lane];
     }
     float *out = part + (int64_t)blockIdx.x * n1 * n2;
     const int col = lane & 15, rowq = (lane >> 4) * 4;
@@ -2211,7 +2234,11 @@ int g2048_wgrad(g2048_stream_t stream, const uint16_t *a, const uint16_t *b, int
     else if (p.bi == 4)
         hipLaunchKernelGGL((wgrad_kernel<4, 4>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, p.bw,
                            partials);
-    else
+    else if (p.wi == 2 && !getenv("G2048_WGRAD_NW4")) {  // 2 x 2 blocks of 7 x 4 tiles: the k-split 8-wave kernel
+        const size_t lds = p.lds > wg_combine_bytes(7, 4) ? p.lds : wg_combine_bytes(7, 4);
+        hipLaunchKernelGGL((wgrad_kernel<7, 4, 8>), grid, dim3(512), lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows,
+                           p.bw, partials);
+    } else
         hipLaunchKernelGGL((wgrad_kernel<7, 4>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, p.bw,
                            partials);
     const int st = status();
