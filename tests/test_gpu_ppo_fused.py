@@ -151,7 +151,10 @@ def test_dropout_mask_depends_on_counter_layer_pass(dev):
     (196, 3001, 0.1, True, True, True, None), (196, 2048, 0.0, True, False, False, None),
     (64, 999, 0.2, False, True, True, None), (300, 1500, 0.1, True, True, False, None),
     (196, 2500, 0.1, False, False, True, "coupled"), (196, 777, 0.0, False, False, False, "decoupled"),
-    (300, 1001, 0.1, True, True, True, "coupled"), (196, 1500, 0.1, False, "three", False, "coupled")])
+    (300, 1001, 0.1, True, True, True, "coupled"), (196, 1500, 0.1, False, "three", False, "coupled"),
+    # the h = 196 tile kernel (ln_bwd196_kernel: <= 2 matmul gradients, no fp32 residual gradient)
+    (196, 4099, 0.1, False, True, False, "coupled"), (196, 65536, 0.1, False, "two", False, "coupled"),
+    (196, 33, 0.2, False, False, False, None), (196, 1000, 0.0, False, "two", False, "decoupled")])
 def test_ln_act_bwd_matches_autograd(dev, h, m, p, with_din, with_pin, with_dout, head):
     from g2048 import _lib as L
     torch.manual_seed(h * 7 + m)
@@ -165,7 +168,8 @@ def test_ln_act_bwd_matches_autograd(dev, h, m, p, with_din, with_pin, with_dout
     rstd = torch.empty(m, device=dev)
     L.ln_act_fwd(g, gamma, beta, None, y, mean, rstd, drop)
     din = torch.randn(m, h, device=dev) if with_din else None
-    pins = [_bf(torch.randn(m, h, device=dev)) for _ in range(3 if with_pin == "three" else int(bool(with_pin)))]
+    npin = {"three": 3, "two": 2}.get(with_pin, int(bool(with_pin)))
+    pins = [_bf(torch.randn(m, h, device=dev)) for _ in range(npin)]
     dg = torch.empty(m, h, dtype=torch.bfloat16, device=dev)
     dout = torch.empty(m, h, device=dev) if with_dout else None
     part = torch.empty(L.ln_act_bwd_partials(m, h), device=dev)
