@@ -1219,8 +1219,8 @@ __host__ __device__ constexpr int mw_pitch(int ks) {
 }
 __device__ __forceinline__ int mw_swz(int r) { return (0x1230 >> (4 * ((r >> 2) & 3))) & 3; }  // 0, 3, 2, 1
 __host__ __device__ constexpr size_t mw_w_bytes(int k) { return (size_t)16 * kMwNT * mw_pitch(mw_ks(k)); }
-__host__ __device__ constexpr size_t mw_lds_bytes(int k) {
-    return mw_w_bytes(k) + (size_t)8 * kMwN + (size_t)kMwWaves * kMwOut;
+__host__ __device__ constexpr size_t mw_lds_bytes(int k, bool kl = false) {
+    return mw_w_bytes(k) + (size_t)8 * kMwN + (size_t)kMwWaves * kMwOut + (kl ? (size_t)4 * 4 * 16 * kMwNT : 0);
 }
 
 // one 16-row output tile from the wave's LDS tile to HBM as contiguous 16-B lanes: `rows` valid
@@ -1238,7 +1238,17 @@ __device__ __forceinline__ void mw_flush(const char *t, uint16_t *dst, int rows,
     }
 }
 
-template <int K, bool RES, bool DROP>
+// KL (the post-step re-forward's last block, train.py:578-601): instead of storing Y, the block
+// output (bf16-rounded, as the stored H would be) goes straight into the action head (fp32 Wa in
+// LDS) and the KL(old || new) of each row is summed / maxed into the block's partial pair, the
+// layout of head_kl_kernel: no H write, no H re-read, no head launch.
+struct KlArgs {
+    const float *wa, *ba, *old_masked;
+    const int64_t *rows;
+    float *part;
+};
+
+template <int K, bool RES, bool DROP, bool KL = false>
 __global__ __launch_bounds__(kMwThreads) void mlp_fwd_wide_kernel(const uint16_t *__restrict__ X,
                                                                   const uint16_t *__restrict__ W,
                                                                   const float *__restrict__ gamma,
@@ -1246,7 +1256,7 @@ __global__ __launch_bounds__(kMwThreads) void mlp_fwd_wide_kernel(const uint16_t
                                                                   uint16_t *__restrict__ G, uint16_t *__restrict__ Y,
                                                                   float *__restrict__ mean_out,
                                                                   float *__restrict__ rstd_out, int64_t M,
-                                                                  DropArgs da) {
+                                                                  DropArgs da, KlArgs ka = KlArgs{}) {
     constexpr int N = kMwN, NT = kMwNT, KS = mw_ks(K), PW = mw_pitch(KS);
     constexpr int CPR = 8 * KS;                                 // 8-byte chunks per padded W row (<= 64)
     constexpr int RPW = (16 * NT + kMwWaves - 1) / kMwWaves;    // padded W rows staged per wave
@@ -1306,9 +1316,18 @@ __global__ __launch_bounds__(kMwThreads) void mlp_fwd_wide_kernel(const uint16_t
         sgb[e] = gamma[e];
         sgb[N + e] = beta[e];
     }
+    // KL: Wa [4][208] fp32 (zero past N) after this block's output tiles
+    float *swa = reinterpret_cast<float *>(smem + mw_w_bytes(K) + 8 * N + (size_t)kMwWaves * kMwOut);
+    if (KL)
+        for (int e = tid; e < 4 * 16 * NT; e += kMwThreads) {
+            const int k = e / (16 * NT), f = e - k * 16 * NT;
+            swa[e] = f < N ? ka.wa[k * N + f] : 0.0f;
+        }
     __syncthreads();
     const Drop d = make_drop(da);
     constexpr float inv_n = 1.0f / (float)N;
+    float ksum = 0.0f, kmax = -INFINITY;
+    const int64_t mv = KL ? (ka.rows ? min(*ka.rows, M) : M) : M;
     const char *wb = sW + col * PW + 16 * (g ^ mw_swz(col));  // rows 16 n + col share the swizzle
     const bool lastok = 16 * (NT - 1) + 4 * g < N;           // this lane's 4-group of the last W tile is real
     auto valid = [&](int n) { return n < NT - 1 || lastok; };
@@ -1355,6 +1374,7 @@ __global__ __launch_bounds__(kMwThreads) void mlp_fwd_wide_kernel(const uint16_t
             rstd_out[m] = rstd;
         }
         uint4 dpair = make_uint4(0u, 0u, 0u, 0u);
+        R::f32x2 lg01 = {0.0f, 0.0f}, lg23 = {0.0f, 0.0f};  // KL: this lane's share of the 4 logits
 #pragma unroll
         for (int n = 0; n < NT; n++) {
             const int f0 = 16 * n + 4 * g;
@@ -1374,9 +1394,74 @@ __global__ __launch_bounds__(kMwThreads) void mlp_fwd_wide_kernel(const uint16_t
                 y0 = R::f32x2{R::bf_lo(xres[n].x), R::bf_hi(xres[n].x)} + y0;
                 y1 = R::f32x2{R::bf_lo(xres[n].y), R::bf_hi(xres[n].y)} + y1;
             }
-            *reinterpret_cast<uint2 *>(orow + 32 * n) = make_uint2(R::pack_bf2(y0.x, y0.y), R::pack_bf2(y1.x, y1.y));
+            const uint2 yb = make_uint2(R::pack_bf2(y0.x, y0.y), R::pack_bf2(y1.x, y1.y));
+            if (KL) {  // logits of the bf16 output: feature f contributes yb[f] * Wa[k][f] to logit k
+                const float yv[4] = {R::bf_lo(yb.x), R::bf_hi(yb.x), R::bf_lo(yb.y), R::bf_hi(yb.y)};
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const R::f32x2 y2 = {yv[u], yv[u]};
+                    lg01 = __builtin_elementwise_fma(y2, R::f32x2{swa[f0 + u], swa[16 * NT + f0 + u]}, lg01);
+                    lg23 = __builtin_elementwise_fma(y2, R::f32x2{swa[2 * 16 * NT + f0 + u], swa[3 * 16 * NT + f0 + u]}, lg23);
+                }
+            } else {
+                *reinterpret_cast<uint2 *>(orow + 32 * n) = yb;
+            }
         }
-        mw_flush(sO, Y + 16 * tile * N, rows, lane);
+        if (!KL) {
+            mw_flush(sO, Y + 16 * tile * N, rows, lane);
+        } else {  // the row's logits (all 4 lanes of the row), then its KL on lane g == 0
+            const float z[4] = {R::xor32_add(R::xor16_add(lg01.x)) + ka.ba[0], R::xor32_add(R::xor16_add(lg01.y)) + ka.ba[1],
+                                R::xor32_add(R::xor16_add(lg23.x)) + ka.ba[2], R::xor32_add(R::xor16_add(lg23.y)) + ka.ba[3]};
+            if (g == 0 && m < mv) {
+                const float4 o4 = *reinterpret_cast<const float4 *>(ka.old_masked + m * 4);
+                const float o[4] = {o4.x, o4.y, o4.z, o4.w};
+                bool ok4[4];
+                float mo = -INFINITY, mn = -INFINITY, nz[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    ok4[k] = o[k] != -INFINITY;
+                    nz[k] = ok4[k] ? z[k] : -INFINITY;
+                    mo = fmaxf(mo, o[k]);
+                    mn = fmaxf(mn, nz[k]);
+                }
+                float so = 0.0f, sn = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    so += ok4[k] ? expf(o[k] - mo) : 0.0f;
+                    sn += ok4[k] ? expf(nz[k] - mn) : 0.0f;
+                }
+                const float lso = mo + logf(so), lsn = mn + logf(sn);
+                float kl = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    if (!ok4[k]) continue;
+                    const float lo = o[k] - lso, ln = nz[k] - lsn;
+                    kl += expf(lo) * (lo - ln);
+                }
+                ksum += kl;
+                kmax = fmaxf(kmax, kl);
+            }
+        }
+    }
+    if (KL) {  // per block: (sum, max) of the rows' KL -> ka.part[blockIdx] (head_kl_kernel's layout)
+        ksum = wave_sum(ksum);
+        kmax = wave_max(kmax);
+        float *red = reinterpret_cast<float *>(sgb);  // gamma / beta are no longer read
+        __syncthreads();
+        if (lane == 0) {
+            red[2 * wave] = ksum;
+            red[2 * wave + 1] = kmax;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            float s2 = 0.0f, mx = -INFINITY;
+            for (int w2 = 0; w2 < kMwWaves; w2++) {
+                s2 += red[2 * w2];
+                mx = fmaxf(mx, red[2 * w2 + 1]);
+            }
+            ka.part[blockIdx.x * 2] = s2;
+            ka.part[blockIdx.x * 2 + 1] = mx;
+        }
     }
 }
 
@@ -2353,6 +2438,35 @@ int g2048_mlp_fwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, c
     return status();
 }
 
+
+int g2048_mlp_fwd_kl(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, const float *gamma,
+                     const float *beta, int64_t m, int32_t n, int32_t k, const g2048_dropout *drop, const float *wa,
+                     const float *ba, const float *old_masked, const int64_t *rows, float *partials, float *out,
+                     g2048_colsum_job *defer) {
+    if (n != kMwN || k != kMwN || m <= 0 || !x || !w || !gamma || !beta || !wa || !ba || !old_masked || !partials ||
+        !out)
+        return G2048_EINVAL;
+    if (!al(x, 8) || !al(w, 8) || !al(gamma, 16) || !al(beta, 16) || !al(old_masked, 16)) return G2048_EINVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    const DropArgs da = drop_args(drop);
+    const int64_t ntile = (m + 15) / 16, nwg = (ntile + kMwWaves - 1) / kMwWaves;
+    const int nb = (int)(nwg > 256 ? 256 : nwg);
+    const KlArgs ka{wa, ba, old_masked, rows, partials};
+    const size_t lds = mw_lds_bytes(kMwN, true);
+    if (drop_on(drop))
+        hipLaunchKernelGGL((mlp_fwd_wide_kernel<kMwN, true, true, true>), dim3(nb), dim3(kMwThreads), lds, s, x, w, gamma,
+                           beta, nullptr, nullptr, nullptr, nullptr, m, da, ka);
+    else
+        hipLaunchKernelGGL((mlp_fwd_wide_kernel<kMwN, true, false, true>), dim3(nb), dim3(kMwThreads), lds, s, x, w,
+                           gamma, beta, nullptr, nullptr, nullptr, nullptr, m, da, ka);
+    const int st = status();
+    if (st) return st;
+    Segs segs{};  // as g2048_ppo_head_kl: out = {sum KL, max KL} over the nb partial pairs
+    segs.n = 1;
+    segs.dst[0] = out;
+    segs.len[0] = 2;
+    return colsum(s, partials, nb, 2, partials + (size_t)nb * 2, segs, 1, defer);
+}
 
 int g2048_head_fwd(g2048_stream_t stream, const uint16_t *x, const float *wa, const float *ba, const float *wv,
                    const float *bv, int64_t m, int32_t h, float *logits, int64_t logits_stride, float *value) {

@@ -33,7 +33,7 @@ EXPORTED = (
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
-    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip",
+    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
     # include/g2048_urm.h
@@ -222,6 +222,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_adamw_step": (ctypes.c_int, [vp, ctypes.POINTER(AdamWGroup), i32, vp, vp, vp, ctypes.c_float,
                                             ctypes.c_float, ctypes.c_float, ctypes.c_float]),
         "g2048_grad_sumsq_tick": (ctypes.c_int, [vp, vp, i64, vp, vp]),
+        "g2048_mlp_fwd_kl": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32, dp, vp, vp, vp, vp, vp, vp, jp]),
         "g2048_muon_adamw_step_clip": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, ctypes.POINTER(AdamWGroup),
                                                       i32, vp, vp, vp, ctypes.c_float, vp, vp,
                                                       ctypes.POINTER(MuonCfg), ctypes.c_float, ctypes.c_float,
@@ -475,6 +476,21 @@ def ppo_head_loss(x, wa, ba, wv, bv, batch: PPOBatch, beta_dev, critic, clip_eps
         _dev(partials, torch.float32, "partials"), _dev(dwa, torch.float32, "dwa"), _dev(dba, torch.float32, "dba"),
         _dev(dwv, torch.float32, "dwv"), _dev(dbv, torch.float32, "dbv"), _dev(sums, torch.float32, "sums"),
         _defer(defer)), "g2048_ppo_head_loss")
+
+
+def mlp_fwd_kl_supported(n: int, k: int) -> bool:
+    return n == 196 and k == 196
+
+
+def mlp_fwd_kl(x, w, gamma, beta, drop, wa, ba, old_masked, partials, out, defer: ColsumJob | None = None, rows=None):
+    """The KL re-forward's last ResidualBlock fused with the action head and the KL reduction."""
+    m, k = x.shape
+    _check(load().g2048_mlp_fwd_kl(
+        _stream(x), _dev(x, torch.bfloat16, "x"), _dev(w, torch.bfloat16, "w"), _dev(gamma, torch.float32, "gamma"),
+        _dev(beta, torch.float32, "beta"), m, w.shape[0], k, ctypes.byref(drop) if drop is not None else None,
+        _dev(wa, torch.float32, "wa"), _dev(ba, torch.float32, "ba"), _dev(old_masked, torch.float32, "old_masked"),
+        _dev(rows, torch.int64, "rows"), _dev(partials, torch.float32, "partials"), _dev(out, torch.float32, "out"),
+        _defer(defer)), "g2048_mlp_fwd_kl")
 
 
 def ppo_head_kl(x, wa, ba, old_masked, partials, out, defer: ColsumJob | None = None, rows=None):

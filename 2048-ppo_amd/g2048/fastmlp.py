@@ -15,7 +15,9 @@ action/value heads), FusedPPOUpdater writes the forward and backward out by hand
               dW_l = dG_l^T H_{l-1}                           g2048_wgrad (bf16 MFMA, fp32 straight
                                                               into the flat gradient bucket)
     step      [RCCL all-reduce] clip, Muon + AdamW            dist.GradBucket / optim.MuonAdamW
-    KL        re-forward with the new weights (train mode)    g2048_ln_act_fwd + g2048_ppo_head_kl
+    KL        re-forward with the new weights (train mode)    g2048_mlp_fwd per layer, the last block fused
+                                                              with the head + KL (g2048_mlp_fwd_kl; else
+                                                              g2048_ppo_head_kl)
 
 Activations are bf16, LayerNorm statistics / gradients / reductions fp32, master weights fp32.
 Dropout keep masks are Philox draws regenerated in the backward pass (nothing stored); they are
@@ -124,9 +126,9 @@ class FusedPPOUpdater(PPOUpdater):
         L.obs_gather(boards, idx, self.x0)
         return self._layers(pass_)
 
-    def _layers(self, pass_: int):
+    def _layers(self, pass_: int, upto: int | None = None):
         x = self.x0
-        for l, (w, ln) in enumerate(zip(self.wbf, self.ln)):
+        for l, (w, ln) in enumerate(zip(self.wbf[:upto], self.ln[:upto])):
             drop = self._drop(l, pass_) if l > 0 else None
             if self.mf_ok[l]:  # Linear + LayerNorm + ReLU + dropout + residual in one MFMA kernel
                 keep = pass_ == 0  # the KL re-forward (pass 1) needs no G / LayerNorm statistics
@@ -206,9 +208,20 @@ class FusedPPOUpdater(PPOUpdater):
             self.opt.step()
             self.refresh_weights()
         with torch.no_grad():
-            x = self._layers(1)  # KL re-forward of the same minibatch (x0 still holds its encoding)
-            kl_job = L.ColsumJob()  # the KL partial rows are reduced by the statistics kernel
-            L.ppo_head_kl(x, self.wa, self.ba, self.masked, self.part_kl, self.kl, defer=kl_job, rows=self.rows)
+            # KL re-forward of the same minibatch (x0 still holds its encoding); the KL partial rows
+            # are reduced by the statistics kernel
+            kl_job = L.ColsumJob()
+            nl = len(self.lin)
+            w_last = self.wbf[-1]
+            if nl > 1 and self.mf_ok[-1] and L.mlp_fwd_kl_supported(w_last.shape[0], w_last.shape[1]):
+                # the last block fused with the action head and the KL reduction (no H write / re-read)
+                x = self._layers(1, upto=nl - 1)
+                ln = self.ln[-1]
+                L.mlp_fwd_kl(x, w_last, ln.weight, ln.bias, self._drop(nl - 1, 1), self.wa, self.ba, self.masked,
+                             self.part_kl, self.kl, defer=kl_job, rows=self.rows)
+            else:
+                x = self._layers(1)
+                L.ppo_head_kl(x, self.wa, self.ba, self.masked, self.part_kl, self.kl, defer=kl_job, rows=self.rows)
             b = beta if torch.is_tensor(beta) else torch.tensor(float(beta), device=self.dev)
             if gn.dim() != 0:
                 gn = gn.reshape(())

@@ -200,6 +200,16 @@ int g2048_ppo_head_kl(g2048_stream_t stream, const uint16_t *x, const float *wa,
                       int32_t h, const float *old_masked, const int64_t *rows, float *partials, float *out,
                       g2048_colsum_job *defer);
 
+/* The KL re-forward's last block and heads in one launch (h = 196 ResidualBlock: n = k = 196):
+ * Y = x + Dropout(ReLU(LN(x W^T))) as g2048_mlp_fwd (residual, no G / statistics), then instead
+ * of storing Y its bf16 values go through the action head (wa [4, 196], ba [4]) and KL(old || new)
+ * of every row is reduced like g2048_ppo_head_kl (same partial pairs, out, defer and rows).
+ * G2048_EINVAL for any other shape (callers then use g2048_mlp_fwd + g2048_ppo_head_kl). */
+int g2048_mlp_fwd_kl(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, const float *gamma,
+                     const float *beta, int64_t m, int32_t n, int32_t k, const g2048_dropout *drop, const float *wa,
+                     const float *ba, const float *old_masked, const int64_t *rows, float *partials, float *out,
+                     g2048_colsum_job *defer);
+
 /* Accumulates one minibatch into the update statistics (train.py:603-642): stats[0..7] +=
  * {loss, policy_loss, entropy_loss, value_loss, grad_norm, entropy, kl_total, kl_average} from the
  * head_loss sums, the KL {sum, max}, the pre-clip gradient norm and beta; stats[8] = max(stats[8],

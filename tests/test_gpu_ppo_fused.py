@@ -126,6 +126,35 @@ def test_mlp_fwd_wide_equals_slab_kernel(dev, m, k, res, p, monkeypatch):
                            b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32))
 
 
+@pytest.mark.parametrize("m,p,ragged", [(65536, 0.1, False), (4099, 0.0, True), (33, 0.2, False)])
+def test_mlp_fwd_kl_equals_block_plus_head_kl(dev, m, p, ragged):
+    """g2048_mlp_fwd_kl (last block + action head + KL in one launch) == g2048_mlp_fwd followed by
+    g2048_ppo_head_kl on the same dropout mask: KL sum and max within fp32 summation-order noise."""
+    from g2048 import _lib as L
+    h = 196
+    torch.manual_seed(m)
+    x = _bf(torch.randn(m, h, device=dev))
+    w = _bf(torch.randn(h, h, device=dev) / h ** 0.5)
+    gamma, beta = torch.rand(h, device=dev) + 0.5, torch.randn(h, device=dev) * 0.1
+    wa, ba = torch.randn(4, h, device=dev) * 0.05, torch.randn(4, device=dev) * 0.1
+    old = torch.randn(m, 4, device=dev)
+    old[torch.rand(m, 4, device=dev) < 0.3] = float("-inf")
+    old[:, 0] = torch.where(torch.isinf(old).all(1), torch.zeros(m, device=dev), old[:, 0])  # >= 1 legal move
+    ctr = torch.tensor([9], dtype=torch.int64, device=dev)
+    drop = L.make_dropout(p, 2, 1, 123, 0, ctr) if p > 0 else None
+    rows = torch.tensor([m - 7 if ragged else m], dtype=torch.int64, device=dev)
+    part = torch.empty(L.ppo_head_partials(m, h), device=dev)
+    ref, got = torch.empty(2, device=dev), torch.empty(2, device=dev)
+    y = torch.empty(m, h, dtype=torch.bfloat16, device=dev)
+    L.mlp_fwd(x, w, gamma, beta, True, None, y, None, None, drop)
+    L.ppo_head_kl(y, wa, ba, old, part, ref, rows=rows)
+    L.mlp_fwd_kl(x, w, gamma, beta, drop, wa, ba, old, part, got, rows=rows)
+    torch.cuda.synchronize()
+    assert float(ref[0]) > 0
+    assert math.isclose(float(got[0]), float(ref[0]), rel_tol=2e-3, abs_tol=1e-6), (got, ref)
+    assert math.isclose(float(got[1]), float(ref[1]), rel_tol=2e-3, abs_tol=1e-6), (got, ref)
+
+
 def test_dropout_mask_depends_on_counter_layer_pass(dev):
     from g2048 import _lib as L
     m, h = 512, 196
@@ -220,6 +249,7 @@ def _head_case(dev, m, h, seed):
     old_logits[~((legal[:, None] >> np.arange(4)) & 1).astype(bool)] = -np.inf
     old_logp = torch.from_numpy(old_logits).log_softmax(-1).numpy()
     idx = g.permutation(M)[:m].astype(np.int64)
+    torch.manual_seed(seed)  # the device tensors too: independent of the tests that ran before
     x = _bf(torch.randn(m, h, device=dev))
     wa = torch.randn(4, h, device=dev) * 0.05
     ba = torch.randn(4, device=dev) * 0.1
