@@ -186,8 +186,15 @@ class GameURMAttention(nn.Module):
 
     def forward(self, h: torch.Tensor) -> torch.Tensor:
         b, s, _ = h.shape
-        q, k, v = self.qkv_proj(h).view(b, s, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).unbind(0)
-        o = F.scaled_dot_product_attention(q, k, v, dropout_p=self.dropout if self.training else 0.0, is_causal=False)
+        qkv = self.qkv_proj(h)
+        p = self.dropout if self.training else 0.0
+        if qkv.is_cuda:
+            from g2048 import urm as _urm  # the HIP attention core and its backward (g2048_urm.h)
+            if _urm.attention_supported(qkv, s, self.hidden_size, self.num_heads, p):
+                o = _urm.URMAttentionFn.apply(qkv.reshape(b * s, 3 * self.hidden_size), self.num_heads)
+                return self.o_proj(o.view(b, s, self.hidden_size))
+        q, k, v = qkv.view(b, s, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).unbind(0)
+        o = F.scaled_dot_product_attention(q, k, v, dropout_p=p, is_causal=False)
         return self.o_proj(o.transpose(1, 2).reshape(b, s, self.hidden_size))
 
 

@@ -949,6 +949,116 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
         }
     }
 }
+// Backward of the attention core for head_dim 16 (the default GameURM: h 64, 4 heads), one wave
+// per (board, head), for training through autograd (agent.GameURMAttention): q, k, v of the 16
+// tokens and dO staged in LDS as fp32, P recomputed (S = Q K^T / 4, row softmax), then
+//   dV = P^T dO,  dP = dO V^T,  dS = P (dP - rowsum(P dP)),  dQ = dS K / 4,  dK = dS^T Q / 4
+// in fp32 (lane t owns row t / 4, columns 4 (t % 4) .. + 3 of each 16 x 16 product; row sums over
+// the 4 lanes of a row by two xor shuffles).  dqkv bf16 [16 n, 3 h] in the qkv layout.
+constexpr int kAbP = 17;  // fp32 LDS row pitch (conflict-free column reads)
+
+__global__ __launch_bounds__(256) void urm_attn_bwd16_kernel(const uint16_t *__restrict__ qkv,
+                                                             const uint16_t *__restrict__ dout,
+                                                             uint16_t *__restrict__ dqkv, int64_t tasks, int h,
+                                                             int heads) {
+    __shared__ float sm[4][6][16 * kAbP];  // per wave: Q, K, V, dO, P, dS
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t task = (int64_t)blockIdx.x * 4 + wave;
+    if (task >= tasks) return;  // wave-uniform; no block barrier below
+    const int64_t b = task / heads;
+    const int hd = (int)(task - b * heads);
+    float *sQ = sm[wave][0], *sK = sm[wave][1], *sV = sm[wave][2], *sO = sm[wave][3], *sP = sm[wave][4],
+          *sS = sm[wave][5];
+    const int r = lane >> 2, c0 = 4 * (lane & 3);
+    const int64_t tok = 16 * b + r;
+    auto sync = [] {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+    };
+    auto put = [&](float *dst, uint2 v) {
+        dst[r * kAbP + c0 + 0] = __uint_as_float(v.x << 16);
+        dst[r * kAbP + c0 + 1] = __uint_as_float(v.x & 0xFFFF0000u);
+        dst[r * kAbP + c0 + 2] = __uint_as_float(v.y << 16);
+        dst[r * kAbP + c0 + 3] = __uint_as_float(v.y & 0xFFFF0000u);
+    };
+    const uint16_t *row = qkv + tok * 3 * h + hd * 16 + c0;
+    const uint2 q = *reinterpret_cast<const uint2 *>(row), k = *reinterpret_cast<const uint2 *>(row + h),
+                v = *reinterpret_cast<const uint2 *>(row + 2 * h),
+                o = *reinterpret_cast<const uint2 *>(dout + tok * h + hd * 16 + c0);
+    put(sQ, q);
+    put(sK, k);
+    put(sV, v);
+    put(sO, o);
+    sync();
+    constexpr float scale = 0.25f;  // 1 / sqrt(16), scaled_dot_product_attention's default
+    auto rowsum4 = [](float x) {     // over the 4 lanes of a row (xor 1, 2)
+        x += __shfl_xor(x, 1);
+        return x + __shfl_xor(x, 2);
+    };
+    // P[r][c0 + u]
+    float p[4];
+    {
+        float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int d = 0; d < 16; d++) {
+            const float qd = sQ[r * kAbP + d];
+#pragma unroll
+            for (int u = 0; u < 4; u++) s[u] = __builtin_fmaf(qd, sK[(c0 + u) * kAbP + d], s[u]);
+        }
+        float mx = fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3]));
+        mx = fmaxf(mx, __shfl_xor(mx, 1));
+        mx = fmaxf(mx, __shfl_xor(mx, 2));
+        float sum = 0.0f;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            p[u] = expf((s[u] - mx) * scale);
+            sum += p[u];
+        }
+        const float inv = 1.0f / rowsum4(sum);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            p[u] *= inv;
+            sP[r * kAbP + c0 + u] = p[u];
+        }
+    }
+    // dP[r][c0 + u] = sum_d dO[r][d] V[c0 + u][d];  dS = P (dP - rowsum(P dP))
+    {
+        float dp[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int d = 0; d < 16; d++) {
+            const float od = sO[r * kAbP + d];
+#pragma unroll
+            for (int u = 0; u < 4; u++) dp[u] = __builtin_fmaf(od, sV[(c0 + u) * kAbP + d], dp[u]);
+        }
+        const float rs = rowsum4(p[0] * dp[0] + p[1] * dp[1] + p[2] * dp[2] + p[3] * dp[3]);
+#pragma unroll
+        for (int u = 0; u < 4; u++) sS[r * kAbP + c0 + u] = p[u] * (dp[u] - rs);
+    }
+    sync();
+    // dV[r][c0 + u] = sum_i P[i][r] dO[i][c0 + u];  dQ[r][..] = sum_j dS[r][j] K[j][..] / 4;
+    // dK[r][..] = sum_i dS[i][r] Q[i][..] / 4
+    float dv[4] = {0, 0, 0, 0}, dq[4] = {0, 0, 0, 0}, dk[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const float pir = sP[i * kAbP + r], sri = sS[r * kAbP + i], sir = sS[i * kAbP + r];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            dv[u] = __builtin_fmaf(pir, sO[i * kAbP + c0 + u], dv[u]);
+            dq[u] = __builtin_fmaf(sri, sK[i * kAbP + c0 + u], dq[u]);
+            dk[u] = __builtin_fmaf(sir, sQ[i * kAbP + c0 + u], dk[u]);
+        }
+    }
+    auto pack = [](float a, float b2) {
+        const __attribute__((ext_vector_type(2))) __bf16 t = {(__bf16)a, (__bf16)b2};
+        return __builtin_bit_cast(uint32_t, t);
+    };
+    uint16_t *drow = dqkv + tok * 3 * h + hd * 16 + c0;
+    *reinterpret_cast<uint2 *>(drow) = make_uint2(pack(dq[0] * scale, dq[1] * scale), pack(dq[2] * scale, dq[3] * scale));
+    *reinterpret_cast<uint2 *>(drow + h) =
+        make_uint2(pack(dk[0] * scale, dk[1] * scale), pack(dk[2] * scale, dk[3] * scale));
+    *reinterpret_cast<uint2 *>(drow + 2 * h) = make_uint2(pack(dv[0], dv[1]), pack(dv[2], dv[3]));
+}
+
 }  // namespace
 
 extern "C" {
@@ -981,6 +1091,17 @@ int g2048_urm_attention(g2048_stream_t stream, const uint16_t *qkv, uint16_t *ou
     else
         hipLaunchKernelGGL(urm_attn_kernel<false>, dim3(blocks(tasks, kThreads / 64)), dim3(kThreads), 0,
                            (hipStream_t)stream, qkv, out, tasks, (int)h, (int)heads);
+    return launch_status();
+}
+
+int g2048_urm_attention_bwd(g2048_stream_t stream, const uint16_t *qkv, const uint16_t *dout, uint16_t *dqkv,
+                            int64_t n, int32_t h, int32_t heads) {
+    if (n < 0 || heads <= 0 || h != 16 * heads || h > 512) return G2048_EINVAL;
+    if (n == 0) return G2048_OK;
+    if (!qkv || !dout || !dqkv || ((uintptr_t)qkv | (uintptr_t)dout | (uintptr_t)dqkv) % 8) return G2048_EINVAL;
+    const int64_t tasks = n * heads;
+    hipLaunchKernelGGL(urm_attn_bwd16_kernel, dim3(blocks(tasks, 4)), dim3(256), 0, (hipStream_t)stream, qkv, dout,
+                       dqkv, tasks, (int)h, (int)heads);
     return launch_status();
 }
 

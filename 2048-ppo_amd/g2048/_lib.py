@@ -33,7 +33,7 @@ EXPORTED = (
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
-    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl",
+    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
     # include/g2048_urm.h
@@ -222,6 +222,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_adamw_step": (ctypes.c_int, [vp, ctypes.POINTER(AdamWGroup), i32, vp, vp, vp, ctypes.c_float,
                                             ctypes.c_float, ctypes.c_float, ctypes.c_float]),
         "g2048_grad_sumsq_tick": (ctypes.c_int, [vp, vp, i64, vp, vp]),
+        "g2048_urm_attention_bwd": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
         "g2048_mlp_fwd_kl": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32, dp, vp, vp, vp, vp, vp, vp, jp]),
         "g2048_muon_adamw_step_clip": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, ctypes.POINTER(AdamWGroup),
                                                       i32, vp, vp, vp, ctypes.c_float, vp, vp,
@@ -699,6 +700,13 @@ def urm_attention(qkv, out, heads: int):
     rows, h3 = qkv.shape
     _check(load().g2048_urm_attention(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"), _dev(out, torch.bfloat16, "out"),
                                       rows // 16, h3 // 3, int(heads)), "g2048_urm_attention")
+
+
+def urm_attention_bwd(qkv, dout, dqkv, heads: int):
+    rows, h3 = qkv.shape
+    _check(load().g2048_urm_attention_bwd(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"),
+                                          _dev(dout, torch.bfloat16, "dout"), _dev(dqkv, torch.bfloat16, "dqkv"),
+                                          rows // 16, h3 // 3, int(heads)), "g2048_urm_attention_bwd")
 
 
 def urm_residual_rms(x, y, emb, xb, eps: float):

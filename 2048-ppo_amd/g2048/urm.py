@@ -147,3 +147,32 @@ class URMPolicy:
         L.urm_pool_heads(self.x, m.action_head.weight, m.action_head.bias, m.value_head.weight, m.value_head.bias,
                          self.logits, self.value)
         return self.logits, self.value
+
+
+class URMAttentionFn(torch.autograd.Function):
+    """The attention core of GameURMAttention (game.py:1296-1317: scaled_dot_product_attention,
+    no mask, no dropout) for autograd training on the device: forward g2048_urm_attention, backward
+    g2048_urm_attention_bwd (P recomputed; head_dim 16).  qkv bf16 [16 n, 3 h] -> out bf16 [16 n, h]."""
+
+    @staticmethod
+    def forward(ctx, qkv: torch.Tensor, heads: int):
+        qkv = qkv.contiguous()
+        out = torch.empty(qkv.shape[0], qkv.shape[1] // 3, dtype=qkv.dtype, device=qkv.device)
+        L.urm_attention(qkv, out, heads)
+        ctx.save_for_backward(qkv)
+        ctx.heads = heads
+        return out
+
+    @staticmethod
+    def backward(ctx, dout: torch.Tensor):
+        (qkv,) = ctx.saved_tensors
+        dqkv = torch.empty_like(qkv)
+        L.urm_attention_bwd(qkv, dout.to(qkv.dtype).contiguous(), dqkv, ctx.heads)
+        return dqkv, None
+
+
+def attention_supported(qkv: torch.Tensor, seq: int, hidden: int, heads: int, dropout: float) -> bool:
+    """The device attention path applies: bf16 qkv on the GPU (autocast), 16 tokens, head_dim 16, no
+    attention dropout."""
+    return (qkv.is_cuda and qkv.dtype == torch.bfloat16 and seq == 16 and hidden == 16 * heads
+            and dropout == 0.0)

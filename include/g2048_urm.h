@@ -44,6 +44,12 @@ int g2048_urm_stem(g2048_stream_t stream, const void *obs, int32_t obs_dtype, co
 int g2048_urm_attention(g2048_stream_t stream, const uint16_t *qkv, uint16_t *out, int64_t n, int32_t h,
                         int32_t heads);
 
+/* Backward of g2048_urm_attention for head_dim 16 (h = 16 heads): dout bf16 [16 n, h] (the
+ * gradient of the attention output) -> dqkv bf16 [16 n, 3 h] (dq, dk, dv in the qkv layout), P
+ * recomputed in fp32 from q, k (autograd path of GameURMAttention, game.py:1296-1317). */
+int g2048_urm_attention_bwd(g2048_stream_t stream, const uint16_t *qkv, const uint16_t *dout, uint16_t *dqkv,
+                            int64_t n, int32_t h, int32_t heads);
+
 /* Post-norm residual (game.py:1346, 1350 with rms_norm :1223-1229):
  *   x = x + y;  x = x * rsqrt(mean(x^2) + eps)  [+ emb, the next loop's input, game.py:1447];
  *   xb = bf16(x).

@@ -325,3 +325,52 @@ def test_urm_forward_megakernel_matches_kernel_chain(dev, layers, loops, n):
     print(f"megakernel vs chain: max {d:.3g} mean {dd.mean().item():.3g}; vs fp32 {e:.3g}")
     # a flipped bf16 rounding in one of the 8 blocks shows up as ~1e-2 at the logits
     assert d <= 0.04 and dd.mean().item() <= 2e-3 and e <= SCALE_REL * ref_l.abs().max().item()
+
+
+@pytest.mark.parametrize("n,heads", [(4096, 4), (37, 2)])
+def test_urm_attention_backward_matches_sdpa(dev, n, heads):
+    """URMAttentionFn (g2048_urm_attention + g2048_urm_attention_bwd, head_dim 16) vs fp32 autograd
+    of scaled_dot_product_attention on the same bf16 qkv: outputs and dq / dk / dv within bf16
+    rounding (max error <= 2 % of the largest gradient, cosine >= 0.9995)."""
+    import torch.nn.functional as F
+    from g2048.urm import URMAttentionFn
+    h = 16 * heads
+    torch.manual_seed(n + heads)
+    qkv = (torch.randn(16 * n, 3 * h, device=dev) * 1.5).bfloat16().requires_grad_(True)
+    wt = torch.randn(16 * n, h, device=dev)
+    out = URMAttentionFn.apply(qkv, heads)
+    (out.float() * wt).sum().backward()
+    ref_in = qkv.detach().float().requires_grad_(True)
+    q, k, v = ref_in.view(n, 16, 3, heads, 16).permute(2, 0, 3, 1, 4).unbind(0)
+    o = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(16 * n, h)
+    (o * wt).sum().backward()
+    assert float((out.float() - o.detach()).abs().max()) <= 0.02 * float(o.abs().max())
+    for name, sl in (("dq", slice(0, h)), ("dk", slice(h, 2 * h)), ("dv", slice(2 * h, 3 * h))):
+        got, want = qkv.grad[:, sl].float().reshape(-1), ref_in.grad[:, sl].reshape(-1)
+        assert float((got - want).abs().max()) <= 0.02 * float(want.abs().max()), name
+        assert float(torch.nn.functional.cosine_similarity(got, want, dim=0)) >= 0.9995, name
+
+
+def test_urm_module_training_uses_device_attention(dev, monkeypatch):
+    """GameURM fwd + bwd under bf16 autocast on the device attention path vs the same model on torch's
+    SDPA path: every parameter gradient at cosine >= 0.999 (both bf16 autocast)."""
+    import agent
+    from g2048 import urm
+    torch.manual_seed(3)
+    m = agent.GameURM(agent.GameURMConfig(dropout=0.0)).to(dev)
+    obs = torch.rand(512, 48, device=dev) * 8
+    grads = []
+    for use_dev in (True, False):
+        m.zero_grad()
+        if not use_dev:
+            monkeypatch.setattr(urm, "attention_supported", lambda *a, **k: False)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            lg, v = m(obs)
+        (lg.float().square().sum() + v.float().sum()).backward()
+        grads.append({k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None})
+    assert grads[0].keys() == grads[1].keys() and len(grads[0]) > 10
+    for k in grads[0]:
+        a, b = grads[0][k].reshape(-1).float(), grads[1][k].reshape(-1).float()
+        if float(b.norm()) == 0:
+            continue
+        assert float(torch.nn.functional.cosine_similarity(a, b, dim=0)) >= 0.999, k
