@@ -208,7 +208,16 @@ class GameURMBlock(nn.Module):
         self.norm_eps = config.rms_norm_eps
 
     def forward(self, h: torch.Tensor) -> torch.Tensor:
-        h = rms_norm(h + self.attn(h), self.norm_eps)
+        a = self.attn(h)
+        if h.is_cuda:
+            from g2048 import urm as _urm  # the device residual RMSNorm and its backward (g2048_urm.h)
+            if _urm.rms_res_supported(h, a):
+                h = _urm.ResidualRMSFn.apply(h, a, self.norm_eps)
+                m = self.mlp(h)
+                if _urm.rms_res_supported(h, m):
+                    return _urm.ResidualRMSFn.apply(h, m, self.norm_eps)
+                return rms_norm(h + m, self.norm_eps)
+        h = rms_norm(h + a, self.norm_eps)
         return rms_norm(h + self.mlp(h), self.norm_eps)
 
 

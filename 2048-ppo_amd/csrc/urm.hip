@@ -1059,6 +1059,66 @@ __global__ __launch_bounds__(256) void urm_attn_bwd16_kernel(const uint16_t *__r
     *reinterpret_cast<uint2 *>(drow + 2 * h) = make_uint2(pack(dv[0], dv[1]), pack(dv[2], dv[3]));
 }
 
+// Training-path residual RMSNorm of GameURMBlock (game.py:1346, 1350 with rms_norm :1223-1229) as
+// one kernel each way, h = 64, for autograd (agent.GameURMBlock): 16 lanes per row (float4 each),
+// row sums by 4 xor shuffles inside the 16-lane group.
+//   forward  s = h + a, r = rsqrt(mean(s^2) + eps), out = s r          (h, out fp32; a bf16 or fp32)
+//   backward ds = r (dout - out mean(dout out));  dh = ds (fp32), da = ds (a's dtype)
+__device__ __forceinline__ float sum16(float x) {
+    x += __shfl_xor(x, 1);
+    x += __shfl_xor(x, 2);
+    x += __shfl_xor(x, 4);
+    return x + __shfl_xor(x, 8);
+}
+
+template <bool ABF>
+__global__ __launch_bounds__(256) void urm_rms_res_fwd_kernel(const float *__restrict__ hin, const void *__restrict__ a,
+                                                              float *__restrict__ out, float *__restrict__ rstd,
+                                                              int64_t rows, float eps) {
+    const int lane = threadIdx.x & 15;
+    const int64_t stride = (int64_t)gridDim.x * 16;
+    for (int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); r < rows; r += stride) {
+        const float4 hv = reinterpret_cast<const float4 *>(hin + r * 64)[lane];
+        float4 av;
+        if (ABF) {
+            const uint2 w = reinterpret_cast<const uint2 *>(static_cast<const uint16_t *>(a) + r * 64)[lane];
+            av = make_float4(__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xFFFF0000u), __uint_as_float(w.y << 16),
+                             __uint_as_float(w.y & 0xFFFF0000u));
+        } else {
+            av = reinterpret_cast<const float4 *>(static_cast<const float *>(a) + r * 64)[lane];
+        }
+        const float4 sv = make_float4(hv.x + av.x, hv.y + av.y, hv.z + av.z, hv.w + av.w);
+        const float ms = sum16(sv.x * sv.x + sv.y * sv.y + sv.z * sv.z + sv.w * sv.w) * (1.0f / 64.0f);
+        const float rs = rsqrtf(ms + eps);
+        reinterpret_cast<float4 *>(out + r * 64)[lane] = make_float4(sv.x * rs, sv.y * rs, sv.z * rs, sv.w * rs);
+        if (lane == 0) rstd[r] = rs;
+    }
+}
+
+template <bool ABF>
+__global__ __launch_bounds__(256) void urm_rms_res_bwd_kernel(const float *__restrict__ dout, const float *__restrict__ out,
+                                                              const float *__restrict__ rstd, float *__restrict__ dh,
+                                                              void *__restrict__ da, int64_t rows) {
+    const int lane = threadIdx.x & 15;
+    const int64_t stride = (int64_t)gridDim.x * 16;
+    for (int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); r < rows; r += stride) {
+        const float4 g = reinterpret_cast<const float4 *>(dout + r * 64)[lane];
+        const float4 o = reinterpret_cast<const float4 *>(out + r * 64)[lane];
+        const float rs = rstd[r];
+        const float mg = sum16(g.x * o.x + g.y * o.y + g.z * o.z + g.w * o.w) * (1.0f / 64.0f);
+        const float4 ds = make_float4(rs * (g.x - o.x * mg), rs * (g.y - o.y * mg), rs * (g.z - o.z * mg),
+                                      rs * (g.w - o.w * mg));
+        reinterpret_cast<float4 *>(dh + r * 64)[lane] = ds;
+        if (ABF) {
+            const __attribute__((ext_vector_type(2))) __bf16 p0 = {(__bf16)ds.x, (__bf16)ds.y}, p1 = {(__bf16)ds.z, (__bf16)ds.w};
+            reinterpret_cast<uint2 *>(static_cast<uint16_t *>(da) + r * 64)[lane] =
+                make_uint2(__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1));
+        } else {
+            reinterpret_cast<float4 *>(static_cast<float *>(da) + r * 64)[lane] = ds;
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1102,6 +1162,39 @@ int g2048_urm_attention_bwd(g2048_stream_t stream, const uint16_t *qkv, const ui
     const int64_t tasks = n * heads;
     hipLaunchKernelGGL(urm_attn_bwd16_kernel, dim3(blocks(tasks, 4)), dim3(256), 0, (hipStream_t)stream, qkv, dout,
                        dqkv, tasks, (int)h, (int)heads);
+    return launch_status();
+}
+
+int g2048_urm_rms_res_fwd(g2048_stream_t stream, const float *h, const void *a, int32_t a_dtype, float *out,
+                          float *rstd, int64_t rows, int32_t hidden, float eps) {
+    if (rows < 0 || hidden != 64 || (a_dtype != 0 && a_dtype != 1)) return G2048_EINVAL;
+    if (rows == 0) return G2048_OK;
+    if (!h || !a || !out || !rstd || ((uintptr_t)h | (uintptr_t)out) % 16 || (uintptr_t)a % 8) return G2048_EINVAL;
+    const int64_t nb = (rows + 15) / 16;
+    const dim3 grid((unsigned)(nb < 4096 ? nb : 4096));
+    if (a_dtype == 1)
+        hipLaunchKernelGGL(urm_rms_res_fwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, h, a, out, rstd, rows, eps);
+    else
+        hipLaunchKernelGGL(urm_rms_res_fwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, h, a, out, rstd, rows,
+                           eps);
+    return launch_status();
+}
+
+int g2048_urm_rms_res_bwd(g2048_stream_t stream, const float *dout, const float *out, const float *rstd, float *dh,
+                          void *da, int32_t a_dtype, int64_t rows, int32_t hidden) {
+    if (rows < 0 || hidden != 64 || (a_dtype != 0 && a_dtype != 1)) return G2048_EINVAL;
+    if (rows == 0) return G2048_OK;
+    if (!dout || !out || !rstd || !dh || !da || ((uintptr_t)dout | (uintptr_t)out | (uintptr_t)dh) % 16 ||
+        (uintptr_t)da % 8)
+        return G2048_EINVAL;
+    const int64_t nb = (rows + 15) / 16;
+    const dim3 grid((unsigned)(nb < 4096 ? nb : 4096));
+    if (a_dtype == 1)
+        hipLaunchKernelGGL(urm_rms_res_bwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, dout, out, rstd, dh, da,
+                           rows);
+    else
+        hipLaunchKernelGGL(urm_rms_res_bwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, dout, out, rstd, dh,
+                           da, rows);
     return launch_status();
 }
 

@@ -33,7 +33,8 @@ EXPORTED = (
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
-    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd",
+    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_rms_res_fwd",
+    "g2048_urm_rms_res_bwd",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
     # include/g2048_urm.h
@@ -223,6 +224,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
                                             ctypes.c_float, ctypes.c_float, ctypes.c_float]),
         "g2048_grad_sumsq_tick": (ctypes.c_int, [vp, vp, i64, vp, vp]),
         "g2048_urm_attention_bwd": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
+        "g2048_urm_rms_res_fwd": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, i64, i32, ctypes.c_float]),
+        "g2048_urm_rms_res_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i32, i64, i32]),
         "g2048_mlp_fwd_kl": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32, dp, vp, vp, vp, vp, vp, vp, jp]),
         "g2048_muon_adamw_step_clip": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, ctypes.POINTER(AdamWGroup),
                                                       i32, vp, vp, vp, ctypes.c_float, vp, vp,
@@ -707,6 +710,24 @@ def urm_attention_bwd(qkv, dout, dqkv, heads: int):
     _check(load().g2048_urm_attention_bwd(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"),
                                           _dev(dout, torch.bfloat16, "dout"), _dev(dqkv, torch.bfloat16, "dqkv"),
                                           rows // 16, h3 // 3, int(heads)), "g2048_urm_attention_bwd")
+
+
+def urm_rms_res_fwd(h, a, out, rstd, eps: float):
+    rows, hid = h.shape
+    abf = a.dtype == torch.bfloat16
+    _check(load().g2048_urm_rms_res_fwd(_stream(h), _dev(h, torch.float32, "h"),
+                                        _dev(a, torch.bfloat16 if abf else torch.float32, "a"), int(abf),
+                                        _dev(out, torch.float32, "out"), _dev(rstd, torch.float32, "rstd"), rows, hid,
+                                        float(eps)), "g2048_urm_rms_res_fwd")
+
+
+def urm_rms_res_bwd(dout, out, rstd, dh, da):
+    rows, hid = out.shape
+    abf = da.dtype == torch.bfloat16
+    _check(load().g2048_urm_rms_res_bwd(_stream(out), _dev(dout, torch.float32, "dout"), _dev(out, torch.float32, "out"),
+                                        _dev(rstd, torch.float32, "rstd"), _dev(dh, torch.float32, "dh"),
+                                        _dev(da, torch.bfloat16 if abf else torch.float32, "da"), int(abf), rows, hid),
+           "g2048_urm_rms_res_bwd")
 
 
 def urm_residual_rms(x, y, emb, xb, eps: float):

@@ -176,3 +176,36 @@ def attention_supported(qkv: torch.Tensor, seq: int, hidden: int, heads: int, dr
     attention dropout."""
     return (qkv.is_cuda and qkv.dtype == torch.bfloat16 and seq == 16 and hidden == 16 * heads
             and dropout == 0.0)
+
+
+class ResidualRMSFn(torch.autograd.Function):
+    """rms_norm(h + a) of GameURMBlock (game.py:1346-1350, h = 64) for autograd training on the
+    device: one kernel forward (g2048_urm_rms_res_fwd), one backward (g2048_urm_rms_res_bwd)
+    instead of torch's ~10 elementwise / reduction launches each way.  h fp32, a fp32 or bf16."""
+
+    @staticmethod
+    def forward(ctx, h: torch.Tensor, a: torch.Tensor, eps: float):
+        shape = h.shape
+        h2 = h.reshape(-1, shape[-1]).contiguous()
+        a2 = a.reshape(-1, shape[-1]).contiguous()
+        out = torch.empty_like(h2)
+        rstd = torch.empty(h2.shape[0], dtype=torch.float32, device=h.device)
+        L.urm_rms_res_fwd(h2, a2, out, rstd, eps)
+        ctx.save_for_backward(out, rstd)
+        ctx.a_dtype = a.dtype
+        ctx.shape = shape
+        return out.view(shape)
+
+    @staticmethod
+    def backward(ctx, dout: torch.Tensor):
+        out, rstd = ctx.saved_tensors
+        dh = torch.empty_like(out)
+        da = torch.empty(out.shape, dtype=ctx.a_dtype, device=out.device)
+        L.urm_rms_res_bwd(dout.reshape(out.shape).float().contiguous(), out, rstd, dh, da)
+        return dh.view(ctx.shape), da.view(ctx.shape), None
+
+
+def rms_res_supported(h: torch.Tensor, a: torch.Tensor) -> bool:
+    """The device residual RMSNorm applies: fp32 residual stream of hidden size 64 on the GPU."""
+    return (h.is_cuda and h.dtype == torch.float32 and a.dtype in (torch.float32, torch.bfloat16)
+            and h.shape == a.shape and h.shape[-1] == 64)

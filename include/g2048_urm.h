@@ -50,6 +50,15 @@ int g2048_urm_attention(g2048_stream_t stream, const uint16_t *qkv, uint16_t *ou
 int g2048_urm_attention_bwd(g2048_stream_t stream, const uint16_t *qkv, const uint16_t *dout, uint16_t *dqkv,
                             int64_t n, int32_t h, int32_t heads);
 
+/* The post-norm residual RMSNorm for autograd training (GameURMBlock, game.py:1346-1350, h = 64):
+ *   forward  out = (h + a) * rsqrt(mean((h + a)^2) + eps), rstd [rows] saved; h, out fp32, a fp32
+ *            (a_dtype 0) or bf16 (1, the autocast projection output)
+ *   backward ds = rstd (dout - out mean(dout out)); dh = ds fp32, da = ds in a's dtype. */
+int g2048_urm_rms_res_fwd(g2048_stream_t stream, const float *h, const void *a, int32_t a_dtype, float *out,
+                          float *rstd, int64_t rows, int32_t hidden, float eps);
+int g2048_urm_rms_res_bwd(g2048_stream_t stream, const float *dout, const float *out, const float *rstd, float *dh,
+                          void *da, int32_t a_dtype, int64_t rows, int32_t hidden);
+
 /* Post-norm residual (game.py:1346, 1350 with rms_norm :1223-1229):
  *   x = x + y;  x = x * rsqrt(mean(x^2) + eps)  [+ emb, the next loop's input, game.py:1447];
  *   xb = bf16(x).

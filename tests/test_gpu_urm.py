@@ -352,8 +352,9 @@ def test_urm_attention_backward_matches_sdpa(dev, n, heads):
 
 
 def test_urm_module_training_uses_device_attention(dev, monkeypatch):
-    """GameURM fwd + bwd under bf16 autocast on the device attention path vs the same model on torch's
-    SDPA path: every parameter gradient at cosine >= 0.999 (both bf16 autocast)."""
+    """GameURM fwd + bwd under bf16 autocast on the device paths (attention core, residual RMSNorm)
+    vs the same model on torch's SDPA + composite rms_norm: every parameter gradient at cosine >=
+    0.999 (both bf16 autocast)."""
     import agent
     from g2048 import urm
     torch.manual_seed(3)
@@ -362,8 +363,9 @@ def test_urm_module_training_uses_device_attention(dev, monkeypatch):
     grads = []
     for use_dev in (True, False):
         m.zero_grad()
-        if not use_dev:
+        if not use_dev:  # the reference run: torch's SDPA and the composite rms_norm
             monkeypatch.setattr(urm, "attention_supported", lambda *a, **k: False)
+            monkeypatch.setattr(urm, "rms_res_supported", lambda *a, **k: False)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             lg, v = m(obs)
         (lg.float().square().sum() + v.float().sum()).backward()
@@ -374,3 +376,25 @@ def test_urm_module_training_uses_device_attention(dev, monkeypatch):
         if float(b.norm()) == 0:
             continue
         assert float(torch.nn.functional.cosine_similarity(a, b, dim=0)) >= 0.999, k
+
+
+@pytest.mark.parametrize("rows,adt", [(65536 * 16, torch.bfloat16), (1000, torch.float32), (17, torch.bfloat16)])
+def test_urm_residual_rms_fn_matches_autograd(dev, rows, adt):
+    """ResidualRMSFn (g2048_urm_rms_res_fwd / _bwd) vs fp32 autograd of agent.rms_norm(h + a):
+    output and both input gradients within fp32 rounding (the bf16 input gradient within its own
+    rounding of the fp32 value)."""
+    import agent
+    from g2048.urm import ResidualRMSFn
+    torch.manual_seed(rows)
+    h = (torch.randn(rows, 64, device=dev) * 2).requires_grad_(True)
+    a = torch.randn(rows, 64, device=dev).to(adt).requires_grad_(True)
+    g = torch.randn(rows, 64, device=dev)
+    out = ResidualRMSFn.apply(h, a, 1e-6)
+    (out * g).sum().backward()
+    hr, ar = h.detach().clone().requires_grad_(True), a.detach().float().requires_grad_(True)
+    ref = agent.rms_norm(hr + ar, 1e-6)
+    (ref * g).sum().backward()
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(h.grad, hr.grad, rtol=1e-4, atol=1e-5)
+    tol = 8e-3 if adt == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(a.grad.float(), ar.grad, rtol=tol, atol=1e-5 if adt == torch.float32 else 1e-3)
