@@ -158,7 +158,15 @@ class GameConvSwiGLU(nn.Module):
         self.down_proj = nn.Linear(inter, hidden_size, bias=False)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        gate, up = self.gate_up_proj(x).chunk(2, dim=-1)
+        gu = self.gate_up_proj(x)
+        if gu.is_cuda:
+            from g2048 import urm as _urm  # the device SwiGLU + conv and its backward (g2048_urm.h)
+            if _urm.swiglu_conv_supported(gu, x.shape[1], self.inter, self.dwconv.kernel_size[0]):
+                b, s, _ = gu.shape
+                act = _urm.SwiGLUConvFn.apply(gu.reshape(b * s, 2 * self.inter), self.dwconv.weight.view(-1, 2),
+                                              self.dwconv.bias)
+                return self.down_proj(act.view(b, s, self.inter))
+        gate, up = gu.chunk(2, dim=-1)
         y = F.silu(gate) * up                                        # [B, S, I]
         if self.dwconv.kernel_size[0] == 2:
             # the kernel-2, padding-1 depthwise conv trimmed to S is y_t w0 shifted by one token plus

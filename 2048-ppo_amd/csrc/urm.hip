@@ -1119,6 +1119,94 @@ __global__ __launch_bounds__(256) void urm_rms_res_bwd_kernel(const float *__res
     }
 }
 
+// Training-path SwiGLU + depthwise conv (kernel 2) of GameConvSwiGLU (game.py:1264-1276) for
+// autograd (agent.GameConvSwiGLU): one thread per channel, a block per board (grid-stride), the 16
+// tokens in a register loop, so the conv's one-token shift is a register carry.  The arithmetic
+// follows the reference's autocast dtypes: y = bf16(bf16(silu(gate)) * up), y2 = y_{t-1} w0 +
+// y_t w1 + b in fp32, act = silu(y2) (stored bf16: the down_proj operand).  The backward recomputes
+// y and y2 and writes dgate / dup (bf16) and per-block partials of dw0, dw1, db (fp32 [3][inter]).
+constexpr int kScThreads = 128;
+
+__device__ __forceinline__ float bfr(float x) { return (float)(__bf16)x; }
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ uint16_t f2bf16(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
+__device__ __forceinline__ float bf16f(uint16_t x) { return __uint_as_float((uint32_t)x << 16); }
+
+__global__ __launch_bounds__(kScThreads) void urm_swiglu_conv_fwd_kernel(const uint16_t *__restrict__ gu,
+                                                                         const float *__restrict__ w,
+                                                                         const float *__restrict__ bias,
+                                                                         uint16_t *__restrict__ act, int64_t nb,
+                                                                         int inter) {
+    const int c = threadIdx.x;
+    if (c >= inter) return;
+    const float w0 = w[2 * c], w1 = w[2 * c + 1], b = bias[c];
+    for (int64_t bd = blockIdx.x; bd < nb; bd += gridDim.x) {
+        float yp = 0.0f;
+        for (int t = 0; t < 16; t++) {
+            const int64_t r = 16 * bd + t;
+            const float g = bf16f(gu[r * 2 * inter + c]), u = bf16f(gu[r * 2 * inter + inter + c]);
+            const float y = bfr(bfr(g * sigm(g)) * u);
+            const float y2 = yp * w0 + y * w1 + b;
+            act[r * inter + c] = f2bf16(y2 * sigm(y2));
+            yp = y;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kScThreads) void urm_swiglu_conv_bwd_kernel(const uint16_t *__restrict__ gu,
+                                                                         const float *__restrict__ w,
+                                                                         const float *__restrict__ bias,
+                                                                         const uint16_t *__restrict__ dact,
+                                                                         uint16_t *__restrict__ dgu,
+                                                                         float *__restrict__ part, int64_t nb,
+                                                                         int inter) {
+    const int c = threadIdx.x;
+    if (c >= inter) return;
+    const float w0 = w[2 * c], w1 = w[2 * c + 1], b = bias[c];
+    float s0 = 0.0f, s1 = 0.0f, sb = 0.0f;
+    for (int64_t bd = blockIdx.x; bd < nb; bd += gridDim.x) {
+        float g[16], u[16], y[16], d2[16];
+        float yp = 0.0f;
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            const int64_t r = 16 * bd + t;
+            g[t] = bf16f(gu[r * 2 * inter + c]);
+            u[t] = bf16f(gu[r * 2 * inter + inter + c]);
+            y[t] = bfr(bfr(g[t] * sigm(g[t])) * u[t]);
+            const float y2 = yp * w0 + y[t] * w1 + b, sg = sigm(y2);
+            d2[t] = bf16f(dact[r * inter + c]) * (sg * (1.0f + y2 * (1.0f - sg)));  // d act / d y2
+            s1 += d2[t] * y[t];
+            s0 += d2[t] * yp;
+            sb += d2[t];
+            yp = y[t];
+        }
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            const int64_t r = 16 * bd + t;
+            const float dy = d2[t] * w1 + (t + 1 < 16 ? d2[t + 1] * w0 : 0.0f);
+            const float sg = sigm(g[t]), sl = bfr(g[t] * sg);
+            dgu[r * 2 * inter + c] = f2bf16(dy * u[t] * (sg * (1.0f + g[t] * (1.0f - sg))));
+            dgu[r * 2 * inter + inter + c] = f2bf16(dy * sl);
+        }
+    }
+    float *pp = part + (int64_t)blockIdx.x * 3 * inter;
+    pp[c] = s0;
+    pp[inter + c] = s1;
+    pp[2 * inter + c] = sb;
+}
+
+// dw [inter][2] (w0, w1 interleaved as the conv weight), db [inter] from the nblk partial rows
+__global__ __launch_bounds__(256) void urm_swiglu_conv_colsum_kernel(const float *__restrict__ part, int nblk, int inter,
+                                                                     float *__restrict__ dw, float *__restrict__ db) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= 3 * inter) return;
+    float t = 0.0f;
+    for (int k = 0; k < nblk; k++) t += part[(int64_t)k * 3 * inter + j];
+    if (j < inter) dw[2 * j] = t;
+    else if (j < 2 * inter) dw[2 * (j - inter) + 1] = t;
+    else db[j - 2 * inter] = t;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1195,6 +1283,37 @@ int g2048_urm_rms_res_bwd(g2048_stream_t stream, const float *dout, const float 
     else
         hipLaunchKernelGGL(urm_rms_res_bwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, dout, out, rstd, dh,
                            da, rows);
+    return launch_status();
+}
+
+static int sc_blocks(int64_t nb) { return (int)(nb < 2048 ? nb : 2048); }
+
+size_t g2048_urm_swiglu_conv_partials(int64_t n, int32_t inter) {
+    if (n <= 0 || inter <= 0 || inter > kScThreads) return 0;
+    return (size_t)sc_blocks(n) * 3 * inter;
+}
+
+int g2048_urm_swiglu_conv_fwd(g2048_stream_t stream, const uint16_t *gu, const float *w, const float *b, uint16_t *act,
+                              int64_t n, int32_t inter) {
+    if (n < 0 || inter <= 0 || inter > kScThreads) return G2048_EINVAL;
+    if (n == 0) return G2048_OK;
+    if (!gu || !w || !b || !act) return G2048_EINVAL;
+    hipLaunchKernelGGL(urm_swiglu_conv_fwd_kernel, dim3(sc_blocks(n)), dim3(kScThreads), 0, (hipStream_t)stream, gu, w, b,
+                       act, n, (int)inter);
+    return launch_status();
+}
+
+int g2048_urm_swiglu_conv_bwd(g2048_stream_t stream, const uint16_t *gu, const float *w, const float *b,
+                              const uint16_t *dact, uint16_t *dgu, float *dw, float *db, float *partials, int64_t n,
+                              int32_t inter) {
+    if (n <= 0 || inter <= 0 || inter > kScThreads) return G2048_EINVAL;
+    if (!gu || !w || !b || !dact || !dgu || !dw || !db || !partials) return G2048_EINVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    const int nblk = sc_blocks(n);
+    hipLaunchKernelGGL(urm_swiglu_conv_bwd_kernel, dim3(nblk), dim3(kScThreads), 0, s, gu, w, b, dact, dgu, partials, n,
+                       (int)inter);
+    hipLaunchKernelGGL(urm_swiglu_conv_colsum_kernel, dim3((3 * inter + 255) / 256), dim3(256), 0, s, partials, nblk,
+                       (int)inter, dw, db);
     return launch_status();
 }
 

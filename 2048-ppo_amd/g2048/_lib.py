@@ -34,7 +34,7 @@ EXPORTED = (
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
     "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_rms_res_fwd",
-    "g2048_urm_rms_res_bwd",
+    "g2048_urm_rms_res_bwd", "g2048_urm_swiglu_conv_partials", "g2048_urm_swiglu_conv_fwd", "g2048_urm_swiglu_conv_bwd",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
     # include/g2048_urm.h
@@ -226,6 +226,9 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_urm_attention_bwd": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_rms_res_fwd": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, i64, i32, ctypes.c_float]),
         "g2048_urm_rms_res_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i32, i64, i32]),
+        "g2048_urm_swiglu_conv_partials": (sz, [i64, i32]),
+        "g2048_urm_swiglu_conv_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32]),
+        "g2048_urm_swiglu_conv_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32]),
         "g2048_mlp_fwd_kl": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32, dp, vp, vp, vp, vp, vp, vp, jp]),
         "g2048_muon_adamw_step_clip": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, ctypes.POINTER(AdamWGroup),
                                                       i32, vp, vp, vp, ctypes.c_float, vp, vp,
@@ -728,6 +731,26 @@ def urm_rms_res_bwd(dout, out, rstd, dh, da):
                                         _dev(rstd, torch.float32, "rstd"), _dev(dh, torch.float32, "dh"),
                                         _dev(da, torch.bfloat16 if abf else torch.float32, "da"), int(abf), rows, hid),
            "g2048_urm_rms_res_bwd")
+
+
+def urm_swiglu_conv_partials(n: int, inter: int) -> int:
+    return int(load().g2048_urm_swiglu_conv_partials(n, inter))
+
+
+def urm_swiglu_conv_fwd(gu, w, b, act):
+    rows, inter = act.shape
+    _check(load().g2048_urm_swiglu_conv_fwd(_stream(gu), _dev(gu, torch.bfloat16, "gu"), _dev(w, torch.float32, "w"),
+                                            _dev(b, torch.float32, "b"), _dev(act, torch.bfloat16, "act"), rows // 16,
+                                            inter), "g2048_urm_swiglu_conv_fwd")
+
+
+def urm_swiglu_conv_bwd(gu, w, b, dact, dgu, dw, db, partials):
+    rows, inter = dact.shape
+    _check(load().g2048_urm_swiglu_conv_bwd(_stream(gu), _dev(gu, torch.bfloat16, "gu"), _dev(w, torch.float32, "w"),
+                                            _dev(b, torch.float32, "b"), _dev(dact, torch.bfloat16, "dact"),
+                                            _dev(dgu, torch.bfloat16, "dgu"), _dev(dw, torch.float32, "dw"),
+                                            _dev(db, torch.float32, "db"), _dev(partials, torch.float32, "partials"),
+                                            rows // 16, inter), "g2048_urm_swiglu_conv_bwd")
 
 
 def urm_residual_rms(x, y, emb, xb, eps: float):

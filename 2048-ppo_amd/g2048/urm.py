@@ -209,3 +209,36 @@ def rms_res_supported(h: torch.Tensor, a: torch.Tensor) -> bool:
     """The device residual RMSNorm applies: fp32 residual stream of hidden size 64 on the GPU."""
     return (h.is_cuda and h.dtype == torch.float32 and a.dtype in (torch.float32, torch.bfloat16)
             and h.shape == a.shape and h.shape[-1] == 64)
+
+
+class SwiGLUConvFn(torch.autograd.Function):
+    """silu(conv2(silu(gate) * up)) of GameConvSwiGLU (game.py:1264-1276, kernel-2 depthwise conv
+    over the 16 tokens of a board) for autograd training on the device: gu bf16 [16 n, 2 inter] ->
+    act bf16 [16 n, inter] (the down_proj operand); backward dgu, dw [inter, 2], db [inter]."""
+
+    @staticmethod
+    def forward(ctx, gu: torch.Tensor, w: torch.Tensor, b: torch.Tensor):
+        gu = gu.contiguous()
+        wf, bf = w.detach().float().contiguous(), b.detach().float().contiguous()
+        act = torch.empty(gu.shape[0], gu.shape[1] // 2, dtype=torch.bfloat16, device=gu.device)
+        L.urm_swiglu_conv_fwd(gu, wf, bf, act)
+        ctx.save_for_backward(gu, wf, bf)
+        ctx.w_dtype, ctx.b_dtype = w.dtype, b.dtype
+        return act
+
+    @staticmethod
+    def backward(ctx, dact: torch.Tensor):
+        gu, wf, bf = ctx.saved_tensors
+        rows, inter = gu.shape[0], gu.shape[1] // 2
+        dgu = torch.empty_like(gu)
+        dw = torch.empty(inter, 2, dtype=torch.float32, device=gu.device)
+        db = torch.empty(inter, dtype=torch.float32, device=gu.device)
+        part = torch.empty(L.urm_swiglu_conv_partials(rows // 16, inter), dtype=torch.float32, device=gu.device)
+        L.urm_swiglu_conv_bwd(gu, wf, bf, dact.to(torch.bfloat16).contiguous(), dgu, dw, db, part)
+        return dgu, dw.to(ctx.w_dtype), db.to(ctx.b_dtype)
+
+
+def swiglu_conv_supported(gu: torch.Tensor, seq: int, inter: int, kernel: int) -> bool:
+    """The device SwiGLU + conv applies: bf16 gate_up output on the GPU (autocast), 16 tokens,
+    conv kernel 2, inter <= 128."""
+    return gu.is_cuda and gu.dtype == torch.bfloat16 and seq == 16 and kernel == 2 and inter <= 128

@@ -59,6 +59,19 @@ int g2048_urm_rms_res_fwd(g2048_stream_t stream, const float *h, const void *a, 
 int g2048_urm_rms_res_bwd(g2048_stream_t stream, const float *dout, const float *out, const float *rstd, float *dh,
                           void *da, int32_t a_dtype, int64_t rows, int32_t hidden);
 
+/* SwiGLU + depthwise conv (kernel 2) for autograd training (GameConvSwiGLU, game.py:1264-1276),
+ * n boards of 16 tokens, inter <= 128 channels, the reference's autocast dtypes:
+ *   forward  y = bf16(bf16(silu(gate)) up), y2 = y_{t-1} w[c][0] + y_t w[c][1] + b[c] (fp32),
+ *            act = bf16(silu(y2)) [16 n, inter];  gu bf16 [16 n, 2 inter] (gate | up)
+ *   backward dgu bf16 [16 n, 2 inter], dw fp32 [inter][2], db fp32 [inter] (deterministic column
+ *            sums over g2048_urm_swiglu_conv_partials(n, inter) floats of scratch). */
+size_t g2048_urm_swiglu_conv_partials(int64_t n, int32_t inter);
+int g2048_urm_swiglu_conv_fwd(g2048_stream_t stream, const uint16_t *gu, const float *w, const float *b, uint16_t *act,
+                              int64_t n, int32_t inter);
+int g2048_urm_swiglu_conv_bwd(g2048_stream_t stream, const uint16_t *gu, const float *w, const float *b,
+                              const uint16_t *dact, uint16_t *dgu, float *dw, float *db, float *partials, int64_t n,
+                              int32_t inter);
+
 /* Post-norm residual (game.py:1346, 1350 with rms_norm :1223-1229):
  *   x = x + y;  x = x * rsqrt(mean(x^2) + eps)  [+ emb, the next loop's input, game.py:1447];
  *   xb = bf16(x).

@@ -352,9 +352,9 @@ def test_urm_attention_backward_matches_sdpa(dev, n, heads):
 
 
 def test_urm_module_training_uses_device_attention(dev, monkeypatch):
-    """GameURM fwd + bwd under bf16 autocast on the device paths (attention core, residual RMSNorm)
-    vs the same model on torch's SDPA + composite rms_norm: every parameter gradient at cosine >=
-    0.999 (both bf16 autocast)."""
+    """GameURM fwd + bwd under bf16 autocast on the device paths (attention core, residual RMSNorm,
+    SwiGLU + conv) vs the same model on torch's SDPA + composite rms_norm / SwiGLU / conv: every
+    parameter gradient at cosine >= 0.999 (both bf16 autocast)."""
     import agent
     from g2048 import urm
     torch.manual_seed(3)
@@ -366,6 +366,7 @@ def test_urm_module_training_uses_device_attention(dev, monkeypatch):
         if not use_dev:  # the reference run: torch's SDPA and the composite rms_norm
             monkeypatch.setattr(urm, "attention_supported", lambda *a, **k: False)
             monkeypatch.setattr(urm, "rms_res_supported", lambda *a, **k: False)
+            monkeypatch.setattr(urm, "swiglu_conv_supported", lambda *a, **k: False)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             lg, v = m(obs)
         (lg.float().square().sum() + v.float().sum()).backward()
@@ -398,3 +399,30 @@ def test_urm_residual_rms_fn_matches_autograd(dev, rows, adt):
     torch.testing.assert_close(h.grad, hr.grad, rtol=1e-4, atol=1e-5)
     tol = 8e-3 if adt == torch.bfloat16 else 1e-4
     torch.testing.assert_close(a.grad.float(), ar.grad, rtol=tol, atol=1e-5 if adt == torch.float32 else 1e-3)
+
+
+@pytest.mark.parametrize("n,inter", [(65536, 120), (37, 64)])
+def test_urm_swiglu_conv_fn_matches_autograd(dev, n, inter):
+    """SwiGLUConvFn (g2048_urm_swiglu_conv_fwd / _bwd) vs autograd of the module's composite (bf16
+    silu(gate) * up, fp32 kernel-2 conv, silu) on the same bf16 gate_up output: act within one bf16
+    step, dgu / dw / db at cosine >= 0.999 and max error <= 2 % of the largest."""
+    import torch.nn.functional as F
+    from g2048.urm import SwiGLUConvFn
+    torch.manual_seed(n + inter)
+    gu = (torch.randn(16 * n, 2 * inter, device=dev) * 1.5).bfloat16().requires_grad_(True)
+    w = (torch.randn(inter, 2, device=dev) * 0.5).requires_grad_(True)
+    b = (torch.randn(inter, device=dev) * 0.1).requires_grad_(True)
+    g = torch.randn(16 * n, inter, device=dev)
+    act = SwiGLUConvFn.apply(gu, w, b)
+    (act.float() * g).sum().backward()
+    gr, wr, br = (t.detach().clone().requires_grad_(True) for t in (gu, w, b))
+    gate, up = gr.view(n, 16, 2 * inter).chunk(2, dim=-1)
+    y = F.silu(gate) * up                                     # bf16, as under autocast
+    prev = F.pad(y, (0, 0, 1, 0))[:, :-1]
+    ref = F.silu(prev * wr[:, 0] + y * wr[:, 1] + br).reshape(16 * n, inter)
+    (ref * g).sum().backward()
+    assert float((act.float() - ref.detach()).abs().max()) <= 2 ** -7 * float(ref.abs().max())
+    for name, got, want in (("dgu", gu.grad, gr.grad), ("dw", w.grad, wr.grad), ("db", b.grad, br.grad)):
+        got, want = got.float().reshape(-1), want.float().reshape(-1)
+        assert float(F.cosine_similarity(got, want, dim=0)) >= 0.999, name
+        assert float((got - want).abs().max()) <= 0.02 * float(want.abs().max()), name
