@@ -199,7 +199,7 @@ class GameURMAttention(nn.Module):
         if qkv.is_cuda:
             from g2048 import urm as _urm  # the HIP attention core and its backward (g2048_urm.h)
             if _urm.attention_supported(qkv, s, self.hidden_size, self.num_heads, p):
-                o = _urm.URMAttentionFn.apply(qkv.reshape(b * s, 3 * self.hidden_size), self.num_heads)
+                o = _urm.URMAttentionFn.apply(qkv.reshape(b * s, 3 * self.hidden_size), self.num_heads, p)
                 return self.o_proj(o.view(b, s, self.hidden_size))
         q, k, v = qkv.view(b, s, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).unbind(0)
         o = F.scaled_dot_product_attention(q, k, v, dropout_p=p, is_causal=False)

@@ -21,6 +21,7 @@
 #include <cstdint>
 
 #include "../../include/g2048_urm.h"
+#include "board.hpp"
 
 namespace {
 
@@ -98,10 +99,31 @@ __global__ __launch_bounds__(kThreads) void urm_stem_kernel(const void *__restri
     }
 }
 
-template <bool kAligned>
+// Attention dropout (training mode, game.py:1314 dropout_p): keep multipliers (0 or 1/(1-p)) of
+// P[query i][keys 4g .. 4g+3] of (board b, head hh) -- one Philox4x32-10 draw (words x, y: four
+// 16-bit uniforms, keep iff u >= thr = round(p 2^16)), counter {b, hh|i|g, call counter}, key = the
+// seed.  The forward and backward lane layouts both hold 4 consecutive keys of one query, so both
+// regenerate the same mask from the same draw; nothing is stored.
+struct AttnDrop {
+    uint32_t thr;
+    float scale;
+    uint32_t k0, k1;
+    const uint64_t *counter;  // device call counter (graph-replay safe)
+};
+__device__ __forceinline__ void attn_keep(const AttnDrop &d, int64_t b, int hh, int i, int g, float km[4]) {
+    const uint64_t c = *d.counter;
+    const uint4 r = g2048::philox((uint32_t)b, ((uint32_t)hh << 8) | ((uint32_t)i << 2) | (uint32_t)g, (uint32_t)c,
+                                  (uint32_t)(c >> 32), d.k0, d.k1);
+    km[0] = (r.x & 0xFFFFu) >= d.thr ? d.scale : 0.0f;
+    km[1] = (r.x >> 16) >= d.thr ? d.scale : 0.0f;
+    km[2] = (r.y & 0xFFFFu) >= d.thr ? d.scale : 0.0f;
+    km[3] = (r.y >> 16) >= d.thr ? d.scale : 0.0f;
+}
+
+template <bool kAligned, bool kDrop>
 __global__ __launch_bounds__(kThreads) void urm_attn_kernel(const uint16_t *__restrict__ qkv,
                                                             uint16_t *__restrict__ out, int64_t tasks, int h,
-                                                            int heads) {
+                                                            int heads, AttnDrop drop) {
     const int lane = threadIdx.x & 63;
     const int64_t task = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     if (task >= tasks) return;  // wave-uniform
@@ -152,9 +174,11 @@ __global__ __launch_bounds__(kThreads) void urm_attn_kernel(const uint16_t *__re
     sum += __shfl_xor(sum, 16, 64);
     sum += __shfl_xor(sum, 32, 64);
     const float inv = 1.0f / sum;
+    float km[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+    if (kDrop) attn_keep(drop, b, hh, i, g, km);
     s16x4 pb;  // B operand of O^T = V^T P^T: B[k = key 4g + jj][n = query i]
 #pragma unroll
-    for (int r = 0; r < 4; r++) pb[r] = (short)f2bf(p[r] * inv);
+    for (int r = 0; r < 4; r++) pb[r] = (short)f2bf(kDrop ? p[r] * inv * km[r] : p[r] * inv);
     // A operand: V^T[row = dim d0 + i][k = key 4g + jj] = V[4g + jj][d0 + i]
     const uint16_t *vcol = base + 2 * h + hh * hd;
     uint16_t *orow = out + (b * 16 + i) * (int64_t)h + hh * hd;
@@ -957,10 +981,11 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
 // the 4 lanes of a row by two xor shuffles).  dqkv bf16 [16 n, 3 h] in the qkv layout.
 constexpr int kAbP = 17;  // fp32 LDS row pitch (conflict-free column reads)
 
+template <bool kDrop>
 __global__ __launch_bounds__(256) void urm_attn_bwd16_kernel(const uint16_t *__restrict__ qkv,
                                                              const uint16_t *__restrict__ dout,
                                                              uint16_t *__restrict__ dqkv, int64_t tasks, int h,
-                                                             int heads) {
+                                                             int heads, AttnDrop drop) {
     __shared__ float sm[4][6][16 * kAbP];  // per wave: Q, K, V, dO, P, dS
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t task = (int64_t)blockIdx.x * 4 + wave;
@@ -1016,11 +1041,14 @@ __global__ __launch_bounds__(256) void urm_attn_bwd16_kernel(const uint16_t *__r
         }
         const float inv = 1.0f / rowsum4(sum);
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            p[u] *= inv;
-            sP[r * kAbP + c0 + u] = p[u];
-        }
+        for (int u = 0; u < 4; u++) p[u] *= inv;
     }
+    // dropout: O = Pd V with Pd = P km (the forward's mask, regenerated); dV = Pd^T dO and
+    // dS = P (km dPd - rowsum(Pd dPd)), dPd = dO V^T (rowsum(P dP) = rowsum(Pd dPd))
+    float km[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+    if (kDrop) attn_keep(drop, b, hd, r, lane & 3, km);
+#pragma unroll
+    for (int u = 0; u < 4; u++) sP[r * kAbP + c0 + u] = kDrop ? p[u] * km[u] : p[u];
     // dP[r][c0 + u] = sum_d dO[r][d] V[c0 + u][d];  dS = P (dP - rowsum(P dP))
     {
         float dp[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -1030,9 +1058,16 @@ __global__ __launch_bounds__(256) void urm_attn_bwd16_kernel(const uint16_t *__r
 #pragma unroll
             for (int u = 0; u < 4; u++) dp[u] = __builtin_fmaf(od, sV[(c0 + u) * kAbP + d], dp[u]);
         }
-        const float rs = rowsum4(p[0] * dp[0] + p[1] * dp[1] + p[2] * dp[2] + p[3] * dp[3]);
+        float rs;
+        if (kDrop) {
+            rs = rowsum4(p[0] * km[0] * dp[0] + p[1] * km[1] * dp[1] + p[2] * km[2] * dp[2] + p[3] * km[3] * dp[3]);
 #pragma unroll
-        for (int u = 0; u < 4; u++) sS[r * kAbP + c0 + u] = p[u] * (dp[u] - rs);
+            for (int u = 0; u < 4; u++) sS[r * kAbP + c0 + u] = p[u] * (dp[u] * km[u] - rs);
+        } else {
+            rs = rowsum4(p[0] * dp[0] + p[1] * dp[1] + p[2] * dp[2] + p[3] * dp[3]);
+#pragma unroll
+            for (int u = 0; u < 4; u++) sS[r * kAbP + c0 + u] = p[u] * (dp[u] - rs);
+        }
     }
     sync();
     // dV[r][c0 + u] = sum_i P[i][r] dO[i][c0 + u];  dQ[r][..] = sum_j dS[r][j] K[j][..] / 4;
@@ -1142,9 +1177,17 @@ __global__ __launch_bounds__(kScThreads) void urm_swiglu_conv_fwd_kernel(const u
     const float w0 = w[2 * c], w1 = w[2 * c + 1], b = bias[c];
     for (int64_t bd = blockIdx.x; bd < nb; bd += gridDim.x) {
         float yp = 0.0f;
+        uint16_t gr[16], ur[16];  // the board's 32 loads in flight before any arithmetic
+#pragma unroll
         for (int t = 0; t < 16; t++) {
             const int64_t r = 16 * bd + t;
-            const float g = bf16f(gu[r * 2 * inter + c]), u = bf16f(gu[r * 2 * inter + inter + c]);
+            gr[t] = gu[r * 2 * inter + c];
+            ur[t] = gu[r * 2 * inter + inter + c];
+        }
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            const int64_t r = 16 * bd + t;
+            const float g = bf16f(gr[t]), u = bf16f(ur[t]);
             const float y = bfr(bfr(g * sigm(g)) * u);
             const float y2 = yp * w0 + y * w1 + b;
             act[r * inter + c] = f2bf16(y2 * sigm(y2));
@@ -1195,13 +1238,32 @@ __global__ __launch_bounds__(kScThreads) void urm_swiglu_conv_bwd_kernel(const u
     pp[2 * inter + c] = sb;
 }
 
-// dw [inter][2] (w0, w1 interleaved as the conv weight), db [inter] from the nblk partial rows
+// dw [inter][2] (w0, w1 interleaved as the conv weight), db [inter] from the nblk partial rows:
+// a block per 16 columns, 16 row slices per column (slice s sums rows s, s + 16, ... in order, 8
+// loads in flight), then the 16 slice sums added in slice order -- a fixed order, deterministic.
 __global__ __launch_bounds__(256) void urm_swiglu_conv_colsum_kernel(const float *__restrict__ part, int nblk, int inter,
                                                                      float *__restrict__ dw, float *__restrict__ db) {
-    const int j = blockIdx.x * 256 + threadIdx.x;
-    if (j >= 3 * inter) return;
+    __shared__ float red[16][17];
+    const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
+    const int j = blockIdx.x * 16 + cl, ncol = 3 * inter;
     float t = 0.0f;
-    for (int k = 0; k < nblk; k++) t += part[(int64_t)k * 3 * inter + j];
+    if (j < ncol) {
+        int k = sl;
+        for (; k + 16 * 7 < nblk; k += 16 * 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = part[(int64_t)(k + 16 * u) * ncol + j];
+#pragma unroll
+            for (int u = 0; u < 8; u++) t += v[u];
+        }
+        for (; k < nblk; k += 16) t += part[(int64_t)k * ncol + j];
+    }
+    red[sl][cl] = t;
+    __syncthreads();
+    if (sl != 0 || j >= ncol) return;
+    t = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 16; u++) t += red[u][cl];
     if (j < inter) dw[2 * j] = t;
     else if (j < 2 * inter) dw[2 * (j - inter) + 1] = t;
     else db[j - 2 * inter] = t;
@@ -1227,30 +1289,59 @@ int g2048_urm_stem(g2048_stream_t stream, const void *obs, int32_t obs_dtype, co
     return launch_status();
 }
 
-int g2048_urm_attention(g2048_stream_t stream, const uint16_t *qkv, uint16_t *out, int64_t n, int32_t h,
-                        int32_t heads) {
+static bool attn_drop_args(float p, uint64_t seed, const uint64_t *counter, AttnDrop &d) {
+    if (!(p >= 0.0f && p < 1.0f)) return false;
+    d.thr = (uint32_t)lrintf(p * 65536.0f);
+    d.scale = 1.0f / (1.0f - p);
+    d.k0 = (uint32_t)seed;
+    d.k1 = (uint32_t)(seed >> 32);
+    d.counter = counter;
+    return d.thr == 0 || counter != nullptr;
+}
+
+int g2048_urm_attention_drop(g2048_stream_t stream, const uint16_t *qkv, uint16_t *out, int64_t n, int32_t h,
+                             int32_t heads, float p, uint64_t seed, const uint64_t *counter) {
+    AttnDrop d{};
     if (n < 0 || !h_ok(h) || heads <= 0 || h % heads != 0 || h / heads > 64) return G2048_EINVAL;
+    if (!attn_drop_args(p, seed, counter, d)) return G2048_EINVAL;
     if (n == 0) return G2048_OK;
     if (!qkv || !out) return G2048_EINVAL;
     const int64_t tasks = n * heads;
-    if ((h / heads) % 4 == 0)
-        hipLaunchKernelGGL(urm_attn_kernel<true>, dim3(blocks(tasks, kThreads / 64)), dim3(kThreads), 0,
-                           (hipStream_t)stream, qkv, out, tasks, (int)h, (int)heads);
+    const dim3 grid(blocks(tasks, kThreads / 64));
+    const hipStream_t s = (hipStream_t)stream;
+    const bool al = (h / heads) % 4 == 0, dr = d.thr != 0;
+    if (al && dr) hipLaunchKernelGGL((urm_attn_kernel<true, true>), grid, dim3(kThreads), 0, s, qkv, out, tasks, (int)h, (int)heads, d);
+    else if (al) hipLaunchKernelGGL((urm_attn_kernel<true, false>), grid, dim3(kThreads), 0, s, qkv, out, tasks, (int)h, (int)heads, d);
+    else if (dr) hipLaunchKernelGGL((urm_attn_kernel<false, true>), grid, dim3(kThreads), 0, s, qkv, out, tasks, (int)h, (int)heads, d);
+    else hipLaunchKernelGGL((urm_attn_kernel<false, false>), grid, dim3(kThreads), 0, s, qkv, out, tasks, (int)h, (int)heads, d);
+    return launch_status();
+}
+
+int g2048_urm_attention(g2048_stream_t stream, const uint16_t *qkv, uint16_t *out, int64_t n, int32_t h,
+                        int32_t heads) {
+    return g2048_urm_attention_drop(stream, qkv, out, n, h, heads, 0.0f, 0, nullptr);
+}
+
+int g2048_urm_attention_bwd_drop(g2048_stream_t stream, const uint16_t *qkv, const uint16_t *dout, uint16_t *dqkv,
+                                 int64_t n, int32_t h, int32_t heads, float p, uint64_t seed, const uint64_t *counter) {
+    AttnDrop d{};
+    if (n < 0 || heads <= 0 || h != 16 * heads || h > 512) return G2048_EINVAL;
+    if (!attn_drop_args(p, seed, counter, d)) return G2048_EINVAL;
+    if (n == 0) return G2048_OK;
+    if (!qkv || !dout || !dqkv || ((uintptr_t)qkv | (uintptr_t)dout | (uintptr_t)dqkv) % 8) return G2048_EINVAL;
+    const int64_t tasks = n * heads;
+    if (d.thr != 0)
+        hipLaunchKernelGGL(urm_attn_bwd16_kernel<true>, dim3(blocks(tasks, 4)), dim3(256), 0, (hipStream_t)stream, qkv,
+                           dout, dqkv, tasks, (int)h, (int)heads, d);
     else
-        hipLaunchKernelGGL(urm_attn_kernel<false>, dim3(blocks(tasks, kThreads / 64)), dim3(kThreads), 0,
-                           (hipStream_t)stream, qkv, out, tasks, (int)h, (int)heads);
+        hipLaunchKernelGGL(urm_attn_bwd16_kernel<false>, dim3(blocks(tasks, 4)), dim3(256), 0, (hipStream_t)stream, qkv,
+                           dout, dqkv, tasks, (int)h, (int)heads, d);
     return launch_status();
 }
 
 int g2048_urm_attention_bwd(g2048_stream_t stream, const uint16_t *qkv, const uint16_t *dout, uint16_t *dqkv,
                             int64_t n, int32_t h, int32_t heads) {
-    if (n < 0 || heads <= 0 || h != 16 * heads || h > 512) return G2048_EINVAL;
-    if (n == 0) return G2048_OK;
-    if (!qkv || !dout || !dqkv || ((uintptr_t)qkv | (uintptr_t)dout | (uintptr_t)dqkv) % 8) return G2048_EINVAL;
-    const int64_t tasks = n * heads;
-    hipLaunchKernelGGL(urm_attn_bwd16_kernel, dim3(blocks(tasks, 4)), dim3(256), 0, (hipStream_t)stream, qkv, dout,
-                       dqkv, tasks, (int)h, (int)heads);
-    return launch_status();
+    return g2048_urm_attention_bwd_drop(stream, qkv, dout, dqkv, n, h, heads, 0.0f, 0, nullptr);
 }
 
 int g2048_urm_rms_res_fwd(g2048_stream_t stream, const float *h, const void *a, int32_t a_dtype, float *out,
@@ -1312,7 +1403,7 @@ int g2048_urm_swiglu_conv_bwd(g2048_stream_t stream, const uint16_t *gu, const f
     const int nblk = sc_blocks(n);
     hipLaunchKernelGGL(urm_swiglu_conv_bwd_kernel, dim3(nblk), dim3(kScThreads), 0, s, gu, w, b, dact, dgu, partials, n,
                        (int)inter);
-    hipLaunchKernelGGL(urm_swiglu_conv_colsum_kernel, dim3((3 * inter + 255) / 256), dim3(256), 0, s, partials, nblk,
+    hipLaunchKernelGGL(urm_swiglu_conv_colsum_kernel, dim3((3 * inter + 15) / 16), dim3(256), 0, s, partials, nblk,
                        (int)inter, dw, db);
     return launch_status();
 }

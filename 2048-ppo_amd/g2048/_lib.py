@@ -33,7 +33,7 @@ EXPORTED = (
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
-    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_rms_res_fwd",
+    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_rms_res_fwd",
     "g2048_urm_rms_res_bwd", "g2048_urm_swiglu_conv_partials", "g2048_urm_swiglu_conv_fwd", "g2048_urm_swiglu_conv_bwd",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
@@ -224,6 +224,9 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
                                             ctypes.c_float, ctypes.c_float, ctypes.c_float]),
         "g2048_grad_sumsq_tick": (ctypes.c_int, [vp, vp, i64, vp, vp]),
         "g2048_urm_attention_bwd": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
+        "g2048_urm_attention_drop": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, ctypes.c_float, ctypes.c_uint64, vp]),
+        "g2048_urm_attention_bwd_drop": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32, ctypes.c_float, ctypes.c_uint64,
+                                                        vp]),
         "g2048_urm_rms_res_fwd": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, i64, i32, ctypes.c_float]),
         "g2048_urm_rms_res_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i32, i64, i32]),
         "g2048_urm_swiglu_conv_partials": (sz, [i64, i32]),
@@ -702,14 +705,27 @@ def urm_stem(obs, w, ln_w, ln_b, init_hidden, emb, x, xb):
                                  _dev(xb, torch.bfloat16, "xb"), n, h), "g2048_urm_stem")
 
 
-def urm_attention(qkv, out, heads: int):
+def urm_attention(qkv, out, heads: int, p: float = 0.0, seed: int = 0, counter=None):
+    """counter: device int64 [1] call counter of the dropout mask (required when p > 0)."""
     rows, h3 = qkv.shape
+    if p > 0.0:
+        _check(load().g2048_urm_attention_drop(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"),
+                                               _dev(out, torch.bfloat16, "out"), rows // 16, h3 // 3, int(heads),
+                                               float(p), int(seed) & (2 ** 64 - 1), _dev(counter, torch.int64, "counter")),
+               "g2048_urm_attention_drop")
+        return
     _check(load().g2048_urm_attention(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"), _dev(out, torch.bfloat16, "out"),
                                       rows // 16, h3 // 3, int(heads)), "g2048_urm_attention")
 
 
-def urm_attention_bwd(qkv, dout, dqkv, heads: int):
+def urm_attention_bwd(qkv, dout, dqkv, heads: int, p: float = 0.0, seed: int = 0, counter=None):
     rows, h3 = qkv.shape
+    if p > 0.0:
+        _check(load().g2048_urm_attention_bwd_drop(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"),
+                                                   _dev(dout, torch.bfloat16, "dout"), _dev(dqkv, torch.bfloat16, "dqkv"),
+                                                   rows // 16, h3 // 3, int(heads), float(p), int(seed) & (2 ** 64 - 1),
+                                                   _dev(counter, torch.int64, "counter")), "g2048_urm_attention_bwd_drop")
+        return
     _check(load().g2048_urm_attention_bwd(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"),
                                           _dev(dout, torch.bfloat16, "dout"), _dev(dqkv, torch.bfloat16, "dqkv"),
                                           rows // 16, h3 // 3, int(heads)), "g2048_urm_attention_bwd")

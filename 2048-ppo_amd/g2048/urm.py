@@ -149,33 +149,61 @@ class URMPolicy:
         return self.logits, self.value
 
 
+_ATTN_DROP: dict = {}  # device -> (seed, device int64 [1] call counter) of the attention dropout masks
+
+
+def _attn_drop_state(dev):
+    """The dropout masks' Philox key (drawn once per device from torch's CPU generator, so
+    torch.manual_seed makes runs repeatable) and the device call counter, bumped by every training
+    forward (a captured graph bumps it per replay: a fresh mask per minibatch)."""
+    st = _ATTN_DROP.get(dev)
+    if st is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        st = (seed, torch.zeros(1, dtype=torch.int64, device=dev))
+        _ATTN_DROP[dev] = st
+    return st
+
+
 class URMAttentionFn(torch.autograd.Function):
     """The attention core of GameURMAttention (game.py:1296-1317: scaled_dot_product_attention,
-    no mask, no dropout) for autograd training on the device: forward g2048_urm_attention, backward
-    g2048_urm_attention_bwd (P recomputed; head_dim 16).  qkv bf16 [16 n, 3 h] -> out bf16 [16 n, h]."""
+    no mask, dropout_p = config.dropout in training) for autograd training on the device: forward
+    g2048_urm_attention(_drop), backward g2048_urm_attention_bwd(_drop) (P and the dropout mask
+    regenerated; head_dim 16).  qkv bf16 [16 n, 3 h] -> out bf16 [16 n, h]."""
 
     @staticmethod
-    def forward(ctx, qkv: torch.Tensor, heads: int):
+    def forward(ctx, qkv: torch.Tensor, heads: int, p: float = 0.0):
         qkv = qkv.contiguous()
         out = torch.empty(qkv.shape[0], qkv.shape[1] // 3, dtype=qkv.dtype, device=qkv.device)
-        L.urm_attention(qkv, out, heads)
-        ctx.save_for_backward(qkv)
-        ctx.heads = heads
+        ctx.heads, ctx.p, ctx.seed = heads, float(p), 0
+        if p > 0.0:
+            seed, ctr = _attn_drop_state(qkv.device)
+            c = ctr.clone()  # this call's counter value: the backward regenerates the mask from it
+            L.urm_attention(qkv, out, heads, p, seed, c)
+            ctr.add_(1)
+            ctx.seed = seed
+            ctx.save_for_backward(qkv, c)
+        else:
+            L.urm_attention(qkv, out, heads)
+            ctx.save_for_backward(qkv)
         return out
 
     @staticmethod
     def backward(ctx, dout: torch.Tensor):
-        (qkv,) = ctx.saved_tensors
+        qkv = ctx.saved_tensors[0]
         dqkv = torch.empty_like(qkv)
-        L.urm_attention_bwd(qkv, dout.to(qkv.dtype).contiguous(), dqkv, ctx.heads)
-        return dqkv, None
+        if ctx.p > 0.0:
+            L.urm_attention_bwd(qkv, dout.to(qkv.dtype).contiguous(), dqkv, ctx.heads, ctx.p, ctx.seed,
+                                ctx.saved_tensors[1])
+        else:
+            L.urm_attention_bwd(qkv, dout.to(qkv.dtype).contiguous(), dqkv, ctx.heads)
+        return dqkv, None, None
 
 
 def attention_supported(qkv: torch.Tensor, seq: int, hidden: int, heads: int, dropout: float) -> bool:
-    """The device attention path applies: bf16 qkv on the GPU (autocast), 16 tokens, head_dim 16, no
-    attention dropout."""
+    """The device attention path applies: bf16 qkv on the GPU (autocast), 16 tokens, head_dim 16,
+    attention dropout 0 <= p < 1 (the device mask)."""
     return (qkv.is_cuda and qkv.dtype == torch.bfloat16 and seq == 16 and hidden == 16 * heads
-            and dropout == 0.0)
+            and 0.0 <= dropout < 1.0)
 
 
 class ResidualRMSFn(torch.autograd.Function):

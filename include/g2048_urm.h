@@ -50,6 +50,18 @@ int g2048_urm_attention(g2048_stream_t stream, const uint16_t *qkv, uint16_t *ou
 int g2048_urm_attention_bwd(g2048_stream_t stream, const uint16_t *qkv, const uint16_t *dout, uint16_t *dqkv,
                             int64_t n, int32_t h, int32_t heads);
 
+/* Training-mode attention dropout (GameURMAttention, game.py:1314: dropout_p = config.dropout while
+ * training): the forward / backward above with P replaced by P * keep / (1 - p) before O = P V.
+ * keep: 16-bit Philox4x32-10 uniform >= round(p 2^16), one draw per (board, head, query, group of 4
+ * keys) keyed by `seed` with the device call counter *counter (read at launch, so a captured graph
+ * draws a new mask per replay once the caller bumps it); the backward regenerates the same mask from
+ * the same seed / counter value.  p = 0 is the plain path (counter may be NULL).  The mask is the
+ * same distribution as torch's, not its stream. */
+int g2048_urm_attention_drop(g2048_stream_t stream, const uint16_t *qkv, uint16_t *out, int64_t n, int32_t h,
+                             int32_t heads, float p, uint64_t seed, const uint64_t *counter);
+int g2048_urm_attention_bwd_drop(g2048_stream_t stream, const uint16_t *qkv, const uint16_t *dout, uint16_t *dqkv,
+                                 int64_t n, int32_t h, int32_t heads, float p, uint64_t seed, const uint64_t *counter);
+
 /* The post-norm residual RMSNorm for autograd training (GameURMBlock, game.py:1346-1350, h = 64):
  *   forward  out = (h + a) * rsqrt(mean((h + a)^2) + eps), rstd [rows] saved; h, out fp32, a fp32
  *            (a_dtype 0) or bf16 (1, the autocast projection output)

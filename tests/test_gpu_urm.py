@@ -351,6 +351,90 @@ def test_urm_attention_backward_matches_sdpa(dev, n, heads):
         assert float(torch.nn.functional.cosine_similarity(got, want, dim=0)) >= 0.9995, name
 
 
+def _attn_keep_oracle(n, heads, p, seed, counter):
+    """The device attention-dropout multipliers [n, heads, 16 queries, 16 keys] from the oracle's
+    Philox4x32-10 (include/g2048_urm.h: counter {board, head << 8 | query << 2 | key group, call
+    counter}, key = seed, words x, y = four 16-bit uniforms, keep iff u >= round(p 2^16))."""
+    from oracle import oracle
+    thr = int(round(p * 65536))
+    km = np.zeros((n, heads, 16, 16), np.float32)
+    key = [seed & 0xFFFFFFFF, seed >> 32]
+    for b in range(n):
+        for hh in range(heads):
+            for i in range(16):
+                for g in range(4):
+                    r = oracle.philox4x32_10([b, (hh << 8) | (i << 2) | g, counter & 0xFFFFFFFF, counter >> 32], key)
+                    u = [int(r[0]) & 0xFFFF, int(r[0]) >> 16, int(r[1]) & 0xFFFF, int(r[1]) >> 16]
+                    for j in range(4):
+                        km[b, hh, i, 4 * g + j] = (1.0 / (1.0 - np.float32(p))) if u[j] >= thr else 0.0
+    return km
+
+
+@pytest.mark.parametrize("n,heads,p", [(64, 4, 0.1), (37, 2, 0.3)])
+def test_urm_attention_dropout_matches_masked_autograd(dev, n, heads, p):
+    """URMAttentionFn with attention dropout (training mode, game.py:1314) vs fp32 autograd of
+    softmax(q k^T / 4) * keep @ v with the keep multipliers regenerated by the oracle's Philox at the
+    call's counter: output and dq / dk / dv within the same bf16 bounds as the p = 0 test; the call
+    counter advances by one per training forward; the keep fraction is 1 - p within 3 sigma."""
+    from g2048 import urm
+    from g2048.urm import URMAttentionFn
+    h = 16 * heads
+    torch.manual_seed(n + heads)
+    seed, ctr = urm._attn_drop_state(dev)
+    c0 = int(ctr.item())
+    qkv = (torch.randn(16 * n, 3 * h, device=dev) * 1.5).bfloat16().requires_grad_(True)
+    wt = torch.randn(16 * n, h, device=dev)
+    out = URMAttentionFn.apply(qkv, heads, p)
+    (out.float() * wt).sum().backward()
+    assert int(ctr.item()) == c0 + 1
+    km = torch.from_numpy(_attn_keep_oracle(n, heads, p, seed, c0)).to(dev)
+    frac = float((km > 0).float().mean())
+    sd = (p * (1 - p) / km.numel()) ** 0.5
+    assert abs(frac - (1 - p)) <= 3 * sd + 1e-6, frac
+    ref_in = qkv.detach().float().requires_grad_(True)
+    q, k, v = ref_in.view(n, 16, 3, heads, 16).permute(2, 0, 3, 1, 4).unbind(0)
+    pr = torch.softmax(q @ k.transpose(-1, -2) * 0.25, dim=-1) * km
+    o = (pr @ v).transpose(1, 2).reshape(16 * n, h)
+    (o * wt).sum().backward()
+    assert float((out.float() - o.detach()).abs().max()) <= 0.02 * float(o.abs().max())
+    for name, sl in (("dq", slice(0, h)), ("dk", slice(h, 2 * h)), ("dv", slice(2 * h, 3 * h))):
+        got, want = qkv.grad[:, sl].float().reshape(-1), ref_in.grad[:, sl].reshape(-1)
+        assert float((got - want).abs().max()) <= 0.02 * float(want.abs().max()), name
+        assert float(torch.nn.functional.cosine_similarity(got, want, dim=0)) >= 0.9995, name
+
+
+def test_urm_attention_dropout_graph_replay_draws_new_masks(dev):
+    """Captured in a hipGraph, every replay reads the bumped device counter: two replays give
+    different outputs (different masks), each equal to an eager call at that counter value."""
+    from g2048 import urm
+    from g2048.urm import URMAttentionFn
+    torch.manual_seed(5)
+    n, heads, p = 256, 4, 0.1
+    qkv = (torch.randn(16 * n, 3 * 16 * heads, device=dev)).bfloat16()
+    seed, ctr = urm._attn_drop_state(dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        URMAttentionFn.apply(qkv, heads, p)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = URMAttentionFn.apply(qkv, heads, p)
+    outs = []
+    for _ in range(2):
+        c = int(ctr.item())
+        g.replay()
+        torch.cuda.synchronize()
+        outs.append(out.clone())
+        assert int(ctr.item()) == c + 1
+        ref = torch.empty_like(out)
+        from g2048 import _lib as L
+        L.urm_attention(qkv, ref, heads, p, seed, torch.tensor([c], dtype=torch.int64, device=dev))
+        torch.cuda.synchronize()
+        assert torch.equal(ref, outs[-1])
+    assert not torch.equal(outs[0], outs[1])
+
+
 def test_urm_module_training_uses_device_attention(dev, monkeypatch):
     """GameURM fwd + bwd under bf16 autocast on the device paths (attention core, residual RMSNorm,
     SwiGLU + conv) vs the same model on torch's SDPA + composite rms_norm / SwiGLU / conv: every

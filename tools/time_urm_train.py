@@ -3,7 +3,9 @@ sys.path[:0]=['/root/repo','/root/repo/2048-ppo_amd']
 import agent
 from torch.nn.attention import sdpa_kernel, SDPBackend
 dev=torch.device('cuda',0)
-m=agent.GameURM(agent.GameURMConfig(dropout=0.0)).to(dev)
+drop=float(sys.argv[1]) if len(sys.argv)>1 else 0.1
+m=agent.GameURM(agent.GameURMConfig(dropout=drop)).to(dev)
+print('dropout',drop)
 obs=torch.rand(65536,48,device=dev)*8
 def step():
     with torch.autocast('cuda',dtype=torch.bfloat16):
