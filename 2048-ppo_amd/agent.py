@@ -273,7 +273,15 @@ class GameURM(nn.Module):
         if inputs.ndim == 1:
             inputs = inputs.unsqueeze(0)
         b = inputs.shape[0]
-        emb = self.stem(inputs.view(b, N_CELLS, 3))
+        emb = None
+        if inputs.is_cuda:
+            from g2048 import urm as _urm  # the device training stem and its backward (g2048_urm.h)
+            if _urm.stem_supported(self, inputs):
+                ln = self.stem[1]
+                emb = _urm.StemFn.apply(inputs.reshape(b, 3 * N_CELLS), self.stem[0].weight, ln.weight, ln.bias,
+                                        ln.eps).view(b, N_CELLS, -1)
+        if emb is None:
+            emb = self.stem(inputs.view(b, N_CELLS, 3))
         h = self.init_hidden.expand(b, -1, -1).clone()
         n_trunc = self.config.num_truncated_loops
         if n_trunc > 0:

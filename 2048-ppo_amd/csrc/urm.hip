@@ -1269,6 +1269,150 @@ __global__ __launch_bounds__(256) void urm_swiglu_conv_colsum_kernel(const float
     else db[j - 2 * inter] = t;
 }
 
+// Training-path stem of GameURM (game.py:1376-1380: Linear(3 -> 64, no bias) + LayerNorm + SiLU)
+// for autograd (agent.GameURM under bf16 autocast), one kernel each way, 16 lanes per token row (4
+// features per lane, row sums by 4 xor shuffles).  Autocast's rounding points: the Linear takes
+// bf16 x and W and returns bf16 y; LayerNorm and SiLU run in fp32.
+//   forward  y = bf16(x W^T), xh = (y - mean) rstd, z = xh g + b, emb = z sigmoid(z)
+//   backward dz = demb silu'(z); dg = sum dz xh; db = sum dz; dy = bf16(rstd (dxh - mean(dxh) -
+//            xh mean(dxh xh))) with dxh = dz g; dW = sum dy x (fp32); everything recomputed from x
+//            (12 bytes per token), so nothing is saved between the passes.  The parameter gradients
+//            are per-block partials [nblk][320] (dW f*3+k, dg 192+f, db 256+f) summed in a fixed
+//            order by urm_colsum_kernel: deterministic.
+constexpr int kStemCols = 5 * 64;
+
+template <bool XBF>
+__device__ __forceinline__ void stem_row(const void *__restrict__ obs, int64_t r, const float (&wr)[4][3], float eps,
+                                         float xk[3], float y[4], float xh[4], float &rstd) {
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+        xk[k] = XBF ? bf16f(static_cast<const uint16_t *>(obs)[r * 3 + k]) : bfr(static_cast<const float *>(obs)[r * 3 + k]);
+#pragma unroll
+    for (int u = 0; u < 4; u++) y[u] = bfr(__builtin_fmaf(xk[2], wr[u][2], __builtin_fmaf(xk[1], wr[u][1], xk[0] * wr[u][0])));
+    const float mean = sum16(y[0] + y[1] + y[2] + y[3]) * (1.0f / 64.0f);
+    float d[4], v = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        d[u] = y[u] - mean;
+        v += d[u] * d[u];
+    }
+    rstd = rsqrtf(sum16(v) * (1.0f / 64.0f) + eps);
+#pragma unroll
+    for (int u = 0; u < 4; u++) xh[u] = d[u] * rstd;
+}
+
+template <bool XBF>
+__global__ __launch_bounds__(256) void urm_stem_fwd_kernel(const void *__restrict__ obs, const float *__restrict__ w,
+                                                           const float *__restrict__ lnw, const float *__restrict__ lnb,
+                                                           float *__restrict__ emb, int64_t rows, float eps) {
+    const int lane = threadIdx.x & 15, f0 = 4 * lane;
+    float wr[4][3], g[4], bb[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) wr[u][k] = bfr(w[(f0 + u) * 3 + k]);
+        g[u] = lnw[f0 + u];
+        bb[u] = lnb[f0 + u];
+    }
+    const int64_t stride = (int64_t)gridDim.x * 16;
+    for (int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); r < rows; r += stride) {
+        float xk[3], y[4], xh[4], rstd;
+        stem_row<XBF>(obs, r, wr, eps, xk, y, xh, rstd);
+        float e[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const float z = __builtin_fmaf(xh[u], g[u], bb[u]);
+            e[u] = z * sigm(z);
+        }
+        reinterpret_cast<float4 *>(emb + r * 64)[lane] = make_float4(e[0], e[1], e[2], e[3]);
+    }
+}
+
+template <bool XBF>
+__global__ __launch_bounds__(256) void urm_stem_bwd_kernel(const void *__restrict__ obs, const float *__restrict__ w,
+                                                           const float *__restrict__ lnw, const float *__restrict__ lnb,
+                                                           const float *__restrict__ demb, float *__restrict__ part,
+                                                           int64_t rows, float eps) {
+    __shared__ float red[16][kStemCols + 1];
+    const int lane = threadIdx.x & 15, grp = threadIdx.x >> 4, f0 = 4 * lane;
+    float wr[4][3], g[4], bb[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) wr[u][k] = bfr(w[(f0 + u) * 3 + k]);
+        g[u] = lnw[f0 + u];
+        bb[u] = lnb[f0 + u];
+    }
+    float aw[4][3] = {}, ag[4] = {}, ab[4] = {};
+    const int64_t stride = (int64_t)gridDim.x * 16;
+    for (int64_t r = (int64_t)blockIdx.x * 16 + grp; r < rows; r += stride) {
+        const float4 de = reinterpret_cast<const float4 *>(demb + r * 64)[lane];
+        const float dev[4] = {de.x, de.y, de.z, de.w};
+        float xk[3], y[4], xh[4], rstd;
+        stem_row<XBF>(obs, r, wr, eps, xk, y, xh, rstd);
+        float dxh[4], m1 = 0.0f, m2 = 0.0f;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const float z = __builtin_fmaf(xh[u], g[u], bb[u]), sg = sigm(z);
+            const float dz = dev[u] * (sg * (1.0f + z * (1.0f - sg)));
+            ag[u] += dz * xh[u];
+            ab[u] += dz;
+            dxh[u] = dz * g[u];
+            m1 += dxh[u];
+            m2 += dxh[u] * xh[u];
+        }
+        m1 = sum16(m1) * (1.0f / 64.0f);
+        m2 = sum16(m2) * (1.0f / 64.0f);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const float dy = bfr(rstd * (dxh[u] - m1 - xh[u] * m2));
+#pragma unroll
+            for (int k = 0; k < 3; k++) aw[u][k] = __builtin_fmaf(dy, xk[k], aw[u][k]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) red[grp][(f0 + u) * 3 + k] = aw[u][k];
+        red[grp][192 + f0 + u] = ag[u];
+        red[grp][256 + f0 + u] = ab[u];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < kStemCols; c += 256) {
+        float t = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 16; q++) t += red[q][c];
+        part[(int64_t)blockIdx.x * kStemCols + c] = t;
+    }
+}
+
+// out[c] = sum over the nblk partial rows of column c, in row order per slice (see the swiglu one)
+__global__ __launch_bounds__(256) void urm_colsum_kernel(const float *__restrict__ part, int nblk, int ncol,
+                                                         float *__restrict__ out) {
+    __shared__ float red[16][17];
+    const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
+    const int j = blockIdx.x * 16 + cl;
+    float t = 0.0f;
+    if (j < ncol) {
+        int k = sl;
+        for (; k + 16 * 7 < nblk; k += 16 * 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = part[(int64_t)(k + 16 * u) * ncol + j];
+#pragma unroll
+            for (int u = 0; u < 8; u++) t += v[u];
+        }
+        for (; k < nblk; k += 16) t += part[(int64_t)k * ncol + j];
+    }
+    red[sl][cl] = t;
+    __syncthreads();
+    if (sl != 0 || j >= ncol) return;
+    t = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 16; u++) t += red[u][cl];
+    out[j] = t;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1405,6 +1549,48 @@ int g2048_urm_swiglu_conv_bwd(g2048_stream_t stream, const uint16_t *gu, const f
                        (int)inter);
     hipLaunchKernelGGL(urm_swiglu_conv_colsum_kernel, dim3((3 * inter + 15) / 16), dim3(256), 0, s, partials, nblk,
                        (int)inter, dw, db);
+    return launch_status();
+}
+
+static int stem_blocks(int64_t rows) {
+    const int64_t b = (rows + 15) / 16;
+    return (int)(b < 2048 ? b : 2048);
+}
+
+size_t g2048_urm_stem_partials(int64_t n) { return n <= 0 ? 0 : (size_t)stem_blocks(16 * n) * kStemCols; }
+
+int g2048_urm_stem_fwd(g2048_stream_t stream, const void *obs, int32_t obs_dtype, const float *w, const float *ln_w,
+                       const float *ln_b, float *emb, int64_t n, int32_t h, float eps) {
+    if (n < 0 || h != 64 || (obs_dtype != 0 && obs_dtype != 1)) return G2048_EINVAL;
+    if (n == 0) return G2048_OK;
+    if (!obs || !w || !ln_w || !ln_b || !emb || (uintptr_t)emb % 16) return G2048_EINVAL;
+    const int64_t rows = 16 * n;
+    const hipStream_t s = (hipStream_t)stream;
+    if (obs_dtype == 1)
+        hipLaunchKernelGGL(urm_stem_fwd_kernel<true>, dim3(stem_blocks(rows)), dim3(256), 0, s, obs, w, ln_w, ln_b, emb,
+                           rows, eps);
+    else
+        hipLaunchKernelGGL(urm_stem_fwd_kernel<false>, dim3(stem_blocks(rows)), dim3(256), 0, s, obs, w, ln_w, ln_b, emb,
+                           rows, eps);
+    return launch_status();
+}
+
+int g2048_urm_stem_bwd(g2048_stream_t stream, const void *obs, int32_t obs_dtype, const float *w, const float *ln_w,
+                       const float *ln_b, const float *demb, float *grads, float *partials, int64_t n, int32_t h,
+                       float eps) {
+    if (n <= 0 || h != 64 || (obs_dtype != 0 && obs_dtype != 1)) return G2048_EINVAL;
+    if (!obs || !w || !ln_w || !ln_b || !demb || !grads || !partials || (uintptr_t)demb % 16) return G2048_EINVAL;
+    const int64_t rows = 16 * n;
+    const int nblk = stem_blocks(rows);
+    const hipStream_t s = (hipStream_t)stream;
+    if (obs_dtype == 1)
+        hipLaunchKernelGGL(urm_stem_bwd_kernel<true>, dim3(nblk), dim3(256), 0, s, obs, w, ln_w, ln_b, demb, partials,
+                           rows, eps);
+    else
+        hipLaunchKernelGGL(urm_stem_bwd_kernel<false>, dim3(nblk), dim3(256), 0, s, obs, w, ln_w, ln_b, demb, partials,
+                           rows, eps);
+    hipLaunchKernelGGL(urm_colsum_kernel, dim3((kStemCols + 15) / 16), dim3(256), 0, s, partials, nblk, kStemCols,
+                       grads);
     return launch_status();
 }
 

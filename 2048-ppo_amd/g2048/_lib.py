@@ -33,7 +33,7 @@ EXPORTED = (
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
-    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_rms_res_fwd",
+    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_rms_res_fwd",
     "g2048_urm_rms_res_bwd", "g2048_urm_swiglu_conv_partials", "g2048_urm_swiglu_conv_fwd", "g2048_urm_swiglu_conv_bwd",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
@@ -224,6 +224,9 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
                                             ctypes.c_float, ctypes.c_float, ctypes.c_float]),
         "g2048_grad_sumsq_tick": (ctypes.c_int, [vp, vp, i64, vp, vp]),
         "g2048_urm_attention_bwd": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
+        "g2048_urm_stem_partials": (sz, [i64]),
+        "g2048_urm_stem_fwd": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, i64, i32, ctypes.c_float]),
+        "g2048_urm_stem_bwd": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, vp, vp, i64, i32, ctypes.c_float]),
         "g2048_urm_attention_drop": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, ctypes.c_float, ctypes.c_uint64, vp]),
         "g2048_urm_attention_bwd_drop": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32, ctypes.c_float, ctypes.c_uint64,
                                                         vp]),
@@ -729,6 +732,32 @@ def urm_attention_bwd(qkv, dout, dqkv, heads: int, p: float = 0.0, seed: int = 0
     _check(load().g2048_urm_attention_bwd(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"),
                                           _dev(dout, torch.bfloat16, "dout"), _dev(dqkv, torch.bfloat16, "dqkv"),
                                           rows // 16, h3 // 3, int(heads)), "g2048_urm_attention_bwd")
+
+
+def urm_stem_partials(n: int) -> int:
+    return int(load().g2048_urm_stem_partials(n))
+
+
+def _obs_dtype(obs) -> int:
+    if obs.dtype not in (torch.float32, torch.bfloat16):
+        raise G2048Error(f"obs must be float32 or bfloat16, got {obs.dtype}")
+    return 1 if obs.dtype == torch.bfloat16 else 0
+
+
+def urm_stem_fwd(obs, w, ln_w, ln_b, emb, eps: float):
+    rows, h = emb.shape
+    _check(load().g2048_urm_stem_fwd(_stream(obs), _dev(obs, None, "obs"), _obs_dtype(obs), _dev(w, torch.float32, "w"),
+                                     _dev(ln_w, torch.float32, "ln_w"), _dev(ln_b, torch.float32, "ln_b"),
+                                     _dev(emb, torch.float32, "emb"), rows // 16, h, float(eps)), "g2048_urm_stem_fwd")
+
+
+def urm_stem_bwd(obs, w, ln_w, ln_b, demb, grads, partials, eps: float):
+    rows, h = demb.shape
+    _check(load().g2048_urm_stem_bwd(_stream(obs), _dev(obs, None, "obs"), _obs_dtype(obs), _dev(w, torch.float32, "w"),
+                                     _dev(ln_w, torch.float32, "ln_w"), _dev(ln_b, torch.float32, "ln_b"),
+                                     _dev(demb, torch.float32, "demb"), _dev(grads, torch.float32, "grads"),
+                                     _dev(partials, torch.float32, "partials"), rows // 16, h, float(eps)),
+           "g2048_urm_stem_bwd")
 
 
 def urm_rms_res_fwd(h, a, out, rstd, eps: float):

@@ -206,6 +206,45 @@ def attention_supported(qkv: torch.Tensor, seq: int, hidden: int, heads: int, dr
             and 0.0 <= dropout < 1.0)
 
 
+class StemFn(torch.autograd.Function):
+    """GameURM's stem (game.py:1376-1380: Linear(3 -> 64, no bias) + LayerNorm + SiLU) under bf16
+    autocast, for autograd training on the device: one kernel forward (g2048_urm_stem_fwd), one
+    backward (g2048_urm_stem_bwd: dW, d ln_w, d ln_b with deterministic column sums, everything
+    recomputed from the 12-byte token input) instead of the bf16 GEMM, LayerNorm and SiLU kernels
+    and a K = 16 n weight-gradient GEMM.  obs [n, 48] -> emb fp32 [16 n, 64]; obs gets no gradient."""
+
+    @staticmethod
+    def forward(ctx, obs: torch.Tensor, w: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor, eps: float):
+        obs = obs.contiguous()
+        wf, gf, bf = (t.detach().float().contiguous() for t in (w, ln_w, ln_b))
+        emb = torch.empty(obs.shape[0] * 16, 64, dtype=torch.float32, device=obs.device)
+        L.urm_stem_fwd(obs, wf, gf, bf, emb, eps)
+        ctx.save_for_backward(obs, wf, gf, bf)
+        ctx.eps = eps
+        ctx.dtypes = (w.dtype, ln_w.dtype, ln_b.dtype)
+        return emb
+
+    @staticmethod
+    def backward(ctx, demb: torch.Tensor):
+        obs, wf, gf, bf = ctx.saved_tensors
+        grads = torch.empty(320, dtype=torch.float32, device=obs.device)
+        part = torch.empty(L.urm_stem_partials(obs.shape[0]), dtype=torch.float32, device=obs.device)
+        L.urm_stem_bwd(obs, wf, gf, bf, demb.float().contiguous(), grads, part, ctx.eps)
+        dw, dg, db = grads[:192].view(64, 3), grads[192:256], grads[256:]
+        return (None, dw.to(ctx.dtypes[0]), dg.to(ctx.dtypes[1]), db.to(ctx.dtypes[2]), None)
+
+
+def stem_supported(model, obs: torch.Tensor) -> bool:
+    """The device training stem applies: bf16 autocast on the GPU, h = 64, the default stem
+    (Linear(3, 64, bias=False), affine LayerNorm, SiLU), an observation without gradient."""
+    st = model.stem
+    return (obs.is_cuda and obs.dtype in (torch.float32, torch.bfloat16) and not obs.requires_grad
+            and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+            and len(st) == 3 and isinstance(st[0], torch.nn.Linear) and st[0].bias is None
+            and tuple(st[0].weight.shape) == (64, 3) and isinstance(st[1], torch.nn.LayerNorm)
+            and st[1].weight is not None and st[1].bias is not None and isinstance(st[2], torch.nn.SiLU))
+
+
 class ResidualRMSFn(torch.autograd.Function):
     """rms_norm(h + a) of GameURMBlock (game.py:1346-1350, h = 64) for autograd training on the
     device: one kernel forward (g2048_urm_rms_res_fwd), one backward (g2048_urm_rms_res_bwd)

@@ -84,6 +84,19 @@ int g2048_urm_swiglu_conv_bwd(g2048_stream_t stream, const uint16_t *gu, const f
                               const uint16_t *dact, uint16_t *dgu, float *dw, float *db, float *partials, int64_t n,
                               int32_t inter);
 
+/* The stem for autograd training (GameURM.stem under bf16 autocast, game.py:1376-1380, h = 64):
+ *   forward  emb = SiLU(LayerNorm(bf16(x W^T))) fp32 [16 n, 64]; obs [n, 48] fp32 (obs_dtype 0,
+ *            rounded to bf16 like autocast) or bf16 (1); w [64, 3], ln_w / ln_b [64] fp32
+ *   backward demb fp32 [16 n, 64] -> grads fp32 [320] = dW [64][3] | d ln_w [64] | d ln_b [64]
+ *            (deterministic: per-block partials over g2048_urm_stem_partials(n) floats of scratch
+ *            summed in a fixed order); the observation gets no gradient. */
+size_t g2048_urm_stem_partials(int64_t n);
+int g2048_urm_stem_fwd(g2048_stream_t stream, const void *obs, int32_t obs_dtype, const float *w, const float *ln_w,
+                       const float *ln_b, float *emb, int64_t n, int32_t h, float eps);
+int g2048_urm_stem_bwd(g2048_stream_t stream, const void *obs, int32_t obs_dtype, const float *w, const float *ln_w,
+                       const float *ln_b, const float *demb, float *grads, float *partials, int64_t n, int32_t h,
+                       float eps);
+
 /* Post-norm residual (game.py:1346, 1350 with rms_norm :1223-1229):
  *   x = x + y;  x = x * rsqrt(mean(x^2) + eps)  [+ emb, the next loop's input, game.py:1447];
  *   xb = bf16(x).

@@ -451,6 +451,7 @@ def test_urm_module_training_uses_device_attention(dev, monkeypatch):
             monkeypatch.setattr(urm, "attention_supported", lambda *a, **k: False)
             monkeypatch.setattr(urm, "rms_res_supported", lambda *a, **k: False)
             monkeypatch.setattr(urm, "swiglu_conv_supported", lambda *a, **k: False)
+            monkeypatch.setattr(urm, "stem_supported", lambda *a, **k: False)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             lg, v = m(obs)
         (lg.float().square().sum() + v.float().sum()).backward()
@@ -461,6 +462,59 @@ def test_urm_module_training_uses_device_attention(dev, monkeypatch):
         if float(b.norm()) == 0:
             continue
         assert float(torch.nn.functional.cosine_similarity(a, b, dim=0)) >= 0.999, k
+
+
+@pytest.mark.parametrize("n,odt", [(65536, torch.float32), (37, torch.float32), (1000, torch.bfloat16)])
+def test_urm_stem_fn_matches_autocast_module(dev, n, odt):
+    """StemFn (g2048_urm_stem_fwd / _bwd) vs torch autograd of the stem module under the same bf16
+    autocast (game.py:1376-1380): emb within one bf16 step of the pre-LayerNorm activation (the 3-term
+    dot product may round the other way; measured max 7e-4, mean 2e-8), and the three parameter
+    gradients at cosine >= 0.9999, max error <= 1 % of the largest component."""
+    import agent
+    from g2048.urm import StemFn
+    torch.manual_seed(n)
+    m = agent.GameURM(agent.GameURMConfig()).to(dev)
+    with torch.no_grad():  # a non-trivial affine LayerNorm
+        m.stem[1].weight.uniform_(0.5, 1.5)
+        m.stem[1].bias.uniform_(-0.3, 0.3)
+    obs = (torch.rand(n, 48, device=dev) * 8).to(odt)
+    g = torch.randn(16 * n, 64, device=dev)
+    outs, grads = [], []
+    for use_dev in (True, False):
+        m.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            if use_dev:
+                e = StemFn.apply(obs, m.stem[0].weight, m.stem[1].weight, m.stem[1].bias, m.stem[1].eps)
+            else:
+                e = m.stem(obs.view(n, 16, 3)).reshape(16 * n, 64)
+        (e.float() * g).sum().backward()
+        outs.append(e.detach().float())
+        grads.append([p.grad.detach().clone() for p in m.stem.parameters()])
+    d = (outs[0] - outs[1]).abs()
+    print(f"stem emb: max {d.max().item():.3g} mean {d.mean().item():.3g}")
+    assert d.max().item() <= 0.05 and d.mean().item() <= 2e-4
+    for a, b in zip(*grads):
+        a, b = a.reshape(-1).float(), b.reshape(-1).float()
+        assert float(torch.nn.functional.cosine_similarity(a, b, dim=0)) >= 0.9999
+        assert float((a - b).abs().max()) <= 0.01 * float(b.abs().max())
+
+
+def test_urm_stem_fn_is_deterministic(dev):
+    """Two backward passes on the same input give bitwise equal parameter gradients."""
+    from g2048.urm import StemFn
+    torch.manual_seed(1)
+    w, lw, lb = torch.randn(64, 3, device=dev), torch.rand(64, device=dev) + 0.5, torch.randn(64, device=dev) * 0.1
+    obs = torch.rand(4096, 48, device=dev) * 8
+    g = torch.randn(4096 * 16, 64, device=dev)
+    res = []
+    for _ in range(2):
+        ps = [t.clone().requires_grad_(True) for t in (w, lw, lb)]
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            e = StemFn.apply(obs, *ps, 1e-5)
+        (e * g).sum().backward()
+        res.append([p.grad.clone() for p in ps])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("rows,adt", [(65536 * 16, torch.bfloat16), (1000, torch.float32), (17, torch.bfloat16)])
