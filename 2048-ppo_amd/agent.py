@@ -192,9 +192,10 @@ class GameURMAttention(nn.Module):
         self.qkv_proj = nn.Linear(hidden_size, 3 * hidden_size, bias=False)
         self.o_proj = nn.Linear(hidden_size, hidden_size, bias=False)
 
-    def forward(self, h: torch.Tensor) -> torch.Tensor:
+    def forward(self, h: torch.Tensor, hb: torch.Tensor | None = None) -> torch.Tensor:
+        """hb: h's bf16 copy when the caller already has it (bf16 autocast: the same operand)."""
         b, s, _ = h.shape
-        qkv = self.qkv_proj(h)
+        qkv = self.qkv_proj(h if hb is None else hb)
         p = self.dropout if self.training else 0.0
         if qkv.is_cuda:
             from g2048 import urm as _urm  # the HIP attention core and its backward (g2048_urm.h)
@@ -215,18 +216,31 @@ class GameURMBlock(nn.Module):
         self.mlp = GameConvSwiGLU(config.hidden_dim, config.expansion, config.conv_kernel)
         self.norm_eps = config.rms_norm_eps
 
-    def forward(self, h: torch.Tensor) -> torch.Tensor:
-        a = self.attn(h)
+    def forward(self, h: torch.Tensor, hb: torch.Tensor | None = None, want_hb: bool = False):
+        """want_hb: also return the output's bf16 copy (None when not produced) for the next block's
+        qkv projection; on the device under bf16 autocast the residual RMSNorm kernel writes it, so
+        autocast's cast kernels (and their backward) disappear."""
+        a = self.attn(h, hb)
         if h.is_cuda:
             from g2048 import urm as _urm  # the device residual RMSNorm and its backward (g2048_urm.h)
             if _urm.rms_res_supported(h, a):
-                h = _urm.ResidualRMSFn.apply(h, a, self.norm_eps)
-                m = self.mlp(h)
+                fuse = torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+                if fuse:
+                    h, hb1 = _urm.ResidualRMSFn.apply(h, a, self.norm_eps, True)
+                    m = self.mlp(hb1)
+                else:
+                    h = _urm.ResidualRMSFn.apply(h, a, self.norm_eps)
+                    m = self.mlp(h)
                 if _urm.rms_res_supported(h, m):
-                    return _urm.ResidualRMSFn.apply(h, m, self.norm_eps)
-                return rms_norm(h + m, self.norm_eps)
+                    if want_hb and fuse:
+                        return _urm.ResidualRMSFn.apply(h, m, self.norm_eps, True)
+                    out = _urm.ResidualRMSFn.apply(h, m, self.norm_eps)
+                else:
+                    out = rms_norm(h + m, self.norm_eps)
+                return (out, None) if want_hb else out
         h = rms_norm(h + a, self.norm_eps)
-        return rms_norm(h + self.mlp(h), self.norm_eps)
+        out = rms_norm(h + self.mlp(h), self.norm_eps)
+        return (out, None) if want_hb else out
 
 
 class GameURM(nn.Module):
@@ -265,8 +279,13 @@ class GameURM(nn.Module):
 
     def _loop(self, h: torch.Tensor, emb: torch.Tensor) -> torch.Tensor:
         h = h + emb
-        for layer in self.layers:
-            h = layer(h)
+        hb = None  # bf16 copy of h handed from block to block (device path, bf16 autocast)
+        last = len(self.layers) - 1
+        for i, layer in enumerate(self.layers):
+            if i < last:
+                h, hb = layer(h, hb, want_hb=True)
+            else:
+                h = layer(h, hb)
         return h
 
     def forward(self, inputs: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:

@@ -1109,7 +1109,7 @@ __device__ __forceinline__ float sum16(float x) {
 template <bool ABF>
 __global__ __launch_bounds__(256) void urm_rms_res_fwd_kernel(const float *__restrict__ hin, const void *__restrict__ a,
                                                               float *__restrict__ out, float *__restrict__ rstd,
-                                                              int64_t rows, float eps) {
+                                                              int64_t rows, float eps, uint16_t *__restrict__ outb) {
     const int lane = threadIdx.x & 15;
     const int64_t stride = (int64_t)gridDim.x * 16;
     for (int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); r < rows; r += stride) {
@@ -1125,7 +1125,13 @@ __global__ __launch_bounds__(256) void urm_rms_res_fwd_kernel(const float *__res
         const float4 sv = make_float4(hv.x + av.x, hv.y + av.y, hv.z + av.z, hv.w + av.w);
         const float ms = sum16(sv.x * sv.x + sv.y * sv.y + sv.z * sv.z + sv.w * sv.w) * (1.0f / 64.0f);
         const float rs = rsqrtf(ms + eps);
-        reinterpret_cast<float4 *>(out + r * 64)[lane] = make_float4(sv.x * rs, sv.y * rs, sv.z * rs, sv.w * rs);
+        const float4 ov = make_float4(sv.x * rs, sv.y * rs, sv.z * rs, sv.w * rs);
+        reinterpret_cast<float4 *>(out + r * 64)[lane] = ov;
+        if (outb) {  // the next projection's bf16 operand (what autocast's cast would produce)
+            const __attribute__((ext_vector_type(2))) __bf16 p0 = {(__bf16)ov.x, (__bf16)ov.y}, p1 = {(__bf16)ov.z, (__bf16)ov.w};
+            reinterpret_cast<uint2 *>(outb + r * 64)[lane] =
+                make_uint2(__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1));
+        }
         if (lane == 0) rstd[r] = rs;
     }
 }
@@ -1133,11 +1139,19 @@ __global__ __launch_bounds__(256) void urm_rms_res_fwd_kernel(const float *__res
 template <bool ABF>
 __global__ __launch_bounds__(256) void urm_rms_res_bwd_kernel(const float *__restrict__ dout, const float *__restrict__ out,
                                                               const float *__restrict__ rstd, float *__restrict__ dh,
-                                                              void *__restrict__ da, int64_t rows) {
+                                                              void *__restrict__ da, int64_t rows,
+                                                              const uint16_t *__restrict__ doutb) {
     const int lane = threadIdx.x & 15;
     const int64_t stride = (int64_t)gridDim.x * 16;
     for (int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); r < rows; r += stride) {
-        const float4 g = reinterpret_cast<const float4 *>(dout + r * 64)[lane];
+        float4 g = dout ? reinterpret_cast<const float4 *>(dout + r * 64)[lane] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (doutb) {  // + the bf16 copy's gradient (autocast's cast backward: to fp32, then added)
+            const uint2 w = reinterpret_cast<const uint2 *>(doutb + r * 64)[lane];
+            g.x += __uint_as_float(w.x << 16);
+            g.y += __uint_as_float(w.x & 0xFFFF0000u);
+            g.z += __uint_as_float(w.y << 16);
+            g.w += __uint_as_float(w.y & 0xFFFF0000u);
+        }
         const float4 o = reinterpret_cast<const float4 *>(out + r * 64)[lane];
         const float rs = rstd[r];
         const float mg = sum16(g.x * o.x + g.y * o.y + g.z * o.z + g.w * o.w) * (1.0f / 64.0f);
@@ -1192,6 +1206,42 @@ __global__ __launch_bounds__(kScThreads) void urm_swiglu_conv_fwd_kernel(const u
             const float y2 = yp * w0 + y * w1 + b;
             act[r * inter + c] = f2bf16(y2 * sigm(y2));
             yp = y;
+        }
+    }
+}
+
+// The same forward with one thread per channel PAIR (4-byte gate / up loads and act stores) and
+// four boards per 256-thread block (64 threads per board, inter / 2 <= 64 of them active): half the
+// memory instructions of the one-channel kernel and twice the boards in flight per CU.  Same
+// arithmetic per channel, so the outputs are identical.
+__global__ __launch_bounds__(256) void urm_swiglu_conv_fwd2_kernel(const uint16_t *__restrict__ gu,
+                                                                   const float *__restrict__ w,
+                                                                   const float *__restrict__ bias,
+                                                                   uint16_t *__restrict__ act, int64_t nb, int inter) {
+    const int cp = threadIdx.x & 63;
+    if (2 * cp >= inter) return;
+    const int c = 2 * cp;
+    const float w00 = w[2 * c], w01 = w[2 * c + 1], w10 = w[2 * c + 2], w11 = w[2 * c + 3];
+    const float b0 = bias[c], b1 = bias[c + 1];
+    for (int64_t bd = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); bd < nb; bd += (int64_t)gridDim.x * 4) {
+        uint32_t gr[16], ur[16];
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            const uint16_t *row = gu + (16 * bd + t) * 2 * inter;
+            gr[t] = *reinterpret_cast<const uint32_t *>(row + c);
+            ur[t] = *reinterpret_cast<const uint32_t *>(row + inter + c);
+        }
+        float yp0 = 0.0f, yp1 = 0.0f;
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            const float g0 = __uint_as_float(gr[t] << 16), g1 = __uint_as_float(gr[t] & 0xFFFF0000u);
+            const float u0 = __uint_as_float(ur[t] << 16), u1 = __uint_as_float(ur[t] & 0xFFFF0000u);
+            const float y0 = bfr(bfr(g0 * sigm(g0)) * u0), y1 = bfr(bfr(g1 * sigm(g1)) * u1);
+            const float z0 = yp0 * w00 + y0 * w01 + b0, z1 = yp1 * w10 + y1 * w11 + b1;
+            *reinterpret_cast<uint32_t *>(act + (16 * bd + t) * inter + c) =
+                (uint32_t)f2bf16(z0 * sigm(z0)) | ((uint32_t)f2bf16(z1 * sigm(z1)) << 16);
+            yp0 = y0;
+            yp1 = y1;
         }
     }
 }
@@ -1488,37 +1538,50 @@ int g2048_urm_attention_bwd(g2048_stream_t stream, const uint16_t *qkv, const ui
     return g2048_urm_attention_bwd_drop(stream, qkv, dout, dqkv, n, h, heads, 0.0f, 0, nullptr);
 }
 
-int g2048_urm_rms_res_fwd(g2048_stream_t stream, const float *h, const void *a, int32_t a_dtype, float *out,
-                          float *rstd, int64_t rows, int32_t hidden, float eps) {
+int g2048_urm_rms_res_fwd2(g2048_stream_t stream, const float *h, const void *a, int32_t a_dtype, float *out,
+                           uint16_t *outb, float *rstd, int64_t rows, int32_t hidden, float eps) {
     if (rows < 0 || hidden != 64 || (a_dtype != 0 && a_dtype != 1)) return G2048_EINVAL;
     if (rows == 0) return G2048_OK;
-    if (!h || !a || !out || !rstd || ((uintptr_t)h | (uintptr_t)out) % 16 || (uintptr_t)a % 8) return G2048_EINVAL;
+    if (!h || !a || !out || !rstd || ((uintptr_t)h | (uintptr_t)out) % 16 || ((uintptr_t)a | (uintptr_t)outb) % 8)
+        return G2048_EINVAL;
     const int64_t nb = (rows + 15) / 16;
     const dim3 grid((unsigned)(nb < 4096 ? nb : 4096));
     if (a_dtype == 1)
-        hipLaunchKernelGGL(urm_rms_res_fwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, h, a, out, rstd, rows, eps);
+        hipLaunchKernelGGL(urm_rms_res_fwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, h, a, out, rstd, rows, eps,
+                           outb);
     else
         hipLaunchKernelGGL(urm_rms_res_fwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, h, a, out, rstd, rows,
-                           eps);
+                           eps, outb);
     return launch_status();
 }
 
-int g2048_urm_rms_res_bwd(g2048_stream_t stream, const float *dout, const float *out, const float *rstd, float *dh,
-                          void *da, int32_t a_dtype, int64_t rows, int32_t hidden) {
+int g2048_urm_rms_res_fwd(g2048_stream_t stream, const float *h, const void *a, int32_t a_dtype, float *out,
+                          float *rstd, int64_t rows, int32_t hidden, float eps) {
+    return g2048_urm_rms_res_fwd2(stream, h, a, a_dtype, out, nullptr, rstd, rows, hidden, eps);
+}
+
+int g2048_urm_rms_res_bwd2(g2048_stream_t stream, const float *dout, const uint16_t *doutb, const float *out,
+                           const float *rstd, float *dh, void *da, int32_t a_dtype, int64_t rows, int32_t hidden) {
     if (rows < 0 || hidden != 64 || (a_dtype != 0 && a_dtype != 1)) return G2048_EINVAL;
     if (rows == 0) return G2048_OK;
-    if (!dout || !out || !rstd || !dh || !da || ((uintptr_t)dout | (uintptr_t)out | (uintptr_t)dh) % 16 ||
-        (uintptr_t)da % 8)
+    if ((!dout && !doutb) || !out || !rstd || !dh || !da || ((uintptr_t)dout | (uintptr_t)out | (uintptr_t)dh) % 16 ||
+        ((uintptr_t)da | (uintptr_t)doutb) % 8)
         return G2048_EINVAL;
     const int64_t nb = (rows + 15) / 16;
     const dim3 grid((unsigned)(nb < 4096 ? nb : 4096));
     if (a_dtype == 1)
         hipLaunchKernelGGL(urm_rms_res_bwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, dout, out, rstd, dh, da,
-                           rows);
+                           rows, doutb);
     else
         hipLaunchKernelGGL(urm_rms_res_bwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, dout, out, rstd, dh,
-                           da, rows);
+                           da, rows, doutb);
     return launch_status();
+}
+
+int g2048_urm_rms_res_bwd(g2048_stream_t stream, const float *dout, const float *out, const float *rstd, float *dh,
+                          void *da, int32_t a_dtype, int64_t rows, int32_t hidden) {
+    if (!dout) return G2048_EINVAL;
+    return g2048_urm_rms_res_bwd2(stream, dout, nullptr, out, rstd, dh, da, a_dtype, rows, hidden);
 }
 
 static int sc_blocks(int64_t nb) { return (int)(nb < 2048 ? nb : 2048); }
@@ -1533,6 +1596,12 @@ int g2048_urm_swiglu_conv_fwd(g2048_stream_t stream, const uint16_t *gu, const f
     if (n < 0 || inter <= 0 || inter > kScThreads) return G2048_EINVAL;
     if (n == 0) return G2048_OK;
     if (!gu || !w || !b || !act) return G2048_EINVAL;
+    if (inter % 2 == 0 && inter <= 128 && ((uintptr_t)gu | (uintptr_t)act) % 4 == 0) {
+        const int64_t nb4 = (n + 3) / 4;
+        hipLaunchKernelGGL(urm_swiglu_conv_fwd2_kernel, dim3((unsigned)(nb4 < 4096 ? nb4 : 4096)), dim3(256), 0,
+                           (hipStream_t)stream, gu, w, b, act, n, (int)inter);
+        return launch_status();
+    }
     hipLaunchKernelGGL(urm_swiglu_conv_fwd_kernel, dim3(sc_blocks(n)), dim3(kScThreads), 0, (hipStream_t)stream, gu, w, b,
                        act, n, (int)inter);
     return launch_status();

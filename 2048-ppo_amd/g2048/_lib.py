@@ -33,7 +33,7 @@ EXPORTED = (
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
-    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_rms_res_fwd",
+    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_rms_res_fwd2", "g2048_urm_rms_res_bwd2", "g2048_urm_rms_res_fwd",
     "g2048_urm_rms_res_bwd", "g2048_urm_swiglu_conv_partials", "g2048_urm_swiglu_conv_fwd", "g2048_urm_swiglu_conv_bwd",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
@@ -224,6 +224,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
                                             ctypes.c_float, ctypes.c_float, ctypes.c_float]),
         "g2048_grad_sumsq_tick": (ctypes.c_int, [vp, vp, i64, vp, vp]),
         "g2048_urm_attention_bwd": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
+        "g2048_urm_rms_res_fwd2": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, vp, i64, i32, ctypes.c_float]),
+        "g2048_urm_rms_res_bwd2": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, i64, i32]),
         "g2048_urm_stem_partials": (sz, [i64]),
         "g2048_urm_stem_fwd": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, i64, i32, ctypes.c_float]),
         "g2048_urm_stem_bwd": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, vp, vp, i64, i32, ctypes.c_float]),
@@ -760,22 +762,26 @@ def urm_stem_bwd(obs, w, ln_w, ln_b, demb, grads, partials, eps: float):
            "g2048_urm_stem_bwd")
 
 
-def urm_rms_res_fwd(h, a, out, rstd, eps: float):
+def urm_rms_res_fwd(h, a, out, rstd, eps: float, outb=None):
+    """outb: optional bf16 [rows, 64] copy of out (g2048_urm_rms_res_fwd2)."""
     rows, hid = h.shape
     abf = a.dtype == torch.bfloat16
-    _check(load().g2048_urm_rms_res_fwd(_stream(h), _dev(h, torch.float32, "h"),
-                                        _dev(a, torch.bfloat16 if abf else torch.float32, "a"), int(abf),
-                                        _dev(out, torch.float32, "out"), _dev(rstd, torch.float32, "rstd"), rows, hid,
-                                        float(eps)), "g2048_urm_rms_res_fwd")
+    _check(load().g2048_urm_rms_res_fwd2(_stream(h), _dev(h, torch.float32, "h"),
+                                         _dev(a, torch.bfloat16 if abf else torch.float32, "a"), int(abf),
+                                         _dev(out, torch.float32, "out"), _dev(outb, torch.bfloat16, "outb"),
+                                         _dev(rstd, torch.float32, "rstd"), rows, hid, float(eps)),
+           "g2048_urm_rms_res_fwd2")
 
 
-def urm_rms_res_bwd(dout, out, rstd, dh, da):
+def urm_rms_res_bwd(dout, out, rstd, dh, da, doutb=None):
+    """dout fp32 and / or doutb bf16 (the bf16 copy's gradient); either may be None."""
     rows, hid = out.shape
     abf = da.dtype == torch.bfloat16
-    _check(load().g2048_urm_rms_res_bwd(_stream(out), _dev(dout, torch.float32, "dout"), _dev(out, torch.float32, "out"),
-                                        _dev(rstd, torch.float32, "rstd"), _dev(dh, torch.float32, "dh"),
-                                        _dev(da, torch.bfloat16 if abf else torch.float32, "da"), int(abf), rows, hid),
-           "g2048_urm_rms_res_bwd")
+    _check(load().g2048_urm_rms_res_bwd2(_stream(out), _dev(dout, torch.float32, "dout"),
+                                         _dev(doutb, torch.bfloat16, "doutb"), _dev(out, torch.float32, "out"),
+                                         _dev(rstd, torch.float32, "rstd"), _dev(dh, torch.float32, "dh"),
+                                         _dev(da, torch.bfloat16 if abf else torch.float32, "da"), int(abf), rows, hid),
+           "g2048_urm_rms_res_bwd2")
 
 
 def urm_swiglu_conv_partials(n: int, inter: int) -> int:

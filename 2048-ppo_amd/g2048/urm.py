@@ -247,29 +247,39 @@ def stem_supported(model, obs: torch.Tensor) -> bool:
 
 class ResidualRMSFn(torch.autograd.Function):
     """rms_norm(h + a) of GameURMBlock (game.py:1346-1350, h = 64) for autograd training on the
-    device: one kernel forward (g2048_urm_rms_res_fwd), one backward (g2048_urm_rms_res_bwd)
-    instead of torch's ~10 elementwise / reduction launches each way.  h fp32, a fp32 or bf16."""
+    device: one kernel forward (g2048_urm_rms_res_fwd2), one backward (g2048_urm_rms_res_bwd2)
+    instead of torch's ~10 elementwise / reduction launches each way.  h fp32, a fp32 or bf16.
+    with_bf16=True also returns the output's bf16 copy (the next projection's autocast operand),
+    written by the same kernel; its gradient is added in the backward kernel (no cast kernels)."""
 
     @staticmethod
-    def forward(ctx, h: torch.Tensor, a: torch.Tensor, eps: float):
+    def forward(ctx, h: torch.Tensor, a: torch.Tensor, eps: float, with_bf16: bool = False):
+        ctx.set_materialize_grads(False)
         shape = h.shape
         h2 = h.reshape(-1, shape[-1]).contiguous()
         a2 = a.reshape(-1, shape[-1]).contiguous()
         out = torch.empty_like(h2)
+        outb = torch.empty(h2.shape, dtype=torch.bfloat16, device=h.device) if with_bf16 else None
         rstd = torch.empty(h2.shape[0], dtype=torch.float32, device=h.device)
-        L.urm_rms_res_fwd(h2, a2, out, rstd, eps)
+        L.urm_rms_res_fwd(h2, a2, out, rstd, eps, outb)
         ctx.save_for_backward(out, rstd)
         ctx.a_dtype = a.dtype
         ctx.shape = shape
+        if with_bf16:
+            return out.view(shape), outb.view(shape)
         return out.view(shape)
 
     @staticmethod
-    def backward(ctx, dout: torch.Tensor):
+    def backward(ctx, dout: torch.Tensor, doutb: torch.Tensor | None = None):
         out, rstd = ctx.saved_tensors
+        if dout is None and doutb is None:
+            return None, None, None, None
         dh = torch.empty_like(out)
         da = torch.empty(out.shape, dtype=ctx.a_dtype, device=out.device)
-        L.urm_rms_res_bwd(dout.reshape(out.shape).float().contiguous(), out, rstd, dh, da)
-        return dh.view(ctx.shape), da.view(ctx.shape), None
+        d32 = None if dout is None else dout.reshape(out.shape).float().contiguous()
+        db16 = None if doutb is None else doutb.reshape(out.shape).to(torch.bfloat16).contiguous()
+        L.urm_rms_res_bwd(d32, out, rstd, dh, da, db16)
+        return dh.view(ctx.shape), da.view(ctx.shape), None, None
 
 
 def rms_res_supported(h: torch.Tensor, a: torch.Tensor) -> bool:

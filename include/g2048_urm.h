@@ -70,6 +70,14 @@ int g2048_urm_rms_res_fwd(g2048_stream_t stream, const float *h, const void *a, 
                           float *rstd, int64_t rows, int32_t hidden, float eps);
 int g2048_urm_rms_res_bwd(g2048_stream_t stream, const float *dout, const float *out, const float *rstd, float *dh,
                           void *da, int32_t a_dtype, int64_t rows, int32_t hidden);
+/* The same with the output's bf16 copy fused in (the next projection's autocast operand):
+ *   fwd2  also outb = bf16(out) [rows, 64] when outb != NULL
+ *   bwd2  the output gradient is dout (fp32, may be NULL) + doutb (bf16, may be NULL: the bf16
+ *         copy's gradient, converted and added like autocast's cast backward) */
+int g2048_urm_rms_res_fwd2(g2048_stream_t stream, const float *h, const void *a, int32_t a_dtype, float *out,
+                           uint16_t *outb, float *rstd, int64_t rows, int32_t hidden, float eps);
+int g2048_urm_rms_res_bwd2(g2048_stream_t stream, const float *dout, const uint16_t *doutb, const float *out,
+                           const float *rstd, float *dh, void *da, int32_t a_dtype, int64_t rows, int32_t hidden);
 
 /* SwiGLU + depthwise conv (kernel 2) for autograd training (GameConvSwiGLU, game.py:1264-1276),
  * n boards of 16 tokens, inter <= 128 channels, the reference's autocast dtypes:

@@ -464,6 +464,33 @@ def test_urm_module_training_uses_device_attention(dev, monkeypatch):
         assert float(torch.nn.functional.cosine_similarity(a, b, dim=0)) >= 0.999, k
 
 
+@pytest.mark.parametrize("rows", [65536 * 16, 33])
+def test_urm_residual_rms_fn_bf16_copy(dev, rows):
+    """ResidualRMSFn(with_bf16=True): the bf16 copy equals out.bfloat16() bitwise, and the backward
+    with gradients on both outputs equals the fp32-only backward of dout + float(doutb) bitwise (the
+    kernel adds what autocast's cast backward would have added); only-bf16 and only-fp32 gradients."""
+    from g2048.urm import ResidualRMSFn
+    torch.manual_seed(rows)
+    h = torch.randn(rows, 64, device=dev) * 2
+    a = torch.randn(rows, 64, device=dev).bfloat16()
+    g32 = torch.randn(rows, 64, device=dev)
+    g16 = torch.randn(rows, 64, device=dev).bfloat16()
+    for use32, use16 in ((True, True), (False, True), (True, False)):
+        h1, a1 = h.clone().requires_grad_(True), a.clone().requires_grad_(True)
+        out, outb = ResidualRMSFn.apply(h1, a1, 1e-6, True)
+        assert torch.equal(outb, out.detach().bfloat16())
+        loss = (out * g32).sum() if use32 else 0.0
+        if use16:
+            loss = loss + (outb.float() * g16.float()).sum()
+        loss.backward()
+        h2, a2 = h.clone().requires_grad_(True), a.clone().requires_grad_(True)
+        out2 = ResidualRMSFn.apply(h2, a2, 1e-6)
+        gt = (g32 if use32 else torch.zeros_like(g32)) + (g16.float() if use16 else 0.0)
+        out2.backward(gt)
+        assert torch.equal(out.detach(), out2.detach())
+        assert torch.equal(h1.grad, h2.grad) and torch.equal(a1.grad, a2.grad)
+
+
 @pytest.mark.parametrize("n,odt", [(65536, torch.float32), (37, torch.float32), (1000, torch.bfloat16)])
 def test_urm_stem_fn_matches_autocast_module(dev, n, odt):
     """StemFn (g2048_urm_stem_fwd / _bwd) vs torch autograd of the stem module under the same bf16
