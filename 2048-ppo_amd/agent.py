@@ -292,6 +292,11 @@ class GameURM(nn.Module):
         if inputs.ndim == 1:
             inputs = inputs.unsqueeze(0)
         b = inputs.shape[0]
+        if inputs.is_cuda and self.training and not torch.is_grad_enabled():
+            from g2048 import urm as _urm  # training-mode no-grad forward (the KL re-forward) in one launch
+            out = _urm.train_nograd_forward(self, inputs)
+            if out is not None:
+                return out
         emb = None
         if inputs.is_cuda:
             from g2048 import urm as _urm  # the device training stem and its backward (g2048_urm.h)

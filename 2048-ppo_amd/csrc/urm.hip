@@ -110,14 +110,16 @@ struct AttnDrop {
     uint32_t k0, k1;
     const uint64_t *counter;  // device call counter (graph-replay safe)
 };
-__device__ __forceinline__ void attn_keep(const AttnDrop &d, int64_t b, int hh, int i, int g, float km[4]) {
-    const uint64_t c = *d.counter;
+__device__ __forceinline__ void attn_keep_c(const AttnDrop &d, uint64_t c, int64_t b, int hh, int i, int g, float km[4]) {
     const uint4 r = g2048::philox((uint32_t)b, ((uint32_t)hh << 8) | ((uint32_t)i << 2) | (uint32_t)g, (uint32_t)c,
                                   (uint32_t)(c >> 32), d.k0, d.k1);
     km[0] = (r.x & 0xFFFFu) >= d.thr ? d.scale : 0.0f;
     km[1] = (r.x >> 16) >= d.thr ? d.scale : 0.0f;
     km[2] = (r.y & 0xFFFFu) >= d.thr ? d.scale : 0.0f;
     km[3] = (r.y >> 16) >= d.thr ? d.scale : 0.0f;
+}
+__device__ __forceinline__ void attn_keep(const AttnDrop &d, int64_t b, int hh, int i, int g, float km[4]) {
+    attn_keep_c(d, *d.counter, b, hh, i, g, km);
 }
 
 template <bool kAligned, bool kDrop>
@@ -608,6 +610,7 @@ struct UrmW {  // device pointers (see g2048_urm_weights)
     const float *cw[2], *cb[2];
     int layers, loops;
     float eps;
+    AttnDrop drop;  // thr == 0: no attention dropout; else block application `app` uses counter *counter + app
 };
 
 // butterfly steps across the 16-lane rows on the VALU lane swaps (v_permlane16/32_swap) instead of
@@ -742,6 +745,7 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
     const int64_t per_batch = (int64_t)mk::WAVES * mk::NB;
     const int64_t batches = (n + per_batch - 1) / per_batch;
     const int apps = W.layers * W.loops;
+    const uint64_t drop_c0 = W.drop.thr ? *W.drop.counter : 0ull;  // attention dropout (training-mode forward)
     for (int e = tid; e < mk::W_BYTES / 16; e += mk::THREADS) reinterpret_cast<uint4 *>(smem)[e] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();  // the parameters and the zeroed padding are read by every wave
     for (int64_t bt = blockIdx.x; bt < batches; bt += gridDim.x) {
@@ -883,8 +887,17 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
                     sum = xsum32(xsum16(sum));
                     const float inv = 1.0f / sum;
                     s16x4 pb;
+                    if (W.drop.thr) {  // wave-uniform; the mask of URMAttentionFn at counter c0 + app
+                        float km[4];
+                        int64_t b = bt * per_batch + wave * mk::NB + nb;
+                        b = b < n ? b : n - 1;
+                        attn_keep_c(W.drop, drop_c0 + (uint64_t)app, b, hh, t, g, km);
 #pragma unroll
-                    for (int r = 0; r < 4; r++) pb[r] = (short)f2bf(p[r] * inv);
+                        for (int r = 0; r < 4; r++) pb[r] = (short)f2bf(p[r] * inv * km[r]);
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; r++) pb[r] = (short)f2bf(p[r] * inv);
+                    }
                     const f32x4 o = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, pb, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
                     wave_lds_sync();  // every lane's Q / K / V reads of this head are done
                     *reinterpret_cast<uint2 *>(tile + (t * mk::TP + 16 * hh + 4 * g) * 2) =
@@ -1750,6 +1763,13 @@ int g2048_urm_forward_supported(int32_t hidden, int32_t heads, int32_t inter, in
 
 int g2048_urm_forward(g2048_stream_t stream, const g2048_urm_weights *w, const void *obs, int32_t obs_dtype,
                       float *logits, float *value, int64_t n) {
+    return g2048_urm_forward_drop(stream, w, obs, obs_dtype, logits, value, n, 0.0f, 0, nullptr);
+}
+
+int g2048_urm_forward_drop(g2048_stream_t stream, const g2048_urm_weights *w, const void *obs, int32_t obs_dtype,
+                           float *logits, float *value, int64_t n, float p, uint64_t seed, const uint64_t *counter) {
+    AttnDrop drop{};
+    if (!attn_drop_args(p, seed, counter, drop)) return G2048_EINVAL;
     if (!w || n < 0 || (obs_dtype != 0 && obs_dtype != 1) || w->num_loops <= 0 ||
         !g2048_urm_forward_supported(w->hidden, w->heads, w->inter, w->num_layers, 2))
         return G2048_EINVAL;
@@ -1772,6 +1792,7 @@ int g2048_urm_forward(g2048_stream_t stream, const g2048_urm_weights *w, const v
     a.layers = w->num_layers;
     a.loops = w->num_loops;
     a.eps = w->eps;
+    a.drop = drop;
     const int64_t per_batch = (int64_t)mk::WAVES * mk::NB;
     int64_t grid = (n + per_batch - 1) / per_batch;
     grid = grid > 256 ? 256 : grid;  // one block per CU: the layer's weights fill most of the LDS

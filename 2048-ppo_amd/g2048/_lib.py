@@ -33,7 +33,7 @@ EXPORTED = (
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
-    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_rms_res_fwd2", "g2048_urm_rms_res_bwd2", "g2048_urm_rms_res_fwd",
+    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_rms_res_fwd2", "g2048_urm_rms_res_bwd2", "g2048_urm_forward_drop", "g2048_urm_rms_res_fwd",
     "g2048_urm_rms_res_bwd", "g2048_urm_swiglu_conv_partials", "g2048_urm_swiglu_conv_fwd", "g2048_urm_swiglu_conv_bwd",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
@@ -212,6 +212,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_urm_linear_supported": (ctypes.c_int, [i32, i32, i32, i32]),
         "g2048_urm_forward_supported": (ctypes.c_int, [i32, i32, i32, i32, i32]),
         "g2048_urm_forward": (ctypes.c_int, [vp, ctypes.POINTER(UrmWeights), vp, i32, vp, vp, i64]),
+        "g2048_urm_forward_drop": (ctypes.c_int, [vp, ctypes.POINTER(UrmWeights), vp, i32, vp, vp, i64, ctypes.c_float,
+                                                  ctypes.c_uint64, vp]),
         "g2048_urm_linear": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_linear_rms": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32, ctypes.c_float]),
         "g2048_urm_linear_swiglu": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32]),
@@ -858,6 +860,17 @@ def urm_linear_swiglu(inp, w, conv_w, conv_b, out):
 def urm_forward_supported(hidden: int, heads: int, inter: int, num_layers: int, conv_kernel: int) -> bool:
     return bool(load().g2048_urm_forward_supported(int(hidden), int(heads), int(inter), int(num_layers),
                                                    int(conv_kernel)))
+
+
+def urm_forward_drop(weights: UrmWeights, obs, logits, value, p: float, seed: int, counter):
+    """g2048_urm_forward in training mode (attention dropout p, mask counter *counter + block app)."""
+    if obs.dtype not in (torch.float32, torch.bfloat16):
+        raise G2048Error("obs must be float32 or bfloat16")
+    _check(load().g2048_urm_forward_drop(_stream(obs), ctypes.byref(weights), _dev(obs, None, "obs"),
+                                         int(obs.dtype == torch.bfloat16), _dev(logits, torch.float32, "logits"),
+                                         _dev(value, torch.float32, "value"), obs.shape[0], float(p),
+                                         int(seed) & (2 ** 64 - 1), _dev(counter, torch.int64, "counter")),
+           "g2048_urm_forward_drop")
 
 
 def urm_forward(weights: UrmWeights, obs, logits, value):

@@ -71,6 +71,26 @@ class URMPolicy:
         self._n = -1
         self.sync()
 
+    def param_ptrs(self) -> tuple:
+        """The master parameters the one-launch forward reads in place (an optimizer that re-homes
+        parameters into flat buffers changes these: the caller rebuilds the policy then)."""
+        m = self.master
+        return tuple(t.data_ptr() for t in (m.stem[0].weight, m.stem[1].weight, m.stem[1].bias, m.action_head.weight,
+                                            m.action_head.bias, m.value_head.weight, m.value_head.bias))
+
+    def forward_train(self, obs: torch.Tensor, p: float):
+        """The one-launch forward with the model's attention dropout (training mode, no gradient):
+        the PPO update's KL re-forward (train.py:577-582).  Masks from the same Philox key and device
+        call counter as URMAttentionFn (application app at counter + app; the counter is bumped by the
+        number of applications).  Fresh output tensors."""
+        n = obs.shape[0]
+        logits = torch.empty(n, 4, dtype=torch.float32, device=obs.device)
+        value = torch.empty(n, dtype=torch.float32, device=obs.device)
+        seed, ctr = _attn_drop_state(obs.device)
+        L.urm_forward_drop(self._w, obs.contiguous(), logits, value, p, seed, ctr)
+        ctr.add_(self.loops * len(self.master.layers))
+        return logits, value
+
     @staticmethod
     def supports(model) -> bool:
         try:
@@ -232,6 +252,30 @@ class StemFn(torch.autograd.Function):
         L.urm_stem_bwd(obs, wf, gf, bf, demb.float().contiguous(), grads, part, ctx.eps)
         dw, dg, db = grads[:192].view(64, 3), grads[192:256], grads[256:]
         return (None, dw.to(ctx.dtypes[0]), dg.to(ctx.dtypes[1]), db.to(ctx.dtypes[2]), None)
+
+
+def train_nograd_forward(model, obs: torch.Tensor):
+    """GameURM.forward in training mode without autograd on the device (the PPO update's KL
+    diagnostic re-forward, train.py:577-582): the one-launch forward g2048_urm_forward_drop with the
+    model's attention dropout instead of ~50 per-op kernels.  Rounding points are the inference
+    kernel's (fp32 stem, fused epilogues), not autocast's; the KL is a logged diagnostic only.
+    Returns None when the one-launch forward does not cover the model (caller falls back)."""
+    if not (obs.is_cuda and obs.dtype in (torch.float32, torch.bfloat16) and obs.ndim == 2 and obs.shape[1] == 48):
+        return None
+    c = model.config
+    if not (URMPolicy.supports(model) and 0.0 <= c.dropout < 1.0
+            and L.urm_forward_supported(c.hidden_dim, c.num_heads, model.layers[0].mlp.inter, len(model.layers),
+                                        c.conv_kernel)):
+        return None
+    pol = model.__dict__.get("_g2048_train_fwd")
+    if pol is None or pol.param_ptrs() != pol._ptrs:
+        pol = URMPolicy(model)
+        pol._ptrs = pol.param_ptrs()
+        model.__dict__["_g2048_train_fwd"] = pol
+    else:
+        pol.sync()  # the bf16 weight copies of the current parameters (captured with a graph)
+    logits, value = pol.forward_train(obs, float(c.dropout))
+    return logits, value.view(-1, 1)
 
 
 def stem_supported(model, obs: torch.Tensor) -> bool:

@@ -159,6 +159,13 @@ int g2048_urm_forward_supported(int32_t hidden, int32_t heads, int32_t inter, in
 int g2048_urm_forward(g2048_stream_t stream, const g2048_urm_weights *w, const void *obs, int32_t obs_dtype,
                       float *logits, float *value, int64_t n);
 
+/* g2048_urm_forward in training mode (the model's attention dropout, game.py:1314): block
+ * application `app` (0 .. num_loops * num_layers - 1) draws the mask of g2048_urm_attention_drop at
+ * counter *counter + app (the caller bumps the counter by that many afterwards).  Used for the PPO
+ * update's no-grad KL re-forward (train.py:577-582, model still in train mode).  p = 0: g2048_urm_forward. */
+int g2048_urm_forward_drop(g2048_stream_t stream, const g2048_urm_weights *w, const void *obs, int32_t obs_dtype,
+                           float *logits, float *value, int64_t n, float p, uint64_t seed, const uint64_t *counter);
+
 #ifdef __cplusplus
 }
 #endif

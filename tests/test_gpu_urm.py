@@ -464,6 +464,49 @@ def test_urm_module_training_uses_device_attention(dev, monkeypatch):
         assert float(torch.nn.functional.cosine_similarity(a, b, dim=0)) >= 0.999, k
 
 
+def test_urm_train_nograd_forward_matches_module_with_dropout(dev):
+    """The training-mode no-grad forward (the PPO update's KL re-forward) runs the one-launch kernel
+    with attention dropout.  At the same counter its masks are the autograd module path's
+    (URMAttentionFn at counters c .. c + 7 for the 8 block applications): its distance to the module
+    output is that of the dropout-free pair (the two paths' different bf16 rounding points: fp32 vs
+    bf16 stem, fused epilogues) -- mean within 1.5x + 1e-3 of it, max <= 0.08 of the logit scale like
+    the module-vs-fp32 bound -- and well below the distance with the masks of another counter.
+    The counter advances by 8 either way; eval mode keeps the module path."""
+    import agent
+    from g2048 import urm
+    torch.manual_seed(11)
+    m = agent.GameURM(agent.GameURMConfig(dropout=0.1)).to(dev).train()
+    obs = torch.rand(3000, 48, device=dev) * 8
+    seed, ctr = urm._attn_drop_state(dev)
+
+    def run(p, grad, c):
+        m.config.dropout = p
+        for blk in m.layers:
+            blk.attn.dropout = p
+        ctr.fill_(c)
+        with torch.set_grad_enabled(grad), torch.autocast("cuda", dtype=torch.bfloat16):
+            lg, v = m(obs)
+        assert int(ctr.item()) == c + (8 if p > 0 else 0) or (p == 0 and not grad)
+        return torch.cat([lg.float().reshape(-1), v.float().reshape(-1)]).detach()
+
+    c = int(ctr.item()) + 100
+    mod0, one0 = run(0.0, True, c), run(0.0, False, c)
+    mod1, one1 = run(0.1, True, c), run(0.1, False, c)
+    other = run(0.1, False, c + 1000)
+    assert "_g2048_train_fwd" in m.__dict__
+    d0, d1, dx = (one0 - mod0).abs(), (one1 - mod1).abs(), (other - mod1).abs()
+    print(f"one-launch vs module: p=0 max {d0.max().item():.3g} mean {d0.mean().item():.3g}; p=0.1 same masks "
+          f"max {d1.max().item():.3g} mean {d1.mean().item():.3g}; other masks mean {dx.mean().item():.3g}")
+    assert d1.mean().item() <= 1.5 * d0.mean().item() + 1e-3
+    assert d1.max().item() <= 0.08 * mod1.abs().max().item()
+    assert dx.mean().item() >= 3 * d1.mean().item()
+    m.eval()
+    c2 = int(ctr.item())
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        m(obs)
+    assert int(ctr.item()) == c2  # eval: no dropout, module path
+
+
 @pytest.mark.parametrize("rows", [65536 * 16, 33])
 def test_urm_residual_rms_fn_bf16_copy(dev, rows):
     """ResidualRMSFn(with_bf16=True): the bf16 copy equals out.bfloat16() bitwise, and the backward
