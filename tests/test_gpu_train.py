@@ -58,11 +58,12 @@ def test_calculate_advantage_matches_reference(dev, case):
     assert aug == []
 
 
-def test_rtg_scan_large_time_major_vs_oracle(dev):
-    """[T=96, N=4096] trajectory with auto-reset episode ends and inactive tails, fp64 oracle."""
+@pytest.mark.parametrize("T,n", [(96, 4096), (64, 65536)])
+def test_rtg_scan_large_time_major_vs_oracle(dev, T, n):
+    """[T, N] trajectory with auto-reset episode ends and inactive tails vs the fp64 oracle; the
+    second case is BASELINE config 3's full per-GPU shape (65 536 envs x T = 64: 3.1 M live steps)."""
     from g2048 import _lib as L
-    T, n = 96, 4096
-    g = np.random.default_rng(0)
+    g = np.random.default_rng(n)
     points = (g.integers(0, 5, size=(T, n)) * 4).astype(np.int32)
     pot = g.integers(0, 17, size=(T, n, 4)).astype(np.int8)
     flags = np.where(g.random((T, n)) < 0.02, L.FLAG_DONE, 0).astype(np.uint8)
@@ -84,15 +85,13 @@ def test_rtg_scan_large_time_major_vs_oracle(dev):
     gr, gn, ad = (o.cpu().numpy() for o in outs)
     # oracle: per env episodes in time order
     exp_gr = np.zeros((T, n))
-    rows, ends, idx = [], [], []
-    for e in range(n):
-        for t in range(tail[e]):
-            idx.append((t, e))
-            ends.append(bool(flags[t, e] & L.FLAG_DONE) or t == tail[e] - 1)
-    ii = np.array(idx)
-    sel = (ii[:, 0], ii[:, 1])
+    # episode order: env-major, time ascending, the live prefix t < tail[e] of each env
+    ee = np.repeat(np.arange(n), tail)
+    tt = np.arange(len(ee)) - np.repeat(np.cumsum(tail) - tail, tail)
+    sel = (tt, ee)
+    ends = ((flags[sel] & L.FLAG_DONE) != 0) | (tt == tail[ee] - 1)
     r = O.reward_rtg_normalize(points[sel], pot[sel][:, 0], pot[sel][:, 1], pot[sel][:, 2], pot[sel][:, 3],
-                               (flags[sel] & L.FLAG_DONE) != 0, value[sel], np.array(ends), gamma, wp, wm, we, beta,
+                               (flags[sel] & L.FLAG_DONE) != 0, value[sel], ends, gamma, wp, wm, we, beta,
                                state0[1], state0[0], int(state0[3]), state0[2])
     np.testing.assert_allclose(gr[sel], r["g_raw"], rtol=1e-6, atol=1e-4)
     np.testing.assert_allclose(gn[sel], r["g_norm"], rtol=1e-5, atol=1e-5)
@@ -233,6 +232,28 @@ def test_trainer_runs_and_learns_signal(dev, horizon, ratio, hidden):
     assert mom["rtg_step"] == 5
     ev = tr.evaluate(16, 200)
     assert ev["eval/max_score"] >= ev["eval/avg_score"] > 0
+
+
+def test_trainer_full_config3_shape(dev):
+    """BASELINE config 3 at its full per-GPU shape (65 536 envs, h = 196, T = 64, minibatch 65 536,
+    up-sampling 0.25, graphs on): two train steps run, every metric finite, the update moves the
+    weights, the sample count is envs x T, and the augmented count is 0.25 x samples within 6 sigma."""
+    from g2048.trainer import TrainConfig, VecTrainer
+    cfg = TrainConfig(steps=4, episodes=65536, horizon=64, batch_size=65536, hidden=196, points=0.1, mono=1.0,
+                      rtg_beta=0.99, entropy=0.02, critic=0.2, warmup_steps=1, lr=1e-3, critic_lr=1e-4,
+                      upsample_ratio=0.25)
+    tr = VecTrainer(cfg, dev)
+    before = [p.detach().clone() for p in tr.model.parameters()]
+    ms = [tr.train_step(s) for s in range(2)]
+    for m in ms:
+        for k, v in m.items():
+            assert v is None or not isinstance(v, float) or math.isfinite(v), k
+        assert m["samples"] == 65536 * 64
+        k = int(m["samples"] * 0.25)
+        assert abs(m["augmented_samples"] - k) < 6 * k ** 0.5 + 2
+        assert m["grad_norm"] > 0 and 0 < m["entropy"] <= math.log(4) + 1e-5
+    moved = sum(float((p.detach() - q).abs().max()) > 0 for p, q in zip(tr.model.parameters(), before))
+    assert moved == len(before)
 
 
 def test_episodic_trainer_respects_max_steps(dev):
