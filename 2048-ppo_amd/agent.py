@@ -158,6 +158,13 @@ class GameConvSwiGLU(nn.Module):
         self.down_proj = nn.Linear(inter, hidden_size, bias=False)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda:
+            from g2048 import urm as _urm  # fused gate_up + SwiGLU + conv (training, g2048_urm.h)
+            if _urm.gate_up_swiglu_supported(self, x):
+                b, s, h = x.shape
+                act = _urm.GateUpSwiGLUFn.apply(x.reshape(b * s, h), self.gate_up_proj.weight,
+                                                self.dwconv.weight.view(-1, 2), self.dwconv.bias)
+                return _urm.project(self.down_proj, act.view(b, s, self.inter))
         gu = self.gate_up_proj(x)
         if gu.is_cuda:
             from g2048 import urm as _urm  # the device SwiGLU + conv and its backward (g2048_urm.h)
@@ -195,13 +202,15 @@ class GameURMAttention(nn.Module):
     def forward(self, h: torch.Tensor, hb: torch.Tensor | None = None) -> torch.Tensor:
         """hb: h's bf16 copy when the caller already has it (bf16 autocast: the same operand)."""
         b, s, _ = h.shape
-        qkv = self.qkv_proj(h if hb is None else hb)
         p = self.dropout if self.training else 0.0
-        if qkv.is_cuda:
+        if h.is_cuda:
             from g2048 import urm as _urm  # the HIP attention core and its backward (g2048_urm.h)
+            qkv = _urm.project(self.qkv_proj, h if hb is None else hb)
             if _urm.attention_supported(qkv, s, self.hidden_size, self.num_heads, p):
                 o = _urm.URMAttentionFn.apply(qkv.reshape(b * s, 3 * self.hidden_size), self.num_heads, p)
-                return self.o_proj(o.view(b, s, self.hidden_size))
+                return _urm.project(self.o_proj, o.view(b, s, self.hidden_size))
+        else:
+            qkv = self.qkv_proj(h)
         q, k, v = qkv.view(b, s, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).unbind(0)
         o = F.scaled_dot_product_attention(q, k, v, dropout_p=p, is_causal=False)
         return self.o_proj(o.transpose(1, 2).reshape(b, s, self.hidden_size))
@@ -312,6 +321,11 @@ class GameURM(nn.Module):
             with torch.no_grad():
                 for _ in range(n_trunc):
                     h = self._loop(h, emb)
+            if torch.is_autocast_enabled(h.device.type):
+                # autocast caches its bf16 weight casts; the ones made under no_grad carry no
+                # autograd history, and reusing them in the loops below would leave every projection
+                # weight without a gradient -- drop them so those loops cast again with history
+                torch.clear_autocast_cache()
         for _ in range(self.config.num_loops - n_trunc):
             h = self._loop(h, emb)
         pooled = h.mean(dim=1)

@@ -356,7 +356,12 @@ __global__ __launch_bounds__(kThreads) void urm_pool_heads_kernel(const float *_
 //              16-lane DPP row (row_shr:1; token 0 gets the conv's zero padding), then
 //              SiLU(w0 a_{t-1} + w1 a_t + b) -> act bf16 [rows, inter]
 // The projection outputs stay fp32 into the epilogue (no bf16 round trip through HBM).
-enum { EPI_STORE = 0, EPI_RMS = 1, EPI_SWIGLU = 2 };
+//   EPI_SWIGLU_T the training variant (autograd GateUpSwiGLUFn): the gate / up accumulators are
+//              rounded to bf16 and stored as gu [rows, 2 inter] (the backward's input, autocast's
+//              gate_up output) and act follows urm_swiglu_conv_fwd's arithmetic on those rounded
+//              values (y = bf16(bf16(silu(g)) u), act = bf16(silu(y_{t-1} w0 + y_t w1 + b))): the
+//              gu round trip through HBM of the unfused path (GEMM write + SwiGLU read) is gone.
+enum { EPI_STORE = 0, EPI_RMS = 1, EPI_SWIGLU = 2, EPI_SWIGLU_T = 3 };
 
 __device__ __forceinline__ float dpp_prev_token(float v) {  // lane t-1 of the 16-lane row, 0 for t = 0
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xF, 0xF, false));
@@ -387,7 +392,7 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
         for (int e = tid; e < kRowsW * k4; e += kThreads) {
             const int q = e / k4, c4 = e - q * k4;
             int src = q;
-            if (EPI == EPI_SWIGLU) {
+            if (EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_T) {
                 const int hq = q - kRowsW / 2;
                 src = q < kRowsW / 2 ? (q < inter ? q : -1) : (hq < inter ? inter + hq : -1);
             } else if (q >= N) {
@@ -493,6 +498,40 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
                                    (uint32_t)f2bf(o.z) | ((uint32_t)f2bf(o.w) << 16));
                 }
             }
+        } else if constexpr (EPI == EPI_SWIGLU_T) {
+            constexpr int CH = CT / 2;
+            auto sg = [](float v) { return 1.0f / (1.0f + expf(-v)); };
+            auto rb = [](float v) { return (float)(__bf16)v; };
+            auto pk = [](float a0, float a1, float a2, float a3) {
+                const __attribute__((ext_vector_type(2))) __bf16 p0 = {(__bf16)a0, (__bf16)a1}, p1 = {(__bf16)a2, (__bf16)a3};
+                return make_uint2(__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1));
+            };
+#pragma unroll
+            for (int ct = 0; ct < CH; ct++) {
+                const int c = 16 * ct + 4 * g;
+                const int cc = c < inter ? c : 0;
+                const float4 w01 = *reinterpret_cast<const float4 *>(cw + 2 * cc);
+                const float4 w23 = *reinterpret_cast<const float4 *>(cw + 2 * cc + 4);
+                const float4 bb = *reinterpret_cast<const float4 *>(cb + cc);
+                const float wk0[4] = {w01.x, w01.z, w23.x, w23.z}, wk1[4] = {w01.y, w01.w, w23.y, w23.w};
+                const float bk[4] = {bb.x, bb.y, bb.z, bb.w};
+                float gq[4], uq[4], o[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    gq[i] = rb(acc[ct][i]);
+                    uq[i] = rb(acc[ct + CH][i]);
+                    const float yv = rb(rb(gq[i] * sg(gq[i])) * uq[i]);
+                    const float prev = dpp_prev_token(yv);
+                    const float z = prev * wk0[i] + yv * wk1[i] + bk[i];
+                    o[i] = z * sg(z);
+                }
+                if (c < inter) {
+                    uint16_t *gr = xb + r * 2 * inter;  // gu output (xb carries it for this epilogue)
+                    *reinterpret_cast<uint2 *>(gr + c) = pk(gq[0], gq[1], gq[2], gq[3]);
+                    *reinterpret_cast<uint2 *>(gr + inter + c) = pk(uq[0], uq[1], uq[2], uq[3]);
+                    *reinterpret_cast<uint2 *>(y + r * inter + c) = pk(o[0], o[1], o[2], o[3]);
+                }
+            }
         } else {
             constexpr int CH = CT / 2;
 #pragma unroll
@@ -527,7 +566,7 @@ struct LinShape {
 };
 inline LinShape lin_shape(int K, int N, int inter, int epi) {
     const int ks = (K + 31) / 32;
-    const int ct = epi == EPI_SWIGLU ? 2 * ((inter + 15) / 16) : (N + 15) / 16;
+    const int ct = (epi == EPI_SWIGLU || epi == EPI_SWIGLU_T) ? 2 * ((inter + 15) / 16) : (N + 15) / 16;
     return {ks, ct};
 }
 
@@ -559,6 +598,8 @@ int dispatch_lin(hipStream_t s, int epi, const uint16_t *in, const uint16_t *w, 
     G2048_LIN(EPI_RMS, 2, 2)      // h 32 down_proj (K = 64)
     G2048_LIN(EPI_SWIGLU, 2, 16)  // h 64 gate_up (inter 120 -> 2 x 8 tiles)
     G2048_LIN(EPI_SWIGLU, 1, 8)   // h 32 gate_up (inter 64)
+    G2048_LIN(EPI_SWIGLU_T, 2, 16)  // training variants of the two
+    G2048_LIN(EPI_SWIGLU_T, 1, 8)
 #undef G2048_LIN
     return G2048_EINVAL;
 }
@@ -601,7 +642,10 @@ constexpr int THREADS = 64 * WAVES;
 constexpr int PS_STEM = 0, PS_LNW = PS_STEM + 3 * H, PS_LNB = PS_LNW + H, PS_INIT = PS_LNB + H,
               PS_WA = PS_INIT + 16 * H, PS_WV = PS_WA + 4 * H, PS_BA = PS_WV + H, PS_BV = PS_BA + 4,
               PS_ALL = PS_BV + 4;
-constexpr int NB = 2;                            // boards per wave per batch (unrolled)
+#ifndef G2048_URM_NB
+#define G2048_URM_NB 2
+#endif
+constexpr int NB = G2048_URM_NB;                 // boards per wave per batch (unrolled)
 }  // namespace mk
 
 struct UrmW {  // device pointers (see g2048_urm_weights)
@@ -719,7 +763,7 @@ __device__ __forceinline__ void rms_update(f32x4 (&x)[4], const f32x4 (&y)[4], c
         for (int i = 0; i < 4; i++) x[ct][i] = x[ct][i] * r + (add_emb ? emb[ct][i] : 0.0f);
 }
 
-template <bool kBf16Obs>
+template <bool kBf16Obs, bool kDrop>
 __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__restrict__ obs, UrmW W,
                                                                   float *__restrict__ logits,
                                                                   float *__restrict__ value, int64_t n) {
@@ -745,7 +789,7 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
     const int64_t per_batch = (int64_t)mk::WAVES * mk::NB;
     const int64_t batches = (n + per_batch - 1) / per_batch;
     const int apps = W.layers * W.loops;
-    const uint64_t drop_c0 = W.drop.thr ? *W.drop.counter : 0ull;  // attention dropout (training-mode forward)
+    const uint64_t drop_c0 = kDrop ? *W.drop.counter : 0ull;  // attention dropout (training-mode forward)
     for (int e = tid; e < mk::W_BYTES / 16; e += mk::THREADS) reinterpret_cast<uint4 *>(smem)[e] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();  // the parameters and the zeroed padding are read by every wave
     for (int64_t bt = blockIdx.x; bt < batches; bt += gridDim.x) {
@@ -887,7 +931,7 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
                     sum = xsum32(xsum16(sum));
                     const float inv = 1.0f / sum;
                     s16x4 pb;
-                    if (W.drop.thr) {  // wave-uniform; the mask of URMAttentionFn at counter c0 + app
+                    if constexpr (kDrop) {  // the mask of URMAttentionFn at counter c0 + app
                         float km[4];
                         int64_t b = bt * per_batch + wave * mk::NB + nb;
                         b = b < n ? b : n - 1;
@@ -1476,6 +1520,116 @@ __global__ __launch_bounds__(256) void urm_colsum_kernel(const float *__restrict
     out[j] = t;
 }
 
+// Weight gradient of a projection for autograd training (the URM Functions' backward and any
+// y = x W^T of the default GameURM): dW [N, K] = dY^T X over M token rows, dY bf16 [M, N], X bf16
+// [M, K], fp32 result.  The reduction runs over M (1 M rows per minibatch): a block per CU takes a
+// contiguous row range in 64-row chunks staged in LDS (the next chunk's 16-byte global loads in
+// flight during the MFMAs), both operands read back M-major by the transposing ds_read_b64_tr_b16
+// (the fragment layout of v_mfma_f32_16x16x32_bf16 needs 8 consecutive rows per lane), the output
+// tiles spread over the 8 waves; per-block partials [nblk][N K] summed in a fixed order by
+// urm_colsum_kernel -- deterministic.  (A library GEMM with K = 1 M and N, K <= 240 runs ~1-2 ms.)
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+constexpr int kWgChunk = 64, kWgMaxT = 8, kWgThreads = 512;
+
+__device__ __forceinline__ int wg_pitch(int cols) {  // bytes; row stride = 8 (mod 32) dwords
+    const int dw = cols / 2;                           // dwords of a row of `cols` bf16
+    return 4 * (dw + ((8 - dw % 32) + 32) % 32);
+}
+
+__device__ __forceinline__ bf16x8 wg_frag(const char *img, int pitch, int m0, int c0, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int r1 = m0 + 8 * g + q;
+    const char *a1 = img + r1 * pitch + (c0 + 4 * p) * 2;
+    const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)a1);
+    const s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(a1 + 4 * pitch));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(t1, t2, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+__global__ __launch_bounds__(kWgThreads) void urm_wgrad_kernel(const uint16_t *__restrict__ dy,
+                                                               const uint16_t *__restrict__ x, int64_t M, int N,
+                                                               int K, int Kp, int64_t rows_per_blk,
+                                                               float *__restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int pn = wg_pitch(N), pk = wg_pitch(Kp);
+    char *sY = smem, *sX = smem + kWgChunk * pn;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int NT = N / 16, KT = Kp / 16, T = NT * KT;
+    const int64_t m_beg = (int64_t)blockIdx.x * rows_per_blk;
+    const int64_t m_end = m_beg + rows_per_blk < M ? m_beg + rows_per_blk : M;
+    // zero the X image's K padding columns once (Kp > K); chunk stores never touch them
+    for (int e = tid; e < kWgChunk * (Kp - K); e += kWgThreads) {
+        const int r = e / (Kp - K), c = K + e % (Kp - K);
+        reinterpret_cast<uint16_t *>(sX + r * pk)[c] = 0;
+    }
+    const int yq = N / 8, xq = K / 8;  // 16-byte pieces per row (N % 8 == K % 8 == 0)
+    const int per_chunk = kWgChunk * (yq + xq);
+    constexpr int kMaxPer = 8;  // pieces per thread per chunk: 64 x (240 + 120) / 8 / 512 < 6
+    uint4 v[kMaxPer];
+    auto load = [&](int64_t m0) {
+#pragma unroll
+        for (int u = 0; u < kMaxPer; u++) {
+            const int e = tid + u * kWgThreads;
+            uint4 w = make_uint4(0u, 0u, 0u, 0u);
+            if (e < per_chunk) {
+                const bool isy = e < kWgChunk * yq;
+                const int e2 = isy ? e : e - kWgChunk * yq, q = isy ? yq : xq;
+                const int r = e2 / q, c8 = e2 - r * q;
+                if (m0 + r < m_end)
+                    w = isy ? reinterpret_cast<const uint4 *>(dy + (m0 + r) * N)[c8]
+                            : reinterpret_cast<const uint4 *>(x + (m0 + r) * K)[c8];
+            }
+            v[u] = w;
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int u = 0; u < kMaxPer; u++) {
+            const int e = tid + u * kWgThreads;
+            if (e < per_chunk) {
+                const bool isy = e < kWgChunk * yq;
+                const int e2 = isy ? e : e - kWgChunk * yq, q = isy ? yq : xq;
+                const int r = e2 / q, c8 = e2 - r * q;
+                *reinterpret_cast<uint4 *>((isy ? sY + r * pn : sX + r * pk) + 16 * c8) = v[u];
+            }
+        }
+    };
+    f32x4 acc[kWgMaxT];
+#pragma unroll
+    for (int j = 0; j < kWgMaxT; j++) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (m_beg < m_end) load(m_beg);
+    for (int64_t m0 = m_beg; m0 < m_end; m0 += kWgChunk) {
+        __syncthreads();  // the previous chunk's fragment reads are done
+        store();
+        __syncthreads();
+        if (m0 + kWgChunk < m_end) load(m0 + kWgChunk);  // in flight during the MFMAs
+#pragma unroll
+        for (int ks = 0; ks < kWgChunk; ks += 32) {
+#pragma unroll
+            for (int j = 0; j < kWgMaxT; j++) {
+                int t = wave + 8 * j;
+                t = t < T ? t : T - 1;  // duplicates are computed but never stored (no divergent MFMA)
+                const int ti = t / KT, tk = t - ti * KT;
+                const bf16x8 fa = wg_frag(sY, pn, ks, 16 * ti, lane);
+                const bf16x8 fb = wg_frag(sX, pk, ks, 16 * tk, lane);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[j], 0, 0, 0);
+            }
+        }
+    }
+    // lane: acc[j][r] = dW[16 ti + 4 (lane >> 4) + r][16 tk + (lane & 15)]
+    float *pp = part + (int64_t)blockIdx.x * N * K;
+#pragma unroll
+    for (int j = 0; j < kWgMaxT; j++) {
+        const int t = wave + 8 * j;
+        if (t >= T) break;
+        const int ti = t / KT, tk = t - ti * KT;
+        const int col = 16 * tk + (lane & 15);
+        if (col < K) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) pp[(16 * ti + 4 * (lane >> 4) + r) * K + col] = acc[j][r];
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1676,6 +1830,36 @@ int g2048_urm_stem_bwd(g2048_stream_t stream, const void *obs, int32_t obs_dtype
     return launch_status();
 }
 
+static int wgrad_blocks(int64_t m) {
+    const int64_t chunks = (m + kWgChunk - 1) / kWgChunk;
+    return (int)(chunks < 256 ? chunks : 256);
+}
+
+size_t g2048_urm_wgrad_partials(int64_t m, int32_t n, int32_t k) {
+    if (m <= 0 || n <= 0 || k <= 0) return 0;
+    return (size_t)wgrad_blocks(m) * n * k;
+}
+
+int g2048_urm_wgrad(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x, float *dw, float *partials,
+                    int64_t m, int32_t n, int32_t k) {
+    if (m <= 0 || n <= 0 || k <= 0 || n % 16 || k % 8 || n > 256 || k > 256 ||
+        (n / 16) * ((k + 15) / 16) > kWgMaxT * (kWgThreads / 64))
+        return G2048_EINVAL;
+    if (!dy || !x || !dw || !partials || ((uintptr_t)dy | (uintptr_t)x) % 16) return G2048_EINVAL;
+    const int nblk = wgrad_blocks(m);
+    int64_t rows = (m + nblk - 1) / nblk;
+    rows = (rows + kWgChunk - 1) / kWgChunk * kWgChunk;
+    const int kp = (k + 15) / 16 * 16;
+    auto pitch = [](int cols) { const int dw = cols / 2; return 4 * (dw + ((8 - dw % 32) + 32) % 32); };
+    const size_t lds = (size_t)kWgChunk * (pitch(n) + pitch(kp));
+    const hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(urm_wgrad_kernel, dim3(nblk), dim3(kWgThreads), lds, s, dy, x, m, (int)n, (int)k, kp, rows,
+                       partials);
+    hipLaunchKernelGGL(urm_colsum_kernel, dim3((unsigned)((n * k + 15) / 16)), dim3(256), 0, s, partials, nblk,
+                       (int)(n * k), dw);
+    return launch_status();
+}
+
 int g2048_urm_residual_rms(g2048_stream_t stream, float *x, const uint16_t *y, const float *emb, uint16_t *xb,
                            int64_t rows, int32_t h, float eps) {
     if (rows < 0 || !h_ok(h)) return G2048_EINVAL;
@@ -1723,7 +1907,8 @@ int g2048_urm_pool_heads(g2048_stream_t stream, const float *x, const float *wa,
 
 
 int g2048_urm_linear_supported(int32_t epilogue, int32_t k, int32_t n, int32_t inter) {
-    if (epilogue < 0 || epilogue > 2 || k <= 0 || k % 4 || n <= 0 || n % 4 || (epilogue == 2 && (inter <= 0 || inter % 4)))
+    if (epilogue < 0 || epilogue > 3 || k <= 0 || k % 4 || n <= 0 || n % 4 ||
+        (epilogue >= 2 && (inter <= 0 || inter % 4)))
         return 0;
     return dispatch_lin(nullptr, epilogue, nullptr, nullptr, 0, k, n, inter, nullptr, nullptr, nullptr, nullptr, 0.0f,
                         nullptr, nullptr, true) == G2048_OK ? 1 : 0;
@@ -1755,6 +1940,17 @@ int g2048_urm_linear_swiglu(g2048_stream_t stream, const uint16_t *in, const uin
                         conv_w, conv_b, false);
 }
 
+int g2048_urm_linear_swiglu_train(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *conv_w,
+                                  const float *conv_b, uint16_t *gu, uint16_t *act, int64_t rows, int32_t h,
+                                  int32_t inter) {
+    if (rows < 0 || rows % 16 || !g2048_urm_linear_supported(3, h, 2 * inter, inter)) return G2048_EINVAL;
+    if (rows == 0) return G2048_OK;
+    if (!in || !w || !conv_w || !conv_b || !gu || !act || ((uintptr_t)conv_w | (uintptr_t)conv_b) % 16 ||
+        ((uintptr_t)gu | (uintptr_t)act) % 8)
+        return G2048_EINVAL;
+    return dispatch_lin((hipStream_t)stream, 3, in, w, rows, h, 2 * inter, inter, act, nullptr, nullptr, gu, 0.0f,
+                        conv_w, conv_b, false);
+}
 
 int g2048_urm_forward_supported(int32_t hidden, int32_t heads, int32_t inter, int32_t num_layers, int32_t conv_kernel) {
     return hidden == mk::H && heads == 4 && inter == mk::INTER && (num_layers == 1 || num_layers == 2) &&
@@ -1797,12 +1993,15 @@ int g2048_urm_forward_drop(g2048_stream_t stream, const g2048_urm_weights *w, co
     int64_t grid = (n + per_batch - 1) / per_batch;
     grid = grid > 256 ? 256 : grid;  // one block per CU: the layer's weights fill most of the LDS
     const size_t lds = (size_t)mk::W_BYTES + (size_t)mk::WAVES * mk::TILE_BYTES + (size_t)mk::PS_ALL * 4;
-    if (obs_dtype == 1)
-        hipLaunchKernelGGL(urm_forward_kernel<true>, dim3((unsigned)grid), dim3(mk::THREADS), lds, (hipStream_t)stream,
-                           obs, a, logits, value, n);
-    else
-        hipLaunchKernelGGL(urm_forward_kernel<false>, dim3((unsigned)grid), dim3(mk::THREADS), lds, (hipStream_t)stream,
-                           obs, a, logits, value, n);
+    const hipStream_t s = (hipStream_t)stream;
+    const dim3 gd((unsigned)grid), bk(mk::THREADS);
+    if (drop.thr) {  // the training-mode variant carries the Philox mask code; inference does not
+        if (obs_dtype == 1) hipLaunchKernelGGL((urm_forward_kernel<true, true>), gd, bk, lds, s, obs, a, logits, value, n);
+        else hipLaunchKernelGGL((urm_forward_kernel<false, true>), gd, bk, lds, s, obs, a, logits, value, n);
+    } else {
+        if (obs_dtype == 1) hipLaunchKernelGGL((urm_forward_kernel<true, false>), gd, bk, lds, s, obs, a, logits, value, n);
+        else hipLaunchKernelGGL((urm_forward_kernel<false, false>), gd, bk, lds, s, obs, a, logits, value, n);
+    }
     return launch_status();
 }
 

@@ -40,7 +40,7 @@ EXPORTED = (
     # include/g2048_urm.h
     "g2048_urm_stem", "g2048_urm_attention", "g2048_urm_residual_rms", "g2048_urm_swiglu_conv",
     "g2048_urm_pool_heads", "g2048_urm_linear_supported", "g2048_urm_linear", "g2048_urm_linear_rms",
-    "g2048_urm_linear_swiglu", "g2048_urm_forward_supported", "g2048_urm_forward",
+    "g2048_urm_linear_swiglu", "g2048_urm_linear_swiglu_train", "g2048_urm_wgrad_partials", "g2048_urm_wgrad", "g2048_urm_forward_supported", "g2048_urm_forward",
 )
 
 
@@ -217,6 +217,9 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_urm_linear": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_linear_rms": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32, ctypes.c_float]),
         "g2048_urm_linear_swiglu": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32]),
+        "g2048_urm_linear_swiglu_train": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32]),
+        "g2048_urm_wgrad_partials": (sz, [i64, i32, i32]),
+        "g2048_urm_wgrad": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32]),
         "g2048_muon_supported": (ctypes.c_int, [i32, i32]),
         "g2048_muon_step": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.POINTER(MuonCfg)]),
         "g2048_grad_sumsq": (ctypes.c_int, [vp, vp, i64, vp]),
@@ -846,6 +849,27 @@ def urm_linear_rms(inp, w, x, emb, xb, eps: float):
                                        _dev(x, torch.float32, "x"), _dev(emb, torch.float32, "emb"),
                                        _dev(xb, torch.bfloat16, "xb"), rows, k, w.shape[0], float(eps)),
            "g2048_urm_linear_rms")
+
+
+def urm_wgrad_partials(m: int, n: int, k: int) -> int:
+    return int(load().g2048_urm_wgrad_partials(m, n, k))
+
+
+def urm_wgrad(dy, x, dw, partials):
+    """dw fp32 [n, k] = dy^T x (g2048_urm_wgrad); dy bf16 [m, n], x bf16 [m, k]."""
+    m, n = dy.shape
+    _check(load().g2048_urm_wgrad(_stream(dy), _dev(dy, torch.bfloat16, "dy"), _dev(x, torch.bfloat16, "x"),
+                                  _dev(dw, torch.float32, "dw"), _dev(partials, torch.float32, "partials"), m, n,
+                                  x.shape[1]), "g2048_urm_wgrad")
+
+
+def urm_linear_swiglu_train(inp, w, conv_w, conv_b, gu, act):
+    rows, h = inp.shape
+    _check(load().g2048_urm_linear_swiglu_train(_stream(inp), _dev(inp, torch.bfloat16, "in"),
+                                                _dev(w, torch.bfloat16, "w"), _dev(conv_w, torch.float32, "conv_w"),
+                                                _dev(conv_b, torch.float32, "conv_b"), _dev(gu, torch.bfloat16, "gu"),
+                                                _dev(act, torch.bfloat16, "act"), rows, h, act.shape[1]),
+           "g2048_urm_linear_swiglu_train")
 
 
 def urm_linear_swiglu(inp, w, conv_w, conv_b, out):

@@ -359,6 +359,100 @@ class SwiGLUConvFn(torch.autograd.Function):
         return dgu, dw.to(ctx.w_dtype), db.to(ctx.b_dtype)
 
 
+def _wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """dW fp32 [n, k] = dy^T x over the token rows (g2048_urm_wgrad, deterministic)."""
+    m, n = dy.shape
+    k = x.shape[1]
+    dw = torch.empty(n, k, dtype=torch.float32, device=dy.device)
+    part = torch.empty(L.urm_wgrad_partials(m, n, k), dtype=torch.float32, device=dy.device)
+    L.urm_wgrad(dy.contiguous(), x.contiguous(), dw, part)
+    return dw
+
+
+class URMLinearFn(torch.autograd.Function):
+    """A bias-free projection y = x W^T of the GameURM blocks (qkv_proj, o_proj, down_proj) under bf16
+    autocast: forward and input gradient are the same bf16 GEMMs autocast runs, the weight gradient
+    (a reduction over 16 n token rows) is g2048_urm_wgrad instead of a library GEMM with K = 16 n.
+    x [rows, k] (bf16 or fp32: cast like autocast), w [n, k] -> y bf16 [rows, n]."""
+
+    @staticmethod
+    def forward(ctx, x: torch.Tensor, w: torch.Tensor):
+        xb = x.to(torch.bfloat16).contiguous()
+        wb = w.detach().to(torch.bfloat16)
+        ctx.save_for_backward(xb, wb)
+        ctx.dtypes = (x.dtype, w.dtype)
+        return torch.mm(xb, wb.t())
+
+    @staticmethod
+    def backward(ctx, dy: torch.Tensor):
+        xb, wb = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = torch.mm(dy, wb) if ctx.needs_input_grad[0] else None
+        dW = _wgrad(dy, xb).to(ctx.dtypes[1])
+        return (None if dx is None else dx.to(ctx.dtypes[0])), dW
+
+
+def linear_supported(lin, x: torch.Tensor) -> bool:
+    """URMLinearFn applies: bf16 autocast on the GPU, no bias, g2048_urm_wgrad's shapes."""
+    n, k = lin.weight.shape
+    return (x.is_cuda and lin.bias is None and x.shape[-1] == k and n % 16 == 0 and k % 8 == 0 and n <= 256
+            and k <= 256 and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+
+
+def project(lin, x: torch.Tensor) -> torch.Tensor:
+    """lin(x) through URMLinearFn when it applies (any leading shape), else the module."""
+    if linear_supported(lin, x):
+        return URMLinearFn.apply(x.reshape(-1, x.shape[-1]), lin.weight).view(*x.shape[:-1], lin.weight.shape[0])
+    return lin(x)
+
+
+class GateUpSwiGLUFn(torch.autograd.Function):
+    """gate_up_proj + SwiGLU + kernel-2 depthwise conv + SiLU of GameConvSwiGLU (game.py:1264-1276)
+    under bf16 autocast, for autograd training on the device: ONE forward kernel
+    (g2048_urm_linear_swiglu_train: the projection on MFMA with the SwiGLU-conv epilogue, gu stored
+    once for the backward) instead of a library GEMM writing gu and a SwiGLU kernel reading it back;
+    backward = g2048_urm_swiglu_conv_bwd + the projection's two bf16 GEMMs.
+    x [rows, h] (bf16 or fp32: cast like autocast), w [2 inter, h], cw [inter, 2], cb [inter]."""
+
+    @staticmethod
+    def forward(ctx, x: torch.Tensor, w: torch.Tensor, cw: torch.Tensor, cb: torch.Tensor):
+        xb = x.to(torch.bfloat16).contiguous()
+        wb = w.detach().to(torch.bfloat16).contiguous()
+        # fresh fp32 copies: the kernel reads the conv parameters as 16-byte vectors
+        cwf = cw.detach().to(torch.float32, copy=True).contiguous()
+        cbf = cb.detach().to(torch.float32, copy=True).contiguous()
+        inter = w.shape[0] // 2
+        gu = torch.empty(xb.shape[0], 2 * inter, dtype=torch.bfloat16, device=x.device)
+        act = torch.empty(xb.shape[0], inter, dtype=torch.bfloat16, device=x.device)
+        L.urm_linear_swiglu_train(xb, wb, cwf, cbf, gu, act)
+        ctx.save_for_backward(xb, wb, gu, cwf, cbf)
+        ctx.dtypes = (x.dtype, w.dtype, cw.dtype, cb.dtype)
+        return act
+
+    @staticmethod
+    def backward(ctx, dact: torch.Tensor):
+        xb, wb, gu, cwf, cbf = ctx.saved_tensors
+        rows, inter = gu.shape[0], gu.shape[1] // 2
+        dgu = torch.empty_like(gu)
+        dw = torch.empty(inter, 2, dtype=torch.float32, device=gu.device)
+        db = torch.empty(inter, dtype=torch.float32, device=gu.device)
+        part = torch.empty(L.urm_swiglu_conv_partials(rows // 16, inter), dtype=torch.float32, device=gu.device)
+        L.urm_swiglu_conv_bwd(gu, cwf, cbf, dact.to(torch.bfloat16).contiguous(), dgu, dw, db, part)
+        dx = torch.mm(dgu, wb)        # autocast's bf16 input-gradient GEMM
+        dW = _wgrad(dgu, xb)          # the weight gradient on g2048_urm_wgrad (fp32)
+        return dx.to(ctx.dtypes[0]), dW.to(ctx.dtypes[1]), dw.to(ctx.dtypes[2]), db.to(ctx.dtypes[3])
+
+
+def gate_up_swiglu_supported(mlp, x: torch.Tensor) -> bool:
+    """The fused training gate_up + SwiGLU-conv applies: bf16 autocast on the GPU, 16 tokens, conv
+    kernel 2, a bias-free gate_up projection whose shape the fused kernel covers."""
+    h = x.shape[-1]
+    return (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.ndim == 3 and x.shape[1] == 16
+            and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+            and mlp.dwconv.kernel_size[0] == 2 and mlp.gate_up_proj.bias is None
+            and L.urm_linear_supported(3, h, 2 * mlp.inter, mlp.inter))
+
+
 def swiglu_conv_supported(gu: torch.Tensor, seq: int, inter: int, kernel: int) -> bool:
     """The device SwiGLU + conv applies: bf16 gate_up output on the GPU (autocast), 16 tokens,
     conv kernel 2, inter <= 128."""

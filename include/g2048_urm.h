@@ -105,6 +105,14 @@ int g2048_urm_stem_bwd(g2048_stream_t stream, const void *obs, int32_t obs_dtype
                        const float *ln_b, const float *demb, float *grads, float *partials, int64_t n, int32_t h,
                        float eps);
 
+/* Weight gradient of a projection y = x W^T for autograd training: dw fp32 [n, k] = dy^T x over m
+ * rows, dy bf16 [m, n], x bf16 [m, k] (n % 16 == 0, k % 8 == 0, n, k <= 256; the default GameURM's
+ * qkv / o / gate_up / down shapes), deterministic (per-block partials over
+ * g2048_urm_wgrad_partials(m, n, k) floats of scratch, summed in a fixed order). */
+size_t g2048_urm_wgrad_partials(int64_t m, int32_t n, int32_t k);
+int g2048_urm_wgrad(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x, float *dw, float *partials,
+                    int64_t m, int32_t n, int32_t k);
+
 /* Post-norm residual (game.py:1346, 1350 with rms_norm :1223-1229):
  *   x = x + y;  x = x * rsqrt(mean(x^2) + eps)  [+ emb, the next loop's input, game.py:1447];
  *   xb = bf16(x).
@@ -139,6 +147,15 @@ int g2048_urm_linear_rms(g2048_stream_t stream, const uint16_t *in, const uint16
                          uint16_t *xb, int64_t rows, int32_t k, int32_t h, float eps);
 int g2048_urm_linear_swiglu(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *conv_w,
                             const float *conv_b, uint16_t *out, int64_t rows, int32_t h, int32_t inter);
+
+/* Training variant of g2048_urm_linear_swiglu (epilogue 3 of g2048_urm_linear_supported) for the
+ * autograd GateUpSwiGLUFn: also stores gu = bf16(x W_gu^T) [rows, 2 inter] (gate | up: the backward's
+ * input) and computes act from those bf16 values with g2048_urm_swiglu_conv_fwd's arithmetic, so the
+ * result equals gate_up Linear (autocast bf16) + g2048_urm_swiglu_conv_fwd up to the GEMM's fp32
+ * summation order.  in bf16 [rows, h], w bf16 [2 inter, h], conv_w fp32 [inter][2], conv_b [inter]. */
+int g2048_urm_linear_swiglu_train(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *conv_w,
+                                  const float *conv_b, uint16_t *gu, uint16_t *act, int64_t rows, int32_t h,
+                                  int32_t inter);
 
 /* The whole forward in one persistent kernel (the default GameURMConfig: hidden 64, 4 heads,
  * inter 120, conv kernel 2, 1 or 2 layers, any loop count): obs [n, 48] (fp32 / bf16) -> logits
