@@ -280,9 +280,12 @@ class GameURM(nn.Module):
         """The reference's GameURM has no parameter groups (its trainer refuses URM, train.py:1523-1532);
         these follow GameMLP's split with Muon taking only the 2-D Linear weights: the depthwise conv
         kernels [inter, 1, 2] and init_hidden [1, 16, h] (a direct parameter, not a child module) go
-        to the AdamW group with the norms and biases."""
+        to the AdamW group with the norms and biases.  init_hidden only feeds the no-grad truncated
+        loops when num_truncated_loops >= 1 (game.py:1437-1443), so it never has a gradient and torch's
+        AdamW would skip it every step: it joins the group only when it can get one."""
         o2, o1, v2, v1 = _split_param_groups(self, value_lr, other_lr)
-        o1["params"] = [p for p in o2["params"] if p.ndim != 2] + o1["params"] + [self.init_hidden]
+        trained = [self.init_hidden] if self.config.num_truncated_loops == 0 else []
+        o1["params"] = [p for p in o2["params"] if p.ndim != 2] + o1["params"] + trained
         o2["params"] = [p for p in o2["params"] if p.ndim == 2]
         return [o2, o1, v2, v1]
 

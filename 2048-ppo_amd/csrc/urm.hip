@@ -1835,6 +1835,11 @@ static int wgrad_blocks(int64_t m) {
     return (int)(chunks < 256 ? chunks : 256);
 }
 
+int g2048_urm_wgrad_supported(int32_t n, int32_t k) {
+    return n > 0 && k > 0 && n % 16 == 0 && k % 8 == 0 && n <= 256 && k <= 256 &&
+           (n / 16) * ((k + 15) / 16) <= kWgMaxT * (kWgThreads / 64);
+}
+
 size_t g2048_urm_wgrad_partials(int64_t m, int32_t n, int32_t k) {
     if (m <= 0 || n <= 0 || k <= 0) return 0;
     return (size_t)wgrad_blocks(m) * n * k;
@@ -1842,9 +1847,7 @@ size_t g2048_urm_wgrad_partials(int64_t m, int32_t n, int32_t k) {
 
 int g2048_urm_wgrad(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x, float *dw, float *partials,
                     int64_t m, int32_t n, int32_t k) {
-    if (m <= 0 || n <= 0 || k <= 0 || n % 16 || k % 8 || n > 256 || k > 256 ||
-        (n / 16) * ((k + 15) / 16) > kWgMaxT * (kWgThreads / 64))
-        return G2048_EINVAL;
+    if (m <= 0 || !g2048_urm_wgrad_supported(n, k)) return G2048_EINVAL;
     if (!dy || !x || !dw || !partials || ((uintptr_t)dy | (uintptr_t)x) % 16) return G2048_EINVAL;
     const int nblk = wgrad_blocks(m);
     int64_t rows = (m + nblk - 1) / nblk;

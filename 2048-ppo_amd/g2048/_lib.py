@@ -40,7 +40,7 @@ EXPORTED = (
     # include/g2048_urm.h
     "g2048_urm_stem", "g2048_urm_attention", "g2048_urm_residual_rms", "g2048_urm_swiglu_conv",
     "g2048_urm_pool_heads", "g2048_urm_linear_supported", "g2048_urm_linear", "g2048_urm_linear_rms",
-    "g2048_urm_linear_swiglu", "g2048_urm_linear_swiglu_train", "g2048_urm_wgrad_partials", "g2048_urm_wgrad", "g2048_urm_forward_supported", "g2048_urm_forward",
+    "g2048_urm_linear_swiglu", "g2048_urm_linear_swiglu_train", "g2048_urm_wgrad_supported", "g2048_urm_wgrad_partials", "g2048_urm_wgrad", "g2048_urm_forward_supported", "g2048_urm_forward",
 )
 
 
@@ -218,6 +218,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_urm_linear_rms": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32, ctypes.c_float]),
         "g2048_urm_linear_swiglu": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_linear_swiglu_train": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32]),
+        "g2048_urm_wgrad_supported": (ctypes.c_int, [i32, i32]),
         "g2048_urm_wgrad_partials": (sz, [i64, i32, i32]),
         "g2048_urm_wgrad": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32]),
         "g2048_muon_supported": (ctypes.c_int, [i32, i32]),
@@ -849,6 +850,11 @@ def urm_linear_rms(inp, w, x, emb, xb, eps: float):
                                        _dev(x, torch.float32, "x"), _dev(emb, torch.float32, "emb"),
                                        _dev(xb, torch.bfloat16, "xb"), rows, k, w.shape[0], float(eps)),
            "g2048_urm_linear_rms")
+
+
+def urm_wgrad_supported(n: int, k: int) -> bool:
+    """g2048_urm_wgrad covers dw [n, k] (the projection shapes of the URM training Functions)."""
+    return bool(load().g2048_urm_wgrad_supported(n, k))
 
 
 def urm_wgrad_partials(m: int, n: int, k: int) -> int:

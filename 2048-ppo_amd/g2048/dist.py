@@ -68,9 +68,31 @@ def trim_rows(data: dict, k: int, n_real: int | None = None, generator: torch.Ge
     return {key: v.index_select(0, keep) for key, v in data.items()}
 
 
+def _host_staged() -> bool:
+    """gloo on device tensors (the CPU-backend tests of the device path: RCCL refuses two ranks on
+    one GPU) goes through a host copy; RCCL ("nccl") takes the device tensor itself."""
+    return dist.get_backend() == "gloo"
+
+
 def allreduce_sum_(t: torch.Tensor) -> torch.Tensor:
     if dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(t)
+        if t.is_cuda and _host_staged():
+            h = t.cpu()
+            dist.all_reduce(h)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t)
+    return t
+
+
+def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        if t.is_cuda and _host_staged():
+            h = t.cpu()
+            dist.broadcast(h, src)
+            t.copy_(h)
+        else:
+            dist.broadcast(t, src)
     return t
 
 
@@ -101,7 +123,7 @@ class GradBucket:
 
     def allreduce_mean(self):
         if dist.is_initialized() and dist.get_world_size() > 1:
-            dist.all_reduce(self.flat)
+            allreduce_sum_(self.flat)
             self.flat.div_(dist.get_world_size())
 
     def clip_(self, max_norm: float) -> torch.Tensor:

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import math
 import time
+import warnings
 from dataclasses import dataclass, field
 from pathlib import Path
 
@@ -21,7 +22,7 @@ import torch
 from . import _lib as L
 from . import fastmlp
 from .advantage import RewardWeights, RTGTracker
-from .dist import GradBucket, allreduce_sum_, equal_rows, world
+from .dist import GradBucket, allreduce_sum_, broadcast_, equal_rows, world
 from .optim import FusedMuonAdamW, MuonAdamW, ScheduledMuonAdamW, build_optimizer
 from .ppo import PPOConfig, PPOUpdater
 from .rollout import Rollout, make_policy
@@ -95,7 +96,7 @@ class VecTrainer:
         self.model = model.to(self.dev)
         if self.world > 1:  # identical initial replicas
             for p in self.model.parameters():
-                torch.distributed.broadcast(p.data, 0)
+                broadcast_(p.data, 0)
         if cfg.graph_update:
             opt = None
             if cfg.fused_update and self.dev.type == "cuda":
@@ -146,6 +147,38 @@ class VecTrainer:
         self._chunk_graphs = {}
         self.profile = False
         self.timings: dict[str, float] = {}
+        self.paths, self.fallbacks = self._fast_paths()
+        for msg in self.fallbacks:
+            warnings.warn(f"g2048: {msg}", stacklevel=2)
+
+    def _fast_paths(self) -> tuple[dict, list[str]]:
+        """Which kernel path each phase runs on, and a message per GameMLP phase that fell back from
+        its fused kernel (shapes the kernels do not cover, e.g. -l 3 or -h 256): the CLI prints them
+        and bench.py puts `paths` in its JSON line, so a fallback is never silent."""
+        import agent
+        pol, up = self.policy, self.ppo
+        mlp = isinstance(self.model, agent.GameMLP)
+        fused_up = isinstance(up, fastmlp.FusedPPOUpdater)
+        inner = getattr(self.opt, "opt", self.opt)
+        paths = {"policy": type(pol).__name__,
+                 "rollout": "policy_rollout_kernel" if getattr(pol, "fused_rollout", False) else "per-step kernels",
+                 "update": type(up).__name__,
+                 "update_forward": ("mlp_fwd kernels" if fused_up and all(up.mf_ok)
+                                    else "hipBLASLt + ln_act_fwd" if fused_up else "autograd"),
+                 "optimizer": "fused Muon/AdamW kernels" if getattr(inner, "supported", False) else type(inner).__name__}
+        fb = []
+        if mlp and self.dev.type == "cuda":
+            h, nl = self.model.config.hidden_dim, len(self.model.backbone)
+            if not getattr(pol, "fused_rollout", False):
+                fb.append(f"rollout: no fused policy_rollout_kernel for GameMLP h={h}, {nl} blocks "
+                          f"({paths['policy']} per step)")
+            if self.cfg.amp and self.cfg.fused_update and not fused_up:
+                fb.append(f"update: FusedPPOUpdater does not cover h={h}; autograd PPOUpdater")
+            elif fused_up and not all(up.mf_ok):
+                fb.append(f"update forward: no MFMA layer kernel for h={h}; hipBLASLt GEMM + ln_act_fwd")
+            if self.cfg.graph_update and self.cfg.fused_update and not getattr(inner, "supported", False):
+                fb.append(f"optimizer: the fused Muon kernel does not cover h={h}; torch-op Newton-Schulz")
+        return paths, fb
 
     # ------------------------------------------------------------------ rollout ---------------
     def _encode(self, boards: torch.Tensor) -> torch.Tensor:

@@ -263,6 +263,9 @@ def train_nograd_forward(model, obs: torch.Tensor):
     if not (obs.is_cuda and obs.dtype in (torch.float32, torch.bfloat16) and obs.ndim == 2 and obs.shape[1] == 48):
         return None
     c = model.config
+    # the kernel rounds like bf16 autocast: an fp32 (--fp32) update keeps the module's own forward
+    if not (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return None
     if not (URMPolicy.supports(model) and 0.0 <= c.dropout < 1.0
             and L.urm_forward_supported(c.hidden_dim, c.num_heads, model.layers[0].mlp.inter, len(model.layers),
                                         c.conv_kernel)):
@@ -395,8 +398,8 @@ class URMLinearFn(torch.autograd.Function):
 def linear_supported(lin, x: torch.Tensor) -> bool:
     """URMLinearFn applies: bf16 autocast on the GPU, no bias, g2048_urm_wgrad's shapes."""
     n, k = lin.weight.shape
-    return (x.is_cuda and lin.bias is None and x.shape[-1] == k and n % 16 == 0 and k % 8 == 0 and n <= 256
-            and k <= 256 and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+    return (x.is_cuda and lin.bias is None and x.shape[-1] == k and L.urm_wgrad_supported(n, k)
+            and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
 
 
 def project(lin, x: torch.Tensor) -> torch.Tensor:
@@ -450,7 +453,7 @@ def gate_up_swiglu_supported(mlp, x: torch.Tensor) -> bool:
     return (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.ndim == 3 and x.shape[1] == 16
             and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
             and mlp.dwconv.kernel_size[0] == 2 and mlp.gate_up_proj.bias is None
-            and L.urm_linear_supported(3, h, 2 * mlp.inter, mlp.inter))
+            and L.urm_linear_supported(3, h, 2 * mlp.inter, mlp.inter) and L.urm_wgrad_supported(2 * mlp.inter, h))
 
 
 def swiglu_conv_supported(gu: torch.Tensor, seq: int, inter: int, kernel: int) -> bool:

@@ -279,6 +279,9 @@ def train(
     logger.print(f"Creating {name} model (hidden={hidden_size}, layers={num_layers}{extra}); "
                  f"{num_episodes} envs/GPU x {ws}")
     tr = VecTrainer(cfg, device)
+    logger.print("Kernel paths: " + ", ".join(f"{k}={v}" for k, v in tr.paths.items()))
+    for msg in tr.fallbacks:
+        logger.print(f"Fallback: {msg}")
     best_eval = 0.0
     highest = 0
     from tqdm import tqdm
@@ -320,15 +323,24 @@ def train(
     logger.close()
 
 
+def load_checkpoint_model(ck) -> torch.nn.Module:
+    """The policy of a best_model.pt (train.py:1893-1901 layout; a bare state_dict loads as GameMLP):
+    GameURM when the saved config carries URM fields (num_loops / num_heads), else GameMLP."""
+    cfg = ck["config"] if isinstance(ck, dict) and "config" in ck else {}
+    sd = ck["model_state_dict"] if isinstance(ck, dict) and "model_state_dict" in ck else ck
+    if "num_loops" in cfg or "num_heads" in cfg:
+        model = GameURM(GameURMConfig(**cfg))
+    else:
+        model = GameMLP(MLPConfig(**cfg))
+    model.load_state_dict(sd)
+    return model
+
+
 @app.command()
 def evaluate(model_path: Path = typer.Argument(...), games: int = typer.Option(100, "--games", "-g")):
     """Evaluate a checkpoint on `games` seeded games (game i spawns like random.seed(i))."""
     from g2048.episodes import play_games
-    ck = torch.load(model_path, map_location="cpu", weights_only=True)
-    cfg = MLPConfig(**ck["config"]) if isinstance(ck, dict) and "config" in ck else MLPConfig()
-    sd = ck["model_state_dict"] if isinstance(ck, dict) and "model_state_dict" in ck else ck
-    model = GameMLP(cfg)
-    model.load_state_dict(sd)
+    model = load_checkpoint_model(torch.load(model_path, map_location="cpu", weights_only=True))
     dev = torch.device("cuda", 0)
     res = play_games(model.to(dev).eval(), games, None, dev, seeds=list(range(games)), record=False)
     s, tiles = res["scores"], res["max_tiles"]
@@ -349,10 +361,7 @@ def export_demo_cmd(model_path: Path = typer.Option("checkpoints/best_model.pt",
     if not model_path.exists():
         typer.echo(f"Error: Model checkpoint not found at {model_path}")
         raise typer.Exit(1)
-    ck = torch.load(model_path, map_location="cpu", weights_only=True)
-    cfg = MLPConfig(**ck["config"]) if isinstance(ck, dict) and "config" in ck else MLPConfig()
-    model = GameMLP(cfg)
-    model.load_state_dict(ck["model_state_dict"] if "model_state_dict" in ck else ck)
+    model = load_checkpoint_model(torch.load(model_path, map_location="cpu", weights_only=True))
     model.eval()
     dev = torch.device("cuda", 0)
     model = model.to(dev)

@@ -106,9 +106,12 @@ int g2048_urm_stem_bwd(g2048_stream_t stream, const void *obs, int32_t obs_dtype
                        float eps);
 
 /* Weight gradient of a projection y = x W^T for autograd training: dw fp32 [n, k] = dy^T x over m
- * rows, dy bf16 [m, n], x bf16 [m, k] (n % 16 == 0, k % 8 == 0, n, k <= 256; the default GameURM's
- * qkv / o / gate_up / down shapes), deterministic (per-block partials over
- * g2048_urm_wgrad_partials(m, n, k) floats of scratch, summed in a fixed order). */
+ * rows, dy bf16 [m, n], x bf16 [m, k] (the shapes g2048_urm_wgrad_supported(n, k) accepts: n % 16 == 0,
+ * k % 8 == 0, n, k <= 256 and at most 64 output tiles of 16 x 16 -- the default GameURM's qkv / o /
+ * gate_up / down), deterministic (per-block partials over g2048_urm_wgrad_partials(m, n, k) floats of
+ * scratch, summed in a fixed order).  Replaces the K = 16 n weight-gradient GEMMs of autocast's
+ * nn.Linear backward for GameURMAttention / GameConvSwiGLU (game.py:1264-1352). */
+int g2048_urm_wgrad_supported(int32_t n, int32_t k);
 size_t g2048_urm_wgrad_partials(int64_t m, int32_t n, int32_t k);
 int g2048_urm_wgrad(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x, float *dw, float *partials,
                     int64_t m, int32_t n, int32_t k);

@@ -59,3 +59,14 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.PPOBatch) == 56 and _lib.PPOBatch.rows.offset == 48
     assert ctypes.sizeof(_lib.Dy) == 64 and _lib.Dy.dz.offset == 40 and _lib.DY_MAX_P == 4
     assert ctypes.sizeof(_lib.ColsumJob) == 88 and _lib.ColsumJob.len.offset == 64
+
+
+def test_urm_wgrad_supported_shapes():
+    """The URM training Functions pick g2048_urm_wgrad only for shapes it accepts (<= 64 output
+    tiles): hidden 64 (default) qkv / o / gate_up / down yes; hidden 80 qkv (240 x 80 = 75 tiles) and
+    hidden 192 o_proj (144 tiles) fall back to autocast's nn.Linear."""
+    from g2048 import _lib
+    for n, k in ((192, 64), (64, 64), (240, 64), (64, 120)):
+        assert _lib.urm_wgrad_supported(n, k), (n, k)
+    for n, k in ((240, 80), (192, 192), (256, 256), (8, 64), (64, 60)):
+        assert not _lib.urm_wgrad_supported(n, k), (n, k)

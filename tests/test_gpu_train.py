@@ -421,3 +421,25 @@ def test_augment_kernel_matches_oracle(dev, n, k):
     for a, w, full in zip(got, want, (boards, actions, legal, logp, adv, ret)):
         assert np.array_equal(a[:n], full[:n])
         assert np.array_equal(a[n:c], w)
+
+
+@pytest.mark.parametrize("hidden,layers,want", [(196, 2, []), (196, 3, ["rollout"]),
+                                                (256, 2, ["rollout", "update forward", "optimizer"])])
+def test_trainer_reports_kernel_fallbacks(dev, hidden, layers, want):
+    """A GameMLP shape outside a fused kernel's cover (-l 3: no fused rollout; -h 256: no MFMA layer
+    kernel, no one-block Newton-Schulz) is reported (warning + VecTrainer.fallbacks, printed by the
+    CLI), never silent; the README model (h 196, 2 blocks) runs every fused path."""
+    import warnings
+    from g2048.trainer import TrainConfig, VecTrainer
+    cfg = TrainConfig(steps=2, episodes=64, horizon=8, batch_size=256, hidden=hidden, num_layers=layers,
+                      warmup_steps=0)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        tr = VecTrainer(cfg, dev)
+    got = [m.split(":")[0] for m in tr.fallbacks]
+    assert got == want, tr.fallbacks
+    assert len([x for x in w if "g2048:" in str(x.message)]) == len(want)
+    if not want:
+        assert tr.paths["rollout"] == "policy_rollout_kernel" and tr.paths["update"] == "FusedPPOUpdater"
+    m = tr.train_step(0)
+    assert math.isfinite(m["loss"])

@@ -215,8 +215,9 @@ def test_urm_kernels_reject_bad_arguments(dev):
 @pytest.mark.parametrize("horizon", [16, 0])
 def test_urm_trainer_steps(dev, horizon):
     """VecTrainer with --model-type urm: URMPolicy rollouts, autograd bf16 update with Muon on the
-    2-D weights and AdamW on the rest (incl. init_hidden and the conv kernels); parameters move,
-    metrics finite; fixed-horizon and episodic modes."""
+    2-D weights and AdamW on the rest (the conv kernels; init_hidden only with num_truncated_loops 0:
+    it has no gradient otherwise, and torch's AdamW skips it); parameters move, metrics finite;
+    fixed-horizon and episodic modes."""
     import math
     from g2048.rollout import Rollout  # noqa: F401
     from g2048.trainer import TrainConfig, VecTrainer
@@ -233,7 +234,8 @@ def test_urm_trainer_steps(dev, horizon):
             assert math.isfinite(m[k]), (k, m[k])
         assert m["samples"] > 0
     moved = {k for k, v in tr.model.named_parameters() if not torch.equal(v, before[k])}
-    assert "init_hidden" in moved and "layers.0.attn.qkv_proj.weight" in moved and "layers.1.mlp.dwconv.weight" in moved
+    assert "layers.0.attn.qkv_proj.weight" in moved and "layers.1.mlp.dwconv.weight" in moved
+    assert "init_hidden" not in moved  # num_truncated_loops = 1: no gradient, not in the optimizer
 
 
 @pytest.mark.parametrize("h,inter,rows", [(64, 120, 16 * 4097), (32, 64, 16 * 33)])
@@ -721,3 +723,56 @@ def test_urm_swiglu_conv_fn_matches_autograd(dev, n, inter):
         got, want = got.float().reshape(-1), want.float().reshape(-1)
         assert float(F.cosine_similarity(got, want, dim=0)) >= 0.999, name
         assert float((got - want).abs().max()) <= 0.02 * float(want.abs().max()), name
+
+
+def test_urm_config5_forward_full_shape(dev):
+    """BASELINE config 5's per-GPU shape (65 536 boards of the default GameURM, game.py:1355-1458):
+    the one-launch forward (g2048_urm_forward) against the per-op kernel chain on every board, and
+    against the fp32 module on a 4 096-board subsample with the bounds stated at the top."""
+    import agent
+    from g2048 import _lib as L
+    from g2048.urm import URMPolicy
+    n = 65536
+    torch.manual_seed(55)
+    m = agent.GameURM(agent.GameURMConfig(dropout=0.0)).to(dev).eval()
+    rng = np.random.default_rng(5)
+    boards = rng.integers(0, 15, size=(n, 16)).astype(np.int8)
+    boards[rng.random(boards.shape) < 0.4] = 0
+    obs = torch.empty(n, 48, dtype=torch.bfloat16, device=dev)
+    L.obs_encode(torch.from_numpy(boards).to(dev), obs)
+    pol = URMPolicy(m)
+    assert pol.mega and pol.fused
+    lm, vm = [t.clone() for t in pol(obs)]
+    pol.mega = False
+    lc, vc = [t.clone() for t in pol(obs)]
+    dd = torch.cat([(lm - lc).abs().reshape(-1), (vm - vc).abs().reshape(-1)])
+    print(f"65536 boards, megakernel vs chain: max {dd.max().item():.3g} mean {dd.mean().item():.3g}")
+    assert torch.isfinite(lm).all() and torch.isfinite(vm).all()
+    assert dd.max().item() <= 0.04 and dd.mean().item() <= 2e-3
+    sub = torch.from_numpy(rng.choice(n, 4096, replace=False)).to(dev)
+    with torch.no_grad():
+        ref_l, ref_v = m(obs.index_select(0, sub).float())
+    e = max((lm[sub] - ref_l).abs().max().item(), (vm[sub] - ref_v.view(-1)).abs().max().item())
+    print(f"subsample vs fp32 module: {e:.3g} (max |logit| {ref_l.abs().max().item():.3g})")
+    assert e <= SCALE_REL * ref_l.abs().max().item()
+    _check_emul(lm[sub], vm[sub], m, obs.index_select(0, sub).float(), pol.fused)
+
+
+def test_urm_config5_trainer_step_full_shape(dev):
+    """One --model-type urm train step at config 5's per-GPU shape: 65 536 envs x T = 16, minibatch
+    65 536 (16 minibatches of 1 M token rows), dropout 0.1: finite metrics and every parameter moves
+    (init_hidden gets no gradient with num_truncated_loops >= 1, game.py:1437-1443, and stays)."""
+    import math
+    from g2048.trainer import TrainConfig, VecTrainer
+    from g2048.urm import URMPolicy
+    cfg = TrainConfig(steps=4, episodes=65536, horizon=16, batch_size=65536, hidden=64, model_type="urm",
+                      points=0.1, mono=1.0, rtg_beta=0.99, gamma=0.99, entropy=0.02, critic=0.2, warmup_steps=0)
+    tr = VecTrainer(cfg, dev)
+    assert isinstance(tr.policy, URMPolicy)
+    before = {k: v.detach().clone() for k, v in tr.model.named_parameters()}
+    m = tr.train_step(1)
+    for k in ("loss", "entropy", "grad_norm", "avg_score", "explained_var", "kl_average"):
+        assert math.isfinite(m[k]), (k, m[k])
+    assert m["samples"] == 65536 * 16
+    still = {k for k, v in tr.model.named_parameters() if torch.equal(v, before[k])}
+    assert still == {"init_hidden"}, still

@@ -144,3 +144,34 @@ def test_trim_rows_drops_copies_first_then_random_real_rows():
     assert int(a.max()) >= 45  # not a head/tail slice of the time-major rows
     assert a.tolist() != list(range(30))
     assert trim_rows(data, m, n_real) is data
+
+
+@pytest.mark.parametrize("kind", ["mlp", "urm"])
+def test_checkpoint_reload_picks_model_type(kind, tmp_path):
+    """evaluate / export-demo rebuild the saved policy from best_model.pt's config (train.py:1893-1901
+    layout): a GameURM checkpoint (the trainer's --model-type urm) reloads as GameURM, not GameMLP."""
+    import agent
+    import train
+    torch.manual_seed(0)
+    if kind == "urm":
+        m = agent.GameURM(agent.GameURMConfig(hidden_dim=32, num_heads=2, num_layers=1, num_loops=2))
+    else:
+        m = agent.GameMLP(agent.MLPConfig(hidden_dim=32))
+    torch.save({"model_state_dict": m.state_dict(), "config": m.config.model_dump(), "eval_avg_score": 1.0,
+                "train_step": 3}, tmp_path / "best_model.pt")
+    got = train.load_checkpoint_model(torch.load(tmp_path / "best_model.pt", map_location="cpu", weights_only=True))
+    assert type(got) is type(m)
+    x = torch.rand(5, 48)
+    with torch.no_grad():
+        a, b = m.eval()(x), got.eval()(x)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+def test_urm_optimizer_groups_skip_gradless_init_hidden():
+    """init_hidden feeds only the no-grad truncated loops when num_truncated_loops >= 1 (no gradient:
+    torch's AdamW would skip it), so it is in the AdamW group only with num_truncated_loops = 0."""
+    import agent
+    for trunc, want in ((1, False), (0, True)):
+        m = agent.GameURM(agent.GameURMConfig(hidden_dim=32, num_heads=2, num_truncated_loops=trunc))
+        ids = {id(p) for g in m.get_param_groups(1e-3, 1e-3) for p in g["params"]}
+        assert (id(m.init_hidden) in ids) is want
