@@ -32,6 +32,7 @@
 #include "board.hpp"
 #include "step.hpp"
 #include "ln_row.hpp"
+#include "mlp_tile.hpp"
 #include "../../include/g2048.h"
 #include "../../include/g2048_ppo.h"
 
@@ -39,94 +40,14 @@ using namespace g2048;
 
 namespace {
 
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
+using namespace g2048::tile;
 
 constexpr int kPrThreads = 256;
 constexpr int kPrLdsMax = 163840;
-constexpr int kMaxLayers = 3;  // stem + 2 residual blocks (GameMLP num_layers = 2)
 #ifndef PR_TILES
 #define PR_TILES 2
 #endif
 constexpr int kQ = PR_TILES;  // board tiles (of 16 boards) per MLP pass: accumulators of kQ x NT tiles
-
-// ---------------------------------------------------------------- stem fragment table -------
-// The stem's B fragment of k-step ks for lane group g holds obs features k = 32 ks + 8 g + j
-// (to_model_format order: [exponent, row/3, col/3] per cell).  Per (g, ks): the position features
-// as bf16 constants (exponent slots zero), the up to three exponent cells c0 .. c0+2 (inside board
-// dwords d, d+1; `xsel` gathers their bytes), and per fragment dword a v_perm selector merging the
-// exponents (bf16) into the constants.
-struct StemFrag {
-    uint32_t c[4], sel[4], xsel, d, pad_[2];
-};
-struct StemTable {
-    StemFrag f[4][2];
-    static constexpr uint32_t bf16_rne(float x) {
-        const uint32_t u = __builtin_bit_cast(uint32_t, x);
-        return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
-    }
-    constexpr StemTable() : f{} {
-        constexpr float thirds[4] = {0.0f, 1.0f / 3.0f, 2.0f / 3.0f, 1.0f};
-        for (int g = 0; g < 4; g++)
-            for (int ks = 0; ks < 2; ks++) {
-                StemFrag &e = f[g][ks];
-                int c0 = -1, slot[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
-                uint32_t val[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                for (int j = 0; j < 8; j++) {
-                    const int k = 32 * ks + 8 * g + j, cell = k / 3, kind = k % 3;
-                    if (k >= 48) continue;
-                    if (kind == 0) {
-                        if (c0 < 0) c0 = cell;
-                        slot[j] = cell - c0;  // exponent number 0..2
-                    } else {
-                        val[j] = bf16_rne(thirds[kind == 1 ? (cell >> 2) : (cell & 3)]);
-                    }
-                }
-                const int cc = c0 < 0 ? 0 : c0;
-                const int d = (cc >> 2) < 3 ? (cc >> 2) : 2;
-                e.d = (uint32_t)d;
-                e.xsel = 0x0C0C0C0Cu;
-                for (int s = 0; s < 3; s++) {
-                    const int byte = cc + s - 4 * d;
-                    if (byte < 8) e.xsel = (e.xsel & ~(0xFFu << (8 * s))) | ((uint32_t)byte << (8 * s));
-                }
-                for (int w = 0; w < 4; w++) {
-                    e.c[w] = val[2 * w] | (val[2 * w + 1] << 16);
-                    uint32_t sel = 0;
-                    for (int p = 0; p < 2; p++) {
-                        const int j = 2 * w + p, sl = slot[j];
-                        // exponent s: bf16 in E01 (s = 0: bytes 0,1; s = 1: bytes 2,3) or E2 (bytes
-                        // 0,1) = the v_perm high source (selector 4..7); a constant: bytes of c[w]
-                        const uint32_t b0 = sl < 0 ? (uint32_t)(2 * p) : (uint32_t)(4 + 2 * (sl == 1));
-                        sel |= (b0 | ((b0 + 1u) << 8)) << (16 * p);
-                    }
-                    e.sel[w] = sel;
-                }
-            }
-    }
-};
-__constant__ const StemTable kStem = StemTable();
-
-__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
-    const bf16x2_t v = {(__bf16)a, (__bf16)b};
-    return __builtin_bit_cast(uint32_t, v);
-}
-__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
-__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
-__device__ __forceinline__ bf16x8_t as_frag(const uint4 &v) { return __builtin_bit_cast(bf16x8_t, v); }
-
-// LDS geometry of one block weight image for hidden size h: row pitch P = round_up(h, 8) bf16 in
-// 16-byte granules.  (At h = 196, P = 400 B: the 16 rows of a fragment load hit 2-way bank
-// conflicts; a conflict-free pitch, 544 B, does not fit two images in 160 KiB.)
-__host__ __device__ constexpr int pr_pitch(int h) { return ((2 * ((h + 7) & ~7)) + 15) & ~15; }
-__host__ __device__ constexpr int pr_shift(int, int) { return 0; }
-__host__ __device__ constexpr int pr_wbytes(int h) { return h * pr_pitch(h); }
-__host__ __device__ constexpr int pr_ln_floats(int nt) { return 16 * nt; }  // one affine vector, zero padded
-__host__ __device__ constexpr int pr_lds_bytes(int h, int nt) {
-    return 2 * pr_wbytes(h) + 2 * kMaxLayers * pr_ln_floats(nt) * 4 + 16;
-}
 
 struct PrArgs {
     uint4 *boards;      // [T+1][n][16] int8: row t0 read, rows t0+1 .. t1 written
@@ -165,50 +86,6 @@ __device__ __forceinline__ void debug_act(const PrArgs &a, int l, int64_t board,
         d[f + 2] = bf_lo(act[n].y);
         d[f + 3] = bf_hi(act[n].y);
     }
-}
-
-// --------------------------------------------------------------- layer epilogues --------------
-// g2048_mlp_fwd's epilogue (ppo_update.hip, mlp_fwd_kernel) on one board tile: G = bf16(acc),
-// LayerNorm statistics in the same order (features in tile order, then the xor-16 and xor-32 lane
-// sums), Y = [X +] ReLU(LN(G)) rounded to bf16.  act[n] holds the layer input (residual) on entry
-// and the output on exit; features >= h are zero.
-template <int NT, int h, bool RES>
-__device__ __forceinline__ void ln_epilogue(f32x4_t (&acc)[NT], uint2 (&act)[NT], const float *sgam, const float *sbet,
-                                            int g, float inv_n) {
-    namespace R = lnrow;
-    R::f32x2 v[NT][2];
-    uint2 gb[NT];
-    R::round_g<NT>(acc, v, gb);
-    auto valid = [&](int n) { return 16 * n + 4 * g < h; };  // folds to true except in the last tile
-    float mean, rstd;
-    R::stats<NT>(v, valid, inv_n, mean, rstd);
-#pragma unroll
-    for (int n = 0; n < NT; n++) {
-        const int f0 = 16 * n + 4 * g;
-        const float4 ga = *reinterpret_cast<const float4 *>(sgam + f0);
-        const float4 be = *reinterpret_cast<const float4 *>(sbet + f0);
-        R::f32x2 y0 = R::affine_relu(v[n][0], rstd, R::f32x2{ga.x, ga.y}, R::f32x2{be.x, be.y});
-        R::f32x2 y1 = R::affine_relu(v[n][1], rstd, R::f32x2{ga.z, ga.w}, R::f32x2{be.z, be.w});
-        if (RES) {  // Y = X + ..., the residual being this layer's input
-            y0 = R::f32x2{bf_lo(act[n].x), bf_hi(act[n].x)} + y0;
-            y1 = R::f32x2{bf_lo(act[n].y), bf_hi(act[n].y)} + y1;
-        }
-        act[n] = valid(n) ? make_uint2(pack_bf2(y0.x, y0.y), pack_bf2(y1.x, y1.y)) : make_uint2(0u, 0u);
-    }
-}
-
-// The B fragment of k-step ks (k = 32 ks + 8 g .. + 7 of the board in column c) from the layer
-// output tiles 2 ks and 2 ks + 1 held as "lane g: features 4g .. 4g+3" (see the file comment).
-template <int NT>
-__device__ __forceinline__ uint4 act_frag(const uint2 (&act)[NT], int ks) {
-    const int t0 = 2 * ks, t1 = 2 * ks + 1;
-    const uint32_t a0 = act[t0].x, a1 = act[t0].y;
-    const uint32_t b0 = t1 < NT ? act[t1 < NT ? t1 : 0].x : 0u, b1 = t1 < NT ? act[t1 < NT ? t1 : 0].y : 0u;
-    const auto s0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-    const auto s1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-    const auto f0 = __builtin_amdgcn_permlane16_swap(s0[0], s0[1], false, false);
-    const auto f1 = __builtin_amdgcn_permlane16_swap(s1[0], s1[1], false, false);
-    return make_uint4(f0[0], f1[0], f0[1], f1[1]);
 }
 
 // The sampler of g2048_sample_actions (g2048.hip, sample_kernel; built there with

@@ -1,0 +1,521 @@
+// ppo_fused.hip -- the PPO minibatch's forward passes of GameMLP (model_optimize_step,
+// train.py:414-642; GameMLP.forward, game.py:1145-1220) as ONE persistent launch each:
+//
+//   train pass   boards[idx] -> to_model_format (game.py:92-101) -> stem Linear + LayerNorm + ReLU
+//                -> 2 x ResidualBlock with nn.Dropout (train mode) -> action / value heads
+//                -> masked log-softmax, PPO-clip ratio, clamped-logit entropy, smooth-L1 value loss
+//                   and their gradient dz = dloss / d(logits, value)            (train.py:491-546)
+//   KL pass      the same forward with the updated weights and the second dropout draw -> the
+//                action head -> KL(old || new) per row, summed / maxed           (train.py:578-601)
+//
+// replacing g2048_obs_gather + three g2048_mlp_fwd + g2048_ppo_head_loss (train pass) and two
+// g2048_mlp_fwd + g2048_mlp_fwd_kl (KL pass).  The layers run on the register hand-off of the fused
+// rollout (mlp_tile.hpp): a wave owns 64 minibatch rows = 4 MFMA board tiles, the two h x h block
+// weights sit in LDS, the stem weights and heads come from L1/L2, each layer's output becomes the
+// next layer's B fragment by permlane swaps.  Every layer's epilogue is g2048_mlp_fwd's arithmetic
+// (same MFMA k order from zero, ln_row.hpp, the same dropout keep masks), so the activations, G and
+// the LayerNorm statistics are bitwise those of the per-layer kernels (tests/test_gpu_ppo_fused.py).
+//
+// Heads: one MFMA chain per board tile whose 16-row A operand is the fp32 head matrix [wa; wv]
+// split exactly into three bf16 terms (rows 0-4 hi, 5-9 mid, 10-14 lo: all 24 mantissa bits, so
+// the logits keep the fp32 weights as g2048_ppo_head_loss does); two permlane swap stages turn the
+// four tiles' accumulators into "lane = row" (lane 16 q + c holds all 16 head rows of row 16 q + c
+// of its 64), where the per-row loss / KL runs once per row.
+//
+// The train pass writes what the backward needs: x0 (bf16 obs, the stem weight-gradient operand),
+// per layer G (bf16, pre-norm), H (bf16 output) and mean / rstd, masked logits (for the KL), dz as
+// fp32 [m][8] (the blocks' output gradient source) and as bf16 [m][8] (the head weight-gradient
+// operand: dW_heads = dz^T H2 runs on g2048_wgrad, autocast's bf16 operands), and per block
+// partials [dba 4 | dbv | sum ppo, sum H, sum v] summed by the deferred column sum.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "board.hpp"
+#include "ln_row.hpp"
+#include "mlp_tile.hpp"
+#include "ppo_common.hpp"
+#include "../../include/g2048_ppo.h"
+
+using namespace g2048::tile;
+namespace P = g2048::ppo;
+
+static_assert(sizeof(g2048_mlp_pass_args) == 408 && offsetof(g2048_mlp_pass_args, drop) == 176 &&
+                  offsetof(g2048_mlp_pass_args, partials) == 400,
+              "g2048_mlp_pass_args layout (tests/test_abi.py)");
+
+namespace {
+
+constexpr int kFpThreads = 256;  // 4 waves x 64 rows per block iteration; one block per CU (LDS)
+constexpr int kFpLdsMax = 163840;
+constexpr int kFpQ = 2;          // board tiles per MLP pass (accumulators of kFpQ x NT tiles)
+constexpr int kTrainParts = 8;   // partial floats per block: dba[4], dbv, sum ppo, sum H, sum v
+
+struct FpArgs {
+    const int8_t *boards;
+    int64_t m;
+    P::HeadLossArgs la;            // idx, action, legal, old_logp, adv, ret, beta_dev, rows, critic, clip, inv_m, decouple
+    const uint16_t *w0, *w1, *w2;  // bf16 stem [h][48], blocks [h][h]
+    const float *gamma[kMaxLayers], *beta[kMaxLayers];
+    const float *ba, *bv;
+    const uint4 *head;             // head_split_kernel's fragments [KS][64]
+    P::DropArgs drop[2];           // blocks 1, 2
+    uint16_t *x0;                  // train: bf16 [m][48] (nullable)
+    uint16_t *g[kMaxLayers];       // train: bf16 [m][h] (nullable each)
+    uint16_t *h[kMaxLayers];       // train: bf16 [m][h] (nullable each)
+    float *mean[kMaxLayers], *rstd[kMaxLayers];
+    float *masked;                 // train: [m][4] out; KL: the stored old masked logits (in)
+    float *dz;                     // train: fp32 [m][8]
+    uint16_t *dzb;                 // train: bf16 [m][8]
+    float *part;                   // per block: train kTrainParts floats, KL {sum, max}
+};
+
+// The head matrix [wa (4 rows); wv] as three exact bf16 terms in the 16 rows of the head chain's A
+// operand, laid out in fragment order: frag[ks][lane] (uint4) holds row c = lane & 15, k = 32 ks +
+// 8 (lane >> 4) .. + 7 (zero past h and in row 15), so a lane reads its fragment as one coalesced
+// 16-byte load.  Rows 0-4 hi (wa 0..3, wv), 5-9 mid, 10-14 lo: hi + mid + lo = the fp32 weight.
+__global__ __launch_bounds__(256) void head_split_kernel(const float *__restrict__ wa, const float *__restrict__ wv,
+                                                         int h, int ks_n, uint4 *__restrict__ frag) {
+    const int e = blockIdx.x * 256 + threadIdx.x;  // (ks, lane)
+    if (e >= ks_n * 64) return;
+    const int ks = e >> 6, lane = e & 63, g = lane >> 4, c = lane & 15;
+    const int term = c < 5 ? 0 : c < 10 ? 1 : c < 15 ? 2 : 3, which = c - 5 * term;  // which: 0-3 wa row, 4 wv
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+        uint32_t pr = 0;
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int k = 32 * ks + 8 * g + j + u;
+            const float x = (term < 3 && k < h) ? (which < 4 ? wa[which * h + k] : (wv ? wv[k] : 0.0f)) : 0.0f;
+            const __bf16 hi = (__bf16)x;
+            const float r1 = x - (float)hi;
+            const __bf16 mid = (__bf16)r1;
+            const __bf16 lo = (__bf16)(r1 - (float)mid);
+            const __bf16 t = term == 0 ? hi : term == 1 ? mid : lo;
+            pr |= (uint32_t)__builtin_bit_cast(uint16_t, t) << (16 * u);
+        }
+        w[j / 2] = pr;
+    }
+    frag[e] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// The four board tiles' head accumulators (lane (g, c) of tile q: head rows 4 g .. 4 g + 3 of row
+// 16 q + c) -> lane (q, c): R[g'] = head rows 4 g' .. 4 g' + 3 of its own row 16 q + c.
+__device__ __forceinline__ void heads_to_rows(f32x4_t (&R)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(R[0][i]), __float_as_uint(R[2][i]), false, false);
+        const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(R[1][i]), __float_as_uint(R[3][i]), false, false);
+        const auto c = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+        const auto d = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+        R[0][i] = __uint_as_float(c[0]);
+        R[1][i] = __uint_as_float(c[1]);
+        R[2][i] = __uint_as_float(d[0]);
+        R[3][i] = __uint_as_float(d[1]);
+    }
+}
+
+// 8-byte feature groups of one layer output tile row: lane (g, c) stores its valid groups of the
+// row at byte offset `off` (row * 2 H, < 2^32: a uniform base + 32-bit lane offset per store)
+template <int NT, int H>
+__device__ __forceinline__ void store_tile(uint16_t *dst, uint32_t off, const uint2 (&v)[NT], int g) {
+    char *p = reinterpret_cast<char *>(dst) + (off + 8u * (uint32_t)g);
+#pragma unroll
+    for (int n = 0; n < NT; n++)
+        if (16 * n + 4 * g < H) *reinterpret_cast<uint2 *>(p + 32 * n) = v[n];
+}
+
+template <int H, bool TRAIN, bool DROP>
+__global__ __launch_bounds__(kFpThreads, 1) void mlp_pass_kernel(FpArgs a) {
+    constexpr int NT = (H + 15) / 16, KS = ((H + 7) / 8 * 8 + 31) / 32;
+    constexpr int h = H;
+    constexpr int PW = pr_pitch(h), WB = pr_wbytes(h);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float *sLN = reinterpret_cast<float *>(smem + 2 * WB);  // [layer][gamma | beta][16 NT]
+    char *sZero = smem + 2 * WB + 2 * kMaxLayers * pr_ln_floats(NT) * 4;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, col = lane & 15;
+    const int64_t m = a.m;
+    const int64_t mv = a.la.rows ? min(*a.la.rows, m) : m;  // rows >= mv: padding of a ragged minibatch
+    const float inv_m = a.la.rows ? 1.0f / (float)max(mv, (int64_t)1) : a.la.inv_m;
+
+    // ---- the block weight images (bank-spread rows, zero K padding): 16 8-byte loads in flight per
+    // thread per batch; LayerNorm affines; the zero fragment
+    {
+        constexpr int q8 = PW / 8, h4 = h / 4, per = h * q8;
+        const uint16_t *wsrc[2] = {a.w1, a.w2};
+#pragma unroll
+        for (int l = 0; l < 2; l++)
+            for (int c0 = 0; c0 < per; c0 += 16 * kFpThreads) {
+                uint2 v[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const int c = c0 + tid + u * kFpThreads, r = c / q8, q = c - r * q8;
+                    v[u] = (c < per && q < h4) ? *reinterpret_cast<const uint2 *>(wsrc[l] + (int64_t)r * h + 4 * q)
+                                               : make_uint2(0u, 0u);
+                }
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const int c = c0 + tid + u * kFpThreads, r = c / q8, q = c - r * q8;
+                    if (c < per) *reinterpret_cast<uint2 *>(smem + l * WB + r * PW + 8 * q) = v[u];
+                }
+            }
+        for (int e = tid; e < kMaxLayers * 2 * 16 * NT; e += kFpThreads) {
+            const int l = e / (32 * NT), rem = e - l * 32 * NT, which = rem / (16 * NT), f = rem - which * 16 * NT;
+            const float *src = which ? a.beta[l] : a.gamma[l];
+            sLN[e] = f < h ? src[f] : 0.0f;
+        }
+        if (tid < 4) reinterpret_cast<uint32_t *>(sZero)[tid] = 0u;
+    }
+    __syncthreads();
+
+    constexpr float inv_n = 1.0f / (float)h;
+    constexpr int hp8 = (h + 7) & ~7;
+    constexpr int last_rows = h - 16 * (NT - 1);
+    const StemRecipe sr = stem_recipe(g);
+    const P::Drop d1 = P::make_drop(a.drop[0]), d2 = P::make_drop(a.drop[1]);
+    const int wlane = col * PW + 16 * g;
+    const int zoff = (int)(sZero - smem);
+    const float bias[5] = {a.ba[0], a.ba[1], a.ba[2], a.ba[3], TRAIN ? a.bv[0] : 0.0f};
+    const float beta_c = TRAIN ? *a.la.beta_dev : 0.0f;
+    // per lane: TRAIN dba[4], dbv, sum ppo, sum H, sum v;  KL sum, max
+    float acc_s[kTrainParts] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float kmax = -INFINITY;
+
+    for (int64_t base = (int64_t)blockIdx.x * kFpThreads; base < m; base += (int64_t)gridDim.x * kFpThreads) {
+        const int64_t r0 = base + 64 * wave;
+        if (r0 >= m) continue;  // an empty wave (no barrier below)
+        const int64_t r = r0 + lane;  // this lane's row for the loss / KL ("lane = row")
+        const bool live = r < m, real = r < mv;
+        const uint4 b = live ? *reinterpret_cast<const uint4 *>(a.boards + a.la.idx[r] * 16) : make_uint4(0u, 0u, 0u, 0u);
+
+        int wlane_t = wlane, glane_t = (col * 48 + 8 * g) * 2;
+        asm volatile("" : "+v"(wlane_t), "+v"(glane_t));
+        const char *w0b = reinterpret_cast<const char *>(a.w0) + glane_t;
+        f32x4_t accH[4];
+#pragma unroll 1
+        for (int pr = 0; pr < 4 / kFpQ; pr++) {
+            uint2 act[kFpQ][NT];
+            // ---------------- stem: obs fragments from the board bytes ----------------------
+            uint4 xs[kFpQ][2];
+#pragma unroll
+            for (int q = 0; q < kFpQ; q++) {
+                const int s = 16 * (kFpQ * pr + q) + col;
+                const uint32_t B0 = __shfl(b.x, s), B1 = __shfl(b.y, s), B2 = __shfl(b.z, s), B3 = __shfl(b.w, s);
+#pragma unroll
+                for (int ks = 0; ks < 2; ks++) xs[q][ks] = stem_frag(sr, ks, B0, B1, B2, B3);
+                if (TRAIN && a.x0) {
+                    const uint32_t row = (uint32_t)(r0 + s);
+                    if ((int64_t)row < m) {
+                        char *xo = reinterpret_cast<char *>(a.x0) + (row * 96u + 16u * (uint32_t)g);
+                        *reinterpret_cast<uint4 *>(xo) = xs[q][0];
+                        if (g < 2) *reinterpret_cast<uint4 *>(xo + 64) = xs[q][1];
+                    }
+                }
+            }
+            f32x4_t acc[kFpQ][NT];
+#pragma unroll
+            for (int q = 0; q < kFpQ; q++)
+#pragma unroll
+                for (int n = 0; n < NT; n++) acc[q][n] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int ks = 0; ks < 2; ks++) {
+#pragma unroll
+                for (int n = 0; n < NT; n++) {
+                    const int row = 16 * n + col, k = 32 * ks + 8 * g;
+                    uint4 fw = make_uint4(0u, 0u, 0u, 0u);
+                    if (row < h && k < 48) fw = *reinterpret_cast<const uint4 *>(w0b + 2 * (16 * n * 48 + 32 * ks));
+#pragma unroll
+                    for (int q = 0; q < kFpQ; q++)
+                        acc[q][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(fw), as_frag(xs[q][ks]), acc[q][n], 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            // ---------------- epilogue of layer l, tile q (row of lane (g, col) = r0 + 16 tq + col)
+#define FP_EPILOGUE(L_, Q_, RES_, DROP_)                                                                           \
+    do {                                                                                                        \
+        const uint32_t row = (uint32_t)(r0 + 16 * (kFpQ * pr + (Q_)) + col);                                     \
+        const float *lnp = sLN + (L_) * 32 * NT;                                                                \
+        const bool st = TRAIN && (int64_t)row < m;                                                              \
+        float mean, rstd;                                                                                       \
+        ln_epilogue_train<NT, H, RES_, DROP_>(acc[Q_], act[Q_], lnp, lnp + 16 * NT, g, inv_n, (L_) == 2 ? d2 : d1, \
+                                              row, st ? a.g[L_] : nullptr, row * (2u * H), mean, rstd);         \
+        if (st) {                                                                                               \
+            if (a.h[L_]) store_tile<NT, H>(a.h[L_], row * (2u * H), act[Q_], g);                                \
+            if (g == 0 && a.mean[L_]) {                                                                         \
+                a.mean[L_][row] = mean;                                                                         \
+                a.rstd[L_][row] = rstd;                                                                         \
+            }                                                                                                   \
+        }                                                                                                       \
+    } while (0)
+#pragma unroll
+            for (int q = 0; q < kFpQ; q++) FP_EPILOGUE(0, q, false, false);
+
+            // ---------------- residual blocks ---------------------------------------------------
+#pragma unroll
+            for (int l = 0; l < 2; l++) {
+#pragma unroll
+                for (int q = 0; q < kFpQ; q++)
+#pragma unroll
+                    for (int n = 0; n < NT; n++) acc[q][n] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+                const int wbase = l * WB + wlane_t;
+#pragma unroll
+                for (int ks = 0; ks < KS; ks++) {
+                    uint4 bf[kFpQ];
+#pragma unroll
+                    for (int q = 0; q < kFpQ; q++) bf[q] = act_frag<NT>(act[q], ks);
+                    const bool kok = 32 * ks + 8 * g < hp8;
+                    int kbase = wbase + 64 * ks;
+                    asm volatile("" : "+v"(kbase));
+#pragma unroll
+                    for (int n = 0; n < NT; n++) {
+                        const bool rok = n < NT - 1 || col < last_rows;
+                        const int off = (kok && rok) ? kbase + 16 * n * PW : zoff;
+                        const uint4 fw = *reinterpret_cast<const uint4 *>(smem + off);
+#pragma unroll
+                        for (int q = 0; q < kFpQ; q++)
+                            acc[q][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(fw), as_frag(bf[q]), acc[q][n], 0, 0, 0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int q = 0; q < kFpQ; q++) FP_EPILOGUE(l + 1, q, true, DROP);
+            }
+            // ---------------- heads: tile q's 16-row chain ----------------------------------------
+#pragma unroll
+            for (int q = 0; q < kFpQ; q++) {
+                f32x4_t z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int ks = 0; ks < KS; ks++)
+                    z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a.head[64 * ks + lane]), as_frag(act_frag<NT>(act[q], ks)),
+                                                                z, 0, 0, 0);
+                accH[kFpQ * pr + q] = z;
+            }
+        }
+#undef FP_EPILOGUE
+        // ---------------- lane = row: logits (hi + mid + lo), value; loss / KL -------------------
+        // the row's loss inputs (KL: its stored old logits), loaded only now: they would otherwise
+        // hold registers across the whole MLP
+        P::RowIn in{};
+        float4 old4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (TRAIN && real) in = P::load_row_in(a.la, a.la.idx[r]);
+        if (!TRAIN && real) old4 = *reinterpret_cast<const float4 *>(a.masked + r * 4);
+        heads_to_rows(accH);
+        float z5[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const int hi = k, mid = 5 + k, lo = 10 + k;
+            z5[k] = (accH[hi >> 2][hi & 3] + accH[mid >> 2][mid & 3]) + accH[lo >> 2][lo & 3] + bias[k];
+        }
+        if (TRAIN) {
+            float dz[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+            if (real) {
+                float mk[4], ppo, ent, vl;
+                P::HeadLossArgs la = a.la;
+                la.inv_m = inv_m;
+                P::row_loss(z5, in, la, beta_c, dz, mk, ppo, ent, vl);
+                *reinterpret_cast<float4 *>(a.masked + r * 4) = make_float4(mk[0], mk[1], mk[2], mk[3]);
+                acc_s[5] += ppo;
+                acc_s[6] += ent;
+                acc_s[7] += vl;
+            }
+#pragma unroll
+            for (int k = 0; k < 5; k++) acc_s[k] += dz[k];
+            if (live) {
+                *reinterpret_cast<float4 *>(a.dz + r * 8) = make_float4(dz[0], dz[1], dz[2], dz[3]);
+                *reinterpret_cast<float4 *>(a.dz + r * 8 + 4) = make_float4(dz[4], 0.0f, 0.0f, 0.0f);
+                *reinterpret_cast<uint4 *>(a.dzb + r * 8) =
+                    make_uint4(pack_bf2(dz[0], dz[1]), pack_bf2(dz[2], dz[3]), pack_bf2(dz[4], 0.0f), 0u);
+            }
+        } else if (real) {
+            const float o[4] = {old4.x, old4.y, old4.z, old4.w};
+            const float kl = P::kl_row(o, z5);
+            acc_s[0] += kl;
+            kmax = fmaxf(kmax, kl);
+        }
+    }
+    // ---- per block: fixed-order wave sums (LDS after the last use of the images) ------------
+    constexpr int NP = TRAIN ? kTrainParts : 2;
+    float vals[NP];
+#pragma unroll
+    for (int k = 0; k < NP; k++) {
+        float v = TRAIN || k == 0 ? acc_s[k] : kmax;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float w = __shfl_xor(v, o);
+            v = (!TRAIN && k == 1) ? fmaxf(v, w) : v + w;
+        }
+        vals[k] = v;
+    }
+    __syncthreads();
+    float *red = reinterpret_cast<float *>(smem);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < NP; k++) red[wave * NP + k] = vals[k];
+    __syncthreads();
+    if (tid < NP) {
+        float t = red[tid];
+        for (int w = 1; w < kFpThreads / 64; w++) t = (!TRAIN && tid == 1) ? fmaxf(t, red[w * NP + tid]) : t + red[w * NP + tid];
+        a.part[(int64_t)blockIdx.x * NP + tid] = t;
+    }
+}
+
+inline int fp_status() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK : (int)e;
+}
+
+inline bool al(const void *p, unsigned n) { return ((uintptr_t)p % n) == 0u; }
+
+size_t fp_lds(int h) { return (size_t)pr_lds_bytes(h, (h + 15) / 16); }
+
+int fp_blocks(int64_t m) {
+    const int64_t b = (m + kFpThreads - 1) / kFpThreads;
+    return (int)(b < 1 ? 1 : (b > 256 ? 256 : b));
+}
+
+bool fp_shape(int h) { return (h == 196 || h == 192 || h == 128 || h == 64 || h == 32) && fp_lds(h) <= (size_t)kFpLdsMax; }
+
+// Segments of the deferred / immediate column sums (ppo_update.hip's colsum, re-stated here for
+// this translation unit's two kernels).
+int fp_colsum(hipStream_t s, const float *part, int nb, int cols, int max_col, float *const *dst, const int *len,
+              int nseg, g2048_colsum_job *defer) {
+    g2048_colsum_job job{};
+    job.part = part;
+    job.nb = nb;
+    job.cols = cols;
+    job.max_col = max_col;
+    job.nseg = nseg;
+    for (int k = 0; k < nseg; k++) {
+        job.dst[k] = dst[k];
+        job.len[k] = len[k];
+    }
+    if (defer) {
+        *defer = job;
+        return fp_status();
+    }
+    return g2048_colsum_batch((g2048_stream_t)s, &job, 1);
+}
+
+int fp_fill(const g2048_mlp_pass_args *p, FpArgs &a, bool train) {
+    const int h = p->hidden;
+    // byte offsets of a row in the [m][h] bf16 outputs are 32-bit (m 2 h < 2^32: m up to ~10 M rows)
+    if (!fp_shape(h) || p->m <= 0 || p->m * 2 * h >= (int64_t(1) << 32)) return G2048_EINVAL;
+    if (!p->boards || !p->batch.idx || !p->w_stem || !p->w_block[0] || !p->w_block[1] || !p->head_frag || !p->ba ||
+        !p->masked || !p->partials)
+        return G2048_EINVAL;
+    for (int l = 0; l < 3; l++)
+        if (!p->ln_gamma[l] || !p->ln_beta[l]) return G2048_EINVAL;
+    if (!al(p->boards, 16) || !al(p->head_frag, 16) || !al(p->w_stem, 16) || !al(p->w_block[0], 8) || !al(p->w_block[1], 8) || !al(p->masked, 16))
+        return G2048_EINVAL;
+    if (train) {
+        if (!p->bv || !p->dz || !p->dz_bf16 || !p->beta_dev || !p->batch.action || !p->batch.legal ||
+            !p->batch.old_logp || !p->batch.adv || !p->batch.ret)
+            return G2048_EINVAL;
+        if (!al(p->dz, 16) || !al(p->dz_bf16, 16) || (p->x0 && !al(p->x0, 16)) || !al(p->batch.old_logp, 16))
+            return G2048_EINVAL;
+        for (int l = 0; l < 3; l++)
+            if ((p->g[l] && !al(p->g[l], 8)) || (p->h[l] && !al(p->h[l], 8)) || (!p->mean[l]) != (!p->rstd[l]))
+                return G2048_EINVAL;
+    }
+    a = FpArgs{};
+    a.boards = p->boards;
+    a.m = p->m;
+    a.la = P::HeadLossArgs{p->batch.idx, p->batch.action, p->batch.legal, p->batch.old_logp, p->batch.adv, p->batch.ret,
+                           p->beta_dev, p->batch.rows, p->critic, 1.0f - p->clip_eps, 1.0f + p->clip_eps,
+                           1.0f / (float)p->m, p->decouple_critic};
+    a.w0 = (const uint16_t *)p->w_stem;
+    a.w1 = (const uint16_t *)p->w_block[0];
+    a.w2 = (const uint16_t *)p->w_block[1];
+    for (int l = 0; l < 3; l++) {
+        a.gamma[l] = p->ln_gamma[l];
+        a.beta[l] = p->ln_beta[l];
+        a.g[l] = (uint16_t *)p->g[l];
+        a.h[l] = (uint16_t *)p->h[l];
+        a.mean[l] = p->mean[l];
+        a.rstd[l] = p->rstd[l];
+    }
+    a.ba = p->ba;
+    a.bv = p->bv;
+    a.head = (const uint4 *)p->head_frag;
+    a.drop[0] = P::drop_args(&p->drop[0]);
+    a.drop[1] = P::drop_args(&p->drop[1]);
+    if ((a.drop[0].thr != 0u) != (a.drop[1].thr != 0u)) return G2048_EINVAL;  // both blocks share nn.Dropout(p)
+    a.x0 = (uint16_t *)p->x0;
+    a.masked = p->masked;
+    a.dz = p->dz;
+    a.dzb = (uint16_t *)p->dz_bf16;
+    a.part = p->partials;
+    return G2048_OK;
+}
+
+template <bool TRAIN, bool DROP>
+int fp_launch2(hipStream_t s, const FpArgs &a, int h, int nb) {
+    const size_t lds = fp_lds(h);
+    switch (h) {
+    case 196: hipLaunchKernelGGL((mlp_pass_kernel<196, TRAIN, DROP>), dim3(nb), dim3(kFpThreads), lds, s, a); break;
+    case 192: hipLaunchKernelGGL((mlp_pass_kernel<192, TRAIN, DROP>), dim3(nb), dim3(kFpThreads), lds, s, a); break;
+    case 128: hipLaunchKernelGGL((mlp_pass_kernel<128, TRAIN, DROP>), dim3(nb), dim3(kFpThreads), lds, s, a); break;
+    case 64: hipLaunchKernelGGL((mlp_pass_kernel<64, TRAIN, DROP>), dim3(nb), dim3(kFpThreads), lds, s, a); break;
+    case 32: hipLaunchKernelGGL((mlp_pass_kernel<32, TRAIN, DROP>), dim3(nb), dim3(kFpThreads), lds, s, a); break;
+    default: return G2048_EINVAL;
+    }
+    return fp_status();
+}
+
+template <bool TRAIN>
+int fp_launch(hipStream_t s, const FpArgs &a, int h, int nb) {
+    return a.drop[0].thr != 0u ? fp_launch2<TRAIN, true>(s, a, h, nb) : fp_launch2<TRAIN, false>(s, a, h, nb);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t g2048_head_split_bytes(int32_t hidden) { return hidden > 0 ? (size_t)16 * 64 * ((hidden + 31) / 32) : 0; }
+
+int g2048_head_split(g2048_stream_t stream, const float *wa, const float *wv, int32_t hidden, void *frag) {
+    if (hidden <= 0 || hidden > 1024 || !wa || !frag || !al(frag, 16)) return G2048_EINVAL;
+    const int ks = (hidden + 31) / 32;
+    hipLaunchKernelGGL(head_split_kernel, dim3((unsigned)((ks * 64 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, wa,
+                       wv, (int)hidden, ks, (uint4 *)frag);
+    return fp_status();
+}
+
+int g2048_mlp_pass_supported(int32_t hidden, int32_t num_layers) { return num_layers == 2 && fp_shape(hidden) ? 1 : 0; }
+
+size_t g2048_mlp_pass_partials(int64_t m, int32_t train) {
+    if (m <= 0) return 0;
+    return (size_t)fp_blocks(m) * (train ? kTrainParts : 2);
+}
+
+int g2048_ppo_forward_loss(g2048_stream_t stream, const g2048_mlp_pass_args *p, float *dba, float *dbv, float *sums,
+                           g2048_colsum_job *defer) {
+    if (!p || !dba || !dbv || !sums) return G2048_EINVAL;
+    FpArgs a;
+    const int st = fp_fill(p, a, true);
+    if (st) return st;
+    const hipStream_t s = (hipStream_t)stream;
+    const int nb = fp_blocks(p->m);
+    const int rc = fp_launch<true>(s, a, p->hidden, nb);
+    if (rc) return rc;
+    float *dst[3] = {dba, dbv, sums};
+    const int len[3] = {4, 1, 3};
+    return fp_colsum(s, p->partials, nb, kTrainParts, -1, dst, len, 3, defer);
+}
+
+int g2048_ppo_forward_kl(g2048_stream_t stream, const g2048_mlp_pass_args *p, float *out, g2048_colsum_job *defer) {
+    if (!p || !out) return G2048_EINVAL;
+    FpArgs a;
+    const int st = fp_fill(p, a, false);
+    if (st) return st;
+    const hipStream_t s = (hipStream_t)stream;
+    const int nb = fp_blocks(p->m);
+    const int rc = fp_launch<false>(s, a, p->hidden, nb);
+    if (rc) return rc;
+    float *dst[1] = {out};
+    const int len[1] = {2};
+    return fp_colsum(s, p->partials, nb, 2, 1, dst, len, 1, defer);
+}
+
+}  // extern "C"

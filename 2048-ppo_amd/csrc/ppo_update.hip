@@ -22,11 +22,14 @@
 
 #include "board.hpp"
 #include "ln_row.hpp"
+#include "ppo_common.hpp"
 #include "../../include/g2048_ppo.h"
 
 using g2048::philox;
 
 namespace {
+
+using namespace g2048::ppo;
 
 constexpr int kWaves = 4;  // waves per block
 constexpr int kThreads = 64 * kWaves;
@@ -84,53 +87,6 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
     return v;
-}
-
-struct DropArgs {
-    uint32_t thr;       // keep iff 16-bit draw >= thr  (thr = round(p 2^16))
-    float scale;        // 1 / (1 - p)
-    uint32_t c1base;    // layer << 12 | pass << 20
-    uint32_t k0, k1;    // seed
-    uint64_t counter;
-    const uint64_t *counter_dev;
-};
-
-struct Drop {
-    uint32_t thr, c1base, c2, c3, k0, k1;
-    float scale;
-};
-
-__device__ __forceinline__ Drop make_drop(const DropArgs &a) {
-    const uint64_t c = a.counter + (a.counter_dev ? *a.counter_dev : 0ull);
-    return Drop{a.thr, a.c1base, (uint32_t)c, (uint32_t)(c >> 32), a.k0, a.k1, a.scale};
-}
-
-// One Philox4x32-10 call gives 8 16-bit uniforms: the keep draws of column groups cg and cg ^ 4
-// (cg = 8a + 4h + b shares the call (a, b); h picks the half), so a lane that owns both -- the
-// fused forward's layout -- draws once per two groups.
-__device__ __forceinline__ uint4 drop_draw4(const Drop &d, uint32_t row, uint32_t cg) {
-    const uint32_t pair = ((cg >> 3) << 2) | (cg & 3u);
-    return philox(row, pair | d.c1base, d.c2, d.c3, d.k0, d.k1);
-}
-
-__device__ __forceinline__ uint2 drop_half(const uint4 &r, uint32_t cg) {
-    return (cg & 4u) ? make_uint2(r.z, r.w) : make_uint2(r.x, r.y);
-}
-
-__device__ __forceinline__ uint2 drop_draw(const Drop &d, uint32_t row, uint32_t cg) {
-    return drop_half(drop_draw4(d, row, cg), cg);
-}
-
-__device__ __forceinline__ void drop_mult_bits(const Drop &d, uint2 w, float k[4]) {
-    k[0] = (w.x & 0xFFFFu) >= d.thr ? d.scale : 0.0f;
-    k[1] = (w.x >> 16) >= d.thr ? d.scale : 0.0f;
-    k[2] = (w.y & 0xFFFFu) >= d.thr ? d.scale : 0.0f;
-    k[3] = (w.y >> 16) >= d.thr ? d.scale : 0.0f;
-}
-
-// keep multipliers (0 or 1/(1-p)) of columns 4cg .. 4cg+3 of `row`
-__device__ __forceinline__ void drop_mult(const Drop &d, uint32_t row, uint32_t cg, float k[4]) {
-    drop_mult_bits(d, drop_draw(d, row, cg), k);
 }
 
 __constant__ float kThirds[4] = {0.0f, 1.0f / 3.0f, 2.0f / 3.0f, 1.0f};
@@ -410,117 +366,6 @@ __global__ __launch_bounds__(kBwdThreads) void ln_bwd_kernel(
 }
 
 // ------------------------------------------------------------------ heads + PPO loss ---------
-struct HeadLossArgs {
-    const int64_t *idx;
-    const uint8_t *action;
-    const uint8_t *legal;
-    const float *old_logp;
-    const float *adv;
-    const float *ret;
-    const float *beta_dev;
-    const int64_t *rows;  // nullable: valid-row count of a padded minibatch
-    float critic, clip_lo, clip_hi, inv_m;
-    int decouple;
-};
-
-// The PPO-clip / entropy / smooth-L1 loss of one row and its gradient w.r.t. the 5 head outputs
-// (train.py:497-546, with torch's backward conventions: minimum splits ties, clamp passes its
-// bounds); z = {4 logits, value}, i = the row's index in the flat trajectory.
-struct RowIn {
-    uint32_t act, legal;
-    float olp[4], adv, ret;
-};
-
-// The per-row inputs of trajectory row i (independent loads, issued together).
-__device__ __forceinline__ RowIn load_row_in(const HeadLossArgs &a, int64_t i) {
-    RowIn in;
-    in.act = a.action[i] & 3u;
-    in.legal = a.legal[i] & 0xFu;
-    const float4 o = *reinterpret_cast<const float4 *>(a.old_logp + i * 4);
-    in.olp[0] = o.x;
-    in.olp[1] = o.y;
-    in.olp[2] = o.z;
-    in.olp[3] = o.w;
-    in.adv = a.adv[i];
-    in.ret = a.ret[i];
-    return in;
-}
-
-__device__ __forceinline__ void row_loss(const float z[5], const RowIn &in, const HeadLossArgs &a, float beta_c,
-                                         float dz[5], float mk[4], float &ppo_out, float &ent_out, float &vl_out) {
-    const int act = (int)in.act;
-    const uint32_t legal = in.legal;
-    float mx = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        mk[k] = (legal >> k) & 1u ? z[k] : -INFINITY;
-        mx = fmaxf(mx, mk[k]);
-    }
-    float se = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 4; k++) se += (legal >> k) & 1u ? expf(mk[k] - mx) : 0.0f;
-    const float lse = mx + logf(se);
-    float sm[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) sm[k] = (legal >> k) & 1u ? expf(mk[k] - lse) : 0.0f;
-    const float lp_a = mk[act] - lse;
-    const float olp_a = act == 0 ? in.olp[0] : act == 1 ? in.olp[1] : act == 2 ? in.olp[2] : in.olp[3];
-    const float dlt = lp_a - olp_a;
-    const float ratio = expf(fminf(fmaxf(dlt, -20.0f), 20.0f));
-    const bool in20 = dlt >= -20.0f && dlt <= 20.0f;
-    const float A = in.adv;
-    const float rc = fminf(fmaxf(ratio, a.clip_lo), a.clip_hi);
-    const bool inr = ratio >= a.clip_lo && ratio <= a.clip_hi;
-    const float t1 = A * ratio, t2 = A * rc;
-    const float ppo = fminf(t1, t2);
-    // torch.minimum backward: the smaller side takes the gradient, a tie splits it in halves
-    float dp;
-    if (t1 < t2) dp = A;
-    else if (t1 > t2) dp = inr ? A : 0.0f;
-    else dp = 0.5f * A + (inr ? 0.5f * A : 0.0f);
-    const float dd = in20 ? dp * ratio : 0.0f;  // d ppo / d (logpi(a) - old)
-
-    // entropy of softmax(clamp(masked, -20, 20)) summed over the legal actions
-    float ck[4], cmx = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        ck[k] = fminf(fmaxf(mk[k], -20.0f), 20.0f);
-        cmx = fmaxf(cmx, ck[k]);
-    }
-    float se2 = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 4; k++) se2 += expf(ck[k] - cmx);
-    const float lse2 = cmx + logf(se2);
-    float lp2[4], p2[4], ent = 0.0f, S = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        lp2[k] = ck[k] - lse2;
-        p2[k] = expf(lp2[k]);
-        if ((legal >> k) & 1u) {
-            ent -= p2[k] * lp2[k];
-            S += p2[k] * (lp2[k] + 1.0f);
-        }
-    }
-    const float dv0 = z[4] - in.ret;
-    const float adv0 = fabsf(dv0);
-    const float vl = adv0 < 1.0f ? 0.5f * dv0 * dv0 : adv0 - 0.5f;
-    const float dvl = fminf(fmaxf(dv0, -1.0f), 1.0f);
-
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const bool valid = (legal >> k) & 1u;
-        const bool cpass = valid && mk[k] >= -20.0f && mk[k] <= 20.0f;
-        const float dent = -(p2[k] * (lp2[k] + 1.0f) - p2[k] * S);
-        const float g = dd * ((k == act ? 1.0f : 0.0f) - sm[k]) + (cpass ? beta_c * dent : 0.0f);
-        dz[k] = valid ? -a.inv_m * g : 0.0f;
-    }
-    dz[4] = a.inv_m * a.critic * dvl;
-
-    ppo_out = ppo;
-    ent_out = ent;
-    vl_out = vl;
-}
-
 // B fragments (lane (g, c): k = 32 ks + 8 g + j, column c) of the head matrix [wa (4 rows); wv],
 // zero beyond column 4 and row h, split w = hi + mid + lo into three bf16 terms.
 template <int KS>
@@ -1877,25 +1722,6 @@ inline int partial_blocks(int64_t m) {
     const int64_t b = (m + 4 * kWaves - 1) / (4 * kWaves);
     return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
 }
-
-inline DropArgs drop_args(const g2048_dropout *d) {
-    DropArgs a{};
-    a.thr = 0;
-    a.scale = 1.0f;
-    if (d && d->p > 0.0f) {
-        const double t = (double)d->p * 65536.0;
-        a.thr = t >= 65536.0 ? 0x10000u : (uint32_t)(t + 0.5);
-        a.scale = 1.0f / (1.0f - d->p);
-        a.c1base = (d->layer << 12) | (d->pass << 20);
-        a.k0 = (uint32_t)d->seed;
-        a.k1 = (uint32_t)(d->seed >> 32);
-        a.counter = d->counter;
-        a.counter_dev = d->counter_dev;
-    }
-    return a;
-}
-
-inline bool drop_on(const g2048_dropout *d) { return d && d->p > 0.0f; }
 
 int colsum(hipStream_t s, const float *part, int nb, int C, float *scratch2, const Segs &segs, int max_col,
            g2048_colsum_job *defer = nullptr) {

@@ -37,6 +37,8 @@ EXPORTED = (
     "g2048_urm_rms_res_bwd", "g2048_urm_swiglu_conv_partials", "g2048_urm_swiglu_conv_fwd", "g2048_urm_swiglu_conv_bwd",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
+    "g2048_head_split_bytes", "g2048_head_split", "g2048_mlp_pass_supported", "g2048_mlp_pass_partials",
+    "g2048_ppo_forward_loss", "g2048_ppo_forward_kl",
     # include/g2048_urm.h
     "g2048_urm_stem", "g2048_urm_attention", "g2048_urm_residual_rms", "g2048_urm_swiglu_conv",
     "g2048_urm_pool_heads", "g2048_urm_linear_supported", "g2048_urm_linear", "g2048_urm_linear_rms",
@@ -131,6 +133,17 @@ class AdamWGroup(ctypes.Structure):
                 ("pad_", ctypes.c_int32)]
 
 
+class MlpPassArgs(ctypes.Structure):
+    """struct g2048_mlp_pass_args"""
+    vp = ctypes.c_void_p
+    _fields_ = [("boards", vp), ("batch", PPOBatch), ("m", ctypes.c_int64), ("hidden", ctypes.c_int32),
+                ("decouple_critic", ctypes.c_int32), ("w_stem", vp), ("w_block", vp * 2), ("ln_gamma", vp * 3),
+                ("ln_beta", vp * 3), ("head_frag", vp), ("ba", vp), ("bv", vp), ("drop", Dropout * 2),
+                ("beta_dev", vp), ("critic", ctypes.c_float), ("clip_eps", ctypes.c_float), ("x0", vp), ("g", vp * 3),
+                ("h", vp * 3), ("mean", vp * 3), ("rstd", vp * 3), ("masked", vp), ("dz", vp), ("dz_bf16", vp),
+                ("partials", vp)]
+
+
 class PolicyRolloutArgs(ctypes.Structure):
     """struct g2048_policy_rollout_args"""
     vp = ctypes.c_void_p
@@ -202,6 +215,12 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_policy_rollout_supported": (ctypes.c_int, [i32, i32]),
         "g2048_policy_rollout_lds_bytes": (sz, [i32]),
         "g2048_policy_rollout": (ctypes.c_int, [vp, ctypes.POINTER(PolicyRolloutArgs)]),
+        "g2048_head_split_bytes": (sz, [i32]),
+        "g2048_head_split": (ctypes.c_int, [vp, vp, vp, i32, vp]),
+        "g2048_mlp_pass_supported": (ctypes.c_int, [i32, i32]),
+        "g2048_mlp_pass_partials": (sz, [i64, i32]),
+        "g2048_ppo_forward_loss": (ctypes.c_int, [vp, ctypes.POINTER(MlpPassArgs), vp, vp, vp, jp]),
+        "g2048_ppo_forward_kl": (ctypes.c_int, [vp, ctypes.POINTER(MlpPassArgs), vp, jp]),
         "g2048_linear_dgrad_supported": (ctypes.c_int, [i32, i32]),
         "g2048_linear_dgrad": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_stem": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, i64, i32]),
@@ -521,6 +540,75 @@ def ppo_head_kl(x, wa, ba, old_masked, partials, out, defer: ColsumJob | None = 
         _dev(old_masked, torch.float32, "old_masked"), _dev(rows, torch.int64, "rows"),
         _dev(partials, torch.float32, "partials"),
         _dev(out, torch.float32, "out"), _defer(defer)), "g2048_ppo_head_kl")
+
+
+def mlp_pass_supported(hidden: int, num_layers: int) -> bool:
+    """The fused train / KL passes (g2048_ppo_forward_loss / _kl) cover this GameMLP shape."""
+    return bool(load().g2048_mlp_pass_supported(int(hidden), int(num_layers)))
+
+
+def mlp_pass_partials(m: int, train: bool) -> int:
+    return int(load().g2048_mlp_pass_partials(int(m), int(bool(train))))
+
+
+def head_split_bytes(hidden: int) -> int:
+    return int(load().g2048_head_split_bytes(int(hidden)))
+
+
+def head_split(wa, wv, frag):
+    """frag (uint8 device buffer of head_split_bytes(h)) <- the 3-term bf16 split of [wa; wv]."""
+    h = wa.shape[1]
+    _check(load().g2048_head_split(_stream(wa), _dev(wa, torch.float32, "wa"), _dev(wv, torch.float32, "wv"), h,
+                                   _dev(frag, None, "frag")), "g2048_head_split")
+
+
+def make_mlp_pass(boards, batch: PPOBatch, m: int, w_stem, w_blocks, gammas, betas, head_frag, ba, bv=None,
+                  drops=(None, None), beta_dev=None, critic=0.0, clip_eps=0.2, decouple=False, x0=None,
+                  g=(None, None, None), h=(None, None, None), mean=(None, None, None), rstd=(None, None, None),
+                  masked=None, dz=None, dz_bf16=None, partials=None) -> MlpPassArgs:
+    """struct g2048_mlp_pass_args for g2048_ppo_forward_loss / g2048_ppo_forward_kl (GameMLP, 2 blocks)."""
+    a = MlpPassArgs()
+    a.boards = _dev(boards, torch.int8, "boards")
+    a.batch = batch
+    a.m = int(m)
+    a.hidden = int(w_stem.shape[0])
+    a.decouple_critic = int(bool(decouple))
+    a.w_stem = _dev(w_stem, torch.bfloat16, "w_stem")
+    for i, w in enumerate(w_blocks):
+        a.w_block[i] = _dev(w, torch.bfloat16, f"w_block[{i}]")
+    for i, (gm, bt) in enumerate(zip(gammas, betas)):
+        a.ln_gamma[i], a.ln_beta[i] = _dev(gm, torch.float32, "gamma"), _dev(bt, torch.float32, "beta")
+    a.head_frag = _dev(head_frag, None, "head_frag")
+    a.ba, a.bv = _dev(ba, torch.float32, "ba"), _dev(bv, torch.float32, "bv")
+    for i, d in enumerate(drops):
+        if d is not None:
+            a.drop[i] = d
+    a.beta_dev = _dev(beta_dev, torch.float32, "beta_dev")
+    a.critic, a.clip_eps = float(critic), float(clip_eps)
+    a.x0 = _dev(x0, torch.bfloat16, "x0")
+    for i in range(3):
+        a.g[i] = _dev(g[i], torch.bfloat16, f"g[{i}]")
+        a.h[i] = _dev(h[i], torch.bfloat16, f"h[{i}]")
+        a.mean[i] = _dev(mean[i], torch.float32, f"mean[{i}]")
+        a.rstd[i] = _dev(rstd[i], torch.float32, f"rstd[{i}]")
+    a.masked = _dev(masked, torch.float32, "masked")
+    a.dz = _dev(dz, torch.float32, "dz")
+    a.dz_bf16 = _dev(dz_bf16, torch.bfloat16, "dz_bf16")
+    a.partials = _dev(partials, torch.float32, "partials")
+    return a
+
+
+def ppo_forward_loss(args: MlpPassArgs, dba, dbv, sums, defer: ColsumJob | None = None, like=None):
+    """The fused train pass (obs -> GameMLP -> heads -> PPO loss / dz) of one minibatch."""
+    _check(load().g2048_ppo_forward_loss(_stream(like if like is not None else dba), ctypes.byref(args),
+                                         _dev(dba, torch.float32, "dba"), _dev(dbv, torch.float32, "dbv"),
+                                         _dev(sums, torch.float32, "sums"), _defer(defer)), "g2048_ppo_forward_loss")
+
+
+def ppo_forward_kl(args: MlpPassArgs, out, defer: ColsumJob | None = None):
+    """The fused KL re-forward of one minibatch: out[2] = {sum KL, max KL}."""
+    _check(load().g2048_ppo_forward_kl(_stream(out), ctypes.byref(args), _dev(out, torch.float32, "out"),
+                                       _defer(defer)), "g2048_ppo_forward_kl")
 
 
 def dropout_mask(m: int, h: int, drop: Dropout, mask):

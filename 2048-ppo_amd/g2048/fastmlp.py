@@ -77,6 +77,7 @@ class FusedPPOUpdater(PPOUpdater):
             optimizer.set_bf16_copies(dict(zip(self.lin, self.wbf)))
         self.seed = seed
         self.bs = 0
+        self.fused_pass = False
 
     # ---------------------------------------------------------------- buffers -------------
     def _alloc(self, bs: int):
@@ -110,15 +111,66 @@ class FusedPPOUpdater(PPOUpdater):
         self.sums = torch.zeros(3, dtype=torch.float32, device=d)
         self.kl = torch.zeros(2, dtype=torch.float32, device=d)
         self.rows = torch.full((1,), bs, dtype=torch.int64, device=d)  # valid rows (ragged last minibatch)
+        # the fused train / KL passes (g2048_ppo_forward_loss / _kl): dz as bf16 for the head weight
+        # gradient dz^T H2 on g2048_wgrad, the head weights split for the passes' MFMA operand
+        self.fused_pass = (L.mlp_pass_supported(h, nl - 1) and bs * 2 * h < 2 ** 32
+                           and L.wgrad_partials(bs, 8, h) > 0 and not self.force_layer_kernels)
+        if self.fused_pass:
+            self.dzb = torch.empty(bs, 8, dtype=bf, device=d)
+            self.head_frag = torch.zeros(L.head_split_bytes(h), dtype=torch.uint8, device=d)
+            self.part_fwd = torch.empty(L.mlp_pass_partials(bs, True), dtype=f32, device=d)
+            self.part_klp = torch.empty(L.mlp_pass_partials(bs, False), dtype=f32, device=d)
+            self.part_wh = torch.empty(L.wgrad_partials(bs, 8, h), dtype=f32, device=d)
+            self.wh_spill = torch.empty(3 * h, dtype=f32, device=d)  # rows 5..7 of dz^T H2 (zero columns)
+            self.wh_out = torch.empty(8, h, dtype=f32, device=d)    # (unused: the job's segments route it)
         self.bs = bs
 
     def _drop(self, layer: int, pass_: int):
         return L.make_dropout(self.p_drop if self.model.training else 0.0, layer, pass_, self.seed, 0, self.counter)
 
+    force_layer_kernels = False  # tests: the per-layer kernel chain instead of the fused passes
+
     @torch.no_grad()
     def refresh_weights(self):
         for w, b in zip(self.lin, self.wbf):
             b.copy_(w)
+        self._split_heads()
+
+    def _split_heads(self):
+        if self.bs and self.fused_pass:
+            L.head_split(self.wa, self.wv, self.head_frag)
+
+    def _pass_args(self, data, idx, pass_: int, train: bool):
+        """g2048_mlp_pass_args of this minibatch (pass 0: the train pass, 1: the KL re-forward)."""
+        batch = L.make_ppo_batch(idx, data["actions"], data["legal"], data["logp"], data["adv"], data["ret"],
+                                 rows=self.rows)
+        common = dict(w_stem=self.wbf[0], w_blocks=self.wbf[1:], gammas=[ln.weight for ln in self.ln],
+                      betas=[ln.bias for ln in self.ln], head_frag=self.head_frag, ba=self.ba,
+                      drops=(self._drop(1, pass_), self._drop(2, pass_)), masked=self.masked)
+        if not train:
+            return L.make_mlp_pass(data["boards"], batch, idx.shape[0], partials=self.part_klp, **common)
+        return L.make_mlp_pass(data["boards"], batch, idx.shape[0], bv=self.bv, beta_dev=self._beta_dev,
+                               critic=self.cfg.critic, clip_eps=self.cfg.clip_eps, decouple=self.decouple, x0=self.x0,
+                               g=self.G, h=self.H, mean=self.mean, rstd=self.rstd, dz=self.dz, dz_bf16=self.dzb,
+                               partials=self.part_fwd, **common)
+
+    def fused_forward_loss(self, data, idx, beta):
+        """The train pass in one launch (obs -> GameMLP -> heads -> PPO loss, dz), then the head weight
+        gradient dz^T H2 (bf16 operands, as autocast's Linear backward) on g2048_wgrad; returns the
+        deferred column-sum jobs (bias gradients / loss sums, head weight gradients)."""
+        self._beta_dev = beta if torch.is_tensor(beta) else torch.tensor(float(beta), device=self.dev)
+        args = self._pass_args(data, idx, 0, True)
+        self._kl_args = self._pass_args(data, idx, 1, False)
+        j_loss, j_head = L.ColsumJob(), L.ColsumJob()
+        L.ppo_forward_loss(args, self.ba.grad, self.bv.grad, self.sums, defer=j_loss)
+        L.wgrad(self.dzb, self.H[-1], self.part_wh, self.wh_out, defer=j_head)
+        # route dz^T H2 [8, h]: rows 0-3 -> action_head.weight.grad, row 4 -> value_head.weight.grad
+        h = self.h
+        j_head.nseg = 3
+        for k, (dst, n) in enumerate(((self.wa.grad, 4 * h), (self.wv.grad, h), (self.wh_spill, 3 * h))):
+            j_head.dst[k] = dst.data_ptr()
+            j_head.len[k] = n
+        return [j_loss, j_head]
 
     # ---------------------------------------------------------------- passes --------------
     def forward_features(self, boards, idx, pass_: int):
@@ -141,17 +193,20 @@ class FusedPPOUpdater(PPOUpdater):
             x = self.H[l]
         return x
 
-    def loss_backward(self, data, idx, beta):
-        """Heads + PPO loss + backward of the minibatch; gradients land in the GradBucket views."""
+    def loss_backward(self, data, idx, beta, jobs=None):
+        """Heads + PPO loss (unless the fused train pass did them: its `jobs`) + backward of the
+        minibatch; gradients land in the GradBucket views."""
         nl = len(self.lin)
-        batch = L.make_ppo_batch(idx, data["actions"], data["legal"], data["logp"], data["adv"], data["ret"],
-                                 rows=self.rows)
-        # the heads write only their output gradient dz [m, 8]; the last block's backward recomputes
-        # their share dz W of its output gradient (no [m, h] head gradient in HBM)
-        jobs = [L.ColsumJob()]
-        L.ppo_head_loss(self.H[-1], self.wa, self.ba, self.wv, self.bv, batch, beta, self.cfg.critic,
-                        self.cfg.clip_eps, self.decouple, self.masked, None, self.part_head,
-                        self.wa.grad, self.ba.grad, self.wv.grad, self.bv.grad, self.sums, dz=self.dz, defer=jobs[-1])
+        if jobs is None:
+            batch = L.make_ppo_batch(idx, data["actions"], data["legal"], data["logp"], data["adv"], data["ret"],
+                                     rows=self.rows)
+            # the heads write only their output gradient dz [m, 8]; the last block's backward
+            # recomputes their share dz W of its output gradient (no [m, h] head gradient in HBM)
+            jobs = [L.ColsumJob()]
+            L.ppo_head_loss(self.H[-1], self.wa, self.ba, self.wv, self.bv, batch, beta, self.cfg.critic,
+                            self.cfg.clip_eps, self.decouple, self.masked, None, self.part_head,
+                            self.wa.grad, self.ba.grad, self.wv.grad, self.bv.grad, self.sums, dz=self.dz,
+                            defer=jobs[-1])
         head = (self.dz, self.wa, None if self.decouple else self.wv)
         for l in range(nl - 1, -1, -1):
             ln = self.ln[l]
@@ -195,8 +250,12 @@ class FusedPPOUpdater(PPOUpdater):
     def _pre(self, idx, data, beta, encode):
         if idx.shape[0] != self.bs:  # ragged last minibatch of an eager pass
             self._alloc(idx.shape[0])
-        self.forward_features(data["boards"], idx, 0)
-        self.loss_backward(data, idx, beta)
+            self._split_heads()
+        if self.fused_pass:
+            self.loss_backward(data, idx, beta, jobs=self.fused_forward_loss(data, idx, beta))
+        else:
+            self.forward_features(data["boards"], idx, 0)
+            self.loss_backward(data, idx, beta)
         return {}
 
     def _post(self, st, beta):
@@ -213,7 +272,10 @@ class FusedPPOUpdater(PPOUpdater):
             kl_job = L.ColsumJob()
             nl = len(self.lin)
             w_last = self.wbf[-1]
-            if nl > 1 and self.mf_ok[-1] and L.mlp_fwd_kl_supported(w_last.shape[0], w_last.shape[1]):
+            if self.fused_pass:  # the whole re-forward + KL in one launch (the step changed the heads)
+                self._split_heads()
+                L.ppo_forward_kl(self._kl_args, self.kl, defer=kl_job)
+            elif nl > 1 and self.mf_ok[-1] and L.mlp_fwd_kl_supported(w_last.shape[0], w_last.shape[1]):
                 # the last block fused with the action head and the KL reduction (no H write / re-read)
                 x = self._layers(1, upto=nl - 1)
                 ln = self.ln[-1]

@@ -210,6 +210,58 @@ int g2048_mlp_fwd_kl(g2048_stream_t stream, const uint16_t *x, const uint16_t *w
                      const float *ba, const float *old_masked, const int64_t *rows, float *partials, float *out,
                      g2048_colsum_job *defer);
 
+/* ---- fused forward passes of the minibatch step (csrc/ppo_fused.hip) --------------------------
+ * GameMLP (num_layers 2, hidden in {32, 64, 128, 192, 196}) over the minibatch boards[idx[r]] in ONE
+ * persistent launch each, on the fused rollout's register hand-off (weights in LDS):
+ *   g2048_ppo_forward_loss  the train pass (train.py:491-546): to_model_format -> stem -> 2 blocks with
+ *       Dropout(p) of pass 0 -> heads -> the PPO-clip / entropy / smooth-L1 loss and dz.  Replaces
+ *       g2048_obs_gather + 3 x g2048_mlp_fwd + g2048_ppo_head_loss (the logits keep the fp32 head weights
+ *       through g2048_head_split); its G / H / mean / rstd are bitwise
+ *       those of g2048_mlp_fwd.  Writes x0 (bf16 [m,48], optional), g[l] / h[l] (bf16 [m,h], optional
+ *       each: h[2] is the head weight-gradient operand), mean[l] / rstd[l] (optional pairs), masked
+ *       (fp32 [m,4]), dz (fp32 [m,8], g2048_dy.dz) and dz_bf16 (bf16 [m,8]: columns 0..4 = dz, the
+ *       operand of dW_heads = dz^T h[2] on g2048_wgrad), and reduces dba [4], dbv [1] and sums [3] =
+ *       {sum ppo, sum H, sum v} through g2048_mlp_pass_partials(m, 1) floats of partials.
+ *   g2048_ppo_forward_kl  the KL re-forward (train.py:578-601) with the updated weights and the
+ *       dropout draw of pass 1 (drop[].pass): KL(old || new) against `masked` (the train pass's
+ *       output, read), out[2] = {sum KL, max KL} through g2048_mlp_pass_partials(m, 0) floats.
+ * Both take the g2048_ppo_batch conventions (rows: padded ragged minibatch) and the deferred
+ * column-sum job (defer, nullable). */
+typedef struct g2048_mlp_pass_args {
+    const int8_t *boards;          /* [M][16] the flat trajectory's boards (16-byte aligned) */
+    g2048_ppo_batch batch;         /* idx (both passes), rows; the loss inputs (train pass) */
+    int64_t m;                     /* minibatch rows */
+    int32_t hidden, decouple_critic;
+    const void *w_stem;            /* bf16 [h][48], 16-byte aligned */
+    const void *w_block[2];        /* bf16 [h][h] */
+    const float *ln_gamma[3], *ln_beta[3];
+    const void *head_frag;         /* g2048_head_split of the current head weights */
+    const float *ba, *bv;          /* fp32 head biases (bv: train pass only) */
+    g2048_dropout drop[2];         /* blocks 1 and 2 (p == 0: eval-mode blocks) */
+    const float *beta_dev;         /* train: the entropy coefficient (device float) */
+    float critic, clip_eps;
+    void *x0;                      /* train outputs (see above) */
+    void *g[3];
+    void *h[3];
+    float *mean[3], *rstd[3];
+    float *masked;                 /* train: out; KL: in */
+    float *dz;
+    void *dz_bf16;
+    float *partials;
+} g2048_mlp_pass_args;
+
+/* The head weights [wa (4 rows); wv] (fp32) as the passes' MFMA operand: an exact three-term bf16
+ * split laid out in fragment order, g2048_head_split_bytes(h) bytes (16-byte aligned).  Run after
+ * every change of the head weights (the optimizer step) and before the passes that read them;
+ * wv NULL = zero value rows (the KL pass reads only the action rows). */
+size_t g2048_head_split_bytes(int32_t hidden);
+int g2048_head_split(g2048_stream_t stream, const float *wa, const float *wv, int32_t hidden, void *frag);
+int g2048_mlp_pass_supported(int32_t hidden, int32_t num_layers);
+size_t g2048_mlp_pass_partials(int64_t m, int32_t train);
+int g2048_ppo_forward_loss(g2048_stream_t stream, const g2048_mlp_pass_args *args, float *dba, float *dbv, float *sums,
+                           g2048_colsum_job *defer);
+int g2048_ppo_forward_kl(g2048_stream_t stream, const g2048_mlp_pass_args *args, float *out, g2048_colsum_job *defer);
+
 /* Accumulates one minibatch into the update statistics (train.py:603-642): stats[0..7] +=
  * {loss, policy_loss, entropy_loss, value_loss, grad_norm, entropy, kl_total, kl_average} from the
  * head_loss sums, the KL {sum, max}, the pre-clip gradient norm and beta; stats[8] = max(stats[8],

@@ -885,3 +885,163 @@ def test_linear_dgrad_matches_matmul(dev, h, m):
     assert torch.equal(again, out[:m])
     assert not L.linear_dgrad_supported(196, 48) and L.linear_dgrad_supported(196, 196)
     assert not L.linear_dgrad_supported(256, 256)  # the library GEMM is faster there
+
+
+def _pass_case(dev, h, M, m, p, seed):
+    """Random GameMLP weights (bf16 copies), a flat trajectory of M rows and a minibatch idx of m rows."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    rnd = lambda *s: torch.randn(*s, generator=g, device=dev)  # noqa: E731
+    w = [_bf(rnd(h, 48) / 48 ** 0.5)] + [_bf(rnd(h, h) / h ** 0.5) for _ in range(2)]
+    gam = [torch.rand(h, generator=g, device=dev) + 0.5 for _ in range(3)]
+    bet = [rnd(h) * 0.1 for _ in range(3)]
+    wa, ba, wv, bv = rnd(4, h) * 0.1, rnd(4) * 0.1, rnd(1, h) * 0.1, rnd(1) * 0.1
+    rng = np.random.default_rng(seed)
+    boards = rng.integers(0, 13, size=(M, 16)).astype(np.int8)
+    boards[rng.random(boards.shape) < 0.4] = 0
+    legal = O.legal_mask(boards)
+    legal[legal == 0] = 1
+    actions = np.array([[a for a in range(4) if mk >> a & 1][rng.integers(0, bin(mk).count("1"))] for mk in legal],
+                       np.uint8)
+    logp = np.log(rng.dirichlet(np.ones(4), size=M)).astype(np.float32)
+    logp[(legal[:, None] >> np.arange(4)) & 1 == 0] = -np.inf
+    data = {"boards": torch.from_numpy(boards).to(dev), "actions": torch.from_numpy(actions).to(dev),
+            "legal": torch.from_numpy(legal.astype(np.uint8)).to(dev), "logp": torch.from_numpy(logp).to(dev),
+            "adv": torch.from_numpy(rng.normal(size=M).astype(np.float32)).to(dev),
+            "ret": torch.from_numpy(rng.normal(size=M).astype(np.float32)).to(dev)}
+    idx = torch.from_numpy(rng.permutation(M)[:m].astype(np.int64)).to(dev)
+    ctr = torch.tensor([11], dtype=torch.int64, device=dev)
+    return w, gam, bet, (wa, ba, wv, bv), data, idx, ctr
+
+
+@pytest.mark.parametrize("h,M,m,p,ragged", [(196, 70000, 65536, 0.1, False), (196, 5000, 4099, 0.0, True),
+                                            (64, 3000, 1000, 0.25, False), (196, 200, 33, 0.1, True),
+                                            (192, 900, 700, 0.1, False)])
+def test_fused_train_pass_matches_layer_kernels(dev, h, M, m, p, ragged):
+    """g2048_ppo_forward_loss (the whole train forward + loss in one launch) against the per-layer
+    chain it replaces (g2048_obs_gather, g2048_mlp_fwd x 3, g2048_ppo_head_loss) on the same dropout
+    masks: x0, every layer's G / H / mean / rstd bitwise; masked logits, dz, the loss sums and the
+    bias gradients to fp32 summation order (the logits' three-term head split vs head_loss's);
+    the head weight gradient dz^T H2 on bf16 operands (autocast's rounding) to 1e-2 of its scale."""
+    from g2048 import _lib as L
+    w, gam, bet, (wa, ba, wv, bv), data, idx, ctr = _pass_case(dev, h, M, m, p, h + m)
+    rows = torch.tensor([m - 5 if ragged else m], dtype=torch.int64, device=dev)
+    beta = torch.tensor(0.03, device=dev)
+    drops = [L.make_dropout(p, l, 0, 321, 0, ctr) for l in (1, 2)]
+    bf, f32 = torch.bfloat16, torch.float32
+    # reference: the per-layer kernels
+    x0 = torch.empty(m, 48, dtype=bf, device=dev)
+    L.obs_gather(data["boards"], idx, x0)
+    G = [torch.empty(m, h, dtype=bf, device=dev) for _ in range(3)]
+    H = [torch.empty(m, h, dtype=bf, device=dev) for _ in range(3)]
+    mu = [torch.empty(m, device=dev) for _ in range(3)]
+    rs = [torch.empty(m, device=dev) for _ in range(3)]
+    x = x0
+    for l in range(3):
+        L.mlp_fwd(x, w[l], gam[l], bet[l], l > 0, G[l], H[l], mu[l], rs[l], drops[l - 1] if l > 0 else None)
+        x = H[l]
+    batch = L.make_ppo_batch(idx, data["actions"], data["legal"], data["logp"], data["adv"], data["ret"], rows=rows)
+    masked0, dz0 = torch.empty(m, 4, device=dev), torch.empty(m, 8, device=dev)
+    dwa0, dba0, dwv0, dbv0, sums0 = (torch.empty(s, device=dev) for s in ((4, h), 4, (1, h), 1, 3))
+    part = torch.empty(L.ppo_head_partials(m, h), device=dev)
+    L.ppo_head_loss(H[2], wa, ba, wv, bv, batch, beta, 0.2, 0.2, False, masked0, None, part, dwa0, dba0, dwv0, dbv0,
+                    sums0, dz=dz0)
+    # the fused pass
+    frag = torch.empty(L.head_split_bytes(h), dtype=torch.uint8, device=dev)
+    L.head_split(wa, wv, frag)
+    out = dict(x0=torch.full((m, 48), float("nan"), dtype=bf, device=dev),
+               g=[torch.full((m, h), float("nan"), dtype=bf, device=dev) for _ in range(3)],
+               h=[torch.full((m, h), float("nan"), dtype=bf, device=dev) for _ in range(3)],
+               mean=[torch.empty(m, device=dev) for _ in range(3)], rstd=[torch.empty(m, device=dev) for _ in range(3)],
+               masked=torch.full((m, 4), float("nan"), device=dev), dz=torch.empty(m, 8, device=dev),
+               dz_bf16=torch.empty(m, 8, dtype=bf, device=dev),
+               partials=torch.empty(L.mlp_pass_partials(m, True), device=dev))
+    args = L.make_mlp_pass(data["boards"], batch, m, w[0], w[1:], gam, bet, frag, ba, bv, drops=drops, beta_dev=beta,
+                           critic=0.2, clip_eps=0.2, **out)
+    dba1, dbv1, sums1 = torch.empty(4, device=dev), torch.empty(1, device=dev), torch.empty(3, device=dev)
+    L.ppo_forward_loss(args, dba1, dbv1, sums1)
+    wh = torch.empty(8, h, device=dev)
+    L.wgrad(out["dz_bf16"], out["h"][2], torch.empty(L.wgrad_partials(m, 8, h), device=dev), wh)
+    torch.cuda.synchronize()
+    bits = lambda t: t.view(torch.int16) if t.dtype == bf else t.view(torch.int32)  # noqa: E731
+    assert torch.equal(bits(out["x0"]), bits(x0))
+    for l in range(3):
+        for name, a, b in (("g", out["g"][l], G[l]), ("h", out["h"][l], H[l]), ("mean", out["mean"][l], mu[l]),
+                           ("rstd", out["rstd"][l], rs[l])):
+            assert torch.equal(bits(a), bits(b)), (name, l, (a.float() - b.float()).abs().max())
+    n = int(rows.item())
+    fin = torch.isfinite(masked0[:n])
+    assert torch.equal(fin, torch.isfinite(out["masked"][:n]))
+    torch.testing.assert_close(out["masked"][:n][fin], masked0[:n][fin], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(out["dz"], dz0, rtol=1e-4, atol=1e-4 / m)
+    assert torch.equal(out["dz"][n:], torch.zeros_like(out["dz"][n:]))
+    torch.testing.assert_close(out["dz_bf16"].float(), out["dz"].to(bf).float(), rtol=0, atol=0)
+    torch.testing.assert_close(sums1, sums0, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dba1, dba0, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(dbv1, dbv0, rtol=1e-4, atol=1e-6)
+    scale = max(dwa0.abs().max().item(), dwv0.abs().max().item())
+    torch.testing.assert_close(wh[:4], dwa0, rtol=0, atol=1e-2 * scale)
+    torch.testing.assert_close(wh[4:5], dwv0, rtol=0, atol=1e-2 * scale)
+    assert torch.equal(wh[5:], torch.zeros_like(wh[5:]))
+
+
+@pytest.mark.parametrize("h,M,m,p,ragged", [(196, 70000, 65536, 0.1, False), (196, 5000, 4099, 0.0, True),
+                                            (64, 700, 333, 0.2, True)])
+def test_fused_kl_pass_matches_layer_kernels(dev, h, M, m, p, ragged):
+    """g2048_ppo_forward_kl (the KL re-forward in one launch, dropout pass 1) against the per-layer
+    chain (g2048_obs_gather, g2048_mlp_fwd x 3, g2048_ppo_head_kl) with the same masks: KL sum and
+    max within fp32 summation-order noise."""
+    from g2048 import _lib as L
+    w, gam, bet, (wa, ba, wv, bv), data, idx, ctr = _pass_case(dev, h, M, m, p, 7 * h + m)
+    rows = torch.tensor([m - 3 if ragged else m], dtype=torch.int64, device=dev)
+    drops = [L.make_dropout(p, l, 1, 55, 0, ctr) for l in (1, 2)]
+    old = data["logp"].index_select(0, idx) + 0.3 * torch.randn(m, 4, device=dev)
+    x = torch.empty(m, 48, dtype=torch.bfloat16, device=dev)
+    L.obs_gather(data["boards"], idx, x)
+    for l in range(3):
+        y = torch.empty(m, h, dtype=torch.bfloat16, device=dev)
+        L.mlp_fwd(x, w[l], gam[l], bet[l], l > 0, None, y, None, None, drops[l - 1] if l > 0 else None)
+        x = y
+    ref, got = torch.empty(2, device=dev), torch.empty(2, device=dev)
+    L.ppo_head_kl(x, wa, ba, old, torch.empty(L.ppo_head_partials(m, h), device=dev), ref, rows=rows)
+    frag = torch.empty(L.head_split_bytes(h), dtype=torch.uint8, device=dev)
+    L.head_split(wa, None, frag)
+    batch = L.make_ppo_batch(idx, data["actions"], data["legal"], data["logp"], data["adv"], data["ret"], rows=rows)
+    args = L.make_mlp_pass(data["boards"], batch, m, w[0], w[1:], gam, bet, frag, ba, drops=drops, masked=old,
+                           partials=torch.empty(L.mlp_pass_partials(m, False), device=dev))
+    L.ppo_forward_kl(args, got)
+    torch.cuda.synchronize()
+    assert float(ref[0]) > 0
+    assert math.isclose(float(got[0]), float(ref[0]), rel_tol=1e-4, abs_tol=1e-6), (got, ref)
+    assert math.isclose(float(got[1]), float(ref[1]), rel_tol=1e-4, abs_tol=1e-6), (got, ref)
+
+
+def test_fused_passes_and_layer_chain_give_the_same_update(dev):
+    """FusedPPOUpdater with the fused passes vs the per-layer kernel chain (force_layer_kernels): one
+    graphed update of 3 minibatches (dropout on) moves every parameter the same way (cosine >= 0.999
+    per Muon matrix, 0.98 per AdamW vector) and the statistics agree to 1e-3."""
+    import agent
+    from g2048.dist import GradBucket
+    from g2048.fastmlp import FusedPPOUpdater
+    from g2048.optim import FusedMuonAdamW
+    from g2048.ppo import PPOConfig
+    _, _, _, _, data, _, _ = _pass_case(dev, 196, 3 * 4096, 1, 0.1, 99)
+    res = []
+    for force in (False, True):
+        torch.manual_seed(5)
+        mdl = agent.GameMLP(agent.MLPConfig(hidden_dim=196, dropout=0.1)).to(dev)
+        opt = FusedMuonAdamW(mdl, 1e-3, 1e-3)
+        order = [p for p, _ in opt.muon] + [p for gr in opt.adam_groups for p in gr["params"]]
+        up = FusedPPOUpdater(mdl, opt, PPOConfig(batch_size=4096), GradBucket(order),
+                             torch.Generator(device=dev).manual_seed(3), graph=True)
+        up.force_layer_kernels = force
+        before = [p.detach().clone() for p in mdl.parameters()]
+        st = up.update(data, 0.02)
+        assert up.fused_pass is (not force)
+        torch.cuda.synchronize()
+        res.append(([p.detach() - b for p, b in zip(mdl.parameters(), before)], {k: float(v) for k, v in st.items()}))
+    for (n, prm), a, b in zip(mdl.named_parameters(), res[0][0], res[1][0]):
+        cos = F.cosine_similarity(a.reshape(1, -1).double(), b.reshape(1, -1).double()).item()
+        # Muon matrices: normalised updates; AdamW's early steps are ~sign(g) (near-zero entries flip)
+        assert cos >= (0.999 if prm.ndim == 2 else 0.98), (n, cos)
+    for k in res[0][1]:
+        assert math.isclose(res[0][1][k], res[1][1][k], rel_tol=1e-3, abs_tol=1e-6), (k, res[0][1][k], res[1][1][k])

@@ -54,7 +54,7 @@ def main(src: str, dst: str):
         summary[k] = e
     (dst_p / "pmc_summary.json").write_text(json.dumps(summary, indent=1) + "\n")
     sq = collections.defaultdict(dict)
-    for sub in ("sqa", "sqb"):
+    for sub in ("sqa", "sqb", "sqc"):
         for f in (src_p / sub).rglob("*counter_collection.csv") if (src_p / sub).exists() else []:
             acc = collections.defaultdict(list)
             for r in csv.DictReader(open(f)):
