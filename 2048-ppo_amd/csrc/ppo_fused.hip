@@ -24,8 +24,9 @@
 //
 // The train pass writes what the backward needs: x0 (bf16 obs, the stem weight-gradient operand),
 // per layer G (bf16, pre-norm), H (bf16 output) and mean / rstd, masked logits (for the KL), dz as
-// fp32 [m][8] (the blocks' output gradient source) and as bf16 [m][8] (the head weight-gradient
-// operand: dW_heads = dz^T H2 runs on g2048_wgrad, autocast's bf16 operands), and per block
+// fp32 [m][8] (the blocks' output gradient source) and as two bf16 terms [m][16] (hi in columns
+// 0-4, lo = bf16(dz - hi) in 8-12: the head weight gradient dz^T H2 runs on g2048_wgrad with fp32
+// accuracy in dz, summing the hi and lo halves of its partial rows), and per block
 // partials [dba 4 | dbv | sum ppo, sum H, sum v] summed by the deferred column sum.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -65,7 +66,7 @@ struct FpArgs {
     float *mean[kMaxLayers], *rstd[kMaxLayers];
     float *masked;                 // train: [m][4] out; KL: the stored old masked logits (in)
     float *dz;                     // train: fp32 [m][8]
-    uint16_t *dzb;                 // train: bf16 [m][8]
+    uint16_t *dzb;                 // train: bf16 [m][16]: hi(dz) 0..4, lo(dz) 8..12
     float *part;                   // per block: train kTrainParts floats, KL {sum, max}
 };
 
@@ -324,8 +325,19 @@ __global__ __launch_bounds__(kFpThreads, 1) void mlp_pass_kernel(FpArgs a) {
             if (live) {
                 *reinterpret_cast<float4 *>(a.dz + r * 8) = make_float4(dz[0], dz[1], dz[2], dz[3]);
                 *reinterpret_cast<float4 *>(a.dz + r * 8 + 4) = make_float4(dz[4], 0.0f, 0.0f, 0.0f);
-                *reinterpret_cast<uint4 *>(a.dzb + r * 8) =
-                    make_uint4(pack_bf2(dz[0], dz[1]), pack_bf2(dz[2], dz[3]), pack_bf2(dz[4], 0.0f), 0u);
+                // dz as two bf16 terms (hi, lo = bf16(dz - hi)): the head weight gradient
+                // dz^T H2 = hi^T H2 + lo^T H2 keeps ~16 mantissa bits of dz (g2048_ppo_head_loss's
+                // fp32 dz x bf16 H2) on the bf16 weight-gradient kernel
+                float lo[5];
+                uint32_t hb[3];
+#pragma unroll
+                for (int k = 0; k < 5; k++) lo[k] = dz[k] - bf_lo(pack_bf2(dz[k], 0.0f));
+                hb[0] = pack_bf2(dz[0], dz[1]);
+                hb[1] = pack_bf2(dz[2], dz[3]);
+                hb[2] = pack_bf2(dz[4], 0.0f);
+                uint4 *zb = reinterpret_cast<uint4 *>(a.dzb + r * 16);
+                zb[0] = make_uint4(hb[0], hb[1], hb[2], 0u);
+                zb[1] = make_uint4(pack_bf2(lo[0], lo[1]), pack_bf2(lo[2], lo[3]), pack_bf2(lo[4], 0.0f), 0u);
             }
         } else if (real) {
             const float o[4] = {old4.x, old4.y, old4.z, old4.w};

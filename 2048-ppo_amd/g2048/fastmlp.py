@@ -47,6 +47,19 @@ def supports(model) -> bool:
     return h % 4 == 0 and h <= 1024
 
 
+def head_grad_job(job, h: int, dwa, dwv, spill):
+    """Re-describes the deferred column sum of g2048_wgrad(dz_bf16 [m, 16], H2 [m, h]) (partial rows
+    [nb][16 h]: hi^T H2 in rows 0-7, lo^T H2 in rows 8-15) as 2 nb rows of 8 h, so the one column-sum
+    adds the hi and lo halves: rows 0-3 -> dwa (action_head.weight.grad), row 4 -> dwv, 5-7 -> spill."""
+    job.nb *= 2
+    job.cols = 8 * h
+    job.nseg = 3
+    for k, (dst, n) in enumerate(((dwa, 4 * h), (dwv, h), (spill, 3 * h))):
+        job.dst[k] = dst.data_ptr()
+        job.len[k] = n
+    return job
+
+
 def _mm(a, b, out):
     """out = a @ b with fp32 accumulation (bf16 operands); fp32 `out` gets an fp32 result."""
     if out.dtype == a.dtype:
@@ -114,15 +127,15 @@ class FusedPPOUpdater(PPOUpdater):
         # the fused train / KL passes (g2048_ppo_forward_loss / _kl): dz as bf16 for the head weight
         # gradient dz^T H2 on g2048_wgrad, the head weights split for the passes' MFMA operand
         self.fused_pass = (L.mlp_pass_supported(h, nl - 1) and bs * 2 * h < 2 ** 32
-                           and L.wgrad_partials(bs, 8, h) > 0 and not self.force_layer_kernels)
+                           and L.wgrad_partials(bs, 16, h) > 0 and not self.force_layer_kernels)
         if self.fused_pass:
-            self.dzb = torch.empty(bs, 8, dtype=bf, device=d)
+            self.dzb = torch.empty(bs, 16, dtype=bf, device=d)
             self.head_frag = torch.zeros(L.head_split_bytes(h), dtype=torch.uint8, device=d)
             self.part_fwd = torch.empty(L.mlp_pass_partials(bs, True), dtype=f32, device=d)
             self.part_klp = torch.empty(L.mlp_pass_partials(bs, False), dtype=f32, device=d)
-            self.part_wh = torch.empty(L.wgrad_partials(bs, 8, h), dtype=f32, device=d)
+            self.part_wh = torch.empty(L.wgrad_partials(bs, 16, h), dtype=f32, device=d)
             self.wh_spill = torch.empty(3 * h, dtype=f32, device=d)  # rows 5..7 of dz^T H2 (zero columns)
-            self.wh_out = torch.empty(8, h, dtype=f32, device=d)    # (unused: the job's segments route it)
+            self.wh_out = torch.empty(16, h, dtype=f32, device=d)   # (unused: the job's segments route it)
         self.bs = bs
 
     def _drop(self, layer: int, pass_: int):
@@ -156,20 +169,16 @@ class FusedPPOUpdater(PPOUpdater):
 
     def fused_forward_loss(self, data, idx, beta):
         """The train pass in one launch (obs -> GameMLP -> heads -> PPO loss, dz), then the head weight
-        gradient dz^T H2 (bf16 operands, as autocast's Linear backward) on g2048_wgrad; returns the
-        deferred column-sum jobs (bias gradients / loss sums, head weight gradients)."""
+        gradient dz^T H2 on g2048_wgrad (dz as two bf16 terms: fp32-accurate, like
+        g2048_ppo_head_loss); returns the deferred column-sum jobs (bias gradients / loss sums, head
+        weight gradients)."""
         self._beta_dev = beta if torch.is_tensor(beta) else torch.tensor(float(beta), device=self.dev)
         args = self._pass_args(data, idx, 0, True)
         self._kl_args = self._pass_args(data, idx, 1, False)
         j_loss, j_head = L.ColsumJob(), L.ColsumJob()
         L.ppo_forward_loss(args, self.ba.grad, self.bv.grad, self.sums, defer=j_loss)
         L.wgrad(self.dzb, self.H[-1], self.part_wh, self.wh_out, defer=j_head)
-        # route dz^T H2 [8, h]: rows 0-3 -> action_head.weight.grad, row 4 -> value_head.weight.grad
-        h = self.h
-        j_head.nseg = 3
-        for k, (dst, n) in enumerate(((self.wa.grad, 4 * h), (self.wv.grad, h), (self.wh_spill, 3 * h))):
-            j_head.dst[k] = dst.data_ptr()
-            j_head.len[k] = n
+        head_grad_job(j_head, self.h, self.wa.grad, self.wv.grad, self.wh_spill)
         return [j_loss, j_head]
 
     # ---------------------------------------------------------------- passes --------------
@@ -288,7 +297,8 @@ class FusedPPOUpdater(PPOUpdater):
             if gn.dim() != 0:
                 gn = gn.reshape(())
             # one launch: the statistics of this minibatch, and the next minibatch's dropout counter
-            L.ppo_stats(self.sums, self.part_kl, gn.float().contiguous(), b, cfg.critic, m, self.stats, self.counter,
+            kl_part = self.part_klp if self.fused_pass else self.part_kl  # the KL kernel's partial rows
+            L.ppo_stats(self.sums, kl_part, gn.float().contiguous(), b, cfg.critic, m, self.stats, self.counter,
                         kl_rows=kl_job.nb, rows=self.rows)
 
     def _extra_snapshot(self):

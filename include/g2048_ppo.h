@@ -219,8 +219,10 @@ int g2048_mlp_fwd_kl(g2048_stream_t stream, const uint16_t *x, const uint16_t *w
  *       through g2048_head_split); its G / H / mean / rstd are bitwise
  *       those of g2048_mlp_fwd.  Writes x0 (bf16 [m,48], optional), g[l] / h[l] (bf16 [m,h], optional
  *       each: h[2] is the head weight-gradient operand), mean[l] / rstd[l] (optional pairs), masked
- *       (fp32 [m,4]), dz (fp32 [m,8], g2048_dy.dz) and dz_bf16 (bf16 [m,8]: columns 0..4 = dz, the
- *       operand of dW_heads = dz^T h[2] on g2048_wgrad), and reduces dba [4], dbv [1] and sums [3] =
+ *       (fp32 [m,4]), dz (fp32 [m,8], g2048_dy.dz) and dz_bf16 (bf16 [m,16]: dz as two bf16 terms,
+ *       hi = bf16(dz) in columns 0..4 and lo = bf16(dz - hi) in 8..12, zeros elsewhere: the operand of
+ *       dW_heads = hi^T h[2] + lo^T h[2] on g2048_wgrad, whose [16][h] partial rows summed as 2 nb rows
+ *       of 8 h give the fp32-accurate head gradient), and reduces dba [4], dbv [1] and sums [3] =
  *       {sum ppo, sum H, sum v} through g2048_mlp_pass_partials(m, 1) floats of partials.
  *   g2048_ppo_forward_kl  the KL re-forward (train.py:578-601) with the updated weights and the
  *       dropout draw of pass 1 (drop[].pass): KL(old || new) against `masked` (the train pass's

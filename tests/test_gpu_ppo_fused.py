@@ -921,7 +921,7 @@ def test_fused_train_pass_matches_layer_kernels(dev, h, M, m, p, ragged):
     chain it replaces (g2048_obs_gather, g2048_mlp_fwd x 3, g2048_ppo_head_loss) on the same dropout
     masks: x0, every layer's G / H / mean / rstd bitwise; masked logits, dz, the loss sums and the
     bias gradients to fp32 summation order (the logits' three-term head split vs head_loss's);
-    the head weight gradient dz^T H2 on bf16 operands (autocast's rounding) to 1e-2 of its scale."""
+    the head weight gradient hi^T H2 + lo^T H2 (dz as two bf16 terms) to 1e-4 of its scale."""
     from g2048 import _lib as L
     w, gam, bet, (wa, ba, wv, bv), data, idx, ctr = _pass_case(dev, h, M, m, p, h + m)
     rows = torch.tensor([m - 5 if ragged else m], dtype=torch.int64, device=dev)
@@ -953,14 +953,15 @@ def test_fused_train_pass_matches_layer_kernels(dev, h, M, m, p, ragged):
                h=[torch.full((m, h), float("nan"), dtype=bf, device=dev) for _ in range(3)],
                mean=[torch.empty(m, device=dev) for _ in range(3)], rstd=[torch.empty(m, device=dev) for _ in range(3)],
                masked=torch.full((m, 4), float("nan"), device=dev), dz=torch.empty(m, 8, device=dev),
-               dz_bf16=torch.empty(m, 8, dtype=bf, device=dev),
+               dz_bf16=torch.empty(m, 16, dtype=bf, device=dev),
                partials=torch.empty(L.mlp_pass_partials(m, True), device=dev))
     args = L.make_mlp_pass(data["boards"], batch, m, w[0], w[1:], gam, bet, frag, ba, bv, drops=drops, beta_dev=beta,
                            critic=0.2, clip_eps=0.2, **out)
     dba1, dbv1, sums1 = torch.empty(4, device=dev), torch.empty(1, device=dev), torch.empty(3, device=dev)
     L.ppo_forward_loss(args, dba1, dbv1, sums1)
-    wh = torch.empty(8, h, device=dev)
-    L.wgrad(out["dz_bf16"], out["h"][2], torch.empty(L.wgrad_partials(m, 8, h), device=dev), wh)
+    wh2 = torch.empty(16, h, device=dev)
+    L.wgrad(out["dz_bf16"], out["h"][2], torch.empty(L.wgrad_partials(m, 16, h), device=dev), wh2)
+    wh = wh2[:8] + wh2[8:]  # hi^T H2 + lo^T H2 (FusedPPOUpdater sums the halves in the column sum)
     torch.cuda.synchronize()
     bits = lambda t: t.view(torch.int16) if t.dtype == bf else t.view(torch.int32)  # noqa: E731
     assert torch.equal(bits(out["x0"]), bits(x0))
@@ -974,13 +975,16 @@ def test_fused_train_pass_matches_layer_kernels(dev, h, M, m, p, ragged):
     torch.testing.assert_close(out["masked"][:n][fin], masked0[:n][fin], rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(out["dz"], dz0, rtol=1e-4, atol=1e-4 / m)
     assert torch.equal(out["dz"][n:], torch.zeros_like(out["dz"][n:]))
-    torch.testing.assert_close(out["dz_bf16"].float(), out["dz"].to(bf).float(), rtol=0, atol=0)
+    hi = out["dz"].to(bf)
+    lo = (out["dz"] - hi.float()).to(bf)
+    assert torch.equal(bits(out["dz_bf16"][:, :5].contiguous()), bits(hi[:, :5].contiguous()))
+    assert torch.equal(bits(out["dz_bf16"][:, 8:13].contiguous()), bits(lo[:, :5].contiguous()))
     torch.testing.assert_close(sums1, sums0, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dba1, dba0, rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(dbv1, dbv0, rtol=1e-4, atol=1e-6)
     scale = max(dwa0.abs().max().item(), dwv0.abs().max().item())
-    torch.testing.assert_close(wh[:4], dwa0, rtol=0, atol=1e-2 * scale)
-    torch.testing.assert_close(wh[4:5], dwv0, rtol=0, atol=1e-2 * scale)
+    torch.testing.assert_close(wh[:4], dwa0, rtol=0, atol=1e-4 * scale)
+    torch.testing.assert_close(wh[4:5], dwv0, rtol=0, atol=1e-4 * scale)
     assert torch.equal(wh[5:], torch.zeros_like(wh[5:]))
 
 
@@ -1016,32 +1020,44 @@ def test_fused_kl_pass_matches_layer_kernels(dev, h, M, m, p, ragged):
 
 
 def test_fused_passes_and_layer_chain_give_the_same_update(dev):
-    """FusedPPOUpdater with the fused passes vs the per-layer kernel chain (force_layer_kernels): one
-    graphed update of 3 minibatches (dropout on) moves every parameter the same way (cosine >= 0.999
-    per Muon matrix, 0.98 per AdamW vector) and the statistics agree to 1e-3."""
+    """FusedPPOUpdater with the fused passes vs the per-layer kernel chain (force_layer_kernels), same
+    dropout masks: the minibatch gradient of every parameter agrees (cosine >= 0.99999: fp32 summation
+    order of the logits and the hi / lo head-gradient split), and a whole graphed update of 3
+    minibatches gives the same statistics (loss terms, entropy, KL) to 1e-2."""
     import agent
     from g2048.dist import GradBucket
     from g2048.fastmlp import FusedPPOUpdater
     from g2048.optim import FusedMuonAdamW
     from g2048.ppo import PPOConfig
     _, _, _, _, data, _, _ = _pass_case(dev, 196, 3 * 4096, 1, 0.1, 99)
-    res = []
+    idx = torch.randperm(3 * 4096, device=dev)[:4096]
+    grads, stats = [], []
     for force in (False, True):
-        torch.manual_seed(5)
-        mdl = agent.GameMLP(agent.MLPConfig(hidden_dim=196, dropout=0.1)).to(dev)
-        opt = FusedMuonAdamW(mdl, 1e-3, 1e-3)
-        order = [p for p, _ in opt.muon] + [p for gr in opt.adam_groups for p in gr["params"]]
-        up = FusedPPOUpdater(mdl, opt, PPOConfig(batch_size=4096), GradBucket(order),
-                             torch.Generator(device=dev).manual_seed(3), graph=True)
-        up.force_layer_kernels = force
-        before = [p.detach().clone() for p in mdl.parameters()]
-        st = up.update(data, 0.02)
-        assert up.fused_pass is (not force)
-        torch.cuda.synchronize()
-        res.append(([p.detach() - b for p, b in zip(mdl.parameters(), before)], {k: float(v) for k, v in st.items()}))
-    for (n, prm), a, b in zip(mdl.named_parameters(), res[0][0], res[1][0]):
+        for full in (False, True):
+            torch.manual_seed(5)
+            mdl = agent.GameMLP(agent.MLPConfig(hidden_dim=196, dropout=0.1)).to(dev).train()
+            with torch.no_grad():  # non-zero heads (the trainer zeroes them; here they must carry signal)
+                mdl.action_head.weight.normal_(0, 0.05)
+                mdl.value_head.weight.normal_(0, 0.05)
+            opt = FusedMuonAdamW(mdl, 1e-3, 1e-3)
+            order = [p for p, _ in opt.muon] + [p for gr in opt.adam_groups for p in gr["params"]]
+            up = FusedPPOUpdater(mdl, opt, PPOConfig(batch_size=4096), GradBucket(order),
+                                 torch.Generator(device=dev).manual_seed(3), graph=True)
+            up.force_layer_kernels = force
+            if full:
+                st = up.update(data, 0.02)
+                assert up.fused_pass is (not force)
+                stats.append({k: float(v) for k, v in st.items()})
+            else:
+                up._alloc(4096)
+                up.refresh_weights()
+                up.beta_t.fill_(0.02)
+                up._pre(idx, data, up.beta_t, None)
+                torch.cuda.synchronize()
+                grads.append([p.grad.clone() for p in mdl.parameters()])
+    for (n, _), a, b in zip(mdl.named_parameters(), grads[0], grads[1]):
         cos = F.cosine_similarity(a.reshape(1, -1).double(), b.reshape(1, -1).double()).item()
-        # Muon matrices: normalised updates; AdamW's early steps are ~sign(g) (near-zero entries flip)
-        assert cos >= (0.999 if prm.ndim == 2 else 0.98), (n, cos)
-    for k in res[0][1]:
-        assert math.isclose(res[0][1][k], res[1][1][k], rel_tol=1e-3, abs_tol=1e-6), (k, res[0][1][k], res[1][1][k])
+        print(n, f"grad cos {cos:.7f}")
+        assert cos >= 0.99999, (n, cos)
+    for k in stats[0]:
+        assert math.isclose(stats[0][k], stats[1][k], rel_tol=1e-2, abs_tol=1e-6), (k, stats[0][k], stats[1][k])
