@@ -16,6 +16,7 @@
 // a matrix is one block and all matrices of the model run concurrently.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/g2048_ppo.h"
 
@@ -135,6 +136,7 @@ struct MuonArgs {
     float *norm_out, *coef_out;  // written by block 0 when partials is set
     AdamArgs adam;               // adam.count > 0: blocks count .. count + nadam - 1 run AdamW
     int nadam;
+    int generic_ns;              // 1: square matrices on the generic schedule too (A/B timing, tests)
 };
 
 // LDS images are row-major bf16 with the K dimension zero-padded to a multiple of 8 (pitch =
@@ -326,6 +328,186 @@ __device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_
     }
 }
 
+// ------------------------------------------------------------------ square Newton-Schulz ------
+// the square sizes of the fast path: 0 = generic schedule
+__host__ __device__ constexpr int ns_square_kind(int n) {
+    return n == 196 ? 1 : n == 192 ? 2 : n == 128 ? 3 : n == 64 ? 4 : n == 32 ? 5 : 0;
+}
+
+// Row pitch (bytes) of an LDS image with `cols` columns of a matrix whose other side is `rows`.
+// The square fast path pads to a pitch of 16 * (2 * odd) bytes: a 16 x 16 row-fragment read
+// (ds_read_b128, lane (g, c) -> row c, 16-byte unit g) then hits 16 distinct 4-bank groups in each
+// of its four lane groups (P / 16 = 25 at 196 columns puts lanes 3 and 20 on one group: 2-way).
+__host__ __device__ constexpr int muon_pitch(int rows, int cols) {
+    return rows == cols && ns_square_kind(cols) ? (cols == 196 || cols == 192 ? 416 : cols == 128 ? 288 : cols == 64 ? 160 : 96)
+                                                : ((cols + 7) & ~7) * 2;
+}
+// The h x h block weights (the update's critical path: every matrix of the model runs in its own
+// block of one launch, the square ones take the longest) on a compile-time schedule:
+//   * 2 x 2-tile blocks (four 16 x 16 accumulators; each A / B fragment feeds two MFMAs), the k loop
+//     unrolled (KS k-steps of 32), every LDS address a per-lane base plus immediates.  Rows past
+//     the n valid ones are clamped to the last (they only feed outputs that are never stored), the
+//     K overflow of the last k-step (k >= round8(n): the next row's data) is cut by zeroing those B
+//     fragments;
+//   * G = X X^T and U = b G + c G G are symmetric: only the blocks on and above the diagonal are
+//     computed, each off-diagonal tile stored twice (transposed and mirrored);
+//   * the blocks of each product go to the 8 waves by a greedy longest-first assignment that
+//     balances the four SIMDs first, then the two waves (w, w + 4) of each SIMD.
+// Per output tile the MFMA sequence (init from the scaled old value, k-steps in order) is the
+// generic path's, so both compute bitwise the same iterate.
+constexpr int kNsMaxPerWave = 10;
+
+struct NsSchedule {
+    uint8_t blk[2][8][kNsMaxPerWave];  // [sym][wave][i] = bi | bj << 4
+    uint8_t cnt[2][8];
+    constexpr NsSchedule(int NT) : blk{}, cnt{} {
+        const int NB = (NT + 1) / 2;
+        for (int sym = 0; sym < 2; sym++) {
+            int bi_[64] = {}, bj_[64] = {}, cost[64] = {}, n = 0;
+            for (int bi = 0; bi < NB; bi++)
+                for (int bj = sym ? bi : 0; bj < NB; bj++) {
+                    bi_[n] = bi;
+                    bj_[n] = bj;
+                    cost[n] = 4;  // edge blocks (odd NT) run all four tiles too
+                    n++;
+                }
+            for (int i = 1; i < n; i++)  // stable insertion sort, cost descending
+                for (int j = i; j > 0 && cost[j] > cost[j - 1]; j--) {
+                    int t = cost[j]; cost[j] = cost[j - 1]; cost[j - 1] = t;
+                    t = bi_[j]; bi_[j] = bi_[j - 1]; bi_[j - 1] = t;
+                    t = bj_[j]; bj_[j] = bj_[j - 1]; bj_[j - 1] = t;
+                }
+            int simd[4] = {}, wave[8] = {};
+            for (int i = 0; i < n; i++) {
+                int sm = 0;
+                for (int k = 1; k < 4; k++)
+                    if (simd[k] < simd[sm]) sm = k;
+                const int w = wave[sm] <= wave[sm + 4] ? sm : sm + 4;
+                simd[sm] += cost[i];
+                wave[w] += cost[i];
+                blk[sym][w][cnt[sym][w]++] = (uint8_t)(bi_[i] | (bj_[i] << 4));
+            }
+        }
+    }
+};
+// the most blocks one wave gets (the register budget of its accumulators)
+constexpr int ns_max_blocks(int NT, int sym) {
+    const NsSchedule s(NT);
+    int m = 0;
+    for (int w = 0; w < 8; w++) m = s.cnt[sym][w] > m ? s.cnt[sym][w] : m;
+    return m;
+}
+static_assert(ns_max_blocks(13, 0) <= 7 && ns_max_blocks(13, 1) <= 4, "NT = 13 schedule");
+__constant__ const NsSchedule kNs13 = NsSchedule(13);
+__constant__ const NsSchedule kNs12 = NsSchedule(12);
+__constant__ const NsSchedule kNs8 = NsSchedule(8);
+__constant__ const NsSchedule kNs4 = NsSchedule(4);
+__constant__ const NsSchedule kNs2 = NsSchedule(2);
+
+// One product of the square schedule: out <- transpose(alpha * (init + A B)) over this wave's
+// blocks, init = (beta / alpha) * old out (transposed) when beta != 0; K = M = N = n, row pitch P.
+template <int NT, int KS, int P, bool SYM, bool AROWS>
+__device__ __forceinline__ void ns_product(const NsSchedule &sch, const char *A, const char *B, char *out, int n,
+                                           float alpha, float beta, int wave, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, c = lane & 15;
+    const int cnt = sch.cnt[SYM][wave];
+    const float ratio = beta / alpha;
+    const int kpad = (n + 7) & ~7;
+    // per-lane LDS bases: row reads (lane (g, c) -> row c, k = 8 g) and transposing reads (lane
+    // (g, q, p) -> row 8 g + q, column 4 p)
+    const int ltr = (8 * g + q) * P + 8 * p;
+    constexpr int MAXB = ns_max_blocks(NT, SYM);
+    f32x4_t acc[MAXB][2][2];
+#pragma unroll
+    for (int u = 0; u < MAXB; u++) {
+        if (u >= cnt) continue;  // wave-uniform
+        const int bb = sch.blk[SYM][wave][u], ti0 = 2 * (bb & 15), tj0 = 2 * (bb >> 4);
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 2; y++) {
+                f32x4_t a0 = {0.0f, 0.0f, 0.0f, 0.0f};
+                if (beta != 0.0f) {  // the old value, scaled (clamped into the image: unused lanes never store)
+                    const int orow = min(16 * (tj0 + y) + c, n - 1), ocol = min(16 * (ti0 + x) + 4 * g, n - 4);
+                    const uint2 w = *reinterpret_cast<const uint2 *>(out + orow * P + ocol * 2);
+                    a0 = f32x4_t{ratio * bf2f(w.x & 0xFFFFu), ratio * bf2f(w.x >> 16), ratio * bf2f(w.y & 0xFFFFu),
+                                 ratio * bf2f(w.y >> 16)};
+                }
+                acc[u][x][y] = a0;
+            }
+        // row c of each tile, clamped to the last valid row (rows >= n only feed unstored outputs)
+        const char *pa0 = AROWS ? A + min(16 * ti0 + c, n - 1) * P + 16 * g : A + ltr + 32 * ti0;
+        const char *pa1 = AROWS ? A + min(16 * ti0 + 16 + c, n - 1) * P + 16 * g : pa0 + 32;
+        const char *pb0 = B + min(16 * tj0 + c, n - 1) * P + 16 * g;
+        const char *pb1 = B + min(16 * tj0 + 16 + c, n - 1) * P + 16 * g;
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            bf16x8_t fa[2], fb[2];
+#pragma unroll
+            for (int y = 0; y < 2; y++) {
+                uint4 v = *reinterpret_cast<const uint4 *>((y ? pb1 : pb0) + 64 * ks);
+                if (ks == KS - 1 && 32 * KS > kpad) {  // k >= round8(n) reads the next row: zero
+                    const bool kin = 32 * ks + 8 * g < kpad;
+                    v = kin ? v : make_uint4(0u, 0u, 0u, 0u);
+                }
+                fb[y] = __builtin_bit_cast(bf16x8_t, v);
+            }
+#pragma unroll
+            for (int x = 0; x < 2; x++) {
+                if (AROWS) {
+                    fa[x] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>((x ? pa1 : pa0) + 64 * ks));
+                } else {  // A = X^T: X[32 ks + 8 g + j][16 ti + i], two transposing reads (rows past
+                          // n fall in the G image behind X: finite, and their B is zero)
+                    const char *a1 = (x ? pa1 : pa0) + 32 * ks * P;
+                    const s16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)a1);
+                    const s16x4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(a1 + 4 * P));
+                    fa[x] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(t1, t2, 0, 1, 2, 3, 4, 5, 6, 7));
+                }
+            }
+#pragma unroll
+            for (int x = 0; x < 2; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++)
+                    acc[u][x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[x], fb[y], acc[u][x][y], 0, 0, 0);
+        }
+    }
+    __syncthreads();  // every read of the old `out` (and of A / B when they alias it) is done
+#pragma unroll
+    for (int u = 0; u < MAXB; u++) {
+        if (u >= cnt) continue;
+        const int bb = sch.blk[SYM][wave][u], ti0 = 2 * (bb & 15), tj0 = 2 * (bb >> 4);
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 2; y++) {
+                const int ti = ti0 + x, tj = tj0 + y;
+                const int col = 16 * tj + c, row0 = 16 * ti + 4 * g;
+                if (col >= n || row0 >= n) continue;
+                const f32x4_t v = acc[u][x][y];
+                const uint32_t w0 = pack_bf2(alpha * v[0], alpha * v[1]), w1 = pack_bf2(alpha * v[2], alpha * v[3]);
+                *reinterpret_cast<uint2 *>(out + col * P + row0 * 2) = make_uint2(w0, w1);  // transposed
+                if (SYM && ti < tj) {  // the mirrored tile of a symmetric product: out[row][col]
+                    uint16_t *o = reinterpret_cast<uint16_t *>(out + row0 * P + col * 2);
+                    o[0] = (uint16_t)(w0 & 0xFFFFu);
+                    o[P / 2] = (uint16_t)(w0 >> 16);
+                    o[P] = (uint16_t)(w1 & 0xFFFFu);
+                    o[3 * P / 2] = (uint16_t)(w1 >> 16);
+                }
+            }
+    }
+    __syncthreads();
+}
+
+template <int NT, int KS, int P>
+__device__ __forceinline__ void ns_square(const NsSchedule &sch, char *sX, char *sG, int n, const MuonArgs &args,
+                                          int wave, int lane) {
+    for (int it = 0; it < args.steps; it++) {
+        ns_product<NT, KS, P, true, true>(sch, sX, sX, sG, n, 1.0f, 0.0f, wave, lane);      // G = X X^T
+        ns_product<NT, KS, P, true, true>(sch, sG, sG, sG, n, args.c, args.b, wave, lane);  // U = b G + c G G
+        ns_product<NT, KS, P, false, false>(sch, sX, sG, sX, n, 1.0f, args.a, wave, lane);  // X = a X + U X
+    }
+}
+
 __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if ((int)blockIdx.x >= args.count) {  // the 1-D parameters' AdamW, in the same launch
@@ -352,7 +534,7 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     const int R = mt.rows, C = mt.cols;
     const bool tr = R > C;  // iterate on the wide orientation (r <= c), like torch
     const int r = tr ? C : R, c = tr ? R : C;
-    const int px = ((c + 7) & ~7) * 2, pg = ((r + 7) & ~7) * 2;  // padded row pitches (bytes)
+    const int px = muon_pitch(r, c), pg = muon_pitch(r, r);  // padded row pitches (bytes)
     char *sX = smem;
     char *sG = smem + ((r * px + 127) & ~127);
     char *zero = sG + ((r * pg + 127) & ~127);  // 64 zero bytes
@@ -412,6 +594,16 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     //   1: U = b G + c G G                (A = G rows, B^T = G rows; U symmetric)
     //   2: X^T = a X^T + X^T U            (A = X^T by the transposing read, B^T = U rows)
     // Every product stores its transpose (= G, U, and X itself for phase 2).
+    const int kind = r == c && !args.generic_ns ? ns_square_kind(r) : 0;
+    if (kind) {  // the square fast path (row pitch muon_pitch(n, n))
+        switch (kind) {
+        case 1: ns_square<13, 7, 416>(kNs13, sX, sG, r, args, wave, lane); break;
+        case 2: ns_square<12, 6, 416>(kNs12, sX, sG, r, args, wave, lane); break;
+        case 3: ns_square<8, 4, 288>(kNs8, sX, sG, r, args, wave, lane); break;
+        case 4: ns_square<4, 2, 160>(kNs4, sX, sG, r, args, wave, lane); break;
+        default: ns_square<2, 1, 96>(kNs2, sX, sG, r, args, wave, lane); break;
+        }
+    } else {
     f32x4_t acc[kBI][kBJ];
     for (int ph = 0; ph < 3 * args.steps; ph++) {
         const int k = ph % 3;
@@ -429,6 +621,7 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
         __syncthreads();
         store_block_t(acc, out, po, M, N, ti0, tj0, alpha, lane);
         __syncthreads();
+    }
     }
 
     // decoupled weight decay + the match_rms_adamw-scaled update, and the bf16 weight copy
@@ -457,7 +650,7 @@ inline int status() {
 
 inline size_t muon_lds_bytes(int R, int C) {
     const int r = R > C ? C : R, c = R > C ? R : C;
-    const int px = ((c + 7) & ~7) * 2, pg = ((r + 7) & ~7) * 2;
+    const int px = muon_pitch(r, c), pg = muon_pitch(r, r);
     return (size_t)((r * px + 127) & ~127) + (size_t)((r * pg + 127) & ~127) + 64;
 }
 
@@ -560,6 +753,7 @@ static int muon_launch(g2048_stream_t stream, const g2048_muon_matrix *mats, int
     a.max_norm = max_norm;
     a.norm_out = norm_out;
     a.coef_out = coef_out;
+    a.generic_ns = getenv("G2048_MUON_GENERIC") ? 1 : 0;
     if (adam) {  // AdamW blocks: ~2 elements per thread, at most 8 blocks
         a.adam = *adam;
         int64_t nmax = 0;

@@ -1061,3 +1061,36 @@ def test_fused_passes_and_layer_chain_give_the_same_update(dev):
         assert cos >= 0.99999, (n, cos)
     for k in stats[0]:
         assert math.isclose(stats[0][k], stats[1][k], rel_tol=1e-2, abs_tol=1e-6), (k, stats[0][k], stats[1][k])
+
+
+@pytest.mark.parametrize("h", [196, 192, 128, 64])
+def test_muon_square_schedule_equals_generic(dev, h, monkeypatch):
+    """The square Newton-Schulz schedule of muon_kernel (symmetric G and U on the upper-triangle
+    2 x 2-tile blocks, load-balanced block lists) computes bitwise the update of the generic 7 x 4
+    tile-block schedule (G2048_MUON_GENERIC=1): same MFMA sequence per output tile."""
+    import agent
+    from g2048.dist import GradBucket
+    from g2048.optim import FusedMuonAdamW
+    torch.manual_seed(h)
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=h, num_layers=2)).to(dev)
+    opt = FusedMuonAdamW(m, 1e-3, 1e-4)
+    order = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
+    bk = GradBucket(order)
+    snap = opt.snapshot()
+    outs = []
+    for generic in (True, False):
+        torch.manual_seed(1)
+        with torch.no_grad():
+            for p in m.parameters():
+                p.copy_(torch.randn_like(p) * 0.05)
+        opt.restore(snap)
+        if generic:
+            monkeypatch.setenv("G2048_MUON_GENERIC", "1")
+        else:
+            monkeypatch.delenv("G2048_MUON_GENERIC", raising=False)
+        for s in range(3):
+            bk.flat.copy_(torch.randn(bk.flat.shape, generator=torch.Generator().manual_seed(s)).to(dev) * 1e-2)
+            opt.step_clipped(bk.flat, 1.0)
+        torch.cuda.synchronize()
+        outs.append(torch.cat([p.detach().reshape(-1) for p in m.parameters()]).clone())
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()

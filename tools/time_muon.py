@@ -12,7 +12,7 @@ sys.path[:0] = [str(ROOT), str(ROOT / "2048-ppo_amd")]
 def main():
     from g2048 import _lib as L
     if len(sys.argv) > 1 and sys.argv[1] != "-":
-        L.load(sys.argv[1])
+        L._lib = L.load(sys.argv[1])  # every wrapper then calls this build
     import agent
     from g2048.dist import GradBucket
     from g2048.optim import FusedMuonAdamW
