@@ -343,39 +343,57 @@ __host__ __device__ constexpr int muon_pitch(int rows, int cols) {
                                                 : ((cols + 7) & ~7) * 2;
 }
 // The h x h block weights (the update's critical path: every matrix of the model runs in its own
-// block of one launch, the square ones take the longest) on a compile-time schedule:
-//   * 2 x 2-tile blocks (four 16 x 16 accumulators; each A / B fragment feeds two MFMAs), the k loop
-//     unrolled (KS k-steps of 32), every LDS address a per-lane base plus immediates.  Rows past
-//     the n valid ones are clamped to the last (they only feed outputs that are never stored), the
-//     K overflow of the last k-step (k >= round8(n): the next row's data) is cut by zeroing those B
-//     fragments;
-//   * G = X X^T and U = b G + c G G are symmetric: only the blocks on and above the diagonal are
-//     computed, each off-diagonal tile stored twice (transposed and mirrored);
-//   * the blocks of each product go to the 8 waves by a greedy longest-first assignment that
-//     balances the four SIMDs first, then the two waves (w, w + 4) of each SIMD.
+// block of one launch, the square ones take the longest) on a schedule fixed at compile time:
+//   * the NT = ceil(n / 16) tile rows split into parts of at most 4 tiles (13 = 4+3+3+3, 12 =
+//     3+3+3+3, 8 = 4+4); a block is part x part (up to 16 accumulators: 8 fragment reads per k-step for 16
+//     MFMAs -- the CU's LDS, shared by its four SIMDs, then keeps pace with the matrix cores);
+//   * the blocks of a product go to the 8 waves by a greedy longest-first assignment that balances
+//     the four SIMDs, then the two waves (w, w + 4) of each; every wave runs its own straight-line
+//     code (a switch on the wave index), so accumulators, LDS addresses and edge clamps are all
+//     compile-time: rows past n are clamped to the last (they only feed outputs that are never
+//     stored) and the K overflow of the last k-step (k >= round8(n): the next row's data) is cut by
+//     zeroing those B fragments;
+//   * G = X X^T and U = b G + c G G are symmetric: only tiles on and above the diagonal are
+//     computed, each off-diagonal one stored twice (transposed and mirrored).
 // Per output tile the MFMA sequence (init from the scaled old value, k-steps in order) is the
 // generic path's, so both compute bitwise the same iterate.
-constexpr int kNsMaxPerWave = 10;
+constexpr int kNsMaxBlocks = 8;  // per wave and product
+constexpr int kNsMaxTiles = 32;  // accumulator tiles per wave (128 VGPRs)
+
+struct NsParts {
+    int n, start[4], size[4];
+    // ceil(NT / 4) parts, but at least 4 from 12 tiles up (4 x 4 = 16 blocks spread evenly over 4 SIMDs)
+    constexpr NsParts(int NT) : n(NT >= 12 ? ((NT + 3) / 4 > 4 ? (NT + 3) / 4 : 4) : (NT + 3) / 4), start{}, size{} {
+        const int base = NT / n, extra = NT % n;
+        int s0 = 0;
+        for (int i = 0; i < n; i++) {
+            size[i] = base + (i < extra ? 1 : 0);
+            start[i] = s0;
+            s0 += size[i];
+        }
+    }
+};
 
 struct NsSchedule {
-    uint8_t blk[2][8][kNsMaxPerWave];  // [sym][wave][i] = bi | bj << 4
-    uint8_t cnt[2][8];
-    constexpr NsSchedule(int NT) : blk{}, cnt{} {
-        const int NB = (NT + 1) / 2;
+    int bi[2][8][kNsMaxBlocks], bj[2][8][kNsMaxBlocks];  // [sym][wave][i]: part indices
+    int cnt[2][8], tiles[2][8];
+    constexpr NsSchedule(int NT) : bi{}, bj{}, cnt{}, tiles{} {
+        const NsParts pt(NT);
         for (int sym = 0; sym < 2; sym++) {
-            int bi_[64] = {}, bj_[64] = {}, cost[64] = {}, n = 0;
-            for (int bi = 0; bi < NB; bi++)
-                for (int bj = sym ? bi : 0; bj < NB; bj++) {
-                    bi_[n] = bi;
-                    bj_[n] = bj;
-                    cost[n] = 4;  // edge blocks (odd NT) run all four tiles too
+            int ai[16] = {}, aj[16] = {}, cost[16] = {}, n = 0;
+            for (int i = 0; i < pt.n; i++)
+                for (int j = sym ? i : 0; j < pt.n; j++) {
+                    ai[n] = i;
+                    aj[n] = j;
+                    // MFMA work: a symmetric product's diagonal block runs its upper triangle only
+                    cost[n] = sym && i == j ? pt.size[i] * (pt.size[i] + 1) / 2 : pt.size[i] * pt.size[j];
                     n++;
                 }
             for (int i = 1; i < n; i++)  // stable insertion sort, cost descending
                 for (int j = i; j > 0 && cost[j] > cost[j - 1]; j--) {
                     int t = cost[j]; cost[j] = cost[j - 1]; cost[j - 1] = t;
-                    t = bi_[j]; bi_[j] = bi_[j - 1]; bi_[j - 1] = t;
-                    t = bj_[j]; bj_[j] = bj_[j - 1]; bj_[j - 1] = t;
+                    t = ai[j]; ai[j] = ai[j - 1]; ai[j - 1] = t;
+                    t = aj[j]; aj[j] = aj[j - 1]; aj[j - 1] = t;
                 }
             int simd[4] = {}, wave[8] = {};
             for (int i = 0; i < n; i++) {
@@ -385,126 +403,186 @@ struct NsSchedule {
                 const int w = wave[sm] <= wave[sm + 4] ? sm : sm + 4;
                 simd[sm] += cost[i];
                 wave[w] += cost[i];
-                blk[sym][w][cnt[sym][w]++] = (uint8_t)(bi_[i] | (bj_[i] << 4));
+                bi[sym][w][cnt[sym][w]] = ai[i];
+                bj[sym][w][cnt[sym][w]] = aj[i];
+                cnt[sym][w]++;
+                tiles[sym][w] += pt.size[ai[i]] * pt.size[aj[i]];  // accumulator slots
             }
         }
+    }
+    constexpr int offset(int sym, int w, int u, const NsParts &pt) const {  // first slot of block u
+        int o = 0;
+        for (int i = 0; i < u; i++) o += pt.size[bi[sym][w][i]] * pt.size[bj[sym][w][i]];
+        return o;
     }
 };
-// the most blocks one wave gets (the register budget of its accumulators)
-constexpr int ns_max_blocks(int NT, int sym) {
-    const NsSchedule s(NT);
-    int m = 0;
-    for (int w = 0; w < 8; w++) m = s.cnt[sym][w] > m ? s.cnt[sym][w] : m;
-    return m;
-}
-static_assert(ns_max_blocks(13, 0) <= 7 && ns_max_blocks(13, 1) <= 4, "NT = 13 schedule");
-__constant__ const NsSchedule kNs13 = NsSchedule(13);
-__constant__ const NsSchedule kNs12 = NsSchedule(12);
-__constant__ const NsSchedule kNs8 = NsSchedule(8);
-__constant__ const NsSchedule kNs4 = NsSchedule(4);
-__constant__ const NsSchedule kNs2 = NsSchedule(2);
 
-// One product of the square schedule: out <- transpose(alpha * (init + A B)) over this wave's
-// blocks, init = (beta / alpha) * old out (transposed) when beta != 0; K = M = N = n, row pitch P.
-template <int NT, int KS, int P, bool SYM, bool AROWS>
-__device__ __forceinline__ void ns_product(const NsSchedule &sch, const char *A, const char *B, char *out, int n,
-                                           float alpha, float beta, int wave, int lane) {
-    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, c = lane & 15;
-    const int cnt = sch.cnt[SYM][wave];
-    const float ratio = beta / alpha;
-    const int kpad = (n + 7) & ~7;
-    // per-lane LDS bases: row reads (lane (g, c) -> row c, k = 8 g) and transposing reads (lane
-    // (g, q, p) -> row 8 g + q, column 4 p)
-    const int ltr = (8 * g + q) * P + 8 * p;
-    constexpr int MAXB = ns_max_blocks(NT, SYM);
-    f32x4_t acc[MAXB][2][2];
+constexpr bool ns_schedule_fits(int NT) {
+    const NsSchedule s(NT);
+    for (int sym = 0; sym < 2; sym++)
+        for (int w = 0; w < 8; w++)
+            if (s.cnt[sym][w] > kNsMaxBlocks || s.tiles[sym][w] > kNsMaxTiles) return false;
+    return true;
+}
+static_assert(ns_schedule_fits(13) && ns_schedule_fits(12) && ns_schedule_fits(8) && ns_schedule_fits(4) &&
+                  ns_schedule_fits(2), "square Newton-Schulz schedule exceeds the register budget");
+
+template <int N>
+struct NsShape {
+    static constexpr int NT = (N + 15) / 16, KPAD = (N + 7) & ~7, KS = (KPAD + 31) / 32;
+    static constexpr int P = muon_pitch(N, N);
+};
+
+// init + k loop of one BI x BJ block at tiles (TI0, TJ0) into acc[OFF ...]
+template <int N, bool SYM, bool AROWS, int BI, int BJ, int TI0, int TJ0, int OFF, int T>
+__device__ __forceinline__ void ns_block(f32x4_t (&acc)[T], const char *A, const char *B, const char *out,
+                                         float ratio, bool init, int g, int c, int ltr) {
+    using S = NsShape<N>;
+    constexpr int P = S::P;
+    constexpr bool DIAG = SYM && TI0 == TJ0;  // upper triangle only
 #pragma unroll
-    for (int u = 0; u < MAXB; u++) {
-        if (u >= cnt) continue;  // wave-uniform
-        const int bb = sch.blk[SYM][wave][u], ti0 = 2 * (bb & 15), tj0 = 2 * (bb >> 4);
+    for (int x = 0; x < BI; x++)
 #pragma unroll
-        for (int x = 0; x < 2; x++)
-#pragma unroll
-            for (int y = 0; y < 2; y++) {
-                f32x4_t a0 = {0.0f, 0.0f, 0.0f, 0.0f};
-                if (beta != 0.0f) {  // the old value, scaled (clamped into the image: unused lanes never store)
-                    const int orow = min(16 * (tj0 + y) + c, n - 1), ocol = min(16 * (ti0 + x) + 4 * g, n - 4);
-                    const uint2 w = *reinterpret_cast<const uint2 *>(out + orow * P + ocol * 2);
-                    a0 = f32x4_t{ratio * bf2f(w.x & 0xFFFFu), ratio * bf2f(w.x >> 16), ratio * bf2f(w.y & 0xFFFFu),
-                                 ratio * bf2f(w.y >> 16)};
-                }
-                acc[u][x][y] = a0;
+        for (int y = 0; y < BJ; y++) {
+            if (DIAG && x > y) continue;
+            f32x4_t a0 = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (init) {  // the old value, scaled (clamped into the image: unused lanes never store)
+                const int orow = min(16 * (TJ0 + y) + c, N - 1), ocol = min(16 * (TI0 + x) + 4 * g, N - 4);
+                const uint2 w = *reinterpret_cast<const uint2 *>(out + orow * P + ocol * 2);
+                a0 = f32x4_t{ratio * bf2f(w.x & 0xFFFFu), ratio * bf2f(w.x >> 16), ratio * bf2f(w.y & 0xFFFFu),
+                             ratio * bf2f(w.y >> 16)};
             }
-        // row c of each tile, clamped to the last valid row (rows >= n only feed unstored outputs)
-        const char *pa0 = AROWS ? A + min(16 * ti0 + c, n - 1) * P + 16 * g : A + ltr + 32 * ti0;
-        const char *pa1 = AROWS ? A + min(16 * ti0 + 16 + c, n - 1) * P + 16 * g : pa0 + 32;
-        const char *pb0 = B + min(16 * tj0 + c, n - 1) * P + 16 * g;
-        const char *pb1 = B + min(16 * tj0 + 16 + c, n - 1) * P + 16 * g;
-#pragma unroll
-        for (int ks = 0; ks < KS; ks++) {
-            bf16x8_t fa[2], fb[2];
-#pragma unroll
-            for (int y = 0; y < 2; y++) {
-                uint4 v = *reinterpret_cast<const uint4 *>((y ? pb1 : pb0) + 64 * ks);
-                if (ks == KS - 1 && 32 * KS > kpad) {  // k >= round8(n) reads the next row: zero
-                    const bool kin = 32 * ks + 8 * g < kpad;
-                    v = kin ? v : make_uint4(0u, 0u, 0u, 0u);
-                }
-                fb[y] = __builtin_bit_cast(bf16x8_t, v);
-            }
-#pragma unroll
-            for (int x = 0; x < 2; x++) {
-                if (AROWS) {
-                    fa[x] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>((x ? pa1 : pa0) + 64 * ks));
-                } else {  // A = X^T: X[32 ks + 8 g + j][16 ti + i], two transposing reads (rows past
-                          // n fall in the G image behind X: finite, and their B is zero)
-                    const char *a1 = (x ? pa1 : pa0) + 32 * ks * P;
-                    const s16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)a1);
-                    const s16x4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(a1 + 4 * P));
-                    fa[x] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(t1, t2, 0, 1, 2, 3, 4, 5, 6, 7));
-                }
-            }
-#pragma unroll
-            for (int x = 0; x < 2; x++)
-#pragma unroll
-                for (int y = 0; y < 2; y++)
-                    acc[u][x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[x], fb[y], acc[u][x][y], 0, 0, 0);
+            acc[OFF + x * BJ + y] = a0;
         }
-    }
-    __syncthreads();  // every read of the old `out` (and of A / B when they alias it) is done
+    const char *pa[BI];
+    const char *pb[BJ];
 #pragma unroll
-    for (int u = 0; u < MAXB; u++) {
-        if (u >= cnt) continue;
-        const int bb = sch.blk[SYM][wave][u], ti0 = 2 * (bb & 15), tj0 = 2 * (bb >> 4);
+    for (int x = 0; x < BI; x++)
+        pa[x] = AROWS ? A + min(16 * (TI0 + x) + c, N - 1) * P + 16 * g : A + ltr + 32 * (TI0 + x);
 #pragma unroll
-        for (int x = 0; x < 2; x++)
+    for (int y = 0; y < BJ; y++) pb[y] = B + min(16 * (TJ0 + y) + c, N - 1) * P + 16 * g;
 #pragma unroll
-            for (int y = 0; y < 2; y++) {
-                const int ti = ti0 + x, tj = tj0 + y;
-                const int col = 16 * tj + c, row0 = 16 * ti + 4 * g;
-                if (col >= n || row0 >= n) continue;
-                const f32x4_t v = acc[u][x][y];
-                const uint32_t w0 = pack_bf2(alpha * v[0], alpha * v[1]), w1 = pack_bf2(alpha * v[2], alpha * v[3]);
-                *reinterpret_cast<uint2 *>(out + col * P + row0 * 2) = make_uint2(w0, w1);  // transposed
-                if (SYM && ti < tj) {  // the mirrored tile of a symmetric product: out[row][col]
-                    uint16_t *o = reinterpret_cast<uint16_t *>(out + row0 * P + col * 2);
-                    o[0] = (uint16_t)(w0 & 0xFFFFu);
-                    o[P / 2] = (uint16_t)(w0 >> 16);
-                    o[P] = (uint16_t)(w1 & 0xFFFFu);
-                    o[3 * P / 2] = (uint16_t)(w1 >> 16);
-                }
+    for (int ks = 0; ks < S::KS; ks++) {
+        bf16x8_t fa[BI], fb[BJ];
+#pragma unroll
+        for (int y = 0; y < BJ; y++) {
+            uint4 v = *reinterpret_cast<const uint4 *>(pb[y] + 64 * ks);
+            if (ks == S::KS - 1 && 32 * S::KS > S::KPAD) {  // k >= round8(n) reads the next row: zero
+                const bool kin = 32 * ks + 8 * g < S::KPAD;
+                v = kin ? v : make_uint4(0u, 0u, 0u, 0u);
+            }
+            fb[y] = __builtin_bit_cast(bf16x8_t, v);
+        }
+#pragma unroll
+        for (int x = 0; x < BI; x++) {
+            if (AROWS) {
+                fa[x] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(pa[x] + 64 * ks));
+            } else {  // A = X^T: X[32 ks + 8 g + j][16 ti + i], two transposing reads (rows past n
+                      // fall in the G image behind X: finite, and their B is zero)
+                const char *a1 = pa[x] + 32 * ks * P;
+                const s16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)a1);
+                const s16x4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(a1 + 4 * P));
+                fa[x] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(t1, t2, 0, 1, 2, 3, 4, 5, 6, 7));
+            }
+        }
+#pragma unroll
+        for (int x = 0; x < BI; x++)
+#pragma unroll
+            for (int y = 0; y < BJ; y++) {
+                if (DIAG && x > y) continue;
+                acc[OFF + x * BJ + y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[x], fb[y], acc[OFF + x * BJ + y], 0, 0, 0);
             }
     }
+}
+
+// the transposed (and for symmetric products mirrored) bf16 store of one block
+template <int N, bool SYM, int BI, int BJ, int TI0, int TJ0, int OFF, int T>
+__device__ __forceinline__ void ns_store(const f32x4_t (&acc)[T], char *out, float alpha, int g, int c) {
+    constexpr int P = NsShape<N>::P;
+    constexpr bool DIAG = SYM && TI0 == TJ0;
+#pragma unroll
+    for (int x = 0; x < BI; x++)
+#pragma unroll
+        for (int y = 0; y < BJ; y++) {
+            if (DIAG && x > y) continue;
+            const int ti = TI0 + x, tj = TJ0 + y;
+            const int col = 16 * tj + c, row0 = 16 * ti + 4 * g;
+            if (col >= N || row0 >= N) continue;
+            const f32x4_t v = acc[OFF + x * BJ + y];
+            const uint32_t w0 = pack_bf2(alpha * v[0], alpha * v[1]), w1 = pack_bf2(alpha * v[2], alpha * v[3]);
+            *reinterpret_cast<uint2 *>(out + col * P + row0 * 2) = make_uint2(w0, w1);  // transposed
+            if (SYM && ti < tj) {  // the mirrored tile of a symmetric product: out[row][col]
+                uint16_t *o = reinterpret_cast<uint16_t *>(out + row0 * P + col * 2);
+                o[0] = (uint16_t)(w0 & 0xFFFFu);
+                o[P / 2] = (uint16_t)(w0 >> 16);
+                o[P] = (uint16_t)(w1 & 0xFFFFu);
+                o[3 * P / 2] = (uint16_t)(w1 >> 16);
+            }
+        }
+}
+
+template <int N, bool SYM, bool AROWS, int W, int U, int T>
+__device__ __forceinline__ void ns_blocks(f32x4_t (&acc)[T], const char *A, const char *B, const char *out,
+                                          float ratio, bool init, int g, int c, int ltr) {
+    constexpr NsParts pt(NsShape<N>::NT);
+    constexpr NsSchedule sch(NsShape<N>::NT);
+    if constexpr (U < sch.cnt[SYM][W]) {
+        constexpr int bi = sch.bi[SYM][W][U], bj = sch.bj[SYM][W][U];
+        ns_block<N, SYM, AROWS, pt.size[bi], pt.size[bj], pt.start[bi], pt.start[bj], sch.offset(SYM, W, U, pt)>(
+            acc, A, B, out, ratio, init, g, c, ltr);
+        ns_blocks<N, SYM, AROWS, W, U + 1>(acc, A, B, out, ratio, init, g, c, ltr);
+    }
+}
+
+template <int N, bool SYM, int W, int U, int T>
+__device__ __forceinline__ void ns_stores(const f32x4_t (&acc)[T], char *out, float alpha, int g, int c) {
+    constexpr NsParts pt(NsShape<N>::NT);
+    constexpr NsSchedule sch(NsShape<N>::NT);
+    if constexpr (U < sch.cnt[SYM][W]) {
+        constexpr int bi = sch.bi[SYM][W][U], bj = sch.bj[SYM][W][U];
+        ns_store<N, SYM, pt.size[bi], pt.size[bj], pt.start[bi], pt.start[bj], sch.offset(SYM, W, U, pt)>(acc, out,
+                                                                                                          alpha, g, c);
+        ns_stores<N, SYM, W, U + 1>(acc, out, alpha, g, c);
+    }
+}
+
+// One product on wave W: out <- transpose(alpha * (init + A B)), init = (beta / alpha) * old out
+// (transposed) when beta != 0.
+template <int N, bool SYM, bool AROWS, int W>
+__device__ __forceinline__ void ns_product_w(const char *A, const char *B, char *out, float alpha, float beta,
+                                             int lane) {
+    constexpr NsSchedule sch(NsShape<N>::NT);
+    constexpr int T = sch.tiles[SYM][W] > 0 ? sch.tiles[SYM][W] : 1;
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, c = lane & 15;
+    const int ltr = (8 * g + q) * NsShape<N>::P + 8 * p;  // transposing reads: row 8 g + q, column 4 p
+    f32x4_t acc[T];
+    ns_blocks<N, SYM, AROWS, W, 0>(acc, A, B, out, beta / alpha, beta != 0.0f, g, c, ltr);
+    __syncthreads();  // every read of the old `out` (and of A / B when they alias it) is done
+    ns_stores<N, SYM, W, 0>(acc, out, alpha, g, c);
     __syncthreads();
 }
 
-template <int NT, int KS, int P>
-__device__ __forceinline__ void ns_square(const NsSchedule &sch, char *sX, char *sG, int n, const MuonArgs &args,
-                                          int wave, int lane) {
+template <int N, bool SYM, bool AROWS>
+__device__ __forceinline__ void ns_product(const char *A, const char *B, char *out, float alpha, float beta,
+                                           int wave, int lane) {
+    switch (wave) {  // wave-uniform
+    case 0: ns_product_w<N, SYM, AROWS, 0>(A, B, out, alpha, beta, lane); break;
+    case 1: ns_product_w<N, SYM, AROWS, 1>(A, B, out, alpha, beta, lane); break;
+    case 2: ns_product_w<N, SYM, AROWS, 2>(A, B, out, alpha, beta, lane); break;
+    case 3: ns_product_w<N, SYM, AROWS, 3>(A, B, out, alpha, beta, lane); break;
+    case 4: ns_product_w<N, SYM, AROWS, 4>(A, B, out, alpha, beta, lane); break;
+    case 5: ns_product_w<N, SYM, AROWS, 5>(A, B, out, alpha, beta, lane); break;
+    case 6: ns_product_w<N, SYM, AROWS, 6>(A, B, out, alpha, beta, lane); break;
+    default: ns_product_w<N, SYM, AROWS, 7>(A, B, out, alpha, beta, lane); break;
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void ns_square(char *sX, char *sG, const MuonArgs &args, int wave, int lane) {
     for (int it = 0; it < args.steps; it++) {
-        ns_product<NT, KS, P, true, true>(sch, sX, sX, sG, n, 1.0f, 0.0f, wave, lane);      // G = X X^T
-        ns_product<NT, KS, P, true, true>(sch, sG, sG, sG, n, args.c, args.b, wave, lane);  // U = b G + c G G
-        ns_product<NT, KS, P, false, false>(sch, sX, sG, sX, n, 1.0f, args.a, wave, lane);  // X = a X + U X
+        ns_product<N, true, true>(sX, sX, sG, 1.0f, 0.0f, wave, lane);          // G = X X^T
+        ns_product<N, true, true>(sG, sG, sG, args.c, args.b, wave, lane);      // U = b G + c G G
+        ns_product<N, false, false>(sX, sG, sX, 1.0f, args.a, wave, lane);      // X = a X + U X
     }
 }
 
@@ -597,11 +675,11 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     const int kind = r == c && !args.generic_ns ? ns_square_kind(r) : 0;
     if (kind) {  // the square fast path (row pitch muon_pitch(n, n))
         switch (kind) {
-        case 1: ns_square<13, 7, 416>(kNs13, sX, sG, r, args, wave, lane); break;
-        case 2: ns_square<12, 6, 416>(kNs12, sX, sG, r, args, wave, lane); break;
-        case 3: ns_square<8, 4, 288>(kNs8, sX, sG, r, args, wave, lane); break;
-        case 4: ns_square<4, 2, 160>(kNs4, sX, sG, r, args, wave, lane); break;
-        default: ns_square<2, 1, 96>(kNs2, sX, sG, r, args, wave, lane); break;
+        case 1: ns_square<196>(sX, sG, args, wave, lane); break;
+        case 2: ns_square<192>(sX, sG, args, wave, lane); break;
+        case 3: ns_square<128>(sX, sG, args, wave, lane); break;
+        case 4: ns_square<64>(sX, sG, args, wave, lane); break;
+        default: ns_square<32>(sX, sG, args, wave, lane); break;
         }
     } else {
     f32x4_t acc[kBI][kBJ];
