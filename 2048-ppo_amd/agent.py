@@ -10,8 +10,9 @@ train.py:1893-1901) loads unchanged:
 
 Sub-modules are created in the reference's order and re-initialised with the same Kaiming-uniform
 scheme, so under the same torch seed the initial weights are identical to the reference's.
-On MI355X the heavy lifting is hipBLASLt GEMMs (bf16 MFMA under autocast) from these modules in
-the update, and the fused HIP rollout policy (g2048.policy) during rollouts.
+On MI355X these modules are the parameter containers and the eager reference: the rollout runs the
+fused HIP policy (g2048.policy), the PPO update the kernel-written forward / backward / optimizer
+of g2048.fastmlp and g2048.optim (GameMLP) and g2048.urm (GameURM) on the same parameters.
 """
 
 from __future__ import annotations

@@ -111,8 +111,9 @@ __device__ __forceinline__ void adamw_elem(const AdamGroup &gr, int64_t i, float
 }
 
 // ------------------------------------------------------------------ Muon ---------------------
-constexpr int kMuonThreads = 512;        // 8 waves, 2 (tile rows) x 4 (tile columns) blocks
-constexpr int kBI = 7, kBJ = 4;          // 16x16 tiles per wave: the block covers 224 x 256
+constexpr int kMuonThreads = 1024;       // 16 waves (4 per SIMD: LDS latency hidden by the others)
+constexpr int kMuonWaves = kMuonThreads / 64;
+constexpr int kBI = 4, kBJ = 4;          // generic schedule: 4 x 4 waves of 4 x 4 16x16 tiles = 256 x 256
 constexpr int kMuonMaxMats = 8;
 constexpr int kMuonLds = 160 * 1024 - 256;  // minus the static red[] / s_norm
 
@@ -246,6 +247,26 @@ __device__ __forceinline__ void store_block_t(const f32x4_t (&acc)[kBI][kBJ], ch
         }
 }
 
+// momentum + nesterov + bf16 rounding of 4 elements: bv = the new momentum, ub = the bf16-valued
+// update; returns the sum of squares of ub
+__device__ __forceinline__ float momentum4(const float4 &g4, const float4 &b4, float coef, float mu, bool nesterov,
+                                          float bv[4], float ub[4]) {
+    const float gv[4] = {g4.x * coef, g4.y * coef, g4.z * coef, g4.w * coef};
+    bv[0] = b4.x;
+    bv[1] = b4.y;
+    bv[2] = b4.z;
+    bv[3] = b4.w;
+    float ss = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        bv[u] = bv[u] + (1.0f - mu) * (gv[u] - bv[u]);                               // buf.lerp_(g, 1 - mu)
+        const float up = nesterov ? bv[u] - (bv[u] - gv[u]) * (1.0f - mu) : bv[u];  // g.lerp(buf, mu)
+        ub[u] = round_bf(up);
+        ss += ub[u] * ub[u];
+    }
+    return ss;
+}
+
 // momentum + nesterov + bf16 cast (+ transpose) of the gradient into the LDS image X; returns the
 // thread's sum of squares of the bf16 values.  Separate function so the restrict qualifiers let the
 // compiler overlap the iterations' loads with the previous stores.
@@ -268,18 +289,10 @@ __device__ __forceinline__ float muon_prologue(const float *__restrict__ grad, f
 #pragma unroll
         for (int v = 0; v < kB; v++) {
             const int e4 = base + v * kMuonThreads;
-            if (e4 >= n4) break;
-            const float gv[4] = {g4[v].x * coef, g4[v].y * coef, g4[v].z * coef, g4[v].w * coef};
-            float bv[4] = {b4[v].x, b4[v].y, b4[v].z, b4[v].w};
+            if (e4 >= n4) continue;
+            float bv[4], ub[4];
+            ss += momentum4(g4[v], b4[v], coef, mu, nesterov, bv, ub);
             const int i = (4 * e4) / C, j0 = 4 * e4 - i * C;  // C % 4 == 0: a float4 stays in one row
-            float ub[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                bv[u] = bv[u] + (1.0f - mu) * (gv[u] - bv[u]);                               // buf.lerp_(g, 1 - mu)
-                const float up = nesterov ? bv[u] - (bv[u] - gv[u]) * (1.0f - mu) : bv[u];  // g.lerp(buf, mu)
-                ub[u] = round_bf(up);
-                ss += ub[u] * ub[u];
-            }
             if (tr) {
 #pragma unroll
                 for (int u = 0; u < 4; u++) reinterpret_cast<uint16_t *>(sX + (j0 + u) * px)[i] = (uint16_t)f2bf(ub[u]);
@@ -306,7 +319,7 @@ __device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_
 #pragma unroll
         for (int v = 0; v < kB; v++) {
             const int e4 = base + v * kMuonThreads;
-            if (e4 >= n4) break;
+            if (e4 >= n4) continue;
             float pv[4] = {p4[v].x, p4[v].y, p4[v].z, p4[v].w};
             const int i = (4 * e4) / C, j0 = 4 * e4 - i * C;
             float x[4];
@@ -357,13 +370,13 @@ __host__ __device__ constexpr int muon_pitch(int rows, int cols) {
 //     computed, each off-diagonal one stored twice (transposed and mirrored).
 // Per output tile the MFMA sequence (init from the scaled old value, k-steps in order) is the
 // generic path's, so both compute bitwise the same iterate.
-constexpr int kNsMaxBlocks = 8;  // per wave and product
-constexpr int kNsMaxTiles = 32;  // accumulator tiles per wave (128 VGPRs)
+constexpr int kNsMaxBlocks = 4;  // per wave and product
+constexpr int kNsMaxTiles = 16;  // accumulator tiles per wave (64 of the 128 VGPRs at 4 waves per SIMD)
 
 struct NsParts {
     int n, start[4], size[4];
-    // ceil(NT / 4) parts, but at least 4 from 12 tiles up (4 x 4 = 16 blocks spread evenly over 4 SIMDs)
-    constexpr NsParts(int NT) : n(NT >= 12 ? ((NT + 3) / 4 > 4 ? (NT + 3) / 4 : 4) : (NT + 3) / 4), start{}, size{} {
+    // 4 parts (16 blocks: one per wave of the full product) from 4 tiles up, of at most 4 tiles
+    constexpr NsParts(int NT) : n(NT >= 4 ? ((NT + 3) / 4 > 4 ? (NT + 3) / 4 : 4) : NT), start{}, size{} {
         const int base = NT / n, extra = NT % n;
         int s0 = 0;
         for (int i = 0; i < n; i++) {
@@ -375,8 +388,8 @@ struct NsParts {
 };
 
 struct NsSchedule {
-    int bi[2][8][kNsMaxBlocks], bj[2][8][kNsMaxBlocks];  // [sym][wave][i]: part indices
-    int cnt[2][8], tiles[2][8];
+    int bi[2][kMuonWaves][kNsMaxBlocks], bj[2][kMuonWaves][kNsMaxBlocks];  // [sym][wave][i]: part indices
+    int cnt[2][kMuonWaves], tiles[2][kMuonWaves];
     constexpr NsSchedule(int NT) : bi{}, bj{}, cnt{}, tiles{} {
         const NsParts pt(NT);
         for (int sym = 0; sym < 2; sym++) {
@@ -395,12 +408,14 @@ struct NsSchedule {
                     t = ai[j]; ai[j] = ai[j - 1]; ai[j - 1] = t;
                     t = aj[j]; aj[j] = aj[j - 1]; aj[j - 1] = t;
                 }
-            int simd[4] = {}, wave[8] = {};
+            int simd[4] = {}, wave[kMuonWaves] = {};
             for (int i = 0; i < n; i++) {
                 int sm = 0;
                 for (int k = 1; k < 4; k++)
                     if (simd[k] < simd[sm]) sm = k;
-                const int w = wave[sm] <= wave[sm + 4] ? sm : sm + 4;
+                int w = sm;  // the SIMD's least loaded wave (waves w, w + 4, ... share SIMD w % 4)
+                for (int k = sm + 4; k < kMuonWaves; k += 4)
+                    if (wave[k] < wave[w]) w = k;
                 simd[sm] += cost[i];
                 wave[w] += cost[i];
                 bi[sym][w][cnt[sym][w]] = ai[i];
@@ -420,7 +435,7 @@ struct NsSchedule {
 constexpr bool ns_schedule_fits(int NT) {
     const NsSchedule s(NT);
     for (int sym = 0; sym < 2; sym++)
-        for (int w = 0; w < 8; w++)
+        for (int w = 0; w < kMuonWaves; w++)
             if (s.cnt[sym][w] > kNsMaxBlocks || s.tiles[sym][w] > kNsMaxTiles) return false;
     return true;
 }
@@ -433,10 +448,39 @@ struct NsShape {
     static constexpr int P = muon_pitch(N, N);
 };
 
+// the A / B fragments of k-step ks of a block (per-lane row bases pa / pb)
+template <int N, bool AROWS, int BI, int BJ>
+__device__ __forceinline__ void ns_frags(int ks, const char *const (&pa)[BI], const char *const (&pb)[BJ],
+                                         bf16x8_t (&fa)[BI], bf16x8_t (&fb)[BJ], int g) {
+    using S = NsShape<N>;
+    constexpr int P = S::P;
+#pragma unroll
+    for (int y = 0; y < BJ; y++) {
+        uint4 v = *reinterpret_cast<const uint4 *>(pb[y] + 64 * ks);
+        if (ks == S::KS - 1 && 32 * S::KS > S::KPAD) {  // k >= round8(n) reads the next row: zero
+            const bool kin = 32 * ks + 8 * g < S::KPAD;
+            v = kin ? v : make_uint4(0u, 0u, 0u, 0u);
+        }
+        fb[y] = __builtin_bit_cast(bf16x8_t, v);
+    }
+#pragma unroll
+    for (int x = 0; x < BI; x++) {
+        if (AROWS) {
+            fa[x] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(pa[x] + 64 * ks));
+        } else {  // A = X^T: X[32 ks + 8 g + j][16 ti + i], two transposing reads (rows past n fall in
+                  // the G image behind X: finite, and their B is zero)
+            const char *a1 = pa[x] + 32 * ks * P;
+            const s16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)a1);
+            const s16x4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(a1 + 4 * P));
+            fa[x] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(t1, t2, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+    }
+}
+
 // init + k loop of one BI x BJ block at tiles (TI0, TJ0) into acc[OFF ...]
-template <int N, bool SYM, bool AROWS, int BI, int BJ, int TI0, int TJ0, int OFF, int T>
-__device__ __forceinline__ void ns_block(f32x4_t (&acc)[T], const char *A, const char *B, const char *out,
-                                         float ratio, bool init, int g, int c, int ltr) {
+template <int N, bool SYM, bool AROWS, int KEEP, int BI, int BJ, int TI0, int TJ0, int OFF, int T>
+__device__ __forceinline__ void ns_block(f32x4_t (&acc)[T], uint2 (&kept)[T], const char *A, const char *B,
+                                         const char *out, float ratio, bool init, int g, int c, int ltr) {
     using S = NsShape<N>;
     constexpr int P = S::P;
     constexpr bool DIAG = SYM && TI0 == TJ0;  // upper triangle only
@@ -446,7 +490,11 @@ __device__ __forceinline__ void ns_block(f32x4_t (&acc)[T], const char *A, const
         for (int y = 0; y < BJ; y++) {
             if (DIAG && x > y) continue;
             f32x4_t a0 = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (init) {  // the old value, scaled (clamped into the image: unused lanes never store)
+            if (KEEP == 2) {  // the old value is this lane's own output of the previous product
+                const uint2 w = kept[OFF + x * BJ + y];
+                a0 = f32x4_t{ratio * bf2f(w.x & 0xFFFFu), ratio * bf2f(w.x >> 16), ratio * bf2f(w.y & 0xFFFFu),
+                             ratio * bf2f(w.y >> 16)};
+            } else if (init) {  // the old value, scaled (clamped into the image: unused lanes never store)
                 const int orow = min(16 * (TJ0 + y) + c, N - 1), ocol = min(16 * (TI0 + x) + 4 * g, N - 4);
                 const uint2 w = *reinterpret_cast<const uint2 *>(out + orow * P + ocol * 2);
                 a0 = f32x4_t{ratio * bf2f(w.x & 0xFFFFu), ratio * bf2f(w.x >> 16), ratio * bf2f(w.y & 0xFFFFu),
@@ -461,151 +509,203 @@ __device__ __forceinline__ void ns_block(f32x4_t (&acc)[T], const char *A, const
         pa[x] = AROWS ? A + min(16 * (TI0 + x) + c, N - 1) * P + 16 * g : A + ltr + 32 * (TI0 + x);
 #pragma unroll
     for (int y = 0; y < BJ; y++) pb[y] = B + min(16 * (TJ0 + y) + c, N - 1) * P + 16 * g;
+    // (4 waves per SIMD: the other waves' MFMAs cover one wave's fragment reads)
 #pragma unroll
     for (int ks = 0; ks < S::KS; ks++) {
         bf16x8_t fa[BI], fb[BJ];
-#pragma unroll
-        for (int y = 0; y < BJ; y++) {
-            uint4 v = *reinterpret_cast<const uint4 *>(pb[y] + 64 * ks);
-            if (ks == S::KS - 1 && 32 * S::KS > S::KPAD) {  // k >= round8(n) reads the next row: zero
-                const bool kin = 32 * ks + 8 * g < S::KPAD;
-                v = kin ? v : make_uint4(0u, 0u, 0u, 0u);
-            }
-            fb[y] = __builtin_bit_cast(bf16x8_t, v);
-        }
-#pragma unroll
-        for (int x = 0; x < BI; x++) {
-            if (AROWS) {
-                fa[x] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(pa[x] + 64 * ks));
-            } else {  // A = X^T: X[32 ks + 8 g + j][16 ti + i], two transposing reads (rows past n
-                      // fall in the G image behind X: finite, and their B is zero)
-                const char *a1 = pa[x] + 32 * ks * P;
-                const s16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)a1);
-                const s16x4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(a1 + 4 * P));
-                fa[x] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(t1, t2, 0, 1, 2, 3, 4, 5, 6, 7));
-            }
-        }
+        ns_frags<N, AROWS, BI, BJ>(ks, pa, pb, fa, fb, g);
 #pragma unroll
         for (int x = 0; x < BI; x++)
 #pragma unroll
             for (int y = 0; y < BJ; y++) {
                 if (DIAG && x > y) continue;
-                acc[OFF + x * BJ + y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[x], fb[y], acc[OFF + x * BJ + y], 0, 0, 0);
+                acc[OFF + x * BJ + y] =
+                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[x], fb[y], acc[OFF + x * BJ + y], 0, 0, 0);
             }
     }
 }
 
-// the transposed (and for symmetric products mirrored) bf16 store of one block
-template <int N, bool SYM, int BI, int BJ, int TI0, int TJ0, int OFF, int T>
-__device__ __forceinline__ void ns_store(const f32x4_t (&acc)[T], char *out, float alpha, int g, int c) {
+// The mirrored tile of a symmetric product, out[row][col] for the lane's D[4g .. 4g+3][c]: a 4 x 4
+// transpose within each quad of lanes (c = 4m + k; two DPP exchanges, at k ^ 2 on whole dwords and
+// at k ^ 1 on bf16 halves) gives lane k row 4g + k, columns 4m .. 4m + 3 -- one 8-byte write whose
+// 16-lane groups cover 16 distinct bank quads (4 rows x 4 column chunks at the 416-byte pitch).
+__device__ __forceinline__ uint2 quad_transpose_bf16(uint32_t w0, uint32_t w1, int k) {
+    // stage A: lanes k < 2 keep rows {0,1} (w0) and take the partner's w0; lanes k >= 2 rows {2,3}
+    const uint32_t sa = k < 2 ? w1 : w0;
+    const uint32_t ra = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sa, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+    const uint32_t p0 = k < 2 ? w0 : ra, p1 = k < 2 ? ra : w1;
+    // stage B: even lanes send their high halves, odd lanes their low halves
+    const bool even = (k & 1) == 0;
+    const uint32_t sb = __builtin_amdgcn_perm(p1, p0, even ? 0x07060302u : 0x05040100u);
+    const uint32_t rb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sb, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+    return make_uint2(__builtin_amdgcn_perm(rb, p0, even ? 0x05040100u : 0x03020504u),
+                      __builtin_amdgcn_perm(rb, p1, even ? 0x07060100u : 0x03020706u));
+}
+
+// the transposed (and for symmetric products mirrored) bf16 store of one block; KEEP == 1: the
+// lane's packed values also stay in `kept` (the next product's initial value)
+template <int N, bool SYM, int KEEP, int BI, int BJ, int TI0, int TJ0, int OFF, int T>
+__device__ __forceinline__ void ns_store(const f32x4_t (&acc)[T], uint2 (&kept)[T], char *out, float alpha, int g,
+                                         int c) {
     constexpr int P = NsShape<N>::P;
     constexpr bool DIAG = SYM && TI0 == TJ0;
+    const int k = c & 3, m = c >> 2;
 #pragma unroll
     for (int x = 0; x < BI; x++)
 #pragma unroll
         for (int y = 0; y < BJ; y++) {
             if (DIAG && x > y) continue;
             const int ti = TI0 + x, tj = TJ0 + y;
-            const int col = 16 * tj + c, row0 = 16 * ti + 4 * g;
-            if (col >= N || row0 >= N) continue;
             const f32x4_t v = acc[OFF + x * BJ + y];
             const uint32_t w0 = pack_bf2(alpha * v[0], alpha * v[1]), w1 = pack_bf2(alpha * v[2], alpha * v[3]);
-            *reinterpret_cast<uint2 *>(out + col * P + row0 * 2) = make_uint2(w0, w1);  // transposed
-            if (SYM && ti < tj) {  // the mirrored tile of a symmetric product: out[row][col]
-                uint16_t *o = reinterpret_cast<uint16_t *>(out + row0 * P + col * 2);
-                o[0] = (uint16_t)(w0 & 0xFFFFu);
-                o[P / 2] = (uint16_t)(w0 >> 16);
-                o[P] = (uint16_t)(w1 & 0xFFFFu);
-                o[3 * P / 2] = (uint16_t)(w1 >> 16);
+            if (KEEP == 1) kept[OFF + x * BJ + y] = make_uint2(w0, w1);
+            if (SYM && ti < tj) {  // the mirrored tile: all lanes take part in the exchange
+                const uint2 t = quad_transpose_bf16(w0, w1, k);
+                const int row = 16 * ti + 4 * g + k, col0 = 16 * tj + 4 * m;
+                if (row < N && col0 < N) *reinterpret_cast<uint2 *>(out + row * P + col0 * 2) = t;
             }
+            const int col = 16 * tj + c, row0 = 16 * ti + 4 * g;
+            if (col < N && row0 < N) *reinterpret_cast<uint2 *>(out + col * P + row0 * 2) = make_uint2(w0, w1);
         }
 }
 
-template <int N, bool SYM, bool AROWS, int W, int U, int T>
-__device__ __forceinline__ void ns_blocks(f32x4_t (&acc)[T], const char *A, const char *B, const char *out,
-                                          float ratio, bool init, int g, int c, int ltr) {
+template <int N, bool SYM, bool AROWS, int KEEP, int W, int U, int T>
+__device__ __forceinline__ void ns_blocks(f32x4_t (&acc)[T], uint2 (&kept)[T], const char *A, const char *B,
+                                          const char *out, float ratio, bool init, int g, int c, int ltr) {
     constexpr NsParts pt(NsShape<N>::NT);
     constexpr NsSchedule sch(NsShape<N>::NT);
     if constexpr (U < sch.cnt[SYM][W]) {
         constexpr int bi = sch.bi[SYM][W][U], bj = sch.bj[SYM][W][U];
-        ns_block<N, SYM, AROWS, pt.size[bi], pt.size[bj], pt.start[bi], pt.start[bj], sch.offset(SYM, W, U, pt)>(
-            acc, A, B, out, ratio, init, g, c, ltr);
-        ns_blocks<N, SYM, AROWS, W, U + 1>(acc, A, B, out, ratio, init, g, c, ltr);
+        ns_block<N, SYM, AROWS, KEEP, pt.size[bi], pt.size[bj], pt.start[bi], pt.start[bj], sch.offset(SYM, W, U, pt)>(
+            acc, kept, A, B, out, ratio, init, g, c, ltr);
+        ns_blocks<N, SYM, AROWS, KEEP, W, U + 1>(acc, kept, A, B, out, ratio, init, g, c, ltr);
     }
 }
 
-template <int N, bool SYM, int W, int U, int T>
-__device__ __forceinline__ void ns_stores(const f32x4_t (&acc)[T], char *out, float alpha, int g, int c) {
+template <int N, bool SYM, int KEEP, int W, int U, int T>
+__device__ __forceinline__ void ns_stores(const f32x4_t (&acc)[T], uint2 (&kept)[T], char *out, float alpha, int g,
+                                          int c) {
     constexpr NsParts pt(NsShape<N>::NT);
     constexpr NsSchedule sch(NsShape<N>::NT);
     if constexpr (U < sch.cnt[SYM][W]) {
         constexpr int bi = sch.bi[SYM][W][U], bj = sch.bj[SYM][W][U];
-        ns_store<N, SYM, pt.size[bi], pt.size[bj], pt.start[bi], pt.start[bj], sch.offset(SYM, W, U, pt)>(acc, out,
-                                                                                                          alpha, g, c);
-        ns_stores<N, SYM, W, U + 1>(acc, out, alpha, g, c);
+        ns_store<N, SYM, KEEP, pt.size[bi], pt.size[bj], pt.start[bi], pt.start[bj], sch.offset(SYM, W, U, pt)>(
+            acc, kept, out, alpha, g, c);
+        ns_stores<N, SYM, KEEP, W, U + 1>(acc, kept, out, alpha, g, c);
     }
+}
+
+template <int N, bool SYM>
+constexpr int ns_tiles(int w) {
+    constexpr NsSchedule sch(NsShape<N>::NT);
+    return sch.tiles[SYM][w] > 0 ? sch.tiles[SYM][w] : 1;
 }
 
 // One product on wave W: out <- transpose(alpha * (init + A B)), init = (beta / alpha) * old out
-// (transposed) when beta != 0.
-template <int N, bool SYM, bool AROWS, int W>
+// (transposed) when beta != 0.  KEEP == 1: the packed outputs also stay in `kept`; KEEP == 2: the
+// old values come from `kept` (this wave computed them in the previous product, same schedule).
+template <int N, bool SYM, bool AROWS, int KEEP, int W>
 __device__ __forceinline__ void ns_product_w(const char *A, const char *B, char *out, float alpha, float beta,
-                                             int lane) {
-    constexpr NsSchedule sch(NsShape<N>::NT);
-    constexpr int T = sch.tiles[SYM][W] > 0 ? sch.tiles[SYM][W] : 1;
+                                             uint2 (&kept)[ns_tiles<N, SYM>(W)], int lane) {
+    constexpr int T = ns_tiles<N, SYM>(W);
     const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, c = lane & 15;
     const int ltr = (8 * g + q) * NsShape<N>::P + 8 * p;  // transposing reads: row 8 g + q, column 4 p
     f32x4_t acc[T];
-    ns_blocks<N, SYM, AROWS, W, 0>(acc, A, B, out, beta / alpha, beta != 0.0f, g, c, ltr);
+    ns_blocks<N, SYM, AROWS, KEEP, W, 0>(acc, kept, A, B, out, beta / alpha, beta != 0.0f, g, c, ltr);
     __syncthreads();  // every read of the old `out` (and of A / B when they alias it) is done
-    ns_stores<N, SYM, W, 0>(acc, out, alpha, g, c);
+    ns_stores<N, SYM, KEEP, W, 0>(acc, kept, out, alpha, g, c);
     __syncthreads();
 }
 
-template <int N, bool SYM, bool AROWS>
-__device__ __forceinline__ void ns_product(const char *A, const char *B, char *out, float alpha, float beta,
-                                           int wave, int lane) {
-    switch (wave) {  // wave-uniform
-    case 0: ns_product_w<N, SYM, AROWS, 0>(A, B, out, alpha, beta, lane); break;
-    case 1: ns_product_w<N, SYM, AROWS, 1>(A, B, out, alpha, beta, lane); break;
-    case 2: ns_product_w<N, SYM, AROWS, 2>(A, B, out, alpha, beta, lane); break;
-    case 3: ns_product_w<N, SYM, AROWS, 3>(A, B, out, alpha, beta, lane); break;
-    case 4: ns_product_w<N, SYM, AROWS, 4>(A, B, out, alpha, beta, lane); break;
-    case 5: ns_product_w<N, SYM, AROWS, 5>(A, B, out, alpha, beta, lane); break;
-    case 6: ns_product_w<N, SYM, AROWS, 6>(A, B, out, alpha, beta, lane); break;
-    default: ns_product_w<N, SYM, AROWS, 7>(A, B, out, alpha, beta, lane); break;
+// The Newton-Schulz iterations on wave W: its own straight-line code for all three products, the
+// lane index laundered per product so the compiler recomputes the few per-lane addresses instead
+// of hoisting every product's out of the loop (register spills at 128 VGPRs).
+template <int N, int W>
+__device__ __forceinline__ void ns_square_w(char *sX, char *sG, const MuonArgs &args, int lane) {
+    for (int it = 0; it < args.steps; it++) {
+        uint2 kept[ns_tiles<N, true>(W)];  // G's tiles, U's initial value
+        uint2 unused[ns_tiles<N, false>(W)];
+        int l = lane;
+        asm volatile("" : "+v"(l));
+        ns_product_w<N, true, true, 1, W>(sX, sX, sG, 1.0f, 0.0f, kept, l);          // G = X X^T
+        l = lane;
+        asm volatile("" : "+v"(l));
+        ns_product_w<N, true, true, 2, W>(sG, sG, sG, args.c, args.b, kept, l);      // U = b G + c G G
+        l = lane;
+        asm volatile("" : "+v"(l));
+        ns_product_w<N, false, false, 0, W>(sX, sG, sX, 1.0f, args.a, unused, l);    // X = a X + U X
     }
 }
 
 template <int N>
 __device__ __forceinline__ void ns_square(char *sX, char *sG, const MuonArgs &args, int wave, int lane) {
-    for (int it = 0; it < args.steps; it++) {
-        ns_product<N, true, true>(sX, sX, sG, 1.0f, 0.0f, wave, lane);          // G = X X^T
-        ns_product<N, true, true>(sG, sG, sG, args.c, args.b, wave, lane);      // U = b G + c G G
-        ns_product<N, false, false>(sX, sG, sX, 1.0f, args.a, wave, lane);      // X = a X + U X
+    switch (wave) {  // wave-uniform
+    case 0: ns_square_w<N, 0>(sX, sG, args, lane); break;
+    case 1: ns_square_w<N, 1>(sX, sG, args, lane); break;
+    case 2: ns_square_w<N, 2>(sX, sG, args, lane); break;
+    case 3: ns_square_w<N, 3>(sX, sG, args, lane); break;
+    case 4: ns_square_w<N, 4>(sX, sG, args, lane); break;
+    case 5: ns_square_w<N, 5>(sX, sG, args, lane); break;
+    case 6: ns_square_w<N, 6>(sX, sG, args, lane); break;
+    case 7: ns_square_w<N, 7>(sX, sG, args, lane); break;
+    case 8: ns_square_w<N, 8>(sX, sG, args, lane); break;
+    case 9: ns_square_w<N, 9>(sX, sG, args, lane); break;
+    case 10: ns_square_w<N, 10>(sX, sG, args, lane); break;
+    case 11: ns_square_w<N, 11>(sX, sG, args, lane); break;
+    case 12: ns_square_w<N, 12>(sX, sG, args, lane); break;
+    case 13: ns_square_w<N, 13>(sX, sG, args, lane); break;
+    case 14: ns_square_w<N, 14>(sX, sG, args, lane); break;
+    default: ns_square_w<N, 15>(sX, sG, args, lane); break;
     }
+}
+
+// The AdamW update of the 1-D groups by block b of nb (clip coefficient from the partials).
+__device__ __forceinline__ void adam_blocks(const MuonArgs &args, int b, int nb) {
+    float cf = 1.0f;
+    if (args.partials) {  // grad_norm_kernel's arithmetic, as in the Muon blocks (same result)
+        float t = args.partials[threadIdx.x & 63];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+        cf = fminf(args.max_norm / (sqrtf(t) + 1e-6f), 1.0f);
+    }
+    const AdamArgs &a = args.adam;
+    const float t = *a.step;
+    const float bc1 = 1.0f - powf(a.b1, t), bc2s = sqrtf(1.0f - powf(a.b2, t));
+    for (int k = 0; k < a.count; k++) {
+        const AdamGroup gr = a.g[k];
+        const float lr = a.lr[gr.lr_index];
+        for (int64_t i = (int64_t)b * blockDim.x + threadIdx.x; i < gr.n; i += (int64_t)nb * blockDim.x)
+            adamw_elem(gr, i, lr, cf, a.b1, a.b2, a.eps, a.wd, bc1, bc2s);
+    }
+}
+
+// The gradient-clip coefficient of this step: grad_norm_kernel's arithmetic on the grad_sumsq
+// partials, in every block (same order, same result); `publish`: write norm / coefficient out.
+__device__ __forceinline__ float block_clip_coef(const MuonArgs &args, int tid, bool publish) {
+    __shared__ float s_coef;
+    if (!args.partials) return args.clip ? *args.clip : 1.0f;
+    if (tid < 64) {
+        float t = args.partials[tid];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+        const float nrm = sqrtf(t);
+        const float cf = fminf(args.max_norm / (nrm + 1e-6f), 1.0f);
+        if (tid == 0) {
+            s_coef = cf;
+            if (publish) {
+                *args.norm_out = nrm;
+                *args.coef_out = cf;
+            }
+        }
+    }
+    __syncthreads();
+    return s_coef;
 }
 
 __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if ((int)blockIdx.x >= args.count) {  // the 1-D parameters' AdamW, in the same launch
-        float cf = 1.0f;
-        if (args.partials) {  // grad_norm_kernel's arithmetic, as in the Muon blocks (same result)
-            float t = args.partials[threadIdx.x & 63];
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
-            cf = fminf(args.max_norm / (sqrtf(t) + 1e-6f), 1.0f);
-        }
-        const AdamArgs &a = args.adam;
-        const float t = *a.step;
-        const float bc1 = 1.0f - powf(a.b1, t), bc2s = sqrtf(1.0f - powf(a.b2, t));
-        const int b = (int)blockIdx.x - args.count;
-        for (int k = 0; k < a.count; k++) {
-            const AdamGroup gr = a.g[k];
-            const float lr = a.lr[gr.lr_index];
-            for (int64_t i = (int64_t)b * kMuonThreads + threadIdx.x; i < gr.n; i += (int64_t)args.nadam * kMuonThreads)
-                adamw_elem(gr, i, lr, cf, a.b1, a.b2, a.eps, a.wd, bc1, bc2s);
-        }
+        adam_blocks(args, (int)blockIdx.x - args.count, args.nadam);
         return;
     }
     const MuonMat mt = args.m[blockIdx.x];
@@ -617,7 +717,7 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     char *sG = smem + ((r * px + 127) & ~127);
     char *zero = sG + ((r * pg + 127) & ~127);  // 64 zero bytes
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ti0 = (wave & 1) * kBI, tj0 = (wave >> 1) * kBJ;  // wave-uniform
+    const int ti0 = (wave & 3) * kBI, tj0 = (wave >> 2) * kBJ;  // wave-uniform
     __shared__ float red[kMuonThreads / 64];
     __shared__ float s_norm;
     // zero both images (their K padding must read as zero) and the zero block
@@ -627,25 +727,7 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     }
     __syncthreads();
 
-    __shared__ float s_coef;
-    if (args.partials) {  // grad_norm_kernel's arithmetic, in every block (same order, same result)
-        if (wave == 0) {
-            float t = args.partials[lane];
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
-            const float nrm = sqrtf(t);
-            const float cf = fminf(args.max_norm / (nrm + 1e-6f), 1.0f);
-            if (lane == 0) {
-                s_coef = cf;
-                if (blockIdx.x == 0) {
-                    *args.norm_out = nrm;
-                    *args.coef_out = cf;
-                }
-            }
-        }
-        __syncthreads();
-    }
-    const float coef = args.partials ? s_coef : (args.clip ? *args.clip : 1.0f);
+    const float coef = block_clip_coef(args, tid, blockIdx.x == 0);
     float ss = muon_prologue(mt.grad, mt.mom, sX, px, R, C, tr, coef, args.momentum, args.nesterov != 0, tid);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
@@ -749,7 +831,7 @@ int g2048_muon_supported(int32_t rows, int32_t cols) {
     if (rows <= 0 || cols <= 0) return 0;
     const int r = rows > cols ? cols : rows, c = rows > cols ? rows : cols;
     if (cols % 4) return 0;  // the element passes read float4s within a row
-    if (r > 16 * 2 * kBI || c > 16 * 4 * kBJ) return 0;
+    if (r > 16 * 4 * kBI || c > 16 * 4 * kBJ) return 0;
     return muon_lds_bytes(rows, cols) <= (size_t)kMuonLds ? 1 : 0;
 }
 

@@ -195,9 +195,10 @@ class MuonAdamW:
 
 
 class FusedMuonAdamW(MuonAdamW):
-    """MuonAdamW with its step as three kernels (include/g2048_ppo.h, csrc/optim.hip): the gradient
-    clip coefficient, every Muon matrix in one launch (momentum, Newton-Schulz on bf16 MFMA in LDS,
-    weight decay, scaled update, bf16 weight copy) and every AdamW group in one launch.
+    """MuonAdamW with its step as two kernels (include/g2048_ppo.h, csrc/optim.hip): the partial sums
+    of squares of the gradient (the clip coefficient), then every Muon matrix in one launch, one
+    block each (momentum, Newton-Schulz on bf16 MFMA in LDS, weight decay, scaled update, bf16
+    weight copy) with the AdamW update of the 1-D groups in the same launch's extra blocks.
 
     Same arithmetic as MuonAdamW up to the accumulation order of the bf16 Newton-Schulz products.
     `supported` is False when a matrix does not fit the one-block Newton-Schulz kernel (h > 196);

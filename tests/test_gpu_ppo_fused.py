@@ -1065,8 +1065,8 @@ def test_fused_passes_and_layer_chain_give_the_same_update(dev):
 
 @pytest.mark.parametrize("h", [196, 192, 128, 64])
 def test_muon_square_schedule_equals_generic(dev, h, monkeypatch):
-    """The square Newton-Schulz schedule of muon_kernel (symmetric G and U on the upper-triangle
-    2 x 2-tile blocks, load-balanced block lists) computes bitwise the update of the generic 7 x 4
+    """The square Newton-Schulz schedule of muon_kernel (per-wave compile-time part x part blocks,
+    symmetric G and U on and above the diagonal) computes bitwise the update of the generic 7 x 4
     tile-block schedule (G2048_MUON_GENERIC=1): same MFMA sequence per output tile."""
     import agent
     from g2048.dist import GradBucket
@@ -1094,3 +1094,4 @@ def test_muon_square_schedule_equals_generic(dev, h, monkeypatch):
         torch.cuda.synchronize()
         outs.append(torch.cat([p.detach().reshape(-1) for p in m.parameters()]).clone())
     assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
+

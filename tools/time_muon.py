@@ -1,5 +1,5 @@
 """Time the fused Muon + AdamW optimizer step (FusedMuonAdamW.step_clipped: grad clip, muon_kernel,
-adamw_kernel) of GameMLP h=196 with HIP events.   python tools/time_muon.py [libpath] [hidden]"""
+adamw_kernel) of GameMLP h=196 with HIP events.   python tools/time_muon.py [libpath] [hidden] [quick]"""
 import sys
 from pathlib import Path
 
@@ -36,7 +36,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     print(f"FusedMuonAdamW.step_clipped h={h}: {e0.elapsed_time(e1) / reps * 1e3:.1f} us per step")
-    for ns in (0, 1, 5):  # split: prologue/epilogue (0 Newton-Schulz steps) vs per-step cost
+    for ns in (() if "quick" in sys.argv[3:] else (0, 1, 5)):  # split: prologue/epilogue (0 Newton-Schulz steps) vs per-step cost
         fo._cfg.ns_steps = ns
         e0.record()
         for _ in range(reps):
