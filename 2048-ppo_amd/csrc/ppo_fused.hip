@@ -372,6 +372,269 @@ __global__ __launch_bounds__(kFpThreads, 1) void mlp_pass_kernel(FpArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ fused backward ----------
+// The minibatch's backward through the MLP in one persistent launch: for each 16-row tile the
+// three LayerNorm backwards (top block first) and the two block input gradients, with every
+// intermediate in registers:
+//     dy2 = dz W_heads                                   (v_mfma_f32_16x16x4_f32, as ln_bwd196)
+//     dG2 = LN/ReLU/Dropout backward(dy2; G2)  -> HBM    (ln_bwd196's arithmetic)
+//     P2  = bf16(dG2 W2)                                 (W2^T by transposing LDS reads, the dG2 tile
+//     dG1 = backward(dy2 + P2; G1)             -> HBM     as B fragments by permlane swaps: the
+//     P1  = bf16(dG1 W1)                                  forward's layer hand-off run backwards)
+//     dG0 = backward(dy2 + P1 + P2; G0)        -> HBM    (the stem: no dropout)
+// replacing 3 g2048_ln_act_bwd + 2 g2048_linear_dgrad: dG, P and dy never round-trip through HBM
+// except dG itself (the weight gradients' operand).  dG / P are bitwise those of the per-layer
+// chain (same head MFMAs, same dgrad k order, same rounding points); dgamma / dbeta are summed in
+// another order: per tile and layer a 16-lane reduce-scatter (DPP mirror / half-mirror / quad
+// swaps) leaves lane c one of its feature group's 8 sums (4 dgamma, 4 dbeta), accumulated per lane
+// -- 3 x NT registers instead of ln_bwd196's 8 NT per layer.
+constexpr int kBpThreads = 256;  // 4 waves (1 per SIMD: 512 registers for the whole chain); one block per CU (LDS)
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+
+struct BpArgs {
+    int64_t m;
+    const uint16_t *w1, *w2;  // bf16 [h][h]
+    const float *gamma[kMaxLayers], *beta[kMaxLayers];
+    const float *wa, *wv;     // fp32 heads [4][h], [h] (wv null: decoupled critic)
+    const float *dz;          // fp32 [m][8]
+    const uint16_t *g[kMaxLayers];
+    const float *mean[kMaxLayers], *rstd[kMaxLayers];
+    P::DropArgs drop[2];      // blocks 1, 2 (the train pass's draws)
+    uint16_t *dg[kMaxLayers];  // out bf16 [m][h]
+    uint16_t *pout[2];        // optional out bf16 [m][h]: P1, P2
+    float *part;              // out [layer][block][2 h]: dgamma | dbeta
+};
+
+// Sum of v[0..7] over the 16 lanes of a DPP row, scattered: lane c ends with the sum of
+// v[4 b3 + 2 b2 + b1] (b = bits of c; lanes c, c ^ 1 hold the same value).
+__device__ __forceinline__ float row16_scatter8(const float (&v)[8], int c) {
+    const bool b3 = (c & 8) != 0, b2 = (c & 4) != 0, b1 = (c & 2) != 0;
+    float h4[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {  // row_mirror: lane c <-> 15 - c (bit 3 differs)
+        const float keep = b3 ? v[4 + j] : v[j], send = b3 ? v[j] : v[4 + j];
+        h4[j] = keep + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(send), 0x140, 0xF, 0xF, false));
+    }
+    float h2[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {  // row_half_mirror: c <-> 7 - c within each half (bit 2 differs)
+        const float keep = b2 ? h4[2 + j] : h4[j], send = b2 ? h4[j] : h4[2 + j];
+        h2[j] = keep + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(send), 0x141, 0xF, 0xF, false));
+    }
+    // quad_perm 3,2,1,0 (bit 1 differs), then quad_perm 1,0,3,2 (bit 0)
+    const float keep = b1 ? h2[1] : h2[0], send = b1 ? h2[0] : h2[1];
+    const float h1 = keep + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(send), 0x1B, 0xF, 0xF, false));
+    return h1 + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(h1), 0xB1, 0xF, 0xF, false));
+}
+
+// One layer's LayerNorm / ReLU / Dropout backward on the lane's tile row (ln_bwd196's two passes):
+// dy = heads' share + P sources in order; dG rounded to bf16 into dgb (zero past h) and stored;
+// the dgamma / dbeta partial sums of the tile go to gb[n].
+template <int NT, int H, bool DROP, int NP>
+__device__ __forceinline__ void bp_layer(const uint16_t *__restrict__ gsrc, float mu, float rs, const float *sgm,
+                                         const float *sbt, const float (&wh)[NT][2], float b0, float b1,
+                                         const uint2 *const (&pr)[NP > 0 ? NP : 1], const P::Drop &d, uint32_t rowu,
+                                         bool live, int gq, int col, uint2 (&dgb)[NT], uint16_t *dgout,
+                                         float (&gb)[NT]) {
+    namespace R = g2048::lnrow;
+    constexpr float inv_h = 1.0f / (float)H;
+    const bool lastok = 16 * (NT - 1) + 4 * gq < H;
+    auto valid = [&](int n) { return n < NT - 1 || lastok; };
+    uint2 gr[NT];
+#pragma unroll
+    for (int n = 0; n < NT; n++) gr[n] = *reinterpret_cast<const uint2 *>(gsrc + 16 * n + 4 * gq * valid(n));
+    R::f32x2 dzr[NT][2];
+    R::f32x2 s1 = {0.0f, 0.0f}, s2 = {0.0f, 0.0f};
+    const R::f32x2 nmu = {-mu, -mu}, rs2 = {rs, rs};
+    uint4 dpair = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int n = 0; n < NT; n++) {
+        const int f0 = 16 * n + 4 * gq;
+        f32x4_t dy = {0.0f, 0.0f, 0.0f, 0.0f};
+        dy = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[n][0], b0, dy, 0, 0, 0);
+        dy = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[n][1], b1, dy, 0, 0, 0);
+        float t[4] = {dy[0], dy[1], dy[2], dy[3]};
+#pragma unroll
+        for (int i = 0; i < NP; i++) {
+            t[0] += R::bf_lo(pr[i][n].x);
+            t[1] += R::bf_hi(pr[i][n].x);
+            t[2] += R::bf_lo(pr[i][n].y);
+            t[3] += R::bf_hi(pr[i][n].y);
+        }
+        const float4 gm = *reinterpret_cast<const float4 *>(sgm + f0);
+        const float4 bt = *reinterpret_cast<const float4 *>(sbt + f0);
+        const R::f32x2 xh0 = (R::f32x2{R::bf_lo(gr[n].x), R::bf_hi(gr[n].x)} + nmu) * rs2;
+        const R::f32x2 xh1 = (R::f32x2{R::bf_lo(gr[n].y), R::bf_hi(gr[n].y)} + nmu) * rs2;
+        const R::f32x2 z0 = __builtin_elementwise_fma(xh0, R::f32x2{gm.x, gm.y}, R::f32x2{bt.x, bt.y});
+        const R::f32x2 z1 = __builtin_elementwise_fma(xh1, R::f32x2{gm.z, gm.w}, R::f32x2{bt.z, bt.w});
+        const bool on = live && valid(n);
+        float k[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+        if (DROP) {
+            if ((n & 1) == 0) dpair = P::drop_draw4(d, rowu, (uint32_t)(f0 >> 2));
+            P::drop_mult_bits(d, P::drop_half(dpair, (uint32_t)(f0 >> 2)), k);
+        }
+        const R::f32x2 d0 = {(on && z0.x > 0.0f) ? t[0] * k[0] : 0.0f, (on && z0.y > 0.0f) ? t[1] * k[1] : 0.0f};
+        const R::f32x2 d1 = {(on && z1.x > 0.0f) ? t[2] * k[2] : 0.0f, (on && z1.y > 0.0f) ? t[3] * k[3] : 0.0f};
+        dzr[n][0] = d0;
+        dzr[n][1] = d1;
+        const float v8[8] = {d0.x * xh0.x, d0.y * xh0.y, d1.x * xh1.x, d1.y * xh1.y, d0.x, d0.y, d1.x, d1.y};
+        gb[n] += row16_scatter8(v8, col);
+        const R::f32x2 x0 = d0 * R::f32x2{gm.x, gm.y}, x1 = d1 * R::f32x2{gm.z, gm.w};  // dxhat
+        s1 = s1 + x0 + x1;
+        s2 = __builtin_elementwise_fma(x1, xh1, __builtin_elementwise_fma(x0, xh0, s2));
+    }
+    const float m1 = R::xor32_add(R::xor16_add(s1.x + s1.y)) * inv_h;
+    const float m2 = R::xor32_add(R::xor16_add(s2.x + s2.y)) * inv_h;
+    const R::f32x2 nm1 = {-m1, -m1}, nm2 = {-m2, -m2};
+#pragma unroll
+    for (int n = 0; n < NT; n++) {
+        const int f0 = 16 * n + 4 * gq;
+        const float4 gm = *reinterpret_cast<const float4 *>(sgm + f0);
+        const R::f32x2 xh0 = (R::f32x2{R::bf_lo(gr[n].x), R::bf_hi(gr[n].x)} + nmu) * rs2;
+        const R::f32x2 xh1 = (R::f32x2{R::bf_lo(gr[n].y), R::bf_hi(gr[n].y)} + nmu) * rs2;
+        const R::f32x2 o0 = __builtin_elementwise_fma(xh0, nm2, dzr[n][0] * R::f32x2{gm.x, gm.y} + nm1) * rs2;
+        const R::f32x2 o1 = __builtin_elementwise_fma(xh1, nm2, dzr[n][1] * R::f32x2{gm.z, gm.w} + nm1) * rs2;
+        dgb[n] = valid(n) ? make_uint2(R::pack_bf2(o0.x, o0.y), R::pack_bf2(o1.x, o1.y)) : make_uint2(0u, 0u);
+        if (live && valid(n)) *reinterpret_cast<uint2 *>(dgout + f0) = dgb[n];
+    }
+}
+
+// P^T tile chain of one block layer: p[n] = bf16(sum_ks W^T[16 n ..][k-step ks] dG^T) -- the
+// dgrad kernel's k order from zero.  A = W^T by two transposing reads of the row-major image
+// (lane (g, q, p): rows 32 ks + 8 g + q and + 4, columns 16 n + 4 p); k-step rows past h are
+// redirected to row 0 (their B is zero: dG past h is zero).
+template <int NT, int H, int KS, int PW>
+__device__ __forceinline__ void bp_dgrad(const char *wimg, const uint2 (&dgb)[NT], int lane, uint2 (&pout)[NT]) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+    f32x4_t acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; n++) acc[n] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ks++) {
+        const uint4 bf = act_frag<NT>(dgb, ks);
+        const int r1 = 32 * ks + 8 * g + q;
+        const int ra = r1 < H ? r1 : 0, rb = r1 + 4 < H ? r1 + 4 : 0;
+        int oa = ra * PW + 8 * p4, ob = rb * PW + 8 * p4;
+        asm volatile("" : "+v"(oa), "+v"(ob));
+#pragma unroll
+        for (int n = 0; n < NT; n++) {
+            const s16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(wimg + oa + 32 * n));
+            const s16x4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(wimg + ob + 32 * n));
+            const bf16x8_t fa = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(t1, t2, 0, 1, 2, 3, 4, 5, 6, 7));
+            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, as_frag(bf), acc[n], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < NT; n++) pout[n] = make_uint2(pack_bf2(acc[n][0], acc[n][1]), pack_bf2(acc[n][2], acc[n][3]));
+}
+
+template <int H, bool DROP>
+__global__ __launch_bounds__(kBpThreads, 1) void mlp_back_kernel(BpArgs a) {
+    constexpr int NT = (H + 15) / 16, KS = ((H + 7) / 8 * 8 + 31) / 32;
+    constexpr int PW = pr_pitch(H), WB = pr_wbytes(H);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float *sLN = reinterpret_cast<float *>(smem + 2 * WB);  // [layer][gamma | beta][16 NT]
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int gq = lane >> 4, col = lane & 15;
+    const int64_t m = a.m;
+    {  // the block weight images (row-major, forward's pitch) and the LayerNorm affines
+        constexpr int q8 = PW / 8, h4 = H / 4, per = H * q8;
+        const uint16_t *wsrc[2] = {a.w1, a.w2};
+#pragma unroll
+        for (int l = 0; l < 2; l++)
+            for (int c0 = 0; c0 < per; c0 += 8 * kBpThreads) {
+                uint2 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int c = c0 + tid + u * kBpThreads, r = c / q8, q = c - r * q8;
+                    v[u] = (c < per && q < h4) ? *reinterpret_cast<const uint2 *>(wsrc[l] + (int64_t)r * H + 4 * q)
+                                               : make_uint2(0u, 0u);
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int c = c0 + tid + u * kBpThreads, r = c / q8, q = c - r * q8;
+                    if (c < per) *reinterpret_cast<uint2 *>(smem + l * WB + r * PW + 8 * q) = v[u];
+                }
+            }
+        for (int e = tid; e < kMaxLayers * 2 * 16 * NT; e += kBpThreads) {
+            const int l = e / (32 * NT), rem = e - l * 32 * NT, which = rem / (16 * NT), f = rem - which * 16 * NT;
+            const float *src = which ? a.beta[l] : a.gamma[l];
+            sLN[e] = f < H ? src[f] : 0.0f;
+        }
+    }
+    // the heads' A fragments of v_mfma_f32_16x16x4_f32 for the whole launch: lane (k = gq, i = col)
+    // holds W_heads[k][16 n + i] and W_heads[4 + k][..] (rows: wa 0..3, wv, zero)
+    float wh[NT][2];
+#pragma unroll
+    for (int n = 0; n < NT; n++) {
+        const int f = 16 * n + col;
+        wh[n][0] = f < H ? a.wa[gq * H + f] : 0.0f;
+        wh[n][1] = (f < H && gq == 0 && a.wv) ? a.wv[f] : 0.0f;
+    }
+    __syncthreads();
+    const P::Drop d1 = P::make_drop(a.drop[0]), d2 = P::make_drop(a.drop[1]);
+    float gb[kMaxLayers][NT];
+#pragma unroll
+    for (int l = 0; l < kMaxLayers; l++)
+#pragma unroll
+        for (int n = 0; n < NT; n++) gb[l][n] = 0.0f;
+    const int64_t ntile = (m + 15) >> 4;
+    for (int64_t tile = (int64_t)blockIdx.x * (kBpThreads / 64) + wave; tile < ntile;
+         tile += (int64_t)gridDim.x * (kBpThreads / 64)) {
+        const int64_t row = 16 * tile + col;
+        const bool live = row < m;
+        const int64_t rc = live ? row : 0;
+        const uint32_t rowu = (uint32_t)rc;
+        const float b0 = a.dz[rc * 8 + gq];
+        const float b1 = gq == 0 ? a.dz[rc * 8 + 4] : 0.0f;
+        uint2 dgb[NT], p2[NT], p1[NT];
+        // block 2 (top): dy = the heads' share
+        {
+            const uint2 *pr[1] = {nullptr};
+            bp_layer<NT, H, DROP, 0>(a.g[2] + rc * H, a.mean[2][rc], a.rstd[2][rc], sLN + 2 * 32 * NT,
+                                     sLN + 2 * 32 * NT + 16 * NT, wh, b0, b1, pr, d2, rowu, live, gq, col, dgb,
+                                     a.dg[2] + rc * H, gb[2]);
+        }
+        bp_dgrad<NT, H, KS, PW>(smem + WB, dgb, lane, p2);
+        if (a.pout[1] && live) store_tile<NT, H>(a.pout[1], (uint32_t)rc * (2u * H), p2, gq);
+        {  // block 1: + P2
+            const uint2 *pr[1] = {p2};
+            bp_layer<NT, H, DROP, 1>(a.g[1] + rc * H, a.mean[1][rc], a.rstd[1][rc], sLN + 32 * NT, sLN + 48 * NT, wh,
+                                     b0, b1, pr, d1, rowu, live, gq, col, dgb, a.dg[1] + rc * H, gb[1]);
+        }
+        bp_dgrad<NT, H, KS, PW>(smem, dgb, lane, p1);
+        if (a.pout[0] && live) store_tile<NT, H>(a.pout[0], (uint32_t)rc * (2u * H), p1, gq);
+        {  // the stem: + P1 + P2 (the per-layer chain's source order), no dropout
+            const uint2 *pr[2] = {p1, p2};
+            bp_layer<NT, H, false, 2>(a.g[0] + rc * H, a.mean[0][rc], a.rstd[0][rc], sLN, sLN + 16 * NT, wh, b0, b1,
+                                      pr, d1, rowu, live, gq, col, dgb, a.dg[0] + rc * H, gb[0]);
+        }
+    }
+    // dgamma / dbeta: lane (gq, col) even col holds slot s = col >> 1 of its feature groups
+    // (s < 4: dgamma of feature 16 n + 4 gq + s, else dbeta of feature s - 4); block sum in LDS
+    __syncthreads();
+    float *red = reinterpret_cast<float *>(smem);  // [wave][layer][2][16 NT]
+    constexpr int RW = kMaxLayers * 2 * 16 * NT;
+    if ((col & 1) == 0) {
+        const int s = col >> 1, which = s >> 2, e = s & 3;
+#pragma unroll
+        for (int l = 0; l < kMaxLayers; l++)
+#pragma unroll
+            for (int n = 0; n < NT; n++) red[wave * RW + (l * 2 + which) * 16 * NT + 16 * n + 4 * gq + e] = gb[l][n];
+    }
+    __syncthreads();
+    const int nb = gridDim.x;
+    for (int c = tid; c < kMaxLayers * 2 * H; c += kBpThreads) {  // partial rows [layer][block][dgamma h | dbeta h]
+        const int l = c / (2 * H), rem = c - l * 2 * H, which = rem >= H, f = rem - which * H;
+        const int src = (l * 2 + which) * 16 * NT + f;
+        float t = 0.0f;
+#pragma unroll
+        for (int w = 0; w < kBpThreads / 64; w++) t += red[w * RW + src];
+        a.part[((int64_t)l * nb + blockIdx.x) * 2 * H + rem] = t;
+    }
+}
+
 inline int fp_status() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK : (int)e;
@@ -480,6 +743,25 @@ int fp_launch(hipStream_t s, const FpArgs &a, int h, int nb) {
     return a.drop[0].thr != 0u ? fp_launch2<TRAIN, true>(s, a, h, nb) : fp_launch2<TRAIN, false>(s, a, h, nb);
 }
 
+int bp_blocks(int64_t m) {
+    const int64_t t = ((m + 15) / 16 + kBpThreads / 64 - 1) / (kBpThreads / 64);
+    return (int)(t < 1 ? 1 : (t > 256 ? 256 : t));
+}
+
+template <bool DROP>
+int bp_launch2(hipStream_t s, const BpArgs &a, int h, int nb) {
+    const size_t lds = fp_lds(h);
+    switch (h) {
+    case 196: hipLaunchKernelGGL((mlp_back_kernel<196, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    case 192: hipLaunchKernelGGL((mlp_back_kernel<192, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    case 128: hipLaunchKernelGGL((mlp_back_kernel<128, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    case 64: hipLaunchKernelGGL((mlp_back_kernel<64, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    case 32: hipLaunchKernelGGL((mlp_back_kernel<32, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    default: return G2048_EINVAL;
+    }
+    return fp_status();
+}
+
 }  // namespace
 
 extern "C" {
@@ -514,6 +796,73 @@ int g2048_ppo_forward_loss(g2048_stream_t stream, const g2048_mlp_pass_args *p, 
     float *dst[3] = {dba, dbv, sums};
     const int len[3] = {4, 1, 3};
     return fp_colsum(s, p->partials, nb, kTrainParts, -1, dst, len, 3, defer);
+}
+
+size_t g2048_mlp_back_partials(int64_t m, int32_t hidden) {
+    if (m <= 0 || hidden <= 0) return 0;
+    return (size_t)kMaxLayers * bp_blocks(m) * 2 * hidden;
+}
+
+int g2048_ppo_backward(g2048_stream_t stream, const g2048_mlp_back_args *p, float *const *dgamma, float *const *dbeta,
+                       g2048_colsum_job *defer) {
+    if (!p || !dgamma || !dbeta) return G2048_EINVAL;
+    const int h = p->hidden;
+    if (!fp_shape(h) || p->m <= 0 || p->m * 2 * h >= (int64_t(1) << 32)) return G2048_EINVAL;
+    if (!p->w_block[0] || !p->w_block[1] || !p->wa || !p->dz || !p->partials || !al(p->dz, 16) ||
+        !al(p->w_block[0], 8) || !al(p->w_block[1], 8))
+        return G2048_EINVAL;
+    BpArgs a{};
+    a.m = p->m;
+    a.w1 = (const uint16_t *)p->w_block[0];
+    a.w2 = (const uint16_t *)p->w_block[1];
+    for (int l = 0; l < kMaxLayers; l++) {
+        if (!p->ln_gamma[l] || !p->ln_beta[l] || !p->g[l] || !p->mean[l] || !p->rstd[l] || !p->dg[l] || !dgamma[l] ||
+            !dbeta[l] || !al(p->g[l], 8) || !al(p->dg[l], 8))
+            return G2048_EINVAL;
+        a.gamma[l] = p->ln_gamma[l];
+        a.beta[l] = p->ln_beta[l];
+        a.g[l] = (const uint16_t *)p->g[l];
+        a.mean[l] = p->mean[l];
+        a.rstd[l] = p->rstd[l];
+        a.dg[l] = (uint16_t *)p->dg[l];
+    }
+    a.wa = p->wa;
+    a.wv = p->wv;
+    a.dz = p->dz;
+    a.drop[0] = P::drop_args(&p->drop[0]);
+    a.drop[1] = P::drop_args(&p->drop[1]);
+    if ((a.drop[0].thr != 0u) != (a.drop[1].thr != 0u)) return G2048_EINVAL;
+    a.part = p->partials;
+    for (int i = 0; i < 2; i++) {
+        if (p->p_out[i] && !al(p->p_out[i], 8)) return G2048_EINVAL;
+        a.pout[i] = (uint16_t *)p->p_out[i];
+    }
+    const hipStream_t s = (hipStream_t)stream;
+    const int nb = bp_blocks(p->m);
+    const int rc = a.drop[0].thr != 0u ? bp_launch2<true>(s, a, h, nb) : bp_launch2<false>(s, a, h, nb);
+    if (rc) return rc;
+    const int w = 2 * h;
+    for (int l = 0; l < kMaxLayers; l++) {  // one column-sum job per layer: [dgamma | dbeta] rows of 2 h
+        float *dst[2] = {dgamma[l], dbeta[l]};
+        const int len[2] = {h, h};
+        g2048_colsum_job job{};
+        job.part = p->partials + (size_t)l * nb * w;
+        job.nb = nb;
+        job.cols = w;
+        job.max_col = -1;
+        job.nseg = 2;
+        job.dst[0] = dst[0];
+        job.dst[1] = dst[1];
+        job.len[0] = len[0];
+        job.len[1] = len[1];
+        if (defer) {
+            defer[l] = job;
+        } else {
+            const int st = g2048_colsum_batch(stream, &job, 1);
+            if (st) return st;
+        }
+    }
+    return fp_status();
 }
 
 int g2048_ppo_forward_kl(g2048_stream_t stream, const g2048_mlp_pass_args *p, float *out, g2048_colsum_job *defer) {

@@ -38,7 +38,7 @@ EXPORTED = (
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
     "g2048_head_split_bytes", "g2048_head_split", "g2048_mlp_pass_supported", "g2048_mlp_pass_partials",
-    "g2048_ppo_forward_loss", "g2048_ppo_forward_kl",
+    "g2048_ppo_forward_loss", "g2048_ppo_forward_kl", "g2048_mlp_back_partials", "g2048_ppo_backward",
     # include/g2048_urm.h
     "g2048_urm_stem", "g2048_urm_attention", "g2048_urm_residual_rms", "g2048_urm_swiglu_conv",
     "g2048_urm_pool_heads", "g2048_urm_linear_supported", "g2048_urm_linear", "g2048_urm_linear_rms",
@@ -144,6 +144,14 @@ class MlpPassArgs(ctypes.Structure):
                 ("partials", vp)]
 
 
+class MlpBackArgs(ctypes.Structure):
+    """struct g2048_mlp_back_args"""
+    vp = ctypes.c_void_p
+    _fields_ = [("m", ctypes.c_int64), ("hidden", ctypes.c_int32), ("pad_", ctypes.c_int32), ("w_block", vp * 2),
+                ("ln_gamma", vp * 3), ("ln_beta", vp * 3), ("wa", vp), ("wv", vp), ("dz", vp), ("g", vp * 3),
+                ("mean", vp * 3), ("rstd", vp * 3), ("drop", Dropout * 2), ("dg", vp * 3), ("p_out", vp * 2), ("partials", vp)]
+
+
 class PolicyRolloutArgs(ctypes.Structure):
     """struct g2048_policy_rollout_args"""
     vp = ctypes.c_void_p
@@ -220,6 +228,9 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_mlp_pass_supported": (ctypes.c_int, [i32, i32]),
         "g2048_mlp_pass_partials": (sz, [i64, i32]),
         "g2048_ppo_forward_loss": (ctypes.c_int, [vp, ctypes.POINTER(MlpPassArgs), vp, vp, vp, jp]),
+        "g2048_mlp_back_partials": (sz, [i64, i32]),
+        "g2048_ppo_backward": (ctypes.c_int, [vp, ctypes.POINTER(MlpBackArgs), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                              jp]),
         "g2048_ppo_forward_kl": (ctypes.c_int, [vp, ctypes.POINTER(MlpPassArgs), vp, jp]),
         "g2048_linear_dgrad_supported": (ctypes.c_int, [i32, i32]),
         "g2048_linear_dgrad": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
@@ -609,6 +620,52 @@ def ppo_forward_kl(args: MlpPassArgs, out, defer: ColsumJob | None = None):
     """The fused KL re-forward of one minibatch: out[2] = {sum KL, max KL}."""
     _check(load().g2048_ppo_forward_kl(_stream(out), ctypes.byref(args), _dev(out, torch.float32, "out"),
                                        _defer(defer)), "g2048_ppo_forward_kl")
+
+
+def mlp_back_partials(m: int, h: int) -> int:
+    return int(load().g2048_mlp_back_partials(int(m), int(h)))
+
+
+def make_mlp_back(m: int, w_blocks, gammas, betas, wa, wv, dz, g, mean, rstd, drops=(None, None), dg=(None,) * 3,
+                  partials=None, p_out=(None, None)) -> MlpBackArgs:
+    """struct g2048_mlp_back_args for g2048_ppo_backward (GameMLP, 2 blocks)."""
+    a = MlpBackArgs()
+    a.m = int(m)
+    a.hidden = int(w_blocks[0].shape[0])
+    for i, w in enumerate(w_blocks):
+        a.w_block[i] = _dev(w, torch.bfloat16, f"w_block[{i}]")
+    for i, (gm, bt) in enumerate(zip(gammas, betas)):
+        a.ln_gamma[i], a.ln_beta[i] = _dev(gm, torch.float32, "gamma"), _dev(bt, torch.float32, "beta")
+    a.wa, a.wv = _dev(wa, torch.float32, "wa"), _dev(wv, torch.float32, "wv")
+    a.dz = _dev(dz, torch.float32, "dz")
+    for i in range(3):
+        a.g[i] = _dev(g[i], torch.bfloat16, f"g[{i}]")
+        a.mean[i] = _dev(mean[i], torch.float32, f"mean[{i}]")
+        a.rstd[i] = _dev(rstd[i], torch.float32, f"rstd[{i}]")
+        a.dg[i] = _dev(dg[i], torch.bfloat16, f"dg[{i}]")
+    for i in range(2):
+        a.p_out[i] = _dev(p_out[i], torch.bfloat16, f"p_out[{i}]")
+    for i, d in enumerate(drops):
+        if d is not None:
+            a.drop[i] = d
+    a.partials = _dev(partials, torch.float32, "partials")
+    return a
+
+
+def ppo_backward(args: MlpBackArgs, dgamma, dbeta, defer=None, like=None):
+    """The fused MLP backward of one minibatch (three dG, the LayerNorm affine gradients); defer: a
+    list of three ColsumJob filled instead of summing at once."""
+    vp = ctypes.c_void_p
+    dgp = (vp * 3)(*[_dev(t, torch.float32, "dgamma") for t in dgamma])
+    dbp = (vp * 3)(*[_dev(t, torch.float32, "dbeta") for t in dbeta])
+    jobs = None
+    if defer is not None:
+        jobs = (ColsumJob * 3)()
+    _check(load().g2048_ppo_backward(_stream(like if like is not None else dgamma[0]), ctypes.byref(args), dgp, dbp,
+                                     jobs), "g2048_ppo_backward")
+    if defer is not None:
+        for i in range(3):
+            defer[i] = jobs[i]
 
 
 def dropout_mask(m: int, h: int, drop: Dropout, mask):

@@ -9,9 +9,10 @@ action/value heads), FusedPPOUpdater writes the forward and backward out by hand
               H_l = H_{l-1} + Drop(ReLU(LN(G_l)))             (hipBLASLt + g2048_ln_act_fwd beyond h=256)
     loss      heads + PPO-clip + entropy + smooth-L1 and      g2048_ppo_head_loss
               d/dH_L, d/d(head params), loss sums
-    backward  dG_l, dgamma_l, dbeta_l from dy_l =            g2048_ln_act_bwd
-              heads(dz) + sum_{j>l} P_j
-              P_l = dG_l W_l                                  GEMM (hipBLASLt)
+    backward  dG_l, dgamma_l, dbeta_l from dy_l =            g2048_ln_act_bwd (after the fused train pass:
+              heads(dz) + sum_{j>l} P_j                        all layers and P_l in ONE launch,
+              P_l = dG_l W_l                                  g2048_ppo_backward; else per layer, P_l on
+                                                              g2048_linear_dgrad)
               dW_l = dG_l^T H_{l-1}                           g2048_wgrad (bf16 MFMA, fp32 straight
                                                               into the flat gradient bucket)
     step      [RCCL all-reduce] clip, Muon + AdamW            dist.GradBucket / optim.MuonAdamW
@@ -136,12 +137,20 @@ class FusedPPOUpdater(PPOUpdater):
             self.part_wh = torch.empty(L.wgrad_partials(bs, 16, h), dtype=f32, device=d)
             self.wh_spill = torch.empty(3 * h, dtype=f32, device=d)  # rows 5..7 of dz^T H2 (zero columns)
             self.wh_out = torch.empty(16, h, dtype=f32, device=d)   # (unused: the job's segments route it)
+            # the fused backward (g2048_ppo_backward): every layer's dG kept for its weight gradient
+            self.DG = [torch.empty(bs, h, dtype=bf, device=d) for _ in range(nl)]
+            self.part_back = torch.empty(L.mlp_back_partials(bs, h), dtype=f32, device=d)
         self.bs = bs
 
     def _drop(self, layer: int, pass_: int):
         return L.make_dropout(self.p_drop if self.model.training else 0.0, layer, pass_, self.seed, 0, self.counter)
 
     force_layer_kernels = False  # tests: the per-layer kernel chain instead of the fused passes
+    force_layer_backward = False  # tests: the fused train pass with the per-layer backward chain
+
+    @property
+    def fused_back(self) -> bool:
+        return self.fused_pass and all(self.wg_ok) and not self.force_layer_backward
 
     @torch.no_grad()
     def refresh_weights(self):
@@ -202,10 +211,29 @@ class FusedPPOUpdater(PPOUpdater):
             x = self.H[l]
         return x
 
+    def fused_backward(self, jobs):
+        """The backward after the fused train pass: g2048_ppo_backward (three LayerNorm backwards and
+        the two block input gradients in one launch), then the three weight gradients dW_l = dG_l^T
+        X_l on g2048_wgrad; every column sum deferred into `jobs`."""
+        ln = self.ln
+        args = L.make_mlp_back(self.bs, self.wbf[1:], [x.weight for x in ln], [x.bias for x in ln], self.wa,
+                               None if self.decouple else self.wv, self.dz, self.G, self.mean, self.rstd,
+                               drops=(self._drop(1, 0), self._drop(2, 0)), dg=self.DG, partials=self.part_back)
+        jb = [L.ColsumJob() for _ in range(3)]
+        L.ppo_backward(args, [x.weight.grad for x in ln], [x.bias.grad for x in ln], defer=jb)
+        jobs.extend(jb)
+        for l in range(len(self.lin)):
+            jobs.append(L.ColsumJob())
+            L.wgrad(self.DG[l], self.H[l - 1] if l > 0 else self.x0, self.part_wg[l], self.lin[l].grad, defer=jobs[-1])
+        for i in range(0, len(jobs), L.COLSUM_MAX_JOBS):
+            L.colsum_batch(jobs[i:i + L.COLSUM_MAX_JOBS])
+
     def loss_backward(self, data, idx, beta, jobs=None):
         """Heads + PPO loss (unless the fused train pass did them: its `jobs`) + backward of the
         minibatch; gradients land in the GradBucket views."""
         nl = len(self.lin)
+        if jobs is not None and self.fused_back:
+            return self.fused_backward(jobs)
         if jobs is None:
             batch = L.make_ppo_batch(idx, data["actions"], data["legal"], data["logp"], data["adv"], data["ret"],
                                      rows=self.rows)

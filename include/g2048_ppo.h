@@ -264,6 +264,32 @@ int g2048_ppo_forward_loss(g2048_stream_t stream, const g2048_mlp_pass_args *arg
                            g2048_colsum_job *defer);
 int g2048_ppo_forward_kl(g2048_stream_t stream, const g2048_mlp_pass_args *args, float *out, g2048_colsum_job *defer);
 
+/* The MLP's backward after the train pass, in one launch (replaces the per-layer chain of three
+ * g2048_ln_act_bwd and two g2048_linear_dgrad): per row tile the top block's LayerNorm / ReLU /
+ * Dropout backward from the heads' share dz W_heads, its input gradient P2 = dG2 W2 (bf16), block
+ * 1 from dz W_heads + P2, P1 = dG1 W1, the stem from dz W_heads + P1 + P2 -- P and dy stay in
+ * registers.  Writes dG of the three layers (the weight gradients' operands, bitwise the chain's)
+ * and the LayerNorm affine gradients (dgamma[l], dbeta[l]; summed in another order than
+ * g2048_ln_act_bwd) through per-block partial rows [3][nb][2 h] (g2048_mlp_back_partials floats):
+ * immediately, or as three deferred column-sum jobs defer[0..2]. */
+typedef struct g2048_mlp_back_args {
+    int64_t m;
+    int32_t hidden, pad_;
+    const void *w_block[2];        /* bf16 [h][h] (blocks 1, 2), 8-byte aligned */
+    const float *ln_gamma[3], *ln_beta[3];
+    const float *wa, *wv;          /* fp32 heads [4][h], [h] (wv NULL: decoupled critic) */
+    const float *dz;               /* fp32 [m][8]: the train pass's head output gradient */
+    const void *g[3];              /* bf16 [m][h] pre-norm G of the train pass */
+    const float *mean[3], *rstd[3];
+    g2048_dropout drop[2];         /* blocks 1, 2: the train pass's draws */
+    void *dg[3];                   /* out: bf16 [m][h] */
+    void *p_out[2];                /* optional out: bf16 [m][h] P1, P2 (tests) */
+    float *partials;
+} g2048_mlp_back_args;
+size_t g2048_mlp_back_partials(int64_t m, int32_t hidden);
+int g2048_ppo_backward(g2048_stream_t stream, const g2048_mlp_back_args *args, float *const *dgamma,
+                       float *const *dbeta, g2048_colsum_job *defer);
+
 /* Accumulates one minibatch into the update statistics (train.py:603-642): stats[0..7] +=
  * {loss, policy_loss, entropy_loss, value_loss, grad_norm, entropy, kl_total, kl_average} from the
  * head_loss sums, the KL {sum, max}, the pre-clip gradient norm and beta; stats[8] = max(stats[8],

@@ -1095,3 +1095,81 @@ def test_muon_square_schedule_equals_generic(dev, h, monkeypatch):
         outs.append(torch.cat([p.detach().reshape(-1) for p in m.parameters()]).clone())
     assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("h,m,p,decouple", [(196, 65536, 0.1, False), (196, 4099, 0.0, False), (196, 333, 0.1, True),
+                                            (128, 1000, 0.25, False), (64, 700, 0.1, False), (192, 500, 0.1, False)])
+def test_fused_backward_matches_layer_chain(dev, h, m, p, decouple):
+    """g2048_ppo_backward (the three LayerNorm backwards and both block input gradients of a
+    minibatch in one launch) against the per-layer chain it replaces (g2048_ln_act_bwd x 3 with
+    the heads' share and the kept P_j, g2048_linear_dgrad x 2) on the same forward (g2048_mlp_fwd,
+    same dropout masks) and head gradient dz: every layer's dG bitwise (h = 192: the chain's input
+    gradient is a library GEMM, so to bf16 rounding; elsewhere rare one-ulp bf16 flips of values on
+    a rounding edge -- h != 196 compares with the generic LayerNorm backward, another row-sum
+    order), the block input gradients bitwise in every row whose dG is, dgamma / dbeta to fp32
+    summation order."""
+    from g2048 import _lib as L
+    w, gam, bet, (wa, ba, wv, bv), data, idx, ctr = _pass_case(dev, h, 2 * m, m, p, h + 7 * m)
+    wv = None if decouple else wv
+    drops = [L.make_dropout(p, l, 0, 321, 0, ctr) for l in (1, 2)]
+    bf = torch.bfloat16
+    x0 = torch.empty(m, 48, dtype=bf, device=dev)
+    L.obs_gather(data["boards"], idx, x0)
+    G = [torch.empty(m, h, dtype=bf, device=dev) for _ in range(3)]
+    H = [torch.empty(m, h, dtype=bf, device=dev) for _ in range(3)]
+    mu = [torch.empty(m, device=dev) for _ in range(3)]
+    rs = [torch.empty(m, device=dev) for _ in range(3)]
+    x = x0
+    for l in range(3):
+        L.mlp_fwd(x, w[l], gam[l], bet[l], l > 0, G[l], H[l], mu[l], rs[l], drops[l - 1] if l > 0 else None)
+        x = H[l]
+    gen = torch.Generator(device=dev).manual_seed(m)
+    dz = torch.zeros(m, 8, device=dev)
+    dz[:, :5] = torch.randn(m, 5, generator=gen, device=dev) / m
+    head = (dz, wa, wv)
+    # the per-layer chain
+    dg0 = [torch.empty(m, h, dtype=bf, device=dev) for _ in range(3)]
+    P = [None, torch.empty(m, h, dtype=bf, device=dev), torch.empty(m, h, dtype=bf, device=dev)]
+    dgam0 = [torch.empty(h, device=dev) for _ in range(3)]
+    dbet0 = [torch.empty(h, device=dev) for _ in range(3)]
+    part = torch.empty(L.ln_act_bwd_partials(m, h), device=dev)
+    for l in (2, 1, 0):
+        dy = L.make_dy(None, P[l + 1:], head)
+        L.ln_act_bwd(None, None, G[l], mu[l], rs[l], gam[l], bet[l], dg0[l], None, part, dgam0[l], dbet0[l],
+                     drops[l - 1] if l > 0 else None, dy=dy)
+        if l > 0:
+            if L.linear_dgrad_supported(h, h):
+                L.linear_dgrad(dg0[l], w[l], P[l])
+            else:
+                P[l].copy_(dg0[l] @ w[l])
+    # the fused backward
+    dg1 = [torch.full((m, h), float("nan"), dtype=bf, device=dev) for _ in range(3)]
+    dgam1 = [torch.full((h,), float("nan"), device=dev) for _ in range(3)]
+    dbet1 = [torch.full((h,), float("nan"), device=dev) for _ in range(3)]
+    p1 = [torch.full((m, h), float("nan"), dtype=bf, device=dev) for _ in range(2)]
+    args = L.make_mlp_back(m, w[1:], gam, bet, wa, wv, dz, G, mu, rs, drops=drops, dg=dg1,
+                           partials=torch.empty(L.mlp_back_partials(m, h), device=dev), p_out=p1)
+    L.ppo_backward(args, dgam1, dbet1)
+    torch.cuda.synchronize()
+    exact = L.linear_dgrad_supported(h, h)
+    for l in (1, 2):  # the block input gradients: the dgrad kernel's MFMA order -> bitwise in every row
+        if exact:         # whose dG_l row is bitwise
+            same = (dg1[l].view(torch.int16) == dg0[l].view(torch.int16)).all(1)
+            assert torch.equal(p1[l - 1][same], P[l][same]), l
+    for l in (2, 1, 0):
+        if exact or l == 2:
+            # bitwise up to rare one-ulp bf16 roundings of fp32 values that sit on a rounding edge
+            # (the two translation units contract one of the LayerNorm-backward fmas differently)
+            # (h != 196: the chain's generic LayerNorm backward sums the rows in another order)
+            ne = dg1[l].view(torch.int16) != dg0[l].view(torch.int16)
+            assert int(ne.sum()) <= max(2, m * h // (100000 if h == 196 else 1000)), (l, int(ne.sum()))
+            d = (dg1[l].float() - dg0[l].float()).abs()
+            tol = dg0[l].float().abs() / 64 + (0.0 if h == 196 else 2e-3 * dg0[l].float().abs().max().item()) + 1e-30
+            assert bool((d <= tol).all()), (l, d.max())  # (cancellation near zero: absolute, 2e-3 of the scale)
+        else:
+            cos = F.cosine_similarity(dg1[l].double().reshape(1, -1), dg0[l].double().reshape(1, -1)).item()
+            assert cos > 0.9999, (l, cos)
+        for a, b in ((dgam1[l], dgam0[l]), (dbet1[l], dbet0[l])):
+            scale = b.abs().max().item() + 1e-30
+            assert (a - b).abs().max().item() <= (1e-5 if h == 196 else 5e-4) * scale + (0 if exact else 1e-2 * scale), (l, (a - b).abs().max(), scale)
