@@ -171,12 +171,11 @@ __device__ __forceinline__ void ln_epilogue(f32x4_t (&acc)[NT], uint2 (&act)[NT]
 // returned for the backward pass -- bitwise g2048_mlp_fwd's G / Y / mean / rstd.
 // gout (nullable): the layer's G [m][h]; this row's bits are written at once (at byte offset goff,
 // uniform base + 32-bit lane offset: they need no register past the rounding).
-// keep (DROP): the lane's keep bits, bit 4 n + r = feature 16 n + 4 g + r kept (uint2: n < 8 | n >= 8).
 template <int NT, int h, bool RES, bool DROP>
 __device__ __forceinline__ void ln_epilogue_train(f32x4_t (&acc)[NT], uint2 (&act)[NT], const float *sgam,
                                                   const float *sbet, int g, float inv_n, const ppo::Drop &d,
                                                   uint32_t row, uint16_t *gout, uint32_t goff, float &mean,
-                                                  float &rstd, uint2 &keep) {
+                                                  float &rstd) {
     namespace R = lnrow;
     R::f32x2 v[NT][2];
     {
@@ -192,7 +191,6 @@ __device__ __forceinline__ void ln_epilogue_train(f32x4_t (&acc)[NT], uint2 (&ac
     auto valid = [&](int n) { return 16 * n + 4 * g < h; };
     R::stats<NT>(v, valid, inv_n, mean, rstd);
     uint4 dpair = make_uint4(0u, 0u, 0u, 0u);
-    keep = make_uint2(0u, 0u);
 #pragma unroll
     for (int n = 0; n < NT; n++) {
         const int f0 = 16 * n + 4 * g;
@@ -203,11 +201,7 @@ __device__ __forceinline__ void ln_epilogue_train(f32x4_t (&acc)[NT], uint2 (&ac
         if (DROP) {  // tiles n, n + 1 hold column groups 4 n + g, 4 n + 4 + g: one Philox call
             float k[4];
             if ((n & 1) == 0) dpair = ppo::drop_draw4(d, row, (uint32_t)(f0 >> 2));
-            const uint2 w = ppo::drop_half(dpair, (uint32_t)(f0 >> 2));
-            ppo::drop_mult_bits(d, w, k);
-            const uint32_t kb = ppo::drop_keep_bits(d, w) << (4 * (n & 7));
-            if (n < 8) keep.x |= kb;
-            else keep.y |= kb;
+            ppo::drop_mult_bits(d, ppo::drop_half(dpair, (uint32_t)(f0 >> 2)), k);
             y0 = y0 * R::f32x2{k[0], k[1]};
             y1 = y1 * R::f32x2{k[2], k[3]};
         }

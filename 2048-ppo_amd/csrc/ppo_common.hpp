@@ -55,18 +55,6 @@ __device__ __forceinline__ void drop_mult_bits(const Drop &d, uint2 w, float k[4
     k[3] = (w.y >> 16) >= d.thr ? d.scale : 0.0f;
 }
 
-// the keep decisions of drop_mult_bits as 4 bits (bit r: element r kept)
-__device__ __forceinline__ uint32_t drop_keep_bits(const Drop &d, uint2 w) {
-    return (uint32_t)((w.x & 0xFFFFu) >= d.thr) | ((uint32_t)((w.x >> 16) >= d.thr) << 1) |
-           ((uint32_t)((w.y & 0xFFFFu) >= d.thr) << 2) | ((uint32_t)((w.y >> 16) >= d.thr) << 3);
-}
-
-// keep multipliers from 4 stored keep bits (the same 0 or 1/(1-p) as drop_mult_bits)
-__device__ __forceinline__ void drop_mult_kept(const Drop &d, uint32_t bits, float k[4]) {
-#pragma unroll
-    for (int r = 0; r < 4; r++) k[r] = (bits >> r) & 1u ? d.scale : 0.0f;
-}
-
 // keep multipliers (0 or 1/(1-p)) of columns 4cg .. 4cg+3 of `row`
 __device__ __forceinline__ void drop_mult(const Drop &d, uint32_t row, uint32_t cg, float k[4]) {
     drop_mult_bits(d, drop_draw(d, row, cg), k);

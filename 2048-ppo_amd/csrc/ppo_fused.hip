@@ -40,8 +40,8 @@
 using namespace g2048::tile;
 namespace P = g2048::ppo;
 
-static_assert(sizeof(g2048_mlp_pass_args) == 424 && offsetof(g2048_mlp_pass_args, drop) == 176 &&
-                  offsetof(g2048_mlp_pass_args, partials) == 416,
+static_assert(sizeof(g2048_mlp_pass_args) == 408 && offsetof(g2048_mlp_pass_args, drop) == 176 &&
+                  offsetof(g2048_mlp_pass_args, partials) == 400,
               "g2048_mlp_pass_args layout (tests/test_abi.py)");
 
 namespace {
@@ -67,7 +67,6 @@ struct FpArgs {
     float *masked;                 // train: [m][4] out; KL: the stored old masked logits (in)
     float *dz;                     // train: fp32 [m][8]
     uint16_t *dzb;                 // train: bf16 [m][16]: hi(dz) 0..4, lo(dz) 8..12
-    uint2 *dmask[2];               // train: blocks 1, 2 keep bits [m][4] (lane g of a row: nullable)
     float *part;                   // per block: train kTrainParts floats, KL {sum, max}
 };
 
@@ -240,11 +239,9 @@ __global__ __launch_bounds__(kFpThreads, 1) void mlp_pass_kernel(FpArgs a) {
         const float *lnp = sLN + (L_) * 32 * NT;                                                                \
         const bool st = TRAIN && (int64_t)row < m;                                                              \
         float mean, rstd;                                                                                       \
-        uint2 keep;                                                                                             \
         ln_epilogue_train<NT, H, RES_, DROP_>(acc[Q_], act[Q_], lnp, lnp + 16 * NT, g, inv_n, (L_) == 2 ? d2 : d1, \
-                                              row, st ? a.g[L_] : nullptr, row * (2u * H), mean, rstd, keep);   \
+                                              row, st ? a.g[L_] : nullptr, row * (2u * H), mean, rstd);         \
         if (st) {                                                                                               \
-            if (DROP_ && a.dmask[(L_) == 2]) a.dmask[(L_) == 2][row * 4u + (uint32_t)g] = keep;               \
             if (a.h[L_]) store_tile<NT, H>(a.h[L_], row * (2u * H), act[Q_], g);                                \
             if (g == 0 && a.mean[L_]) {                                                                         \
                 a.mean[L_][row] = mean;                                                                         \
@@ -404,7 +401,6 @@ struct BpArgs {
     const uint16_t *g[kMaxLayers];
     const float *mean[kMaxLayers], *rstd[kMaxLayers];
     P::DropArgs drop[2];      // blocks 1, 2 (the train pass's draws)
-    const uint2 *dmask[2];    // their keep bits as the train pass stored them (null: redraw)
     uint16_t *dg[kMaxLayers];  // out bf16 [m][h]
     uint16_t *pout[2];        // optional out bf16 [m][h]: P1, P2
     float *part;              // out [layer][block][2 h]: dgamma | dbeta
@@ -435,12 +431,12 @@ __device__ __forceinline__ float row16_scatter8(const float (&v)[8], int c) {
 // One layer's LayerNorm / ReLU / Dropout backward on the lane's tile row (ln_bwd196's two passes):
 // dy = heads' share + P sources in order; dG rounded to bf16 into dgb (zero past h) and stored;
 // the dgamma / dbeta partial sums of the tile go to gb[n].
-template <int NT, int H, bool DROP, bool KEPT, int NP>
+template <int NT, int H, bool DROP, int NP>
 __device__ __forceinline__ void bp_layer(const uint16_t *__restrict__ gsrc, float mu, float rs, const float *sgm,
                                          const float *sbt, const float (&wh)[NT][2], float b0, float b1,
-                                         const uint2 *const (&pr)[NP > 0 ? NP : 1], const P::Drop &d,
-                                         const uint2 *kept, uint32_t rowu, bool live, int gq, int col,
-                                         uint2 (&dgb)[NT], uint16_t *dgout, float (&gb)[NT]) {
+                                         const uint2 *const (&pr)[NP > 0 ? NP : 1], const P::Drop &d, uint32_t rowu,
+                                         bool live, int gq, int col, uint2 (&dgb)[NT], uint16_t *dgout,
+                                         float (&gb)[NT]) {
     namespace R = g2048::lnrow;
     constexpr float inv_h = 1.0f / (float)H;
     const bool lastok = 16 * (NT - 1) + 4 * gq < H;
@@ -452,7 +448,6 @@ __device__ __forceinline__ void bp_layer(const uint16_t *__restrict__ gsrc, floa
     R::f32x2 s1 = {0.0f, 0.0f}, s2 = {0.0f, 0.0f};
     const R::f32x2 nmu = {-mu, -mu}, rs2 = {rs, rs};
     uint4 dpair = make_uint4(0u, 0u, 0u, 0u);
-    const uint2 kb = (DROP && KEPT) ? kept[rowu * 4u + (uint32_t)gq] : make_uint2(0u, 0u);
 #pragma unroll
     for (int n = 0; n < NT; n++) {
         const int f0 = 16 * n + 4 * gq;
@@ -475,9 +470,7 @@ __device__ __forceinline__ void bp_layer(const uint16_t *__restrict__ gsrc, floa
         const R::f32x2 z1 = __builtin_elementwise_fma(xh1, R::f32x2{gm.z, gm.w}, R::f32x2{bt.z, bt.w});
         const bool on = live && valid(n);
         float k[4] = {1.0f, 1.0f, 1.0f, 1.0f};
-        if (DROP && KEPT) {  // the train pass's keep bits (no Philox redraw)
-            P::drop_mult_kept(d, ((n < 8 ? kb.x : kb.y) >> (4 * (n & 7))) & 0xFu, k);
-        } else if (DROP) {
+        if (DROP) {
             if ((n & 1) == 0) dpair = P::drop_draw4(d, rowu, (uint32_t)(f0 >> 2));
             P::drop_mult_bits(d, P::drop_half(dpair, (uint32_t)(f0 >> 2)), k);
         }
@@ -536,7 +529,7 @@ __device__ __forceinline__ void bp_dgrad(const char *wimg, const uint2 (&dgb)[NT
     for (int n = 0; n < NT; n++) pout[n] = make_uint2(pack_bf2(acc[n][0], acc[n][1]), pack_bf2(acc[n][2], acc[n][3]));
 }
 
-template <int H, bool DROP, bool KEPT>
+template <int H, bool DROP>
 __global__ __launch_bounds__(kBpThreads, 1) void mlp_back_kernel(BpArgs a) {
     constexpr int NT = (H + 15) / 16, KS = ((H + 7) / 8 * 8 + 31) / 32;
     constexpr int PW = pr_pitch(H), WB = pr_wbytes(H);
@@ -599,24 +592,23 @@ __global__ __launch_bounds__(kBpThreads, 1) void mlp_back_kernel(BpArgs a) {
         // block 2 (top): dy = the heads' share
         {
             const uint2 *pr[1] = {nullptr};
-            bp_layer<NT, H, DROP, KEPT, 0>(a.g[2] + rc * H, a.mean[2][rc], a.rstd[2][rc], sLN + 2 * 32 * NT,
-                                           sLN + 2 * 32 * NT + 16 * NT, wh, b0, b1, pr, d2, a.dmask[1], rowu, live, gq,
-                                           col, dgb, a.dg[2] + rc * H, gb[2]);
+            bp_layer<NT, H, DROP, 0>(a.g[2] + rc * H, a.mean[2][rc], a.rstd[2][rc], sLN + 2 * 32 * NT,
+                                     sLN + 2 * 32 * NT + 16 * NT, wh, b0, b1, pr, d2, rowu, live, gq, col, dgb,
+                                     a.dg[2] + rc * H, gb[2]);
         }
         bp_dgrad<NT, H, KS, PW>(smem + WB, dgb, lane, p2);
         if (a.pout[1] && live) store_tile<NT, H>(a.pout[1], (uint32_t)rc * (2u * H), p2, gq);
         {  // block 1: + P2
             const uint2 *pr[1] = {p2};
-            bp_layer<NT, H, DROP, KEPT, 1>(a.g[1] + rc * H, a.mean[1][rc], a.rstd[1][rc], sLN + 32 * NT, sLN + 48 * NT,
-                                           wh, b0, b1, pr, d1, a.dmask[0], rowu, live, gq, col, dgb, a.dg[1] + rc * H,
-                                           gb[1]);
+            bp_layer<NT, H, DROP, 1>(a.g[1] + rc * H, a.mean[1][rc], a.rstd[1][rc], sLN + 32 * NT, sLN + 48 * NT, wh,
+                                     b0, b1, pr, d1, rowu, live, gq, col, dgb, a.dg[1] + rc * H, gb[1]);
         }
         bp_dgrad<NT, H, KS, PW>(smem, dgb, lane, p1);
         if (a.pout[0] && live) store_tile<NT, H>(a.pout[0], (uint32_t)rc * (2u * H), p1, gq);
         {  // the stem: + P1 + P2 (the per-layer chain's source order), no dropout
             const uint2 *pr[2] = {p1, p2};
-            bp_layer<NT, H, false, false, 2>(a.g[0] + rc * H, a.mean[0][rc], a.rstd[0][rc], sLN, sLN + 16 * NT, wh, b0,
-                                             b1, pr, d1, nullptr, rowu, live, gq, col, dgb, a.dg[0] + rc * H, gb[0]);
+            bp_layer<NT, H, false, 2>(a.g[0] + rc * H, a.mean[0][rc], a.rstd[0][rc], sLN, sLN + 16 * NT, wh, b0, b1,
+                                      pr, d1, rowu, live, gq, col, dgb, a.dg[0] + rc * H, gb[0]);
         }
     }
     // dgamma / dbeta: lane (gq, col) even col holds slot s = col >> 1 of its feature groups
@@ -728,10 +720,6 @@ int fp_fill(const g2048_mlp_pass_args *p, FpArgs &a, bool train) {
     a.masked = p->masked;
     a.dz = p->dz;
     a.dzb = (uint16_t *)p->dz_bf16;
-    for (int i = 0; i < 2; i++) {
-        if (train && p->drop_mask[i] && !al(p->drop_mask[i], 8)) return G2048_EINVAL;
-        a.dmask[i] = train ? (uint2 *)p->drop_mask[i] : nullptr;
-    }
     a.part = p->partials;
     return G2048_OK;
 }
@@ -760,15 +748,15 @@ int bp_blocks(int64_t m) {
     return (int)(t < 1 ? 1 : (t > 256 ? 256 : t));
 }
 
-template <bool DROP, bool KEPT>
+template <bool DROP>
 int bp_launch2(hipStream_t s, const BpArgs &a, int h, int nb) {
     const size_t lds = fp_lds(h);
     switch (h) {
-    case 196: hipLaunchKernelGGL((mlp_back_kernel<196, DROP, KEPT>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
-    case 192: hipLaunchKernelGGL((mlp_back_kernel<192, DROP, KEPT>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
-    case 128: hipLaunchKernelGGL((mlp_back_kernel<128, DROP, KEPT>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
-    case 64: hipLaunchKernelGGL((mlp_back_kernel<64, DROP, KEPT>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
-    case 32: hipLaunchKernelGGL((mlp_back_kernel<32, DROP, KEPT>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    case 196: hipLaunchKernelGGL((mlp_back_kernel<196, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    case 192: hipLaunchKernelGGL((mlp_back_kernel<192, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    case 128: hipLaunchKernelGGL((mlp_back_kernel<128, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    case 64: hipLaunchKernelGGL((mlp_back_kernel<64, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    case 32: hipLaunchKernelGGL((mlp_back_kernel<32, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
     default: return G2048_EINVAL;
     }
     return fp_status();
@@ -851,14 +839,7 @@ int g2048_ppo_backward(g2048_stream_t stream, const g2048_mlp_back_args *p, floa
     }
     const hipStream_t s = (hipStream_t)stream;
     const int nb = bp_blocks(p->m);
-    for (int i = 0; i < 2; i++) {
-        if (p->drop_mask[i] && !al(p->drop_mask[i], 8)) return G2048_EINVAL;
-        a.dmask[i] = (const uint2 *)p->drop_mask[i];
-    }
-    if ((a.dmask[0] != nullptr) != (a.dmask[1] != nullptr)) return G2048_EINVAL;
-    const bool drop = a.drop[0].thr != 0u, kept = a.dmask[0] != nullptr;
-    const int rc = drop ? (kept ? bp_launch2<true, true>(s, a, h, nb) : bp_launch2<true, false>(s, a, h, nb))
-                        : bp_launch2<false, false>(s, a, h, nb);
+    const int rc = a.drop[0].thr != 0u ? bp_launch2<true>(s, a, h, nb) : bp_launch2<false>(s, a, h, nb);
     if (rc) return rc;
     const int w = 2 * h;
     for (int l = 0; l < kMaxLayers; l++) {  // one column-sum job per layer: [dgamma | dbeta] rows of 2 h

@@ -141,7 +141,7 @@ class MlpPassArgs(ctypes.Structure):
                 ("ln_beta", vp * 3), ("head_frag", vp), ("ba", vp), ("bv", vp), ("drop", Dropout * 2),
                 ("beta_dev", vp), ("critic", ctypes.c_float), ("clip_eps", ctypes.c_float), ("x0", vp), ("g", vp * 3),
                 ("h", vp * 3), ("mean", vp * 3), ("rstd", vp * 3), ("masked", vp), ("dz", vp), ("dz_bf16", vp),
-                ("drop_mask", vp * 2), ("partials", vp)]
+                ("partials", vp)]
 
 
 class MlpBackArgs(ctypes.Structure):
@@ -149,8 +149,7 @@ class MlpBackArgs(ctypes.Structure):
     vp = ctypes.c_void_p
     _fields_ = [("m", ctypes.c_int64), ("hidden", ctypes.c_int32), ("pad_", ctypes.c_int32), ("w_block", vp * 2),
                 ("ln_gamma", vp * 3), ("ln_beta", vp * 3), ("wa", vp), ("wv", vp), ("dz", vp), ("g", vp * 3),
-                ("mean", vp * 3), ("rstd", vp * 3), ("drop", Dropout * 2), ("drop_mask", vp * 2), ("dg", vp * 3),
-                ("p_out", vp * 2), ("partials", vp)]
+                ("mean", vp * 3), ("rstd", vp * 3), ("drop", Dropout * 2), ("dg", vp * 3), ("p_out", vp * 2), ("partials", vp)]
 
 
 class PolicyRolloutArgs(ctypes.Structure):
@@ -577,7 +576,7 @@ def head_split(wa, wv, frag):
 def make_mlp_pass(boards, batch: PPOBatch, m: int, w_stem, w_blocks, gammas, betas, head_frag, ba, bv=None,
                   drops=(None, None), beta_dev=None, critic=0.0, clip_eps=0.2, decouple=False, x0=None,
                   g=(None, None, None), h=(None, None, None), mean=(None, None, None), rstd=(None, None, None),
-                  masked=None, dz=None, dz_bf16=None, partials=None, drop_mask=(None, None)) -> MlpPassArgs:
+                  masked=None, dz=None, dz_bf16=None, partials=None) -> MlpPassArgs:
     """struct g2048_mlp_pass_args for g2048_ppo_forward_loss / g2048_ppo_forward_kl (GameMLP, 2 blocks)."""
     a = MlpPassArgs()
     a.boards = _dev(boards, torch.int8, "boards")
@@ -606,8 +605,6 @@ def make_mlp_pass(boards, batch: PPOBatch, m: int, w_stem, w_blocks, gammas, bet
     a.masked = _dev(masked, torch.float32, "masked")
     a.dz = _dev(dz, torch.float32, "dz")
     a.dz_bf16 = _dev(dz_bf16, torch.bfloat16, "dz_bf16")
-    for i in range(2):
-        a.drop_mask[i] = _dev(drop_mask[i], torch.int32, f"drop_mask[{i}]")
     a.partials = _dev(partials, torch.float32, "partials")
     return a
 
@@ -630,7 +627,7 @@ def mlp_back_partials(m: int, h: int) -> int:
 
 
 def make_mlp_back(m: int, w_blocks, gammas, betas, wa, wv, dz, g, mean, rstd, drops=(None, None), dg=(None,) * 3,
-                  partials=None, p_out=(None, None), drop_mask=(None, None)) -> MlpBackArgs:
+                  partials=None, p_out=(None, None)) -> MlpBackArgs:
     """struct g2048_mlp_back_args for g2048_ppo_backward (GameMLP, 2 blocks)."""
     a = MlpBackArgs()
     a.m = int(m)
@@ -648,7 +645,6 @@ def make_mlp_back(m: int, w_blocks, gammas, betas, wa, wv, dz, g, mean, rstd, dr
         a.dg[i] = _dev(dg[i], torch.bfloat16, f"dg[{i}]")
     for i in range(2):
         a.p_out[i] = _dev(p_out[i], torch.bfloat16, f"p_out[{i}]")
-        a.drop_mask[i] = _dev(drop_mask[i], torch.int32, f"drop_mask[{i}]")
     for i, d in enumerate(drops):
         if d is not None:
             a.drop[i] = d

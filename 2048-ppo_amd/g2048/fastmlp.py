@@ -139,8 +139,6 @@ class FusedPPOUpdater(PPOUpdater):
             self.wh_out = torch.empty(16, h, dtype=f32, device=d)   # (unused: the job's segments route it)
             # the fused backward (g2048_ppo_backward): every layer's dG kept for its weight gradient
             self.DG = [torch.empty(bs, h, dtype=bf, device=d) for _ in range(nl)]
-            # the train pass's dropout keep bits of blocks 1, 2 (read by the backward: no Philox redraw)
-            self.dmask = [torch.empty(bs, 4, 2, dtype=torch.int32, device=d) for _ in range(2)]
             self.part_back = torch.empty(L.mlp_back_partials(bs, h), dtype=f32, device=d)
         self.bs = bs
 
@@ -176,8 +174,7 @@ class FusedPPOUpdater(PPOUpdater):
         return L.make_mlp_pass(data["boards"], batch, idx.shape[0], bv=self.bv, beta_dev=self._beta_dev,
                                critic=self.cfg.critic, clip_eps=self.cfg.clip_eps, decouple=self.decouple, x0=self.x0,
                                g=self.G, h=self.H, mean=self.mean, rstd=self.rstd, dz=self.dz, dz_bf16=self.dzb,
-                               partials=self.part_fwd, drop_mask=self.dmask if self.fused_back else (None, None),
-                               **common)
+                               partials=self.part_fwd, **common)
 
     def fused_forward_loss(self, data, idx, beta):
         """The train pass in one launch (obs -> GameMLP -> heads -> PPO loss, dz), then the head weight
@@ -221,8 +218,7 @@ class FusedPPOUpdater(PPOUpdater):
         ln = self.ln
         args = L.make_mlp_back(self.bs, self.wbf[1:], [x.weight for x in ln], [x.bias for x in ln], self.wa,
                                None if self.decouple else self.wv, self.dz, self.G, self.mean, self.rstd,
-                               drops=(self._drop(1, 0), self._drop(2, 0)), dg=self.DG, partials=self.part_back,
-                               drop_mask=self.dmask)
+                               drops=(self._drop(1, 0), self._drop(2, 0)), dg=self.DG, partials=self.part_back)
         jb = [L.ColsumJob() for _ in range(3)]
         L.ppo_backward(args, [x.weight.grad for x in ln], [x.bias.grad for x in ln], defer=jb)
         jobs.extend(jb)

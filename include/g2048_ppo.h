@@ -249,8 +249,6 @@ typedef struct g2048_mlp_pass_args {
     float *masked;                 /* train: out; KL: in */
     float *dz;
     void *dz_bf16;
-    void *drop_mask[2];            /* train (optional): blocks 1, 2 keep bits, uint32 [m][4][2] (8-byte
-                                      aligned) -- g2048_ppo_backward reads them instead of redrawing */
     float *partials;
 } g2048_mlp_pass_args;
 
@@ -284,7 +282,6 @@ typedef struct g2048_mlp_back_args {
     const void *g[3];              /* bf16 [m][h] pre-norm G of the train pass */
     const float *mean[3], *rstd[3];
     g2048_dropout drop[2];         /* blocks 1, 2: the train pass's draws */
-    const void *drop_mask[2];      /* optional: the train pass's stored keep bits (both or neither) */
     void *dg[3];                   /* out: bf16 [m][h] */
     void *p_out[2];                /* optional out: bf16 [m][h] P1, P2 (tests) */
     float *partials;
