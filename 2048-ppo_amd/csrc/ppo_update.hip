@@ -723,10 +723,19 @@ __device__ __forceinline__ bf16x8_t wg_frag(const char *buf, int pitch, int kb, 
     return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// gridDim.z == 2: a second product of the same shape (A2, B2 -> part2) in the same launch.
 template <int BI, int BJ, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void wgrad_kernel(const uint16_t *__restrict__ A, const uint16_t *__restrict__ B,
                                                         int64_t M, int n1, int n2, int pa, int pb, int wi_n,
-                                                        int64_t rows_per_block, int bw, float *__restrict__ part) {
+                                                        int64_t rows_per_block, int bw, float *__restrict__ part,
+                                                        const uint16_t *__restrict__ A2 = nullptr,
+                                                        const uint16_t *__restrict__ B2 = nullptr,
+                                                        float *__restrict__ part2 = nullptr) {
+    if (blockIdx.z == 1) {  // block-uniform
+        A = A2;
+        B = B2;
+        part = part2;
+    }
     constexpr int kThr = 64 * NW, kItems = wg_items(kThr), KSPLIT = NW / 4;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1756,7 +1765,7 @@ inline int wg_pitch(int n) {  // LDS row bytes: >= 2 * pad16(n) and == 32 (mod 2
     return b + (((32 - b) % 256) + 256) % 256;
 }
 
-inline bool wg_plan(int64_t m, int n1, int n2, WgPlan &p) {
+inline bool wg_plan(int64_t m, int n1, int n2, WgPlan &p, int64_t rows_target = 512) {
     if (n1 <= 0 || n2 <= 0 || n1 % 4 || n2 % 4 || n1 > 224 || n2 > 224 || m <= 0) return false;
     const int TI = (n1 + 15) / 16, TJ0 = (n2 + 15) / 16;
     // split the output columns into ny bands of whole 16-column tiles when there are enough
@@ -1773,7 +1782,7 @@ inline bool wg_plan(int64_t m, int n1, int n2, WgPlan &p) {
                 p.wi = a[0];
                 p.ny = ny;
                 p.bw = 16 * TJ;
-                int64_t nb = m / 512;
+                int64_t nb = m / rows_target;
                 nb = nb < 1 ? 1 : (nb > 256 ? 256 : nb);
                 int64_t rows = (m + nb - 1) / nb;
                 rows = (rows + kWgRows - 1) / kWgRows * kWgRows;
@@ -2132,33 +2141,69 @@ size_t g2048_wgrad_partials(int64_t m, int32_t n1, int32_t n2) {
     return (size_t)p.nb * n1 * n2 + (size_t)kSlices * n1 * n2;
 }
 
+// one launch of wgrad_kernel for plan p (nz = 2: the pair (a, b) and (a2, b2))
+static int wg_launch(hipStream_t s, const WgPlan &p, int nz, const uint16_t *a, const uint16_t *b, float *part,
+                     const uint16_t *a2, const uint16_t *b2, float *part2, int64_t m, int n1, int n2) {
+    const dim3 grid(p.nb, p.ny, nz), blk(kWgThreads);
+    if (p.bi == 2)
+        hipLaunchKernelGGL((wgrad_kernel<2, 2>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, p.bw,
+                           part, a2, b2, part2);
+    else if (p.bi == 4)
+        hipLaunchKernelGGL((wgrad_kernel<4, 4>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, p.bw,
+                           part, a2, b2, part2);
+    else if (p.wi == 2 && !getenv("G2048_WGRAD_NW4")) {  // 2 x 2 blocks of 7 x 4 tiles: the k-split 8-wave kernel
+        const size_t lds = p.lds > wg_combine_bytes(7, 4) ? p.lds : wg_combine_bytes(7, 4);
+        hipLaunchKernelGGL((wgrad_kernel<7, 4, 8>), grid, dim3(512), lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows,
+                           p.bw, part, a2, b2, part2);
+    } else
+        hipLaunchKernelGGL((wgrad_kernel<7, 4>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, p.bw,
+                           part, a2, b2, part2);
+    return status();
+}
+
 int g2048_wgrad(g2048_stream_t stream, const uint16_t *a, const uint16_t *b, int64_t m, int32_t n1, int32_t n2,
                 float *partials, float *out, g2048_colsum_job *defer) {
     WgPlan p;
     if (!a || !b || !partials || !out || !al(a, 8) || !al(b, 8)) return G2048_EINVAL;
     if (!wg_plan(m, n1, n2, p)) return G2048_EINVAL;
     const hipStream_t s = (hipStream_t)stream;
-    const dim3 grid(p.nb, p.ny), blk(kWgThreads);
-    if (p.bi == 2)
-        hipLaunchKernelGGL((wgrad_kernel<2, 2>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, p.bw,
-                           partials);
-    else if (p.bi == 4)
-        hipLaunchKernelGGL((wgrad_kernel<4, 4>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, p.bw,
-                           partials);
-    else if (p.wi == 2 && !getenv("G2048_WGRAD_NW4")) {  // 2 x 2 blocks of 7 x 4 tiles: the k-split 8-wave kernel
-        const size_t lds = p.lds > wg_combine_bytes(7, 4) ? p.lds : wg_combine_bytes(7, 4);
-        hipLaunchKernelGGL((wgrad_kernel<7, 4, 8>), grid, dim3(512), lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows,
-                           p.bw, partials);
-    } else
-        hipLaunchKernelGGL((wgrad_kernel<7, 4>), grid, blk, p.lds, s, a, b, m, n1, n2, p.pa, p.pb, p.wi, p.rows, p.bw,
-                           partials);
-    const int st = status();
+    const int st = wg_launch(s, p, 1, a, b, partials, nullptr, nullptr, nullptr, m, n1, n2);
     if (st) return st;
     Segs segs{};
     segs.n = 1;
     segs.dst[0] = out;
     segs.len[0] = n1 * n2;
     return colsum(s, partials, p.nb, n1 * n2, partials + (size_t)p.nb * n1 * n2, segs, -1, defer);
+}
+
+size_t g2048_wgrad_pair_partials(int64_t m, int32_t n1, int32_t n2) {
+    WgPlan p;
+    if (!wg_plan(m, n1, n2, p, 1024)) return 0;
+    return (size_t)p.nb * n1 * n2 + (size_t)kSlices * n1 * n2;
+}
+
+int g2048_wgrad_pair(g2048_stream_t stream, const uint16_t *a0, const uint16_t *b0, const uint16_t *a1,
+                     const uint16_t *b1, int64_t m, int32_t n1, int32_t n2, float *partials0, float *partials1,
+                     float *out0, float *out1, g2048_colsum_job *defer) {
+    WgPlan p;
+    if (!a0 || !b0 || !a1 || !b1 || !partials0 || !partials1 || !out0 || !out1 || !al(a0, 8) || !al(b0, 8) ||
+        !al(a1, 8) || !al(b1, 8))
+        return G2048_EINVAL;
+    if (!wg_plan(m, n1, n2, p, 1024)) return G2048_EINVAL;  // twice the rows per block: half the partial rows
+    const hipStream_t s = (hipStream_t)stream;
+    const int st = wg_launch(s, p, 2, a0, b0, partials0, a1, b1, partials1, m, n1, n2);
+    if (st) return st;
+    float *part[2] = {partials0, partials1}, *out[2] = {out0, out1};
+    for (int k = 0; k < 2; k++) {
+        Segs segs{};
+        segs.n = 1;
+        segs.dst[0] = out[k];
+        segs.len[0] = n1 * n2;
+        const int rc = colsum(s, part[k], p.nb, n1 * n2, part[k] + (size_t)p.nb * n1 * n2, segs, -1,
+                              defer ? defer + k : nullptr);
+        if (rc) return rc;
+    }
+    return G2048_OK;
 }
 
 

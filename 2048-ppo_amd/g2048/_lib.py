@@ -31,7 +31,7 @@ EXPORTED = (
     # include/g2048_ppo.h
     "g2048_obs_gather", "g2048_ln_act_fwd", "g2048_ln_act_bwd_partials", "g2048_ln_act_bwd",
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
-    "g2048_wgrad_partials", "g2048_wgrad", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
+    "g2048_wgrad_partials", "g2048_wgrad", "g2048_wgrad_pair_partials", "g2048_wgrad_pair", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
     "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_rms_res_fwd2", "g2048_urm_rms_res_bwd2", "g2048_urm_forward_drop", "g2048_urm_rms_res_fwd",
     "g2048_urm_rms_res_bwd", "g2048_urm_swiglu_conv_partials", "g2048_urm_swiglu_conv_fwd", "g2048_urm_swiglu_conv_bwd",
@@ -215,6 +215,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_dropout_mask": (ctypes.c_int, [vp, i64, i32, dp, vp]),
         "g2048_wgrad_partials": (sz, [i64, i32, i32]),
         "g2048_wgrad": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, vp, vp, jp]),
+        "g2048_wgrad_pair_partials": (sz, [i64, i32, i32]),
+        "g2048_wgrad_pair": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, jp]),
         "g2048_grad_clip": (ctypes.c_int, [vp, vp, i64, ctypes.c_float, vp, vp, vp]),
         "g2048_mlp_fwd_lds_bytes": (sz, [i32, i32]),
         "g2048_mlp_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, i64, i32, i32, dp]),
@@ -687,6 +689,26 @@ def wgrad(a, b, partials, out, defer: ColsumJob | None = None):
     _check(load().g2048_wgrad(_stream(a), _dev(a, torch.bfloat16, "a"), _dev(b, torch.bfloat16, "b"), m, n1, n2,
                               _dev(partials, torch.float32, "partials"), _dev(out, torch.float32, "out"),
                               _defer(defer)), "g2048_wgrad")
+
+
+def wgrad_pair_partials(m: int, n1: int, n2: int) -> int:
+    return int(load().g2048_wgrad_pair_partials(m, n1, n2))
+
+
+def wgrad_pair(a0, b0, a1, b1, partials0, partials1, out0, out1, defer=None):
+    """out0 = a0^T b0 and out1 = a1^T b1 (same shapes) in one launch; defer: a list of two ColsumJob."""
+    m, n1 = a0.shape
+    n2 = b0.shape[1]
+    for a, b, o in ((a0, b0, out0), (a1, b1, out1)):
+        if a.shape != (m, n1) or b.shape != (m, n2) or tuple(o.shape) != (n1, n2):
+            raise G2048Error("wgrad_pair shapes")
+    jobs = (ColsumJob * 2)() if defer is not None else None
+    _check(load().g2048_wgrad_pair(_stream(a0), *[_dev(t, torch.bfloat16, "a/b") for t in (a0, b0, a1, b1)], m, n1, n2,
+                                   _dev(partials0, torch.float32, "partials0"), _dev(partials1, torch.float32, "partials1"),
+                                   _dev(out0, torch.float32, "out0"), _dev(out1, torch.float32, "out1"), jobs),
+           "g2048_wgrad_pair")
+    if defer is not None:
+        defer[0], defer[1] = jobs[0], jobs[1]
 
 
 def colsum_batch(jobs):

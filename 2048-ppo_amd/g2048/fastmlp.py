@@ -140,6 +140,8 @@ class FusedPPOUpdater(PPOUpdater):
             # the fused backward (g2048_ppo_backward): every layer's dG kept for its weight gradient
             self.DG = [torch.empty(bs, h, dtype=bf, device=d) for _ in range(nl)]
             self.part_back = torch.empty(L.mlp_back_partials(bs, h), dtype=f32, device=d)
+            npair = L.wgrad_pair_partials(bs, h, h)
+            self.part_pair = [torch.empty(npair, dtype=f32, device=d) for _ in range(2)] if npair else None
         self.bs = bs
 
     def _drop(self, layer: int, pass_: int):
@@ -222,9 +224,17 @@ class FusedPPOUpdater(PPOUpdater):
         jb = [L.ColsumJob() for _ in range(3)]
         L.ppo_backward(args, [x.weight.grad for x in ln], [x.bias.grad for x in ln], defer=jb)
         jobs.extend(jb)
-        for l in range(len(self.lin)):
-            jobs.append(L.ColsumJob())
-            L.wgrad(self.DG[l], self.H[l - 1] if l > 0 else self.x0, self.part_wg[l], self.lin[l].grad, defer=jobs[-1])
+        jobs.append(L.ColsumJob())
+        L.wgrad(self.DG[0], self.x0, self.part_wg[0], self.lin[0].grad, defer=jobs[-1])
+        if self.part_pair is not None:  # the two block layers' weight gradients in one launch
+            jp = [L.ColsumJob(), L.ColsumJob()]
+            L.wgrad_pair(self.DG[1], self.H[0], self.DG[2], self.H[1], self.part_pair[0], self.part_pair[1],
+                         self.lin[1].grad, self.lin[2].grad, defer=jp)
+            jobs.extend(jp)
+        else:
+            for l in (1, 2):
+                jobs.append(L.ColsumJob())
+                L.wgrad(self.DG[l], self.H[l - 1], self.part_wg[l], self.lin[l].grad, defer=jobs[-1])
         for i in range(0, len(jobs), L.COLSUM_MAX_JOBS):
             L.colsum_batch(jobs[i:i + L.COLSUM_MAX_JOBS])
 

@@ -310,6 +310,14 @@ size_t g2048_wgrad_partials(int64_t m, int32_t n1, int32_t n2);
 int g2048_wgrad(g2048_stream_t stream, const uint16_t *a, const uint16_t *b, int64_t m, int32_t n1, int32_t n2,
                 float *partials, float *out, g2048_colsum_job *defer);
 
+/* Two weight gradients of the same shape in ONE launch (out0 = a0^T b0, out1 = a1^T b1; the fused
+ * backward's two block layers): twice the rows per block of g2048_wgrad, so half its partial rows
+ * for the same CU count; partials* each g2048_wgrad_pair_partials floats; defer: two jobs. */
+size_t g2048_wgrad_pair_partials(int64_t m, int32_t n1, int32_t n2);
+int g2048_wgrad_pair(g2048_stream_t stream, const uint16_t *a0, const uint16_t *b0, const uint16_t *a1,
+                     const uint16_t *b1, int64_t m, int32_t n1, int32_t n2, float *partials0, float *partials1,
+                     float *out0, float *out1, g2048_colsum_job *defer);
+
 /* Input gradient of a Linear layer: out = dg w  (dg bf16 [m, n] = dL/d(output), w bf16 [n, k] = the
  * weight [out, in], out bf16 [m, k] = dL/d(input), fp32 accumulate on bf16 MFMA, one rounding)
  * -- the `dG W` GEMM of the backward pass (replaces the library GEMM).  Square layers with

@@ -1173,3 +1173,28 @@ def test_fused_backward_matches_layer_chain(dev, h, m, p, decouple):
         for a, b in ((dgam1[l], dgam0[l]), (dbet1[l], dbet0[l])):
             scale = b.abs().max().item() + 1e-30
             assert (a - b).abs().max().item() <= (1e-5 if h == 196 else 5e-4) * scale + (0 if exact else 1e-2 * scale), (l, (a - b).abs().max(), scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,h", [(65536, 196), (5000, 196), (777, 64)])
+def test_wgrad_pair_matches_two_wgrads(dev, m, h):
+    """g2048_wgrad_pair (two same-shape weight gradients in one launch, 1024 rows per block) against
+    two g2048_wgrad launches (512 rows per block) and an fp64 reference: same products, another
+    grouping of the row sums (fp32 summation order)."""
+    from g2048 import _lib as L
+    g = torch.Generator(device=dev).manual_seed(m + h)
+    a = [torch.randn(m, h, generator=g, device=dev).to(torch.bfloat16) for _ in range(2)]
+    b = [torch.randn(m, h, generator=g, device=dev).to(torch.bfloat16) for _ in range(2)]
+    out1 = [torch.empty(h, h, device=dev) for _ in range(2)]
+    for k in range(2):
+        L.wgrad(a[k], b[k], torch.empty(L.wgrad_partials(m, h, h), device=dev), out1[k])
+    out2 = [torch.full((h, h), float("nan"), device=dev) for _ in range(2)]
+    n = L.wgrad_pair_partials(m, h, h)
+    assert n > 0
+    L.wgrad_pair(a[0], b[0], a[1], b[1], torch.empty(n, device=dev), torch.empty(n, device=dev), out2[0], out2[1])
+    torch.cuda.synchronize()
+    for k in range(2):
+        ref = a[k].double().t() @ b[k].double()
+        scale = ref.abs().max().item()
+        assert (out2[k].double() - ref).abs().max().item() <= 1e-5 * scale
+        torch.testing.assert_close(out2[k], out1[k], rtol=0, atol=2e-6 * scale)
