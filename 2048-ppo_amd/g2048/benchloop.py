@@ -14,6 +14,17 @@ import time
 
 import torch
 
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 (MI355X_MICROARCH.md), not the 2:1-sparsity figure
+
+
+def mlp_flops_per_sample(h: int = 196, obs: int = 48, layers: int = 2, heads: int = 5) -> dict:
+    """Algorithmic FLOP per sample of GameMLP (game.py:1049-1220): the forward's GEMMs, and the PPO
+    update's train forward + backward (input and weight gradients: 2 x forward, the stem's input
+    gradient excluded) + KL re-forward."""
+    fwd = 2 * (obs * h + layers * h * h + h * heads)
+    bwd = 2 * (obs * h + layers * h * h + h * heads) + 2 * (layers * h * h + h * heads)
+    return {"forward": fwd, "update": fwd + bwd + fwd}
+
 
 def bench_train(args, rank: int, world: int, dev) -> dict:
     import torch.distributed as dist
@@ -45,6 +56,19 @@ def bench_train(args, rank: int, world: int, dev) -> dict:
     tr.train_step(args.train_warmup + args.train_iters)
     steps = args.envs * args.train_horizon * args.train_iters * world
     n_mb = -(-(args.envs * args.train_horizon + m["augmented_samples"]) // args.train_batch)
+    # roofline of the two MFMA phases of the profiled iteration (one GPU's share): algorithmic FLOP
+    # over the phase's wall time against the dense bf16 peak
+    fl = mlp_flops_per_sample()
+    rows_update = n_mb * args.train_batch
+    roof = {}
+    for name, ms_key, flop in (("update", "update_ms", fl["update"] * rows_update),
+                               ("policy_rollout", "rollout_ms", fl["forward"] * args.envs * args.train_horizon)):
+        ms = tr.timings.get(ms_key)
+        if ms:
+            ach = flop / (ms * 1e-3) / 1e12
+            roof[name] = {"bound": "mfma", "achieved": ach, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": ach / MFMA_BF16_PEAK_TFLOPS, "flop_per_sample": fl["update" if name == "update" else "forward"],
+                          "samples": rows_update if name == "update" else args.envs * args.train_horizon}
     return {
         "value": steps / wall, "unit": "env-steps/s", "ms_per_iter": wall / args.train_iters * 1e3,
         "iters": args.train_iters, "warmup": args.train_warmup,
@@ -52,6 +76,8 @@ def bench_train(args, rank: int, world: int, dev) -> dict:
                    "envs_per_gpu": args.envs, "horizon": args.train_horizon, "minibatch": args.train_batch,
                    "minibatches_per_iter": n_mb, "upsample_ratio": args.train_upsample, "optimizer": "Muon(2-D)+AdamW(1-D)", "dtype": "bf16 activations / fp32 master weights (MFMA kernels)"},
         "phase_ms_one_iter": {k: round(v, 3) for k, v in tr.timings.items()},
+        "roofline": roof,
+        "kernel_paths": tr.paths, "fallbacks": tr.fallbacks,
         "last_metrics": {k: m[k] for k in ("loss", "entropy", "avg_score", "episodes_finished", "grad_norm",
                                            "augmented_samples")},
     }
@@ -93,8 +119,12 @@ def bench_urm(args, rank: int, world: int, dev) -> dict:
     c = m.config
     flops_tok = 2 * c.num_loops * c.num_layers * (4 * c.hidden_dim ** 2 + 3 * m.layers[0].mlp.inter * c.hidden_dim
                                                   + 2 * 16 * c.hidden_dim)
+    fwd_tflops = flops_tok * 16 * args.envs / (fwd_ms * 1e-3) / 1e12
     out = {"value": args.envs * T * reps * world / wall, "unit": "env-steps/s", "ms_per_step": wall / (reps * T) * 1e3,
-           "forward_ms": fwd_ms, "forward_TFLOPs": flops_tok * 16 * args.envs / (fwd_ms * 1e-3) / 1e12,
+           "forward_ms": fwd_ms, "forward_TFLOPs": fwd_tflops,
+           "roofline": {"bound": "mfma", "kernel": "URM policy forward (one call, 16 tokens per board)",
+                        "achieved": fwd_tflops, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": fwd_tflops / MFMA_BF16_PEAK_TFLOPS, "flop_per_token": flops_tok},
            "config": {"workload": f"{args.envs} envs/GPU, GameURM h={c.hidden_dim} L={c.num_layers} heads={c.num_heads} "
                                   f"loops={c.num_loops}/{c.num_truncated_loops} inter={m.layers[0].mlp.inter}, bf16",
                       "steps_per_graph": T, "replays": reps}}
@@ -113,6 +143,7 @@ def bench_urm(args, rank: int, world: int, dev) -> dict:
     torch.cuda.synchronize()
     it = time.perf_counter() - t0
     out["train_iter"] = {"value": args.envs * T * world / it, "unit": "env-steps/s", "ms_per_iter": it * 1e3,
+                         "kernel_paths": tr.paths, "fallbacks": tr.fallbacks,
                          "phase_ms": {k: round(v, 3) for k, v in tr.timings.items()},
                          "minibatch": args.train_batch, "loss": mt["loss"], "entropy": mt["entropy"]}
     return out

@@ -163,7 +163,9 @@ class VecTrainer:
         paths = {"policy": type(pol).__name__,
                  "rollout": "policy_rollout_kernel" if getattr(pol, "fused_rollout", False) else "per-step kernels",
                  "update": type(up).__name__,
-                 "update_forward": ("mlp_fwd kernels" if fused_up and all(up.mf_ok)
+                 "update_forward": ("fused train / KL passes + fused backward" if fused_up and mlp and L.mlp_pass_supported(
+                                        self.model.config.hidden_dim, len(self.model.backbone))
+                                    else "mlp_fwd kernels" if fused_up and all(up.mf_ok)
                                     else "hipBLASLt + ln_act_fwd" if fused_up else "autograd"),
                  "optimizer": "fused Muon/AdamW kernels" if getattr(inner, "supported", False) else type(inner).__name__}
         fb = []
