@@ -592,6 +592,18 @@ int dispatch_lin(hipStream_t s, int epi, const uint16_t *in, const uint16_t *w, 
         return dry ? G2048_OK : launch_lin<KS_, CT_, EPI_>(s, in, w, rows, K, N, inter, y, x, emb, xb, eps, cw, cb);
     G2048_LIN(EPI_STORE, 2, 12)   // h 64 qkv
     G2048_LIN(EPI_STORE, 1, 6)    // h 32 qkv
+    // the training Functions' plain projections (URMLinearFn / GateUpSwiGLUFn): the forwards of
+    // o_proj / down_proj and every input gradient dX = dY W, run as dY (W^T)^T with W^T staged
+    G2048_LIN(EPI_STORE, 2, 4)    // h 64: o_proj fwd and dX (K 64, N 64)
+    G2048_LIN(EPI_STORE, 4, 4)    // h 64: down_proj fwd (K 120, N 64)
+    G2048_LIN(EPI_STORE, 6, 4)    // h 64: qkv dX (K 192, N 64)
+    G2048_LIN(EPI_STORE, 2, 8)    // h 64: down_proj dX (K 64, N 120)
+    G2048_LIN(EPI_STORE, 8, 4)    // h 64: gate_up dX (K 240, N 64)
+    G2048_LIN(EPI_STORE, 1, 2)    // h 32: o_proj fwd and dX (K 32, N 32)
+    G2048_LIN(EPI_STORE, 2, 2)    // h 32: down_proj fwd (K 64, N 32)
+    G2048_LIN(EPI_STORE, 3, 2)    // h 32: qkv dX (K 96, N 32)
+    G2048_LIN(EPI_STORE, 1, 4)    // h 32: down_proj dX (K 32, N 64)
+    G2048_LIN(EPI_STORE, 4, 2)    // h 32: gate_up dX (K 128, N 32)
     G2048_LIN(EPI_RMS, 2, 4)      // h 64 o_proj
     G2048_LIN(EPI_RMS, 4, 4)      // h 64 down_proj (K = inter = 120)
     G2048_LIN(EPI_RMS, 1, 2)      // h 32 o_proj

@@ -372,10 +372,30 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     return dw
 
 
+def _gemm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """y bf16 [rows, n] = x w^T for bf16 x [rows, k], w [n, k]: the MFMA projection kernel
+    (g2048_urm_linear) when it covers the shape, else autocast's library GEMM (torch.mm)."""
+    rows, k = x.shape
+    n = w.shape[0]
+    if rows % 16 == 0 and n % 8 == 0 and L.urm_linear_supported(0, k, n):
+        y = torch.empty(rows, n, dtype=torch.bfloat16, device=x.device)
+        L.urm_linear(x, w.contiguous(), y)
+        return y
+    return torch.mm(x, w.t())
+
+
+def gemm_supported(n: int, k: int) -> bool:
+    """Both GEMMs of a projection w [n, k] (forward x w^T and input gradient dy w) run on the MFMA
+    projection kernel (no library GEMM)."""
+    return n % 8 == 0 and k % 8 == 0 and L.urm_linear_supported(0, k, n) and L.urm_linear_supported(0, n, k)
+
+
 class URMLinearFn(torch.autograd.Function):
     """A bias-free projection y = x W^T of the GameURM blocks (qkv_proj, o_proj, down_proj) under bf16
-    autocast: forward and input gradient are the same bf16 GEMMs autocast runs, the weight gradient
-    (a reduction over 16 n token rows) is g2048_urm_wgrad instead of a library GEMM with K = 16 n.
+    autocast: forward and input gradient are autocast's bf16 GEMMs (bf16 operands, fp32
+    accumulation, bf16 result) on the MFMA projection kernel g2048_urm_linear -- the input gradient
+    dY W as dY (W^T)^T with a 16-KB transposed weight copy -- and the weight gradient (a reduction
+    over 16 n token rows) is g2048_urm_wgrad instead of a library GEMM with K = 16 n.
     x [rows, k] (bf16 or fp32: cast like autocast), w [n, k] -> y bf16 [rows, n]."""
 
     @staticmethod
@@ -384,13 +404,13 @@ class URMLinearFn(torch.autograd.Function):
         wb = w.detach().to(torch.bfloat16)
         ctx.save_for_backward(xb, wb)
         ctx.dtypes = (x.dtype, w.dtype)
-        return torch.mm(xb, wb.t())
+        return _gemm(xb, wb)
 
     @staticmethod
     def backward(ctx, dy: torch.Tensor):
         xb, wb = ctx.saved_tensors
         dy = dy.to(torch.bfloat16).contiguous()
-        dx = torch.mm(dy, wb) if ctx.needs_input_grad[0] else None
+        dx = _gemm(dy, wb.t().contiguous()) if ctx.needs_input_grad[0] else None
         dW = _wgrad(dy, xb).to(ctx.dtypes[1])
         return (None if dx is None else dx.to(ctx.dtypes[0])), dW
 
@@ -414,7 +434,8 @@ class GateUpSwiGLUFn(torch.autograd.Function):
     under bf16 autocast, for autograd training on the device: ONE forward kernel
     (g2048_urm_linear_swiglu_train: the projection on MFMA with the SwiGLU-conv epilogue, gu stored
     once for the backward) instead of a library GEMM writing gu and a SwiGLU kernel reading it back;
-    backward = g2048_urm_swiglu_conv_bwd + the projection's two bf16 GEMMs.
+    backward = g2048_urm_swiglu_conv_bwd, the input gradient dgu W on g2048_urm_linear (MFMA) and the
+    weight gradient on g2048_urm_wgrad.
     x [rows, h] (bf16 or fp32: cast like autocast), w [2 inter, h], cw [inter, 2], cb [inter]."""
 
     @staticmethod
@@ -441,7 +462,7 @@ class GateUpSwiGLUFn(torch.autograd.Function):
         db = torch.empty(inter, dtype=torch.float32, device=gu.device)
         part = torch.empty(L.urm_swiglu_conv_partials(rows // 16, inter), dtype=torch.float32, device=gu.device)
         L.urm_swiglu_conv_bwd(gu, cwf, cbf, dact.to(torch.bfloat16).contiguous(), dgu, dw, db, part)
-        dx = torch.mm(dgu, wb)        # autocast's bf16 input-gradient GEMM
+        dx = _gemm(dgu, wb.t().contiguous())  # autocast's bf16 input-gradient GEMM, on MFMA
         dW = _wgrad(dgu, xb)          # the weight gradient on g2048_urm_wgrad (fp32)
         return dx.to(ctx.dtypes[0]), dW.to(ctx.dtypes[1]), dw.to(ctx.dtypes[2]), db.to(ctx.dtypes[3])
 

@@ -142,7 +142,11 @@ int g2048_urm_pool_heads(g2048_stream_t stream, const float *x, const float *wa,
  *   g2048_urm_linear_rms      x = rms_norm(x + y) [+ emb], xb = bf16(x), n = h       (o_proj, down_proj)
  *   g2048_urm_linear_swiglu   out bf16 [rows, inter] = SiLU(conv(SiLU(gate) * up))  (gate_up_proj,
  *                             w [2 inter, h]; the conv as g2048_urm_swiglu_conv)
- * The projection output never goes through HBM.  epilogue: 0 / 1 / 2 as listed. */
+ * The projection output never goes through HBM.  epilogue: 0 / 1 / 2 as listed.
+ * g2048_urm_linear also serves the training Functions' plain GEMMs (game.py:1279-1352 under bf16
+ * autocast, in place of torch.mm / hipBLASLt): the o_proj / down_proj forwards and every input
+ * gradient dX = dY W, called with W^T [k_in, n_out] as `w` (h 64: k x n in {64x64, 120x64, 192x64,
+ * 64x120, 240x64}; h 32 the same shapes halved). */
 int g2048_urm_linear_supported(int32_t epilogue, int32_t k, int32_t n, int32_t inter);
 int g2048_urm_linear(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, uint16_t *out, int64_t rows,
                      int32_t k, int32_t n);

@@ -530,25 +530,38 @@ def test_urm_wgrad_matches_fp64(dev, m, n, k):
     assert torch.equal(got, _wgrad(dy, x))
 
 
-def test_urm_linear_fn_matches_autocast_linear(dev):
-    """URMLinearFn (bf16 GEMMs + g2048_urm_wgrad) vs nn.Linear under bf16 autocast: identical output
-    and input gradient (the same bf16 GEMMs), weight gradient within the autocast path's own bf16
-    rounding of dW (ours stays fp32): max <= 2^-8 of the largest component."""
-    from g2048.urm import URMLinearFn
-    torch.manual_seed(7)
-    lin = torch.nn.Linear(64, 192, bias=False).to(dev)
-    x = torch.randn(16 * 4096, 64, device=dev)
-    g = torch.randn(16 * 4096, 192, device=dev)
+@pytest.mark.parametrize("k,n", [(64, 192), (64, 64), (120, 64), (32, 96), (32, 32), (64, 32)])
+def test_urm_linear_fn_matches_autocast_linear(dev, k, n):
+    """URMLinearFn (forward and input gradient on the MFMA projection kernel g2048_urm_linear, weight
+    gradient on g2048_urm_wgrad) vs nn.Linear under bf16 autocast (hipBLASLt), for every projection
+    shape of GameURM h = 64 / 32 (qkv, o_proj, down_proj).  y and dx are bf16(fp32 sum of bf16
+    products) on both paths, only the summation order differs: each element is within one bf16
+    rounding (2^-8 relative, + 1e-4 absolute for the fp32 summation where a sum nearly cancels) of
+    the fp64 product of the same bf16 operands, and within 2^-7 of autocast's; the weight gradient within the autocast path's own bf16 rounding of dW (ours stays
+    fp32): max <= 2^-8 of the largest component.  No library GEMM runs for these shapes."""
+    from g2048 import urm as U
+    assert U.gemm_supported(n, k)
+    torch.manual_seed(7 + k + n)
+    rows = 16 * 4099
+    lin = torch.nn.Linear(k, n, bias=False).to(dev)
+    x = torch.randn(rows, k, device=dev)
+    g = torch.randn(rows, n, device=dev)
     res = []
     for fused in (True, False):
         lin.zero_grad()
         xi = x.clone().requires_grad_(True)
         with torch.autocast("cuda", dtype=torch.bfloat16):
-            y = URMLinearFn.apply(xi, lin.weight) if fused else lin(xi)
+            y = U.URMLinearFn.apply(xi, lin.weight) if fused else lin(xi)
         (y.float() * g).sum().backward()
         res.append((y.detach(), xi.grad.clone(), lin.weight.grad.clone()))
-    assert torch.equal(res[0][0], res[1][0])
-    assert torch.equal(res[0][1], res[1][1])
+    wb = lin.weight.detach().bfloat16().double()
+    y_ref = x.bfloat16().double() @ wb.t()
+    dx_ref = g.bfloat16().double() @ wb
+    for got, ref, lib in ((res[0][0], y_ref, res[1][0]), (res[0][1], dx_ref, res[1][1])):
+        got, lib = got.double(), lib.double()
+        # + an absolute 1e-4 for the fp32 summation error where the sum nearly cancels
+        assert bool(((got - ref).abs() <= 2 ** -8 * ref.abs() + 1e-4).all())
+        assert bool(((got - lib).abs() <= 2 ** -7 * lib.abs() + 2e-4).all())
     d = (res[0][2] - res[1][2]).abs().max().item()
     assert d <= 2 ** -8 * res[1][2].abs().max().item()
 
