@@ -21,6 +21,7 @@ import torch
 
 from . import _lib as L
 from . import fastmlp
+from . import urm as urm_mod
 from .advantage import RewardWeights, RTGTracker
 from .dist import GradBucket, allreduce_sum_, broadcast_, equal_rows, world
 from .optim import FusedMuonAdamW, MuonAdamW, ScheduledMuonAdamW, build_optimizer
@@ -129,8 +130,12 @@ class VecTrainer:
         self.trim_gen.manual_seed(cfg.seed + 15485863 * (self.rank + 1))
         pcfg = PPOConfig(batch_size=cfg.batch_size, epochs=cfg.epochs, critic=cfg.critic,
                          amp_dtype=torch.bfloat16 if cfg.amp else None)
-        # the autograd update of a GameURM (SDPA backward) runs eagerly; GameMLP's is captured
-        graph_up = cfg.graph_update and not self.episodic and isinstance(self.model, agent.GameMLP)
+        # GameMLP's update is captured in a hipGraph; so is a GameURM's whose every training op is a
+        # device Function (urm.training_graph_ok), otherwise it runs eagerly
+        graph_up = cfg.graph_update and not self.episodic and (
+            isinstance(self.model, agent.GameMLP)
+            or (isinstance(self.model, agent.GameURM) and cfg.amp and self.dev.type == "cuda"
+                and urm_mod.training_graph_ok(self.model)))
         if cfg.fused_update and cfg.amp and self.dev.type == "cuda" and fastmlp.supports(self.model):
             self.ppo = fastmlp.FusedPPOUpdater(self.model, self.opt, pcfg, self.grads, gen, graph=graph_up,
                                                seed=cfg.seed * 31 + self.rank)
@@ -167,7 +172,8 @@ class VecTrainer:
                                         self.model.config.hidden_dim, len(self.model.backbone))
                                     else "mlp_fwd kernels" if fused_up and all(up.mf_ok)
                                     else "hipBLASLt + ln_act_fwd" if fused_up else "autograd"),
-                 "optimizer": "fused Muon/AdamW kernels" if getattr(inner, "supported", False) else type(inner).__name__}
+                 "optimizer": "fused Muon/AdamW kernels" if getattr(inner, "supported", False) else type(inner).__name__,
+                 "update_graph": bool(getattr(up, "graph", False))}
         fb = []
         if mlp and self.dev.type == "cuda":
             h, nl = self.model.config.hidden_dim, len(self.model.backbone)

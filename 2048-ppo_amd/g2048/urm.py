@@ -281,6 +281,19 @@ def train_nograd_forward(model, obs: torch.Tensor):
     return logits, value.view(-1, 1)
 
 
+def training_graph_ok(model) -> bool:
+    """The PPO minibatch step of this GameURM can be captured into one hipGraph (like GameMLP's):
+    every op of its training forward / backward is a device Function or a plain torch op (h 64,
+    16-wide heads, conv kernel 2: the one-launch forward's config, so the KL re-forward is that
+    kernel too) -- no library path that would sync the host inside the capture."""
+    c = model.config
+    st = model.stem
+    return (URMPolicy.supports(model) and c.hidden_dim == 64 and c.hidden_dim == 16 * c.num_heads
+            and 0.0 <= c.dropout < 1.0 and len(st) == 3 and isinstance(st[0], torch.nn.Linear) and st[0].bias is None
+            and L.urm_forward_supported(c.hidden_dim, c.num_heads, model.layers[0].mlp.inter, len(model.layers),
+                                        c.conv_kernel))
+
+
 def stem_supported(model, obs: torch.Tensor) -> bool:
     """The device training stem applies: bf16 autocast on the GPU, h = 64, the default stem
     (Linear(3, 64, bias=False), affine LayerNorm, SiLU), an observation without gradient."""

@@ -238,6 +238,31 @@ def test_urm_trainer_steps(dev, horizon):
     assert "init_hidden" not in moved  # num_truncated_loops = 1: no gradient, not in the optimizer
 
 
+def test_urm_graphed_update_equals_eager(dev):
+    """The GameURM minibatch step captured in one hipGraph (urm.training_graph_ok: every op a device
+    Function) replays to the same parameters, bitwise, as the eager autograd step: two train steps
+    of two trainers from the same seed (dropout 0: the masks are the only draw that differs between
+    the capture warm-up and the eager run), 3 minibatches per step incl. a ragged last one."""
+    from g2048.trainer import TrainConfig, VecTrainer
+    res = []
+    for graph in (True, False):
+        cfg = TrainConfig(steps=4, episodes=256, horizon=10, batch_size=1024, hidden=64, model_type="urm",
+                          dropout=0.0, points=0.1, mono=1.0, rtg_beta=0.99, gamma=0.99, entropy=0.02, critic=0.2,
+                          warmup_steps=0, seed=11)
+        torch.manual_seed(5)
+        tr = VecTrainer(cfg, dev)
+        assert tr.ppo.graph and tr.paths["update_graph"]
+        tr.ppo.graph = graph  # the eager run keeps the same (graph-safe) MuonAdamW optimizer
+        ms = [tr.train_step(s) for s in range(2)]
+        res.append(({k: v.detach().clone() for k, v in tr.model.named_parameters()}, ms))
+    (pg, mg), (pe, me) = res
+    for k in pg:
+        assert torch.equal(pg[k], pe[k]), k
+    for a, b in zip(mg, me):
+        for k in ("loss", "entropy", "grad_norm", "kl_average"):
+            assert a[k] == b[k], (k, a[k], b[k])
+
+
 @pytest.mark.parametrize("h,inter,rows", [(64, 120, 16 * 4097), (32, 64, 16 * 33)])
 def test_urm_fused_projection_kernels(dev, h, inter, rows):
     """g2048_urm_linear / _rms / _swiglu vs torch on the same bf16 operands (fp32 reference of the
