@@ -48,6 +48,14 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(const uint4 *__restric
 }
 
 __device__ const lut::Row12Table kRow12 __attribute__((aligned(16))) = lut::Row12Table();
+__device__ const lut::Line12Table kLine12 __attribute__((aligned(16))) = lut::Line12Table();
+
+// LDS layout of env_rollout_kernel: kRow12 at byte 0 (81 KiB), kLine12 right after it.  Lanes whose
+// board holds an exponent >= 12 still issue the (discarded) table reads with 4-bit-masked digits,
+// i.e. indices up to 15 * 1885 = 28 275: those may land in kLine12 (harmless) and the kLine12
+// reads need the region up to kLineBase + 2 * 28 276 bytes.
+constexpr uint32_t kLineBase = lut::kRowEntries * 4u;                        // 82 944
+constexpr uint32_t kRolloutLdsWords = (kLineBase + 2u * 28276u + 15u) / 16u * 4u;  // 139 504 B
 
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
@@ -63,6 +71,15 @@ __device__ __forceinline__ uint32_t row12_addr(uint32_t x) {
 }
 __device__ __forceinline__ uint32_t lds_word(const uint32_t *tab, uint32_t addr) {
     return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(tab) + addr);
+}
+// LDS byte address of the kLine12 entry of a line dword (byte j = cell j): kLineBase + 2 idx
+__device__ __forceinline__ uint32_t line12_addr(uint32_t x) {
+    const u16x2 k02 = {2, 288}, k13 = {24, 3456};
+    return __builtin_amdgcn_udot2(as_u16x2((x >> 8) & 0x000F000Fu), k13,
+                                  __builtin_amdgcn_udot2(as_u16x2(x & 0x000F000Fu), k02, kLineBase, false), false);
+}
+__device__ __forceinline__ uint32_t lds_half(const uint32_t *tab, uint32_t addr) {
+    return *reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(tab) + addr);
 }
 // byte-reverse each row when the lane's selector says so (one v_perm per row, no select)
 __device__ __forceinline__ uint4 perm4(const uint4 &w, uint32_t sel) {
@@ -169,13 +186,17 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 __device__ __forceinline__ void stage_row_table(uint32_t *s_row) {
     constexpr int kPieces = (int)(lut::kRowEntries * 4u / 1024u);  // 81 pieces of 1 KiB
-    static_assert(lut::kRowEntries * 4u % 1024u == 0u, "whole 1 KiB pieces");
+    constexpr int kLinePieces = (int)(lut::kLineEntriesPadded * 2u / 1024u);  // + 41 of kLine12
+    static_assert(lut::kRowEntries * 4u % 1024u == 0u && lut::kLineEntriesPadded * 2u % 1024u == 0u,
+                  "whole 1 KiB pieces");
     const char *src = reinterpret_cast<const char *>(kRow12.v);
+    const char *src2 = reinterpret_cast<const char *>(kLine12.v);
     char *dst = reinterpret_cast<char *>(s_row);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    for (int c = wave; c < kPieces; c += nw)
-        __builtin_amdgcn_global_load_lds((glb_void_t *)(src + 1024 * c + 16 * lane), (lds_void_t *)(dst + 1024 * c), 16,
-                                         0, 0);
+    for (int c = wave; c < kPieces + kLinePieces; c += nw) {
+        const char *g = c < kPieces ? src + 1024 * c : src2 + 1024 * (c - kPieces);
+        __builtin_amdgcn_global_load_lds((glb_void_t *)(g + 16 * lane), (lds_void_t *)(dst + 1024 * c), 16, 0, 0);
+    }
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0): this wave's pieces have landed
     __syncthreads();
 }
@@ -203,7 +224,7 @@ struct TrajRows {  // row t of each time-major trajectory array
 // One env step of the synthetic random-legal policy (oracle or_step_word + auto-reset).  kOdd = the
 // second step of the pair.  One 32-bit word u per step: action k = floor(u * nlegal / 2^32); the
 // low word r of that product (uniform given k) picks the spawn cell and value (spawn_chain).
-template <bool kOdd>
+template <bool kOdd, bool kSmall = false>
 __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__restrict__ tab, const TrajRows &tr,
                                              uint32_t li, uint64_t seed, uint64_t next_pair, uint32_t env) {
     tr.b[li] = s.b;
@@ -228,20 +249,51 @@ __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__r
     // merge points / 4 of the four rows in the high halves, summed as packed u16
     const uint32_t q = __builtin_bit_cast(uint32_t, (as_u16x2(e0) + as_u16x2(e1)) + (as_u16x2(e2) + as_u16x2(e3)));
     uint32_t pts = (q >> 16) << 2;
-    if (s.sb.M > 11u) {  // an exponent outside the table: the SWAR compute path
+    if (!kSmall && s.sb.M > 11u) {  // an exponent outside the table: the SWAR compute path
         uint32_t mx;
         moved = apply_move(s.b, a, pts, mx);
     }
     const uint32_t rm[4] = {moved.x, moved.y, moved.z, moved.w};
     const uint32_t Zm[4] = {zm(moved.x), zm(moved.y), zm(moved.z), zm(moved.w)};
-    const MonoStats sa = mono_stats_z(rm, Zm, board_max(moved));
-    const int mono_a = mono_value(sa);
+    const uint32_t Ma = board_max(moved);
+    const uint32_t pos_a = first_cell_eq(rm, Ma);
     const int empt_a = __popc(Zm[0]) + __popc(Zm[1]) + __popc(Zm[2]) + __popc(Zm[3]);
     uint32_t sp;
     const uint32_t v = spawn_chain(moved, Zm, (uint32_t)empt_a, r, sp);
-    s.b = moved;
-    s.sb = mono_add_tile(sa, moved, sp, v);  // cells other than sp are unchanged by the spawn
-    s.legal = legal_mask(s.b);
+    s.b = moved;  // the next board (after the spawn)
+    // its legal mask and pair counts from kLine12: four rows and four columns
+    const uint4 tc = transpose(moved);
+    uint32_t f0 = lds_half(tab, line12_addr(moved.x)), f1 = lds_half(tab, line12_addr(moved.y));
+    uint32_t f2 = lds_half(tab, line12_addr(moved.z)), f3 = lds_half(tab, line12_addr(moved.w));
+    uint32_t g0 = lds_half(tab, line12_addr(tc.x)), g1 = lds_half(tab, line12_addr(tc.y));
+    uint32_t g2 = lds_half(tab, line12_addr(tc.z)), g3 = lds_half(tab, line12_addr(tc.w));
+    // the spawned tile's pairs (the counts before the spawn are the next board's minus these) and
+    // the next board's maximum / first-argmax cell
+    const MonoStats dsp = mono_add_tile(MonoStats{0, 0, 0, 0, Ma, pos_a}, moved, sp, v);
+    tr.a[li] = (uint8_t)a;
+    tr.p[li] = (int32_t)pts;
+    const uint32_t SR = f0 + f1 + f2 + f3, SC = g0 + g1 + g2 + g3;
+    // #lines that can move per direction in nibbles {UP, DOWN, LEFT, RIGHT} -> legal bits 0..3: a
+    // nibble n in 0..4 gets bit 3 set by n + 7; the 24-bit product gathers bits 3, 7, 11, 15 at 12..15
+    const uint32_t nl = __builtin_amdgcn_perm(SR, SC, 0x0C0C0501u);
+    s.legal = (__umul24((nl + 0x7777u) & 0x8888u, 0x249u) >> 12) & 15u;
+    s.sb.L = (int)(SR & 15u);
+    s.sb.R = (int)((SR >> 4) & 15u);
+    s.sb.T = (int)(SC & 15u);
+    s.sb.B = (int)((SC >> 4) & 15u);
+    s.sb.M = dsp.M;
+    s.sb.pos = dsp.pos;
+    MonoStats sa{s.sb.L - dsp.L, s.sb.R - dsp.R, s.sb.T - dsp.T, s.sb.B - dsp.B, Ma, pos_a};
+    if (!kSmall && Ma > 11u) {  // an exponent outside kLine12: the SWAR statistics and legal mask
+        const uint32_t keep = ~(0xFFu << (8u * (sp & 3u)));
+        const uint32_t q = sp >> 2;
+        const uint4 pre = make_uint4(q == 0u ? moved.x & keep : moved.x, q == 1u ? moved.y & keep : moved.y,
+                                     q == 2u ? moved.z & keep : moved.z, q == 3u ? moved.w & keep : moved.w);
+        sa = mono_stats(pre);
+        s.sb = mono_add_tile(sa, pre, sp, v);
+        s.legal = legal_mask(moved);
+    }
+    const int mono_a = mono_value(sa);
     uint32_t fl = s.legal;
     if (s.legal == 0u) {  // game over: a new game from the pair's spare words
         uint32_t p1, v1, p2, v2;
@@ -249,8 +301,6 @@ __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__r
         s.legal = fresh_stats(p1, v1, p2, v2, s.sb);
         fl = FLAG_DONE | FLAG_RESET | s.legal;
     }
-    tr.a[li] = (uint8_t)a;
-    tr.p[li] = (int32_t)pts;
     tr.pot[li] = (uint32_t)(mono_b & 0xFF) | ((uint32_t)(mono_a & 0xFF) << 8) | ((uint32_t)(s.empt_b & 0xFF) << 16) |
                  ((uint32_t)(empt_a & 0xFF) << 24);
     tr.f[li] = (uint8_t)fl;
@@ -274,8 +324,8 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
                                                            uint4 *__restrict__ tb, uint8_t *__restrict__ ta,
                                                            int32_t *__restrict__ tp, uint32_t *__restrict__ tpot,
                                                            uint8_t *__restrict__ tf, RngArgs rng) {
-    // 32 Ki entries: every 4-bit-masked index (< 15 * 1885) stays inside; the first 20 736 are staged
-    __shared__ __attribute__((aligned(16))) uint32_t s_row[32768];
+    // kRow12 then kLine12; every 4-bit-masked index of either table stays inside (kRolloutLdsWords)
+    __shared__ __attribute__((aligned(16))) uint32_t s_row[kRolloutLdsWords];
     stage_row_table(s_row);
     const uint64_t ctr0 = rng_counter(rng);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -308,8 +358,15 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
             t = 1;
         }
         for (; t + 2 <= steps; t += 2, pair++) {
-            rollout_step<false>(s, s_row, rows(t), li, rng.seed, pair + 2u, env);
-            rollout_step<true>(s, s_row, rows(t + 1), li, rng.seed, pair + 2u, env);
+            // every board of the wave <= 2^9 at the pair's start: both steps stay inside the tables
+            // (the move adds at most 1 to the maximum), so the pair runs without the fallback branches
+            if (__all(s.sb.M <= 9u)) {
+                rollout_step<false, true>(s, s_row, rows(t), li, rng.seed, pair + 2u, env);
+                rollout_step<true, true>(s, s_row, rows(t + 1), li, rng.seed, pair + 2u, env);
+            } else {
+                rollout_step<false>(s, s_row, rows(t), li, rng.seed, pair + 2u, env);
+                rollout_step<true>(s, s_row, rows(t + 1), li, rng.seed, pair + 2u, env);
+            }
         }
         if (t < steps) rollout_step<false>(s, s_row, rows(t), li, rng.seed, pair + 2u, env);
         boards[i] = s.b;

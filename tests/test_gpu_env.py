@@ -185,7 +185,8 @@ def test_philox_random_steps_match_oracle(dev, seed):
 @pytest.mark.parametrize("n,steps", [(4096, 200), (1000, 64), (70000, 20)])
 def test_rollout_kernel_trajectories_match_oracle(dev, n, steps):
     """env_rollout_kernel (the bench workload): every per-step record bit-exact vs the oracle,
-    including boards whose exponents exceed the LDS table's nibble range (compute-path fallback)."""
+    including boards whose exponents exceed the LDS tables' range (compute-path fallback) and boards
+    whose move creates the first exponent 12 (kLine12 -> SWAR statistics fallback)."""
     lib = L()
     init = O.reset(n, O.RNG_PHILOX, seed=31, step_idx=0, env_base=5)
     init[:7] = np.array([1, 2, 1, 2, 2, 1, 2, 1, 1, 2, 1, 2, 2, 1, 2, 1], np.int8)  # finished boards handed in
@@ -193,6 +194,12 @@ def test_rollout_kernel_trajectories_match_oracle(dev, n, steps):
     hi[:, 0] = 14
     hi[:, 1] = 14  # a 14+14 merge produces 15 inside the table path
     init[n // 2:n // 2 + n // 4] = hi
+    # boards inside the table range whose move can create a 12 (11 + 11): the next board's legal mask
+    # and pair counts then come from the SWAR fallback instead of kLine12
+    el = random_boards(n // 8, 78, hi=11, p_empty=0.5)
+    el[:, 0] = 11
+    el[:, 1] = 11
+    init[n // 4:n // 4 + n // 8] = el
     b = to_dev(init, torch.int8, dev)
     tb = torch.zeros(steps, n, 16, dtype=torch.int8, device=dev)
     ta = torch.zeros(steps, n, dtype=torch.uint8, device=dev)
