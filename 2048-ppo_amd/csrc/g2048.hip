@@ -55,7 +55,12 @@ __device__ const lut::Line12Table kLine12 __attribute__((aligned(16))) = lut::Li
 // i.e. indices up to 15 * 1885 = 28 275: those may land in kLine12 (harmless) and the kLine12
 // reads need the region up to kLineBase + 2 * 28 276 bytes.
 constexpr uint32_t kLineBase = lut::kRowEntries * 4u;                        // 82 944
-constexpr uint32_t kRolloutLdsWords = (kLineBase + 2u * 28276u + 15u) / 16u * 4u;  // 139 504 B
+// then the auto-reset boards and their statistics (kFresh) past the masked-read region
+__device__ const lut::FreshTable kFresh __attribute__((aligned(16))) = lut::FreshTable();
+constexpr uint32_t kFreshBoardBase = 137u * 1024u;                          // 15 KiB of boards
+constexpr uint32_t kFreshStatBase = kFreshBoardBase + lut::kFreshEntries * 16u;  // 2 KiB of stats
+constexpr uint32_t kRolloutLdsWords = (kFreshStatBase + 2048u) / 4u;         // 157 696 B
+static_assert(kLineBase + 2u * 28276u <= kFreshBoardBase, "masked kLine12 reads stay below kFresh");
 
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
@@ -187,15 +192,32 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 __device__ __forceinline__ void stage_row_table(uint32_t *s_row) {
     constexpr int kPieces = (int)(lut::kRowEntries * 4u / 1024u);  // 81 pieces of 1 KiB
     constexpr int kLinePieces = (int)(lut::kLineEntriesPadded * 2u / 1024u);  // + 41 of kLine12
-    static_assert(lut::kRowEntries * 4u % 1024u == 0u && lut::kLineEntriesPadded * 2u % 1024u == 0u,
-                  "whole 1 KiB pieces");
+    constexpr int kFreshPieces = (int)(lut::kFreshEntries * 16u / 1024u);  // + 15 boards + 2 stats
+    static_assert(lut::kRowEntries * 4u % 1024u == 0u && lut::kLineEntriesPadded * 2u % 1024u == 0u &&
+                  lut::kFreshEntries * 16u % 1024u == 0u, "whole 1 KiB pieces");
+    constexpr int kAll = kPieces + kLinePieces + kFreshPieces + 2;
     const char *src = reinterpret_cast<const char *>(kRow12.v);
     const char *src2 = reinterpret_cast<const char *>(kLine12.v);
+    const char *src3 = reinterpret_cast<const char *>(kFresh.b);
+    const char *src4 = reinterpret_cast<const char *>(kFresh.st);
     char *dst = reinterpret_cast<char *>(s_row);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    for (int c = wave; c < kPieces + kLinePieces; c += nw) {
-        const char *g = c < kPieces ? src + 1024 * c : src2 + 1024 * (c - kPieces);
-        __builtin_amdgcn_global_load_lds((glb_void_t *)(g + 16 * lane), (lds_void_t *)(dst + 1024 * c), 16, 0, 0);
+    for (int c = wave; c < kAll; c += nw) {
+        const char *g;
+        uint32_t d;
+        if (c < kPieces + kLinePieces) {
+            g = c < kPieces ? src + 1024 * c : src2 + 1024 * (c - kPieces);
+            d = 1024u * (uint32_t)c;
+        } else if (c < kPieces + kLinePieces + kFreshPieces) {
+            const int k = c - kPieces - kLinePieces;
+            g = src3 + 1024 * k;
+            d = kFreshBoardBase + 1024u * (uint32_t)k;
+        } else {
+            const int k = c - kPieces - kLinePieces - kFreshPieces;
+            g = src4 + 1024 * k;
+            d = kFreshStatBase + 1024u * (uint32_t)k;
+        }
+        __builtin_amdgcn_global_load_lds((glb_void_t *)(g + 16 * lane), (lds_void_t *)(dst + d), 16, 0, 0);
     }
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0): this wave's pieces have landed
     __syncthreads();
@@ -211,7 +233,25 @@ struct RolloutLane {
                       // z / w = the words of a reset inside the pair (at most one: a reset board
                       // cannot end again one move later)
     PhiloxState ph;   // draw of the next pair, computed half per step inside the LDS round trip
+    uint4 fb;         // the board a reset inside the current pair starts (D.z, D.w -> kFresh) ...
+    uint32_t flegal;  // ... its legal mask and statistics
+    MonoStats fsb;
 };
+
+// the current pair's auto-reset board from kFresh (fresh_from_pair's board and fresh_stats' results,
+// read once per pair right after the draw is known, long before a step can need them)
+__device__ __forceinline__ void fresh_prep(RolloutLane &s, const uint32_t *__restrict__ tab) {
+    const uint32_t a = s.D.z, bw = s.D.w;
+    const uint32_t k2 = __umulhi(bw, 15u);
+    const uint32_t i = 60u * (a >> 28) + 4u * k2 + ((a << 4) >= kTwoThreshold ? 2u : 0u) +
+                       (bw * 15u >= kTwoThreshold ? 1u : 0u);
+    const char *t = reinterpret_cast<const char *>(tab);
+    s.fb = *reinterpret_cast<const uint4 *>(t + kFreshBoardBase + 16u * i);
+    const uint32_t st = *reinterpret_cast<const uint16_t *>(t + kFreshStatBase + 2u * i);
+    s.flegal = st & 15u;
+    s.fsb = MonoStats{(int)((st >> 4) & 1u), (int)((st >> 5) & 1u), (int)((st >> 6) & 1u), (int)((st >> 7) & 1u),
+                      1u + ((st >> 8) & 1u), st >> 12};
+}
 
 struct TrajRows {  // row t of each time-major trajectory array
     uint4 *b;
@@ -294,13 +334,18 @@ __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__r
         s.legal = legal_mask(moved);
     }
     const int mono_a = mono_value(sa);
-    uint32_t fl = s.legal;
-    if (s.legal == 0u) {  // game over: a new game from the pair's spare words
-        uint32_t p1, v1, p2, v2;
-        s.b = fresh_from_pair(s.D.z, s.D.w, p1, v1, p2, v2);
-        s.legal = fresh_stats(p1, v1, p2, v2, s.sb);
-        fl = FLAG_DONE | FLAG_RESET | s.legal;
-    }
+    // game over: a new game from the pair's spare words (kFresh, prepared with the draw); selects,
+    // so the whole pair stays one basic block
+    const bool over = s.legal == 0u;
+    const uint32_t fl = over ? FLAG_DONE | FLAG_RESET | s.flegal : s.legal;
+    s.b = sel4(over, s.fb, s.b);
+    s.legal = over ? s.flegal : s.legal;
+    s.sb.L = over ? s.fsb.L : s.sb.L;
+    s.sb.R = over ? s.fsb.R : s.sb.R;
+    s.sb.T = over ? s.fsb.T : s.sb.T;
+    s.sb.B = over ? s.fsb.B : s.sb.B;
+    s.sb.M = over ? s.fsb.M : s.sb.M;
+    s.sb.pos = over ? s.fsb.pos : s.sb.pos;
     tr.pot[li] = (uint32_t)(mono_b & 0xFF) | ((uint32_t)(mono_a & 0xFF) << 8) | ((uint32_t)(s.empt_b & 0xFF) << 16) |
                  ((uint32_t)(empt_a & 0xFF) << 24);
     tr.f[li] = (uint8_t)fl;
@@ -308,6 +353,7 @@ __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__r
     if constexpr (kOdd) {
         s.D = make_uint4(s.ph.c0, s.ph.c1, s.ph.c2, s.ph.c3);
         s.ph = philox_start(seed, next_pair, env, 1u);
+        fresh_prep(s, tab);
     }
 }
 
@@ -346,6 +392,7 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
         uint64_t pair = ctr0 >> 1;
         s.D = philox_draw(rng.seed, pair, env, 1u);
         s.ph = philox_start(rng.seed, pair + 1u, env, 1u);
+        fresh_prep(s, s_row);
         auto rows = [&](int64_t t) {
             const int64_t o = t * n;
             return TrajRows{tb + o, ta + o, tp + o, tpot + o, tf + o};
