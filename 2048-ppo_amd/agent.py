@@ -163,8 +163,9 @@ class GameConvSwiGLU(nn.Module):
             from g2048 import urm as _urm  # fused gate_up + SwiGLU + conv (training, g2048_urm.h)
             if _urm.gate_up_swiglu_supported(self, x):
                 b, s, h = x.shape
-                act = _urm.GateUpSwiGLUFn.apply(x.reshape(b * s, h), self.gate_up_proj.weight,
-                                                self.dwconv.weight.view(-1, 2), self.dwconv.bias)
+                args = (x.reshape(b * s, h), self.gate_up_proj.weight, self.dwconv.weight.view(-1, 2), self.dwconv.bias)
+                act = (_urm.GateUpSwiGLUFn.apply(*args) if torch.is_grad_enabled()
+                       else _urm.gate_up_swiglu_nograd(*args))
                 return _urm.project(self.down_proj, act.view(b, s, self.inter))
         gu = self.gate_up_proj(x)
         if gu.is_cuda:

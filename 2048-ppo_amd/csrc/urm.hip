@@ -500,36 +500,57 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
             }
         } else if constexpr (EPI == EPI_SWIGLU_T) {
             constexpr int CH = CT / 2;
+            static_assert(CH % 2 == 0, "column tiles are stored in pairs");
             auto sg = [](float v) { return 1.0f / (1.0f + expf(-v)); };
             auto rb = [](float v) { return (float)(__bf16)v; };
             auto pk = [](float a0, float a1, float a2, float a3) {
                 const __attribute__((ext_vector_type(2))) __bf16 p0 = {(__bf16)a0, (__bf16)a1}, p1 = {(__bf16)a2, (__bf16)a3};
                 return make_uint2(__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1));
             };
+            // tiles ct, ct + 1 are stored together: lane (t, g) holds 4 features of each; one
+            // v_permlane16_swap per dword between the lane rows g, g ^ 1 gives every lane 8
+            // consecutive features (even g: 16 ct + 4 g .. + 7, odd g: 16 ct + 16 + 4 (g - 1) .. + 7),
+            // so each output is written with 16-byte stores (half the store instructions)
+            const int cb8 = (g & 1) ? 16 + 4 * (g - 1) : 4 * g;
 #pragma unroll
-            for (int ct = 0; ct < CH; ct++) {
-                const int c = 16 * ct + 4 * g;
-                const int cc = c < inter ? c : 0;
-                const float4 w01 = *reinterpret_cast<const float4 *>(cw + 2 * cc);
-                const float4 w23 = *reinterpret_cast<const float4 *>(cw + 2 * cc + 4);
-                const float4 bb = *reinterpret_cast<const float4 *>(cb + cc);
-                const float wk0[4] = {w01.x, w01.z, w23.x, w23.z}, wk1[4] = {w01.y, w01.w, w23.y, w23.w};
-                const float bk[4] = {bb.x, bb.y, bb.z, bb.w};
-                float gq[4], uq[4], o[4];
+            for (int cp = 0; cp < CH; cp += 2) {
+                uint2 og[2], ou[2], oo[2];
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    gq[i] = rb(acc[ct][i]);
-                    uq[i] = rb(acc[ct + CH][i]);
-                    const float yv = rb(rb(gq[i] * sg(gq[i])) * uq[i]);
-                    const float prev = dpp_prev_token(yv);
-                    const float z = prev * wk0[i] + yv * wk1[i] + bk[i];
-                    o[i] = z * sg(z);
+                for (int j = 0; j < 2; j++) {
+                    const int ct = cp + j;
+                    const int c = 16 * ct + 4 * g;
+                    const int cc = c < inter ? c : 0;
+                    const float4 w01 = *reinterpret_cast<const float4 *>(cw + 2 * cc);
+                    const float4 w23 = *reinterpret_cast<const float4 *>(cw + 2 * cc + 4);
+                    const float4 bb = *reinterpret_cast<const float4 *>(cb + cc);
+                    const float wk0[4] = {w01.x, w01.z, w23.x, w23.z}, wk1[4] = {w01.y, w01.w, w23.y, w23.w};
+                    const float bk[4] = {bb.x, bb.y, bb.z, bb.w};
+                    float gq[4], uq[4], o[4];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        gq[i] = rb(acc[ct][i]);
+                        uq[i] = rb(acc[ct + CH][i]);
+                        const float yv = rb(rb(gq[i] * sg(gq[i])) * uq[i]);
+                        const float prev = dpp_prev_token(yv);
+                        const float z = prev * wk0[i] + yv * wk1[i] + bk[i];
+                        o[i] = z * sg(z);
+                    }
+                    og[j] = pk(gq[0], gq[1], gq[2], gq[3]);
+                    ou[j] = pk(uq[0], uq[1], uq[2], uq[3]);
+                    oo[j] = pk(o[0], o[1], o[2], o[3]);
                 }
-                if (c < inter) {
+                auto pair16 = [](const uint2 (&v)[2]) {
+                    const auto sx = __builtin_amdgcn_permlane16_swap(v[0].x, v[1].x, false, false);
+                    const auto sy = __builtin_amdgcn_permlane16_swap(v[0].y, v[1].y, false, false);
+                    return make_uint4(sx[0], sy[0], sx[1], sy[1]);
+                };
+                const uint4 vg = pair16(og), vu = pair16(ou), vo = pair16(oo);
+                const int c8 = 16 * cp + cb8;
+                if (c8 < inter) {  // inter % 8 == 0: a lane's 8 features are all valid or all past inter
                     uint16_t *gr = xb + r * 2 * inter;  // gu output (xb carries it for this epilogue)
-                    *reinterpret_cast<uint2 *>(gr + c) = pk(gq[0], gq[1], gq[2], gq[3]);
-                    *reinterpret_cast<uint2 *>(gr + inter + c) = pk(uq[0], uq[1], uq[2], uq[3]);
-                    *reinterpret_cast<uint2 *>(y + r * inter + c) = pk(o[0], o[1], o[2], o[3]);
+                    *reinterpret_cast<uint4 *>(gr + c8) = vg;
+                    *reinterpret_cast<uint4 *>(gr + inter + c8) = vu;
+                    *reinterpret_cast<uint4 *>(y + r * inter + c8) = vo;
                 }
             }
         } else {
@@ -1958,10 +1979,11 @@ int g2048_urm_linear_swiglu(g2048_stream_t stream, const uint16_t *in, const uin
 int g2048_urm_linear_swiglu_train(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *conv_w,
                                   const float *conv_b, uint16_t *gu, uint16_t *act, int64_t rows, int32_t h,
                                   int32_t inter) {
-    if (rows < 0 || rows % 16 || !g2048_urm_linear_supported(3, h, 2 * inter, inter)) return G2048_EINVAL;
+    // the epilogue writes 8 features per lane with 16-byte stores: inter % 8, 16-byte aligned outputs
+    if (rows < 0 || rows % 16 || inter % 8 || !g2048_urm_linear_supported(3, h, 2 * inter, inter)) return G2048_EINVAL;
     if (rows == 0) return G2048_OK;
     if (!in || !w || !conv_w || !conv_b || !gu || !act || ((uintptr_t)conv_w | (uintptr_t)conv_b) % 16 ||
-        ((uintptr_t)gu | (uintptr_t)act) % 8)
+        ((uintptr_t)gu | (uintptr_t)act) % 16)
         return G2048_EINVAL;
     return dispatch_lin((hipStream_t)stream, 3, in, w, rows, h, 2 * inter, inter, act, nullptr, nullptr, gu, 0.0f,
                         conv_w, conv_b, false);

@@ -480,6 +480,20 @@ class GateUpSwiGLUFn(torch.autograd.Function):
         return dx.to(ctx.dtypes[0]), dW.to(ctx.dtypes[1]), dw.to(ctx.dtypes[2]), db.to(ctx.dtypes[3])
 
 
+def gate_up_swiglu_nograd(x: torch.Tensor, w: torch.Tensor, cw: torch.Tensor, cb: torch.Tensor) -> torch.Tensor:
+    """The same block outside autograd (GameURM's no-grad truncated loops, game.py:1437-1443): the
+    inference epilogue g2048_urm_linear_swiglu, which writes only act (no gu for a backward that
+    never comes: 368 instead of 848 MB per call at 65 536 boards) and keeps the projection in fp32
+    into the SwiGLU-conv epilogue (one bf16 rounding fewer than the training kernel)."""
+    xb = x.to(torch.bfloat16).contiguous()
+    wb = w.detach().to(torch.bfloat16).contiguous()
+    cwf = cw.detach().to(torch.float32, copy=True).contiguous()
+    cbf = cb.detach().to(torch.float32, copy=True).contiguous()
+    act = torch.empty(xb.shape[0], w.shape[0] // 2, dtype=torch.bfloat16, device=x.device)
+    L.urm_linear_swiglu(xb, wb, cwf, cbf, act)
+    return act
+
+
 def gate_up_swiglu_supported(mlp, x: torch.Tensor) -> bool:
     """The fused training gate_up + SwiGLU-conv applies: bf16 autocast on the GPU, 16 tokens, conv
     kernel 2, a bias-free gate_up projection whose shape the fused kernel covers."""
@@ -487,7 +501,8 @@ def gate_up_swiglu_supported(mlp, x: torch.Tensor) -> bool:
     return (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.ndim == 3 and x.shape[1] == 16
             and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
             and mlp.dwconv.kernel_size[0] == 2 and mlp.gate_up_proj.bias is None
-            and L.urm_linear_supported(3, h, 2 * mlp.inter, mlp.inter) and L.urm_wgrad_supported(2 * mlp.inter, h))
+            and L.urm_linear_supported(3, h, 2 * mlp.inter, mlp.inter) and L.urm_linear_supported(2, h, 2 * mlp.inter, mlp.inter)
+            and L.urm_wgrad_supported(2 * mlp.inter, h))
 
 
 def swiglu_conv_supported(gu: torch.Tensor, seq: int, inter: int, kernel: int) -> bool:

@@ -1,10 +1,11 @@
 /*
  * g2048_urm.h -- C ABI of the GameURM policy forward (game.py:1223-1458) in libg2048.so: the
- * non-GEMM parts of the Universal-Reasoning-Model transformer over the 16 cell tokens, as fused
- * HIP kernels for gfx950.  The four projections of a block (qkv_proj, o_proj, gate_up_proj,
- * down_proj: plain x W^T GEMMs) go to the platform BLAS (hipBLASLt through torch); everything
- * between them is one of the kernels below (g2048/urm.py strings them together and the rollout
- * captures the whole forward in a hipGraph).
+ * Universal-Reasoning-Model transformer over the 16 cell tokens, as fused HIP kernels for gfx950:
+ * the four projections of a block (qkv_proj, o_proj, gate_up_proj, down_proj) on the MFMA
+ * projection kernel with their epilogues fused (g2048_urm_linear*), everything between them one of
+ * the kernels below, the whole rollout forward also as one persistent launch (g2048_urm_forward);
+ * for training, the autograd Functions of g2048/urm.py run the forwards, input gradients and weight
+ * gradients on these kernels (no library GEMM at the default config).
  *
  * Token layout: board b's 16 cells are rows 16 b .. 16 b + 15 of every [rows, .] activation
  * (row-major, cell order of to_model_format, game.py:92-101), so a board's sequence is contiguous.
@@ -159,7 +160,8 @@ int g2048_urm_linear_swiglu(g2048_stream_t stream, const uint16_t *in, const uin
  * autograd GateUpSwiGLUFn: also stores gu = bf16(x W_gu^T) [rows, 2 inter] (gate | up: the backward's
  * input) and computes act from those bf16 values with g2048_urm_swiglu_conv_fwd's arithmetic, so the
  * result equals gate_up Linear (autocast bf16) + g2048_urm_swiglu_conv_fwd up to the GEMM's fp32
- * summation order.  in bf16 [rows, h], w bf16 [2 inter, h], conv_w fp32 [inter][2], conv_b [inter]. */
+ * summation order.  in bf16 [rows, h], w bf16 [2 inter, h], conv_w fp32 [inter][2], conv_b [inter];
+ * inter % 8 == 0 and gu / act 16-byte aligned (8 features per lane per store). */
 int g2048_urm_linear_swiglu_train(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *conv_w,
                                   const float *conv_b, uint16_t *gu, uint16_t *act, int64_t rows, int32_t h,
                                   int32_t inter);

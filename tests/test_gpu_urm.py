@@ -537,6 +537,35 @@ def test_urm_gate_up_swiglu_fn_matches_unfused(dev, n):
         assert float((a - b).abs().max()) <= 0.01 * float(b.abs().max())
 
 
+@pytest.mark.parametrize("n", [65536, 37])
+def test_urm_gate_up_swiglu_nograd_matches_training_kernel(dev, n):
+    """The no-grad truncated loops' gate_up + SwiGLU-conv (inference epilogue, fp32 projection into
+    the epilogue) vs the training kernel (gu rounded to bf16 first) and vs an fp32 restatement:
+    within two bf16 steps of |act|max of the training kernel (mean <= 1e-4), and no further from
+    fp32 than the training kernel is."""
+    import torch.nn.functional as F
+
+    import agent
+    from g2048.urm import GateUpSwiGLUFn, gate_up_swiglu_nograd
+    torch.manual_seed(n + 1)
+    mlp = agent.GameConvSwiGLU(64, agent.GameURMConfig().expansion, 2).to(dev)
+    x = torch.randn(16 * n, 64, device=dev).bfloat16()
+    args = (x, mlp.gate_up_proj.weight, mlp.dwconv.weight.view(-1, 2), mlp.dwconv.bias)
+    with torch.no_grad():
+        got = gate_up_swiglu_nograd(*args).float()
+        trn = GateUpSwiGLUFn.apply(*args).float()
+        gu = x.float() @ mlp.gate_up_proj.weight.bfloat16().float().t()
+        g, u = gu.chunk(2, -1)
+        a = (F.silu(g) * u).view(n, 16, -1)
+        w = mlp.dwconv.weight.view(-1, 2)
+        prev = torch.cat([torch.zeros_like(a[:, :1]), a[:, :-1]], 1)
+        ref = F.silu(prev * w[:, 0] + a * w[:, 1] + mlp.dwconv.bias).view(16 * n, -1)
+    d = (got - trn).abs()
+    print(f"nograd vs training kernel: max {d.max().item():.3g} mean {d.mean().item():.3g}")
+    assert d.max().item() <= 2 * 2 ** -7 * trn.abs().max().item() and d.mean().item() <= 1e-4
+    assert (got - ref).abs().mean().item() <= (trn - ref).abs().mean().item() * 1.05
+
+
 @pytest.mark.parametrize("m,n,k", [(65536 * 16, 192, 64), (65536 * 16, 240, 64), (16 * 37, 64, 120),
                                    (16 * 1001, 64, 64)])
 def test_urm_wgrad_matches_fp64(dev, m, n, k):
