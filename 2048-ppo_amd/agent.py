@@ -334,6 +334,11 @@ class GameURM(nn.Module):
         for _ in range(self.config.num_loops - n_trunc):
             h = self._loop(h, emb)
         pooled = h.mean(dim=1)
+        if pooled.is_cuda:
+            from g2048 import urm as _urm  # both heads as one device projection (training, g2048_urm.h)
+            if _urm.heads_supported(self, pooled):
+                return _urm.URMHeadsFn.apply(pooled, self.action_head.weight, self.action_head.bias,
+                                             self.value_head.weight, self.value_head.bias)
         return self.action_head(pooled), self.value_head(pooled)
 
 

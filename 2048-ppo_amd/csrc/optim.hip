@@ -114,7 +114,7 @@ __device__ __forceinline__ void adamw_elem(const AdamGroup &gr, int64_t i, float
 constexpr int kMuonThreads = 1024;       // 16 waves (4 per SIMD: LDS latency hidden by the others)
 constexpr int kMuonWaves = kMuonThreads / 64;
 constexpr int kBI = 4, kBJ = 4;          // generic schedule: 4 x 4 waves of 4 x 4 16x16 tiles = 256 x 256
-constexpr int kMuonMaxMats = 8;
+constexpr int kMuonMaxMats = 16;  // GameMLP: 5, GameURM (2 layers): 11
 constexpr int kMuonLds = 160 * 1024 - 256;  // minus the static red[] / s_norm
 
 struct MuonMat {
@@ -273,8 +273,20 @@ __device__ __forceinline__ float momentum4(const float4 &g4, const float4 &b4, f
 __device__ __forceinline__ float muon_prologue(const float *__restrict__ grad, float *__restrict__ mom, char *sX,
                                                int px, int R, int C, bool tr, float coef, float mu, bool nesterov,
                                                int tid) {
-    const int n4 = (R * C) >> 2;
     float ss = 0.0f;
+    if (C & 3) {  // a row length that is not a whole number of float4 (GameURM's [64, 3] stem): per element
+        for (int e = tid; e < R * C; e += kMuonThreads) {
+            const float gv = grad[e] * coef;
+            const float bv = mom[e] + (1.0f - mu) * (gv - mom[e]);
+            const float ub = round_bf(nesterov ? bv - (bv - gv) * (1.0f - mu) : bv);
+            ss += ub * ub;
+            const int i = e / C, j = e - i * C;
+            reinterpret_cast<uint16_t *>(sX + (tr ? j * px : i * px))[tr ? i : j] = (uint16_t)f2bf(ub);
+            mom[e] = bv;
+        }
+        return ss;
+    }
+    const int n4 = (R * C) >> 2;
     // kB float4 of the gradient and of the momentum in flight per thread before any is used: one
     // HBM round trip per batch instead of one per element group (a single CU streams the matrix)
     constexpr int kB = 6;
@@ -307,6 +319,16 @@ __device__ __forceinline__ float muon_prologue(const float *__restrict__ grad, f
 
 __device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_t *__restrict__ pbf, const char *sX,
                                               int px, int R, int C, bool tr, float decay, float step, int tid) {
+    if (C & 3) {  // per element (see muon_prologue)
+        for (int e = tid; e < R * C; e += kMuonThreads) {
+            const int i = e / C, j = e - i * C;
+            const float x = bf2f(reinterpret_cast<const uint16_t *>(sX + (tr ? j * px : i * px))[tr ? i : j]);
+            const float pv = param[e] * decay - x * step;
+            param[e] = pv;
+            if (pbf) pbf[e] = (uint16_t)f2bf(pv);
+        }
+        return;
+    }
     const int n4 = (R * C) >> 2;
     constexpr int kB = 8;
     for (int base = tid; base < n4; base += kB * kMuonThreads) {
@@ -830,7 +852,6 @@ int g2048_grad_clip(g2048_stream_t stream, const float *grad, int64_t n, float m
 int g2048_muon_supported(int32_t rows, int32_t cols) {
     if (rows <= 0 || cols <= 0) return 0;
     const int r = rows > cols ? cols : rows, c = rows > cols ? rows : cols;
-    if (cols % 4) return 0;  // the element passes read float4s within a row
     if (r > 16 * 4 * kBI || c > 16 * 4 * kBJ) return 0;
     return muon_lds_bytes(rows, cols) <= (size_t)kMuonLds ? 1 : 0;
 }

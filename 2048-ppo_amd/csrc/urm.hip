@@ -625,6 +625,8 @@ int dispatch_lin(hipStream_t s, int epi, const uint16_t *in, const uint16_t *w, 
     G2048_LIN(EPI_STORE, 3, 2)    // h 32: qkv dX (K 96, N 32)
     G2048_LIN(EPI_STORE, 1, 4)    // h 32: down_proj dX (K 32, N 64)
     G2048_LIN(EPI_STORE, 4, 2)    // h 32: gate_up dX (K 128, N 32)
+    G2048_LIN(EPI_STORE, 2, 1)    // h 64: the two heads [action | value | 0 pad] forward (K 64, N 8)
+    G2048_LIN(EPI_STORE, 1, 1)    // h 32 heads forward (K 32, N 8)
     G2048_LIN(EPI_RMS, 2, 4)      // h 64 o_proj
     G2048_LIN(EPI_RMS, 4, 4)      // h 64 down_proj (K = inter = 120)
     G2048_LIN(EPI_RMS, 1, 2)      // h 32 o_proj

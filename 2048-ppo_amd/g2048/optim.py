@@ -201,15 +201,16 @@ class FusedMuonAdamW(MuonAdamW):
     weight copy) with the AdamW update of the 1-D groups in the same launch's extra blocks.
 
     Same arithmetic as MuonAdamW up to the accumulation order of the bf16 Newton-Schulz products.
-    `supported` is False when a matrix does not fit the one-block Newton-Schulz kernel (h > 196);
-    callers then use MuonAdamW.
+    `supported` is False when a matrix does not fit the one-block Newton-Schulz kernel (h > 196) or
+    the model has more than 16 Muon matrices; callers then use MuonAdamW.  Serves GameMLP (5 matrices)
+    and GameURM (11, incl. the [64, 3] stem: per-element momentum / update pass).
     """
 
     def __init__(self, model, *args, **kwargs):
         super().__init__(model, *args, **kwargs)
         from . import _lib as L
         self._L = L
-        self.supported = (self.dev.type == "cuda" and 0 < len(self.muon) <= 8 and len(self.adam_groups) <= 4
+        self.supported = (self.dev.type == "cuda" and 0 < len(self.muon) <= 16 and len(self.adam_groups) <= 4
                           and all(p.ndim == 2 and L.muon_supported(*p.shape) for p, _ in self.muon))
         self.norm_t = torch.zeros((), dtype=torch.float32, device=self.dev)
         self.coef_t = torch.ones((), dtype=torch.float32, device=self.dev)

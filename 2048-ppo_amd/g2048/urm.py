@@ -428,6 +428,55 @@ class URMLinearFn(torch.autograd.Function):
         return (None if dx is None else dx.to(ctx.dtypes[0])), dW
 
 
+class URMHeadsFn(torch.autograd.Function):
+    """GameURM's action_head and value_head on the pooled features under bf16 autocast
+    (game.py:1452-1456) without the library's K = n GEMMs (hipBLASLt ran the heads' weight gradient
+    at ~0.2 ms and its input gradient at ~0.16 ms per 65 536 boards): the two heads as one [8, h]
+    projection (action rows 0-3, value row 4, zero rows) on g2048_urm_linear, bias added in fp32 and
+    rounded once more to bf16 (autocast rounds the biased GEMM output once); backward: dW on
+    g2048_urm_wgrad (dy zero-padded to 16 columns), dpooled = dy W on g2048_urm_linear, db a column
+    sum.  pooled fp32 or bf16 [n, h] -> logits bf16 [n, 4], value bf16 [n, 1]."""
+
+    @staticmethod
+    def forward(ctx, pooled: torch.Tensor, wa: torch.Tensor, ba: torch.Tensor, wv: torch.Tensor, bv: torch.Tensor):
+        h = pooled.shape[1]
+        pb = pooled.to(torch.bfloat16).contiguous()
+        w8 = torch.zeros(8, h, dtype=torch.bfloat16, device=pooled.device)
+        w8[:4] = wa.detach()
+        w8[4:5] = wv.detach()
+        y = _gemm(pb, w8).float()
+        logits = (y[:, :4] + ba.detach().float()).to(torch.bfloat16)
+        value = (y[:, 4:5] + bv.detach().float()).to(torch.bfloat16)
+        ctx.save_for_backward(pb, w8)
+        ctx.dtypes = (pooled.dtype, wa.dtype, ba.dtype, wv.dtype, bv.dtype)
+        return logits, value
+
+    @staticmethod
+    def backward(ctx, dlogits: torch.Tensor, dvalue: torch.Tensor):
+        pb, w8 = ctx.saved_tensors
+        n = pb.shape[0]
+        dy = torch.zeros(n, 16, dtype=torch.bfloat16, device=pb.device)
+        if dlogits is not None:
+            dy[:, :4] = dlogits
+        if dvalue is not None:
+            dy[:, 4:5] = dvalue
+        dw = _wgrad(dy, pb)                                        # [16, h] fp32
+        db = dy[:, :5].float().sum(0)
+        dp = _gemm(dy[:, :8].contiguous(), w8.t().contiguous())    # [n, h] bf16 = dy W
+        t = ctx.dtypes
+        return (dp.to(t[0]), dw[:4].to(t[1]), db[:4].to(t[2]), dw[4:5].to(t[3]), db[4:5].to(t[4]))
+
+
+def heads_supported(model, pooled: torch.Tensor) -> bool:
+    """URMHeadsFn applies: bf16 autocast on the GPU, whole boards of 16 (the projection kernel's row
+    granularity), hidden 64 or 32 (the instantiated shapes)."""
+    n, h = pooled.shape
+    return (pooled.is_cuda and n % 16 == 0 and h in (32, 64) and model.action_head.bias is not None
+            and model.value_head.bias is not None and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16 and L.urm_wgrad_supported(16, h)
+            and L.urm_linear_supported(0, h, 8) and L.urm_linear_supported(0, 8, h))
+
+
 def linear_supported(lin, x: torch.Tensor) -> bool:
     """URMLinearFn applies: bf16 autocast on the GPU, no bias, g2048_urm_wgrad's shapes."""
     n, k = lin.weight.shape

@@ -338,7 +338,7 @@ def _c_chunk(args):
     return cnt
 
 
-PMC_PROFILE = ROOT / "profiles" / "r02i"
+PMC_PROFILE = ROOT / "profiles" / "r03o" / "train"
 CPU_RATIO = ROOT / "profiles" / "r02" / "cpu_ref_ratio.json"
 
 

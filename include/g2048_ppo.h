@@ -350,11 +350,12 @@ typedef struct g2048_muon_cfg {
     int32_t ns_steps, nesterov;
 } g2048_muon_cfg;
 
-/* 1 if a [rows, cols] matrix fits the one-block-per-matrix Newton-Schulz kernel (cols % 4 == 0,
- * min dim <= 224, max dim <= 256, both LDS images <= ~159 KB: h <= 196 for square weights). */
+/* 1 if a [rows, cols] matrix fits the one-block-per-matrix Newton-Schulz kernel (min dim <= 224,
+ * max dim <= 256, both LDS images <= ~159 KB: h <= 196 for square weights; rows of a length that
+ * is not a multiple of 4 -- GameURM's [64, 3] stem -- take a per-element momentum / update pass). */
 int g2048_muon_supported(int32_t rows, int32_t cols);
 
-/* Muon step of up to 8 matrices, all concurrently: momentum (nesterov), Newton-Schulz
+/* Muon step of up to 16 matrices (GameMLP: 5, GameURM: 11), all concurrently: momentum (nesterov), Newton-Schulz
  * orthogonalisation in bf16 (ns_steps iterations of X <- a X + (b G + c G^2) X, G = X X^T, on the
  * wide orientation), decoupled weight decay, update scaled by 0.2 sqrt(max(rows, cols)). */
 int g2048_muon_step(g2048_stream_t stream, const g2048_muon_matrix *mats, int32_t count, const float *lr_dev,

@@ -531,17 +531,21 @@ def _muon_models(dev, h=196):
     out = []
     for cls in (MuonAdamW, FusedMuonAdamW):
         torch.manual_seed(21)
-        m = agent.GameMLP(agent.MLPConfig(hidden_dim=h, num_layers=2, dropout=0.0)).to(dev)
+        if h == "urm":  # GameURM default config: 11 Muon matrices incl. the [64, 3] stem
+            m = agent.GameURM(agent.GameURMConfig(dropout=0.0)).to(dev)
+        else:
+            m = agent.GameMLP(agent.MLPConfig(hidden_dim=h, num_layers=2, dropout=0.0)).to(dev)
         opt = cls(m, 2e-3, 5e-4)
         order = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
         out.append((m, opt, GradBucket(order)))
     return out
 
 
-@pytest.mark.parametrize("h", [196, 64])
+@pytest.mark.parametrize("h", [196, 64, "urm"])
 def test_fused_muon_adamw_matches_torch_ops_step(dev, h):
     """FusedMuonAdamW (clip + Muon + AdamW kernels) vs MuonAdamW (torch ops, itself checked against
-    torch.optim.Muon/AdamW) over three steps on the same gradients."""
+    torch.optim.Muon/AdamW) over three steps on the same gradients; GameMLP h 196 / 64 and GameURM
+    (11 matrices, the [64, 3] stem on the per-element pass)."""
     (m0, o0, b0), (m1, o1, b1) = _muon_models(dev, h)
     assert o1.supported
     init = [p.detach().clone() for p in m0.parameters()]
@@ -557,7 +561,7 @@ def test_fused_muon_adamw_matches_torch_ops_step(dev, h):
         assert math.isclose(float(n0), float(n1), rel_tol=1e-5)
     for (name, p0), p1, q in zip(m0.named_parameters(), m1.parameters(), init):
         d0, d1 = (p0 - q).reshape(-1), (p1 - q).reshape(-1)
-        if p0.ndim >= 2:  # bf16 Newton-Schulz: same direction and size up to accumulation order
+        if p0.ndim == 2:  # bf16 Newton-Schulz: same direction and size up to accumulation order
             assert float(F.cosine_similarity(d0, d1, dim=0)) > 0.999, name
             assert math.isclose(float(d0.norm()), float(d1.norm()), rel_tol=1e-2), name
         else:
@@ -568,7 +572,8 @@ def test_fused_muon_supported_shapes():
     from g2048 import _lib as L
     assert L.muon_supported(196, 196) and L.muon_supported(196, 48) and L.muon_supported(4, 196)
     assert L.muon_supported(1, 196) and L.muon_supported(64, 64) and L.muon_supported(6, 196)
-    assert not L.muon_supported(256, 256) and not L.muon_supported(196, 6)
+    assert not L.muon_supported(256, 256) and not L.muon_supported(300, 6)
+    assert L.muon_supported(196, 6) and L.muon_supported(64, 3) and L.muon_supported(64, 120)  # GameURM shapes
 
 
 def test_padded_ragged_minibatch_matches_unpadded(dev):

@@ -537,6 +537,35 @@ def test_urm_gate_up_swiglu_fn_matches_unfused(dev, n):
         assert float((a - b).abs().max()) <= 0.01 * float(b.abs().max())
 
 
+@pytest.mark.parametrize("h,n", [(64, 65536), (32, 4096)])
+def test_urm_heads_fn_matches_autocast_heads(dev, h, n):
+    """URMHeadsFn (both heads as one projection on g2048_urm_linear, weight gradient on
+    g2048_urm_wgrad) vs action_head / value_head under bf16 autocast: outputs within one extra bf16
+    rounding (2^-7 relative + 1e-3), every gradient at cosine >= 0.9999 with max error <= 1 % of its
+    largest component (dW fp32 here, bf16-rounded on the library path)."""
+    from g2048.urm import URMHeadsFn
+    torch.manual_seed(h + n)
+    ha, hv = torch.nn.Linear(h, 4).to(dev), torch.nn.Linear(h, 1).to(dev)
+    p = torch.randn(n, h, device=dev)
+    ga, gv = torch.randn(n, 4, device=dev), torch.randn(n, 1, device=dev)
+    res = []
+    for fused in (True, False):
+        ha.zero_grad()
+        hv.zero_grad()
+        pi = p.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            la, lv = (URMHeadsFn.apply(pi, ha.weight, ha.bias, hv.weight, hv.bias) if fused else (ha(pi), hv(pi)))
+        assert la.dtype == torch.bfloat16 and lv.dtype == torch.bfloat16
+        ((la.float() * ga).sum() + (lv.float() * gv).sum()).backward()
+        res.append([la.float(), lv.float(), pi.grad, ha.weight.grad, ha.bias.grad, hv.weight.grad, hv.bias.grad])
+    for a, b in zip(res[0][:2], res[1][:2]):
+        assert bool(((a - b).abs() <= 2 ** -7 * b.abs() + 1e-3).all())
+    for a, b in zip(res[0][2:], res[1][2:]):
+        a, b = a.reshape(-1).float(), b.reshape(-1).float()
+        assert float(torch.nn.functional.cosine_similarity(a, b, dim=0)) >= 0.9999
+        assert float((a - b).abs().max()) <= 0.01 * float(b.abs().max())
+
+
 @pytest.mark.parametrize("n", [65536, 37])
 def test_urm_gate_up_swiglu_nograd_matches_training_kernel(dev, n):
     """The no-grad truncated loops' gate_up + SwiGLU-conv (inference epilogue, fp32 projection into

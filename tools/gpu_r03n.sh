@@ -3,7 +3,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_urm.py -q -x --timeout 240 --timeout-method thread > gpurun_out/gpu_urm_r03n.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_urm.py tests/test_gpu_ppo_fused.py -k "urm or muon" -q -x --timeout 240 --timeout-method thread > gpurun_out/gpu_urm_r03n.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/gpu_urm_r03n.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python -u tools/time_urm_train.py 0.1 > gpurun_out/time_urm_r03n.log 2>&1; head -3 gpurun_out/time_urm_r03n.log
 timeout -k 10 400 python3 bench.py --steps 2 --warmup 1 --cpu-seconds 0 --single-steps 0 --train-iters 0 --urm-steps 16 --sweep= > gpurun_out/urm_bench_r03n.log 2>&1

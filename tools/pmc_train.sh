@@ -12,6 +12,10 @@ URMS=${URM:+8}
 ARGS=${ARGS:---steps 2 --warmup 1 --cpu-seconds 0 --single-steps 0 --train-iters 1 --train-warmup 1 --urm-steps ${URMS:-0} --sweep=}
 OUT=gpurun_out/ptrain_$TAG
 mkdir -p $OUT
+# progress line every 50 s (PMC passes write nothing until they finish): the pass output sizes so far
+( while true; do sleep 50; echo "$(date +%T) $(du -sk $OUT 2>/dev/null | cut -f1) KiB in $OUT"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 pass() {  # pass <name> <rocprofv3 options...>
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" -T --output-format csv -d $OUT/$name -o run -- python3 bench.py $ARGS > $OUT/$name.log 2>&1
