@@ -31,9 +31,12 @@ def test_init_matches_reference_under_same_seed():
         assert np.array_equal(v.numpy(), u[f"init::{k}"]), k
 
 
-def test_urm_forward_matches_reference():
+@pytest.mark.parametrize("fixture", ["urm.npz", "urm64.npz"])
+def test_urm_forward_matches_reference(fixture):
+    """agent.GameURM (fp32, CPU) on the reference's weights vs the reference's own forward: the
+    small h 32 fixture and the default config (h 64, BASELINE config 5's policy)."""
     import agent
-    g = golden("urm.npz")
+    g = golden(fixture)
     h, L, heads, loops, trunc, k = (int(x) for x in g["config"])
     cfg = agent.GameURMConfig(hidden_dim=h, num_layers=L, num_heads=heads, num_loops=loops,
                               num_truncated_loops=trunc, conv_kernel=k, dropout=0.0,

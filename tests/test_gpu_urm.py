@@ -33,9 +33,9 @@ def dev():
     return torch.device("cuda:0")
 
 
-def _golden_model(dev):
+def _golden_model(dev, fixture="urm.npz"):
     import agent
-    g = golden("urm.npz")
+    g = golden(fixture)
     h, nl, heads, loops, trunc, k = (int(x) for x in g["config"])
     cfg = agent.GameURMConfig(hidden_dim=h, num_layers=nl, num_heads=heads, num_loops=loops, num_truncated_loops=trunc,
                               conv_kernel=k, dropout=0.0, expansion=float(g["expansion"]), rms_norm_eps=float(g["eps"]))
@@ -94,9 +94,13 @@ def _check(got, want, what):
     return err.max()
 
 
-def test_urm_policy_matches_reference_golden(dev):
+@pytest.mark.parametrize("fixture", ["urm.npz", "urm64.npz"])
+def test_urm_policy_matches_reference_golden(dev, fixture):
+    """URMPolicy (the rollout forward; at the default config of urm64.npz the one-launch kernel the
+    bench's URM leg times) vs the reference's own fp32 forward: the small h 32 fixture and the
+    default GameURMConfig (h 64, BASELINE config 5's policy), 512 boards of the golden games."""
     from g2048.urm import URMPolicy
-    m, g = _golden_model(dev)
+    m, g = _golden_model(dev, fixture)
     assert URMPolicy.supports(m)
     pol = URMPolicy(m)
     logits, value = pol(torch.from_numpy(g["obs"]).to(dev))

@@ -18,6 +18,8 @@ Fixture files (all npz, allow_pickle=False):
   sampler.npz     masked softmax / log_softmax / entropy of the rollout (train.py:266-326)
   update.npz      one model_optimize_step (train.py:414-642) with dropout 0, single minibatch
   urm.npz         GameURM forward (game.py:1355-1458), small random-init config
+  urm64.npz       GameURM forward at the default GameURMConfig (h 64: BASELINE config 5), 512 boards
+                  (`python tools/gen_golden.py urm64` regenerates only this file)
 """
 
 from __future__ import annotations
@@ -331,8 +333,34 @@ def gen_urm(game, games):
     print("urm.npz: h=32 L=2 heads=4 loops=4/1, 64 boards")
 
 
+def gen_urm64(game):
+    """urm64.npz: the reference's GameURM at its DEFAULT config (GameURMConfig(): h 64, 4 heads, 2
+    layers, loops 4 / 1 truncated, inter 120 -- BASELINE config 5's policy), eval mode, on 512
+    boards spread over the committed golden games (tests/golden/games.npz 'before'): what the
+    one-launch forward of the bench's URM leg computes."""
+    torch.manual_seed(2048)
+    cfg = game.GameURMConfig(dropout=0.0)
+    model = game.GameURM(cfg).eval()
+    before = np.load(OUT / "games.npz")["before"]
+    boards = before[np.linspace(0, len(before) - 1, 512).astype(np.int64)]
+    obs = torch.stack([game.Game2048(grid_of(b)).to_model_format() for b in boards])
+    with torch.no_grad():
+        logits, value = model(obs)
+    arrays = {f"w::{k}": v.numpy() for k, v in model.state_dict().items()}
+    arrays.update(obs=obs.numpy(), logits=logits.numpy(), value=value.numpy(),
+                  config=np.array([cfg.hidden_dim, cfg.num_layers, cfg.num_heads, cfg.num_loops,
+                                   cfg.num_truncated_loops, cfg.conv_kernel]),
+                  expansion=np.float64(cfg.expansion), eps=np.float64(cfg.rms_norm_eps))
+    np.savez_compressed(OUT / "urm64.npz", **arrays)
+    print(f"urm64.npz: default GameURMConfig {cfg}, 512 boards")
+
+
 def main():
     global DIRS
+    if sys.argv[1:] == ["urm64"]:  # only the default-config URM fixture (the other files unchanged)
+        game, _ = load_reference()
+        gen_urm64(game)
+        return
     OUT.mkdir(parents=True, exist_ok=True)
     game, train = load_reference()
     DIRS = [game.Direction.UP, game.Direction.DOWN, game.Direction.LEFT, game.Direction.RIGHT]
@@ -344,6 +372,7 @@ def main():
     gen_sampler()
     gen_update(game, train, games)
     gen_urm(game, games)
+    gen_urm64(game)
 
 
 if __name__ == "__main__":
