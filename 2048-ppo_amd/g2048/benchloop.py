@@ -86,9 +86,10 @@ def bench_train(args, rank: int, world: int, dev) -> dict:
 def bench_urm(args, rank: int, world: int, dev) -> dict:
     """BASELINE.json configs[4] on this GPU: the GameURM transformer policy (default GameURMConfig:
     h 64, 2 layers, 4 heads, 4 loops / 1 truncated, inter 120) driving 65 536 envs.  (1) rollout:
-    `--urm-steps` policy steps (obs -> URM forward on g2048/urm.py's kernels + hipBLASLt projections
-    -> sampler -> env step), captured in one hipGraph, timed over replays; (2) one full training
-    iteration at horizon `--urm-steps` (RTG + autograd bf16 update in minibatches of --train-batch)."""
+    `--urm-steps` policy steps (obs -> the one-launch URM forward g2048_urm_forward -> sampler -> env
+    step), captured in one hipGraph, timed over replays; (2) one full training iteration at horizon
+    `--urm-steps` (RTG + the bf16 update on the device autograd Functions of g2048/urm.py, one
+    hipGraph per minibatch of --train-batch, fused Muon/AdamW)."""
     import agent
     from g2048.rollout import Rollout, make_policy
     from g2048.trainer import TrainConfig, VecTrainer

@@ -8,9 +8,12 @@ import torch
 from conftest import golden
 
 
-def test_best_model_checkpoint_loads_and_matches_forward():
+@pytest.mark.parametrize("fixture", ["mlp.npz", "mlp196.npz"])
+def test_best_model_checkpoint_loads_and_matches_forward(fixture):
+    """The reference's best_model.pt (h 192) and a reference GameMLP at the bench's train config
+    (h 196, random init): state_dict loads, fp32 forward equals the reference's."""
     import agent
-    g = golden("mlp.npz")
+    g = golden(fixture)
     cfg = agent.MLPConfig(hidden_dim=int(g["hidden_dim"]), num_layers=int(g["num_layers"]))
     m = agent.GameMLP(cfg).eval()
     sd = {k[3:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("w::")}

@@ -825,6 +825,36 @@ def test_fused_policy_on_reference_checkpoint_matches_golden(dev):
     assert np.array_equal(got.argmax(1)[clear], ref.argmax(1)[clear])
 
 
+def test_fused_policy_h196_matches_reference_golden(dev):
+    """FusedPolicy -- bitwise the fused policy rollout's forward (test_gpu_policy_rollout.py) -- at the
+    bench's train configuration (h 196, 2 blocks) against the reference's own fp32 GameMLP forward
+    (tests/golden/mlp196.npz, random init, 512 golden boards).  Absolute bounds from the fixture's
+    output range R (logits R = 3.18, value R = 2.66): max error <= 0.02 R + 0.01, mean <= 0.004 R +
+    0.002 (the bf16 rounding of weights and of each layer's activations through 3 layers, as the
+    h 192 checkpoint test); the greedy legal action equals the reference's where its top-2 logit
+    margin exceeds 0.1."""
+    import agent
+    from g2048.rollout import FusedPolicy
+    g = golden("mlp196.npz")
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=196, num_layers=2)).to(dev)
+    m.load_state_dict({k[3:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("w::")}, strict=True)
+    m.eval()
+    assert FusedPolicy.supports(m)
+    lf, vf = FusedPolicy(m)(torch.from_numpy(g["obs"]).to(dev).to(torch.bfloat16))
+    for got, ref in ((lf.cpu().numpy(), g["logits"]), (vf.cpu().numpy(), g["value"][:, 0])):
+        r = float(np.abs(ref).max())
+        e = np.abs(got - ref)
+        print(f"h196 golden: range {r:.3g} max err {e.max():.4g} mean {e.mean():.4g}")
+        assert e.max() <= 0.02 * r + 0.01 and e.mean() <= 0.004 * r + 0.002, (e.max(), e.mean())
+    legal = O.legal_mask(g["boards"]) & 0xF
+    mask = ((legal[:, None] >> np.arange(4)) & 1).astype(bool)
+    ref = np.where(mask, g["logits"], -np.inf)
+    got = np.where(mask, lf.cpu().numpy(), -np.inf)
+    srt = np.sort(ref, axis=1)
+    clear = (srt[:, -1] - srt[:, -2] > 0.1) & (mask.sum(1) > 0)
+    assert np.array_equal(got.argmax(1)[clear], ref.argmax(1)[clear])
+
+
 def test_fused_update_minibatch4_matches_autograd(dev):
     """The README configuration's --batch-size=4 (train.py:1290): 22 rows = 5 full minibatches of 4 and a
     ragged one of 2.  Fused (bf16 MFMA) vs autograd fp32 update, dropout 0, same Muon+AdamW and the

@@ -20,6 +20,7 @@ Fixture files (all npz, allow_pickle=False):
   urm.npz         GameURM forward (game.py:1355-1458), small random-init config
   urm64.npz       GameURM forward at the default GameURMConfig (h 64: BASELINE config 5), 512 boards
                   (`python tools/gen_golden.py urm64` regenerates only this file)
+  mlp196.npz      GameMLP forward at the bench's train configuration (h 196, 2 blocks), 512 boards
 """
 
 from __future__ import annotations
@@ -333,6 +334,25 @@ def gen_urm(game, games):
     print("urm.npz: h=32 L=2 heads=4 loops=4/1, 64 boards")
 
 
+def gen_mlp196(game):
+    """mlp196.npz: the reference's GameMLP at the bench / README train configuration (h 196, 2
+    residual blocks; random init under torch.manual_seed(196), heads left at their Kaiming init so
+    the logits are not all zero), eval mode, on 512 boards spread over the golden games."""
+    torch.manual_seed(196)
+    cfg = game.MLPConfig(hidden_dim=196, num_layers=2)
+    model = game.GameMLP(cfg).eval()
+    before = np.load(OUT / "games.npz")["before"]
+    boards = before[np.linspace(0, len(before) - 1, 512).astype(np.int64)]
+    obs = torch.stack([game.Game2048(grid_of(b)).to_model_format() for b in boards])
+    with torch.no_grad():
+        logits, value = model(obs)
+    arrays = {f"w::{k}": v.numpy() for k, v in model.state_dict().items()}
+    arrays.update(boards=boards, obs=obs.numpy(), logits=logits.numpy(), value=value.numpy(),
+                  hidden_dim=np.int64(196), num_layers=np.int64(2))
+    np.savez_compressed(OUT / "mlp196.npz", **arrays)
+    print("mlp196.npz: GameMLP h=196 L=2 random init, 512 boards")
+
+
 def gen_urm64(game):
     """urm64.npz: the reference's GameURM at its DEFAULT config (GameURMConfig(): h 64, 4 heads, 2
     layers, loops 4 / 1 truncated, inter 120 -- BASELINE config 5's policy), eval mode, on 512
@@ -357,9 +377,9 @@ def gen_urm64(game):
 
 def main():
     global DIRS
-    if sys.argv[1:] == ["urm64"]:  # only the default-config URM fixture (the other files unchanged)
+    if sys.argv[1:] in (["urm64"], ["mlp196"]):  # only that fixture (the other files unchanged)
         game, _ = load_reference()
-        gen_urm64(game)
+        {"urm64": gen_urm64, "mlp196": gen_mlp196}[sys.argv[1]](game)
         return
     OUT.mkdir(parents=True, exist_ok=True)
     game, train = load_reference()
@@ -373,6 +393,7 @@ def main():
     gen_update(game, train, games)
     gen_urm(game, games)
     gen_urm64(game)
+    gen_mlp196(game)
 
 
 if __name__ == "__main__":
