@@ -292,8 +292,13 @@ class GameURM(nn.Module):
         return [o2, o1, v2, v1]
 
     def _loop(self, h: torch.Tensor, emb: torch.Tensor) -> torch.Tensor:
-        h = h + emb
         hb = None  # bf16 copy of h handed from block to block (device path, bf16 autocast)
+        if emb.is_cuda:
+            from g2048 import urm as _urm  # h + emb with its bf16 copy in one kernel (g2048_urm.h)
+            if _urm.add_cast_supported(h, emb):
+                h, hb = _urm.AddCastFn.apply(h, emb)
+        if hb is None:
+            h = h + emb
         last = len(self.layers) - 1
         for i, layer in enumerate(self.layers):
             if i < last:
@@ -320,7 +325,7 @@ class GameURM(nn.Module):
                                         ln.eps).view(b, N_CELLS, -1)
         if emb is None:
             emb = self.stem(inputs.view(b, N_CELLS, 3))
-        h = self.init_hidden.expand(b, -1, -1).clone()
+        h = self.init_hidden.expand(b, -1, -1)  # (the reference clones it; every use here is out of place)
         n_trunc = self.config.num_truncated_loops
         if n_trunc > 0:
             with torch.no_grad():

@@ -1667,6 +1667,36 @@ __global__ __launch_bounds__(kWgThreads) void urm_wgrad_kernel(const uint16_t *_
 
 }  // namespace
 
+// ---------------------------------------------------------------------------------------------
+// A loop start of GameURM training (game.py:1441: hidden_states + emb): out = a + e (fp32) and its
+// bf16 copy (the first block's qkv operand under autocast) in one pass; `a` may be a per-board
+// broadcast of `a_rows` rows (init_hidden [16, h] expanded over the boards).  Backward: the two
+// gradient halves (fp32 from the residual RMSNorm, bf16 from the projection) summed into one fp32.
+__global__ __launch_bounds__(256) void urm_add_cast_kernel(const float4 *__restrict__ a, int64_t a4,
+                                                           const float4 *__restrict__ e, float4 *__restrict__ out,
+                                                           uint2 *__restrict__ outb, int64_t n4) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        const float4 x = a[a4 ? i % a4 : i], y = e[i];
+        const float4 o = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+        out[i] = o;
+        outb[i] = make_uint2((uint32_t)f2bf(o.x) | ((uint32_t)f2bf(o.y) << 16), (uint32_t)f2bf(o.z) | ((uint32_t)f2bf(o.w) << 16));
+    }
+}
+
+__global__ __launch_bounds__(256) void urm_add_cast_bwd_kernel(const float4 *__restrict__ dout,
+                                                               const uint2 *__restrict__ doutb, float4 *__restrict__ dx,
+                                                               int64_t n4) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        float4 d = dout ? dout[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (doutb) {
+            const uint2 b = doutb[i];
+            d = make_float4(d.x + __uint_as_float(b.x << 16), d.y + __uint_as_float(b.x & 0xFFFF0000u),
+                            d.z + __uint_as_float(b.y << 16), d.w + __uint_as_float(b.y & 0xFFFF0000u));
+        }
+        dx[i] = d;
+    }
+}
+
 extern "C" {
 
 int g2048_urm_stem(g2048_stream_t stream, const void *obs, int32_t obs_dtype, const float *w, const float *ln_w,
@@ -1754,6 +1784,34 @@ int g2048_urm_rms_res_fwd2(g2048_stream_t stream, const float *h, const void *a,
     else
         hipLaunchKernelGGL(urm_rms_res_fwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, h, a, out, rstd, rows,
                            eps, outb);
+    return launch_status();
+}
+
+int g2048_urm_add_cast(g2048_stream_t stream, const float *a, int64_t a_rows, const float *e, float *out, uint16_t *outb,
+                       int64_t rows, int32_t hidden) {
+    if (rows < 0 || hidden <= 0 || hidden % 4 || a_rows < 0 || (a_rows && rows % a_rows)) return G2048_EINVAL;
+    if (rows == 0) return G2048_OK;
+    if (!a || !e || !out || !outb || ((uintptr_t)a | (uintptr_t)e | (uintptr_t)out) % 16 || (uintptr_t)outb % 8)
+        return G2048_EINVAL;
+    const int64_t n4 = rows * hidden / 4;
+    const int64_t blocks = (n4 + 255) / 256;
+    hipLaunchKernelGGL(urm_add_cast_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0,
+                       (hipStream_t)stream, reinterpret_cast<const float4 *>(a), a_rows * hidden / 4,
+                       reinterpret_cast<const float4 *>(e), reinterpret_cast<float4 *>(out),
+                       reinterpret_cast<uint2 *>(outb), n4);
+    return launch_status();
+}
+
+int g2048_urm_add_cast_bwd(g2048_stream_t stream, const float *dout, const uint16_t *doutb, float *dx, int64_t rows,
+                           int32_t hidden) {
+    if (rows < 0 || hidden <= 0 || hidden % 4) return G2048_EINVAL;
+    if (rows == 0) return G2048_OK;
+    if (!dx || ((uintptr_t)dout | (uintptr_t)dx) % 16 || (uintptr_t)doutb % 8) return G2048_EINVAL;
+    const int64_t n4 = rows * hidden / 4;
+    const int64_t blocks = (n4 + 255) / 256;
+    hipLaunchKernelGGL(urm_add_cast_bwd_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0,
+                       (hipStream_t)stream, reinterpret_cast<const float4 *>(dout), reinterpret_cast<const uint2 *>(doutb),
+                       reinterpret_cast<float4 *>(dx), n4);
     return launch_status();
 }
 

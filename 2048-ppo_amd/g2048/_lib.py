@@ -33,7 +33,7 @@ EXPORTED = (
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_wgrad_pair_partials", "g2048_wgrad_pair", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
-    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_rms_res_fwd2", "g2048_urm_rms_res_bwd2", "g2048_urm_forward_drop", "g2048_urm_rms_res_fwd",
+    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_rms_res_fwd2", "g2048_urm_rms_res_bwd2", "g2048_urm_add_cast", "g2048_urm_add_cast_bwd", "g2048_urm_forward_drop", "g2048_urm_rms_res_fwd",
     "g2048_urm_rms_res_bwd", "g2048_urm_swiglu_conv_partials", "g2048_urm_swiglu_conv_fwd", "g2048_urm_swiglu_conv_bwd",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
@@ -263,6 +263,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_grad_sumsq_tick": (ctypes.c_int, [vp, vp, i64, vp, vp]),
         "g2048_urm_attention_bwd": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_rms_res_fwd2": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, vp, i64, i32, ctypes.c_float]),
+        "g2048_urm_add_cast": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, i64, i32]),
+        "g2048_urm_add_cast_bwd": (ctypes.c_int, [vp, vp, vp, vp, i64, i32]),
         "g2048_urm_rms_res_bwd2": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, i64, i32]),
         "g2048_urm_stem_partials": (sz, [i64]),
         "g2048_urm_stem_fwd": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, i64, i32, ctypes.c_float]),
@@ -944,6 +946,22 @@ def urm_rms_res_fwd(h, a, out, rstd, eps: float, outb=None):
                                          _dev(out, torch.float32, "out"), _dev(outb, torch.bfloat16, "outb"),
                                          _dev(rstd, torch.float32, "rstd"), rows, hid, float(eps)),
            "g2048_urm_rms_res_fwd2")
+
+
+def urm_add_cast(a, a_rows: int, e, out, outb):
+    """out = a + e, outb = bf16(out) (g2048_urm_add_cast); a broadcast over groups of a_rows rows
+    when a_rows > 0."""
+    rows, hid = e.shape
+    _check(load().g2048_urm_add_cast(_stream(e), _dev(a, torch.float32, "a"), int(a_rows), _dev(e, torch.float32, "e"),
+                                     _dev(out, torch.float32, "out"), _dev(outb, torch.bfloat16, "outb"), rows, hid),
+           "g2048_urm_add_cast")
+
+
+def urm_add_cast_bwd(dout, doutb, dx):
+    """dx = dout + float(doutb); either may be None (g2048_urm_add_cast_bwd)."""
+    rows, hid = dx.shape
+    _check(load().g2048_urm_add_cast_bwd(_stream(dx), _dev(dout, torch.float32, "dout"), _dev(doutb, torch.bfloat16, "doutb"),
+                                         _dev(dx, torch.float32, "dx"), rows, hid), "g2048_urm_add_cast_bwd")
 
 
 def urm_rms_res_bwd(dout, out, rstd, dh, da, doutb=None):

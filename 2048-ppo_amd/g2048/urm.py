@@ -342,6 +342,53 @@ class ResidualRMSFn(torch.autograd.Function):
         return dh.view(ctx.shape), da.view(ctx.shape), None, None
 
 
+class AddCastFn(torch.autograd.Function):
+    """A loop start of GameURM (game.py:1441: hidden_states + emb) under bf16 autocast, for autograd
+    training on the device: the fp32 sum and its bf16 copy -- the first block's qkv operand, which
+    autocast would cast in a kernel of its own -- in one kernel (g2048_urm_add_cast); the backward
+    sums the fp32 gradient (residual RMSNorm) and the bf16 one (the projection) in one kernel
+    instead of autocast's cast backward plus autograd's accumulation.  Values bitwise those of
+    `h + emb` and its `.to(bfloat16)`.  h [b, 16, 64] (contiguous, or init_hidden [1, 16, 64]
+    expanded over the boards), emb [b, 16, 64] fp32 -> (out fp32, outb bf16)."""
+
+    @staticmethod
+    def forward(ctx, h: torch.Tensor, emb: torch.Tensor):
+        ctx.set_materialize_grads(False)
+        b, s, hid = emb.shape
+        e2 = emb.reshape(-1, hid).contiguous()
+        bcast = h.shape[0] == 1 or h.stride(0) == 0
+        a = (h[:1] if bcast else h).reshape(-1, hid).contiguous()
+        out = torch.empty_like(e2)
+        outb = torch.empty(e2.shape, dtype=torch.bfloat16, device=emb.device)
+        L.urm_add_cast(a, s if bcast else 0, e2, out, outb)
+        ctx.bcast, ctx.shape = bcast, (b, s, hid)
+        return out.view(b, s, hid), outb.view(b, s, hid)
+
+    @staticmethod
+    def backward(ctx, dout: torch.Tensor | None, doutb: torch.Tensor | None):
+        if dout is None and doutb is None:
+            return None, None
+        b, s, hid = ctx.shape
+        dx = torch.empty(b * s, hid, dtype=torch.float32, device=(dout if dout is not None else doutb).device)
+        L.urm_add_cast_bwd(None if dout is None else dout.reshape(-1, hid).float().contiguous(),
+                           None if doutb is None else doutb.reshape(-1, hid).to(torch.bfloat16).contiguous(), dx)
+        dx = dx.view(b, s, hid)
+        # the gradient of h in the shape it came in (an expanded init_hidden: expand's backward sums it)
+        return (dx if ctx.needs_input_grad[0] else None), (dx if ctx.needs_input_grad[1] else None)
+
+
+def add_cast_supported(h: torch.Tensor, emb: torch.Tensor) -> bool:
+    """AddCastFn applies: bf16 autocast on the GPU, fp32 [b, 16, 64] operands (h possibly the
+    expanded init_hidden)."""
+    if not (emb.is_cuda and h.is_cuda and emb.dtype == torch.float32 and h.dtype == torch.float32):
+        return False
+    if emb.ndim != 3 or h.ndim != 3 or tuple(emb.shape[1:]) != (16, 64) or tuple(h.shape[1:]) != (16, 64):
+        return False
+    if not emb.is_contiguous() or h.shape[0] not in (1, emb.shape[0]):
+        return False
+    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
+
 def rms_res_supported(h: torch.Tensor, a: torch.Tensor) -> bool:
     """The device residual RMSNorm applies: fp32 residual stream of hidden size 64 on the GPU."""
     return (h.is_cuda and h.dtype == torch.float32 and a.dtype in (torch.float32, torch.bfloat16)

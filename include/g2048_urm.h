@@ -80,6 +80,16 @@ int g2048_urm_rms_res_fwd2(g2048_stream_t stream, const float *h, const void *a,
 int g2048_urm_rms_res_bwd2(g2048_stream_t stream, const float *dout, const uint16_t *doutb, const float *out,
                            const float *rstd, float *dh, void *da, int32_t a_dtype, int64_t rows, int32_t hidden);
 
+/* A GameURM loop start for autograd training (game.py:1441, hidden_states + emb under bf16
+ * autocast): out fp32 [rows, hidden] = a + e and outb = bf16(out) (the first block's qkv operand) in
+ * one pass; a has rows rows, or a_rows rows broadcast over groups of a_rows (init_hidden [16, h]
+ * over the boards; a_rows 0 = rows).  Backward: dx fp32 = dout + float(doutb) (the fp32 and bf16
+ * gradient halves; either may be NULL). */
+int g2048_urm_add_cast(g2048_stream_t stream, const float *a, int64_t a_rows, const float *e, float *out, uint16_t *outb,
+                       int64_t rows, int32_t hidden);
+int g2048_urm_add_cast_bwd(g2048_stream_t stream, const float *dout, const uint16_t *doutb, float *dx, int64_t rows,
+                           int32_t hidden);
+
 /* SwiGLU + depthwise conv (kernel 2) for autograd training (GameConvSwiGLU, game.py:1264-1276),
  * n boards of 16 tokens, inter <= 128 channels, the reference's autocast dtypes:
  *   forward  y = bf16(bf16(silu(gate)) up), y2 = y_{t-1} w[c][0] + y_t w[c][1] + b[c] (fp32),

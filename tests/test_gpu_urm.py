@@ -541,6 +541,35 @@ def test_urm_gate_up_swiglu_fn_matches_unfused(dev, n):
         assert float((a - b).abs().max()) <= 0.01 * float(b.abs().max())
 
 
+@pytest.mark.parametrize("bcast", [False, True])
+def test_urm_add_cast_fn_is_bitwise_the_module_ops(dev, bcast):
+    """AddCastFn (a loop start h + emb and its bf16 copy in one kernel; backward sums the fp32 and
+    bf16 gradient halves in one kernel) vs the ops it replaces -- h + emb, .to(bfloat16), autograd's
+    cast backward and accumulation: forward and every gradient bitwise equal; h contiguous or the
+    expanded init_hidden."""
+    from g2048.urm import AddCastFn
+    torch.manual_seed(3)
+    b = 4097
+    h0 = torch.randn(1 if bcast else b, 16, 64, device=dev)
+    e0 = torch.randn(b, 16, 64, device=dev)
+    g1, g2 = torch.randn(b, 16, 64, device=dev), torch.randn(b, 16, 64, device=dev)
+    res = []
+    for fused in (True, False):
+        h = h0.clone().requires_grad_(True)
+        e = e0.clone().requires_grad_(True)
+        hx = h.expand(b, -1, -1) if bcast else h
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            if fused:
+                out, outb = AddCastFn.apply(hx, e)
+            else:
+                out = hx + e
+                outb = out.to(torch.bfloat16)
+        ((out * g1).sum() + (outb.float() * g2).sum()).backward()
+        res.append((out.detach(), outb.detach(), h.grad, e.grad))
+    for a, c in zip(*res):
+        assert torch.equal(a, c)
+
+
 @pytest.mark.parametrize("h,n", [(64, 65536), (32, 4096)])
 def test_urm_heads_fn_matches_autocast_heads(dev, h, n):
     """URMHeadsFn (both heads as one projection on g2048_urm_linear, weight gradient on
