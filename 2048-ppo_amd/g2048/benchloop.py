@@ -58,8 +58,10 @@ def bench_train(args, rank: int, world: int, dev) -> dict:
     n_mb = -(-(args.envs * args.train_horizon + m["augmented_samples"]) // args.train_batch)
     # roofline of the two MFMA phases of the profiled iteration (one GPU's share): algorithmic FLOP
     # over the phase's wall time against the dense bf16 peak
-    fl = mlp_flops_per_sample()
-    rows_update = n_mb * args.train_batch
+    mc = tr.model.config
+    fl = mlp_flops_per_sample(h=mc.hidden_dim, layers=len(tr.model.backbone))
+    # the update's work is the real sample rows: the ragged last minibatch's padding is not counted
+    rows_update = args.envs * args.train_horizon + int(m["augmented_samples"])
     roof = {}
     for name, ms_key, flop in (("update", "update_ms", fl["update"] * rows_update),
                                ("policy_rollout", "rollout_ms", fl["forward"] * args.envs * args.train_horizon)):
@@ -91,6 +93,7 @@ def bench_urm(args, rank: int, world: int, dev) -> dict:
     `--urm-steps` (RTG + the bf16 update on the device autograd Functions of g2048/urm.py, one
     hipGraph per minibatch of --train-batch, fused Muon/AdamW)."""
     import agent
+    import torch.distributed as dist
     from g2048.rollout import Rollout, make_policy
     from g2048.trainer import TrainConfig, VecTrainer
     torch.manual_seed(0x2048 + rank)
@@ -135,15 +138,24 @@ def bench_urm(args, rank: int, world: int, dev) -> dict:
                       batch_size=args.train_batch, hidden=64, model_type="urm", points=0.1, mono=1.0, rtg_beta=0.99,
                       warmup_steps=10, horizon=T, seed=0x2048, graph=True, amp=True)
     tr = VecTrainer(cfg, dev)
-    tr.train_step(0)
+    tr.train_step(0)  # warm-up: graph capture
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    iters = max(1, int(getattr(args, "urm_iters", 3)))
+    t0 = time.perf_counter()  # profiling off: no per-phase syncs inside the timed iterations
+    for s in range(iters):
+        mt = tr.train_step(1 + s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    it = (time.perf_counter() - t0) / iters
+    # one more profiled iteration for the phase breakdown (outside the timed region)
     tr.profile = True
     tr.timings = {}
-    t0 = time.perf_counter()
-    mt = tr.train_step(1)
-    torch.cuda.synchronize()
-    it = time.perf_counter() - t0
+    tr.train_step(1 + iters)
     out["train_iter"] = {"value": args.envs * T * world / it, "unit": "env-steps/s", "ms_per_iter": it * 1e3,
+                         "iters": iters,
                          "kernel_paths": tr.paths, "fallbacks": tr.fallbacks,
                          "phase_ms": {k: round(v, 3) for k, v in tr.timings.items()},
                          "minibatch": args.train_batch, "loss": mt["loss"], "entropy": mt["entropy"]}

@@ -3,7 +3,8 @@
 The envs shard trivially (each rank owns its boards and its own Philox key), so the data path has
 only two exchanges per train step:
   * the policy gradient: ONE all-reduce of a single flat fp32 bucket per optimizer step, issued
-    before gradient clipping so every replica clips and steps identically;
+    before gradient clipping so every replica clips and steps identically; under RCCL it is captured
+    inside the minibatch's hipGraph (one graph replay per minibatch, no host round trip);
   * the return-to-go batch statistics: one all-reduce of 3 float64 sums per train step.
 """
 
@@ -75,7 +76,7 @@ def _host_staged() -> bool:
 
 
 def allreduce_sum_(t: torch.Tensor) -> torch.Tensor:
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized() and (dist.get_world_size() > 1 or dist.get_backend() == "nccl"):
         if t.is_cuda and _host_staged():
             h = t.cpu()
             dist.all_reduce(h)
@@ -121,10 +122,26 @@ class GradBucket:
     def world() -> int:
         return dist.get_world_size() if dist.is_initialized() else 1
 
+    @staticmethod
+    def rccl() -> bool:
+        return dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"
+
+    @classmethod
+    def capturable(cls) -> bool:
+        """The gradient all-reduce can be captured into the minibatch hipGraph: RCCL ("nccl")
+        collectives on device buffers are graph-capturable; gloo's host-staged path is not (the
+        updater then splits its graph around an eager all-reduce)."""
+        return cls.world() == 1 or cls.rccl()
+
     def allreduce_mean(self):
-        if dist.is_initialized() and dist.get_world_size() > 1:
+        """Mean of the flat bucket over the ranks.  Under RCCL the collective is issued even with a
+        single rank (a one-rank all-reduce), so a world-size-1 RCCL run exercises -- and captures --
+        the same call as the 8-GPU one."""
+        w = self.world()
+        if w > 1 or self.rccl():
             allreduce_sum_(self.flat)
-            self.flat.div_(dist.get_world_size())
+            if w > 1:
+                self.flat.div_(w)
 
     def clip_(self, max_norm: float) -> torch.Tensor:
         """torch.nn.utils.clip_grad_norm_ semantics on the flat buffer; returns the pre-clip norm."""

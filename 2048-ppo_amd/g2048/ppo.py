@@ -72,8 +72,9 @@ class PPOUpdater:
 
     graph=True (device tensors, graph-safe optimizer such as optim.MuonAdamW): the whole minibatch
     step -- gather, encode, forward, loss, backward, clip, optimizer, KL diagnostic, statistics --
-    is captured once into a hipGraph and replayed per minibatch with a new index vector; with
-    several ranks the step is split into two graphs around the eager RCCL gradient all-reduce.
+    is captured once into a hipGraph and replayed per minibatch with a new index vector; the RCCL
+    gradient all-reduce is captured with it (gloo: the step is split into two graphs around an eager
+    host-staged all-reduce).
     """
 
     def __init__(self, model, optimizer, cfg: PPOConfig, grads, generator: torch.Generator | None = None,
@@ -174,9 +175,11 @@ class PPOUpdater:
             return
         self._g = None
         torch.cuda.synchronize()
-        # several ranks: the gradient all-reduce runs eagerly between two graphs (g1: forward, loss,
-        # backward; g2: clip, optimizer, KL); force_split exercises that path on one GPU
-        split = self.grads.world() > 1 or self.force_split
+        # the gradient all-reduce: captured inside the one graph under RCCL (and a no-op on a single
+        # process without torch.distributed); gloo's host-staged all-reduce cannot be captured, so
+        # there it runs eagerly between two graphs (g1: forward, loss, backward; g2: clip, optimizer,
+        # KL); force_split exercises that path on one GPU
+        split = not self.grads.capturable() or self.force_split
         idx = torch.zeros(bs, dtype=torch.int64, device=self.dev)
         params = [p for p in self.model.parameters()]
         snap_p = [p.detach().clone() for p in params]
@@ -195,6 +198,7 @@ class PPOUpdater:
         with torch.cuda.graph(g1, pool=pool):
             st = self._pre(idx, data, self.beta_t, encode)
             if not split:
+                self.grads.allreduce_mean()
                 self._post(st, self.beta_t)
         if split:
             g2 = torch.cuda.CUDAGraph()

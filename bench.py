@@ -76,6 +76,7 @@ def parse():
     p.add_argument("--train-batch", type=int, default=65536)
     p.add_argument("--train-upsample", type=float, default=0.25, help="--upsample-ratio of the README command")
     p.add_argument("--urm-steps", type=int, default=16, help="GameURM policy rollout leg: steps per graph (0=off)")
+    p.add_argument("--urm-iters", type=int, default=3, help="timed GameURM training iterations")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of each CPU-baseline leg (0=off)")
     p.add_argument("--sweep", default="1048576,4194304,16777216",
                    help="comma list of board counts for the rollout-kernel sweep ('' = off)")
@@ -285,7 +286,12 @@ def cpu_baselines(seconds):
     except Exception as e:  # pragma: no cover
         return {"error": f"oracle unavailable: {e}"}
     import multiprocessing as mp
-    cores = min(len(os.sched_getaffinity(0)), 16)
+    # every core this job may use: the GPU box's CPU share is its OMP_NUM_THREADS (16 per GPU; nproc
+    # there shows the whole machine), capped by the affinity mask
+    visible = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    cores = min(visible, share) if share > 0 else visible
+    out["cores"] = {"used": cores, "visible": visible, "job_share": share or None}
     ratio = json.loads(CPU_RATIO.read_text()) if CPU_RATIO.exists() else None
     src = str(CPU_RATIO.relative_to(ROOT))
 
@@ -461,7 +467,7 @@ def main():
         py = cb.get("python_1core")
         if py:
             result["cpu_baseline"] = dict(py, unit="env-steps/s", cores=1, kind="port")
-        for k in ("c_oracle", "python_pool", "train_loop_cpu"):
+        for k in ("c_oracle", "python_pool", "train_loop_cpu", "cores"):
             if k in cb:
                 result[f"cpu_baseline_{k}"] = cb[k]
     if rank == 0:

@@ -10,8 +10,10 @@ Checked across the ranks:
   * the RTG batch moments (advantage.RTGTracker's 24-byte partials reduce) equal those of the
     concatenated trajectories of both ranks;
   * equal_rows gave both ranks the same sample count, hence the same minibatch count.
-RCCL cannot put two ranks on one GPU, so the collectives here are gloo's CUDA-tensor all-reduces;
-the driver's 8-GPU scaling run uses RCCL through the same calls."""
+Both policies: GameMLP (FusedPPOUpdater) and GameURM (PPOUpdater over g2048/urm.py's device
+Functions, the reference's game.py:1355-1458 model).  RCCL cannot put two ranks on one GPU, so the
+collectives here are gloo's CUDA-tensor all-reduces (host staged, hence the split graph); the RCCL
+path -- the all-reduce captured inside the minibatch graph -- is tests/test_gpu_rccl.py."""
 
 import os
 import socket
@@ -36,7 +38,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, model_type="mlp"):
     for p in (str(ROOT), str(PKG)):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -48,12 +50,22 @@ def _worker(rank, world, port, out):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     torch.manual_seed(rank)  # different local inits: VecTrainer must broadcast rank 0's replica
-    cfg = TrainConfig(steps=10, episodes=512, horizon=16, batch_size=2048, hidden=196, dropout=0.0, points=0.1,
-                      mono=1.0, rtg_beta=0.99, gamma=0.99, entropy=0.02, critic=0.2, warmup_steps=0,
-                      upsample_ratio=0.25)
+    if model_type == "urm":  # GameURM (default config: h 64, 2 layers, 4 heads, 4 / 1 loops) on its device Functions
+        cfg = TrainConfig(steps=10, episodes=256, horizon=8, batch_size=1024, hidden=64, model_type="urm",
+                          dropout=0.0, points=0.1, mono=1.0, rtg_beta=0.99, gamma=0.99, entropy=0.02, critic=0.2,
+                          warmup_steps=0, upsample_ratio=0.25)
+    else:
+        cfg = TrainConfig(steps=10, episodes=512, horizon=16, batch_size=2048, hidden=196, dropout=0.0, points=0.1,
+                          mono=1.0, rtg_beta=0.99, gamma=0.99, entropy=0.02, critic=0.2, warmup_steps=0,
+                          upsample_ratio=0.25)
     tr = VecTrainer(cfg, dev)
     rec = {"before": [], "after": [], "rows": [], "nb": [], "g_raw": [], "moments": []}
-    assert isinstance(tr.ppo, fastmlp.FusedPPOUpdater) and tr.ppo.graph
+    if model_type == "urm":
+        from g2048 import urm as urm_mod
+        assert not isinstance(tr.ppo, fastmlp.FusedPPOUpdater) and tr.ppo.graph == urm_mod.training_graph_ok(tr.model)
+        assert tr.ppo.graph  # the captured (split) URM minibatch step
+    else:
+        assert isinstance(tr.ppo, fastmlp.FusedPPOUpdater) and tr.ppo.graph
     bucket = tr.grads
     orig_ar = bucket.allreduce_mean
 
@@ -85,14 +97,17 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_two_ranks_fused_update_on_device():
+@pytest.mark.parametrize("model_type", ["mlp", "urm"])
+def test_two_ranks_fused_update_on_device(model_type):
+    """GameMLP: the kernel-written FusedPPOUpdater; GameURM (BASELINE config 5's policy): PPOUpdater
+    over the URM device autograd Functions, captured in the same split graph."""
     import torch.multiprocessing as mp
     if not torch.cuda.is_available():
         pytest.fail("no ROCm device visible")
     port = _free_port()
     with mp.Manager() as man:
         out = man.dict()
-        mp.start_processes(_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+        mp.start_processes(_worker, args=(2, port, out, model_type), nprocs=2, join=True, start_method="spawn")
         r0, r1 = out[0], out[1]
     # same sample count and minibatch count on both ranks, every train step
     assert r0["rows"] == r1["rows"] and r0["nb"] == r1["nb"] and len(r0["rows"]) == STEPS
