@@ -152,28 +152,65 @@ class VecTrainer:
         self._chunk_graphs = {}
         self.profile = False
         self.timings: dict[str, float] = {}
-        self.paths, self.fallbacks = self._fast_paths()
         for msg in self.fallbacks:
             warnings.warn(f"g2048: {msg}", stacklevel=2)
 
+    def _update_forward_path(self) -> str:
+        """The update's forward / backward path as FusedPPOUpdater decided it in its buffer allocation
+        (fastmlp.FusedPPOUpdater._alloc: fused_pass / fused_back), or the static prediction before the
+        first update has run."""
+        import agent
+        up = self.ppo
+        if not isinstance(up, fastmlp.FusedPPOUpdater):
+            if isinstance(self.model, agent.GameURM):
+                return "URM device Functions" if self._urm_device_functions() else "autograd (library GEMMs / SDPA)"
+            return "autograd"
+        if up.bs:  # decided by _alloc for the current minibatch size
+            if up.fused_pass:
+                return "fused train / KL passes + " + ("fused backward" if up.fused_back else "per-layer backward")
+            return "mlp_fwd kernels" if all(up.mf_ok) else "hipBLASLt + ln_act_fwd"
+        pred = L.mlp_pass_supported(self.model.config.hidden_dim, len(self.model.backbone))
+        return ("fused train / KL passes + fused backward" if pred else
+                "mlp_fwd kernels" if all(up.mf_ok) else "hipBLASLt + ln_act_fwd") + " (predicted: no update yet)"
+
+    def _urm_device_functions(self) -> bool:
+        """Every training op of this GameURM runs on a device Function (urm.training_graph_ok) and
+        its projections / heads fit the MFMA projection kernel (no torch.mm fallback in urm._gemm)."""
+        m = self.model
+        c = m.config
+        inter = m.layers[0].mlp.inter
+        return (self.dev.type == "cuda" and self.cfg.amp and urm_mod.training_graph_ok(m)
+                and urm_mod.gemm_supported(3 * c.hidden_dim, c.hidden_dim) and urm_mod.gemm_supported(c.hidden_dim, c.hidden_dim)
+                and urm_mod.gemm_supported(c.hidden_dim, inter) and urm_mod.gemm_supported(8, c.hidden_dim))
+
+    @property
+    def paths(self) -> dict:
+        return self._fast_paths()[0]
+
+    @property
+    def fallbacks(self) -> list[str]:
+        return self._fast_paths()[1]
+
     def _fast_paths(self) -> tuple[dict, list[str]]:
-        """Which kernel path each phase runs on, and a message per GameMLP phase that fell back from
-        its fused kernel (shapes the kernels do not cover, e.g. -l 3 or -h 256): the CLI prints them
-        and bench.py puts `paths` in its JSON line, so a fallback is never silent."""
+        """Which kernel path each phase runs on, and a message per phase that fell back from its
+        fused kernel (shapes the kernels do not cover, e.g. -l 3 or -h 256; a GameURM off the device
+        Functions or the captured update): the CLI prints them and bench.py puts `paths` /
+        `fallbacks` in its JSON line, so a fallback is never silent.  Re-evaluated on every read: the
+        update paths come from the updater's own decision once it has allocated its buffers."""
         import agent
         pol, up = self.policy, self.ppo
         mlp = isinstance(self.model, agent.GameMLP)
-        fused_up = isinstance(up, fastmlp.FusedPPOUpdater)
+        urm = isinstance(self.model, agent.GameURM)
         inner = getattr(self.opt, "opt", self.opt)
         paths = {"policy": type(pol).__name__,
                  "rollout": "policy_rollout_kernel" if getattr(pol, "fused_rollout", False) else "per-step kernels",
                  "update": type(up).__name__,
-                 "update_forward": ("fused train / KL passes + fused backward" if fused_up and mlp and L.mlp_pass_supported(
-                                        self.model.config.hidden_dim, len(self.model.backbone))
-                                    else "mlp_fwd kernels" if fused_up and all(up.mf_ok)
-                                    else "hipBLASLt + ln_act_fwd" if fused_up else "autograd"),
+                 "update_forward": self._update_forward_path(),
                  "optimizer": "fused Muon/AdamW kernels" if getattr(inner, "supported", False) else type(inner).__name__,
                  "update_graph": bool(getattr(up, "graph", False))}
+        if urm:
+            paths["urm_rollout"] = ("one-launch g2048_urm_forward" if getattr(pol, "mega", False)
+                                    else "per-op kernels" if getattr(pol, "fused", False) else "torch.mm + kernels")
         fb = []
         if mlp and self.dev.type == "cuda":
             h, nl = self.model.config.hidden_dim, len(self.model.backbone)
@@ -186,6 +223,19 @@ class VecTrainer:
                 fb.append(f"update forward: no MFMA layer kernel for h={h}; hipBLASLt GEMM + ln_act_fwd")
             if self.cfg.graph_update and self.cfg.fused_update and not getattr(inner, "supported", False):
                 fb.append(f"optimizer: the fused Muon kernel does not cover h={h}; torch-op Newton-Schulz")
+            if isinstance(up, fastmlp.FusedPPOUpdater) and up.bs and not (up.fused_pass and up.fused_back):
+                fb.append(f"update: {paths['update_forward']} instead of the fused passes + fused backward")
+        if urm and self.dev.type == "cuda":
+            h = self.model.config.hidden_dim
+            if not self._urm_device_functions():
+                fb.append(f"update: GameURM h={h} is not covered by the device Functions; autograd with library "
+                          f"GEMMs / SDPA where a Function does not apply")
+            if self.cfg.graph_update and not self.episodic and not getattr(up, "graph", False):
+                fb.append("update: GameURM minibatch step runs eagerly (not captured in a hipGraph)")
+            if not getattr(pol, "mega", False):
+                fb.append(f"rollout: GameURM h={h} off the one-launch forward ({paths['urm_rollout']})")
+            if self.cfg.graph_update and self.cfg.fused_update and not getattr(inner, "supported", False):
+                fb.append("optimizer: the fused Muon kernel does not cover this GameURM; torch-op Newton-Schulz")
         return paths, fb
 
     # ------------------------------------------------------------------ rollout ---------------

@@ -443,3 +443,10 @@ def test_trainer_reports_kernel_fallbacks(dev, hidden, layers, want):
         assert tr.paths["rollout"] == "policy_rollout_kernel" and tr.paths["update"] == "FusedPPOUpdater"
     m = tr.train_step(0)
     assert math.isfinite(m["loss"])
+    # after the first update the labels are the updater's own decision (FusedPPOUpdater._alloc)
+    after = [x.split(":")[0] for x in tr.fallbacks]
+    if not want:
+        assert tr.paths["update_forward"] == "fused train / KL passes + fused backward" and after == []
+    else:
+        assert "predicted" not in tr.paths["update_forward"]
+        assert ("update" in after) == (layers != 2 or hidden == 256), tr.fallbacks

@@ -175,3 +175,24 @@ def test_urm_optimizer_groups_skip_gradless_init_hidden():
         m = agent.GameURM(agent.GameURMConfig(hidden_dim=32, num_heads=2, num_truncated_loops=trunc))
         ids = {id(p) for g in m.get_param_groups(1e-3, 1e-3) for p in g["params"]}
         assert (id(m.init_hidden) in ids) is want
+
+
+@pytest.mark.parametrize("ntl", [0, 1])
+def test_urm_param_groups_cover_every_parameter_once(ntl):
+    """GameURM.get_param_groups: Muon gets exactly the 2-D Linear weights (value head apart), AdamW
+    the conv kernels, norms and biases; init_hidden joins the AdamW group only when it can have a
+    gradient (num_truncated_loops == 0: the no-grad truncated loops are the only other user).  Every
+    trainable parameter is in exactly one group (the group layout an optimizer
+    checkpoint is keyed by)."""
+    import agent
+    m = agent.GameURM(agent.GameURMConfig(num_truncated_loops=ntl))
+    o2, o1, v2, v1 = m.get_param_groups(1e-4, 1e-3)
+    ids = [id(p) for g in (o2, o1, v2, v1) for p in g["params"]]
+    assert len(ids) == len(set(ids))
+    every = {id(p) for p in m.parameters()}
+    missing = every - set(ids)
+    assert missing == ({id(m.init_hidden)} if ntl else set())
+    assert all(p.ndim == 2 for p in o2["params"] + v2["params"])
+    assert all(p.ndim != 2 or p is m.init_hidden for p in o1["params"] + v1["params"])
+    assert (any(p is m.init_hidden for p in o1["params"])) == (ntl == 0)
+    assert {id(p) for p in v2["params"] + v1["params"]} == {id(p) for p in m.value_head.parameters()}
