@@ -50,38 +50,59 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(const uint4 *__restric
 __device__ const lut::Row12Table kRow12 __attribute__((aligned(16))) = lut::Row12Table();
 __device__ const lut::Line12Table kLine12 __attribute__((aligned(16))) = lut::Line12Table();
 
-// LDS layout of env_rollout_kernel: kRow12 at byte 0 (81 KiB), kLine12 right after it.  Lanes whose
-// board holds an exponent >= 12 still issue the (discarded) table reads with 4-bit-masked digits,
-// i.e. indices up to 15 * 1885 = 28 275: those may land in kLine12 (harmless) and the kLine12
-// reads need the region up to kLineBase + 2 * 28 276 bytes.
-constexpr uint32_t kLineBase = lut::kRowEntries * 4u;                        // 82 944
-// then the auto-reset boards and their statistics (kFresh) past the masked-read region
+// LDS layout of env_rollout_kernel: kLine12 at byte 0 (41 KiB, so a line's byte address 2 idx fits
+// in 16 bits and four of them come out of packed-u16 arithmetic), kRow12 right after it.  Lanes
+// whose board holds an exponent >= 12 still issue the (discarded) table reads with 4-bit-masked
+// digits, i.e. indices up to 15 * 1885 = 28 275: a kLine12 read may then land in kRow12 and a
+// kRow12 read in kFresh (harmless: both inside the allocation).
+constexpr uint32_t kRowLds = lut::kLineEntriesPadded * 2u;                   // 41 984
+// then the auto-reset boards and their statistics (kFresh)
 __device__ const lut::FreshTable kFresh __attribute__((aligned(16))) = lut::FreshTable();
 constexpr uint32_t kFreshBoardBase = 137u * 1024u;                          // 15 KiB of boards
 constexpr uint32_t kFreshStatBase = kFreshBoardBase + lut::kFreshEntries * 16u;  // 2 KiB of stats
 constexpr uint32_t kRolloutLdsWords = (kFreshStatBase + 2048u) / 4u;         // 157 696 B
-static_assert(kLineBase + 2u * 28276u <= kFreshBoardBase, "masked kLine12 reads stay below kFresh");
+static_assert(kRowLds + lut::kRowEntries * 4u <= kFreshBoardBase, "kRow12 below kFresh");
+static_assert(kRowLds + 4u * 28276u <= kRolloutLdsWords * 4u && 2u * 28276u <= kRowLds + lut::kRowEntries * 4u,
+              "masked table reads stay inside the allocation");
+static_assert(2u * (lut::kRowEntries - 1u) < 65536u, "kLine12 byte addresses fit 16 bits");
 
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
 
 // LDS byte address of the kRow12 entry of a LEFT-frame row dword (byte j = cell j):
-// 4 (c0 + 12 c1 + 144 c2 + 1728 c3) as two packed-u16 dot products.  Bytes are masked to 4 bits
-// so any row (even one holding exponents >= 12, whose lane takes the compute path) addresses
-// inside the 128 KiB LDS allocation (< 15 * 1885 * 4 bytes).
+// kRowLds + 4 (c0 + 12 c1 + 144 c2 + 1728 c3) as two packed-u16 dot products.  Bytes are masked
+// to 4 bits so any row (even one holding exponents >= 12, whose lane takes the compute path)
+// addresses inside the LDS allocation (< kRowLds + 15 * 1885 * 4 bytes).
 __device__ __forceinline__ uint32_t row12_addr(uint32_t x) {
     const u16x2 k02 = {4, 576}, k13 = {48, 6912};
     return __builtin_amdgcn_udot2(as_u16x2((x >> 8) & 0x000F000Fu), k13,
-                                  __builtin_amdgcn_udot2(as_u16x2(x & 0x000F000Fu), k02, 0u, false), false);
+                                  __builtin_amdgcn_udot2(as_u16x2(x & 0x000F000Fu), k02, kRowLds, false), false);
 }
 __device__ __forceinline__ uint32_t lds_word(const uint32_t *tab, uint32_t addr) {
     return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(tab) + addr);
 }
-// LDS byte address of the kLine12 entry of a line dword (byte j = cell j): kLineBase + 2 idx
-__device__ __forceinline__ uint32_t line12_addr(uint32_t x) {
+// LDS byte addresses (2 idx) of the kLine12 entries of a board's four rows (a row read left to
+// right) and four columns (top to bottom), from the rows' 4-bit digit pairs: A_i = cells (i, 0) and
+// (i, 2), B_i = cells (i, 1) and (i, 3) as u16 halves.  Rows: two packed-u16 dot products each.
+// Columns: column pairs (0, 2) and (1, 3) at once as packed-u16 multiply-adds over the rows,
+// 2 (cell(0, j) + 12 cell(1, j) + 144 cell(2, j) + 1728 cell(3, j)) < 2^16 per half -- no transpose.
+__device__ __forceinline__ void line12_addrs(const uint4 &b, uint32_t (&ra)[4], uint32_t (&ca)[4]) {
     const u16x2 k02 = {2, 288}, k13 = {24, 3456};
-    return __builtin_amdgcn_udot2(as_u16x2((x >> 8) & 0x000F000Fu), k13,
-                                  __builtin_amdgcn_udot2(as_u16x2(x & 0x000F000Fu), k02, kLineBase, false), false);
+    const uint32_t w[4] = {b.x, b.y, b.z, b.w};
+    u16x2 A[4], B[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        A[i] = as_u16x2(w[i] & 0x000F000Fu);
+        B[i] = as_u16x2((w[i] >> 8) & 0x000F000Fu);
+        ra[i] = __builtin_amdgcn_udot2(B[i], k13, __builtin_amdgcn_udot2(A[i], k02, 0u, false), false);
+    }
+    const u16x2 c02 = A[0] * (u16x2){2, 2} + A[1] * (u16x2){24, 24} + A[2] * (u16x2){288, 288} + A[3] * (u16x2){3456, 3456};
+    const u16x2 c13 = B[0] * (u16x2){2, 2} + B[1] * (u16x2){24, 24} + B[2] * (u16x2){288, 288} + B[3] * (u16x2){3456, 3456};
+    const uint32_t p02 = __builtin_bit_cast(uint32_t, c02), p13 = __builtin_bit_cast(uint32_t, c13);
+    ca[0] = p02 & 0xFFFFu;
+    ca[1] = p13 & 0xFFFFu;
+    ca[2] = p02 >> 16;
+    ca[3] = p13 >> 16;
 }
 __device__ __forceinline__ uint32_t lds_half(const uint32_t *tab, uint32_t addr) {
     return *reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(tab) + addr);
@@ -184,7 +205,7 @@ __device__ __forceinline__ uint32_t fresh_stats(uint32_t p1, uint32_t v1, uint32
     return legal;
 }
 
-// Copy the 81 KiB row table into LDS by LDS-DMA: each wave instruction moves 1 KiB (16 B per lane)
+// Copy the tables (kLine12, kRow12, kFresh) into LDS by LDS-DMA: each wave instruction moves 1 KiB (16 B per lane)
 // straight from global memory into LDS with no VGPR staging, and every piece of the wave is in
 // flight before the single wait (one L2/MALL round trip per launch instead of one per batch).
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -196,8 +217,8 @@ __device__ __forceinline__ void stage_row_table(uint32_t *s_row) {
     static_assert(lut::kRowEntries * 4u % 1024u == 0u && lut::kLineEntriesPadded * 2u % 1024u == 0u &&
                   lut::kFreshEntries * 16u % 1024u == 0u, "whole 1 KiB pieces");
     constexpr int kAll = kPieces + kLinePieces + kFreshPieces + 2;
-    const char *src = reinterpret_cast<const char *>(kRow12.v);
-    const char *src2 = reinterpret_cast<const char *>(kLine12.v);
+    const char *src = reinterpret_cast<const char *>(kLine12.v);  // pieces 0 .. kLinePieces - 1
+    const char *src2 = reinterpret_cast<const char *>(kRow12.v);
     const char *src3 = reinterpret_cast<const char *>(kFresh.b);
     const char *src4 = reinterpret_cast<const char *>(kFresh.st);
     char *dst = reinterpret_cast<char *>(s_row);
@@ -205,8 +226,8 @@ __device__ __forceinline__ void stage_row_table(uint32_t *s_row) {
     for (int c = wave; c < kAll; c += nw) {
         const char *g;
         uint32_t d;
-        if (c < kPieces + kLinePieces) {
-            g = c < kPieces ? src + 1024 * c : src2 + 1024 * (c - kPieces);
+        if (c < kPieces + kLinePieces) {  // kLine12 at 0, then kRow12 at kRowLds (= kLinePieces KiB)
+            g = c < kLinePieces ? src + 1024 * c : src2 + 1024 * (c - kLinePieces);
             d = 1024u * (uint32_t)c;
         } else if (c < kPieces + kLinePieces + kFreshPieces) {
             const int k = c - kPieces - kLinePieces;
@@ -261,6 +282,7 @@ struct TrajRows {  // row t of each time-major trajectory array
     uint8_t *f;
 };
 
+
 // One env step of the synthetic random-legal policy (oracle or_step_word + auto-reset).  kOdd = the
 // second step of the pair.  One 32-bit word u per step: action k = floor(u * nlegal / 2^32); the
 // low word r of that product (uniform given k) picks the spawn cell and value (spawn_chain).
@@ -302,11 +324,10 @@ __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__r
     const uint32_t v = spawn_chain(moved, Zm, (uint32_t)empt_a, r, sp);
     s.b = moved;  // the next board (after the spawn)
     // its legal mask and pair counts from kLine12: four rows and four columns
-    const uint4 tc = transpose(moved);
-    uint32_t f0 = lds_half(tab, line12_addr(moved.x)), f1 = lds_half(tab, line12_addr(moved.y));
-    uint32_t f2 = lds_half(tab, line12_addr(moved.z)), f3 = lds_half(tab, line12_addr(moved.w));
-    uint32_t g0 = lds_half(tab, line12_addr(tc.x)), g1 = lds_half(tab, line12_addr(tc.y));
-    uint32_t g2 = lds_half(tab, line12_addr(tc.z)), g3 = lds_half(tab, line12_addr(tc.w));
+    uint32_t ra[4], ca[4];
+    line12_addrs(moved, ra, ca);
+    uint32_t f0 = lds_half(tab, ra[0]), f1 = lds_half(tab, ra[1]), f2 = lds_half(tab, ra[2]), f3 = lds_half(tab, ra[3]);
+    uint32_t g0 = lds_half(tab, ca[0]), g1 = lds_half(tab, ca[1]), g2 = lds_half(tab, ca[2]), g3 = lds_half(tab, ca[3]);
     // the spawned tile's pairs (the counts before the spawn are the next board's minus these) and
     // the next board's maximum / first-argmax cell
     const MonoStats dsp = mono_add_tile(MonoStats{0, 0, 0, 0, Ma, pos_a}, moved, sp, v);

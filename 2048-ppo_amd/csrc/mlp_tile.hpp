@@ -23,7 +23,6 @@ namespace {  // internal linkage per translation unit (the __constant__ recipe t
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kMaxLayers = 3;  // stem + 2 residual blocks (GameMLP num_layers = 2)
 
@@ -202,6 +201,49 @@ __device__ __forceinline__ void ln_epilogue_train(f32x4_t (&acc)[NT], uint2 (&ac
             float k[4];
             if ((n & 1) == 0) dpair = ppo::drop_draw4(d, row, (uint32_t)(f0 >> 2));
             ppo::drop_mult_bits(d, ppo::drop_half(dpair, (uint32_t)(f0 >> 2)), k);
+            y0 = y0 * R::f32x2{k[0], k[1]};
+            y1 = y1 * R::f32x2{k[2], k[3]};
+        }
+        if (RES) {
+            y0 = R::f32x2{bf_lo(act[n].x), bf_hi(act[n].x)} + y0;
+            y1 = R::f32x2{bf_lo(act[n].y), bf_hi(act[n].y)} + y1;
+        }
+        act[n] = valid(n) ? make_uint2(pack_bf2(y0.x, y0.y), pack_bf2(y1.x, y1.y)) : make_uint2(0u, 0u);
+    }
+}
+
+// ln_epilogue_train with the keep masks drawn ahead (ppo::drop_keep8 per feature-tile pair, bits
+// 4 n .. 4 n + 3 of kb = the 4 features of tile n): the same multipliers k (0 or 1 / (1 - p)), so
+// bitwise ln_epilogue_train.
+template <int NT, int h, bool RES, bool DROP>
+__device__ __forceinline__ void ln_epilogue_train_kb(f32x4_t (&acc)[NT], uint2 (&act)[NT], const float *sgam,
+                                                     const float *sbet, int g, float inv_n, float scale,
+                                                     const uint32_t (&kb)[2], uint16_t *gout, uint32_t goff,
+                                                     float &mean, float &rstd) {
+    namespace R = lnrow;
+    R::f32x2 v[NT][2];
+    {
+        uint2 gb[NT];
+        R::round_g<NT>(acc, v, gb);
+        if (gout) {
+            char *p = reinterpret_cast<char *>(gout) + (goff + 8u * (uint32_t)g);
+#pragma unroll
+            for (int n = 0; n < NT; n++)
+                if (16 * n + 4 * g < h) *reinterpret_cast<uint2 *>(p + 32 * n) = gb[n];
+        }
+    }
+    auto valid = [&](int n) { return 16 * n + 4 * g < h; };
+    R::stats<NT>(v, valid, inv_n, mean, rstd);
+#pragma unroll
+    for (int n = 0; n < NT; n++) {
+        const int f0 = 16 * n + 4 * g;
+        const float4 ga = *reinterpret_cast<const float4 *>(sgam + f0);
+        const float4 be = *reinterpret_cast<const float4 *>(sbet + f0);
+        R::f32x2 y0 = R::affine_relu(v[n][0], rstd, R::f32x2{ga.x, ga.y}, R::f32x2{be.x, be.y});
+        R::f32x2 y1 = R::affine_relu(v[n][1], rstd, R::f32x2{ga.z, ga.w}, R::f32x2{be.z, be.w});
+        if (DROP) {
+            float k[4];
+            ppo::keep_mult(kb, n, scale, k);
             y0 = y0 * R::f32x2{k[0], k[1]};
             y1 = y1 * R::f32x2{k[2], k[3]};
         }

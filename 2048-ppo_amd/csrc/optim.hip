@@ -115,6 +115,10 @@ constexpr int kMuonThreads = 1024;       // 16 waves (4 per SIMD: LDS latency hi
 constexpr int kMuonWaves = kMuonThreads / 64;
 constexpr int kBI = 4, kBJ = 4;          // generic schedule: 4 x 4 waves of 4 x 4 16x16 tiles = 256 x 256
 constexpr int kMuonMaxMats = 16;  // GameMLP: 5, GameURM (2 layers): 11
+static_assert(sizeof(g2048_muon_cfg) == 48 && offsetof(g2048_muon_cfg, workspace) == 40,
+              "g2048_muon_cfg layout (tests/test_abi.py)");
+constexpr int kMuonMaxJobs = 64;  // blocks of the Muon matrices (multi-CU squares: nparts each)
+constexpr int kMuonSyncBytes = kMuonMaxMats * 64;  // one 64-byte line per matrix counter
 constexpr int kMuonLds = 160 * 1024 - 256;  // minus the static red[] / s_norm
 
 struct MuonMat {
@@ -138,6 +142,13 @@ struct MuonArgs {
     AdamArgs adam;               // adam.count > 0: blocks count .. count + nadam - 1 run AdamW
     int nadam;
     int generic_ns;              // 1: square matrices on the generic schedule too (A/B timing, tests)
+    // blocks 0 .. njobs - 1: Muon parts; a square matrix of the multi-CU path is split over nparts
+    // blocks (row blocks of its Newton-Schulz products, one exchange of X per iteration)
+    int njobs;
+    uint8_t job_mat[kMuonMaxJobs], job_part[kMuonMaxJobs], job_nparts[kMuonMaxJobs];
+    uint32_t *sync;              // per matrix: the exchange counter (zeroed before every launch)
+    char *xg;                    // per matrix: two N x P-byte bf16 exchange images (X of even / odd iterations)
+    int64_t xg_stride;           // bytes per matrix
 };
 
 // LDS images are row-major bf16 with the K dimension zero-padded to a multiple of 8 (pitch =
@@ -272,7 +283,9 @@ __device__ __forceinline__ float momentum4(const float4 &g4, const float4 &b4, f
 // compiler overlap the iterations' loads with the previous stores.
 __device__ __forceinline__ float muon_prologue(const float *__restrict__ grad, float *__restrict__ mom, char *sX,
                                                int px, int R, int C, bool tr, float coef, float mu, bool nesterov,
-                                               int tid) {
+                                               int tid, int mr0 = 0, int mr1 = 1 << 30) {
+    // (rows [mr0, mr1) of the momentum are written back: a multi-CU part computes the whole image
+    // -- every part the same values -- and owns the momentum rows of its row block)
     float ss = 0.0f;
     if (C & 3) {  // a row length that is not a whole number of float4 (GameURM's [64, 3] stem): per element
         for (int e = tid; e < R * C; e += kMuonThreads) {
@@ -311,14 +324,15 @@ __device__ __forceinline__ float muon_prologue(const float *__restrict__ grad, f
             } else {
                 *reinterpret_cast<uint2 *>(sX + i * px + 2 * j0) = make_uint2(pack_bf2(ub[0], ub[1]), pack_bf2(ub[2], ub[3]));
             }
-            reinterpret_cast<float4 *>(mom)[e4] = make_float4(bv[0], bv[1], bv[2], bv[3]);
+            if (i >= mr0 && i < mr1) reinterpret_cast<float4 *>(mom)[e4] = make_float4(bv[0], bv[1], bv[2], bv[3]);
         }
     }
     return ss;
 }
 
 __device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_t *__restrict__ pbf, const char *sX,
-                                              int px, int R, int C, bool tr, float decay, float step, int tid) {
+                                              int px, int R, int C, bool tr, float decay, float step, int tid,
+                                              int pr0 = 0, int pr1 = 1 << 30) {  // parameter rows [pr0, pr1)
     if (C & 3) {  // per element (see muon_prologue)
         for (int e = tid; e < R * C; e += kMuonThreads) {
             const int i = e / C, j = e - i * C;
@@ -329,9 +343,10 @@ __device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_
         }
         return;
     }
-    const int n4 = (R * C) >> 2;
+    const int e0 = tr ? 0 : (pr0 < R ? pr0 : R) * C / 4;  // (the multi-CU parts are square: tr false)
+    const int n4 = tr ? (R * C) >> 2 : (pr1 < R ? pr1 : R) * C / 4;
     constexpr int kB = 8;
-    for (int base = tid; base < n4; base += kB * kMuonThreads) {
+    for (int base = e0 + tid; base < n4; base += kB * kMuonThreads) {
         float4 p4[kB];
 #pragma unroll
         for (int u = 0; u < kB; u++) {
@@ -681,6 +696,228 @@ __device__ __forceinline__ void ns_square(char *sX, char *sG, const MuonArgs &ar
     }
 }
 
+// ------------------------------------------------------------------ multi-CU Newton-Schulz ----
+// A square h x h matrix (h = 196 / 192) on `np` blocks (CUs).  Every block holds the whole X and
+// computes G = X X^T whole (the symmetric schedule above: replicated, so no exchange of G); each
+// block then computes only its row block R of U = b G + c G G and of X' = a X + U X (tile rows
+// [t0, t1)), and the blocks exchange their rows of X' once per iteration through a global image
+// (agent-scope hand-off, cdna_hip_programming.md Guideline 16: write-through 8-byte stores, one
+// counter add per block after a drain + barrier, a relaxed poll, one acquire, plain loads).  Per
+// output tile the MFMA sequence (init from the scaled old value, k-steps in order) is the
+// single-block path's, with the operand roles of the X product swapped (A = U rows, B = X by the
+// transposing read instead of A = X^T, B^T = U rows): the same products summed in the same order.
+typedef __attribute__((address_space(1))) uint32_t gu32_t;
+typedef __attribute__((address_space(1))) uint64_t gu64_t;
+
+// G = X X^T alone, on the square schedule (no kept tiles: the row-block U product re-reads G)
+template <int N, int W>
+__device__ __forceinline__ void ns_g_w(char *sX, char *sG, int lane) {
+    uint2 unused[ns_tiles<N, true>(W)];
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    ns_product_w<N, true, true, 0, W>(sX, sX, sG, 1.0f, 0.0f, unused, l);
+}
+
+template <int N>
+__device__ __forceinline__ void ns_square_g(char *sX, char *sG, int wave, int lane) {
+    switch (wave) {  // wave-uniform
+    case 0: ns_g_w<N, 0>(sX, sG, lane); break;
+    case 1: ns_g_w<N, 1>(sX, sG, lane); break;
+    case 2: ns_g_w<N, 2>(sX, sG, lane); break;
+    case 3: ns_g_w<N, 3>(sX, sG, lane); break;
+    case 4: ns_g_w<N, 4>(sX, sG, lane); break;
+    case 5: ns_g_w<N, 5>(sX, sG, lane); break;
+    case 6: ns_g_w<N, 6>(sX, sG, lane); break;
+    case 7: ns_g_w<N, 7>(sX, sG, lane); break;
+    case 8: ns_g_w<N, 8>(sX, sG, lane); break;
+    case 9: ns_g_w<N, 9>(sX, sG, lane); break;
+    case 10: ns_g_w<N, 10>(sX, sG, lane); break;
+    case 11: ns_g_w<N, 11>(sX, sG, lane); break;
+    case 12: ns_g_w<N, 12>(sX, sG, lane); break;
+    case 13: ns_g_w<N, 13>(sX, sG, lane); break;
+    case 14: ns_g_w<N, 14>(sX, sG, lane); break;
+    default: ns_g_w<N, 15>(sX, sG, lane); break;
+    }
+}
+
+template <int N>
+struct McShape {
+    static constexpr int NT = (N + 15) / 16, KPAD = (N + 7) & ~7, KS = (KPAD + 31) / 32;
+    static constexpr int P = muon_pitch(N, N);
+};
+
+// The old value of output tile (ti, tj) in the accumulator layout (lane (g, c): rows 16 ti + 4 g ..
+// + 3 of column 16 tj + c), scaled: from a SYMMETRIC image by one 8-byte read of the transposed
+// position, else by a row read + the quad transpose (a 4 x 4 transpose is its own inverse).
+template <int N, bool SYM>
+__device__ __forceinline__ f32x4_t mc_init(const char *img, int ti, int tj, float ratio, int g, int c) {
+    constexpr int P = McShape<N>::P;
+    uint32_t w0, w1;
+    if (SYM) {
+        const int row = min(16 * tj + c, N - 1), col = min(16 * ti + 4 * g, N - 4);
+        const uint2 w = *reinterpret_cast<const uint2 *>(img + row * P + col * 2);
+        w0 = w.x;
+        w1 = w.y;
+    } else {
+        const int k = c & 3, m = c >> 2;
+        const int row = min(16 * ti + 4 * g + k, N - 1), col = 16 * tj + 4 * m;  // col < 16 NT: inside the pitch
+        const uint2 w = *reinterpret_cast<const uint2 *>(img + row * P + col * 2);
+        const uint2 t = quad_transpose_bf16(w.x, w.y, k);
+        w0 = t.x;
+        w1 = t.y;
+    }
+    return f32x4_t{ratio * bf2f(w0 & 0xFFFFu), ratio * bf2f(w0 >> 16), ratio * bf2f(w1 & 0xFFFFu), ratio * bf2f(w1 >> 16)};
+}
+
+// acc[x] (+)= sum_ks A[16 (t0 + x) + ..][k] B[k][16 tj + ..] for the RB tile rows of the block.
+// A: rows of image A (row reads; rows past N clamped, k past KPAD cut to zero: they read the next
+// row).  B: BT_ROWS -- B^T rows = rows 16 tj + c of image B (row reads; B symmetric), else B = image
+// B read by columns (the transposing read; rows past N read the image behind it: finite, times a
+// zero A fragment).
+template <int N, int RB, bool BT_ROWS>
+__device__ __forceinline__ void mc_mfma(const char *A, const char *B, int t0, int tj, int lane, f32x4_t (&acc)[RB]) {
+    using S = McShape<N>;
+    constexpr int P = S::P;
+    const int g = lane >> 4, c = lane & 15, q = (lane >> 2) & 3, p = lane & 3;
+    const char *pa[RB];
+#pragma unroll
+    for (int x = 0; x < RB; x++) pa[x] = A + min(16 * (t0 + x) + c, N - 1) * P + 16 * g;
+    const char *pb = BT_ROWS ? B + min(16 * tj + c, N - 1) * P + 16 * g : B + (8 * g + q) * P + 8 * p + 32 * tj;
+#pragma unroll
+    for (int ks = 0; ks < S::KS; ks++) {
+        const bool kin = 32 * ks + 8 * g < S::KPAD;
+        bf16x8_t fb;
+        if (BT_ROWS) {
+            uint4 v = *reinterpret_cast<const uint4 *>(pb + 64 * ks);
+            if (ks == S::KS - 1 && 32 * S::KS > S::KPAD) v = kin ? v : make_uint4(0u, 0u, 0u, 0u);
+            fb = __builtin_bit_cast(bf16x8_t, v);
+        } else {
+            const char *b1 = pb + 32 * ks * P;
+            const s16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)b1);
+            const s16x4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(b1 + 4 * P));
+            fb = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(t1, t2, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+#pragma unroll
+        for (int x = 0; x < RB; x++) {
+            uint4 v = *reinterpret_cast<const uint4 *>(pa[x] + 64 * ks);
+            if (!BT_ROWS && ks == S::KS - 1 && 32 * S::KS > S::KPAD) v = kin ? v : make_uint4(0u, 0u, 0u, 0u);
+            acc[x] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, v), fb, acc[x], 0, 0, 0);
+        }
+    }
+}
+
+// lane (g, c) of tile (ti, tj): alpha * acc as rows 16 ti + 4 g + k, columns 16 tj + 4 m .. + 3
+// (c = 4 m + k) -- one 8-byte row segment per lane; columns past N become zero (the image padding)
+template <int N>
+__device__ __forceinline__ uint2 mc_row_segment(const f32x4_t &v, float alpha, int tj, int c) {
+    const uint32_t w0 = pack_bf2(alpha * v[0], alpha * v[1]), w1 = pack_bf2(alpha * v[2], alpha * v[3]);
+    const uint2 t = quad_transpose_bf16(w0, w1, c & 3);
+    return 16 * tj + 4 * (c >> 2) < N ? t : make_uint2(0u, 0u);
+}
+
+// One row-block product of this block: tiles (t0 .. t0 + RB - 1, tj = wave) for waves < NT.
+// SYM_B: U = c (b/c G + G G) (A = G rows, B^T = G rows, old value G); else X' = a X + U X (A = U
+// rows of sG, B = X columns of sX, old value X).  The result stays in acc (stored by the caller).
+template <int N, int RB, bool U_PRODUCT>
+__device__ __forceinline__ void mc_product(const char *sX, const char *sG, int t0, int wave, int lane, float ratio,
+                                           f32x4_t (&acc)[RB]) {
+    const int g = lane >> 4, c = lane & 15;
+    const int tj = wave;
+#pragma unroll
+    for (int x = 0; x < RB; x++) acc[x] = mc_init<N, U_PRODUCT>(U_PRODUCT ? sG : sX, t0 + x, tj, ratio, g, c);
+    if (U_PRODUCT) mc_mfma<N, RB, true>(sG, sG, t0, tj, lane, acc);
+    else mc_mfma<N, RB, false>(sG, sX, t0, tj, lane, acc);
+}
+
+// bounded relaxed poll of a counter (one wave); false after ~0.2 s (a lost block: results are
+// garbage, the error word is set, but no wave spins forever)
+__device__ __forceinline__ bool mc_wait(gu32_t *ctr, uint32_t target, gu32_t *err) {
+    for (uint32_t spins = 0;; spins++) {
+        if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+        if (spins > (1u << 21)) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+template <int N, int RB>
+__device__ __forceinline__ void ns_square_mc_rb(char *sX, char *sG, const MuonArgs &args, int mat, int part, int np,
+                                                int wave, int lane) {
+    using S = McShape<N>;
+    constexpr int P = S::P;
+    const int tid = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int t0 = part * S::NT / np;  // tile rows t0 .. t0 + RB - 1 (RB = (part + 1) NT / np - t0)
+    gu32_t *ctr = (gu32_t *)(args.sync + 16 * mat);
+    gu32_t *err = (gu32_t *)(args.sync + 16 * mat + 1);
+    char *xg = args.xg + mat * args.xg_stride;
+    for (int it = 0; it < args.steps; it++) {
+        // G = X X^T, whole (the single-block symmetric schedule; two barriers inside)
+        ns_square_g<N>(sX, sG, wave, lane);
+        f32x4_t acc[RB];
+        // U rows of this block, in place over G's rows once every wave is done reading G
+        if (wave < S::NT) mc_product<N, RB, true>(sX, sG, t0, wave, lane, args.b / args.c, acc);
+        __syncthreads();
+        if (wave < S::NT)
+#pragma unroll
+            for (int x = 0; x < RB; x++) {
+                const int row = 16 * (t0 + x) + 4 * g + (c & 3);
+                const uint2 v = mc_row_segment<N>(acc[x], args.c, wave, c);
+                if (row < N) *reinterpret_cast<uint2 *>(sG + row * P + (16 * wave + 4 * (c >> 2)) * 2) = v;
+            }
+        __syncthreads();
+        // X' rows of this block
+        if (wave < S::NT) mc_product<N, RB, false>(sX, sG, t0, wave, lane, args.a, acc);
+        __syncthreads();  // every read of X is done
+        const bool last = it == args.steps - 1;
+        char *img = last ? sX : xg + (it & 1) * N * P;
+        if (wave < S::NT)
+#pragma unroll
+            for (int x = 0; x < RB; x++) {
+                const int row = 16 * (t0 + x) + 4 * g + (c & 3);
+                const uint2 v = mc_row_segment<N>(acc[x], 1.0f, wave, c);
+                if (row < N) {
+                    char *dst = img + row * P + (16 * wave + 4 * (c >> 2)) * 2;
+                    if (last) {
+                        *reinterpret_cast<uint2 *>(dst) = v;
+                    } else {  // write-through: no release fence needed before the counter add
+                        const uint64_t w = (uint64_t)v.x | ((uint64_t)v.y << 32);
+                        __hip_atomic_store((gu64_t *)dst, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+            }
+        if (last) {
+            __syncthreads();
+            break;
+        }
+        // hand-off: every storing wave drains, the barrier, one lane adds; one wave polls, acquires
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (wave == 0) {
+            mc_wait(ctr, (uint32_t)(np * (it + 1)), err);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        // the whole X' (every block's rows, padding columns zero) into the LDS image
+        const char *src = xg + (it & 1) * N * P;
+        for (int o = tid * 16; o < N * P; o += kMuonThreads * 16)
+            *reinterpret_cast<uint4 *>(sX + o) = *reinterpret_cast<const uint4 *>(src + o);
+        __syncthreads();
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void ns_square_mc(char *sX, char *sG, const MuonArgs &args, int mat, int part, int np,
+                                             int wave, int lane) {
+    constexpr int NT = McShape<N>::NT;
+    const int rb = (part + 1) * NT / np - part * NT / np;  // block-uniform; the host picks np >= NT / 2
+    if (rb == 1) ns_square_mc_rb<N, 1>(sX, sG, args, mat, part, np, wave, lane);
+    else ns_square_mc_rb<N, 2>(sX, sG, args, mat, part, np, wave, lane);
+}
+
 // The AdamW update of the 1-D groups by block b of nb (clip coefficient from the partials).
 __device__ __forceinline__ void adam_blocks(const MuonArgs &args, int b, int nb) {
     float cf = 1.0f;
@@ -726,11 +963,12 @@ __device__ __forceinline__ float block_clip_coef(const MuonArgs &args, int tid, 
 
 __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    if ((int)blockIdx.x >= args.count) {  // the 1-D parameters' AdamW, in the same launch
-        adam_blocks(args, (int)blockIdx.x - args.count, args.nadam);
+    if ((int)blockIdx.x >= args.njobs) {  // the 1-D parameters' AdamW, in the same launch
+        adam_blocks(args, (int)blockIdx.x - args.njobs, args.nadam);
         return;
     }
-    const MuonMat mt = args.m[blockIdx.x];
+    const int mat = args.job_mat[blockIdx.x], part = args.job_part[blockIdx.x], np = args.job_nparts[blockIdx.x];
+    const MuonMat mt = args.m[mat];
     const int R = mt.rows, C = mt.cols;
     const bool tr = R > C;  // iterate on the wide orientation (r <= c), like torch
     const int r = tr ? C : R, c = tr ? R : C;
@@ -750,7 +988,10 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     __syncthreads();
 
     const float coef = block_clip_coef(args, tid, blockIdx.x == 0);
-    float ss = muon_prologue(mt.grad, mt.mom, sX, px, R, C, tr, coef, args.momentum, args.nesterov != 0, tid);
+    // a multi-CU part (square: tr false) owns the momentum / parameter rows of its tile rows
+    const int NT = (r + 15) >> 4;
+    const int own0 = np > 1 ? 16 * (part * NT / np) : 0, own1 = np > 1 ? 16 * ((part + 1) * NT / np) : R;
+    float ss = muon_prologue(mt.grad, mt.mom, sX, px, R, C, tr, coef, args.momentum, args.nesterov != 0, tid, own0, own1);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
     if (lane == 0) red[wave] = ss;
@@ -777,7 +1018,10 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     //   2: X^T = a X^T + X^T U            (A = X^T by the transposing read, B^T = U rows)
     // Every product stores its transpose (= G, U, and X itself for phase 2).
     const int kind = r == c && !args.generic_ns ? ns_square_kind(r) : 0;
-    if (kind) {  // the square fast path (row pitch muon_pitch(n, n))
+    if (np > 1) {  // the square matrix over np blocks (the host only splits h = 196 / 192)
+        if (r == 196) ns_square_mc<196>(sX, sG, args, mat, part, np, wave, lane);
+        else ns_square_mc<192>(sX, sG, args, mat, part, np, wave, lane);
+    } else if (kind) {  // the square fast path (row pitch muon_pitch(n, n))
         switch (kind) {
         case 1: ns_square<196>(sX, sG, args, wave, lane); break;
         case 2: ns_square<192>(sX, sG, args, wave, lane); break;
@@ -809,7 +1053,7 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     // decoupled weight decay + the match_rms_adamw-scaled update, and the bf16 weight copy
     const float lr = args.lr[mt.lr_index];
     const float step = lr * (0.2f * sqrtf((float)(R > C ? R : C)));
-    muon_epilogue(mt.param, mt.pbf, sX, px, R, C, tr, 1.0f - lr * args.wd, step, tid);
+    muon_epilogue(mt.param, mt.pbf, sX, px, R, C, tr, 1.0f - lr * args.wd, step, tid, own0, own1);
 }
 
 __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
@@ -847,6 +1091,10 @@ int g2048_grad_clip(g2048_stream_t stream, const float *grad, int64_t n, float m
     hipLaunchKernelGGL(grad_sumsq_kernel, dim3(kNormBlocks), dim3(256), 0, s, grad, n, partials);
     hipLaunchKernelGGL(grad_norm_kernel, dim3(1), dim3(kNormBlocks), 0, s, partials, max_norm, norm_out, coef_out);
     return status();
+}
+
+size_t g2048_muon_workspace_bytes(void) {
+    return (size_t)kMuonSyncBytes + (size_t)kMuonMaxMats * 2 * max(196 * muon_pitch(196, 196), 192 * muon_pitch(192, 192));
 }
 
 int g2048_muon_supported(int32_t rows, int32_t cols) {
@@ -935,6 +1183,31 @@ static int muon_launch(g2048_stream_t stream, const g2048_muon_matrix *mats, int
     a.norm_out = norm_out;
     a.coef_out = coef_out;
     a.generic_ns = getenv("G2048_MUON_GENERIC") ? 1 : 0;
+    // blocks: one per matrix, or cfg->parts per h = 196 / 192 square matrix with a workspace
+    const int parts = cfg->workspace && !a.generic_ns && !getenv("G2048_MUON_ONE_CU") ? cfg->parts : 1;
+    if (parts > 1 && (parts < 7 || parts > 12)) return G2048_EINVAL;  // one or two tile rows per block
+    int nj = 0;
+    for (int i = 0; i < count; i++) {
+        const g2048_muon_matrix &m = mats[i];
+        const bool split = parts > 1 && m.rows == m.cols && (m.rows == 196 || m.rows == 192);
+        const int np = split ? parts : 1;
+        if (nj + np > kMuonMaxJobs) return G2048_EINVAL;
+        for (int p = 0; p < np; p++) {
+            a.job_mat[nj] = (uint8_t)i;
+            a.job_part[nj] = (uint8_t)p;
+            a.job_nparts[nj] = (uint8_t)np;
+            nj++;
+        }
+    }
+    a.njobs = nj;
+    if (parts > 1) {
+        char *ws = static_cast<char *>(cfg->workspace);
+        a.sync = reinterpret_cast<uint32_t *>(ws);
+        a.xg = ws + kMuonSyncBytes;
+        a.xg_stride = 2 * (int64_t)max(196 * muon_pitch(196, 196), 192 * muon_pitch(192, 192));
+        const hipError_t e = hipMemsetAsync(ws, 0, kMuonSyncBytes, (hipStream_t)stream);  // the counters, every call
+        if (e != hipSuccess) return (int)e;
+    }
     if (adam) {  // AdamW blocks: ~2 elements per thread, at most 8 blocks
         a.adam = *adam;
         int64_t nmax = 0;
@@ -942,7 +1215,7 @@ static int muon_launch(g2048_stream_t stream, const g2048_muon_matrix *mats, int
         const int64_t nb = (nmax + 2 * kMuonThreads - 1) / (2 * kMuonThreads);
         a.nadam = (int)(nb < 1 ? 1 : (nb > 8 ? 8 : nb));
     }
-    hipLaunchKernelGGL(muon_kernel, dim3(count + a.nadam), dim3(kMuonThreads), lds, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(muon_kernel, dim3(a.njobs + a.nadam), dim3(kMuonThreads), lds, (hipStream_t)stream, a);
     return status();
 }
 

@@ -55,6 +55,31 @@ __device__ __forceinline__ void drop_mult_bits(const Drop &d, uint2 w, float k[4
     k[3] = (w.y >> 16) >= d.thr ? d.scale : 0.0f;
 }
 
+// The same draw as 8 keep bits: bits 0-3 = columns 4 cg .. + 3 (cg & 4 == 0: the x, y words, as
+// drop_mult_bits on drop_half), bits 4-7 = columns of cg ^ 4 (z, w) -- so a kernel can draw a row's
+// masks ahead (between its MFMAs) and hold them in a register instead of 4 Philox words.
+__device__ __forceinline__ uint32_t drop_keep8(const Drop &d, uint32_t row, uint32_t cg) {
+    const uint4 r = drop_draw4(d, row, cg);
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+    uint32_t b = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        b |= ((w[j] & 0xFFFFu) >= d.thr ? 1u : 0u) << (2 * j);
+        b |= ((w[j] >> 16) >= d.thr ? 1u : 0u) << (2 * j + 1);
+    }
+    return b;
+}
+
+// The multipliers (0 or scale) of feature tile n from keep bits 4 n .. 4 n + 3 of kb[0] | kb[1] << 32:
+// a sign-extended one-bit field masks the bits of `scale` (two VALU per feature).
+__device__ __forceinline__ void keep_mult(const uint32_t (&kb)[2], int n, float scale, float k[4]) {
+    const uint32_t w = kb[n >> 3];
+    const int s = 4 * (n & 7);
+    const int sc = __float_as_int(scale);
+#pragma unroll
+    for (int j = 0; j < 4; j++) k[j] = __int_as_float(((int)(w << (31 - s - j)) >> 31) & sc);
+}
+
 // keep multipliers (0 or 1/(1-p)) of columns 4cg .. 4cg+3 of `row`
 __device__ __forceinline__ void drop_mult(const Drop &d, uint32_t row, uint32_t cg, float k[4]) {
     drop_mult_bits(d, drop_draw(d, row, cg), k);

@@ -46,9 +46,30 @@ static_assert(sizeof(g2048_mlp_pass_args) == 408 && offsetof(g2048_mlp_pass_args
 
 namespace {
 
-constexpr int kFpThreads = 256;  // 4 waves x 64 rows per block iteration; one block per CU (LDS)
+#ifndef FP_WAVES
+#define FP_WAVES 8
+#endif
+#ifndef FP_KSB
+#define FP_KSB 1
+#endif
+#ifndef FP_LUNROLL
+#define FP_LUNROLL 0
+#endif
+#ifndef BP_WAVES
+#define BP_WAVES 8
+#endif
+#ifndef BP_HOLD  // 1: the backward holds each feature tile's masked gradient between its two passes
+#define BP_HOLD (BP_WAVES == 4)
+#endif
+constexpr int kFpThreads = 64 * FP_WAVES;  // 8 waves = 2 per SIMD sharing the one LDS weight image (one block per CU)
 constexpr int kFpLdsMax = 163840;
-constexpr int kFpQ = 2;          // board tiles per MLP pass (accumulators of kFpQ x NT tiles)
+constexpr int kFpRows = FP_WAVES == 8 ? 32 : 64;  // rows per wave iteration (the loss runs "lane = row")
+constexpr int kFpTiles = kFpRows / 16;
+#ifndef FP_Q
+#define FP_Q (FP_WAVES == 8 ? 1 : 2)
+#endif
+constexpr int kFpQ = FP_Q;          // board tiles per MLP pass (accumulators of kFpQ x NT tiles: 256 registers per wave)
+constexpr int kFpBlockRows = kFpThreads / 64 * kFpRows;
 constexpr int kTrainParts = 8;   // partial floats per block: dba[4], dbv, sum ppo, sum H, sum v
 
 struct FpArgs {
@@ -127,7 +148,7 @@ __device__ __forceinline__ void store_tile(uint16_t *dst, uint32_t off, const ui
 }
 
 template <int H, bool TRAIN, bool DROP>
-__global__ __launch_bounds__(kFpThreads, 1) void mlp_pass_kernel(FpArgs a) {
+__global__ __launch_bounds__(kFpThreads) void mlp_pass_kernel(FpArgs a) {
     constexpr int NT = (H + 15) / 16, KS = ((H + 7) / 8 * 8 + 31) / 32;
     constexpr int h = H;
     constexpr int PW = pr_pitch(h), WB = pr_wbytes(h);
@@ -183,19 +204,30 @@ __global__ __launch_bounds__(kFpThreads, 1) void mlp_pass_kernel(FpArgs a) {
     float acc_s[kTrainParts] = {0, 0, 0, 0, 0, 0, 0, 0};
     float kmax = -INFINITY;
 
-    for (int64_t base = (int64_t)blockIdx.x * kFpThreads; base < m; base += (int64_t)gridDim.x * kFpThreads) {
-        const int64_t r0 = base + 64 * wave;
+    for (int64_t base = (int64_t)blockIdx.x * kFpBlockRows; base < m; base += (int64_t)gridDim.x * kFpBlockRows) {
+        const int64_t r0 = base + kFpRows * wave;
         if (r0 >= m) continue;  // an empty wave (no barrier below)
         const int64_t r = r0 + lane;  // this lane's row for the loss / KL ("lane = row")
-        const bool live = r < m, real = r < mv;
+        const bool live = lane < kFpRows && r < m, real = live && r < mv;
         const uint4 b = live ? *reinterpret_cast<const uint4 *>(a.boards + a.la.idx[r] * 16) : make_uint4(0u, 0u, 0u, 0u);
 
         int wlane_t = wlane, glane_t = (col * 48 + 8 * g) * 2;
         asm volatile("" : "+v"(wlane_t), "+v"(glane_t));
-        const char *w0b = reinterpret_cast<const char *>(a.w0) + glane_t;
+        // the LayerNorm affines are re-read from LDS per layer: an opaque base keeps the compiler
+        // from hoisting all 3 x 2 x NT float4 of them out of the row loop (registers: 2 waves per SIMD)
+        int lnoff = 0;
+        asm volatile("" : "+v"(lnoff));
+        const float *sLNr = sLN + lnoff;
+        // the stem weight fragments through a buffer descriptor: per-lane 32-bit offset + a constant
+        // SGPR offset per (n, ks) -- no 64-bit address register pair per fragment.  Rows past h read
+        // out of range (zero); k past 48 (ks 1, lane groups 2, 3) is sent out of range too.
+        const __amdgpu_buffer_rsrc_t w0r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(a.w0), 0, h * 96, 0x00020000);
+        const int w0off[2] = {glane_t, g < 2 ? glane_t + 64 : h * 96};
         f32x4_t accH[4];
+#pragma unroll
+        for (int t = kFpTiles; t < 4; t++) accH[t] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll 1
-        for (int pr = 0; pr < 4 / kFpQ; pr++) {
+        for (int pr = 0; pr < kFpTiles / kFpQ; pr++) {
             uint2 act[kFpQ][NT];
             // ---------------- stem: obs fragments from the board bytes ----------------------
             uint4 xs[kFpQ][2];
@@ -215,6 +247,7 @@ __global__ __launch_bounds__(kFpThreads, 1) void mlp_pass_kernel(FpArgs a) {
                 }
             }
             f32x4_t acc[kFpQ][NT];
+            uint32_t kb[kFpQ][2] = {};  // the next block's dropout keep bits, drawn between its MFMAs
 #pragma unroll
             for (int q = 0; q < kFpQ; q++)
 #pragma unroll
@@ -223,9 +256,7 @@ __global__ __launch_bounds__(kFpThreads, 1) void mlp_pass_kernel(FpArgs a) {
             for (int ks = 0; ks < 2; ks++) {
 #pragma unroll
                 for (int n = 0; n < NT; n++) {
-                    const int row = 16 * n + col, k = 32 * ks + 8 * g;
-                    uint4 fw = make_uint4(0u, 0u, 0u, 0u);
-                    if (row < h && k < 48) fw = *reinterpret_cast<const uint4 *>(w0b + 2 * (16 * n * 48 + 32 * ks));
+                    const uint4 fw = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(w0r, w0off[ks], 2 * 16 * n * 48, 0));
 #pragma unroll
                     for (int q = 0; q < kFpQ; q++)
                         acc[q][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(fw), as_frag(xs[q][ks]), acc[q][n], 0, 0, 0);
@@ -236,11 +267,11 @@ __global__ __launch_bounds__(kFpThreads, 1) void mlp_pass_kernel(FpArgs a) {
 #define FP_EPILOGUE(L_, Q_, RES_, DROP_)                                                                           \
     do {                                                                                                        \
         const uint32_t row = (uint32_t)(r0 + 16 * (kFpQ * pr + (Q_)) + col);                                     \
-        const float *lnp = sLN + (L_) * 32 * NT;                                                                \
+        const float *lnp = sLNr + (L_) * 32 * NT;                                                               \
         const bool st = TRAIN && (int64_t)row < m;                                                              \
         float mean, rstd;                                                                                       \
-        ln_epilogue_train<NT, H, RES_, DROP_>(acc[Q_], act[Q_], lnp, lnp + 16 * NT, g, inv_n, (L_) == 2 ? d2 : d1, \
-                                              row, st ? a.g[L_] : nullptr, row * (2u * H), mean, rstd);         \
+        ln_epilogue_train_kb<NT, H, RES_, DROP_>(acc[Q_], act[Q_], lnp, lnp + 16 * NT, g, inv_n, d1.scale, kb[Q_],   \
+                                                 st ? a.g[L_] : nullptr, row * (2u * H), mean, rstd);            \
         if (st) {                                                                                               \
             if (a.h[L_]) store_tile<NT, H>(a.h[L_], row * (2u * H), act[Q_], g);                                \
             if (g == 0 && a.mean[L_]) {                                                                         \
@@ -252,8 +283,12 @@ __global__ __launch_bounds__(kFpThreads, 1) void mlp_pass_kernel(FpArgs a) {
 #pragma unroll
             for (int q = 0; q < kFpQ; q++) FP_EPILOGUE(0, q, false, false);
 
-            // ---------------- residual blocks ---------------------------------------------------
+            // ---------------- residual blocks (one copy of the code for both: instruction cache) ----
+#if FP_LUNROLL
 #pragma unroll
+#else
+#pragma unroll 1
+#endif
             for (int l = 0; l < 2; l++) {
 #pragma unroll
                 for (int q = 0; q < kFpQ; q++)
@@ -268,6 +303,14 @@ __global__ __launch_bounds__(kFpThreads, 1) void mlp_pass_kernel(FpArgs a) {
                     const bool kok = 32 * ks + 8 * g < hp8;
                     int kbase = wbase + 64 * ks;
                     asm volatile("" : "+v"(kbase));
+                    // keep bits of feature tiles 2 ks, 2 ks + 1 (column groups 8 ks + g, + 4) of this
+                    // block's dropout: VALU work beside the k-step's MFMAs instead of in the epilogue
+                    if (DROP && 2 * ks < NT)
+#pragma unroll
+                        for (int q = 0; q < kFpQ; q++) {
+                            const uint32_t row = (uint32_t)(r0 + 16 * (kFpQ * pr + q) + col);
+                            kb[q][ks >> 2] |= P::drop_keep8(l ? d2 : d1, row, (uint32_t)(8 * ks + g)) << (8 * (ks & 3));
+                        }
 #pragma unroll
                     for (int n = 0; n < NT; n++) {
                         const bool rok = n < NT - 1 || col < last_rows;
@@ -277,10 +320,13 @@ __global__ __launch_bounds__(kFpThreads, 1) void mlp_pass_kernel(FpArgs a) {
                         for (int q = 0; q < kFpQ; q++)
                             acc[q][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(fw), as_frag(bf[q]), acc[q][n], 0, 0, 0);
                     }
-                    __builtin_amdgcn_sched_barrier(0);
+                    if (FP_KSB) __builtin_amdgcn_sched_barrier(0);
                 }
 #pragma unroll
-                for (int q = 0; q < kFpQ; q++) FP_EPILOGUE(l + 1, q, true, DROP);
+                for (int q = 0; q < kFpQ; q++) {
+                    FP_EPILOGUE(l + 1, q, true, DROP);
+                    kb[q][0] = kb[q][1] = 0u;
+                }
             }
             // ---------------- heads: tile q's 16-row chain ----------------------------------------
 #pragma unroll
@@ -388,7 +434,7 @@ __global__ __launch_bounds__(kFpThreads, 1) void mlp_pass_kernel(FpArgs a) {
 // another order: per tile and layer a 16-lane reduce-scatter (DPP mirror / half-mirror / quad
 // swaps) leaves lane c one of its feature group's 8 sums (4 dgamma, 4 dbeta), accumulated per lane
 // -- 3 x NT registers instead of ln_bwd196's 8 NT per layer.
-constexpr int kBpThreads = 256;  // 4 waves (1 per SIMD: 512 registers for the whole chain); one block per CU (LDS)
+constexpr int kBpThreads = 64 * BP_WAVES;  // 8 waves = 2 per SIMD (256 registers each); one block per CU (LDS)
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
@@ -428,15 +474,44 @@ __device__ __forceinline__ float row16_scatter8(const float (&v)[8], int c) {
     return h1 + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(h1), 0xB1, 0xF, 0xF, false));
 }
 
+// Sum of v[0..15] over the 16 lanes of a DPP row, scattered: lane c ends with the sum of v[c] (the
+// same four butterfly stages as row16_scatter8 with a selecting last stage).
+__device__ __forceinline__ float row16_scatter16(const float (&v)[16], int c) {
+    const bool b3 = (c & 8) != 0, b2 = (c & 4) != 0, b1 = (c & 2) != 0, b0 = (c & 1) != 0;
+    float h8[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {  // row_mirror (bit 3 differs)
+        const float keep = b3 ? v[8 + j] : v[j], send = b3 ? v[j] : v[8 + j];
+        h8[j] = keep + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(send), 0x140, 0xF, 0xF, false));
+    }
+    float h4[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {  // row_half_mirror (bit 2)
+        const float keep = b2 ? h8[4 + j] : h8[j], send = b2 ? h8[j] : h8[4 + j];
+        h4[j] = keep + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(send), 0x141, 0xF, 0xF, false));
+    }
+    float h2[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {  // quad_perm 3,2,1,0 (bit 1)
+        const float keep = b1 ? h4[2 + j] : h4[j], send = b1 ? h4[j] : h4[2 + j];
+        h2[j] = keep + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(send), 0x1B, 0xF, 0xF, false));
+    }
+    const float keep = b0 ? h2[1] : h2[0], send = b0 ? h2[0] : h2[1];  // quad_perm 1,0,3,2 (bit 0)
+    return keep + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(send), 0xB1, 0xF, 0xF, false));
+}
+
 // One layer's LayerNorm / ReLU / Dropout backward on the lane's tile row (ln_bwd196's two passes):
 // dy = heads' share + P sources in order; dG rounded to bf16 into dgb (zero past h) and stored;
-// the dgamma / dbeta partial sums of the tile go to gb[n].
+// the dgamma / dbeta partial sums of the tile go to gb[n].  The masked output gradient of a feature
+// tile (dy times the ReLU and dropout masks) is computed in BOTH passes instead of being held
+// between them (52 registers: the kernel runs two waves per SIMD); the dropout multipliers come from
+// keep bits drawn ahead (kb, ppo::drop_keep8), the same values as the Philox-in-place form.
 template <int NT, int H, bool DROP, int NP>
 __device__ __forceinline__ void bp_layer(const uint16_t *__restrict__ gsrc, float mu, float rs, const float *sgm,
                                          const float *sbt, const float (&wh)[NT][2], float b0, float b1,
-                                         const uint2 *const (&pr)[NP > 0 ? NP : 1], const P::Drop &d, uint32_t rowu,
-                                         bool live, int gq, int col, uint2 (&dgb)[NT], uint16_t *dgout,
-                                         float (&gb)[NT]) {
+                                         const uint2 *const (&pr)[NP > 0 ? NP : 1], float scale,
+                                         const uint32_t (&kb)[2], bool live, int gq, int col, uint2 (&dgb)[NT],
+                                         uint16_t *dgout, float (&gb)[(NT + 1) / 2]) {
     namespace R = g2048::lnrow;
     constexpr float inv_h = 1.0f / (float)H;
     const bool lastok = 16 * (NT - 1) + 4 * gq < H;
@@ -444,12 +519,9 @@ __device__ __forceinline__ void bp_layer(const uint16_t *__restrict__ gsrc, floa
     uint2 gr[NT];
 #pragma unroll
     for (int n = 0; n < NT; n++) gr[n] = *reinterpret_cast<const uint2 *>(gsrc + 16 * n + 4 * gq * valid(n));
-    R::f32x2 dzr[NT][2];
-    R::f32x2 s1 = {0.0f, 0.0f}, s2 = {0.0f, 0.0f};
     const R::f32x2 nmu = {-mu, -mu}, rs2 = {rs, rs};
-    uint4 dpair = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-    for (int n = 0; n < NT; n++) {
+    // feature tile n: xhat pairs, the masked output gradient pairs, gamma
+    auto dtile = [&](int n, R::f32x2 &xh0, R::f32x2 &xh1, R::f32x2 &d0, R::f32x2 &d1, float4 &gm) {
         const int f0 = 16 * n + 4 * gq;
         f32x4_t dy = {0.0f, 0.0f, 0.0f, 0.0f};
         dy = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[n][0], b0, dy, 0, 0, 0);
@@ -462,54 +534,89 @@ __device__ __forceinline__ void bp_layer(const uint16_t *__restrict__ gsrc, floa
             t[2] += R::bf_lo(pr[i][n].y);
             t[3] += R::bf_hi(pr[i][n].y);
         }
-        const float4 gm = *reinterpret_cast<const float4 *>(sgm + f0);
+        gm = *reinterpret_cast<const float4 *>(sgm + f0);
         const float4 bt = *reinterpret_cast<const float4 *>(sbt + f0);
-        const R::f32x2 xh0 = (R::f32x2{R::bf_lo(gr[n].x), R::bf_hi(gr[n].x)} + nmu) * rs2;
-        const R::f32x2 xh1 = (R::f32x2{R::bf_lo(gr[n].y), R::bf_hi(gr[n].y)} + nmu) * rs2;
-        const R::f32x2 z0 = __builtin_elementwise_fma(xh0, R::f32x2{gm.x, gm.y}, R::f32x2{bt.x, bt.y});
-        const R::f32x2 z1 = __builtin_elementwise_fma(xh1, R::f32x2{gm.z, gm.w}, R::f32x2{bt.z, bt.w});
+        xh0 = (R::f32x2{R::bf_lo(gr[n].x), R::bf_hi(gr[n].x)} + nmu) * rs2;
+        xh1 = (R::f32x2{R::bf_lo(gr[n].y), R::bf_hi(gr[n].y)} + nmu) * rs2;
+        const R::f32x2 z0 = R::fma2(xh0, R::f32x2{gm.x, gm.y}, R::f32x2{bt.x, bt.y});
+        const R::f32x2 z1 = R::fma2(xh1, R::f32x2{gm.z, gm.w}, R::f32x2{bt.z, bt.w});
         const bool on = live && valid(n);
         float k[4] = {1.0f, 1.0f, 1.0f, 1.0f};
-        if (DROP) {
-            if ((n & 1) == 0) dpair = P::drop_draw4(d, rowu, (uint32_t)(f0 >> 2));
-            P::drop_mult_bits(d, P::drop_half(dpair, (uint32_t)(f0 >> 2)), k);
+        if (DROP) P::keep_mult(kb, n, scale, k);
+        d0 = R::f32x2{(on && z0.x > 0.0f) ? t[0] * k[0] : 0.0f, (on && z0.y > 0.0f) ? t[1] * k[1] : 0.0f};
+        d1 = R::f32x2{(on && z1.x > 0.0f) ? t[2] * k[2] : 0.0f, (on && z1.y > 0.0f) ? t[3] * k[3] : 0.0f};
+    };
+    R::f32x2 s1 = {0.0f, 0.0f}, s2 = {0.0f, 0.0f};
+    float v16[16];  // tiles n (even slots) and n + 1 (odd): [d xhat 0..3 | d 0..3] each
+    R::f32x2 dzr[BP_HOLD ? NT : 1][2];
+#pragma unroll
+    for (int n = 0; n < NT; n++) {
+        R::f32x2 xh0, xh1, d0, d1;
+        float4 gm;
+        dtile(n, xh0, xh1, d0, d1, gm);
+        if (BP_HOLD) {
+            dzr[n][0] = d0;
+            dzr[n][1] = d1;
         }
-        const R::f32x2 d0 = {(on && z0.x > 0.0f) ? t[0] * k[0] : 0.0f, (on && z0.y > 0.0f) ? t[1] * k[1] : 0.0f};
-        const R::f32x2 d1 = {(on && z1.x > 0.0f) ? t[2] * k[2] : 0.0f, (on && z1.y > 0.0f) ? t[3] * k[3] : 0.0f};
-        dzr[n][0] = d0;
-        dzr[n][1] = d1;
         const float v8[8] = {d0.x * xh0.x, d0.y * xh0.y, d1.x * xh1.x, d1.y * xh1.y, d0.x, d0.y, d1.x, d1.y};
-        gb[n] += row16_scatter8(v8, col);
+#pragma unroll
+        for (int j = 0; j < 8; j++) v16[2 * j + (n & 1)] = v8[j];
+        if ((n & 1) == 1 || n == NT - 1) {
+            if ((n & 1) == 0)
+#pragma unroll
+                for (int j = 0; j < 8; j++) v16[2 * j + 1] = 0.0f;
+            gb[n >> 1] += row16_scatter16(v16, col);
+        }
         const R::f32x2 x0 = d0 * R::f32x2{gm.x, gm.y}, x1 = d1 * R::f32x2{gm.z, gm.w};  // dxhat
         s1 = s1 + x0 + x1;
-        s2 = __builtin_elementwise_fma(x1, xh1, __builtin_elementwise_fma(x0, xh0, s2));
+        s2 = R::fma2(x1, xh1, R::fma2(x0, xh0, s2));
+        __builtin_amdgcn_sched_barrier(0);  // one feature tile at a time (registers; the other wave overlaps)
     }
     const float m1 = R::xor32_add(R::xor16_add(s1.x + s1.y)) * inv_h;
     const float m2 = R::xor32_add(R::xor16_add(s2.x + s2.y)) * inv_h;
     const R::f32x2 nm1 = {-m1, -m1}, nm2 = {-m2, -m2};
+    if (!BP_HOLD) {
+        // opaque inputs: the compiler would otherwise keep pass 1's tiles (and LDS loads) live instead
+        // of recomputing / re-reading them
+        asm volatile("" : "+v"(b0), "+v"(b1), "+v"(sgm), "+v"(sbt));
+#pragma unroll
+        for (int n = 0; n < NT; n++) asm volatile("" : "+v"(gr[n].x), "+v"(gr[n].y));
+    }
 #pragma unroll
     for (int n = 0; n < NT; n++) {
         const int f0 = 16 * n + 4 * gq;
-        const float4 gm = *reinterpret_cast<const float4 *>(sgm + f0);
-        const R::f32x2 xh0 = (R::f32x2{R::bf_lo(gr[n].x), R::bf_hi(gr[n].x)} + nmu) * rs2;
-        const R::f32x2 xh1 = (R::f32x2{R::bf_lo(gr[n].y), R::bf_hi(gr[n].y)} + nmu) * rs2;
-        const R::f32x2 o0 = __builtin_elementwise_fma(xh0, nm2, dzr[n][0] * R::f32x2{gm.x, gm.y} + nm1) * rs2;
-        const R::f32x2 o1 = __builtin_elementwise_fma(xh1, nm2, dzr[n][1] * R::f32x2{gm.z, gm.w} + nm1) * rs2;
+        R::f32x2 xh0, xh1, d0, d1;
+        float4 gm;
+        if (BP_HOLD) {
+            gm = *reinterpret_cast<const float4 *>(sgm + f0);
+            xh0 = (R::f32x2{R::bf_lo(gr[n].x), R::bf_hi(gr[n].x)} + nmu) * rs2;
+            xh1 = (R::f32x2{R::bf_lo(gr[n].y), R::bf_hi(gr[n].y)} + nmu) * rs2;
+            d0 = dzr[n][0];
+            d1 = dzr[n][1];
+        } else {
+            dtile(n, xh0, xh1, d0, d1, gm);
+        }
+        const R::f32x2 o0 = R::fma2(xh0, nm2, R::fma2(d0, R::f32x2{gm.x, gm.y}, nm1)) * rs2;
+        const R::f32x2 o1 = R::fma2(xh1, nm2, R::fma2(d1, R::f32x2{gm.z, gm.w}, nm1)) * rs2;
         dgb[n] = valid(n) ? make_uint2(R::pack_bf2(o0.x, o0.y), R::pack_bf2(o1.x, o1.y)) : make_uint2(0u, 0u);
         if (live && valid(n)) *reinterpret_cast<uint2 *>(dgout + f0) = dgb[n];
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
 // P^T tile chain of one block layer: p[n] = bf16(sum_ks W^T[16 n ..][k-step ks] dG^T) -- the
 // dgrad kernel's k order from zero.  A = W^T by two transposing reads of the row-major image
 // (lane (g, q, p): rows 32 ks + 8 g + q and + 4, columns 16 n + 4 p); k-step rows past h are
-// redirected to row 0 (their B is zero: dG past h is zero).
-template <int NT, int H, int KS, int PW>
-__device__ __forceinline__ void bp_dgrad(const char *wimg, const uint2 (&dgb)[NT], int lane, uint2 (&pout)[NT]) {
+// redirected to row 0 (their B is zero: dG past h is zero).  DRAW: beside k-step ks's MFMAs, the
+// keep bits of feature-tile pair ks of dropout `d` for row `drow` (the next layer's masks).
+template <int NT, int H, int KS, int PW, bool DRAW>
+__device__ __forceinline__ void bp_dgrad(const char *wimg, const uint2 (&dgb)[NT], int lane, uint2 (&pout)[NT],
+                                         const P::Drop &d, uint32_t drow, uint32_t (&kb)[2]) {
     const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
     f32x4_t acc[NT];
 #pragma unroll
     for (int n = 0; n < NT; n++) acc[n] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+    if (DRAW) kb[0] = kb[1] = 0u;
 #pragma unroll
     for (int ks = 0; ks < KS; ks++) {
         const uint4 bf = act_frag<NT>(dgb, ks);
@@ -517,6 +624,7 @@ __device__ __forceinline__ void bp_dgrad(const char *wimg, const uint2 (&dgb)[NT
         const int ra = r1 < H ? r1 : 0, rb = r1 + 4 < H ? r1 + 4 : 0;
         int oa = ra * PW + 8 * p4, ob = rb * PW + 8 * p4;
         asm volatile("" : "+v"(oa), "+v"(ob));
+        if (DRAW && 2 * ks < NT) kb[ks >> 2] |= P::drop_keep8(d, drow, (uint32_t)(8 * ks + g)) << (8 * (ks & 3));
 #pragma unroll
         for (int n = 0; n < NT; n++) {
             const s16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(wimg + oa + 32 * n));
@@ -529,8 +637,16 @@ __device__ __forceinline__ void bp_dgrad(const char *wimg, const uint2 (&dgb)[NT
     for (int n = 0; n < NT; n++) pout[n] = make_uint2(pack_bf2(acc[n][0], acc[n][1]), pack_bf2(acc[n][2], acc[n][3]));
 }
 
+// keep bits of all feature tiles of dropout `d` for row `row` (the first tile's top block)
+template <int NT>
+__device__ __forceinline__ void draw_keep(const P::Drop &d, uint32_t row, int g, uint32_t (&kb)[2]) {
+    kb[0] = kb[1] = 0u;
+#pragma unroll
+    for (int ks = 0; 2 * ks < NT; ks++) kb[ks >> 2] |= P::drop_keep8(d, row, (uint32_t)(8 * ks + g)) << (8 * (ks & 3));
+}
+
 template <int H, bool DROP>
-__global__ __launch_bounds__(kBpThreads, 1) void mlp_back_kernel(BpArgs a) {
+__global__ __launch_bounds__(kBpThreads) void mlp_back_kernel(BpArgs a) {
     constexpr int NT = (H + 15) / 16, KS = ((H + 7) / 8 * 8 + 31) / 32;
     constexpr int PW = pr_pitch(H), WB = pr_wbytes(H);
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -574,41 +690,56 @@ __global__ __launch_bounds__(kBpThreads, 1) void mlp_back_kernel(BpArgs a) {
     }
     __syncthreads();
     const P::Drop d1 = P::make_drop(a.drop[0]), d2 = P::make_drop(a.drop[1]);
-    float gb[kMaxLayers][NT];
+    constexpr int NG = (NT + 1) / 2;  // dgamma / dbeta sums per layer and lane: tile pair n >> 1, slot col
+    float gb[kMaxLayers][NG];
 #pragma unroll
     for (int l = 0; l < kMaxLayers; l++)
 #pragma unroll
-        for (int n = 0; n < NT; n++) gb[l][n] = 0.0f;
+        for (int n = 0; n < NG; n++) gb[l][n] = 0.0f;
     const int64_t ntile = (m + 15) >> 4;
-    for (int64_t tile = (int64_t)blockIdx.x * (kBpThreads / 64) + wave; tile < ntile;
-         tile += (int64_t)gridDim.x * (kBpThreads / 64)) {
+    constexpr int kW = kBpThreads / 64;
+    const int64_t tstride = (int64_t)gridDim.x * kW;
+    // dropout keep bits: the top block's for the wave's first tile now, then each tile's block-1 bits
+    // beside its P2 chain and the NEXT tile's top-block bits beside its P1 chain
+    uint32_t kb2[2] = {0u, 0u}, kb1[2] = {0u, 0u};
+    {
+        const int64_t t0 = (int64_t)blockIdx.x * kW + wave, r = 16 * t0 + col;
+        if (DROP && t0 < ntile) draw_keep<NT>(d2, (uint32_t)(r < m ? r : 0), gq, kb2);
+    }
+    for (int64_t tile = (int64_t)blockIdx.x * kW + wave; tile < ntile; tile += tstride) {
         const int64_t row = 16 * tile + col;
         const bool live = row < m;
         const int64_t rc = live ? row : 0;
         const uint32_t rowu = (uint32_t)rc;
+        const int64_t rn = 16 * (tile + tstride) + col;  // the next tile's row (its top-block masks)
+        const uint32_t rnu = (uint32_t)(rn < m ? rn : 0);
+        // an opaque base: the LayerNorm affines are re-read per tile, not hoisted into registers
+        int lnoff = 0;
+        asm volatile("" : "+v"(lnoff));
+        const float *sLNr = sLN + lnoff;
         const float b0 = a.dz[rc * 8 + gq];
         const float b1 = gq == 0 ? a.dz[rc * 8 + 4] : 0.0f;
         uint2 dgb[NT], p2[NT], p1[NT];
         // block 2 (top): dy = the heads' share
         {
             const uint2 *pr[1] = {nullptr};
-            bp_layer<NT, H, DROP, 0>(a.g[2] + rc * H, a.mean[2][rc], a.rstd[2][rc], sLN + 2 * 32 * NT,
-                                     sLN + 2 * 32 * NT + 16 * NT, wh, b0, b1, pr, d2, rowu, live, gq, col, dgb,
+            bp_layer<NT, H, DROP, 0>(a.g[2] + rc * H, a.mean[2][rc], a.rstd[2][rc], sLNr + 2 * 32 * NT,
+                                     sLNr + 2 * 32 * NT + 16 * NT, wh, b0, b1, pr, d2.scale, kb2, live, gq, col, dgb,
                                      a.dg[2] + rc * H, gb[2]);
         }
-        bp_dgrad<NT, H, KS, PW>(smem + WB, dgb, lane, p2);
+        bp_dgrad<NT, H, KS, PW, DROP>(smem + WB, dgb, lane, p2, d1, rowu, kb1);
         if (a.pout[1] && live) store_tile<NT, H>(a.pout[1], (uint32_t)rc * (2u * H), p2, gq);
         {  // block 1: + P2
             const uint2 *pr[1] = {p2};
-            bp_layer<NT, H, DROP, 1>(a.g[1] + rc * H, a.mean[1][rc], a.rstd[1][rc], sLN + 32 * NT, sLN + 48 * NT, wh,
-                                     b0, b1, pr, d1, rowu, live, gq, col, dgb, a.dg[1] + rc * H, gb[1]);
+            bp_layer<NT, H, DROP, 1>(a.g[1] + rc * H, a.mean[1][rc], a.rstd[1][rc], sLNr + 32 * NT, sLNr + 48 * NT,
+                                     wh, b0, b1, pr, d1.scale, kb1, live, gq, col, dgb, a.dg[1] + rc * H, gb[1]);
         }
-        bp_dgrad<NT, H, KS, PW>(smem, dgb, lane, p1);
+        bp_dgrad<NT, H, KS, PW, DROP>(smem, dgb, lane, p1, d2, rnu, kb2);
         if (a.pout[0] && live) store_tile<NT, H>(a.pout[0], (uint32_t)rc * (2u * H), p1, gq);
         {  // the stem: + P1 + P2 (the per-layer chain's source order), no dropout
             const uint2 *pr[2] = {p1, p2};
-            bp_layer<NT, H, false, 2>(a.g[0] + rc * H, a.mean[0][rc], a.rstd[0][rc], sLN, sLN + 16 * NT, wh, b0, b1,
-                                      pr, d1, rowu, live, gq, col, dgb, a.dg[0] + rc * H, gb[0]);
+            bp_layer<NT, H, false, 2>(a.g[0] + rc * H, a.mean[0][rc], a.rstd[0][rc], sLNr, sLNr + 16 * NT, wh, b0,
+                                      b1, pr, 1.0f, kb1, live, gq, col, dgb, a.dg[0] + rc * H, gb[0]);
         }
     }
     // dgamma / dbeta: lane (gq, col) even col holds slot s = col >> 1 of its feature groups
@@ -616,12 +747,15 @@ __global__ __launch_bounds__(kBpThreads, 1) void mlp_back_kernel(BpArgs a) {
     __syncthreads();
     float *red = reinterpret_cast<float *>(smem);  // [wave][layer][2][16 NT]
     constexpr int RW = kMaxLayers * 2 * 16 * NT;
-    if ((col & 1) == 0) {
+    {
         const int s = col >> 1, which = s >> 2, e = s & 3;
 #pragma unroll
         for (int l = 0; l < kMaxLayers; l++)
 #pragma unroll
-            for (int n = 0; n < NT; n++) red[wave * RW + (l * 2 + which) * 16 * NT + 16 * n + 4 * gq + e] = gb[l][n];
+            for (int j = 0; j < NG; j++) {
+                const int n = 2 * j + (col & 1);
+                if (n < NT) red[wave * RW + (l * 2 + which) * 16 * NT + 16 * n + 4 * gq + e] = gb[l][j];
+            }
     }
     __syncthreads();
     const int nb = gridDim.x;
@@ -645,7 +779,7 @@ inline bool al(const void *p, unsigned n) { return ((uintptr_t)p % n) == 0u; }
 size_t fp_lds(int h) { return (size_t)pr_lds_bytes(h, (h + 15) / 16); }
 
 int fp_blocks(int64_t m) {
-    const int64_t b = (m + kFpThreads - 1) / kFpThreads;
+    const int64_t b = (m + kFpBlockRows - 1) / kFpBlockRows;
     return (int)(b < 1 ? 1 : (b > 256 ? 256 : b));
 }
 

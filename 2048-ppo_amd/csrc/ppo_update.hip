@@ -1254,8 +1254,8 @@ __global__ __launch_bounds__(kMwThreads) void mlp_fwd_wide_kernel(const uint16_t
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     const R::f32x2 y2 = {yv[u], yv[u]};
-                    lg01 = __builtin_elementwise_fma(y2, R::f32x2{swa[f0 + u], swa[16 * NT + f0 + u]}, lg01);
-                    lg23 = __builtin_elementwise_fma(y2, R::f32x2{swa[2 * 16 * NT + f0 + u], swa[3 * 16 * NT + f0 + u]}, lg23);
+                    lg01 = R::fma2(y2, R::f32x2{swa[f0 + u], swa[16 * NT + f0 + u]}, lg01);
+                    lg23 = R::fma2(y2, R::f32x2{swa[2 * 16 * NT + f0 + u], swa[3 * 16 * NT + f0 + u]}, lg23);
                 }
             } else {
                 *reinterpret_cast<uint2 *>(orow + 32 * n) = yb;
@@ -1428,8 +1428,8 @@ __global__ __launch_bounds__(kLbThreads) void ln_bwd196_kernel(DySrc src, const 
             const float4 bt = *reinterpret_cast<const float4 *>(sbt + f0);
             const R::f32x2 xh0 = (R::f32x2{R::bf_lo(gr[n].x), R::bf_hi(gr[n].x)} + nmu) * rs2;
             const R::f32x2 xh1 = (R::f32x2{R::bf_lo(gr[n].y), R::bf_hi(gr[n].y)} + nmu) * rs2;
-            const R::f32x2 z0 = __builtin_elementwise_fma(xh0, R::f32x2{gm.x, gm.y}, R::f32x2{bt.x, bt.y});
-            const R::f32x2 z1 = __builtin_elementwise_fma(xh1, R::f32x2{gm.z, gm.w}, R::f32x2{bt.z, bt.w});
+            const R::f32x2 z0 = R::fma2(xh0, R::f32x2{gm.x, gm.y}, R::f32x2{bt.x, bt.y});
+            const R::f32x2 z1 = R::fma2(xh1, R::f32x2{gm.z, gm.w}, R::f32x2{bt.z, bt.w});
             const bool on = live && valid(n);
             float k[4] = {1.0f, 1.0f, 1.0f, 1.0f};
             if (DROP) {
@@ -1440,13 +1440,13 @@ __global__ __launch_bounds__(kLbThreads) void ln_bwd196_kernel(DySrc src, const 
             const R::f32x2 d1 = {(on && z1.x > 0.0f) ? t[2] * k[2] : 0.0f, (on && z1.y > 0.0f) ? t[3] * k[3] : 0.0f};
             dzr[n][0] = d0;
             dzr[n][1] = d1;
-            ag[n][0] = __builtin_elementwise_fma(d0, xh0, ag[n][0]);
-            ag[n][1] = __builtin_elementwise_fma(d1, xh1, ag[n][1]);
+            ag[n][0] = R::fma2(d0, xh0, ag[n][0]);
+            ag[n][1] = R::fma2(d1, xh1, ag[n][1]);
             ab[n][0] = ab[n][0] + d0;
             ab[n][1] = ab[n][1] + d1;
             const R::f32x2 x0 = d0 * R::f32x2{gm.x, gm.y}, x1 = d1 * R::f32x2{gm.z, gm.w};  // dxhat
             s1 = s1 + x0 + x1;
-            s2 = __builtin_elementwise_fma(x1, xh1, __builtin_elementwise_fma(x0, xh0, s2));
+            s2 = R::fma2(x1, xh1, R::fma2(x0, xh0, s2));
         }
         const float m1 = R::xor32_add(R::xor16_add(s1.x + s1.y)) * inv_h;
         const float m2 = R::xor32_add(R::xor16_add(s2.x + s2.y)) * inv_h;
@@ -1459,8 +1459,8 @@ __global__ __launch_bounds__(kLbThreads) void ln_bwd196_kernel(DySrc src, const 
             const float4 gm = *reinterpret_cast<const float4 *>(sgm + f0);
             const R::f32x2 xh0 = (R::f32x2{R::bf_lo(gr[n].x), R::bf_hi(gr[n].x)} + nmu) * rs2;
             const R::f32x2 xh1 = (R::f32x2{R::bf_lo(gr[n].y), R::bf_hi(gr[n].y)} + nmu) * rs2;
-            const R::f32x2 o0 = __builtin_elementwise_fma(xh0, nm2, dzr[n][0] * R::f32x2{gm.x, gm.y} + nm1) * rs2;
-            const R::f32x2 o1 = __builtin_elementwise_fma(xh1, nm2, dzr[n][1] * R::f32x2{gm.z, gm.w} + nm1) * rs2;
+            const R::f32x2 o0 = R::fma2(xh0, nm2, R::fma2(dzr[n][0], R::f32x2{gm.x, gm.y}, nm1)) * rs2;
+            const R::f32x2 o1 = R::fma2(xh1, nm2, R::fma2(dzr[n][1], R::f32x2{gm.z, gm.w}, nm1)) * rs2;
             *reinterpret_cast<uint2 *>(orow + 32 * n) = make_uint2(R::pack_bf2(o0.x, o0.y), R::pack_bf2(o1.x, o1.y));
         }
         mw_flush(sO, dg + 16 * tile * N, rows, lane);

@@ -86,6 +86,18 @@ def allreduce_sum_(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+def allreduce_min_(t: torch.Tensor) -> torch.Tensor:
+    """In-place MIN over the ranks (RCCL on the device tensor itself; gloo host-staged)."""
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        if t.is_cuda and _host_staged():
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.MIN)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return t
+
+
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     if dist.is_initialized() and dist.get_world_size() > 1:
         if t.is_cuda and _host_staged():

@@ -219,6 +219,17 @@ class FusedMuonAdamW(MuonAdamW):
         self._mats = self._groups = None
         self._cfg = L.MuonCfg(self.momentum, self.wd, self.ns[0], self.ns[1], self.ns[2], self.ns_eps, self.ns_steps,
                               int(self.nesterov))
+        # the h 196 / 192 square matrices' Newton-Schulz on MUON_PARTS CUs each (row blocks, one
+        # exchange of X per iteration through this workspace); G2048_MUON_PARTS=1: one CU per matrix
+        if self.supported:
+            import os
+            parts = int(os.environ.get("G2048_MUON_PARTS", self.MUON_PARTS))
+            if parts > 1:
+                self._ws = torch.empty(int(L.load().g2048_muon_workspace_bytes()), dtype=torch.uint8, device=self.dev)
+                self._cfg.parts = parts
+                self._cfg.workspace = self._ws.data_ptr()
+
+    MUON_PARTS = 8
 
     def set_bf16_copies(self, mapping: dict):
         """{parameter: bf16 tensor} refreshed by the Muon kernel after each step."""

@@ -23,7 +23,7 @@ from . import _lib as L
 from . import fastmlp
 from . import urm as urm_mod
 from .advantage import RewardWeights, RTGTracker
-from .dist import GradBucket, allreduce_sum_, broadcast_, equal_rows, world
+from .dist import GradBucket, allreduce_min_, allreduce_sum_, broadcast_, equal_rows, world
 from .optim import FusedMuonAdamW, MuonAdamW, ScheduledMuonAdamW, build_optimizer
 from .ppo import PPOConfig, PPOUpdater
 from .rollout import Rollout, make_policy
@@ -212,6 +212,7 @@ class VecTrainer:
             paths["urm_rollout"] = ("one-launch g2048_urm_forward" if getattr(pol, "mega", False)
                                     else "per-op kernels" if getattr(pol, "fused", False) else "torch.mm + kernels")
         fb = []
+        fused_up = isinstance(up, fastmlp.FusedPPOUpdater)
         if mlp and self.dev.type == "cuda":
             h, nl = self.model.config.hidden_dim, len(self.model.backbone)
             if not getattr(pol, "fused_rollout", False):
@@ -333,10 +334,16 @@ class VecTrainer:
             data = {k: v.index_select(0, valid) for k, v in data.items()}
         n_aug = 0
         n_real = data["actions"].shape[0]
-        if cfg.upsample_ratio > 0:
-            data, n_aug = self._augment(data, step)
-        if self.world > 1:  # every rank runs the same number of minibatches (one all-reduce each)
-            data = equal_rows(data, n_real, self.trim_gen)
+        if cfg.upsample_ratio > 0 and self.world > 1 and not self.episodic:
+            # fixed horizon, several ranks: every rank has the same n_real real rows, so equal_rows is
+            # "keep the smallest rank's copy count": the MIN all-reduce runs on the device count and
+            # ONE host read serves both the copy count and the trim (no separate count read)
+            data, n_aug = self._augment(data, step, min_over_ranks=True)
+        else:
+            if cfg.upsample_ratio > 0:
+                data, n_aug = self._augment(data, step)
+            if self.world > 1:  # every rank runs the same number of minibatches (one all-reduce each)
+                data = equal_rows(data, n_real, self.trim_gen)
         self._mark("augment_ms")
         ustats = self.ppo.update(data, self.beta, self._encode)
         self.opt.scheduler_step()
@@ -351,11 +358,13 @@ class VecTrainer:
         metrics["current_beta"] = self.beta
         return metrics
 
-    def _augment(self, data: dict, step: int):
+    def _augment(self, data: dict, step: int, min_over_ranks: bool = False):
         """calculate_advantage's D4 up-sampling (train.py:774-881) on the device: the real samples are
         copied into a fixed pool (stable pointers for the captured update) and g2048_augment appends
         the mirror / rotation copies of int(n * ratio) distinct samples.  Returns (pool views over
-        real + copies, number of copies); one host read of the copy count."""
+        real + copies, number of copies); one host read of the copy count.  min_over_ranks: the
+        count is first MIN-all-reduced on the device (dist.equal_rows for equal real-row counts: the
+        copies past the smallest rank's count are dropped), so that read is the only sync."""
         n = data["actions"].shape[0]
         k = min(int(n * self.cfg.upsample_ratio), n)
         cap = n + 2 * k
@@ -372,6 +381,8 @@ class VecTrainer:
             self._aug_ws = torch.empty(L.augment_workspace_bytes(k), dtype=torch.uint8, device=self.dev)
         L.augment(pool["boards"], pool["actions"], pool["legal"], pool["logp"], pool["adv"], pool["ret"], n, k,
                   self.cfg.seed * 131 + self.rank, step, self._aug_ws, self._aug_count)
+        if min_over_ranks:
+            allreduce_min_(self._aug_count)
         c = int(self._aug_count.item())
         return {key: v[:c] for key, v in pool.items()}, c - n
 

@@ -348,7 +348,15 @@ typedef struct g2048_muon_matrix {
 typedef struct g2048_muon_cfg {
     float momentum, weight_decay, ns_a, ns_b, ns_c, ns_eps;
     int32_t ns_steps, nesterov;
+    /* parts > 1 with a workspace: every 196 x 196 / 192 x 192 matrix runs on `parts` blocks (CUs, 7 <=
+     * parts <= 13) that split the row blocks of the Newton-Schulz products and exchange X once per
+     * iteration through the workspace (g2048_muon_workspace_bytes(), device memory; its first bytes
+     * are zeroed by a memset node of every call).  parts <= 1 or workspace NULL: one block per matrix. */
+    int32_t parts, pad_;
+    void *workspace;
 } g2048_muon_cfg;
+
+size_t g2048_muon_workspace_bytes(void);
 
 /* 1 if a [rows, cols] matrix fits the one-block-per-matrix Newton-Schulz kernel (min dim <= 224,
  * max dim <= 256, both LDS images <= ~159 KB: h <= 196 for square weights; rows of a length that

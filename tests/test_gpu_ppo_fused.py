@@ -568,6 +568,34 @@ def test_fused_muon_adamw_matches_torch_ops_step(dev, h):
             torch.testing.assert_close(p1, p0, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("h,parts", [(196, 8), (196, 12), (196, 7), (192, 8)])
+def test_muon_multi_cu_equals_one_cu(dev, h, parts, monkeypatch):
+    """The multi-CU Newton-Schulz (the h x h blocks' row blocks on `parts` CUs, X exchanged once per
+    iteration through the workspace, optim.hip ns_square_mc) is bitwise the one-CU square schedule:
+    same MFMA sequence per output tile (the X product with its operand roles swapped).  Three steps,
+    every parameter and the momentum buffers compared."""
+    import agent
+    from g2048.dist import GradBucket
+    from g2048.optim import FusedMuonAdamW
+    outs = []
+    for p in (1, parts):
+        monkeypatch.setenv("G2048_MUON_PARTS", str(p))
+        torch.manual_seed(h)
+        m = agent.GameMLP(agent.MLPConfig(hidden_dim=h, num_layers=2)).to(dev)
+        opt = FusedMuonAdamW(m, 1e-3, 1e-4)
+        assert opt._cfg.parts == (p if p > 1 else 0)
+        order = [q for q, _ in opt.muon] + [q for grp in opt.adam_groups for q in grp["params"]]
+        bk = GradBucket(order)
+        for s in range(3):
+            bk.flat.copy_(torch.randn(bk.flat.shape, generator=torch.Generator().manual_seed(s)).to(dev) * 1e-2)
+            opt.step_clipped(bk.flat, 1.0)
+        torch.cuda.synchronize()
+        outs.append((torch.cat([q.detach().reshape(-1) for q in m.parameters()]).clone(),
+                     torch.cat([b.reshape(-1) for b in opt.muon_buf]).clone()))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b), (a - b).abs().max()
+
+
 def test_fused_muon_supported_shapes():
     from g2048 import _lib as L
     assert L.muon_supported(196, 196) and L.muon_supported(196, 48) and L.muon_supported(4, 196)
@@ -1198,7 +1226,7 @@ def test_fused_backward_matches_layer_chain(dev, h, m, p, decouple):
             # (the two translation units contract one of the LayerNorm-backward fmas differently)
             # (h != 196: the chain's generic LayerNorm backward sums the rows in another order)
             ne = dg1[l].view(torch.int16) != dg0[l].view(torch.int16)
-            assert int(ne.sum()) <= max(2, m * h // (100000 if h == 196 else 1000)), (l, int(ne.sum()))
+            assert int(ne.sum()) <= max(2, m * h // (100000 if h == 196 else 500)), (l, int(ne.sum()))
             d = (dg1[l].float() - dg0[l].float()).abs()
             tol = dg0[l].float().abs() / 64 + (0.0 if h == 196 else 2e-3 * dg0[l].float().abs().max().item()) + 1e-30
             assert bool((d <= tol).all()), (l, d.max())  # (cancellation near zero: absolute, 2e-3 of the scale)

@@ -40,7 +40,7 @@ def main():
     import os
     from g2048 import _lib as L
     if os.environ.get("G2048_LIB"):  # A/B timing against another build of the library
-        L.load(os.environ["G2048_LIB"])
+        L._lib = L.load(os.environ["G2048_LIB"])  # every wrapper then calls this build
     ms = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "65536").split(",")]
     h = int(sys.argv[2]) if len(sys.argv) > 2 else 196
     for m in ms:

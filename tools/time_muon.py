@@ -35,7 +35,24 @@ def main():
         step()
     e1.record()
     torch.cuda.synchronize()
-    print(f"FusedMuonAdamW.step_clipped h={h}: {e0.elapsed_time(e1) / reps * 1e3:.1f} us per step")
+    print(f"FusedMuonAdamW.step_clipped h={h}: {e0.elapsed_time(e1) / reps * 1e3:.1f} us per step (eager)")
+    s = torch.cuda.Stream()  # the training path replays the step from a hipGraph: time that too
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(10):
+                step()
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps // 10):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"FusedMuonAdamW.step_clipped h={h}: {e0.elapsed_time(e1) / reps * 1e3:.1f} us per step (hipGraph)")
     for ns in (() if "quick" in sys.argv[3:] else (0, 1, 5)):  # split: prologue/epilogue (0 Newton-Schulz steps) vs per-step cost
         fo._cfg.ns_steps = ns
         e0.record()
