@@ -117,7 +117,8 @@ constexpr int kBI = 4, kBJ = 4;          // generic schedule: 4 x 4 waves of 4 x
 constexpr int kMuonMaxMats = 16;  // GameMLP: 5, GameURM (2 layers): 11
 static_assert(sizeof(g2048_muon_cfg) == 48 && offsetof(g2048_muon_cfg, workspace) == 40,
               "g2048_muon_cfg layout (tests/test_abi.py)");
-constexpr int kMuonMaxJobs = 64;  // blocks of the Muon matrices (multi-CU squares: nparts each)
+constexpr int kMuonMaxJobs = 128;  // grid blocks: Muon parts, AdamW blocks, idle gaps (XCD placement)
+constexpr uint8_t kRoleAdam = 0xFE, kRoleIdle = 0xFF;
 constexpr int kMuonSyncBytes = kMuonMaxMats * 64;  // one 64-byte line per matrix counter
 constexpr int kMuonLds = 160 * 1024 - 256;  // minus the static red[] / s_norm
 
@@ -142,13 +143,15 @@ struct MuonArgs {
     AdamArgs adam;               // adam.count > 0: blocks count .. count + nadam - 1 run AdamW
     int nadam;
     int generic_ns;              // 1: square matrices on the generic schedule too (A/B timing, tests)
-    // blocks 0 .. njobs - 1: Muon parts; a square matrix of the multi-CU path is split over nparts
-    // blocks (row blocks of its Newton-Schulz products, one exchange of X per iteration)
-    int njobs;
+    // per grid block: job_mat = the matrix (a square matrix of the multi-CU path is split over
+    // job_nparts blocks: row blocks of its Newton-Schulz products, one exchange of X per iteration),
+    // kRoleAdam (job_part = the AdamW block index) or kRoleIdle (a gap of the XCD placement)
+    int njobs;  // grid size
     uint8_t job_mat[kMuonMaxJobs], job_part[kMuonMaxJobs], job_nparts[kMuonMaxJobs];
     uint32_t *sync;              // per matrix: the exchange counter (zeroed before every launch)
     char *xg;                    // per matrix: two N x P-byte bf16 exchange images (X of even / odd iterations)
     int64_t xg_stride;           // bytes per matrix
+    uint64_t *trace;             // MUON_TRACE builds: phase clocks
 };
 
 // LDS images are row-major bf16 with the K dimension zero-padded to a multiple of 8 (pitch =
@@ -328,6 +331,20 @@ __device__ __forceinline__ float muon_prologue(const float *__restrict__ grad, f
         }
     }
     return ss;
+}
+
+// The new momentum of rows [r0, r1) (C % 4 == 0), recomputed from the gradient and the old momentum
+// exactly as muon_prologue computes it: a multi-CU part writes its rows only after every part has
+// read the old momentum of all rows for its image (the momentum is read by all, written by one).
+__device__ __forceinline__ void muon_momentum_rows(const float *__restrict__ grad, float *__restrict__ mom, int C,
+                                                   float coef, float mu, bool nesterov, int r0, int r1, int tid) {
+    const int e0 = (r0 * C) >> 2, e1 = (r1 * C) >> 2;
+    for (int e4 = e0 + tid; e4 < e1; e4 += kMuonThreads) {
+        const float4 g4 = reinterpret_cast<const float4 *>(grad)[e4], b4 = reinterpret_cast<const float4 *>(mom)[e4];
+        float bv[4], ub[4];
+        momentum4(g4, b4, coef, mu, nesterov, bv, ub);
+        reinterpret_cast<float4 *>(mom)[e4] = make_float4(bv[0], bv[1], bv[2], bv[3]);
+    }
 }
 
 __device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_t *__restrict__ pbf, const char *sX,
@@ -709,6 +726,24 @@ __device__ __forceinline__ void ns_square(char *sX, char *sG, const MuonArgs &ar
 typedef __attribute__((address_space(1))) uint32_t gu32_t;
 typedef __attribute__((address_space(1))) uint64_t gu64_t;
 
+// MUON_TRACE builds (tools/trace_muon.py): per block, the shader clock at phase points, in the
+// workspace after the exchange images ([block][64] uint64, slot 0 = number of points)
+#ifdef MUON_TRACE
+constexpr int kMuonTraceBytes = kMuonMaxJobs * 64 * 8;
+#define MUON_TP(args_)                                                                      \
+    do {                                                                                    \
+        if (threadIdx.x == 0 && (args_).trace) {                                            \
+            uint64_t *t_ = (args_).trace + 64 * blockIdx.x;                                 \
+            const uint64_t k_ = t_[0] + 1;                                                  \
+            if (k_ < 64) t_[k_] = __builtin_amdgcn_s_memtime();                             \
+            t_[0] = k_;                                                                     \
+        }                                                                                   \
+    } while (0)
+#else
+constexpr int kMuonTraceBytes = 0;
+#define MUON_TP(args_) do {} while (0)
+#endif
+
 // G = X X^T alone, on the square schedule (no kept tiles: the row-block U product re-reads G)
 template <int N, int W>
 __device__ __forceinline__ void ns_g_w(char *sX, char *sG, int lane) {
@@ -855,6 +890,7 @@ __device__ __forceinline__ void ns_square_mc_rb(char *sX, char *sG, const MuonAr
     for (int it = 0; it < args.steps; it++) {
         // G = X X^T, whole (the single-block symmetric schedule; two barriers inside)
         ns_square_g<N>(sX, sG, wave, lane);
+        MUON_TP(args);
         f32x4_t acc[RB];
         // U rows of this block, in place over G's rows once every wave is done reading G
         if (wave < S::NT) mc_product<N, RB, true>(sX, sG, t0, wave, lane, args.b / args.c, acc);
@@ -867,9 +903,11 @@ __device__ __forceinline__ void ns_square_mc_rb(char *sX, char *sG, const MuonAr
                 if (row < N) *reinterpret_cast<uint2 *>(sG + row * P + (16 * wave + 4 * (c >> 2)) * 2) = v;
             }
         __syncthreads();
+        MUON_TP(args);
         // X' rows of this block
         if (wave < S::NT) mc_product<N, RB, false>(sX, sG, t0, wave, lane, args.a, acc);
         __syncthreads();  // every read of X is done
+        MUON_TP(args);
         const bool last = it == args.steps - 1;
         char *img = last ? sX : xg + (it & 1) * N * P;
         if (wave < S::NT)
@@ -894,6 +932,7 @@ __device__ __forceinline__ void ns_square_mc_rb(char *sX, char *sG, const MuonAr
         // hand-off: every storing wave drains, the barrier, one lane adds; one wave polls, acquires
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        MUON_TP(args);
         if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (wave == 0) {
             mc_wait(ctr, (uint32_t)(np * (it + 1)), err);
@@ -901,11 +940,24 @@ __device__ __forceinline__ void ns_square_mc_rb(char *sX, char *sG, const MuonAr
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
-        // the whole X' (every block's rows, padding columns zero) into the LDS image
+        MUON_TP(args);
+        // the whole X' (every block's rows, padding columns zero) into the LDS image: every load in
+        // flight before the first LDS store (one L2 round trip, not one per 16 KB)
         const char *src = xg + (it & 1) * N * P;
-        for (int o = tid * 16; o < N * P; o += kMuonThreads * 16)
-            *reinterpret_cast<uint4 *>(sX + o) = *reinterpret_cast<const uint4 *>(src + o);
+        constexpr int kCopy = (N * P / 16 + kMuonThreads - 1) / kMuonThreads;
+        uint4 cv[kCopy];
+#pragma unroll
+        for (int u = 0; u < kCopy; u++) {
+            const int o = (tid + u * kMuonThreads) * 16;
+            cv[u] = o < N * P ? *reinterpret_cast<const uint4 *>(src + o) : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < kCopy; u++) {
+            const int o = (tid + u * kMuonThreads) * 16;
+            if (o < N * P) *reinterpret_cast<uint4 *>(sX + o) = cv[u];
+        }
         __syncthreads();
+        MUON_TP(args);
     }
 }
 
@@ -963,8 +1015,10 @@ __device__ __forceinline__ float block_clip_coef(const MuonArgs &args, int tid, 
 
 __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    if ((int)blockIdx.x >= args.njobs) {  // the 1-D parameters' AdamW, in the same launch
-        adam_blocks(args, (int)blockIdx.x - args.njobs, args.nadam);
+    const uint8_t role = args.job_mat[blockIdx.x];
+    if (role == kRoleIdle) return;
+    if (role == kRoleAdam) {  // the 1-D parameters' AdamW, in the same launch
+        adam_blocks(args, args.job_part[blockIdx.x], args.nadam);
         return;
     }
     const int mat = args.job_mat[blockIdx.x], part = args.job_part[blockIdx.x], np = args.job_nparts[blockIdx.x];
@@ -978,6 +1032,7 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     char *zero = sG + ((r * pg + 127) & ~127);  // 64 zero bytes
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ti0 = (wave & 3) * kBI, tj0 = (wave >> 2) * kBJ;  // wave-uniform
+    MUON_TP(args);
     __shared__ float red[kMuonThreads / 64];
     __shared__ float s_norm;
     // zero both images (their K padding must read as zero) and the zero block
@@ -988,10 +1043,14 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     __syncthreads();
 
     const float coef = block_clip_coef(args, tid, blockIdx.x == 0);
+    MUON_TP(args);
     // a multi-CU part (square: tr false) owns the momentum / parameter rows of its tile rows
     const int NT = (r + 15) >> 4;
     const int own0 = np > 1 ? 16 * (part * NT / np) : 0, own1 = np > 1 ? 16 * ((part + 1) * NT / np) : R;
-    float ss = muon_prologue(mt.grad, mt.mom, sX, px, R, C, tr, coef, args.momentum, args.nesterov != 0, tid, own0, own1);
+    // (multi-CU: no momentum write-back here -- the other parts may not have read those rows yet)
+    float ss = muon_prologue(mt.grad, mt.mom, sX, px, R, C, tr, coef, args.momentum, args.nesterov != 0, tid,
+                             np > 1 ? 0 : own0, np > 1 ? 0 : own1);
+    MUON_TP(args);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
     if (lane == 0) red[wave] = ss;
@@ -1003,14 +1062,39 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     }
     __syncthreads();
     const float nrm = s_norm;
-    // X /= ||X|| over the flat image (the zero padding stays zero): 4 elements per access
-    for (int e4 = tid; e4 < (r * px) >> 3; e4 += kMuonThreads) {
-        uint2 *p = reinterpret_cast<uint2 *>(sX) + e4;
-        const uint2 w = *p;
-        *p = make_uint2(pack_bf2(bf2f(w.x & 0xFFFFu) / nrm, bf2f(w.x >> 16) / nrm),
-                        pack_bf2(bf2f(w.y & 0xFFFFu) / nrm, bf2f(w.y >> 16) / nrm));
+    // X /= ||X|| over the flat image (the zero padding stays zero): 4 elements per access.  The
+    // quotient of the uniform divisor: q0 = y (1/nrm), one fma residual, one fma correction -- the
+    // correctly rounded fp32 y / nrm for every pair of bf16 operands (all 128 x 128 significand
+    // pairs checked exactly, tools/check_bf16_division.py), zeros passed through with their sign
+    const float inv = 1.0f / nrm;
+    auto qdiv = [&](float y) {
+        const float q0 = y * inv;
+        const float q = __builtin_fmaf(__builtin_fmaf(-q0, nrm, y), inv, q0);
+        return y == 0.0f ? y : q;
+    };
+    {  // four 8-byte groups per thread in flight per pass (one LDS round trip per pass, not per group)
+        const int n8 = (r * px) >> 3;
+        uint2 *img = reinterpret_cast<uint2 *>(sX);
+        for (int e0 = tid; e0 < n8; e0 += 4 * kMuonThreads) {
+            uint2 w[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int e = e0 + u * kMuonThreads;
+                w[u] = e < n8 ? img[e] : make_uint2(0u, 0u);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int e = e0 + u * kMuonThreads;
+                if (e < n8)
+                    img[e] = make_uint2(pack_bf2(qdiv(bf2f(w[u].x & 0xFFFFu)), qdiv(bf2f(w[u].x >> 16))),
+                                        pack_bf2(qdiv(bf2f(w[u].y & 0xFFFFu)), qdiv(bf2f(w[u].y >> 16))));
+            }
+        }
     }
     __syncthreads();
+    MUON_TP(args);
+    gu32_t *pro = np > 1 ? (gu32_t *)(args.sync + 16 * mat + 3) : nullptr;  // parts done reading the momentum
+    if (pro && tid == 0) __hip_atomic_fetch_add(pro, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
     // Newton-Schulz, three products per iteration, all through ONE gemm/store code path:
     //   0: G = X X^T                      (A = X rows, B^T = X rows; G symmetric)
@@ -1054,6 +1138,23 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     const float lr = args.lr[mt.lr_index];
     const float step = lr * (0.2f * sqrtf((float)(R > C ? R : C)));
     muon_epilogue(mt.param, mt.pbf, sX, px, R, C, tr, 1.0f - lr * args.wd, step, tid, own0, own1);
+    if (pro) {  // this part's momentum rows, once every part has read the old ones
+        if (wave == 0) mc_wait(pro, (uint32_t)np, (gu32_t *)(args.sync + 16 * mat + 1));
+        __syncthreads();
+        muon_momentum_rows(mt.grad, mt.mom, C, coef, args.momentum, args.nesterov != 0, own0, min(own1, R), tid);
+        // the last part through here puts the matrix's counters back to zero for the next launch
+        // (no memset node per step): every other part has finished all its polls when it counts in
+        if (tid == 0) {
+            gu32_t *ctr = (gu32_t *)(args.sync + 16 * mat), *done = (gu32_t *)(args.sync + 16 * mat + 2);
+            if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(np - 1)) {
+                __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(pro, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    __syncthreads();
+    MUON_TP(args);
 }
 
 __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
@@ -1094,7 +1195,8 @@ int g2048_grad_clip(g2048_stream_t stream, const float *grad, int64_t n, float m
 }
 
 size_t g2048_muon_workspace_bytes(void) {
-    return (size_t)kMuonSyncBytes + (size_t)kMuonMaxMats * 2 * max(196 * muon_pitch(196, 196), 192 * muon_pitch(192, 192));
+    return (size_t)kMuonSyncBytes + (size_t)kMuonMaxMats * 2 * max(196 * muon_pitch(196, 196), 192 * muon_pitch(192, 192)) +
+           kMuonTraceBytes;
 }
 
 int g2048_muon_supported(int32_t rows, int32_t cols) {
@@ -1183,39 +1285,74 @@ static int muon_launch(g2048_stream_t stream, const g2048_muon_matrix *mats, int
     a.norm_out = norm_out;
     a.coef_out = coef_out;
     a.generic_ns = getenv("G2048_MUON_GENERIC") ? 1 : 0;
-    // blocks: one per matrix, or cfg->parts per h = 196 / 192 square matrix with a workspace
+    // blocks: one per matrix, or cfg->parts (7 .. 13, at most one per 16-row tile row) per h = 196 /
+    // 192 square matrix with a workspace.  Placement (speed only: the hand-off is agent-scope): the
+    // parts of split matrix k sit on blocks k, k + 8, k + 16, ... -- one XCD under the round-robin
+    // dispatch, so their exchange images are read from that XCD's L2; the other matrices and the
+    // AdamW blocks fill the remaining slots in order, the rest of the grid idles.
     const int parts = cfg->workspace && !a.generic_ns && !getenv("G2048_MUON_ONE_CU") ? cfg->parts : 1;
-    if (parts > 1 && (parts < 7 || parts > 12)) return G2048_EINVAL;  // one or two tile rows per block
-    int nj = 0;
-    for (int i = 0; i < count; i++) {
-        const g2048_muon_matrix &m = mats[i];
-        const bool split = parts > 1 && m.rows == m.cols && (m.rows == 196 || m.rows == 192);
-        const int np = split ? parts : 1;
-        if (nj + np > kMuonMaxJobs) return G2048_EINVAL;
-        for (int p = 0; p < np; p++) {
-            a.job_mat[nj] = (uint8_t)i;
-            a.job_part[nj] = (uint8_t)p;
-            a.job_nparts[nj] = (uint8_t)np;
-            nj++;
-        }
-    }
-    a.njobs = nj;
-    if (parts > 1) {
-        char *ws = static_cast<char *>(cfg->workspace);
-        a.sync = reinterpret_cast<uint32_t *>(ws);
-        a.xg = ws + kMuonSyncBytes;
-        a.xg_stride = 2 * (int64_t)max(196 * muon_pitch(196, 196), 192 * muon_pitch(192, 192));
-        const hipError_t e = hipMemsetAsync(ws, 0, kMuonSyncBytes, (hipStream_t)stream);  // the counters, every call
-        if (e != hipSuccess) return (int)e;
-    }
+    if (parts > 1 && (parts < 7 || parts > 13)) return G2048_EINVAL;  // one or two tile rows per block
     if (adam) {  // AdamW blocks: ~2 elements per thread, at most 8 blocks
-        a.adam = *adam;
         int64_t nmax = 0;
         for (int k = 0; k < adam->count; k++) nmax = adam->g[k].n > nmax ? adam->g[k].n : nmax;
         const int64_t nb = (nmax + 2 * kMuonThreads - 1) / (2 * kMuonThreads);
         a.nadam = (int)(nb < 1 ? 1 : (nb > 8 ? 8 : nb));
     }
-    hipLaunchKernelGGL(muon_kernel, dim3(a.njobs + a.nadam), dim3(kMuonThreads), lds, (hipStream_t)stream, a);
+    for (int b = 0; b < kMuonMaxJobs; b++) a.job_mat[b] = kRoleIdle;
+    int nsplit = 0, grid = 0;
+    for (int i = 0; i < count; i++) {  // split matrices first: their XCD columns
+        const g2048_muon_matrix &m = mats[i];
+        if (!(parts > 1 && m.rows == m.cols && (m.rows == 196 || m.rows == 192))) continue;
+        const int nt = (m.rows + 15) / 16, np = parts < nt ? parts : nt;
+        for (int p = 0; p < np; p++) {
+            const int b = nsplit < 8 ? nsplit + 8 * p : -1;
+            if (b < 0 || b >= kMuonMaxJobs) return G2048_EINVAL;
+            a.job_mat[b] = (uint8_t)i;
+            a.job_part[b] = (uint8_t)p;
+            a.job_nparts[b] = (uint8_t)np;
+            grid = b + 1 > grid ? b + 1 : grid;
+        }
+        nsplit++;
+    }
+    int next = 0;
+    auto free_slot = [&]() {
+        while (next < kMuonMaxJobs && a.job_mat[next] != kRoleIdle) next++;
+        return next < kMuonMaxJobs ? next++ : -1;
+    };
+    for (int i = 0; i < count; i++) {  // one-block matrices
+        const g2048_muon_matrix &m = mats[i];
+        if (parts > 1 && m.rows == m.cols && (m.rows == 196 || m.rows == 192)) continue;
+        const int b = free_slot();
+        if (b < 0) return G2048_EINVAL;
+        a.job_mat[b] = (uint8_t)i;
+        a.job_part[b] = 0;
+        a.job_nparts[b] = 1;
+        grid = b + 1 > grid ? b + 1 : grid;
+    }
+    for (int k = 0; k < (adam ? a.nadam : 0); k++) {
+        const int b = free_slot();
+        if (b < 0) return G2048_EINVAL;
+        a.job_mat[b] = kRoleAdam;
+        a.job_part[b] = (uint8_t)k;
+        grid = b + 1 > grid ? b + 1 : grid;
+    }
+    a.njobs = grid;
+    if (parts > 1) {  // the counters: zero from the caller's first fill, left zero by every launch
+        char *ws = static_cast<char *>(cfg->workspace);
+        a.sync = reinterpret_cast<uint32_t *>(ws);
+        a.xg = ws + kMuonSyncBytes;
+        a.xg_stride = 2 * (int64_t)max(196 * muon_pitch(196, 196), 192 * muon_pitch(192, 192));
+    }
+#ifdef MUON_TRACE
+    if (cfg->workspace) {
+        a.trace = reinterpret_cast<uint64_t *>(static_cast<char *>(cfg->workspace) + kMuonSyncBytes +
+                                               (size_t)kMuonMaxMats * 2 * max(196 * muon_pitch(196, 196), 192 * muon_pitch(192, 192)));
+        const hipError_t e = hipMemsetAsync(a.trace, 0, kMuonTraceBytes, (hipStream_t)stream);
+        if (e != hipSuccess) return (int)e;
+    }
+#endif
+    if (adam) a.adam = *adam;
+    hipLaunchKernelGGL(muon_kernel, dim3(a.njobs), dim3(kMuonThreads), lds, (hipStream_t)stream, a);
     return status();
 }
 

@@ -40,9 +40,11 @@
 using namespace g2048::tile;
 namespace P = g2048::ppo;
 
-static_assert(sizeof(g2048_mlp_pass_args) == 408 && offsetof(g2048_mlp_pass_args, drop) == 176 &&
-                  offsetof(g2048_mlp_pass_args, partials) == 400,
+static_assert(sizeof(g2048_mlp_pass_args) == 416 && offsetof(g2048_mlp_pass_args, drop) == 176 &&
+                  offsetof(g2048_mlp_pass_args, partials) == 400 && offsetof(g2048_mlp_pass_args, keep) == 408,
               "g2048_mlp_pass_args layout (tests/test_abi.py)");
+static_assert(sizeof(g2048_mlp_back_args) == 312 && offsetof(g2048_mlp_back_args, keep) == 304,
+              "g2048_mlp_back_args layout (tests/test_abi.py)");
 
 namespace {
 
@@ -54,12 +56,6 @@ namespace {
 #endif
 #ifndef FP_LUNROLL
 #define FP_LUNROLL 0
-#endif
-#ifndef BP_WAVES
-#define BP_WAVES 8
-#endif
-#ifndef BP_HOLD  // 1: the backward holds each feature tile's masked gradient between its two passes
-#define BP_HOLD (BP_WAVES == 4)
 #endif
 constexpr int kFpThreads = 64 * FP_WAVES;  // 8 waves = 2 per SIMD sharing the one LDS weight image (one block per CU)
 constexpr int kFpLdsMax = 163840;
@@ -89,6 +85,7 @@ struct FpArgs {
     float *dz;                     // train: fp32 [m][8]
     uint16_t *dzb;                 // train: bf16 [m][16]: hi(dz) 0..4, lo(dz) 8..12
     float *part;                   // per block: train kTrainParts floats, KL {sum, max}
+    uint2 *keep;                   // train, optional: the blocks' keep bits [block][m][lane group]
 };
 
 // The head matrix [wa (4 rows); wv] as three exact bf16 terms in the 16 rows of the head chain's A
@@ -325,6 +322,10 @@ __global__ __launch_bounds__(kFpThreads) void mlp_pass_kernel(FpArgs a) {
 #pragma unroll
                 for (int q = 0; q < kFpQ; q++) {
                     FP_EPILOGUE(l + 1, q, true, DROP);
+                    if (TRAIN && DROP && a.keep) {  // for the backward: bit 4 n + e = feature 16 n + 4 g + e
+                        const int64_t row = r0 + 16 * (kFpQ * pr + q) + col;
+                        if (row < m) a.keep[((int64_t)l * m + row) * 4 + g] = make_uint2(kb[q][0], kb[q][1]);
+                    }
                     kb[q][0] = kb[q][1] = 0u;
                 }
             }
@@ -434,7 +435,7 @@ __global__ __launch_bounds__(kFpThreads) void mlp_pass_kernel(FpArgs a) {
 // another order: per tile and layer a 16-lane reduce-scatter (DPP mirror / half-mirror / quad
 // swaps) leaves lane c one of its feature group's 8 sums (4 dgamma, 4 dbeta), accumulated per lane
 // -- 3 x NT registers instead of ln_bwd196's 8 NT per layer.
-constexpr int kBpThreads = 64 * BP_WAVES;  // 8 waves = 2 per SIMD (256 registers each); one block per CU (LDS)
+constexpr int kBpThreads = 256;  // 4 waves (1 per SIMD: 512 registers for the whole chain); one block per CU (LDS)
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
@@ -450,6 +451,7 @@ struct BpArgs {
     uint16_t *dg[kMaxLayers];  // out bf16 [m][h]
     uint16_t *pout[2];        // optional out bf16 [m][h]: P1, P2
     float *part;              // out [layer][block][2 h]: dgamma | dbeta
+    const uint2 *keep;        // optional: the train pass's keep bits [block][m][4] (else re-drawn)
 };
 
 // Sum of v[0..7] over the 16 lanes of a DPP row, scattered: lane c ends with the sum of
@@ -474,44 +476,32 @@ __device__ __forceinline__ float row16_scatter8(const float (&v)[8], int c) {
     return h1 + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(h1), 0xB1, 0xF, 0xF, false));
 }
 
-// Sum of v[0..15] over the 16 lanes of a DPP row, scattered: lane c ends with the sum of v[c] (the
-// same four butterfly stages as row16_scatter8 with a selecting last stage).
-__device__ __forceinline__ float row16_scatter16(const float (&v)[16], int c) {
-    const bool b3 = (c & 8) != 0, b2 = (c & 4) != 0, b1 = (c & 2) != 0, b0 = (c & 1) != 0;
-    float h8[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {  // row_mirror (bit 3 differs)
-        const float keep = b3 ? v[8 + j] : v[j], send = b3 ? v[j] : v[8 + j];
-        h8[j] = keep + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(send), 0x140, 0xF, 0xF, false));
-    }
-    float h4[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {  // row_half_mirror (bit 2)
-        const float keep = b2 ? h8[4 + j] : h8[j], send = b2 ? h8[j] : h8[4 + j];
-        h4[j] = keep + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(send), 0x141, 0xF, 0xF, false));
-    }
-    float h2[2];
-#pragma unroll
-    for (int j = 0; j < 2; j++) {  // quad_perm 3,2,1,0 (bit 1)
-        const float keep = b1 ? h4[2 + j] : h4[j], send = b1 ? h4[j] : h4[2 + j];
-        h2[j] = keep + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(send), 0x1B, 0xF, 0xF, false));
-    }
-    const float keep = b0 ? h2[1] : h2[0], send = b0 ? h2[0] : h2[1];  // quad_perm 1,0,3,2 (bit 0)
-    return keep + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(send), 0xB1, 0xF, 0xF, false));
-}
+#ifndef BP_PK  // 1: the backward's LayerNorm pairs as packed fp32 (v_pk_*: few MFMAs beside them here)
+#define BP_PK 1
+#endif
+#if BP_PK
+typedef float bp2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bp2 bp_fma(bp2 a, bp2 b, bp2 c) { return __builtin_elementwise_fma(a, b, c); }
+#else
+using bp2 = g2048::lnrow::f32x2;
+__device__ __forceinline__ bp2 bp_fma(bp2 a, bp2 b, bp2 c) { return g2048::lnrow::fma2(a, b, c); }
+#endif
+
+// dropout source of a block layer's backward: none, Philox re-draws, the train pass's stored keep bits
+enum { kDmNone = 0, kDmDraw = 1, kDmBits = 2 };
 
 // One layer's LayerNorm / ReLU / Dropout backward on the lane's tile row (ln_bwd196's two passes):
 // dy = heads' share + P sources in order; dG rounded to bf16 into dgb (zero past h) and stored;
-// the dgamma / dbeta partial sums of the tile go to gb[n].  The masked output gradient of a feature
-// tile (dy times the ReLU and dropout masks) is computed in BOTH passes instead of being held
-// between them (52 registers: the kernel runs two waves per SIMD); the dropout multipliers come from
-// keep bits drawn ahead (kb, ppo::drop_keep8), the same values as the Philox-in-place form.
-template <int NT, int H, bool DROP, int NP>
+// the dgamma / dbeta partial sums of the tile go to gb[n].  The masked output gradient of each
+// feature tile is held between the passes (52 registers: one wave per SIMD).  The keep multipliers
+// (DM): Philox re-draws (one call per tile pair, as the per-layer kernels), or the train pass's
+// stored keep bits kw (bit 4 n + e of kw.x | kw.y << 32: ppo::keep_mult) -- the same values.
+template <int NT, int H, int DM, int NP>
 __device__ __forceinline__ void bp_layer(const uint16_t *__restrict__ gsrc, float mu, float rs, const float *sgm,
                                          const float *sbt, const float (&wh)[NT][2], float b0, float b1,
-                                         const uint2 *const (&pr)[NP > 0 ? NP : 1], float scale,
-                                         const uint32_t (&kb)[2], bool live, int gq, int col, uint2 (&dgb)[NT],
-                                         uint16_t *dgout, float (&gb)[(NT + 1) / 2]) {
+                                         const uint2 *const (&pr)[NP > 0 ? NP : 1], const P::Drop &d, uint32_t rowu,
+                                         uint2 kw, bool live, int gq, int col, uint2 (&dgb)[NT], uint16_t *dgout,
+                                         float (&gb)[NT]) {
     namespace R = g2048::lnrow;
     constexpr float inv_h = 1.0f / (float)H;
     const bool lastok = 16 * (NT - 1) + 4 * gq < H;
@@ -519,9 +509,13 @@ __device__ __forceinline__ void bp_layer(const uint16_t *__restrict__ gsrc, floa
     uint2 gr[NT];
 #pragma unroll
     for (int n = 0; n < NT; n++) gr[n] = *reinterpret_cast<const uint2 *>(gsrc + 16 * n + 4 * gq * valid(n));
-    const R::f32x2 nmu = {-mu, -mu}, rs2 = {rs, rs};
-    // feature tile n: xhat pairs, the masked output gradient pairs, gamma
-    auto dtile = [&](int n, R::f32x2 &xh0, R::f32x2 &xh1, R::f32x2 &d0, R::f32x2 &d1, float4 &gm) {
+    bp2 dzr[NT][2];
+    bp2 s1 = {0.0f, 0.0f}, s2 = {0.0f, 0.0f};
+    const bp2 nmu = {-mu, -mu}, rs2 = {rs, rs};
+    const uint32_t kb[2] = {kw.x, kw.y};
+    uint4 dpair = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int n = 0; n < NT; n++) {
         const int f0 = 16 * n + 4 * gq;
         f32x4_t dy = {0.0f, 0.0f, 0.0f, 0.0f};
         dy = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[n][0], b0, dy, 0, 0, 0);
@@ -534,89 +528,56 @@ __device__ __forceinline__ void bp_layer(const uint16_t *__restrict__ gsrc, floa
             t[2] += R::bf_lo(pr[i][n].y);
             t[3] += R::bf_hi(pr[i][n].y);
         }
-        gm = *reinterpret_cast<const float4 *>(sgm + f0);
+        const float4 gm = *reinterpret_cast<const float4 *>(sgm + f0);
         const float4 bt = *reinterpret_cast<const float4 *>(sbt + f0);
-        xh0 = (R::f32x2{R::bf_lo(gr[n].x), R::bf_hi(gr[n].x)} + nmu) * rs2;
-        xh1 = (R::f32x2{R::bf_lo(gr[n].y), R::bf_hi(gr[n].y)} + nmu) * rs2;
-        const R::f32x2 z0 = R::fma2(xh0, R::f32x2{gm.x, gm.y}, R::f32x2{bt.x, bt.y});
-        const R::f32x2 z1 = R::fma2(xh1, R::f32x2{gm.z, gm.w}, R::f32x2{bt.z, bt.w});
+        const bp2 xh0 = (bp2{R::bf_lo(gr[n].x), R::bf_hi(gr[n].x)} + nmu) * rs2;
+        const bp2 xh1 = (bp2{R::bf_lo(gr[n].y), R::bf_hi(gr[n].y)} + nmu) * rs2;
+        const bp2 z0 = bp_fma(xh0, bp2{gm.x, gm.y}, bp2{bt.x, bt.y});
+        const bp2 z1 = bp_fma(xh1, bp2{gm.z, gm.w}, bp2{bt.z, bt.w});
         const bool on = live && valid(n);
         float k[4] = {1.0f, 1.0f, 1.0f, 1.0f};
-        if (DROP) P::keep_mult(kb, n, scale, k);
-        d0 = R::f32x2{(on && z0.x > 0.0f) ? t[0] * k[0] : 0.0f, (on && z0.y > 0.0f) ? t[1] * k[1] : 0.0f};
-        d1 = R::f32x2{(on && z1.x > 0.0f) ? t[2] * k[2] : 0.0f, (on && z1.y > 0.0f) ? t[3] * k[3] : 0.0f};
-    };
-    R::f32x2 s1 = {0.0f, 0.0f}, s2 = {0.0f, 0.0f};
-    float v16[16];  // tiles n (even slots) and n + 1 (odd): [d xhat 0..3 | d 0..3] each
-    R::f32x2 dzr[BP_HOLD ? NT : 1][2];
-#pragma unroll
-    for (int n = 0; n < NT; n++) {
-        R::f32x2 xh0, xh1, d0, d1;
-        float4 gm;
-        dtile(n, xh0, xh1, d0, d1, gm);
-        if (BP_HOLD) {
-            dzr[n][0] = d0;
-            dzr[n][1] = d1;
+        if (DM == kDmDraw) {
+            if ((n & 1) == 0) dpair = P::drop_draw4(d, rowu, (uint32_t)(f0 >> 2));
+            P::drop_mult_bits(d, P::drop_half(dpair, (uint32_t)(f0 >> 2)), k);
+        } else if (DM == kDmBits) {
+            P::keep_mult(kb, n, d.scale, k);
         }
+        const bp2 d0 = {(on && z0.x > 0.0f) ? t[0] * k[0] : 0.0f, (on && z0.y > 0.0f) ? t[1] * k[1] : 0.0f};
+        const bp2 d1 = {(on && z1.x > 0.0f) ? t[2] * k[2] : 0.0f, (on && z1.y > 0.0f) ? t[3] * k[3] : 0.0f};
+        dzr[n][0] = d0;
+        dzr[n][1] = d1;
         const float v8[8] = {d0.x * xh0.x, d0.y * xh0.y, d1.x * xh1.x, d1.y * xh1.y, d0.x, d0.y, d1.x, d1.y};
-#pragma unroll
-        for (int j = 0; j < 8; j++) v16[2 * j + (n & 1)] = v8[j];
-        if ((n & 1) == 1 || n == NT - 1) {
-            if ((n & 1) == 0)
-#pragma unroll
-                for (int j = 0; j < 8; j++) v16[2 * j + 1] = 0.0f;
-            gb[n >> 1] += row16_scatter16(v16, col);
-        }
-        const R::f32x2 x0 = d0 * R::f32x2{gm.x, gm.y}, x1 = d1 * R::f32x2{gm.z, gm.w};  // dxhat
+        gb[n] += row16_scatter8(v8, col);
+        const bp2 x0 = d0 * bp2{gm.x, gm.y}, x1 = d1 * bp2{gm.z, gm.w};  // dxhat
         s1 = s1 + x0 + x1;
-        s2 = R::fma2(x1, xh1, R::fma2(x0, xh0, s2));
-        __builtin_amdgcn_sched_barrier(0);  // one feature tile at a time (registers; the other wave overlaps)
+        s2 = bp_fma(x1, xh1, bp_fma(x0, xh0, s2));
     }
     const float m1 = R::xor32_add(R::xor16_add(s1.x + s1.y)) * inv_h;
     const float m2 = R::xor32_add(R::xor16_add(s2.x + s2.y)) * inv_h;
-    const R::f32x2 nm1 = {-m1, -m1}, nm2 = {-m2, -m2};
-    if (!BP_HOLD) {
-        // opaque inputs: the compiler would otherwise keep pass 1's tiles (and LDS loads) live instead
-        // of recomputing / re-reading them
-        asm volatile("" : "+v"(b0), "+v"(b1), "+v"(sgm), "+v"(sbt));
-#pragma unroll
-        for (int n = 0; n < NT; n++) asm volatile("" : "+v"(gr[n].x), "+v"(gr[n].y));
-    }
+    const bp2 nm1 = {-m1, -m1}, nm2 = {-m2, -m2};
 #pragma unroll
     for (int n = 0; n < NT; n++) {
         const int f0 = 16 * n + 4 * gq;
-        R::f32x2 xh0, xh1, d0, d1;
-        float4 gm;
-        if (BP_HOLD) {
-            gm = *reinterpret_cast<const float4 *>(sgm + f0);
-            xh0 = (R::f32x2{R::bf_lo(gr[n].x), R::bf_hi(gr[n].x)} + nmu) * rs2;
-            xh1 = (R::f32x2{R::bf_lo(gr[n].y), R::bf_hi(gr[n].y)} + nmu) * rs2;
-            d0 = dzr[n][0];
-            d1 = dzr[n][1];
-        } else {
-            dtile(n, xh0, xh1, d0, d1, gm);
-        }
-        const R::f32x2 o0 = R::fma2(xh0, nm2, R::fma2(d0, R::f32x2{gm.x, gm.y}, nm1)) * rs2;
-        const R::f32x2 o1 = R::fma2(xh1, nm2, R::fma2(d1, R::f32x2{gm.z, gm.w}, nm1)) * rs2;
+        const float4 gm = *reinterpret_cast<const float4 *>(sgm + f0);
+        const bp2 xh0 = (bp2{R::bf_lo(gr[n].x), R::bf_hi(gr[n].x)} + nmu) * rs2;
+        const bp2 xh1 = (bp2{R::bf_lo(gr[n].y), R::bf_hi(gr[n].y)} + nmu) * rs2;
+        const bp2 o0 = bp_fma(xh0, nm2, bp_fma(dzr[n][0], bp2{gm.x, gm.y}, nm1)) * rs2;
+        const bp2 o1 = bp_fma(xh1, nm2, bp_fma(dzr[n][1], bp2{gm.z, gm.w}, nm1)) * rs2;
         dgb[n] = valid(n) ? make_uint2(R::pack_bf2(o0.x, o0.y), R::pack_bf2(o1.x, o1.y)) : make_uint2(0u, 0u);
         if (live && valid(n)) *reinterpret_cast<uint2 *>(dgout + f0) = dgb[n];
-        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
 // P^T tile chain of one block layer: p[n] = bf16(sum_ks W^T[16 n ..][k-step ks] dG^T) -- the
 // dgrad kernel's k order from zero.  A = W^T by two transposing reads of the row-major image
 // (lane (g, q, p): rows 32 ks + 8 g + q and + 4, columns 16 n + 4 p); k-step rows past h are
-// redirected to row 0 (their B is zero: dG past h is zero).  DRAW: beside k-step ks's MFMAs, the
-// keep bits of feature-tile pair ks of dropout `d` for row `drow` (the next layer's masks).
-template <int NT, int H, int KS, int PW, bool DRAW>
-__device__ __forceinline__ void bp_dgrad(const char *wimg, const uint2 (&dgb)[NT], int lane, uint2 (&pout)[NT],
-                                         const P::Drop &d, uint32_t drow, uint32_t (&kb)[2]) {
+// redirected to row 0 (their B is zero: dG past h is zero).
+template <int NT, int H, int KS, int PW>
+__device__ __forceinline__ void bp_dgrad(const char *wimg, const uint2 (&dgb)[NT], int lane, uint2 (&pout)[NT]) {
     const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
     f32x4_t acc[NT];
 #pragma unroll
     for (int n = 0; n < NT; n++) acc[n] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-    if (DRAW) kb[0] = kb[1] = 0u;
 #pragma unroll
     for (int ks = 0; ks < KS; ks++) {
         const uint4 bf = act_frag<NT>(dgb, ks);
@@ -624,7 +585,6 @@ __device__ __forceinline__ void bp_dgrad(const char *wimg, const uint2 (&dgb)[NT
         const int ra = r1 < H ? r1 : 0, rb = r1 + 4 < H ? r1 + 4 : 0;
         int oa = ra * PW + 8 * p4, ob = rb * PW + 8 * p4;
         asm volatile("" : "+v"(oa), "+v"(ob));
-        if (DRAW && 2 * ks < NT) kb[ks >> 2] |= P::drop_keep8(d, drow, (uint32_t)(8 * ks + g)) << (8 * (ks & 3));
 #pragma unroll
         for (int n = 0; n < NT; n++) {
             const s16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(wimg + oa + 32 * n));
@@ -637,16 +597,8 @@ __device__ __forceinline__ void bp_dgrad(const char *wimg, const uint2 (&dgb)[NT
     for (int n = 0; n < NT; n++) pout[n] = make_uint2(pack_bf2(acc[n][0], acc[n][1]), pack_bf2(acc[n][2], acc[n][3]));
 }
 
-// keep bits of all feature tiles of dropout `d` for row `row` (the first tile's top block)
-template <int NT>
-__device__ __forceinline__ void draw_keep(const P::Drop &d, uint32_t row, int g, uint32_t (&kb)[2]) {
-    kb[0] = kb[1] = 0u;
-#pragma unroll
-    for (int ks = 0; 2 * ks < NT; ks++) kb[ks >> 2] |= P::drop_keep8(d, row, (uint32_t)(8 * ks + g)) << (8 * (ks & 3));
-}
-
-template <int H, bool DROP>
-__global__ __launch_bounds__(kBpThreads) void mlp_back_kernel(BpArgs a) {
+template <int H, int DM>
+__global__ __launch_bounds__(kBpThreads, 1) void mlp_back_kernel(BpArgs a) {
     constexpr int NT = (H + 15) / 16, KS = ((H + 7) / 8 * 8 + 31) / 32;
     constexpr int PW = pr_pitch(H), WB = pr_wbytes(H);
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -690,56 +642,47 @@ __global__ __launch_bounds__(kBpThreads) void mlp_back_kernel(BpArgs a) {
     }
     __syncthreads();
     const P::Drop d1 = P::make_drop(a.drop[0]), d2 = P::make_drop(a.drop[1]);
-    constexpr int NG = (NT + 1) / 2;  // dgamma / dbeta sums per layer and lane: tile pair n >> 1, slot col
-    float gb[kMaxLayers][NG];
+    float gb[kMaxLayers][NT];
 #pragma unroll
     for (int l = 0; l < kMaxLayers; l++)
 #pragma unroll
-        for (int n = 0; n < NG; n++) gb[l][n] = 0.0f;
+        for (int n = 0; n < NT; n++) gb[l][n] = 0.0f;
     const int64_t ntile = (m + 15) >> 4;
-    constexpr int kW = kBpThreads / 64;
-    const int64_t tstride = (int64_t)gridDim.x * kW;
-    // dropout keep bits: the top block's for the wave's first tile now, then each tile's block-1 bits
-    // beside its P2 chain and the NEXT tile's top-block bits beside its P1 chain
-    uint32_t kb2[2] = {0u, 0u}, kb1[2] = {0u, 0u};
-    {
-        const int64_t t0 = (int64_t)blockIdx.x * kW + wave, r = 16 * t0 + col;
-        if (DROP && t0 < ntile) draw_keep<NT>(d2, (uint32_t)(r < m ? r : 0), gq, kb2);
-    }
-    for (int64_t tile = (int64_t)blockIdx.x * kW + wave; tile < ntile; tile += tstride) {
+    for (int64_t tile = (int64_t)blockIdx.x * (kBpThreads / 64) + wave; tile < ntile;
+         tile += (int64_t)gridDim.x * (kBpThreads / 64)) {
         const int64_t row = 16 * tile + col;
         const bool live = row < m;
         const int64_t rc = live ? row : 0;
         const uint32_t rowu = (uint32_t)rc;
-        const int64_t rn = 16 * (tile + tstride) + col;  // the next tile's row (its top-block masks)
-        const uint32_t rnu = (uint32_t)(rn < m ? rn : 0);
-        // an opaque base: the LayerNorm affines are re-read per tile, not hoisted into registers
-        int lnoff = 0;
-        asm volatile("" : "+v"(lnoff));
-        const float *sLNr = sLN + lnoff;
         const float b0 = a.dz[rc * 8 + gq];
         const float b1 = gq == 0 ? a.dz[rc * 8 + 4] : 0.0f;
+        uint2 kw1 = make_uint2(0u, 0u), kw2 = make_uint2(0u, 0u);
+        if (DM == kDmBits) {  // [block][row][lane group]: the train pass's keep bits of this row
+            kw1 = a.keep[rc * 4 + gq];
+            kw2 = a.keep[(m + rc) * 4 + gq];
+        }
         uint2 dgb[NT], p2[NT], p1[NT];
         // block 2 (top): dy = the heads' share
         {
             const uint2 *pr[1] = {nullptr};
-            bp_layer<NT, H, DROP, 0>(a.g[2] + rc * H, a.mean[2][rc], a.rstd[2][rc], sLNr + 2 * 32 * NT,
-                                     sLNr + 2 * 32 * NT + 16 * NT, wh, b0, b1, pr, d2.scale, kb2, live, gq, col, dgb,
-                                     a.dg[2] + rc * H, gb[2]);
+            bp_layer<NT, H, DM, 0>(a.g[2] + rc * H, a.mean[2][rc], a.rstd[2][rc], sLN + 2 * 32 * NT,
+                                   sLN + 2 * 32 * NT + 16 * NT, wh, b0, b1, pr, d2, rowu, kw2, live, gq, col, dgb,
+                                   a.dg[2] + rc * H, gb[2]);
         }
-        bp_dgrad<NT, H, KS, PW, DROP>(smem + WB, dgb, lane, p2, d1, rowu, kb1);
+        bp_dgrad<NT, H, KS, PW>(smem + WB, dgb, lane, p2);
         if (a.pout[1] && live) store_tile<NT, H>(a.pout[1], (uint32_t)rc * (2u * H), p2, gq);
         {  // block 1: + P2
             const uint2 *pr[1] = {p2};
-            bp_layer<NT, H, DROP, 1>(a.g[1] + rc * H, a.mean[1][rc], a.rstd[1][rc], sLNr + 32 * NT, sLNr + 48 * NT,
-                                     wh, b0, b1, pr, d1.scale, kb1, live, gq, col, dgb, a.dg[1] + rc * H, gb[1]);
+            bp_layer<NT, H, DM, 1>(a.g[1] + rc * H, a.mean[1][rc], a.rstd[1][rc], sLN + 32 * NT, sLN + 48 * NT, wh,
+                                   b0, b1, pr, d1, rowu, kw1, live, gq, col, dgb, a.dg[1] + rc * H, gb[1]);
         }
-        bp_dgrad<NT, H, KS, PW, DROP>(smem, dgb, lane, p1, d2, rnu, kb2);
+        bp_dgrad<NT, H, KS, PW>(smem, dgb, lane, p1);
         if (a.pout[0] && live) store_tile<NT, H>(a.pout[0], (uint32_t)rc * (2u * H), p1, gq);
         {  // the stem: + P1 + P2 (the per-layer chain's source order), no dropout
             const uint2 *pr[2] = {p1, p2};
-            bp_layer<NT, H, false, 2>(a.g[0] + rc * H, a.mean[0][rc], a.rstd[0][rc], sLNr, sLNr + 16 * NT, wh, b0,
-                                      b1, pr, 1.0f, kb1, live, gq, col, dgb, a.dg[0] + rc * H, gb[0]);
+            bp_layer<NT, H, kDmNone, 2>(a.g[0] + rc * H, a.mean[0][rc], a.rstd[0][rc], sLN, sLN + 16 * NT,
+                                                  wh, b0, b1, pr, d1, rowu, kw1, live, gq, col, dgb, a.dg[0] + rc * H,
+                                                  gb[0]);
         }
     }
     // dgamma / dbeta: lane (gq, col) even col holds slot s = col >> 1 of its feature groups
@@ -747,15 +690,12 @@ __global__ __launch_bounds__(kBpThreads) void mlp_back_kernel(BpArgs a) {
     __syncthreads();
     float *red = reinterpret_cast<float *>(smem);  // [wave][layer][2][16 NT]
     constexpr int RW = kMaxLayers * 2 * 16 * NT;
-    {
+    if ((col & 1) == 0) {
         const int s = col >> 1, which = s >> 2, e = s & 3;
 #pragma unroll
         for (int l = 0; l < kMaxLayers; l++)
 #pragma unroll
-            for (int j = 0; j < NG; j++) {
-                const int n = 2 * j + (col & 1);
-                if (n < NT) red[wave * RW + (l * 2 + which) * 16 * NT + 16 * n + 4 * gq + e] = gb[l][j];
-            }
+            for (int n = 0; n < NT; n++) red[wave * RW + (l * 2 + which) * 16 * NT + 16 * n + 4 * gq + e] = gb[l][n];
     }
     __syncthreads();
     const int nb = gridDim.x;
@@ -855,6 +795,8 @@ int fp_fill(const g2048_mlp_pass_args *p, FpArgs &a, bool train) {
     a.dz = p->dz;
     a.dzb = (uint16_t *)p->dz_bf16;
     a.part = p->partials;
+    if (train && p->keep && !al(p->keep, 8)) return G2048_EINVAL;
+    a.keep = train ? (uint2 *)p->keep : nullptr;
     return G2048_OK;
 }
 
@@ -882,15 +824,15 @@ int bp_blocks(int64_t m) {
     return (int)(t < 1 ? 1 : (t > 256 ? 256 : t));
 }
 
-template <bool DROP>
+template <int DM>
 int bp_launch2(hipStream_t s, const BpArgs &a, int h, int nb) {
     const size_t lds = fp_lds(h);
     switch (h) {
-    case 196: hipLaunchKernelGGL((mlp_back_kernel<196, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
-    case 192: hipLaunchKernelGGL((mlp_back_kernel<192, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
-    case 128: hipLaunchKernelGGL((mlp_back_kernel<128, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
-    case 64: hipLaunchKernelGGL((mlp_back_kernel<64, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
-    case 32: hipLaunchKernelGGL((mlp_back_kernel<32, DROP>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    case 196: hipLaunchKernelGGL((mlp_back_kernel<196, DM>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    case 192: hipLaunchKernelGGL((mlp_back_kernel<192, DM>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    case 128: hipLaunchKernelGGL((mlp_back_kernel<128, DM>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    case 64: hipLaunchKernelGGL((mlp_back_kernel<64, DM>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
+    case 32: hipLaunchKernelGGL((mlp_back_kernel<32, DM>), dim3(nb), dim3(kBpThreads), lds, s, a); break;
     default: return G2048_EINVAL;
     }
     return fp_status();
@@ -967,13 +909,17 @@ int g2048_ppo_backward(g2048_stream_t stream, const g2048_mlp_back_args *p, floa
     a.drop[1] = P::drop_args(&p->drop[1]);
     if ((a.drop[0].thr != 0u) != (a.drop[1].thr != 0u)) return G2048_EINVAL;
     a.part = p->partials;
+    if (p->keep && !al(p->keep, 8)) return G2048_EINVAL;
+    a.keep = (const uint2 *)p->keep;
     for (int i = 0; i < 2; i++) {
         if (p->p_out[i] && !al(p->p_out[i], 8)) return G2048_EINVAL;
         a.pout[i] = (uint16_t *)p->p_out[i];
     }
     const hipStream_t s = (hipStream_t)stream;
     const int nb = bp_blocks(p->m);
-    const int rc = a.drop[0].thr != 0u ? bp_launch2<true>(s, a, h, nb) : bp_launch2<false>(s, a, h, nb);
+    const int rc = a.drop[0].thr == 0u ? bp_launch2<kDmNone>(s, a, h, nb)
+                   : a.keep        ? bp_launch2<kDmBits>(s, a, h, nb)
+                                   : bp_launch2<kDmDraw>(s, a, h, nb);
     if (rc) return rc;
     const int w = 2 * h;
     for (int l = 0; l < kMaxLayers; l++) {  // one column-sum job per layer: [dgamma | dbeta] rows of 2 h

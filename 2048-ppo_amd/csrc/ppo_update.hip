@@ -1659,36 +1659,71 @@ struct ColsumBatch {
     int njobs;
 };
 
+// a job whose partial rows are whole float4s runs 4 columns per lane (256 per block: 16-byte loads);
+// every column is summed in the same order either way (rows rg, rg + 16, ... per group, then the
+// 16 groups in order), so the two forms give the same bits
+__host__ __device__ inline bool colsum_vec(const g2048_colsum_job &jb) {
+    return jb.cols % 4 == 0 && ((uintptr_t)jb.part % 16) == 0;
+}
+
 __global__ __launch_bounds__(1024) void colsum_batch_kernel(const ColsumBatch cb) {
-    __shared__ float lds[16][64];
+    __shared__ float4 lds[16][64];
     int j = 0;
     while (j + 1 < cb.njobs && (int)blockIdx.x >= cb.first[j + 1]) j++;
     const g2048_colsum_job &jb = cb.job[j];
     const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-    const int c = ((int)blockIdx.x - cb.first[j]) * 64 + cl;
-    const bool is_max = c == jb.max_col;
-    float t = is_max ? -INFINITY : 0.0f;
-    if (c < jb.cols) {
-        const float *p = jb.part + c;
+    const bool vec = colsum_vec(jb);  // block-uniform
+    const int W = vec ? 4 : 1;
+    const int c0 = ((int)blockIdx.x - cb.first[j]) * 64 * W + cl * W;
+    float t[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) t[u] = c0 + u == jb.max_col ? -INFINITY : 0.0f;
+    if (c0 < jb.cols) {
+        const float *p = jb.part + c0;
+        if (vec) {
 #pragma unroll 4
-        for (int b = rg; b < jb.nb; b += 16) {
-            const float v = p[(int64_t)b * jb.cols];
-            t = is_max ? fmaxf(t, v) : t + v;
+            for (int b = rg; b < jb.nb; b += 16) {
+                const float4 v = *reinterpret_cast<const float4 *>(p + (int64_t)b * jb.cols);
+                const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int u = 0; u < 4; u++) t[u] = c0 + u == jb.max_col ? fmaxf(t[u], vv[u]) : t[u] + vv[u];
+            }
+        } else {
+#pragma unroll 4
+            for (int b = rg; b < jb.nb; b += 16) {
+                const float v = p[(int64_t)b * jb.cols];
+                t[0] = c0 == jb.max_col ? fmaxf(t[0], v) : t[0] + v;
+            }
         }
     }
-    lds[rg][cl] = t;
+    lds[rg][cl] = make_float4(t[0], t[1], t[2], t[3]);
     __syncthreads();
-    if (rg != 0 || c >= jb.cols) return;
-    float acc = lds[0][cl];
+    if (rg != 0 || c0 >= jb.cols) return;
+    float acc[4];
+    {
+        const float4 a0 = lds[0][cl];
+        acc[0] = a0.x;
+        acc[1] = a0.y;
+        acc[2] = a0.z;
+        acc[3] = a0.w;
+    }
 #pragma unroll
-    for (int g = 1; g < 16; g++) acc = is_max ? fmaxf(acc, lds[g][cl]) : acc + lds[g][cl];
-    int off = 0;
-    for (int k = 0; k < jb.nseg; k++) {
-        if (c < off + jb.len[k]) {
-            jb.dst[k][c - off] = acc;
-            return;
+    for (int g = 1; g < 16; g++) {
+        const float4 a = lds[g][cl];
+        const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int u = 0; u < 4; u++) acc[u] = c0 + u == jb.max_col ? fmaxf(acc[u], av[u]) : acc[u] + av[u];
+    }
+    for (int u = 0; u < W; u++) {
+        const int c = c0 + u;
+        int off = 0;
+        for (int k = 0; k < jb.nseg; k++) {
+            if (c < off + jb.len[k]) {
+                jb.dst[k][c - off] = acc[u];
+                break;
+            }
+            off += jb.len[k];
         }
-        off += jb.len[k];
     }
 }
 
@@ -2384,7 +2419,7 @@ int g2048_colsum_batch(g2048_stream_t stream, const g2048_colsum_job *jobs, int3
         cb.job[cb.njobs] = jb;
         cb.first[cb.njobs] = blocks;
         cb.njobs++;
-        blocks += (jb.cols + 63) / 64;
+        blocks += colsum_vec(jb) ? (jb.cols + 255) / 256 : (jb.cols + 63) / 64;
     }
     cb.first[cb.njobs] = blocks;
     if (!blocks) return G2048_OK;

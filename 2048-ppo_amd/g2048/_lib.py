@@ -39,6 +39,7 @@ EXPORTED = (
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
     "g2048_head_split_bytes", "g2048_head_split", "g2048_mlp_pass_supported", "g2048_mlp_pass_partials",
     "g2048_ppo_forward_loss", "g2048_ppo_forward_kl", "g2048_mlp_back_partials", "g2048_ppo_backward",
+    "g2048_mlp_wgrad_partials", "g2048_mlp_wgrad",
     # include/g2048_urm.h
     "g2048_urm_stem", "g2048_urm_attention", "g2048_urm_residual_rms", "g2048_urm_swiglu_conv",
     "g2048_urm_pool_heads", "g2048_urm_linear_supported", "g2048_urm_linear", "g2048_urm_linear_rms",
@@ -142,7 +143,7 @@ class MlpPassArgs(ctypes.Structure):
                 ("ln_beta", vp * 3), ("head_frag", vp), ("ba", vp), ("bv", vp), ("drop", Dropout * 2),
                 ("beta_dev", vp), ("critic", ctypes.c_float), ("clip_eps", ctypes.c_float), ("x0", vp), ("g", vp * 3),
                 ("h", vp * 3), ("mean", vp * 3), ("rstd", vp * 3), ("masked", vp), ("dz", vp), ("dz_bf16", vp),
-                ("partials", vp)]
+                ("partials", vp), ("keep", vp)]
 
 
 class MlpBackArgs(ctypes.Structure):
@@ -150,7 +151,15 @@ class MlpBackArgs(ctypes.Structure):
     vp = ctypes.c_void_p
     _fields_ = [("m", ctypes.c_int64), ("hidden", ctypes.c_int32), ("pad_", ctypes.c_int32), ("w_block", vp * 2),
                 ("ln_gamma", vp * 3), ("ln_beta", vp * 3), ("wa", vp), ("wv", vp), ("dz", vp), ("g", vp * 3),
-                ("mean", vp * 3), ("rstd", vp * 3), ("drop", Dropout * 2), ("dg", vp * 3), ("p_out", vp * 2), ("partials", vp)]
+                ("mean", vp * 3), ("rstd", vp * 3), ("drop", Dropout * 2), ("dg", vp * 3), ("p_out", vp * 2), ("partials", vp),
+                ("keep", vp)]
+
+
+class MlpWgradArgs(ctypes.Structure):
+    """struct g2048_mlp_wgrad_args"""
+    vp = ctypes.c_void_p
+    _fields_ = [("m", ctypes.c_int64), ("hidden", ctypes.c_int32), ("pad_", ctypes.c_int32), ("dz_bf16", vp),
+                ("h2", vp), ("dg", vp * 3), ("x", vp * 3), ("partials", vp)]
 
 
 class PolicyRolloutArgs(ctypes.Structure):
@@ -235,6 +244,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_ppo_backward": (ctypes.c_int, [vp, ctypes.POINTER(MlpBackArgs), ctypes.POINTER(vp), ctypes.POINTER(vp),
                                               jp]),
         "g2048_ppo_forward_kl": (ctypes.c_int, [vp, ctypes.POINTER(MlpPassArgs), vp, jp]),
+        "g2048_mlp_wgrad_partials": (sz, [i64, i32]),
+        "g2048_mlp_wgrad": (ctypes.c_int, [vp, ctypes.POINTER(MlpWgradArgs), vp, ctypes.POINTER(vp), jp]),
         "g2048_linear_dgrad_supported": (ctypes.c_int, [i32, i32]),
         "g2048_linear_dgrad": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_stem": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, i64, i32]),
@@ -587,8 +598,9 @@ def head_split(wa, wv, frag):
 def make_mlp_pass(boards, batch: PPOBatch, m: int, w_stem, w_blocks, gammas, betas, head_frag, ba, bv=None,
                   drops=(None, None), beta_dev=None, critic=0.0, clip_eps=0.2, decouple=False, x0=None,
                   g=(None, None, None), h=(None, None, None), mean=(None, None, None), rstd=(None, None, None),
-                  masked=None, dz=None, dz_bf16=None, partials=None) -> MlpPassArgs:
-    """struct g2048_mlp_pass_args for g2048_ppo_forward_loss / g2048_ppo_forward_kl (GameMLP, 2 blocks)."""
+                  masked=None, dz=None, dz_bf16=None, partials=None, keep=None) -> MlpPassArgs:
+    """struct g2048_mlp_pass_args for g2048_ppo_forward_loss / g2048_ppo_forward_kl (GameMLP, 2 blocks).
+    keep (train pass, optional): int64 [2, m, 4] out, the blocks' dropout keep bits for the backward."""
     a = MlpPassArgs()
     a.boards = _dev(boards, torch.int8, "boards")
     a.batch = batch
@@ -617,6 +629,7 @@ def make_mlp_pass(boards, batch: PPOBatch, m: int, w_stem, w_blocks, gammas, bet
     a.dz = _dev(dz, torch.float32, "dz")
     a.dz_bf16 = _dev(dz_bf16, torch.bfloat16, "dz_bf16")
     a.partials = _dev(partials, torch.float32, "partials")
+    a.keep = _dev(keep, torch.int64, "keep")
     return a
 
 
@@ -638,8 +651,9 @@ def mlp_back_partials(m: int, h: int) -> int:
 
 
 def make_mlp_back(m: int, w_blocks, gammas, betas, wa, wv, dz, g, mean, rstd, drops=(None, None), dg=(None,) * 3,
-                  partials=None, p_out=(None, None)) -> MlpBackArgs:
-    """struct g2048_mlp_back_args for g2048_ppo_backward (GameMLP, 2 blocks)."""
+                  partials=None, p_out=(None, None), keep=None) -> MlpBackArgs:
+    """struct g2048_mlp_back_args for g2048_ppo_backward (GameMLP, 2 blocks).  keep: the train pass's
+    keep bits (make_mlp_pass(keep=...)) for the same drops, read instead of re-drawing the masks."""
     a = MlpBackArgs()
     a.m = int(m)
     a.hidden = int(w_blocks[0].shape[0])
@@ -660,7 +674,35 @@ def make_mlp_back(m: int, w_blocks, gammas, betas, wa, wv, dz, g, mean, rstd, dr
         if d is not None:
             a.drop[i] = d
     a.partials = _dev(partials, torch.float32, "partials")
+    a.keep = _dev(keep, torch.int64, "keep")
     return a
+
+
+def mlp_wgrad_partials(m: int, h: int) -> int:
+    return int(load().g2048_mlp_wgrad_partials(int(m), int(h)))
+
+
+def mlp_wgrad(m: int, dz_bf16, h2, dg, x, partials, out_head, out_w, defer=None):
+    """The four weight gradients of the GameMLP minibatch in one launch (g2048_mlp_wgrad):
+    out_head [16, h] = dz_bf16^T h2, out_w[0] [h, 48] = dg[0]^T x[0], out_w[l] [h, h] = dg[l]^T x[l];
+    defer: a list of four ColsumJob (head, stem, block 1, block 2) filled instead of summing."""
+    a = MlpWgradArgs()
+    a.m = int(m)
+    a.hidden = int(h2.shape[1])
+    a.dz_bf16 = _dev(dz_bf16, torch.bfloat16, "dz_bf16")
+    a.h2 = _dev(h2, torch.bfloat16, "h2")
+    for i in range(3):
+        a.dg[i] = _dev(dg[i], torch.bfloat16, f"dg[{i}]")
+        a.x[i] = _dev(x[i], torch.bfloat16, f"x[{i}]")
+    a.partials = _dev(partials, torch.float32, "partials")
+    vp = ctypes.c_void_p
+    outs = (vp * 3)(*[_dev(t, torch.float32, "out_w") for t in out_w])
+    jobs = (ColsumJob * 4)() if defer is not None else None
+    _check(load().g2048_mlp_wgrad(_stream(out_head), ctypes.byref(a), _dev(out_head, torch.float32, "out_head"), outs,
+                                  jobs), "g2048_mlp_wgrad")
+    if defer is not None:
+        for i in range(4):
+            defer[i] = jobs[i]
 
 
 def ppo_backward(args: MlpBackArgs, dgamma, dbeta, defer=None, like=None):

@@ -140,8 +140,14 @@ class FusedPPOUpdater(PPOUpdater):
             # the fused backward (g2048_ppo_backward): every layer's dG kept for its weight gradient
             self.DG = [torch.empty(bs, h, dtype=bf, device=d) for _ in range(nl)]
             self.part_back = torch.empty(L.mlp_back_partials(bs, h), dtype=f32, device=d)
+            # the blocks' dropout keep bits of the train pass (64 B per row), read by the backward
+            # instead of re-drawing its Philox masks
+            self.keep = torch.empty(2, bs, 4, dtype=torch.int64, device=d)
             npair = L.wgrad_pair_partials(bs, h, h)
             self.part_pair = [torch.empty(npair, dtype=f32, device=d) for _ in range(2)] if npair else None
+            # the four weight gradients (head, stem, both blocks) in one streaming launch
+            nmw = L.mlp_wgrad_partials(bs, h) if nl == 3 and bs * 4 * h < 2 ** 31 else 0
+            self.part_mw = torch.empty(nmw, dtype=f32, device=d) if nmw else None
         self.bs = bs
 
     def _drop(self, layer: int, pass_: int):
@@ -150,9 +156,16 @@ class FusedPPOUpdater(PPOUpdater):
     force_layer_kernels = False  # tests: the per-layer kernel chain instead of the fused passes
     force_layer_backward = False  # tests: the fused train pass with the per-layer backward chain
 
+    force_split_wgrad = False  # tests: g2048_wgrad / g2048_wgrad_pair instead of the one-launch g2048_mlp_wgrad
+
     @property
     def fused_back(self) -> bool:
         return self.fused_pass and all(self.wg_ok) and not self.force_layer_backward
+
+    @property
+    def wgrad_one_launch(self) -> bool:
+        """The fused backward's weight gradients (and the head's) in one g2048_mlp_wgrad launch."""
+        return self.fused_back and getattr(self, "part_mw", None) is not None and not self.force_split_wgrad
 
     @torch.no_grad()
     def refresh_weights(self):
@@ -176,7 +189,7 @@ class FusedPPOUpdater(PPOUpdater):
         return L.make_mlp_pass(data["boards"], batch, idx.shape[0], bv=self.bv, beta_dev=self._beta_dev,
                                critic=self.cfg.critic, clip_eps=self.cfg.clip_eps, decouple=self.decouple, x0=self.x0,
                                g=self.G, h=self.H, mean=self.mean, rstd=self.rstd, dz=self.dz, dz_bf16=self.dzb,
-                               partials=self.part_fwd, **common)
+                               partials=self.part_fwd, keep=self.keep, **common)
 
     def fused_forward_loss(self, data, idx, beta):
         """The train pass in one launch (obs -> GameMLP -> heads -> PPO loss, dz), then the head weight
@@ -188,6 +201,8 @@ class FusedPPOUpdater(PPOUpdater):
         self._kl_args = self._pass_args(data, idx, 1, False)
         j_loss, j_head = L.ColsumJob(), L.ColsumJob()
         L.ppo_forward_loss(args, self.ba.grad, self.bv.grad, self.sums, defer=j_loss)
+        if self.wgrad_one_launch:  # the head weight gradient joins the backward's weight-gradient launch
+            return [j_loss]
         L.wgrad(self.dzb, self.H[-1], self.part_wh, self.wh_out, defer=j_head)
         head_grad_job(j_head, self.h, self.wa.grad, self.wv.grad, self.wh_spill)
         return [j_loss, j_head]
@@ -215,15 +230,26 @@ class FusedPPOUpdater(PPOUpdater):
 
     def fused_backward(self, jobs):
         """The backward after the fused train pass: g2048_ppo_backward (three LayerNorm backwards and
-        the two block input gradients in one launch), then the three weight gradients dW_l = dG_l^T
-        X_l on g2048_wgrad; every column sum deferred into `jobs`."""
+        the two block input gradients in one launch), then the weight gradients dW_l = dG_l^T X_l and
+        the head's dz^T H2 in one g2048_mlp_wgrad launch (else g2048_wgrad / g2048_wgrad_pair); every
+        column sum deferred into `jobs` and run as one g2048_colsum_batch."""
         ln = self.ln
         args = L.make_mlp_back(self.bs, self.wbf[1:], [x.weight for x in ln], [x.bias for x in ln], self.wa,
                                None if self.decouple else self.wv, self.dz, self.G, self.mean, self.rstd,
-                               drops=(self._drop(1, 0), self._drop(2, 0)), dg=self.DG, partials=self.part_back)
+                               drops=(self._drop(1, 0), self._drop(2, 0)), dg=self.DG, partials=self.part_back,
+                               keep=self.keep)
         jb = [L.ColsumJob() for _ in range(3)]
         L.ppo_backward(args, [x.weight.grad for x in ln], [x.bias.grad for x in ln], defer=jb)
         jobs.extend(jb)
+        if self.wgrad_one_launch:  # head, stem and both blocks: one streaming launch, four column sums
+            jw = [L.ColsumJob() for _ in range(4)]
+            L.mlp_wgrad(self.bs, self.dzb, self.H[-1], self.DG, [self.x0, self.H[0], self.H[1]], self.part_mw,
+                        self.wh_out, [w.grad for w in self.lin], defer=jw)
+            head_grad_job(jw[0], self.h, self.wa.grad, self.wv.grad, self.wh_spill)
+            jobs.extend(jw)
+            for i in range(0, len(jobs), L.COLSUM_MAX_JOBS):
+                L.colsum_batch(jobs[i:i + L.COLSUM_MAX_JOBS])
+            return
         jobs.append(L.ColsumJob())
         L.wgrad(self.DG[0], self.x0, self.part_wg[0], self.lin[0].grad, defer=jobs[-1])
         if self.part_pair is not None:  # the two block layers' weight gradients in one launch
@@ -284,6 +310,7 @@ class FusedPPOUpdater(PPOUpdater):
 
     # ---------------------------------------------------------------- PPOUpdater hooks ----
     ragged_pad = True  # the ragged last minibatch runs padded to full size (g2048_ppo_batch.rows)
+    double_idx = True  # next minibatch's index copy beside the current replay (two captures)
 
     def _set_rows(self, n: int):
         self.rows.fill_(n)

@@ -225,11 +225,11 @@ class FusedMuonAdamW(MuonAdamW):
             import os
             parts = int(os.environ.get("G2048_MUON_PARTS", self.MUON_PARTS))
             if parts > 1:
-                self._ws = torch.empty(int(L.load().g2048_muon_workspace_bytes()), dtype=torch.uint8, device=self.dev)
+                self._ws = torch.zeros(int(L.load().g2048_muon_workspace_bytes()), dtype=torch.uint8, device=self.dev)
                 self._cfg.parts = parts
                 self._cfg.workspace = self._ws.data_ptr()
 
-    MUON_PARTS = 8
+    MUON_PARTS = 13
 
     def set_bf16_copies(self, mapping: dict):
         """{parameter: bf16 tensor} refreshed by the Muon kernel after each step."""

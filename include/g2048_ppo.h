@@ -250,6 +250,9 @@ typedef struct g2048_mlp_pass_args {
     float *dz;
     void *dz_bf16;
     float *partials;
+    void *keep;                    /* train, optional out: the blocks' dropout keep bits, uint64 [2][m][4]
+                                    * (block, row, lane group g: bit 4 n + e = feature 16 n + 4 g + e),
+                                    * g2048_ppo_backward's `keep` (8-byte aligned; NULL: not stored) */
 } g2048_mlp_pass_args;
 
 /* The head weights [wa (4 rows); wv] (fp32) as the passes' MFMA operand: an exact three-term bf16
@@ -285,6 +288,8 @@ typedef struct g2048_mlp_back_args {
     void *dg[3];                   /* out: bf16 [m][h] */
     void *p_out[2];                /* optional out: bf16 [m][h] P1, P2 (tests) */
     float *partials;
+    const void *keep;              /* optional: the train pass's keep bits (g2048_mlp_pass_args.keep) for
+                                    * the same drop[] -- read instead of re-drawing the Philox masks */
 } g2048_mlp_back_args;
 size_t g2048_mlp_back_partials(int64_t m, int32_t hidden);
 int g2048_ppo_backward(g2048_stream_t stream, const g2048_mlp_back_args *args, float *const *dgamma,
@@ -300,6 +305,27 @@ int g2048_ppo_backward(g2048_stream_t stream, const g2048_mlp_back_args *args, f
 int g2048_ppo_stats(g2048_stream_t stream, const float *sums, const float *kl, int32_t kl_rows, const float *grad_norm,
                     const float *beta_dev, float critic, int64_t m, const int64_t *rows, float *stats,
                     uint64_t *counter);
+
+/* The four weight gradients of the GameMLP minibatch backward in ONE launch (mlp_wgrad.hip):
+ *   out_head [16][h] = dz_bf16^T H2   (dz as two bf16 terms: hi in rows 0-4, lo in rows 8-12)
+ *   out_w[0] [h][48] = dg[0]^T x[0]    (the stem: x[0] = the bf16 observations [m][48])
+ *   out_w[l] [h][h]  = dg[l]^T x[l]    (block l = 1, 2: x[l] = the block's input H_{l-1})
+ * Every operand bf16 row-major with m rows, 16-byte aligned; h in {196, 192, 128, 64, 32}.  The CUs
+ * split the products' rows in proportion to their bytes; each block writes an fp32 partial that
+ * g2048_colsum_batch sums in a fixed order: `defer` (4 jobs: head, stem, block 1, block 2) receives
+ * those jobs instead of summing at once.  Replaces g2048_wgrad (head, stem) + g2048_wgrad_pair. */
+typedef struct g2048_mlp_wgrad_args {
+    int64_t m;
+    int32_t hidden, pad_;
+    const void *dz_bf16;           /* [m][16] */
+    const void *h2;                /* [m][h]  block 2's output */
+    const void *dg[3];             /* [m][h]  the train step's dG of the stem, block 1, block 2 */
+    const void *x[3];              /* the layers' inputs: x0 [m][48], H0 [m][h], H1 [m][h] */
+    float *partials;               /* g2048_mlp_wgrad_partials(m, hidden) floats */
+} g2048_mlp_wgrad_args;
+size_t g2048_mlp_wgrad_partials(int64_t m, int32_t hidden);
+int g2048_mlp_wgrad(g2048_stream_t stream, const g2048_mlp_wgrad_args *args, float *out_head, float *const *out_w,
+                    g2048_colsum_job *defer);
 
 /* Scratch floats of g2048_wgrad for (m, n1, n2); 0 when the shape is unsupported. */
 size_t g2048_wgrad_partials(int64_t m, int32_t n1, int32_t n2);
@@ -349,9 +375,10 @@ typedef struct g2048_muon_cfg {
     float momentum, weight_decay, ns_a, ns_b, ns_c, ns_eps;
     int32_t ns_steps, nesterov;
     /* parts > 1 with a workspace: every 196 x 196 / 192 x 192 matrix runs on `parts` blocks (CUs, 7 <=
-     * parts <= 13) that split the row blocks of the Newton-Schulz products and exchange X once per
-     * iteration through the workspace (g2048_muon_workspace_bytes(), device memory; its first bytes
-     * are zeroed by a memset node of every call).  parts <= 1 or workspace NULL: one block per matrix. */
+     * parts <= 12) that split the row blocks of the Newton-Schulz products and exchange X once per
+     * iteration through the workspace (g2048_muon_workspace_bytes(), device memory, ZERO-FILLED ONCE
+     * by the caller: each launch leaves its counters zero again).  parts <= 1 or workspace NULL: one
+     * block per matrix. */
     int32_t parts, pad_;
     void *workspace;
 } g2048_muon_cfg;

@@ -87,7 +87,7 @@ def _worker(rank, world, port, out, model_type="mlp"):
     tr.ppo.update = update
     for s in range(STEPS):
         m = tr.train_step(s)
-        assert np.isfinite(m["loss"]) and np.isfinite(m["grad_norm"])
+        assert np.isfinite(m["loss"]) and np.isfinite(m["grad_norm"]), (rank, s, m)
         T = tr.rollout.T
         rec["g_raw"].append(tr.rollout.buf.g_raw[:T].reshape(-1).double().cpu().numpy())
         rec["moments"].append(tr.rtg.state.cpu().numpy().copy())

@@ -568,15 +568,21 @@ def test_fused_muon_adamw_matches_torch_ops_step(dev, h):
             torch.testing.assert_close(p1, p0, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("h,parts", [(196, 8), (196, 12), (196, 7), (192, 8)])
-def test_muon_multi_cu_equals_one_cu(dev, h, parts, monkeypatch):
+@pytest.mark.parametrize("h,parts,loaded", [(196, 8, False), (196, 12, False), (196, 7, False), (192, 8, False),
+                                           (196, 13, False), (192, 13, False), (196, 8, True), (196, 13, True)])
+def test_muon_multi_cu_equals_one_cu(dev, h, parts, loaded, monkeypatch):
     """The multi-CU Newton-Schulz (the h x h blocks' row blocks on `parts` CUs, X exchanged once per
     iteration through the workspace, optim.hip ns_square_mc) is bitwise the one-CU square schedule:
     same MFMA sequence per output tile (the X product with its operand roles swapped).  Three steps,
-    every parameter and the momentum buffers compared."""
+    every parameter and the momentum buffers compared.  loaded: every step runs beside GEMMs on a
+    second stream, so the parts start and reach the exchanges at uneven times (cdna_hip_programming.md
+    Guideline 16, Pitfall 3) -- the case where a part could read momentum rows another part already
+    updated."""
     import agent
     from g2048.dist import GradBucket
     from g2048.optim import FusedMuonAdamW
+    side = torch.cuda.Stream()
+    big = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
     outs = []
     for p in (1, parts):
         monkeypatch.setenv("G2048_MUON_PARTS", str(p))
@@ -588,6 +594,11 @@ def test_muon_multi_cu_equals_one_cu(dev, h, parts, monkeypatch):
         bk = GradBucket(order)
         for s in range(3):
             bk.flat.copy_(torch.randn(bk.flat.shape, generator=torch.Generator().manual_seed(s)).to(dev) * 1e-2)
+            if loaded:
+                torch.cuda.synchronize()
+                with torch.cuda.stream(side):
+                    for _ in range(4):
+                        big = (big @ big).clamp_(-1, 1)
             opt.step_clipped(bk.flat, 1.0)
         torch.cuda.synchronize()
         outs.append((torch.cat([q.detach().reshape(-1) for q in m.parameters()]).clone(),
@@ -1049,6 +1060,116 @@ def test_fused_train_pass_matches_layer_kernels(dev, h, M, m, p, ragged):
     torch.testing.assert_close(wh[:4], dwa0, rtol=0, atol=1e-4 * scale)
     torch.testing.assert_close(wh[4:5], dwv0, rtol=0, atol=1e-4 * scale)
     assert torch.equal(wh[5:], torch.zeros_like(wh[5:]))
+
+
+@pytest.mark.parametrize("h,m", [(196, 65536), (196, 4099), (192, 700), (128, 1000), (64, 333), (32, 40), (196, 31)])
+def test_mlp_wgrad_matches_fp32(dev, h, m):
+    """g2048_mlp_wgrad (head, stem and both block weight gradients in one streaming launch, ragged m
+    included) against fp32 matmuls of the same bf16 operands: fp32 accumulation in another order,
+    so within 2e-6 of the output scale per sqrt(m) row."""
+    from g2048 import _lib as L
+    g = torch.Generator(device=dev).manual_seed(h + m)
+    bf = torch.bfloat16
+    rnd = lambda *s: torch.randn(*s, generator=g, device=dev).to(bf)  # noqa: E731
+    dzb, h2 = rnd(m, 16), rnd(m, h)
+    dg = [rnd(m, h) for _ in range(3)]
+    x = [rnd(m, 48), rnd(m, h), rnd(m, h)]
+    part = torch.full((L.mlp_wgrad_partials(m, h),), float("nan"), device=dev)
+    out_head = torch.full((16, h), float("nan"), device=dev)
+    out_w = [torch.full((h, 48), float("nan"), device=dev), torch.full((h, h), float("nan"), device=dev),
+             torch.full((h, h), float("nan"), device=dev)]
+    L.mlp_wgrad(m, dzb, h2, dg, x, part, out_head, out_w)
+    torch.cuda.synchronize()
+    refs = [dzb.float().t() @ h2.float()] + [dg[l].float().t() @ x[l].float() for l in range(3)]
+    for got, ref in zip([out_head] + out_w, refs):
+        assert torch.isfinite(got).all()
+        tol = 2e-6 * math.sqrt(m) * ref.abs().max().item() + 1e-6
+        assert (got - ref).abs().max().item() <= tol, ((got - ref).abs().max().item(), tol)
+
+
+def test_one_launch_wgrad_update_matches_split_wgrad(dev):
+    """FusedPPOUpdater's minibatch gradient with the one-launch weight gradients (g2048_mlp_wgrad)
+    equals the one with g2048_wgrad / g2048_wgrad_pair to fp32 summation order, every parameter."""
+    import agent
+    from g2048.dist import GradBucket
+    from g2048.fastmlp import FusedPPOUpdater
+    from g2048.optim import FusedMuonAdamW
+    from g2048.ppo import PPOConfig
+    _, _, _, _, data, _, _ = _pass_case(dev, 196, 3 * 4096, 1, 0.1, 98)
+    idx = torch.randperm(3 * 4096, device=dev)[:4096]
+    grads = []
+    for split in (False, True):
+        torch.manual_seed(5)
+        mdl = agent.GameMLP(agent.MLPConfig(hidden_dim=196, dropout=0.1)).to(dev).train()
+        with torch.no_grad():  # non-zero heads (the trainer zeroes them; here they must carry signal)
+            mdl.action_head.weight.normal_(0, 0.05)
+            mdl.value_head.weight.normal_(0, 0.05)
+        opt = FusedMuonAdamW(mdl, 1e-3, 1e-3)
+        order = [p for p, _ in opt.muon] + [p for gr in opt.adam_groups for p in gr["params"]]
+        up = FusedPPOUpdater(mdl, opt, PPOConfig(batch_size=4096), GradBucket(order),
+                             torch.Generator(device=dev).manual_seed(3), graph=False)
+        up.force_split_wgrad = split
+        up._alloc(4096)
+        assert up.wgrad_one_launch == (not split)
+        up.refresh_weights()
+        up.beta_t.fill_(0.02)
+        up._pre(idx, data, up.beta_t, None)
+        torch.cuda.synchronize()
+        grads.append([p.grad.clone() for p in mdl.parameters()])
+    for (n, _), a, b in zip(mdl.named_parameters(), grads[0], grads[1]):
+        assert torch.isfinite(a).all(), n
+        assert (a - b).abs().max().item() <= 1e-4 * b.abs().max().item() + 1e-12, (n, (a - b).abs().max())
+
+
+@pytest.mark.parametrize("h,M,m,p", [(196, 5000, 4099, 0.1), (128, 1200, 1000, 0.25), (64, 700, 333, 0.2),
+                                     (192, 900, 700, 0.1)])
+def test_backward_reads_the_train_pass_keep_bits(dev, h, M, m, p):
+    """The train pass's stored dropout keep bits (g2048_mlp_pass_args.keep) are the masks the
+    backward re-draws: g2048_ppo_backward with `keep` is bitwise the Philox re-draw path (dG of every
+    layer, dgamma / dbeta), and the bits keep about 1 - p of the valid features."""
+    from g2048 import _lib as L
+    w, gam, bet, (wa, ba, wv, bv), data, idx, ctr = _pass_case(dev, h, M, m, p, 3 * h + m)
+    rows = torch.tensor([m], dtype=torch.int64, device=dev)
+    drops = [L.make_dropout(p, l, 0, 777, 0, ctr) for l in (1, 2)]
+    bf = torch.bfloat16
+    batch = L.make_ppo_batch(idx, data["actions"], data["legal"], data["logp"], data["adv"], data["ret"], rows=rows)
+    frag = torch.empty(L.head_split_bytes(h), dtype=torch.uint8, device=dev)
+    L.head_split(wa, wv, frag)
+    G = [torch.empty(m, h, dtype=bf, device=dev) for _ in range(3)]
+    mu = [torch.empty(m, device=dev) for _ in range(3)]
+    rs = [torch.empty(m, device=dev) for _ in range(3)]
+    dz = torch.empty(m, 8, device=dev)
+    keep = torch.full((2, m, 4), -1, dtype=torch.int64, device=dev)
+    args = L.make_mlp_pass(data["boards"], batch, m, w[0], w[1:], gam, bet, frag, ba, bv, drops=drops,
+                           beta_dev=torch.tensor(0.02, device=dev), critic=0.2, clip_eps=0.2,
+                           x0=torch.empty(m, 48, dtype=bf, device=dev), g=G,
+                           h=[torch.empty(m, h, dtype=bf, device=dev) for _ in range(3)], mean=mu, rstd=rs,
+                           masked=torch.empty(m, 4, device=dev), dz=dz, dz_bf16=torch.empty(m, 16, dtype=bf, device=dev),
+                           partials=torch.empty(L.mlp_pass_partials(m, True), device=dev), keep=keep)
+    L.ppo_forward_loss(args, torch.empty(4, device=dev), torch.empty(1, device=dev), torch.empty(3, device=dev))
+    outs = []
+    for kb in (None, keep):
+        dg = [torch.full((m, h), float("nan"), dtype=bf, device=dev) for _ in range(3)]
+        dgam = [torch.empty(h, device=dev) for _ in range(3)]
+        dbet = [torch.empty(h, device=dev) for _ in range(3)]
+        bargs = L.make_mlp_back(m, w[1:], gam, bet, wa, wv, dz, G, mu, rs, drops=drops, dg=dg,
+                                partials=torch.empty(L.mlp_back_partials(m, h), device=dev), keep=kb)
+        L.ppo_backward(bargs, dgam, dbet)
+        outs.append(dg + dgam + dbet)
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        ai = a.view(torch.int16) if a.dtype == bf else a.view(torch.int32)
+        bi = b.view(torch.int16) if b.dtype == bf else b.view(torch.int32)
+        assert torch.equal(ai, bi)
+    # bit 4 n + e of lane group g = feature 16 n + 4 g + e
+    kk = keep.cpu().numpy().view(np.uint64)
+    bitpos = np.arange(64, dtype=np.uint64)
+    on = ((kk[..., None] >> bitpos) & np.uint64(1)).astype(bool)  # [2, m, 4, 64]
+    n_, e_ = bitpos.astype(int) // 4, bitpos.astype(int) % 4
+    feat = 16 * n_[None, :] + 4 * np.arange(4)[:, None] + e_[None, :]  # [4, 64]
+    valid = feat < h  # (bits of features past h are drawn too and unused: the passes mask those features)
+    frac = on[:, :, valid].mean()
+    assert abs(frac - (1 - p)) < 0.01, frac
 
 
 @pytest.mark.parametrize("h,M,m,p,ragged", [(196, 70000, 65536, 0.1, False), (196, 5000, 4099, 0.0, True),

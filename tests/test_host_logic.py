@@ -196,3 +196,18 @@ def test_urm_param_groups_cover_every_parameter_once(ntl):
     assert all(p.ndim != 2 or p is m.init_hidden for p in o1["params"] + v1["params"])
     assert (any(p is m.init_hidden for p in o1["params"])) == (ntl == 0)
     assert {id(p) for p in v2["params"] + v1["params"]} == {id(p) for p in m.value_head.parameters()}
+
+
+def test_muon_normalisation_quotient_is_correctly_rounded():
+    """optim.hip's muon_kernel divides the bf16 image by its norm with one reciprocal and two fmas:
+    exactly the correctly rounded fp32 quotient for every pair of bf16 significands (rational
+    arithmetic, tools/check_bf16_division.py)."""
+    import runpy
+    import io
+    import contextlib
+    from pathlib import Path
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        runpy.run_path(str(Path(__file__).resolve().parent.parent / "tools" / "check_bf16_division.py"),
+                       run_name="__main__")
+    assert "mismatches 0 of 16384" in out.getvalue()

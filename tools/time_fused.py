@@ -80,8 +80,9 @@ def run(L, m, h):
                dz_bf16=torch.empty(m, 16, dtype=bf, device=dev),
                partials=torch.empty(L.mlp_pass_partials(m, True), device=dev))
     drops = [L.make_dropout(0.1, l, 0, 321, 0, ctr) for l in (1, 2)]
+    keep = torch.empty(2, m, 4, dtype=torch.int64, device=dev)  # the blocks' keep bits, as FusedPPOUpdater
     args = L.make_mlp_pass(boards, batch, m, w[0], w[1:], gam, bet, frag, ba, bv, drops=drops, beta_dev=beta,
-                           critic=0.2, clip_eps=0.2, **out)
+                           critic=0.2, clip_eps=0.2, keep=keep, **out)
     dba, dbv, sums = torch.empty(4, device=dev), torch.empty(1, device=dev), torch.empty(3, device=dev)
     j = L.ColsumJob()
     res = {}
@@ -96,9 +97,27 @@ def run(L, m, h):
     dgam = [torch.empty(h, device=dev) for _ in range(3)]
     dbet = [torch.empty(h, device=dev) for _ in range(3)]
     bargs = L.make_mlp_back(m, w[1:], gam, bet, wa, wv, dz, G, mu, rs, drops=drops, dg=dg,
-                            partials=torch.empty(L.mlp_back_partials(m, h), device=dev))
+                            partials=torch.empty(L.mlp_back_partials(m, h), device=dev), keep=keep)
     jobs = [L.ColsumJob() for _ in range(3)]
     res["backward (ppo_backward, deferred colsums)"] = timed(lambda: L.ppo_backward(bargs, dgam, dbet, defer=jobs))
+    # the weight gradients: one g2048_mlp_wgrad launch vs g2048_wgrad (head, stem) + g2048_wgrad_pair
+    if hasattr(L, "mlp_wgrad_partials") and L.mlp_wgrad_partials(m, h) > 0:
+        dzb = out["dz_bf16"]
+        pw = torch.empty(L.mlp_wgrad_partials(m, h), device=dev)
+        oh, ow = torch.empty(16, h, device=dev), [torch.empty(h, 48, device=dev)] + [torch.empty(h, h, device=dev) for _ in range(2)]
+        jw = [L.ColsumJob() for _ in range(4)]
+        res["weight gradients (g2048_mlp_wgrad, deferred colsums)"] = timed(
+            lambda: L.mlp_wgrad(m, dzb, H[2], dg, [out["x0"], H[0], H[1]], pw, oh, ow, defer=jw))
+    ph, ps = torch.empty(L.wgrad_partials(m, 16, h), device=dev), torch.empty(L.wgrad_partials(m, h, 48), device=dev)
+    pp = [torch.empty(L.wgrad_pair_partials(m, h, h), device=dev) for _ in range(2)]
+    oh, ow = torch.empty(16, h, device=dev), [torch.empty(h, 48, device=dev)] + [torch.empty(h, h, device=dev) for _ in range(2)]
+    j3 = [L.ColsumJob() for _ in range(4)]
+
+    def split():
+        L.wgrad(out["dz_bf16"], H[2], ph, oh, defer=j3[0])
+        L.wgrad(dg[0], out["x0"], ps, ow[0], defer=j3[1])
+        L.wgrad_pair(dg[1], H[0], dg[2], H[1], pp[0], pp[1], ow[1], ow[2], defer=j3[2:])
+    res["weight gradients (2 x g2048_wgrad + g2048_wgrad_pair)"] = timed(split)
     for k, v in res.items():
         print(f"{k:55s} {v:8.1f} us   (m={m}, h={h})")
 
