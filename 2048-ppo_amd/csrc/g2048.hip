@@ -274,12 +274,19 @@ __device__ __forceinline__ void fresh_prep(RolloutLane &s, const uint32_t *__res
                       1u + ((st >> 8) & 1u), st >> 12};
 }
 
-struct TrajRows {  // row t of each time-major trajectory array
+struct TrajRows {  // this lane's element of row t of each time-major trajectory array (advanced by n per step)
     uint4 *b;
     uint8_t *a;
     int32_t *p;
     uint32_t *pot;
     uint8_t *f;
+    __device__ __forceinline__ void next(int64_t n) {
+        b += n;
+        a += n;
+        p += n;
+        pot += n;
+        f += n;
+    }
 };
 
 
@@ -288,8 +295,8 @@ struct TrajRows {  // row t of each time-major trajectory array
 // low word r of that product (uniform given k) picks the spawn cell and value (spawn_chain).
 template <bool kOdd, bool kSmall = false>
 __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__restrict__ tab, const TrajRows &tr,
-                                             uint32_t li, uint64_t seed, uint64_t next_pair, uint32_t env) {
-    tr.b[li] = s.b;
+                                             uint64_t seed, uint64_t next_pair, uint32_t env) {
+    *tr.b = s.b;
     const uint32_t u = kOdd ? s.D.y : s.D.x;
     const uint64_t pa = (uint64_t)u * (uint32_t)__popc(s.legal);
     const uint32_t a = kth_bit4(s.legal, (uint32_t)(pa >> 32)), r = (uint32_t)pa;
@@ -331,8 +338,8 @@ __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__r
     // the spawned tile's pairs (the counts before the spawn are the next board's minus these) and
     // the next board's maximum / first-argmax cell
     const MonoStats dsp = mono_add_tile(MonoStats{0, 0, 0, 0, Ma, pos_a}, moved, sp, v);
-    tr.a[li] = (uint8_t)a;
-    tr.p[li] = (int32_t)pts;
+    *tr.a = (uint8_t)a;
+    *tr.p = (int32_t)pts;
     const uint32_t SR = f0 + f1 + f2 + f3, SC = g0 + g1 + g2 + g3;
     // #lines that can move per direction in nibbles {UP, DOWN, LEFT, RIGHT} -> legal bits 0..3: a
     // nibble n in 0..4 gets bit 3 set by n + 7; the 24-bit product gathers bits 3, 7, 11, 15 at 12..15
@@ -367,9 +374,9 @@ __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__r
     s.sb.B = over ? s.fsb.B : s.sb.B;
     s.sb.M = over ? s.fsb.M : s.sb.M;
     s.sb.pos = over ? s.fsb.pos : s.sb.pos;
-    tr.pot[li] = (uint32_t)(mono_b & 0xFF) | ((uint32_t)(mono_a & 0xFF) << 8) | ((uint32_t)(s.empt_b & 0xFF) << 16) |
+    *tr.pot = (uint32_t)(mono_b & 0xFF) | ((uint32_t)(mono_a & 0xFF) << 8) | ((uint32_t)(s.empt_b & 0xFF) << 16) |
                  ((uint32_t)(empt_a & 0xFF) << 24);
-    tr.f[li] = (uint8_t)fl;
+    *tr.f = (uint8_t)fl;
     s.empt_b = (fl & FLAG_RESET) ? 14 : empt_a - 1;
     if constexpr (kOdd) {
         s.D = make_uint4(s.ph.c0, s.ph.c1, s.ph.c2, s.ph.c3);
@@ -414,14 +421,14 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
         s.D = philox_draw(rng.seed, pair, env, 1u);
         s.ph = philox_start(rng.seed, pair + 1u, env, 1u);
         fresh_prep(s, s_row);
-        auto rows = [&](int64_t t) {
-            const int64_t o = t * n;
-            return TrajRows{tb + o, ta + o, tp + o, tpot + o, tf + o};
-        };
+        // per-lane record addresses, advanced one row (n elements) per step: no array base in an SGPR
+        // pair across the loop (the loop's SGPR spills)
+        TrajRows tr{tb + li, ta + li, tp + li, tpot + li, tf + li};
         int64_t t = 0;
         if ((ctr0 & 1u) && steps > 0) {  // the launch starts on the second step of a pair
             philox_rounds<0, 5>(s.ph);
-            rollout_step<true>(s, s_row, rows(0), li, rng.seed, pair + 2u, env);
+            rollout_step<true>(s, s_row, tr, rng.seed, pair + 2u, env);
+            tr.next(n);
             pair++;
             t = 1;
         }
@@ -429,14 +436,17 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
             // every board of the wave <= 2^9 at the pair's start: both steps stay inside the tables
             // (the move adds at most 1 to the maximum), so the pair runs without the fallback branches
             if (__all(s.sb.M <= 9u)) {
-                rollout_step<false, true>(s, s_row, rows(t), li, rng.seed, pair + 2u, env);
-                rollout_step<true, true>(s, s_row, rows(t + 1), li, rng.seed, pair + 2u, env);
+                rollout_step<false, true>(s, s_row, tr, rng.seed, pair + 2u, env);
+                tr.next(n);
+                rollout_step<true, true>(s, s_row, tr, rng.seed, pair + 2u, env);
             } else {
-                rollout_step<false>(s, s_row, rows(t), li, rng.seed, pair + 2u, env);
-                rollout_step<true>(s, s_row, rows(t + 1), li, rng.seed, pair + 2u, env);
+                rollout_step<false>(s, s_row, tr, rng.seed, pair + 2u, env);
+                tr.next(n);
+                rollout_step<true>(s, s_row, tr, rng.seed, pair + 2u, env);
             }
+            tr.next(n);
         }
-        if (t < steps) rollout_step<false>(s, s_row, rows(t), li, rng.seed, pair + 2u, env);
+        if (t < steps) rollout_step<false>(s, s_row, tr, rng.seed, pair + 2u, env);
         boards[i] = s.b;
     }
 }

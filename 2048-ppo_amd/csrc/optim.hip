@@ -115,6 +115,8 @@ constexpr int kMuonThreads = 1024;       // 16 waves (4 per SIMD: LDS latency hi
 constexpr int kMuonWaves = kMuonThreads / 64;
 constexpr int kBI = 4, kBJ = 4;          // generic schedule: 4 x 4 waves of 4 x 4 16x16 tiles = 256 x 256
 constexpr int kMuonMaxMats = 16;  // GameMLP: 5, GameURM (2 layers): 11
+static_assert(sizeof(g2048_muon_matrix) == 56 && offsetof(g2048_muon_matrix, head_frag) == 32,
+              "g2048_muon_matrix layout (tests/test_abi.py)");
 static_assert(sizeof(g2048_muon_cfg) == 48 && offsetof(g2048_muon_cfg, workspace) == 40,
               "g2048_muon_cfg layout (tests/test_abi.py)");
 constexpr int kMuonMaxJobs = 128;  // grid blocks: Muon parts, AdamW blocks, idle gaps (XCD placement)
@@ -127,8 +129,24 @@ struct MuonMat {
     const float *grad;
     float *mom;
     uint16_t *pbf;
-    int rows, cols, lr_index, pad;
+    uint16_t *frag;  // head matrices: the passes' three-term bf16 fragment image (g2048_head_split)
+    int rows, cols, lr_index, frag_row;
 };
+
+// g2048_head_split's arithmetic for one weight w of head row `which`, column k (h columns): the exact
+// terms hi = bf16(w), mid = bf16(w - hi), lo = bf16(w - hi - mid) into fragment rows which, 5 + which,
+// 10 + which at k-step k / 32, lane group (k % 32) / 8, element k % 8
+__device__ __forceinline__ void head_frag_put(uint16_t *frag, int which, int k, float w) {
+    const __bf16 hi = (__bf16)w;
+    const float r1 = w - (float)hi;
+    const __bf16 mid = (__bf16)r1;
+    const __bf16 lo = (__bf16)(r1 - (float)mid);
+    const int ks = k >> 5, g = (k >> 3) & 3, e = k & 7;
+    const int base = (ks * 64 + 16 * g) * 8 + e;
+    frag[base + which * 8] = __builtin_bit_cast(uint16_t, hi);
+    frag[base + (5 + which) * 8] = __builtin_bit_cast(uint16_t, mid);
+    frag[base + (10 + which) * 8] = __builtin_bit_cast(uint16_t, lo);
+}
 
 struct MuonArgs {
     MuonMat m[kMuonMaxMats];
@@ -349,7 +367,8 @@ __device__ __forceinline__ void muon_momentum_rows(const float *__restrict__ gra
 
 __device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_t *__restrict__ pbf, const char *sX,
                                               int px, int R, int C, bool tr, float decay, float step, int tid,
-                                              int pr0 = 0, int pr1 = 1 << 30) {  // parameter rows [pr0, pr1)
+                                              int pr0 = 0, int pr1 = 1 << 30, uint16_t *frag = nullptr,
+                                              int frag_row = 0) {  // parameter rows [pr0, pr1)
     if (C & 3) {  // per element (see muon_prologue)
         for (int e = tid; e < R * C; e += kMuonThreads) {
             const int i = e / C, j = e - i * C;
@@ -391,6 +410,9 @@ __device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_
             for (int u = 0; u < 4; u++) pv[u] = pv[u] * decay - x[u] * step;
             reinterpret_cast<float4 *>(param)[e4] = make_float4(pv[0], pv[1], pv[2], pv[3]);
             if (pbf) reinterpret_cast<uint2 *>(pbf)[e4] = make_uint2(pack_bf2(pv[0], pv[1]), pack_bf2(pv[2], pv[3]));
+            if (frag && !tr)
+#pragma unroll
+                for (int u = 0; u < 4; u++) head_frag_put(frag, frag_row + i, j0 + u, pv[u]);
         }
     }
 }
@@ -1137,7 +1159,7 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     // decoupled weight decay + the match_rms_adamw-scaled update, and the bf16 weight copy
     const float lr = args.lr[mt.lr_index];
     const float step = lr * (0.2f * sqrtf((float)(R > C ? R : C)));
-    muon_epilogue(mt.param, mt.pbf, sX, px, R, C, tr, 1.0f - lr * args.wd, step, tid, own0, own1);
+    muon_epilogue(mt.param, mt.pbf, sX, px, R, C, tr, 1.0f - lr * args.wd, step, tid, own0, own1, mt.frag, mt.frag_row);
     if (pro) {  // this part's momentum rows, once every part has read the old ones
         if (wave == 0) mc_wait(pro, (uint32_t)np, (gu32_t *)(args.sync + 16 * mat + 1));
         __syncthreads();
@@ -1265,7 +1287,10 @@ static int muon_launch(g2048_stream_t stream, const g2048_muon_matrix *mats, int
         if (!m.param || !m.grad || !m.momentum || !g2048_muon_supported(m.rows, m.cols)) return G2048_EINVAL;
         if (((uintptr_t)m.param | (uintptr_t)m.grad | (uintptr_t)m.momentum) % 16 || (uintptr_t)m.param_bf16 % 8)
             return G2048_EINVAL;
-        a.m[i] = MuonMat{m.param, m.grad, m.momentum, m.param_bf16, m.rows, m.cols, m.lr_index, 0};
+        if (m.head_frag && (m.rows > m.cols || m.cols % 4 || m.frag_row < 0 || m.frag_row + m.rows > 5 || m.cols > 1024))
+            return G2048_EINVAL;  // a head matrix: <= 5 rows of h columns, row-major epilogue
+        a.m[i] = MuonMat{m.param, m.grad, m.momentum, m.param_bf16, (uint16_t *)m.head_frag, m.rows, m.cols, m.lr_index,
+                         m.frag_row};
         const size_t b = muon_lds_bytes(m.rows, m.cols);
         lds = b > lds ? b : lds;
     }

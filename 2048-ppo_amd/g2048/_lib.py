@@ -116,8 +116,8 @@ class Dy(ctypes.Structure):
 class MuonMatrix(ctypes.Structure):
     """struct g2048_muon_matrix"""
     _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("momentum", ctypes.c_void_p),
-                ("param_bf16", ctypes.c_void_p), ("rows", ctypes.c_int32), ("cols", ctypes.c_int32),
-                ("lr_index", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+                ("param_bf16", ctypes.c_void_p), ("head_frag", ctypes.c_void_p), ("rows", ctypes.c_int32),
+                ("cols", ctypes.c_int32), ("lr_index", ctypes.c_int32), ("frag_row", ctypes.c_int32)]
 
 
 class MuonCfg(ctypes.Structure):

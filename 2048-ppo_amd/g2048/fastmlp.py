@@ -92,6 +92,7 @@ class FusedPPOUpdater(PPOUpdater):
         self.seed = seed
         self.bs = 0
         self.fused_pass = False
+        self.opt_splits_heads = False
 
     # ---------------------------------------------------------------- buffers -------------
     def _alloc(self, bs: int):
@@ -132,6 +133,9 @@ class FusedPPOUpdater(PPOUpdater):
         if self.fused_pass:
             self.dzb = torch.empty(bs, 16, dtype=bf, device=d)
             self.head_frag = torch.zeros(L.head_split_bytes(h), dtype=torch.uint8, device=d)
+            # the fused Muon step writes the heads' split itself (no g2048_head_split per minibatch)
+            self.opt_splits_heads = bool(self.fused_opt and hasattr(self.opt, "set_head_frag") and self.opt.set_head_frag(
+                self.head_frag, {self.wa: 0, self.wv: 4}))
             self.part_fwd = torch.empty(L.mlp_pass_partials(bs, True), dtype=f32, device=d)
             self.part_klp = torch.empty(L.mlp_pass_partials(bs, False), dtype=f32, device=d)
             self.part_wh = torch.empty(L.wgrad_partials(bs, 16, h), dtype=f32, device=d)
@@ -347,7 +351,8 @@ class FusedPPOUpdater(PPOUpdater):
             nl = len(self.lin)
             w_last = self.wbf[-1]
             if self.fused_pass:  # the whole re-forward + KL in one launch (the step changed the heads)
-                self._split_heads()
+                if not self.opt_splits_heads:
+                    self._split_heads()
                 L.ppo_forward_kl(self._kl_args, self.kl, defer=kl_job)
             elif nl > 1 and self.mf_ok[-1] and L.mlp_fwd_kl_supported(w_last.shape[0], w_last.shape[1]):
                 # the last block fused with the action head and the KL reduction (no H write / re-read)

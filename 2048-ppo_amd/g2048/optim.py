@@ -236,6 +236,18 @@ class FusedMuonAdamW(MuonAdamW):
         self._bf16 = {id(p): t for p, t in mapping.items()}
         self._mats = None
 
+    def set_head_frag(self, frag, rows: dict) -> bool:
+        """frag: g2048_head_split's fragment image; rows {head weight parameter: its first head row}
+        (action head 0, value head 4).  The Muon kernel then writes those matrices' three-term bf16
+        split with each step (no g2048_head_split launch after it).  False when a head is not a
+        Muon matrix of this optimizer (the caller keeps splitting)."""
+        ids = {id(p) for p, _ in self.muon}
+        if not all(id(p) in ids for p in rows):
+            return False
+        self._frag = (frag, {id(p): r for p, r in rows.items()})
+        self._mats = None
+        return True
+
     def _build(self):
         L = self._L
         mats = (L.MuonMatrix * len(self.muon))()
@@ -243,8 +255,11 @@ class FusedMuonAdamW(MuonAdamW):
             if p.grad is None or not p.grad.is_contiguous():
                 raise RuntimeError("FusedMuonAdamW needs contiguous gradients (a GradBucket)")
             bf = self._bf16.get(id(p))
+            frag, frow = getattr(self, "_frag", (None, {}))
+            fr = frow.get(id(p))
             mats[k] = L.MuonMatrix(p.data_ptr(), p.grad.data_ptr(), buf.data_ptr(), bf.data_ptr() if bf is not None else None,
-                                   p.shape[0], p.shape[1], gi, 0)
+                                   frag.data_ptr() if fr is not None else None, p.shape[0], p.shape[1], gi,
+                                   fr if fr is not None else 0)
         groups = (L.AdamWGroup * len(self.adam_groups))()
         for k, grp in enumerate(self.adam_groups):
             g = self._flat_grad(grp)
@@ -313,6 +328,9 @@ class ScheduledMuonAdamW:
 
     def set_bf16_copies(self, mapping):
         self.opt.set_bf16_copies(mapping)
+
+    def set_head_frag(self, frag, rows):
+        return self.opt.set_head_frag(frag, rows)
 
     def zero_grad(self, set_to_none: bool = False):
         pass

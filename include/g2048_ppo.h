@@ -366,9 +366,12 @@ typedef struct g2048_muon_matrix {
     const float *grad;     /* [rows, cols] fp32 (multiplied by *clip_coef_dev when given) */
     float *momentum;       /* [rows, cols] fp32 momentum buffer */
     uint16_t *param_bf16;  /* optional: bf16 copy of the updated weight */
+    void *head_frag;       /* optional: a head matrix ([wa] or [wv], cols = h): the updated weight's
+                            * three-term bf16 split written into rows frag_row .. frag_row + rows - 1
+                            * of g2048_head_split's fragment image (its other bytes untouched) */
     int32_t rows, cols;
     int32_t lr_index;      /* this matrix's learning rate is lr_dev[lr_index] */
-    int32_t pad_;
+    int32_t frag_row;      /* the first head row of this matrix in head_frag (wa: 0, wv: 4) */
 } g2048_muon_matrix;
 
 typedef struct g2048_muon_cfg {

@@ -63,6 +63,7 @@ def test_struct_layouts_match_header():
     assert _lib.MlpPassArgs.keep.offset == 408
     assert ctypes.sizeof(_lib.MlpBackArgs) == 312 and _lib.MlpBackArgs.keep.offset == 304
     assert ctypes.sizeof(_lib.MuonCfg) == 48 and _lib.MuonCfg.workspace.offset == 40
+    assert ctypes.sizeof(_lib.MuonMatrix) == 56 and _lib.MuonMatrix.head_frag.offset == 32
     assert _lib.MlpPassArgs.partials.offset == 400
 
 

@@ -607,6 +607,35 @@ def test_muon_multi_cu_equals_one_cu(dev, h, parts, loaded, monkeypatch):
         assert torch.equal(a, b), (a - b).abs().max()
 
 
+@pytest.mark.parametrize("h", [196, 64])
+def test_muon_step_writes_the_head_split(dev, h):
+    """FusedMuonAdamW with the head fragment image registered (set_head_frag): after each step the
+    image is bitwise g2048_head_split of the updated action / value head weights (the per-minibatch
+    head_split launch it replaces)."""
+    import agent
+    from g2048 import _lib as L
+    from g2048.dist import GradBucket
+    from g2048.optim import FusedMuonAdamW
+    torch.manual_seed(h)
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=h, num_layers=2)).to(dev)
+    with torch.no_grad():
+        m.action_head.weight.normal_(0, 0.05)
+        m.value_head.weight.normal_(0, 0.05)
+    opt = FusedMuonAdamW(m, 1e-3, 1e-4)
+    order = [q for q, _ in opt.muon] + [q for grp in opt.adam_groups for q in grp["params"]]
+    bk = GradBucket(order)
+    frag = torch.zeros(L.head_split_bytes(h), dtype=torch.uint8, device=dev)
+    assert opt.set_head_frag(frag, {m.action_head.weight: 0, m.value_head.weight: 4})
+    L.head_split(m.action_head.weight, m.value_head.weight, frag)
+    ref = torch.empty_like(frag)
+    for s in range(3):
+        bk.flat.copy_(torch.randn(bk.flat.shape, generator=torch.Generator().manual_seed(s)).to(dev) * 1e-2)
+        opt.step_clipped(bk.flat, 1.0)
+        L.head_split(m.action_head.weight, m.value_head.weight, ref)
+        torch.cuda.synchronize()
+        assert torch.equal(frag, ref), s
+
+
 def test_fused_muon_supported_shapes():
     from g2048 import _lib as L
     assert L.muon_supported(196, 196) and L.muon_supported(196, 48) and L.muon_supported(4, 196)
