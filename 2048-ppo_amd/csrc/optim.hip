@@ -165,6 +165,7 @@ struct MuonArgs {
     // job_nparts blocks: row blocks of its Newton-Schulz products, one exchange of X per iteration),
     // kRoleAdam (job_part = the AdamW block index) or kRoleIdle (a gap of the XCD placement)
     int njobs;  // grid size
+    int npartials;  // clip partial sums (64: g2048_grad_sumsq's)
     uint8_t job_mat[kMuonMaxJobs], job_part[kMuonMaxJobs], job_nparts[kMuonMaxJobs];
     uint32_t *sync;              // per matrix: the exchange counter (zeroed before every launch)
     char *xg;                    // per matrix: two N x P-byte bf16 exchange images (X of even / odd iterations)
@@ -993,12 +994,20 @@ __device__ __forceinline__ void ns_square_mc(char *sX, char *sG, const MuonArgs 
 }
 
 // The AdamW update of the 1-D groups by block b of nb (clip coefficient from the partials).
+// the clip's sum of squares from the partials: lane l sums entries l, l + 64, ... in order (one entry
+// per lane for g2048_grad_sumsq's 64: grad_norm_kernel's arithmetic), then the wave's xor tree
+__device__ __forceinline__ float clip_sumsq(const MuonArgs &args, int lane) {
+    float t = 0.0f;
+    for (int i = lane; i < args.npartials; i += 64) t += args.partials[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    return t;
+}
+
 __device__ __forceinline__ void adam_blocks(const MuonArgs &args, int b, int nb) {
     float cf = 1.0f;
     if (args.partials) {  // grad_norm_kernel's arithmetic, as in the Muon blocks (same result)
-        float t = args.partials[threadIdx.x & 63];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+        const float t = clip_sumsq(args, threadIdx.x & 63);
         cf = fminf(args.max_norm / (sqrtf(t) + 1e-6f), 1.0f);
     }
     const AdamArgs &a = args.adam;
@@ -1018,9 +1027,7 @@ __device__ __forceinline__ float block_clip_coef(const MuonArgs &args, int tid, 
     __shared__ float s_coef;
     if (!args.partials) return args.clip ? *args.clip : 1.0f;
     if (tid < 64) {
-        float t = args.partials[tid];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+        const float t = clip_sumsq(args, tid);
         const float nrm = sqrtf(t);
         const float cf = fminf(args.max_norm / (nrm + 1e-6f), 1.0f);
         if (tid == 0) {
@@ -1306,6 +1313,8 @@ static int muon_launch(g2048_stream_t stream, const g2048_muon_matrix *mats, int
     a.lr = lr_dev;
     a.clip = clip_coef_dev;
     a.partials = partials;
+    a.npartials = cfg->npartials > 0 ? cfg->npartials : 64;
+    if (a.npartials > G2048_COLSUM_SQ_MAX) return G2048_EINVAL;
     a.max_norm = max_norm;
     a.norm_out = norm_out;
     a.coef_out = coef_out;

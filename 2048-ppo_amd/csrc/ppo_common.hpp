@@ -85,6 +85,60 @@ __device__ __forceinline__ void drop_mult(const Drop &d, uint32_t row, uint32_t 
     drop_mult_bits(d, drop_draw(d, row, cg), k);
 }
 
+// ------------------------------------------------------------------ minibatch statistics -------
+struct StatsArgs {
+    const float *sums, *gn, *beta;
+    const int64_t *rows;
+    float *stats;
+    uint64_t *counter;
+    uint32_t *sync;
+    float critic, m;
+    int64_t *idx_off;  // nullable: += idx_step (the next minibatch's rows in the epoch's permutation)
+    int64_t idx_step;
+};
+
+// g2048_ppo_stats' arithmetic by the threads of one block (>= 256; LDS scratch of 2 KiB + 4): the KL
+// partial rows [kl_rows][2] summed / maxed in ppo_stats_kernel's fixed order, then the stats update
+// by thread 0, which also puts the ticket word back to zero
+__device__ __forceinline__ void stats_block(const StatsArgs &a, const float *kl, int kl_rows, char *lds, int tid) {
+    float(*red)[256] = reinterpret_cast<float(*)[256]>(lds);
+    float ks = 0.0f, km = -INFINITY;
+    if (tid < 256) {
+        for (int b = tid; b < kl_rows; b += 256) {
+            ks += kl[2 * b];
+            km = fmaxf(km, kl[2 * b + 1]);
+        }
+        red[0][tid] = ks;
+        red[1][tid] = km;
+    }
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (tid < w) {
+            red[0][tid] += red[0][tid + w];
+            red[1][tid] = fmaxf(red[1][tid], red[1][tid + w]);
+        }
+        __syncthreads();
+    }
+    if (tid != 0) return;
+    ks = red[0][0];
+    km = red[1][0];
+    const float m = a.rows ? (float)max(*a.rows, (int64_t)1) : a.m;
+    const float s_ppo = a.sums[0] / m, s_ent = a.sums[1] / m, s_v = a.sums[2] / m, b = *a.beta;
+    a.stats[0] += -(s_ppo - a.critic * s_v + b * s_ent);
+    a.stats[1] += -s_ppo;
+    a.stats[2] += -b * s_ent;
+    a.stats[3] += a.critic * s_v;
+    a.stats[4] += *a.gn;
+    a.stats[5] += s_ent;
+    a.stats[6] += ks;
+    a.stats[7] += ks / m;
+    a.stats[8] = fmaxf(a.stats[8], km);
+    if (a.counter) *a.counter += 1ull;
+    if (a.idx_off) *a.idx_off += a.idx_step;
+    __hip_atomic_store((__attribute__((address_space(1))) uint32_t *)a.sync, 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ------------------------------------------------------------------ heads + PPO loss ---------
 struct HeadLossArgs {
     const int64_t *idx;

@@ -40,9 +40,12 @@
 using namespace g2048::tile;
 namespace P = g2048::ppo;
 
-static_assert(sizeof(g2048_mlp_pass_args) == 416 && offsetof(g2048_mlp_pass_args, drop) == 176 &&
-                  offsetof(g2048_mlp_pass_args, partials) == 400 && offsetof(g2048_mlp_pass_args, keep) == 408,
+static_assert(sizeof(g2048_mlp_pass_args) == 424 && offsetof(g2048_mlp_pass_args, drop) == 176 &&
+                  offsetof(g2048_mlp_pass_args, partials) == 400 && offsetof(g2048_mlp_pass_args, keep) == 408 &&
+                  offsetof(g2048_mlp_pass_args, idx_offset) == 416,
               "g2048_mlp_pass_args layout (tests/test_abi.py)");
+static_assert(sizeof(g2048_ppo_stats_args) == 88 && offsetof(g2048_ppo_stats_args, idx_offset) == 72,
+              "g2048_ppo_stats_args layout (tests/test_abi.py)");
 static_assert(sizeof(g2048_mlp_back_args) == 312 && offsetof(g2048_mlp_back_args, keep) == 304,
               "g2048_mlp_back_args layout (tests/test_abi.py)");
 
@@ -86,6 +89,8 @@ struct FpArgs {
     uint16_t *dzb;                 // train: bf16 [m][16]: hi(dz) 0..4, lo(dz) 8..12
     float *part;                   // per block: train kTrainParts floats, KL {sum, max}
     uint2 *keep;                   // train, optional: the blocks' keep bits [block][m][lane group]
+    P::StatsArgs st;               // KL, optional (st.stats): the last block folds g2048_ppo_stats in
+    const int64_t *idx_off;        // optional: rows batch.idx[*idx_off + r]
 };
 
 // The head matrix [wa (4 rows); wv] as three exact bf16 terms in the 16 rows of the head chain's A
@@ -156,6 +161,7 @@ __global__ __launch_bounds__(kFpThreads) void mlp_pass_kernel(FpArgs a) {
     const int g = lane >> 4, col = lane & 15;
     const int64_t m = a.m;
     const int64_t mv = a.la.rows ? min(*a.la.rows, m) : m;  // rows >= mv: padding of a ragged minibatch
+    const int64_t *idxp = a.la.idx + (a.idx_off ? *a.idx_off : 0);  // this minibatch's rows
     const float inv_m = a.la.rows ? 1.0f / (float)max(mv, (int64_t)1) : a.la.inv_m;
 
     // ---- the block weight images (bank-spread rows, zero K padding): 16 8-byte loads in flight per
@@ -206,7 +212,7 @@ __global__ __launch_bounds__(kFpThreads) void mlp_pass_kernel(FpArgs a) {
         if (r0 >= m) continue;  // an empty wave (no barrier below)
         const int64_t r = r0 + lane;  // this lane's row for the loss / KL ("lane = row")
         const bool live = lane < kFpRows && r < m, real = live && r < mv;
-        const uint4 b = live ? *reinterpret_cast<const uint4 *>(a.boards + a.la.idx[r] * 16) : make_uint4(0u, 0u, 0u, 0u);
+        const uint4 b = live ? *reinterpret_cast<const uint4 *>(a.boards + idxp[r] * 16) : make_uint4(0u, 0u, 0u, 0u);
 
         int wlane_t = wlane, glane_t = (col * 48 + 8 * g) * 2;
         asm volatile("" : "+v"(wlane_t), "+v"(glane_t));
@@ -346,7 +352,7 @@ __global__ __launch_bounds__(kFpThreads) void mlp_pass_kernel(FpArgs a) {
         // hold registers across the whole MLP
         P::RowIn in{};
         float4 old4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (TRAIN && real) in = P::load_row_in(a.la, a.la.idx[r]);
+        if (TRAIN && real) in = P::load_row_in(a.la, idxp[r]);
         if (!TRAIN && real) old4 = *reinterpret_cast<const float4 *>(a.masked + r * 4);
         heads_to_rows(accH);
         float z5[5];
@@ -416,6 +422,30 @@ __global__ __launch_bounds__(kFpThreads) void mlp_pass_kernel(FpArgs a) {
         float t = red[tid];
         for (int w = 1; w < kFpThreads / 64; w++) t = (!TRAIN && tid == 1) ? fmaxf(t, red[w * NP + tid]) : t + red[w * NP + tid];
         a.part[(int64_t)blockIdx.x * NP + tid] = t;
+    }
+    if (!TRAIN && a.st.stats) {
+        // the last block to finish reduces every block's {sum, max} and accumulates the minibatch
+        // statistics (g2048_ppo_stats folded in): cdna_hip_programming.md Guideline 16's counter
+        // form -- plain partial stores, every wave drains, one release + ticket; the last arriver
+        // acquires, reads with plain loads and puts the ticket back to zero for the next launch
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int *flag = reinterpret_cast<int *>(smem + 4096);
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t k = __hip_atomic_fetch_add((__attribute__((address_space(1))) uint32_t *)a.st.sync, 1u,
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *flag = k == gridDim.x - 1u;
+        }
+        __syncthreads();
+        if (!*flag) return;
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        P::stats_block(a.st, a.part, (int)gridDim.x, smem, tid);
     }
 }
 
@@ -797,6 +827,7 @@ int fp_fill(const g2048_mlp_pass_args *p, FpArgs &a, bool train) {
     a.part = p->partials;
     if (train && p->keep && !al(p->keep, 8)) return G2048_EINVAL;
     a.keep = train ? (uint2 *)p->keep : nullptr;
+    a.idx_off = p->idx_offset;
     return G2048_OK;
 }
 
@@ -943,6 +974,17 @@ int g2048_ppo_backward(g2048_stream_t stream, const g2048_mlp_back_args *p, floa
         }
     }
     return fp_status();
+}
+
+int g2048_ppo_forward_kl_stats(g2048_stream_t stream, const g2048_mlp_pass_args *p, const g2048_ppo_stats_args *st) {
+    if (!p || !st || !st->sums || !st->grad_norm || !st->beta_dev || !st->stats || !st->sync || st->m <= 0)
+        return G2048_EINVAL;
+    FpArgs a;
+    const int rc0 = fp_fill(p, a, false);
+    if (rc0) return rc0;
+    a.st = P::StatsArgs{st->sums, st->grad_norm, st->beta_dev, st->rows, st->stats, st->counter, st->sync,
+                        st->critic, (float)st->m, st->idx_offset, st->idx_step};
+    return fp_launch<false>((hipStream_t)stream, a, p->hidden, fp_blocks(p->m));
 }
 
 int g2048_ppo_forward_kl(g2048_stream_t stream, const g2048_mlp_pass_args *p, float *out, g2048_colsum_job *defer) {

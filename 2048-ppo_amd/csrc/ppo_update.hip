@@ -1657,6 +1657,9 @@ struct ColsumBatch {
     g2048_colsum_job job[G2048_COLSUM_MAX_JOBS];
     int first[G2048_COLSUM_MAX_JOBS + 1];
     int njobs;
+    int nsq;      // sq: per-block sums of squares of the gradient segments (pad_ bit k: segment k)
+    float *sq;
+    float *tick;  // += 1 by block 0 (the optimizer's step count)
 };
 
 // a job whose partial rows are whole float4s runs 4 columns per lane (256 per block: 16-byte loads);
@@ -1698,7 +1701,21 @@ __global__ __launch_bounds__(1024) void colsum_batch_kernel(const ColsumBatch cb
     }
     lds[rg][cl] = make_float4(t[0], t[1], t[2], t[3]);
     __syncthreads();
-    if (rg != 0 || c0 >= jb.cols) return;
+    if (cb.sq) {  // block 0: the step count and the zero tail of the partials
+        if (blockIdx.x == 0 && threadIdx.x == 0 && cb.tick) *cb.tick += 1.0f;
+        if (blockIdx.x == 0)
+            for (int b = (int)gridDim.x + (int)threadIdx.x; b < cb.nsq; b += 1024) cb.sq[b] = 0.0f;
+    }
+    if (rg != 0) return;
+    if (c0 >= jb.cols) {
+        if (cb.sq) {  // this wave still joins the block's sum of squares
+            float z = 0.0f;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) z += __shfl_xor(z, o);
+            if (cl == 0) cb.sq[blockIdx.x] = z;
+        }
+        return;
+    }
     float acc[4];
     {
         const float4 a0 = lds[0][cl];
@@ -1714,16 +1731,24 @@ __global__ __launch_bounds__(1024) void colsum_batch_kernel(const ColsumBatch cb
 #pragma unroll
         for (int u = 0; u < 4; u++) acc[u] = c0 + u == jb.max_col ? fmaxf(acc[u], av[u]) : acc[u] + av[u];
     }
+    float ss = 0.0f;
     for (int u = 0; u < W; u++) {
         const int c = c0 + u;
+        if (c >= jb.cols) break;
         int off = 0;
         for (int k = 0; k < jb.nseg; k++) {
             if (c < off + jb.len[k]) {
                 jb.dst[k][c - off] = acc[u];
+                if ((jb.pad_ >> k) & 1) ss += acc[u] * acc[u];
                 break;
             }
             off += jb.len[k];
         }
+    }
+    if (cb.sq) {  // rg == 0: one wave holds the block's outputs
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+        if (cl == 0) cb.sq[blockIdx.x] = ss;
     }
 }
 
@@ -2402,10 +2427,42 @@ int g2048_ppo_stats(g2048_stream_t stream, const float *sums, const float *kl, i
     return status();
 }
 
+static int colsum_batch_build(const g2048_colsum_job *jobs, int32_t njobs, ColsumBatch &cb, int &blocks);
+
 int g2048_colsum_batch(g2048_stream_t stream, const g2048_colsum_job *jobs, int32_t njobs) {
-    if (njobs < 0 || njobs > G2048_COLSUM_MAX_JOBS || (njobs && !jobs)) return G2048_EINVAL;
     ColsumBatch cb{};
     int blocks = 0;
+    const int st = colsum_batch_build(jobs, njobs, cb, blocks);
+    if (st || !blocks) return st;
+    hipLaunchKernelGGL(colsum_batch_kernel, dim3(blocks), dim3(1024), 0, (hipStream_t)stream, cb);
+    return status();
+}
+
+int g2048_colsum_batch_blocks(const g2048_colsum_job *jobs, int32_t njobs) {
+    ColsumBatch cb{};
+    int blocks = 0;
+    const int st = colsum_batch_build(jobs, njobs, cb, blocks);
+    return st ? -1 : blocks;
+}
+
+int g2048_colsum_batch_sq(g2048_stream_t stream, const g2048_colsum_job *jobs, int32_t njobs, float *sq, int32_t nsq,
+                          float *tick) {
+    ColsumBatch cb{};
+    int blocks = 0;
+    const int st = colsum_batch_build(jobs, njobs, cb, blocks);
+    if (st) return st;
+    if (!sq || nsq < 1 || nsq > G2048_COLSUM_SQ_MAX || blocks > nsq || ((uintptr_t)sq & 3u)) return G2048_EINVAL;
+    cb.sq = sq;
+    cb.nsq = nsq;
+    cb.tick = tick;
+    if (!blocks) blocks = 1;  // (an empty batch still ticks and zeroes the partials)
+    hipLaunchKernelGGL(colsum_batch_kernel, dim3(blocks), dim3(1024), 0, (hipStream_t)stream, cb);
+    return status();
+}
+
+static int colsum_batch_build(const g2048_colsum_job *jobs, int32_t njobs, ColsumBatch &cb, int &blocks) {
+    if (njobs < 0 || njobs > G2048_COLSUM_MAX_JOBS || (njobs && !jobs)) return G2048_EINVAL;
+    blocks = 0;
     for (int j = 0; j < njobs; j++) {
         const g2048_colsum_job &jb = jobs[j];
         if (!jb.part && jb.cols == 0) continue;  // empty (m = 0) job
@@ -2422,9 +2479,7 @@ int g2048_colsum_batch(g2048_stream_t stream, const g2048_colsum_job *jobs, int3
         blocks += colsum_vec(jb) ? (jb.cols + 255) / 256 : (jb.cols + 63) / 64;
     }
     cb.first[cb.njobs] = blocks;
-    if (!blocks) return G2048_OK;
-    hipLaunchKernelGGL(colsum_batch_kernel, dim3(blocks), dim3(1024), 0, (hipStream_t)stream, cb);
-    return status();
+    return G2048_OK;
 }
 
 int g2048_dropout_mask(g2048_stream_t stream, int64_t m, int32_t h, const g2048_dropout *drop, uint8_t *mask) {

@@ -31,6 +31,7 @@ EXPORTED = (
     # include/g2048_ppo.h
     "g2048_obs_gather", "g2048_ln_act_fwd", "g2048_ln_act_bwd_partials", "g2048_ln_act_bwd",
     "g2048_ppo_head_partials", "g2048_ppo_head_loss", "g2048_ppo_head_kl", "g2048_dropout_mask", "g2048_colsum_batch",
+    "g2048_colsum_batch_blocks", "g2048_colsum_batch_sq",
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_wgrad_pair_partials", "g2048_wgrad_pair", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
     "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_muon_workspace_bytes", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_rms_res_fwd2", "g2048_urm_rms_res_bwd2", "g2048_urm_add_cast", "g2048_urm_add_cast_bwd", "g2048_urm_forward_drop", "g2048_urm_rms_res_fwd",
@@ -38,7 +39,7 @@ EXPORTED = (
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
     "g2048_head_split_bytes", "g2048_head_split", "g2048_mlp_pass_supported", "g2048_mlp_pass_partials",
-    "g2048_ppo_forward_loss", "g2048_ppo_forward_kl", "g2048_mlp_back_partials", "g2048_ppo_backward",
+    "g2048_ppo_forward_loss", "g2048_ppo_forward_kl", "g2048_ppo_forward_kl_stats", "g2048_mlp_back_partials", "g2048_ppo_backward",
     "g2048_mlp_wgrad_partials", "g2048_mlp_wgrad",
     # include/g2048_urm.h
     "g2048_urm_stem", "g2048_urm_attention", "g2048_urm_residual_rms", "g2048_urm_swiglu_conv",
@@ -98,6 +99,7 @@ class PPOBatch(ctypes.Structure):
 DY_MAX_P = 4
 COLSUM_SEGS = 5
 COLSUM_MAX_JOBS = 16
+COLSUM_SQ_MAX = 1024
 
 
 class ColsumJob(ctypes.Structure):
@@ -125,7 +127,7 @@ class MuonCfg(ctypes.Structure):
     _fields_ = [("momentum", ctypes.c_float), ("weight_decay", ctypes.c_float), ("ns_a", ctypes.c_float),
                 ("ns_b", ctypes.c_float), ("ns_c", ctypes.c_float), ("ns_eps", ctypes.c_float),
                 ("ns_steps", ctypes.c_int32), ("nesterov", ctypes.c_int32), ("parts", ctypes.c_int32),
-                ("pad_", ctypes.c_int32), ("workspace", ctypes.c_void_p)]
+                ("npartials", ctypes.c_int32), ("workspace", ctypes.c_void_p)]
 
 
 class AdamWGroup(ctypes.Structure):
@@ -143,7 +145,7 @@ class MlpPassArgs(ctypes.Structure):
                 ("ln_beta", vp * 3), ("head_frag", vp), ("ba", vp), ("bv", vp), ("drop", Dropout * 2),
                 ("beta_dev", vp), ("critic", ctypes.c_float), ("clip_eps", ctypes.c_float), ("x0", vp), ("g", vp * 3),
                 ("h", vp * 3), ("mean", vp * 3), ("rstd", vp * 3), ("masked", vp), ("dz", vp), ("dz_bf16", vp),
-                ("partials", vp), ("keep", vp)]
+                ("partials", vp), ("keep", vp), ("idx_offset", vp)]
 
 
 class MlpBackArgs(ctypes.Structure):
@@ -160,6 +162,14 @@ class MlpWgradArgs(ctypes.Structure):
     vp = ctypes.c_void_p
     _fields_ = [("m", ctypes.c_int64), ("hidden", ctypes.c_int32), ("pad_", ctypes.c_int32), ("dz_bf16", vp),
                 ("h2", vp), ("dg", vp * 3), ("x", vp * 3), ("partials", vp)]
+
+
+class PPOStatsArgs(ctypes.Structure):
+    """struct g2048_ppo_stats_args"""
+    vp = ctypes.c_void_p
+    _fields_ = [("sums", vp), ("grad_norm", vp), ("beta_dev", vp), ("rows", vp), ("stats", vp), ("counter", vp),
+                ("sync", vp), ("critic", ctypes.c_float), ("pad_", ctypes.c_int32), ("m", ctypes.c_int64),
+                ("idx_offset", vp), ("idx_step", ctypes.c_int64)]
 
 
 class PolicyRolloutArgs(ctypes.Structure):
@@ -218,6 +228,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_ln_act_bwd": (ctypes.c_int, [vp, ctypes.POINTER(Dy), vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32,
                                             dp, jp]),
         "g2048_colsum_batch": (ctypes.c_int, [vp, jp, i32]),
+        "g2048_colsum_batch_blocks": (ctypes.c_int, [jp, i32]),
+        "g2048_colsum_batch_sq": (ctypes.c_int, [vp, jp, i32, vp, i32, vp]),
         "g2048_ppo_head_partials": (sz, [i64, i32]),
         "g2048_ppo_head_loss": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, bp, vp, ctypes.c_float,
                                                ctypes.c_float, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, jp]),
@@ -244,6 +256,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_ppo_backward": (ctypes.c_int, [vp, ctypes.POINTER(MlpBackArgs), ctypes.POINTER(vp), ctypes.POINTER(vp),
                                               jp]),
         "g2048_ppo_forward_kl": (ctypes.c_int, [vp, ctypes.POINTER(MlpPassArgs), vp, jp]),
+        "g2048_ppo_forward_kl_stats": (ctypes.c_int, [vp, ctypes.POINTER(MlpPassArgs), ctypes.POINTER(PPOStatsArgs)]),
         "g2048_mlp_wgrad_partials": (sz, [i64, i32]),
         "g2048_mlp_wgrad": (ctypes.c_int, [vp, ctypes.POINTER(MlpWgradArgs), vp, ctypes.POINTER(vp), jp]),
         "g2048_linear_dgrad_supported": (ctypes.c_int, [i32, i32]),
@@ -598,7 +611,7 @@ def head_split(wa, wv, frag):
 def make_mlp_pass(boards, batch: PPOBatch, m: int, w_stem, w_blocks, gammas, betas, head_frag, ba, bv=None,
                   drops=(None, None), beta_dev=None, critic=0.0, clip_eps=0.2, decouple=False, x0=None,
                   g=(None, None, None), h=(None, None, None), mean=(None, None, None), rstd=(None, None, None),
-                  masked=None, dz=None, dz_bf16=None, partials=None, keep=None) -> MlpPassArgs:
+                  masked=None, dz=None, dz_bf16=None, partials=None, keep=None, idx_offset=None) -> MlpPassArgs:
     """struct g2048_mlp_pass_args for g2048_ppo_forward_loss / g2048_ppo_forward_kl (GameMLP, 2 blocks).
     keep (train pass, optional): int64 [2, m, 4] out, the blocks' dropout keep bits for the backward."""
     a = MlpPassArgs()
@@ -630,6 +643,7 @@ def make_mlp_pass(boards, batch: PPOBatch, m: int, w_stem, w_blocks, gammas, bet
     a.dz_bf16 = _dev(dz_bf16, torch.bfloat16, "dz_bf16")
     a.partials = _dev(partials, torch.float32, "partials")
     a.keep = _dev(keep, torch.int64, "keep")
+    a.idx_offset = _dev(idx_offset, torch.int64, "idx_offset")
     return a
 
 
@@ -644,6 +658,19 @@ def ppo_forward_kl(args: MlpPassArgs, out, defer: ColsumJob | None = None):
     """The fused KL re-forward of one minibatch: out[2] = {sum KL, max KL}."""
     _check(load().g2048_ppo_forward_kl(_stream(out), ctypes.byref(args), _dev(out, torch.float32, "out"),
                                        _defer(defer)), "g2048_ppo_forward_kl")
+
+
+def ppo_forward_kl_stats(args: MlpPassArgs, sums, grad_norm, beta_dev, critic: float, m: int, stats, sync,
+                         counter=None, rows=None, idx_offset=None, idx_step: int = 0):
+    """The fused KL re-forward whose last block also accumulates the minibatch statistics
+    (g2048_ppo_stats folded in); sync: a zeroed int32 device word kept across calls."""
+    st = PPOStatsArgs(_dev(sums, torch.float32, "sums"), _dev(grad_norm, torch.float32, "grad_norm"),
+                      _dev(beta_dev, torch.float32, "beta_dev"), _dev(rows, torch.int64, "rows"),
+                      _dev(stats, torch.float32, "stats"), _dev(counter, torch.int64, "counter"),
+                      _dev(sync, torch.int32, "sync"), float(critic), 0, int(m),
+                      _dev(idx_offset, torch.int64, "idx_offset"), int(idx_step))
+    _check(load().g2048_ppo_forward_kl_stats(_stream(stats), ctypes.byref(args), ctypes.byref(st)),
+           "g2048_ppo_forward_kl_stats")
 
 
 def mlp_back_partials(m: int, h: int) -> int:
@@ -772,6 +799,25 @@ def colsum_batch(jobs):
         jobs = (ColsumJob * max(1, n))(*jobs)
     stream = torch.cuda.current_stream().cuda_stream
     _check(load().g2048_colsum_batch(ctypes.c_void_p(stream), jobs, n), "g2048_colsum_batch")
+
+
+def colsum_batch_sq(jobs, sq, tick=None):
+    """colsum_batch + the gradient norm's partials: sq (fp32, COLSUM_SQ_MAX) <- per-block sums of
+    squares of the segments marked in each job's pad_ (bit k = segment k is gradient), *tick += 1."""
+    n = len(jobs)
+    if n > COLSUM_MAX_JOBS:
+        raise G2048Error(f"at most {COLSUM_MAX_JOBS} column-sum jobs per launch")
+    if not isinstance(jobs, ctypes.Array):
+        jobs = (ColsumJob * max(1, n))(*jobs)
+    stream = torch.cuda.current_stream().cuda_stream
+    _check(load().g2048_colsum_batch_sq(ctypes.c_void_p(stream), jobs, n, _dev(sq, torch.float32, "sq"), sq.numel(),
+                                        _dev(tick, torch.float32, "tick")), "g2048_colsum_batch_sq")
+
+
+def colsum_batch_blocks(jobs) -> int:
+    if not isinstance(jobs, ctypes.Array):
+        jobs = (ColsumJob * max(1, len(jobs)))(*jobs)
+    return int(load().g2048_colsum_batch_blocks(jobs, len(jobs)))
 
 
 # ------------------------------------------------------------- optimizer step -------------------

@@ -33,6 +33,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib as L
+from .dist import world
 from .ppo import STAT_KEYS, PPOConfig, PPOUpdater
 
 
@@ -188,6 +189,8 @@ class FusedPPOUpdater(PPOUpdater):
         common = dict(w_stem=self.wbf[0], w_blocks=self.wbf[1:], gammas=[ln.weight for ln in self.ln],
                       betas=[ln.bias for ln in self.ln], head_frag=self.head_frag, ba=self.ba,
                       drops=(self._drop(1, pass_), self._drop(2, pass_)), masked=self.masked)
+        if self._offset:
+            common["idx_offset"] = self.idx_off
         if not train:
             return L.make_mlp_pass(data["boards"], batch, idx.shape[0], partials=self.part_klp, **common)
         return L.make_mlp_pass(data["boards"], batch, idx.shape[0], bv=self.bv, beta_dev=self._beta_dev,
@@ -251,8 +254,7 @@ class FusedPPOUpdater(PPOUpdater):
                         self.wh_out, [w.grad for w in self.lin], defer=jw)
             head_grad_job(jw[0], self.h, self.wa.grad, self.wv.grad, self.wh_spill)
             jobs.extend(jw)
-            for i in range(0, len(jobs), L.COLSUM_MAX_JOBS):
-                L.colsum_batch(jobs[i:i + L.COLSUM_MAX_JOBS])
+            self._colsum(jobs)
             return
         jobs.append(L.ColsumJob())
         L.wgrad(self.DG[0], self.x0, self.part_wg[0], self.lin[0].grad, defer=jobs[-1])
@@ -265,8 +267,30 @@ class FusedPPOUpdater(PPOUpdater):
             for l in (1, 2):
                 jobs.append(L.ColsumJob())
                 L.wgrad(self.DG[l], self.H[l - 1], self.part_wg[l], self.lin[l].grad, defer=jobs[-1])
+        self._colsum(jobs)
+
+    def _colsum(self, jobs):
+        """The minibatch's deferred column sums in one launch; single process with the fused optimizer:
+        g2048_colsum_batch_sq, which also writes the gradient norm's partials and counts the step, so
+        the optimizer step needs no pass over the bucket (self._sq_done)."""
+        inner = getattr(self.opt, "opt", self.opt)
+        self._sq_done = False
+        if (self.fused_opt and len(jobs) <= L.COLSUM_MAX_JOBS and hasattr(inner, "step_t") and world()[1] == 1
+                and L.colsum_batch_blocks(jobs) <= L.COLSUM_SQ_MAX):
+            skip = {self.sums.data_ptr(), getattr(self, "wh_spill", self.sums).data_ptr()}
+            for j in jobs:  # pad_ bit k: segment k is a gradient (not the loss sums, not the head spill)
+                j.pad_ = sum(1 << k for k in range(j.nseg) if j.dst[k] not in skip)
+            if self.sq_part is None:
+                self.sq_part = torch.zeros(L.COLSUM_SQ_MAX, dtype=torch.float32, device=self.dev)
+            L.colsum_batch_sq(jobs, self.sq_part, inner.step_t)
+            self._sq_done = True
+            return
         for i in range(0, len(jobs), L.COLSUM_MAX_JOBS):
             L.colsum_batch(jobs[i:i + L.COLSUM_MAX_JOBS])
+
+    sq_part = None
+    _sq_done = False
+    kl_sync = None  # the fused KL pass's ticket word (g2048_ppo_forward_kl_stats)
 
     def loss_backward(self, data, idx, beta, jobs=None):
         """Heads + PPO loss (unless the fused train pass did them: its `jobs`) + backward of the
@@ -314,7 +338,17 @@ class FusedPPOUpdater(PPOUpdater):
 
     # ---------------------------------------------------------------- PPOUpdater hooks ----
     ragged_pad = True  # the ragged last minibatch runs padded to full size (g2048_ppo_batch.rows)
-    double_idx = True  # next minibatch's index copy beside the current replay (two captures)
+    MULTI = 8          # minibatch steps per captured graph in the offset path
+    _og = None         # the offset path's graphs (see _update_offset)
+    _offset = False    # the fused passes read rows perm[*idx_off + r] (set while capturing that path)
+
+    @property
+    def captured(self) -> bool:
+        return self._g is not None or self._og is not None
+
+    @property
+    def graph_split(self) -> bool:
+        return self._og is None and self._g is not None and self._g["g2"] is not None
 
     def _set_rows(self, n: int):
         self.rows.fill_(n)
@@ -323,7 +357,91 @@ class FusedPPOUpdater(PPOUpdater):
         bs = min(self.cfg.batch_size, data["actions"].shape[0])
         self._alloc(bs)
         self.refresh_weights()
+        if self.graph and self.fused_pass and self.grads.capturable() and not self.force_split:
+            return self._update_offset(data, beta, bs)
         return super().update(data, beta, encode)
+
+    # ---------------------------------------------------------------- offset path ---------
+    # The epoch's permutation lives in one device buffer and the fused passes read the minibatch's
+    # rows at a device offset that the KL pass's last block advances, so consecutive minibatch steps
+    # need no index copy and no host work between them: MULTI steps are captured in one hipGraph
+    # (plus a one-step graph for the rest and the padded ragged minibatch).
+    def _update_offset(self, data: dict, beta: float, bs: int) -> dict:
+        cfg = self.cfg
+        m_total = data["actions"].shape[0]
+        self.stats.zero_()
+        self.beta_t.fill_(beta)
+        self.model.train()
+        g = self._ensure_offset_graphs(data, bs)
+        nb = 0
+        for _ in range(cfg.epochs):
+            perm = torch.randperm(m_total, device=self.dev, generator=self.gen)
+            g["perm"][:m_total].copy_(perm)
+            g["perm"][m_total:m_total + bs].zero_()  # the padded ragged minibatch reads row 0
+            self.idx_off.zero_()
+            nfull, rag = divmod(m_total, bs)
+            k = 0
+            while k + self.MULTI <= nfull:
+                g["multi"].replay()
+                k += self.MULTI
+            while k < nfull:
+                g["single"].replay()
+                k += 1
+            if rag:
+                self._set_rows(rag)
+                g["single"].replay()
+                self._set_rows(bs)
+                k += 1
+            nb += k
+        st = self.stats / max(nb, 1)
+        st[STAT_KEYS.index("kl_max")] = self.stats[STAT_KEYS.index("kl_max")]
+        return {k: st[i] for i, k in enumerate(STAT_KEYS)}
+
+    def _ensure_offset_graphs(self, data, bs):
+        cap = data["actions"].untyped_storage().nbytes() // data["actions"].element_size()
+        key = (bs, cap) + tuple(t.data_ptr() for t in data.values())
+        if self._og is not None and self._og["key"] == key:
+            return self._og
+        self._og = None
+        torch.cuda.synchronize()
+        perm = torch.zeros(cap + bs, dtype=torch.int64, device=self.dev)
+        if getattr(self, "idx_off", None) is None:
+            self.idx_off = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        idx = perm[:bs]
+        params = list(self.model.parameters())
+        snap_p = [p.detach().clone() for p in params]
+        snap_o = self.opt.snapshot()
+        snap_s = self.stats.clone()
+        snap_x = self._extra_snapshot()
+        self._offset = True
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):  # warm-up outside the capture
+                    self._minibatch(idx, data, self.beta_t, None)
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            pool = torch.cuda.graph_pool_handle()
+            graphs = {}
+            for name, n in (("single", 1), ("multi", self.MULTI)):
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr, pool=pool):
+                    for _ in range(n):
+                        st = self._pre(idx, data, self.beta_t, None)
+                        self.grads.allreduce_mean()
+                        self._post(st, self.beta_t)
+                graphs[name] = gr
+        finally:
+            self._offset = False
+        with torch.no_grad():
+            for p, q in zip(params, snap_p):
+                p.copy_(q)
+        self.opt.restore(snap_o)
+        self.stats.copy_(snap_s)
+        self._extra_restore(snap_x)
+        self._og = {"key": key, "perm": perm, **graphs}
+        return self._og
 
     def _pre(self, idx, data, beta, encode):
         if idx.shape[0] != self.bs:  # ragged last minibatch of an eager pass
@@ -339,7 +457,8 @@ class FusedPPOUpdater(PPOUpdater):
     def _post(self, st, beta):
         cfg, m = self.cfg, self.bs
         if self.fused_opt:
-            gn = self.opt.step_clipped(self.grads.flat, cfg.max_grad_norm)
+            gn = self.opt.step_clipped(self.grads.flat, cfg.max_grad_norm,
+                                       sq=self.sq_part if self._sq_done else None)
         else:
             gn = self.grads.clip_(cfg.max_grad_norm)
             self.opt.step()
@@ -350,10 +469,18 @@ class FusedPPOUpdater(PPOUpdater):
             kl_job = L.ColsumJob()
             nl = len(self.lin)
             w_last = self.wbf[-1]
-            if self.fused_pass:  # the whole re-forward + KL in one launch (the step changed the heads)
+            b = beta if torch.is_tensor(beta) else torch.tensor(float(beta), device=self.dev)
+            if gn.dim() != 0:
+                gn = gn.reshape(())
+            if self.fused_pass:  # the whole re-forward + KL + the statistics in one launch
                 if not self.opt_splits_heads:
                     self._split_heads()
-                L.ppo_forward_kl(self._kl_args, self.kl, defer=kl_job)
+                if self.kl_sync is None:
+                    self.kl_sync = torch.zeros(1, dtype=torch.int32, device=self.dev)
+                L.ppo_forward_kl_stats(self._kl_args, self.sums, gn.float().contiguous(), b, cfg.critic, m,
+                                       self.stats, self.kl_sync, counter=self.counter, rows=self.rows,
+                                       idx_offset=self.idx_off if self._offset else None, idx_step=m)
+                return
             elif nl > 1 and self.mf_ok[-1] and L.mlp_fwd_kl_supported(w_last.shape[0], w_last.shape[1]):
                 # the last block fused with the action head and the KL reduction (no H write / re-read)
                 x = self._layers(1, upto=nl - 1)
@@ -371,9 +498,13 @@ class FusedPPOUpdater(PPOUpdater):
             L.ppo_stats(self.sums, kl_part, gn.float().contiguous(), b, cfg.critic, m, self.stats, self.counter,
                         kl_rows=kl_job.nb, rows=self.rows)
 
+    idx_off = None  # the offset path's device row offset (advanced by the KL pass's last block)
+
     def _extra_snapshot(self):
-        return self.counter.clone()
+        return (self.counter.clone(), None if self.idx_off is None else self.idx_off.clone())
 
     def _extra_restore(self, snap):
-        self.counter.copy_(snap)
+        self.counter.copy_(snap[0])
+        if snap[1] is not None:
+            self.idx_off.copy_(snap[1])
         self.refresh_weights()  # the capture warm-up stepped (and then restored) the master weights

@@ -288,16 +288,21 @@ class FusedMuonAdamW(MuonAdamW):
         self._run(None)
 
     @torch.no_grad()
-    def step_clipped(self, flat_grad: torch.Tensor, max_norm: float) -> torch.Tensor:
+    def step_clipped(self, flat_grad: torch.Tensor, max_norm: float, sq: torch.Tensor | None = None) -> torch.Tensor:
         """clip_grad_norm_(max_norm) folded into the step (the bucket itself is left unclipped);
-        returns the pre-clip norm as a device scalar."""
+        returns the pre-clip norm as a device scalar.  sq: the gradient's sum-of-squares partials
+        already written (g2048_colsum_batch_sq, which also counted the step) -- then one launch."""
         if self._mats is None:
             self._build()
         # two launches: partial sums of squares (+ the step count), then Muon with the clip folded in
         # and the AdamW blocks of the 1-D groups
-        self._L.grad_sumsq_tick(flat_grad, self.norm_part, self.step_t)
+        if sq is None:
+            self._L.grad_sumsq_tick(flat_grad, self.norm_part, self.step_t)
+            part, self._cfg.npartials = self.norm_part, 0
+        else:
+            part, self._cfg.npartials = sq, sq.numel()
         self._L.muon_adamw_step_clip(self._mats, self._groups if len(self._groups) else None, self.lr, self.step_t,
-                                     self.norm_part, max_norm, self.norm_t, self.coef_t, self._cfg, self.b1, self.b2,
+                                     part, max_norm, self.norm_t, self.coef_t, self._cfg, self.b1, self.b2,
                                      self.eps, self.wd)
         return self.norm_t
 
@@ -323,8 +328,8 @@ class ScheduledMuonAdamW:
     def fused(self) -> bool:
         return getattr(self.opt, "supported", False)
 
-    def step_clipped(self, flat_grad, max_norm):
-        return self.opt.step_clipped(flat_grad, max_norm)
+    def step_clipped(self, flat_grad, max_norm, sq=None):
+        return self.opt.step_clipped(flat_grad, max_norm, sq=sq)
 
     def set_bf16_copies(self, mapping):
         self.opt.set_bf16_copies(mapping)

@@ -133,6 +133,15 @@ typedef struct g2048_colsum_job {
 
 #define G2048_COLSUM_MAX_JOBS 16
 int g2048_colsum_batch(g2048_stream_t stream, const g2048_colsum_job *jobs, int32_t njobs);
+/* g2048_colsum_batch that also prices the gradient norm: bit k of a job's pad_ marks segment k as
+ * gradient; sq[b] = the sum of squares of block b's gradient outputs (b < nsq: the blocks past the
+ * launch's grid are zeroed), *tick += 1 (the optimizer's step count) -- the partials the fused
+ * optimizer step reads instead of a g2048_grad_sumsq_tick pass over the bucket (single process: the
+ * gradient is final when summed).  nsq >= g2048_colsum_batch_blocks(jobs, njobs). */
+#define G2048_COLSUM_SQ_MAX 1024
+int g2048_colsum_batch_blocks(const g2048_colsum_job *jobs, int32_t njobs);
+int g2048_colsum_batch_sq(g2048_stream_t stream, const g2048_colsum_job *jobs, int32_t njobs, float *sq, int32_t nsq,
+                          float *tick);
 
 #define G2048_DY_MAX_P 4
 
@@ -253,6 +262,9 @@ typedef struct g2048_mlp_pass_args {
     void *keep;                    /* train, optional out: the blocks' dropout keep bits, uint64 [2][m][4]
                                     * (block, row, lane group g: bit 4 n + e = feature 16 n + 4 g + e),
                                     * g2048_ppo_backward's `keep` (8-byte aligned; NULL: not stored) */
+    const int64_t *idx_offset;     /* optional device scalar: row r of the minibatch is
+                                    * batch.idx[*idx_offset + r] (a whole epoch's permutation in one
+                                    * buffer; g2048_ppo_forward_kl_stats advances it) */
 } g2048_mlp_pass_args;
 
 /* The head weights [wa (4 rows); wv] (fp32) as the passes' MFMA operand: an exact three-term bf16
@@ -266,6 +278,24 @@ size_t g2048_mlp_pass_partials(int64_t m, int32_t train);
 int g2048_ppo_forward_loss(g2048_stream_t stream, const g2048_mlp_pass_args *args, float *dba, float *dbv, float *sums,
                            g2048_colsum_job *defer);
 int g2048_ppo_forward_kl(g2048_stream_t stream, const g2048_mlp_pass_args *args, float *out, g2048_colsum_job *defer);
+/* The KL re-forward with the minibatch statistics folded in: the pass's last block reduces the KL
+ * partial rows and applies g2048_ppo_stats (same arithmetic) -- one launch instead of two.  sync: a
+ * 4-byte device word, zero before the first call (each call leaves it zero). */
+typedef struct g2048_ppo_stats_args {
+    const float *sums;             /* the train pass's loss sums [3] */
+    const float *grad_norm;        /* the pre-clip gradient norm (device scalar) */
+    const float *beta_dev;
+    const int64_t *rows;           /* nullable: the padded ragged minibatch's device row count */
+    float *stats;                  /* [9] accumulated (g2048_ppo_stats) */
+    uint64_t *counter;             /* nullable: += 1 (the next minibatch's dropout counter) */
+    uint32_t *sync;
+    float critic;
+    int32_t pad_;
+    int64_t m;
+    int64_t *idx_offset;           /* nullable: += idx_step once the pass is done (the next minibatch) */
+    int64_t idx_step;
+} g2048_ppo_stats_args;
+int g2048_ppo_forward_kl_stats(g2048_stream_t stream, const g2048_mlp_pass_args *args, const g2048_ppo_stats_args *st);
 
 /* The MLP's backward after the train pass, in one launch (replaces the per-layer chain of three
  * g2048_ln_act_bwd and two g2048_linear_dgrad): per row tile the top block's LayerNorm / ReLU /
@@ -382,7 +412,9 @@ typedef struct g2048_muon_cfg {
      * iteration through the workspace (g2048_muon_workspace_bytes(), device memory, ZERO-FILLED ONCE
      * by the caller: each launch leaves its counters zero again).  parts <= 1 or workspace NULL: one
      * block per matrix. */
-    int32_t parts, pad_;
+    int32_t parts;
+    int32_t npartials;             /* the clip's sum-of-squares partials: 0 = g2048_grad_sumsq's 64, else
+                                    * this many (g2048_colsum_batch_sq's, <= G2048_COLSUM_SQ_MAX) */
     void *workspace;
 } g2048_muon_cfg;
 

@@ -59,8 +59,9 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.PPOBatch) == 56 and _lib.PPOBatch.rows.offset == 48
     assert ctypes.sizeof(_lib.Dy) == 64 and _lib.Dy.dz.offset == 40 and _lib.DY_MAX_P == 4
     assert ctypes.sizeof(_lib.ColsumJob) == 88 and _lib.ColsumJob.len.offset == 64
-    assert ctypes.sizeof(_lib.MlpPassArgs) == 416 and _lib.MlpPassArgs.drop.offset == 176
-    assert _lib.MlpPassArgs.keep.offset == 408
+    assert ctypes.sizeof(_lib.MlpPassArgs) == 424 and _lib.MlpPassArgs.drop.offset == 176
+    assert _lib.MlpPassArgs.keep.offset == 408 and _lib.MlpPassArgs.idx_offset.offset == 416
+    assert ctypes.sizeof(_lib.PPOStatsArgs) == 88 and _lib.PPOStatsArgs.idx_offset.offset == 72
     assert ctypes.sizeof(_lib.MlpBackArgs) == 312 and _lib.MlpBackArgs.keep.offset == 304
     assert ctypes.sizeof(_lib.MuonCfg) == 48 and _lib.MuonCfg.workspace.offset == 40
     assert ctypes.sizeof(_lib.MuonMatrix) == 56 and _lib.MuonMatrix.head_frag.offset == 32

@@ -697,7 +697,7 @@ def test_fused_graphed_update_equals_eager(dev, fused_opt, bs):
         st = None
         for _ in range(3):
             st = {k: float(v) for k, v in up.update(data, 0.02).items()}
-        assert (up._g is not None) == graph
+        assert up.captured == graph
         out.append((torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy(), st))
     np.testing.assert_array_equal(out[0][0], out[1][0])
     for k in ("loss", "entropy", "grad_norm", "kl_average", "kl_max"):
@@ -849,7 +849,7 @@ def test_fused_split_graph_equals_unsplit(dev):
         up = FusedPPOUpdater(m, opt, PPOConfig(batch_size=3000, critic=0.2), GradBucket(order), gen, graph=True)
         up.force_split = split
         sts = [{k: float(v) for k, v in up.update(data, 0.02).items()} for _ in range(2)]
-        assert (up._g["g2"] is not None) == split
+        assert up.graph_split == split
         def flat(x):
             if torch.is_tensor(x):
                 return [x.detach().cpu()]
@@ -1150,6 +1150,43 @@ def test_one_launch_wgrad_update_matches_split_wgrad(dev):
         assert (a - b).abs().max().item() <= 1e-4 * b.abs().max().item() + 1e-12, (n, (a - b).abs().max())
 
 
+def test_colsum_partials_price_the_gradient_norm(dev):
+    """Single process: the minibatch's one column-sum launch (g2048_colsum_batch_sq) also writes the
+    gradient's sum-of-squares partials and counts the optimizer step, so the fused step skips the
+    g2048_grad_sumsq pass: the partials sum to the bucket's squared norm (fp32 summation order), the
+    step count moves by one per minibatch, and the clipped step's norm matches the bucket's."""
+    import agent
+    from g2048.dist import GradBucket
+    from g2048.fastmlp import FusedPPOUpdater
+    from g2048.optim import FusedMuonAdamW
+    from g2048.ppo import PPOConfig
+    _, _, _, _, data, _, _ = _pass_case(dev, 196, 3 * 4096, 1, 0.1, 97)
+    idx = torch.randperm(3 * 4096, device=dev)[:4096]
+    torch.manual_seed(5)
+    mdl = agent.GameMLP(agent.MLPConfig(hidden_dim=196, dropout=0.1)).to(dev).train()
+    with torch.no_grad():
+        mdl.action_head.weight.normal_(0, 0.05)
+        mdl.value_head.weight.normal_(0, 0.05)
+    opt = FusedMuonAdamW(mdl, 1e-3, 1e-3)
+    order = [p for p, _ in opt.muon] + [p for gr in opt.adam_groups for p in gr["params"]]
+    up = FusedPPOUpdater(mdl, opt, PPOConfig(batch_size=4096), GradBucket(order),
+                         torch.Generator(device=dev).manual_seed(3), graph=False)
+    up._alloc(4096)
+    up.refresh_weights()
+    up.beta_t.fill_(0.02)
+    step0 = float(opt.step_t)
+    up._pre(idx, data, up.beta_t, None)
+    torch.cuda.synchronize()
+    assert up._sq_done
+    assert float(opt.step_t) == step0 + 1
+    want = float(up.grads.flat.double().pow(2).sum())
+    got = float(up.sq_part.double().sum())
+    assert want > 0 and abs(got - want) <= 1e-5 * want, (got, want)
+    gn = opt.step_clipped(up.grads.flat, 1.0, sq=up.sq_part)
+    torch.cuda.synchronize()
+    assert abs(float(gn) - want ** 0.5) <= 1e-5 * want ** 0.5
+
+
 @pytest.mark.parametrize("h,M,m,p", [(196, 5000, 4099, 0.1), (128, 1200, 1000, 0.25), (64, 700, 333, 0.2),
                                      (192, 900, 700, 0.1)])
 def test_backward_reads_the_train_pass_keep_bits(dev, h, M, m, p):
@@ -1230,6 +1267,74 @@ def test_fused_kl_pass_matches_layer_kernels(dev, h, M, m, p, ragged):
     assert float(ref[0]) > 0
     assert math.isclose(float(got[0]), float(ref[0]), rel_tol=1e-4, abs_tol=1e-6), (got, ref)
     assert math.isclose(float(got[1]), float(ref[1]), rel_tol=1e-4, abs_tol=1e-6), (got, ref)
+
+
+@pytest.mark.parametrize("m,ragged", [(65536, False), (4099, True)])
+def test_kl_pass_with_folded_statistics_equals_kl_then_stats(dev, m, ragged):
+    """g2048_ppo_forward_kl_stats (the KL re-forward whose last block reduces the KL partial rows and
+    applies g2048_ppo_stats) gives bitwise the statistics, dropout counter and KL of the two-launch
+    form (g2048_ppo_forward_kl deferred + g2048_ppo_stats), three minibatches in a row (the ticket
+    word is left zero by each launch)."""
+    from g2048 import _lib as L
+    h = 196
+    w, gam, bet, (wa, ba, wv, bv), data, idx, ctr = _pass_case(dev, h, m + 77, m, 0.1, 5 * h + m)
+    rows = torch.tensor([m - 9 if ragged else m], dtype=torch.int64, device=dev)
+    frag = torch.empty(L.head_split_bytes(h), dtype=torch.uint8, device=dev)
+    L.head_split(wa, None, frag)
+    batch = L.make_ppo_batch(idx, data["actions"], data["legal"], data["logp"], data["adv"], data["ret"], rows=rows)
+    old = data["logp"].index_select(0, idx) + 0.3 * torch.randn(m, 4, device=dev)
+    sums = torch.tensor([0.3, -0.2, 0.7], device=dev)
+    gn, beta = torch.tensor(1.7, device=dev), torch.tensor(0.02, device=dev)
+    outs = []
+    for fold in (False, True):
+        stats = torch.zeros(9, device=dev)
+        stats[8] = -float("inf")
+        counter = torch.tensor([11], dtype=torch.int64, device=dev)
+        sync = torch.zeros(1, dtype=torch.int32, device=dev)
+        part = torch.empty(L.mlp_pass_partials(m, False), device=dev)
+        for it in range(3):
+            drops = [L.make_dropout(0.1, l, 1, 55, 0, counter) for l in (1, 2)]
+            args = L.make_mlp_pass(data["boards"], batch, m, w[0], w[1:], gam, bet, frag, ba, drops=drops,
+                                   masked=old, partials=part)
+            if fold:
+                L.ppo_forward_kl_stats(args, sums, gn, beta, 0.2, m, stats, sync, counter=counter, rows=rows)
+            else:
+                job = L.ColsumJob()
+                L.ppo_forward_kl(args, torch.empty(2, device=dev), defer=job)
+                L.ppo_stats(sums, part, gn, beta, 0.2, m, stats, counter, kl_rows=job.nb, rows=rows)
+        torch.cuda.synchronize()
+        outs.append((stats.clone(), counter.clone(), int(sync.item())))
+    assert torch.equal(outs[0][0].view(torch.int32), outs[1][0].view(torch.int32)), (outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert outs[1][2] == 0 and float(outs[1][0][6]) > 0
+
+
+def test_offset_path_multi_step_graph_equals_eager(dev):
+    """FusedPPOUpdater's offset path (the epoch's permutation in one buffer, rows read at a device
+    offset advanced by the KL pass; MULTI minibatch steps per captured graph + one-step graphs for the
+    rest and the padded ragged minibatch) is bitwise the eager per-minibatch update: 9 full
+    minibatches + a ragged one, two epochs, parameters and statistics."""
+    import agent
+    from g2048.dist import GradBucket
+    from g2048.fastmlp import FusedPPOUpdater
+    from g2048.optim import FusedMuonAdamW
+    from g2048.ppo import PPOConfig
+    data = _synthetic_data(dev, 9 * 2048 + 777, seed=8)
+    out = []
+    for graph in (False, True):
+        torch.manual_seed(4)
+        m = agent.GameMLP(agent.MLPConfig(hidden_dim=196, num_layers=2, dropout=0.1)).to(dev)
+        opt = FusedMuonAdamW(m, 1e-3, 1e-4)
+        order = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(9)
+        up = FusedPPOUpdater(m, opt, PPOConfig(batch_size=2048, critic=0.2, epochs=2), GradBucket(order), gen,
+                             graph=graph)
+        sts = [{k: float(v) for k, v in up.update(data, 0.02).items()} for _ in range(2)]
+        assert (up._og is not None) == graph
+        out.append((torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy(), sts))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
 
 
 def test_fused_passes_and_layer_chain_give_the_same_update(dev):

@@ -8,7 +8,7 @@ size 1 BEFORE any other GPU call, the way bench.py / torch.distributed.run ranks
     INSIDE the single minibatch hipGraph -- no split graph, no eager collective between replays --
     and the captured update is bitwise the eager one (parameters and statistics, 3 updates with a
     ragged padded last minibatch);
-  * checks that the all-reduce really was issued during the capture (once per captured copy);
+  * checks that the all-reduce really was issued during the capture (once per captured step);
   * runs two VecTrainer train steps (rollout, RTG, D4 up-sampling, graphed update) on that process
     group.
 RCCL cannot put two ranks on one GPU, so the 2-rank case runs on gloo (tests/test_gpu_dist.py)."""
@@ -70,7 +70,8 @@ def _child():
         before = dict(calls)
         sts = [{k: float(v) for k, v in up.update(data, 0.02).items()} for _ in range(3)]
         if graph:
-            rep["split"] = up._g["g2"] is not None
+            rep["split"] = up.graph_split
+            rep["multi"] = up.MULTI
             rep["captured_allreduces"] = calls["captured"] - before["captured"]
             # replays issue no eager collective: only the capture warm-up's eager steps did
             rep["eager_allreduces_graph_run"] = calls["eager"] - before["eager"]
@@ -85,7 +86,7 @@ def _child():
     tr = VecTrainer(cfg, dev)
     ms = [tr.train_step(s) for s in range(2)]
     rep["trainer_finite"] = all(np.isfinite(x["loss"]) and np.isfinite(x["grad_norm"]) for x in ms)
-    rep["trainer_split"] = tr.ppo._g["g2"] is not None
+    rep["trainer_split"] = tr.ppo.graph_split
     torch.cuda.synchronize()
     dist.destroy_process_group()
     print("RCCL_REPORT " + json.dumps(rep), flush=True)
@@ -104,9 +105,9 @@ def test_rccl_world1_captured_allreduce_graph_equals_eager():
     print(rep)
     assert rep["backend"] == "nccl" and rep["world"] == 1
     assert rep["split"] is False and rep["trainer_split"] is False  # one graph per minibatch
-    # the collective is a node of the minibatch graph: one per captured copy of the step (FusedPPOUpdater
-    # captures two, alternating index buffers, so the index copy overlaps the previous replay)
-    assert rep["captured_allreduces"] == 2
+    # the collective is a node of the captured minibatch steps: one in the one-step graph and one per
+    # step of the MULTI-step graph (FusedPPOUpdater's offset path)
+    assert rep["captured_allreduces"] == 1 + rep["multi"]
     assert rep["eager_allreduces"] == 3 * 3  # eager path: one per minibatch (3 updates x 3 minibatches)
     assert rep["params_equal"] and rep["stats_equal"] and rep["moved"]
     assert rep["trainer_finite"]
