@@ -94,7 +94,13 @@ struct MonoStats {
 
 // first row-major cell whose byte equals M (M present on the board): per-row v_ffbl (~0 for a row
 // without M, which never wins the unsigned min), row i offset by OR-ing 32*i into the bit index
-__device__ __forceinline__ uint32_t ffbl(uint32_t x) { return (uint32_t)__builtin_ctzg(x, -1); }
+// v_ffbl_b32 itself returns ~0 for a zero input; the generic count-trailing-zeros adds a compare and a
+// select to guarantee that, so the instruction is written out
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
 __device__ __forceinline__ uint32_t first_cell_eq(const uint32_t (&r)[4], uint32_t M) {
     const uint32_t mb = M * 0x01010101u;
     const uint32_t f0 = ffbl(zm(r[0] ^ mb)), f1 = ffbl(zm(r[1] ^ mb)) | 32u;

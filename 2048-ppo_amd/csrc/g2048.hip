@@ -59,8 +59,8 @@ constexpr uint32_t kRowLds = lut::kLineEntriesPadded * 2u;                   // 
 // then the auto-reset boards and their statistics (kFresh)
 __device__ const lut::FreshTable kFresh __attribute__((aligned(16))) = lut::FreshTable();
 constexpr uint32_t kFreshBoardBase = 137u * 1024u;                          // 15 KiB of boards
-constexpr uint32_t kFreshStatBase = kFreshBoardBase + lut::kFreshEntries * 16u;  // 2 KiB of stats
-constexpr uint32_t kRolloutLdsWords = (kFreshStatBase + 2048u) / 4u;         // 157 696 B
+constexpr uint32_t kFreshStatBase = kFreshBoardBase + lut::kFreshEntries * 16u;  // 4 KiB of stats
+constexpr uint32_t kRolloutLdsWords = (kFreshStatBase + 4096u) / 4u;         // 159 744 B
 static_assert(kRowLds + lut::kRowEntries * 4u <= kFreshBoardBase, "kRow12 below kFresh");
 static_assert(kRowLds + 4u * 28276u <= kRolloutLdsWords * 4u && 2u * 28276u <= kRowLds + lut::kRowEntries * 4u,
               "masked table reads stay inside the allocation");
@@ -113,38 +113,34 @@ __device__ __forceinline__ uint4 perm4(const uint4 &w, uint32_t sel) {
                       __builtin_amdgcn_perm(w.z, w.z, sel), __builtin_amdgcn_perm(w.w, w.w, sel));
 }
 
-// nibble-packed row (bits 0..15 of a table entry) -> row dword with one exponent per byte
-__device__ __forceinline__ uint32_t unpack_row(uint32_t e) {
-    const uint32_t t = __builtin_amdgcn_perm(0u, e, 0x0C010C00u);  // bytes {e.b0, 0, e.b1, 0}
-    return (t & 0x000F000Fu) | ((t & 0x00F000F0u) << 4);
+// nibble-packed row (bits 0..15 of a table entry) -> row dword with one exponent per byte, byte
+// reversed or not by the lane's selector: nibble j is the low nibble of byte j/2 of e (j even) or of
+// e >> 4 (j odd), so one v_perm over (e >> 4, e) places all four and a mask clears the high nibbles.
+constexpr uint32_t kUnpackSel = 0x05010400u;     // bytes {n0, n1, n2, n3}
+constexpr uint32_t kUnpackRevSel = 0x00040105u;  // bytes {n3, n2, n1, n0}
+__device__ __forceinline__ uint32_t unpack_row(uint32_t e, uint32_t sel) {
+    return __builtin_amdgcn_perm(e >> 4, e, sel) & 0x0F0F0F0Fu;
 }
 
-// spawn on the k-th empty cell (row-major) of a board whose rows have empty masks Z (cnt empties),
-// from ONE uniform word r: k = floor(r * cnt / 2^32), value 1 if the low word of r * cnt is below
-// 0.9 * 2^32 (given k that low word is uniform to within cnt / 2^32).
-__device__ __forceinline__ uint32_t spawn_chain(uint4 &b, const uint32_t (&Z)[4], uint32_t cnt, uint32_t r,
-                                                uint32_t &pos) {
-    const uint64_t prod = (uint64_t)r * cnt;
-    uint32_t k = (uint32_t)(prod >> 32);
-    const uint32_t v = (uint32_t)prod < kTwoThreshold ? 1u : 2u;
-    const uint32_t c0 = __popc(Z[0]), c1 = __popc(Z[1]), c2 = __popc(Z[2]);
-    const bool g0 = k >= c0;
-    k -= g0 ? c0 : 0u;
-    const bool g1 = g0 && k >= c1;
-    k -= g1 ? c1 : 0u;
-    const bool g2 = g1 && k >= c2;
-    k -= g2 ? c2 : 0u;
-    const uint32_t row = (uint32_t)g0 + (uint32_t)g1 + (uint32_t)g2;
-    const uint32_t z = g2 ? Z[3] : g1 ? Z[2] : g0 ? Z[1] : Z[0];
-    const uint32_t b0 = (z >> 7) & 1u, b1 = (z >> 15) & 1u, b2 = (z >> 23) & 1u;
-    const uint32_t col = (uint32_t)(k >= b0) + (uint32_t)(k >= b0 + b1) + (uint32_t)(k >= b0 + b1 + b2);
-    pos = 4u * row + col;
-    const uint32_t bits = v << (8u * col);
-    b.x |= row == 0u ? bits : 0u;
-    b.y |= row == 1u ? bits : 0u;
-    b.z |= row == 2u ? bits : 0u;
-    b.w |= row == 3u ? bits : 0u;
-    return v;
+// Packed monotonicity statistics of the rollout kernel, one VGPR per board: bits 0..3 pos (the
+// first row-major cell holding the maximum), 8..11 L, 12..15 R, 16..19 T, 20..23 B (board.hpp
+// MonoStats), 24..27 M.  Bytes 1 and 2 are the low bytes of a board's kLine12 row / column sums.
+__device__ __forceinline__ uint32_t pack_stats(const MonoStats &s) {
+    return s.pos | ((uint32_t)s.L << 8) | ((uint32_t)s.R << 12) | ((uint32_t)s.T << 16) | ((uint32_t)s.B << 20) |
+           (s.M << 24);
+}
+// board.hpp mono_value on the packed word: (L, T) and (R, B) as u16 pairs (L, R scaled by 256),
+// one packed max and one dot product give 256 (max(L, R) + max(T, B)); x2 for a corner maximum
+// (>> 7), floor(/2) otherwise (>> 9).  The bit-field extract reads its offset from bits 0..4 of S.
+__device__ __forceinline__ uint32_t mono_value_packed(uint32_t S) {
+    const u16x2 m = __builtin_elementwise_max(as_u16x2(S & 0x000F0F00u), as_u16x2((S >> 4) & 0x000F0F00u));
+    const uint32_t best256 = __builtin_amdgcn_udot2(m, (u16x2){1, 256}, 0u, false);
+    const uint32_t corner = __builtin_amdgcn_ubfe(0x9009u, S, 1u);
+    return best256 >> (9u - 2u * corner);
+}
+// L|R and T|B bytes of a board's kLine12 row sum SR and column sum SC into bytes 1 and 2
+__device__ __forceinline__ uint32_t stats_bytes(uint32_t SR, uint32_t SC) {
+    return __builtin_amdgcn_perm(SC, SR, 0x0C04000Cu);
 }
 
 // Game2048.reset (game.py:942-950) from the four words of one Philox draw: the two spawns of reset()
@@ -213,10 +209,10 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 __device__ __forceinline__ void stage_row_table(uint32_t *s_row) {
     constexpr int kPieces = (int)(lut::kRowEntries * 4u / 1024u);  // 81 pieces of 1 KiB
     constexpr int kLinePieces = (int)(lut::kLineEntriesPadded * 2u / 1024u);  // + 41 of kLine12
-    constexpr int kFreshPieces = (int)(lut::kFreshEntries * 16u / 1024u);  // + 15 boards + 2 stats
+    constexpr int kFreshPieces = (int)(lut::kFreshEntries * 16u / 1024u);  // + 15 boards + 4 stats
     static_assert(lut::kRowEntries * 4u % 1024u == 0u && lut::kLineEntriesPadded * 2u % 1024u == 0u &&
                   lut::kFreshEntries * 16u % 1024u == 0u, "whole 1 KiB pieces");
-    constexpr int kAll = kPieces + kLinePieces + kFreshPieces + 2;
+    constexpr int kAll = kPieces + kLinePieces + kFreshPieces + 4;
     const char *src = reinterpret_cast<const char *>(kLine12.v);  // pieces 0 .. kLinePieces - 1
     const char *src2 = reinterpret_cast<const char *>(kRow12.v);
     const char *src3 = reinterpret_cast<const char *>(kFresh.b);
@@ -248,15 +244,15 @@ __device__ __forceinline__ void stage_row_table(uint32_t *s_row) {
 struct RolloutLane {
     uint4 b;          // current board (never finished between steps)
     uint32_t legal;   // its legal mask
-    MonoStats sb;     // its monotonicity statistics
+    uint32_t S;       // its packed monotonicity statistics (pack_stats)
     int empt_b;       // its empty-cell count
     uint4 D;          // Philox draw of the current pair of steps: x / y = the two steps' words,
                       // z / w = the words of a reset inside the pair (at most one: a reset board
                       // cannot end again one move later)
     PhiloxState ph;   // draw of the next pair, computed half per step inside the LDS round trip
     uint4 fb;         // the board a reset inside the current pair starts (D.z, D.w -> kFresh) ...
-    uint32_t flegal;  // ... its legal mask and statistics
-    MonoStats fsb;
+    uint32_t flegal;  // ... its legal mask and packed statistics
+    uint32_t fS;
 };
 
 // the current pair's auto-reset board from kFresh (fresh_from_pair's board and fresh_stats' results,
@@ -268,10 +264,9 @@ __device__ __forceinline__ void fresh_prep(RolloutLane &s, const uint32_t *__res
                        (bw * 15u >= kTwoThreshold ? 1u : 0u);
     const char *t = reinterpret_cast<const char *>(tab);
     s.fb = *reinterpret_cast<const uint4 *>(t + kFreshBoardBase + 16u * i);
-    const uint32_t st = *reinterpret_cast<const uint16_t *>(t + kFreshStatBase + 2u * i);
-    s.flegal = st & 15u;
-    s.fsb = MonoStats{(int)((st >> 4) & 1u), (int)((st >> 5) & 1u), (int)((st >> 6) & 1u), (int)((st >> 7) & 1u),
-                      1u + ((st >> 8) & 1u), st >> 12};
+    const uint32_t st = *reinterpret_cast<const uint32_t *>(t + kFreshStatBase + 4u * i);
+    s.flegal = st >> 28;
+    s.fS = st & 0x0FFFFFFFu;
 }
 
 struct TrajRows {  // this lane's element of row t of each time-major trajectory array (advanced by n per step)
@@ -292,7 +287,7 @@ struct TrajRows {  // this lane's element of row t of each time-major trajectory
 
 // One env step of the synthetic random-legal policy (oracle or_step_word + auto-reset).  kOdd = the
 // second step of the pair.  One 32-bit word u per step: action k = floor(u * nlegal / 2^32); the
-// low word r of that product (uniform given k) picks the spawn cell and value (spawn_chain).
+// low word r of that product (uniform given k) picks the spawn cell and value.
 template <bool kOdd, bool kSmall = false>
 __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__restrict__ tab, const TrajRows &tr,
                                              uint64_t seed, uint64_t next_pair, uint32_t env) {
@@ -303,8 +298,8 @@ __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__r
     // the move through the LDS row table in the LEFT frame.  Half of the next pair's Philox rounds
     // fill the LDS round trip: the empty asm statements start them after the table loads are issued
     // (memory clobber) and consume the loaded entries after them.
-    const bool vert = a < 2u;
-    const uint32_t rsel = (a & 1u) ? 0x00010203u : 0x03020100u;  // DOWN / RIGHT: byte-reversed rows
+    const bool vert = a < 2u, rev = (a & 1u) != 0u;  // DOWN / RIGHT: byte-reversed rows
+    const uint32_t rsel = rev ? 0x00010203u : 0x03020100u, usel = rev ? kUnpackRevSel : kUnpackSel;
     uint4 w = perm4(sel4(vert, transpose(s.b), s.b), rsel);
     uint32_t e0 = lds_word(tab, row12_addr(w.x)), e1 = lds_word(tab, row12_addr(w.y));
     uint32_t e2 = lds_word(tab, row12_addr(w.z)), e3 = lds_word(tab, row12_addr(w.w));
@@ -312,72 +307,86 @@ __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__r
     if constexpr (kOdd) philox_rounds<5, 10>(s.ph);
     else philox_rounds<0, 5>(s.ph);
     asm volatile("" : "+v"(s.ph.c0), "+v"(s.ph.c1), "+v"(s.ph.c2), "+v"(s.ph.c3), "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3));
-    const int mono_b = mono_value(s.sb);
-    w = perm4(make_uint4(unpack_row(e0), unpack_row(e1), unpack_row(e2), unpack_row(e3)), rsel);
+    const uint32_t mono_b = mono_value_packed(s.S);
+    w = make_uint4(unpack_row(e0, usel), unpack_row(e1, usel), unpack_row(e2, usel), unpack_row(e3, usel));
     uint4 moved = sel4(vert, transpose(w), w);
-    // merge points / 4 of the four rows in the high halves, summed as packed u16
-    const uint32_t q = __builtin_bit_cast(uint32_t, (as_u16x2(e0) + as_u16x2(e1)) + (as_u16x2(e2) + as_u16x2(e3)));
-    uint32_t pts = (q >> 16) << 2;
-    if (!kSmall && s.sb.M > 11u) {  // an exponent outside the table: the SWAR compute path
+    // merge points / 4 in bits 16..27 of each entry, the slid row's maximum in bits 28..31
+    uint32_t pts = (((e0 >> 16) & 0xFFFu) + ((e1 >> 16) & 0xFFFu) + ((e2 >> 16) & 0xFFFu) + ((e3 >> 16) & 0xFFFu)) << 2;
+    uint32_t Ma = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_elementwise_max(as_u16x2(e0), as_u16x2(e1)),
+                                                                         __builtin_elementwise_max(as_u16x2(e2), as_u16x2(e3)))) >> 28;
+    if (!kSmall && (s.S >> 24) > 11u) {  // an exponent outside the table: the SWAR compute path
         uint32_t mx;
         moved = apply_move(s.b, a, pts, mx);
+        Ma = board_max(moved);
     }
     const uint32_t rm[4] = {moved.x, moved.y, moved.z, moved.w};
     const uint32_t Zm[4] = {zm(moved.x), zm(moved.y), zm(moved.z), zm(moved.w)};
-    const uint32_t Ma = board_max(moved);
     const uint32_t pos_a = first_cell_eq(rm, Ma);
-    const int empt_a = __popc(Zm[0]) + __popc(Zm[1]) + __popc(Zm[2]) + __popc(Zm[3]);
-    uint32_t sp;
-    const uint32_t v = spawn_chain(moved, Zm, (uint32_t)empt_a, r, sp);
-    s.b = moved;  // the next board (after the spawn)
-    // its legal mask and pair counts from kLine12: four rows and four columns
+    // the moved board's (pre-spawn) lines in kLine12: four rows and four columns, read before the
+    // spawn is known; the spawn then changes one row and one column, read again below
     uint32_t ra[4], ca[4];
     line12_addrs(moved, ra, ca);
-    uint32_t f0 = lds_half(tab, ra[0]), f1 = lds_half(tab, ra[1]), f2 = lds_half(tab, ra[2]), f3 = lds_half(tab, ra[3]);
-    uint32_t g0 = lds_half(tab, ca[0]), g1 = lds_half(tab, ca[1]), g2 = lds_half(tab, ca[2]), g3 = lds_half(tab, ca[3]);
-    // the spawned tile's pairs (the counts before the spawn are the next board's minus these) and
-    // the next board's maximum / first-argmax cell
-    const MonoStats dsp = mono_add_tile(MonoStats{0, 0, 0, 0, Ma, pos_a}, moved, sp, v);
+    const uint32_t f0 = lds_half(tab, ra[0]), f1 = lds_half(tab, ra[1]), f2 = lds_half(tab, ra[2]), f3 = lds_half(tab, ra[3]);
+    const uint32_t g0 = lds_half(tab, ca[0]), g1 = lds_half(tab, ca[1]), g2 = lds_half(tab, ca[2]), g3 = lds_half(tab, ca[3]);
+    // spawn on the k-th empty cell (row-major), k = floor(r * empties / 2^32), value 1 if the low
+    // word of r * empties is below 0.9 * 2^32 (given k that low word is uniform to within
+    // empties / 2^32); the row from the prefix counts of empties, the column inside the row likewise
+    const uint32_t n0 = __popc(Zm[0]), n01 = __popc(Zm[1]) + n0, n012 = __popc(Zm[2]) + n01;
+    const uint32_t empt_a = __popc(Zm[3]) + n012;
+    const uint64_t prod = (uint64_t)r * empt_a;
+    const uint32_t k = (uint32_t)(prod >> 32);
+    const uint32_t v = (uint32_t)prod < kTwoThreshold ? 1u : 2u;
+    const bool r1 = k >= n0, r2 = k >= n01, r3 = k >= n012;  // spawn row >= 1, >= 2, == 3
+    const uint32_t kr = k - (r3 ? n012 : r2 ? n01 : r1 ? n0 : 0u);
+    const uint32_t z = r3 ? Zm[3] : r2 ? Zm[2] : r1 ? Zm[1] : Zm[0];
+    const uint32_t b0 = (z >> 7) & 1u, b01 = b0 + ((z >> 15) & 1u), b012 = b01 + ((z >> 23) & 1u);
+    const bool c1 = kr >= b0, c2 = kr >= b01, c3 = kr >= b012;  // spawn column >= 1, >= 2, == 3
+    const uint32_t row = (uint32_t)r1 + (uint32_t)r2 + (uint32_t)r3, col = (uint32_t)c1 + (uint32_t)c2 + (uint32_t)c3;
+    const uint32_t sp = 4u * row + col;
+    const uint4 pre = moved;
+    const uint32_t bits = v << (8u * col);
+    moved.x |= r1 ? 0u : bits;
+    moved.y |= (r1 && !r2) ? bits : 0u;
+    moved.z |= (r2 && !r3) ? bits : 0u;
+    moved.w |= r3 ? bits : 0u;
+    s.b = moved;  // the next board (after the spawn)
+    // the spawn's row and column in the next board: kLine12 byte address + v * 2 * 12^(column / row)
+    constexpr uint64_t kW12 = 0x0D80012000180002ull;  // {2, 24, 288, 3456}
+    const uint32_t rq = (r3 ? ra[3] : r2 ? ra[2] : r1 ? ra[1] : ra[0]) + v * ((uint32_t)(kW12 >> (16u * col)) & 0xFFFFu);
+    const uint32_t cq = (c3 ? ca[3] : c2 ? ca[2] : c1 ? ca[1] : ca[0]) + v * ((uint32_t)(kW12 >> (16u * row)) & 0xFFFFu);
+    const uint32_t fq = lds_half(tab, rq), gq = lds_half(tab, cq);
     *tr.a = (uint8_t)a;
     *tr.p = (int32_t)pts;
-    const uint32_t SR = f0 + f1 + f2 + f3, SC = g0 + g1 + g2 + g3;
+    // line sums of the pre-spawn board; the next board's swap the spawn's row and column entries
+    const uint32_t SRp = f0 + f1 + f2 + f3, SCp = g0 + g1 + g2 + g3;
+    const uint32_t SR = SRp - (r3 ? f3 : r2 ? f2 : r1 ? f1 : f0) + fq;
+    const uint32_t SC = SCp - (c3 ? g3 : c2 ? g2 : c1 ? g1 : g0) + gq;
     // #lines that can move per direction in nibbles {UP, DOWN, LEFT, RIGHT} -> legal bits 0..3: a
     // nibble n in 0..4 gets bit 3 set by n + 7; the 24-bit product gathers bits 3, 7, 11, 15 at 12..15
     const uint32_t nl = __builtin_amdgcn_perm(SR, SC, 0x0C0C0501u);
     s.legal = (__umul24((nl + 0x7777u) & 0x8888u, 0x249u) >> 12) & 15u;
-    s.sb.L = (int)(SR & 15u);
-    s.sb.R = (int)((SR >> 4) & 15u);
-    s.sb.T = (int)(SC & 15u);
-    s.sb.B = (int)((SC >> 4) & 15u);
-    s.sb.M = dsp.M;
-    s.sb.pos = dsp.pos;
-    MonoStats sa{s.sb.L - dsp.L, s.sb.R - dsp.R, s.sb.T - dsp.T, s.sb.B - dsp.B, Ma, pos_a};
+    // statistics before the spawn (the record's mono_a) and after it (carried to the next step): the
+    // spawned tile changes the maximum / its first cell only when it reaches the maximum
+    uint32_t sa = stats_bytes(SRp, SCp) | pos_a;
+    const uint32_t pos2 = v > Ma ? sp : v == Ma ? min(pos_a, sp) : pos_a;
+    uint32_t S = stats_bytes(SR, SC) | pos2 | (max(Ma, v) << 24);
     if (!kSmall && Ma > 11u) {  // an exponent outside kLine12: the SWAR statistics and legal mask
-        const uint32_t keep = ~(0xFFu << (8u * (sp & 3u)));
-        const uint32_t q = sp >> 2;
-        const uint4 pre = make_uint4(q == 0u ? moved.x & keep : moved.x, q == 1u ? moved.y & keep : moved.y,
-                                     q == 2u ? moved.z & keep : moved.z, q == 3u ? moved.w & keep : moved.w);
-        sa = mono_stats(pre);
-        s.sb = mono_add_tile(sa, pre, sp, v);
+        const MonoStats ms = mono_stats(pre);
+        sa = pack_stats(ms);
+        S = pack_stats(mono_add_tile(ms, pre, sp, v));
         s.legal = legal_mask(moved);
     }
-    const int mono_a = mono_value(sa);
+    const uint32_t mono_a = mono_value_packed(sa);
     // game over: a new game from the pair's spare words (kFresh, prepared with the draw); selects,
     // so the whole pair stays one basic block
     const bool over = s.legal == 0u;
     const uint32_t fl = over ? FLAG_DONE | FLAG_RESET | s.flegal : s.legal;
     s.b = sel4(over, s.fb, s.b);
     s.legal = over ? s.flegal : s.legal;
-    s.sb.L = over ? s.fsb.L : s.sb.L;
-    s.sb.R = over ? s.fsb.R : s.sb.R;
-    s.sb.T = over ? s.fsb.T : s.sb.T;
-    s.sb.B = over ? s.fsb.B : s.sb.B;
-    s.sb.M = over ? s.fsb.M : s.sb.M;
-    s.sb.pos = over ? s.fsb.pos : s.sb.pos;
-    *tr.pot = (uint32_t)(mono_b & 0xFF) | ((uint32_t)(mono_a & 0xFF) << 8) | ((uint32_t)(s.empt_b & 0xFF) << 16) |
-                 ((uint32_t)(empt_a & 0xFF) << 24);
+    s.S = over ? s.fS : S;
+    *tr.pot = mono_b | (mono_a << 8) | ((uint32_t)s.empt_b << 16) | (empt_a << 24);
     *tr.f = (uint8_t)fl;
-    s.empt_b = (fl & FLAG_RESET) ? 14 : empt_a - 1;
+    s.empt_b = over ? 14 : (int)empt_a - 1;
     if constexpr (kOdd) {
         s.D = make_uint4(s.ph.c0, s.ph.c1, s.ph.c2, s.ph.c3);
         s.ph = philox_start(seed, next_pair, env, 1u);
@@ -412,9 +421,11 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
         if (s.legal == 0u) {  // a finished board handed in: start a new game first (counter ctr0 + steps)
             uint32_t p1, v1, p2, v2;
             s.b = fresh_from_words(philox_draw(rng.seed, ctr0 + (uint64_t)steps, env, 2u), p1, v1, p2, v2);
-            s.legal = fresh_stats(p1, v1, p2, v2, s.sb);
+            MonoStats ms;
+            s.legal = fresh_stats(p1, v1, p2, v2, ms);
+            s.S = pack_stats(ms);
         } else {
-            s.sb = mono_stats(s.b);
+            s.S = pack_stats(mono_stats(s.b));
         }
         s.empt_b = emptiness(s.b);
         uint64_t pair = ctr0 >> 1;
@@ -435,7 +446,7 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
         for (; t + 2 <= steps; t += 2, pair++) {
             // every board of the wave <= 2^9 at the pair's start: both steps stay inside the tables
             // (the move adds at most 1 to the maximum), so the pair runs without the fallback branches
-            if (__all(s.sb.M <= 9u)) {
+            if (__all(s.S < (10u << 24))) {
                 rollout_step<false, true>(s, s_row, tr, rng.seed, pair + 2u, env);
                 tr.next(n);
                 rollout_step<true, true>(s, s_row, tr, rng.seed, pair + 2u, env);
