@@ -352,15 +352,16 @@ __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__r
     s.b = moved;  // the next board (after the spawn)
     // the spawn's row and column in the next board: kLine12 byte address + v * 2 * 12^(column / row)
     constexpr uint64_t kW12 = 0x0D80012000180002ull;  // {2, 24, 288, 3456}
-    const uint32_t rq = (r3 ? ra[3] : r2 ? ra[2] : r1 ? ra[1] : ra[0]) + v * ((uint32_t)(kW12 >> (16u * col)) & 0xFFFFu);
-    const uint32_t cq = (c3 ? ca[3] : c2 ? ca[2] : c1 ? ca[1] : ca[0]) + v * ((uint32_t)(kW12 >> (16u * row)) & 0xFFFFu);
-    const uint32_t fq = lds_half(tab, rq), gq = lds_half(tab, cq);
+    const uint32_t rp = r3 ? ra[3] : r2 ? ra[2] : r1 ? ra[1] : ra[0], cp = c3 ? ca[3] : c2 ? ca[2] : c1 ? ca[1] : ca[0];
+    const uint32_t rq = rp + v * ((uint32_t)(kW12 >> (16u * col)) & 0xFFFFu);
+    const uint32_t cq = cp + v * ((uint32_t)(kW12 >> (16u * row)) & 0xFFFFu);
+    // the spawn row / column entries before (read again: cheaper than selecting among f0..g3) and after
+    const uint32_t fp = lds_half(tab, rp), gp = lds_half(tab, cp), fq = lds_half(tab, rq), gq = lds_half(tab, cq);
     *tr.a = (uint8_t)a;
     *tr.p = (int32_t)pts;
     // line sums of the pre-spawn board; the next board's swap the spawn's row and column entries
     const uint32_t SRp = f0 + f1 + f2 + f3, SCp = g0 + g1 + g2 + g3;
-    const uint32_t SR = SRp - (r3 ? f3 : r2 ? f2 : r1 ? f1 : f0) + fq;
-    const uint32_t SC = SCp - (c3 ? g3 : c2 ? g2 : c1 ? g1 : g0) + gq;
+    const uint32_t SR = SRp - fp + fq, SC = SCp - gp + gq;
     // #lines that can move per direction in nibbles {UP, DOWN, LEFT, RIGHT} -> legal bits 0..3: a
     // nibble n in 0..4 gets bit 3 set by n + 7; the 24-bit product gathers bits 3, 7, 11, 15 at 12..15
     const uint32_t nl = __builtin_amdgcn_perm(SR, SC, 0x0C0C0501u);

@@ -32,9 +32,12 @@ constexpr int kThreads = 256;
 constexpr int kMaxPerLane = 8;  // h <= 512 over 64 lanes
 
 __device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
-__device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even (finite inputs)
-    const uint32_t u = __float_as_uint(f);
-    return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+// round to nearest even on the hardware converter (v_cvt_pk_bf16_f32: one instruction per pair)
+typedef __bf16 bf16x2_hw __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+__device__ __forceinline__ uint32_t pk2bf(float a, float b) {
+    const bf16x2_hw v = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
 }
 // x * sigmoid(x) with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE division
 // sequence: exp overflow for x << 0 gives rcp(inf) = 0, i.e. -0
@@ -196,8 +199,8 @@ __global__ __launch_bounds__(kThreads) void urm_attn_kernel(const uint16_t *__re
         const int dd = d0 + 4 * g;
         if (kAligned) {
             if (dd < hd)
-                *reinterpret_cast<uint2 *>(orow + dd) = make_uint2((uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16),
-                                                                   (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16));
+                *reinterpret_cast<uint2 *>(orow + dd) = make_uint2(pk2bf(o[0], o[1]),
+                                                                   pk2bf(o[2], o[3]));
         } else {
 #pragma unroll
             for (int r = 0; r < 4; r++)
@@ -265,8 +268,8 @@ __global__ __launch_bounds__(kThreads) void urm_residual_rms_vec_kernel(float *_
         out = make_float4(out.x + e.x, out.y + e.y, out.z + e.z, out.w + e.w);
     }
     *reinterpret_cast<float4 *>(x + o) = out;
-    *reinterpret_cast<uint2 *>(xb + o) = make_uint2((uint32_t)f2bf(out.x) | ((uint32_t)f2bf(out.y) << 16),
-                                                    (uint32_t)f2bf(out.z) | ((uint32_t)f2bf(out.w) << 16));
+    *reinterpret_cast<uint2 *>(xb + o) = make_uint2(pk2bf(out.x, out.y),
+                                                    pk2bf(out.z, out.w));
 }
 
 // two channels per thread (inter % 8 == 0): 4-byte bf16 pairs
@@ -289,7 +292,7 @@ __global__ __launch_bounds__(kThreads) void urm_swiglu_conv2_kernel(const uint16
         const float a0 = silu(bf2f(g2 & 0xFFFFu)) * bf2f(u2 & 0xFFFFu);
         const float a1 = silu(bf2f(g2 >> 16)) * bf2f(u2 >> 16);
         const float c0 = fmaf(wc.y, a0, fmaf(wc.x, p0, b0)), c1 = fmaf(wc.w, a1, fmaf(wc.z, p1, b1));
-        *reinterpret_cast<uint32_t *>(out + row * inter + c) = (uint32_t)f2bf(silu(c0)) | ((uint32_t)f2bf(silu(c1)) << 16);
+        *reinterpret_cast<uint32_t *>(out + row * inter + c) = pk2bf(silu(c0), silu(c1));
         p0 = a0;
         p1 = a1;
     }
@@ -452,8 +455,8 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
                 const int c = 16 * ct + 4 * g;
                 if (c < N)
                     *reinterpret_cast<uint2 *>(tile + t * tp + 2 * c) =
-                        make_uint2((uint32_t)f2bf(acc[ct][0]) | ((uint32_t)f2bf(acc[ct][1]) << 16),
-                                   (uint32_t)f2bf(acc[ct][2]) | ((uint32_t)f2bf(acc[ct][3]) << 16));
+                        make_uint2(pk2bf(acc[ct][0], acc[ct][1]),
+                                   pk2bf(acc[ct][2], acc[ct][3]));
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
@@ -494,8 +497,8 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
                     }
                     *reinterpret_cast<float4 *>(x + r * N + c) = o;
                     *reinterpret_cast<uint2 *>(xb + r * N + c) =
-                        make_uint2((uint32_t)f2bf(o.x) | ((uint32_t)f2bf(o.y) << 16),
-                                   (uint32_t)f2bf(o.z) | ((uint32_t)f2bf(o.w) << 16));
+                        make_uint2(pk2bf(o.x, o.y),
+                                   pk2bf(o.z, o.w));
                 }
             }
         } else if constexpr (EPI == EPI_SWIGLU_T) {
@@ -574,8 +577,8 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
                 }
                 if (c < inter)
                     *reinterpret_cast<uint2 *>(y + r * inter + c) =
-                        make_uint2((uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16),
-                                   (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16));
+                        make_uint2(pk2bf(o[0], o[1]),
+                                   pk2bf(o[2], o[3]));
             }
         }
     }
@@ -729,8 +732,8 @@ __device__ __forceinline__ void tile_put(char *tile, const f32x4 (&v)[CT], int t
 #pragma unroll
     for (int ct = 0; ct < CT; ct++)
         *reinterpret_cast<uint2 *>(tile + (t * mk::TP + col0 + 16 * ct + 4 * g) * 2) =
-            make_uint2((uint32_t)f2bf(v[ct][0]) | ((uint32_t)f2bf(v[ct][1]) << 16),
-                       (uint32_t)f2bf(v[ct][2]) | ((uint32_t)f2bf(v[ct][3]) << 16));
+            make_uint2(pk2bf(v[ct][0], v[ct][1]),
+                       pk2bf(v[ct][2], v[ct][3]));
 }
 
 // acc[CT] = W X^T for the board in `tile` (B fragments [t][32 s + 8 g]); W rows at `w` with pitch
@@ -971,17 +974,16 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
                         int64_t b = bt * per_batch + wave * mk::NB + nb;
                         b = b < n ? b : n - 1;
                         attn_keep_c(W.drop, drop_c0 + (uint64_t)app, b, hh, t, g, km);
-#pragma unroll
-                        for (int r = 0; r < 4; r++) pb[r] = (short)f2bf(p[r] * inv * km[r]);
+                        pb = __builtin_bit_cast(s16x4, make_uint2(pk2bf(p[0] * inv * km[0], p[1] * inv * km[1]),
+                                                                  pk2bf(p[2] * inv * km[2], p[3] * inv * km[3])));
                     } else {
-#pragma unroll
-                        for (int r = 0; r < 4; r++) pb[r] = (short)f2bf(p[r] * inv);
+                        pb = __builtin_bit_cast(s16x4, make_uint2(pk2bf(p[0] * inv, p[1] * inv), pk2bf(p[2] * inv, p[3] * inv)));
                     }
                     const f32x4 o = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, pb, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
                     wave_lds_sync();  // every lane's Q / K / V reads of this head are done
                     *reinterpret_cast<uint2 *>(tile + (t * mk::TP + 16 * hh + 4 * g) * 2) =
-                        make_uint2((uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16),
-                                   (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16));
+                        make_uint2(pk2bf(o[0], o[1]),
+                                   pk2bf(o[2], o[3]));
                 }
                 wave_lds_sync();
                 {   // o_proj + residual + RMSNorm
@@ -1331,7 +1333,7 @@ __global__ __launch_bounds__(256) void urm_swiglu_conv_fwd2_kernel(const uint16_
             const float y0 = bfr(bfr(g0 * sigm(g0)) * u0), y1 = bfr(bfr(g1 * sigm(g1)) * u1);
             const float z0 = yp0 * w00 + y0 * w01 + b0, z1 = yp1 * w10 + y1 * w11 + b1;
             *reinterpret_cast<uint32_t *>(act + (16 * bd + t) * inter + c) =
-                (uint32_t)f2bf16(z0 * sigm(z0)) | ((uint32_t)f2bf16(z1 * sigm(z1)) << 16);
+                pk2bf(z0 * sigm(z0), z1 * sigm(z1));
             yp0 = y0;
             yp1 = y1;
         }
@@ -1679,7 +1681,7 @@ __global__ __launch_bounds__(256) void urm_add_cast_kernel(const float4 *__restr
         const float4 x = a[a4 ? i % a4 : i], y = e[i];
         const float4 o = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
         out[i] = o;
-        outb[i] = make_uint2((uint32_t)f2bf(o.x) | ((uint32_t)f2bf(o.y) << 16), (uint32_t)f2bf(o.z) | ((uint32_t)f2bf(o.w) << 16));
+        outb[i] = make_uint2(pk2bf(o.x, o.y), pk2bf(o.z, o.w));
     }
 }
 
