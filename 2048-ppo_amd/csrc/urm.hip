@@ -22,6 +22,7 @@
 
 #include "../../include/g2048_urm.h"
 #include "board.hpp"
+#include "wgrad_ring.hpp"
 
 namespace {
 
@@ -46,6 +47,29 @@ __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
+}
+
+// butterfly steps across the 16-lane rows on the VALU lane swaps (v_permlane16/32_swap) instead of
+// ds_bpermute round trips through LDS: x op x[lane ^ 16], x op x[lane ^ 32]
+__device__ __forceinline__ float xsum16(float x) {
+    const uint32_t u = __float_as_uint(x);
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xsum32(float x) {
+    const uint32_t u = __float_as_uint(x);
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xmax16(float x) {
+    const uint32_t u = __float_as_uint(x);
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xmax32(float x) {
+    const uint32_t u = __float_as_uint(x);
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
 inline int launch_status() {
@@ -168,16 +192,14 @@ __global__ __launch_bounds__(kThreads) void urm_attn_kernel(const uint16_t *__re
         p[r] = st[r] * scale;
         m = fmaxf(m, p[r]);
     }
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    m = xmax32(xmax16(m));
     float sum = 0.0f;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         p[r] = __expf(p[r] - m);
         sum += p[r];
     }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
+    sum = xsum32(xsum16(sum));
     const float inv = 1.0f / sum;
     float km[4] = {1.0f, 1.0f, 1.0f, 1.0f};
     if (kDrop) attn_keep(drop, b, hh, i, g, km);
@@ -187,6 +209,19 @@ __global__ __launch_bounds__(kThreads) void urm_attn_kernel(const uint16_t *__re
     // A operand: V^T[row = dim d0 + i][k = key 4g + jj] = V[4g + jj][d0 + i]
     const uint16_t *vcol = base + 2 * h + hh * hd;
     uint16_t *orow = out + (b * 16 + i) * (int64_t)h + hh * hd;
+    if (kAligned && hd == 16) {
+        // V^T from V's row fragments (lane (i, g): V[i][4g..4g+3], one 8-byte load) by one MFMA
+        // against the identity (exact) instead of four strided 2-byte loads per lane
+        s16x4 eye;
+#pragma unroll
+        for (int r = 0; r < 4; r++) eye[r] = (short)(4 * g + r == i ? 0x3F80 : 0);
+        const s16x4 vrow = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint2 *>(vcol + (int64_t)i * (3 * h) + 4 * g));
+        const f32x4 vt = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vrow, eye, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+        const s16x4 va = __builtin_bit_cast(s16x4, make_uint2(pk2bf(vt[0], vt[1]), pk2bf(vt[2], vt[3])));
+        const f32x4 o = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, pb, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+        *reinterpret_cast<uint2 *>(orow + 4 * g) = make_uint2(pk2bf(o[0], o[1]), pk2bf(o[2], o[3]));
+        return;
+    }
     for (int d0 = 0; d0 < hd; d0 += 16) {
         s16x4 va;
         const int d = d0 + i;
@@ -504,7 +539,7 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
         } else if constexpr (EPI == EPI_SWIGLU_T) {
             constexpr int CH = CT / 2;
             static_assert(CH % 2 == 0, "column tiles are stored in pairs");
-            auto sg = [](float v) { return 1.0f / (1.0f + expf(-v)); };
+            auto sg = [](float v) { return __builtin_amdgcn_rcpf(1.0f + __expf(-v)); };  // = sigm below
             auto rb = [](float v) { return (float)(__bf16)v; };
             auto pk = [](float a0, float a1, float a2, float a3) {
                 const __attribute__((ext_vector_type(2))) __bf16 p0 = {(__bf16)a0, (__bf16)a1}, p1 = {(__bf16)a2, (__bf16)a3};
@@ -694,29 +729,6 @@ struct UrmW {  // device pointers (see g2048_urm_weights)
     float eps;
     AttnDrop drop;  // thr == 0: no attention dropout; else block application `app` uses counter *counter + app
 };
-
-// butterfly steps across the 16-lane rows on the VALU lane swaps (v_permlane16/32_swap) instead of
-// ds_bpermute round trips through LDS: x op x[lane ^ 16], x op x[lane ^ 32]
-__device__ __forceinline__ float xsum16(float x) {
-    const uint32_t u = __float_as_uint(x);
-    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float xsum32(float x) {
-    const uint32_t u = __float_as_uint(x);
-    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float xmax16(float x) {
-    const uint32_t u = __float_as_uint(x);
-    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
-    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-__device__ __forceinline__ float xmax32(float x) {
-    const uint32_t u = __float_as_uint(x);
-    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
 
 __device__ __forceinline__ void wave_lds_sync() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1068,124 +1080,86 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
     }
 }
 // Backward of the attention core for head_dim 16 (the default GameURM: h 64, 4 heads), one wave
-// per (board, head), for training through autograd (agent.GameURMAttention): q, k, v of the 16
-// tokens and dO staged in LDS as fp32, P recomputed (S = Q K^T / 4, row softmax), then
-//   dV = P^T dO,  dP = dO V^T,  dS = P (dP - rowsum(P dP)),  dQ = dS K / 4,  dK = dS^T Q / 4
-// in fp32 (lane t owns row t / 4, columns 4 (t % 4) .. + 3 of each 16 x 16 product; row sums over
-// the 4 lanes of a row by two xor shuffles).  dqkv bf16 [16 n, 3 h] in the qkv layout.
-constexpr int kAbP = 17;  // fp32 LDS row pitch (conflict-free column reads)
-
+// per (board, head), for training through autograd (agent.GameURMAttention), on
+// v_mfma_f32_16x16x16_bf16 (round 4; the fp32 VALU version read its operands ~400 times per lane
+// from LDS and was LDS-bound at ~400 us per call).  Lane (t, g) = (l & 15, l >> 4) loads the 4
+// features 4g..4g+3 of head hd of token t of q, k, v and dO -- the A layout of a 16 x 16 operand with
+// the token as its row, and the B layout of its transpose.  Then
+//   S^T  = K Q^T              lane (i, g) holds S[i][4g + r]: the forward's product, bit for bit,
+//                             and its softmax code, so P is the forward's P
+//   dP^T = V dO^T             same layout: dP[i][4g + r]  (dP = dO V^T of the dropped P)
+//   dS   = P (km dP - rowsum(P km dP))          elementwise + two cross-lane steps
+//   dQ^T = K^T dS^T,  dK^T = Q^T dS,  dV^T = dO^T (P km)   each leaves lane (t, g) the features
+//                             4g..4g+3 of token t's gradient (one 8-byte store per output)
+// The transposed operands (K^T, Q^T, dO^T as A; dS, P km as B with the query as K index) are ONE
+// MFMA each against the identity (exact: bf16 values times 1 accumulated in fp32).  P and dS enter
+// their products as bf16 (torch's bf16 autocast backward of the same attention does the same).
 template <bool kDrop>
 __global__ __launch_bounds__(256) void urm_attn_bwd16_kernel(const uint16_t *__restrict__ qkv,
                                                              const uint16_t *__restrict__ dout,
                                                              uint16_t *__restrict__ dqkv, int64_t tasks, int h,
                                                              int heads, AttnDrop drop) {
-    __shared__ float sm[4][6][16 * kAbP];  // per wave: Q, K, V, dO, P, dS
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t task = (int64_t)blockIdx.x * 4 + wave;
     if (task >= tasks) return;  // wave-uniform; no block barrier below
     const int64_t b = task / heads;
     const int hd = (int)(task - b * heads);
-    float *sQ = sm[wave][0], *sK = sm[wave][1], *sV = sm[wave][2], *sO = sm[wave][3], *sP = sm[wave][4],
-          *sS = sm[wave][5];
-    const int r = lane >> 2, c0 = 4 * (lane & 3);
-    const int64_t tok = 16 * b + r;
-    auto sync = [] {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
+    const int t = lane & 15, g = lane >> 4;
+    const int64_t tok = 16 * b + t;
+    const uint16_t *row = qkv + tok * 3 * h + hd * 16 + 4 * g;
+    const s16x4 qa = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint2 *>(row));
+    const s16x4 ka = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint2 *>(row + h));
+    const s16x4 va = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint2 *>(row + 2 * h));
+    const s16x4 oa = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint2 *>(dout + tok * h + hd * 16 + 4 * g));
+    s16x4 eye;  // B operand identity: lane (n, g) holds I[4g + r][n]
+#pragma unroll
+    for (int r = 0; r < 4; r++) eye[r] = (short)(4 * g + r == t ? 0x3F80 : 0);
+    const f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+    auto pack4 = [](float a0, float a1, float a2, float a3) {
+        return __builtin_bit_cast(s16x4, make_uint2(pk2bf(a0, a1), pk2bf(a2, a3)));
     };
-    auto put = [&](float *dst, uint2 v) {
-        dst[r * kAbP + c0 + 0] = __uint_as_float(v.x << 16);
-        dst[r * kAbP + c0 + 1] = __uint_as_float(v.x & 0xFFFF0000u);
-        dst[r * kAbP + c0 + 2] = __uint_as_float(v.y << 16);
-        dst[r * kAbP + c0 + 3] = __uint_as_float(v.y & 0xFFFF0000u);
+    auto tr = [&](s16x4 x) {  // A-layout operand -> its transpose's A layout (= its own B layout)
+        const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(x, eye, zero, 0, 0, 0);
+        return pack4(d[0], d[1], d[2], d[3]);
     };
-    const uint16_t *row = qkv + tok * 3 * h + hd * 16 + c0;
-    const uint2 q = *reinterpret_cast<const uint2 *>(row), k = *reinterpret_cast<const uint2 *>(row + h),
-                v = *reinterpret_cast<const uint2 *>(row + 2 * h),
-                o = *reinterpret_cast<const uint2 *>(dout + tok * h + hd * 16 + c0);
-    put(sQ, q);
-    put(sK, k);
-    put(sV, v);
-    put(sO, o);
-    sync();
-    constexpr float scale = 0.25f;  // 1 / sqrt(16), scaled_dot_product_attention's default
-    auto rowsum4 = [](float x) {     // over the 4 lanes of a row (xor 1, 2)
-        x += __shfl_xor(x, 1);
-        return x + __shfl_xor(x, 2);
-    };
-    // P[r][c0 + u]
+    // P = softmax(Q K^T / 4), exactly urm_attn_kernel's arithmetic
+    const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ka, qa, zero, 0, 0, 0);
+    const float scale = 0.25f;  // 1 / sqrt(16), scaled_dot_product_attention's default
     float p[4];
-    {
-        float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    float m = -INFINITY;
 #pragma unroll
-        for (int d = 0; d < 16; d++) {
-            const float qd = sQ[r * kAbP + d];
-#pragma unroll
-            for (int u = 0; u < 4; u++) s[u] = __builtin_fmaf(qd, sK[(c0 + u) * kAbP + d], s[u]);
-        }
-        float mx = fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3]));
-        mx = fmaxf(mx, __shfl_xor(mx, 1));
-        mx = fmaxf(mx, __shfl_xor(mx, 2));
-        float sum = 0.0f;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            p[u] = expf((s[u] - mx) * scale);
-            sum += p[u];
-        }
-        const float inv = 1.0f / rowsum4(sum);
-#pragma unroll
-        for (int u = 0; u < 4; u++) p[u] *= inv;
+    for (int r = 0; r < 4; r++) {
+        p[r] = st[r] * scale;
+        m = fmaxf(m, p[r]);
     }
+    m = xmax32(xmax16(m));  // = the forward's two xor shuffles (max / + are commutative)
+    float sum = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        p[r] = __expf(p[r] - m);
+        sum += p[r];
+    }
+    sum = xsum32(xsum16(sum));
+    const float inv = 1.0f / sum;
+#pragma unroll
+    for (int r = 0; r < 4; r++) p[r] *= inv;
     // dropout: O = Pd V with Pd = P km (the forward's mask, regenerated); dV = Pd^T dO and
-    // dS = P (km dPd - rowsum(Pd dPd)), dPd = dO V^T (rowsum(P dP) = rowsum(Pd dPd))
+    // dS = P (km dPd - rowsum(Pd dPd)), dPd = dO V^T
     float km[4] = {1.0f, 1.0f, 1.0f, 1.0f};
-    if (kDrop) attn_keep(drop, b, hd, r, lane & 3, km);
-#pragma unroll
-    for (int u = 0; u < 4; u++) sP[r * kAbP + c0 + u] = kDrop ? p[u] * km[u] : p[u];
-    // dP[r][c0 + u] = sum_d dO[r][d] V[c0 + u][d];  dS = P (dP - rowsum(P dP))
-    {
-        float dp[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int d = 0; d < 16; d++) {
-            const float od = sO[r * kAbP + d];
-#pragma unroll
-            for (int u = 0; u < 4; u++) dp[u] = __builtin_fmaf(od, sV[(c0 + u) * kAbP + d], dp[u]);
-        }
-        float rs;
-        if (kDrop) {
-            rs = rowsum4(p[0] * km[0] * dp[0] + p[1] * km[1] * dp[1] + p[2] * km[2] * dp[2] + p[3] * km[3] * dp[3]);
-#pragma unroll
-            for (int u = 0; u < 4; u++) sS[r * kAbP + c0 + u] = p[u] * (dp[u] * km[u] - rs);
-        } else {
-            rs = rowsum4(p[0] * dp[0] + p[1] * dp[1] + p[2] * dp[2] + p[3] * dp[3]);
-#pragma unroll
-            for (int u = 0; u < 4; u++) sS[r * kAbP + c0 + u] = p[u] * (dp[u] - rs);
-        }
-    }
-    sync();
-    // dV[r][c0 + u] = sum_i P[i][r] dO[i][c0 + u];  dQ[r][..] = sum_j dS[r][j] K[j][..] / 4;
-    // dK[r][..] = sum_i dS[i][r] Q[i][..] / 4
-    float dv[4] = {0, 0, 0, 0}, dq[4] = {0, 0, 0, 0}, dk[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-        const float pir = sP[i * kAbP + r], sri = sS[r * kAbP + i], sir = sS[i * kAbP + r];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            dv[u] = __builtin_fmaf(pir, sO[i * kAbP + c0 + u], dv[u]);
-            dq[u] = __builtin_fmaf(sri, sK[i * kAbP + c0 + u], dq[u]);
-            dk[u] = __builtin_fmaf(sir, sQ[i * kAbP + c0 + u], dk[u]);
-        }
-    }
-    auto pack = [](float a, float b2) {
-        const __attribute__((ext_vector_type(2))) __bf16 t = {(__bf16)a, (__bf16)b2};
-        return __builtin_bit_cast(uint32_t, t);
-    };
-    uint16_t *drow = dqkv + tok * 3 * h + hd * 16 + c0;
-    *reinterpret_cast<uint2 *>(drow) = make_uint2(pack(dq[0] * scale, dq[1] * scale), pack(dq[2] * scale, dq[3] * scale));
-    *reinterpret_cast<uint2 *>(drow + h) =
-        make_uint2(pack(dk[0] * scale, dk[1] * scale), pack(dk[2] * scale, dk[3] * scale));
-    *reinterpret_cast<uint2 *>(drow + 2 * h) = make_uint2(pack(dv[0], dv[1]), pack(dv[2], dv[3]));
+    if (kDrop) attn_keep(drop, b, hd, t, g, km);
+    const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, oa, zero, 0, 0, 0);
+    float rs = (p[0] * km[0] * dp[0] + p[1] * km[1] * dp[1]) + (p[2] * km[2] * dp[2] + p[3] * km[3] * dp[3]);
+    rs = xsum32(xsum16(rs));
+    const s16x4 dsa = pack4(p[0] * (dp[0] * km[0] - rs), p[1] * (dp[1] * km[1] - rs), p[2] * (dp[2] * km[2] - rs),
+                            p[3] * (dp[3] * km[3] - rs));
+    const s16x4 pda = pack4(p[0] * km[0], p[1] * km[1], p[2] * km[2], p[3] * km[3]);
+    const f32x4 dq = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(tr(ka), dsa, zero, 0, 0, 0);
+    const f32x4 dk = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(tr(qa), tr(dsa), zero, 0, 0, 0);
+    const f32x4 dv = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(tr(oa), tr(pda), zero, 0, 0, 0);
+    uint16_t *drow = dqkv + tok * 3 * h + hd * 16 + 4 * g;
+    *reinterpret_cast<uint2 *>(drow) = make_uint2(pk2bf(dq[0] * scale, dq[1] * scale), pk2bf(dq[2] * scale, dq[3] * scale));
+    *reinterpret_cast<uint2 *>(drow + h) = make_uint2(pk2bf(dk[0] * scale, dk[1] * scale), pk2bf(dk[2] * scale, dk[3] * scale));
+    *reinterpret_cast<uint2 *>(drow + 2 * h) = make_uint2(pk2bf(dv[0], dv[1]), pk2bf(dv[2], dv[3]));
 }
 
 // Training-path residual RMSNorm of GameURMBlock (game.py:1346, 1350 with rms_norm :1223-1229) as
@@ -1271,7 +1245,9 @@ __global__ __launch_bounds__(256) void urm_rms_res_bwd_kernel(const float *__res
 constexpr int kScThreads = 128;
 
 __device__ __forceinline__ float bfr(float x) { return (float)(__bf16)x; }
-__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+// sigmoid on the hardware exp / reciprocal (v_exp_f32, v_rcp_f32: 1-2 ulp) instead of the libm expf
+// and an IEEE division (~25 instructions, which made these kernels VALU-bound)
+__device__ __forceinline__ float sigm(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ __forceinline__ uint16_t f2bf16(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
 __device__ __forceinline__ float bf16f(uint16_t x) { return __uint_as_float((uint32_t)x << 16); }
 
@@ -1352,14 +1328,15 @@ __global__ __launch_bounds__(kScThreads) void urm_swiglu_conv_bwd_kernel(const u
     const float w0 = w[2 * c], w1 = w[2 * c + 1], b = bias[c];
     float s0 = 0.0f, s1 = 0.0f, sb = 0.0f;
     for (int64_t bd = blockIdx.x; bd < nb; bd += gridDim.x) {
-        float g[16], u[16], y[16], d2[16];
+        float g[16], u[16], y[16], d2[16], sgg[16];
         float yp = 0.0f;
 #pragma unroll
         for (int t = 0; t < 16; t++) {
             const int64_t r = 16 * bd + t;
             g[t] = bf16f(gu[r * 2 * inter + c]);
             u[t] = bf16f(gu[r * 2 * inter + inter + c]);
-            y[t] = bfr(bfr(g[t] * sigm(g[t])) * u[t]);
+            sgg[t] = sigm(g[t]);
+            y[t] = bfr(bfr(g[t] * sgg[t]) * u[t]);
             const float y2 = yp * w0 + y[t] * w1 + b, sg = sigm(y2);
             d2[t] = bf16f(dact[r * inter + c]) * (sg * (1.0f + y2 * (1.0f - sg)));  // d act / d y2
             s1 += d2[t] * y[t];
@@ -1371,7 +1348,7 @@ __global__ __launch_bounds__(kScThreads) void urm_swiglu_conv_bwd_kernel(const u
         for (int t = 0; t < 16; t++) {
             const int64_t r = 16 * bd + t;
             const float dy = d2[t] * w1 + (t + 1 < 16 ? d2[t + 1] * w0 : 0.0f);
-            const float sg = sigm(g[t]), sl = bfr(g[t] * sg);
+            const float sg = sgg[t], sl = bfr(g[t] * sg);
             dgu[r * 2 * inter + c] = f2bf16(dy * u[t] * (sg * (1.0f + g[t] * (1.0f - sg))));
             dgu[r * 2 * inter + inter + c] = f2bf16(dy * sl);
         }
@@ -1380,6 +1357,78 @@ __global__ __launch_bounds__(kScThreads) void urm_swiglu_conv_bwd_kernel(const u
     pp[c] = s0;
     pp[inter + c] = s1;
     pp[2 * inter + c] = sb;
+}
+
+// The same backward with one thread per channel PAIR (4-byte gu / dact loads and dgu stores) and
+// four partial rows per 256-thread block (64 threads each, inter / 2 <= 64 of them active), the 16
+// tokens in ONE pass with a one-token lag (token t - 1's dgate / dup need d2 of token t): nothing
+// but the board's raw loads is kept in registers.  Partial row `row` takes boards row, row + nrows,
+// ... exactly like block `row` of urm_swiglu_conv_bwd_kernel, with the same per-channel arithmetic,
+// so dgu and the partials are bitwise those of the one-channel kernel.
+__global__ __launch_bounds__(256) void urm_swiglu_conv_bwd2_kernel(const uint16_t *__restrict__ gu,
+                                                                   const float *__restrict__ w,
+                                                                   const float *__restrict__ bias,
+                                                                   const uint16_t *__restrict__ dact,
+                                                                   uint16_t *__restrict__ dgu, float *__restrict__ part,
+                                                                   int64_t nb, int inter, int nrows) {
+    const int cp = threadIdx.x & 63, row = (int)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= nrows || 2 * cp >= inter) return;  // no barriers below
+    const int c = 2 * cp;
+    const float w0[2] = {w[2 * c], w[2 * c + 2]}, w1[2] = {w[2 * c + 1], w[2 * c + 3]}, bb[2] = {bias[c], bias[c + 1]};
+    float s0[2] = {0.0f, 0.0f}, s1[2] = {0.0f, 0.0f}, sb[2] = {0.0f, 0.0f};
+    for (int64_t bd = row; bd < nb; bd += nrows) {
+        uint32_t gr[16], ur[16], dr[16];  // the board's 48 loads in flight before any arithmetic
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            const uint16_t *rw = gu + (16 * bd + t) * 2 * inter;
+            gr[t] = *reinterpret_cast<const uint32_t *>(rw + c);
+            ur[t] = *reinterpret_cast<const uint32_t *>(rw + inter + c);
+            dr[t] = *reinterpret_cast<const uint32_t *>(dact + (16 * bd + t) * inter + c);
+        }
+        float yp[2] = {0.0f, 0.0f}, gq[2] = {0.0f, 0.0f}, uq[2] = {0.0f, 0.0f}, sq[2] = {0.0f, 0.0f}, dq[2] = {0.0f, 0.0f};
+#pragma unroll
+        for (int t = 0; t <= 16; t++) {
+            float d2[2] = {0.0f, 0.0f}, g[2] = {0.0f, 0.0f}, u[2] = {0.0f, 0.0f}, sg[2] = {0.0f, 0.0f};
+            uint16_t og[2], ou[2];
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                if (t < 16) {
+                    g[j] = __uint_as_float(j ? gr[t] & 0xFFFF0000u : gr[t] << 16);
+                    u[j] = __uint_as_float(j ? ur[t] & 0xFFFF0000u : ur[t] << 16);
+                    const float da = __uint_as_float(j ? dr[t] & 0xFFFF0000u : dr[t] << 16);
+                    sg[j] = sigm(g[j]);
+                    const float y = bfr(bfr(g[j] * sg[j]) * u[j]);
+                    const float y2 = yp[j] * w0[j] + y * w1[j] + bb[j], s2 = sigm(y2);
+                    d2[j] = da * (s2 * (1.0f + y2 * (1.0f - s2)));  // d act / d y2
+                    s1[j] += d2[j] * y;
+                    s0[j] += d2[j] * yp[j];
+                    sb[j] += d2[j];
+                    yp[j] = y;
+                }
+                if (t > 0) {  // token t - 1
+                    const float dy = dq[j] * w1[j] + (t < 16 ? d2[j] * w0[j] : 0.0f);
+                    og[j] = f2bf16(dy * uq[j] * (sq[j] * (1.0f + gq[j] * (1.0f - sq[j]))));
+                    ou[j] = f2bf16(dy * bfr(gq[j] * sq[j]));
+                }
+                gq[j] = g[j];
+                uq[j] = u[j];
+                sq[j] = sg[j];
+                dq[j] = d2[j];
+            }
+            if (t > 0) {
+                uint16_t *dw = dgu + (16 * bd + t - 1) * 2 * inter;
+                *reinterpret_cast<uint32_t *>(dw + c) = (uint32_t)og[0] | ((uint32_t)og[1] << 16);
+                *reinterpret_cast<uint32_t *>(dw + inter + c) = (uint32_t)ou[0] | ((uint32_t)ou[1] << 16);
+            }
+        }
+    }
+    float *pp = part + (int64_t)row * 3 * inter;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        pp[c + j] = s0[j];
+        pp[inter + c + j] = s1[j];
+        pp[2 * inter + c + j] = sb[j];
+    }
 }
 
 // dw [inter][2] (w0, w1 interleaved as the conv weight), db [inter] from the nblk partial rows:
@@ -1667,6 +1716,15 @@ __global__ __launch_bounds__(kWgThreads) void urm_wgrad_kernel(const uint16_t *_
     }
 }
 
+// The same product on the LDS-DMA ring of wgrad_ring.hpp (round 4) for the default GameURM's
+// shapes: the kernel above keeps one 64-row chunk in flight per CU (3.7-4.6 TB/s on 1 M rows); the
+// ring keeps three 32-row stages in flight with no register staging.  Same partial layout.
+template <int N, int K, int BI, int BJ, int WI>
+__global__ __launch_bounds__(g2048::wgr::kThreads) void urm_wgrad_ring_kernel(g2048::wgr::Prod pr, int64_t m) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    g2048::wgr::product<N, K, BI, BJ, WI>(pr, m, blockIdx.x, smem);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -1876,8 +1934,12 @@ int g2048_urm_swiglu_conv_bwd(g2048_stream_t stream, const uint16_t *gu, const f
     if (!gu || !w || !b || !dact || !dgu || !dw || !db || !partials) return G2048_EINVAL;
     const hipStream_t s = (hipStream_t)stream;
     const int nblk = sc_blocks(n);
-    hipLaunchKernelGGL(urm_swiglu_conv_bwd_kernel, dim3(nblk), dim3(kScThreads), 0, s, gu, w, b, dact, dgu, partials, n,
-                       (int)inter);
+    if (inter % 2 == 0 && inter <= 128 && ((uintptr_t)gu | (uintptr_t)dact | (uintptr_t)dgu) % 4 == 0)
+        hipLaunchKernelGGL(urm_swiglu_conv_bwd2_kernel, dim3((unsigned)((nblk + 3) / 4)), dim3(256), 0, s, gu, w, b, dact,
+                           dgu, partials, n, (int)inter, nblk);
+    else
+        hipLaunchKernelGGL(urm_swiglu_conv_bwd_kernel, dim3(nblk), dim3(kScThreads), 0, s, gu, w, b, dact, dgu, partials,
+                           n, (int)inter);
     hipLaunchKernelGGL(urm_swiglu_conv_colsum_kernel, dim3((3 * inter + 15) / 16), dim3(256), 0, s, partials, nblk,
                        (int)inter, dw, db);
     return launch_status();
@@ -1945,12 +2007,31 @@ int g2048_urm_wgrad(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x
     if (m <= 0 || !g2048_urm_wgrad_supported(n, k)) return G2048_EINVAL;
     if (!dy || !x || !dw || !partials || ((uintptr_t)dy | (uintptr_t)x) % 16) return G2048_EINVAL;
     const int nblk = wgrad_blocks(m);
+    const hipStream_t s = (hipStream_t)stream;
+    {   // the ring kernel for the default GameURM's projections (every block writes its partial)
+        int64_t rr = (m + nblk - 1) / nblk;
+        rr = (rr + g2048::wgr::kRows - 1) / g2048::wgr::kRows * g2048::wgr::kRows;
+        const g2048::wgr::Prod pr{reinterpret_cast<const char *>(dy), reinterpret_cast<const char *>(x), partials, rr,
+                                  nblk, 0};
+        bool ring = true;
+        const dim3 gd((unsigned)nblk), bk(g2048::wgr::kThreads);
+        const size_t lds = g2048::wgr::kLds;
+        if (n == 192 && k == 64) hipLaunchKernelGGL((urm_wgrad_ring_kernel<192, 64, 3, 2, 4>), gd, bk, lds, s, pr, m);
+        else if (n == 64 && k == 64) hipLaunchKernelGGL((urm_wgrad_ring_kernel<64, 64, 1, 2, 4>), gd, bk, lds, s, pr, m);
+        else if (n == 240 && k == 64) hipLaunchKernelGGL((urm_wgrad_ring_kernel<240, 64, 4, 2, 4>), gd, bk, lds, s, pr, m);
+        else if (n == 64 && k == 120) hipLaunchKernelGGL((urm_wgrad_ring_kernel<64, 120, 1, 4, 4>), gd, bk, lds, s, pr, m);
+        else ring = false;
+        if (ring) {
+            hipLaunchKernelGGL(urm_colsum_kernel, dim3((unsigned)((n * k + 15) / 16)), dim3(256), 0, s, partials, nblk,
+                               (int)(n * k), dw);
+            return launch_status();
+        }
+    }
     int64_t rows = (m + nblk - 1) / nblk;
     rows = (rows + kWgChunk - 1) / kWgChunk * kWgChunk;
     const int kp = (k + 15) / 16 * 16;
     auto pitch = [](int cols) { const int dw = cols / 2; return 4 * (dw + ((8 - dw % 32) + 32) % 32); };
     const size_t lds = (size_t)kWgChunk * (pitch(n) + pitch(kp));
-    const hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(urm_wgrad_kernel, dim3(nblk), dim3(kWgThreads), lds, s, dy, x, m, (int)n, (int)k, kp, rows,
                        partials);
     hipLaunchKernelGGL(urm_colsum_kernel, dim3((unsigned)((n * k + 15) / 16)), dim3(256), 0, s, partials, nblk,
