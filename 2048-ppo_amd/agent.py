@@ -158,7 +158,9 @@ class GameConvSwiGLU(nn.Module):
                                 bias=True)
         self.down_proj = nn.Linear(inter, hidden_size, bias=False)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def act(self, x: torch.Tensor) -> torch.Tensor | None:
+        """The down_proj operand act [B, S, I] on the fused device path (gate_up + SwiGLU + conv in one
+        kernel), or None where that path does not apply (the caller then runs forward)."""
         if x.is_cuda:
             from g2048 import urm as _urm  # fused gate_up + SwiGLU + conv (training, g2048_urm.h)
             if _urm.gate_up_swiglu_supported(self, x):
@@ -166,7 +168,14 @@ class GameConvSwiGLU(nn.Module):
                 args = (x.reshape(b * s, h), self.gate_up_proj.weight, self.dwconv.weight.view(-1, 2), self.dwconv.bias)
                 act = (_urm.GateUpSwiGLUFn.apply(*args) if torch.is_grad_enabled()
                        else _urm.gate_up_swiglu_nograd(*args))
-                return _urm.project(self.down_proj, act.view(b, s, self.inter))
+                return act.view(b, s, self.inter)
+        return None
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        act = self.act(x)
+        if act is not None:
+            from g2048 import urm as _urm
+            return _urm.project(self.down_proj, act)
         gu = self.gate_up_proj(x)
         if gu.is_cuda:
             from g2048 import urm as _urm  # the device SwiGLU + conv and its backward (g2048_urm.h)
@@ -201,8 +210,10 @@ class GameURMAttention(nn.Module):
         self.qkv_proj = nn.Linear(hidden_size, 3 * hidden_size, bias=False)
         self.o_proj = nn.Linear(hidden_size, hidden_size, bias=False)
 
-    def forward(self, h: torch.Tensor, hb: torch.Tensor | None = None) -> torch.Tensor:
-        """hb: h's bf16 copy when the caller already has it (bf16 autocast: the same operand)."""
+    def forward(self, h: torch.Tensor, hb: torch.Tensor | None = None, pre_proj: bool = False):
+        """hb: h's bf16 copy when the caller already has it (bf16 autocast: the same operand).
+        pre_proj: return (o, True) -- the attention output BEFORE o_proj -- where the device attention
+        ran (the caller fuses o_proj into its residual RMSNorm), else (attn(h), False)."""
         b, s, _ = h.shape
         p = self.dropout if self.training else 0.0
         if h.is_cuda:
@@ -210,12 +221,15 @@ class GameURMAttention(nn.Module):
             qkv = _urm.project(self.qkv_proj, h if hb is None else hb)
             if _urm.attention_supported(qkv, s, self.hidden_size, self.num_heads, p):
                 o = _urm.URMAttentionFn.apply(qkv.reshape(b * s, 3 * self.hidden_size), self.num_heads, p)
+                if pre_proj:
+                    return o.view(b, s, self.hidden_size), True
                 return _urm.project(self.o_proj, o.view(b, s, self.hidden_size))
         else:
             qkv = self.qkv_proj(h)
         q, k, v = qkv.view(b, s, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).unbind(0)
         o = F.scaled_dot_product_attention(q, k, v, dropout_p=p, is_causal=False)
-        return self.o_proj(o.transpose(1, 2).reshape(b, s, self.hidden_size))
+        a = self.o_proj(o.transpose(1, 2).reshape(b, s, self.hidden_size))
+        return (a, False) if pre_proj else a
 
 
 class GameURMBlock(nn.Module):
@@ -231,6 +245,19 @@ class GameURMBlock(nn.Module):
         """want_hb: also return the output's bf16 copy (None when not produced) for the next block's
         qkv projection; on the device under bf16 autocast the residual RMSNorm kernel writes it, so
         autocast's cast kernels (and their backward) disappear."""
+        if h.is_cuda:
+            from g2048 import urm as _urm
+            if _urm.linres_supported(self.attn.o_proj, h) and _urm.linres_supported(self.mlp.down_proj, h):
+                # o_proj / down_proj fused with their residual RMSNorm (LinResRMSFn, one kernel each)
+                o, pre = self.attn(h, hb, pre_proj=True)
+                h, hb1 = (_urm.LinResRMSFn.apply(h, o, self.attn.o_proj.weight, self.norm_eps, True) if pre
+                          else _urm.ResidualRMSFn.apply(h, o, self.norm_eps, True))
+                act = self.mlp.act(hb1)
+                if act is not None:
+                    res = _urm.LinResRMSFn.apply(h, act, self.mlp.down_proj.weight, self.norm_eps, want_hb)
+                else:
+                    res = _urm.ResidualRMSFn.apply(h, self.mlp(hb1), self.norm_eps, want_hb)
+                return res
         a = self.attn(h, hb)
         if h.is_cuda:
             from g2048 import urm as _urm  # the device residual RMSNorm and its backward (g2048_urm.h)

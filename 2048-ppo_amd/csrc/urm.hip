@@ -399,7 +399,11 @@ __global__ __launch_bounds__(kThreads) void urm_pool_heads_kernel(const float *_
 //              gate_up output) and act follows urm_swiglu_conv_fwd's arithmetic on those rounded
 //              values (y = bf16(bf16(silu(g)) u), act = bf16(silu(y_{t-1} w0 + y_t w1 + b))): the
 //              gu round trip through HBM of the unfused path (GEMM write + SwiGLU read) is gone.
-enum { EPI_STORE = 0, EPI_RMS = 1, EPI_SWIGLU = 2, EPI_SWIGLU_T = 3 };
+//   EPI_RMS_T  the training variant of EPI_RMS (autograd LinResRMSFn): a = bf16(x W^T) (autocast's
+//              projection output), s = h + a with h read from `emb` (not written: autograd keeps it),
+//              out = s rsqrt(mean(s^2) + eps) -> x (fp32), xb (bf16), rstd [rows] -- the projection's
+//              bf16 output never round-trips through HBM.
+enum { EPI_STORE = 0, EPI_RMS = 1, EPI_SWIGLU = 2, EPI_SWIGLU_T = 3, EPI_RMS_T = 4 };
 
 __device__ __forceinline__ float dpp_prev_token(float v) {  // lane t-1 of the 16-lane row, 0 for t = 0
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xF, 0xF, false));
@@ -414,7 +418,8 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
                                                               float *__restrict__ x, const float *__restrict__ emb,
                                                               uint16_t *__restrict__ xb, float eps,
                                                               const float *__restrict__ cw,
-                                                              const float *__restrict__ cb) {
+                                                              const float *__restrict__ cb,
+                                                              float *__restrict__ rstd) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int kPitch = 32 * KS + 8;  // bf16 per staged row
     constexpr int kRowsW = 16 * CT;
@@ -488,10 +493,18 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
 #pragma unroll
             for (int ct = 0; ct < CT; ct++) {
                 const int c = 16 * ct + 4 * g;
-                if (c < N)
+                if (c < N) {
+                    if (cw) {  // g2048_urm_linear_bias: the fp32 bias added before the single rounding
+                        const float4 bv = *reinterpret_cast<const float4 *>(cw + c);
+                        acc[ct][0] += bv.x;
+                        acc[ct][1] += bv.y;
+                        acc[ct][2] += bv.z;
+                        acc[ct][3] += bv.w;
+                    }
                     *reinterpret_cast<uint2 *>(tile + t * tp + 2 * c) =
                         make_uint2(pk2bf(acc[ct][0], acc[ct][1]),
                                    pk2bf(acc[ct][2], acc[ct][3]));
+                }
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
@@ -536,6 +549,34 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
                                    pk2bf(o.z, o.w));
                 }
             }
+        } else if constexpr (EPI == EPI_RMS_T) {
+            f32x4 sv[CT];
+            float ss = 0.0f;
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) {
+                const int c = 16 * ct + 4 * g;
+                sv[ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+                if (c < N) {
+                    const float4 hv = *reinterpret_cast<const float4 *>(emb + r * N + c);
+                    sv[ct][0] = hv.x + (float)(__bf16)acc[ct][0];
+                    sv[ct][1] = hv.y + (float)(__bf16)acc[ct][1];
+                    sv[ct][2] = hv.z + (float)(__bf16)acc[ct][2];
+                    sv[ct][3] = hv.w + (float)(__bf16)acc[ct][3];
+                    ss += (sv[ct][0] * sv[ct][0] + sv[ct][1] * sv[ct][1]) + (sv[ct][2] * sv[ct][2] + sv[ct][3] * sv[ct][3]);
+                }
+            }
+            ss = xsum32(xsum16(ss));
+            const float rs = rsqrtf(ss * (1.0f / (float)N) + eps);
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) {
+                const int c = 16 * ct + 4 * g;
+                if (c < N) {
+                    const float4 o = make_float4(sv[ct][0] * rs, sv[ct][1] * rs, sv[ct][2] * rs, sv[ct][3] * rs);
+                    *reinterpret_cast<float4 *>(x + r * N + c) = o;
+                    if (xb) *reinterpret_cast<uint2 *>(xb + r * N + c) = make_uint2(pk2bf(o.x, o.y), pk2bf(o.z, o.w));
+                }
+            }
+            if (g == 0) rstd[r] = rs;
         } else if constexpr (EPI == EPI_SWIGLU_T) {
             constexpr int CH = CT / 2;
             static_assert(CH % 2 == 0, "column tiles are stored in pairs");
@@ -585,9 +626,11 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
                 const uint4 vg = pair16(og), vu = pair16(ou), vo = pair16(oo);
                 const int c8 = 16 * cp + cb8;
                 if (c8 < inter) {  // inter % 8 == 0: a lane's 8 features are all valid or all past inter
-                    uint16_t *gr = xb + r * 2 * inter;  // gu output (xb carries it for this epilogue)
-                    *reinterpret_cast<uint4 *>(gr + c8) = vg;
-                    *reinterpret_cast<uint4 *>(gr + inter + c8) = vu;
+                    if (xb) {  // gu output (xb carries it; null: the no-grad loops, act only)
+                        uint16_t *gr = xb + r * 2 * inter;
+                        *reinterpret_cast<uint4 *>(gr + c8) = vg;
+                        *reinterpret_cast<uint4 *>(gr + inter + c8) = vu;
+                    }
                     *reinterpret_cast<uint4 *>(y + r * inter + c8) = vo;
                 }
             }
@@ -631,24 +674,25 @@ inline LinShape lin_shape(int K, int N, int inter, int epi) {
 
 template <int KS, int CT, int EPI>
 int launch_lin(hipStream_t s, const uint16_t *in, const uint16_t *w, int64_t rows, int K, int N, int inter,
-               uint16_t *y, float *x, const float *emb, uint16_t *xb, float eps, const float *cw, const float *cb) {
+               uint16_t *y, float *x, const float *emb, uint16_t *xb, float eps, const float *cw, const float *cb,
+               float *rstd) {
     const size_t tile = EPI == EPI_STORE ? 16 * (2 * 16 * CT + 8) : 0;
     const size_t lds = (size_t)16 * CT * (32 * KS + 8) * 2 + (size_t)(kThreads / 64) * tile;
     int64_t grid = ((rows >> 4) + (kThreads / 64) - 1) / (kThreads / 64);
     grid = grid > 1024 ? 1024 : grid;  // persistent over boards; W staged once per block
     hipLaunchKernelGGL((urm_linear_kernel<KS, CT, EPI>), dim3((unsigned)grid), dim3(kThreads), lds, s, in, w, rows, K, N,
-                       inter, y, x, emb, xb, eps, cw, cb);
+                       inter, y, x, emb, xb, eps, cw, cb, rstd);
     return launch_status();
 }
 
 // the instantiated shapes: GameURMConfig h = 64 (inter 120) and h = 32 (inter 64, the golden config)
 int dispatch_lin(hipStream_t s, int epi, const uint16_t *in, const uint16_t *w, int64_t rows, int K, int N, int inter,
                  uint16_t *y, float *x, const float *emb, uint16_t *xb, float eps, const float *cw, const float *cb,
-                 bool dry) {
+                 bool dry, float *rstd = nullptr) {
     const LinShape sh = lin_shape(K, N, inter, epi);
 #define G2048_LIN(EPI_, KS_, CT_)                                                                              \
     if (epi == EPI_ && sh.ks == KS_ && sh.ct == CT_)                                                            \
-        return dry ? G2048_OK : launch_lin<KS_, CT_, EPI_>(s, in, w, rows, K, N, inter, y, x, emb, xb, eps, cw, cb);
+        return dry ? G2048_OK : launch_lin<KS_, CT_, EPI_>(s, in, w, rows, K, N, inter, y, x, emb, xb, eps, cw, cb, rstd);
     G2048_LIN(EPI_STORE, 2, 12)   // h 64 qkv
     G2048_LIN(EPI_STORE, 1, 6)    // h 32 qkv
     // the training Functions' plain projections (URMLinearFn / GateUpSwiGLUFn): the forwards of
@@ -669,6 +713,10 @@ int dispatch_lin(hipStream_t s, int epi, const uint16_t *in, const uint16_t *w, 
     G2048_LIN(EPI_RMS, 4, 4)      // h 64 down_proj (K = inter = 120)
     G2048_LIN(EPI_RMS, 1, 2)      // h 32 o_proj
     G2048_LIN(EPI_RMS, 2, 2)      // h 32 down_proj (K = 64)
+    G2048_LIN(EPI_RMS_T, 2, 4)    // h 64 o_proj, training (LinResRMSFn)
+    G2048_LIN(EPI_RMS_T, 4, 4)    // h 64 down_proj, training
+    G2048_LIN(EPI_RMS_T, 1, 2)    // h 32 o_proj, training
+    G2048_LIN(EPI_RMS_T, 2, 2)    // h 32 down_proj, training
     G2048_LIN(EPI_SWIGLU, 2, 16)  // h 64 gate_up (inter 120 -> 2 x 8 tiles)
     G2048_LIN(EPI_SWIGLU, 1, 8)   // h 32 gate_up (inter 64)
     G2048_LIN(EPI_SWIGLU_T, 2, 16)  // training variants of the two
@@ -2086,8 +2134,8 @@ int g2048_urm_pool_heads(g2048_stream_t stream, const float *x, const float *wa,
 
 
 int g2048_urm_linear_supported(int32_t epilogue, int32_t k, int32_t n, int32_t inter) {
-    if (epilogue < 0 || epilogue > 3 || k <= 0 || k % 4 || n <= 0 || n % 4 ||
-        (epilogue >= 2 && (inter <= 0 || inter % 4)))
+    if (epilogue < 0 || epilogue > 4 || k <= 0 || k % 4 || n <= 0 || n % 4 ||
+        ((epilogue == 2 || epilogue == 3) && (inter <= 0 || inter % 4)))
         return 0;
     return dispatch_lin(nullptr, epilogue, nullptr, nullptr, 0, k, n, inter, nullptr, nullptr, nullptr, nullptr, 0.0f,
                         nullptr, nullptr, true) == G2048_OK ? 1 : 0;
@@ -2110,6 +2158,25 @@ int g2048_urm_linear_rms(g2048_stream_t stream, const uint16_t *in, const uint16
     return dispatch_lin((hipStream_t)stream, 1, in, w, rows, k, h, 0, nullptr, x, emb, xb, eps, nullptr, nullptr, false);
 }
 
+int g2048_urm_linear_bias(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *bias, uint16_t *out,
+                          int64_t rows, int32_t k, int32_t n) {
+    if (rows < 0 || rows % 16 || n % 8 || !g2048_urm_linear_supported(0, k, n, 0)) return G2048_EINVAL;
+    if (rows == 0) return G2048_OK;
+    if (!in || !w || !bias || !out || (uintptr_t)bias % 16) return G2048_EINVAL;
+    return dispatch_lin((hipStream_t)stream, 0, in, w, rows, k, n, 0, out, nullptr, nullptr, nullptr, 0.0f, bias, nullptr,
+                        false);
+}
+
+int g2048_urm_linear_res_rms(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *h, float *out,
+                             uint16_t *outb, float *rstd, int64_t rows, int32_t k, int32_t n, float eps) {
+    if (rows < 0 || rows % 16 || !g2048_urm_linear_supported(4, k, n, 0)) return G2048_EINVAL;
+    if (rows == 0) return G2048_OK;
+    if (!in || !w || !h || !out || !rstd || ((uintptr_t)h | (uintptr_t)out) % 16 || (outb && (uintptr_t)outb % 8))
+        return G2048_EINVAL;
+    return dispatch_lin((hipStream_t)stream, 4, in, w, rows, k, n, 0, nullptr, out, h, outb, eps, nullptr, nullptr, false,
+                        rstd);
+}
+
 int g2048_urm_linear_swiglu(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *conv_w,
                             const float *conv_b, uint16_t *out, int64_t rows, int32_t h, int32_t inter) {
     if (rows < 0 || rows % 16 || !g2048_urm_linear_supported(2, h, 2 * inter, inter)) return G2048_EINVAL;
@@ -2125,7 +2192,7 @@ int g2048_urm_linear_swiglu_train(g2048_stream_t stream, const uint16_t *in, con
     // the epilogue writes 8 features per lane with 16-byte stores: inter % 8, 16-byte aligned outputs
     if (rows < 0 || rows % 16 || inter % 8 || !g2048_urm_linear_supported(3, h, 2 * inter, inter)) return G2048_EINVAL;
     if (rows == 0) return G2048_OK;
-    if (!in || !w || !conv_w || !conv_b || !gu || !act || ((uintptr_t)conv_w | (uintptr_t)conv_b) % 16 ||
+    if (!in || !w || !conv_w || !conv_b || !act || ((uintptr_t)conv_w | (uintptr_t)conv_b) % 16 ||
         ((uintptr_t)gu | (uintptr_t)act) % 16)
         return G2048_EINVAL;
     return dispatch_lin((hipStream_t)stream, 3, in, w, rows, h, 2 * inter, inter, act, nullptr, nullptr, gu, 0.0f,

@@ -44,7 +44,7 @@ EXPORTED = (
     # include/g2048_urm.h
     "g2048_urm_stem", "g2048_urm_attention", "g2048_urm_residual_rms", "g2048_urm_swiglu_conv",
     "g2048_urm_pool_heads", "g2048_urm_linear_supported", "g2048_urm_linear", "g2048_urm_linear_rms",
-    "g2048_urm_linear_swiglu", "g2048_urm_linear_swiglu_train", "g2048_urm_wgrad_supported", "g2048_urm_wgrad_partials", "g2048_urm_wgrad", "g2048_urm_forward_supported", "g2048_urm_forward",
+    "g2048_urm_linear_swiglu", "g2048_urm_linear_swiglu_train", "g2048_urm_linear_res_rms", "g2048_urm_linear_bias", "g2048_urm_wgrad_supported", "g2048_urm_wgrad_partials", "g2048_urm_wgrad", "g2048_urm_forward_supported", "g2048_urm_forward",
 )
 
 
@@ -273,6 +273,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
                                                   ctypes.c_uint64, vp]),
         "g2048_urm_linear": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_linear_rms": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32, ctypes.c_float]),
+        "g2048_urm_linear_bias": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32]),
+        "g2048_urm_linear_res_rms": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, ctypes.c_float]),
         "g2048_urm_linear_swiglu": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_linear_swiglu_train": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_wgrad_supported": (ctypes.c_int, [i32, i32]),
@@ -1121,6 +1123,23 @@ def urm_linear(inp, w, out):
     rows, k = inp.shape
     _check(load().g2048_urm_linear(_stream(inp), _dev(inp, torch.bfloat16, "in"), _dev(w, torch.bfloat16, "w"),
                                    _dev(out, torch.bfloat16, "out"), rows, k, w.shape[0]), "g2048_urm_linear")
+
+
+def urm_linear_bias(inp, w, bias, out):
+    """out = bf16(inp w^T + bias) with one rounding (autocast's biased Linear; g2048_urm_linear_bias)."""
+    rows, k = inp.shape
+    _check(load().g2048_urm_linear_bias(_stream(inp), _dev(inp, torch.bfloat16, "in"), _dev(w, torch.bfloat16, "w"),
+                                        _dev(bias, torch.float32, "bias"), _dev(out, torch.bfloat16, "out"), rows, k,
+                                        w.shape[0]), "g2048_urm_linear_bias")
+
+
+def urm_linear_res_rms(inp, w, h, out, outb, rstd, eps: float):
+    """out = rms_norm(h + bf16(inp w^T)), outb = bf16(out) (optional), rstd (g2048_urm_linear_res_rms)."""
+    rows, k = inp.shape
+    _check(load().g2048_urm_linear_res_rms(_stream(inp), _dev(inp, torch.bfloat16, "in"), _dev(w, torch.bfloat16, "w"),
+                                           _dev(h, torch.float32, "h"), _dev(out, torch.float32, "out"),
+                                           _dev(outb, torch.bfloat16, "outb"), _dev(rstd, torch.float32, "rstd"), rows,
+                                           k, w.shape[0], float(eps)), "g2048_urm_linear_res_rms")
 
 
 def urm_linear_rms(inp, w, x, emb, xb, eps: float):

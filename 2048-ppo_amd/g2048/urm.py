@@ -479,8 +479,8 @@ class URMHeadsFn(torch.autograd.Function):
     """GameURM's action_head and value_head on the pooled features under bf16 autocast
     (game.py:1452-1456) without the library's K = n GEMMs (hipBLASLt ran the heads' weight gradient
     at ~0.2 ms and its input gradient at ~0.16 ms per 65 536 boards): the two heads as one [8, h]
-    projection (action rows 0-3, value row 4, zero rows) on g2048_urm_linear, bias added in fp32 and
-    rounded once more to bf16 (autocast rounds the biased GEMM output once); backward: dW on
+    projection (action rows 0-3, value row 4, zero rows) on g2048_urm_linear_bias, the bf16 bias added
+    to the fp32 accumulator before the one rounding (autocast's biased GEMM); backward: dW on
     g2048_urm_wgrad (dy zero-padded to 16 columns), dpooled = dy W on g2048_urm_linear, db a column
     sum.  pooled fp32 or bf16 [n, h] -> logits bf16 [n, 4], value bf16 [n, 1]."""
 
@@ -491,9 +491,12 @@ class URMHeadsFn(torch.autograd.Function):
         w8 = torch.zeros(8, h, dtype=torch.bfloat16, device=pooled.device)
         w8[:4] = wa.detach()
         w8[4:5] = wv.detach()
-        y = _gemm(pb, w8).float()
-        logits = (y[:, :4] + ba.detach().float()).to(torch.bfloat16)
-        value = (y[:, 4:5] + bv.detach().float()).to(torch.bfloat16)
+        b8 = torch.zeros(8, dtype=torch.float32, device=pooled.device)  # autocast casts the bias to bf16
+        b8[:4] = ba.detach().to(torch.bfloat16).float()
+        b8[4:5] = bv.detach().to(torch.bfloat16).float()
+        y = torch.empty(pb.shape[0], 8, dtype=torch.bfloat16, device=pooled.device)
+        L.urm_linear_bias(pb, w8, b8, y)  # x W^T + b accumulated in fp32, ONE bf16 rounding (round 4)
+        logits, value = y[:, :4].contiguous(), y[:, 4:5].contiguous()
         ctx.save_for_backward(pb, w8)
         ctx.dtypes = (pooled.dtype, wa.dtype, ba.dtype, wv.dtype, bv.dtype)
         return logits, value
@@ -538,6 +541,56 @@ def project(lin, x: torch.Tensor) -> torch.Tensor:
     return lin(x)
 
 
+class LinResRMSFn(torch.autograd.Function):
+    """o_proj / down_proj + residual + post-norm of GameURMBlock (game.py:1346-1350: h = rms_norm(h +
+    proj(x))) under bf16 autocast in ONE forward kernel (g2048_urm_linear_res_rms: the projection on
+    MFMA, its autocast bf16 output added to h in the epilogue, RMSNorm, fp32 out + bf16 copy + rstd):
+    the projection output's HBM round trip of URMLinearFn + ResidualRMSFn is gone.  Backward =
+    ResidualRMSFn's kernel (dh fp32, da bf16) then URMLinearFn's (dX on the projection kernel, dW on
+    g2048_urm_wgrad).  h fp32 [..., n], x [..., k] (bf16, or cast like autocast), w [n, k] -> out fp32
+    (and its bf16 copy with with_bf16)."""
+
+    @staticmethod
+    def forward(ctx, h: torch.Tensor, x: torch.Tensor, w: torch.Tensor, eps: float, with_bf16: bool = False):
+        ctx.set_materialize_grads(False)
+        shape = h.shape
+        h2 = h.reshape(-1, shape[-1]).contiguous()
+        xb = x.reshape(-1, x.shape[-1]).to(torch.bfloat16).contiguous()
+        wb = w.detach().to(torch.bfloat16).contiguous()
+        out = torch.empty_like(h2)
+        outb = torch.empty(h2.shape, dtype=torch.bfloat16, device=h.device) if with_bf16 else None
+        rstd = torch.empty(h2.shape[0], dtype=torch.float32, device=h.device)
+        L.urm_linear_res_rms(xb, wb, h2, out, outb, rstd, eps)
+        ctx.save_for_backward(out, rstd, xb, wb)
+        ctx.shape, ctx.xshape, ctx.dtypes = shape, x.shape, (x.dtype, w.dtype)
+        if with_bf16:
+            return out.view(shape), outb.view(shape)
+        return out.view(shape)
+
+    @staticmethod
+    def backward(ctx, dout: torch.Tensor | None, doutb: torch.Tensor | None = None):
+        out, rstd, xb, wb = ctx.saved_tensors
+        if dout is None and doutb is None:
+            return None, None, None, None, None
+        dh = torch.empty_like(out)
+        da = torch.empty(out.shape, dtype=torch.bfloat16, device=out.device)
+        d32 = None if dout is None else dout.reshape(out.shape).float().contiguous()
+        db16 = None if doutb is None else doutb.reshape(out.shape).to(torch.bfloat16).contiguous()
+        L.urm_rms_res_bwd(d32, out, rstd, dh, da, db16)
+        dx = _gemm(da, wb.t().contiguous()) if ctx.needs_input_grad[1] else None
+        dw = _wgrad(da, xb).to(ctx.dtypes[1]) if ctx.needs_input_grad[2] else None
+        return (dh.view(ctx.shape), None if dx is None else dx.to(ctx.dtypes[0]).view(ctx.xshape), dw, None, None)
+
+
+def linres_supported(lin, h: torch.Tensor) -> bool:
+    """LinResRMSFn applies: URMLinearFn's conditions, an fp32 residual stream of hidden size 64 (the
+    residual RMSNorm kernels), the instantiated projection shapes."""
+    n, k = lin.weight.shape
+    return (h.is_cuda and h.dtype == torch.float32 and lin.bias is None and h.shape[-1] == n == 64
+            and L.urm_wgrad_supported(n, k) and L.urm_linear_supported(4, k, n) and L.urm_linear_supported(0, n, k)
+            and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+
+
 class GateUpSwiGLUFn(torch.autograd.Function):
     """gate_up_proj + SwiGLU + kernel-2 depthwise conv + SiLU of GameConvSwiGLU (game.py:1264-1276)
     under bf16 autocast, for autograd training on the device: ONE forward kernel
@@ -578,15 +631,16 @@ class GateUpSwiGLUFn(torch.autograd.Function):
 
 def gate_up_swiglu_nograd(x: torch.Tensor, w: torch.Tensor, cw: torch.Tensor, cb: torch.Tensor) -> torch.Tensor:
     """The same block outside autograd (GameURM's no-grad truncated loops, game.py:1437-1443): the
-    inference epilogue g2048_urm_linear_swiglu, which writes only act (no gu for a backward that
-    never comes: 368 instead of 848 MB per call at 65 536 boards) and keeps the projection in fp32
-    into the SwiGLU-conv epilogue (one bf16 rounding fewer than the training kernel)."""
+    training kernel's epilogue with no gu stored (g2048_urm_linear_swiglu_train, gu = NULL: act only,
+    368 instead of 848 MB per call at 65 536 boards), so the hidden state handed to the gradient loops
+    follows autocast's rounding points (gu rounded to bf16 before SwiGLU) and equals the training
+    kernel's bit for bit (round 4; round 3 kept the projection in fp32 into the epilogue)."""
     xb = x.to(torch.bfloat16).contiguous()
     wb = w.detach().to(torch.bfloat16).contiguous()
     cwf = cw.detach().to(torch.float32, copy=True).contiguous()
     cbf = cb.detach().to(torch.float32, copy=True).contiguous()
     act = torch.empty(xb.shape[0], w.shape[0] // 2, dtype=torch.bfloat16, device=x.device)
-    L.urm_linear_swiglu(xb, wb, cwf, cbf, act)
+    L.urm_linear_swiglu_train(xb, wb, cwf, cbf, None, act)
     return act
 
 

@@ -161,6 +161,10 @@ int g2048_urm_pool_heads(g2048_stream_t stream, const float *x, const float *wa,
 int g2048_urm_linear_supported(int32_t epilogue, int32_t k, int32_t n, int32_t inter);
 int g2048_urm_linear(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, uint16_t *out, int64_t rows,
                      int32_t k, int32_t n);
+/* g2048_urm_linear with an fp32 bias [n] added to the fp32 accumulator before the one bf16 rounding
+ * (autocast's biased Linear: bf16 operands and bias, one rounding of x W^T + b; bias 16-byte aligned). */
+int g2048_urm_linear_bias(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *bias, uint16_t *out,
+                          int64_t rows, int32_t k, int32_t n);
 int g2048_urm_linear_rms(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, float *x, const float *emb,
                          uint16_t *xb, int64_t rows, int32_t k, int32_t h, float eps);
 int g2048_urm_linear_swiglu(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *conv_w,
@@ -171,10 +175,20 @@ int g2048_urm_linear_swiglu(g2048_stream_t stream, const uint16_t *in, const uin
  * input) and computes act from those bf16 values with g2048_urm_swiglu_conv_fwd's arithmetic, so the
  * result equals gate_up Linear (autocast bf16) + g2048_urm_swiglu_conv_fwd up to the GEMM's fp32
  * summation order.  in bf16 [rows, h], w bf16 [2 inter, h], conv_w fp32 [inter][2], conv_b [inter];
- * inter % 8 == 0 and gu / act 16-byte aligned (8 features per lane per store). */
+ * inter % 8 == 0 and gu / act 16-byte aligned (8 features per lane per store).  gu may be NULL (round
+ * 4: the no-grad truncated loops, act with the training arithmetic and nothing else stored). */
 int g2048_urm_linear_swiglu_train(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *conv_w,
                                   const float *conv_b, uint16_t *gu, uint16_t *act, int64_t rows, int32_t h,
                                   int32_t inter);
+
+/* Training variant of g2048_urm_linear_rms (epilogue 4 of g2048_urm_linear_supported) for the autograd
+ * LinResRMSFn -- o_proj / down_proj + residual + post-norm of GameURMBlock (game.py:1346-1350) under bf16
+ * autocast: a = bf16(in W^T) (the projection's autocast output), s = h + a, out = s rsqrt(mean(s^2) +
+ * eps) -> out fp32 [rows, n], outb bf16 copy (optional, the next projection's operand), rstd fp32
+ * [rows] (the backward's g2048_urm_rms_res_bwd2 input); h is read only.  Replaces g2048_urm_linear +
+ * g2048_urm_rms_res_fwd2 (the projection output's HBM round trip).  h / out 16-byte aligned. */
+int g2048_urm_linear_res_rms(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *h, float *out,
+                             uint16_t *outb, float *rstd, int64_t rows, int32_t k, int32_t n, float eps);
 
 /* The whole forward in one persistent kernel (the default GameURMConfig: hidden 64, 4 heads,
  * inter 120, conv kernel 2, 1 or 2 layers, any loop count): obs [n, 48] (fp32 / bf16) -> logits

@@ -1,0 +1,38 @@
+"""torch.profiler census of the GameURM training iteration's torch-side ops (eager, no graph): which
+aten ops launch the small elementwise / reduce / copy kernels between the device Functions.
+    python tools/prof_urm_ops.py [envs] [horizon]"""
+import sys
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT), str(ROOT / "2048-ppo_amd")]
+
+
+def main():
+    from torch.profiler import ProfilerActivity, profile
+    from g2048.trainer import TrainConfig, VecTrainer
+    envs = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    T = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+    dev = torch.device("cuda", 0)
+    cfg = TrainConfig(steps=1000, lr=1e-3, critic_lr=1e-4, gamma=0.99, entropy=0.02, critic=0.2, episodes=envs,
+                      batch_size=65536, hidden=64, model_type="urm", points=0.1, mono=1.0, rtg_beta=0.99,
+                      warmup_steps=10, horizon=T, seed=0x2048, graph=False, amp=True)
+    tr = VecTrainer(cfg, dev)
+    tr.train_step(0)
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        tr.train_step(1)
+        torch.cuda.synchronize()
+    ka = prof.key_averages()
+    rows = sorted(ka, key=lambda e: -e.count)
+    print(f"{'op':60s} {'count':>6s} {'dev_us':>10s}")
+    for e in rows[:70]:
+        if e.key.startswith("aten::") or "Function" in e.key or "Backward" in e.key:
+            print(f"{e.key[:60]:60s} {e.count:6d} {e.device_time_total:10.0f}")
+    print(ka.table(sort_by="device_time_total", row_limit=45, max_name_column_width=70))
+
+
+if __name__ == "__main__":
+    main()
