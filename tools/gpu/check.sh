@@ -1,0 +1,60 @@
+#!/bin/bash
+# GPU box recipes behind the committed profiles (one gpurun call each; every GPU step has its own
+# time limit, the chain stops at the first failure or fault):
+#   TAG=r04x bash tools/gpu/check.sh env    env parity tests, the env bench line, trace + FETCH /
+#                                           WRITE / SQ passes of the rollout leg (-> pmc_env_rollout.json)
+#   TAG=r04x bash tools/gpu/check.sh fused  GameMLP update: fused tests, train-loop trace, SQ passes of
+#                                           tools/time_fused.py
+#   TAG=r04x bash tools/gpu/check.sh urm    GameURM: tests, bench leg, kernel trace, torch-op census,
+#                                           SQ passes of the one-launch forward
+#   TAG=r04x bash tools/gpu/check.sh full   every GPU test, smoke, the default bench line
+cd "${GRAFT_REPO_ROOT:-.}"
+TAG=${TAG:-check}
+O=gpurun_out/$TAG; mkdir -p $O
+export TMPDIR=/tmp
+fatal() { case $1 in 124|134|137|139) echo "FATAL rc=$1 in $2"; exit $1;; esac; }
+run_tests() {  # run_tests <log> <timeout> <pytest args...>
+  local log=$1 lim=$2; shift 2
+  timeout -k 10 $lim python -u -m pytest -m gpu -q --timeout 240 --timeout-method thread "$@" > $log 2>&1
+  local rc=$?; echo "tests rc=$rc"; tail -2 $log; grep -E "^FAILED|^ERROR" $log | head -20; fatal $rc tests
+  [ $rc -eq 0 ] || exit 1
+}
+case "$1" in
+env)
+  run_tests $O/tests.log 300 tests/test_gpu_env.py tests/test_gpu_train.py
+  timeout -k 10 300 python3 bench.py --cpu-seconds 0 --urm-steps 0 --train-iters 0 --single-steps 0 --sweep '' > $O/bench_env.log 2>&1
+  rc=$?; echo "bench rc=$rc"; fatal $rc bench
+  TAG=$TAG ARGS="--steps 20 --warmup 3 --cpu-seconds 0 --train-iters 0 --urm-steps 0 --single-steps 0 --sweep=" \
+    PMC_ARGS="--steps 4 --warmup 1 --cpu-seconds 0 --single-steps 0 --train-iters 0 --urm-steps 0 --sweep=" \
+    bash tools/profile.sh > $O/prof.log 2>&1
+  rc=$?; echo "prof rc=$rc"; tail -6 $O/prof.log; fatal $rc prof
+  python3 tools/summarize_profile.py gpurun_out/prof_$TAG $O/summary > /dev/null 2>&1
+  python3 -c "import json; d=json.load(open('$O/summary/pmc_env_rollout.json')); print({k: d[k] for k in ('valu_per_wave_step', 'lds_per_wave_step', 'hbm_bytes_per_env_step')})"
+  ;;
+fused)
+  run_tests $O/tests.log 400 tests/test_gpu_ppo_fused.py
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/trace -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --urm-steps 0 --single-steps 0 --sweep '' > $O/trace.log 2>&1
+  rc=$?; echo "trace rc=$rc"; fatal $rc trace
+  TAG=${TAG}_fused bash tools/pmc_kernel.sh python3 tools/time_fused.py 65536 > $O/pmc.log 2>&1
+  echo "pmc rc=$?"; python3 tools/pmc_table.py gpurun_out/pmck_${TAG}_fused mlp_ 2>&1 | head -60
+  ;;
+urm)
+  run_tests $O/tests.log 400 tests/test_gpu_urm.py
+  timeout -k 10 300 python3 bench.py --cpu-seconds 0 --train-iters 0 --urm-steps 16 --urm-iters 3 --single-steps 0 --sweep '' > $O/bench_urm.log 2>&1
+  rc=$?; echo "bench rc=$rc"; fatal $rc bench
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/urm -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --train-iters 0 --urm-steps 16 --urm-iters 1 --single-steps 0 --sweep '' > $O/urm_trace.log 2>&1
+  rc=$?; echo "urm trace rc=$rc"; fatal $rc urm
+  timeout -k 10 400 python3 tools/prof_urm_ops.py 65536 16 > $O/prof_ops.log 2>&1
+  echo "census rc=$?"
+  TAG=${TAG}_urmfwd bash tools/pmc_kernel.sh python3 tools/time_urm.py 65536 64 3 > $O/pmc.log 2>&1
+  echo "pmc rc=$?"; python3 tools/pmc_table.py gpurun_out/pmck_${TAG}_urmfwd urm_forward 2>&1 | head -30
+  ;;
+full)
+  run_tests $O/tests.log 700 tests
+  timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+  rc=$?; echo "smoke rc=$rc"; tail -1 $O/smoke.log; fatal $rc smoke
+  timeout -k 10 600 python3 bench.py > $O/bench.log 2>&1
+  rc=$?; echo "bench rc=$rc"; fatal $rc bench
+  ;;
+*) echo "usage: TAG=... bash tools/gpu/check.sh env|fused|urm|full"; exit 2 ;;
+esac
