@@ -62,8 +62,9 @@ constexpr uint32_t kFreshBoardBase = 137u * 1024u;                          // 1
 constexpr uint32_t kFreshStatBase = kFreshBoardBase + lut::kFreshEntries * 16u;  // 4 KiB of stats
 constexpr uint32_t kRolloutLdsWords = (kFreshStatBase + 4096u) / 4u;         // 159 744 B
 static_assert(kRowLds + lut::kRowEntries * 4u <= kFreshBoardBase, "kRow12 below kFresh");
-static_assert(kRowLds + 4u * 28276u <= kRolloutLdsWords * 4u && 2u * 28276u <= kRowLds + lut::kRowEntries * 4u,
-              "masked table reads stay inside the allocation");
+static_assert(kRowLds + 4u * 28276u <= kRolloutLdsWords * 4u, "masked kRow12 reads stay inside the allocation");
+// kLine12 reads take unmasked digits (line12_addrs): exponents <= 17 and the spawn's + 2 x 2 x 12^3
+static_assert(2u * 17u * 1885u + 2u * 2u * 1728u + 2u <= kRolloutLdsWords * 4u, "kLine12 reads stay inside the allocation");
 static_assert(2u * (lut::kRowEntries - 1u) < 65536u, "kLine12 byte addresses fit 16 bits");
 
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
@@ -73,10 +74,13 @@ __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cas
 // kRowLds + 4 (c0 + 12 c1 + 144 c2 + 1728 c3) as two packed-u16 dot products.  Bytes are masked
 // to 4 bits so any row (even one holding exponents >= 12, whose lane takes the compute path)
 // addresses inside the LDS allocation (< kRowLds + 15 * 1885 * 4 bytes).
+// kSmall (every exponent <= 10): the digits need no mask, so each pair is one byte-select v_perm
+template <bool kSmall = false>
 __device__ __forceinline__ uint32_t row12_addr(uint32_t x) {
     const u16x2 k02 = {4, 576}, k13 = {48, 6912};
-    return __builtin_amdgcn_udot2(as_u16x2((x >> 8) & 0x000F000Fu), k13,
-                                  __builtin_amdgcn_udot2(as_u16x2(x & 0x000F000Fu), k02, kRowLds, false), false);
+    const uint32_t a = kSmall ? __builtin_amdgcn_perm(0u, x, 0x0C020C00u) : x & 0x000F000Fu;         // cells 0, 2
+    const uint32_t b = kSmall ? __builtin_amdgcn_perm(0u, x, 0x0C030C01u) : (x >> 8) & 0x000F000Fu;  // cells 1, 3
+    return __builtin_amdgcn_udot2(as_u16x2(b), k13, __builtin_amdgcn_udot2(as_u16x2(a), k02, kRowLds, false), false);
 }
 __device__ __forceinline__ uint32_t lds_word(const uint32_t *tab, uint32_t addr) {
     return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(tab) + addr);
@@ -86,14 +90,17 @@ __device__ __forceinline__ uint32_t lds_word(const uint32_t *tab, uint32_t addr)
 // (i, 2), B_i = cells (i, 1) and (i, 3) as u16 halves.  Rows: two packed-u16 dot products each.
 // Columns: column pairs (0, 2) and (1, 3) at once as packed-u16 multiply-adds over the rows,
 // 2 (cell(0, j) + 12 cell(1, j) + 144 cell(2, j) + 1728 cell(3, j)) < 2^16 per half -- no transpose.
+// The digit pairs are the bytes themselves (one v_perm each, no 4-bit mask): a board of the SWAR
+// fallback (exponents up to 17) gives indices up to 2 x 17 x 1885 = 64 090 bytes, inside the LDS
+// allocation (its reads are discarded), and no u16 sum below overflows.
 __device__ __forceinline__ void line12_addrs(const uint4 &b, uint32_t (&ra)[4], uint32_t (&ca)[4]) {
     const u16x2 k02 = {2, 288}, k13 = {24, 3456};
     const uint32_t w[4] = {b.x, b.y, b.z, b.w};
     u16x2 A[4], B[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        A[i] = as_u16x2(w[i] & 0x000F000Fu);
-        B[i] = as_u16x2((w[i] >> 8) & 0x000F000Fu);
+        A[i] = as_u16x2(__builtin_amdgcn_perm(0u, w[i], 0x0C020C00u));
+        B[i] = as_u16x2(__builtin_amdgcn_perm(0u, w[i], 0x0C030C01u));
         ra[i] = __builtin_amdgcn_udot2(B[i], k13, __builtin_amdgcn_udot2(A[i], k02, 0u, false), false);
     }
     const u16x2 c02 = A[0] * (u16x2){2, 2} + A[1] * (u16x2){24, 24} + A[2] * (u16x2){288, 288} + A[3] * (u16x2){3456, 3456};
@@ -259,9 +266,10 @@ struct RolloutLane {
 // read once per pair right after the draw is known, long before a step can need them)
 __device__ __forceinline__ void fresh_prep(RolloutLane &s, const uint32_t *__restrict__ tab) {
     const uint32_t a = s.D.z, bw = s.D.w;
-    const uint32_t k2 = __umulhi(bw, 15u);
+    const uint64_t pb = (uint64_t)bw * 15u;  // one v_mad_u64_u32: k2 and the low word
+    const uint32_t k2 = (uint32_t)(pb >> 32);
     const uint32_t i = 60u * (a >> 28) + 4u * k2 + ((a << 4) >= kTwoThreshold ? 2u : 0u) +
-                       (bw * 15u >= kTwoThreshold ? 1u : 0u);
+                       ((uint32_t)pb >= kTwoThreshold ? 1u : 0u);
     const char *t = reinterpret_cast<const char *>(tab);
     s.fb = *reinterpret_cast<const uint4 *>(t + kFreshBoardBase + 16u * i);
     const uint32_t st = *reinterpret_cast<const uint32_t *>(t + kFreshStatBase + 4u * i);
@@ -301,8 +309,8 @@ __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__r
     const bool vert = a < 2u, rev = (a & 1u) != 0u;  // DOWN / RIGHT: byte-reversed rows
     const uint32_t rsel = rev ? 0x00010203u : 0x03020100u, usel = rev ? kUnpackRevSel : kUnpackSel;
     uint4 w = perm4(sel4(vert, transpose(s.b), s.b), rsel);
-    uint32_t e0 = lds_word(tab, row12_addr(w.x)), e1 = lds_word(tab, row12_addr(w.y));
-    uint32_t e2 = lds_word(tab, row12_addr(w.z)), e3 = lds_word(tab, row12_addr(w.w));
+    uint32_t e0 = lds_word(tab, row12_addr<kSmall>(w.x)), e1 = lds_word(tab, row12_addr<kSmall>(w.y));
+    uint32_t e2 = lds_word(tab, row12_addr<kSmall>(w.z)), e3 = lds_word(tab, row12_addr<kSmall>(w.w));
     asm volatile("" : "+v"(s.ph.c0), "+v"(s.ph.c1), "+v"(s.ph.c2), "+v"(s.ph.c3)::"memory");
     if constexpr (kOdd) philox_rounds<5, 10>(s.ph);
     else philox_rounds<0, 5>(s.ph);

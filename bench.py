@@ -344,7 +344,7 @@ def _c_chunk(args):
     return cnt
 
 
-PMC_PROFILE = ROOT / "profiles" / "r04l"
+PMC_PROFILE = ROOT / "profiles" / "r04u"
 CPU_RATIO = ROOT / "profiles" / "r02" / "cpu_ref_ratio.json"
 
 
