@@ -971,6 +971,312 @@ __global__ __launch_bounds__(kBlock) void episode_scan_kernel(const int32_t *__r
     run_max[e] = rm;
 }
 
+// ------------------------------------------------------------------ rollout statistics ------
+// The rollout half of the train step's metrics (the reward / advantage / return summaries and
+// compute_batch_stats' finished-game statistics, train.py:1040-1120 and :1700-1760) in two launches
+// instead of ~60 torch ops: rollout_stats_kernel walks each env's T steps once (the episode scan
+// of episode_scan_kernel plus every row statistic, float64 per-thread sums, a fixed-order block
+// reduction into per-block partials; finished scores are appended to a key list at a range each
+// block reserves with one atomic), rollout_stats_final_kernel sums the partials in block order and finds the lower median
+// of the finished scores by a three-pass radix select.  Deterministic: the atomics only decide
+// the order of the key list, which the selection does not see.
+namespace rstat {
+enum : int { N, R, R2, RZ, A, A2, GN, GN2, GR, GR2, V, V2, G0, G0N, CNT, SSUM, T9, T10, T11, AMIN, AMAX, GNMIN,
+             GNMAX, SMAX, K };
+constexpr size_t kHead = 256;  // the key counter, then the partials, then the keys
+__device__ __forceinline__ bool is_min(int j) { return j == AMIN || j == GNMIN; }
+__device__ __forceinline__ bool is_max(int j) { return j == AMAX || j == GNMAX || j == SMAX; }
+__device__ __forceinline__ double combine(int j, double a, double b) {
+    return is_min(j) ? fmin(a, b) : is_max(j) ? fmax(a, b) : a + b;
+}
+}  // namespace rstat
+
+// kEpi: episodic mode.  The walk is latency-bound at one wave per SIMD (n / 64 waves), so the
+// loads of kChunk steps are issued before any of them is used.
+template <bool kEpi>
+__global__ __launch_bounds__(kBlock) void rollout_stats_kernel(
+    const int32_t *__restrict__ points, const uint32_t *__restrict__ pot, const uint8_t *__restrict__ sf,
+    const float *__restrict__ value, const float *__restrict__ g_raw, const float *__restrict__ g_norm,
+    const float *__restrict__ adv, const uint4 *__restrict__ boards, const int8_t *__restrict__ max_tile, int64_t T,
+    int64_t n, float wp, float wm, float we, float gamma, int64_t *__restrict__ run_score,
+    int32_t *__restrict__ run_max, uint32_t *__restrict__ counter, double *__restrict__ part,
+    uint32_t *__restrict__ keys) {
+    using namespace rstat;
+    constexpr int kChunk = 8;
+    const int64_t e0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool act = e0 < n;
+    const int64_t e = act ? e0 : n - 1;  // every lane walks (the ballots), only act lanes count
+    double acc[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) acc[j] = is_min(j) ? INFINITY : is_max(j) ? -INFINITY : 0.0;
+    acc[SMAX] = -1.0;
+    const int64_t rsc0 = kEpi ? 0 : run_score[e];
+    int64_t rsc = rsc0;
+    int32_t rmx = kEpi ? 0 : run_max[e];
+    uint32_t prev = 0;
+    for (int64_t t0 = 0; t0 < T; t0 += kChunk) {
+        uint32_t fl[kChunk], pw[kChunk], bm[kChunk];
+        int32_t pt[kChunk], mt[kChunk];
+        float av[kChunk], gnv[kChunk], grv[kChunk], vv[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; u++) {
+            const int64_t k = min(t0 + u, T - 1) * n + e;
+            fl[u] = sf[k];
+            pw[u] = pot[k];
+            pt[u] = points[k];
+            av[u] = adv[k];
+            gnv[u] = g_norm[k];
+            grv[u] = g_raw[k];
+            vv[u] = value[k];
+            if (!kEpi) {
+                const uint4 b = boards[k];
+                uint32_t m = bytemax(bytemax(b.x, b.y), bytemax(b.z, b.w));
+                m = bytemax(m, m >> 8);
+                bm[u] = bytemax(m, m >> 16) & 0xFFu;
+                mt[u] = max_tile[k];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kChunk; u++) {
+            if (t0 + u >= T) break;  // wave-uniform
+            const uint32_t f = fl[u];
+            const bool inactive = (f & FLAG_INACTIVE) != 0;
+            const bool start = kEpi ? t0 + u == 0 : (prev & FLAG_RESET) != 0;
+            prev = f;
+            if (act && start) {
+                acc[G0] += (double)grv[u];
+                acc[G0N] += 1.0;
+            }
+            if (act && (!kEpi || !inactive)) {
+                // the metric's reward in float32, operation for operation as the torch expression
+                // points * w_p + w_m * (gamma * pot1 * (1 - done) - pot0) + w_e * (gamma * pot3 * (1 - done) - pot2)
+                const uint32_t q = pw[u];
+                const float p0 = (float)(int8_t)(q & 0xFFu), p1 = (float)(int8_t)((q >> 8) & 0xFFu);
+                const float p2 = (float)(int8_t)((q >> 16) & 0xFFu), p3 = (float)(int8_t)(q >> 24);
+                const float nd = (f & FLAG_DONE) ? 0.0f : 1.0f;
+                const float x1 = __fsub_rn(__fmul_rn(__fmul_rn(gamma, p1), nd), p0);
+                const float x2 = __fsub_rn(__fmul_rn(__fmul_rn(gamma, p3), nd), p2);
+                const float r = __fadd_rn(__fadd_rn(__fmul_rn((float)pt[u], wp), __fmul_rn(wm, x1)), __fmul_rn(we, x2));
+                const double rd = r, a = av[u], gn = gnv[u], gr = grv[u], v = vv[u];
+                acc[N] += 1.0;
+                acc[R] += rd;
+                acc[R2] += rd * rd;
+                acc[RZ] += r == 0.0f ? 1.0 : 0.0;
+                acc[A] += a;
+                acc[A2] += a * a;
+                acc[AMIN] = fmin(acc[AMIN], a);
+                acc[AMAX] = fmax(acc[AMAX], a);
+                acc[GN] += gn;
+                acc[GN2] += gn * gn;
+                acc[GNMIN] = fmin(acc[GNMIN], gn);
+                acc[GNMAX] = fmax(acc[GNMAX], gn);
+                acc[GR] += gr;
+                acc[GR2] += gr * gr;
+                acc[V] += v;
+                acc[V2] += v * v;
+            }
+            if (kEpi) {
+                if (!inactive) rsc += pt[u];
+                continue;
+            }
+            // fixed horizon: episode_scan_kernel's running score / max tile of the current game
+            rsc += pt[u];
+            rmx = max(rmx, max((int32_t)bm[u], mt[u]));
+            const bool ends = (f & FLAG_DONE) && !inactive;
+            if (act && ends) {
+                acc[CNT] += 1.0;
+                acc[SSUM] += (double)rsc;
+                acc[SMAX] = fmax(acc[SMAX], (double)(int32_t)rsc);
+                acc[T9] += rmx >= 9 ? 1.0 : 0.0;
+                acc[T10] += rmx >= 10 ? 1.0 : 0.0;
+                acc[T11] += rmx >= 11 ? 1.0 : 0.0;
+            }
+            if (ends) {
+                rsc = 0;
+                rmx = 0;
+            }
+        }
+    }
+    if (kEpi) {  // every env's game is finished: its score and the max tile of its final board
+        const uint4 b = boards[T * n + e];
+        uint32_t m = bytemax(bytemax(b.x, b.y), bytemax(b.z, b.w));
+        m = bytemax(m, m >> 8);
+        m = bytemax(m, m >> 16);
+        const int32_t mx = (int32_t)(m & 0xFFu);
+        if (act) {
+            acc[CNT] = 1.0;
+            acc[SSUM] = (double)rsc;
+            acc[SMAX] = (double)(int32_t)rsc;
+            acc[T9] = mx >= 9 ? 1.0 : 0.0;
+            acc[T10] = mx >= 10 ? 1.0 : 0.0;
+            acc[T11] = mx >= 11 ? 1.0 : 0.0;
+        }
+    } else if (act) {
+        run_score[e] = rsc;
+        run_max[e] = rmx;
+    }
+    // the finished scores into keys[]: the block reserves its range with ONE atomic (a per-step
+    // atomic per wave serialises on the counter), lanes take block-exclusive-scan offsets, and the
+    // fixed-horizon walk is replayed over points / flags to emit its keys in place
+    __shared__ uint32_t wsum[kBlock / 64 + 1];
+    {
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        const uint32_t mine = act ? (uint32_t)acc[CNT] : 0u;
+        uint32_t incl = mine;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
+            for (int q = 0; q < kBlock / 64; q++) {
+                const uint32_t c = wsum[q];
+                wsum[q] = tot;
+                tot += c;
+            }
+            wsum[kBlock / 64] = tot ? atomicAdd(counter, tot) : 0u;
+        }
+        __syncthreads();
+        uint32_t at = wsum[kBlock / 64] + wsum[w] + incl - mine;
+        if (kEpi) {
+            if (act) keys[at] = (uint32_t)(int32_t)rsc;
+        } else if (mine) {
+            int64_t r2 = rsc0;
+            for (int64_t t0 = 0; t0 < T; t0 += kChunk) {
+                uint32_t fl[kChunk];
+                int32_t pt[kChunk];
+#pragma unroll
+                for (int u = 0; u < kChunk; u++) {
+                    const int64_t k = min(t0 + u, T - 1) * n + e;
+                    fl[u] = sf[k];
+                    pt[u] = points[k];
+                }
+#pragma unroll
+                for (int u = 0; u < kChunk; u++) {
+                    if (t0 + u >= T) break;
+                    r2 += pt[u];
+                    if ((fl[u] & FLAG_DONE) && !(fl[u] & FLAG_INACTIVE)) {
+                        keys[at++] = (uint32_t)(int32_t)r2;
+                        r2 = 0;
+                    }
+                }
+            }
+        }
+    }
+    // block reduction: wave butterflies, then the block's waves in order
+    __shared__ double red[kBlock / 64][K];
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+        double x = acc[j];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x = combine(j, x, __shfl_xor(x, o));
+        acc[j] = x;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0)
+#pragma unroll
+        for (int j = 0; j < K; j++) red[w][j] = acc[j];
+    __syncthreads();
+    if (threadIdx.x < K) {
+        const int j = threadIdx.x;
+        double x = red[0][j];
+        for (int q = 1; q < kBlock / 64; q++) x = combine(j, x, red[q][j]);
+        part[(int64_t)blockIdx.x * K + j] = x;
+    }
+}
+
+__global__ __launch_bounds__(1024) void rollout_stats_final_kernel(const double *__restrict__ part, int nb,
+                                                                   uint32_t *__restrict__ counter,
+                                                                   const uint32_t *__restrict__ keys,
+                                                                   float *__restrict__ out) {
+    using namespace rstat;
+    __shared__ double tot[K];
+    __shared__ uint32_t hist[2048];
+    __shared__ uint32_t sel[2];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int j = w; j < K; j += 16) {  // column j: lanes stride the blocks in order, then a butterfly
+        double x = is_min(j) ? INFINITY : is_max(j) ? -INFINITY : 0.0;
+        if (j == SMAX) x = -1.0;
+        for (int b = lane; b < nb; b += 64) x = combine(j, x, part[(int64_t)b * K + j]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x = combine(j, x, __shfl_xor(x, o));
+        if (lane == 0) tot[j] = x;
+    }
+    const uint32_t cnt = counter[0];
+    // lower median = the key of rank (cnt - 1) / 2: radix select, digits of at most 11 bits from the
+    // highest bit any key has set (the OR of the keys) down
+    __shared__ uint32_t kor;
+    if (tid == 0) kor = 0;
+    __syncthreads();
+    {
+        uint32_t o = 0;
+        for (uint32_t i = tid; i < cnt; i += 1024) o |= keys[i];
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) o |= __shfl_xor(o, d);
+        if (lane == 0 && o) atomicOr(&kor, o);
+    }
+    __syncthreads();
+    uint32_t prefix = 0, pmask = 0, rank = cnt > 0 ? (cnt - 1) / 2 : 0;
+    for (int hb = kor ? 32 - __clz((int)kor) : 0; hb > 0 && cnt > 0;) {
+        const int sh = hb > 11 ? hb - 11 : 0;
+        const uint32_t bm = (1u << (hb - sh)) - 1u;
+        for (int i = tid; i < 2048; i += 1024) hist[i] = 0;
+        __syncthreads();
+        for (uint32_t i = tid; i < cnt; i += 1024) {
+            const uint32_t key = keys[i];
+            if ((key & pmask) == prefix) atomicAdd(&hist[(key >> sh) & bm], 1u);
+        }
+        __syncthreads();
+        if (w == 0) {  // lane owns bins [32 lane, 32 lane + 32)
+            uint32_t s = 0;
+            for (int j = 0; j < 32; j++) s += hist[lane * 32 + j];
+            uint32_t incl = s;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            const uint32_t excl = incl - s;
+            if (excl <= rank && rank < incl) {
+                uint32_t c = excl;
+                for (int j = 0; j < 32; j++) {
+                    const uint32_t h = hist[lane * 32 + j];
+                    if (rank < c + h) {
+                        sel[0] = (uint32_t)(lane * 32 + j);
+                        sel[1] = rank - c;
+                        break;
+                    }
+                    c += h;
+                }
+            }
+        }
+        __syncthreads();
+        prefix |= sel[0] << sh;
+        pmask |= bm << sh;
+        rank = sel[1];
+        hb = sh;
+        __syncthreads();
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const double nr = tot[N], cf = fmax(tot[CNT], 1.0);
+        const double rm = tot[R] / nr, am = tot[A] / nr, gnm = tot[GN] / nr, grm = tot[GR] / nr, vm = tot[V] / nr;
+        const double o[23] = {
+            nr, rm, fmax(tot[R2] / nr - rm * rm, 0.0), tot[RZ] / nr * 100.0,
+            am, fmax(tot[A2] / nr - am * am, 0.0), sqrt(tot[A2]), tot[AMIN], tot[AMAX],
+            gnm, sqrt(fmax(tot[GN2] / nr - gnm * gnm, 0.0)), tot[GNMIN], tot[GNMAX],
+            sqrt(fmax(tot[GR2] / nr - grm * grm, 0.0)), sqrt(fmax(tot[V2] / nr - vm * vm, 0.0)),
+            tot[G0] / fmax(tot[G0N], 1.0),
+            tot[SSUM] / cf, cnt > 0 ? (double)(int32_t)prefix : -1.0, tot[SMAX],
+            tot[T9] / cf * 100.0, tot[T10] / cf * 100.0, tot[T11] / cf * 100.0, tot[CNT]};
+        for (int j = 0; j < 23; j++) out[j] = (float)o[j];
+        counter[0] = 0;  // every thread has read it (the barrier above): the workspace is left zeroed
+    }
+}
+
 inline int launch_status() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK : (int)e;
@@ -1343,6 +1649,42 @@ int g2048_episode_scan(g2048_stream_t stream, const int32_t *points, const int8_
     if (n == 0 || T == 0) return G2048_OK;
     hipLaunchKernelGGL(episode_scan_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, (hipStream_t)stream, points,
                        (const uint4 *)boards, max_tile, step_flags, T, n, run_score, run_max, scores, tiles);
+    return launch_status();
+}
+
+size_t g2048_rollout_stats_workspace_bytes(int64_t T, int64_t n) {
+    if (T < 1 || n < 1) return rstat::kHead;
+    return rstat::kHead + (size_t)blocks_for(n) * rstat::K * sizeof(double) + (size_t)T * (size_t)n * sizeof(uint32_t);
+}
+
+int g2048_rollout_stats(g2048_stream_t stream, const int32_t *points, const int8_t *pot, const uint8_t *step_flags,
+                        const float *value, const float *g_raw, const float *g_norm, const float *adv,
+                        const int8_t *boards, const int8_t *max_tile, int64_t T, int64_t n, int32_t episodic,
+                        const g2048_reward_cfg *cfg, int64_t *run_score, int32_t *run_max, void *workspace,
+                        size_t workspace_bytes, float *out) {
+    if (T < 1 || n < 1 || n > (int64_t)UINT32_MAX || T * n > (int64_t)UINT32_MAX || !points || !pot || !step_flags ||
+        !value || !g_raw || !g_norm || !adv || !boards || !cfg || !workspace || !out)
+        return G2048_EINVAL;
+    if (!episodic && (!max_tile || !run_score || !run_max)) return G2048_EINVAL;
+    if (!aligned16(boards) || ((uintptr_t)pot & 3u) || ((uintptr_t)workspace & 15u)) return G2048_EINVAL;
+    if (workspace_bytes < g2048_rollout_stats_workspace_bytes(T, n)) return G2048_EINVAL;
+    const unsigned nb = blocks_for(n);
+    char *ws = (char *)workspace;
+    uint32_t *counter = (uint32_t *)ws;
+    double *part = (double *)(ws + rstat::kHead);
+    uint32_t *keys = (uint32_t *)(ws + rstat::kHead + (size_t)nb * rstat::K * sizeof(double));
+    const hipStream_t s = (hipStream_t)stream;
+    const float wp = (float)cfg->w_points, wm = (float)cfg->w_mono, we = (float)cfg->w_empt, gm = (float)cfg->gamma;
+    if (episodic)
+        hipLaunchKernelGGL(rollout_stats_kernel<true>, dim3(nb), dim3(kBlock), 0, s, points, (const uint32_t *)pot,
+                           step_flags, value, g_raw, g_norm, adv, (const uint4 *)boards, max_tile, T, n, wp, wm, we, gm,
+                           run_score, run_max, counter, part, keys);
+    else
+        hipLaunchKernelGGL(rollout_stats_kernel<false>, dim3(nb), dim3(kBlock), 0, s, points, (const uint32_t *)pot,
+                           step_flags, value, g_raw, g_norm, adv, (const uint4 *)boards, max_tile, T, n, wp, wm, we, gm,
+                           run_score, run_max, counter, part, keys);
+    hipLaunchKernelGGL(rollout_stats_final_kernel, dim3(1), dim3(1024), 0, s, (const double *)part, (int)nb, counter,
+                       (const uint32_t *)keys, out);
     return launch_status();
 }
 

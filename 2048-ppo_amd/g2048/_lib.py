@@ -27,6 +27,7 @@ EXPORTED = (
     "g2048_preview_points", "g2048_legal_mask",
     "g2048_obs_encode", "g2048_info_deltas", "g2048_sample_actions", "g2048_rtg_prepare", "g2048_reward_rtg_workspace_bytes",
     "g2048_reward_rtg", "g2048_reward_rtg_ex", "g2048_rtg_finalize", "g2048_build_info", "g2048_episode_scan",
+    "g2048_rollout_stats_workspace_bytes", "g2048_rollout_stats",
     "g2048_augment_workspace_bytes", "g2048_augment",
     # include/g2048_ppo.h
     "g2048_obs_gather", "g2048_ln_act_fwd", "g2048_ln_act_bwd_partials", "g2048_ln_act_bwd",
@@ -220,6 +221,9 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_rtg_finalize": (ctypes.c_int, [vp, vp, vp, cp]),
         "g2048_build_info": (ctypes.c_char_p, []),
         "g2048_episode_scan": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp]),
+        "g2048_rollout_stats_workspace_bytes": (sz, [i64, i64]),
+        "g2048_rollout_stats": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32, cp, vp, vp, vp,
+                                               sz, vp]),
         "g2048_augment_workspace_bytes": (ctypes.c_size_t, [i64]),
         "g2048_augment": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, i64, u64, u64, vp, ctypes.c_size_t, vp]),
         "g2048_obs_gather": (ctypes.c_int, [vp, vp, vp, i64, vp]),
@@ -455,6 +459,31 @@ def episode_scan(points, boards, max_tile, step_flags, run_score, run_max, score
         _dev(max_tile, torch.int8, "max_tile"), _dev(step_flags, torch.uint8, "step_flags"), T, n,
         _dev(run_score, torch.int64, "run_score"), _dev(run_max, torch.int32, "run_max"),
         _dev(scores, torch.int64, "scores"), _dev(tiles, torch.int32, "tiles")), "g2048_episode_scan")
+
+
+ROLLOUT_STATS = 23  # g2048_rollout_stats' output vector
+
+
+def rollout_stats_workspace_bytes(T: int, n: int) -> int:
+    return int(load().g2048_rollout_stats_workspace_bytes(int(T), int(n)))
+
+
+def rollout_stats(points, pot, step_flags, value, g_raw, g_norm, adv, boards, max_tile, episodic, cfg,
+                  run_score, run_max, workspace, out):
+    """The rollout metrics vector out [23] float32 (include/g2048.h g2048_rollout_stats).  points /
+    step_flags / value / g_raw / g_norm / adv [T, n], pot [T, n, 4]; fixed horizon: boards [T, n, 16],
+    max_tile [T, n], run_score / run_max [n] carried; episodic: boards [T + 1, n, 16] (the final board
+    read), max_tile / run_* may be None.  cfg: RewardCfg.  workspace: a zero-filled uint8 tensor of
+    rollout_stats_workspace_bytes(T, n) bytes, left zeroed."""
+    T, n = points.shape[0], points.shape[1]
+    _check(load().g2048_rollout_stats(
+        _stream(points), _dev(points, torch.int32, "points"), _dev(pot, torch.int8, "pot"),
+        _dev(step_flags, torch.uint8, "step_flags"), _dev(value, torch.float32, "value"),
+        _dev(g_raw, torch.float32, "g_raw"), _dev(g_norm, torch.float32, "g_norm"), _dev(adv, torch.float32, "adv"),
+        _dev(boards, torch.int8, "boards"), _dev(max_tile, torch.int8, "max_tile"), T, n, 1 if episodic else 0,
+        ctypes.byref(cfg), _dev(run_score, torch.int64, "run_score"), _dev(run_max, torch.int32, "run_max"),
+        _dev(workspace, torch.uint8, "workspace"), workspace.numel(), _dev(out, torch.float32, "out")),
+        "g2048_rollout_stats")
 
 
 def augment_workspace_bytes(k: int) -> int:

@@ -387,65 +387,30 @@ class VecTrainer:
         return {key: v[:c] for key, v in pool.items()}, c - n
 
     # ------------------------------------------------------------------ metrics ---------------
-    def _episode_stats(self, T):
-        """(scores, max tile exponents, finished mask) of the games that end in this rollout, as dense
-        device tensors (no compaction, no host sync): g2048_episode_scan carries each env's running
-        score / max tile across rollouts in fixed-horizon mode."""
+    def _rollout_stats(self, T) -> torch.Tensor:
+        """The rollout half of the metrics as one device vector [23] (g2048_rollout_stats: reward /
+        advantage / return summaries and the finished games of compute_batch_stats, train.py:1040-1120,
+        in two launches, no host sync; fixed horizon carries each env's running score / max tile
+        across rollouts in run_score / run_maxexp)."""
         b = self.rollout.buf
-        sf = b.step_flags[:T]
+        need = L.rollout_stats_workspace_bytes(T, self.rollout.n)
+        if getattr(self, "_rs_ws", None) is None or self._rs_ws.numel() < need:
+            self._rs_ws = torch.zeros(need, dtype=torch.uint8, device=self.dev)  # the key counter starts at 0
+            self._rs_out = torch.empty(L.ROLLOUT_STATS, dtype=torch.float32, device=self.dev)
         if self.episodic:
-            pts = torch.where((sf & L.FLAG_INACTIVE) == 0, b.points[:T], 0).sum(0)
-            mx = b.boards[T].max(dim=1).values.to(torch.int32)
-            return pts, mx, torch.ones_like(pts, dtype=torch.bool)
-        if getattr(self, "_ep_scores", None) is None or self._ep_scores.shape[0] != T:
-            self._ep_scores = torch.empty(T, self.rollout.n, dtype=torch.int64, device=self.dev)
-            self._ep_tiles = torch.empty(T, self.rollout.n, dtype=torch.int32, device=self.dev)
-        L.episode_scan(b.points[:T], b.boards[:T], b.max_tile[:T], sf, self.run_score, self.run_maxexp,
-                       self._ep_scores, self._ep_tiles)
-        return self._ep_scores, self._ep_tiles, self._ep_scores >= 0
+            L.rollout_stats(b.points[:T], b.pot[:T], b.step_flags[:T], b.value[:T], b.g_raw[:T], b.g_norm[:T],
+                            b.adv[:T], b.boards[:T + 1], None, True, self.weights.cfg(), None, None, self._rs_ws,
+                            self._rs_out)
+        else:
+            L.rollout_stats(b.points[:T], b.pot[:T], b.step_flags[:T], b.value[:T], b.g_raw[:T], b.g_norm[:T],
+                            b.adv[:T], b.boards[:T], b.max_tile[:T], False, self.weights.cfg(), self.run_score,
+                            self.run_maxexp, self._rs_ws, self._rs_out)
+        return self._rs_out
 
     def _metrics(self, T, valid, ustats) -> dict:
-        b, w = self.rollout.buf, self.weights
-        sf = b.step_flags[:T]
-        done = ((sf & L.FLAG_DONE) != 0).float()
-        pot = b.pot[:T].float()
-        r = (b.points[:T].float() * w.points + w.mono * (w.gamma * pot[..., 1] * (1 - done) - pot[..., 0])
-             + w.emptiness * (w.gamma * pot[..., 3] * (1 - done) - pot[..., 2]))
-        fields = [r, b.adv[:T], b.g_norm[:T], b.g_raw[:T], b.value[:T]]
-        if valid is not None:
-            fields = [f.reshape(-1).index_select(0, valid) for f in fields]
-        else:
-            fields = [f.reshape(-1) for f in fields]
-        r, a, gn, gr, v = fields
-        starts = torch.zeros_like(sf, dtype=torch.bool)
-        if self.episodic:
-            starts[0] = True
-        else:
-            starts[1:] = (sf[:-1] & L.FLAG_RESET) != 0
-        g0 = (b.g_raw[:T] * starts).sum() / starts.sum().clamp(min=1)  # mean return of episode starts
-        scores, tiles, fin = self._episode_stats(T)
-        dev = self.dev
-        s_flat = torch.where(fin, scores, -1).reshape(-1).to(torch.int32)
-        cnt = fin.sum()
-        cntf = cnt.float().clamp(min=1.0)
-        # median without compaction: finished scores sort to the top of the -1 filler
-        srt = torch.sort(s_flat).values
-        med_idx = (s_flat.numel() - cnt + (cnt - 1).clamp(min=0) // 2).clamp(max=s_flat.numel() - 1)
-        vec = torch.stack([
-            torch.tensor(float(r.numel()), device=dev), r.mean(), r.var(unbiased=False), (r == 0).float().mean() * 100,
-            a.mean(), a.var(unbiased=False), a.pow(2).sum().sqrt(), a.min(), a.max(),
-            gn.mean(), gn.std(unbiased=False), gn.min(), gn.max(), gr.std(unbiased=False), v.std(unbiased=False),
-            g0,
-            torch.where(fin, scores, 0).sum().float() / cntf,
-            srt[med_idx].float(),
-            s_flat.max().float(),
-            (fin & (tiles >= 9)).sum().float() / cntf * 100,
-            (fin & (tiles >= 10)).sum().float() / cntf * 100,
-            (fin & (tiles >= 11)).sum().float() / cntf * 100,
-            cnt.float(),
-            *[ustats[k] for k in ("loss", "policy_loss", "entropy_loss", "value_loss", "grad_norm", "entropy",
-                                  "kl_total", "kl_average", "kl_max")],
-        ]).tolist()  # the one host synchronisation of the train step
+        vec = torch.cat([self._rollout_stats(T), torch.stack([ustats[k] for k in (
+            "loss", "policy_loss", "entropy_loss", "value_loss", "grad_norm", "entropy", "kl_total", "kl_average",
+            "kl_max")])]).tolist()  # the one host synchronisation of the train step
         (n, rm, rv, zr, am, av, al2, amin, amax, gnm, gns, gnmin, gnmax, grs, vs, g0m, avg_s, med_s, max_s, p512,
          p1024, p2048, n_eps, loss, pl, el, vl, gnorm, ent, klt, kla, klm) = vec
         if n_eps > 0:

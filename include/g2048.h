@@ -192,6 +192,28 @@ int g2048_episode_scan(g2048_stream_t stream, const int32_t *points, const int8_
                        const uint8_t *step_flags, int64_t T, int64_t n, int64_t *run_score, int32_t *run_max,
                        int64_t *scores, int32_t *tiles);
 
+/* The rollout half of a train step's metrics (train.py:1700-1760's reward / advantage / return
+ * summaries and compute_batch_stats' finished games, train.py:1040-1120) in two launches, no host
+ * sync.  out[23] (float32) = {rows, reward mean, reward var, zero-reward %, adv mean, adv var,
+ * adv L2, adv min, adv max, G_norm mean, G_norm std, G_norm min, G_norm max, G_raw std, value
+ * std, mean G_raw of episode starts, finished-score mean, lower median (-1: none), max (-1: none),
+ * % finished with max tile >= 512 / 1024 / 2048, finished count}; variances are population ones,
+ * sums in float64.  The reward is the float32 metric r = w_p points + w_m (gamma pot1 (1-done) -
+ * pot0) + w_e (gamma pot3 (1-done) - pot2) over pot [T][n][4] int8 (4-B aligned).
+ * episodic = 0 (fixed horizon): every row counts; the finished games are episode_scan's (run_score
+ * / run_max carried, boards [T][n][16] = the board before each step, max_tile [T][n]); episode
+ * starts are the steps after a FLAG_RESET.  episodic = 1: rows flagged INACTIVE are skipped; each
+ * env is one finished game (its active points, the max tile of boards[T], boards [T+1][n][16]);
+ * starts are t = 0; max_tile / run_* unused.  workspace: g2048_rollout_stats_workspace_bytes(T, n)
+ * bytes, 16-B aligned; its first 4 bytes (the finished-key counter) must be zero on entry, and
+ * every call leaves them zero (zero-fill the workspace once when allocating it). */
+size_t g2048_rollout_stats_workspace_bytes(int64_t T, int64_t n);
+int g2048_rollout_stats(g2048_stream_t stream, const int32_t *points, const int8_t *pot, const uint8_t *step_flags,
+                        const float *value, const float *g_raw, const float *g_norm, const float *adv,
+                        const int8_t *boards, const int8_t *max_tile, int64_t T, int64_t n, int32_t episodic,
+                        const g2048_reward_cfg *cfg, int64_t *run_score, int32_t *run_max, void *workspace,
+                        size_t workspace_bytes, float *out);
+
 /* EMA moment update with the batch statistics (train.py:898-901); advances rtg_step. */
 int g2048_rtg_finalize(g2048_stream_t stream, double *state, const double *partials,
                        const g2048_reward_cfg *cfg);

@@ -388,6 +388,103 @@ def test_episode_scan_matches_loop(dev):
         assert torch.equal(rs, rs2) and torch.equal(rm, rm2)
 
 
+def _rollout_stats_torch(pts, pot, sf, value, g_raw, g_norm, adv, boards, mt, episodic, w, rs, rm):
+    """The train step's rollout metrics as the torch expression the trainer used before
+    g2048_rollout_stats (float32 reductions; the same 23 entries).  rs / rm: carried state (fixed
+    horizon), advanced in place."""
+    T, n = pts.shape
+    done = ((sf & 0x80) != 0).float()
+    p = pot.float()
+    r = (pts.float() * w.points + w.mono * (w.gamma * p[..., 1] * (1 - done) - p[..., 0])
+         + w.emptiness * (w.gamma * p[..., 3] * (1 - done) - p[..., 2]))
+    fields = [r, adv, g_norm, g_raw, value]
+    if episodic:
+        valid = torch.nonzero(((sf & 0x40) == 0).reshape(-1)).squeeze(1)
+        fields = [f.reshape(-1).index_select(0, valid) for f in fields]
+    else:
+        fields = [f.reshape(-1) for f in fields]
+    r, a, gn, gr, v = fields
+    starts = torch.zeros_like(sf, dtype=torch.bool)
+    if episodic:
+        starts[0] = True
+    else:
+        starts[1:] = (sf[:-1] & 0x20) != 0
+    g0 = (g_raw * starts).sum() / starts.sum().clamp(min=1)
+    if episodic:
+        scores = torch.where((sf & 0x40) == 0, pts, 0).sum(0)
+        tiles = boards[T].max(dim=1).values.to(torch.int32)
+        fin = torch.ones_like(scores, dtype=torch.bool)
+    else:
+        sc = torch.empty(T, n, dtype=torch.int64, device=pts.device)
+        ti = torch.empty(T, n, dtype=torch.int32, device=pts.device)
+        from g2048 import _lib as L
+        L.episode_scan(pts, boards, mt, sf, rs, rm, sc, ti)
+        scores, tiles, fin = sc, ti, sc >= 0
+    s_flat = torch.where(fin, scores, -1).reshape(-1).to(torch.int32)
+    cnt = fin.sum()
+    cntf = cnt.float().clamp(min=1.0)
+    srt = torch.sort(s_flat).values
+    med_idx = (s_flat.numel() - cnt + (cnt - 1).clamp(min=0) // 2).clamp(max=s_flat.numel() - 1)
+    return torch.stack([
+        torch.tensor(float(r.numel()), device=pts.device), r.mean(), r.var(unbiased=False),
+        (r == 0).float().mean() * 100, a.mean(), a.var(unbiased=False), a.pow(2).sum().sqrt(), a.min(), a.max(),
+        gn.mean(), gn.std(unbiased=False), gn.min(), gn.max(), gr.std(unbiased=False), v.std(unbiased=False), g0,
+        torch.where(fin, scores, 0).sum().float() / cntf, srt[med_idx].float(), s_flat.max().float(),
+        (fin & (tiles >= 9)).sum().float() / cntf * 100, (fin & (tiles >= 10)).sum().float() / cntf * 100,
+        (fin & (tiles >= 11)).sum().float() / cntf * 100, cnt.float()]).double().cpu().numpy()
+
+
+@pytest.mark.parametrize("episodic,T,n,p_done", [(False, 64, 5000, 0.03), (False, 7, 300, 0.0), (False, 33, 1000, 0.4),
+                                                 (True, 50, 2000, 0.02)])
+def test_rollout_stats_kernel_matches_torch(dev, episodic, T, n, p_done):
+    """g2048_rollout_stats (two launches) vs the torch expression it replaced: counts, the integer
+    score statistics (median by radix select, max, finished mean) and the tile percentages exactly,
+    every float moment within 1e-5 relative (the kernel sums in float64, torch in float32); the
+    carried running score / max tile equal episode_scan's over three consecutive rollouts; the
+    workspace's key counter is left zeroed.  Edge cases: no finished game (median / max -1), many finished games,
+    episodic inactive tails."""
+    from g2048 import _lib as L
+    from g2048.advantage import RewardWeights
+    g = np.random.default_rng(T * 7 + n)
+    w = RewardWeights(gamma=0.99, points=0.1, mono=1.0, emptiness=0.5, rtg_beta=0.9)
+    rs = torch.randint(0, 5000, (n,), dtype=torch.int64, device=dev)
+    rm = torch.randint(0, 9, (n,), dtype=torch.int32, device=dev)
+    rs_ref, rm_ref = rs.clone(), rm.clone()
+    ws = torch.zeros(L.rollout_stats_workspace_bytes(T, n), dtype=torch.uint8, device=dev)
+    out = torch.empty(L.ROLLOUT_STATS, dtype=torch.float32, device=dev)
+    for it in range(3):
+        pts = torch.from_numpy(np.where(g.random((T, n)) < 0.3, 0, g.integers(0, 2048, size=(T, n))).astype(np.int32)).to(dev)
+        pot = g.integers(-20, 60, size=(T, n, 4)) * (g.random((T, n, 1)) >= 0.3)  # zero rewards where pts = 0 too
+        pot = torch.from_numpy(pot.astype(np.int8)).to(dev)
+        fl = np.where(g.random((T, n)) < p_done, 0x80, 0) | np.where(g.random((T, n)) < 0.1, 0x20, 0)
+        if episodic:  # games end at a random step; the rest of the column is inactive
+            end = g.integers(1, T + 1, size=n)
+            tt = np.arange(T)[:, None]
+            fl = np.where(tt == end - 1, 0x80, 0) | np.where(tt >= end, 0x40, 0)
+        sf = torch.from_numpy(fl.astype(np.uint8)).to(dev)
+        value, g_raw, g_norm, adv = (torch.from_numpy((g.standard_normal((T, n)) * s).astype(np.float32)).to(dev)
+                                     for s in (1.0, 30.0, 1.0, 1.5))
+        boards = torch.from_numpy(g.integers(0, 12, size=(T + 1, n, 16)).astype(np.int8)).to(dev)
+        mt = torch.from_numpy(g.integers(0, 13, size=(T, n)).astype(np.int8)).to(dev)
+        bview = boards if episodic else boards[:T]
+        if episodic:
+            L.rollout_stats(pts, pot, sf, value, g_raw, g_norm, adv, bview, None, True, w.cfg(), None, None, ws, out)
+        else:
+            L.rollout_stats(pts, pot, sf, value, g_raw, g_norm, adv, bview, mt, False, w.cfg(), rs, rm, ws, out)
+        ref = _rollout_stats_torch(pts, pot, sf, value, g_raw, g_norm, adv, bview, mt, episodic, w, rs_ref, rm_ref)
+        got = out.double().cpu().numpy()
+        exact = [0, 17, 18, 22]  # rows, median, max, finished count
+        np.testing.assert_array_equal(got[exact], ref[exact], err_msg=f"rollout {it}")
+        np.testing.assert_allclose(got[19:22], ref[19:22], rtol=1e-6, atol=1e-4, err_msg=f"tile % rollout {it}")
+        scale = np.maximum(np.abs(ref), 1.0)
+        np.testing.assert_array_less(np.abs(got - ref) / scale, 1e-5, err_msg=f"moments rollout {it}")
+        if not episodic:
+            assert torch.equal(rs, rs_ref) and torch.equal(rm, rm_ref)
+        if p_done == 0.0 and not episodic:
+            assert got[17] == -1 and got[18] == -1 and got[22] == 0
+        assert int(ws[:4].view(torch.int32)[0]) == 0  # the key counter is left zeroed
+
+
 @pytest.mark.parametrize("n,k", [(3000, 750), (257, 256), (1000, 0)])
 def test_augment_kernel_matches_oracle(dev, n, k):
     """g2048_augment (D4 up-sampling, train.py:774-881) vs oracle.augment_plan + augment_rows: the
