@@ -957,23 +957,25 @@ __device__ __forceinline__ void ns_square_mc_rb(char *sX, char *sG, const MuonAr
         __syncthreads();
         MUON_TP(args);
         if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (wave == 0) {
-            mc_wait(ctr, (uint32_t)(np * (it + 1)), err);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        if (wave == 0) mc_wait(ctr, (uint32_t)(np * (it + 1)), err);
         __syncthreads();
         MUON_TP(args);
         // the whole X' (every block's rows, padding columns zero) into the LDS image: every load in
-        // flight before the first LDS store (one L2 round trip, not one per 16 KB)
+        // flight before the first LDS store (one L2 round trip, not one per 16 KB).  No acquire
+        // fence (its L1 invalidate was ~1.7 us per hand-off): the loads are sc1 buffer loads, served
+        // by L2 past this CU's L1, every byte was stored sc1 by its producer, whose storing waves all
+        // drained (vmcnt(0)) before the barrier behind which one lane adds to the counter, and only
+        // the polling wave's match releases the barrier above (MI355X_MICROARCH.md, the hand-off
+        // table's first row).  Offsets past N * P read zero (the descriptor's record count).
         const char *src = xg + (it & 1) * N * P;
+        const __amdgpu_buffer_rsrc_t rsrc =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(src), (short)0, N * P, 0x00020000);
         constexpr int kCopy = (N * P / 16 + kMuonThreads - 1) / kMuonThreads;
+        constexpr int kSc1 = 16;  // cache-policy bit of the buffer load: sc1
         uint4 cv[kCopy];
 #pragma unroll
-        for (int u = 0; u < kCopy; u++) {
-            const int o = (tid + u * kMuonThreads) * 16;
-            cv[u] = o < N * P ? *reinterpret_cast<const uint4 *>(src + o) : make_uint4(0u, 0u, 0u, 0u);
-        }
+        for (int u = 0; u < kCopy; u++)
+            cv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, (tid + u * kMuonThreads) * 16, 0, kSc1));
 #pragma unroll
         for (int u = 0; u < kCopy; u++) {
             const int o = (tid + u * kMuonThreads) * 16;
