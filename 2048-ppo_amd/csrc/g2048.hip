@@ -1688,6 +1688,30 @@ int g2048_rollout_stats(g2048_stream_t stream, const int32_t *points, const int8
     return launch_status();
 }
 
+// The epoch's minibatch order (DataLoader(shuffle=True), train.py:470): out[i] = a keyed Feistel
+// bijection of [0, n) (feistel_row: 4 rounds over [0, 4^k), cycle-walked), round keys Philox-drawn
+// in the kernel from *key_dev (a device draw of the update's generator: no host read) or `seed`.
+__global__ __launch_bounds__(kBlock) void permutation_kernel(int64_t *__restrict__ out, uint32_t n, uint32_t half,
+                                                             const int64_t *__restrict__ key_dev, uint64_t seed,
+                                                             uint64_t counter) {
+    const uint64_t sd = key_dev ? (uint64_t)key_dev[0] : seed;
+    const uint4 key = philox_draw(sd, counter, 0xFFFFFFFEu, 5u);
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
+        out[i] = (int64_t)feistel_row(i, n, half, key);
+}
+
+int g2048_permutation(g2048_stream_t stream, int64_t *out, int64_t n, const int64_t *key_dev, uint64_t seed,
+                      uint64_t counter) {
+    if (n < 0 || n >= (int64_t(1) << 31) || (n > 0 && !out)) return G2048_EINVAL;
+    if (n == 0) return G2048_OK;
+    uint32_t bits = 2u;
+    while ((1ull << bits) < (uint64_t)n) bits += 2u;
+    const unsigned blocks = blocks_for(n) < 2048u ? blocks_for(n) : 2048u;
+    hipLaunchKernelGGL(permutation_kernel, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, out, (uint32_t)n,
+                       bits / 2u, key_dev, seed, counter);
+    return launch_status();
+}
+
 // Philox4x32-10 on the host (the Feistel round keys of g2048_augment)
 static uint4 philox_host(uint64_t seed, uint64_t step, uint32_t env, uint32_t stream) {
     uint32_t c0 = (uint32_t)step, c1 = (uint32_t)(step >> 32), c2 = env, c3 = stream;

@@ -27,7 +27,7 @@ EXPORTED = (
     "g2048_preview_points", "g2048_legal_mask",
     "g2048_obs_encode", "g2048_info_deltas", "g2048_sample_actions", "g2048_rtg_prepare", "g2048_reward_rtg_workspace_bytes",
     "g2048_reward_rtg", "g2048_reward_rtg_ex", "g2048_rtg_finalize", "g2048_build_info", "g2048_episode_scan",
-    "g2048_rollout_stats_workspace_bytes", "g2048_rollout_stats",
+    "g2048_rollout_stats_workspace_bytes", "g2048_rollout_stats", "g2048_permutation",
     "g2048_augment_workspace_bytes", "g2048_augment",
     # include/g2048_ppo.h
     "g2048_obs_gather", "g2048_ln_act_fwd", "g2048_ln_act_bwd_partials", "g2048_ln_act_bwd",
@@ -222,6 +222,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_build_info": (ctypes.c_char_p, []),
         "g2048_episode_scan": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp]),
         "g2048_rollout_stats_workspace_bytes": (sz, [i64, i64]),
+        "g2048_permutation": (ctypes.c_int, [vp, vp, i64, vp, u64, u64]),
         "g2048_rollout_stats": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32, cp, vp, vp, vp,
                                                sz, vp]),
         "g2048_augment_workspace_bytes": (ctypes.c_size_t, [i64]),
@@ -459,6 +460,16 @@ def episode_scan(points, boards, max_tile, step_flags, run_score, run_max, score
         _dev(max_tile, torch.int8, "max_tile"), _dev(step_flags, torch.uint8, "step_flags"), T, n,
         _dev(run_score, torch.int64, "run_score"), _dev(run_max, torch.int32, "run_max"),
         _dev(scores, torch.int64, "scores"), _dev(tiles, torch.int32, "tiles")), "g2048_episode_scan")
+
+
+def permutation(out, n: int, key=None, seed: int = 0, counter: int = 0):
+    """out[:n] (int64, device) = a keyed random permutation of [0, n) (g2048_permutation); key: a
+    device int64 [1] (e.g. drawn from the caller's generator: no host read) or None for (seed, counter)."""
+    if out.numel() < n:
+        raise G2048Error("permutation: out too small")
+    _check(load().g2048_permutation(_stream(out), _dev(out, torch.int64, "out"), int(n),
+                                    _dev(key, torch.int64, "key"), int(seed) & (2 ** 64 - 1),
+                                    int(counter) & (2 ** 64 - 1)), "g2048_permutation")
 
 
 ROLLOUT_STATS = 23  # g2048_rollout_stats' output vector

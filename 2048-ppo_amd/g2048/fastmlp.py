@@ -375,8 +375,7 @@ class FusedPPOUpdater(PPOUpdater):
         g = self._ensure_offset_graphs(data, bs)
         nb = 0
         for _ in range(cfg.epochs):
-            perm = torch.randperm(m_total, device=self.dev, generator=self.gen)
-            g["perm"][:m_total].copy_(perm)
+            self._epoch_perm(m_total, out=g["perm"])
             g["perm"][m_total:m_total + bs].zero_()  # the padded ragged minibatch reads row 0
             self.idx_off.zero_()
             nfull, rag = divmod(m_total, bs)

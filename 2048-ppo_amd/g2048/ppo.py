@@ -114,7 +114,7 @@ class PPOUpdater:
         if use_graph:
             self._ensure_graph(data, bs, encode)
         for _ in range(cfg.epochs):
-            perm = torch.randperm(m_total, device=self.dev, generator=self.gen)
+            perm = self._epoch_perm(m_total)
             if use_graph and len(self._g["idx"]) == 2:
                 self._g["perm_ready"].record()
             for s in range(0, m_total, bs):
@@ -141,6 +141,20 @@ class PPOUpdater:
         st = self.stats / max(nb, 1)
         st[STAT_KEYS.index("kl_max")] = self.stats[STAT_KEYS.index("kl_max")]
         return {k: st[i] for i, k in enumerate(STAT_KEYS)}
+
+    def _epoch_perm(self, m_total: int, out: torch.Tensor | None = None) -> torch.Tensor:
+        """The epoch's minibatch order (DataLoader(shuffle=True), train.py:470).  On the device:
+        g2048_permutation keyed by one int64 drawn from the update's generator (no host read; one
+        launch instead of torch.randperm's radix sort of m_total keys); `out` (optional) receives it."""
+        if self.dev.type != "cuda":  # the CPU (gloo) updater of the host tests
+            perm = torch.randperm(m_total, device=self.dev, generator=self.gen)
+            return perm if out is None else out[:m_total].copy_(perm)
+        from . import _lib as L
+        key = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64, device=self.dev, generator=self.gen)
+        if out is None:
+            out = torch.empty(m_total, dtype=torch.int64, device=self.dev)
+        L.permutation(out, m_total, key)
+        return out[:m_total]
 
     # ---------------------------------------------------------------- eager minibatch ------
     def _pre(self, idx, data, beta, encode):

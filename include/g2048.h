@@ -214,6 +214,14 @@ int g2048_rollout_stats(g2048_stream_t stream, const int32_t *points, const int8
                         const g2048_reward_cfg *cfg, int64_t *run_score, int32_t *run_max, void *workspace,
                         size_t workspace_bytes, float *out);
 
+/* The PPO update's per-epoch minibatch order (DataLoader(shuffle=True), train.py:470; replaces
+ * torch.randperm, a 4 M-key radix sort): out[i] (int64, i < n < 2^31) = a keyed Feistel bijection of
+ * [0, n) (4 rounds over [0, 4^k) >= n, cycle-walked), round keys Philox-drawn from (*key_dev if
+ * key_dev is non-NULL -- a device int64, e.g. a draw of the caller's generator, so no host read --
+ * else seed, counter).  One launch, no workspace. */
+int g2048_permutation(g2048_stream_t stream, int64_t *out, int64_t n, const int64_t *key_dev, uint64_t seed,
+                      uint64_t counter);
+
 /* EMA moment update with the batch statistics (train.py:898-901); advances rtg_step. */
 int g2048_rtg_finalize(g2048_stream_t stream, double *state, const double *partials,
                        const g2048_reward_cfg *cfg);
