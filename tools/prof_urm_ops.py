@@ -32,6 +32,13 @@ def main():
         if e.key.startswith("aten::") or "Function" in e.key or "Backward" in e.key:
             print(f"{e.key[:60]:60s} {e.count:6d} {e.device_time_total:10.0f}")
     print(ka.table(sort_by="device_time_total", row_limit=45, max_name_column_width=70))
+    # the aten ops by input shape: which calls launch the small kernels
+    ks = prof.key_averages(group_by_input_shape=True)
+    rows = sorted((e for e in ks if e.key.startswith("aten::") and e.device_time_total > 0),
+                  key=lambda e: -e.device_time_total)
+    print(f"{'aten op':28s} {'count':>6s} {'dev_us':>9s}  input shapes")
+    for e in rows[:40]:
+        print(f"{e.key[:28]:28s} {e.count:6d} {e.device_time_total:9.0f}  {str(e.input_shapes)[:110]}")
 
 
 if __name__ == "__main__":
