@@ -121,7 +121,11 @@ static_assert(sizeof(g2048_muon_cfg) == 48 && offsetof(g2048_muon_cfg, workspace
               "g2048_muon_cfg layout (tests/test_abi.py)");
 constexpr int kMuonMaxJobs = 128;  // grid blocks: Muon parts, AdamW blocks, idle gaps (XCD placement)
 constexpr uint8_t kRoleAdam = 0xFE, kRoleIdle = 0xFF;
-constexpr int kMuonSyncBytes = kMuonMaxMats * 64;  // one 64-byte line per matrix counter
+// one 64-byte line per matrix (exchange / prologue / done counters, the matrix's timeout flag),
+// then one line whose first word counts every timed-out wait of every launch (sticky: only the host
+// clears it -- FusedMuonAdamW reads it with the train step's metrics and raises, g2048_ppo.h)
+constexpr int kMuonSyncBytes = kMuonMaxMats * 64 + 64;
+constexpr int kMuonErrWord = kMuonMaxMats * 16;  // uint32 index of the sticky timeout count
 constexpr int kMuonLds = 160 * 1024 - 256;  // minus the static red[] / s_norm
 
 struct MuonMat {
@@ -168,6 +172,7 @@ struct MuonArgs {
     int npartials;  // clip partial sums (64: g2048_grad_sumsq's)
     uint8_t job_mat[kMuonMaxJobs], job_part[kMuonMaxJobs], job_nparts[kMuonMaxJobs];
     uint32_t *sync;              // per matrix: the exchange counter (zeroed before every launch)
+    uint32_t spin_limit;         // polls of a hand-off counter before a wait gives up (~0.2 s by default)
     char *xg;                    // per matrix: two N x P-byte bf16 exchange images (X of even / odd iterations)
     int64_t xg_stride;           // bytes per matrix
     uint64_t *trace;             // MUON_TRACE builds: phase clocks
@@ -756,15 +761,26 @@ constexpr int kMuonTraceBytes = kMuonMaxJobs * 64 * 8;
 #define MUON_TP(args_)                                                                      \
     do {                                                                                    \
         if (threadIdx.x == 0 && (args_).trace) {                                            \
-            uint64_t *t_ = (args_).trace + 64 * blockIdx.x;                                 \
-            const uint64_t k_ = t_[0] + 1;                                                  \
-            if (k_ < 64) t_[k_] = __builtin_amdgcn_s_memtime();                             \
-            t_[0] = k_;                                                                     \
+            if (blockIdx.x >= (unsigned)kMuonMaxJobs) {                                     \
+                printf("MUON_CHECK trace block %u out of range\n", blockIdx.x);              \
+            } else {                                                                        \
+                uint64_t *t_ = (args_).trace + 64 * blockIdx.x;                             \
+                const uint64_t k_ = t_[0] + 1;                                              \
+                if (k_ < 64) t_[k_] = __builtin_amdgcn_s_memtime();                         \
+                t_[0] = k_;                                                                 \
+            }                                                                               \
         }                                                                                   \
+    } while (0)
+// trace builds also bound-check every exchange-image access and the job table (printf + skip)
+#define MUON_CHECK(cond_, what_, a_, b_)                                                    \
+    do {                                                                                    \
+        if (!(cond_)) printf("MUON_CHECK %s blk %u tid %u: %lld %lld\n", what_, blockIdx.x, threadIdx.x, \
+                             (long long)(a_), (long long)(b_));                             \
     } while (0)
 #else
 constexpr int kMuonTraceBytes = 0;
 #define MUON_TP(args_) do {} while (0)
+#define MUON_CHECK(cond_, what_, a_, b_) do {} while (0)
 #endif
 
 // G = X X^T alone, on the square schedule (no kept tiles: the row-block U product re-reads G)
@@ -887,13 +903,18 @@ __device__ __forceinline__ void mc_product(const char *sX, const char *sG, int t
     else mc_mfma<N, RB, false>(sG, sX, t0, tj, lane, acc);
 }
 
-// bounded relaxed poll of a counter (one wave); false after ~0.2 s (a lost block: results are
-// garbage, the error word is set, but no wave spins forever)
-__device__ __forceinline__ bool mc_wait(gu32_t *ctr, uint32_t target, gu32_t *err) {
+// bounded relaxed poll of a counter (one wave); false after `limit` polls (~0.2 s at the default
+// 2^21: a part that never became resident).  No wave spins forever; the results of the launch are
+// then garbage, so the timeout is recorded in the matrix's flag and counted in the sticky error word
+// that the host reads with the train step's metrics and raises on (FusedMuonAdamW.check_errors).
+__device__ __forceinline__ bool mc_wait(gu32_t *ctr, uint32_t target, gu32_t *err, gu32_t *errors, uint32_t limit) {
     for (uint32_t spins = 0;; spins++) {
         if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
-        if (spins > (1u << 21)) {
-            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (spins >= limit) {
+            if ((threadIdx.x & 63) == 0) {
+                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(errors, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             return false;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -940,6 +961,8 @@ __device__ __forceinline__ void ns_square_mc_rb(char *sX, char *sG, const MuonAr
                 const uint2 v = mc_row_segment<N>(acc[x], 1.0f, wave, c);
                 if (row < N) {
                     char *dst = img + row * P + (16 * wave + 4 * (c >> 2)) * 2;
+                    MUON_CHECK(last || (dst >= xg && dst + 8 <= xg + args.xg_stride), "xg store", dst - xg, args.xg_stride);
+                    MUON_CHECK(!last || (16 * wave + 4 * (c >> 2)) * 2 + 8 <= P, "sX store", (16 * wave + 4 * (c >> 2)) * 2, P);
                     if (last) {
                         *reinterpret_cast<uint2 *>(dst) = v;
                     } else {  // write-through: no release fence needed before the counter add
@@ -957,7 +980,7 @@ __device__ __forceinline__ void ns_square_mc_rb(char *sX, char *sG, const MuonAr
         __syncthreads();
         MUON_TP(args);
         if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (wave == 0) mc_wait(ctr, (uint32_t)(np * (it + 1)), err);
+        if (wave == 0) mc_wait(ctr, (uint32_t)(np * (it + 1)), err, (gu32_t *)(args.sync + kMuonErrWord), args.spin_limit);
         __syncthreads();
         MUON_TP(args);
         // the whole X' (every block's rows, padding columns zero) into the LDS image: every load in
@@ -968,6 +991,7 @@ __device__ __forceinline__ void ns_square_mc_rb(char *sX, char *sG, const MuonAr
         // the polling wave's match releases the barrier above (MI355X_MICROARCH.md, the hand-off
         // table's first row).  Offsets past N * P read zero (the descriptor's record count).
         const char *src = xg + (it & 1) * N * P;
+        MUON_CHECK(src + N * P <= xg + args.xg_stride, "xg image", (it & 1) * N * P + N * P, args.xg_stride);
         const __amdgpu_buffer_rsrc_t rsrc =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(src), (short)0, N * P, 0x00020000);
         constexpr int kCopy = (N * P / 16 + kMuonThreads - 1) / kMuonThreads;
@@ -1053,6 +1077,7 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
         return;
     }
     const int mat = args.job_mat[blockIdx.x], part = args.job_part[blockIdx.x], np = args.job_nparts[blockIdx.x];
+    MUON_CHECK(blockIdx.x < (unsigned)kMuonMaxJobs && mat < args.count && part < np, "job", mat, part * 256 + np);
     const MuonMat mt = args.m[mat];
     const int R = mt.rows, C = mt.cols;
     const bool tr = R > C;  // iterate on the wide orientation (r <= c), like torch
@@ -1170,14 +1195,20 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     const float step = lr * (0.2f * sqrtf((float)(R > C ? R : C)));
     muon_epilogue(mt.param, mt.pbf, sX, px, R, C, tr, 1.0f - lr * args.wd, step, tid, own0, own1, mt.frag, mt.frag_row);
     if (pro) {  // this part's momentum rows, once every part has read the old ones
-        if (wave == 0) mc_wait(pro, (uint32_t)np, (gu32_t *)(args.sync + 16 * mat + 1));
+        if (wave == 0)
+            mc_wait(pro, (uint32_t)np, (gu32_t *)(args.sync + 16 * mat + 1), (gu32_t *)(args.sync + kMuonErrWord),
+                    args.spin_limit);
         __syncthreads();
         muon_momentum_rows(mt.grad, mt.mom, C, coef, args.momentum, args.nesterov != 0, own0, min(own1, R), tid);
         // the last part through here puts the matrix's counters back to zero for the next launch
-        // (no memset node per step): every other part has finished all its polls when it counts in
+        // (no memset node per step): every other part has finished all its polls when it counts in.
+        // The done add is a release (this part's ctr / pro adds, same thread, happen before it) and
+        // the last arriver acquires before its reset stores, so the reset is ordered after every
+        // part's counter adds by the memory model, not by the order L2 happens to apply atomics in.
         if (tid == 0) {
             gu32_t *ctr = (gu32_t *)(args.sync + 16 * mat), *done = (gu32_t *)(args.sync + 16 * mat + 2);
-            if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(np - 1)) {
+            if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(np - 1)) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(pro, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1206,6 +1237,23 @@ inline int status() {
     return e == hipSuccess ? G2048_OK : (int)e;
 }
 
+// CUs of the current device (cached per device)
+inline int device_cus() {
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (!cached[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+        cached[dev] = n;
+    }
+    return cached[dev];
+}
+
+inline bool muon_splits(const g2048_muon_matrix &m, int parts) {
+    return parts > 1 && m.rows == m.cols && (m.rows == 196 || m.rows == 192);
+}
+
 inline size_t muon_lds_bytes(int R, int C) {
     const int r = R > C ? C : R, c = R > C ? R : C;
     const int px = muon_pitch(r, c), pg = muon_pitch(r, r);
@@ -1229,6 +1277,8 @@ size_t g2048_muon_workspace_bytes(void) {
     return (size_t)kMuonSyncBytes + (size_t)kMuonMaxMats * 2 * max(196 * muon_pitch(196, 196), 192 * muon_pitch(192, 192)) +
            kMuonTraceBytes;
 }
+
+size_t g2048_muon_error_offset(void) { return (size_t)kMuonErrWord * sizeof(uint32_t); }
 
 int g2048_muon_supported(int32_t rows, int32_t cols) {
     if (rows <= 0 || cols <= 0) return 0;
@@ -1326,52 +1376,66 @@ static int muon_launch(g2048_stream_t stream, const g2048_muon_matrix *mats, int
     // parts of split matrix k sit on blocks k, k + 8, k + 16, ... -- one XCD under the round-robin
     // dispatch, so their exchange images are read from that XCD's L2; the other matrices and the
     // AdamW blocks fill the remaining slots in order, the rest of the grid idles.
-    const int parts = cfg->workspace && !a.generic_ns && !getenv("G2048_MUON_ONE_CU") ? cfg->parts : 1;
+    int parts = cfg->workspace && !a.generic_ns && !getenv("G2048_MUON_ONE_CU") ? cfg->parts : 1;
     if (parts > 1 && (parts < 7 || parts > 13)) return G2048_EINVAL;  // one or two tile rows per block
+    const char *spin = getenv("G2048_MUON_SPIN_LIMIT");  // tests: force the timeout path
+    a.spin_limit = spin ? (uint32_t)strtoul(spin, nullptr, 0) : (1u << 21);
     if (adam) {  // AdamW blocks: ~2 elements per thread, at most 8 blocks
         int64_t nmax = 0;
         for (int k = 0; k < adam->count; k++) nmax = adam->g[k].n > nmax ? adam->g[k].n : nmax;
         const int64_t nb = (nmax + 2 * kMuonThreads - 1) / (2 * kMuonThreads);
         a.nadam = (int)(nb < 1 ? 1 : (nb > 8 ? 8 : nb));
     }
-    for (int b = 0; b < kMuonMaxJobs; b++) a.job_mat[b] = kRoleIdle;
-    int nsplit = 0, grid = 0;
-    for (int i = 0; i < count; i++) {  // split matrices first: their XCD columns
-        const g2048_muon_matrix &m = mats[i];
-        if (!(parts > 1 && m.rows == m.cols && (m.rows == 196 || m.rows == 192))) continue;
-        const int nt = (m.rows + 15) / 16, np = parts < nt ? parts : nt;
-        for (int p = 0; p < np; p++) {
-            const int b = nsplit < 8 ? nsplit + 8 * p : -1;
-            if (b < 0 || b >= kMuonMaxJobs) return G2048_EINVAL;
+    // the job table for `np_req` parts per split matrix; returns the grid size (-1: does not fit)
+    auto place = [&](int np_req) {
+        for (int b = 0; b < kMuonMaxJobs; b++) a.job_mat[b] = kRoleIdle;
+        int nsplit = 0, grid = 0;
+        for (int i = 0; i < count; i++) {  // split matrices first: their XCD columns
+            const g2048_muon_matrix &m = mats[i];
+            if (!muon_splits(m, np_req)) continue;
+            const int nt = (m.rows + 15) / 16, np = np_req < nt ? np_req : nt;
+            for (int p = 0; p < np; p++) {
+                const int b = nsplit < 8 ? nsplit + 8 * p : -1;
+                if (b < 0 || b >= kMuonMaxJobs) return -1;
+                a.job_mat[b] = (uint8_t)i;
+                a.job_part[b] = (uint8_t)p;
+                a.job_nparts[b] = (uint8_t)np;
+                grid = b + 1 > grid ? b + 1 : grid;
+            }
+            nsplit++;
+        }
+        int next = 0;
+        auto free_slot = [&]() {
+            while (next < kMuonMaxJobs && a.job_mat[next] != kRoleIdle) next++;
+            return next < kMuonMaxJobs ? next++ : -1;
+        };
+        for (int i = 0; i < count; i++) {  // one-block matrices
+            if (muon_splits(mats[i], np_req)) continue;
+            const int b = free_slot();
+            if (b < 0) return -1;
             a.job_mat[b] = (uint8_t)i;
-            a.job_part[b] = (uint8_t)p;
-            a.job_nparts[b] = (uint8_t)np;
+            a.job_part[b] = 0;
+            a.job_nparts[b] = 1;
             grid = b + 1 > grid ? b + 1 : grid;
         }
-        nsplit++;
-    }
-    int next = 0;
-    auto free_slot = [&]() {
-        while (next < kMuonMaxJobs && a.job_mat[next] != kRoleIdle) next++;
-        return next < kMuonMaxJobs ? next++ : -1;
+        for (int k = 0; k < (adam ? a.nadam : 0); k++) {
+            const int b = free_slot();
+            if (b < 0) return -1;
+            a.job_mat[b] = kRoleAdam;
+            a.job_part[b] = (uint8_t)k;
+            grid = b + 1 > grid ? b + 1 : grid;
+        }
+        return grid;
     };
-    for (int i = 0; i < count; i++) {  // one-block matrices
-        const g2048_muon_matrix &m = mats[i];
-        if (parts > 1 && m.rows == m.cols && (m.rows == 196 || m.rows == 192)) continue;
-        const int b = free_slot();
-        if (b < 0) return G2048_EINVAL;
-        a.job_mat[b] = (uint8_t)i;
-        a.job_part[b] = 0;
-        a.job_nparts[b] = 1;
-        grid = b + 1 > grid ? b + 1 : grid;
+    int grid = place(parts);
+    // the split parts poll each other, so every block of the grid must be resident at once (one per
+    // CU: 1 024 threads, ~160 KB of LDS): a device with fewer CUs than the grid (a partitioned GPU, a
+    // smaller part) runs every matrix on one CU instead
+    if (parts > 1 && (grid < 0 || grid > device_cus())) {
+        parts = 1;
+        grid = place(1);
     }
-    for (int k = 0; k < (adam ? a.nadam : 0); k++) {
-        const int b = free_slot();
-        if (b < 0) return G2048_EINVAL;
-        a.job_mat[b] = kRoleAdam;
-        a.job_part[b] = (uint8_t)k;
-        grid = b + 1 > grid ? b + 1 : grid;
-    }
+    if (grid < 0) return G2048_EINVAL;
     a.njobs = grid;
     if (parts > 1) {  // the counters: zero from the caller's first fill, left zero by every launch
         char *ws = static_cast<char *>(cfg->workspace);

@@ -62,10 +62,12 @@ def bench_train(args, rank: int, world: int, dev) -> dict:
     fl = mlp_flops_per_sample(h=mc.hidden_dim, layers=len(tr.model.backbone))
     # the update's work is the real sample rows: the ragged last minibatch's padding is not counted
     rows_update = args.envs * args.train_horizon + int(m["augmented_samples"])
+    paths, fallbacks, phases = tr.paths, tr.fallbacks, dict(tr.timings)
+    tr.close()  # its graphs hold captured RCCL all-reduces at world > 1: released before the process group
     roof = {}
     for name, ms_key, flop in (("update", "update_ms", fl["update"] * rows_update),
                                ("policy_rollout", "rollout_ms", fl["forward"] * args.envs * args.train_horizon)):
-        ms = tr.timings.get(ms_key)
+        ms = phases.get(ms_key)
         if ms:
             ach = flop / (ms * 1e-3) / 1e12
             roof[name] = {"bound": "mfma", "achieved": ach, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -77,9 +79,9 @@ def bench_train(args, rank: int, world: int, dev) -> dict:
         "config": {"workload": "65536 envs/GPU MLP h=196 bf16: rollout + RTG/entropy + PPO update",
                    "envs_per_gpu": args.envs, "horizon": args.train_horizon, "minibatch": args.train_batch,
                    "minibatches_per_iter": n_mb, "upsample_ratio": args.train_upsample, "optimizer": "Muon(2-D)+AdamW(1-D)", "dtype": "bf16 activations / fp32 master weights (MFMA kernels)"},
-        "phase_ms_one_iter": {k: round(v, 3) for k, v in tr.timings.items()},
+        "phase_ms_one_iter": {k: round(v, 3) for k, v in phases.items()},
         "roofline": roof,
-        "kernel_paths": tr.paths, "fallbacks": tr.fallbacks,
+        "kernel_paths": paths, "fallbacks": fallbacks,
         "last_metrics": {k: m[k] for k in ("loss", "entropy", "avg_score", "episodes_finished", "grad_norm",
                                            "augmented_samples")},
     }
@@ -154,9 +156,11 @@ def bench_urm(args, rank: int, world: int, dev) -> dict:
     tr.profile = True
     tr.timings = {}
     tr.train_step(1 + iters)
+    paths, fallbacks, phases = tr.paths, tr.fallbacks, dict(tr.timings)
+    tr.close()
     out["train_iter"] = {"value": args.envs * T * world / it, "unit": "env-steps/s", "ms_per_iter": it * 1e3,
                          "iters": iters,
-                         "kernel_paths": tr.paths, "fallbacks": tr.fallbacks,
-                         "phase_ms": {k: round(v, 3) for k, v in tr.timings.items()},
+                         "kernel_paths": paths, "fallbacks": fallbacks,
+                         "phase_ms": {k: round(v, 3) for k, v in phases.items()},
                          "minibatch": args.train_batch, "loss": mt["loss"], "entropy": mt["entropy"]}
     return out

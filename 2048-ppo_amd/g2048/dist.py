@@ -69,6 +69,23 @@ def trim_rows(data: dict, k: int, n_real: int | None = None, generator: torch.Ge
     return {key: v.index_select(0, keep) for key, v in data.items()}
 
 
+def graph(g, pool=None):
+    """torch.cuda.graph(g, pool) for every capture of the package, in "thread_local" capture mode.
+
+    torch's default "global" mode makes a capture-unsafe call from ANY thread of the process an
+    error while the capture is open.  With a process group alive, ProcessGroupNCCL's watchdog thread
+    polls the events of the eager collectives (hipEventQuery) every ~100 ms; a poll that lands inside
+    one of our captures -- the minibatch graphs are captured right after two eager warm-up steps,
+    whose all-reduces are still on the watchdog's list -- fails under "global" mode, and the
+    watchdog turns the failure into an uncaught c10::DistBackendError on its own thread: SIGABRT with
+    a C++ frame dump whose last frame is libc's thread start.  That is the shape of the RCCL child
+    abort seen once in round 4.  "thread_local" keeps the capture-safety check for
+    this thread, which issues all of the package's GPU work, and leaves the watchdog's queries
+    alone."""
+    import torch
+    return torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local")
+
+
 def _host_staged() -> bool:
     """gloo on device tensors (the CPU-backend tests of the device path: RCCL refuses two ranks on
     one GPU) goes through a host copy; RCCL ("nccl") takes the device tensor itself."""

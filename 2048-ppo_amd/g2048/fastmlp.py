@@ -33,6 +33,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib as L
+from .dist import graph as graph_capture
 from .dist import world
 from .ppo import STAT_KEYS, PPOConfig, PPOUpdater
 
@@ -425,7 +426,7 @@ class FusedPPOUpdater(PPOUpdater):
             graphs = {}
             for name, n in (("single", 1), ("multi", self.MULTI)):
                 gr = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gr, pool=pool):
+                with graph_capture(gr, pool=pool):
                     for _ in range(n):
                         st = self._pre(idx, data, self.beta_t, None)
                         self.grads.allreduce_mean()
@@ -498,6 +499,12 @@ class FusedPPOUpdater(PPOUpdater):
                         kl_rows=kl_job.nb, rows=self.rows)
 
     idx_off = None  # the offset path's device row offset (advanced by the KL pass's last block)
+
+    def close(self):
+        """PPOUpdater.close(), and the offset path's graphs (MULTI captured all-reduces each)."""
+        torch.cuda.synchronize(self.dev)
+        self._og = None
+        super().close()
 
     def _extra_snapshot(self):
         return (self.counter.clone(), None if self.idx_off is None else self.idx_off.clone())

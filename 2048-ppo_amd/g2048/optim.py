@@ -231,6 +231,25 @@ class FusedMuonAdamW(MuonAdamW):
 
     MUON_PARTS = 13
 
+    def error_count(self):
+        """Device int32 [1] view of the Muon workspace's sticky count of timed-out hand-off waits (a
+        multi-CU Newton-Schulz part that never became resident: that step's weights are garbage), or
+        None without a multi-CU workspace.  Read with the train step's one host sync."""
+        ws = getattr(self, "_ws", None)
+        if ws is None:
+            return None
+        off = int(self._L.load().g2048_muon_error_offset())
+        return ws[off:off + 4].view(torch.int32)
+
+    def check_errors(self, count: float | int | None = None):
+        """Raise when a multi-CU Muon step timed out (count: the value already read by the caller)."""
+        if count is None:
+            t = self.error_count()
+            count = 0 if t is None else int(t.item())
+        if count:
+            raise RuntimeError(f"fused Muon: {int(count)} multi-CU Newton-Schulz hand-off wait(s) timed out (a part "
+                               f"was not resident); the optimizer state is invalid")
+
     def set_bf16_copies(self, mapping: dict):
         """{parameter: bf16 tensor} refreshed by the Muon kernel after each step."""
         self._bf16 = {id(p): t for p, t in mapping.items()}

@@ -21,6 +21,8 @@ from dataclasses import dataclass
 import torch
 import torch.nn.functional as F
 
+from .dist import graph as graph_capture
+
 STAT_KEYS = ("loss", "policy_loss", "entropy_loss", "value_loss", "grad_norm", "entropy", "kl_total", "kl_average",
              "kl_max")
 
@@ -115,19 +117,9 @@ class PPOUpdater:
             self._ensure_graph(data, bs, encode)
         for _ in range(cfg.epochs):
             perm = self._epoch_perm(m_total)
-            if use_graph and len(self._g["idx"]) == 2:
-                self._g["perm_ready"].record()
             for s in range(0, m_total, bs):
                 idx = perm[s:s + bs]
                 n = idx.shape[0]
-                if use_graph and len(self._g["idx"]) == 2:  # the index copy beside the previous replay
-                    if n < bs:
-                        self._set_rows(n)
-                    self._replay_double(idx)
-                    if n < bs:
-                        self._set_rows(bs)
-                    nb += 1
-                    continue
                 if n < bs and self.ragged_pad:  # DataLoader's ragged last batch (drop_last=False), padded
                     idx = torch.cat([idx, idx.new_zeros(bs - n)])
                     self._set_rows(n)
@@ -204,11 +196,7 @@ class PPOUpdater:
         # there it runs eagerly between two graphs (g1: forward, loss, backward; g2: clip, optimizer,
         # KL); force_split exercises that path on one GPU
         split = not self.grads.capturable() or self.force_split
-        # double_idx: two captures of the step, reading two index buffers alternately, so that the
-        # next minibatch's index copy runs on a side stream beside the current replay instead of
-        # ahead of it on the replay's stream
-        idxs = [torch.zeros(bs, dtype=torch.int64, device=self.dev) for _ in range(2 if self.double_idx else 1)]
-        idx = idxs[0]
+        idx = torch.zeros(bs, dtype=torch.int64, device=self.dev)
         params = [p for p in self.model.parameters()]
         snap_p = [p.detach().clone() for p in params]
         snap_o = self.opt.snapshot()
@@ -222,30 +210,23 @@ class PPOUpdater:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
-        caps = []
-        for ib in idxs:
-            g1, g2 = torch.cuda.CUDAGraph(), None
-            with torch.cuda.graph(g1, pool=pool):
-                st = self._pre(ib, data, self.beta_t, encode)
-                if not split:
-                    self.grads.allreduce_mean()
-                    self._post(st, self.beta_t)
-            if split:
-                g2 = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g2, pool=pool):
-                    self._post(st, self.beta_t)
-            caps.append((g1, g2, st))
+        g1, g2 = torch.cuda.CUDAGraph(), None
+        with graph_capture(g1, pool=pool):
+            st = self._pre(idx, data, self.beta_t, encode)
+            if not split:
+                self.grads.allreduce_mean()
+                self._post(st, self.beta_t)
+        if split:
+            g2 = torch.cuda.CUDAGraph()
+            with graph_capture(g2, pool=pool):
+                self._post(st, self.beta_t)
         with torch.no_grad():
             for p, q in zip(params, snap_p):
                 p.copy_(q)
         self.opt.restore(snap_o)
         self.stats.copy_(snap_s)
         self._extra_restore(snap_x)
-        g1, g2, st = caps[0]
-        self._g = {"key": key, "idx": idxs, "caps": caps, "g1": g1, "g2": g2, "st": st, "k": 0,
-                   "side": torch.cuda.Stream() if len(idxs) == 2 else None,
-                   "perm_ready": torch.cuda.Event(), "copied": [torch.cuda.Event(), torch.cuda.Event()],
-                   "free": [torch.cuda.Event(), torch.cuda.Event()]}
+        self._g = {"key": key, "idx": idx, "g1": g1, "g2": g2, "st": st}
 
     force_split = False
 
@@ -255,37 +236,21 @@ class PPOUpdater:
     def _extra_restore(self, snap):
         pass
 
-    double_idx = False  # FusedPPOUpdater: two captured copies of the step (see _ensure_graph)
-
     def _replay(self, idx):
         g = self._g
-        g["idx"][0].copy_(idx)
+        g["idx"].copy_(idx)
         g["g1"].replay()
         if g["g2"] is not None:
             self.grads.allreduce_mean()
             g["g2"].replay()
 
-    def _replay_double(self, idx):
-        """Minibatch k on capture k % 2: its index buffer is filled on the side stream once the
-        replay that last read it (k - 2) is done -- beside replay k - 1 -- and the replay waits for
-        that copy only.  A ragged slice is zero-padded (its rows count set by the caller)."""
-        g = self._g
-        k = g["k"]
-        g["k"] ^= 1
-        buf, side, main = g["idx"][k], g["side"], torch.cuda.current_stream()
-        side.wait_event(g["perm_ready"])
-        side.wait_event(g["free"][k])
-        with torch.cuda.stream(side):
-            n = idx.shape[0]
-            buf[:n].copy_(idx)
-            if n < buf.shape[0]:
-                buf[n:].zero_()
-            g["copied"][k].record(side)
-        idx.record_stream(side)
-        main.wait_event(g["copied"][k])
-        g1, g2, _ = g["caps"][k]
-        g1.replay()
-        if g2 is not None:
-            self.grads.allreduce_mean()
-            g2.replay()
-        g["free"][k].record(main)
+    def close(self):
+        """Drop the captured minibatch graphs (and, under RCCL, the all-reduce nodes captured in them)
+        once the device is idle.  Call before torch.distributed.destroy_process_group(): a graph
+        holding a captured collective must not outlive its communicator (RCCL frees the graph's
+        persistent plan through the communicator when the graph is destroyed)."""
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)
+        self._g = None
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)

@@ -16,6 +16,7 @@ import copy
 import torch
 
 from . import _lib as L
+from .dist import graph as graph_capture
 
 
 class InferencePolicy:
@@ -234,7 +235,7 @@ class Rollout:
             self.steps(0, self.T, policy)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with graph_capture(g):
             self.steps(0, self.T, policy)
             self.counter.add_(2 * self.T)
         # capture does not execute: restore the pre-warm-up state so replay #1 is the first rollout

@@ -24,6 +24,7 @@ from . import fastmlp
 from . import urm as urm_mod
 from .advantage import RewardWeights, RTGTracker
 from .dist import GradBucket, allreduce_min_, allreduce_sum_, broadcast_, equal_rows, world
+from .dist import graph as graph_capture
 from .optim import FusedMuonAdamW, MuonAdamW, ScheduledMuonAdamW, build_optimizer
 from .ppo import PPOConfig, PPOUpdater
 from .rollout import Rollout, make_policy
@@ -282,7 +283,7 @@ class VecTrainer:
             ro.steps(c0, c1, self.policy)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with graph_capture(g):
             ro.steps(c0, c1, self.policy)
         b.boards[c0].copy_(snap[0])
         b.flags[c0].copy_(snap[1])
@@ -327,10 +328,8 @@ class VecTrainer:
         data = {"boards": b.boards[:T].reshape(T * n, 16), "actions": b.actions[:T].reshape(-1),
                 "legal": b.flags[:T].reshape(-1), "logp": b.logp[:T].reshape(T * n, 4),
                 "adv": b.adv[:T].reshape(-1), "ret": b.g_norm[:T].reshape(-1)}
-        valid = None
         if self.episodic:
-            valid_mask = (sf & L.FLAG_INACTIVE) == 0
-            valid = torch.nonzero(valid_mask.reshape(-1)).squeeze(1)
+            valid = torch.nonzero(((sf & L.FLAG_INACTIVE) == 0).reshape(-1)).squeeze(1)
             data = {k: v.index_select(0, valid) for k, v in data.items()}
         n_aug = 0
         n_real = data["actions"].shape[0]
@@ -348,7 +347,7 @@ class VecTrainer:
         ustats = self.ppo.update(data, self.beta, self._encode)
         self.opt.scheduler_step()
         self._mark("update_ms")
-        metrics = self._metrics(T, valid, ustats)
+        metrics = self._metrics(T, ustats)
         metrics["augmented_samples"] = n_aug
         self._mark("metrics_ms")
         self._collect_timings()
@@ -407,10 +406,20 @@ class VecTrainer:
                             self.run_maxexp, self._rs_ws, self._rs_out)
         return self._rs_out
 
-    def _metrics(self, T, valid, ustats) -> dict:
-        vec = torch.cat([self._rollout_stats(T), torch.stack([ustats[k] for k in (
+    def _metrics(self, T, ustats) -> dict:
+        """The train step's metrics: the rollout half from g2048_rollout_stats (which also drops the
+        inactive steps of episodic mode itself: FLAG_INACTIVE), the update half from the updater, and
+        the fused Muon's sticky timeout count (raised on, never silent)."""
+        inner = getattr(self.opt, "opt", self.opt)
+        err = inner.error_count() if hasattr(inner, "error_count") else None
+        parts = [self._rollout_stats(T), torch.stack([ustats[k] for k in (
             "loss", "policy_loss", "entropy_loss", "value_loss", "grad_norm", "entropy", "kl_total", "kl_average",
-            "kl_max")])]).tolist()  # the one host synchronisation of the train step
+            "kl_max")])]
+        if err is not None:
+            parts.append(err.float())
+        vec = torch.cat(parts).tolist()  # the one host synchronisation of the train step
+        if err is not None:
+            inner.check_errors(vec.pop())
         (n, rm, rv, zr, am, av, al2, amin, amax, gnm, gns, gnmin, gnmax, grs, vs, g0m, avg_s, med_s, max_s, p512,
          p1024, p2048, n_eps, loss, pl, el, vl, gnorm, ent, klt, kla, klm) = vec
         if n_eps > 0:
@@ -481,6 +490,19 @@ class VecTrainer:
                 "eval/pct_512": sum(1 for t in tiles if t >= 512) / k * 100,
                 "eval/pct_1024": sum(1 for t in tiles if t >= 1024) / k * 100,
                 "eval/pct_2048": sum(1 for t in tiles if t >= 2048) / k * 100}
+
+    def close(self):
+        """Release every captured hipGraph (the update's -- holding the captured RCCL all-reduces at
+        world > 1 -- the rollout's and the episodic chunks') once the device is idle.  Call before
+        torch.distributed.destroy_process_group() (bench.py, the CLI, the RCCL test)."""
+        if self.dev.type != "cuda":
+            return
+        torch.cuda.synchronize(self.dev)
+        if hasattr(self.ppo, "close"):
+            self.ppo.close()
+        self.rollout._graph = None
+        self._chunk_graphs.clear()
+        torch.cuda.synchronize(self.dev)
 
     def save_checkpoint(self, path, eval_avg_score: float, train_step: int):
         import agent

@@ -321,6 +321,11 @@ def train(
         export_best_game_for_demo(best, "docs/data/best_game.json")
         logger.print("ONNX export needs the `onnx` package, which is not installed")
     logger.close()
+    # the captured graphs (with their RCCL all-reduce nodes at world > 1) go before the communicator
+    tr.close()
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 def load_checkpoint_model(ck) -> torch.nn.Module:

@@ -147,6 +147,11 @@ def sum_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
+def graph_capture(g):
+    from g2048.dist import graph
+    return graph(g)
+
+
 class RolloutBench:
     """Fused random-legal rollout: `chunk` env steps of every board per launch."""
 
@@ -183,12 +188,12 @@ class RolloutBench:
         torch.cuda.current_stream().wait_stream(s)
         self.per_graph = max(1, per_graph)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with graph_capture(self.graph):
             self.launch()
         self.graph_g = self.graph
         if self.per_graph > 1:
             self.graph_g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph_g):
+            with graph_capture(self.graph_g):
                 for _ in range(self.per_graph):
                     self.launch()
 
@@ -251,7 +256,7 @@ def bench_single_step(n, steps, rank, dev, world):
         body()  # warm-up outside capture
     torch.cuda.current_stream().wait_stream(s)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with graph_capture(g):
         body()
     reps = max(1, steps // per_graph)
     g.replay()
@@ -462,7 +467,9 @@ def main():
         from g2048 import benchloop
         result["urm"] = benchloop.bench_urm(args, rank, world, dev)
 
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    # the CPU baseline on rank 0's host cores after every GPU leg (at world > 1 the other ranks wait
+    # at the barrier below, so the timed GPU regions never share the host with it)
+    if rank == 0 and args.cpu_seconds > 0:
         cb = cpu_baselines(args.cpu_seconds)
         py = cb.get("python_1core")
         if py:
@@ -474,6 +481,7 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         import torch.distributed as dist
+        barrier(world)
         dist.destroy_process_group()
 
 

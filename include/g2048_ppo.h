@@ -408,10 +408,14 @@ typedef struct g2048_muon_cfg {
     float momentum, weight_decay, ns_a, ns_b, ns_c, ns_eps;
     int32_t ns_steps, nesterov;
     /* parts > 1 with a workspace: every 196 x 196 / 192 x 192 matrix runs on `parts` blocks (CUs, 7 <=
-     * parts <= 12) that split the row blocks of the Newton-Schulz products and exchange X once per
+     * parts <= 13) that split the row blocks of the Newton-Schulz products and exchange X once per
      * iteration through the workspace (g2048_muon_workspace_bytes(), device memory, ZERO-FILLED ONCE
      * by the caller: each launch leaves its counters zero again).  parts <= 1 or workspace NULL: one
-     * block per matrix. */
+     * block per matrix.  The parts poll each other, so the grid must be resident at once: a device
+     * with fewer CUs than the split grid needs runs every matrix on one block instead.  A poll that
+     * gives up (~0.2 s: a part never became resident) leaves that launch's results garbage and adds
+     * one to the workspace's sticky timeout count (g2048_muon_error_offset()), which only the caller
+     * clears: read it and fail (FusedMuonAdamW.check_errors, with the train step's metrics). */
     int32_t parts;
     int32_t npartials;             /* the clip's sum-of-squares partials: 0 = g2048_grad_sumsq's 64, else
                                     * this many (g2048_colsum_batch_sq's, <= G2048_COLSUM_SQ_MAX) */
@@ -419,6 +423,10 @@ typedef struct g2048_muon_cfg {
 } g2048_muon_cfg;
 
 size_t g2048_muon_workspace_bytes(void);
+
+/* Byte offset in the Muon workspace of the uint32 count of timed-out hand-off waits (sticky across
+ * launches; zero = every multi-CU Newton-Schulz so far was valid). */
+size_t g2048_muon_error_offset(void);
 
 /* 1 if a [rows, cols] matrix fits the one-block-per-matrix Newton-Schulz kernel (min dim <= 224,
  * max dim <= 256, both LDS images <= ~159 KB: h <= 196 for square weights; rows of a length that

@@ -94,6 +94,7 @@ def _worker(rank, world, port, out, model_type="mlp"):
     torch.cuda.synchronize()
     rec["params"] = torch.cat([p.detach().reshape(-1) for p in tr.model.parameters()]).cpu().numpy()
     out[rank] = rec
+    tr.close()  # graphs before the process group (teardown order)
     dist.destroy_process_group()
 
 

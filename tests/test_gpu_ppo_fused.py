@@ -607,6 +607,57 @@ def test_muon_multi_cu_equals_one_cu(dev, h, parts, loaded, monkeypatch):
         assert torch.equal(a, b), (a - b).abs().max()
 
 
+def test_muon_hand_off_timeout_is_reported(dev, monkeypatch):
+    """A multi-CU Newton-Schulz wait that gives up (a part that never became resident: its launch's
+    weights are garbage) is never silent: forced here by a poll limit of 0 (G2048_MUON_SPIN_LIMIT,
+    read at launch), every timed-out wait is counted in the workspace's sticky error word, the
+    optimizer's check raises, and the trainer's metrics read raises with it.  With the word cleared
+    and the default limit, the next launches count nothing and the counters were left consistent (the
+    steps after are bitwise the one-CU result from the same state)."""
+    import agent
+    from g2048.dist import GradBucket
+    from g2048.optim import FusedMuonAdamW
+    monkeypatch.setenv("G2048_MUON_PARTS", "13")
+    torch.manual_seed(196)
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=196, num_layers=2)).to(dev)
+    opt = FusedMuonAdamW(m, 1e-3, 1e-4)
+    assert opt._cfg.parts == 13
+    order = [q for q, _ in opt.muon] + [q for grp in opt.adam_groups for q in grp["params"]]
+    bk = GradBucket(order)
+    err = opt.error_count()
+    assert err is not None and int(err.item()) == 0
+    monkeypatch.setenv("G2048_MUON_SPIN_LIMIT", "0")
+    bk.flat.copy_(torch.randn(bk.flat.shape, generator=torch.Generator().manual_seed(0)).to(dev) * 1e-2)
+    opt.step_clipped(bk.flat, 1.0)
+    torch.cuda.synchronize()
+    n = int(err.item())
+    assert n > 0, "a poll limit of 0 must time out at least one hand-off wait"
+    with pytest.raises(RuntimeError, match="timed out"):
+        opt.check_errors()
+    # clear, default limit: the counters the forced launch left behind are consistent -- two more
+    # multi-CU steps equal the one-CU schedule (G2048_MUON_ONE_CU, read at launch) from the same state
+    monkeypatch.delenv("G2048_MUON_SPIN_LIMIT")
+    err.zero_()
+    snap_p = [q.detach().clone() for q in m.parameters()]
+    snap_o = opt.snapshot()
+    outs = []
+    for one_cu in (False, True):
+        if one_cu:
+            monkeypatch.setenv("G2048_MUON_ONE_CU", "1")
+        with torch.no_grad():
+            for q, s0 in zip(m.parameters(), snap_p):
+                q.copy_(s0)
+        opt.restore(snap_o)
+        for s in range(2):
+            bk.flat.copy_(torch.randn(bk.flat.shape, generator=torch.Generator().manual_seed(10 + s)).to(dev) * 1e-2)
+            opt.step_clipped(bk.flat, 1.0)
+        torch.cuda.synchronize()
+        outs.append(torch.cat([q.detach().reshape(-1) for q in m.parameters()] + [b.reshape(-1) for b in opt.muon_buf]))
+    assert int(err.item()) == 0
+    opt.check_errors()
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
+
+
 @pytest.mark.parametrize("h", [196, 64])
 def test_muon_step_writes_the_head_split(dev, h):
     """FusedMuonAdamW with the head fragment image registered (set_head_frag): after each step the

@@ -88,21 +88,36 @@ def _child():
     rep["trainer_finite"] = all(np.isfinite(x["loss"]) and np.isfinite(x["grad_norm"]) for x in ms)
     rep["trainer_split"] = tr.ppo.graph_split
     torch.cuda.synchronize()
+    print("RCCL_REPORT " + json.dumps(rep), flush=True)  # before the teardown: an abort there keeps it
+    # teardown order: every graph holding a captured all-reduce goes before the communicator
+    up.close()
+    tr.close()
+    del up, tr
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
     dist.destroy_process_group()
-    print("RCCL_REPORT " + json.dumps(rep), flush=True)
+    print("RCCL_TEARDOWN_OK", flush=True)
 
 
 @pytest.mark.gpu
-def test_rccl_world1_captured_allreduce_graph_equals_eager():
+def test_rccl_world1_captured_allreduce_graph_equals_eager(tmp_path):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
                LOCAL_RANK="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
     env["PYTHONPATH"] = os.pathsep.join([str(ROOT / "tests"), str(ROOT), str(PKG), env.get("PYTHONPATH", "")])
-    r = subprocess.run([sys.executable, "-u", __file__, "--child"], env=env, capture_output=True, text=True,
-                       timeout=300)
-    lines = [x for x in r.stdout.splitlines() if x.startswith("RCCL_REPORT ")]
-    if r.returncode != 0 or not lines:  # the child's own words, without the C++ frame dump
-        said = [x for x in (r.stdout + "\n" + r.stderr).splitlines() if x.strip() and not x.startswith("frame #")]
-        pytest.fail(f"RCCL child exited {r.returncode}:\n" + "\n".join(said[-40:]), pytrace=False)
+    # the child's whole stdout / stderr go to a file (kept under gpurun_out/ on the GPU box, so a
+    # failure's full C++ message -- which thread threw, and what -- survives the run)
+    out_dir = ROOT / "gpurun_out" if os.environ.get("GRAFT_REPO_ROOT") else tmp_path
+    out_dir.mkdir(parents=True, exist_ok=True)
+    log = out_dir / "rccl_child_full.log"
+    with open(log, "w") as f:
+        r = subprocess.run([sys.executable, "-u", __file__, "--child"], env=env, stdout=f, stderr=subprocess.STDOUT,
+                           text=True, timeout=300)
+    text = log.read_text()
+    lines = [x for x in text.splitlines() if x.startswith("RCCL_REPORT ")]
+    if r.returncode != 0 or not lines or "RCCL_TEARDOWN_OK" not in text:
+        pytest.fail(f"RCCL child exited {r.returncode} (full log: {log}):\n" + "\n".join(text.splitlines()[-80:]),
+                    pytrace=False)
     rep = json.loads(lines[-1][len("RCCL_REPORT "):])
     print(rep)
     assert rep["backend"] == "nccl" and rep["world"] == 1

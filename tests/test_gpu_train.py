@@ -277,46 +277,78 @@ def test_episodic_trainer_respects_max_steps(dev):
     assert m["samples"] <= 512 * 100
 
 
-def test_ppo_updater_gpu_matches_compat_update(dev):
-    """Tensor-path PPOUpdater (fp32, one minibatch) == list-of-dict model_optimize_step on the same data."""
+def _update_once(dev, u, mode: str, order_seed: int):
+    """One PPO update of GameMLP(h 64, fp32, dropout 0) from torch seed 1234 on the golden update
+    data (train.py:414-642): `tensor` = PPOUpdater on device tensors (rows in the device
+    permutation's order), `compat` = the list-of-dict model_optimize_step (rows in randperm's order).
+    `order_seed` seeds the row order only.  Returns (flat parameters, {name: tensor}, stats)."""
     import agent
     import train
     from g2048 import _lib as L
     from g2048.dist import GradBucket
     from g2048.optim import build_optimizer
     from g2048.ppo import PPOConfig, PPOUpdater
-    u = golden("update.npz")
     n = len(u["actions"])
-    legal = np.array([sum(1 << a for a in range(4) if not u["invalid"][i, a]) for i in range(n)], np.uint8)
-    boards = np.rint(u["obs"][:, 0::3]).astype(np.int8)
-    res = []
-    for mode in ("tensor", "compat"):
-        torch.manual_seed(1234)
-        m = agent.GameMLP(agent.MLPConfig(hidden_dim=64, num_layers=2, dropout=0.0)).to(dev)
-        opt = build_optimizer(m, 1e-3, 1e-4, schedule=False)
-        if mode == "tensor":
-            up = PPOUpdater(m, opt, PPOConfig(batch_size=n, critic=0.2, amp_dtype=None), GradBucket(m.parameters()))
+    torch.manual_seed(1234)
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=64, num_layers=2, dropout=0.0)).to(dev)
+    opt = build_optimizer(m, 1e-3, 1e-4, schedule=False)
+    torch.manual_seed(order_seed)
+    if mode == "tensor":
+        legal = np.array([sum(1 << a for a in range(4) if not u["invalid"][i, a]) for i in range(n)], np.uint8)
+        boards = np.rint(u["obs"][:, 0::3]).astype(np.int8)
+        up = PPOUpdater(m, opt, PPOConfig(batch_size=n, critic=0.2, amp_dtype=None), GradBucket(m.parameters()))
 
-            def enc(b):
-                o = torch.empty(b.shape[0], 48, dtype=torch.float32, device=dev)
-                L.obs_encode(b.contiguous(), o)
-                return o
-            data = {"boards": torch.from_numpy(boards).to(dev), "actions": torch.from_numpy(u["actions"]).to(dev),
-                    "legal": torch.from_numpy(legal).to(dev), "logp": torch.from_numpy(u["old_logprobs"]).to(dev),
-                    "adv": torch.from_numpy(u["advantage"]).to(dev), "ret": torch.from_numpy(u["future_reward"]).to(dev)}
-            st = {k: float(v) for k, v in up.update(data, 0.02, enc).items()}
-        else:
-            moves = [{"game_state": torch.from_numpy(u["obs"][i]), "selected_direction": int(u["actions"][i]),
-                      "action_mask": u["invalid"][i].tolist(), "advantage": float(u["advantage"][i]),
-                      "future_reward": float(u["future_reward"][i]), "policy_logprobs": u["old_logprobs"][i].tolist()}
-                     for i in range(n)]
-            st = train.model_optimize_step(m, [{"moves": moves}], opt, None, 0.02, 0.2, dev, n, 1)
-        res.append((torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy(), st))
-    # one minibatch of all n samples in two different orders (the device permutation vs the
-    # DataLoader's): only the fp32 summation order of the gradients differs
-    np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-4, atol=1e-5)
+        def enc(b):
+            o = torch.empty(b.shape[0], 48, dtype=torch.float32, device=dev)
+            L.obs_encode(b.contiguous(), o)
+            return o
+        data = {"boards": torch.from_numpy(boards).to(dev), "actions": torch.from_numpy(u["actions"]).to(dev),
+                "legal": torch.from_numpy(legal).to(dev), "logp": torch.from_numpy(u["old_logprobs"]).to(dev),
+                "adv": torch.from_numpy(u["advantage"]).to(dev), "ret": torch.from_numpy(u["future_reward"]).to(dev)}
+        st = {k: float(v) for k, v in up.update(data, 0.02, enc).items()}
+    else:
+        moves = [{"game_state": torch.from_numpy(u["obs"][i]), "selected_direction": int(u["actions"][i]),
+                  "action_mask": u["invalid"][i].tolist(), "advantage": float(u["advantage"][i]),
+                  "future_reward": float(u["future_reward"][i]), "policy_logprobs": u["old_logprobs"][i].tolist()}
+                 for i in range(n)]
+        st = train.model_optimize_step(m, [{"moves": moves}], opt, None, 0.02, 0.2, dev, n, 1)
+    named = {k: v.detach().reshape(-1).cpu().numpy().copy() for k, v in m.named_parameters()}
+    return np.concatenate(list(named.values())), named, st
+
+
+def test_ppo_updater_gpu_matches_compat_update(dev):
+    """Tensor-path PPOUpdater (fp32, one minibatch) == list-of-dict model_optimize_step on the same data.
+
+    Where the bound comes from (round-5 analysis of the round-4 flake, 21 of 11 973 parameters off by
+    <= 9.4e-6 under a fixed atol of 2e-6): the two paths see the n rows in different orders, so their
+    fp32 gradient sums differ in the last bits, and torch.optim.Muon's bf16 Newton-Schulz turns that
+    into bf16-rounding-sized differences of the update (lr 1e-3: ~1e-6..1e-5 absolute).  The test
+    measures both facts instead of assuming a number:
+      1. each path, run twice from the same seeds in this process, is BITWISE reproducible (no
+         non-deterministic kernel on either side: a flake cannot come from run-to-run noise);
+      2. the order noise floor: compat runs of 4 other row orders; per parameter tensor, the
+         tensor-vs-compat difference must stay within 2x the largest difference between those runs
+         (+ 1e-7 absolute for tensors the order does not move)."""
+    u = golden("update.npz")
+    t1, tn, ts = _update_once(dev, u, "tensor", 1234)
+    t2, _, _ = _update_once(dev, u, "tensor", 1234)
+    c1, cn, cs = _update_once(dev, u, "compat", 1234)
+    c2, _, _ = _update_once(dev, u, "compat", 1234)
+    det = {"tensor": bool(np.array_equal(t1, t2)), "compat": bool(np.array_equal(c1, c2))}
+    orders = [_update_once(dev, u, "compat", 1000 + k)[1] for k in range(4)]
+    report = {}
+    for name, tv in tn.items():
+        spread = max(float(np.abs(a[name] - b[name]).max()) for i, a in enumerate(orders) for b in orders[i + 1:])
+        diff = float(np.abs(tv - cn[name]).max())
+        report[name] = (diff, spread)
+    print("determinism", det, "| per tensor (tensor-vs-compat max diff, order spread):",
+          {k: (f"{d:.2e}", f"{s:.2e}") for k, (d, s) in report.items()})
+    assert det["tensor"], "PPOUpdater's tensor path is not run-to-run deterministic on this device"
+    assert det["compat"], "model_optimize_step is not run-to-run deterministic on this device"
+    for name, (diff, spread) in report.items():
+        assert diff <= 2.0 * spread + 1e-7, (name, diff, spread)
     for k in ("loss", "policy_loss", "value_loss", "entropy", "grad_norm"):
-        assert math.isclose(res[0][1][k], res[1][1][k], rel_tol=1e-4, abs_tol=1e-6), k
+        assert math.isclose(ts[k], cs[k], rel_tol=1e-4, abs_tol=1e-6), k
 
 
 def test_graphed_update_equals_eager_update(dev):

@@ -8,6 +8,8 @@
 #   TAG=r04x bash tools/gpu/check.sh urm    GameURM: tests, bench leg, kernel trace, torch-op census,
 #                                           SQ passes of the one-launch forward
 #   TAG=r04x bash tools/gpu/check.sh full   every GPU test, smoke, the default bench line
+#   TAG=r05a bash tools/gpu/check.sh muon   Muon: its tests, the MUON_TRACE build (make trace) at 13 and 8
+#                                           parts (phase clocks + bound checks), HIP-event timing
 cd "${GRAFT_REPO_ROOT:-.}"
 TAG=${TAG:-check}
 O=gpurun_out/$TAG; mkdir -p $O
@@ -48,6 +50,16 @@ urm)
   echo "census rc=$?"
   TAG=${TAG}_urmfwd bash tools/pmc_kernel.sh python3 tools/time_urm.py 65536 64 3 > $O/pmc.log 2>&1
   echo "pmc rc=$?"; python3 tools/pmc_table.py gpurun_out/pmck_${TAG}_urmfwd urm_forward 2>&1 | head -30
+  ;;
+muon)
+  run_tests $O/tests.log 300 tests/test_gpu_ppo_fused.py -k "muon or Muon"
+  for p in 13 8; do
+    timeout -k 10 120 python3 tools/trace_muon.py tools/alt/libg2048_mtrace.so $p > $O/trace_muon_$p.log 2>&1
+    rc=$?; echo "trace parts=$p rc=$rc"; grep -c MUON_CHECK $O/trace_muon_$p.log; tail -3 $O/trace_muon_$p.log; fatal $rc trace
+    [ $rc -eq 0 ] || exit 1
+  done
+  timeout -k 10 120 python3 tools/time_muon.py > $O/time_muon.log 2>&1
+  echo "time rc=$?"; head -6 $O/time_muon.log
   ;;
 full)
   run_tests $O/tests.log 700 tests
