@@ -318,12 +318,14 @@ class GameURM(nn.Module):
         o2["params"] = [p for p in o2["params"] if p.ndim == 2]
         return [o2, o1, v2, v1]
 
-    def _loop(self, h: torch.Tensor, emb: torch.Tensor) -> torch.Tensor:
+    def _loop(self, h: torch.Tensor, emb: torch.Tensor, acc=None) -> torch.Tensor:
         hb = None  # bf16 copy of h handed from block to block (device path, bf16 autocast)
         if emb.is_cuda:
             from g2048 import urm as _urm  # h + emb with its bf16 copy in one kernel (g2048_urm.h)
             if _urm.add_cast_supported(h, emb):
-                h, hb = _urm.AddCastFn.apply(h, emb)
+                if acc is not None:
+                    acc.pending += 1
+                h, hb = _urm.AddCastFn.apply(h, emb, acc)
         if hb is None:
             h = h + emb
         last = len(self.layers) - 1
@@ -363,9 +365,17 @@ class GameURM(nn.Module):
                 # autograd history, and reusing them in the loops below would leave every projection
                 # weight without a gradient -- drop them so those loops cast again with history
                 torch.clear_autocast_cache()
+        acc = None
+        if emb.is_cuda and torch.is_grad_enabled() and emb.requires_grad:
+            from g2048 import urm as _urm  # the loops' emb gradient summed in their backward kernels
+            acc = _urm.EmbGradAcc()
         for _ in range(self.config.num_loops - n_trunc):
-            h = self._loop(h, emb)
-        pooled = h.mean(dim=1)
+            h = self._loop(h, emb, acc)
+        if h.is_cuda and torch.is_grad_enabled() and h.requires_grad and h.dim() == 3 and h.shape[1] == N_CELLS:
+            from g2048 import urm as _urm  # its backward hands the last RMSNorm a [b, h] gradient
+            pooled = _urm.MeanPoolFn.apply(h)
+        else:
+            pooled = h.mean(dim=1)
         if pooled.is_cuda:
             from g2048 import urm as _urm  # both heads as one device projection (training, g2048_urm.h)
             if _urm.heads_supported(self, pooled):

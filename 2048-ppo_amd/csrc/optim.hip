@@ -289,6 +289,9 @@ __device__ __forceinline__ void store_block_t(const f32x4_t (&acc)[kBI][kBJ], ch
 // update; returns the sum of squares of ub
 __device__ __forceinline__ float momentum4(const float4 &g4, const float4 &b4, float coef, float mu, bool nesterov,
                                           float bv[4], float ub[4]) {
+    // no fma contraction: the one-CU, generic and multi-CU schedules inline this in different places
+    // and must round identically (their bitwise equality is tested)
+#pragma clang fp contract(off)
     const float gv[4] = {g4.x * coef, g4.y * coef, g4.z * coef, g4.w * coef};
     bv[0] = b4.x;
     bv[1] = b4.y;
@@ -300,7 +303,7 @@ __device__ __forceinline__ float momentum4(const float4 &g4, const float4 &b4, f
         bv[u] = bv[u] + (1.0f - mu) * (gv[u] - bv[u]);                               // buf.lerp_(g, 1 - mu)
         const float up = nesterov ? bv[u] - (bv[u] - gv[u]) * (1.0f - mu) : bv[u];  // g.lerp(buf, mu)
         ub[u] = round_bf(up);
-        ss += ub[u] * ub[u];
+        ss = __builtin_fmaf(ub[u], ub[u], ss);  // explicit: the same rounding wherever this is inlined
     }
     return ss;
 }
@@ -355,20 +358,6 @@ __device__ __forceinline__ float muon_prologue(const float *__restrict__ grad, f
         }
     }
     return ss;
-}
-
-// The new momentum of rows [r0, r1) (C % 4 == 0), recomputed from the gradient and the old momentum
-// exactly as muon_prologue computes it: a multi-CU part writes its rows only after every part has
-// read the old momentum of all rows for its image (the momentum is read by all, written by one).
-__device__ __forceinline__ void muon_momentum_rows(const float *__restrict__ grad, float *__restrict__ mom, int C,
-                                                   float coef, float mu, bool nesterov, int r0, int r1, int tid) {
-    const int e0 = (r0 * C) >> 2, e1 = (r1 * C) >> 2;
-    for (int e4 = e0 + tid; e4 < e1; e4 += kMuonThreads) {
-        const float4 g4 = reinterpret_cast<const float4 *>(grad)[e4], b4 = reinterpret_cast<const float4 *>(mom)[e4];
-        float bv[4], ub[4];
-        momentum4(g4, b4, coef, mu, nesterov, bv, ub);
-        reinterpret_cast<float4 *>(mom)[e4] = make_float4(bv[0], bv[1], bv[2], bv[3]);
-    }
 }
 
 __device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_t *__restrict__ pbf, const char *sX,
@@ -923,7 +912,7 @@ __device__ __forceinline__ bool mc_wait(gu32_t *ctr, uint32_t target, gu32_t *er
 
 template <int N, int RB>
 __device__ __forceinline__ void ns_square_mc_rb(char *sX, char *sG, const MuonArgs &args, int mat, int part, int np,
-                                                int wave, int lane) {
+                                                int wave, int lane, uint32_t ctr0) {
     using S = McShape<N>;
     constexpr int P = S::P;
     const int tid = threadIdx.x, g = lane >> 4, c = lane & 15;
@@ -980,7 +969,8 @@ __device__ __forceinline__ void ns_square_mc_rb(char *sX, char *sG, const MuonAr
         __syncthreads();
         MUON_TP(args);
         if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (wave == 0) mc_wait(ctr, (uint32_t)(np * (it + 1)), err, (gu32_t *)(args.sync + kMuonErrWord), args.spin_limit);
+        if (wave == 0)
+            mc_wait(ctr, ctr0 + (uint32_t)(np * (it + 1)), err, (gu32_t *)(args.sync + kMuonErrWord), args.spin_limit);
         __syncthreads();
         MUON_TP(args);
         // the whole X' (every block's rows, padding columns zero) into the LDS image: every load in
@@ -1012,11 +1002,123 @@ __device__ __forceinline__ void ns_square_mc_rb(char *sX, char *sG, const MuonAr
 
 template <int N>
 __device__ __forceinline__ void ns_square_mc(char *sX, char *sG, const MuonArgs &args, int mat, int part, int np,
-                                             int wave, int lane) {
+                                             int wave, int lane, uint32_t ctr0) {
     constexpr int NT = McShape<N>::NT;
     const int rb = (part + 1) * NT / np - part * NT / np;  // block-uniform; the host picks np >= NT / 2
-    if (rb == 1) ns_square_mc_rb<N, 1>(sX, sG, args, mat, part, np, wave, lane);
-    else ns_square_mc_rb<N, 2>(sX, sG, args, mat, part, np, wave, lane);
+    if (rb == 1) ns_square_mc_rb<N, 1>(sX, sG, args, mat, part, np, wave, lane, ctr0);
+    else ns_square_mc_rb<N, 2>(sX, sG, args, mat, part, np, wave, lane, ctr0);
+}
+
+
+// ---- the update's sum of squares of a square 196 / 192 matrix, in ONE order for every schedule
+// (one CU, generic, multi-CU): per 16-row tile row t, thread i < 16 N / 4 holds float4 i of the tile
+// row (momentum4's fma order), the block sum is a fixed tree (wave xor butterfly, lane 0 of each
+// wave, the waves in order), and the tile-row sums are added in tile order.  A multi-CU part
+// computes the sums of its own tile rows only and publishes them with its rows of X.
+
+// lane 0's butterfly sum per wave, the waves in order: the same value in every thread
+__device__ __forceinline__ float block_sum_fixed(float v, float *red, int tid) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((tid & 63) == 0) red[tid >> 6] = v;
+    __syncthreads();
+    float t = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kMuonWaves; w++) t += red[w];
+    __syncthreads();
+    return t;
+}
+
+// the new momentum and the bf16 update of float4 e of a row-major [N, N] matrix: momentum stored,
+// the update's 8 bf16 bytes returned, its fma-ordered sum of squares in ss
+__device__ __forceinline__ uint2 momentum_q(const float4 &g4, const float4 &b4, float *mom, int e, float coef,
+                                            float mu, bool nesterov, float &ss) {
+    float bv[4], ub[4];
+    ss = momentum4(g4, b4, coef, mu, nesterov, bv, ub);
+    reinterpret_cast<float4 *>(mom)[e] = make_float4(bv[0], bv[1], bv[2], bv[3]);
+    return make_uint2(pack_bf2(ub[0], ub[1]), pack_bf2(ub[2], ub[3]));
+}
+
+// One CU: the momentum of the whole square matrix, its bf16 update into the LDS image X (pitch P),
+// and the sum of squares in tile-row order (four tile rows of loads in flight per batch).
+template <int N>
+__device__ __forceinline__ float tile_prologue(const float *__restrict__ grad, float *__restrict__ mom, char *sX,
+                                               float coef, float mu, bool nesterov, float *red, int tid) {
+    constexpr int P = muon_pitch(N, N), NT = (N + 15) / 16, C4 = N / 4, TR4 = 16 * C4;
+    float total = 0.0f;
+    for (int t0 = 0; t0 < NT; t0 += 4) {
+        float4 g4[4], b4[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int e = (t0 + u) * TR4 + tid;
+            const bool ok = t0 + u < NT && tid < TR4 && e < N * C4;
+            g4[u] = ok ? reinterpret_cast<const float4 *>(grad)[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+            b4[u] = ok ? reinterpret_cast<const float4 *>(mom)[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (t0 + u >= NT) break;  // block-uniform
+            const int e = (t0 + u) * TR4 + tid;
+            float ss = 0.0f;
+            if (tid < TR4 && e < N * C4) {
+                const uint2 q = momentum_q(g4[u], b4[u], mom, e, coef, mu, nesterov, ss);
+                const int row = e / C4, j0 = 4 * (e - row * C4);
+                *reinterpret_cast<uint2 *>(sX + row * P + 2 * j0) = q;
+            }
+            total += block_sum_fixed(ss, red, tid);
+        }
+    }
+    return total;
+}
+
+// X /= max(bf16(sqrt(ss)), eps) over the flat LDS image of nbytes (the zero padding stays zero): 4
+// elements per access, four 8-byte groups per thread in flight per pass.  The quotient of the uniform
+// divisor: q0 = y (1/nrm), one fma residual, one fma correction -- the correctly rounded fp32 y / nrm
+// for every pair of bf16 operands (all 128 x 128 significand pairs checked exactly,
+// tools/check_bf16_division.py), zeros passed through with their sign
+__device__ __forceinline__ void normalise_image(char *sX, int nbytes, float nrm, int tid) {
+    const float inv = 1.0f / nrm;
+    auto qdiv = [&](float y) {
+        const float q0 = y * inv;
+        const float q = __builtin_fmaf(__builtin_fmaf(-q0, nrm, y), inv, q0);
+        return y == 0.0f ? y : q;
+    };
+    const int n8 = nbytes >> 3;
+    uint2 *img = reinterpret_cast<uint2 *>(sX);
+    for (int e0 = tid; e0 < n8; e0 += 4 * kMuonThreads) {
+        uint2 w[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int e = e0 + u * kMuonThreads;
+            w[u] = e < n8 ? img[e] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int e = e0 + u * kMuonThreads;
+            if (e < n8)
+                img[e] = make_uint2(pack_bf2(qdiv(bf2f(w[u].x & 0xFFFFu)), qdiv(bf2f(w[u].x >> 16))),
+                                    pack_bf2(qdiv(bf2f(w[u].y & 0xFFFFu)), qdiv(bf2f(w[u].y >> 16))));
+        }
+    }
+}
+
+// the whole N x P-byte global image `src` into the LDS image (sc1 buffer loads: every load in flight
+// before the first LDS store; offsets past N * P read zero by the descriptor's record count)
+template <int N>
+__device__ __forceinline__ void mc_copy_image(char *sX, const char *src, int tid) {
+    constexpr int P = McShape<N>::P;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(src), (short)0, N * P, 0x00020000);
+    constexpr int kCopy = (N * P / 16 + kMuonThreads - 1) / kMuonThreads;
+    constexpr int kSc1 = 16;  // cache-policy bit of the buffer load: sc1
+    uint4 cv[kCopy];
+#pragma unroll
+    for (int u = 0; u < kCopy; u++)
+        cv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, (tid + u * kMuonThreads) * 16, 0, kSc1));
+#pragma unroll
+    for (int u = 0; u < kCopy; u++) {
+        const int o = (tid + u * kMuonThreads) * 16;
+        if (o < N * P) *reinterpret_cast<uint4 *>(sX + o) = cv[u];
+    }
 }
 
 // The AdamW update of the 1-D groups by block b of nb (clip coefficient from the partials).
@@ -1068,6 +1170,102 @@ __device__ __forceinline__ float block_clip_coef(const MuonArgs &args, int tid, 
     return s_coef;
 }
 
+// A split square matrix (h = 196 / 192) on part `part` of np blocks, the whole job:
+//   prologue  this part's tile rows only: gradient + old momentum (loads issued before the clip
+//             coefficient's read), the new momentum written back at once (no other part reads these
+//             rows), the bf16 update rows into exchange image 1 and the tile rows' sums of squares
+//             into the matrix's sync line -- hand-off 0 -- then every part copies the whole image,
+//             sums the NT tile-row sums in order and normalises (the one-CU arithmetic:
+//             tile_prologue + normalise_image)
+//   Newton-Schulz  ns_square_mc_rb, hand-offs 1 .. steps - 1 (image 0, 1, 0, ...)
+//   epilogue  this part's parameter rows, then the counters back to zero by the last part.
+// The old path read the whole gradient and momentum on every part (308 KB per part for h = 196) and
+// wrote its momentum rows only after a second counter said every part had read them.
+template <int N>
+__device__ __forceinline__ void mc_matrix(char *smem, float *red, const MuonArgs &args, const MuonMat &mt, int mat,
+                                          int part, int np, int tid, int wave, int lane) {
+    using S = McShape<N>;
+    constexpr int P = S::P, NT = S::NT, C4 = N / 4, TR4 = 16 * C4;
+    constexpr int PAD8 = (P / 2 - N) / 4;  // 8-byte zero groups of a row's padding columns
+    char *sX = smem;
+    char *sG = smem + ((N * P + 127) & ~127);
+    const int t0 = part * NT / np, rb = (part + 1) * NT / np - t0;  // this part's tile rows (1 or 2)
+    gu32_t *line = (gu32_t *)(args.sync + 16 * mat);  // [0] exchange counter [1] timeout flag [2] done [3 + t] tile-row ss
+    gu32_t *errors = (gu32_t *)(args.sync + kMuonErrWord);
+    char *xg = args.xg + mat * args.xg_stride;
+    char *img1 = xg + N * P;
+    // own rows' gradient and momentum in flight first
+    float4 g4[2], b4[2];
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        const int e = (t0 + x) * TR4 + tid;
+        const bool ok = x < rb && tid < TR4 && e < N * C4;
+        g4[x] = ok ? reinterpret_cast<const float4 *>(mt.grad)[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+        b4[x] = ok ? reinterpret_cast<const float4 *>(mt.mom)[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    {  // zero both LDS images (their K padding must read as zero)
+        const int bytes = (int)(sG - smem) + ((N * P + 127) & ~127);
+        for (int o = tid * 16; o < bytes; o += kMuonThreads * 16) *reinterpret_cast<uint4 *>(smem + o) = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    const float coef = block_clip_coef(args, tid, blockIdx.x == 0);
+    MUON_TP(args);
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        if (x >= rb) break;  // block-uniform
+        const int e = (t0 + x) * TR4 + tid;
+        float ss = 0.0f;
+        if (tid < TR4 && e < N * C4) {
+            const uint2 q = momentum_q(g4[x], b4[x], mt.mom, e, coef, args.momentum, args.nesterov != 0, ss);
+            const int row = e / C4, j0 = 4 * (e - row * C4);
+            __hip_atomic_store((gu64_t *)(img1 + row * P + 2 * j0), (uint64_t)q.x | ((uint64_t)q.y << 32),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through (the hand-off)
+        } else if (tid >= TR4 && tid < TR4 + 16 * PAD8) {  // the rows' padding columns stay zero
+            const int k = tid - TR4, row = 16 * (t0 + x) + k / PAD8;
+            if (row < N)
+                __hip_atomic_store((gu64_t *)(img1 + row * P + 2 * N + 8 * (k % PAD8)), (uint64_t)0,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const float tss = block_sum_fixed(ss, red, tid);
+        if (tid == 0) __hip_atomic_store(line + 3 + t0 + x, __float_as_uint(tss), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    MUON_TP(args);
+    // hand-off 0: every storing wave drains, the barrier, one lane adds; one wave polls
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(line, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == 0) mc_wait(line, (uint32_t)np, line + 1, errors, args.spin_limit);
+    __syncthreads();
+    MUON_TP(args);
+    mc_copy_image<N>(sX, img1, tid);
+    float total = 0.0f;
+#pragma unroll
+    for (int t = 0; t < NT; t++)
+        total += __uint_as_float(__hip_atomic_load(line + 3 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    __syncthreads();
+    normalise_image(sX, N * P, fmaxf(round_bf(sqrtf(total)), args.eps), tid);  // x.norm() of the bf16 X, clamped
+    __syncthreads();
+    MUON_TP(args);
+    ns_square_mc<N>(sX, sG, args, mat, part, np, wave, lane, (uint32_t)np);
+    // decoupled weight decay + the match_rms_adamw-scaled update of this part's rows, bf16 copies
+    const float lr = args.lr[mt.lr_index];
+    const float step = lr * (0.2f * sqrtf((float)N));
+    muon_epilogue(mt.param, mt.pbf, sX, P, N, N, false, 1.0f - lr * args.wd, step, tid, 16 * t0, 16 * (t0 + rb));
+    // the last part through here puts the matrix's counters back to zero for the next launch (no
+    // memset node per step): every other part has finished all its polls when it counts in.  The
+    // done add is a release (this part's counter adds, same thread, happen before it) and the last
+    // arriver acquires before its reset stores, so the reset is ordered after every part's adds by
+    // the memory model, not by the order L2 happens to apply atomics in.
+    if (tid == 0) {
+        gu32_t *done = line + 2;
+        if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(np - 1)) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __hip_atomic_store(line, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint8_t role = args.job_mat[blockIdx.x];
@@ -1091,6 +1289,13 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     MUON_TP(args);
     __shared__ float red[kMuonThreads / 64];
     __shared__ float s_norm;
+    if (np > 1) {  // a part of a split square matrix (the host only splits h = 196 / 192)
+        if (r == 196) mc_matrix<196>(smem, red, args, mt, mat, part, np, tid, wave, lane);
+        else mc_matrix<192>(smem, red, args, mt, mat, part, np, tid, wave, lane);
+        __syncthreads();
+        MUON_TP(args);
+        return;
+    }
     // zero both images (their K padding must read as zero) and the zero block
     {
         const int bytes = (int)(zero - smem) + 64;
@@ -1100,57 +1305,31 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
 
     const float coef = block_clip_coef(args, tid, blockIdx.x == 0);
     MUON_TP(args);
-    // a multi-CU part (square: tr false) owns the momentum / parameter rows of its tile rows
-    const int NT = (r + 15) >> 4;
-    const int own0 = np > 1 ? 16 * (part * NT / np) : 0, own1 = np > 1 ? 16 * ((part + 1) * NT / np) : R;
-    // (multi-CU: no momentum write-back here -- the other parts may not have read those rows yet)
-    float ss = muon_prologue(mt.grad, mt.mom, sX, px, R, C, tr, coef, args.momentum, args.nesterov != 0, tid,
-                             np > 1 ? 0 : own0, np > 1 ? 0 : own1);
-    MUON_TP(args);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
-    if (lane == 0) red[wave] = ss;
-    __syncthreads();
-    if (tid == 0) {
-        float t = 0.0f;
-        for (int w = 0; w < kMuonThreads / 64; w++) t += red[w];
-        s_norm = fmaxf(round_bf(sqrtf(t)), args.eps);  // x.norm() of a bf16 tensor, clamp(min=eps)
+    const bool sq196 = !tr && R == C && (R == 196 || R == 192);  // the multi-CU schedule's sum order
+    float ss = 0.0f;
+    if (sq196) {
+        const float t = R == 196 ? tile_prologue<196>(mt.grad, mt.mom, sX, coef, args.momentum, args.nesterov != 0, red, tid)
+                                 : tile_prologue<192>(mt.grad, mt.mom, sX, coef, args.momentum, args.nesterov != 0, red, tid);
+        if (tid == 0) s_norm = fmaxf(round_bf(sqrtf(t)), args.eps);
+    } else {
+        ss = muon_prologue(mt.grad, mt.mom, sX, px, R, C, tr, coef, args.momentum, args.nesterov != 0, tid);
     }
-    __syncthreads();
-    const float nrm = s_norm;
-    // X /= ||X|| over the flat image (the zero padding stays zero): 4 elements per access.  The
-    // quotient of the uniform divisor: q0 = y (1/nrm), one fma residual, one fma correction -- the
-    // correctly rounded fp32 y / nrm for every pair of bf16 operands (all 128 x 128 significand
-    // pairs checked exactly, tools/check_bf16_division.py), zeros passed through with their sign
-    const float inv = 1.0f / nrm;
-    auto qdiv = [&](float y) {
-        const float q0 = y * inv;
-        const float q = __builtin_fmaf(__builtin_fmaf(-q0, nrm, y), inv, q0);
-        return y == 0.0f ? y : q;
-    };
-    {  // four 8-byte groups per thread in flight per pass (one LDS round trip per pass, not per group)
-        const int n8 = (r * px) >> 3;
-        uint2 *img = reinterpret_cast<uint2 *>(sX);
-        for (int e0 = tid; e0 < n8; e0 += 4 * kMuonThreads) {
-            uint2 w[4];
+    MUON_TP(args);
+    if (!sq196) {
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int e = e0 + u * kMuonThreads;
-                w[u] = e < n8 ? img[e] : make_uint2(0u, 0u);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int e = e0 + u * kMuonThreads;
-                if (e < n8)
-                    img[e] = make_uint2(pack_bf2(qdiv(bf2f(w[u].x & 0xFFFFu)), qdiv(bf2f(w[u].x >> 16))),
-                                        pack_bf2(qdiv(bf2f(w[u].y & 0xFFFFu)), qdiv(bf2f(w[u].y >> 16))));
-            }
+        for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+        if (lane == 0) red[wave] = ss;
+        __syncthreads();
+        if (tid == 0) {
+            float t = 0.0f;
+            for (int w = 0; w < kMuonThreads / 64; w++) t += red[w];
+            s_norm = fmaxf(round_bf(sqrtf(t)), args.eps);  // x.norm() of a bf16 tensor, clamp(min=eps)
         }
     }
     __syncthreads();
+    normalise_image(sX, r * px, s_norm, tid);
+    __syncthreads();
     MUON_TP(args);
-    gu32_t *pro = np > 1 ? (gu32_t *)(args.sync + 16 * mat + 3) : nullptr;  // parts done reading the momentum
-    if (pro && tid == 0) __hip_atomic_fetch_add(pro, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
     // Newton-Schulz, three products per iteration, all through ONE gemm/store code path:
     //   0: G = X X^T                      (A = X rows, B^T = X rows; G symmetric)
@@ -1158,10 +1337,7 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     //   2: X^T = a X^T + X^T U            (A = X^T by the transposing read, B^T = U rows)
     // Every product stores its transpose (= G, U, and X itself for phase 2).
     const int kind = r == c && !args.generic_ns ? ns_square_kind(r) : 0;
-    if (np > 1) {  // the square matrix over np blocks (the host only splits h = 196 / 192)
-        if (r == 196) ns_square_mc<196>(sX, sG, args, mat, part, np, wave, lane);
-        else ns_square_mc<192>(sX, sG, args, mat, part, np, wave, lane);
-    } else if (kind) {  // the square fast path (row pitch muon_pitch(n, n))
+    if (kind) {  // the square fast path (row pitch muon_pitch(n, n))
         switch (kind) {
         case 1: ns_square<196>(sX, sG, args, wave, lane); break;
         case 2: ns_square<192>(sX, sG, args, wave, lane); break;
@@ -1193,28 +1369,7 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     // decoupled weight decay + the match_rms_adamw-scaled update, and the bf16 weight copy
     const float lr = args.lr[mt.lr_index];
     const float step = lr * (0.2f * sqrtf((float)(R > C ? R : C)));
-    muon_epilogue(mt.param, mt.pbf, sX, px, R, C, tr, 1.0f - lr * args.wd, step, tid, own0, own1, mt.frag, mt.frag_row);
-    if (pro) {  // this part's momentum rows, once every part has read the old ones
-        if (wave == 0)
-            mc_wait(pro, (uint32_t)np, (gu32_t *)(args.sync + 16 * mat + 1), (gu32_t *)(args.sync + kMuonErrWord),
-                    args.spin_limit);
-        __syncthreads();
-        muon_momentum_rows(mt.grad, mt.mom, C, coef, args.momentum, args.nesterov != 0, own0, min(own1, R), tid);
-        // the last part through here puts the matrix's counters back to zero for the next launch
-        // (no memset node per step): every other part has finished all its polls when it counts in.
-        // The done add is a release (this part's ctr / pro adds, same thread, happen before it) and
-        // the last arriver acquires before its reset stores, so the reset is ordered after every
-        // part's counter adds by the memory model, not by the order L2 happens to apply atomics in.
-        if (tid == 0) {
-            gu32_t *ctr = (gu32_t *)(args.sync + 16 * mat), *done = (gu32_t *)(args.sync + 16 * mat + 2);
-            if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(np - 1)) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(pro, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
+    muon_epilogue(mt.param, mt.pbf, sX, px, R, C, tr, 1.0f - lr * args.wd, step, tid, 0, R, mt.frag, mt.frag_row);
     __syncthreads();
     MUON_TP(args);
 }

@@ -17,6 +17,7 @@
 // fp32 arithmetic throughout (bf16 only as GEMM operands / attention probabilities, like torch's
 // bf16 autocast of the same module); parity vs the fp32 module in tests/test_gpu_urm.py.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 
 #include <cstdint>
 
@@ -411,44 +412,85 @@ __device__ __forceinline__ float dpp_prev_token(float v) {  // lane t-1 of the 1
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+// The staged W image of a projection with K <= 32 KS (round 5): rows unpadded with their 16-byte
+// chunks XOR-swizzled by the row (mask SW) where that makes the fragment reads (lane (t, g): row
+// 16 ct + t, chunk 4 s + g) conflict-free in every ds_read_b128 lane group (KS 2 / 6: mask 7, KS 4 /
+// 8: mask 15); the other K keep the padded pitch 32 KS + 8.  Values unchanged: bitwise the same MFMAs.
+template <int KS>
+struct LinW {
+    static constexpr int SW = (KS == 2 || KS == 6) ? 7 : (KS == 4 || KS == 8) ? 15 : 0;
+    static constexpr int PITCH = SW ? 32 * KS : 32 * KS + 8;  // bf16 per staged row
+    // byte offset of the 8-byte piece c4 (bf16 4 c4 .. + 3) of staged row q
+    static __device__ __forceinline__ int piece(int q, int c4) {
+        return q * PITCH * 2 + ((((c4 >> 1) ^ (q & SW)) << 4) | ((c4 & 1) << 3));
+    }
+    // byte offset of lane (t, g)'s A fragment of k-step s in the row block of tile 0
+    static __device__ __forceinline__ int frag(int t, int g, int s) { return t * PITCH * 2 + (((4 * s + g) ^ (t & SW)) << 4); }
+};
+
 template <int KS, int CT, int EPI>
 __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__restrict__ in,
                                                               const uint16_t *__restrict__ w, int64_t rows, int K,
                                                               int N, int inter, uint16_t *__restrict__ y,
                                                               float *__restrict__ x, const float *__restrict__ emb,
                                                               uint16_t *__restrict__ xb, float eps,
-                                                              const float *__restrict__ cw,
-                                                              const float *__restrict__ cb,
-                                                              float *__restrict__ rstd) {
+                                                              const float *__restrict__ cw_g,
+                                                              const float *__restrict__ cb_g,
+                                                              float *__restrict__ rstd, int wt) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int kPitch = 32 * KS + 8;  // bf16 per staged row
+    constexpr int kPitch = LinW<KS>::PITCH;  // bf16 per staged row
     constexpr int kRowsW = 16 * CT;
     constexpr int kLinWBytes = kRowsW * kPitch * 2;
     // per-wave LDS tile of EPI_STORE: the 16-row bf16 output (staging the fp32 residual stream of
     // EPI_RMS the same way measured slower: 194 -> 213 us for o_proj)
     constexpr int kLinTileBytes = EPI == EPI_STORE ? 16 * (2 * 16 * CT + 8) : 0;
+    constexpr bool kSwi = EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_T;
     const int tid = threadIdx.x;
     for (int e = tid; e < kRowsW * kPitch / 8; e += kThreads) reinterpret_cast<uint4 *>(smem)[e] = make_uint4(0u, 0u, 0u, 0u);
+    // the SwiGLU epilogues' conv taps w [inter][2] and biases [inter], staged once per block (zero past
+    // inter): 16-byte LDS reads whatever the parameters' alignment in global memory (an optimizer may
+    // re-home them into a flat buffer at any 4-byte offset)
+    float *s_cw = reinterpret_cast<float *>(smem + kLinWBytes), *s_cb = s_cw + kRowsW;
+    if constexpr (kSwi) {
+        for (int e = tid; e < kRowsW / 2; e += kThreads) {
+            const bool ok = e < inter;
+            s_cw[2 * e] = ok ? cw_g[2 * e] : 0.0f;
+            s_cw[2 * e + 1] = ok ? cw_g[2 * e + 1] : 0.0f;
+            s_cb[e] = ok ? cb_g[e] : 0.0f;
+        }
+    }
+    const float *cw = kSwi ? s_cw : cw_g, *cb = kSwi ? s_cb : cb_g;
     __syncthreads();
-    {   // staged row q <- W row src(q) (EPI_SWIGLU: gate rows at q < kRowsW / 2, up rows above)
+    if (wt) {  // w given as the [K, N] row-major matrix whose transpose is staged (dX = dY W, no W^T copy)
+        for (int e = tid; e < N * (K >> 2); e += kThreads) {
+            const int q = e % N, c4 = e / N;  // 4 consecutive k of output row q: 2-byte gathers of column q
+            const uint16_t *src = w + (int64_t)(4 * c4) * N + q;
+            const uint32_t lo = (uint32_t)src[0] | ((uint32_t)src[N] << 16);
+            const uint32_t hi = (uint32_t)src[2 * N] | ((uint32_t)src[3 * N] << 16);
+            *reinterpret_cast<uint2 *>(smem + LinW<KS>::piece(q, c4)) = make_uint2(lo, hi);
+        }
+    } else {   // staged row q <- W row src(q) (EPI_SWIGLU: gate rows at q < kRowsW / 2, up rows above)
         const int k4 = K >> 2;
         for (int e = tid; e < kRowsW * k4; e += kThreads) {
             const int q = e / k4, c4 = e - q * k4;
             int src = q;
-            if (EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_T) {
+            if (kSwi) {
                 const int hq = q - kRowsW / 2;
                 src = q < kRowsW / 2 ? (q < inter ? q : -1) : (hq < inter ? inter + hq : -1);
             } else if (q >= N) {
                 src = -1;
             }
             if (src >= 0)
-                *reinterpret_cast<uint2 *>(smem + (q * kPitch + 4 * c4) * 2) =
+                *reinterpret_cast<uint2 *>(smem + LinW<KS>::piece(q, c4)) =
                     *reinterpret_cast<const uint2 *>(w + (int64_t)src * K + 4 * c4);
         }
     }
     __syncthreads();
     const int lane = tid & 63, wave = tid >> 6, t = lane & 15, g = lane >> 4;
     const int64_t boards = rows >> 4;
+    int wo[KS];
+#pragma unroll
+    for (int s = 0; s < KS; s++) wo[s] = LinW<KS>::frag(t, g, s);
     for (int64_t bd = (int64_t)blockIdx.x * (kThreads / 64) + wave; bd < boards; bd += (int64_t)gridDim.x * (kThreads / 64)) {
         const int64_t r = bd * 16 + t;
         const uint16_t *xr = in + r * K;
@@ -468,16 +510,15 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
         f32x4 acc[CT];
 #pragma unroll
         for (int ct = 0; ct < CT; ct++) acc[ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        const char *base = smem + (t * kPitch + 8 * g) * 2;
         bf16x8 fa[2][KS];
 #pragma unroll
-        for (int s = 0; s < KS; s++) fa[0][s] = *reinterpret_cast<const bf16x8 *>(base + 64 * s);
+        for (int s = 0; s < KS; s++) fa[0][s] = *reinterpret_cast<const bf16x8 *>(smem + wo[s]);
 #pragma unroll
         for (int ct = 0; ct < CT; ct++) {
             if (ct + 1 < CT) {
 #pragma unroll
                 for (int s = 0; s < KS; s++)
-                    fa[(ct + 1) & 1][s] = *reinterpret_cast<const bf16x8 *>(base + 16 * (ct + 1) * kPitch * 2 + 64 * s);
+                    fa[(ct + 1) & 1][s] = *reinterpret_cast<const bf16x8 *>(smem + 16 * (ct + 1) * kPitch * 2 + wo[s]);
             }
             asm volatile("" ::: "memory");
 #pragma unroll
@@ -675,24 +716,25 @@ inline LinShape lin_shape(int K, int N, int inter, int epi) {
 template <int KS, int CT, int EPI>
 int launch_lin(hipStream_t s, const uint16_t *in, const uint16_t *w, int64_t rows, int K, int N, int inter,
                uint16_t *y, float *x, const float *emb, uint16_t *xb, float eps, const float *cw, const float *cb,
-               float *rstd) {
+               float *rstd, int wt) {
     const size_t tile = EPI == EPI_STORE ? 16 * (2 * 16 * CT + 8) : 0;
-    const size_t lds = (size_t)16 * CT * (32 * KS + 8) * 2 + (size_t)(kThreads / 64) * tile;
+    const size_t conv = (EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_T) ? (size_t)16 * CT * 2 * 4 : 0;  // w + b per channel
+    const size_t lds = (size_t)16 * CT * LinW<KS>::PITCH * 2 + std::max((size_t)(kThreads / 64) * tile, conv);
     int64_t grid = ((rows >> 4) + (kThreads / 64) - 1) / (kThreads / 64);
     grid = grid > 1024 ? 1024 : grid;  // persistent over boards; W staged once per block
     hipLaunchKernelGGL((urm_linear_kernel<KS, CT, EPI>), dim3((unsigned)grid), dim3(kThreads), lds, s, in, w, rows, K, N,
-                       inter, y, x, emb, xb, eps, cw, cb, rstd);
+                       inter, y, x, emb, xb, eps, cw, cb, rstd, wt);
     return launch_status();
 }
 
 // the instantiated shapes: GameURMConfig h = 64 (inter 120) and h = 32 (inter 64, the golden config)
 int dispatch_lin(hipStream_t s, int epi, const uint16_t *in, const uint16_t *w, int64_t rows, int K, int N, int inter,
                  uint16_t *y, float *x, const float *emb, uint16_t *xb, float eps, const float *cw, const float *cb,
-                 bool dry, float *rstd = nullptr) {
+                 bool dry, float *rstd = nullptr, int wt = 0) {
     const LinShape sh = lin_shape(K, N, inter, epi);
 #define G2048_LIN(EPI_, KS_, CT_)                                                                              \
     if (epi == EPI_ && sh.ks == KS_ && sh.ct == CT_)                                                            \
-        return dry ? G2048_OK : launch_lin<KS_, CT_, EPI_>(s, in, w, rows, K, N, inter, y, x, emb, xb, eps, cw, cb, rstd);
+        return dry ? G2048_OK : launch_lin<KS_, CT_, EPI_>(s, in, w, rows, K, N, inter, y, x, emb, xb, eps, cw, cb, rstd, wt);
     G2048_LIN(EPI_STORE, 2, 12)   // h 64 qkv
     G2048_LIN(EPI_STORE, 1, 6)    // h 32 qkv
     // the training Functions' plain projections (URMLinearFn / GateUpSwiGLUFn): the forwards of
@@ -745,8 +787,12 @@ int dispatch_lin(hipStream_t s, int epi, const uint16_t *in, const uint16_t *w, 
 // (16-byte fragment reads); wave-local s_waitcnt + wave barrier order the lanes' LDS accesses.
 namespace mk {
 constexpr int H = 64, QKV = 192, INTER = 120, GU = 256, KD = 128;
-constexpr int P64 = H + 8;     // bf16 pitch of K = 64 weight rows (36 dwords: conflict-free)
-constexpr int PD = KD + 8;     // bf16 pitch of the down-proj rows (68 dwords)
+// Weight rows padded to 36 / 68 dwords.  (Round 5 measured the alternative: unpadded rows with their
+// 16-byte chunks XOR-swizzled by the row, conflict-free fragment reads in every ds_read_b128 lane
+// group by the bank model -- the forward got SLOWER, 2.23 -> 2.36 ms per 65 536 boards: the LDS
+// conflicts are not what bounds it at two waves per SIMD, the extra addressing registers spilled.)
+constexpr int P64 = H + 8;     // bf16 pitch of K = 64 weight rows
+constexpr int PD = KD + 8;     // bf16 pitch of the down-proj rows
 constexpr int OFF_QKV = 0;
 constexpr int OFF_O = OFF_QKV + QKV * P64 * 2;
 constexpr int OFF_GU = OFF_O + H * P64 * 2;
@@ -1252,15 +1298,20 @@ __global__ __launch_bounds__(256) void urm_rms_res_fwd_kernel(const float *__res
     }
 }
 
+// dpool (optional, instead of dout): the mean-pool's gradient [rows / 16, 64], broadcast over the 16
+// token rows of each board (GameURM.forward's h.mean(dim=1), game.py:1450, whose backward is
+// dpooled / 16 expanded): never materialised as a [rows, 64] tensor
 template <bool ABF>
 __global__ __launch_bounds__(256) void urm_rms_res_bwd_kernel(const float *__restrict__ dout, const float *__restrict__ out,
                                                               const float *__restrict__ rstd, float *__restrict__ dh,
                                                               void *__restrict__ da, int64_t rows,
-                                                              const uint16_t *__restrict__ doutb) {
+                                                              const uint16_t *__restrict__ doutb,
+                                                              const float *__restrict__ dpool) {
     const int lane = threadIdx.x & 15;
     const int64_t stride = (int64_t)gridDim.x * 16;
     for (int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); r < rows; r += stride) {
         float4 g = dout ? reinterpret_cast<const float4 *>(dout + r * 64)[lane] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (dpool) g = reinterpret_cast<const float4 *>(dpool + (r >> 4) * 64)[lane];
         if (doutb) {  // + the bf16 copy's gradient (autocast's cast backward: to fp32, then added)
             const uint2 w = reinterpret_cast<const uint2 *>(doutb + r * 64)[lane];
             g.x += __uint_as_float(w.x << 16);
@@ -1791,9 +1842,13 @@ __global__ __launch_bounds__(256) void urm_add_cast_kernel(const float4 *__restr
     }
 }
 
+// acc_out (optional) = acc_in + dx (acc_in NULL: = dx): the emb gradient summed over the loops in the
+// order autograd would sum it (the last loop's first), so the separate accumulation adds over
+// [rows, h] fp32 disappear; dx itself may be skipped (NULL) when h needs no gradient.
 __global__ __launch_bounds__(256) void urm_add_cast_bwd_kernel(const float4 *__restrict__ dout,
                                                                const uint2 *__restrict__ doutb, float4 *__restrict__ dx,
-                                                               int64_t n4) {
+                                                               int64_t n4, const float4 *__restrict__ acc_in,
+                                                               float4 *__restrict__ acc_out) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
         float4 d = dout ? dout[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (doutb) {
@@ -1801,8 +1856,166 @@ __global__ __launch_bounds__(256) void urm_add_cast_bwd_kernel(const float4 *__r
             d = make_float4(d.x + __uint_as_float(b.x << 16), d.y + __uint_as_float(b.x & 0xFFFF0000u),
                             d.z + __uint_as_float(b.y << 16), d.w + __uint_as_float(b.y & 0xFFFF0000u));
         }
-        dx[i] = d;
+        if (dx) dx[i] = d;
+        if (acc_out) {
+            if (acc_in) {
+                const float4 a = acc_in[i];
+                d = make_float4(a.x + d.x, a.y + d.y, a.z + d.z, a.w + d.w);
+            }
+            acc_out[i] = d;
+        }
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The backward of GateUpSwiGLUFn with gu RECOMPUTED (round 5): the forward no longer stores gate_up's
+// output gu [rows, 2 inter] (503 MB per call at 65 536 boards) -- this kernel recomputes it from the
+// saved operand x [rows, h] (128 MB) on MFMA, with exactly the forward's fragments and k order
+// (urm_linear_kernel<.., EPI_SWIGLU_T>: the same gu bits), hands it through a per-wave LDS tile from
+// the MFMA layout (lane = token) to urm_swiglu_conv_bwd2_kernel's (lane = channel pair, the 16
+// tokens in a register loop with a one-token lag), and runs bwd2's arithmetic on it.  Waves take
+// the boards of bwd2's partial rows (row = global wave index, nrows = the grid's waves, boards row,
+// row + nrows, ...), each wave writes its own partial row: dgu and the dw / db partials are those of
+// bwd2 on the stored gu, term for term.
+constexpr int kGusTP = 16 * 16 + 4;  // bf16 pitch of the gu tile rows (130 dwords: conflict-free 8-byte stores)
+
+template <int KS, int CT>
+__global__ __launch_bounds__(kThreads) void urm_gate_up_swiglu_bwd_kernel(
+    const uint16_t *__restrict__ in, const uint16_t *__restrict__ w, const float *__restrict__ cw,
+    const float *__restrict__ cb, const uint16_t *__restrict__ dact, uint16_t *__restrict__ dgu,
+    float *__restrict__ part, int64_t rows, int K, int inter, int nrows) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int kPitch = LinW<KS>::PITCH;
+    constexpr int kRowsW = 16 * CT, CH = CT / 2;
+    constexpr int kLinWBytes = kRowsW * kPitch * 2;
+    static_assert(kRowsW <= 16 * 16, "gu tile width");
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, t = lane & 15, g = lane >> 4;
+    char *tile = smem + kLinWBytes + wave * (16 * kGusTP * 2);
+    for (int e = tid; e < kRowsW * kPitch / 8; e += kThreads) reinterpret_cast<uint4 *>(smem)[e] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    {   // the forward's staging: gate rows at q < kRowsW / 2, up rows above (zero past inter)
+        const int k4 = K >> 2;
+        for (int e = tid; e < kRowsW * k4; e += kThreads) {
+            const int q = e / k4, c4 = e - q * k4;
+            const int hq = q - kRowsW / 2;
+            const int src = q < kRowsW / 2 ? (q < inter ? q : -1) : (hq < inter ? inter + hq : -1);
+            if (src >= 0)
+                *reinterpret_cast<uint2 *>(smem + LinW<KS>::piece(q, c4)) =
+                    *reinterpret_cast<const uint2 *>(w + (int64_t)src * K + 4 * c4);
+        }
+    }
+    __syncthreads();
+    int wo[KS];
+#pragma unroll
+    for (int s = 0; s < KS; s++) wo[s] = LinW<KS>::frag(t, g, s);
+    // the channel pair of this lane in the token loop (bwd2's thread); lanes past inter / 2 idle there
+    const int c = 2 * lane;
+    const bool act_ch = c < inter;
+    const int cc = act_ch ? c : 0;
+    const float w0[2] = {cw[2 * cc], cw[2 * cc + 2]}, w1[2] = {cw[2 * cc + 1], cw[2 * cc + 3]}, bb[2] = {cb[cc], cb[cc + 1]};
+    float s0[2] = {0.0f, 0.0f}, s1[2] = {0.0f, 0.0f}, sb[2] = {0.0f, 0.0f};
+    const int64_t nb = rows >> 4;
+    const int row = blockIdx.x * (kThreads / 64) + wave;  // (waves past nrows: no boards, no partial row)
+    for (int64_t bd = row; row < nrows && bd < nb; bd += nrows) {
+        // the board's output gradient (bwd2's loads), in flight during the gu recompute
+        uint32_t dr[16];
+#pragma unroll
+        for (int tt = 0; tt < 16; tt++)
+            dr[tt] = act_ch ? *reinterpret_cast<const uint32_t *>(dact + (16 * bd + tt) * inter + c) : 0u;
+        // gu = bf16(x W^T) in the forward's MFMA order -> the wave's tile [token][gate 0..127 | up 128..255]
+        const uint16_t *xr = in + (bd * 16 + t) * K;
+        bf16x8 fb[KS];
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+            const int kk = 32 * s + 8 * g;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (kk + 8 <= K) {
+                v = *reinterpret_cast<const uint4 *>(xr + kk);
+            } else if (kk < K) {
+                const uint2 tl = *reinterpret_cast<const uint2 *>(xr + kk);
+                v = make_uint4(tl.x, tl.y, 0u, 0u);
+            }
+            fb[s] = __builtin_bit_cast(bf16x8, v);
+        }
+#pragma unroll 2
+        for (int ct = 0; ct < CT; ct++) {
+            asm volatile("" ::: "memory");
+            f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int s = 0; s < KS; s++)
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8 *>(smem + 16 * ct * kPitch * 2 + wo[s]),
+                                                              fb[s], acc, 0, 0, 0);
+            const int col = ct < CH ? 16 * ct + 4 * g : 128 + 16 * (ct - CH) + 4 * g;
+            *reinterpret_cast<uint2 *>(tile + (t * kGusTP + col) * 2) = make_uint2(pk2bf(acc[0], acc[1]), pk2bf(acc[2], acc[3]));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        uint32_t gr[16], ur[16];
+#pragma unroll
+        for (int tt = 0; tt < 16; tt++) {
+            gr[tt] = *reinterpret_cast<const uint32_t *>(tile + (tt * kGusTP + cc) * 2);
+            ur[tt] = *reinterpret_cast<const uint32_t *>(tile + (tt * kGusTP + 128 + cc) * 2);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();  // the next board's tile stores come after every lane's reads
+        if (act_ch) {  // urm_swiglu_conv_bwd2_kernel's token loop, verbatim arithmetic
+            float yp[2] = {0.0f, 0.0f}, gq[2] = {0.0f, 0.0f}, uq[2] = {0.0f, 0.0f}, sq[2] = {0.0f, 0.0f}, dq[2] = {0.0f, 0.0f};
+#pragma unroll
+            for (int tt = 0; tt <= 16; tt++) {
+                float d2[2] = {0.0f, 0.0f}, gv[2] = {0.0f, 0.0f}, uv[2] = {0.0f, 0.0f}, sg[2] = {0.0f, 0.0f};
+                uint16_t og[2], ou[2];
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    if (tt < 16) {
+                        gv[j] = __uint_as_float(j ? gr[tt] & 0xFFFF0000u : gr[tt] << 16);
+                        uv[j] = __uint_as_float(j ? ur[tt] & 0xFFFF0000u : ur[tt] << 16);
+                        const float da = __uint_as_float(j ? dr[tt] & 0xFFFF0000u : dr[tt] << 16);
+                        sg[j] = sigm(gv[j]);
+                        const float y = bfr(bfr(gv[j] * sg[j]) * uv[j]);
+                        const float y2 = yp[j] * w0[j] + y * w1[j] + bb[j], s2 = sigm(y2);
+                        d2[j] = da * (s2 * (1.0f + y2 * (1.0f - s2)));  // d act / d y2
+                        s1[j] += d2[j] * y;
+                        s0[j] += d2[j] * yp[j];
+                        sb[j] += d2[j];
+                        yp[j] = y;
+                    }
+                    if (tt > 0) {  // token tt - 1
+                        const float dy = dq[j] * w1[j] + (tt < 16 ? d2[j] * w0[j] : 0.0f);
+                        og[j] = f2bf16(dy * uq[j] * (sq[j] * (1.0f + gq[j] * (1.0f - sq[j]))));
+                        ou[j] = f2bf16(dy * bfr(gq[j] * sq[j]));
+                    }
+                    gq[j] = gv[j];
+                    uq[j] = uv[j];
+                    sq[j] = sg[j];
+                    dq[j] = d2[j];
+                }
+                if (tt > 0) {
+                    uint16_t *dw = dgu + (16 * bd + tt - 1) * 2 * inter;
+                    *reinterpret_cast<uint32_t *>(dw + c) = (uint32_t)og[0] | ((uint32_t)og[1] << 16);
+                    *reinterpret_cast<uint32_t *>(dw + inter + c) = (uint32_t)ou[0] | ((uint32_t)ou[1] << 16);
+                }
+            }
+        }
+    }
+    if (act_ch && row < nrows) {  // this wave's partial row (bwd2's row `row`)
+        float *pp = part + (int64_t)row * 3 * inter;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            pp[c + j] = s0[j];
+            pp[inter + c + j] = s1[j];
+            pp[2 * inter + c + j] = sb[j];
+        }
+    }
+}
+
+template <int KS, int CT>
+int launch_gus_bwd(hipStream_t s, const uint16_t *in, const uint16_t *w, const float *cw, const float *cb,
+                   const uint16_t *dact, uint16_t *dgu, float *part, int64_t rows, int K, int inter, int nrows) {
+    const size_t lds = (size_t)16 * CT * LinW<KS>::PITCH * 2 + (size_t)(kThreads / 64) * 16 * kGusTP * 2;
+    const int nblk = (nrows + kThreads / 64 - 1) / (kThreads / 64);
+    hipLaunchKernelGGL((urm_gate_up_swiglu_bwd_kernel<KS, CT>), dim3((unsigned)nblk), dim3(kThreads), lds, s, in, w, cw, cb,
+                       dact, dgu, part, rows, K, inter, nrows);
+    return launch_status();
 }
 
 extern "C" {
@@ -1910,17 +2123,26 @@ int g2048_urm_add_cast(g2048_stream_t stream, const float *a, int64_t a_rows, co
     return launch_status();
 }
 
-int g2048_urm_add_cast_bwd(g2048_stream_t stream, const float *dout, const uint16_t *doutb, float *dx, int64_t rows,
-                           int32_t hidden) {
-    if (rows < 0 || hidden <= 0 || hidden % 4) return G2048_EINVAL;
+int g2048_urm_add_cast_bwd_acc(g2048_stream_t stream, const float *dout, const uint16_t *doutb, float *dx,
+                               const float *acc_in, float *acc_out, int64_t rows, int32_t hidden) {
+    if (rows < 0 || hidden <= 0 || hidden % 4 || (acc_in && !acc_out)) return G2048_EINVAL;
     if (rows == 0) return G2048_OK;
-    if (!dx || ((uintptr_t)dout | (uintptr_t)dx) % 16 || (uintptr_t)doutb % 8) return G2048_EINVAL;
+    if ((!dx && !acc_out) || ((uintptr_t)dout | (uintptr_t)dx | (uintptr_t)acc_in | (uintptr_t)acc_out) % 16 ||
+        (uintptr_t)doutb % 8)
+        return G2048_EINVAL;
     const int64_t n4 = rows * hidden / 4;
     const int64_t blocks = (n4 + 255) / 256;
     hipLaunchKernelGGL(urm_add_cast_bwd_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0,
                        (hipStream_t)stream, reinterpret_cast<const float4 *>(dout), reinterpret_cast<const uint2 *>(doutb),
-                       reinterpret_cast<float4 *>(dx), n4);
+                       reinterpret_cast<float4 *>(dx), n4, reinterpret_cast<const float4 *>(acc_in),
+                       reinterpret_cast<float4 *>(acc_out));
     return launch_status();
+}
+
+int g2048_urm_add_cast_bwd(g2048_stream_t stream, const float *dout, const uint16_t *doutb, float *dx, int64_t rows,
+                           int32_t hidden) {
+    if (!dx) return G2048_EINVAL;
+    return g2048_urm_add_cast_bwd_acc(stream, dout, doutb, dx, nullptr, nullptr, rows, hidden);
 }
 
 int g2048_urm_rms_res_fwd(g2048_stream_t stream, const float *h, const void *a, int32_t a_dtype, float *out,
@@ -1928,22 +2150,29 @@ int g2048_urm_rms_res_fwd(g2048_stream_t stream, const float *h, const void *a, 
     return g2048_urm_rms_res_fwd2(stream, h, a, a_dtype, out, nullptr, rstd, rows, hidden, eps);
 }
 
-int g2048_urm_rms_res_bwd2(g2048_stream_t stream, const float *dout, const uint16_t *doutb, const float *out,
-                           const float *rstd, float *dh, void *da, int32_t a_dtype, int64_t rows, int32_t hidden) {
-    if (rows < 0 || hidden != 64 || (a_dtype != 0 && a_dtype != 1)) return G2048_EINVAL;
+int g2048_urm_rms_res_bwd3(g2048_stream_t stream, const float *dout, const float *dpool, const uint16_t *doutb,
+                           const float *out, const float *rstd, float *dh, void *da, int32_t a_dtype, int64_t rows,
+                           int32_t hidden) {
+    if (rows < 0 || hidden != 64 || (a_dtype != 0 && a_dtype != 1) || (dout && dpool) || (dpool && rows % 16))
+        return G2048_EINVAL;
     if (rows == 0) return G2048_OK;
-    if ((!dout && !doutb) || !out || !rstd || !dh || !da || ((uintptr_t)dout | (uintptr_t)out | (uintptr_t)dh) % 16 ||
-        ((uintptr_t)da | (uintptr_t)doutb) % 8)
+    if ((!dout && !doutb && !dpool) || !out || !rstd || !dh || !da ||
+        ((uintptr_t)dout | (uintptr_t)dpool | (uintptr_t)out | (uintptr_t)dh) % 16 || ((uintptr_t)da | (uintptr_t)doutb) % 8)
         return G2048_EINVAL;
     const int64_t nb = (rows + 15) / 16;
     const dim3 grid((unsigned)(nb < 4096 ? nb : 4096));
     if (a_dtype == 1)
         hipLaunchKernelGGL(urm_rms_res_bwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, dout, out, rstd, dh, da,
-                           rows, doutb);
+                           rows, doutb, dpool);
     else
         hipLaunchKernelGGL(urm_rms_res_bwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, dout, out, rstd, dh,
-                           da, rows, doutb);
+                           da, rows, doutb, dpool);
     return launch_status();
+}
+
+int g2048_urm_rms_res_bwd2(g2048_stream_t stream, const float *dout, const uint16_t *doutb, const float *out,
+                           const float *rstd, float *dh, void *da, int32_t a_dtype, int64_t rows, int32_t hidden) {
+    return g2048_urm_rms_res_bwd3(stream, dout, nullptr, doutb, out, rstd, dh, da, a_dtype, rows, hidden);
 }
 
 int g2048_urm_rms_res_bwd(g2048_stream_t stream, const float *dout, const float *out, const float *rstd, float *dh,
@@ -1957,6 +2186,31 @@ static int sc_blocks(int64_t nb) { return (int)(nb < 2048 ? nb : 2048); }
 size_t g2048_urm_swiglu_conv_partials(int64_t n, int32_t inter) {
     if (n <= 0 || inter <= 0 || inter > kScThreads) return 0;
     return (size_t)sc_blocks(n) * 3 * inter;
+}
+
+int g2048_urm_gate_up_swiglu_bwd_supported(int32_t h, int32_t inter) {
+    return (h == 64 && inter > 64 && inter <= 128 && inter % 8 == 0) || (h == 32 && inter > 32 && inter <= 64 && inter % 8 == 0)
+               ? 1 : 0;
+}
+
+int g2048_urm_gate_up_swiglu_bwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, const float *conv_w,
+                                 const float *conv_b, const uint16_t *dact, uint16_t *dgu, float *dw, float *db,
+                                 float *partials, int64_t n, int32_t h, int32_t inter) {
+    if (n <= 0 || !g2048_urm_gate_up_swiglu_bwd_supported(h, inter)) return G2048_EINVAL;
+    if (!x || !w || !conv_w || !conv_b || !dact || !dgu || !dw || !db || !partials ||
+        ((uintptr_t)x | (uintptr_t)dgu) % 16 || ((uintptr_t)w | (uintptr_t)dact) % 8)
+        return G2048_EINVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    // bwd2's partial rows (sc_blocks(n) of them, boards row, row + nrows, ...): one per wave
+    const int nrows = sc_blocks(n);
+    const int64_t rows = 16 * n;
+    int st = G2048_EINVAL;
+    if (h == 64) st = launch_gus_bwd<2, 16>(s, x, w, conv_w, conv_b, dact, dgu, partials, rows, h, inter, nrows);
+    else st = launch_gus_bwd<1, 8>(s, x, w, conv_w, conv_b, dact, dgu, partials, rows, h, inter, nrows);
+    if (st) return st;
+    hipLaunchKernelGGL(urm_swiglu_conv_colsum_kernel, dim3((3 * inter + 15) / 16), dim3(256), 0, s, partials, nrows,
+                       (int)inter, dw, db);
+    return launch_status();
 }
 
 int g2048_urm_swiglu_conv_fwd(g2048_stream_t stream, const uint16_t *gu, const float *w, const float *b, uint16_t *act,
@@ -2158,6 +2412,15 @@ int g2048_urm_linear_rms(g2048_stream_t stream, const uint16_t *in, const uint16
     return dispatch_lin((hipStream_t)stream, 1, in, w, rows, k, h, 0, nullptr, x, emb, xb, eps, nullptr, nullptr, false);
 }
 
+int g2048_urm_linear_t(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, uint16_t *out, int64_t rows,
+                       int32_t k, int32_t n) {
+    if (rows < 0 || rows % 16 || n % 8 || k % 4 || !g2048_urm_linear_supported(0, k, n, 0)) return G2048_EINVAL;
+    if (rows == 0) return G2048_OK;
+    if (!in || !w || !out) return G2048_EINVAL;
+    return dispatch_lin((hipStream_t)stream, 0, in, w, rows, k, n, 0, out, nullptr, nullptr, nullptr, 0.0f, nullptr,
+                        nullptr, false, nullptr, 1);
+}
+
 int g2048_urm_linear_bias(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *bias, uint16_t *out,
                           int64_t rows, int32_t k, int32_t n) {
     if (rows < 0 || rows % 16 || n % 8 || !g2048_urm_linear_supported(0, k, n, 0)) return G2048_EINVAL;
@@ -2181,7 +2444,7 @@ int g2048_urm_linear_swiglu(g2048_stream_t stream, const uint16_t *in, const uin
                             const float *conv_b, uint16_t *out, int64_t rows, int32_t h, int32_t inter) {
     if (rows < 0 || rows % 16 || !g2048_urm_linear_supported(2, h, 2 * inter, inter)) return G2048_EINVAL;
     if (rows == 0) return G2048_OK;
-    if (!in || !w || !conv_w || !conv_b || !out || ((uintptr_t)conv_w | (uintptr_t)conv_b) % 16) return G2048_EINVAL;
+    if (!in || !w || !conv_w || !conv_b || !out) return G2048_EINVAL;  // conv params: staged through LDS
     return dispatch_lin((hipStream_t)stream, 2, in, w, rows, h, 2 * inter, inter, out, nullptr, nullptr, nullptr, 0.0f,
                         conv_w, conv_b, false);
 }
@@ -2192,9 +2455,8 @@ int g2048_urm_linear_swiglu_train(g2048_stream_t stream, const uint16_t *in, con
     // the epilogue writes 8 features per lane with 16-byte stores: inter % 8, 16-byte aligned outputs
     if (rows < 0 || rows % 16 || inter % 8 || !g2048_urm_linear_supported(3, h, 2 * inter, inter)) return G2048_EINVAL;
     if (rows == 0) return G2048_OK;
-    if (!in || !w || !conv_w || !conv_b || !act || ((uintptr_t)conv_w | (uintptr_t)conv_b) % 16 ||
-        ((uintptr_t)gu | (uintptr_t)act) % 16)
-        return G2048_EINVAL;
+    if (!in || !w || !conv_w || !conv_b || !act || ((uintptr_t)gu | (uintptr_t)act) % 16)
+        return G2048_EINVAL;  // (conv params: staged through LDS, any 4-byte alignment)
     return dispatch_lin((hipStream_t)stream, 3, in, w, rows, h, 2 * inter, inter, act, nullptr, nullptr, gu, 0.0f,
                         conv_w, conv_b, false);
 }

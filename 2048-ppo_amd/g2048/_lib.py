@@ -35,7 +35,7 @@ EXPORTED = (
     "g2048_colsum_batch_blocks", "g2048_colsum_batch_sq",
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_wgrad_pair_partials", "g2048_wgrad_pair", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
-    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_muon_workspace_bytes", "g2048_muon_error_offset", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_rms_res_fwd2", "g2048_urm_rms_res_bwd2", "g2048_urm_add_cast", "g2048_urm_add_cast_bwd", "g2048_urm_forward_drop", "g2048_urm_rms_res_fwd",
+    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_muon_workspace_bytes", "g2048_muon_error_offset", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_rms_res_fwd2", "g2048_urm_rms_res_bwd2", "g2048_urm_rms_res_bwd3", "g2048_urm_add_cast", "g2048_urm_add_cast_bwd", "g2048_urm_add_cast_bwd_acc", "g2048_urm_forward_drop", "g2048_urm_rms_res_fwd",
     "g2048_urm_rms_res_bwd", "g2048_urm_swiglu_conv_partials", "g2048_urm_swiglu_conv_fwd", "g2048_urm_swiglu_conv_bwd",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
@@ -45,7 +45,7 @@ EXPORTED = (
     # include/g2048_urm.h
     "g2048_urm_stem", "g2048_urm_attention", "g2048_urm_residual_rms", "g2048_urm_swiglu_conv",
     "g2048_urm_pool_heads", "g2048_urm_linear_supported", "g2048_urm_linear", "g2048_urm_linear_rms",
-    "g2048_urm_linear_swiglu", "g2048_urm_linear_swiglu_train", "g2048_urm_linear_res_rms", "g2048_urm_linear_bias", "g2048_urm_wgrad_supported", "g2048_urm_wgrad_partials", "g2048_urm_wgrad", "g2048_urm_forward_supported", "g2048_urm_forward",
+    "g2048_urm_linear_swiglu", "g2048_urm_linear_swiglu_train", "g2048_urm_linear_t", "g2048_urm_gate_up_swiglu_bwd_supported", "g2048_urm_gate_up_swiglu_bwd", "g2048_urm_linear_res_rms", "g2048_urm_linear_bias", "g2048_urm_wgrad_supported", "g2048_urm_wgrad_partials", "g2048_urm_wgrad", "g2048_urm_forward_supported", "g2048_urm_forward",
 )
 
 
@@ -282,6 +282,9 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_urm_linear_res_rms": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, ctypes.c_float]),
         "g2048_urm_linear_swiglu": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_linear_swiglu_train": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32]),
+        "g2048_urm_linear_t": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
+        "g2048_urm_gate_up_swiglu_bwd_supported": (ctypes.c_int, [i32, i32]),
+        "g2048_urm_gate_up_swiglu_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_wgrad_supported": (ctypes.c_int, [i32, i32]),
         "g2048_urm_wgrad_partials": (sz, [i64, i32, i32]),
         "g2048_urm_wgrad": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32]),
@@ -299,6 +302,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_urm_rms_res_fwd2": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, vp, i64, i32, ctypes.c_float]),
         "g2048_urm_add_cast": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, i64, i32]),
         "g2048_urm_add_cast_bwd": (ctypes.c_int, [vp, vp, vp, vp, i64, i32]),
+        "g2048_urm_add_cast_bwd_acc": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32]),
+        "g2048_urm_rms_res_bwd3": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, i32]),
         "g2048_urm_rms_res_bwd2": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, i64, i32]),
         "g2048_urm_stem_partials": (sz, [i64]),
         "g2048_urm_stem_fwd": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, i64, i32, ctypes.c_float]),
@@ -1095,26 +1100,47 @@ def urm_add_cast(a, a_rows: int, e, out, outb):
            "g2048_urm_add_cast")
 
 
-def urm_add_cast_bwd(dout, doutb, dx):
-    """dx = dout + float(doutb); either may be None (g2048_urm_add_cast_bwd)."""
-    rows, hid = dx.shape
-    _check(load().g2048_urm_add_cast_bwd(_stream(dx), _dev(dout, torch.float32, "dout"), _dev(doutb, torch.bfloat16, "doutb"),
-                                         _dev(dx, torch.float32, "dx"), rows, hid), "g2048_urm_add_cast_bwd")
+def urm_add_cast_bwd(dout, doutb, dx, acc_in=None, acc_out=None):
+    """dx = dout + float(doutb) (either may be None); acc_out = acc_in + dx when given, dx may then be
+    None (g2048_urm_add_cast_bwd_acc)."""
+    ref = dx if dx is not None else acc_out
+    rows, hid = ref.shape
+    _check(load().g2048_urm_add_cast_bwd_acc(_stream(ref), _dev(dout, torch.float32, "dout"),
+                                             _dev(doutb, torch.bfloat16, "doutb"), _dev(dx, torch.float32, "dx"),
+                                             _dev(acc_in, torch.float32, "acc_in"), _dev(acc_out, torch.float32, "acc_out"),
+                                             rows, hid), "g2048_urm_add_cast_bwd_acc")
 
 
-def urm_rms_res_bwd(dout, out, rstd, dh, da, doutb=None):
-    """dout fp32 and / or doutb bf16 (the bf16 copy's gradient); either may be None."""
+def urm_rms_res_bwd(dout, out, rstd, dh, da, doutb=None, dpool=None):
+    """dout fp32 and / or doutb bf16 (the bf16 copy's gradient); either may be None.  dpool (instead of
+    dout): fp32 [rows / 16, 64] broadcast over each board's 16 token rows (the mean-pool backward)."""
     rows, hid = out.shape
     abf = da.dtype == torch.bfloat16
-    _check(load().g2048_urm_rms_res_bwd2(_stream(out), _dev(dout, torch.float32, "dout"),
+    _check(load().g2048_urm_rms_res_bwd3(_stream(out), _dev(dout, torch.float32, "dout"), _dev(dpool, torch.float32, "dpool"),
                                          _dev(doutb, torch.bfloat16, "doutb"), _dev(out, torch.float32, "out"),
                                          _dev(rstd, torch.float32, "rstd"), _dev(dh, torch.float32, "dh"),
                                          _dev(da, torch.bfloat16 if abf else torch.float32, "da"), int(abf), rows, hid),
-           "g2048_urm_rms_res_bwd2")
+           "g2048_urm_rms_res_bwd3")
 
 
 def urm_swiglu_conv_partials(n: int, inter: int) -> int:
     return int(load().g2048_urm_swiglu_conv_partials(n, inter))
+
+
+def urm_gate_up_swiglu_bwd_supported(h: int, inter: int) -> bool:
+    return bool(load().g2048_urm_gate_up_swiglu_bwd_supported(h, inter))
+
+
+def urm_gate_up_swiglu_bwd(x, w, conv_w, conv_b, dact, dgu, dw, db, partials):
+    """dgu, dw, db of the SwiGLU-conv with gu = bf16(x w^T) recomputed on MFMA (g2048_urm_gate_up_swiglu_bwd)."""
+    rows, h = x.shape
+    inter = w.shape[0] // 2
+    _check(load().g2048_urm_gate_up_swiglu_bwd(_stream(x), _dev(x, torch.bfloat16, "x"), _dev(w, torch.bfloat16, "w"),
+                                               _dev(conv_w, torch.float32, "conv_w"), _dev(conv_b, torch.float32, "conv_b"),
+                                               _dev(dact, torch.bfloat16, "dact"), _dev(dgu, torch.bfloat16, "dgu"),
+                                               _dev(dw, torch.float32, "dw"), _dev(db, torch.float32, "db"),
+                                               _dev(partials, torch.float32, "partials"), rows // 16, h, inter),
+           "g2048_urm_gate_up_swiglu_bwd")
 
 
 def urm_swiglu_conv_fwd(gu, w, b, act):
@@ -1164,6 +1190,13 @@ def urm_linear(inp, w, out):
     rows, k = inp.shape
     _check(load().g2048_urm_linear(_stream(inp), _dev(inp, torch.bfloat16, "in"), _dev(w, torch.bfloat16, "w"),
                                    _dev(out, torch.bfloat16, "out"), rows, k, w.shape[0]), "g2048_urm_linear")
+
+
+def urm_linear_t(inp, w, out):
+    """out = inp w for w [k, n] (bf16): dX = dY W without a transposed copy (g2048_urm_linear_t)."""
+    rows, k = inp.shape
+    _check(load().g2048_urm_linear_t(_stream(inp), _dev(inp, torch.bfloat16, "in"), _dev(w, torch.bfloat16, "w"),
+                                     _dev(out, torch.bfloat16, "out"), rows, k, w.shape[1]), "g2048_urm_linear_t")
 
 
 def urm_linear_bias(inp, w, bias, out):

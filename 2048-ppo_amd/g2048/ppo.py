@@ -88,6 +88,7 @@ class PPOUpdater:
         self.graph = graph and self.dev.type == "cuda"
         self.beta_t = torch.zeros((), dtype=torch.float32, device=self.dev)
         self._g = None
+        self.weight_cache = None  # urm.Bf16Weights (refreshed at every update and after a capture)
 
     ragged_pad = False  # True: the updater runs a ragged minibatch padded to full size (_set_rows)
 
@@ -112,6 +113,8 @@ class PPOUpdater:
         self.beta_t.fill_(beta)
         nb = 0
         self.model.train()
+        if self.weight_cache is not None:
+            self.weight_cache.refresh()
         use_graph = self.graph and (m_total % bs == 0 or self.ragged_pad)
         if use_graph:
             self._ensure_graph(data, bs, encode)
@@ -226,6 +229,8 @@ class PPOUpdater:
         self.opt.restore(snap_o)
         self.stats.copy_(snap_s)
         self._extra_restore(snap_x)
+        if self.weight_cache is not None:  # the warm-up's optimizer steps wrote the stepped weights' copies
+            self.weight_cache.refresh()
         self._g = {"key": key, "idx": idx, "g1": g1, "g2": g2, "st": st}
 
     force_split = False

@@ -115,6 +115,11 @@ class VecTrainer:
             self.grads = GradBucket(self.model.parameters())
             self.opt = build_optimizer(self.model, cfg.lr, cfg.critic_lr, cfg.beta1, cfg.beta2, cfg.weight_decay,
                                        cfg.warmup_steps, cfg.steps)
+        # GameURM: bf16 copies of the projection weights written by the fused optimizer step (no cast
+        # kernels per use in the update; the rollout and KL re-forward read them too)
+        self.bf16w = (urm_mod.attach_bf16_weights(self.model, self.opt)
+                      if cfg.graph_update and cfg.amp and isinstance(self.model, agent.GameURM) and self.dev.type == "cuda"
+                      else None)
         self.policy = make_policy(self.model, torch.bfloat16 if cfg.amp else torch.float32)
         n = cfg.episodes
         self.episodic = cfg.horizon <= 0
@@ -142,6 +147,7 @@ class VecTrainer:
                                                seed=cfg.seed * 31 + self.rank)
         else:
             self.ppo = PPOUpdater(self.model, self.opt, pcfg, self.grads, gen, graph=graph_up)
+            self.ppo.weight_cache = self.bf16w
         self.beta = cfg.entropy
         self.obs_mb = None
         self.run_score = torch.zeros(n, dtype=torch.int64, device=self.dev)

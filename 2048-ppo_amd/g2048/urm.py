@@ -38,10 +38,14 @@ class URMPolicy:
         self.loops, self.eps = cfg.num_loops, float(cfg.rms_norm_eps)
         self.inter = model.layers[0].mlp.inter
         self.mats = []  # per layer (Wqkv, Wo, Wgu, Wd) as bf16 copies
+        # the trainer's Bf16Weights copies when attached (kept current by the optimizer; sync()
+        # refreshes them like its own), else this policy's own copies
+        self.shared = all(getattr(w, "_g2048_bf16", None) is not None for blk in model.layers
+                          for w in (blk.attn.qkv_proj.weight, blk.attn.o_proj.weight, blk.mlp.gate_up_proj.weight,
+                                    blk.mlp.down_proj.weight))
         for blk in model.layers:
-            self.mats.append([torch.empty_like(w, dtype=torch.bfloat16) for w in
-                              (blk.attn.qkv_proj.weight, blk.attn.o_proj.weight, blk.mlp.gate_up_proj.weight,
-                               blk.mlp.down_proj.weight)])
+            ws = (blk.attn.qkv_proj.weight, blk.attn.o_proj.weight, blk.mlp.gate_up_proj.weight, blk.mlp.down_proj.weight)
+            self.mats.append([w._g2048_bf16 if self.shared else torch.empty_like(w, dtype=torch.bfloat16) for w in ws])
         dev = model.stem[0].weight.device
         self.conv_w = [torch.empty(self.inter, 2, dtype=torch.float32, device=dev) for _ in model.layers]
         # own copies of the conv biases: an optimizer may re-home the 1-D parameters into a flat
@@ -104,11 +108,15 @@ class URMPolicy:
                 and c.hidden_dim // c.num_heads <= 64)
 
     @torch.no_grad()
-    def sync(self):
-        for blk, mats, cw in zip(self.master.layers, self.mats, self.conv_w):
-            for dst, src in zip(mats, (blk.attn.qkv_proj.weight, blk.attn.o_proj.weight, blk.mlp.gate_up_proj.weight,
-                                       blk.mlp.down_proj.weight)):
-                dst.copy_(src)
+    def sync(self, mats: bool = True):
+        """Refresh the copies from the master weights (mats=False: only the conv / init_hidden copies --
+        the KL re-forward inside the update, whose shared bf16 projection copies the optimizer step
+        itself has just written)."""
+        for blk, mt, cw in zip(self.master.layers, self.mats, self.conv_w):
+            if mats or not self.shared:
+                for dst, src in zip(mt, (blk.attn.qkv_proj.weight, blk.attn.o_proj.weight, blk.mlp.gate_up_proj.weight,
+                                         blk.mlp.down_proj.weight)):
+                    dst.copy_(src)
             cw.copy_(blk.mlp.dwconv.weight.view(self.inter, 2))
         for blk, cb in zip(self.master.layers, self.conv_b):
             cb.copy_(blk.mlp.dwconv.bias)
@@ -271,12 +279,17 @@ def train_nograd_forward(model, obs: torch.Tensor):
                                         c.conv_kernel)):
         return None
     pol = model.__dict__.get("_g2048_train_fwd")
-    if pol is None or pol.param_ptrs() != pol._ptrs:
+    shared = all(getattr(w, "_g2048_bf16", None) is not None for blk in model.layers
+                 for w in (blk.attn.qkv_proj.weight, blk.attn.o_proj.weight, blk.mlp.gate_up_proj.weight,
+                           blk.mlp.down_proj.weight))
+    if pol is None or pol.param_ptrs() != pol._ptrs or pol.shared != shared:
         pol = URMPolicy(model)
         pol._ptrs = pol.param_ptrs()
         model.__dict__["_g2048_train_fwd"] = pol
     else:
-        pol.sync()  # the bf16 weight copies of the current parameters (captured with a graph)
+        # the bf16 weight copies of the current parameters (captured with a graph); shared Bf16Weights
+        # copies were written by the optimizer step itself: only the conv / init_hidden copies
+        pol.sync(mats=False)
     logits, value = pol.forward_train(obs, float(c.dropout))
     return logits, value.view(-1, 1)
 
@@ -342,6 +355,17 @@ class ResidualRMSFn(torch.autograd.Function):
         return dh.view(ctx.shape), da.view(ctx.shape), None, None
 
 
+class EmbGradAcc:
+    """The emb gradient of GameURM's grad-enabled loops, summed inside their AddCastFn backward kernels
+    (g2048_urm_add_cast_bwd_acc) instead of by autograd's accumulation adds over [rows, h] fp32: the
+    loops' backwards run last loop first, each adds its gradient to the running sum, and the earliest
+    loop returns the total -- the sum autograd would form, in its order ((g_K + g_K-1) + ...)."""
+
+    def __init__(self):
+        self.pending = 0  # AddCastFn applications recorded with this accumulator (agent.GameURM._loop)
+        self.acc = None
+
+
 class AddCastFn(torch.autograd.Function):
     """A loop start of GameURM (game.py:1441: hidden_states + emb) under bf16 autocast, for autograd
     training on the device: the fp32 sum and its bf16 copy -- the first block's qkv operand, which
@@ -349,10 +373,11 @@ class AddCastFn(torch.autograd.Function):
     sums the fp32 gradient (residual RMSNorm) and the bf16 one (the projection) in one kernel
     instead of autocast's cast backward plus autograd's accumulation.  Values bitwise those of
     `h + emb` and its `.to(bfloat16)`.  h [b, 16, 64] (contiguous, or init_hidden [1, 16, 64]
-    expanded over the boards), emb [b, 16, 64] fp32 -> (out fp32, outb bf16)."""
+    expanded over the boards), emb [b, 16, 64] fp32 -> (out fp32, outb bf16).  acc (EmbGradAcc,
+    optional): the emb gradient is summed over the loops in the backward kernels (round 5)."""
 
     @staticmethod
-    def forward(ctx, h: torch.Tensor, emb: torch.Tensor):
+    def forward(ctx, h: torch.Tensor, emb: torch.Tensor, acc: EmbGradAcc | None = None):
         ctx.set_materialize_grads(False)
         b, s, hid = emb.shape
         e2 = emb.reshape(-1, hid).contiguous()
@@ -361,20 +386,73 @@ class AddCastFn(torch.autograd.Function):
         out = torch.empty_like(e2)
         outb = torch.empty(e2.shape, dtype=torch.bfloat16, device=emb.device)
         L.urm_add_cast(a, s if bcast else 0, e2, out, outb)
-        ctx.bcast, ctx.shape = bcast, (b, s, hid)
+        ctx.bcast, ctx.shape, ctx.acc = bcast, (b, s, hid), acc
         return out.view(b, s, hid), outb.view(b, s, hid)
 
     @staticmethod
     def backward(ctx, dout: torch.Tensor | None, doutb: torch.Tensor | None):
+        acc = ctx.acc
         if dout is None and doutb is None:
-            return None, None
+            if acc is not None:
+                acc.pending -= 1
+                if acc.pending == 0 and acc.acc is not None:
+                    total, acc.acc = acc.acc, None
+                    return None, (total.view(ctx.shape) if ctx.needs_input_grad[1] else None), None
+            return None, None, None
         b, s, hid = ctx.shape
-        dx = torch.empty(b * s, hid, dtype=torch.float32, device=(dout if dout is not None else doutb).device)
-        L.urm_add_cast_bwd(None if dout is None else dout.reshape(-1, hid).float().contiguous(),
-                           None if doutb is None else doutb.reshape(-1, hid).to(torch.bfloat16).contiguous(), dx)
-        dx = dx.view(b, s, hid)
-        # the gradient of h in the shape it came in (an expanded init_hidden: expand's backward sums it)
-        return (dx if ctx.needs_input_grad[0] else None), (dx if ctx.needs_input_grad[1] else None)
+        dev = (dout if dout is not None else doutb).device
+        d32 = None if dout is None else dout.reshape(-1, hid).float().contiguous()
+        d16 = None if doutb is None else doutb.reshape(-1, hid).to(torch.bfloat16).contiguous()
+        need_h, need_e = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if acc is None or not need_e:
+            dx = torch.empty(b * s, hid, dtype=torch.float32, device=dev)
+            L.urm_add_cast_bwd(d32, d16, dx)
+            dx = dx.view(b, s, hid)
+            # the gradient of h in the shape it came in (an expanded init_hidden: expand's backward sums it)
+            return (dx if need_h else None), (dx if need_e else None), None
+        acc.pending -= 1
+        if acc.pending < 0:
+            raise RuntimeError("EmbGradAcc: more AddCastFn backwards than grad-enabled loops (retain_graph?)")
+        if acc.acc is None and acc.pending > 0:  # the last loop (first backward): the running sum is its dx
+            dx = torch.empty(b * s, hid, dtype=torch.float32, device=dev)
+            L.urm_add_cast_bwd(d32, d16, dx)
+            acc.acc = dx
+            return (dx.view(b, s, hid) if need_h else None), None, None
+        out = torch.empty(b * s, hid, dtype=torch.float32, device=dev)
+        dx = torch.empty(b * s, hid, dtype=torch.float32, device=dev) if need_h and acc.acc is not None else None
+        L.urm_add_cast_bwd(d32, d16, dx, acc_in=acc.acc, acc_out=out)
+        if acc.acc is None:  # a single loop: the sum is dx itself
+            dx = out
+        if acc.pending == 0:  # the earliest loop: the total is emb's gradient
+            acc.acc = None
+            return (dx.view(b, s, hid) if need_h else None), out.view(b, s, hid), None
+        acc.acc = out
+        return (dx.view(b, s, hid) if need_h else None), None, None
+
+
+class MeanPoolFn(torch.autograd.Function):
+    """GameURM's token mean-pool (game.py:1450, h.mean(dim=1)) whose backward hands on dpooled / 16
+    EXPANDED over the 16 tokens (a stride-0 view) instead of torch's materialised [b, 16, h] division:
+    the last residual RMSNorm backward reads the [b, h] gradient itself (g2048_urm_rms_res_bwd3),
+    anything else materialises the view on use.  Values bitwise torch's mean backward."""
+
+    @staticmethod
+    def forward(ctx, h: torch.Tensor):
+        ctx.shape = h.shape
+        return h.mean(dim=1)
+
+    @staticmethod
+    def backward(ctx, dp: torch.Tensor):
+        b, s, hid = ctx.shape
+        return (dp / s).unsqueeze(1).expand(b, s, hid)
+
+
+def _pooled_grad(dout: torch.Tensor | None, shape) -> torch.Tensor | None:
+    """The [b, h] base of a mean-pool gradient (MeanPoolFn's expanded view over the 16 tokens), or None."""
+    if dout is None or dout.dim() != 3 or dout.shape[1] != 16 or dout.stride(1) != 0 or dout.dtype != torch.float32:
+        return None
+    base = dout[:, 0, :]
+    return base if base.is_contiguous() and tuple(dout.shape) == tuple(shape) else None
 
 
 def add_cast_supported(h: torch.Tensor, emb: torch.Tensor) -> bool:
@@ -444,6 +522,70 @@ def _gemm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return torch.mm(x, w.t())
 
 
+def _gemm_t(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dx bf16 [rows, k] = dy [rows, n] w for w [n, k] (a projection's input gradient): the MFMA
+    projection kernel stages W^T itself (g2048_urm_linear_t; bitwise _gemm(dy, w.t().contiguous())),
+    else the library GEMM."""
+    rows, n = dy.shape
+    k = w.shape[1]
+    if rows % 16 == 0 and k % 8 == 0 and n % 4 == 0 and L.urm_linear_supported(0, n, k):
+        y = torch.empty(rows, k, dtype=torch.bfloat16, device=dy.device)
+        L.urm_linear_t(dy, w.contiguous(), y)
+        return y
+    return torch.mm(dy, w)
+
+
+def bf16_weight(w: torch.Tensor) -> torch.Tensor:
+    """The autocast bf16 operand of a projection weight: its Bf16Weights copy (written by the fused
+    Muon step with the weight itself, so no cast kernel per use) when one is attached, else a cast."""
+    c = getattr(w, "_g2048_bf16", None)
+    return c if c is not None else w.detach().to(torch.bfloat16)
+
+
+class Bf16Weights:
+    """bf16 copies of GameURM's projection weights (qkv, o, gate_up, down of every layer) kept current
+    by the optimizer: FusedMuonAdamW writes them in the same launch that updates the fp32 weights
+    (set_bf16_copies), refresh() copies them eagerly (the trainer calls it at the start of every
+    update and after a capture's warm-up restored the weights).  The training Functions read them
+    through bf16_weight() instead of casting every weight at every use (~40 cast / transpose kernels
+    per minibatch); the KL re-forward's one-launch kernel reads them too."""
+
+    def __init__(self, model, opt):
+        self.pairs = []
+        for blk in model.layers:
+            for w in (blk.attn.qkv_proj.weight, blk.attn.o_proj.weight, blk.mlp.gate_up_proj.weight,
+                      blk.mlp.down_proj.weight):
+                t = torch.empty_like(w, dtype=torch.bfloat16)
+                w._g2048_bf16 = t
+                self.pairs.append((w, t))
+        inner = getattr(opt, "opt", opt)
+        inner.set_bf16_copies({w: t for w, t in self.pairs})
+        self.refresh()
+
+    @torch.no_grad()
+    def refresh(self):
+        for w, t in self.pairs:
+            t.copy_(w)
+
+    def detach(self):
+        for w, _ in self.pairs:
+            w._g2048_bf16 = None
+
+
+def attach_bf16_weights(model, opt):
+    """Bf16Weights for a GameURM whose optimizer writes bf16 copies (the fused Muon/AdamW kernel covers
+    every projection), else None."""
+    inner = getattr(opt, "opt", opt)
+    if not getattr(inner, "supported", False) or not hasattr(inner, "set_bf16_copies"):
+        return None
+    muon_ids = {id(p) for p, _ in inner.muon}
+    ws = [w for blk in model.layers for w in (blk.attn.qkv_proj.weight, blk.attn.o_proj.weight,
+                                              blk.mlp.gate_up_proj.weight, blk.mlp.down_proj.weight)]
+    if not all(id(w) in muon_ids for w in ws):
+        return None
+    return Bf16Weights(model, opt)
+
+
 def gemm_supported(n: int, k: int) -> bool:
     """Both GEMMs of a projection w [n, k] (forward x w^T and input gradient dy w) run on the MFMA
     projection kernel (no library GEMM)."""
@@ -461,7 +603,7 @@ class URMLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: torch.Tensor, w: torch.Tensor):
         xb = x.to(torch.bfloat16).contiguous()
-        wb = w.detach().to(torch.bfloat16)
+        wb = bf16_weight(w)
         ctx.save_for_backward(xb, wb)
         ctx.dtypes = (x.dtype, w.dtype)
         return _gemm(xb, wb)
@@ -470,7 +612,7 @@ class URMLinearFn(torch.autograd.Function):
     def backward(ctx, dy: torch.Tensor):
         xb, wb = ctx.saved_tensors
         dy = dy.to(torch.bfloat16).contiguous()
-        dx = _gemm(dy, wb.t().contiguous()) if ctx.needs_input_grad[0] else None
+        dx = _gemm_t(dy, wb) if ctx.needs_input_grad[0] else None
         dW = _wgrad(dy, xb).to(ctx.dtypes[1])
         return (None if dx is None else dx.to(ctx.dtypes[0])), dW
 
@@ -512,7 +654,7 @@ class URMHeadsFn(torch.autograd.Function):
             dy[:, 4:5] = dvalue
         dw = _wgrad(dy, pb)                                        # [16, h] fp32
         db = dy[:, :5].float().sum(0)
-        dp = _gemm(dy[:, :8].contiguous(), w8.t().contiguous())    # [n, h] bf16 = dy W
+        dp = _gemm_t(dy[:, :8].contiguous(), w8)                   # [n, h] bf16 = dy W
         t = ctx.dtypes
         return (dp.to(t[0]), dw[:4].to(t[1]), db[:4].to(t[2]), dw[4:5].to(t[3]), db[4:5].to(t[4]))
 
@@ -556,7 +698,7 @@ class LinResRMSFn(torch.autograd.Function):
         shape = h.shape
         h2 = h.reshape(-1, shape[-1]).contiguous()
         xb = x.reshape(-1, x.shape[-1]).to(torch.bfloat16).contiguous()
-        wb = w.detach().to(torch.bfloat16).contiguous()
+        wb = bf16_weight(w)
         out = torch.empty_like(h2)
         outb = torch.empty(h2.shape, dtype=torch.bfloat16, device=h.device) if with_bf16 else None
         rstd = torch.empty(h2.shape[0], dtype=torch.float32, device=h.device)
@@ -574,10 +716,11 @@ class LinResRMSFn(torch.autograd.Function):
             return None, None, None, None, None
         dh = torch.empty_like(out)
         da = torch.empty(out.shape, dtype=torch.bfloat16, device=out.device)
-        d32 = None if dout is None else dout.reshape(out.shape).float().contiguous()
+        dpool = _pooled_grad(dout, ctx.shape)  # the mean-pool's broadcast gradient, read as [b, h]
+        d32 = None if dout is None or dpool is not None else dout.reshape(out.shape).float().contiguous()
         db16 = None if doutb is None else doutb.reshape(out.shape).to(torch.bfloat16).contiguous()
-        L.urm_rms_res_bwd(d32, out, rstd, dh, da, db16)
-        dx = _gemm(da, wb.t().contiguous()) if ctx.needs_input_grad[1] else None
+        L.urm_rms_res_bwd(d32, out, rstd, dh, da, db16, dpool=dpool)
+        dx = _gemm_t(da, wb) if ctx.needs_input_grad[1] else None
         dw = _wgrad(da, xb).to(ctx.dtypes[1]) if ctx.needs_input_grad[2] else None
         return (dh.view(ctx.shape), None if dx is None else dx.to(ctx.dtypes[0]).view(ctx.xshape), dw, None, None)
 
@@ -594,37 +737,50 @@ def linres_supported(lin, h: torch.Tensor) -> bool:
 class GateUpSwiGLUFn(torch.autograd.Function):
     """gate_up_proj + SwiGLU + kernel-2 depthwise conv + SiLU of GameConvSwiGLU (game.py:1264-1276)
     under bf16 autocast, for autograd training on the device: ONE forward kernel
-    (g2048_urm_linear_swiglu_train: the projection on MFMA with the SwiGLU-conv epilogue, gu stored
-    once for the backward) instead of a library GEMM writing gu and a SwiGLU kernel reading it back;
-    backward = g2048_urm_swiglu_conv_bwd, the input gradient dgu W on g2048_urm_linear (MFMA) and the
-    weight gradient on g2048_urm_wgrad.
+    (g2048_urm_linear_swiglu_train: the projection on MFMA with the SwiGLU-conv epilogue) instead of a
+    library GEMM writing gu and a SwiGLU kernel reading it back.  Round 5: gu is not stored at all --
+    the backward (g2048_urm_gate_up_swiglu_bwd) recomputes it from x on MFMA, bit for bit, instead of
+    reading 2 inter bf16 per token back (x is h) -- then the input gradient dgu W on g2048_urm_linear_t
+    and the weight gradient on g2048_urm_wgrad.  recompute=False (tests) stores gu and runs
+    g2048_urm_swiglu_conv_bwd on it, the round-4 path.
     x [rows, h] (bf16 or fp32: cast like autocast), w [2 inter, h], cw [inter, 2], cb [inter]."""
+
+    recompute = True
 
     @staticmethod
     def forward(ctx, x: torch.Tensor, w: torch.Tensor, cw: torch.Tensor, cb: torch.Tensor):
         xb = x.to(torch.bfloat16).contiguous()
-        wb = w.detach().to(torch.bfloat16).contiguous()
-        # fresh fp32 copies: the kernel reads the conv parameters as 16-byte vectors
-        cwf = cw.detach().to(torch.float32, copy=True).contiguous()
-        cbf = cb.detach().to(torch.float32, copy=True).contiguous()
+        wb = bf16_weight(w)
+        # the conv parameters as they are (fp32, contiguous views: the kernels stage them through LDS)
+        cwf = cw.detach().float().contiguous()
+        cbf = cb.detach().float().contiguous()
         inter = w.shape[0] // 2
-        gu = torch.empty(xb.shape[0], 2 * inter, dtype=torch.bfloat16, device=x.device)
+        rec = GateUpSwiGLUFn.recompute and L.urm_gate_up_swiglu_bwd_supported(xb.shape[1], inter)
+        gu = None if rec else torch.empty(xb.shape[0], 2 * inter, dtype=torch.bfloat16, device=x.device)
         act = torch.empty(xb.shape[0], inter, dtype=torch.bfloat16, device=x.device)
         L.urm_linear_swiglu_train(xb, wb, cwf, cbf, gu, act)
-        ctx.save_for_backward(xb, wb, gu, cwf, cbf)
+        if rec:
+            ctx.save_for_backward(xb, wb, cwf, cbf)
+        else:
+            ctx.save_for_backward(xb, wb, cwf, cbf, gu)
+        ctx.rec, ctx.inter = rec, inter
         ctx.dtypes = (x.dtype, w.dtype, cw.dtype, cb.dtype)
         return act
 
     @staticmethod
     def backward(ctx, dact: torch.Tensor):
-        xb, wb, gu, cwf, cbf = ctx.saved_tensors
-        rows, inter = gu.shape[0], gu.shape[1] // 2
-        dgu = torch.empty_like(gu)
-        dw = torch.empty(inter, 2, dtype=torch.float32, device=gu.device)
-        db = torch.empty(inter, dtype=torch.float32, device=gu.device)
-        part = torch.empty(L.urm_swiglu_conv_partials(rows // 16, inter), dtype=torch.float32, device=gu.device)
-        L.urm_swiglu_conv_bwd(gu, cwf, cbf, dact.to(torch.bfloat16).contiguous(), dgu, dw, db, part)
-        dx = _gemm(dgu, wb.t().contiguous())  # autocast's bf16 input-gradient GEMM, on MFMA
+        xb, wb, cwf, cbf = ctx.saved_tensors[:4]
+        rows, inter = xb.shape[0], ctx.inter
+        dgu = torch.empty(rows, 2 * inter, dtype=torch.bfloat16, device=xb.device)
+        dw = torch.empty(inter, 2, dtype=torch.float32, device=xb.device)
+        db = torch.empty(inter, dtype=torch.float32, device=xb.device)
+        part = torch.empty(L.urm_swiglu_conv_partials(rows // 16, inter), dtype=torch.float32, device=xb.device)
+        da = dact.to(torch.bfloat16).contiguous()
+        if ctx.rec:
+            L.urm_gate_up_swiglu_bwd(xb, wb, cwf, cbf, da, dgu, dw, db, part)
+        else:
+            L.urm_swiglu_conv_bwd(ctx.saved_tensors[4], cwf, cbf, da, dgu, dw, db, part)
+        dx = _gemm_t(dgu, wb)  # autocast's bf16 input-gradient GEMM, on MFMA
         dW = _wgrad(dgu, xb)          # the weight gradient on g2048_urm_wgrad (fp32)
         return dx.to(ctx.dtypes[0]), dW.to(ctx.dtypes[1]), dw.to(ctx.dtypes[2]), db.to(ctx.dtypes[3])
 
@@ -636,9 +792,9 @@ def gate_up_swiglu_nograd(x: torch.Tensor, w: torch.Tensor, cw: torch.Tensor, cb
     follows autocast's rounding points (gu rounded to bf16 before SwiGLU) and equals the training
     kernel's bit for bit (round 4; round 3 kept the projection in fp32 into the epilogue)."""
     xb = x.to(torch.bfloat16).contiguous()
-    wb = w.detach().to(torch.bfloat16).contiguous()
-    cwf = cw.detach().to(torch.float32, copy=True).contiguous()
-    cbf = cb.detach().to(torch.float32, copy=True).contiguous()
+    wb = bf16_weight(w)
+    cwf = cw.detach().float().contiguous()
+    cbf = cb.detach().float().contiguous()
     act = torch.empty(xb.shape[0], w.shape[0] // 2, dtype=torch.bfloat16, device=x.device)
     L.urm_linear_swiglu_train(xb, wb, cwf, cbf, None, act)
     return act

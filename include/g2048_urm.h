@@ -79,6 +79,12 @@ int g2048_urm_rms_res_fwd2(g2048_stream_t stream, const float *h, const void *a,
                            uint16_t *outb, float *rstd, int64_t rows, int32_t hidden, float eps);
 int g2048_urm_rms_res_bwd2(g2048_stream_t stream, const float *dout, const uint16_t *doutb, const float *out,
                            const float *rstd, float *dh, void *da, int32_t a_dtype, int64_t rows, int32_t hidden);
+/*   bwd3  bwd2, or with dpool (fp32 [rows / 16, 64], instead of dout) as the output gradient broadcast
+ *         over each board's 16 token rows: the backward of GameURM's token mean-pool (game.py:1450,
+ *         dpooled / 16 expanded over the tokens) read without materialising [rows, 64]. */
+int g2048_urm_rms_res_bwd3(g2048_stream_t stream, const float *dout, const float *dpool, const uint16_t *doutb,
+                           const float *out, const float *rstd, float *dh, void *da, int32_t a_dtype, int64_t rows,
+                           int32_t hidden);
 
 /* A GameURM loop start for autograd training (game.py:1441, hidden_states + emb under bf16
  * autocast): out fp32 [rows, hidden] = a + e and outb = bf16(out) (the first block's qkv operand) in
@@ -89,6 +95,11 @@ int g2048_urm_add_cast(g2048_stream_t stream, const float *a, int64_t a_rows, co
                        int64_t rows, int32_t hidden);
 int g2048_urm_add_cast_bwd(g2048_stream_t stream, const float *dout, const uint16_t *doutb, float *dx, int64_t rows,
                            int32_t hidden);
+/* The same, with the loops' emb gradient accumulated in the pass: acc_out = acc_in + dx (acc_in NULL:
+ * dx), the order autograd sums a tensor's incoming gradients in (the last loop's first); dx may be
+ * NULL (h needs no gradient) when acc_out is given. */
+int g2048_urm_add_cast_bwd_acc(g2048_stream_t stream, const float *dout, const uint16_t *doutb, float *dx,
+                               const float *acc_in, float *acc_out, int64_t rows, int32_t hidden);
 
 /* SwiGLU + depthwise conv (kernel 2) for autograd training (GameConvSwiGLU, game.py:1264-1276),
  * n boards of 16 tokens, inter <= 128 channels, the reference's autocast dtypes:
@@ -97,6 +108,17 @@ int g2048_urm_add_cast_bwd(g2048_stream_t stream, const float *dout, const uint1
  *   backward dgu bf16 [16 n, 2 inter], dw fp32 [inter][2], db fp32 [inter] (deterministic column
  *            sums over g2048_urm_swiglu_conv_partials(n, inter) floats of scratch). */
 size_t g2048_urm_swiglu_conv_partials(int64_t n, int32_t inter);
+/* The SwiGLU-conv backward with gu RECOMPUTED from gate_up's operand (round 5; the training forward
+ * then stores act only): gu = bf16(x W^T) on MFMA with the fused forward's fragments and k order
+ * (bitwise the gu g2048_urm_linear_swiglu_train would have stored), then the backward above: dgu
+ * bf16 [16 n, 2 inter], dw fp32 [inter][2], db fp32 [inter] (deterministic; the partial scratch of
+ * g2048_urm_swiglu_conv_partials).  x bf16 [16 n, h], w bf16 [2 inter, h] (gate rows, then up rows),
+ * conv_w fp32 [inter][2], conv_b fp32 [inter] (any 4-byte alignment), dact bf16 [16 n, inter].
+ * h 64 (inter 72..128) or h 32 (inter 40..64), inter % 8 == 0. */
+int g2048_urm_gate_up_swiglu_bwd_supported(int32_t h, int32_t inter);
+int g2048_urm_gate_up_swiglu_bwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, const float *conv_w,
+                                 const float *conv_b, const uint16_t *dact, uint16_t *dgu, float *dw, float *db,
+                                 float *partials, int64_t n, int32_t h, int32_t inter);
 int g2048_urm_swiglu_conv_fwd(g2048_stream_t stream, const uint16_t *gu, const float *w, const float *b, uint16_t *act,
                               int64_t n, int32_t inter);
 int g2048_urm_swiglu_conv_bwd(g2048_stream_t stream, const uint16_t *gu, const float *w, const float *b,
@@ -161,6 +183,11 @@ int g2048_urm_pool_heads(g2048_stream_t stream, const float *x, const float *wa,
 int g2048_urm_linear_supported(int32_t epilogue, int32_t k, int32_t n, int32_t inter);
 int g2048_urm_linear(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, uint16_t *out, int64_t rows,
                      int32_t k, int32_t n);
+/* out [rows, n] = in [rows, k] w with w given as [k, n] row-major: the input gradient dX = dY W of a
+ * projection W [k = out features, n = in features] without a transposed copy of W (the kernel
+ * stages W^T itself).  Same MFMA order as g2048_urm_linear on W^T (bitwise equal). */
+int g2048_urm_linear_t(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, uint16_t *out, int64_t rows,
+                       int32_t k, int32_t n);
 /* g2048_urm_linear with an fp32 bias [n] added to the fp32 accumulator before the one bf16 rounding
  * (autocast's biased Linear: bf16 operands and bias, one rounding of x W^T + b; bias 16-byte aligned). */
 int g2048_urm_linear_bias(g2048_stream_t stream, const uint16_t *in, const uint16_t *w, const float *bias, uint16_t *out,

@@ -977,3 +977,116 @@ def test_urm_config5_trainer_step_full_shape(dev):
     assert m["samples"] == 65536 * 16
     still = {k for k, v in tr.model.named_parameters() if torch.equal(v, before[k])}
     assert still == {"init_hidden"}, still
+
+
+# ------------------------------------------------------------------ round 5 ---------------------
+@pytest.mark.parametrize("h,n", [(64, 65536), (64, 37), (32, 1000)])
+def test_urm_gate_up_recompute_backward_matches_stored_gu(dev, h, n):
+    """GateUpSwiGLUFn with gu recomputed in the backward (g2048_urm_gate_up_swiglu_bwd: the forward
+    stores act only) vs the round-4 path that stores gu and runs g2048_urm_swiglu_conv_bwd on it:
+    the forward is the same kernel (act bitwise), the recomputed gu is the stored one bit for bit, so
+    dgu -- and with it dx and dW -- agrees up to the fma contraction of two separately compiled
+    kernels (<= 1 bf16 step on a handful of elements); dw / db are summed in another fixed order
+    (fp32 rounding: rtol 1e-4)."""
+    import agent
+    from g2048.urm import GateUpSwiGLUFn
+    torch.manual_seed(h * n)
+    mlp = agent.GameConvSwiGLU(h, agent.GameURMConfig().expansion, 2).to(dev)
+    with torch.no_grad():
+        mlp.dwconv.weight.mul_(3.0)
+        mlp.dwconv.bias.uniform_(-0.5, 0.5)
+    x = torch.randn(16 * n, h, device=dev).bfloat16()
+    g = torch.randn(16 * n, mlp.inter, device=dev)
+    params = [mlp.gate_up_proj.weight, mlp.dwconv.weight, mlp.dwconv.bias]
+    res = []
+    try:
+        for rec in (True, False):
+            GateUpSwiGLUFn.recompute = rec
+            mlp.zero_grad()
+            xi = x.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                act = GateUpSwiGLUFn.apply(xi, params[0], params[1].view(-1, 2), params[2])
+            (act.float() * g).sum().backward()
+            res.append([act.detach().float(), xi.grad.float()] + [p.grad.detach().clone() for p in params])
+    finally:
+        GateUpSwiGLUFn.recompute = True
+    assert torch.equal(res[0][0], res[1][0])  # the same forward kernel
+    for k, (a, b) in enumerate(zip(res[0][1:], res[1][1:])):
+        a, b = a.reshape(-1).float(), b.reshape(-1).float()
+        d = (a - b).abs()
+        print(f"grad {k}: max {d.max().item():.3g} of {b.abs().max().item():.3g}, differing {(d > 0).float().mean().item():.2e}")
+        if k == 0:  # dx = dgu W: a contraction flip in dgu moves an element by <= 1 bf16 step
+            assert float(d.max()) <= 2 ** -7 * float(b.abs().max())
+        elif k == 1:  # dW = dgu^T x over 16 n rows: the flips average out in the fp32 sum
+            assert float(d.max()) <= 1e-4 * float(b.abs().max())
+        else:      # dw0 / dw1 / db: another fixed summation order
+            assert torch.allclose(a, b, rtol=1e-4, atol=1e-6 * float(b.abs().max()))
+
+
+@pytest.mark.parametrize("k,n", [(64, 64), (120, 64), (192, 64), (240, 64), (64, 120)])
+def test_urm_linear_t_is_bitwise_the_transposed_copy(dev, k, n):
+    """g2048_urm_linear_t (the input gradient dY W with W^T staged by the kernel itself) is bitwise
+    g2048_urm_linear on W^T's contiguous copy (the round-4 path): same fragments, same MFMA order."""
+    from g2048 import _lib as L
+    torch.manual_seed(k + n)
+    rows = 16 * 4099
+    dy = torch.randn(rows, k, device=dev).bfloat16()
+    w = torch.randn(k, n, device=dev).bfloat16()  # [k = out features, n = in features]
+    a = torch.empty(rows, n, dtype=torch.bfloat16, device=dev)
+    b = torch.empty_like(a)
+    L.urm_linear_t(dy, w, a)
+    L.urm_linear(dy, w.t().contiguous(), b)
+    assert torch.equal(a, b)
+
+
+def test_urm_emb_accumulation_and_mean_pool_are_bitwise_autograd(dev, monkeypatch):
+    """The round-5 backward glue of GameURM: the loops' emb gradient summed inside the AddCastFn
+    backward kernels (EmbGradAcc) and the mean-pool's gradient read as [b, h] by the last residual
+    RMSNorm backward (MeanPoolFn + g2048_urm_rms_res_bwd3) vs autograd's own accumulation adds and
+    materialised mean backward: every parameter gradient bitwise equal (the same sums in the same
+    order), in a GameURM forward with 1 truncated and 3 gradient loops."""
+    import agent
+    from g2048 import urm
+    torch.manual_seed(11)
+    m = agent.GameURM(agent.GameURMConfig(dropout=0.0)).to(dev)
+    obs = torch.randn(512, 48, device=dev)
+    ga, gv = torch.randn(512, 4, device=dev), torch.randn(512, 1, device=dev)
+    grads = []
+    for fused in (True, False):
+        if not fused:  # autograd's accumulation (no accumulator) and torch's mean
+            monkeypatch.setattr(urm, "EmbGradAcc", lambda: None)
+            monkeypatch.setattr(urm.MeanPoolFn, "apply", staticmethod(lambda h: h.mean(dim=1)))
+        m.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            la, lv = m(obs)
+        ((la.float() * ga).sum() + (lv.float() * gv).sum()).backward()
+        grads.append({k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None})
+    assert grads[0].keys() == grads[1].keys() and len(grads[0]) > 10
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), k
+
+
+def test_urm_bf16_weight_cache_tracks_the_optimizer(dev):
+    """Bf16Weights (round 5): the fused Muon step writes the projection weights' bf16 copies with the
+    weights themselves, so after steps the copies equal weight.to(bfloat16) bitwise, and the training
+    Functions read them instead of casting."""
+    import agent
+    from g2048 import urm
+    from g2048.dist import GradBucket
+    from g2048.optim import FusedMuonAdamW
+    torch.manual_seed(5)
+    m = agent.GameURM(agent.GameURMConfig(dropout=0.0)).to(dev)
+    opt = FusedMuonAdamW(m, 1e-3, 1e-4)
+    assert opt.supported
+    order = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
+    bk = GradBucket(order)
+    cache = urm.attach_bf16_weights(m, opt)
+    assert cache is not None and len(cache.pairs) == 4 * len(m.layers)
+    for s in range(3):
+        bk.flat.copy_(torch.randn(bk.flat.shape, generator=torch.Generator().manual_seed(s)).to(dev) * 1e-2)
+        opt.step_clipped(bk.flat, 1.0)
+    torch.cuda.synchronize()
+    for w, t in cache.pairs:
+        assert torch.equal(t, w.detach().to(torch.bfloat16))
+        assert urm.bf16_weight(w) is t
+    cache.detach()

@@ -1,7 +1,8 @@
 """torch.profiler census of the GameURM training iteration's torch-side ops (eager, no graph): which
 aten ops launch the small elementwise / reduce / copy kernels between the device Functions.
-    python tools/prof_urm_ops.py [envs] [horizon] [eager]   (eager: the update without its hipGraph,
-    so every launch is attributed to its aten op and input shapes)"""
+    python tools/prof_urm_ops.py [envs] [horizon] [eager]   (eager: the update without its hipGraph --
+    the same optimizer (the fused Muon/AdamW kernel) and device Functions as the captured update, so
+    every launch is attributed to its aten op and input shapes)"""
 import sys
 from pathlib import Path
 
@@ -19,9 +20,10 @@ def main():
     dev = torch.device("cuda", 0)
     cfg = TrainConfig(steps=1000, lr=1e-3, critic_lr=1e-4, gamma=0.99, entropy=0.02, critic=0.2, episodes=envs,
                       batch_size=65536, hidden=64, model_type="urm", points=0.1, mono=1.0, rtg_beta=0.99,
-                      warmup_steps=10, horizon=T, seed=0x2048, graph=False, amp=True,
-                      graph_update=len(sys.argv) <= 3 or sys.argv[3] != "eager")
+                      warmup_steps=10, horizon=T, seed=0x2048, graph=False, amp=True)
     tr = VecTrainer(cfg, dev)
+    if len(sys.argv) > 3 and sys.argv[3] == "eager":
+        tr.ppo.graph = False  # the captured update's ops, launched one by one
     tr.train_step(0)
     torch.cuda.synchronize()
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:

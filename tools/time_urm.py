@@ -14,7 +14,7 @@ def main():
     import agent
     from g2048 import _lib
     if os.environ.get("G2048_LIB"):  # time a variant build (tools/alt/...) instead of the in-tree library
-        _lib.load(os.environ["G2048_LIB"])
+        _lib._lib = _lib.load(os.environ["G2048_LIB"])
     from g2048.urm import URMPolicy
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     h = int(sys.argv[2]) if len(sys.argv) > 2 else 64
