@@ -350,7 +350,7 @@ def _c_chunk(args):
 
 
 PMC_PROFILE = ROOT / "profiles" / "r04u"
-CPU_RATIO = ROOT / "profiles" / "r02" / "cpu_ref_ratio.json"
+CPU_RATIO = ROOT / "profiles" / "r05b" / "cpu_ref_ratio.json"  # re-measured in round 5 (r02: 1.45 / 1.14)
 
 
 def rollout_counters():
