@@ -339,12 +339,32 @@ class GameURM(nn.Module):
     def forward(self, inputs: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
         if inputs.ndim == 1:
             inputs = inputs.unsqueeze(0)
-        b = inputs.shape[0]
         if inputs.is_cuda and self.training and not torch.is_grad_enabled():
             from g2048 import urm as _urm  # training-mode no-grad forward (the KL re-forward) in one launch
             out = _urm.train_nograd_forward(self, inputs)
             if out is not None:
                 return out
+        pooled = self.features(inputs)
+        if pooled.is_cuda:
+            from g2048 import urm as _urm  # both heads as one device projection (training, g2048_urm.h)
+            if _urm.heads_supported(self, pooled):
+                return _urm.URMHeadsFn.apply(pooled, self.action_head.weight, self.action_head.bias,
+                                             self.value_head.weight, self.value_head.bias)
+        return self.action_head(pooled), self.value_head(pooled)
+
+    def features(self, inputs: torch.Tensor) -> torch.Tensor:
+        """The pooled features [b, h] the two heads read (game.py:1409-1451): stem, loops, token mean.
+        On the device its attention applications share one dropout-counter scope (urm.attn_forward)."""
+        if inputs.ndim == 1:
+            inputs = inputs.unsqueeze(0)
+        if not inputs.is_cuda:
+            return self._features(inputs)
+        from g2048 import urm as _urm
+        with _urm.attn_forward(inputs.device):
+            return self._features(inputs)
+
+    def _features(self, inputs: torch.Tensor) -> torch.Tensor:
+        b = inputs.shape[0]
         emb = None
         if inputs.is_cuda:
             from g2048 import urm as _urm  # the device training stem and its backward (g2048_urm.h)
@@ -373,15 +393,8 @@ class GameURM(nn.Module):
             h = self._loop(h, emb, acc)
         if h.is_cuda and torch.is_grad_enabled() and h.requires_grad and h.dim() == 3 and h.shape[1] == N_CELLS:
             from g2048 import urm as _urm  # its backward hands the last RMSNorm a [b, h] gradient
-            pooled = _urm.MeanPoolFn.apply(h)
-        else:
-            pooled = h.mean(dim=1)
-        if pooled.is_cuda:
-            from g2048 import urm as _urm  # both heads as one device projection (training, g2048_urm.h)
-            if _urm.heads_supported(self, pooled):
-                return _urm.URMHeadsFn.apply(pooled, self.action_head.weight, self.action_head.bias,
-                                             self.value_head.weight, self.value_head.bias)
-        return self.action_head(pooled), self.value_head(pooled)
+            return _urm.MeanPoolFn.apply(h)
+        return h.mean(dim=1)
 
 
 def mlp_flops_per_sample(hidden: int, layers: int) -> int:

@@ -137,6 +137,7 @@ struct AttnDrop {
     float scale;
     uint32_t k0, k1;
     const uint64_t *counter;  // device call counter (graph-replay safe)
+    uint64_t offset;          // this application's offset from *counter (round 5: one counter bump per forward)
 };
 __device__ __forceinline__ void attn_keep_c(const AttnDrop &d, uint64_t c, int64_t b, int hh, int i, int g, float km[4]) {
     const uint4 r = g2048::philox((uint32_t)b, ((uint32_t)hh << 8) | ((uint32_t)i << 2) | (uint32_t)g, (uint32_t)c,
@@ -147,7 +148,7 @@ __device__ __forceinline__ void attn_keep_c(const AttnDrop &d, uint64_t c, int64
     km[3] = (r.y >> 16) >= d.thr ? d.scale : 0.0f;
 }
 __device__ __forceinline__ void attn_keep(const AttnDrop &d, int64_t b, int hh, int i, int g, float km[4]) {
-    attn_keep_c(d, *d.counter, b, hh, i, g, km);
+    attn_keep_c(d, *d.counter + d.offset, b, hh, i, g, km);
 }
 
 template <bool kAligned, bool kDrop>
@@ -1534,7 +1535,8 @@ __global__ __launch_bounds__(256) void urm_swiglu_conv_bwd2_kernel(const uint16_
 // a block per 16 columns, 16 row slices per column (slice s sums rows s, s + 16, ... in order, 8
 // loads in flight), then the 16 slice sums added in slice order -- a fixed order, deterministic.
 __global__ __launch_bounds__(256) void urm_swiglu_conv_colsum_kernel(const float *__restrict__ part, int nblk, int inter,
-                                                                     float *__restrict__ dw, float *__restrict__ db) {
+                                                                     float *__restrict__ dw, float *__restrict__ db,
+                                                                     int acc) {
     __shared__ float red[16][17];
     const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
     const int j = blockIdx.x * 16 + cl, ncol = 3 * inter;
@@ -1556,9 +1558,10 @@ __global__ __launch_bounds__(256) void urm_swiglu_conv_colsum_kernel(const float
     t = 0.0f;
 #pragma unroll
     for (int u = 0; u < 16; u++) t += red[u][cl];
-    if (j < inter) dw[2 * j] = t;
-    else if (j < 2 * inter) dw[2 * (j - inter) + 1] = t;
-    else db[j - 2 * inter] = t;
+    // acc: added to the gradient already there (a weight shared by several applications, summed in
+    // autograd's order: the same bits as its accumulation of returned gradients)
+    float *o = j < inter ? dw + 2 * j : j < 2 * inter ? dw + 2 * (j - inter) + 1 : db + (j - 2 * inter);
+    *o = acc ? *o + t : t;
 }
 
 // Training-path stem of GameURM (game.py:1376-1380: Linear(3 -> 64, no bias) + LayerNorm + SiLU)
@@ -1680,7 +1683,8 @@ __global__ __launch_bounds__(256) void urm_stem_bwd_kernel(const void *__restric
 
 // out[c] = sum over the nblk partial rows of column c, in row order per slice (see the swiglu one)
 __global__ __launch_bounds__(256) void urm_colsum_kernel(const float *__restrict__ part, int nblk, int ncol,
-                                                         float *__restrict__ out) {
+                                                         float *__restrict__ out, int acc = 0, float *out2 = nullptr,
+                                                         int j2 = 0, float *out3 = nullptr, int j3 = 0) {
     __shared__ float red[16][17];
     const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
     const int j = blockIdx.x * 16 + cl;
@@ -1702,7 +1706,9 @@ __global__ __launch_bounds__(256) void urm_colsum_kernel(const float *__restrict
     t = 0.0f;
 #pragma unroll
     for (int u = 0; u < 16; u++) t += red[u][cl];
-    out[j] = t;
+    // columns j2.. / j3.. to their own outputs when given (one launch for several parameters)
+    float *o = out3 && j >= j3 ? out3 + (j - j3) : out2 && j >= j2 ? out2 + (j - j2) : out + j;
+    *o = acc ? *o + t : t;
 }
 
 // Weight gradient of a projection for autograd training (the URM Functions' backward and any
@@ -2046,11 +2052,12 @@ static bool attn_drop_args(float p, uint64_t seed, const uint64_t *counter, Attn
     return d.thr == 0 || counter != nullptr;
 }
 
-int g2048_urm_attention_drop(g2048_stream_t stream, const uint16_t *qkv, uint16_t *out, int64_t n, int32_t h,
-                             int32_t heads, float p, uint64_t seed, const uint64_t *counter) {
+int g2048_urm_attention_drop_at(g2048_stream_t stream, const uint16_t *qkv, uint16_t *out, int64_t n, int32_t h,
+                                int32_t heads, float p, uint64_t seed, const uint64_t *counter, uint64_t offset) {
     AttnDrop d{};
     if (n < 0 || !h_ok(h) || heads <= 0 || h % heads != 0 || h / heads > 64) return G2048_EINVAL;
     if (!attn_drop_args(p, seed, counter, d)) return G2048_EINVAL;
+    d.offset = offset;
     if (n == 0) return G2048_OK;
     if (!qkv || !out) return G2048_EINVAL;
     const int64_t tasks = n * heads;
@@ -2064,16 +2071,23 @@ int g2048_urm_attention_drop(g2048_stream_t stream, const uint16_t *qkv, uint16_
     return launch_status();
 }
 
+int g2048_urm_attention_drop(g2048_stream_t stream, const uint16_t *qkv, uint16_t *out, int64_t n, int32_t h,
+                             int32_t heads, float p, uint64_t seed, const uint64_t *counter) {
+    return g2048_urm_attention_drop_at(stream, qkv, out, n, h, heads, p, seed, counter, 0);
+}
+
 int g2048_urm_attention(g2048_stream_t stream, const uint16_t *qkv, uint16_t *out, int64_t n, int32_t h,
                         int32_t heads) {
     return g2048_urm_attention_drop(stream, qkv, out, n, h, heads, 0.0f, 0, nullptr);
 }
 
-int g2048_urm_attention_bwd_drop(g2048_stream_t stream, const uint16_t *qkv, const uint16_t *dout, uint16_t *dqkv,
-                                 int64_t n, int32_t h, int32_t heads, float p, uint64_t seed, const uint64_t *counter) {
+int g2048_urm_attention_bwd_drop_at(g2048_stream_t stream, const uint16_t *qkv, const uint16_t *dout,
+                                    uint16_t *dqkv, int64_t n, int32_t h, int32_t heads, float p, uint64_t seed,
+                                    const uint64_t *counter, uint64_t offset) {
     AttnDrop d{};
     if (n < 0 || heads <= 0 || h != 16 * heads || h > 512) return G2048_EINVAL;
     if (!attn_drop_args(p, seed, counter, d)) return G2048_EINVAL;
+    d.offset = offset;
     if (n == 0) return G2048_OK;
     if (!qkv || !dout || !dqkv || ((uintptr_t)qkv | (uintptr_t)dout | (uintptr_t)dqkv) % 8) return G2048_EINVAL;
     const int64_t tasks = n * heads;
@@ -2084,6 +2098,11 @@ int g2048_urm_attention_bwd_drop(g2048_stream_t stream, const uint16_t *qkv, con
         hipLaunchKernelGGL(urm_attn_bwd16_kernel<false>, dim3(blocks(tasks, 4)), dim3(256), 0, (hipStream_t)stream, qkv,
                            dout, dqkv, tasks, (int)h, (int)heads, d);
     return launch_status();
+}
+
+int g2048_urm_attention_bwd_drop(g2048_stream_t stream, const uint16_t *qkv, const uint16_t *dout, uint16_t *dqkv,
+                                 int64_t n, int32_t h, int32_t heads, float p, uint64_t seed, const uint64_t *counter) {
+    return g2048_urm_attention_bwd_drop_at(stream, qkv, dout, dqkv, n, h, heads, p, seed, counter, 0);
 }
 
 int g2048_urm_attention_bwd(g2048_stream_t stream, const uint16_t *qkv, const uint16_t *dout, uint16_t *dqkv,
@@ -2193,9 +2212,9 @@ int g2048_urm_gate_up_swiglu_bwd_supported(int32_t h, int32_t inter) {
                ? 1 : 0;
 }
 
-int g2048_urm_gate_up_swiglu_bwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, const float *conv_w,
-                                 const float *conv_b, const uint16_t *dact, uint16_t *dgu, float *dw, float *db,
-                                 float *partials, int64_t n, int32_t h, int32_t inter) {
+int g2048_urm_gate_up_swiglu_bwd_acc(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, const float *conv_w,
+                                     const float *conv_b, const uint16_t *dact, uint16_t *dgu, float *dw, float *db,
+                                     float *partials, int64_t n, int32_t h, int32_t inter, int32_t accumulate) {
     if (n <= 0 || !g2048_urm_gate_up_swiglu_bwd_supported(h, inter)) return G2048_EINVAL;
     if (!x || !w || !conv_w || !conv_b || !dact || !dgu || !dw || !db || !partials ||
         ((uintptr_t)x | (uintptr_t)dgu) % 16 || ((uintptr_t)w | (uintptr_t)dact) % 8)
@@ -2209,8 +2228,14 @@ int g2048_urm_gate_up_swiglu_bwd(g2048_stream_t stream, const uint16_t *x, const
     else st = launch_gus_bwd<1, 8>(s, x, w, conv_w, conv_b, dact, dgu, partials, rows, h, inter, nrows);
     if (st) return st;
     hipLaunchKernelGGL(urm_swiglu_conv_colsum_kernel, dim3((3 * inter + 15) / 16), dim3(256), 0, s, partials, nrows,
-                       (int)inter, dw, db);
+                       (int)inter, dw, db, accumulate ? 1 : 0);
     return launch_status();
+}
+
+int g2048_urm_gate_up_swiglu_bwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, const float *conv_w,
+                                 const float *conv_b, const uint16_t *dact, uint16_t *dgu, float *dw, float *db,
+                                 float *partials, int64_t n, int32_t h, int32_t inter) {
+    return g2048_urm_gate_up_swiglu_bwd_acc(stream, x, w, conv_w, conv_b, dact, dgu, dw, db, partials, n, h, inter, 0);
 }
 
 int g2048_urm_swiglu_conv_fwd(g2048_stream_t stream, const uint16_t *gu, const float *w, const float *b, uint16_t *act,
@@ -2243,7 +2268,7 @@ int g2048_urm_swiglu_conv_bwd(g2048_stream_t stream, const uint16_t *gu, const f
         hipLaunchKernelGGL(urm_swiglu_conv_bwd_kernel, dim3(nblk), dim3(kScThreads), 0, s, gu, w, b, dact, dgu, partials,
                            n, (int)inter);
     hipLaunchKernelGGL(urm_swiglu_conv_colsum_kernel, dim3((3 * inter + 15) / 16), dim3(256), 0, s, partials, nblk,
-                       (int)inter, dw, db);
+                       (int)inter, dw, db, 0);
     return launch_status();
 }
 
@@ -2270,11 +2295,12 @@ int g2048_urm_stem_fwd(g2048_stream_t stream, const void *obs, int32_t obs_dtype
     return launch_status();
 }
 
-int g2048_urm_stem_bwd(g2048_stream_t stream, const void *obs, int32_t obs_dtype, const float *w, const float *ln_w,
-                       const float *ln_b, const float *demb, float *grads, float *partials, int64_t n, int32_t h,
-                       float eps) {
+int g2048_urm_stem_bwd3(g2048_stream_t stream, const void *obs, int32_t obs_dtype, const float *w, const float *ln_w,
+                        const float *ln_b, const float *demb, float *dw, float *dln_w, float *dln_b, int32_t accumulate,
+                        float *partials, int64_t n, int32_t h, float eps) {
     if (n <= 0 || h != 64 || (obs_dtype != 0 && obs_dtype != 1)) return G2048_EINVAL;
-    if (!obs || !w || !ln_w || !ln_b || !demb || !grads || !partials || (uintptr_t)demb % 16) return G2048_EINVAL;
+    if (!obs || !w || !ln_w || !ln_b || !demb || !dw || !dln_w || !dln_b || !partials || (uintptr_t)demb % 16)
+        return G2048_EINVAL;
     const int64_t rows = 16 * n;
     const int nblk = stem_blocks(rows);
     const hipStream_t s = (hipStream_t)stream;
@@ -2285,8 +2311,16 @@ int g2048_urm_stem_bwd(g2048_stream_t stream, const void *obs, int32_t obs_dtype
         hipLaunchKernelGGL(urm_stem_bwd_kernel<false>, dim3(nblk), dim3(256), 0, s, obs, w, ln_w, ln_b, demb, partials,
                            rows, eps);
     hipLaunchKernelGGL(urm_colsum_kernel, dim3((kStemCols + 15) / 16), dim3(256), 0, s, partials, nblk, kStemCols,
-                       grads);
+                       dw, accumulate ? 1 : 0, dln_w, 192, dln_b, 256);
     return launch_status();
+}
+
+int g2048_urm_stem_bwd(g2048_stream_t stream, const void *obs, int32_t obs_dtype, const float *w, const float *ln_w,
+                       const float *ln_b, const float *demb, float *grads, float *partials, int64_t n, int32_t h,
+                       float eps) {
+    if (!grads) return G2048_EINVAL;
+    return g2048_urm_stem_bwd3(stream, obs, obs_dtype, w, ln_w, ln_b, demb, grads, grads + 192, grads + 256, 0, partials,
+                               n, h, eps);
 }
 
 static int wgrad_blocks(int64_t m) {
@@ -2304,8 +2338,9 @@ size_t g2048_urm_wgrad_partials(int64_t m, int32_t n, int32_t k) {
     return (size_t)wgrad_blocks(m) * n * k;
 }
 
-int g2048_urm_wgrad(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x, float *dw, float *partials,
-                    int64_t m, int32_t n, int32_t k) {
+int g2048_urm_wgrad_acc(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x, float *dw, float *partials,
+                        int64_t m, int32_t n, int32_t k, int32_t accumulate) {
+    const int acc = accumulate ? 1 : 0;
     if (m <= 0 || !g2048_urm_wgrad_supported(n, k)) return G2048_EINVAL;
     if (!dy || !x || !dw || !partials || ((uintptr_t)dy | (uintptr_t)x) % 16) return G2048_EINVAL;
     const int nblk = wgrad_blocks(m);
@@ -2325,7 +2360,7 @@ int g2048_urm_wgrad(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x
         else ring = false;
         if (ring) {
             hipLaunchKernelGGL(urm_colsum_kernel, dim3((unsigned)((n * k + 15) / 16)), dim3(256), 0, s, partials, nblk,
-                               (int)(n * k), dw);
+                               (int)(n * k), dw, acc);
             return launch_status();
         }
     }
@@ -2337,8 +2372,13 @@ int g2048_urm_wgrad(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x
     hipLaunchKernelGGL(urm_wgrad_kernel, dim3(nblk), dim3(kWgThreads), lds, s, dy, x, m, (int)n, (int)k, kp, rows,
                        partials);
     hipLaunchKernelGGL(urm_colsum_kernel, dim3((unsigned)((n * k + 15) / 16)), dim3(256), 0, s, partials, nblk,
-                       (int)(n * k), dw);
+                       (int)(n * k), dw, acc);
     return launch_status();
+}
+
+int g2048_urm_wgrad(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x, float *dw, float *partials,
+                    int64_t m, int32_t n, int32_t k) {
+    return g2048_urm_wgrad_acc(stream, dy, x, dw, partials, m, n, k, 0);
 }
 
 int g2048_urm_residual_rms(g2048_stream_t stream, float *x, const uint16_t *y, const float *emb, uint16_t *xb,

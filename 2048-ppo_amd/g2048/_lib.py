@@ -35,7 +35,7 @@ EXPORTED = (
     "g2048_colsum_batch_blocks", "g2048_colsum_batch_sq",
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_wgrad_pair_partials", "g2048_wgrad_pair", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
-    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_muon_workspace_bytes", "g2048_muon_error_offset", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_rms_res_fwd2", "g2048_urm_rms_res_bwd2", "g2048_urm_rms_res_bwd3", "g2048_urm_add_cast", "g2048_urm_add_cast_bwd", "g2048_urm_add_cast_bwd_acc", "g2048_urm_forward_drop", "g2048_urm_rms_res_fwd",
+    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_muon_workspace_bytes", "g2048_muon_error_offset", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_attention_drop_at", "g2048_urm_attention_bwd_drop_at", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_stem_bwd3", "g2048_urm_rms_res_fwd2", "g2048_urm_rms_res_bwd2", "g2048_urm_rms_res_bwd3", "g2048_urm_add_cast", "g2048_urm_add_cast_bwd", "g2048_urm_add_cast_bwd_acc", "g2048_urm_forward_drop", "g2048_urm_rms_res_fwd",
     "g2048_urm_rms_res_bwd", "g2048_urm_swiglu_conv_partials", "g2048_urm_swiglu_conv_fwd", "g2048_urm_swiglu_conv_bwd",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
@@ -45,7 +45,7 @@ EXPORTED = (
     # include/g2048_urm.h
     "g2048_urm_stem", "g2048_urm_attention", "g2048_urm_residual_rms", "g2048_urm_swiglu_conv",
     "g2048_urm_pool_heads", "g2048_urm_linear_supported", "g2048_urm_linear", "g2048_urm_linear_rms",
-    "g2048_urm_linear_swiglu", "g2048_urm_linear_swiglu_train", "g2048_urm_linear_t", "g2048_urm_gate_up_swiglu_bwd_supported", "g2048_urm_gate_up_swiglu_bwd", "g2048_urm_linear_res_rms", "g2048_urm_linear_bias", "g2048_urm_wgrad_supported", "g2048_urm_wgrad_partials", "g2048_urm_wgrad", "g2048_urm_forward_supported", "g2048_urm_forward",
+    "g2048_urm_linear_swiglu", "g2048_urm_linear_swiglu_train", "g2048_urm_linear_t", "g2048_urm_gate_up_swiglu_bwd_supported", "g2048_urm_gate_up_swiglu_bwd", "g2048_urm_gate_up_swiglu_bwd_acc", "g2048_urm_linear_res_rms", "g2048_urm_linear_bias", "g2048_urm_wgrad_supported", "g2048_urm_wgrad_partials", "g2048_urm_wgrad", "g2048_urm_wgrad_acc", "g2048_urm_head_loss_partials", "g2048_urm_head_loss", "g2048_urm_head_loss_bwd", "g2048_urm_kl_stats", "g2048_urm_forward_supported", "g2048_urm_forward",
 )
 
 
@@ -285,9 +285,17 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_urm_linear_t": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_gate_up_swiglu_bwd_supported": (ctypes.c_int, [i32, i32]),
         "g2048_urm_gate_up_swiglu_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32]),
+        "g2048_urm_gate_up_swiglu_bwd_acc": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32]),
         "g2048_urm_wgrad_supported": (ctypes.c_int, [i32, i32]),
         "g2048_urm_wgrad_partials": (sz, [i64, i32, i32]),
         "g2048_urm_wgrad": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32]),
+        "g2048_urm_wgrad_acc": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32, i32]),
+        "g2048_urm_head_loss_partials": (sz, [i64, i32]),
+        "g2048_urm_head_loss": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, i64, i32, bp, vp, ctypes.c_float,
+                                               ctypes.c_float, vp, vp, vp, vp, vp, vp]),
+        "g2048_urm_head_loss_bwd": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i64,
+                                                   i32]),
+        "g2048_urm_kl_stats": (ctypes.c_int, [vp, vp, vp, i64, vp, vp, vp, ctypes.c_float, vp, vp, vp]),
         "g2048_muon_supported": (ctypes.c_int, [i32, i32]),
         "g2048_muon_step": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.POINTER(MuonCfg)]),
         "g2048_grad_sumsq": (ctypes.c_int, [vp, vp, i64, vp]),
@@ -308,9 +316,15 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_urm_stem_partials": (sz, [i64]),
         "g2048_urm_stem_fwd": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, i64, i32, ctypes.c_float]),
         "g2048_urm_stem_bwd": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, vp, vp, i64, i32, ctypes.c_float]),
+        "g2048_urm_stem_bwd3": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, i32, vp, i64, i32,
+                                               ctypes.c_float]),
         "g2048_urm_attention_drop": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, ctypes.c_float, ctypes.c_uint64, vp]),
         "g2048_urm_attention_bwd_drop": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32, ctypes.c_float, ctypes.c_uint64,
                                                         vp]),
+        "g2048_urm_attention_drop_at": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, ctypes.c_float, ctypes.c_uint64, vp,
+                                                       ctypes.c_uint64]),
+        "g2048_urm_attention_bwd_drop_at": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32, ctypes.c_float,
+                                                           ctypes.c_uint64, vp, ctypes.c_uint64]),
         "g2048_urm_rms_res_fwd": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, i64, i32, ctypes.c_float]),
         "g2048_urm_rms_res_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i32, i64, i32]),
         "g2048_urm_swiglu_conv_partials": (sz, [i64, i32]),
@@ -1028,26 +1042,30 @@ def urm_stem(obs, w, ln_w, ln_b, init_hidden, emb, x, xb):
                                  _dev(xb, torch.bfloat16, "xb"), n, h), "g2048_urm_stem")
 
 
-def urm_attention(qkv, out, heads: int, p: float = 0.0, seed: int = 0, counter=None):
-    """counter: device int64 [1] call counter of the dropout mask (required when p > 0)."""
+def urm_attention(qkv, out, heads: int, p: float = 0.0, seed: int = 0, counter=None, offset: int = 0):
+    """counter: device int64 [1] call counter of the dropout mask (required when p > 0); the mask is
+    keyed by *counter + offset."""
     rows, h3 = qkv.shape
     if p > 0.0:
-        _check(load().g2048_urm_attention_drop(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"),
-                                               _dev(out, torch.bfloat16, "out"), rows // 16, h3 // 3, int(heads),
-                                               float(p), int(seed) & (2 ** 64 - 1), _dev(counter, torch.int64, "counter")),
-               "g2048_urm_attention_drop")
+        _check(load().g2048_urm_attention_drop_at(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"),
+                                                  _dev(out, torch.bfloat16, "out"), rows // 16, h3 // 3, int(heads),
+                                                  float(p), int(seed) & (2 ** 64 - 1),
+                                                  _dev(counter, torch.int64, "counter"), int(offset)),
+               "g2048_urm_attention_drop_at")
         return
     _check(load().g2048_urm_attention(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"), _dev(out, torch.bfloat16, "out"),
                                       rows // 16, h3 // 3, int(heads)), "g2048_urm_attention")
 
 
-def urm_attention_bwd(qkv, dout, dqkv, heads: int, p: float = 0.0, seed: int = 0, counter=None):
+def urm_attention_bwd(qkv, dout, dqkv, heads: int, p: float = 0.0, seed: int = 0, counter=None, offset: int = 0):
     rows, h3 = qkv.shape
     if p > 0.0:
-        _check(load().g2048_urm_attention_bwd_drop(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"),
-                                                   _dev(dout, torch.bfloat16, "dout"), _dev(dqkv, torch.bfloat16, "dqkv"),
-                                                   rows // 16, h3 // 3, int(heads), float(p), int(seed) & (2 ** 64 - 1),
-                                                   _dev(counter, torch.int64, "counter")), "g2048_urm_attention_bwd_drop")
+        _check(load().g2048_urm_attention_bwd_drop_at(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"),
+                                                      _dev(dout, torch.bfloat16, "dout"),
+                                                      _dev(dqkv, torch.bfloat16, "dqkv"), rows // 16, h3 // 3, int(heads),
+                                                      float(p), int(seed) & (2 ** 64 - 1),
+                                                      _dev(counter, torch.int64, "counter"), int(offset)),
+               "g2048_urm_attention_bwd_drop_at")
         return
     _check(load().g2048_urm_attention_bwd(_stream(qkv), _dev(qkv, torch.bfloat16, "qkv"),
                                           _dev(dout, torch.bfloat16, "dout"), _dev(dqkv, torch.bfloat16, "dqkv"),
@@ -1078,6 +1096,17 @@ def urm_stem_bwd(obs, w, ln_w, ln_b, demb, grads, partials, eps: float):
                                      _dev(demb, torch.float32, "demb"), _dev(grads, torch.float32, "grads"),
                                      _dev(partials, torch.float32, "partials"), rows // 16, h, float(eps)),
            "g2048_urm_stem_bwd")
+
+
+def urm_stem_bwd3(obs, w, ln_w, ln_b, demb, dw, dln_w, dln_b, partials, eps: float, accumulate: bool = False):
+    """g2048_urm_stem_bwd3: the three stem gradients at their own addresses (accumulate: added to)."""
+    rows, h = demb.shape
+    _check(load().g2048_urm_stem_bwd3(_stream(obs), _dev(obs, None, "obs"), _obs_dtype(obs), _dev(w, torch.float32, "w"),
+                                      _dev(ln_w, torch.float32, "ln_w"), _dev(ln_b, torch.float32, "ln_b"),
+                                      _dev(demb, torch.float32, "demb"), _dev(dw, torch.float32, "dw"),
+                                      _dev(dln_w, torch.float32, "dln_w"), _dev(dln_b, torch.float32, "dln_b"),
+                                      int(bool(accumulate)), _dev(partials, torch.float32, "partials"), rows // 16, h,
+                                      float(eps)), "g2048_urm_stem_bwd3")
 
 
 def urm_rms_res_fwd(h, a, out, rstd, eps: float, outb=None):
@@ -1131,16 +1160,18 @@ def urm_gate_up_swiglu_bwd_supported(h: int, inter: int) -> bool:
     return bool(load().g2048_urm_gate_up_swiglu_bwd_supported(h, inter))
 
 
-def urm_gate_up_swiglu_bwd(x, w, conv_w, conv_b, dact, dgu, dw, db, partials):
-    """dgu, dw, db of the SwiGLU-conv with gu = bf16(x w^T) recomputed on MFMA (g2048_urm_gate_up_swiglu_bwd)."""
+def urm_gate_up_swiglu_bwd(x, w, conv_w, conv_b, dact, dgu, dw, db, partials, accumulate: bool = False):
+    """dgu, dw, db of the SwiGLU-conv with gu = bf16(x w^T) recomputed on MFMA
+    (g2048_urm_gate_up_swiglu_bwd_acc; accumulate: dw / db += the sums)."""
     rows, h = x.shape
     inter = w.shape[0] // 2
-    _check(load().g2048_urm_gate_up_swiglu_bwd(_stream(x), _dev(x, torch.bfloat16, "x"), _dev(w, torch.bfloat16, "w"),
-                                               _dev(conv_w, torch.float32, "conv_w"), _dev(conv_b, torch.float32, "conv_b"),
-                                               _dev(dact, torch.bfloat16, "dact"), _dev(dgu, torch.bfloat16, "dgu"),
-                                               _dev(dw, torch.float32, "dw"), _dev(db, torch.float32, "db"),
-                                               _dev(partials, torch.float32, "partials"), rows // 16, h, inter),
-           "g2048_urm_gate_up_swiglu_bwd")
+    _check(load().g2048_urm_gate_up_swiglu_bwd_acc(_stream(x), _dev(x, torch.bfloat16, "x"), _dev(w, torch.bfloat16, "w"),
+                                                   _dev(conv_w, torch.float32, "conv_w"),
+                                                   _dev(conv_b, torch.float32, "conv_b"),
+                                                   _dev(dact, torch.bfloat16, "dact"), _dev(dgu, torch.bfloat16, "dgu"),
+                                                   _dev(dw, torch.float32, "dw"), _dev(db, torch.float32, "db"),
+                                                   _dev(partials, torch.float32, "partials"), rows // 16, h, inter,
+                                                   int(bool(accumulate))), "g2048_urm_gate_up_swiglu_bwd_acc")
 
 
 def urm_swiglu_conv_fwd(gu, w, b, act):
@@ -1234,12 +1265,56 @@ def urm_wgrad_partials(m: int, n: int, k: int) -> int:
     return int(load().g2048_urm_wgrad_partials(m, n, k))
 
 
-def urm_wgrad(dy, x, dw, partials):
-    """dw fp32 [n, k] = dy^T x (g2048_urm_wgrad); dy bf16 [m, n], x bf16 [m, k]."""
+def urm_head_loss_partials(m: int, h: int) -> int:
+    return int(load().g2048_urm_head_loss_partials(m, h))
+
+
+def _pooled_dtype(t) -> int:
+    if t.dtype not in (torch.float32, torch.bfloat16):
+        raise G2048Error("pooled must be float32 or bfloat16")
+    return int(t.dtype == torch.bfloat16)
+
+
+def urm_head_loss(pooled, wa, ba, wv, bv, batch: PPOBatch, beta_dev, critic, clip_eps, dz, masked, partials, sync,
+                  sums, loss):
+    """GameURM's heads + PPO loss + dz / masked / sums / loss (g2048_urm_head_loss)."""
+    m, h = pooled.shape
+    _check(load().g2048_urm_head_loss(
+        _stream(pooled), _dev(pooled, None, "pooled"), _pooled_dtype(pooled), _dev(wa, torch.float32, "wa"),
+        _dev(ba, torch.float32, "ba"), _dev(wv, torch.float32, "wv"), _dev(bv, torch.float32, "bv"), m, h,
+        ctypes.byref(batch), _dev(beta_dev, torch.float32, "beta"), float(critic), float(clip_eps),
+        _dev(dz, torch.float32, "dz"), _dev(masked, torch.float32, "masked"), _dev(partials, torch.float32, "partials"),
+        _dev(sync, torch.int32, "sync"), _dev(sums, torch.float32, "sums"), _dev(loss, torch.float32, "loss")),
+        "g2048_urm_head_loss")
+
+
+def urm_head_loss_bwd(pooled, wa, wv, dz, grad_out, dpooled, partials, sync, dwa, dba, dwv, dbv,
+                      accumulate: bool = False):
+    """dpooled and the head gradients of g2048_urm_head_loss (g2048_urm_head_loss_bwd)."""
+    m, h = pooled.shape
+    _check(load().g2048_urm_head_loss_bwd(
+        _stream(pooled), _dev(pooled, None, "pooled"), _pooled_dtype(pooled), _dev(wa, torch.float32, "wa"),
+        _dev(wv, torch.float32, "wv"), _dev(dz, torch.float32, "dz"), _dev(grad_out, torch.float32, "grad_out"),
+        _dev(dpooled, pooled.dtype, "dpooled"), _dev(partials, torch.float32, "partials"), _dev(sync, torch.int32, "sync"),
+        _dev(dwa, torch.float32, "dwa"), _dev(dba, torch.float32, "dba"), _dev(dwv, torch.float32, "dwv"),
+        _dev(dbv, torch.float32, "dbv"), int(bool(accumulate)), m, h), "g2048_urm_head_loss_bwd")
+
+
+def urm_kl_stats(old_masked, logits, sums, gn, beta_dev, critic, stats, partials, sync):
+    """KL(old || new) + the minibatch statistics update (g2048_urm_kl_stats)."""
+    _check(load().g2048_urm_kl_stats(
+        _stream(logits), _dev(old_masked, torch.float32, "old_masked"), _dev(logits, torch.float32, "logits"),
+        logits.shape[0], _dev(sums, torch.float32, "sums"), _dev(gn, torch.float32, "gn"),
+        _dev(beta_dev, torch.float32, "beta"), float(critic), _dev(stats, torch.float32, "stats"),
+        _dev(partials, torch.float32, "partials"), _dev(sync, torch.int32, "sync")), "g2048_urm_kl_stats")
+
+
+def urm_wgrad(dy, x, dw, partials, accumulate: bool = False):
+    """dw fp32 [n, k] = dy^T x (g2048_urm_wgrad_acc; accumulate: dw += dy^T x); dy bf16 [m, n], x bf16 [m, k]."""
     m, n = dy.shape
-    _check(load().g2048_urm_wgrad(_stream(dy), _dev(dy, torch.bfloat16, "dy"), _dev(x, torch.bfloat16, "x"),
-                                  _dev(dw, torch.float32, "dw"), _dev(partials, torch.float32, "partials"), m, n,
-                                  x.shape[1]), "g2048_urm_wgrad")
+    _check(load().g2048_urm_wgrad_acc(_stream(dy), _dev(dy, torch.bfloat16, "dy"), _dev(x, torch.bfloat16, "x"),
+                                      _dev(dw, torch.float32, "dw"), _dev(partials, torch.float32, "partials"), m, n,
+                                      x.shape[1], int(bool(accumulate))), "g2048_urm_wgrad_acc")
 
 
 def urm_linear_swiglu_train(inp, w, conv_w, conv_b, gu, act):

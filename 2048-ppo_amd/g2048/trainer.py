@@ -22,6 +22,7 @@ import torch
 from . import _lib as L
 from . import fastmlp
 from . import urm as urm_mod
+from . import urmppo
 from .advantage import RewardWeights, RTGTracker
 from .dist import GradBucket, allreduce_min_, allreduce_sum_, broadcast_, equal_rows, world
 from .dist import graph as graph_capture
@@ -145,6 +146,11 @@ class VecTrainer:
         if cfg.fused_update and cfg.amp and self.dev.type == "cuda" and fastmlp.supports(self.model):
             self.ppo = fastmlp.FusedPPOUpdater(self.model, self.opt, pcfg, self.grads, gen, graph=graph_up,
                                                seed=cfg.seed * 31 + self.rank)
+        elif (cfg.fused_update and cfg.amp and self.dev.type == "cuda" and urm_mod.training_graph_ok(self.model)
+              and urmppo.supports(self.model, pcfg.amp_dtype)):
+            # GameURM: the loss, its backward and the KL statistics on device kernels
+            self.ppo = urmppo.URMPPOUpdater(self.model, self.opt, pcfg, self.grads, gen, graph=graph_up)
+            self.ppo.weight_cache = self.bf16w
         else:
             self.ppo = PPOUpdater(self.model, self.opt, pcfg, self.grads, gen, graph=graph_up)
             self.ppo.weight_cache = self.bf16w

@@ -47,11 +47,25 @@ class URMPolicy:
             ws = (blk.attn.qkv_proj.weight, blk.attn.o_proj.weight, blk.mlp.gate_up_proj.weight, blk.mlp.down_proj.weight)
             self.mats.append([w._g2048_bf16 if self.shared else torch.empty_like(w, dtype=torch.bfloat16) for w in ws])
         dev = model.stem[0].weight.device
-        self.conv_w = [torch.empty(self.inter, 2, dtype=torch.float32, device=dev) for _ in model.layers]
-        # own copies of the conv biases: an optimizer may re-home the 1-D parameters into a flat
-        # buffer at any 4-byte offset, and the one-launch forward stages them as 16-byte chunks
-        self.conv_b = [torch.empty(self.inter, dtype=torch.float32, device=dev) for _ in model.layers]
-        self.init_hidden = torch.empty(16, self.h, dtype=torch.float32, device=dev)
+        # the conv taps / biases and init_hidden: the master tensors themselves where the one-launch
+        # forward can stage them (fp32, contiguous, 16-byte aligned: it reads 16-byte chunks), else own
+        # copies -- an optimizer may re-home the 1-D parameters into a flat buffer at any 4-byte offset
+        # (round 5: read in place, the KL re-forward's ~5 copy kernels per minibatch are gone)
+        def direct(t, shape):
+            ok = t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 16 == 0 and t.device.type == "cuda"
+            return t.detach().view(shape) if ok else None
+        self._direct = {}
+        self.conv_w, self.conv_b = [], []
+        for blk in model.layers:
+            cw = direct(blk.mlp.dwconv.weight, (self.inter, 2))
+            cb = direct(blk.mlp.dwconv.bias, (self.inter,))
+            self.conv_w.append(cw if cw is not None else torch.empty(self.inter, 2, dtype=torch.float32, device=dev))
+            self.conv_b.append(cb if cb is not None else torch.empty(self.inter, dtype=torch.float32, device=dev))
+            self._direct[id(self.conv_w[-1])] = cw is not None
+            self._direct[id(self.conv_b[-1])] = cb is not None
+        ih = direct(model.init_hidden, (16, self.h))
+        self.init_hidden = ih if ih is not None else torch.empty(16, self.h, dtype=torch.float32, device=dev)
+        self._direct[id(self.init_hidden)] = ih is not None
         h, i = self.h, self.inter
         # projections with fused epilogues when the kernels cover these shapes (h <= 64)
         self.fused = (L.urm_linear_supported(0, h, 3 * h) and L.urm_linear_supported(1, h, h)
@@ -79,8 +93,10 @@ class URMPolicy:
         """The master parameters the one-launch forward reads in place (an optimizer that re-homes
         parameters into flat buffers changes these: the caller rebuilds the policy then)."""
         m = self.master
-        return tuple(t.data_ptr() for t in (m.stem[0].weight, m.stem[1].weight, m.stem[1].bias, m.action_head.weight,
-                                            m.action_head.bias, m.value_head.weight, m.value_head.bias))
+        ts = [m.stem[0].weight, m.stem[1].weight, m.stem[1].bias, m.action_head.weight, m.action_head.bias,
+              m.value_head.weight, m.value_head.bias, m.init_hidden]
+        ts += [t for blk in m.layers for t in (blk.mlp.dwconv.weight, blk.mlp.dwconv.bias)]
+        return tuple(t.data_ptr() for t in ts)
 
     def forward_train(self, obs: torch.Tensor, p: float):
         """The one-launch forward with the model's attention dropout (training mode, no gradient):
@@ -117,10 +133,13 @@ class URMPolicy:
                 for dst, src in zip(mt, (blk.attn.qkv_proj.weight, blk.attn.o_proj.weight, blk.mlp.gate_up_proj.weight,
                                          blk.mlp.down_proj.weight)):
                     dst.copy_(src)
-            cw.copy_(blk.mlp.dwconv.weight.view(self.inter, 2))
+            if not self._direct[id(cw)]:
+                cw.copy_(blk.mlp.dwconv.weight.view(self.inter, 2))
         for blk, cb in zip(self.master.layers, self.conv_b):
-            cb.copy_(blk.mlp.dwconv.bias)
-        self.init_hidden.copy_(self.master.init_hidden.view(16, self.h))
+            if not self._direct[id(cb)]:
+                cb.copy_(blk.mlp.dwconv.bias)
+        if not self._direct[id(self.init_hidden)]:
+            self.init_hidden.copy_(self.master.init_hidden.view(16, self.h))
 
     def _buffers(self, n: int, dev):
         if self._n == n:
@@ -192,22 +211,60 @@ def _attn_drop_state(dev):
     return st
 
 
+_ATTN_FWD: dict = {}  # device -> [counter snapshot, next application, counter] of the forward in progress
+
+
+class attn_forward:
+    """The scope of one GameURM forward (agent.GameURM.forward): its attention applications k = 0, 1, ...
+    draw their dropout masks at (the counter when the first one ran) + k, and the device counter is bumped
+    ONCE at the end by the number of applications -- the masks of round 4's per-application
+    snapshot-and-bump, with two kernels per forward instead of two per application.  A nested scope
+    joins the outer one."""
+
+    def __init__(self, dev: torch.device):
+        self.dev, self.st = dev, None
+
+    def __enter__(self):
+        if self.dev.type == "cuda" and self.dev not in _ATTN_FWD:
+            self.st = [None, 0, None]
+            _ATTN_FWD[self.dev] = self.st
+        return self
+
+    def __exit__(self, *exc):
+        if self.st is None:
+            return False
+        del _ATTN_FWD[self.dev]
+        if self.st[1] and exc[0] is None:
+            self.st[2].add_(self.st[1])
+        return False
+
+
 class URMAttentionFn(torch.autograd.Function):
     """The attention core of GameURMAttention (game.py:1296-1317: scaled_dot_product_attention,
     no mask, dropout_p = config.dropout in training) for autograd training on the device: forward
     g2048_urm_attention(_drop), backward g2048_urm_attention_bwd(_drop) (P and the dropout mask
-    regenerated; head_dim 16).  qkv bf16 [16 n, 3 h] -> out bf16 [16 n, h]."""
+    regenerated; head_dim 16).  qkv bf16 [16 n, 3 h] -> out bf16 [16 n, h].  Inside attn_forward the
+    mask counter is the forward's snapshot + this application's index; alone, a snapshot of its own
+    and a bump of the device counter by one."""
 
     @staticmethod
     def forward(ctx, qkv: torch.Tensor, heads: int, p: float = 0.0):
         qkv = qkv.contiguous()
         out = torch.empty(qkv.shape[0], qkv.shape[1] // 3, dtype=qkv.dtype, device=qkv.device)
-        ctx.heads, ctx.p, ctx.seed = heads, float(p), 0
+        ctx.heads, ctx.p, ctx.seed, ctx.off = heads, float(p), 0, 0
         if p > 0.0:
             seed, ctr = _attn_drop_state(qkv.device)
-            c = ctr.clone()  # this call's counter value: the backward regenerates the mask from it
-            L.urm_attention(qkv, out, heads, p, seed, c)
-            ctr.add_(1)
+            st = _ATTN_FWD.get(qkv.device)
+            if st is not None:
+                if st[0] is None:
+                    st[0], st[2] = ctr.clone(), ctr
+                c, ctx.off = st[0], st[1]
+                st[1] += 1
+            else:
+                c = ctr.clone()  # this call's counter value: the backward regenerates the mask from it
+            L.urm_attention(qkv, out, heads, p, seed, c, offset=ctx.off)
+            if st is None:
+                ctr.add_(1)
             ctx.seed = seed
             ctx.save_for_backward(qkv, c)
         else:
@@ -221,7 +278,7 @@ class URMAttentionFn(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         if ctx.p > 0.0:
             L.urm_attention_bwd(qkv, dout.to(qkv.dtype).contiguous(), dqkv, ctx.heads, ctx.p, ctx.seed,
-                                ctx.saved_tensors[1])
+                                ctx.saved_tensors[1], offset=ctx.off)
         else:
             L.urm_attention_bwd(qkv, dout.to(qkv.dtype).contiguous(), dqkv, ctx.heads)
         return dqkv, None, None
@@ -250,13 +307,18 @@ class StemFn(torch.autograd.Function):
         ctx.save_for_backward(obs, wf, gf, bf)
         ctx.eps = eps
         ctx.dtypes = (w.dtype, ln_w.dtype, ln_b.dtype)
+        ctx.targets = tuple(_direct_target(t) for t in (w, ln_w, ln_b))
         return emb
 
     @staticmethod
     def backward(ctx, demb: torch.Tensor):
         obs, wf, gf, bf = ctx.saved_tensors
-        grads = torch.empty(320, dtype=torch.float32, device=obs.device)
         part = torch.empty(L.urm_stem_partials(obs.shape[0]), dtype=torch.float32, device=obs.device)
+        sinks = [_grad_sink(t, s) for t, s in zip(ctx.targets, ((64, 3), (64,), (64,)))]
+        if all(k is not None for k in sinks):  # direct_weight_grads: straight into the three .grad
+            L.urm_stem_bwd3(obs, wf, gf, bf, demb.float().contiguous(), *sinks, part, ctx.eps, accumulate=True)
+            return None, None, None, None, None
+        grads = torch.empty(320, dtype=torch.float32, device=obs.device)
         L.urm_stem_bwd(obs, wf, gf, bf, demb.float().contiguous(), grads, part, ctx.eps)
         dw, dg, db = grads[:192].view(64, 3), grads[192:256], grads[256:]
         return (None, dw.to(ctx.dtypes[0]), dg.to(ctx.dtypes[1]), db.to(ctx.dtypes[2]), None)
@@ -510,6 +572,58 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     return dw
 
 
+_DIRECT = [False]  # direct_weight_grads() in force
+
+
+class direct_weight_grads:
+    """Within this scope the training Functions add the gradients of GameURM's shared weights (the
+    projections and the conv, applied once per loop) straight into the parameters' fp32 .grad, inside
+    the kernels that produce them (g2048_urm_wgrad_acc / g2048_urm_gate_up_swiglu_bwd_acc), and return
+    None for them: autograd's accumulation of the returned gradients -- an add_ kernel per extra
+    application and parameter, ~40 per minibatch -- is gone, and the bits are the same (each
+    application's sum is rounded once and added in the order autograd would add it; the first lands
+    on the zeroed .grad).  For callers that zero .grad before the backward (the PPO update's
+    GradBucket); torch.autograd.grad-style callers stay outside the scope."""
+
+    def __enter__(self):
+        self.prev = _DIRECT[0]
+        _DIRECT[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _DIRECT[0] = self.prev
+        return False
+
+
+def _direct_target(w: torch.Tensor):
+    """w (a leaf parameter) when its gradient may be accumulated in place (direct_weight_grads), else
+    None; decided at forward time, checked again at backward (_grad_sink)."""
+    return w if (_DIRECT[0] and w.is_leaf and w.requires_grad and w.dtype == torch.float32) else None
+
+
+def _grad_sink(w: torch.Tensor | None, shape) -> torch.Tensor | None:
+    """w.grad as an fp32 contiguous [shape] view to accumulate into, or None (then return the gradient)."""
+    if w is None:
+        return None
+    g = w.grad
+    if g is None or g.dtype != torch.float32 or not g.is_contiguous() or not g.is_cuda:
+        return None
+    return g.view(shape)
+
+
+def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, target, dtype):
+    """The weight gradient dy^T x: added into target.grad (returns None) when it is a direct target,
+    else returned (fp32, cast to `dtype`)."""
+    m, n = dy.shape
+    k = x.shape[1]
+    sink = _grad_sink(target, (n, k))
+    if sink is None:
+        return _wgrad(dy, x).to(dtype)
+    part = torch.empty(L.urm_wgrad_partials(m, n, k), dtype=torch.float32, device=dy.device)
+    L.urm_wgrad(dy.contiguous(), x.contiguous(), sink, part, accumulate=True)
+    return None
+
+
 def _gemm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """y bf16 [rows, n] = x w^T for bf16 x [rows, k], w [n, k]: the MFMA projection kernel
     (g2048_urm_linear) when it covers the shape, else autocast's library GEMM (torch.mm)."""
@@ -606,6 +720,7 @@ class URMLinearFn(torch.autograd.Function):
         wb = bf16_weight(w)
         ctx.save_for_backward(xb, wb)
         ctx.dtypes = (x.dtype, w.dtype)
+        ctx.wt = _direct_target(w)
         return _gemm(xb, wb)
 
     @staticmethod
@@ -613,7 +728,7 @@ class URMLinearFn(torch.autograd.Function):
         xb, wb = ctx.saved_tensors
         dy = dy.to(torch.bfloat16).contiguous()
         dx = _gemm_t(dy, wb) if ctx.needs_input_grad[0] else None
-        dW = _wgrad(dy, xb).to(ctx.dtypes[1])
+        dW = _wgrad_into(dy, xb, ctx.wt, ctx.dtypes[1])
         return (None if dx is None else dx.to(ctx.dtypes[0])), dW
 
 
@@ -705,6 +820,7 @@ class LinResRMSFn(torch.autograd.Function):
         L.urm_linear_res_rms(xb, wb, h2, out, outb, rstd, eps)
         ctx.save_for_backward(out, rstd, xb, wb)
         ctx.shape, ctx.xshape, ctx.dtypes = shape, x.shape, (x.dtype, w.dtype)
+        ctx.wt = _direct_target(w)
         if with_bf16:
             return out.view(shape), outb.view(shape)
         return out.view(shape)
@@ -721,7 +837,7 @@ class LinResRMSFn(torch.autograd.Function):
         db16 = None if doutb is None else doutb.reshape(out.shape).to(torch.bfloat16).contiguous()
         L.urm_rms_res_bwd(d32, out, rstd, dh, da, db16, dpool=dpool)
         dx = _gemm_t(da, wb) if ctx.needs_input_grad[1] else None
-        dw = _wgrad(da, xb).to(ctx.dtypes[1]) if ctx.needs_input_grad[2] else None
+        dw = _wgrad_into(da, xb, ctx.wt, ctx.dtypes[1]) if ctx.needs_input_grad[2] else None
         return (dh.view(ctx.shape), None if dx is None else dx.to(ctx.dtypes[0]).view(ctx.xshape), dw, None, None)
 
 
@@ -765,6 +881,10 @@ class GateUpSwiGLUFn(torch.autograd.Function):
             ctx.save_for_backward(xb, wb, cwf, cbf, gu)
         ctx.rec, ctx.inter = rec, inter
         ctx.dtypes = (x.dtype, w.dtype, cw.dtype, cb.dtype)
+        ctx.wt = _direct_target(w)
+        # the conv parameters: cw arrives as a view ([inter, 1, 2] -> [inter, 2]) of the leaf
+        ctx.cwt = _direct_target(cw._base if cw._base is not None else cw)
+        ctx.cbt = _direct_target(cb)
         return act
 
     @staticmethod
@@ -772,17 +892,25 @@ class GateUpSwiGLUFn(torch.autograd.Function):
         xb, wb, cwf, cbf = ctx.saved_tensors[:4]
         rows, inter = xb.shape[0], ctx.inter
         dgu = torch.empty(rows, 2 * inter, dtype=torch.bfloat16, device=xb.device)
-        dw = torch.empty(inter, 2, dtype=torch.float32, device=xb.device)
-        db = torch.empty(inter, dtype=torch.float32, device=xb.device)
         part = torch.empty(L.urm_swiglu_conv_partials(rows // 16, inter), dtype=torch.float32, device=xb.device)
         da = dact.to(torch.bfloat16).contiguous()
+        # the conv gradients straight into both parameters' .grad (direct_weight_grads), else returned
+        sw, sb = _grad_sink(ctx.cwt, (inter, 2)), _grad_sink(ctx.cbt, (inter,))
+        acc = ctx.rec and sw is not None and sb is not None
+        if acc:
+            dw, db = sw, sb
+        else:
+            dw = torch.empty(inter, 2, dtype=torch.float32, device=xb.device)
+            db = torch.empty(inter, dtype=torch.float32, device=xb.device)
         if ctx.rec:
-            L.urm_gate_up_swiglu_bwd(xb, wb, cwf, cbf, da, dgu, dw, db, part)
+            L.urm_gate_up_swiglu_bwd(xb, wb, cwf, cbf, da, dgu, dw, db, part, accumulate=acc)
         else:
             L.urm_swiglu_conv_bwd(ctx.saved_tensors[4], cwf, cbf, da, dgu, dw, db, part)
         dx = _gemm_t(dgu, wb)  # autocast's bf16 input-gradient GEMM, on MFMA
-        dW = _wgrad(dgu, xb)          # the weight gradient on g2048_urm_wgrad (fp32)
-        return dx.to(ctx.dtypes[0]), dW.to(ctx.dtypes[1]), dw.to(ctx.dtypes[2]), db.to(ctx.dtypes[3])
+        dW = _wgrad_into(dgu, xb, ctx.wt, ctx.dtypes[1])  # the weight gradient on g2048_urm_wgrad (fp32)
+        if acc:
+            return dx.to(ctx.dtypes[0]), dW, None, None
+        return dx.to(ctx.dtypes[0]), dW, dw.to(ctx.dtypes[2]), db.to(ctx.dtypes[3])
 
 
 def gate_up_swiglu_nograd(x: torch.Tensor, w: torch.Tensor, cw: torch.Tensor, cb: torch.Tensor) -> torch.Tensor:

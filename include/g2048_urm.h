@@ -62,6 +62,14 @@ int g2048_urm_attention_drop(g2048_stream_t stream, const uint16_t *qkv, uint16_
                              int32_t heads, float p, uint64_t seed, const uint64_t *counter);
 int g2048_urm_attention_bwd_drop(g2048_stream_t stream, const uint16_t *qkv, const uint16_t *dout, uint16_t *dqkv,
                                  int64_t n, int32_t h, int32_t heads, float p, uint64_t seed, const uint64_t *counter);
+/* The same with the mask keyed by *counter + offset (round 5: the forward's k-th attention application
+ * passes offset k and the caller bumps the counter once per forward by the number of applications,
+ * instead of a counter snapshot and a bump per application -- the same masks). */
+int g2048_urm_attention_drop_at(g2048_stream_t stream, const uint16_t *qkv, uint16_t *out, int64_t n, int32_t h,
+                                int32_t heads, float p, uint64_t seed, const uint64_t *counter, uint64_t offset);
+int g2048_urm_attention_bwd_drop_at(g2048_stream_t stream, const uint16_t *qkv, const uint16_t *dout,
+                                    uint16_t *dqkv, int64_t n, int32_t h, int32_t heads, float p, uint64_t seed,
+                                    const uint64_t *counter, uint64_t offset);
 
 /* The post-norm residual RMSNorm for autograd training (GameURMBlock, game.py:1346-1350, h = 64):
  *   forward  out = (h + a) * rsqrt(mean((h + a)^2) + eps), rstd [rows] saved; h, out fp32, a fp32
@@ -119,6 +127,11 @@ int g2048_urm_gate_up_swiglu_bwd_supported(int32_t h, int32_t inter);
 int g2048_urm_gate_up_swiglu_bwd(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, const float *conv_w,
                                  const float *conv_b, const uint16_t *dact, uint16_t *dgu, float *dw, float *db,
                                  float *partials, int64_t n, int32_t h, int32_t inter);
+/* accumulate != 0: dw / db are ADDED to (dw += its sum, db += its sum) -- the conv parameters' gradient
+ * summed over the loop applications in autograd's order, straight into the parameters' .grad (round 5) */
+int g2048_urm_gate_up_swiglu_bwd_acc(g2048_stream_t stream, const uint16_t *x, const uint16_t *w, const float *conv_w,
+                                     const float *conv_b, const uint16_t *dact, uint16_t *dgu, float *dw, float *db,
+                                     float *partials, int64_t n, int32_t h, int32_t inter, int32_t accumulate);
 int g2048_urm_swiglu_conv_fwd(g2048_stream_t stream, const uint16_t *gu, const float *w, const float *b, uint16_t *act,
                               int64_t n, int32_t inter);
 int g2048_urm_swiglu_conv_bwd(g2048_stream_t stream, const uint16_t *gu, const float *w, const float *b,
@@ -137,6 +150,11 @@ int g2048_urm_stem_fwd(g2048_stream_t stream, const void *obs, int32_t obs_dtype
 int g2048_urm_stem_bwd(g2048_stream_t stream, const void *obs, int32_t obs_dtype, const float *w, const float *ln_w,
                        const float *ln_b, const float *demb, float *grads, float *partials, int64_t n, int32_t h,
                        float eps);
+/* The same with the three gradients at their own addresses (dw [64][3], dln_w [64], dln_b [64]: the
+ * parameters' .grad) and, with accumulate, added to (round 5: no copies / accumulation kernels). */
+int g2048_urm_stem_bwd3(g2048_stream_t stream, const void *obs, int32_t obs_dtype, const float *w, const float *ln_w,
+                        const float *ln_b, const float *demb, float *dw, float *dln_w, float *dln_b, int32_t accumulate,
+                        float *partials, int64_t n, int32_t h, float eps);
 
 /* Weight gradient of a projection y = x W^T for autograd training: dw fp32 [n, k] = dy^T x over m
  * rows, dy bf16 [m, n], x bf16 [m, k] (the shapes g2048_urm_wgrad_supported(n, k) accepts: n % 16 == 0,
@@ -148,6 +166,10 @@ int g2048_urm_wgrad_supported(int32_t n, int32_t k);
 size_t g2048_urm_wgrad_partials(int64_t m, int32_t n, int32_t k);
 int g2048_urm_wgrad(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x, float *dw, float *partials,
                     int64_t m, int32_t n, int32_t k);
+/* accumulate != 0: dw += dy^T x (the sum rounded once, then added: the bits of autograd's accumulation of
+ * a returned gradient into the weight's .grad, round 5) */
+int g2048_urm_wgrad_acc(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x, float *dw, float *partials,
+                        int64_t m, int32_t n, int32_t k, int32_t accumulate);
 
 /* Post-norm residual (game.py:1346, 1350 with rms_norm :1223-1229):
  *   x = x + y;  x = x * rsqrt(mean(x^2) + eps)  [+ emb, the next loop's input, game.py:1447];
@@ -242,6 +264,39 @@ int g2048_urm_forward(g2048_stream_t stream, const g2048_urm_weights *w, const v
  * update's no-grad KL re-forward (train.py:577-582, model still in train mode).  p = 0: g2048_urm_forward. */
 int g2048_urm_forward_drop(g2048_stream_t stream, const g2048_urm_weights *w, const void *obs, int32_t obs_dtype,
                            float *logits, float *value, int64_t n, float p, uint64_t seed, const uint64_t *counter);
+
+/* GameURM's PPO minibatch loss on device kernels (model_optimize_step, train.py:491-601, with GameURM's
+ * heads, game.py:1451-1456), replacing the ~50 small torch kernels of the heads' autocast projection,
+ * the loss expression, its autograd backward, the KL's masked softmaxes and the statistics stack:
+ *   g2048_urm_head_loss      pooled [m, h] (fp32: pooled_dtype 0, or bf16: 1) -> z = bf16(bf16(pooled)
+ *                            bf16(W)^T + bf16(b)) for W = [Wa; Wv] (autocast's rounding points), the
+ *                            per-row PPO-clip / entropy / smooth-L1 loss of g2048_ppo_head_loss
+ *                            (batch: the trajectory columns at idx; rows must be NULL), dz fp32 [m, 8]
+ *                            (d mean-loss / d(logits, value), columns 5..7 zero), masked fp32 [m, 4]
+ *                            (logits with -inf at illegal actions), sums[3] = {sum ppo, sum H, sum v},
+ *                            loss[1] = -(mean ppo - critic mean v + beta mean H)
+ *   g2048_urm_head_loss_bwd  dy = bf16(grad_out dz) -> dpooled = bf16(dy W) in pooled's dtype, dWa [4, h],
+ *                            dba [4], dWv [h], dbv [1] = dy^T bf16(pooled), column sums of dy (overwritten,
+ *                            or added to with accumulate)
+ *   g2048_urm_kl_stats       KL(old || new) per row from masked and the re-forward's logits fp32 [m, 4],
+ *                            then stats[9] += the minibatch's loss / entropy / value / grad-norm / KL
+ *                            statistics (g2048_ppo_stats' update: sums, gn, beta_dev, critic, m)
+ * h 64 or 32; partials: g2048_urm_head_loss_partials(m, h) floats; sync: a device uint32 ticket word,
+ * zero at the first call (each kernel's last block puts it back to zero).  Deterministic: fixed-order
+ * block trees and a last-block pass over the block partials. */
+struct g2048_ppo_batch;
+size_t g2048_urm_head_loss_partials(int64_t m, int32_t h);
+int g2048_urm_head_loss(g2048_stream_t stream, const void *pooled, int32_t pooled_dtype, const float *wa,
+                        const float *ba, const float *wv, const float *bv, int64_t m, int32_t h,
+                        const struct g2048_ppo_batch *batch, const float *beta_dev, float critic, float clip_eps,
+                        float *dz, float *masked, float *partials, uint32_t *sync, float *sums, float *loss);
+int g2048_urm_head_loss_bwd(g2048_stream_t stream, const void *pooled, int32_t pooled_dtype, const float *wa,
+                            const float *wv, const float *dz, const float *grad_out, void *dpooled, float *partials,
+                            uint32_t *sync, float *dwa, float *dba, float *dwv, float *dbv, int32_t accumulate,
+                            int64_t m, int32_t h);
+int g2048_urm_kl_stats(g2048_stream_t stream, const float *old_masked, const float *logits, int64_t m,
+                       const float *sums, const float *gn, const float *beta_dev, float critic, float *stats,
+                       float *partials, uint32_t *sync);
 
 #ifdef __cplusplus
 }

@@ -87,7 +87,18 @@ def _worker(rank, world, port, out, model_type="mlp"):
     tr.ppo.update = update
     for s in range(STEPS):
         m = tr.train_step(s)
-        assert np.isfinite(m["loss"]) and np.isfinite(m["grad_norm"]), (rank, s, m)
+        if not (np.isfinite(m["loss"]) and np.isfinite(m["grad_norm"])):
+            # an intermittent non-finite grad_norm with a finite loss / KL was seen in this MLP test (r04c,
+            # r05d): record what the norm was computed from, for the cause
+            torch.cuda.synchronize()
+            inner = getattr(tr.opt, "opt", tr.opt)
+            diag = {"bucket_finite": bool(torch.isfinite(bucket.flat).all()),
+                    "params_finite": all(bool(torch.isfinite(p).all()) for p in tr.model.parameters()),
+                    "norm_part": getattr(inner, "norm_part", torch.zeros(1)).cpu().tolist(),
+                    "norm_t": float(getattr(inner, "norm_t", torch.zeros(1)).reshape(-1)[0]),
+                    "coef_t": float(getattr(inner, "coef_t", torch.zeros(1)).reshape(-1)[0]),
+                    "stats": tr.ppo.stats.cpu().tolist()}
+            raise AssertionError((rank, s, m, diag))
         T = tr.rollout.T
         rec["g_raw"].append(tr.rollout.buf.g_raw[:T].reshape(-1).double().cpu().numpy())
         rec["moments"].append(tr.rtg.state.cpu().numpy().copy())

@@ -1090,3 +1090,216 @@ def test_urm_bf16_weight_cache_tracks_the_optimizer(dev):
         assert torch.equal(t, w.detach().to(torch.bfloat16))
         assert urm.bf16_weight(w) is t
     cache.detach()
+
+
+def _urm_columns(dev, M, seed=0):
+    """Random trajectory columns of M rows (boards, a legal action, logp, adv, ret) as the update reads them."""
+    from oracle import oracle as O
+    g = np.random.default_rng(seed)
+    boards = g.integers(0, 10, size=(M, 16)).astype(np.int8)
+    legal = O.legal_mask(boards)
+    legal[legal == 0] = 1
+    acts = np.array([g.choice([a for a in range(4) if m >> a & 1]) for m in legal], np.uint8)
+    logp = np.log(g.dirichlet(np.ones(4), size=M)).astype(np.float32)
+    return {"boards": torch.from_numpy(boards).to(dev), "actions": torch.from_numpy(acts).to(dev),
+            "legal": torch.from_numpy(legal).to(dev), "logp": torch.from_numpy(logp).to(dev),
+            "adv": torch.from_numpy(g.normal(size=M).astype(np.float32)).to(dev),
+            "ret": torch.from_numpy(g.normal(size=M).astype(np.float32)).to(dev)}
+
+
+@pytest.mark.parametrize("m,pdt", [(4096, torch.float32), (3001, torch.float32), (1000, torch.bfloat16)])
+def test_urm_head_loss_fn_matches_torch_loss(dev, m, pdt):
+    """URMHeadLossFn (g2048_urm_head_loss / _bwd, round 5) vs the round-4 path it replaces -- URMHeadsFn
+    under bf16 autocast + ppo.ppo_losses + autograd -- on the same pooled features and columns: the
+    logits follow autocast's rounding points in both (bf16 operands, one rounding of the biased fp32
+    sum), so they differ only where the two dot-product orders round across a bf16 step; measured
+    bounds: loss / loss sums within 1e-4 relative, masked logits within one bf16 step, dpooled and
+    the head gradients at cosine >= 0.9999 and max error <= 1 % of their scale."""
+    import agent
+    from g2048 import _lib as L
+    from g2048.ppo import invalid_from_legal, ppo_losses
+    from g2048.urm import URMHeadsFn
+    from g2048.urmppo import URMHeadLossFn
+    torch.manual_seed(m)
+    mod = agent.GameURM(agent.GameURMConfig(dropout=0.0)).to(dev)
+    with torch.no_grad():
+        mod.action_head.weight.mul_(4.0)
+        mod.action_head.bias.uniform_(-0.5, 0.5)
+        mod.value_head.bias.uniform_(-0.5, 0.5)
+    cols = _urm_columns(dev, 3 * m, seed=m)
+    idx = torch.randperm(3 * m, device=dev)[:m].contiguous()
+    pooled = (torch.randn(m, 64, device=dev) * 1.5).to(pdt)
+    beta = torch.tensor(0.02, device=dev)
+    heads = [mod.action_head.weight, mod.action_head.bias, mod.value_head.weight, mod.value_head.bias]
+    # reference: the round-4 modules + torch loss
+    p_ref = pooled.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        if m % 16 == 0:
+            lg, v = URMHeadsFn.apply(p_ref, *heads)
+        else:  # (URMHeadsFn takes whole boards of 16 rows: autocast's own Linear, the same rounding points)
+            lg, v = mod.action_head(p_ref), mod.value_head(p_ref)
+    inv = invalid_from_legal(cols["legal"][idx])
+    loss_ref, parts = ppo_losses(lg.float(), v.float(), cols["actions"][idx], inv, cols["logp"][idx], cols["adv"][idx],
+                                 cols["ret"][idx], beta, 0.2, 0.2)
+    loss_ref.backward()
+    g_ref = [p.grad.clone() for p in heads]
+    for p in heads:
+        p.grad = None
+    # the device loss
+    sync = torch.zeros(1, dtype=torch.int32, device=dev)
+    run = {"batch": L.make_ppo_batch(idx, cols["actions"], cols["legal"], cols["logp"], cols["adv"], cols["ret"]),
+           "beta": beta, "critic": 0.2, "clip": 0.2, "sync": sync}
+    p_dev = pooled.clone().requires_grad_(True)
+    loss = URMHeadLossFn.apply(p_dev, *heads, run)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert int(sync.item()) == 0  # the ticket is back at zero after both kernels
+    assert abs(float(loss) - float(loss_ref)) <= 1e-4 * abs(float(loss_ref)) + 1e-6, (float(loss), float(loss_ref))
+    want = torch.stack([parts["ppo"].sum(), parts["entropy"].sum(), parts["vloss"].sum()])
+    torch.testing.assert_close(run["sums"], want, rtol=1e-4, atol=1e-3)
+    mk, mk_ref = run["masked"], parts["masked"]
+    assert torch.equal(torch.isinf(mk), torch.isinf(mk_ref))
+    fin = torch.isfinite(mk_ref)
+    assert float((mk[fin] - mk_ref[fin]).abs().max()) <= 2 ** -7 * float(mk_ref[fin].abs().max())
+    for name, a, b in [("dpooled", p_dev.grad, p_ref.grad)] + [(n, p.grad, r) for n, p, r in
+                                                                zip(("dwa", "dba", "dwv", "dbv"), heads, g_ref)]:
+        a, b = a.float().reshape(-1), b.float().reshape(-1)
+        print(f"{name}: max {float((a - b).abs().max()):.3g} of {float(b.abs().max()):.3g}")
+        assert float(torch.nn.functional.cosine_similarity(a, b, dim=0)) >= 0.9999, name
+        assert float((a - b).abs().max()) <= 0.01 * float(b.abs().max()) + 1e-7, name
+
+
+def test_urm_kl_stats_matches_torch(dev):
+    """g2048_urm_kl_stats vs the torch statistics of PPOUpdater._post (ppo.kl_old_new + the stacked
+    minibatch statistics) on the same masked / new logits, sums and grad norm: every entry of the
+    accumulated statistics within 1e-5 relative, kl_max as the max."""
+    from g2048 import _lib as L
+    from g2048.ppo import kl_old_new
+    torch.manual_seed(9)
+    m = 5000
+    legal = torch.randint(1, 16, (m,), device=dev, dtype=torch.int32)
+    inv = ((legal.unsqueeze(-1) >> torch.arange(4, device=dev)) & 1) == 0
+    old = (torch.randn(m, 4, device=dev) * 2).masked_fill(inv, float("-inf"))
+    new = torch.randn(m, 4, device=dev) * 2
+    sums = torch.tensor([12.5, 3000.0, 800.0], device=dev)
+    gn = torch.tensor(0.75, device=dev)
+    beta = torch.tensor(0.02, device=dev)
+    stats = torch.zeros(9, device=dev)
+    sync = torch.zeros(1, dtype=torch.int32, device=dev)
+    part = torch.empty(2 * ((m + 255) // 256), device=dev)
+    for _ in range(2):
+        L.urm_kl_stats(old, new, sums, gn, beta, 0.2, stats, part, sync)
+    kl = kl_old_new(old, new, inv)
+    s_ppo, s_ent, s_v = (sums / m).tolist()
+    one = torch.tensor([-(s_ppo - 0.2 * s_v + 0.02 * s_ent), -s_ppo, -0.02 * s_ent, 0.2 * s_v, 0.75, s_ent,
+                        float(kl.sum()), float(kl.mean()), 0.0], device=dev)
+    want = 2 * one
+    want[8] = kl.max()
+    torch.testing.assert_close(stats, want, rtol=1e-5, atol=1e-6)
+    assert int(sync.item()) == 0
+
+
+def test_urm_direct_weight_grads_are_bitwise_autograd(dev):
+    """urm.direct_weight_grads (round 5): the shared weights' gradients added into .grad inside the
+    producing kernels (g2048_urm_wgrad_acc, g2048_urm_gate_up_swiglu_bwd_acc) equal, bit for bit,
+    autograd's accumulation of the returned gradients -- every parameter, with attention dropout (both
+    runs at the same mask counter) and a truncated loop."""
+    import agent
+    from g2048 import urm
+    torch.manual_seed(3)
+    mod = agent.GameURM(agent.GameURMConfig(dropout=0.1)).to(dev).train()
+    obs = (torch.rand(2048, 48, device=dev) * 8).bfloat16()
+    wt = torch.randn(2048, 64, device=dev)
+    _, ctr = urm._attn_drop_state(dev)
+    c0 = int(ctr.item())
+    grads = []
+    for direct in (False, True):
+        ctr.fill_(c0)
+        for p in mod.parameters():
+            p.grad = torch.zeros_like(p)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            if direct:
+                with urm.direct_weight_grads():
+                    pooled = mod.features(obs)
+                    (pooled.float() * wt).sum().backward()
+            else:
+                pooled = mod.features(obs)
+                (pooled.float() * wt).sum().backward()
+        grads.append({k: p.grad.clone() for k, p in mod.named_parameters()})
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), k
+    assert float(grads[1]["layers.0.mlp.gate_up_proj.weight"].abs().sum()) > 0
+
+
+def test_urm_attention_forward_scope_draws_the_per_application_masks(dev):
+    """urm.attn_forward (round 5): inside one GameURM forward the attention applications read the
+    forward's counter snapshot + their index and the counter is bumped once at the end -- the same
+    masks as round 4's snapshot-and-bump per application (the Function outside a scope): pooled
+    features and every gradient bitwise equal, the counter advanced by the same count."""
+    import agent
+    from g2048 import urm
+    torch.manual_seed(4)
+    mod = agent.GameURM(agent.GameURMConfig(dropout=0.2)).to(dev).train()
+    obs = (torch.rand(1024, 48, device=dev) * 8).bfloat16()
+    wt = torch.randn(1024, 64, device=dev)
+    _, ctr = urm._attn_drop_state(dev)
+    c0 = int(ctr.item())
+    res = []
+    for scoped in (True, False):
+        ctr.fill_(c0)
+        mod.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            pooled = mod.features(obs) if scoped else mod._features(obs)
+            (pooled.float() * wt).sum().backward()
+        res.append((pooled.detach().clone(), int(ctr.item()),
+                    {k: p.grad.clone() for k, p in mod.named_parameters() if p.grad is not None}))
+    assert torch.equal(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1] == c0 + 8
+    for k in res[0][2]:
+        assert torch.equal(res[0][2][k], res[1][2][k]), k
+
+
+def test_urm_ppo_updater_matches_generic_updater(dev):
+    """URMPPOUpdater (device loss kernels, direct weight gradients, one-launch KL statistics) vs
+    PPOUpdater (torch loss + autograd) from the same weights on the same minibatches (torch-op
+    MuonAdamW for both, dropout 0): the update directions agree (cosine >= 0.999 per 2-D weight, norm
+    within 2 %; 1-D parameters within 2e-3 of their step) and the statistics within 1e-3 relative
+    (kl_max 2e-2) --
+    what is left is the heads' dot-product order and the kernels' summation orders, amplified by
+    Muon's bf16 Newton-Schulz."""
+    import math
+
+    import agent
+    from g2048.dist import GradBucket
+    from g2048.optim import MuonAdamW
+    from g2048.ppo import PPOConfig, PPOUpdater
+    from g2048.urmppo import URMPPOUpdater
+    cols = _urm_columns(dev, 4096, seed=7)
+
+    def enc(b):
+        from g2048 import _lib as L
+        o = torch.empty(b.shape[0], 48, dtype=torch.float32, device=dev)
+        L.obs_encode(b.contiguous(), o)
+        return o
+    res = []
+    for cls in (URMPPOUpdater, PPOUpdater):
+        torch.manual_seed(2)
+        mod = agent.GameURM(agent.GameURMConfig(dropout=0.0)).to(dev)
+        opt = MuonAdamW(mod, 1e-3, 1e-4)
+        order = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(5)
+        init = {k: p.detach().clone() for k, p in mod.named_parameters()}
+        up = cls(mod, opt, PPOConfig(batch_size=2048, critic=0.2), GradBucket(order), gen, graph=False)
+        st = {k: float(v) for k, v in up.update(cols, 0.02, enc).items()}
+        res.append(({k: p.detach() - init[k] for k, p in mod.named_parameters()}, st))
+    (d0, s0), (d1, s1) = res
+    for k in d0:
+        a, b = d0[k].reshape(-1), d1[k].reshape(-1)
+        if d0[k].ndim == 2 and b.norm() > 0:
+            assert float(torch.nn.functional.cosine_similarity(a, b, dim=0)) >= 0.999, k
+            assert math.isclose(float(a.norm()), float(b.norm()), rel_tol=0.02), k
+        else:
+            assert float((a - b).abs().max()) <= 2e-3 * float(b.abs().max()) + 1e-9, k
+    for k in s0:  # (kl_max: the largest single-row KL, the most order-sensitive entry -- measured 0.9 %)
+        assert math.isclose(s0[k], s1[k], rel_tol=2e-2 if k == "kl_max" else 1e-3, abs_tol=1e-6), (k, s0[k], s1[k])

@@ -29,6 +29,20 @@ def main():
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
         tr.train_step(1)
         torch.cuda.synchronize()
+    # every device kernel of the iteration: the library's (libg2048: urm_* / muon / colsum / env ...)
+    # vs torch's own (at::native elementwise / reduce / copy, rocclr copy and fill blits), and torch's
+    # per minibatch (minibatches = the loss launches, one urm_head_loss_kernel each; else the KL
+    # re-forwards, the training-mode urm_forward_kernel<*, true>)
+    kern = [e for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+    torch_k = [e for e in kern if "at::" in e.name or "rocclr" in e.name or "Memset" in e.name
+               or "Memcpy" in e.name or e.name.startswith("void at_")]
+    nmb = sum(1 for e in kern if "urm_head_loss_kernel" in e.name) or sum(
+        1 for e in kern if "urm_forward_kernel" in e.name and ", true>" in e.name) or 1
+    from collections import Counter
+    print(f"device kernels: {len(kern)}; torch's: {len(torch_k)} over {nmb} minibatches + the rollout = "
+          f"{len(torch_k) / nmb:.1f} per minibatch (upper bound: the rollout's are included)")
+    for name, c in Counter(e.name[:90] for e in torch_k).most_common(12):
+        print(f"  {c:6d}  {name}")
     ka = prof.key_averages()
     rows = sorted(ka, key=lambda e: -e.count)
     print(f"{'op':60s} {'count':>6s} {'dev_us':>10s}")
