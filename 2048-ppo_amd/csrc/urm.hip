@@ -1257,6 +1257,157 @@ __global__ __launch_bounds__(256) void urm_attn_bwd16_kernel(const uint16_t *__r
     *reinterpret_cast<uint2 *>(drow + 2 * h) = make_uint2(pk2bf(dv[0], dv[1]), pk2bf(dv[2], dv[3]));
 }
 
+// The same two products with one wave per BOARD (round 5; head_dim 16, h = 16 heads <= 64): the
+// board's qkv rows (16 x 3h bf16, contiguous in HBM) come into the wave's LDS tile with 16-byte loads
+// (6 per lane at h 64) and the heads' fragments are read from there; the per-(board, head) kernels
+// above issued three or four 8-byte loads per lane per wave and ran at about half of HBM.  Every
+// product, softmax and rounding is theirs, operand for operand (V^T read transposed from the tile is
+// the identity-MFMA transpose's exact value), so the results are bit for bit the same.  Outputs
+// go back through the tile (each head's region is only its own) and leave as 16-byte stores.
+constexpr int kAbTP = 200;  // bf16 pitch of a board tile row (>= 3 x 64 + 8: rows 36 banks apart)
+
+constexpr int kAbOP = 72;   // bf16 pitch of the dO tile (h <= 64 columns, rows 36 banks apart)
+
+__device__ __forceinline__ void attn_board_load(uint16_t *tile, const uint16_t *src, int cols, int lane,
+                                                int pitch = kAbTP) {
+    const int cpr = cols / 8;  // 16-byte chunks per row
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    for (int c = lane; c < 16 * cpr; c += 64) {
+        const int r = c / cpr, k = c - r * cpr;
+        *reinterpret_cast<uint4 *>(tile + r * pitch + 8 * k) = s4[c];
+    }
+}
+
+__device__ __forceinline__ void attn_board_store(uint16_t *dst, const uint16_t *tile, int cols, int lane) {
+    const int cpr = cols / 8;
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+    for (int c = lane; c < 16 * cpr; c += 64) {
+        const int r = c / cpr, k = c - r * cpr;
+        d4[c] = *reinterpret_cast<const uint4 *>(tile + r * kAbTP + 8 * k);
+    }
+}
+
+template <bool kDrop>
+__global__ __launch_bounds__(256) void urm_attn16b_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
+                                                          int64_t n, int h, int heads, AttnDrop drop) {
+    __shared__ __attribute__((aligned(16))) uint16_t tiles[4][16 * kAbTP];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+    if (b >= n) return;  // wave-uniform; no block barrier below
+    uint16_t *tile = tiles[wave];
+    const int t = lane & 15, g = lane >> 4;
+    attn_board_load(tile, qkv + b * 16 * (int64_t)(3 * h), 3 * h, lane);
+    wave_lds_sync();
+    for (int hh = 0; hh < heads; hh++) {
+        const s16x4 ka = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint2 *>(tile + t * kAbTP + h + 16 * hh + 4 * g));
+        const s16x4 qb = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint2 *>(tile + t * kAbTP + 16 * hh + 4 * g));
+        s16x4 va;  // V^T[dim t][key 4g + jj]
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) va[jj] = (short)tile[(4 * g + jj) * kAbTP + 2 * h + 16 * hh + t];
+        const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ka, qb, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+        const float scale = 1.0f / sqrtf(16.0f);
+        float p[4];
+        float m = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            p[r] = st[r] * scale;
+            m = fmaxf(m, p[r]);
+        }
+        m = xmax32(xmax16(m));
+        float sum = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            p[r] = __expf(p[r] - m);
+            sum += p[r];
+        }
+        sum = xsum32(xsum16(sum));
+        const float inv = 1.0f / sum;
+        float km[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+        if (kDrop) attn_keep(drop, b, hh, t, g, km);
+        s16x4 pb;
+#pragma unroll
+        for (int r = 0; r < 4; r++) pb[r] = (short)f2bf(kDrop ? p[r] * inv * km[r] : p[r] * inv);
+        const f32x4 o = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, pb, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+        wave_lds_sync();  // every lane's Q / K / V reads of this head are done
+        *reinterpret_cast<uint2 *>(tile + t * kAbTP + 16 * hh + 4 * g) = make_uint2(pk2bf(o[0], o[1]), pk2bf(o[2], o[3]));
+    }
+    wave_lds_sync();
+    attn_board_store(out + b * 16 * (int64_t)h, tile, h, lane);
+}
+
+template <bool kDrop>
+__global__ __launch_bounds__(256) void urm_attn_bwd16b_kernel(const uint16_t *__restrict__ qkv,
+                                                              const uint16_t *__restrict__ dout,
+                                                              uint16_t *__restrict__ dqkv, int64_t n, int h, int heads,
+                                                              AttnDrop drop) {
+    __shared__ __attribute__((aligned(16))) uint16_t tiles[4][16 * kAbTP];
+    __shared__ __attribute__((aligned(16))) uint16_t otiles[4][16 * kAbOP];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+    if (b >= n) return;
+    uint16_t *tile = tiles[wave], *otile = otiles[wave];
+    const int t = lane & 15, g = lane >> 4;
+    attn_board_load(tile, qkv + b * 16 * (int64_t)(3 * h), 3 * h, lane);
+    attn_board_load(otile, dout + b * 16 * (int64_t)h, h, lane, kAbOP);
+    wave_lds_sync();
+    s16x4 eye;
+#pragma unroll
+    for (int r = 0; r < 4; r++) eye[r] = (short)(4 * g + r == t ? 0x3F80 : 0);
+    const f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+    auto pack4 = [](float a0, float a1, float a2, float a3) {
+        return __builtin_bit_cast(s16x4, make_uint2(pk2bf(a0, a1), pk2bf(a2, a3)));
+    };
+    auto tr = [&](s16x4 x) {
+        const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(x, eye, zero, 0, 0, 0);
+        return pack4(d[0], d[1], d[2], d[3]);
+    };
+    for (int hd = 0; hd < heads; hd++) {
+        const uint16_t *row = tile + t * kAbTP + hd * 16 + 4 * g;
+        const s16x4 qa = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint2 *>(row));
+        const s16x4 ka = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint2 *>(row + h));
+        const s16x4 va = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint2 *>(row + 2 * h));
+        const s16x4 oa = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint2 *>(otile + t * kAbOP + hd * 16 + 4 * g));
+        const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ka, qa, zero, 0, 0, 0);
+        const float scale = 0.25f;
+        float p[4];
+        float m = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            p[r] = st[r] * scale;
+            m = fmaxf(m, p[r]);
+        }
+        m = xmax32(xmax16(m));
+        float sum = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            p[r] = __expf(p[r] - m);
+            sum += p[r];
+        }
+        sum = xsum32(xsum16(sum));
+        const float inv = 1.0f / sum;
+#pragma unroll
+        for (int r = 0; r < 4; r++) p[r] *= inv;
+        float km[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+        if (kDrop) attn_keep(drop, b, hd, t, g, km);
+        const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, oa, zero, 0, 0, 0);
+        float rs = (p[0] * km[0] * dp[0] + p[1] * km[1] * dp[1]) + (p[2] * km[2] * dp[2] + p[3] * km[3] * dp[3]);
+        rs = xsum32(xsum16(rs));
+        const s16x4 dsa = pack4(p[0] * (dp[0] * km[0] - rs), p[1] * (dp[1] * km[1] - rs), p[2] * (dp[2] * km[2] - rs),
+                                p[3] * (dp[3] * km[3] - rs));
+        const s16x4 pda = pack4(p[0] * km[0], p[1] * km[1], p[2] * km[2], p[3] * km[3]);
+        const f32x4 dq = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(tr(ka), dsa, zero, 0, 0, 0);
+        const f32x4 dk = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(tr(qa), tr(dsa), zero, 0, 0, 0);
+        const f32x4 dv = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(tr(oa), tr(pda), zero, 0, 0, 0);
+        wave_lds_sync();  // this head's reads are done: its region takes the gradients
+        uint16_t *drow = tile + t * kAbTP + hd * 16 + 4 * g;
+        *reinterpret_cast<uint2 *>(drow) = make_uint2(pk2bf(dq[0] * scale, dq[1] * scale), pk2bf(dq[2] * scale, dq[3] * scale));
+        *reinterpret_cast<uint2 *>(drow + h) = make_uint2(pk2bf(dk[0] * scale, dk[1] * scale), pk2bf(dk[2] * scale, dk[3] * scale));
+        *reinterpret_cast<uint2 *>(drow + 2 * h) = make_uint2(pk2bf(dv[0], dv[1]), pk2bf(dv[2], dv[3]));
+    }
+    wave_lds_sync();
+    attn_board_store(dqkv + b * 16 * (int64_t)(3 * h), tile, 3 * h, lane);
+}
+
 // Training-path residual RMSNorm of GameURMBlock (game.py:1346, 1350 with rms_norm :1223-1229) as
 // one kernel each way, h = 64, for autograd (agent.GameURMBlock): 16 lanes per row (float4 each),
 // row sums by 4 xor shuffles inside the 16-lane group.
@@ -2060,9 +2211,15 @@ int g2048_urm_attention_drop_at(g2048_stream_t stream, const uint16_t *qkv, uint
     d.offset = offset;
     if (n == 0) return G2048_OK;
     if (!qkv || !out) return G2048_EINVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    if (h == 16 * heads && h <= 64 && ((uintptr_t)qkv | (uintptr_t)out) % 16 == 0) {  // one wave per board
+        const dim3 gb((unsigned)((n + 3) / 4));
+        if (d.thr != 0) hipLaunchKernelGGL(urm_attn16b_kernel<true>, gb, dim3(256), 0, s, qkv, out, n, (int)h, (int)heads, d);
+        else hipLaunchKernelGGL(urm_attn16b_kernel<false>, gb, dim3(256), 0, s, qkv, out, n, (int)h, (int)heads, d);
+        return launch_status();
+    }
     const int64_t tasks = n * heads;
     const dim3 grid(blocks(tasks, kThreads / 64));
-    const hipStream_t s = (hipStream_t)stream;
     const bool al = (h / heads) % 4 == 0, dr = d.thr != 0;
     if (al && dr) hipLaunchKernelGGL((urm_attn_kernel<true, true>), grid, dim3(kThreads), 0, s, qkv, out, tasks, (int)h, (int)heads, d);
     else if (al) hipLaunchKernelGGL((urm_attn_kernel<true, false>), grid, dim3(kThreads), 0, s, qkv, out, tasks, (int)h, (int)heads, d);
@@ -2090,6 +2247,16 @@ int g2048_urm_attention_bwd_drop_at(g2048_stream_t stream, const uint16_t *qkv, 
     d.offset = offset;
     if (n == 0) return G2048_OK;
     if (!qkv || !dout || !dqkv || ((uintptr_t)qkv | (uintptr_t)dout | (uintptr_t)dqkv) % 8) return G2048_EINVAL;
+    if (h <= 64 && ((uintptr_t)qkv | (uintptr_t)dout | (uintptr_t)dqkv) % 16 == 0) {  // one wave per board
+        const dim3 gb((unsigned)((n + 3) / 4));
+        if (d.thr != 0)
+            hipLaunchKernelGGL(urm_attn_bwd16b_kernel<true>, gb, dim3(256), 0, (hipStream_t)stream, qkv, dout, dqkv, n,
+                               (int)h, (int)heads, d);
+        else
+            hipLaunchKernelGGL(urm_attn_bwd16b_kernel<false>, gb, dim3(256), 0, (hipStream_t)stream, qkv, dout, dqkv, n,
+                               (int)h, (int)heads, d);
+        return launch_status();
+    }
     const int64_t tasks = n * heads;
     if (d.thr != 0)
         hipLaunchKernelGGL(urm_attn_bwd16_kernel<true>, dim3(blocks(tasks, 4)), dim3(256), 0, (hipStream_t)stream, qkv,

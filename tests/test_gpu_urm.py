@@ -1303,3 +1303,41 @@ def test_urm_ppo_updater_matches_generic_updater(dev):
             assert float((a - b).abs().max()) <= 2e-3 * float(b.abs().max()) + 1e-9, k
     for k in s0:  # (kl_max: the largest single-row KL, the most order-sensitive entry -- measured 0.9 %)
         assert math.isclose(s0[k], s1[k], rel_tol=2e-2 if k == "kl_max" else 1e-3, abs_tol=1e-6), (k, s0[k], s1[k])
+
+
+@pytest.mark.parametrize("n,heads,p", [(4099, 4, 0.0), (1000, 4, 0.1), (333, 2, 0.2)])
+def test_urm_attention_board_kernels_are_bitwise_the_head_kernels(dev, n, heads, p):
+    """The one-wave-per-board attention kernels (round 5: the board's qkv / dO rows staged in LDS by
+    16-byte loads) vs the per-(board, head) kernels they replace for head_dim 16 -- which still run on
+    8-byte-aligned (not 16) buffers: forward output and dq / dk / dv bitwise equal, with and without
+    dropout (the same mask counter)."""
+    from g2048 import _lib as L
+    from g2048 import urm
+    torch.manual_seed(n)
+    h = 16 * heads
+    qkv = (torch.randn(16 * n, 3 * h, device=dev) * 1.5).bfloat16()
+    dout = torch.randn(16 * n, h, device=dev).bfloat16()
+    seed, _ = urm._attn_drop_state(dev)
+    ctr = torch.tensor([77], dtype=torch.int64, device=dev)
+
+    def shifted(t):  # the same values at an address 8 bytes past a 16-byte boundary
+        buf = torch.empty(t.numel() + 8, dtype=t.dtype, device=dev)
+        v = buf[4:4 + t.numel()].view(t.shape)
+        v.copy_(t)
+        assert v.data_ptr() % 16 == 8
+        return v
+    res = []
+    for aligned in (True, False):
+        q = qkv if aligned else shifted(qkv)
+        d = dout if aligned else shifted(dout)
+        out = torch.empty(16 * n, h, dtype=torch.bfloat16, device=dev)
+        dq = torch.empty_like(qkv) if aligned else shifted(torch.zeros_like(qkv))
+        if aligned:
+            out_t = out
+        else:
+            out_t = shifted(torch.zeros_like(out))
+        L.urm_attention(q, out_t, heads, p, seed, ctr, offset=3)
+        L.urm_attention_bwd(q, d, dq, heads, p, seed, ctr, offset=3)
+        res.append((out_t.clone(), dq.clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
