@@ -360,6 +360,13 @@ __device__ __forceinline__ float muon_prologue(const float *__restrict__ grad, f
     return ss;
 }
 
+// p decay - x step without contraction: the same bits in every inlining context (the one-CU epilogue
+// and the multi-CU parts' prefetched form)
+__device__ __forceinline__ float muon_update(float p, float decay, float x, float step) {
+#pragma clang fp contract(off)
+    return p * decay - x * step;
+}
+
 __device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_t *__restrict__ pbf, const char *sX,
                                               int px, int R, int C, bool tr, float decay, float step, int tid,
                                               int pr0 = 0, int pr1 = 1 << 30, uint16_t *frag = nullptr,
@@ -368,7 +375,7 @@ __device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_
         for (int e = tid; e < R * C; e += kMuonThreads) {
             const int i = e / C, j = e - i * C;
             const float x = bf2f(reinterpret_cast<const uint16_t *>(sX + (tr ? j * px : i * px))[tr ? i : j]);
-            const float pv = param[e] * decay - x * step;
+            const float pv = muon_update(param[e], decay, x, step);
             param[e] = pv;
             if (pbf) pbf[e] = (uint16_t)f2bf(pv);
         }
@@ -402,7 +409,7 @@ __device__ __forceinline__ void muon_epilogue(float *__restrict__ param, uint16_
                 x[3] = bf2f(w.y >> 16);
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) pv[u] = pv[u] * decay - x[u] * step;
+            for (int u = 0; u < 4; u++) pv[u] = muon_update(pv[u], decay, x[u], step);
             reinterpret_cast<float4 *>(param)[e4] = make_float4(pv[0], pv[1], pv[2], pv[3]);
             if (pbf) reinterpret_cast<uint2 *>(pbf)[e4] = make_uint2(pack_bf2(pv[0], pv[1]), pack_bf2(pv[2], pv[3]));
             if (frag && !tr)
@@ -863,7 +870,7 @@ __device__ __forceinline__ void mc_mfma(const char *A, const char *B, int t0, in
 #pragma unroll
         for (int x = 0; x < RB; x++) {
             uint4 v = *reinterpret_cast<const uint4 *>(pa[x] + 64 * ks);
-            if (!BT_ROWS && ks == S::KS - 1 && 32 * S::KS > S::KPAD) v = kin ? v : make_uint4(0u, 0u, 0u, 0u);
+            if (ks == S::KS - 1 && 32 * S::KS > S::KPAD) v = kin ? v : make_uint4(0u, 0u, 0u, 0u);
             acc[x] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, v), fb, acc[x], 0, 0, 0);
         }
     }
@@ -1076,13 +1083,27 @@ __device__ __forceinline__ float tile_prologue(const float *__restrict__ grad, f
 // divisor: q0 = y (1/nrm), one fma residual, one fma correction -- the correctly rounded fp32 y / nrm
 // for every pair of bf16 operands (all 128 x 128 significand pairs checked exactly,
 // tools/check_bf16_division.py), zeros passed through with their sign
+// y / nrm correctly rounded (the reference's X / X.norm() in fp32), zero kept
+__device__ __forceinline__ float norm_qdiv(float y, float nrm, float inv) {
+    const float q0 = y * inv;
+    const float q = __builtin_fmaf(__builtin_fmaf(-q0, nrm, y), inv, q0);
+    return y == 0.0f ? y : q;
+}
+
+// 8 bf16 of an image / nrm, re-rounded to bf16 (normalise_image's arithmetic on a 16-byte chunk)
+__device__ __forceinline__ uint4 normalise16(const uint4 v, float nrm) {
+    const float inv = 1.0f / nrm;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        o[k] = pack_bf2(norm_qdiv(bf2f(w[k] & 0xFFFFu), nrm, inv), norm_qdiv(bf2f(w[k] >> 16), nrm, inv));
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 __device__ __forceinline__ void normalise_image(char *sX, int nbytes, float nrm, int tid) {
     const float inv = 1.0f / nrm;
-    auto qdiv = [&](float y) {
-        const float q0 = y * inv;
-        const float q = __builtin_fmaf(__builtin_fmaf(-q0, nrm, y), inv, q0);
-        return y == 0.0f ? y : q;
-    };
+    auto qdiv = [&](float y) { return norm_qdiv(y, nrm, inv); };
     const int n8 = nbytes >> 3;
     uint2 *img = reinterpret_cast<uint2 *>(sX);
     for (int e0 = tid; e0 < n8; e0 += 4 * kMuonThreads) {
@@ -1126,7 +1147,17 @@ __device__ __forceinline__ void mc_copy_image(char *sX, const char *src, int tid
 // per lane for g2048_grad_sumsq's 64: grad_norm_kernel's arithmetic), then the wave's xor tree
 __device__ __forceinline__ float clip_sumsq(const MuonArgs &args, int lane) {
     float t = 0.0f;
-    for (int i = lane; i < args.npartials; i += 64) t += args.partials[i];
+    int i = lane;
+    // 8 loads in flight, added in index order (round 5: one dependent L2 round trip per entry was ~2 us
+    // on the critical path of every Muon part with the colsum's ~360 partials)
+    for (; i + 64 * 7 < args.npartials; i += 64 * 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = args.partials[i + 64 * u];
+#pragma unroll
+        for (int u = 0; u < 8; u++) t += v[u];
+    }
+    for (; i < args.npartials; i += 64) t += args.partials[i];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
     return t;
@@ -1203,8 +1234,12 @@ __device__ __forceinline__ void mc_matrix(char *smem, float *red, const MuonArgs
         g4[x] = ok ? reinterpret_cast<const float4 *>(mt.grad)[e] : make_float4(0.f, 0.f, 0.f, 0.f);
         b4[x] = ok ? reinterpret_cast<const float4 *>(mt.mom)[e] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    {  // zero both LDS images (their K padding must read as zero)
-        const int bytes = (int)(sG - smem) + ((N * P + 127) & ~127);
+    {  // zero both LDS images (their K padding must read as zero) and the 64 bytes behind them (part of
+       // the allocation, muon_lds_bytes): the last k-step of a row of G reads 32 bytes past the row (B is
+       // zero there), and for G's last row that is past the image -- uninitialised LDS, whose NaN / Inf
+       // bit patterns (left by an earlier kernel on the CU) made X NaN for h = 196 on one box (round 5;
+       // h = 192 has no ragged k-step; the one-CU path always zeroed them)
+        const int bytes = (int)(sG - smem) + ((N * P + 127) & ~127) + 64;
         for (int o = tid * 16; o < bytes; o += kMuonThreads * 16) *reinterpret_cast<uint4 *>(smem + o) = make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
@@ -1237,26 +1272,42 @@ __device__ __forceinline__ void mc_matrix(char *smem, float *red, const MuonArgs
     if (wave == 0) mc_wait(line, (uint32_t)np, line + 1, errors, args.spin_limit);
     __syncthreads();
     MUON_TP(args);
-    mc_copy_image<N>(sX, img1, tid);
-    float total = 0.0f;
+    // the NT tile-row sums: one relaxed load per thread < NT (not NT dependent loads in every thread),
+    // summed in tile order from LDS
+    static_assert(NT <= kMuonThreads / 64, "tile-row sums staged in red[]");
+    if (tid < NT) red[tid] = __uint_as_float(__hip_atomic_load(line + 3 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    // the whole image in flight into registers, then normalised there on its way into LDS
+    // (normalise_image's per-element arithmetic: no LDS round trip and barrier of its own)
+    {
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(img1, (short)0, N * P, 0x00020000);
+        constexpr int kCopy = (N * P / 16 + kMuonThreads - 1) / kMuonThreads;
+        uint4 cv[kCopy];
 #pragma unroll
-    for (int t = 0; t < NT; t++)
-        total += __uint_as_float(__hip_atomic_load(line + 3 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    __syncthreads();
-    normalise_image(sX, N * P, fmaxf(round_bf(sqrtf(total)), args.eps), tid);  // x.norm() of the bf16 X, clamped
+        for (int u = 0; u < kCopy; u++)
+            cv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, (tid + u * kMuonThreads) * 16, 0, 16));
+        __syncthreads();
+        float total = 0.0f;
+#pragma unroll
+        for (int t = 0; t < NT; t++) total += red[t];
+        const float nrm = fmaxf(round_bf(sqrtf(total)), args.eps);  // x.norm() of the bf16 X, clamped
+#pragma unroll
+        for (int u = 0; u < kCopy; u++) {
+            const int o = (tid + u * kMuonThreads) * 16;
+            if (o < N * P) *reinterpret_cast<uint4 *>(sX + o) = normalise16(cv[u], nrm);
+        }
+    }
     __syncthreads();
     MUON_TP(args);
+    // the epilogue's learning rate in flight now, not after the last product
+    const float lr_pre = args.lr[mt.lr_index];
     ns_square_mc<N>(sX, sG, args, mat, part, np, wave, lane, (uint32_t)np);
-    // decoupled weight decay + the match_rms_adamw-scaled update of this part's rows, bf16 copies
-    const float lr = args.lr[mt.lr_index];
-    const float step = lr * (0.2f * sqrtf((float)N));
-    muon_epilogue(mt.param, mt.pbf, sX, P, N, N, false, 1.0f - lr * args.wd, step, tid, 16 * t0, 16 * (t0 + rb));
     // the last part through here puts the matrix's counters back to zero for the next launch (no
     // memset node per step): every other part has finished all its polls when it counts in.  The
     // done add is a release (this part's counter adds, same thread, happen before it) and the last
     // arriver acquires before its reset stores, so the reset is ordered after every part's adds by
-    // the memory model, not by the order L2 happens to apply atomics in.
-    if (tid == 0) {
+    // the memory model, not by the order L2 happens to apply atomics in.  (By the last wave, whose
+    // round trip overlaps the other waves' epilogue.)
+    if (tid == kMuonThreads - 64) {
         gu32_t *done = line + 2;
         if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(np - 1)) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1264,6 +1315,19 @@ __device__ __forceinline__ void mc_matrix(char *smem, float *red, const MuonArgs
             __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+    // decoupled weight decay + the match_rms_adamw-scaled update of this part's rows, bf16 copies
+    // (the learning rate read before the products.  Round 5 also measured the parameter rows
+    // prefetched there: the 8 registers they held through the products cost the first G product
+    // ~3 k cycles more than the epilogue saved)
+    const float step = lr_pre * (0.2f * sqrtf((float)N));
+    muon_epilogue(mt.param, mt.pbf, sX, P, N, N, false, 1.0f - lr_pre * args.wd, step, tid, 16 * t0, 16 * (t0 + rb));
+}
+
+__global__ __launch_bounds__(1024) void lds_poison_kernel(uint32_t word) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint32_t *w = reinterpret_cast<uint32_t *>(smem);
+    for (int i = threadIdx.x; i < kMuonLds / 4; i += 1024) w[i] = word;
+    __syncthreads();
 }
 
 __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
@@ -1434,6 +1498,13 @@ size_t g2048_muon_workspace_bytes(void) {
 }
 
 size_t g2048_muon_error_offset(void) { return (size_t)kMuonErrWord * sizeof(uint32_t); }
+
+int g2048_lds_poison(g2048_stream_t stream, uint32_t word) {
+    // 2 blocks per CU of the whole LDS each, every dword = word (tests: kernels must not read LDS
+    // they did not write -- a NaN pattern left behind turns such a read into a NaN)
+    hipLaunchKernelGGL(lds_poison_kernel, dim3(512), dim3(1024), kMuonLds, (hipStream_t)stream, word);
+    return hipGetLastError() == hipSuccess ? G2048_OK : G2048_EINVAL;
+}
 
 int g2048_muon_supported(int32_t rows, int32_t cols) {
     if (rows <= 0 || cols <= 0) return 0;

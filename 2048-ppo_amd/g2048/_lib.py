@@ -35,7 +35,7 @@ EXPORTED = (
     "g2048_colsum_batch_blocks", "g2048_colsum_batch_sq",
     "g2048_wgrad_partials", "g2048_wgrad", "g2048_wgrad_pair_partials", "g2048_wgrad_pair", "g2048_linear_dgrad_supported", "g2048_linear_dgrad",
     "g2048_grad_clip", "g2048_muon_supported", "g2048_muon_step", "g2048_adamw_step",
-    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_muon_workspace_bytes", "g2048_muon_error_offset", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_attention_drop_at", "g2048_urm_attention_bwd_drop_at", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_stem_bwd3", "g2048_urm_rms_res_fwd2", "g2048_urm_rms_res_bwd2", "g2048_urm_rms_res_bwd3", "g2048_urm_add_cast", "g2048_urm_add_cast_bwd", "g2048_urm_add_cast_bwd_acc", "g2048_urm_forward_drop", "g2048_urm_rms_res_fwd",
+    "g2048_grad_sumsq", "g2048_muon_step_clip", "g2048_muon_workspace_bytes", "g2048_muon_error_offset", "g2048_lds_poison", "g2048_grad_sumsq_tick", "g2048_muon_adamw_step_clip", "g2048_mlp_fwd_kl", "g2048_urm_attention_bwd", "g2048_urm_attention_drop", "g2048_urm_attention_bwd_drop", "g2048_urm_attention_drop_at", "g2048_urm_attention_bwd_drop_at", "g2048_urm_stem_partials", "g2048_urm_stem_fwd", "g2048_urm_stem_bwd", "g2048_urm_stem_bwd3", "g2048_urm_rms_res_fwd2", "g2048_urm_rms_res_bwd2", "g2048_urm_rms_res_bwd3", "g2048_urm_add_cast", "g2048_urm_add_cast_bwd", "g2048_urm_add_cast_bwd_acc", "g2048_urm_forward_drop", "g2048_urm_rms_res_fwd",
     "g2048_urm_rms_res_bwd", "g2048_urm_swiglu_conv_partials", "g2048_urm_swiglu_conv_fwd", "g2048_urm_swiglu_conv_bwd",
     "g2048_mlp_fwd_lds_bytes", "g2048_mlp_fwd", "g2048_head_fwd", "g2048_ppo_stats",
     "g2048_policy_rollout_supported", "g2048_policy_rollout_lds_bytes", "g2048_policy_rollout",
@@ -301,6 +301,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_grad_sumsq": (ctypes.c_int, [vp, vp, i64, vp]),
         "g2048_muon_workspace_bytes": (sz, []),
         "g2048_muon_error_offset": (sz, []),
+        "g2048_lds_poison": (ctypes.c_int, [vp, u32]),
         "g2048_muon_step_clip": (ctypes.c_int, [vp, ctypes.POINTER(MuonMatrix), i32, vp, vp, ctypes.c_float, vp, vp,
                                                 ctypes.POINTER(MuonCfg)]),
         "g2048_adamw_step": (ctypes.c_int, [vp, ctypes.POINTER(AdamWGroup), i32, vp, vp, vp, ctypes.c_float,
@@ -1263,6 +1264,13 @@ def urm_wgrad_supported(n: int, k: int) -> bool:
 
 def urm_wgrad_partials(m: int, n: int, k: int) -> int:
     return int(load().g2048_urm_wgrad_partials(m, n, k))
+
+
+def lds_poison(word: int, device=None):
+    """Test hook: every CU's LDS filled with the 32-bit `word` (g2048_lds_poison)."""
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    _check(load().g2048_lds_poison(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream), int(word) & 0xFFFFFFFF),
+           "g2048_lds_poison")
 
 
 def urm_head_loss_partials(m: int, h: int) -> int:

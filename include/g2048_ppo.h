@@ -428,6 +428,11 @@ size_t g2048_muon_workspace_bytes(void);
  * launches; zero = every multi-CU Newton-Schulz so far was valid). */
 size_t g2048_muon_error_offset(void);
 
+/* Test hook: fill every CU's LDS with `word` (two 1024-thread blocks of the whole LDS per CU), so a
+ * following kernel that reads LDS it did not write sees that pattern (a NaN bit pattern makes such a
+ * read visible in its results).  Used by tests/test_gpu_ppo_fused.py; no part of the update. */
+int g2048_lds_poison(g2048_stream_t stream, uint32_t word);
+
 /* 1 if a [rows, cols] matrix fits the one-block-per-matrix Newton-Schulz kernel (min dim <= 224,
  * max dim <= 256, both LDS images <= ~159 KB: h <= 196 for square weights; rows of a length that
  * is not a multiple of 4 -- GameURM's [64, 3] stem -- take a per-element momentum / update pass). */

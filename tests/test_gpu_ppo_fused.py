@@ -607,6 +607,34 @@ def test_muon_multi_cu_equals_one_cu(dev, h, parts, loaded, monkeypatch):
         assert torch.equal(a, b), (a - b).abs().max()
 
 
+@pytest.mark.parametrize("h", [196, 192])
+def test_muon_multi_cu_reads_no_stale_lds(dev, h, monkeypatch):
+    """Every CU's LDS filled with a NaN pattern before each step (g2048_lds_poison): the multi-CU
+    Newton-Schulz still equals the one-CU schedule bitwise and nothing is NaN.  Round 5: G's last row
+    read 32 bytes past the image in its ragged last k-step (h = 196) and the multi-CU part had not
+    zeroed them, so a NaN left in LDS by an earlier kernel made the whole update NaN on one box."""
+    import agent
+    from g2048 import _lib as L
+    from g2048.dist import GradBucket
+    from g2048.optim import FusedMuonAdamW
+    outs = []
+    for p in (1, 13):
+        monkeypatch.setenv("G2048_MUON_PARTS", str(p))
+        torch.manual_seed(h)
+        m = agent.GameMLP(agent.MLPConfig(hidden_dim=h, num_layers=2)).to(dev)
+        opt = FusedMuonAdamW(m, 1e-3, 1e-4)
+        order = [q for q, _ in opt.muon] + [q for grp in opt.adam_groups for q in grp["params"]]
+        bk = GradBucket(order)
+        for s in range(2):
+            bk.flat.copy_(torch.randn(bk.flat.shape, generator=torch.Generator().manual_seed(s)).to(dev) * 1e-2)
+            L.lds_poison(0x7FC07FC0, dev)  # fp32 NaN = a bf16 NaN in each half
+            opt.step_clipped(bk.flat, 1.0)
+        torch.cuda.synchronize()
+        outs.append(torch.cat([q.detach().reshape(-1) for q in m.parameters()]).clone())
+    assert not outs[1].isnan().any() and not outs[0].isnan().any()
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_muon_hand_off_timeout_is_reported(dev, monkeypatch):
     """A multi-CU Newton-Schulz wait that gives up (a part that never became resident: its launch's
     weights are garbage) is never silent: forced here by a poll limit of 0 (G2048_MUON_SPIN_LIMIT,
