@@ -25,3 +25,18 @@ def golden(name: str):
 @pytest.fixture(scope="session")
 def games():
     return golden("games.npz")
+
+
+@pytest.fixture(autouse=True)
+def _stale_lds_poison(request):
+    """Every GPU test starts with every CU's LDS filled with a NaN pattern (g2048_lds_poison): a kernel
+    that reads LDS it did not write turns it into NaN in its results instead of passing on whatever
+    an earlier kernel left there (round 5: the multi-CU Muon read 32 such bytes and failed on one box
+    only).  CPU tests are untouched."""
+    if request.node.get_closest_marker("gpu") is not None:
+        import torch
+        if torch.cuda.is_available():
+            from g2048 import _lib as L
+            L.lds_poison(0x7FC07FC0)
+            torch.cuda.synchronize()
+    yield
