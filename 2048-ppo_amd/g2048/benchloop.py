@@ -15,6 +15,10 @@ import time
 import torch
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 (MI355X_MICROARCH.md), not the 2:1-sparsity figure
+HBM_PEAK_GBPS = 8000.0
+# the update kernels' HBM bytes per 65 536-row minibatch from the committed PMC passes of this build
+# (FETCH_SIZE / WRITE_SIZE, tools/pmc_train.sh -> tools/summarize_profile.py)
+UPDATE_HBM = "profiles/r05m/train/update_hbm.json"
 
 
 def mlp_flops_per_sample(h: int = 196, obs: int = 48, layers: int = 2, heads: int = 5) -> dict:
@@ -73,6 +77,23 @@ def bench_train(args, rank: int, world: int, dev) -> dict:
             roof[name] = {"bound": "mfma", "achieved": ach, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": ach / MFMA_BF16_PEAK_TFLOPS, "flop_per_sample": fl["update" if name == "update" else "forward"],
                           "samples": rows_update if name == "update" else args.envs * args.train_horizon}
+    # the same phase against HBM: the PMC-measured bytes of the update kernels per minibatch x the
+    # minibatches of the iteration over the update's wall time
+    try:
+        import json
+        from pathlib import Path
+        hb = json.loads((Path(__file__).resolve().parents[2] / UPDATE_HBM).read_text())
+        ms = phases.get("update_ms")
+        if ms and hb.get("minibatch_rows") == args.train_batch:
+            traffic = hb["bytes_per_minibatch"] * n_mb
+            ach = traffic / (ms * 1e-3) / 1e9
+            roof["update_hbm"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                  "frac": ach / HBM_PEAK_GBPS, "traffic_per_minibatch": hb["bytes_per_minibatch"],
+                                  "minibatches": n_mb, "per_kernel_bytes": {k: v["hbm_bytes_per_launch"] * v["launches_per_minibatch"]
+                                                                           for k, v in hb["kernels"].items()},
+                                  "traffic_source": UPDATE_HBM}
+    except (OSError, ValueError, KeyError):
+        pass
     return {
         "value": steps / wall, "unit": "env-steps/s", "ms_per_iter": wall / args.train_iters * 1e3,
         "iters": args.train_iters, "warmup": args.train_warmup,

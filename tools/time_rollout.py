@@ -19,6 +19,10 @@ def main():
     ap.add_argument("--h", type=int, default=196)
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
+    import os
+    if os.environ.get("G2048_LIB"):  # A/B timing against another build of the library
+        from g2048 import _lib as L
+        L._lib = L.load(os.environ["G2048_LIB"])
     import agent
     from g2048.rollout import FusedPolicy, Rollout
     dev = torch.device("cuda", 0)
