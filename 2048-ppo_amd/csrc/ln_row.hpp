@@ -12,10 +12,14 @@
 namespace g2048 {
 namespace lnrow {
 
-// A pair of fp32 features as two scalars: the VALU runs v_fma_f32 / v_add_f32 at the issue cost of
-// one 2-cycle instruction each, while a packed v_pk_fma_f32 beside MFMAs costs ~22 cycles more than
-// the two scalar ones (MI355X_MICROARCH.md, 'price of one filler beside MFMAs') -- and these
-// epilogues run beside the partner wave's MFMAs.  Per element the same IEEE operation either way.
+// A pair of fp32 features.  Round 5: a native 2-vector, so + * fma become v_pk_add_f32 /
+// v_pk_mul_f32 / v_pk_fma_f32 -- per element the same IEEE operation (same bits), two features per
+// instruction.  These epilogues run between a wave's own products at one wave per SIMD (no partner
+// wave's MFMAs beside them), where tools/probe/pk_rate.hip measured 4.6 cycles per v_pk_fma_f32 vs
+// 5.1 per v_fma_f32: 2.2x the FMAs.  (Beside MFMAs a packed op costs ~22 cycles more than the two
+// scalar ones, MI355X_MICROARCH.md 'price of one filler beside MFMAs': G2048_LN_SCALAR restores the
+// scalar pairs.)
+#ifdef G2048_LN_SCALAR
 struct f32x2 {
     float x, y;
 };
@@ -24,6 +28,10 @@ __device__ __forceinline__ f32x2 operator*(f32x2 a, f32x2 b) { return f32x2{a.x 
 __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) {
     return f32x2{__builtin_fmaf(a.x, b.x, c.x), __builtin_fmaf(a.y, b.y, c.y)};
 }
+#else
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+#endif
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
