@@ -72,7 +72,7 @@ __device__ __forceinline__ void round_g(const f32x4 (&acc)[NT], f32x2 (&v)[NT][2
 // Row statistics over the valid features (valid(n): tile n's 4-group of this lane is < h): the sum
 // as packed fp32 pairs in tile order (element pairs (0, 1) and (2, 3) of a tile), the pair's two
 // halves added, then the xor-16 / xor-32 lane sums; v becomes dv = v - sum/h (one fma); the
-// variance of dv likewise (packed fmas); rstd = 1 / sqrt(var/h + eps).  Returns the mean (sum/h)
+// variance of dv likewise (packed fmas); rstd = rsqrt(var/h + eps).  Returns the mean (sum/h)
 // and rstd.
 template <int NT, class Valid>
 __device__ __forceinline__ void stats(f32x2 (&v)[NT][2], Valid valid, float inv_n, float &mean, float &rstd) {
@@ -94,7 +94,10 @@ __device__ __forceinline__ void stats(f32x2 (&v)[NT][2], Valid valid, float inv_
     }
     const float var = xor32_add(xor16_add(q2.x + q2.y));
     mean = sum * inv_n;
-    rstd = 1.0f / sqrtf(__builtin_fmaf(var, inv_n, kEps));
+    // round 5: the hardware reciprocal square root (v_rsq_f32, ~1 ulp; torch's layer_norm kernel
+    // takes rsqrt too) instead of the correctly rounded 1 / sqrt (~25 instructions per row per layer
+    // with its denormal scaling): every kernel on this header computes the same rstd bits
+    rstd = __builtin_amdgcn_rsqf(__builtin_fmaf(var, inv_n, kEps));
 }
 
 // ReLU(LayerNorm) of a feature pair: max(fma(dv * rstd, gamma, beta), 0)

@@ -44,10 +44,14 @@ using namespace g2048::tile;
 
 constexpr int kPrThreads = 256;
 constexpr int kPrLdsMax = 163840;
+constexpr int kPrRecBytes = 4 * 80;  // the stem fragment recipes of the 4 lane groups (LDS, after the zero fragment)
 #ifndef PR_TILES
 #define PR_TILES 2
 #endif
-constexpr int kQ = PR_TILES;  // board tiles (of 16 boards) per MLP pass: accumulators of kQ x NT tiles
+constexpr int kQ = PR_TILES;
+#ifndef PR_NSPLIT
+#define PR_NSPLIT 0
+#endif  // board tiles (of 16 boards) per MLP pass: accumulators of kQ x NT tiles
 
 struct PrArgs {
     uint4 *boards;      // [T+1][n][16] int8: row t0 read, rows t0+1 .. t1 written
@@ -138,6 +142,7 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
     char *sW[2] = {smem, smem + WB};  // block weight images (LDS offsets 0 and WB)
     float *sLN = reinterpret_cast<float *>(smem + 2 * WB);  // [layer][gamma | beta][16 NT]
     char *sZero = smem + 2 * WB + 2 * kMaxLayers * pr_ln_floats(NT) * 4;
+    char *sRec = sZero + 16;  // [g][sc0 sc1 ss0 ss1 {sx0 sx1 sd0 sd1}] uint4
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, col = lane & 15;
 
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
             for (int c = tid; c < h * q8; c += kPrThreads) {
                 const int r = c / q8, q = c - r * q8;
                 const uint2 v = q < h4 ? *reinterpret_cast<const uint2 *>(wsrc[l] + (int64_t)r * h + 4 * q) : make_uint2(0u, 0u);
-                *reinterpret_cast<uint2 *>(sW[l] + r * P + pr_shift(h, r) + 8 * q) = v;
+                *reinterpret_cast<uint2 *>(sW[l] + pr_piece(h, r, q)) = v;
             }
         for (int e = tid; e < kMaxLayers * 2 * 16 * NT; e += kPrThreads) {
             const int l = e / (32 * NT), rem = e - l * 32 * NT, which = rem / (16 * NT), f = rem - which * 16 * NT;
@@ -157,6 +162,15 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
             sLN[e] = f < h ? src[f] : 0.0f;
         }
         if (tid < 4) reinterpret_cast<uint32_t *>(sZero)[tid] = 0u;
+        if (tid < 20) {
+            const StemFrag &e = kStem.f[tid / 5][0], &f = kStem.f[tid / 5][1];
+            const int j = tid % 5;
+            reinterpret_cast<uint4 *>(sRec)[tid] = j == 0 ? make_uint4(e.c[0], e.c[1], e.c[2], e.c[3])
+                                                 : j == 1 ? make_uint4(f.c[0], f.c[1], f.c[2], f.c[3])
+                                                 : j == 2 ? make_uint4(e.sel[0], e.sel[1], e.sel[2], e.sel[3])
+                                                 : j == 3 ? make_uint4(f.sel[0], f.sel[1], f.sel[2], f.sel[3])
+                                                          : make_uint4(e.xsel, f.xsel, e.d, f.d);
+        }
     }
     __syncthreads();
 
@@ -166,19 +180,10 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
     const uint64_t ctr0 = a.counter + (a.counter_dev ? *a.counter_dev : 0ull);
     RngArgs rng{a.seed, 0ull, nullptr, a.env_base, nullptr, nullptr};
 
-    // this lane group's stem fragment recipe (kStem)
-    uint4 sc[2], ss[2];
-    uint32_t sx[2], sd[2];
-#pragma unroll
-    for (int ks = 0; ks < 2; ks++) {
-        const StemFrag &e = kStem.f[g][ks];
-        sc[ks] = make_uint4(e.c[0], e.c[1], e.c[2], e.c[3]);
-        ss[ks] = make_uint4(e.sel[0], e.sel[1], e.sel[2], e.sel[3]);
-        sx[ks] = e.xsel;
-        sd[ks] = e.d;
-    }
-    // A-fragment LDS offsets of the block weights: row 16 n + col, k = 32 ks + 8 g (+ 16 n P per tile)
-    const int wlane = col * P + pr_shift(h, col) + 16 * g;
+    const int recoff = (int)(sRec - smem) + 80 * g;  // this lane group's stem fragment recipe (kStem)
+    // A-fragment LDS offsets of the block weights: row 16 n + col, k = 32 ks + 8 g (+ 16 n P per tile);
+    // wlane_x in the swizzled k-step groups (pr_piece)
+    const int wlane = col * P + 16 * g, wlane_x = col * P + 16 * (g ^ pr_swz(h, col));
     const int zoff = (int)(sZero - smem);
     constexpr int last_rows = h - 16 * (NT - 1);  // valid rows of the last tile
 
@@ -192,9 +197,12 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
         for (int t = a.t0; t < a.t1; t++) {
             // opaque per-step copies of the lane offsets: without them the compiler hoists every
             // (tile, k-step) fragment address out of the step loop and spills them
-            int wlane_t = wlane, glane_t = (col * 48 + 8 * g) * 2, hlane_t = ((col & 3) * KP + 8 * g) * 2;
-            asm volatile("" : "+v"(wlane_t), "+v"(glane_t), "+v"(hlane_t));
-            const char *w0b = reinterpret_cast<const char *>(a.w0) + glane_t;
+            int wlane_t = wlane, wlane_xt = wlane_x, glane_t = (col * 48 + 8 * g) * 2, hlane_t = ((col & 3) * KP + 8 * g) * 2;
+            asm volatile("" : "+v"(wlane_t), "+v"(wlane_xt), "+v"(glane_t), "+v"(hlane_t));
+            // the stem weight fragments through a buffer descriptor (as ppo_fused.hip): rows past h and
+            // k past 48 (ks 1, lane groups 2, 3) read out of range = zero, no per-lane branch / zeroing
+            const __amdgpu_buffer_rsrc_t w0r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(a.w0), 0, h * 96, 0x00020000);
+            const int w0off[2] = {glane_t, g < 2 ? glane_t + 64 : h * 96};
             const char *hdb = reinterpret_cast<const char *>(a.head) + hlane_t;
             const char *hvb = reinterpret_cast<const char *>(a.head) + (4 * KP + 8 * g) * 2;
             // The MLP runs on two board tiles at a time (accumulators of 2 x NT tiles; the weight
@@ -206,6 +214,16 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
                 uint2 act[kQ][NT];
                 // ---------------- stem: obs fragments (to_model_format, natural k order) ------
                 uint4 xs[kQ][2];
+                // the recipe re-read from LDS per pair (20 registers less across the MLP); an opaque
+                // offset keeps the reads inside the loop
+                int rco = recoff, lno = 0;
+                asm volatile("" : "+v"(rco), "+v"(lno));
+                // the LayerNorm affines from an opaque per-pair base: one address register and
+                // immediate offsets (else every (layer, tile) address is hoisted and parked in AGPRs)
+                const float *sLNr = sLN + lno;
+                const uint4 *rec = reinterpret_cast<const uint4 *>(smem + rco);
+                const uint4 sc[2] = {rec[0], rec[1]}, ss[2] = {rec[2], rec[3]}, r4 = rec[4];
+                const uint32_t sx[2] = {r4.x, r4.y}, sd[2] = {r4.z, r4.w};
 #pragma unroll
                 for (int q = 0; q < kQ; q++) {
                     const int src = 16 * (kQ * pr + q) + col;
@@ -234,9 +252,7 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
                 for (int ks = 0; ks < 2; ks++) {
 #pragma unroll
                     for (int n = 0; n < NT; n++) {
-                        const int row = 16 * n + col, k = 32 * ks + 8 * g;
-                        uint4 fw = make_uint4(0u, 0u, 0u, 0u);
-                        if (row < h && k < 48) fw = *reinterpret_cast<const uint4 *>(w0b + 2 * (16 * n * 48 + 32 * ks));
+                        const uint4 fw = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(w0r, w0off[ks], 2 * 16 * n * 48, 0));
 #pragma unroll
                         for (int q = 0; q < kQ; q++)
                             acc[q][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(fw), as_frag(xs[q][ks]), acc[q][n], 0, 0, 0);
@@ -244,7 +260,7 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
                     __builtin_amdgcn_sched_barrier(0);
                 }
 #pragma unroll
-                for (int q = 0; q < kQ; q++) ln_epilogue<NT, H, false>(acc[q], act[q], sLN, sLN + 16 * NT, g, inv_n);
+                for (int q = 0; q < kQ; q++) ln_epilogue<NT, H, false>(acc[q], act[q], sLNr, sLNr + 16 * NT, g, inv_n);
                 if (a.debug && t == a.t0)
                     for (int q = 0; q < kQ; q++) debug_act<NT>(a, 0, base + 64 * wave + 16 * (kQ * pr + q) + col, act[q], g);
 
@@ -255,14 +271,14 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
                     for (int q = 0; q < kQ; q++)
 #pragma unroll
                         for (int n = 0; n < NT; n++) acc[q][n] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-                    const int wbase = l * WB + wlane_t;
 #pragma unroll
                     for (int ks = 0; ks < KS; ks++) {
                         uint4 bf[kQ];
 #pragma unroll
                         for (int q = 0; q < kQ; q++) bf[q] = act_frag<NT>(act[q], ks);
                         const bool kok = 32 * ks + 8 * g < hp8;
-                        int kbase = wbase + 64 * ks;  // materialised here, per k-step (see wlane_t)
+                        // materialised here, per k-step (see wlane_t)
+                        int kbase = l * WB + (pr_ks_swz(h, ks) ? wlane_xt : wlane_t) + 64 * ks;
                         asm volatile("" : "+v"(kbase));
 #pragma unroll
                         for (int n = 0; n < NT; n++) {
@@ -277,7 +293,7 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
                         // (they would all be live at once)
                         __builtin_amdgcn_sched_barrier(0);
                     }
-                    const float *lnp = sLN + (l + 1) * 32 * NT;
+                    const float *lnp = sLNr + (l + 1) * 32 * NT;
 #pragma unroll
                     for (int q = 0; q < kQ; q++) ln_epilogue<NT, H, true>(acc[q], act[q], lnp, lnp + 16 * NT, g, inv_n);
                     if (a.debug && t == a.t0)
@@ -340,7 +356,7 @@ extern "C" {
 size_t g2048_policy_rollout_lds_bytes(int32_t h) {
     if (h <= 0 || h % 4 != 0) return 0;
     const int nt = (h + 15) / 16;
-    const size_t b = (size_t)pr_lds_bytes(h, nt);
+    const size_t b = (size_t)pr_lds_bytes(h, nt) + kPrRecBytes;
     return b <= (size_t)kPrLdsMax ? b : 0;
 }
 

@@ -182,7 +182,7 @@ __global__ __launch_bounds__(kFpThreads) void mlp_pass_kernel(FpArgs a) {
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
                     const int c = c0 + tid + u * kFpThreads, r = c / q8, q = c - r * q8;
-                    if (c < per) *reinterpret_cast<uint2 *>(smem + l * WB + r * PW + 8 * q) = v[u];
+                    if (c < per) *reinterpret_cast<uint2 *>(smem + l * WB + pr_piece(h, r, q)) = v[u];
                 }
             }
         for (int e = tid; e < kMaxLayers * 2 * 16 * NT; e += kFpThreads) {
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(kFpThreads) void mlp_pass_kernel(FpArgs a) {
     constexpr int last_rows = h - 16 * (NT - 1);
     const StemRecipe sr = stem_recipe(g);
     const P::Drop d1 = P::make_drop(a.drop[0]), d2 = P::make_drop(a.drop[1]);
-    const int wlane = col * PW + 16 * g;
+    const int wlane = col * PW + 16 * g, wlane_x = col * PW + 16 * (g ^ pr_swz(h, col));  // plain / swizzled k groups
     const int zoff = (int)(sZero - smem);
     const float bias[5] = {a.ba[0], a.ba[1], a.ba[2], a.ba[3], TRAIN ? a.bv[0] : 0.0f};
     const float beta_c = TRAIN ? *a.la.beta_dev : 0.0f;
@@ -214,8 +214,8 @@ __global__ __launch_bounds__(kFpThreads) void mlp_pass_kernel(FpArgs a) {
         const bool live = lane < kFpRows && r < m, real = live && r < mv;
         const uint4 b = live ? *reinterpret_cast<const uint4 *>(a.boards + idxp[r] * 16) : make_uint4(0u, 0u, 0u, 0u);
 
-        int wlane_t = wlane, glane_t = (col * 48 + 8 * g) * 2;
-        asm volatile("" : "+v"(wlane_t), "+v"(glane_t));
+        int wlane_t = wlane, wlane_xt = wlane_x, glane_t = (col * 48 + 8 * g) * 2;
+        asm volatile("" : "+v"(wlane_t), "+v"(wlane_xt), "+v"(glane_t));
         // the LayerNorm affines are re-read from LDS per layer: an opaque base keeps the compiler
         // from hoisting all 3 x 2 x NT float4 of them out of the row loop (registers: 2 waves per SIMD)
         int lnoff = 0;
@@ -297,14 +297,14 @@ __global__ __launch_bounds__(kFpThreads) void mlp_pass_kernel(FpArgs a) {
                 for (int q = 0; q < kFpQ; q++)
 #pragma unroll
                     for (int n = 0; n < NT; n++) acc[q][n] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-                const int wbase = l * WB + wlane_t;
+                const int wbase = l * WB + wlane_t, wbase_x = l * WB + wlane_xt;
 #pragma unroll
                 for (int ks = 0; ks < KS; ks++) {
                     uint4 bf[kFpQ];
 #pragma unroll
                     for (int q = 0; q < kFpQ; q++) bf[q] = act_frag<NT>(act[q], ks);
                     const bool kok = 32 * ks + 8 * g < hp8;
-                    int kbase = wbase + 64 * ks;
+                    int kbase = (pr_ks_swz(h, ks) ? wbase_x : wbase) + 64 * ks;
                     asm volatile("" : "+v"(kbase));
                     // keep bits of feature tiles 2 ks, 2 ks + 1 (column groups 8 ks + g, + 4) of this
                     // block's dropout: VALU work beside the k-step's MFMAs instead of in the epilogue
