@@ -1981,6 +1981,229 @@ __global__ __launch_bounds__(g2048::wgr::kThreads) void urm_wgrad_ring_kernel(g2
     g2048::wgr::product<N, K, BI, BJ, WI>(pr, m, blockIdx.x, smem);
 }
 
+// ---------------------------------------------------------------------------------------------
+// The whole backward of LinResRMSFn (o_proj / down_proj + residual + post-norm at h = 64, K = the
+// projection's input width 64 / 120) in ONE pass (round 5).  A wave takes 32 token rows (two boards)
+// at a time:
+//   prologue  g = dout [or the board's dpool row] [+ the bf16 doutb], ds = rstd (g - out mean(g out))
+//             (urm_rms_res_bwd_kernel's formula; the mean summed 16 features per lane, then across the
+//             token's 4 lanes) -> dh fp32, and da = bf16(ds) straight into the dgrad's B fragments
+//             (registers) and the wave's da image in LDS -- da never goes to HBM
+//   dgrad     dx [rows, K] = da W on v_mfma_f32_16x16x32_bf16 with W^T staged once per block:
+//             urm_linear_kernel's wt path (its fragments, k order and 16-byte output stores), so dx
+//             is bitwise g2048_urm_linear_t of the same da
+//   wgrad     dW [64, K] += da^T x over the 32 rows: the x rows copied into the wave's LDS image,
+//             both operands read back by ds_read_b64_tr_b16 (wgrad_ring.hpp's frag: 32 rows = one
+//             k-step), accumulated in registers over all of the wave's row pairs; the block's waves
+//             added in wave order -> per-block partials [nblk][64 K] -> urm_colsum_kernel
+// Replaces urm_rms_res_bwd_kernel + urm_linear_kernel<2, CT, EPI_STORE> (wt) + urm_wgrad_ring_kernel:
+// the bf16 da write and its two reads (3 x 2 B per element) and two launches.  One wave per SIMD
+// (512 registers: the 4 x CT dW tiles stay resident); a wave has its next pair's loads in flight
+// only through the other three waves of the CU, so each wave issues a whole pair's loads at once.
+constexpr int kLrThreads = 256;
+
+template <int K>
+struct LinResBwd {
+    static constexpr int CT = (K + 15) / 16;  // dx output tiles = dW column tiles
+    static constexpr int KS = 2;              // contraction of the dgrad: 64 features, two k-steps
+    static constexpr int W_BYTES = 16 * CT * LinW<KS>::PITCH * 2;
+    static constexpr int A_BYTES = 32 * 128;            // da image: 32 rows x 64 bf16
+    static constexpr int B_BYTES = 32 * 2 * K + 16;     // x image: 32 rows x K bf16 (+ the last tile's over-read)
+    static constexpr int TP = 2 * K + 16;               // dx staging row pitch (bytes)
+    static constexpr int T_BYTES = 16 * TP;
+    static constexpr int WAVE_BYTES = (A_BYTES + B_BYTES + T_BYTES + 15) / 16 * 16;
+    static constexpr int RED_BYTES = 64 * 16 * CT * 4;  // the block's dW sum [64][16 CT] fp32
+    static constexpr int LDS = (W_BYTES + 4 * WAVE_BYTES) > RED_BYTES ? (W_BYTES + 4 * WAVE_BYTES) : RED_BYTES;
+};
+
+template <int K>
+__global__ __launch_bounds__(kLrThreads, K == 64 ? 2 : 1) void urm_linres_bwd_kernel(
+    const float *__restrict__ dout, const float *__restrict__ dpool, const uint16_t *__restrict__ doutb,
+    const float *__restrict__ out, const float *__restrict__ rstd, const uint16_t *__restrict__ w,
+    const uint16_t *__restrict__ xin, float *__restrict__ dh, uint16_t *__restrict__ dx, float *__restrict__ part,
+    int64_t rows) {
+    using C = LinResBwd<K>;
+    using LW = LinW<C::KS>;
+    constexpr int CT = C::CT;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, t = lane & 15, g = lane >> 4;
+    // W^T staged (rows q = dx feature < K, 64 k each; rows past K zero): the wt path of urm_linear_kernel
+    for (int e = tid; e < C::W_BYTES / 16; e += kLrThreads) reinterpret_cast<uint4 *>(smem)[e] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    for (int e = tid; e < K * 16; e += kLrThreads) {
+        const int q = e % K, c4 = e / K;
+        const uint16_t *src = w + (int64_t)(4 * c4) * K + q;
+        const uint32_t lo = (uint32_t)src[0] | ((uint32_t)src[K] << 16);
+        const uint32_t hi = (uint32_t)src[2 * K] | ((uint32_t)src[3 * K] << 16);
+        *reinterpret_cast<uint2 *>(smem + LW::piece(q, c4)) = make_uint2(lo, hi);
+    }
+    __syncthreads();
+    char *imgA = smem + C::W_BYTES + wave * C::WAVE_BYTES;
+    char *imgB = imgA + C::A_BYTES;
+    char *tile = imgB + C::B_BYTES;
+    int wo[C::KS];
+#pragma unroll
+    for (int s = 0; s < C::KS; s++) wo[s] = LW::frag(t, g, s);
+    f32x4 aw[4][CT];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < CT; j++) aw[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const int64_t boards = rows >> 4, pairs = (boards + 1) >> 1;
+    constexpr int NX = (4 * K + 63) / 64;  // 16-byte chunks of the pair's x rows per lane
+    for (int64_t pr = (int64_t)blockIdx.x * 4 + wave; pr < pairs; pr += (int64_t)gridDim.x * 4) {
+        const int64_t r0 = 32 * pr;
+        const int64_t nbytes = (rows - r0 < 32 ? rows - r0 : 32) * 2 * K;  // valid bytes of the pair's x rows
+        // ---- every load of the pair first: x rows, then per board g / doutb / out / rstd
+        uint4 xv[NX];
+#pragma unroll
+        for (int u = 0; u < NX; u++) {
+            const int c = lane + 64 * u;
+            xv[u] = (c < 4 * K && 16 * (int64_t)c < nbytes) ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(xin + r0 * K) + 16 * c)
+                                                          : make_uint4(0u, 0u, 0u, 0u);
+        }
+        float gv[2][16], ov[2][16], rs[2];
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+            const int64_t bd = 2 * pr + b;
+            const bool ok = bd < boards;
+            const int64_t r = ok ? 16 * bd + t : 0;
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const int64_t base = r * 64 + 32 * s + 8 * g;
+                float4 g0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), g1 = g0;
+                if (dpool) {
+                    g0 = *reinterpret_cast<const float4 *>(dpool + (r >> 4) * 64 + 32 * s + 8 * g);
+                    g1 = *reinterpret_cast<const float4 *>(dpool + (r >> 4) * 64 + 32 * s + 8 * g + 4);
+                } else if (dout) {
+                    g0 = *reinterpret_cast<const float4 *>(dout + base);
+                    g1 = *reinterpret_cast<const float4 *>(dout + base + 4);
+                }
+                float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+                if (doutb) {  // + the bf16 copy's gradient (autocast's cast backward: to fp32, then added)
+                    const uint4 wv = *reinterpret_cast<const uint4 *>(doutb + base);
+                    const uint32_t wd[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        gg[2 * i] += __uint_as_float(wd[i] << 16);
+                        gg[2 * i + 1] += __uint_as_float(wd[i] & 0xFFFF0000u);
+                    }
+                }
+                const float4 o0 = *reinterpret_cast<const float4 *>(out + base);
+                const float4 o1 = *reinterpret_cast<const float4 *>(out + base + 4);
+                const float oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    gv[b][8 * s + i] = ok ? gg[i] : 0.0f;
+                    ov[b][8 * s + i] = ok ? oo[i] : 0.0f;
+                }
+            }
+            rs[b] = ok ? rstd[r] : 0.0f;
+        }
+        // ---- x rows into the image (the wgrad's B' operand)
+#pragma unroll
+        for (int u = 0; u < NX; u++) {
+            const int c = lane + 64 * u;
+            if (c < 4 * K) *reinterpret_cast<uint4 *>(imgB + 16 * c) = xv[u];
+        }
+        // ---- prologue + dgrad per board
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+            const int64_t bd = 2 * pr + b;
+            const bool ok = bd < boards;
+            const int64_t r = 16 * bd + t;
+            float dot = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 16; i++) dot += gv[b][i] * ov[b][i];
+            const float mg = xsum32(xsum16(dot)) * (1.0f / 64.0f);
+            bf16x8 fb[2];
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                float d[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) d[i] = rs[b] * (gv[b][8 * s + i] - ov[b][8 * s + i] * mg);
+                if (ok) {
+                    float *dp = dh + r * 64 + 32 * s + 8 * g;
+                    *reinterpret_cast<float4 *>(dp) = make_float4(d[0], d[1], d[2], d[3]);
+                    *reinterpret_cast<float4 *>(dp + 4) = make_float4(d[4], d[5], d[6], d[7]);
+                }
+                const uint4 da = make_uint4(pk2bf(d[0], d[1]), pk2bf(d[2], d[3]), pk2bf(d[4], d[5]), pk2bf(d[6], d[7]));
+                fb[s] = __builtin_bit_cast(bf16x8, da);
+                *reinterpret_cast<uint4 *>(imgA + (16 * b + t) * 128 + (32 * s + 8 * g) * 2) = da;
+            }
+            if (dx) {  // dx = da W: urm_linear_kernel<2, CT, EPI_STORE>'s products and stores
+                f32x4 acc[CT];
+#pragma unroll
+                for (int ct = 0; ct < CT; ct++) {
+                    acc[ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                    for (int s = 0; s < C::KS; s++)
+                        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8 *>(smem + 16 * ct * LW::PITCH * 2 + wo[s]),
+                                                                          fb[s], acc[ct], 0, 0, 0);
+                }
+#pragma unroll
+                for (int ct = 0; ct < CT; ct++) {
+                    const int c = 16 * ct + 4 * g;
+                    if (c < K)
+                        *reinterpret_cast<uint2 *>(tile + t * C::TP + 2 * c) = make_uint2(pk2bf(acc[ct][0], acc[ct][1]), pk2bf(acc[ct][2], acc[ct][3]));
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                if (ok) {
+                    constexpr int per_row = K / 8;  // 16-byte chunks per row
+                    uint16_t *dst = dx + bd * 16 * (int64_t)K;
+                    for (int q = lane; q < 16 * per_row; q += 64) {
+                        const int row = q / per_row, c8 = q - row * per_row;
+                        *reinterpret_cast<uint4 *>(dst + row * K + 8 * c8) = *reinterpret_cast<const uint4 *>(tile + row * C::TP + 16 * c8);
+                    }
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();  // the tile is rewritten by the next board
+            }
+        }
+        // ---- dW += da^T x over the pair's 32 rows (images written by this wave only)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        {
+            g2048::wgr::bf16x8_t fx[CT];
+#pragma unroll
+            for (int j = 0; j < CT; j++) fx[j] = g2048::wgr::frag(imgB, 2 * K, 16 * j, lane);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const g2048::wgr::bf16x8_t fa = g2048::wgr::frag(imgA, 128, 16 * i, lane);
+#pragma unroll
+                for (int j = 0; j < CT; j++) aw[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fx[j], aw[i][j], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();  // the images are rewritten by the next pair
+    }
+    // ---- the block's dW: waves added in order into LDS, then the partial row [64][K]
+    __syncthreads();
+    float *red = reinterpret_cast<float *>(smem);
+    constexpr int KP = 16 * CT;
+    const int c = lane & 15, rq = (lane >> 4) * 4;
+    for (int wv = 0; wv < 4; wv++) {
+        if (wave == wv) {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < CT; j++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        float *p = red + (16 * i + rq + r) * KP + 16 * j + c;
+                        *p = wv == 0 ? aw[i][j][r] : *p + aw[i][j][r];
+                    }
+        }
+        __syncthreads();
+    }
+    float *pb = part + (int64_t)blockIdx.x * 64 * K;
+    for (int e = tid; e < 64 * K; e += kLrThreads) {
+        const int n = e / K, k = e - n * K;
+        pb[e] = red[n * KP + k];
+    }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -2546,6 +2769,42 @@ int g2048_urm_wgrad_acc(g2048_stream_t stream, const uint16_t *dy, const uint16_
 int g2048_urm_wgrad(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x, float *dw, float *partials,
                     int64_t m, int32_t n, int32_t k) {
     return g2048_urm_wgrad_acc(stream, dy, x, dw, partials, m, n, k, 0);
+}
+
+// blocks of urm_linres_bwd_kernel: up to one per CU (K = 120: 282 registers per lane, one wave per
+// SIMD) or two (K = 64: 200 registers, 50 KB of LDS)
+static int linres_bwd_blocks(int64_t rows, int k) {
+    const int64_t pairs = ((rows >> 4) + 1) >> 1;
+    const int64_t b = (pairs + 3) / 4, cap = k == 64 ? 512 : 256;
+    return (int)(b < 1 ? 1 : (b > cap ? cap : b));
+}
+
+int g2048_urm_linres_bwd_supported(int32_t hidden, int32_t k) { return hidden == 64 && (k == 64 || k == 120) ? 1 : 0; }
+
+size_t g2048_urm_linres_bwd_partials(int64_t rows, int32_t k) {
+    return rows <= 0 || (k != 64 && k != 120) ? 0 : (size_t)linres_bwd_blocks(rows, k) * 64 * (size_t)k;
+}
+
+int g2048_urm_linres_bwd(g2048_stream_t stream, const float *dout, const float *dpool, const uint16_t *doutb,
+                         const float *out, const float *rstd, const uint16_t *w, const uint16_t *x, float *dh,
+                         uint16_t *dx, float *dw, float *partials, int32_t accumulate, int64_t rows, int32_t hidden,
+                         int32_t k) {
+    if (!g2048_urm_linres_bwd_supported(hidden, k) || rows <= 0 || rows % 16) return G2048_EINVAL;
+    if (!out || !rstd || !w || !x || !dh || !dw || !partials) return G2048_EINVAL;
+    const uintptr_t al = (uintptr_t)dout | (uintptr_t)dpool | (uintptr_t)doutb | (uintptr_t)out | (uintptr_t)x |
+                         (uintptr_t)dh | (uintptr_t)dx;
+    if (al % 16 || (uintptr_t)w % 2) return G2048_EINVAL;
+    const hipStream_t s = (hipStream_t)stream;
+    const int nblk = linres_bwd_blocks(rows, k);
+    if (k == 64)
+        hipLaunchKernelGGL(urm_linres_bwd_kernel<64>, dim3(nblk), dim3(kLrThreads), LinResBwd<64>::LDS, s, dout, dpool, doutb,
+                           out, rstd, w, x, dh, dx, partials, rows);
+    else
+        hipLaunchKernelGGL(urm_linres_bwd_kernel<120>, dim3(nblk), dim3(kLrThreads), LinResBwd<120>::LDS, s, dout, dpool,
+                           doutb, out, rstd, w, x, dh, dx, partials, rows);
+    hipLaunchKernelGGL(urm_colsum_kernel, dim3((unsigned)((64 * k + 15) / 16)), dim3(256), 0, s, partials, nblk, 64 * k,
+                       dw, accumulate ? 1 : 0);
+    return launch_status();
 }
 
 int g2048_urm_residual_rms(g2048_stream_t stream, float *x, const uint16_t *y, const float *emb, uint16_t *xb,

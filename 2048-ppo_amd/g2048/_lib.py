@@ -45,7 +45,7 @@ EXPORTED = (
     # include/g2048_urm.h
     "g2048_urm_stem", "g2048_urm_attention", "g2048_urm_residual_rms", "g2048_urm_swiglu_conv",
     "g2048_urm_pool_heads", "g2048_urm_linear_supported", "g2048_urm_linear", "g2048_urm_linear_rms",
-    "g2048_urm_linear_swiglu", "g2048_urm_linear_swiglu_train", "g2048_urm_linear_t", "g2048_urm_gate_up_swiglu_bwd_supported", "g2048_urm_gate_up_swiglu_bwd", "g2048_urm_gate_up_swiglu_bwd_acc", "g2048_urm_linear_res_rms", "g2048_urm_linear_bias", "g2048_urm_wgrad_supported", "g2048_urm_wgrad_partials", "g2048_urm_wgrad", "g2048_urm_wgrad_acc", "g2048_urm_head_loss_partials", "g2048_urm_head_loss", "g2048_urm_head_loss_bwd", "g2048_urm_kl_stats", "g2048_urm_forward_supported", "g2048_urm_forward",
+    "g2048_urm_linear_swiglu", "g2048_urm_linear_swiglu_train", "g2048_urm_linear_t", "g2048_urm_gate_up_swiglu_bwd_supported", "g2048_urm_gate_up_swiglu_bwd", "g2048_urm_gate_up_swiglu_bwd_acc", "g2048_urm_linear_res_rms", "g2048_urm_linear_bias", "g2048_urm_wgrad_supported", "g2048_urm_wgrad_partials", "g2048_urm_wgrad", "g2048_urm_wgrad_acc", "g2048_urm_linres_bwd_supported", "g2048_urm_linres_bwd_partials", "g2048_urm_linres_bwd", "g2048_urm_head_loss_partials", "g2048_urm_head_loss", "g2048_urm_head_loss_bwd", "g2048_urm_kl_stats", "g2048_urm_forward_supported", "g2048_urm_forward",
 )
 
 
@@ -290,6 +290,9 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_urm_wgrad_partials": (sz, [i64, i32, i32]),
         "g2048_urm_wgrad": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32]),
         "g2048_urm_wgrad_acc": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32, i32]),
+        "g2048_urm_linres_bwd_supported": (ctypes.c_int, [i32, i32]),
+        "g2048_urm_linres_bwd_partials": (sz, [i64, i32]),
+        "g2048_urm_linres_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, i32]),
         "g2048_urm_head_loss_partials": (sz, [i64, i32]),
         "g2048_urm_head_loss": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, i64, i32, bp, vp, ctypes.c_float,
                                                ctypes.c_float, vp, vp, vp, vp, vp, vp]),
@@ -1323,6 +1326,31 @@ def urm_wgrad(dy, x, dw, partials, accumulate: bool = False):
     _check(load().g2048_urm_wgrad_acc(_stream(dy), _dev(dy, torch.bfloat16, "dy"), _dev(x, torch.bfloat16, "x"),
                                       _dev(dw, torch.float32, "dw"), _dev(partials, torch.float32, "partials"), m, n,
                                       x.shape[1], int(bool(accumulate))), "g2048_urm_wgrad_acc")
+
+
+def urm_linres_bwd_supported(hidden: int, k: int) -> bool:
+    return bool(load().g2048_urm_linres_bwd_supported(hidden, k))
+
+
+def urm_linres_bwd_partials(rows: int, k: int) -> int:
+    return int(load().g2048_urm_linres_bwd_partials(rows, k))
+
+
+def urm_linres_bwd(out, rstd, w, x, dh, dw, partials, dout=None, dpool=None, doutb=None, dx=None,
+                   accumulate: bool = False):
+    """The residual-RMSNorm projection's backward in one pass (g2048_urm_linres_bwd): dh fp32 [rows, 64],
+    dx bf16 [rows, k] (None: skipped), dw fp32 [64, k] (+= with accumulate) from dout fp32 [rows, 64] /
+    dpool fp32 [rows / 16, 64] / doutb bf16 [rows, 64] (each may be None), out fp32, rstd fp32 [rows],
+    w bf16 [64, k], x bf16 [rows, k]."""
+    rows, hid = out.shape
+    k = x.shape[1]
+    _check(load().g2048_urm_linres_bwd(_stream(out), _dev(dout, torch.float32, "dout"), _dev(dpool, torch.float32, "dpool"),
+                                       _dev(doutb, torch.bfloat16, "doutb"), _dev(out, torch.float32, "out"),
+                                       _dev(rstd, torch.float32, "rstd"), _dev(w, torch.bfloat16, "w"),
+                                       _dev(x, torch.bfloat16, "x"), _dev(dh, torch.float32, "dh"),
+                                       _dev(dx, torch.bfloat16, "dx"), _dev(dw, torch.float32, "dw"),
+                                       _dev(partials, torch.float32, "partials"), int(bool(accumulate)), rows, hid, k),
+           "g2048_urm_linres_bwd")
 
 
 def urm_linear_swiglu_train(inp, w, conv_w, conv_b, gu, act):

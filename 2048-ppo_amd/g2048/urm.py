@@ -802,10 +802,13 @@ class LinResRMSFn(torch.autograd.Function):
     """o_proj / down_proj + residual + post-norm of GameURMBlock (game.py:1346-1350: h = rms_norm(h +
     proj(x))) under bf16 autocast in ONE forward kernel (g2048_urm_linear_res_rms: the projection on
     MFMA, its autocast bf16 output added to h in the epilogue, RMSNorm, fp32 out + bf16 copy + rstd):
-    the projection output's HBM round trip of URMLinearFn + ResidualRMSFn is gone.  Backward =
-    ResidualRMSFn's kernel (dh fp32, da bf16) then URMLinearFn's (dX on the projection kernel, dW on
-    g2048_urm_wgrad).  h fp32 [..., n], x [..., k] (bf16, or cast like autocast), w [n, k] -> out fp32
+    the projection output's HBM round trip of URMLinearFn + ResidualRMSFn is gone.  Backward (round 5,
+    h 64, k 64 / 120): ONE pass, g2048_urm_linres_bwd (dh fp32, and from the bf16 da held on chip dX
+    on MFMA and dW accumulated per block); otherwise ResidualRMSFn's kernel (dh fp32, da bf16) then
+    URMLinearFn's (dX on the projection kernel, dW on g2048_urm_wgrad).  h fp32 [..., n], x [..., k] (bf16, or cast like autocast), w [n, k] -> out fp32
     (and its bf16 copy with with_bf16)."""
+
+    fused_bwd = True  # False: the round-4 three-launch backward (tests compare the two)
 
     @staticmethod
     def forward(ctx, h: torch.Tensor, x: torch.Tensor, w: torch.Tensor, eps: float, with_bf16: bool = False):
@@ -831,10 +834,22 @@ class LinResRMSFn(torch.autograd.Function):
         if dout is None and doutb is None:
             return None, None, None, None, None
         dh = torch.empty_like(out)
-        da = torch.empty(out.shape, dtype=torch.bfloat16, device=out.device)
         dpool = _pooled_grad(dout, ctx.shape)  # the mean-pool's broadcast gradient, read as [b, h]
         d32 = None if dout is None or dpool is not None else dout.reshape(out.shape).float().contiguous()
         db16 = None if doutb is None else doutb.reshape(out.shape).to(torch.bfloat16).contiguous()
+        n, k = wb.shape
+        rows = out.shape[0]
+        if LinResRMSFn.fused_bwd and ctx.needs_input_grad[2] and rows % 16 == 0 and L.urm_linres_bwd_supported(n, k):
+            # round 5: one pass (g2048_urm_linres_bwd) -- the bf16 da never round-trips through HBM
+            dx = torch.empty(rows, k, dtype=torch.bfloat16, device=out.device) if ctx.needs_input_grad[1] else None
+            sink = _grad_sink(ctx.wt, (n, k))
+            dwt = sink if sink is not None else torch.empty(n, k, dtype=torch.float32, device=out.device)
+            part = torch.empty(L.urm_linres_bwd_partials(rows, k), dtype=torch.float32, device=out.device)
+            L.urm_linres_bwd(out, rstd, wb, xb, dh, dwt, part, dout=d32, dpool=dpool, doutb=db16, dx=dx,
+                             accumulate=sink is not None)
+            dw = None if sink is not None else dwt.to(ctx.dtypes[1])
+            return (dh.view(ctx.shape), None if dx is None else dx.to(ctx.dtypes[0]).view(ctx.xshape), dw, None, None)
+        da = torch.empty(out.shape, dtype=torch.bfloat16, device=out.device)
         L.urm_rms_res_bwd(d32, out, rstd, dh, da, db16, dpool=dpool)
         dx = _gemm_t(da, wb) if ctx.needs_input_grad[1] else None
         dw = _wgrad_into(da, xb, ctx.wt, ctx.dtypes[1]) if ctx.needs_input_grad[2] else None

@@ -171,6 +171,25 @@ int g2048_urm_wgrad(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x
 int g2048_urm_wgrad_acc(g2048_stream_t stream, const uint16_t *dy, const uint16_t *x, float *dw, float *partials,
                         int64_t m, int32_t n, int32_t k, int32_t accumulate);
 
+/* The whole backward of the residual-RMSNorm projection out = rms_norm(h + bf16(x W^T)) (o_proj /
+ * down_proj of GameURMBlock, game.py:1346-1350; LinResRMSFn) in one pass (round 5), for hidden 64
+ * and input width k 64 / 120 (g2048_urm_linres_bwd_supported):
+ *   g  = dout [or dpool broadcast over each board's 16 rows] [+ doutb as fp32]   (any may be NULL)
+ *   dh = rstd (g - out mean(g out))                  fp32 [rows, 64]  (the residual's gradient)
+ *   dx = bf16(dh) W                                  bf16 [rows, k]   (NULL: not computed)
+ *   dw = bf16(dh)^T x   (accumulate: dw += ...)      fp32 [64, k]
+ * out fp32 [rows, 64] and rstd [rows] as the forward wrote them, w bf16 [64, k], x bf16 [rows, k];
+ * rows % 16 == 0; every row pointer 16-byte aligned; partials: g2048_urm_linres_bwd_partials(rows, k)
+ * floats of scratch.  = g2048_urm_rms_res_bwd2 + g2048_urm_linear_t + g2048_urm_wgrad_acc without
+ * the bf16 dh round trip through HBM (dx bitwise g2048_urm_linear_t of the same bf16 dh; dh and dw
+ * within fp32 rounding of them: the row mean and the row sum are added in another order). */
+int g2048_urm_linres_bwd_supported(int32_t hidden, int32_t k);
+size_t g2048_urm_linres_bwd_partials(int64_t rows, int32_t k);
+int g2048_urm_linres_bwd(g2048_stream_t stream, const float *dout, const float *dpool, const uint16_t *doutb,
+                         const float *out, const float *rstd, const uint16_t *w, const uint16_t *x, float *dh,
+                         uint16_t *dx, float *dw, float *partials, int32_t accumulate, int64_t rows, int32_t hidden,
+                         int32_t k);
+
 /* Post-norm residual (game.py:1346, 1350 with rms_norm :1223-1229):
  *   x = x + y;  x = x * rsqrt(mean(x^2) + eps)  [+ emb, the next loop's input, game.py:1447];
  *   xb = bf16(x).

@@ -1264,7 +1264,7 @@ def test_urm_ppo_updater_matches_generic_updater(dev):
     PPOUpdater (torch loss + autograd) from the same weights on the same minibatches (torch-op
     MuonAdamW for both, dropout 0): the update directions agree (cosine >= 0.999 per 2-D weight, norm
     within 2 %; 1-D parameters within 2e-3 of their step) and the statistics within 1e-3 relative
-    (kl_max 2e-2) --
+    (the KL statistics: kl_total / kl_average 1e-2, kl_max 5e-2, see below) --
     what is left is the heads' dot-product order and the kernels' summation orders, amplified by
     Muon's bf16 Newton-Schulz."""
     import math
@@ -1301,8 +1301,17 @@ def test_urm_ppo_updater_matches_generic_updater(dev):
             assert math.isclose(float(a.norm()), float(b.norm()), rel_tol=0.02), k
         else:
             assert float((a - b).abs().max()) <= 2e-3 * float(b.abs().max()) + 1e-9, k
-    for k in s0:  # (kl_max: the largest single-row KL, the most order-sensitive entry -- measured 0.9 %)
-        assert math.isclose(s0[k], s1[k], rel_tol=2e-2 if k == "kl_max" else 1e-3, abs_tol=1e-6), (k, s0[k], s1[k])
+    # the KL statistics measure the update itself, and Muon's orthogonalisation (U V^T of the
+    # gradient) amplifies rounding in the gradient's weak singular directions: with the one-pass
+    # residual-RMSNorm backward in both updaters (round 5) the gradients agree with the three-launch
+    # ones at cosine >= 0.9999998 while the weakest matrix's update turns to cosine 0.963
+    # (tools/urm_grad_fused_check.py, tools/urm_stats_spread.py) -- so the KL statistics of two
+    # updaters that differ only in the heads' / loss kernels' summation orders carry that noise:
+    # measured kl_total / kl_average 0.33 %, kl_max 2.5 % (0.06 / 0.9 % with the three-launch
+    # backward); the first-order statistics stay within 1e-3
+    for k in s0:
+        tol = 5e-2 if k == "kl_max" else 1e-2 if k.startswith("kl") else 1e-3
+        assert math.isclose(s0[k], s1[k], rel_tol=tol, abs_tol=1e-6), (k, s0[k], s1[k])
 
 
 @pytest.mark.parametrize("n,heads,p", [(4099, 4, 0.0), (1000, 4, 0.1), (333, 2, 0.2)])
@@ -1341,3 +1350,63 @@ def test_urm_attention_board_kernels_are_bitwise_the_head_kernels(dev, n, heads,
         res.append((out_t.clone(), dq.clone()))
     assert torch.equal(res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("k,n", [(64, 65536), (120, 65536), (64, 37), (120, 1001)])
+@pytest.mark.parametrize("grad_src", ["dout", "dout+bf16", "bf16", "pool"])
+def test_urm_linres_fused_backward(dev, k, n, grad_src):
+    """LinResRMSFn's one-pass backward (g2048_urm_linres_bwd: residual-RMSNorm backward, dX and dW from
+    the bf16 da held on chip) vs its three-launch backward (g2048_urm_rms_res_bwd2, g2048_urm_linear_t,
+    g2048_urm_wgrad) on the same forward: dh within fp32 rounding (the row mean summed in another
+    order, <= 1e-5 of the largest component); dx BITWISE the projection kernel's dx of the fused
+    path's own bf16(dh) (same fragments, same k order); dW within fp32 summation order of the
+    unfused weight-gradient kernel on that bf16(dh); and fused vs three-launch dx / dW at cosine
+    >= 0.99999 with max error <= one bf16 step (2^-7) of the largest component (da can flip a
+    rounding).  Gradient sources: fp32 dout, fp32 + the bf16 copy's gradient, the bf16 one alone, and
+    the mean-pool's broadcast [b, 64] gradient (odd board counts: the kernel's ragged row pair)."""
+    from g2048 import _lib as L
+    from g2048.urm import LinResRMSFn, MeanPoolFn
+    torch.manual_seed(k + 7 * n)
+    h0 = torch.randn(n, 16, 64, device=dev)
+    x0 = torch.randn(n, 16, k, device=dev).bfloat16()
+    w = torch.nn.Parameter(torch.randn(64, k, device=dev) * k ** -0.5)
+    g1 = torch.randn(n, 16, 64, device=dev)
+    g2 = torch.randn(n, 16, 64, device=dev)
+    gp = torch.randn(n, 64, device=dev)
+    want_b = grad_src in ("dout+bf16", "bf16")
+    res = []
+    for fused in (True, False):
+        LinResRMSFn.fused_bwd = fused
+        try:
+            w.grad = None
+            h = h0.clone().requires_grad_(True)
+            x = x0.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                r = LinResRMSFn.apply(h, x, w, 1e-6, want_b)
+            out, outb = r if want_b else (r, None)
+            if grad_src == "pool":
+                loss = (MeanPoolFn.apply(out) * gp).sum()
+            else:
+                loss = (outb.float() * g2).sum() if want_b else 0.0
+                if grad_src != "bf16":
+                    loss = loss + (out * g1).sum()
+            loss.backward()
+            res.append((h.grad.clone(), x.grad.float().clone(), w.grad.clone()))
+        finally:
+            LinResRMSFn.fused_bwd = True
+    (dh1, dx1, dw1), (dh2, dx2, dw2) = res
+    assert float((dh1 - dh2).abs().max()) <= 1e-5 * float(dh2.abs().max())
+    # the fused pass's own products, recomputed from the dh it wrote
+    da = dh1.reshape(-1, 64).to(torch.bfloat16).contiguous()
+    wb = w.detach().to(torch.bfloat16).contiguous()
+    dx_ref = torch.empty(16 * n, k, dtype=torch.bfloat16, device=dev)
+    L.urm_linear_t(da, wb, dx_ref)
+    assert torch.equal(dx1.reshape(-1, k).bfloat16(), dx_ref)
+    dw_ref = torch.empty(64, k, dtype=torch.float32, device=dev)
+    part = torch.empty(L.urm_wgrad_partials(16 * n, 64, k), dtype=torch.float32, device=dev)
+    L.urm_wgrad(da, x0.reshape(-1, k).contiguous(), dw_ref, part)
+    assert float((dw1 - dw_ref).abs().max()) <= 1e-5 * float(dw_ref.abs().max())
+    for a, b in ((dx1, dx2), (dw1, dw2)):
+        a, b = a.reshape(-1).float(), b.reshape(-1).float()
+        assert float(torch.nn.functional.cosine_similarity(a, b, dim=0)) >= 0.99999
+        assert float((a - b).abs().max()) <= 2 ** -7 * float(b.abs().max())
