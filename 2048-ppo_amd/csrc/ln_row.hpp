@@ -33,6 +33,9 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 #endif
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+#ifndef LN_PERM
+#define LN_PERM 1
+#endif
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 constexpr float kEps = 1e-5f;  // nn.LayerNorm default
@@ -64,8 +67,15 @@ __device__ __forceinline__ void round_g(const f32x4 (&acc)[NT], f32x2 (&v)[NT][2
     for (int n = 0; n < NT; n++) {
         const uint32_t w0 = pack_bf2(acc[n][0], acc[n][1]), w1 = pack_bf2(acc[n][2], acc[n][3]);
         gbits[n] = make_uint2(w0, w1);
+#if LN_PERM
+        // the halves by v_perm (zero bytes below): the compiler cannot fold these back into
+        // single conversions + shift + mask, as it does with bf_lo / bf_hi of a fresh pack
+        v[n][0] = f32x2{__uint_as_float(__builtin_amdgcn_perm(w0, 0u, 0x05040C0Cu)), __uint_as_float(__builtin_amdgcn_perm(w0, 0u, 0x07060C0Cu))};
+        v[n][1] = f32x2{__uint_as_float(__builtin_amdgcn_perm(w1, 0u, 0x05040C0Cu)), __uint_as_float(__builtin_amdgcn_perm(w1, 0u, 0x07060C0Cu))};
+#else
         v[n][0] = f32x2{bf_lo(w0), bf_hi(w0)};
         v[n][1] = f32x2{bf_lo(w1), bf_hi(w1)};
+#endif
     }
 }
 

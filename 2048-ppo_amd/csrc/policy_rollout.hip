@@ -203,8 +203,10 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
             // k past 48 (ks 1, lane groups 2, 3) read out of range = zero, no per-lane branch / zeroing
             const __amdgpu_buffer_rsrc_t w0r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(a.w0), 0, h * 96, 0x00020000);
             const int w0off[2] = {glane_t, g < 2 ? glane_t + 64 : h * 96};
-            const char *hdb = reinterpret_cast<const char *>(a.head) + hlane_t;
-            const char *hvb = reinterpret_cast<const char *>(a.head) + (4 * KP + 8 * g) * 2;
+            // the head rows through a buffer descriptor: a lane whose board tile is not the chain's
+            // reads out of range (zero) -- one select per tile instead of 8 per k-step
+            const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(a.head), 0, 5 * KP * 2, 0x00020000);
+            const int hvlane = (4 * KP + 8 * g) * 2;
             // The MLP runs on two board tiles at a time (accumulators of 2 x NT tiles; the weight
             // fragments are read once per pair): stem, blocks and the pair's share of the head
             // chains.  A pair's epilogue overwrites its own layer input (the residual) in place.
@@ -304,15 +306,15 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
 #pragma unroll
                 for (int q = 0; q < kQ; q++) {
                     const int bt = kQ * pr + q;
+                    constexpr int kOut = 1 << 30;  // past the 5 head rows
+                    const int offl = (col >> 2) == bt ? hlane_t : kOut, offv = col == 4 * bt ? hvlane : kOut;
 #pragma unroll
                     for (int ks = 0; ks < KS; ks++) {
                         const uint4 bf = act_frag<NT>(act[q], ks);
-                        const uint4 hl = *reinterpret_cast<const uint4 *>(hdb + 64 * ks);
-                        const uint4 hv = *reinterpret_cast<const uint4 *>(hvb + 64 * ks);
-                        const bool mine_l = (col >> 2) == bt, mine_v = col == 4 * bt;
-                        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-                        accL = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(mine_l ? hl : z), as_frag(bf), accL, 0, 0, 0);
-                        accV = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(mine_v ? hv : z), as_frag(bf), accV, 0, 0, 0);
+                        const uint4 hl = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(hr, offl + 64 * ks, 0, 0));
+                        const uint4 hv = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(hr, offv + 64 * ks, 0, 0));
+                        accL = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(hl), as_frag(bf), accL, 0, 0, 0);
+                        accV = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(hv), as_frag(bf), accV, 0, 0, 0);
                     }
                 }
             }
