@@ -177,6 +177,28 @@ __device__ __forceinline__ void ln_epilogue(f32x4_t (&acc)[NT], uint2 (&act)[NT]
     }
 }
 
+// A layer output row in the lane layout (lane (g, c): features 16 n + 4 g .. + 3 of row c as v[n])
+// written with 16-byte stores: tiles n, n + 1 (n even) paired by one v_permlane16_swap per dword
+// between the lane rows g, g ^ 1 -- lane g even then holds features 16 n + 4 g .. + 7, lane g odd
+// 16 (n + 1) + 4 (g - 1) .. + 7 (urm.hip EPI_SWIGLU_T's pairing); an odd last tile keeps 8-byte
+// stores.  Round 5: half the store instructions of the train pass's G / H rows (its stores were a
+// third of its time: time_fused 71.7 -> 50.4 us with none).  p = the row's first byte.
+template <int NT, int h>
+__device__ __forceinline__ void store_row16(char *p, const uint2 (&v)[NT], int g) {
+    static_assert(16 * (NT - (NT & 1)) <= h, "paired tiles lie inside the row");
+    const int cb = (g & 1) ? 16 + 4 * (g - 1) : 4 * g;
+#pragma unroll
+    for (int n = 0; n + 1 < NT; n += 2) {
+        const auto sx = __builtin_amdgcn_permlane16_swap(v[n].x, v[n + 1].x, false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(v[n].y, v[n + 1].y, false, false);
+        *reinterpret_cast<uint4 *>(p + 2 * (16 * n + cb)) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+    }
+    if constexpr ((NT & 1) != 0) {
+        const int f = 16 * (NT - 1) + 4 * g;
+        if (f < h) *reinterpret_cast<uint2 *>(p + 2 * f) = v[NT - 1];
+    }
+}
+
 // The training epilogue: ln_epilogue with nn.Dropout in train mode (the keep mask of row `row`
 // drawn exactly as mlp_fwd_wide_kernel draws it: one Philox call per feature-tile pair n, n + 1)
 // between the ReLU and the residual add, the pre-norm G bits stored and the row statistics
@@ -238,12 +260,7 @@ __device__ __forceinline__ void ln_epilogue_train_kb(f32x4_t (&acc)[NT], uint2 (
     {
         uint2 gb[NT];
         R::round_g<NT>(acc, v, gb);
-        if (gout) {
-            char *p = reinterpret_cast<char *>(gout) + (goff + 8u * (uint32_t)g);
-#pragma unroll
-            for (int n = 0; n < NT; n++)
-                if (16 * n + 4 * g < h) *reinterpret_cast<uint2 *>(p + 32 * n) = gb[n];
-        }
+        if (gout) store_row16<NT, h>(reinterpret_cast<char *>(gout) + goff, gb, g);
     }
     auto valid = [&](int n) { return 16 * n + 4 * g < h; };
     R::stats<NT>(v, valid, inv_n, mean, rstd);

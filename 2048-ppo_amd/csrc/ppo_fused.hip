@@ -276,7 +276,7 @@ __global__ __launch_bounds__(kFpThreads) void mlp_pass_kernel(FpArgs a) {
         ln_epilogue_train_kb<NT, H, RES_, DROP_>(acc[Q_], act[Q_], lnp, lnp + 16 * NT, g, inv_n, d1.scale, kb[Q_],   \
                                                  st ? a.g[L_] : nullptr, row * (2u * H), mean, rstd);            \
         if (st) {                                                                                               \
-            if (a.h[L_]) store_tile<NT, H>(a.h[L_], row * (2u * H), act[Q_], g);                                \
+            if (a.h[L_]) store_row16<NT, H>(reinterpret_cast<char *>(a.h[L_]) + row * (2u * H), act[Q_], g);     \
             if (g == 0 && a.mean[L_]) {                                                                         \
                 a.mean[L_][row] = mean;                                                                         \
                 a.rstd[L_][row] = rstd;                                                                         \
@@ -506,6 +506,9 @@ __device__ __forceinline__ float row16_scatter8(const float (&v)[8], int c) {
     return h1 + __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(h1), 0xB1, 0xF, 0xF, false));
 }
 
+#ifndef BP_STORE8  // 1: dG as 8-byte pieces per tile (round 4); 0: paired 16-byte stores
+#define BP_STORE8 0
+#endif
 #ifndef BP_PK  // 1: the backward's LayerNorm pairs as packed fp32 (v_pk_*: few MFMAs beside them here)
 #define BP_PK 1
 #endif
@@ -594,8 +597,13 @@ __device__ __forceinline__ void bp_layer(const uint16_t *__restrict__ gsrc, floa
         const bp2 o0 = bp_fma(xh0, nm2, bp_fma(dzr[n][0], bp2{gm.x, gm.y}, nm1)) * rs2;
         const bp2 o1 = bp_fma(xh1, nm2, bp_fma(dzr[n][1], bp2{gm.z, gm.w}, nm1)) * rs2;
         dgb[n] = valid(n) ? make_uint2(R::pack_bf2(o0.x, o0.y), R::pack_bf2(o1.x, o1.y)) : make_uint2(0u, 0u);
+#if BP_STORE8
         if (live && valid(n)) *reinterpret_cast<uint2 *>(dgout + f0) = dgb[n];
+#endif
     }
+#if !BP_STORE8
+    if (live) store_row16<NT, H>(reinterpret_cast<char *>(dgout), dgb, gq);  // 16-byte stores (mlp_tile.hpp)
+#endif
 }
 
 // P^T tile chain of one block layer: p[n] = bf16(sum_ks W^T[16 n ..][k-step ks] dG^T) -- the
