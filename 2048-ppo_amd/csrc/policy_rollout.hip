@@ -42,16 +42,25 @@ namespace {
 
 using namespace g2048::tile;
 
-constexpr int kPrThreads = 256;
+#ifndef PR_BPW
+#define PR_BPW 32
+#endif
+// Round 5: 32 boards per wave, i.e. two waves per SIMD at 256 VGPRs each with one 16-board tile per
+// MLP pass (kQ = 1).  The env step and the sampler then run on half-empty waves, but a partner wave's
+// MFMAs cover each wave's LN epilogues and LDS waits: 31.4 -> 29.3 us per step at 65 536 envs
+// (kQ = 1 at 64 boards per wave, one wave per SIMD, measured 37 us; kQ = 2 at 32 spills 376 B).
+constexpr int kBpw = PR_BPW;               // boards per wave (64: one wave per SIMD; 32: two)
+constexpr int kPrBoards = 256;             // boards per workgroup (one per CU: the LDS weight images)
+constexpr int kPrThreads = kPrBoards / kBpw * 64;
 constexpr int kPrLdsMax = 163840;
 constexpr int kPrRecBytes = 4 * 80;  // the stem fragment recipes of the 4 lane groups (LDS, after the zero fragment)
 #ifndef PR_TILES
-#define PR_TILES 2
+#define PR_TILES 1
 #endif
-constexpr int kQ = PR_TILES;
+constexpr int kQ = PR_TILES;  // board tiles (of 16 boards) per MLP pass: accumulators of kQ x NT tiles
 #ifndef PR_NSPLIT
 #define PR_NSPLIT 0
-#endif  // board tiles (of 16 boards) per MLP pass: accumulators of kQ x NT tiles
+#endif
 
 struct PrArgs {
     uint4 *boards;      // [T+1][n][16] int8: row t0 read, rows t0+1 .. t1 written
@@ -187,10 +196,10 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
     const int zoff = (int)(sZero - smem);
     constexpr int last_rows = h - 16 * (NT - 1);  // valid rows of the last tile
 
-    for (int64_t base = (int64_t)blockIdx.x * kPrThreads; base < a.n; base += (int64_t)gridDim.x * kPrThreads) {
-        if (base + 64 * wave >= a.n) continue;  // an empty wave (no barrier below)
-        const int64_t i = base + 64 * wave + lane;
-        const bool live = i < a.n;
+    for (int64_t base = (int64_t)blockIdx.x * kPrBoards; base < a.n; base += (int64_t)gridDim.x * kPrBoards) {
+        if (base + kBpw * wave >= a.n) continue;  // an empty wave (no barrier below)
+        const int64_t i = base + kBpw * wave + lane;
+        const bool live = lane < kBpw && i < a.n;  // (kBpw 32: lanes 32..63 carry no board)
         uint4 b = live ? a.boards[(int64_t)a.t0 * a.n + i] : make_uint4(0u, 0u, 0u, 0u);
         uint32_t legal = live ? (uint32_t)(a.flags[(int64_t)a.t0 * a.n + i] & 0xFu) : 0u;
 
@@ -212,7 +221,7 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
             // chains.  A pair's epilogue overwrites its own layer input (the residual) in place.
             f32x4_t accL = {0.0f, 0.0f, 0.0f, 0.0f}, accV = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll 1
-            for (int pr = 0; pr < 4 / kQ; pr++) {
+            for (int pr = 0; pr < kBpw / 16 / kQ; pr++) {
                 uint2 act[kQ][NT];
                 // ---------------- stem: obs fragments (to_model_format, natural k order) ------
                 uint4 xs[kQ][2];
@@ -264,7 +273,7 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
 #pragma unroll
                 for (int q = 0; q < kQ; q++) ln_epilogue<NT, H, false>(acc[q], act[q], sLNr, sLNr + 16 * NT, g, inv_n);
                 if (a.debug && t == a.t0)
-                    for (int q = 0; q < kQ; q++) debug_act<NT>(a, 0, base + 64 * wave + 16 * (kQ * pr + q) + col, act[q], g);
+                    for (int q = 0; q < kQ; q++) debug_act<NT>(a, 0, base + kBpw * wave + 16 * (kQ * pr + q) + col, act[q], g);
 
                 // ---------------- residual blocks ---------------------------------------------
 #pragma unroll
@@ -300,7 +309,7 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
                     for (int q = 0; q < kQ; q++) ln_epilogue<NT, H, true>(acc[q], act[q], lnp, lnp + 16 * NT, g, inv_n);
                     if (a.debug && t == a.t0)
                         for (int q = 0; q < kQ; q++)
-                            debug_act<NT>(a, l + 1, base + 64 * wave + 16 * (kQ * pr + q) + col, act[q], g);
+                            debug_act<NT>(a, l + 1, base + kBpw * wave + 16 * (kQ * pr + q) + col, act[q], g);
                 }
                 // ---------------- heads: logits of board 16 g + col land in lane (g, col) -------
 #pragma unroll
@@ -411,7 +420,7 @@ int g2048_policy_rollout(g2048_stream_t stream, const g2048_policy_rollout_args 
     a.debug = p->debug;
     const int nt = (h + 15) / 16;
     const size_t lds = g2048_policy_rollout_lds_bytes(h);
-    const int64_t groups = (p->n + kPrThreads - 1) / kPrThreads;
+    const int64_t groups = (p->n + kPrBoards - 1) / kPrBoards;
     const unsigned grid = (unsigned)(groups < 256 ? groups : 256);
     hipStream_t s = (hipStream_t)stream;
     (void)nt;
