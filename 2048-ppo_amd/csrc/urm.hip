@@ -788,12 +788,22 @@ int dispatch_lin(hipStream_t s, int epi, const uint16_t *in, const uint16_t *w, 
 // (16-byte fragment reads); wave-local s_waitcnt + wave barrier order the lanes' LDS accesses.
 namespace mk {
 constexpr int H = 64, QKV = 192, INTER = 120, GU = 256, KD = 128;
-// Weight rows padded to 36 / 68 dwords.  (Round 5 measured the alternative: unpadded rows with their
+// Weight rows padded to 40 / 72 dwords = 10 / 18 16-byte units.  Round 5: a unit pitch of 2 x odd
+// puts the 16 lanes of every ds_read_b128 lane group (rows {0-3, 12-15} of one column unit with rows
+// 4-11 of the next, MI355X_MICROARCH.md's LDS table) on 16 distinct units, where round 4's 9 / 17
+// units met two by two (SQ_LDS_BANK_CONFLICT 2.8 -> 1.0 cycles per LDS instruction, 2.31 -> 2.26 ms
+// in tools/time_urm.py, profiles/r05al).  (Round 5 also measured the alternative: unpadded rows with their
 // 16-byte chunks XOR-swizzled by the row, conflict-free fragment reads in every ds_read_b128 lane
 // group by the bank model -- the forward got SLOWER, 2.23 -> 2.36 ms per 65 536 boards: the LDS
 // conflicts are not what bounds it at two waves per SIMD, the extra addressing registers spilled.)
-constexpr int P64 = H + 8;     // bf16 pitch of K = 64 weight rows
-constexpr int PD = KD + 8;     // bf16 pitch of the down-proj rows
+#ifndef G2048_URM_WPAD
+#define G2048_URM_WPAD 16
+#endif
+#ifndef G2048_URM_TPAD
+#define G2048_URM_TPAD 8
+#endif
+constexpr int P64 = H + G2048_URM_WPAD;     // bf16 pitch of K = 64 weight rows
+constexpr int PD = KD + G2048_URM_WPAD;     // bf16 pitch of the down-proj rows
 constexpr int OFF_QKV = 0;
 constexpr int OFF_O = OFF_QKV + QKV * P64 * 2;
 constexpr int OFF_GU = OFF_O + H * P64 * 2;
@@ -801,7 +811,7 @@ constexpr int OFF_D = OFF_GU + GU * P64 * 2;
 constexpr int OFF_CW = OFF_D + H * PD * 2;       // conv taps fp32 [128][2]
 constexpr int OFF_CB = OFF_CW + KD * 2 * 4;      // conv bias fp32 [128]
 constexpr int W_BYTES = OFF_CB + KD * 4;         // 92 672
-constexpr int TP = QKV + 8;                      // bf16 pitch of a wave's tile (100 dwords)
+constexpr int TP = QKV + G2048_URM_TPAD;         // bf16 pitch of a wave's tile (100 dwords)
 constexpr int TILE_BYTES = 16 * TP * 2;          // 6 400
 constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
@@ -810,6 +820,7 @@ constexpr int THREADS = 64 * WAVES;
 constexpr int PS_STEM = 0, PS_LNW = PS_STEM + 3 * H, PS_LNB = PS_LNW + H, PS_INIT = PS_LNB + H,
               PS_WA = PS_INIT + 16 * H, PS_WV = PS_WA + 4 * H, PS_BA = PS_WV + H, PS_BV = PS_BA + 4,
               PS_ALL = PS_BV + 4;
+static_assert(W_BYTES + WAVES * TILE_BYTES + PS_ALL * 4 <= 163840, "one workgroup's LDS");
 #ifndef G2048_URM_NB
 #define G2048_URM_NB 2
 #endif
@@ -833,14 +844,24 @@ __device__ __forceinline__ void wave_lds_sync() {
 // 16 B (8 bf16) from LDS
 __device__ __forceinline__ bf16x8 lds16(const char *p) { return *reinterpret_cast<const bf16x8 *>(p); }
 
-// acc-layout values (4 per tile) -> bf16 in the tile at [t][16 ct + 4 g]
+// acc-layout values (4 per tile) -> bf16 in the tile at [t][16 ct + 4 g].  Round 5: 16-byte stores,
+// tiles ct, ct + 1 paired by one v_permlane16_swap per dword between the lane rows g, g ^ 1 (lane g
+// even then holds columns 16 ct + 4 g .. + 7, lane g odd 16 (ct + 1) + 4 (g - 1) .. + 7; mlp_tile.hpp
+// store_row16): half the store instructions, and the 8 lanes of a ds_write_b128 group (8 rows, one
+// column unit) fall on distinct banks at the 100-dword tile pitch, where the 16 same-column lanes
+// of a ds_write_b64 group met two by two (the forward's LDS conflict cycles 1.0 -> 0.4 per LDS
+// instruction)
 template <int CT>
 __device__ __forceinline__ void tile_put(char *tile, const f32x4 (&v)[CT], int t, int g, int col0 = 0) {
+    static_assert(CT % 2 == 0, "column tiles are stored in pairs");
+    char *p = tile + (t * mk::TP + col0) * 2;
+    const int cb = (g & 1) ? 16 + 4 * (g - 1) : 4 * g;
 #pragma unroll
-    for (int ct = 0; ct < CT; ct++)
-        *reinterpret_cast<uint2 *>(tile + (t * mk::TP + col0 + 16 * ct + 4 * g) * 2) =
-            make_uint2(pk2bf(v[ct][0], v[ct][1]),
-                       pk2bf(v[ct][2], v[ct][3]));
+    for (int ct = 0; ct < CT; ct += 2) {
+        const auto sx = __builtin_amdgcn_permlane16_swap(pk2bf(v[ct][0], v[ct][1]), pk2bf(v[ct + 1][0], v[ct + 1][1]), false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(pk2bf(v[ct][2], v[ct][3]), pk2bf(v[ct + 1][2], v[ct + 1][3]), false, false);
+        *reinterpret_cast<uint4 *>(p + 2 * (16 * ct + cb)) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+    }
 }
 
 // acc[CT] = W X^T for the board in `tile` (B fragments [t][32 s + 8 g]); W rows at `w` with pitch
