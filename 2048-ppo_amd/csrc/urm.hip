@@ -821,6 +821,9 @@ constexpr int PS_STEM = 0, PS_LNW = PS_STEM + 3 * H, PS_LNB = PS_LNW + H, PS_INI
               PS_WA = PS_INIT + 16 * H, PS_WV = PS_WA + 4 * H, PS_BA = PS_WV + H, PS_BV = PS_BA + 4,
               PS_ALL = PS_BV + 4;
 static_assert(W_BYTES + WAVES * TILE_BYTES + PS_ALL * 4 <= 163840, "one workgroup's LDS");
+#ifndef G2048_URM_STAGE_OPAQUE
+#define G2048_URM_STAGE_OPAQUE 1
+#endif
 #ifndef G2048_URM_NB
 #define G2048_URM_NB 2
 #endif
@@ -1018,9 +1021,18 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
                 constexpr int PER = (C_ALL + mk::THREADS - 1) / mk::THREADS;
                 uint4 v[PER];
                 int dst[PER];
+#if G2048_URM_STAGE_OPAQUE
+                // an opaque per-staging copy of the thread index: the chunks' source offsets are then
+                // recomputed here (a few VALU each) instead of hoisted out of the batch loop, spilled
+                // to scratch and reloaded one vmcnt(0) wait at a time (which serialised the loads)
+                int tid_s = tid;
+                asm volatile("" : "+v"(tid_s));
+#else
+                const int tid_s = tid;
+#endif
 #pragma unroll
                 for (int u = 0; u < PER; u++) {
-                    int e = tid + u * mk::THREADS;
+                    int e = tid_s + u * mk::THREADS;
                     const char *src = nullptr;
                     int d = -1;
                     if (e < C_QKV) {
