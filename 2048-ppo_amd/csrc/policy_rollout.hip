@@ -54,6 +54,10 @@ constexpr int kPrBoards = 256;             // boards per workgroup (one per CU: 
 constexpr int kPrThreads = kPrBoards / kBpw * 64;
 constexpr int kPrLdsMax = 163840;
 constexpr int kPrRecBytes = 4 * 80;  // the stem fragment recipes of the 4 lane groups (LDS, after the zero fragment)
+#ifndef PR_NOSEL
+#define PR_NOSEL 1
+#endif
+constexpr int kPrGap = PR_NOSEL ? 64 : 0;
 #ifndef PR_TILES
 #define PR_TILES 1
 #endif
@@ -149,8 +153,9 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
     constexpr int h = H;
     constexpr int P = pr_pitch(h), WB = pr_wbytes(h);
     char *sW[2] = {smem, smem + WB};  // block weight images (LDS offsets 0 and WB)
-    float *sLN = reinterpret_cast<float *>(smem + 2 * WB);  // [layer][gamma | beta][16 NT]
-    char *sZero = smem + 2 * WB + 2 * kMaxLayers * pr_ln_floats(NT) * 4;
+    // kPrGap zero bytes behind the second image: the last k-step's reads past row h - 1 (PR_NOSEL)
+    float *sLN = reinterpret_cast<float *>(smem + 2 * WB + kPrGap);  // [layer][gamma | beta][16 NT]
+    char *sZero = smem + 2 * WB + kPrGap + 2 * kMaxLayers * pr_ln_floats(NT) * 4;
     char *sRec = sZero + 16;  // [g][sc0 sc1 ss0 ss1 {sx0 sx1 sd0 sd1}] uint4
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, col = lane & 15;
@@ -171,6 +176,7 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
             sLN[e] = f < h ? src[f] : 0.0f;
         }
         if (tid < 4) reinterpret_cast<uint32_t *>(sZero)[tid] = 0u;
+        if (tid < kPrGap / 4) reinterpret_cast<uint32_t *>(smem + 2 * WB)[tid] = 0u;
         if (tid < 20) {
             const StemFrag &e = kStem.f[tid / 5][0], &f = kStem.f[tid / 5][1];
             const int j = tid % 5;
@@ -193,8 +199,8 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
     // A-fragment LDS offsets of the block weights: row 16 n + col, k = 32 ks + 8 g (+ 16 n P per tile);
     // wlane_x in the swizzled k-step groups (pr_piece)
     const int wlane = col * P + 16 * g, wlane_x = col * P + 16 * (g ^ pr_swz(h, col));
-    const int zoff = (int)(sZero - smem);
-    constexpr int last_rows = h - 16 * (NT - 1);  // valid rows of the last tile
+    [[maybe_unused]] const int zoff = (int)(sZero - smem);
+    [[maybe_unused]] constexpr int last_rows = h - 16 * (NT - 1);  // valid rows of the last tile
 
     for (int64_t base = (int64_t)blockIdx.x * kPrBoards; base < a.n; base += (int64_t)gridDim.x * kPrBoards) {
         if (base + kBpw * wave >= a.n) continue;  // an empty wave (no barrier below)
@@ -293,8 +299,17 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
                         asm volatile("" : "+v"(kbase));
 #pragma unroll
                         for (int n = 0; n < NT; n++) {
+#if PR_NOSEL
+                            // no zero redirection: a k-step past h reads the next row's first units
+                            // (or the zero gap behind the last image) against a zero B fragment (dG
+                            // past h is zero: +-0 products), a row past h reads whatever follows
+                            // into an output feature past h, which every epilogue masks by select
+                            (void)kok;
+                            const int off = kbase + 16 * n * P;
+#else
                             const bool rok = n < NT - 1 || col < last_rows;
                             const int off = (kok && rok) ? kbase + 16 * n * P : zoff;
+#endif
                             const uint4 fw = *reinterpret_cast<const uint4 *>(smem + off);
 #pragma unroll
                             for (int q = 0; q < kQ; q++)
@@ -367,7 +382,7 @@ extern "C" {
 size_t g2048_policy_rollout_lds_bytes(int32_t h) {
     if (h <= 0 || h % 4 != 0) return 0;
     const int nt = (h + 15) / 16;
-    const size_t b = (size_t)pr_lds_bytes(h, nt) + kPrRecBytes;
+    const size_t b = (size_t)pr_lds_bytes(h, nt) + kPrRecBytes + kPrGap;
     return b <= (size_t)kPrLdsMax ? b : 0;
 }
 
