@@ -329,6 +329,21 @@ __device__ __forceinline__ uint4 philox_draw(uint64_t seed, uint64_t step, uint3
     return philox((uint32_t)step, (uint32_t)(step >> 32), env, stream, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
+// The transcendentals of the masked-softmax sampler (g2048.hip sample_kernel and the fused rollout's
+// sample_row, bitwise the same code).  Round 5: the hardware forms (v_exp_f32 / v_log_f32 /
+// v_rcp_f32, ~1e-7 relative) instead of the correctly rounded libm sequences (~15 VALU each, five per
+// sampled row): logp / entropy stay within the 1e-5 of the reference's golden rows
+// (test_sampler_matches_reference_masked_softmax).  G2048_SAMPLE_EXACT restores the libm forms.
+#ifdef G2048_SAMPLE_EXACT
+__device__ __forceinline__ float smp_exp(float x) { return expf(x); }
+__device__ __forceinline__ float smp_log(float x) { return logf(x); }
+__device__ __forceinline__ float smp_rcp(float x) { return 1.0f / x; }
+#else
+__device__ __forceinline__ float smp_exp(float x) { return __expf(x); }
+__device__ __forceinline__ float smp_log(float x) { return __logf(x); }
+__device__ __forceinline__ float smp_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+#endif
+
 // 0.9 threshold of `random.random() < 0.9` (game.py:939) on a 32-bit uniform: u*2^-32 < 0.9
 constexpr uint32_t kTwoThreshold = 3865470567u;
 

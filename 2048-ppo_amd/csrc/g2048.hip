@@ -582,10 +582,10 @@ __global__ __launch_bounds__(kBlock) void sample_kernel(const float *__restrict_
     float e[4], s = 0.0f;
 #pragma unroll
     for (int a = 0; a < 4; a++) {
-        e[a] = ((legal >> a) & 1u) ? expf(l[a] - m) : 0.0f;
+        e[a] = ((legal >> a) & 1u) ? smp_exp(l[a] - m) : 0.0f;
         s += e[a];
     }
-    const float ls = logf(s), inv = 1.0f / s;
+    const float ls = smp_log(s), inv = smp_rcp(s);
     const float u = (float)(d.x >> 8) * (1.0f / 16777216.0f);
     float cum = 0.0f, h = 0.0f;
     uint32_t act = 0xFFu;

@@ -54,6 +54,14 @@ constexpr int kPrBoards = 256;             // boards per workgroup (one per CU: 
 constexpr int kPrThreads = kPrBoards / kBpw * 64;
 constexpr int kPrLdsMax = 163840;
 constexpr int kPrRecBytes = 4 * 80;  // the stem fragment recipes of the 4 lane groups (LDS, after the zero fragment)
+#ifndef PR_PHPAIR
+#define PR_PHPAIR (PR_BPW == 32)
+#endif
+static_assert(!PR_PHPAIR || PR_BPW == 32, "the paired Philox draws need half-empty waves");
+#ifndef PR_CARRY
+#define PR_CARRY PR_PHPAIR
+#endif
+static_assert(!PR_CARRY || PR_PHPAIR, "the carried step takes the paired spawn words");
 #ifndef PR_NOSEL
 #define PR_NOSEL 1
 #endif
@@ -117,10 +125,10 @@ __device__ __forceinline__ uint32_t sample_row(const float (&l)[4], uint32_t leg
     float e[4], s = 0.0f;
 #pragma unroll
     for (int a = 0; a < 4; a++) {
-        e[a] = ((legal >> a) & 1u) ? expf(l[a] - m) : 0.0f;
+        e[a] = ((legal >> a) & 1u) ? smp_exp(l[a] - m) : 0.0f;
         s += e[a];
     }
-    const float ls = logf(s), inv = 1.0f / s;
+    const float ls = smp_log(s), inv = smp_rcp(s);
     const float u = (float)(u32 >> 8) * (1.0f / 16777216.0f);
     float cum = 0.0f, hh = 0.0f;
     uint32_t act = 0xFFu;
@@ -208,6 +216,9 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
         const bool live = lane < kBpw && i < a.n;  // (kBpw 32: lanes 32..63 carry no board)
         uint4 b = live ? a.boards[(int64_t)a.t0 * a.n + i] : make_uint4(0u, 0u, 0u, 0u);
         uint32_t legal = live ? (uint32_t)(a.flags[(int64_t)a.t0 * a.n + i] & 0xFu) : 0u;
+#if PR_CARRY
+        BoardCarry carry = board_carry(b);  // the board's statistics, carried (step.hpp step_board_carry)
+#endif
 
         for (int t = a.t0; t < a.t1; t++) {
             // opaque per-step copies of the lane offsets: without them the compiler hoists every
@@ -354,10 +365,28 @@ __global__ __launch_bounds__(kPrThreads, 1) void policy_rollout_kernel(PrArgs a)
 
             // ---------------- sample + env step (lane = board) ----------------------------------
             const uint64_t cs = ctr0 + 2ull * (uint64_t)t;
-            const uint4 d = philox_draw(a.seed, cs, a.env_base + (uint32_t)i, 1u);
             float lp[4], ent;
+#if PR_PHPAIR
+            // 32 boards per wave: the board's two Philox draws of the step on the two half-waves at
+            // once -- lanes 0..31 the sampler's (counter cs, stream 1), lanes 32..63 the spawn's
+            // (cs + 1, stream 0) -- the spawn words then handed down by one permlane32 swap each
+            const bool upper = lane >= 32;
+            const uint4 d = philox_draw(a.seed, upper ? cs + 1ull : cs, a.env_base + (uint32_t)(upper ? i - 32 : i),
+                                        upper ? 0u : 1u);
+            const uint32_t sp0 = __builtin_amdgcn_permlane32_swap(d.x, d.x, false, false)[1];
+            const uint32_t sp1 = __builtin_amdgcn_permlane32_swap(d.y, d.y, false, false)[1];
+            const uint32_t act_a = sample_row(lg, legal, d.x, lp, ent);
+#if PR_CARRY
+            const StepResult res = step_board_carry(b, carry, act_a, rng, i, cs + 1ull, (uint32_t)a.opts, sp0, sp1);
+#else
+            const StepResult res =
+                step_board<G2048_RNG_PHILOX, true>(b, true, act_a, nullptr, rng, i, cs + 1ull, (uint32_t)a.opts, sp0, sp1);
+#endif
+#else
+            const uint4 d = philox_draw(a.seed, cs, a.env_base + (uint32_t)i, 1u);
             const uint32_t act_a = sample_row(lg, legal, d.x, lp, ent);
             const StepResult res = step_board<G2048_RNG_PHILOX>(b, true, act_a, nullptr, rng, i, cs + 1ull, (uint32_t)a.opts);
+#endif
             legal = res.fl & 0xFu;
             if (live) {
                 const int64_t o = (int64_t)t * a.n + i;
