@@ -44,6 +44,15 @@ __device__ __forceinline__ uint32_t pk2bf(float a, float b) {
 // x * sigmoid(x) with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE division
 // sequence: exp overflow for x << 0 gives rcp(inf) = 0, i.e. -0
 __device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+// silu of a feature pair with the multiplies / adds packed (v_pk_mul_f32 / v_pk_add_f32) around the
+// per-element v_exp_f32 / v_rcp_f32: per element the operations of silu() (__expf(-x) is
+// exp2(x * -log2 e)), so the same bits
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 silu2(f32x2 x) {
+    const f32x2 t = x * f32x2{-1.44269504088896341f, -1.44269504088896341f};
+    const f32x2 d = f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + f32x2{1.0f, 1.0f};
+    return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -821,6 +830,12 @@ constexpr int PS_STEM = 0, PS_LNW = PS_STEM + 3 * H, PS_LNB = PS_LNW + H, PS_INI
               PS_WA = PS_INIT + 16 * H, PS_WV = PS_WA + 4 * H, PS_BA = PS_WV + H, PS_BV = PS_BA + 4,
               PS_ALL = PS_BV + 4;
 static_assert(W_BYTES + WAVES * TILE_BYTES + PS_ALL * 4 <= 163840, "one workgroup's LDS");
+#ifndef G2048_URM_RCP
+#define G2048_URM_RCP 1
+#endif
+#ifndef G2048_URM_PK
+#define G2048_URM_PK 1
+#endif
 #ifndef G2048_URM_STAGE_OPAQUE
 #define G2048_URM_STAGE_OPAQUE 1
 #endif
@@ -1107,7 +1122,11 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
                         sum += p[r];
                     }
                     sum = xsum32(xsum16(sum));
+#if G2048_URM_RCP
+                    const float inv = __builtin_amdgcn_rcpf(sum);  // v_rcp_f32 (1 ulp) instead of the IEEE division sequence
+#else
                     const float inv = 1.0f / sum;
+#endif
                     s16x4 pb;
                     if constexpr (kDrop) {  // the mask of URMAttentionFn at counter c0 + app
                         float km[4];
@@ -1156,12 +1175,36 @@ __global__ __launch_bounds__(mk::THREADS) void urm_forward_kernel(const void *__
                         const float4 bb = *reinterpret_cast<const float4 *>(cbl + c);
                         const float wk0[4] = {w01.x, w01.z, w23.x, w23.z}, wk1[4] = {w01.y, w01.w, w23.y, w23.w};
                         const float bk[4] = {bb.x, bb.y, bb.z, bb.w};
+#if G2048_URM_PK
+                        // the same arithmetic on feature pairs: packed multiplies / adds / fmas around the
+                        // per-element exp2 / rcp (bitwise the scalar form: silu2)
+                        float av[4], prev[4];
+#pragma unroll
+                        for (int i = 0; i < 4; i += 2) {
+                            const f32x2 y = silu2(f32x2{ga[i], ga[i + 1]}) * f32x2{up[i], up[i + 1]};
+                            av[i] = y.x;
+                            av[i + 1] = y.y;
+                        }
+#pragma unroll
+                        for (int i = 0; i < 4; i++) prev[i] = dpp_prev_token(av[i]);
+#pragma unroll
+                        for (int i = 0; i < 4; i += 2) {
+                            const f32x2 z = __builtin_elementwise_fma(f32x2{wk1[i], wk1[i + 1]}, f32x2{av[i], av[i + 1]},
+                                                                      __builtin_elementwise_fma(f32x2{wk0[i], wk0[i + 1]},
+                                                                                                f32x2{prev[i], prev[i + 1]},
+                                                                                                f32x2{bk[i], bk[i + 1]}));
+                            const f32x2 o = silu2(z);
+                            a[ct][i] = c + i < mk::INTER ? o.x : 0.0f;
+                            a[ct][i + 1] = c + i + 1 < mk::INTER ? o.y : 0.0f;
+                        }
+#else
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
                             const float av = silu(ga[i]) * up[i];
                             const float prev = dpp_prev_token(av);
                             a[ct][i] = c + i < mk::INTER ? silu(fmaf(wk1[i], av, fmaf(wk0[i], prev, bk[i]))) : 0.0f;
                         }
+#endif
                     }
                     wave_lds_sync();
                     tile_put<8>(tile, a, t, g);
