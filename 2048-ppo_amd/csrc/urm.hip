@@ -836,6 +836,9 @@ static_assert(W_BYTES + WAVES * TILE_BYTES + PS_ALL * 4 <= 163840, "one workgrou
 #ifndef G2048_URM_PK
 #define G2048_URM_PK 1
 #endif
+#ifndef G2048_URM_PK_RMS
+#define G2048_URM_PK_RMS G2048_URM_PK
+#endif
 #ifndef G2048_URM_STAGE_OPAQUE
 #define G2048_URM_STAGE_OPAQUE 1
 #endif
@@ -931,6 +934,30 @@ __device__ __forceinline__ void frag_gemm(f32x4 (&acc)[CT], const char *w, int p
 // x = rms_norm(x + y) [+ emb]  (the token's 64 features in 4 lanes x 16 values)
 __device__ __forceinline__ void rms_update(f32x4 (&x)[4], const f32x4 (&y)[4], const f32x4 (&emb)[4], bool add_emb,
                                            float eps) {
+#if G2048_URM_PK_RMS
+    // round 5: feature pairs on packed adds / fmas (the sum of squares as two interleaved partial sums)
+    f32x2 s2 = {0.0f, 0.0f};
+#pragma unroll
+    for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+            const f32x2 v = f32x2{x[ct][i], x[ct][i + 1]} + f32x2{y[ct][i], y[ct][i + 1]};
+            x[ct][i] = v.x;
+            x[ct][i + 1] = v.y;
+            s2 = __builtin_elementwise_fma(v, v, s2);
+        }
+    const float ss = xsum32(xsum16(s2.x + s2.y));
+    const float r = rsqrtf(ss * (1.0f / mk::H) + eps);
+#pragma unroll
+    for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+            const f32x2 e = add_emb ? f32x2{emb[ct][i], emb[ct][i + 1]} : f32x2{0.0f, 0.0f};
+            const f32x2 v = __builtin_elementwise_fma(f32x2{x[ct][i], x[ct][i + 1]}, f32x2{r, r}, e);
+            x[ct][i] = v.x;
+            x[ct][i + 1] = v.y;
+        }
+#else
     float ss = 0.0f;
 #pragma unroll
     for (int ct = 0; ct < 4; ct++)
@@ -945,6 +972,7 @@ __device__ __forceinline__ void rms_update(f32x4 (&x)[4], const f32x4 (&y)[4], c
     for (int ct = 0; ct < 4; ct++)
 #pragma unroll
         for (int i = 0; i < 4; i++) x[ct][i] = x[ct][i] * r + (add_emb ? emb[ct][i] : 0.0f);
+#endif
 }
 
 template <bool kBf16Obs, bool kDrop>
