@@ -29,6 +29,9 @@ def main():
     a = ap.parse_args()
     import agent
     from g2048 import _lib as L
+    import os
+    if os.environ.get("G2048_LIB"):  # A/B timing against another build of the library
+        L._lib = L.load(os.environ["G2048_LIB"])
     from g2048.dist import GradBucket
     from g2048.fastmlp import FusedPPOUpdater
     from g2048.optim import FusedMuonAdamW, MuonAdamW
