@@ -3,7 +3,7 @@
 // adjust_lr_fn="match_rms_adamw", nesterov, 5 Newton-Schulz steps in bf16) as three launches:
 //
 //   grad_sumsq/norm      ||g|| over the flat gradient bucket and the clip coefficient
-//                        min(max_norm / (||g|| + 1e-6), 1) into device scalars
+//                        clamp(max_norm / (||g|| + 1e-6), max=1) into device scalars (NaN kept)
 //   muon_kernel          one 512-thread block per weight matrix: momentum + nesterov, bf16 cast,
 //                        Frobenius normalisation, the 5 Newton-Schulz iterations
 //                            G = X X^T;  U = b G + c G G;  X = a X + U X
@@ -65,6 +65,16 @@ __global__ __launch_bounds__(256) void grad_sumsq_kernel(const float *__restrict
     if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// torch.nn.utils.clip_grad_norm_'s coefficient (train.py:560): clamp(max_norm / (norm + 1e-6), max=1).
+// torch.clamp passes a NaN through, so a NaN norm makes the step NaN exactly as in the reference;
+// fminf(c, 1) returned 1 for a NaN c (v_min_f32 drops the NaN operand): the step then ran unclipped
+// with finite weights and only the logged norm showed the fault (round-5 verdict).  The
+// trainer raises on a non-finite norm at its one metrics read.
+__device__ __forceinline__ float clip_coef(float max_norm, float nrm) {
+    const float c = max_norm / (nrm + 1e-6f);
+    return c > 1.0f ? 1.0f : c;  // NaN > 1 is false: the NaN is kept
+}
+
 __global__ __launch_bounds__(64) void grad_norm_kernel(const float *__restrict__ part, float max_norm,
                                                        float *__restrict__ norm_out, float *__restrict__ coef_out) {
     float s = part[threadIdx.x];
@@ -73,7 +83,7 @@ __global__ __launch_bounds__(64) void grad_norm_kernel(const float *__restrict__
     if (threadIdx.x == 0) {
         const float nrm = sqrtf(s);
         *norm_out = nrm;
-        *coef_out = fminf(max_norm / (nrm + 1e-6f), 1.0f);
+        *coef_out = clip_coef(max_norm, nrm);
     }
 }
 
@@ -1167,7 +1177,7 @@ __device__ __forceinline__ void adam_blocks(const MuonArgs &args, int b, int nb)
     float cf = 1.0f;
     if (args.partials) {  // grad_norm_kernel's arithmetic, as in the Muon blocks (same result)
         const float t = clip_sumsq(args, threadIdx.x & 63);
-        cf = fminf(args.max_norm / (sqrtf(t) + 1e-6f), 1.0f);
+        cf = clip_coef(args.max_norm, sqrtf(t));
     }
     const AdamArgs &a = args.adam;
     const float t = *a.step;
@@ -1188,7 +1198,7 @@ __device__ __forceinline__ float block_clip_coef(const MuonArgs &args, int tid, 
     if (tid < 64) {
         const float t = clip_sumsq(args, tid);
         const float nrm = sqrtf(t);
-        const float cf = fminf(args.max_norm / (nrm + 1e-6f), 1.0f);
+        const float cf = clip_coef(args.max_norm, nrm);
         if (tid == 0) {
             s_coef = cf;
             if (publish) {

@@ -434,6 +434,11 @@ class VecTrainer:
             inner.check_errors(vec.pop())
         (n, rm, rv, zr, am, av, al2, amin, amax, gnm, gns, gnmin, gnmax, grs, vs, g0m, avg_s, med_s, max_s, p512,
          p1024, p2048, n_eps, loss, pl, el, vl, gnorm, ent, klt, kla, klm) = vec
+        if not math.isfinite(gnorm):
+            # torch's clip_grad_norm_ lets a NaN norm through into the step (the fused optimizer now
+            # does the same, optim.hip clip_coef); the trainer does not train on silently
+            raise FloatingPointError(f"non-finite gradient norm ({gnorm}) in this train step's update: "
+                                     f"{self.nonfinite_report()}")
         if n_eps > 0:
             self.highest = max(self.highest, int(max_s))
             d = 0.001
@@ -515,6 +520,28 @@ class VecTrainer:
         self.rollout._graph = None
         self._chunk_graphs.clear()
         torch.cuda.synchronize(self.dev)
+        if self.bf16w is not None:  # the weights may be reused with another optimizer / a loaded state
+            self.bf16w.detach()
+            self.bf16w = None
+        inner = getattr(self.opt, "opt", self.opt)
+        if hasattr(inner, "check_errors"):  # a Muon hand-off timeout after the last metrics read
+            inner.check_errors()
+
+    def nonfinite_report(self) -> str:
+        """Which gradient-bucket segments and parameters hold non-finite values (names, counts), for the
+        error raised on a non-finite gradient norm.  One host read of per-tensor counts."""
+        names = {id(p): n for n, p in self.model.named_parameters()}
+        rows = []
+        for p in self.grads.params:
+            bad_g = int((~torch.isfinite(p.grad)).sum()) if p.grad is not None else 0
+            bad_p = int((~torch.isfinite(p.detach())).sum())
+            if bad_g or bad_p:
+                rows.append(f"{names.get(id(p), '?')}: grad {bad_g}/{p.numel()}, param {bad_p}/{p.numel()}")
+        inner = getattr(self.opt, "opt", self.opt)
+        part = getattr(inner, "norm_part", None)
+        if part is not None:
+            rows.append(f"norm partials non-finite: {int((~torch.isfinite(part)).sum())}/{part.numel()}")
+        return "; ".join(rows) if rows else "gradient bucket and parameters finite now (the last minibatch's bucket)"
 
     def save_checkpoint(self, path, eval_avg_score: float, train_step: int):
         import agent

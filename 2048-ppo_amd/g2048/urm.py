@@ -651,9 +651,14 @@ def _gemm_t(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 def bf16_weight(w: torch.Tensor) -> torch.Tensor:
     """The autocast bf16 operand of a projection weight: its Bf16Weights copy (written by the fused
-    Muon step with the weight itself, so no cast kernel per use) when one is attached, else a cast."""
+    Muon step with the weight itself, so no cast kernel per use) when one is attached and current,
+    else a cast.  Current = no torch op wrote the weight since the copy's last refresh (the fused
+    step writes both through raw pointers and bumps no version counter; load_state_dict, a torch
+    optimizer or any in-place op on the weight does): a stale copy is never used silently."""
     c = getattr(w, "_g2048_bf16", None)
-    return c if c is not None else w.detach().to(torch.bfloat16)
+    if c is not None and getattr(w, "_g2048_bf16_ver", None) == w._version:
+        return c
+    return w.detach().to(torch.bfloat16)
 
 
 class Bf16Weights:
@@ -680,10 +685,12 @@ class Bf16Weights:
     def refresh(self):
         for w, t in self.pairs:
             t.copy_(w)
+            w._g2048_bf16_ver = w._version
 
     def detach(self):
         for w, _ in self.pairs:
             w._g2048_bf16 = None
+            w._g2048_bf16_ver = None
 
 
 def attach_bf16_weights(model, opt):

@@ -49,6 +49,12 @@ def _worker(rank, world, port, out, model_type="mlp"):
     from g2048.trainer import TrainConfig, VecTrainer
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    from g2048 import _lib as L
+    # a spawned rank is a fresh process: conftest's autouse poison ran only in the pytest process, so
+    # each rank fills every CU's LDS with the NaN pattern itself before its first kernel (a kernel of
+    # the path that reads LDS it did not write then turns it into NaN here, not on one box in ten)
+    L.lds_poison(0x7FC07FC0)
+    torch.cuda.synchronize()
     torch.manual_seed(rank)  # different local inits: VecTrainer must broadcast rank 0's replica
     if model_type == "urm":  # GameURM (default config: h 64, 2 layers, 4 heads, 4 / 1 loops) on its device Functions
         cfg = TrainConfig(steps=10, episodes=256, horizon=8, batch_size=1024, hidden=64, model_type="urm",
@@ -85,20 +91,29 @@ def _worker(rank, world, port, out, model_type="mlp"):
         rec["nb"].append(-(-m // cfg.batch_size))
         return orig_up(data, beta, encode)
     tr.ppo.update = update
+    # every minibatch's gradient norm, read right after its step (the split path's g2 replay): an
+    # intermittent non-finite grad_norm with a finite loss / KL was seen in this MLP test (r04c, r05d,
+    # DESIGN.md §7); a recurrence names its minibatch and the non-finite bucket segments / parameters
+    inner = getattr(tr.opt, "opt", tr.opt)
+    rec["norms"] = []
+
+    def checked(fn):  # the graphed minibatch (_replay) and the eager one (_minibatch: warm-ups, ragged URM)
+        def run(*args):
+            fn(*args)
+            nt = getattr(inner, "norm_t", None)
+            if nt is None:
+                return
+            v = float(nt)
+            if not np.isfinite(v):
+                raise AssertionError((rank, "minibatch", len(rec["norms"]), v, tr.nonfinite_report(),
+                                      inner.norm_part.cpu().tolist()))
+            rec["norms"].append(v)
+        return run
+    tr.ppo._replay = checked(tr.ppo._replay)
+    tr.ppo._minibatch = checked(tr.ppo._minibatch)
     for s in range(STEPS):
-        m = tr.train_step(s)
-        if not (np.isfinite(m["loss"]) and np.isfinite(m["grad_norm"])):
-            # an intermittent non-finite grad_norm with a finite loss / KL was seen in this MLP test (r04c,
-            # r05d): record what the norm was computed from, for the cause
-            torch.cuda.synchronize()
-            inner = getattr(tr.opt, "opt", tr.opt)
-            diag = {"bucket_finite": bool(torch.isfinite(bucket.flat).all()),
-                    "params_finite": all(bool(torch.isfinite(p).all()) for p in tr.model.parameters()),
-                    "norm_part": getattr(inner, "norm_part", torch.zeros(1)).cpu().tolist(),
-                    "norm_t": float(getattr(inner, "norm_t", torch.zeros(1)).reshape(-1)[0]),
-                    "coef_t": float(getattr(inner, "coef_t", torch.zeros(1)).reshape(-1)[0]),
-                    "stats": tr.ppo.stats.cpu().tolist()}
-            raise AssertionError((rank, s, m, diag))
+        m = tr.train_step(s)  # raises FloatingPointError itself on a non-finite norm (trainer._metrics)
+        assert np.isfinite(m["loss"]) and np.isfinite(m["grad_norm"]), (rank, s, m)
         T = tr.rollout.T
         rec["g_raw"].append(tr.rollout.buf.g_raw[:T].reshape(-1).double().cpu().numpy())
         rec["moments"].append(tr.rtg.state.cpu().numpy().copy())
@@ -123,6 +138,9 @@ def test_two_ranks_fused_update_on_device(model_type):
         r0, r1 = out[0], out[1]
     # same sample count and minibatch count on both ranks, every train step
     assert r0["rows"] == r1["rows"] and r0["nb"] == r1["nb"] and len(r0["rows"]) == STEPS
+    # the per-minibatch norms were read on every graphed minibatch and agree across the replicas
+    # (the same all-reduced bucket)
+    assert len(r0["norms"]) >= sum(r0["nb"]) and r0["norms"] == r1["norms"]
     assert len(r0["before"]) == 3 and len(r1["before"]) == 3
     # the all-reduced bucket is the mean of the two local ones (sum then / 2: exact in fp32)
     for k in range(3):

@@ -396,12 +396,15 @@ def _golden_model(dev, u):
 # Absolute per-tensor bounds of the fused update vs the reference's fp32 step.  Muon moves a matrix
 # by the orthogonalised gradient (Newton-Schulz equalises its singular values), so a direction whose
 # singular value sits at bf16 noise level is scaled up like the others: the lower the gradient's
-# effective rank the looser the cosine.  Measured on MI355X (fused / torch bf16 autocast):
+# effective rank the looser the cosine.  Measured on MI355X (fused / torch bf16 autocast, rounds 4-6,
+# the same bits every run: the step is deterministic):
 # stem 0.9900 / 0.9918, backbone.0 0.9885 / 0.9905, backbone.1 0.9724 / 0.9775, action_head
 # (rank <= 4) 0.8859 / 0.8620, value_head (rank 1: Muon is a normalisation) 0.9990 / 0.9948.
-MUON_COS = {"stem.0.weight": 0.98, "backbone.0.mlp.0.weight": 0.98, "backbone.1.mlp.0.weight": 0.96,
-            "action_head.weight": 0.85, "value_head.weight": 0.99}
-ADAMW_SIGN = 0.95  # measured worst 0.9688 (backbone.1 LayerNorm bias; autocast 0.9688)
+# Round 6 tightened them to the measured value less half its distance to 1 (rounded down), and
+# added the live bound of the h 196 test beside it: 1 - cos <= 1.5 (1 - cos_autocast) + 2e-3.
+MUON_COS = {"stem.0.weight": 0.985, "backbone.0.mlp.0.weight": 0.98, "backbone.1.mlp.0.weight": 0.955,
+            "action_head.weight": 0.83, "value_head.weight": 0.998}
+ADAMW_SIGN = 0.965  # measured worst 0.9688 = 62 / 64 (backbone.1 LayerNorm bias; autocast 0.9688): 61 / 64 fails
 
 
 def test_fused_update_matches_reference_step(dev):
@@ -449,8 +452,9 @@ def test_fused_update_matches_reference_step(dev):
             cos_ac = float(F.cosine_similarity(ac, want, dim=0))
             ratio = float(got.norm() / want.norm())
             rows.append(f"{k}: cos {cos:.4f} (autocast {cos_ac:.4f}), norm ratio {ratio:.4f}")
-            # stated bound: cosine >= MUON_COS[k] and the move's norm within 5 % of the reference's
-            if cos < MUON_COS[k] or abs(ratio - 1) > 5e-2:
+            # stated bound: cosine >= MUON_COS[k], within 1.5 x torch autocast's distance from the
+            # reference (+ 2e-3), and the move's norm within 5 % of the reference's
+            if cos < MUON_COS[k] or (1 - cos) > 1.5 * (1 - cos_ac) + 2e-3 or abs(ratio - 1) > 5e-2:
                 bad.append(rows[-1])
         else:
             # AdamW's first step is lr * sign(grad) (|move| = lr where the gradient is not ~0): the
@@ -461,6 +465,100 @@ def test_fused_update_matches_reference_step(dev):
             rows.append(f"{k}: sign agreement {agree:.4f} (autocast {agree_ac:.4f})")
             if agree < ADAMW_SIGN:
                 bad.append(rows[-1])
+    print("\n".join(rows))
+    assert not bad, bad
+
+
+# h 196 absolute floors, from the first MI355X run (fused / autocast / fp32 cosines to the reference:
+# stem 0.99507 / 0.99432 / 0.99997, backbone.0 0.98644 / 0.98394 / 0.99980, backbone.1 0.98421 /
+# 0.97740 / 0.99989, action_head 0.89830 / 0.82369 / 0.99970, value_head 1.00000 / 0.99999 / 1.0;
+# AdamW tensors >= 0.99367; norm ratios within 1.9 %; profiles/r06a/ref196.log)
+MUON_COS196 = {"stem.0.weight": 0.99, "backbone.0.mlp.0.weight": 0.98, "backbone.1.mlp.0.weight": 0.975,
+               "action_head.weight": 0.87, "value_head.weight": 0.9999}
+
+
+def test_fused_update_matches_reference_step_h196(dev):
+    """The shipped update at the README / bench policy shape against the reference itself
+    (tests/golden/update196.npz: model_optimize_step, train.py:414-642, at h 196, dropout 0, 4 096
+    rows in the reference's own two shuffled minibatches of 2 048, clip_grad_norm_ active -- both
+    norms ~3.6 -- Muon + AdamW at fixed learning rates).  Run as the trainer runs it: FusedPPOUpdater on
+    the captured offset path (one-launch passes, fused backward, one-launch weight gradients) with
+    FusedMuonAdamW on 13 CUs per h x h matrix.  The two minibatches are the reference's (the data is
+    fed in its DataLoader order and the device permutation is the identity).
+
+    Bounds are derived from the spread measured beside it on the same inputs: torch's bf16 autocast of
+    the same step (PPOUpdater + torch.optim.Muon / AdamW) and the fp32 step in device reduction order
+    (PPOUpdater without autocast: the reference's arithmetic, summed in another order -- Muon's bf16
+    Newton-Schulz amplifies that alone: measured cosines >= 0.9997).  Per Muon matrix: cosine >=
+    MUON_COS196, 1 - cos(fused, ref) <= 2 (1 - cos(autocast, ref)) + 1e-3 and the move's norm within
+    3 %; per AdamW tensor (two Adam steps): cosine >= 0.99 and within 2 x the autocast deviation +
+    0.01; statistics within 1 % (grad_norm, loss, value_loss, entropy) of the reference's."""
+    from g2048.dist import GradBucket
+    from g2048.fastmlp import FusedPPOUpdater
+    from g2048.optim import FusedMuonAdamW, build_optimizer
+    from g2048.ppo import PPOConfig, PPOUpdater
+    import agent
+    u = golden("update196.npz")
+    order = torch.from_numpy(u["order"]).to(dev)
+    n, bs = len(u["actions"]), int(u["batch_size"])
+    lr, clr, b1, b2, wd, beta, critic = (float(x) for x in u["hparams"])
+    legal = np.array([sum(1 << a for a in range(4) if not u["invalid"][i, a]) for i in range(n)], np.uint8)
+    raw = {"boards": u["boards"].astype(np.int8), "actions": u["actions"].astype(np.uint8), "legal": legal,
+           "logp": u["old_logprobs"], "adv": u["advantage"], "ret": u["future_reward"]}
+    data = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev).index_select(0, order) for k, v in raw.items()}
+
+    def ident(m_total, out=None):  # the reference's minibatches: data already in its DataLoader order
+        r = torch.arange(m_total, device=dev)
+        return r if out is None else out[:m_total].copy_(r)
+
+    def enc(b):
+        from g2048 import _lib as L
+        o = torch.empty(b.shape[0], 48, dtype=torch.float32, device=dev)
+        L.obs_encode(b.contiguous(), o)
+        return o
+    ref_stats = dict(zip([str(k) for k in u["stat_keys"]], u["stat_vals"]))
+    init = {k[len("init::"):]: torch.from_numpy(u[k]) for k in u.files if k.startswith("init::")}
+    moves, stats = {}, {}
+    for mode in ("fused", "autocast", "fp32"):
+        m = agent.GameMLP(agent.MLPConfig(hidden_dim=196, num_layers=2, dropout=0.0)).to(dev)
+        m.load_state_dict(init)
+        if mode == "fused":
+            opt = FusedMuonAdamW(m, lr, clr, b1, b2, wd)
+            assert opt.supported and opt._cfg.parts == 13
+            bo = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
+            up = FusedPPOUpdater(m, opt, PPOConfig(batch_size=bs, critic=critic), GradBucket(bo), graph=True)
+        else:
+            opt = build_optimizer(m, lr, clr, b1, b2, wd, schedule=False)
+            pc = PPOConfig(batch_size=bs, critic=critic, amp_dtype=torch.bfloat16 if mode == "autocast" else None)
+            up = PPOUpdater(m, opt, pc, GradBucket(m.parameters()))
+        up._epoch_perm = ident
+        stats[mode] = {k: float(v) for k, v in up.update(data, beta, enc).items()}
+        if mode == "fused":
+            assert up._og is not None and up.wgrad_one_launch  # the captured offset path ran
+        moves[mode] = {k: (v.detach().cpu() - init[k]).reshape(-1).double() for k, v in m.state_dict().items()}
+        up.close()
+    rows, bad = [], []
+    for k in ("loss", "value_loss", "entropy", "grad_norm", "policy_loss", "kl_average"):
+        rows.append(f"{k}: ref {ref_stats[k]:.6g} fused {stats['fused'][k]:.6g} autocast {stats['autocast'][k]:.6g} "
+                    f"fp32 {stats['fp32'][k]:.6g}")
+        tol = 1e-2 if k in ("loss", "value_loss", "entropy", "grad_norm") else 0.1
+        if not math.isclose(stats["fused"][k], ref_stats[k], rel_tol=tol, abs_tol=2e-4):
+            bad.append(rows[-1])
+
+    def cos(a, b):
+        return float(F.cosine_similarity(a, b, dim=0))
+    for k in moves["fused"]:
+        want = torch.from_numpy(u["final::" + k]).reshape(-1).double() - init[k].reshape(-1).double()
+        got, ac, f32 = moves["fused"][k], moves["autocast"][k], moves["fp32"][k]
+        c, c_ac, c_32 = cos(got, want), cos(ac, want), cos(f32, want)
+        ratio = float(got.norm() / want.norm())
+        rows.append(f"{k}: cos fused {c:.5f} autocast {c_ac:.5f} fp32 {c_32:.5f}; norm ratio {ratio:.4f}")
+        if init[k].ndim >= 2:
+            ok = c >= MUON_COS196[k] and (1 - c) <= 2 * (1 - c_ac) + 1e-3 and abs(ratio - 1) <= 3e-2
+        else:
+            ok = c >= 0.99 and (1 - c) <= 2 * (1 - c_ac) + 1e-2
+        if not ok:
+            bad.append(rows[-1])
     print("\n".join(rows))
     assert not bad, bad
 

@@ -39,6 +39,9 @@ def _child():
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)  # before any other GPU work
     sys.path[:0] = [str(ROOT), str(PKG)]
+    from g2048 import _lib as L
+    L.lds_poison(0x7FC07FC0)  # a fresh process: conftest's per-test LDS poison did not run here
+    torch.cuda.synchronize()
     import numpy as np
     import agent
     from g2048.dist import GradBucket

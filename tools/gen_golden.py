@@ -21,6 +21,8 @@ Fixture files (all npz, allow_pickle=False):
   urm64.npz       GameURM forward at the default GameURMConfig (h 64: BASELINE config 5), 512 boards
                   (`python tools/gen_golden.py urm64` regenerates only this file)
   mlp196.npz      GameMLP forward at the bench's train configuration (h 196, 2 blocks), 512 boards
+  update196.npz   model_optimize_step at h 196, dropout 0, 4 096 rows in two minibatches of 2 048, the
+                  DataLoader order recorded (`python tools/gen_golden.py update196`)
 """
 
 from __future__ import annotations
@@ -317,6 +319,76 @@ def gen_update(game, train, games):
     print(f"update.npz: h=64 single minibatch of {len(moves)}; stats {stats}")
 
 
+def gen_update196(game, train):
+    """update196.npz: the reference's model_optimize_step (train.py:414-642) at the README / bench
+    policy shape -- GameMLP h 196, 2 residual blocks, dropout 0 -- on 4 096 rows of the golden games
+    in TWO minibatches of 2 048, one epoch; Muon (match_rms_adamw) + AdamW at fixed learning rates
+    (no scheduler).  The DataLoader's shuffle order is recorded (RandomSampler, wrapped here) and
+    stored as `order`, so a test can feed the same two minibatches; the per-minibatch statistics
+    come from the reference's own totals (stats) plus the two grad norms (clip_grad_norm_, wrapped
+    here).  `python tools/gen_golden.py update196` regenerates only this file."""
+    import torch.utils.data as tud
+    torch.manual_seed(1960)
+    cfg = game.MLPConfig(hidden_dim=196, num_layers=2, dropout=0.0, decouple_critic=False)
+    model = game.GameMLP(cfg)
+    g = np.load(OUT / "games.npz")
+    n = 4096
+    boards = g["before"][:n]
+    obs = torch.stack([game.Game2048(grid_of(b)).to_model_format() for b in boards])
+    assert np.array_equal(np.rint(obs[:, 0::3].numpy()).astype(np.int8), boards)  # exponent channel
+    invalid = np.array([[not (m >> k & 1) for k in range(4)] for m in g["mask_before"][:n]])
+    actions = g["action"][:n].copy()
+    for i in range(n):  # the trainer samples legal actions only (the fixture's games hold ~5 % illegal)
+        if invalid[i, actions[i]]:
+            actions[i] = int(np.nonzero(~invalid[i])[0][0])
+    rng = np.random.default_rng(196)
+    adv = rng.normal(size=n).astype(np.float32)
+    fut = rng.normal(size=n).astype(np.float32)
+    with torch.no_grad():  # heads at their Kaiming init: non-uniform old policies
+        lg, _ = model(obs)
+        lg = lg.masked_fill(torch.from_numpy(invalid), float("-inf"))
+        old_lp = lg.log_softmax(-1) + torch.from_numpy(rng.normal(scale=0.05, size=(n, 4)).astype(np.float32))
+    moves = [{"game_state": obs[i], "selected_direction": int(actions[i]), "action_mask": invalid[i].tolist(),
+              "advantage": float(adv[i]), "future_reward": float(fut[i]), "policy_logprobs": old_lp[i].tolist()}
+             for i in range(n)]
+    init = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    lr, clr, wd = 1e-3, 1e-4, 0.01
+    o2d, o1d, v2d, v1d = model.get_param_groups(clr, lr)
+    adamw = torch.optim.AdamW([o1d, v1d], betas=(0.9, 0.999), weight_decay=wd)
+    muon = torch.optim.Muon([o2d, v2d], adjust_lr_fn="match_rms_adamw", weight_decay=wd)
+    opt = train.MultiOptimizer(muon, adamw)
+    order, norms = [], []
+    orig_iter, orig_clip = tud.RandomSampler.__iter__, torch.nn.utils.clip_grad_norm_
+
+    def rec_iter(self):
+        for i in orig_iter(self):
+            order.append(int(i))
+            yield i
+
+    def rec_clip(params, max_norm, *a, **k):
+        r = orig_clip(params, max_norm, *a, **k)
+        norms.append(float(r))
+        return r
+    tud.RandomSampler.__iter__ = rec_iter
+    torch.nn.utils.clip_grad_norm_ = rec_clip
+    try:
+        stats = train.model_optimize_step(model=model, episodes=[{"moves": moves}], optimizer=opt,
+                                          lr_scheduler=None, kl_strength=0.02, critic_strength=0.2,
+                                          device=None, batch_size=2048, epochs=1)
+    finally:
+        tud.RandomSampler.__iter__ = orig_iter
+        torch.nn.utils.clip_grad_norm_ = orig_clip
+    assert sorted(order) == list(range(n)) and len(norms) == 2
+    arrays = {f"init::{k}": v.numpy() for k, v in init.items()}
+    arrays.update({f"final::{k}": v.detach().numpy() for k, v in model.state_dict().items()})
+    arrays.update(boards=boards, actions=actions, invalid=invalid, advantage=adv, future_reward=fut,
+                  old_logprobs=old_lp.numpy(), order=np.array(order, np.int64), grad_norms=np.array(norms),
+                  stat_keys=np.array(sorted(stats)), stat_vals=np.array([float(stats[k]) for k in sorted(stats)]),
+                  hparams=np.array([lr, clr, 0.9, 0.999, wd, 0.02, 0.2]), batch_size=np.int64(2048))
+    np.savez_compressed(OUT / "update196.npz", **arrays)
+    print(f"update196.npz: h=196, {n} rows in 2 minibatches; grad norms {norms}; stats {stats}")
+
+
 def gen_urm(game, games):
     torch.manual_seed(77)
     cfg = game.GameURMConfig(hidden_dim=32, num_layers=2, num_heads=4, dropout=0.0, num_loops=4,
@@ -381,6 +453,10 @@ def main():
         game, _ = load_reference()
         {"urm64": gen_urm64, "mlp196": gen_mlp196}[sys.argv[1]](game)
         return
+    if sys.argv[1:] == ["update196"]:
+        game, train = load_reference()
+        gen_update196(game, train)
+        return
     OUT.mkdir(parents=True, exist_ok=True)
     game, train = load_reference()
     DIRS = [game.Direction.UP, game.Direction.DOWN, game.Direction.LEFT, game.Direction.RIGHT]
@@ -394,6 +470,7 @@ def main():
     gen_urm(game, games)
     gen_urm64(game)
     gen_mlp196(game)
+    gen_update196(game, train)
 
 
 if __name__ == "__main__":

@@ -8,6 +8,7 @@
 #   TAG=r04x bash tools/gpu/check.sh urm    GameURM: tests, bench leg, kernel trace, torch-op census,
 #                                           SQ passes of the one-launch forward
 #   TAG=r04x bash tools/gpu/check.sh full   every GPU test, smoke, the default bench line
+#   TAG=r06a bash tools/gpu/check.sh dist   stale-memory detector of the update, the 2-rank and RCCL tests
 #   TAG=r05a bash tools/gpu/check.sh muon   Muon: its tests, the MUON_TRACE build (make trace) at 13 and 8
 #                                           parts (phase clocks + bound checks), HIP-event timing
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -52,6 +53,7 @@ urm)
   echo "pmc rc=$?"; python3 tools/pmc_table.py gpurun_out/pmck_${TAG}_urmfwd urm_forward 2>&1 | head -30
   ;;
 muon)
+  make -C 2048-ppo_amd/csrc trace > $O/make_trace.log 2>&1 || { echo "make trace failed"; tail -5 $O/make_trace.log; exit 1; }
   run_tests $O/tests.log 300 tests/test_gpu_ppo_fused.py -k "muon or Muon"
   for p in 13 8; do
     timeout -k 10 120 python3 tools/trace_muon.py tools/alt/libg2048_mtrace.so $p > $O/trace_muon_$p.log 2>&1
@@ -60,6 +62,10 @@ muon)
   done
   timeout -k 10 120 python3 tools/time_muon.py > $O/time_muon.log 2>&1
   echo "time rc=$?"; head -6 $O/time_muon.log
+  ;;
+dist)
+  run_tests $O/stale.log 400 tests/test_gpu_stale_reads.py
+  run_tests $O/dist.log 400 tests/test_gpu_dist.py tests/test_gpu_rccl.py
   ;;
 full)
   run_tests $O/tests.log 700 tests
