@@ -46,6 +46,42 @@ def test_model_optimize_step_matches_reference_update():
     assert stats["lr"] == ref["lr"] == 0.0
 
 
+def test_model_optimize_step_matches_reference_update_h196(monkeypatch):
+    """The same at the README / bench policy shape (tests/golden/update196.npz: h 196, 4 096 rows in the
+    reference's two shuffled minibatches of 2 048, clip active): with the DataLoader's recorded order,
+    the CPU restatement's parameters and statistics match the reference run (fp32; Muon's bf16
+    Newton-Schulz is torch's own here, so only the reduction order of the two runs differs)."""
+    import agent
+    import train
+    from g2048.augment import encode_grid
+    from g2048.optim import MultiOptimizer
+    u = golden("update196.npz")
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=196, num_layers=2, dropout=0.0))
+    m.load_state_dict({k[len("init::"):]: torch.from_numpy(u[k]) for k in u.files if k.startswith("init::")})
+    lr, clr, b1, b2, wd, beta, critic = (float(x) for x in u["hparams"])
+    moves = [{"game_state": encode_grid(u["boards"][i].reshape(4, 4).tolist()), "selected_direction": int(u["actions"][i]),
+              "action_mask": u["invalid"][i].tolist(), "advantage": float(u["advantage"][i]),
+              "future_reward": float(u["future_reward"][i]), "policy_logprobs": u["old_logprobs"][i].tolist()}
+             for i in range(len(u["actions"]))]
+    order = torch.from_numpy(u["order"])
+    real_randperm = torch.randperm
+    monkeypatch.setattr(torch, "randperm", lambda n, *a, **k: order.clone() if n == len(order) else real_randperm(n, *a, **k))
+    o2d, o1d, v2d, v1d = m.get_param_groups(clr, lr)
+    adamw = torch.optim.AdamW([o1d, v1d], betas=(b1, b2), weight_decay=wd)
+    muon = torch.optim.Muon([o2d, v2d], adjust_lr_fn="match_rms_adamw", weight_decay=wd)
+    stats = train.model_optimize_step(m, [{"moves": moves}], MultiOptimizer(muon, adamw), None, beta, critic,
+                                      None, batch_size=int(u["batch_size"]), epochs=1)
+    for k, v in m.state_dict().items():
+        want = u[f"final::{k}"] - u[f"init::{k}"]
+        got = v.numpy() - u[f"init::{k}"]
+        cos = float(np.dot(got.ravel(), want.ravel()) / (np.linalg.norm(got) * np.linalg.norm(want) + 1e-30))
+        assert cos > 0.9995, (k, cos)  # the two fp32 runs differ by summation order only (measured >= 0.9997 on device)
+        np.testing.assert_allclose(v.numpy(), u[f"final::{k}"], rtol=1e-3, atol=2e-5, err_msg=k)
+    ref = dict(zip(u["stat_keys"].tolist(), u["stat_vals"].tolist()))
+    for k in ("loss", "policy_loss", "entropy_loss", "value_loss", "grad_norm", "entropy"):
+        assert math.isclose(stats[k], ref[k], rel_tol=1e-4, abs_tol=1e-6), (k, stats[k], ref[k])
+
+
 def test_cosine_schedule_matches_transformers():
     from transformers import get_scheduler
     from g2048.optim import cosine_with_warmup
