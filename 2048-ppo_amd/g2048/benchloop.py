@@ -19,6 +19,9 @@ HBM_PEAK_GBPS = 8000.0
 # the update kernels' HBM bytes per 65 536-row minibatch from the committed PMC passes of this build
 # (FETCH_SIZE / WRITE_SIZE, tools/pmc_train.sh -> tools/summarize_profile.py)
 UPDATE_HBM = "profiles/r05m/train/update_hbm.json"
+# the GameURM update's HBM bytes (every dispatch of one update, tools/urm_update_pmc.py under FETCH /
+# WRITE passes -> tools/urm_update_hbm.py)
+URM_UPDATE_HBM = "profiles/r06b/urm_update_hbm.json"
 
 
 def mlp_flops_per_sample(h: int = 196, obs: int = 48, layers: int = 2, heads: int = 5) -> dict:
@@ -183,5 +186,38 @@ def bench_urm(args, rank: int, world: int, dev) -> dict:
                          "iters": iters,
                          "kernel_paths": paths, "fallbacks": fallbacks,
                          "phase_ms": {k: round(v, 3) for k, v in phases.items()},
-                         "minibatch": args.train_batch, "loss": mt["loss"], "entropy": mt["entropy"]}
+                         "minibatch": args.train_batch, "loss": mt["loss"], "entropy": mt["entropy"],
+                         "roofline": urm_update_roofline(c, args.envs * T, args.train_batch, phases.get("update_ms"),
+                                                         flops_tok)}
     return out
+
+
+def urm_update_roofline(c, rows: int, minibatch: int, update_ms, flops_tok: float) -> dict:
+    """The GameURM update phase (one GPU's share of one train iteration) against both peaks.
+    FLOP basis per token: the forward of every loop (flops_tok: projections 2 (4 h^2 + 3 inter h) and
+    the 16-key attention products 2 x 2 x 16 h per layer application), the backward of the gradient
+    loops (2 x forward x (loops - truncated) / loops: input and weight gradients) and the KL
+    re-forward (one forward): flops_tok x (2 + 2 (L - Lt) / L); 16 tokens per sample, every sample of
+    the iteration (no up-sampling in this leg).  HBM: the PMC bytes of one update (URM_UPDATE_HBM)
+    over the update phase's wall time."""
+    if not update_ms:
+        return {}
+    L_, Lt = c.num_loops, c.num_truncated_loops
+    ftok = flops_tok * (2 + 2 * (L_ - Lt) / L_)
+    ach = ftok * 16 * rows / (update_ms * 1e-3) / 1e12
+    roof = {"update": {"bound": "mfma", "achieved": ach, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                       "frac": ach / MFMA_BF16_PEAK_TFLOPS, "flop_per_token": ftok, "tokens": 16 * rows,
+                       "update_ms": update_ms}}
+    try:
+        import json
+        from pathlib import Path
+        hb = json.loads((Path(__file__).resolve().parents[2] / URM_UPDATE_HBM).read_text())
+        if hb.get("minibatch") == minibatch and hb.get("rows") == rows:
+            a = hb["bytes_per_update"] / (update_ms * 1e-3) / 1e9
+            roof["update_hbm"] = {"bound": "hbm", "achieved": a, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                  "frac": a / HBM_PEAK_GBPS, "traffic_per_update": hb["bytes_per_update"],
+                                  "top_kernels": {k: v["hbm_bytes"] for k, v in list(hb["kernels"].items())[:6]},
+                                  "traffic_source": URM_UPDATE_HBM}
+    except (OSError, ValueError, KeyError):
+        pass
+    return roof

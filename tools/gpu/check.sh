@@ -9,6 +9,7 @@
 #                                           SQ passes of the one-launch forward
 #   TAG=r04x bash tools/gpu/check.sh full   every GPU test, smoke, the default bench line
 #   TAG=r06a bash tools/gpu/check.sh dist   stale-memory detector of the update, the 2-rank and RCCL tests
+#   TAG=r06b bash tools/gpu/check.sh urmhbm the GameURM update's HBM bytes (-> urm_update_hbm.json)
 #   TAG=r05a bash tools/gpu/check.sh muon   Muon: its tests, the MUON_TRACE build (make trace) at 13 and 8
 #                                           parts (phase clocks + bound checks), HIP-event timing
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -66,6 +67,16 @@ muon)
 dist)
   run_tests $O/stale.log 400 tests/test_gpu_stale_reads.py
   run_tests $O/dist.log 400 tests/test_gpu_dist.py tests/test_gpu_rccl.py
+  ;;
+urmhbm)
+  # the GameURM update's FETCH / WRITE bytes between tools/urm_update_pmc.py's markers
+  P=gpurun_out/purmhbm_$TAG; mkdir -p $P
+  for c in FETCH_SIZE WRITE_SIZE; do
+    n=$(echo $c | cut -d_ -f1 | tr A-Z a-z)
+    timeout -s KILL 300 rocprofv3 --pmc $c -T --output-format csv -d $P/$n -o run -- python3 tools/urm_update_pmc.py > $P/$n.log 2>&1
+    rc=$?; echo "$c rc=$rc"; tail -1 $P/$n.log; fatal $rc $c; [ $rc -eq 0 ] || exit 1
+  done
+  python3 tools/urm_update_hbm.py $P $O/urm_update_hbm.json
   ;;
 full)
   run_tests $O/tests.log 700 tests
