@@ -415,7 +415,8 @@ __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__r
 __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ boards, int64_t n, int64_t steps,
                                                            uint4 *__restrict__ tb, uint8_t *__restrict__ ta,
                                                            int32_t *__restrict__ tp, uint32_t *__restrict__ tpot,
-                                                           uint8_t *__restrict__ tf, RngArgs rng) {
+                                                           uint8_t *__restrict__ tf, RngArgs rng,
+                                                           uint32_t *__restrict__ ticket = nullptr) {
     // kRow12 then kLine12; every 4-bit-masked index of either table stays inside (kRolloutLdsWords)
     __shared__ __attribute__((aligned(16))) uint32_t s_row[kRolloutLdsWords];
     stage_row_table(s_row);
@@ -468,6 +469,21 @@ __global__ __launch_bounds__(1024) void env_rollout_kernel(uint4 *__restrict__ b
         }
         if (t < steps) rollout_step<false>(s, s_row, tr, rng.seed, pair + 2u, env);
         boards[i] = s.b;
+    }
+    if (ticket) {
+        // g2048_env_rollout_random_adv: the device counter advances by `steps` once every block has
+        // read it (each block read it before its boards, i.e. before it arrives here): the last block
+        // to arrive adds and puts the ticket back to zero -- no counter-bump kernel between launches.
+        // Relaxed: every block's counter read was consumed long before its arrival, the next launch
+        // sees the add across the kernel boundary, and an agent-scope release here would write back
+        // L2 -- with this launch's records in it (measured +6 us per launch with acq_rel)
+        __syncthreads();
+        if (threadIdx.x == 0 &&
+            __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u) {
+            __hip_atomic_fetch_add(const_cast<uint64_t *>(rng.counter_dev), (uint64_t)steps, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -1532,9 +1548,29 @@ int g2048_env_step(g2048_stream_t stream, const int8_t *boards_in, int8_t *board
     return launch_status();
 }
 
+static int rollout_launch(g2048_stream_t stream, int8_t *boards, int64_t n, int64_t steps, int8_t *traj_boards,
+                          uint8_t *traj_actions, int32_t *traj_points, int8_t *traj_pot, uint8_t *traj_flags,
+                          const g2048_rng *rng, uint32_t *ticket);
+
 int g2048_env_rollout_random(g2048_stream_t stream, int8_t *boards, int64_t n, int64_t steps, int8_t *traj_boards,
                              uint8_t *traj_actions, int32_t *traj_points, int8_t *traj_pot, uint8_t *traj_flags,
                              const g2048_rng *rng) {
+    return rollout_launch(stream, boards, n, steps, traj_boards, traj_actions, traj_points, traj_pot, traj_flags, rng,
+                          nullptr);
+}
+
+int g2048_env_rollout_random_adv(g2048_stream_t stream, int8_t *boards, int64_t n, int64_t steps, int8_t *traj_boards,
+                                 uint8_t *traj_actions, int32_t *traj_points, int8_t *traj_pot, uint8_t *traj_flags,
+                                 const g2048_rng *rng, uint32_t *ticket) {
+    if (!rng || !rng->counter_dev || !ticket || ((uintptr_t)rng->counter_dev & 7u) || ((uintptr_t)ticket & 3u))
+        return G2048_EINVAL;
+    return rollout_launch(stream, boards, n, steps, traj_boards, traj_actions, traj_points, traj_pot, traj_flags, rng,
+                          ticket);
+}
+
+static int rollout_launch(g2048_stream_t stream, int8_t *boards, int64_t n, int64_t steps, int8_t *traj_boards,
+                          uint8_t *traj_actions, int32_t *traj_points, int8_t *traj_pot, uint8_t *traj_flags,
+                          const g2048_rng *rng, uint32_t *ticket) {
     // n < 2^28: a lane's byte offset into a trajectory row (16 * board id) fits the 32-bit saddr offset
     if (n < 0 || n >= (int64_t(1) << 28) || steps < 0 || !rng || rng->mode != G2048_RNG_PHILOX) return G2048_EINVAL;
     if (n == 0 || steps == 0) return G2048_OK;
@@ -1549,7 +1585,7 @@ int g2048_env_rollout_random(g2048_stream_t stream, int8_t *boards, int64_t n, i
     grid = grid > 256 ? 256 : grid;
     hipLaunchKernelGGL(env_rollout_kernel, dim3((unsigned)grid), dim3((unsigned)threads), 0, (hipStream_t)stream,
                        (uint4 *)boards, n, steps, (uint4 *)traj_boards, traj_actions, traj_points, (uint32_t *)traj_pot,
-                       traj_flags, rng_args(rng));
+                       traj_flags, rng_args(rng), ticket);
     return launch_status();
 }
 

@@ -24,6 +24,7 @@ RTG_STATE_DOUBLES = 8
 
 EXPORTED = (
     "g2048_mt_state_words", "g2048_mt_seed", "g2048_env_reset", "g2048_env_step", "g2048_env_rollout_random",
+    "g2048_env_rollout_random_adv",
     "g2048_preview_points", "g2048_legal_mask",
     "g2048_obs_encode", "g2048_info_deltas", "g2048_sample_actions", "g2048_rtg_prepare", "g2048_reward_rtg_workspace_bytes",
     "g2048_reward_rtg", "g2048_reward_rtg_ex", "g2048_rtg_finalize", "g2048_build_info", "g2048_episode_scan",
@@ -209,6 +210,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         "g2048_env_reset": (ctypes.c_int, [vp, vp, vp, vp, i64, rp]),
         "g2048_env_step": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, rp, u32]),
         "g2048_env_rollout_random": (ctypes.c_int, [vp, vp, i64, i64, vp, vp, vp, vp, vp, rp]),
+        "g2048_env_rollout_random_adv": (ctypes.c_int, [vp, vp, i64, i64, vp, vp, vp, vp, vp, rp, vp]),
         "g2048_preview_points": (ctypes.c_int, [vp, vp, vp, i64]),
         "g2048_legal_mask": (ctypes.c_int, [vp, vp, vp, i64]),
         "g2048_obs_encode": (ctypes.c_int, [vp, vp, vp, i32, i64]),
@@ -403,12 +405,19 @@ def env_step(boards_in, boards_out, actions_in, actions_out, points, max_tile, p
         _dev(flags, torch.uint8, "flags"), n, ctypes.byref(rng), options), "g2048_env_step")
 
 
-def env_rollout_random(boards, steps, traj_boards, traj_actions, traj_points, traj_pot, traj_flags, rng: Rng):
-    _check(load().g2048_env_rollout_random(
-        _stream(boards), _dev(boards, torch.int8, "boards"), boards.shape[0], steps,
-        _dev(traj_boards, torch.int8, "traj_boards"), _dev(traj_actions, torch.uint8, "traj_actions"),
-        _dev(traj_points, torch.int32, "traj_points"), _dev(traj_pot, torch.int8, "traj_pot"),
-        _dev(traj_flags, torch.uint8, "traj_flags"), ctypes.byref(rng)), "g2048_env_rollout_random")
+def env_rollout_random(boards, steps, traj_boards, traj_actions, traj_points, traj_pot, traj_flags, rng: Rng,
+                       ticket=None):
+    """ticket (a zero-filled int32 device word): the launch also advances rng's device counter by `steps`
+    (g2048_env_rollout_random_adv: no counter-bump kernel between consecutive launches)."""
+    args = (_stream(boards), _dev(boards, torch.int8, "boards"), boards.shape[0], steps,
+            _dev(traj_boards, torch.int8, "traj_boards"), _dev(traj_actions, torch.uint8, "traj_actions"),
+            _dev(traj_points, torch.int32, "traj_points"), _dev(traj_pot, torch.int8, "traj_pot"),
+            _dev(traj_flags, torch.uint8, "traj_flags"), ctypes.byref(rng))
+    if ticket is None:
+        _check(load().g2048_env_rollout_random(*args), "g2048_env_rollout_random")
+    else:
+        _check(load().g2048_env_rollout_random_adv(*args, _dev(ticket, torch.int32, "ticket")),
+               "g2048_env_rollout_random_adv")
 
 
 def preview_points(boards, points4):

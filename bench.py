@@ -10,9 +10,9 @@ with their status.  Workload (BASELINE.md /
 SURVEY.md §8d): `--envs` independent 4x4 boards per GPU, uniform random legal actions (Philox
 keyed by 0x2048 + rank), auto-reset on done.  One bench "step" = one launch of the fused
 rollout kernel `env_rollout_kernel` = `--chunk` consecutive env steps of every board, writing the
-full per-step trajectory record (board, action, points, potentials, flags); the launch and its
-device-side Philox counter bump are replayed from a hipGraph (host issue cost: one graph launch per
-step).  value = total legal transitions of all ranks / max-over-ranks wall time of the K timed
+full per-step trajectory record (board, action, points, potentials, flags); the launch (which also
+advances its device-side Philox counter, in its last workgroup) is replayed from a hipGraph (host issue
+cost: one graph launch per step).  value = total legal transitions of all ranks / max-over-ranks wall time of the K timed
 steps (weak scaling: the boards per GPU are fixed; the envs are independent, so no data-path
 collective exists).
 
@@ -171,11 +171,14 @@ class RolloutBench:
         # replayed from a hipGraph, so the host issue cost per bench step is one graph launch
         self.ctr = torch.ones(1, dtype=torch.int64, device=dev)
         self.rng = L.make_rng(L.RNG_PHILOX, self.env.seed, 0, self.env.env_base, counter_dev=self.ctr)
+        # the launch advances the counter itself (its last workgroup: g2048_env_rollout_random_adv), so
+        # consecutive launches in a graph have no counter-bump kernel between them
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graph = None
 
     def launch(self):
-        self.L.env_rollout_random(self.env.boards, self.chunk, self.tb, self.ta, self.tp, self.tpot, self.tf, self.rng)
-        self.ctr.add_(self.chunk)
+        self.L.env_rollout_random(self.env.boards, self.chunk, self.tb, self.ta, self.tp, self.tpot, self.tf, self.rng,
+                                  ticket=self.ticket)
 
     def capture(self, per_graph=1):
         """Two hipGraphs: `per_graph` consecutive launches (each with its counter bump) and a single

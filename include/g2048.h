@@ -110,6 +110,15 @@ int g2048_env_rollout_random(g2048_stream_t stream, int8_t *boards, int64_t n, i
                              int8_t *traj_boards, uint8_t *traj_actions, int32_t *traj_points,
                              int8_t *traj_pot, uint8_t *traj_flags, const g2048_rng *rng);
 
+/* g2048_env_rollout_random that also advances the Philox counter base: *rng->counter_dev += steps
+   once the whole launch has read it (the last workgroup to finish adds; `ticket` is a ZERO-FILLED
+   uint32 device word, left zero again by every launch).  rng->counter_dev is required (8-byte
+   aligned, writable).  A graph of K such launches replays K consecutive chunks with no counter-bump
+   kernel between them (bench.py's rollout leg). */
+int g2048_env_rollout_random_adv(g2048_stream_t stream, int8_t *boards, int64_t n, int64_t steps, int8_t *traj_boards,
+                                 uint8_t *traj_actions, int32_t *traj_points, int8_t *traj_pot, uint8_t *traj_flags,
+                                 const g2048_rng *rng, uint32_t *ticket);
+
 /* Game2048.preview_move_rewards (game.py:167-184): points4[i] = merge points of UP, DOWN, LEFT,
    RIGHT on board i, 0 for an illegal direction.  points4 is int32 [N][4], 16-B aligned. */
 int g2048_preview_points(g2048_stream_t stream, const int8_t *boards, int32_t *points4, int64_t n);

@@ -218,20 +218,21 @@ def test_rollout_kernel_trajectories_match_oracle(dev, n, steps):
     assert (rec["flags"] & 0x80).sum() > 0  # episodes ended and were reset inside the launch
 
 
-@pytest.mark.parametrize("chunk,per_graph,k", [(5, 8, 11), (64, 8, 8)])
-def test_bench_graph_replay_matches_oracle(dev, chunk, per_graph, k):
+@pytest.mark.parametrize("n,chunk,per_graph,k", [(1000, 5, 8, 11), (1000, 64, 8, 8), (65536, 8, 8, 3)])
+def test_bench_graph_replay_matches_oracle(dev, n, chunk, per_graph, k):
     """bench.py's timed region: k rollout launches replayed from hipGraphs of `per_graph` launches
-    (plus 1-launch graphs for the remainder), the Philox counter bumped on the device inside the
-    graph, equal one oracle rollout of k * chunk steps; the last launch's records match its tail."""
+    (plus 1-launch graphs for the remainder), each launch advancing the device Philox counter itself
+    (g2048_env_rollout_random_adv: its last workgroup adds `chunk`, the ticket word is left zero;
+    65 536 boards = the bench's 256-workgroup grid), equal one oracle rollout of k * chunk steps; the
+    last launch's records match its tail."""
     from bench import RolloutBench
-    n = 1000
     rb = RolloutBench(n, chunk, 0, dev)
     rb.capture(per_graph)  # runs one eager warm-up launch, then captures
     torch.cuda.synchronize()
     init, ctr0 = rb.env.boards.cpu().numpy().copy(), int(rb.ctr.item())
     rb.run(k)
     torch.cuda.synchronize()
-    assert int(rb.ctr.item()) == ctr0 + k * chunk
+    assert int(rb.ctr.item()) == ctr0 + k * chunk and int(rb.ticket.item()) == 0
     ob, rec = O.random_rollout_record(init, k * chunk, rb.env.seed, step0=ctr0, env_base=rb.env.env_base)
     assert np.array_equal(rb.env.boards.cpu().numpy(), ob)
     assert np.array_equal(rb.tb.cpu().numpy(), rec["boards"][-chunk:])
