@@ -104,9 +104,12 @@ __device__ __forceinline__ void stats_block(const StatsArgs &a, const float *kl,
     float(*red)[256] = reinterpret_cast<float(*)[256]>(lds);
     float ks = 0.0f, km = -INFINITY;
     if (tid < 256) {
+        // sc1 loads (L2-served, past this CU's L1): the partials were handed off by other workgroups
+        // (MI355X_MICROARCH.md hand-off table, row 1); the same bits as plain loads after an acquire
+        float *klw = const_cast<float *>(kl);
         for (int b = tid; b < kl_rows; b += 256) {
-            ks += kl[2 * b];
-            km = fmaxf(km, kl[2 * b + 1]);
+            ks += __hip_atomic_load(klw + 2 * b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            km = fmaxf(km, __hip_atomic_load(klw + 2 * b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         }
         red[0][tid] = ks;
         red[1][tid] = km;

@@ -418,33 +418,32 @@ __global__ __launch_bounds__(kFpThreads) void mlp_pass_kernel(FpArgs a) {
 #pragma unroll
         for (int k = 0; k < NP; k++) red[wave * NP + k] = vals[k];
     __syncthreads();
+    const bool fold = !TRAIN && a.st.stats;  // the KL pass with the minibatch statistics folded in
     if (tid < NP) {
         float t = red[tid];
         for (int w = 1; w < kFpThreads / 64; w++) t = (!TRAIN && tid == 1) ? fmaxf(t, red[w * NP + tid]) : t + red[w * NP + tid];
-        a.part[(int64_t)blockIdx.x * NP + tid] = t;
+        float *dst = a.part + (int64_t)blockIdx.x * NP + tid;
+        if (fold) __hip_atomic_store(dst, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: the hand-off below
+        else *dst = t;
     }
-    if (!TRAIN && a.st.stats) {
+    if (fold) {
         // the last block to finish reduces every block's {sum, max} and accumulates the minibatch
-        // statistics (g2048_ppo_stats folded in): cdna_hip_programming.md Guideline 16's counter
-        // form -- plain partial stores, every wave drains, one release + ticket; the last arriver
-        // acquires, reads with plain loads and puts the ticket back to zero for the next launch
+        // statistics (g2048_ppo_stats folded in).  The hand-off is MI355X_MICROARCH.md's table row 1
+        // (one workgroup per CU here): partials stored sc1, every wave drains, a barrier, ONE lane's
+        // relaxed agent-scope ticket add; the block whose add came last (told by its returned value)
+        // reads the partials with sc1 loads behind a barrier (stats_block) and puts the ticket back to
+        // zero.  Round 6: no agent release / acquire fence any more -- the release wrote back the XCD's
+        // L2 in every one of the 256 blocks and the acquire invalidated L1 (~1.7 us each per the guide)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         int *flag = reinterpret_cast<int *>(smem + 4096);
         if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const uint32_t k = __hip_atomic_fetch_add((__attribute__((address_space(1))) uint32_t *)a.st.sync, 1u,
                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             *flag = k == gridDim.x - 1u;
         }
         __syncthreads();
         if (!*flag) return;
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
         P::stats_block(a.st, a.part, (int)gridDim.x, smem, tid);
     }
 }
