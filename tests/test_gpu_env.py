@@ -238,6 +238,16 @@ def test_bench_graph_replay_matches_oracle(dev, n, chunk, per_graph, k):
     assert np.array_equal(rb.tb.cpu().numpy(), rec["boards"][-chunk:])
     assert np.array_equal(rb.tf.cpu().numpy(), rec["flags"][-chunk:])
     assert np.array_equal(rb.tp.cpu().numpy(), rec["points"][-chunk:])
+    # the same k launches as ONE k-launch graph (bench.py's timed region, capture_exact)
+    rb.capture_exact(k)
+    init, ctr0 = rb.env.boards.cpu().numpy().copy(), int(rb.ctr.item())
+    rb.run(k)
+    torch.cuda.synchronize()
+    assert int(rb.ctr.item()) == ctr0 + k * chunk and int(rb.ticket.item()) == 0
+    ob, rec = O.random_rollout_record(init, k * chunk, rb.env.seed, step0=ctr0, env_base=rb.env.env_base)
+    assert np.array_equal(rb.env.boards.cpu().numpy(), ob)
+    assert np.array_equal(rb.tb.cpu().numpy(), rec["boards"][-chunk:])
+    assert np.array_equal(rb.tpot.cpu().numpy(), rec["pot"][-chunk:])
 
 
 def test_auto_reset_matches_oracle(dev):

@@ -32,7 +32,8 @@ env)
     PMC_ARGS="--steps 4 --warmup 1 --cpu-seconds 0 --single-steps 0 --train-iters 0 --urm-steps 0 --sweep=" \
     bash tools/profile.sh > $O/prof.log 2>&1
   rc=$?; echo "prof rc=$rc"; tail -6 $O/prof.log; fatal $rc prof
-  python3 tools/summarize_profile.py gpurun_out/prof_$TAG $O/summary > /dev/null 2>&1
+  # the PMC passes ran bench.py at its default --chunk (1024 steps per launch since round 6)
+  PMC_CHUNK=1024 python3 tools/summarize_profile.py gpurun_out/prof_$TAG $O/summary > /dev/null 2>&1
   python3 -c "import json; d=json.load(open('$O/summary/pmc_env_rollout.json')); print({k: d[k] for k in ('valu_per_wave_step', 'lds_per_wave_step', 'hbm_bytes_per_env_step')})"
   ;;
 fused)
