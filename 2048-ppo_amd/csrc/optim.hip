@@ -1312,15 +1312,17 @@ __device__ __forceinline__ void mc_matrix(char *smem, float *red, const MuonArgs
     const float lr_pre = args.lr[mt.lr_index];
     ns_square_mc<N>(sX, sG, args, mat, part, np, wave, lane, (uint32_t)np);
     // the last part through here puts the matrix's counters back to zero for the next launch (no
-    // memset node per step): every other part has finished all its polls when it counts in.  The
-    // done add is a release (this part's counter adds, same thread, happen before it) and the last
-    // arriver acquires before its reset stores, so the reset is ordered after every part's adds by
-    // the memory model, not by the order L2 happens to apply atomics in.  (By the last wave, whose
-    // round trip overlaps the other waves' epilogue.)
+    // memset node per step): every other part has finished all its polls when it counts in.  Every
+    // exchange-counter add of every part was OBSERVED complete before that part's done add: each
+    // part's polling wave saw the counter reach np x (hand-offs so far), its own add included, and a
+    // barrier separates that poll from the done add; the last part's poll (the last hand-off) came
+    // before every done add likewise.  So the reset stores of the part whose done add comes last
+    // (told by its returned value) follow every add and every poll with relaxed atomics alone.
+    // Round 6: no agent release / acquire here any more -- the release wrote back the XCD's L2
+    // (~1.7-6.5 us, MI355X_MICROARCH.md price list) on the last wave of every part.
     if (tid == kMuonThreads - 64) {
         gu32_t *done = line + 2;
-        if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(np - 1)) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(np - 1)) {
             __hip_atomic_store(line, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }

@@ -501,21 +501,30 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
     int wo[KS];
 #pragma unroll
     for (int s = 0; s < KS; s++) wo[s] = LinW<KS>::frag(t, g, s);
-    for (int64_t bd = (int64_t)blockIdx.x * (kThreads / 64) + wave; bd < boards; bd += (int64_t)gridDim.x * (kThreads / 64)) {
-        const int64_t r = bd * 16 + t;
-        const uint16_t *xr = in + r * K;
-        bf16x8 fb[KS];
+    // the board's B fragments (its 16 token rows of `in`), K % 4 == 0 with a 4-element tail
+    auto load_b = [&](int64_t board, bf16x8 (&f)[KS]) {
+        const uint16_t *xr = in + (board * 16 + t) * K;
 #pragma unroll
         for (int s = 0; s < KS; s++) {
             const int kk = 32 * s + 8 * g;
             uint4 v = make_uint4(0u, 0u, 0u, 0u);
             if (kk + 8 <= K) {
                 v = *reinterpret_cast<const uint4 *>(xr + kk);
-            } else if (kk < K) {  // K % 4 == 0: a 4-element tail
+            } else if (kk < K) {
                 const uint2 tl = *reinterpret_cast<const uint2 *>(xr + kk);
                 v = make_uint4(tl.x, tl.y, 0u, 0u);
             }
-            fb[s] = __builtin_bit_cast(bf16x8, v);
+            f[s] = __builtin_bit_cast(bf16x8, v);
+        }
+    };
+    const int64_t bstride = (int64_t)gridDim.x * (kThreads / 64);
+    int64_t bd = (int64_t)blockIdx.x * (kThreads / 64) + wave;
+    bf16x8 fb[KS];
+    if (bd < boards) load_b(bd, fb);
+    for (; bd < boards; bd += bstride) {
+        const int64_t r = bd * 16 + t;
+        if constexpr (EPI == EPI_STORE) {
+            if (bd != (int64_t)blockIdx.x * (kThreads / 64) + wave) load_b(bd, fb);  // (the first: above)
         }
         f32x4 acc[CT];
 #pragma unroll
@@ -534,6 +543,13 @@ __global__ __launch_bounds__(kThreads) void urm_linear_kernel(const uint16_t *__
 #pragma unroll
             for (int s = 0; s < KS; s++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ct & 1][s], fb[s], acc[ct], 0, 0, 0);
         }
+        // round 6: the next board's fragments are requested now, so their HBM latency runs under this
+        // board's epilogue (each wave used to wait for its loads at the top of every board).  The
+        // RMSNorm / SwiGLU epilogues gain (gate_up + SwiGLU-conv training 184.7 -> 170.9 us, o_proj /
+        // down_proj -1.5 %); the plain store epilogue -- its LDS output tile, short epilogue -- lost 4 %
+        // and keeps the loads at the top (profiles/r06j/ab_urm_linear.log)
+        constexpr bool kPrefetch = EPI != EPI_STORE;
+        if (kPrefetch && bd + bstride < boards) load_b(bd + bstride, fb);
         // lane (t, g), tile ct: acc[ct][i] = Y[r][16 ct + 4 g + i]
         if constexpr (EPI == EPI_STORE) {
             // the board's 16 x N outputs are one contiguous span of y: stage them in this wave's LDS
@@ -731,7 +747,13 @@ int launch_lin(hipStream_t s, const uint16_t *in, const uint16_t *w, int64_t row
     const size_t conv = (EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_T) ? (size_t)16 * CT * 2 * 4 : 0;  // w + b per channel
     const size_t lds = (size_t)16 * CT * LinW<KS>::PITCH * 2 + std::max((size_t)(kThreads / 64) * tile, conv);
     int64_t grid = ((rows >> 4) + (kThreads / 64) - 1) / (kThreads / 64);
-    grid = grid > 1024 ? 1024 : grid;  // persistent over boards; W staged once per block
+    // persistent over boards, W staged once per block.  The cap is per instance, from a sweep of
+    // 512..3072 blocks at 65 536 boards (profiles/r06j/grid_sweep.log): the h 64 qkv forward is 17 %
+    // faster at 768 (115.6 vs 138.6 us), the SwiGLU training epilogue that also stores gu 15 % faster
+    // at 3072 (265.7 vs 313.0 us: more waves in flight for its two output streams); every other
+    // instance is within noise of 1024.
+    const int64_t cap = (EPI == EPI_STORE && CT == 12) ? 768 : (EPI == EPI_SWIGLU_T && xb) ? 3072 : 1024;
+    grid = grid > cap ? cap : grid;
     hipLaunchKernelGGL((urm_linear_kernel<KS, CT, EPI>), dim3((unsigned)grid), dim3(kThreads), lds, s, in, w, rows, K, N,
                        inter, y, x, emb, xb, eps, cw, cb, rstd, wt);
     return launch_status();
