@@ -363,8 +363,10 @@ __device__ __forceinline__ void rollout_step(RolloutLane &s, const uint32_t *__r
     const uint32_t rp = r3 ? ra[3] : r2 ? ra[2] : r1 ? ra[1] : ra[0], cp = c3 ? ca[3] : c2 ? ca[2] : c1 ? ca[1] : ca[0];
     const uint32_t rq = rp + v * ((uint32_t)(kW12 >> (16u * col)) & 0xFFFFu);
     const uint32_t cq = cp + v * ((uint32_t)(kW12 >> (16u * row)) & 0xFFFFu);
-    // the spawn row / column entries before (read again: cheaper than selecting among f0..g3) and after
-    const uint32_t fp = lds_half(tab, rp), gp = lds_half(tab, cp), fq = lds_half(tab, rq), gq = lds_half(tab, cq);
+    // the spawn row / column entries after the spawn (the last LDS round trip of the step: two reads)
+    // and before it (selected among f0..g3, which have landed by now)
+    const uint32_t fq = lds_half(tab, rq), gq = lds_half(tab, cq);
+    const uint32_t fp = r3 ? f3 : r2 ? f2 : r1 ? f1 : f0, gp = c3 ? g3 : c2 ? g2 : c1 ? g1 : g0;
     *tr.a = (uint8_t)a;
     *tr.p = (int32_t)pts;
     // line sums of the pre-spawn board; the next board's swap the spawn's row and column entries
