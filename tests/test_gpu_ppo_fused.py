@@ -476,6 +476,80 @@ def test_fused_update_matches_reference_step(dev):
 MUON_COS196 = {"stem.0.weight": 0.99, "backbone.0.mlp.0.weight": 0.98, "backbone.1.mlp.0.weight": 0.975,
                "action_head.weight": 0.87, "value_head.weight": 0.9999}
 
+# eight-step pin (test_fused_update_matches_reference_eight_steps_h196): absolute floors from the first
+# MI355X run (profiles/r06l/e4.log; fused / autocast / fp32 move cosines to the reference: stem 0.99867
+# / 0.99831 / 0.99964, backbone.0 0.99644 / 0.99564 / 0.99904, backbone.1 0.99551 / 0.99351 / 0.99887,
+# action_head 0.96834 / 0.91987 / 0.98116, value_head 1.0; AdamW tensors >= 0.99562; Muon norm ratios
+# within 0.1 %; statistics within 0.05 %; final policy mean KL(ref || run) 3.1e-6 / 3.9e-5 / 1.7e-6,
+# largest value difference 2.5e-3 / 3.8e-3 / 1.2e-3)
+E4_COS = {"stem.0.weight": 0.995, "backbone.0.mlp.0.weight": 0.99, "backbone.1.mlp.0.weight": 0.99,
+          "action_head.weight": 0.95, "value_head.weight": 0.9999}
+E4_COS_ADAMW = 0.99
+E4_NORM_TOL = 0.02
+E4_STAT_TOL = 5e-3
+E4_KL = 2e-5
+E4_DV = 0.01
+
+
+def _update196_runs(dev, u, orders, epochs):
+    """update196's inputs through the shipped update (FusedPPOUpdater on the captured offset path,
+    FusedMuonAdamW on 13 CUs per h x h matrix) and, beside it, torch's bf16 autocast of the same step
+    (PPOUpdater + torch.optim.Muon / AdamW) and the fp32 step in device reduction order; each epoch
+    takes the reference's recorded DataLoader order (`orders[e]`, indices into the fixture's rows).
+    Returns the three runs' statistics, parameter moves (final - init, float64) and final models."""
+    from g2048.dist import GradBucket
+    from g2048.fastmlp import FusedPPOUpdater
+    from g2048.optim import FusedMuonAdamW, build_optimizer
+    from g2048.ppo import PPOConfig, PPOUpdater
+    import agent
+    n, bs = len(u["actions"]), int(u["batch_size"])
+    lr, clr, b1, b2, wd, beta, critic = (float(x) for x in u["hparams"])
+    legal = np.array([sum(1 << a for a in range(4) if not u["invalid"][i, a]) for i in range(n)], np.uint8)
+    raw = {"boards": u["boards"].astype(np.int8), "actions": u["actions"].astype(np.uint8), "legal": legal,
+           "logp": u["old_logprobs"], "adv": u["advantage"], "ret": u["future_reward"]}
+    data = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in raw.items()}
+    init = {k[len("init::"):]: torch.from_numpy(u[k]) for k in u.files if k.startswith("init::")}
+    moves, stats, models = {}, {}, {}
+    for mode in ("fused", "autocast", "fp32"):
+        m = agent.GameMLP(agent.MLPConfig(hidden_dim=196, num_layers=2, dropout=0.0)).to(dev)
+        m.load_state_dict(init)
+        if mode == "fused":
+            opt = FusedMuonAdamW(m, lr, clr, b1, b2, wd)
+            assert opt.supported and opt._cfg.parts == 13
+            bo = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
+            up = FusedPPOUpdater(m, opt, PPOConfig(batch_size=bs, critic=critic, epochs=epochs), GradBucket(bo),
+                                 graph=True)
+        else:
+            opt = build_optimizer(m, lr, clr, b1, b2, wd, schedule=False)
+            pc = PPOConfig(batch_size=bs, critic=critic, epochs=epochs,
+                           amp_dtype=torch.bfloat16 if mode == "autocast" else None)
+            up = PPOUpdater(m, opt, pc, GradBucket(m.parameters()))
+        seq = iter([torch.as_tensor(np.asarray(o, np.int64), device=dev) for o in orders])
+
+        def recorded(m_total, out=None):  # the reference's minibatches, epoch after epoch
+            r = next(seq)
+            assert r.numel() == m_total
+            return r if out is None else out[:m_total].copy_(r)
+        up._epoch_perm = recorded
+        stats[mode] = {k: float(v) for k, v in up.update(data, beta, _enc).items()}
+        if mode == "fused":
+            assert up._og is not None and up.wgrad_one_launch  # the captured offset path ran
+        moves[mode] = {k: (v.detach().cpu() - init[k]).reshape(-1).double() for k, v in m.state_dict().items()}
+        up.close()
+        models[mode] = m
+    return stats, moves, models, init
+
+
+def _enc(b):
+    from g2048 import _lib as L
+    o = torch.empty(b.shape[0], 48, dtype=torch.float32, device=b.device)
+    L.obs_encode(b.contiguous(), o)
+    return o
+
+
+def _cos(a, b):
+    return float(F.cosine_similarity(a, b, dim=0))
+
 
 def test_fused_update_matches_reference_step_h196(dev):
     """The shipped update at the README / bench policy shape against the reference itself
@@ -484,7 +558,7 @@ def test_fused_update_matches_reference_step_h196(dev):
     norms ~3.6 -- Muon + AdamW at fixed learning rates).  Run as the trainer runs it: FusedPPOUpdater on
     the captured offset path (one-launch passes, fused backward, one-launch weight gradients) with
     FusedMuonAdamW on 13 CUs per h x h matrix.  The two minibatches are the reference's (the data is
-    fed in its DataLoader order and the device permutation is the identity).
+    fed in its DataLoader order).
 
     Bounds are derived from the spread measured beside it on the same inputs: torch's bf16 autocast of
     the same step (PPOUpdater + torch.optim.Muon / AdamW) and the fp32 step in device reduction order
@@ -493,50 +567,9 @@ def test_fused_update_matches_reference_step_h196(dev):
     MUON_COS196, 1 - cos(fused, ref) <= 2 (1 - cos(autocast, ref)) + 1e-3 and the move's norm within
     3 %; per AdamW tensor (two Adam steps): cosine >= 0.99 and within 2 x the autocast deviation +
     0.01; statistics within 1 % (grad_norm, loss, value_loss, entropy) of the reference's."""
-    from g2048.dist import GradBucket
-    from g2048.fastmlp import FusedPPOUpdater
-    from g2048.optim import FusedMuonAdamW, build_optimizer
-    from g2048.ppo import PPOConfig, PPOUpdater
-    import agent
     u = golden("update196.npz")
-    order = torch.from_numpy(u["order"]).to(dev)
-    n, bs = len(u["actions"]), int(u["batch_size"])
-    lr, clr, b1, b2, wd, beta, critic = (float(x) for x in u["hparams"])
-    legal = np.array([sum(1 << a for a in range(4) if not u["invalid"][i, a]) for i in range(n)], np.uint8)
-    raw = {"boards": u["boards"].astype(np.int8), "actions": u["actions"].astype(np.uint8), "legal": legal,
-           "logp": u["old_logprobs"], "adv": u["advantage"], "ret": u["future_reward"]}
-    data = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev).index_select(0, order) for k, v in raw.items()}
-
-    def ident(m_total, out=None):  # the reference's minibatches: data already in its DataLoader order
-        r = torch.arange(m_total, device=dev)
-        return r if out is None else out[:m_total].copy_(r)
-
-    def enc(b):
-        from g2048 import _lib as L
-        o = torch.empty(b.shape[0], 48, dtype=torch.float32, device=dev)
-        L.obs_encode(b.contiguous(), o)
-        return o
+    stats, moves, _, init = _update196_runs(dev, u, [u["order"]], 1)
     ref_stats = dict(zip([str(k) for k in u["stat_keys"]], u["stat_vals"]))
-    init = {k[len("init::"):]: torch.from_numpy(u[k]) for k in u.files if k.startswith("init::")}
-    moves, stats = {}, {}
-    for mode in ("fused", "autocast", "fp32"):
-        m = agent.GameMLP(agent.MLPConfig(hidden_dim=196, num_layers=2, dropout=0.0)).to(dev)
-        m.load_state_dict(init)
-        if mode == "fused":
-            opt = FusedMuonAdamW(m, lr, clr, b1, b2, wd)
-            assert opt.supported and opt._cfg.parts == 13
-            bo = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
-            up = FusedPPOUpdater(m, opt, PPOConfig(batch_size=bs, critic=critic), GradBucket(bo), graph=True)
-        else:
-            opt = build_optimizer(m, lr, clr, b1, b2, wd, schedule=False)
-            pc = PPOConfig(batch_size=bs, critic=critic, amp_dtype=torch.bfloat16 if mode == "autocast" else None)
-            up = PPOUpdater(m, opt, pc, GradBucket(m.parameters()))
-        up._epoch_perm = ident
-        stats[mode] = {k: float(v) for k, v in up.update(data, beta, enc).items()}
-        if mode == "fused":
-            assert up._og is not None and up.wgrad_one_launch  # the captured offset path ran
-        moves[mode] = {k: (v.detach().cpu() - init[k]).reshape(-1).double() for k, v in m.state_dict().items()}
-        up.close()
     rows, bad = [], []
     for k in ("loss", "value_loss", "entropy", "grad_norm", "policy_loss", "kl_average"):
         rows.append(f"{k}: ref {ref_stats[k]:.6g} fused {stats['fused'][k]:.6g} autocast {stats['autocast'][k]:.6g} "
@@ -544,13 +577,10 @@ def test_fused_update_matches_reference_step_h196(dev):
         tol = 1e-2 if k in ("loss", "value_loss", "entropy", "grad_norm") else 0.1
         if not math.isclose(stats["fused"][k], ref_stats[k], rel_tol=tol, abs_tol=2e-4):
             bad.append(rows[-1])
-
-    def cos(a, b):
-        return float(F.cosine_similarity(a, b, dim=0))
     for k in moves["fused"]:
         want = torch.from_numpy(u["final::" + k]).reshape(-1).double() - init[k].reshape(-1).double()
         got, ac, f32 = moves["fused"][k], moves["autocast"][k], moves["fp32"][k]
-        c, c_ac, c_32 = cos(got, want), cos(ac, want), cos(f32, want)
+        c, c_ac, c_32 = _cos(got, want), _cos(ac, want), _cos(f32, want)
         ratio = float(got.norm() / want.norm())
         rows.append(f"{k}: cos fused {c:.5f} autocast {c_ac:.5f} fp32 {c_32:.5f}; norm ratio {ratio:.4f}")
         if init[k].ndim >= 2:
@@ -559,6 +589,60 @@ def test_fused_update_matches_reference_step_h196(dev):
             ok = c >= 0.99 and (1 - c) <= 2 * (1 - c_ac) + 1e-2
         if not ok:
             bad.append(rows[-1])
+    print("\n".join(rows))
+    assert not bad, bad
+
+
+def test_fused_update_matches_reference_eight_steps_h196(dev):
+    """The multi-step pin (tests/golden/update196e4.npz): update196's inputs through FOUR epochs of
+    the reference's two minibatches -- eight consecutive optimizer steps, each epoch in the
+    reference's recorded order -- on the shipped update, beside torch's bf16 autocast and the fp32
+    device step.  What accumulates over the eight steps is measured three ways against the reference:
+    each parameter's total move (cosine, norm ratio), the final policy on the 4 096 boards (mean
+    KL(ref || run) of the masked action distributions, largest value difference; fp32 eval forward
+    of each run's final weights) and the update's mean statistics.  Bounds: relative to the autocast
+    run (the bf16 arithmetic torch itself would use) plus the absolute floors E4_* measured on the
+    first MI355X run."""
+    u, e = golden("update196.npz"), golden("update196e4.npz")
+    stats, moves, models, init = _update196_runs(dev, u, list(e["order"]), int(e["epochs"]))
+    ref_stats = dict(zip([str(k) for k in e["stat_keys"]], e["stat_vals"]))
+    rows, bad = [], []
+    for k in ("loss", "value_loss", "entropy", "grad_norm", "policy_loss", "kl_average"):
+        rows.append(f"{k}: ref {ref_stats[k]:.6g} fused {stats['fused'][k]:.6g} autocast {stats['autocast'][k]:.6g} "
+                    f"fp32 {stats['fp32'][k]:.6g}")
+        tol = E4_STAT_TOL if k in ("loss", "value_loss", "entropy", "grad_norm") else 0.15
+        if not math.isclose(stats["fused"][k], ref_stats[k], rel_tol=tol, abs_tol=2e-4):
+            bad.append(rows[-1])
+    for k in moves["fused"]:
+        want = torch.from_numpy(e["final::" + k]).reshape(-1).double() - init[k].reshape(-1).double()
+        got, ac, f32 = moves["fused"][k], moves["autocast"][k], moves["fp32"][k]
+        c, c_ac, c_32 = _cos(got, want), _cos(ac, want), _cos(f32, want)
+        ratio = float(got.norm() / want.norm())
+        rows.append(f"{k}: cos fused {c:.5f} autocast {c_ac:.5f} fp32 {c_32:.5f}; norm ratio {ratio:.4f}")
+        floor = E4_COS.get(k, E4_COS_ADAMW)
+        ok = c >= floor and (1 - c) <= 2 * (1 - c_ac) + (2e-3 if init[k].ndim >= 2 else 1e-2)
+        if init[k].ndim >= 2:
+            ok = ok and abs(ratio - 1) <= E4_NORM_TOL
+        if not ok:
+            bad.append(rows[-1])
+    boards = torch.from_numpy(u["boards"].astype(np.int8)).to(dev)
+    invalid = torch.from_numpy(u["invalid"]).to(dev)
+    ref_lp = torch.from_numpy(e["logits"]).to(dev).masked_fill(invalid, float("-inf")).log_softmax(-1)
+    ref_v = torch.from_numpy(e["value"]).to(dev)
+    kl = {}
+    for mode, m in models.items():
+        m.eval()
+        with torch.no_grad():
+            lg, v = m(_enc(boards))
+        lp = lg.float().masked_fill(invalid, float("-inf")).log_softmax(-1)
+        p = ref_lp.exp()
+        kl[mode] = float(torch.where(invalid, torch.zeros_like(p), p * (ref_lp - lp)).sum(-1).mean())
+        dv = float((v.reshape(-1).float() - ref_v).abs().max())
+        rows.append(f"final policy {mode}: mean KL(ref || run) {kl[mode]:.3e}, max |value diff| {dv:.3e}")
+        if mode == "fused" and (kl[mode] > E4_KL or dv > E4_DV):
+            bad.append(rows[-1])
+    if kl["fused"] > 2 * kl["autocast"] + 1e-6:
+        bad.append(f"final policy KL fused {kl['fused']:.3e} > 2 x autocast {kl['autocast']:.3e}")
     print("\n".join(rows))
     assert not bad, bad
 

@@ -11,6 +11,14 @@ import torch
 from conftest import golden
 
 
+# bounds of the eight-step CPU pin (test_model_optimize_step_matches_reference_four_epochs_h196): its
+# first run here reproduced the reference bit for bit (every move cosine 1.000000, final logits and
+# values identical: the same torch CPU kernels in the same order); the bounds leave room for another
+# CPU's thread count / vector width changing a reduction order
+COS_E4_CPU = 0.9999
+LOGIT_E4_CPU = 1e-4
+
+
 def _golden_model():
     import agent
     u = golden("update.npz")
@@ -80,6 +88,48 @@ def test_model_optimize_step_matches_reference_update_h196(monkeypatch):
     ref = dict(zip(u["stat_keys"].tolist(), u["stat_vals"].tolist()))
     for k in ("loss", "policy_loss", "entropy_loss", "value_loss", "grad_norm", "entropy"):
         assert math.isclose(stats[k], ref[k], rel_tol=1e-4, abs_tol=1e-6), (k, stats[k], ref[k])
+
+
+def test_model_optimize_step_matches_reference_four_epochs_h196(monkeypatch):
+    """The multi-step pin on CPU (tests/golden/update196e4.npz: update196's inputs through FOUR epochs,
+    eight optimizer steps, each epoch in the reference's recorded order): the restatement's final
+    parameters, statistics and final policy agree with the reference run after eight steps (fp32, the
+    two runs differ in summation order only, which Muon's bf16 Newton-Schulz amplifies step by step)."""
+    import agent
+    import train
+    from g2048.augment import encode_grid
+    from g2048.optim import MultiOptimizer
+    u, e = golden("update196.npz"), golden("update196e4.npz")
+    m = agent.GameMLP(agent.MLPConfig(hidden_dim=196, num_layers=2, dropout=0.0))
+    m.load_state_dict({k[len("init::"):]: torch.from_numpy(u[k]) for k in u.files if k.startswith("init::")})
+    lr, clr, b1, b2, wd, beta, critic = (float(x) for x in u["hparams"])
+    n = len(u["actions"])
+    obs = [encode_grid(u["boards"][i].reshape(4, 4).tolist()) for i in range(n)]
+    moves = [{"game_state": obs[i], "selected_direction": int(u["actions"][i]),
+              "action_mask": u["invalid"][i].tolist(), "advantage": float(u["advantage"][i]),
+              "future_reward": float(u["future_reward"][i]), "policy_logprobs": u["old_logprobs"][i].tolist()}
+             for i in range(n)]
+    orders = iter([torch.from_numpy(o.astype(np.int64)) for o in e["order"]])
+    real_randperm = torch.randperm
+    monkeypatch.setattr(torch, "randperm", lambda k, *a, **kw: next(orders) if k == n else real_randperm(k, *a, **kw))
+    o2d, o1d, v2d, v1d = m.get_param_groups(clr, lr)
+    adamw = torch.optim.AdamW([o1d, v1d], betas=(b1, b2), weight_decay=wd)
+    muon = torch.optim.Muon([o2d, v2d], adjust_lr_fn="match_rms_adamw", weight_decay=wd)
+    stats = train.model_optimize_step(m, [{"moves": moves}], MultiOptimizer(muon, adamw), None, beta, critic,
+                                      None, batch_size=int(e["batch_size"]), epochs=int(e["epochs"]))
+    for k, v in m.state_dict().items():
+        want = e[f"final::{k}"] - u[f"init::{k}"]
+        got = v.numpy() - u[f"init::{k}"]
+        cos = float(np.dot(got.ravel(), want.ravel()) / (np.linalg.norm(got) * np.linalg.norm(want) + 1e-30))
+        assert cos > COS_E4_CPU, (k, cos)
+    ref = dict(zip(e["stat_keys"].tolist(), e["stat_vals"].tolist()))
+    for k in ("loss", "policy_loss", "entropy_loss", "value_loss", "grad_norm", "entropy"):
+        assert math.isclose(stats[k], ref[k], rel_tol=1e-4, abs_tol=1e-6), (k, stats[k], ref[k])
+    m.eval()
+    with torch.no_grad():
+        lg, val = m(torch.stack(obs))
+    np.testing.assert_allclose(lg.numpy(), e["logits"], rtol=0, atol=LOGIT_E4_CPU)
+    np.testing.assert_allclose(val.reshape(-1).numpy(), e["value"], rtol=0, atol=LOGIT_E4_CPU)
 
 
 def test_cosine_schedule_matches_transformers():

@@ -23,6 +23,8 @@ Fixture files (all npz, allow_pickle=False):
   mlp196.npz      GameMLP forward at the bench's train configuration (h 196, 2 blocks), 512 boards
   update196.npz   model_optimize_step at h 196, dropout 0, 4 096 rows in two minibatches of 2 048, the
                   DataLoader order recorded (`python tools/gen_golden.py update196`)
+  update196e4.npz the same inputs over four epochs (eight optimizer steps): orders, the eight grad
+                  norms, final weights and the final policy's outputs (`... update196e4`)
 """
 
 from __future__ import annotations
@@ -319,20 +321,14 @@ def gen_update(game, train, games):
     print(f"update.npz: h=64 single minibatch of {len(moves)}; stats {stats}")
 
 
-def gen_update196(game, train):
-    """update196.npz: the reference's model_optimize_step (train.py:414-642) at the README / bench
-    policy shape -- GameMLP h 196, 2 residual blocks, dropout 0 -- on 4 096 rows of the golden games
-    in TWO minibatches of 2 048, one epoch; Muon (match_rms_adamw) + AdamW at fixed learning rates
-    (no scheduler).  The DataLoader's shuffle order is recorded (RandomSampler, wrapped here) and
-    stored as `order`, so a test can feed the same two minibatches; the per-minibatch statistics
-    come from the reference's own totals (stats) plus the two grad norms (clip_grad_norm_, wrapped
-    here).  `python tools/gen_golden.py update196` regenerates only this file."""
-    import torch.utils.data as tud
+def _update196_inputs(game, n=4096):
+    """The inputs of update196.npz / update196e4.npz: GameMLP h 196 at torch.manual_seed(1960), n rows
+    of the golden games (illegal recorded actions replaced by the first legal one), advantages and
+    returns from default_rng(196), old log-probabilities = the initial policy's + N(0, 0.05)."""
     torch.manual_seed(1960)
     cfg = game.MLPConfig(hidden_dim=196, num_layers=2, dropout=0.0, decouple_critic=False)
     model = game.GameMLP(cfg)
     g = np.load(OUT / "games.npz")
-    n = 4096
     boards = g["before"][:n]
     obs = torch.stack([game.Game2048(grid_of(b)).to_model_format() for b in boards])
     assert np.array_equal(np.rint(obs[:, 0::3].numpy()).astype(np.int8), boards)  # exponent channel
@@ -351,8 +347,13 @@ def gen_update196(game, train):
     moves = [{"game_state": obs[i], "selected_direction": int(actions[i]), "action_mask": invalid[i].tolist(),
               "advantage": float(adv[i]), "future_reward": float(fut[i]), "policy_logprobs": old_lp[i].tolist()}
              for i in range(n)]
-    init = {k: v.detach().clone() for k, v in model.state_dict().items()}
-    lr, clr, wd = 1e-3, 1e-4, 0.01
+    return model, boards, obs, invalid, actions, adv, fut, old_lp, moves
+
+
+def _run_recorded(train, model, moves, batch_size, epochs, lr=1e-3, clr=1e-4, wd=0.01):
+    """model_optimize_step (train.py:414-642) with Muon (match_rms_adamw) + AdamW at fixed learning
+    rates, the DataLoader's RandomSampler order and every clip_grad_norm_ result recorded."""
+    import torch.utils.data as tud
     o2d, o1d, v2d, v1d = model.get_param_groups(clr, lr)
     adamw = torch.optim.AdamW([o1d, v1d], betas=(0.9, 0.999), weight_decay=wd)
     muon = torch.optim.Muon([o2d, v2d], adjust_lr_fn="match_rms_adamw", weight_decay=wd)
@@ -374,10 +375,57 @@ def gen_update196(game, train):
     try:
         stats = train.model_optimize_step(model=model, episodes=[{"moves": moves}], optimizer=opt,
                                           lr_scheduler=None, kl_strength=0.02, critic_strength=0.2,
-                                          device=None, batch_size=2048, epochs=1)
+                                          device=None, batch_size=batch_size, epochs=epochs)
     finally:
         tud.RandomSampler.__iter__ = orig_iter
         torch.nn.utils.clip_grad_norm_ = orig_clip
+    return stats, order, norms
+
+
+def gen_update196e4(game, train):
+    """update196e4.npz: the multi-step pin.  The same inputs and initial weights as update196.npz
+    (asserted equal), run through model_optimize_step for FOUR epochs of two minibatches of 2 048 --
+    eight consecutive optimizer steps, each epoch in its own recorded shuffle order -- so a test can
+    measure how far the bf16 device update drifts from the fp32 reference over several steps.
+    Stored: the 4 x 4 096 order, the eight clip_grad_norm_ results, the reference's statistics, the
+    final weights, and the final policy's logits / value on the 4 096 boards (eval mode; dropout 0).
+    The initial weights and inputs are update196.npz's (not stored again).
+    `python tools/gen_golden.py update196e4` regenerates only this file."""
+    model, boards, obs, invalid, actions, adv, fut, old_lp, moves = _update196_inputs(game)
+    base = np.load(OUT / "update196.npz")
+    for k, v in model.state_dict().items():
+        assert np.array_equal(v.numpy(), base[f"init::{k}"]), k
+    assert np.array_equal(old_lp.numpy(), base["old_logprobs"]) and np.array_equal(actions, base["actions"])
+    stats, order, norms = _run_recorded(train, model, moves, 2048, 4)
+    n = len(moves)
+    assert len(order) == 4 * n and len(norms) == 8
+    for e in range(4):
+        assert sorted(order[e * n:(e + 1) * n]) == list(range(n))
+    model.eval()
+    with torch.no_grad():
+        logits, value = model(obs)
+    arrays = {f"final::{k}": v.detach().numpy() for k, v in model.state_dict().items()}
+    arrays.update(order=np.array(order, np.int16).reshape(4, n), grad_norms=np.array(norms),
+                  stat_keys=np.array(sorted(stats)), stat_vals=np.array([float(stats[k]) for k in sorted(stats)]),
+                  logits=logits.numpy(), value=value.reshape(-1).numpy(), epochs=np.int64(4),
+                  batch_size=np.int64(2048))
+    np.savez_compressed(OUT / "update196e4.npz", **arrays)
+    print(f"update196e4.npz: h=196, {n} rows, 4 epochs x 2 minibatches; grad norms {norms}; stats {stats}")
+
+
+def gen_update196(game, train):
+    """update196.npz: the reference's model_optimize_step (train.py:414-642) at the README / bench
+    policy shape -- GameMLP h 196, 2 residual blocks, dropout 0 -- on 4 096 rows of the golden games
+    in TWO minibatches of 2 048, one epoch; Muon (match_rms_adamw) + AdamW at fixed learning rates
+    (no scheduler).  The DataLoader's shuffle order is recorded (RandomSampler, wrapped here) and
+    stored as `order`, so a test can feed the same two minibatches; the per-minibatch statistics
+    come from the reference's own totals (stats) plus the two grad norms (clip_grad_norm_, wrapped
+    here).  `python tools/gen_golden.py update196` regenerates only this file."""
+    model, boards, obs, invalid, actions, adv, fut, old_lp, moves = _update196_inputs(game)
+    n = len(moves)
+    init = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    lr, clr, wd = 1e-3, 1e-4, 0.01
+    stats, order, norms = _run_recorded(train, model, moves, 2048, 1, lr, clr, wd)
     assert sorted(order) == list(range(n)) and len(norms) == 2
     arrays = {f"init::{k}": v.numpy() for k, v in init.items()}
     arrays.update({f"final::{k}": v.detach().numpy() for k, v in model.state_dict().items()})
@@ -457,6 +505,10 @@ def main():
         game, train = load_reference()
         gen_update196(game, train)
         return
+    if sys.argv[1:] == ["update196e4"]:
+        game, train = load_reference()
+        gen_update196e4(game, train)
+        return
     OUT.mkdir(parents=True, exist_ok=True)
     game, train = load_reference()
     DIRS = [game.Direction.UP, game.Direction.DOWN, game.Direction.LEFT, game.Direction.RIGHT]
@@ -471,6 +523,7 @@ def main():
     gen_urm64(game)
     gen_mlp196(game)
     gen_update196(game, train)
+    gen_update196e4(game, train)
 
 
 if __name__ == "__main__":
