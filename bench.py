@@ -373,7 +373,7 @@ def _c_chunk(args):
     return cnt
 
 
-PMC_PROFILE = ROOT / "profiles" / "r06g"  # round 6: this build, 65 536 boards x 1024 steps per launch
+PMC_PROFILE = ROOT / "profiles" / "r06l"  # round 6, final env kernel: 65 536 boards x 1024 steps per launch
 CPU_RATIO = ROOT / "profiles" / "r05b" / "cpu_ref_ratio.json"  # re-measured in round 5 (r02: 1.45 / 1.14)
 
 
