@@ -1,7 +1,7 @@
 """HIP-event timings of the GameURM training update's projection-kernel calls (urm_linear_kernel
 instances) at N boards, h = 64, inter = 120: the forwards (qkv store, o_proj / down_proj + residual
 RMSNorm training epilogue, gate_up + SwiGLU-conv training epilogue with and without gu) and the
-input gradients dX = dY W (qkv, gate_up).  G2048_LIB=<path> times another build (A/B).  Each line
+input gradients dX = dY W (qkv, gate_up), and the gate_up + SwiGLU-conv backward (gu recomputed).  G2048_LIB=<path> times another build (A/B).  Each line
 also prints a checksum of the outputs, so two builds can be compared for identical results.
 
     python tools/time_urm_train_linear.py [boards]
@@ -54,6 +54,9 @@ def main():
     out, outb, rstd = torch.empty(r, h, device=dev), torch.empty(r, h, dtype=bf, device=dev), torch.empty(r, device=dev)
     gu, a_out = torch.empty(r, 2 * i, dtype=bf, device=dev), torch.empty(r, i, dtype=bf, device=dev)
     dx = torch.empty(r, h, dtype=bf, device=dev)
+    dact = torch.randn(r, i, device=dev, generator=g).to(bf)
+    dgu2, dwc, dbc = torch.empty(r, 2 * i, dtype=bf, device=dev), torch.empty(i, 2, device=dev), torch.empty(i, device=dev)
+    part = torch.empty(L.urm_swiglu_conv_partials(n, i), device=dev)
     cases = {
         "qkv fwd (store)": (lambda: L.urm_linear(xb, wq, qkv), r * (h + 3 * h) * 2, (qkv,)),
         "o_proj + rms_t": (lambda: L.urm_linear_res_rms(xb, wo, hres, out, outb, rstd, 1e-5),
@@ -65,6 +68,8 @@ def main():
         "gate_up swiglu_t": (lambda: L.urm_linear_swiglu_train(xb, wg, cw, cb, None, a_out), r * (h + i) * 2, (a_out,)),
         "qkv dX (linear_t)": (lambda: L.urm_linear_t(dqkv, wq, dx), r * (3 * h + h) * 2, (dx,)),
         "gate_up dX (linear_t)": (lambda: L.urm_linear_t(dgu, wg, dx), r * (2 * i + h) * 2, (dx,)),
+        "gate_up swiglu bwd": (lambda: L.urm_gate_up_swiglu_bwd(xb, wg, cw, cb, dact, dgu2, dwc, dbc, part),
+                               r * (h + i + 2 * i) * 2, (dgu2, dwc, dbc)),
     }
     for name, (fn, nbytes, outs) in cases.items():
         us = timed(fn)
