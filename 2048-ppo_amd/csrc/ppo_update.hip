@@ -1662,34 +1662,37 @@ struct ColsumBatch {
     float *tick;  // += 1 by block 0 (the optimizer's step count)
 };
 
-// a job whose partial rows are whole float4s runs 4 columns per lane (256 per block: 16-byte loads);
+// a job whose partial rows are whole float2s runs 2 columns per lane (128 per block: 8-byte loads);
 // every column is summed in the same order either way (rows rg, rg + 16, ... per group, then the
-// 16 groups in order), so the two forms give the same bits
+// 16 groups in order), so the two forms give the same bits.  (Round 6: 2 columns per lane, not 4 --
+// the bench minibatch's 27.8 MB of partials then spread over 706 blocks instead of 353, i.e. ~2.8
+// blocks per CU instead of 1 or 2.)
+constexpr int kColsumW = 2;
 __host__ __device__ inline bool colsum_vec(const g2048_colsum_job &jb) {
-    return jb.cols % 4 == 0 && ((uintptr_t)jb.part % 16) == 0;
+    return jb.cols % kColsumW == 0 && ((uintptr_t)jb.part % (4 * kColsumW)) == 0;
 }
 
 __global__ __launch_bounds__(1024) void colsum_batch_kernel(const ColsumBatch cb) {
-    __shared__ float4 lds[16][64];
+    __shared__ float2 lds[16][64];
     int j = 0;
     while (j + 1 < cb.njobs && (int)blockIdx.x >= cb.first[j + 1]) j++;
     const g2048_colsum_job &jb = cb.job[j];
     const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
     const bool vec = colsum_vec(jb);  // block-uniform
-    const int W = vec ? 4 : 1;
+    const int W = vec ? kColsumW : 1;
     const int c0 = ((int)blockIdx.x - cb.first[j]) * 64 * W + cl * W;
-    float t[4];
+    float t[kColsumW];
 #pragma unroll
-    for (int u = 0; u < 4; u++) t[u] = c0 + u == jb.max_col ? -INFINITY : 0.0f;
+    for (int u = 0; u < kColsumW; u++) t[u] = c0 + u == jb.max_col ? -INFINITY : 0.0f;
     if (c0 < jb.cols) {
         const float *p = jb.part + c0;
         if (vec) {
 #pragma unroll 4
             for (int b = rg; b < jb.nb; b += 16) {
-                const float4 v = *reinterpret_cast<const float4 *>(p + (int64_t)b * jb.cols);
-                const float vv[4] = {v.x, v.y, v.z, v.w};
+                const float2 v = *reinterpret_cast<const float2 *>(p + (int64_t)b * jb.cols);
+                const float vv[kColsumW] = {v.x, v.y};
 #pragma unroll
-                for (int u = 0; u < 4; u++) t[u] = c0 + u == jb.max_col ? fmaxf(t[u], vv[u]) : t[u] + vv[u];
+                for (int u = 0; u < kColsumW; u++) t[u] = c0 + u == jb.max_col ? fmaxf(t[u], vv[u]) : t[u] + vv[u];
             }
         } else {
 #pragma unroll 4
@@ -1699,7 +1702,7 @@ __global__ __launch_bounds__(1024) void colsum_batch_kernel(const ColsumBatch cb
             }
         }
     }
-    lds[rg][cl] = make_float4(t[0], t[1], t[2], t[3]);
+    lds[rg][cl] = make_float2(t[0], t[1]);
     __syncthreads();
     if (cb.sq) {  // block 0: the step count and the zero tail of the partials
         if (blockIdx.x == 0 && threadIdx.x == 0 && cb.tick) *cb.tick += 1.0f;
@@ -1716,20 +1719,18 @@ __global__ __launch_bounds__(1024) void colsum_batch_kernel(const ColsumBatch cb
         }
         return;
     }
-    float acc[4];
+    float acc[kColsumW];
     {
-        const float4 a0 = lds[0][cl];
+        const float2 a0 = lds[0][cl];
         acc[0] = a0.x;
         acc[1] = a0.y;
-        acc[2] = a0.z;
-        acc[3] = a0.w;
     }
 #pragma unroll
     for (int g = 1; g < 16; g++) {
-        const float4 a = lds[g][cl];
-        const float av[4] = {a.x, a.y, a.z, a.w};
+        const float2 a = lds[g][cl];
+        const float av[kColsumW] = {a.x, a.y};
 #pragma unroll
-        for (int u = 0; u < 4; u++) acc[u] = c0 + u == jb.max_col ? fmaxf(acc[u], av[u]) : acc[u] + av[u];
+        for (int u = 0; u < kColsumW; u++) acc[u] = c0 + u == jb.max_col ? fmaxf(acc[u], av[u]) : acc[u] + av[u];
     }
     float ss = 0.0f;
     for (int u = 0; u < W; u++) {
@@ -2476,7 +2477,7 @@ static int colsum_batch_build(const g2048_colsum_job *jobs, int32_t njobs, Colsu
         cb.job[cb.njobs] = jb;
         cb.first[cb.njobs] = blocks;
         cb.njobs++;
-        blocks += colsum_vec(jb) ? (jb.cols + 255) / 256 : (jb.cols + 63) / 64;
+        blocks += colsum_vec(jb) ? (jb.cols + 64 * kColsumW - 1) / (64 * kColsumW) : (jb.cols + 63) / 64;
     }
     cb.first[cb.njobs] = blocks;
     return G2048_OK;
