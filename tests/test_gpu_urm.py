@@ -16,6 +16,7 @@ Two stated bounds on the fp32 logits / value:
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F
 
 from conftest import golden
 
@@ -1312,6 +1313,64 @@ def test_urm_ppo_updater_matches_generic_updater(dev):
     for k in s0:
         tol = 5e-2 if k == "kl_max" else 1e-2 if k.startswith("kl") else 1e-3
         assert math.isclose(s0[k], s1[k], rel_tol=tol, abs_tol=1e-6), (k, s0[k], s1[k])
+
+
+def test_urm_ppo_updater_minibatch_gradients_match_autocast(dev):
+    """One minibatch's gradients (before clipping / the optimizer) of URMPPOUpdater -- device loss
+    and head kernels, fused projections, direct weight gradients -- against PPOUpdater under bf16
+    autocast (torch loss + autograd) and PPOUpdater in fp32, same weights, same rows, dropout 0.  Bound
+    derived from bf16 rounding: per parameter, the URM updater's relative distance to the fp32
+    gradient is at most 1.1 x autocast's own + 1e-4 (autocast is the arithmetic the URM kernels
+    restate: the same bf16 operands and rounding points, other summation orders), and the two bf16
+    paths within URM_GRAD_REL of each other (relative L2)."""
+    import agent
+    from g2048.dist import GradBucket
+    from g2048.optim import MuonAdamW
+    from g2048.ppo import PPOConfig, PPOUpdater
+    from g2048.urmppo import URMPPOUpdater
+    cols = _urm_columns(dev, 2048, seed=11)
+    idx = torch.randperm(2048, device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+
+    def enc(b):
+        from g2048 import _lib as L
+        o = torch.empty(b.shape[0], 48, dtype=torch.float32, device=dev)
+        L.obs_encode(b.contiguous(), o)
+        return o
+    grads = {}
+    for name, cls, amp in (("urm", URMPPOUpdater, torch.bfloat16), ("autocast", PPOUpdater, torch.bfloat16),
+                           ("fp32", PPOUpdater, None)):
+        torch.manual_seed(2)
+        mod = agent.GameURM(agent.GameURMConfig(dropout=0.0)).to(dev).train()
+        with torch.no_grad():  # heads away from their init scale: a loss gradient in every head row
+            mod.action_head.weight.mul_(4.0)
+            mod.action_head.bias.uniform_(-0.5, 0.5)
+        opt = MuonAdamW(mod, 1e-3, 1e-4)
+        order = [p for p, _ in opt.muon] + [p for grp in opt.adam_groups for p in grp["params"]]
+        up = cls(mod, opt, PPOConfig(batch_size=2048, critic=0.2, amp_dtype=amp), GradBucket(order), None,
+                 graph=False)
+        up._pre(idx, cols, torch.tensor(0.02, device=dev), enc)
+        torch.cuda.synchronize()
+        grads[name] = {k: p.grad.detach().double().reshape(-1).clone() for k, p in mod.named_parameters()
+                       if p.grad is not None and float(p.grad.abs().sum()) > 0}
+    assert set(grads["urm"]) == set(grads["autocast"]) == set(grads["fp32"])
+    rows, bad = [], []
+    for k in grads["fp32"]:
+        u, a, f = grads["urm"][k], grads["autocast"][k], grads["fp32"][k]
+        e_u, e_a = float((u - f).norm() / f.norm()), float((a - f).norm() / f.norm())
+        d_ua = float((u - a).norm() / a.norm())
+        rows.append(f"{k}: |urm - fp32| {e_u:.3e}  |autocast - fp32| {e_a:.3e}  |urm - autocast| {d_ua:.2e}")
+        if e_u > 1.1 * e_a + 1e-4 or d_ua > URM_GRAD_REL:
+            bad.append(rows[-1])
+    print("\n".join(rows))
+    assert not bad, bad
+
+
+# the URM updater's minibatch gradients against autocast's: measured on MI355X (profiles/r06n/
+# urm_grads2.log) within 5.7e-6 relative of each other for every parameter (the heads within 2.3e-7,
+# value_head.bias equal), each at the same distance (4 digits) from the fp32 gradient as autocast's
+# own (0.26-2.3 % for the bf16 paths): the head / loss kernels and the autograd loss differ only in
+# summation order.  Bound: ~10 x the largest measured difference
+URM_GRAD_REL = 5e-5
 
 
 @pytest.mark.parametrize("n,heads,p", [(4099, 4, 0.0), (1000, 4, 0.1), (333, 2, 0.2)])
