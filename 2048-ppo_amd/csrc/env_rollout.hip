@@ -1,8 +1,8 @@
 // env_rollout.hip -- the synthetic random-legal rollout (the bench's headline workload,
 // g2048_env_rollout_random / _adv of include/g2048.h): env_rollout_kernel with its LDS tables and
-// per-step helpers, in a translation unit of its own so that it alone is built with the max-ILP
-// machine scheduler (Makefile: one wave per SIMD at the benchmark size, where the issue schedule,
-// not occupancy, sets the step time; the rest of libg2048 keeps the default, occupancy-aware one).
+// per-step helpers, in a translation unit of its own so that it alone is built with the machine
+// scheduler's occupancy bias at 0 (Makefile: one wave per SIMD at the benchmark size, where the issue
+// schedule, not occupancy, sets the step time; the rest of libg2048 keeps the default bias).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
