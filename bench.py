@@ -373,7 +373,7 @@ def _c_chunk(args):
     return cnt
 
 
-PMC_PROFILE = ROOT / "profiles" / "r06l"  # round 6, final env kernel: 65 536 boards x 1024 steps per launch
+PMC_PROFILE = ROOT / "profiles" / "r06q"  # round 6, final env kernel (env_rollout.hip, scheduler bias 0): 65 536 boards x 1024 steps per launch
 CPU_RATIO = ROOT / "profiles" / "r05b" / "cpu_ref_ratio.json"  # re-measured in round 5 (r02: 1.45 / 1.14)
 
 
