@@ -197,21 +197,22 @@ struct MuonArgs {
 // row-major X [K][M], with the transposing read.  kp = round8(K) = the padded K of row images.
 // One copy of this loop serves all three Newton-Schulz products (a_rows is wave-uniform): the
 // kernel has to fit the instruction cache, unrolled per product it does not.
-__device__ __forceinline__ void gemm_block(f32x4_t (&acc)[kBI][kBJ], const char *A, int pa, bool a_rows,
+template <int BI = kBI, int BJ = kBJ>
+__device__ __forceinline__ void gemm_block(f32x4_t (&acc)[BI][BJ], const char *A, int pa, bool a_rows,
                                            const char *B, int pb, int M, int N, int K, int ti0, int tj0,
                                            const char *zero, int lane) {
     const int TI = (M + 15) >> 4, TJ = (N + 15) >> 4, kp = (K + 7) & ~7;
     if (ti0 >= TI || tj0 >= TJ) return;  // wave-uniform: nothing of this wave's block is in range
     // Per-lane row offsets are fixed for the whole product (-1: out of range -> zero block).
     const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    int boff[kBJ], aoff[kBI];
+    int boff[BJ], aoff[BI];
 #pragma unroll
-    for (int j = 0; j < kBJ; j++) {
+    for (int j = 0; j < BJ; j++) {
         const int row = 16 * (tj0 + j) + (lane & 15);
         boff[j] = row < N ? row * pb : -1;
     }
 #pragma unroll
-    for (int i = 0; i < kBI; i++) {
+    for (int i = 0; i < BI; i++) {
         const int row = 16 * (ti0 + i) + (lane & 15);
         aoff[i] = a_rows ? (row < M ? row * pa : -1) : (16 * (ti0 + i) + 4 * p) * 2;  // col bytes for tr reads
     }
@@ -221,15 +222,15 @@ __device__ __forceinline__ void gemm_block(f32x4_t (&acc)[kBI][kBJ], const char 
     for (int k0 = 0; k0 < kp; k0 += 32) {
         const int kl = k0 + 8 * g;
         const bool kin = kl < kp;
-        bf16x8_t fb[kBJ], fa[kBI];
+        bf16x8_t fb[BJ], fa[BI];
 #pragma unroll
-        for (int j = 0; j < kBJ; j++) {
+        for (int j = 0; j < BJ; j++) {
             const char *pp = (kin && boff[j] >= 0) ? B + boff[j] + 2 * kl : zero;
             fb[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(pp));
         }
         if (a_rows) {
 #pragma unroll
-            for (int i = 0; i < kBI; i++) {
+            for (int i = 0; i < BI; i++) {
                 const char *pp = (kin && aoff[i] >= 0) ? A + aoff[i] + 2 * kl : zero;
                 fa[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(pp));
             }
@@ -237,7 +238,7 @@ __device__ __forceinline__ void gemm_block(f32x4_t (&acc)[kBI][kBJ], const char 
             const int r1 = k0 + 8 * g + q, r2 = r1 + 4;
             const char *b1 = A + r1 * pa, *b2 = A + r2 * pa;
 #pragma unroll
-            for (int i = 0; i < kBI; i++) {
+            for (int i = 0; i < BI; i++) {
                 const char *a1 = r1 < K ? b1 + aoff[i] : zero;
                 const char *a2 = r2 < K ? b2 + aoff[i] : zero;
                 const s16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)a1);
@@ -246,21 +247,22 @@ __device__ __forceinline__ void gemm_block(f32x4_t (&acc)[kBI][kBJ], const char 
             }
         }
 #pragma unroll
-        for (int i = 0; i < kBI; i++)
+        for (int i = 0; i < BI; i++)
 #pragma unroll
-            for (int j = 0; j < kBJ; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < BJ; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
 }
 
 // The accumulators start from the scaled previous output, (beta / alpha) * out[col][row] (zero when
 // beta == 0, and for tiles outside the product), read BEFORE the GEMM: the read and its conversion
 // overlap the MFMA work instead of sitting between the two barriers, and the store is a plain write.
-__device__ __forceinline__ void init_block_t(f32x4_t (&acc)[kBI][kBJ], const char *out, int pitch, int M, int N,
+template <int BI = kBI, int BJ = kBJ>
+__device__ __forceinline__ void init_block_t(f32x4_t (&acc)[BI][BJ], const char *out, int pitch, int M, int N,
                                              int ti0, int tj0, float ratio, bool use_old, int lane) {
 #pragma unroll
-    for (int i = 0; i < kBI; i++)
+    for (int i = 0; i < BI; i++)
 #pragma unroll
-        for (int j = 0; j < kBJ; j++) {
+        for (int j = 0; j < BJ; j++) {
             const int col = 16 * (tj0 + j) + (lane & 15);
             const int row0 = 16 * (ti0 + i) + 4 * (lane >> 4);
             f32x4_t a = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -278,14 +280,15 @@ __device__ __forceinline__ void init_block_t(f32x4_t (&acc)[kBI][kBJ], const cha
 // A lane holds 4 consecutive rows of one column, i.e. 4 consecutive elements of one output row:
 // one 8-byte LDS write.  Rows M .. round4(M)-1 land in the zero K padding and are zero (their
 // operands are zero fragments).  Callers put a barrier between the GEMM's last read of `out` and this.
-__device__ __forceinline__ void store_block_t(const f32x4_t (&acc)[kBI][kBJ], char *out, int pitch, int M, int N,
+template <int BI = kBI, int BJ = kBJ>
+__device__ __forceinline__ void store_block_t(const f32x4_t (&acc)[BI][BJ], char *out, int pitch, int M, int N,
                                               int ti0, int tj0, float alpha, int lane) {
     const int TI = (M + 15) >> 4, TJ = (N + 15) >> 4;
     if (ti0 >= TI || tj0 >= TJ) return;
 #pragma unroll
-    for (int i = 0; i < kBI; i++)
+    for (int i = 0; i < BI; i++)
 #pragma unroll
-        for (int j = 0; j < kBJ; j++) {
+        for (int j = 0; j < BJ; j++) {
             const int col = 16 * (tj0 + j) + (lane & 15);
             const int row0 = 16 * (ti0 + i) + 4 * (lane >> 4);
             if (col < N && row0 < M)
@@ -1342,6 +1345,30 @@ __global__ __launch_bounds__(1024) void lds_poison_kernel(uint32_t word) {
     __syncthreads();
 }
 
+// One Newton-Schulz product of the generic (non-square) schedule on this wave's BI x BJ tile block:
+// the 4 x 4 blocks of the original mapping (waves 4 x 4, 256 x 256), or blocks of one column of BI
+// tiles numbered down the TI tile rows first
+template <int BI, int BJ>
+__device__ __forceinline__ void generic_phase(const char *A, int pa, bool a_rows, const char *B, int pb, char *out,
+                                              int po, int M, int N, int K, float alpha, float beta, const char *zero,
+                                              int wave, int lane, int TI) {
+    int ti0, tj0;
+    if constexpr (BI == kBI && BJ == kBJ) {
+        ti0 = (wave & 3) * kBI;
+        tj0 = (wave >> 2) * kBJ;
+    } else {
+        const int WI = (TI + BI - 1) / BI;
+        ti0 = (wave % WI) * BI;
+        tj0 = (wave / WI) * BJ;
+    }
+    f32x4_t acc[BI][BJ];
+    init_block_t<BI, BJ>(acc, out, po, M, N, ti0, tj0, beta / alpha, beta != 0.0f, lane);
+    gemm_block<BI, BJ>(acc, A, pa, a_rows, B, pb, M, N, K, ti0, tj0, zero, lane);
+    __syncthreads();
+    store_block_t<BI, BJ>(acc, out, po, M, N, ti0, tj0, alpha, lane);
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint8_t role = args.job_mat[blockIdx.x];
@@ -1361,7 +1388,6 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
     char *sG = smem + ((r * px + 127) & ~127);
     char *zero = sG + ((r * pg + 127) & ~127);  // 64 zero bytes
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ti0 = (wave & 3) * kBI, tj0 = (wave >> 2) * kBJ;  // wave-uniform
     MUON_TP(args);
     __shared__ float red[kMuonThreads / 64];
     __shared__ float s_norm;
@@ -1422,7 +1448,6 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
         default: ns_square<32>(sX, sG, args, wave, lane); break;
         }
     } else {
-    f32x4_t acc[kBI][kBJ];
     for (int ph = 0; ph < 3 * args.steps; ph++) {
         const int k = ph % 3;
         const char *A = k == 1 ? sG : sX;
@@ -1434,11 +1459,18 @@ __global__ __launch_bounds__(kMuonThreads) void muon_kernel(MuonArgs args) {
         const int po = k == 2 ? px : pg;
         const float alpha = k == 1 ? args.c : 1.0f;
         const float beta = k == 0 ? 0.0f : (k == 1 ? args.b : args.a);
-        init_block_t(acc, out, po, M, N, ti0, tj0, beta / alpha, beta != 0.0f, lane);
-        gemm_block(acc, A, pa, k != 2, B, pb, M, N, K, ti0, tj0, zero, lane);
-        __syncthreads();
-        store_block_t(acc, out, po, M, N, ti0, tj0, alpha, lane);
-        __syncthreads();
+        // round 6: the tiles of a small product spread over the 16 waves (one 16 x 16 tile per wave,
+        // or a column of four) instead of one wave's 4 x 4 block -- the stem's 48 x 48 G and U ran on
+        // ONE wave and made this block the launch's critical path (119 k cycles vs the 13-part
+        // squares' 105-108 k, profiles/r06x/trace_muon_13.log).  Per tile the MFMA sequence (init,
+        // k-steps in order, store) is unchanged: the same bits
+        const int TI = (M + 15) >> 4, TJ = (N + 15) >> 4;
+        if (TI * TJ <= kMuonWaves)
+            generic_phase<1, 1>(A, pa, k != 2, B, pb, out, po, M, N, K, alpha, beta, zero, wave, lane, TI);
+        else if (TJ <= 4 && ((TI + 3) >> 2) * TJ <= kMuonWaves)
+            generic_phase<4, 1>(A, pa, k != 2, B, pb, out, po, M, N, K, alpha, beta, zero, wave, lane, TI);
+        else
+            generic_phase<kBI, kBJ>(A, pa, k != 2, B, pb, out, po, M, N, K, alpha, beta, zero, wave, lane, TI);
     }
     }
 
