@@ -1,5 +1,6 @@
 """Time the fused Muon + AdamW optimizer step (FusedMuonAdamW.step_clipped: grad clip, muon_kernel,
-adamw_kernel) of GameMLP h=196 with HIP events.   python tools/time_muon.py [libpath] [hidden] [quick]"""
+adamw_kernel) of GameMLP h=196 (or GameURM: hidden = "urm") with HIP events.
+    python tools/time_muon.py [libpath|-] [hidden|urm] [quick]"""
 import sys
 from pathlib import Path
 
@@ -16,10 +17,11 @@ def main():
     import agent
     from g2048.dist import GradBucket
     from g2048.optim import FusedMuonAdamW
-    h = int(sys.argv[2]) if len(sys.argv) > 2 else 196
+    urm = len(sys.argv) > 2 and sys.argv[2] == "urm"  # the default GameURMConfig's 11 matrices instead
+    h = 64 if urm else int(sys.argv[2]) if len(sys.argv) > 2 else 196
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    m = agent.GameMLP(agent.MLPConfig(hidden_dim=h, num_layers=2)).to(dev)
+    m = (agent.GameURM(agent.GameURMConfig()) if urm else agent.GameMLP(agent.MLPConfig(hidden_dim=h, num_layers=2))).to(dev)
     fo = FusedMuonAdamW(m, 1e-3, 1e-4)
     order = [p for p, _ in fo.muon] + [p for grp in fo.adam_groups for p in grp["params"]]
     bk = GradBucket(order)
@@ -61,7 +63,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         print(f"  ns_steps={ns}: {e0.elapsed_time(e1) / reps * 1e3:.1f} us")
-    w = m.backbone[0].mlp[0].weight
+    w = m.layers[0].attn.qkv_proj.weight if urm else m.backbone[0].mlp[0].weight
     print("checksum", float(w.double().sum()), float(w.double().abs().sum()))
 
 
