@@ -464,10 +464,20 @@ __host__ __device__ constexpr int muon_pitch(int rows, int cols) {
 constexpr int kNsMaxBlocks = 4;  // per wave and product
 constexpr int kNsMaxTiles = 16;  // accumulator tiles per wave (64 of the 128 VGPRs at 4 waves per SIMD)
 
+constexpr int ns_nparts(int NT, bool sym) {
+    int n = NT >= 4 ? ((NT + 3) / 4 > 4 ? (NT + 3) / 4 : 4) : NT;
+    const int n3 = (NT + 2) / 3;
+    if (sym && n3 > n && n3 * (n3 + 1) / 2 <= kMuonWaves && n3 <= 8) n = n3;
+    return n;
+}
+
 struct NsParts {
-    int n, start[4], size[4];
-    // 4 parts (16 blocks: one per wave of the full product) from 4 tiles up, of at most 4 tiles
-    constexpr NsParts(int NT) : n(NT >= 4 ? ((NT + 3) / 4 > 4 ? (NT + 3) / 4 : 4) : NT), start{}, size{} {
+    int n, start[8], size[8];
+    // 4 parts (16 blocks: one per wave of the full product) from 4 tiles up, of at most 4 tiles.
+    // Symmetric products (sym: the upper-triangle blocks only) take parts of at most 3 tiles when
+    // their block count still fits the 16 waves (round 6: at h 196, 5 parts -> 15 blocks of <= 9 tiles
+    // instead of 10 blocks of <= 12: the slowest wave of G = X X^T carries 3/4 of the MFMAs)
+    constexpr NsParts(int NT, bool sym = false) : n(ns_nparts(NT, sym)), start{}, size{} {
         const int base = NT / n, extra = NT % n;
         int s0 = 0;
         for (int i = 0; i < n; i++) {
@@ -482,8 +492,8 @@ struct NsSchedule {
     int bi[2][kMuonWaves][kNsMaxBlocks], bj[2][kMuonWaves][kNsMaxBlocks];  // [sym][wave][i]: part indices
     int cnt[2][kMuonWaves], tiles[2][kMuonWaves];
     constexpr NsSchedule(int NT) : bi{}, bj{}, cnt{}, tiles{} {
-        const NsParts pt(NT);
         for (int sym = 0; sym < 2; sym++) {
+            const NsParts pt(NT, sym != 0);
             int ai[16] = {}, aj[16] = {}, cost[16] = {}, n = 0;
             for (int i = 0; i < pt.n; i++)
                 for (int j = sym ? i : 0; j < pt.n; j++) {
@@ -663,7 +673,7 @@ __device__ __forceinline__ void ns_store(const f32x4_t (&acc)[T], uint2 (&kept)[
 template <int N, bool SYM, bool AROWS, int KEEP, int W, int U, int T>
 __device__ __forceinline__ void ns_blocks(f32x4_t (&acc)[T], uint2 (&kept)[T], const char *A, const char *B,
                                           const char *out, float ratio, bool init, int g, int c, int ltr) {
-    constexpr NsParts pt(NsShape<N>::NT);
+    constexpr NsParts pt(NsShape<N>::NT, SYM);
     constexpr NsSchedule sch(NsShape<N>::NT);
     if constexpr (U < sch.cnt[SYM][W]) {
         constexpr int bi = sch.bi[SYM][W][U], bj = sch.bj[SYM][W][U];
@@ -676,7 +686,7 @@ __device__ __forceinline__ void ns_blocks(f32x4_t (&acc)[T], uint2 (&kept)[T], c
 template <int N, bool SYM, int KEEP, int W, int U, int T>
 __device__ __forceinline__ void ns_stores(const f32x4_t (&acc)[T], uint2 (&kept)[T], char *out, float alpha, int g,
                                           int c) {
-    constexpr NsParts pt(NsShape<N>::NT);
+    constexpr NsParts pt(NsShape<N>::NT, SYM);
     constexpr NsSchedule sch(NsShape<N>::NT);
     if constexpr (U < sch.cnt[SYM][W]) {
         constexpr int bi = sch.bi[SYM][W][U], bj = sch.bj[SYM][W][U];
